@@ -1,0 +1,277 @@
+/*
+ * pinot_gpu.h -- C ABI of libpinot_gpu.so, the MI355X (gfx950) segment query hot path.
+ *
+ * This is the drop-in boundary of SURVEY.md §8(b): the Java side keeps Pinot's PlanMaker /
+ * Operator / AggregationFunction / ForwardIndexReader / Dictionary SPIs and calls these
+ * entry points through JNI (binding stub in INTEGRATION.md).  Plain C types only; no HIP,
+ * torch or C++ types cross this line.  All functions return 0 (PG_OK) or a negative
+ * pg_status; the thread-local message is available from pg_last_error().  Nothing is ever
+ * thrown or aborted across the ABI.
+ *
+ * Reference interfaces each entry point replaces (paths relative to navina/pinot):
+ *   pg_column_upload  <- IndexingOverrides.registerProvider / DefaultIndexReaderProvider
+ *                        (pinot-segment-spi/.../index/IndexingOverrides.java:82-92,
+ *                         pinot-segment-local/.../readers/DefaultIndexReaderProvider.java:79-122):
+ *                        the reader factories that wrap a segment's PinotDataBuffer at load time.
+ *                        Here the same on-disk big-endian bytes are made device-resident.
+ *   pg_segment_release<- IndexSegment.destroy (pinot-segment-spi/.../IndexSegment.java:122)
+ *   pg_execute        <- PlanMaker.makeInstancePlan + Plan.execute for aggregation / group-by
+ *                        queries (pinot-core/.../plan/maker/PlanMaker.java:42,
+ *                        plan/GlobalPlanImplV0.java:48): per-segment FilterPlanNode ->
+ *                        AggregationOperator / AggregationGroupByOrderByOperator, merged by
+ *                        AggregationOnlyCombineOperator / GroupByOrderByCombineOperator
+ *                        (operator/combine/).  Leaf predicates arrive already lowered to
+ *                        dictId space exactly as PredicateEvaluatorProvider.getPredicateEvaluator
+ *                        (operator/filter/predicate/PredicateEvaluatorProvider.java:38-90) does.
+ *   pg_execute_partial / pg_partials_* <- the per-server partial results that
+ *                        BaseCombineOperator.mergeResults (operator/combine/BaseCombineOperator.java:190-233)
+ *                        merges; exposed as dense device arrays so that ranks (one process per
+ *                        GPU) can merge them with an RCCL all-reduce over xGMI.
+ *   pg_cancel         <- BaseOperator.nextBlock interrupt check (operator/BaseOperator.java:35-37)
+ *   pg_last_error     <- ProcessingException text carried in the IntermediateResultsBlock
+ *                        (operator/combine/BaseCombineOperator.java:104-108)
+ */
+#ifndef PINOT_GPU_H
+#define PINOT_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PG_ABI_VERSION 1
+
+typedef enum pg_status {
+  PG_OK = 0,
+  PG_E_INVALID = -1,      /* malformed argument / plan */
+  PG_E_HIP = -2,          /* HIP runtime error */
+  PG_E_NOMEM = -3,        /* device allocation failed */
+  PG_E_NOTFOUND = -4,     /* segment / column index not resident */
+  PG_E_UNSUPPORTED = -5,  /* query shape not handled on the GPU: caller falls back to the CPU plan */
+  PG_E_CANCELLED = -6,    /* pg_cancel() observed */
+  PG_E_TIMEOUT = -7,      /* plan deadline passed */
+  PG_E_STATE = -8         /* pg_init not called / wrong device */
+} pg_status;
+
+/* ---------------------------------------------------------------- device / library */
+
+/* Bind the calling process to HIP device `device` (one process per GPU).  Idempotent. */
+int pg_init(int device);
+/* Copy the calling thread's last error message (NUL-terminated, truncated to n). Returns its length. */
+int pg_last_error(char *buf, size_t n);
+/* Bytes of device memory held by resident segments. */
+int pg_resident_bytes(uint64_t *out);
+/* Request cancellation of an in-flight pg_execute carrying this query_id (checked between launches). */
+int pg_cancel(uint64_t query_id);
+/* Library ABI version (PG_ABI_VERSION). */
+int pg_abi_version(void);
+
+/* ---------------------------------------------------------------- segment residency */
+
+typedef enum pg_index_kind {
+  PG_IDX_DICT = 1,            /* sorted dictionary, fixed-width big-endian values (V1 `.dict`)          */
+  PG_IDX_FWD_SV_BITPACKED = 2,/* FixedBitSVForwardIndexWriter layout (`.sv.unsorted.fwd`)               */
+  PG_IDX_FWD_SV_SORTED = 3,   /* sorted column: per dictId big-endian int32 [startDoc,endDoc] (`.sv.sorted.fwd`) */
+  PG_IDX_FWD_MV_BITPACKED = 4,/* FixedBitMVForwardIndexWriter layout (`.mv.fwd`)                        */
+  PG_IDX_INV_BITMAP = 5,      /* BitmapInvertedIndexWriter layout: (card+1) BE uint32 offsets + roaring */
+  PG_IDX_KEYMAP = 6           /* native int32[card]: dictId -> table-global key id (host-built, for
+                                 group-by / DISTINCTCOUNT keys that are not integer value ranges)       */
+} pg_index_kind;
+
+typedef enum pg_data_type {
+  PG_INT = 0, PG_LONG = 1, PG_FLOAT = 2, PG_DOUBLE = 3, PG_STRING = 4, PG_BYTES = 5
+} pg_data_type;
+
+#define PG_SRC_DEVICE 0x1u /* pg_col_desc.flags: `src` is a device pointer (same byte layout) */
+
+typedef struct pg_col_desc {
+  uint32_t kind;             /* pg_index_kind */
+  uint32_t data_type;        /* pg_data_type of the dictionary values (stored type) */
+  uint32_t num_docs;         /* segment.total.docs */
+  uint32_t cardinality;      /* column.<c>.cardinality */
+  uint32_t bits_per_element; /* column.<c>.bitsPerElement */
+  uint32_t num_values;       /* column.<c>.totalNumberOfEntries (MV: total values; SV: num_docs) */
+  uint32_t entry_bytes;      /* dictionary bytes per entry (4/8 numeric, lengthOfEachEntry for strings) */
+  uint32_t flags;            /* PG_SRC_DEVICE */
+} pg_col_desc;
+
+/* Make one index of one column of one segment device-resident.  `src` holds `nbytes` bytes in the
+ * reference's on-disk (big-endian) layout and is borrowed only for the duration of the call.
+ * Re-uploading the same (seg_key, col_id, kind) replaces it. */
+int pg_column_upload(uint64_t seg_key, uint32_t col_id, const pg_col_desc *desc, const void *src,
+                     uint64_t nbytes);
+/* Free every device buffer of a segment. */
+int pg_segment_release(uint64_t seg_key);
+
+/* ---------------------------------------------------------------- query plan */
+
+typedef enum pg_leaf_kind {
+  PG_LEAF_MATCH_ALL = 0,  /* MatchAllFilterOperator / predicate evaluator isAlwaysTrue                  */
+  PG_LEAF_EMPTY = 1,      /* EmptyFilterOperator / isAlwaysFalse                                        */
+  PG_LEAF_SV_SCAN = 2,    /* ScanBasedFilterOperator over a bit-packed SV forward index                 */
+  PG_LEAF_SORTED = 3,     /* SortedIndexBasedFilterOperator over PG_IDX_FWD_SV_SORTED                   */
+  PG_LEAF_INVERTED = 4,   /* BitmapBasedFilterOperator over PG_IDX_INV_BITMAP                           */
+  PG_LEAF_MV_SCAN = 5     /* ScanBasedFilterOperator over a bit-packed MV forward index (any / all)     */
+} pg_leaf_kind;
+
+/* A leaf matches dictIds in the set S, where S = [lo, hi) when num_ids == 0, else S = ids[0..num_ids).
+ * exclusive = 0: SV doc matches iff dictId in S; MV doc matches iff ANY value in S.
+ * exclusive = 1 (NOT_EQ / NOT_IN): SV doc matches iff dictId not in S; MV doc matches iff ALL values
+ *   are not in S (BaseDictionaryBasedPredicateEvaluator.applyMV, :133-150); inverted: flip of the OR.
+ * dictIds are per segment: each pg_segment_ref carries its own array of leaves. */
+typedef struct pg_leaf {
+  uint32_t kind;       /* pg_leaf_kind */
+  uint32_t col_id;
+  uint32_t exclusive;
+  uint32_t num_ids;
+  int32_t lo, hi;
+  const int32_t *ids;  /* host pointer, sorted ascending, no duplicates */
+} pg_leaf;
+
+/* Filter program: postfix over leaves.  op >= 0 pushes leaf `op`; PG_OP_AND(n)/PG_OP_OR(n) pop n
+ * operands; PG_OP_NOT pops one.  An empty program means match-all. */
+#define PG_OP_NOT (-1)
+#define PG_OP_AND(n) (-(int32_t)(0x100 | (n)))
+#define PG_OP_OR(n) (-(int32_t)(0x200 | (n)))
+
+typedef enum pg_agg_fn {
+  PG_AGG_COUNT = 0,         /* CountAggregationFunction (COUNT(*))                 -> count          */
+  PG_AGG_SUM = 1,           /* SumAggregationFunction                              -> double sum     */
+  PG_AGG_MIN = 2,           /* MinAggregationFunction                              -> double         */
+  PG_AGG_MAX = 3,           /* MaxAggregationFunction                              -> double         */
+  PG_AGG_AVG = 4,           /* AvgAggregationFunction                              -> (sum, count)   */
+  PG_AGG_DISTINCTCOUNT = 5, /* DistinctCountAggregationFunction (dictionary path) -> #distinct keys  */
+  PG_AGG_COUNTMV = 6        /* CountMVAggregationFunction                          -> sum numValues  */
+} pg_agg_fn;
+
+typedef enum pg_expr_op {   /* transform applied to the aggregation input (TransformFunction)      */
+  PG_EXPR_COL = 0,          /* value(col_a)                                                          */
+  PG_EXPR_MUL = 1,          /* MultiplicationTransformFunction: value(col_a) * value(col_b)          */
+  PG_EXPR_ADD = 2,          /* AdditionTransformFunction                                             */
+  PG_EXPR_SUB = 3           /* SubtractionTransformFunction                                          */
+} pg_expr_op;
+
+typedef struct pg_agg {
+  uint32_t fn;      /* pg_agg_fn */
+  uint32_t op;      /* pg_expr_op (SUM/MIN/MAX/AVG) */
+  uint32_t col_a;   /* input column (unused for COUNT) */
+  uint32_t col_b;   /* second operand for PG_EXPR_MUL/ADD/SUB */
+  /* DISTINCTCOUNT only: how the value's table-global id is formed (see pg_key) */
+  uint32_t key_kind;
+  uint32_t key_cardinality;
+  int64_t key_base;
+} pg_agg;
+
+typedef enum pg_key_kind {
+  PG_KEY_VALUE_OFFSET = 0,  /* INT/LONG dictionary: global id = value - base                         */
+  PG_KEY_KEYMAP = 1         /* global id = PG_IDX_KEYMAP[dictId] of (segment, col)                   */
+} pg_key_kind;
+
+typedef struct pg_key {
+  uint32_t col_id;
+  uint32_t kind;            /* pg_key_kind */
+  uint32_t cardinality;     /* size of the table-global key space of this column */
+  uint32_t pad;
+  int64_t base;             /* PG_KEY_VALUE_OFFSET */
+} pg_key;
+
+typedef struct pg_segment_ref {
+  uint64_t seg_key;
+  uint32_t num_docs;
+  uint32_t pad;
+  const pg_leaf *leaves;    /* plan.num_leaves entries */
+} pg_segment_ref;
+
+typedef struct pg_plan {
+  uint32_t abi_version;     /* PG_ABI_VERSION */
+  uint32_t num_segments;
+  const pg_segment_ref *segments;
+  uint32_t num_leaves;
+  uint32_t num_ops;
+  const int32_t *ops;       /* filter program (postfix) */
+  uint32_t num_aggs;
+  uint32_t num_keys;        /* 0 => aggregation-only query */
+  const pg_agg *aggs;
+  const pg_key *keys;       /* group-by expressions, in GROUP BY order */
+  uint64_t num_groups_limit;/* InstancePlanMakerImplV2 num.groups.limit (per segment)                 */
+  uint64_t query_id;        /* for pg_cancel */
+  int64_t deadline_ms;      /* CLOCK_MONOTONIC ms; 0 = none (QueryContext.getEndTimeMs)              */
+  void *stream;             /* hipStream_t to launch on; NULL = the library's per-thread stream      */
+} pg_plan;
+
+/* ---------------------------------------------------------------- results */
+
+typedef struct pg_stats {     /* ExecutionStatistics, summed over the plan's segments */
+  uint64_t num_docs_scanned;
+  uint64_t num_entries_scanned_in_filter;   /* device's own count; not a parity target */
+  uint64_t num_entries_scanned_post_filter;
+  uint64_t num_total_docs;
+  uint64_t num_segments_processed;
+  uint64_t num_segments_matched;
+} pg_stats;
+
+/* Host-side final result of one plan (library-owned until pg_result_free).
+ * Aggregation-only: num_groups = 1.  Group-by: one row per group with at least one matching doc.
+ * keys[g*num_keys + k] = table-global key id of group g's k-th key.
+ * values[g*num_aggs + a]: COUNT / COUNTMV count, SUM sum, MIN/MAX value, AVG sum, DISTINCTCOUNT count.
+ * counts[g*num_aggs + a]: AVG count (0 for the others). */
+typedef struct pg_result {
+  pg_stats stats;
+  uint64_t num_groups;
+  uint32_t num_keys;
+  uint32_t num_aggs;
+  uint32_t *keys;
+  double *values;
+  int64_t *counts;
+} pg_result;
+
+int pg_execute(const pg_plan *plan, pg_result **out);
+int pg_result_free(pg_result *res);
+
+/* ---------------------------------------------------------------- partial state (multi-GPU) */
+
+/* Dense partial state of one plan on this device, laid out per group slot g in [0, num_slots):
+ *   i64 [num_slots][n_i64] : merged by SUM   (per-slot doc count, integer sums, AVG counts, COUNTMV)
+ *   f64 [num_slots][n_f64] : merged by SUM   (floating-point sums)
+ *   mn  [num_slots][n_min] : merged by MIN   (order-preserving int64 image of double MIN)
+ *   mx  [num_slots][n_max] : merged by MAX   (order-preserving int64 image of double MAX)
+ *   flags [num_slots][flag_bytes_per_slot] : merged by MAX (DISTINCTCOUNT presence bytes)
+ * All pointers are device pointers owned by the handle; ranks all-reduce them in place. */
+typedef struct pg_partials {
+  pg_stats stats;
+  uint64_t num_slots;
+  uint32_t n_i64, n_f64, n_min, n_max;
+  uint64_t flag_bytes_per_slot;
+  int64_t *i64;
+  double *f64;
+  int64_t *mn;
+  int64_t *mx;
+  uint8_t *flags;
+  void *impl;
+} pg_partials;
+
+int pg_execute_partial(const pg_plan *plan, pg_partials **out);
+/* Decode (possibly all-reduced) partial state into a host pg_result.  `plan` must be the plan
+ * the partials were produced from (only its aggs / keys are read). */
+int pg_partials_finalize(pg_partials *p, const pg_plan *plan, pg_result **out);
+int pg_partials_free(pg_partials *p);
+
+/* ---------------------------------------------------------------- measurement hooks */
+
+/* Device time (ms, HIP events on the execution stream) of the last pg_execute* on this thread,
+ * split into the filter-materialisation pre-pass and the fused scan/aggregate kernel. */
+typedef struct pg_timing {
+  float prepass_ms;
+  float scan_ms;
+  float finalize_ms;
+  uint32_t scan_launches;
+  uint32_t pad;
+} pg_timing;
+int pg_last_timing(pg_timing *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PINOT_GPU_H */

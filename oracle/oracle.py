@@ -1,0 +1,196 @@
+"""Python driver of the C oracle (oracle/pinot_oracle.c).  TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module, and only
+as the checker.  The product path (pinot_amd.gpu) never imports it.
+
+Executes a lowered plan segment by segment with the restated Pinot operators, then merges the
+per-segment results by VALUE key exactly like the combine operators do:
+  AggregationOnlyCombineOperator.mergeResultsBlocks (operator/combine/AggregationOnlyCombineOperator.java:47-57),
+  GroupByOrderByCombineOperator.processSegments -> IndexedTable.upsert (operator/combine/GroupByOrderByCombineOperator.java:127-214,
+  data/table/IndexedTable.java:103-118), with DISTINCTCOUNT sets converted from dictIds to values at
+  extraction (DistinctCountAggregationFunction.extractAggregationResult, function/DistinctCountAggregationFunction.java:252-310).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from concurrent.futures import ThreadPoolExecutor
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from pinot_amd import abi
+from pinot_amd.plan import (CPlan, DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY, ExecutionStats, IntermediateResult,
+                            Table, merge_intermediate)
+from pinot_amd.query import QueryContext, parse
+from pinot_amd.segment import ImmutableSegment
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(_HERE, "libpinot_oracle.so")
+ORC_FWD_SV, ORC_FWD_SORTED, ORC_FWD_MV = 0, 1, 2
+
+
+class orc_column(C.Structure):
+    _fields_ = [("dict", C.c_void_p), ("fwd", C.c_void_p), ("inv", C.c_void_p), ("inv_bytes", C.c_uint64),
+                ("keymap", C.c_void_p), ("fwd_kind", C.c_uint32), ("data_type", C.c_uint32),
+                ("num_docs", C.c_uint32), ("cardinality", C.c_uint32), ("bits", C.c_uint32),
+                ("num_values", C.c_uint32), ("entry_bytes", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class orc_segment_result(C.Structure):
+    _fields_ = [("stats", abi.pg_stats), ("num_groups", C.c_uint64), ("num_keys", C.c_uint32),
+                ("num_aggs", C.c_uint32), ("key_dict_ids", C.POINTER(C.c_int32)),
+                ("values", C.POINTER(C.c_double)), ("counts", C.POINTER(C.c_int64)),
+                ("num_distinct", C.c_uint64), ("distinct_group_agg", C.POINTER(C.c_uint64)),
+                ("distinct_dict_ids", C.POINTER(C.c_int32))]
+
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        lib = C.CDLL(LIB)
+        lib.orc_execute_segment.argtypes = [C.POINTER(abi.pg_plan), C.c_uint32, C.POINTER(orc_column), C.c_uint64,
+                                            C.POINTER(C.POINTER(orc_segment_result))]
+        lib.orc_execute_segment.restype = C.c_int
+        lib.orc_result_free.argtypes = [C.POINTER(orc_segment_result)]
+        lib.orc_unpack.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p]
+        lib.orc_roaring_decode.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32]
+        lib.orc_num_bits_per_value.argtypes = [C.c_int32]
+        lib.orc_num_bits_per_value.restype = C.c_int
+        _lib = lib
+    return _lib
+
+
+class _SegmentColumns:
+    """orc_column array for one segment, indexed by table column id (keeps the byte buffers alive)."""
+
+    def __init__(self, seg: ImmutableSegment, table: Table):
+        n = len(table.column_ids)
+        self.arr = (orc_column * max(n, 1))()
+        self.keep = []
+        for name, col in seg.columns.items():
+            c = self.arr[table.column_ids[name]]
+            d = np.frombuffer(col.dictionary.to_bytes() or b"\0", dtype=np.uint8)
+            f = np.frombuffer(col.fwd or b"\0", dtype=np.uint8)
+            self.keep += [d, f]
+            c.dict = d.ctypes.data
+            c.fwd = f.ctypes.data
+            if col.inverted is not None:
+                iv = np.frombuffer(col.inverted, dtype=np.uint8)
+                self.keep.append(iv)
+                c.inv = iv.ctypes.data
+                c.inv_bytes = len(col.inverted)
+            c.fwd_kind = {"sv": ORC_FWD_SV, "sorted": ORC_FWD_SORTED, "mv": ORC_FWD_MV}[col.fwd_kind]
+            c.data_type = abi.DTYPE_CODES[col.data_type]
+            c.num_docs = col.num_docs
+            c.cardinality = col.cardinality
+            c.bits = col.bits_per_element
+            c.num_values = col.num_values
+            c.entry_bytes = col.dictionary.entry_bytes
+
+
+class OracleEngine:
+    """Runs plans on the CPU restatement.  `threads` parallelises over segments (ctypes drops the GIL)."""
+
+    def __init__(self, threads: int = 1, array_based_threshold: int = DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY):
+        self.lib = load()
+        self.threads = threads
+        self.array_based_threshold = array_based_threshold
+        self._cols = {}
+
+    def columns(self, seg, table):
+        k = (id(seg), id(table))
+        if k not in self._cols:
+            self._cols[k] = _SegmentColumns(seg, table)
+        return self._cols[k]
+
+    def run_segment(self, plan: CPlan, si: int, seg: ImmutableSegment):
+        cols = self.columns(seg, plan.table)
+        out = C.POINTER(orc_segment_result)()
+        rc = self.lib.orc_execute_segment(C.byref(plan.plan), si, cols.arr, self.array_based_threshold, C.byref(out))
+        if rc:
+            raise RuntimeError(f"oracle failed rc={rc}")
+        try:
+            return self._to_value_rows(plan, seg, out.contents)
+        finally:
+            self.lib.orc_result_free(out)
+
+    def _to_value_rows(self, plan: CPlan, seg: ImmutableSegment, r: orc_segment_result):
+        A, K, G = r.num_aggs, r.num_keys, r.num_groups
+        aggs = plan.aggs
+        vals = np.ctypeslib.as_array(r.values, shape=(G * A,)).reshape(G, A).copy() if G and A else np.zeros((G, A))
+        cnts = np.ctypeslib.as_array(r.counts, shape=(G * A,)).reshape(G, A).copy() if G and A else \
+            np.zeros((G, A), dtype=np.int64)
+        keys = np.ctypeslib.as_array(r.key_dict_ids, shape=(G * K,)).reshape(G, K).copy() if G and K else \
+            np.zeros((G, K), dtype=np.int32)
+        distinct = {}
+        if r.num_distinct:
+            ga = np.ctypeslib.as_array(r.distinct_group_agg, shape=(r.num_distinct,))
+            di = np.ctypeslib.as_array(r.distinct_dict_ids, shape=(r.num_distinct,))
+            for g_a, d in zip(ga.tolist(), di.tolist()):
+                distinct.setdefault(g_a, []).append(d)
+        key_dicts = [seg.columns[c].dictionary for c in plan.query.group_by]
+        rows = {}
+        for g in range(G):
+            key = tuple(_py(key_dicts[k].values[int(keys[g, k])]) for k in range(K))
+            row = []
+            for a, ag in enumerate(aggs):
+                f = ag.function
+                v = float(vals[g, a])
+                if f in ("COUNT", "COUNTMV"):
+                    row.append(int(v))
+                elif f == "AVG":
+                    row.append((v, int(cnts[g, a])))
+                elif f == "DISTINCTCOUNT":
+                    dct = seg.columns[ag.arg.cols[0]].dictionary
+                    row.append({_py(dct.values[i]) for i in distinct.get(g * A + a, [])})
+                else:
+                    row.append(v)
+            rows[key] = row
+        s = r.stats
+        st = ExecutionStats(s.num_docs_scanned, s.num_entries_scanned_in_filter, s.num_entries_scanned_post_filter,
+                            s.num_total_docs, s.num_segments_processed, s.num_segments_matched)
+        return rows, st
+
+    def execute(self, table: Table, query, segments: Optional[Sequence[ImmutableSegment]] = None,
+                num_groups_limit=None) -> IntermediateResult:
+        if isinstance(query, str):
+            query = parse(query)
+        segments = list(table.segments if segments is None else segments)
+        plan = CPlan(table, query, segments, list(range(1, len(segments) + 1)), num_groups_limit)
+        return self.run_plan(plan, segments)
+
+    def run_plan(self, plan: CPlan, segments: Sequence[ImmutableSegment]) -> IntermediateResult:
+        if self.threads > 1:
+            with ThreadPoolExecutor(self.threads) as ex:
+                parts = list(ex.map(lambda i: self.run_segment(plan, i, segments[i]), range(len(segments))))
+        else:
+            parts = [self.run_segment(plan, i, s) for i, s in enumerate(segments)]
+        merged = {}
+        stats = ExecutionStats()
+        for rows, st in parts:
+            for k, v in rows.items():
+                merged[k] = merge_intermediate(plan.aggs, merged[k], v) if k in merged else v
+            for f in stats.__dataclass_fields__:
+                setattr(stats, f, getattr(stats, f) + getattr(st, f))
+        if not plan.query.group_by and () not in merged:
+            merged[()] = None
+        return IntermediateResult(plan.aggs, list(plan.query.group_by), merged, stats)
+
+
+def _py(v):
+    if isinstance(v, (np.integer,)):
+        return int(v)
+    if isinstance(v, (np.floating,)):
+        return float(v)
+    return v

@@ -1,0 +1,643 @@
+/*
+ * pinot_oracle.c -- CPU restatement of Pinot's per-segment filter -> projection -> aggregation /
+ * group-by path.  TEST INFRASTRUCTURE ONLY: linked only by tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py, as the checker.  It is never the thing measured or shipped.
+ *
+ * Pinning: its results are checked against the reference's own known answers on the reference's
+ * own fixture (test_data-sv.avro -> tests/golden), see tests/test_oracle_golden.py and
+ * tests/golden/expected.json.  Roaring decoding follows the published portable format of
+ * RoaringBitmap 0.9.28 (not vendored in the reference; round-trip only -> parity unpinned there).
+ *
+ * It consumes the reference's ON-DISK byte layouts (big-endian) and the lowered plan structs of
+ * include/pinot_gpu.h (leaf predicates already in dictId space, as PredicateEvaluatorProvider
+ * produces them).  Each function cites the reference code it follows (paths under navina/pinot).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/pinot_gpu.h"
+
+#define MAX_DOC_PER_CALL 10000 /* plan/DocIdSetPlanNode.java:29 */
+#define ORC_FWD_SV 0
+#define ORC_FWD_SORTED 1
+#define ORC_FWD_MV 2
+
+typedef struct orc_column {
+  const uint8_t *dict;   /* BE fixed-width values */
+  const uint8_t *fwd;    /* forward index bytes (layout by fwd_kind) */
+  const uint8_t *inv;    /* bitmap inverted index bytes or NULL */
+  uint64_t inv_bytes;
+  const int32_t *keymap; /* optional dictId -> global key (native) */
+  uint32_t fwd_kind;     /* ORC_FWD_* */
+  uint32_t data_type;    /* pg_data_type */
+  uint32_t num_docs;
+  uint32_t cardinality;
+  uint32_t bits;
+  uint32_t num_values;
+  uint32_t entry_bytes;
+  uint32_t pad;
+} orc_column;
+
+typedef struct orc_segment_result {
+  pg_stats stats;
+  uint64_t num_groups;
+  uint32_t num_keys, num_aggs;
+  int32_t *key_dict_ids;   /* [num_groups][num_keys] segment-local dictIds */
+  double *values;          /* [num_groups][num_aggs] */
+  int64_t *counts;         /* [num_groups][num_aggs] (AVG count) */
+  /* DISTINCTCOUNT: per (group, agg) list of dictIds present, flattened */
+  uint64_t num_distinct;   /* entries in distinct_* */
+  uint64_t *distinct_group_agg; /* group * num_aggs + agg */
+  int32_t *distinct_dict_ids;
+} orc_segment_result;
+
+/* ------------------------------------------------------------------ readers */
+
+static inline uint32_t be32(const uint8_t *p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+static inline uint64_t be64(const uint8_t *p) { return ((uint64_t)be32(p) << 32) | be32(p + 4); }
+
+/* PinotDataBitSet.readInt (io/util/PinotDataBitSet.java:72-95): value `index` of `b` bits, MSB first. */
+static inline uint32_t read_bits(const uint8_t *buf, uint64_t index, uint32_t b) {
+  uint64_t bit_offset = index * (uint64_t)b;
+  uint64_t byte_offset = bit_offset >> 3;
+  uint32_t bit_in_first = (uint32_t)(bit_offset & 7);
+  uint64_t cur = buf[byte_offset] & (0xFFu >> bit_in_first);
+  int left = (int)b - (8 - (int)bit_in_first);
+  if (left <= 0) return (uint32_t)(cur >> (-left));
+  while (left > 8) {
+    byte_offset++;
+    cur = (cur << 8) | buf[byte_offset];
+    left -= 8;
+  }
+  return (uint32_t)((cur << left) | (buf[byte_offset + 1] >> (8 - left)));
+}
+
+/* PinotDataBitSet bit test (MSB-first in each byte). */
+static inline int bit_is_set(const uint8_t *bm, uint64_t i) { return (bm[i >> 3] >> (7 - (i & 7))) & 1; }
+
+/* Dictionary value as double: Dictionary.getDoubleValue (IntDictionary/LongDictionary/... ). */
+static inline double dict_double(const orc_column *c, int32_t id) {
+  const uint8_t *p = c->dict + (uint64_t)id * c->entry_bytes;
+  switch (c->data_type) {
+    case PG_INT: return (double)(int32_t)be32(p);
+    case PG_LONG: return (double)(int64_t)be64(p);
+    case PG_FLOAT: { uint32_t u = be32(p); float f; memcpy(&f, &u, 4); return (double)f; }
+    case PG_DOUBLE: { uint64_t u = be64(p); double d; memcpy(&d, &u, 8); return d; }
+    default: return NAN;
+  }
+}
+
+/* Per-doc SV dictIds: FixedBitSVForwardIndexReaderV2.readDictIds (readers/forward/FixedBitSVForwardIndexReaderV2.java:62-97)
+ * or, for sorted columns, SortedIndexReaderImpl.getDictId (readers/sorted/SortedIndexReaderImpl.java:82-112). */
+static int32_t *sv_dict_ids(const orc_column *c) {
+  int32_t *ids = (int32_t *)malloc(sizeof(int32_t) * (c->num_docs ? c->num_docs : 1));
+  if (c->fwd_kind == ORC_FWD_SV) {
+    for (uint32_t d = 0; d < c->num_docs; d++) ids[d] = (int32_t)read_bits(c->fwd, d, c->bits);
+  } else {
+    for (uint32_t id = 0; id < c->cardinality; id++) {
+      int32_t s = (int32_t)be32(c->fwd + 8ull * id), e = (int32_t)be32(c->fwd + 8ull * id + 4);
+      for (int32_t d = s; d <= e; d++) ids[d] = (int32_t)id;
+    }
+  }
+  return ids;
+}
+
+/* MV row offsets from the start-of-row bitmap (FixedBitMVForwardIndexReader.java:61-75, getNumValuesMV
+ * :167-204): docsPerChunk = ceil((float) 2048 / (numValues / numDocs)); chunk offsets header, then a
+ * bitmap of numValues bits with a set bit at each row start, then the packed values. */
+typedef struct { const uint8_t *bitmap; const uint8_t *raw; uint64_t *offsets; } mv_view;
+static void mv_open(const orc_column *c, mv_view *v) {
+  uint32_t nd = c->num_docs, nv = c->num_values;
+  uint32_t avg = nd ? nv / nd : 0;
+  uint32_t dpc = avg ? (uint32_t)ceilf(2048.0f / (float)avg) : 2048u;
+  uint32_t nchunks = (nd + dpc - 1) / dpc;
+  uint64_t bitmap_bytes = ((uint64_t)nv + 7) / 8;
+  v->bitmap = c->fwd + 4ull * nchunks;
+  v->raw = v->bitmap + bitmap_bytes;
+  v->offsets = (uint64_t *)malloc(sizeof(uint64_t) * (nd + 1ull));
+  uint64_t doc = 0;
+  for (uint64_t i = 0; i < nv; i++)
+    if (bit_is_set(v->bitmap, i)) v->offsets[doc++] = i;
+  v->offsets[nd] = nv;
+}
+
+/* Portable RoaringBitmap decode (RoaringBitmap 0.9.28 serialization spec) into a doc flag array;
+ * used by BitmapInvertedIndexReader.getDocIds (readers/BitmapInvertedIndexReader.java:54-63). */
+static void roaring_or_into(const uint8_t *b, uint8_t *flags, uint32_t num_docs) {
+  uint32_t cookie = (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
+  uint32_t size, pos;
+  const uint8_t *run_flags = NULL;
+  if ((cookie & 0xFFFF) == 12347) {
+    size = (cookie >> 16) + 1;
+    pos = 4;
+    run_flags = b + pos;
+    pos += (size + 7) / 8;
+  } else {
+    size = (uint32_t)b[4] | ((uint32_t)b[5] << 8) | ((uint32_t)b[6] << 16) | ((uint32_t)b[7] << 24);
+    pos = 8;
+  }
+  uint32_t hdr = pos;
+  pos += 4 * size;
+  int has_offsets = (run_flags == NULL) || size >= 4;
+  uint32_t off_pos = pos;
+  if (has_offsets) pos += 4 * size;
+  uint32_t cur = pos;
+  for (uint32_t i = 0; i < size; i++) {
+    uint32_t key = (uint32_t)b[hdr + 4 * i] | ((uint32_t)b[hdr + 4 * i + 1] << 8);
+    uint32_t card = ((uint32_t)b[hdr + 4 * i + 2] | ((uint32_t)b[hdr + 4 * i + 3] << 8)) + 1;
+    if (has_offsets) {
+      const uint8_t *o = b + off_pos + 4 * i;
+      cur = (uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16) | ((uint32_t)o[3] << 24);
+    }
+    uint32_t base = key << 16;
+    int is_run = run_flags && ((run_flags[i / 8] >> (i % 8)) & 1);
+    if (is_run) {
+      uint32_t nruns = (uint32_t)b[cur] | ((uint32_t)b[cur + 1] << 8);
+      for (uint32_t r = 0; r < nruns; r++) {
+        const uint8_t *q = b + cur + 2 + 4 * r;
+        uint32_t s = (uint32_t)q[0] | ((uint32_t)q[1] << 8), l = (uint32_t)q[2] | ((uint32_t)q[3] << 8);
+        for (uint32_t x = s; x <= s + l; x++)
+          if (base + x < num_docs) flags[base + x] = 1;
+      }
+      cur += 2 + 4 * nruns;
+    } else if (card <= 4096) {
+      for (uint32_t j = 0; j < card; j++) {
+        uint32_t x = (uint32_t)b[cur + 2 * j] | ((uint32_t)b[cur + 2 * j + 1] << 8);
+        if (base + x < num_docs) flags[base + x] = 1;
+      }
+      cur += 2 * card;
+    } else {
+      for (uint32_t w = 0; w < 1024; w++) {
+        uint64_t word = 0;
+        for (int k = 7; k >= 0; k--) word = (word << 8) | b[cur + 8 * w + k];
+        while (word) {
+          int t = __builtin_ctzll(word);
+          uint32_t x = base + w * 64 + (uint32_t)t;
+          if (x < num_docs) flags[x] = 1;
+          word &= word - 1;
+        }
+      }
+      cur += 8192;
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ filter */
+
+static int leaf_in_set(const pg_leaf *l, int32_t id) {
+  if (l->num_ids == 0) return id >= l->lo && id < l->hi;
+  /* IntOpenHashSet.contains -> binary search over the sorted id list (same membership) */
+  int32_t lo = 0, hi = (int32_t)l->num_ids - 1;
+  while (lo <= hi) {
+    int32_t mid = (lo + hi) >> 1;
+    if (l->ids[mid] < id) lo = mid + 1;
+    else if (l->ids[mid] > id) hi = mid - 1;
+    else return 1;
+  }
+  return 0;
+}
+
+/* One leaf -> doc flags.  Scan: SVScanDocIdIterator / MVScanDocIdIterator with PredicateEvaluator.applySV /
+ * applyMV (dociditerators/SVScanDocIdIterator.java:67-125, MVScanDocIdIterator.java:59-104,
+ * predicate/BaseDictionaryBasedPredicateEvaluator.java:133-150).  Sorted: SortedIndexBasedFilterOperator
+ * (filter/SortedIndexBasedFilterOperator.java:51-138).  Inverted: BitmapBasedFilterOperator
+ * (filter/BitmapBasedFilterOperator.java:66-115: OR of the matching dictIds' bitmaps, flip if exclusive). */
+static void eval_leaf(const pg_leaf *l, const orc_column *cols, uint32_t num_docs, uint8_t *out,
+                      uint64_t *entries_scanned) {
+  const orc_column *c = &cols[l->col_id];
+  switch (l->kind) {
+    case PG_LEAF_MATCH_ALL: memset(out, 1, num_docs); return;
+    case PG_LEAF_EMPTY: memset(out, 0, num_docs); return;
+    case PG_LEAF_SV_SCAN: {
+      int32_t *ids = sv_dict_ids(c);
+      for (uint32_t d = 0; d < num_docs; d++) out[d] = (uint8_t)(leaf_in_set(l, ids[d]) ^ (l->exclusive != 0));
+      *entries_scanned += num_docs;
+      free(ids);
+      return;
+    }
+    case PG_LEAF_MV_SCAN: {
+      mv_view v;
+      mv_open(c, &v);
+      for (uint32_t d = 0; d < num_docs; d++) {
+        int any = 0;
+        for (uint64_t i = v.offsets[d]; i < v.offsets[d + 1]; i++) {
+          if (leaf_in_set(l, (int32_t)read_bits(v.raw, i, c->bits))) { any = 1; break; }
+        }
+        out[d] = (uint8_t)(any ^ (l->exclusive != 0));
+        *entries_scanned += v.offsets[d + 1] - v.offsets[d];
+      }
+      free(v.offsets);
+      return;
+    }
+    case PG_LEAF_SORTED: {
+      memset(out, 0, num_docs);
+      for (uint32_t id = 0; id < c->cardinality; id++) {
+        if (!leaf_in_set(l, (int32_t)id)) continue;
+        int32_t s = (int32_t)be32(c->fwd + 8ull * id), e = (int32_t)be32(c->fwd + 8ull * id + 4);
+        for (int32_t d = s; d <= e; d++) out[d] = 1;
+      }
+      if (l->exclusive)
+        for (uint32_t d = 0; d < num_docs; d++) out[d] ^= 1;
+      return;
+    }
+    case PG_LEAF_INVERTED: {
+      memset(out, 0, num_docs);
+      uint32_t n = c->cardinality;
+      uint32_t first = be32(c->inv);
+      const uint8_t *bitmaps = c->inv + 4ull * (n + 1);
+      for (uint32_t id = 0; id < n; id++) {
+        if (!leaf_in_set(l, (int32_t)id)) continue;
+        uint32_t o = be32(c->inv + 4ull * id);
+        roaring_or_into(bitmaps + (o - first), out, num_docs);
+      }
+      if (l->exclusive)
+        for (uint32_t d = 0; d < num_docs; d++) out[d] ^= 1;
+      return;
+    }
+  }
+}
+
+/* Postfix program over leaf doc-sets: AndFilterOperator / OrFilterOperator / NotFilterOperator
+ * (filter/AndFilterOperator.java:42-49, OrFilterOperator.java:44-82, NotFilterOperator.java:53-77). */
+static int eval_filter(const pg_plan *plan, const pg_leaf *leaves, const orc_column *cols, uint32_t num_docs,
+                       uint8_t *match, uint64_t *entries_scanned) {
+  if (plan->num_ops == 0) { memset(match, 1, num_docs); return 0; }
+  uint8_t **stack = (uint8_t **)calloc(plan->num_ops + 1, sizeof(uint8_t *));
+  int sp = 0;
+  for (uint32_t i = 0; i < plan->num_ops; i++) {
+    int32_t op = plan->ops[i];
+    if (op >= 0) {
+      uint8_t *f = (uint8_t *)malloc(num_docs ? num_docs : 1);
+      eval_leaf(&leaves[op], cols, num_docs, f, entries_scanned);
+      stack[sp++] = f;
+    } else if (op == PG_OP_NOT) {
+      uint8_t *f = stack[sp - 1];
+      for (uint32_t d = 0; d < num_docs; d++) f[d] ^= 1;
+    } else {
+      int n = (-op) & 0xFF;
+      int is_and = ((-op) & 0x100) != 0;
+      uint8_t *dst = stack[sp - n];
+      for (int k = 1; k < n; k++) {
+        uint8_t *src = stack[sp - n + k];
+        if (is_and) for (uint32_t d = 0; d < num_docs; d++) dst[d] &= src[d];
+        else for (uint32_t d = 0; d < num_docs; d++) dst[d] |= src[d];
+        free(src);
+      }
+      sp -= n - 1;
+    }
+  }
+  memcpy(match, stack[0], num_docs);
+  free(stack[0]);
+  free(stack);
+  return 0;
+}
+
+/* ------------------------------------------------------------------ aggregation */
+
+typedef struct agg_input {
+  int32_t *ids_a, *ids_b;   /* SV dictIds */
+  mv_view mv;               /* COUNTMV */
+  int has_mv;
+} agg_input;
+
+/* Transform value: TransformFunction.transformToDoubleValuesSV; MultiplicationTransformFunction
+ * (transform/function/MultiplicationTransformFunction.java:91-111) starts from the literal product 1.0
+ * and multiplies the arguments in order. */
+static inline double agg_value(const pg_agg *a, const orc_column *cols, const agg_input *in, uint32_t d) {
+  double va = dict_double(&cols[a->col_a], in->ids_a[d]);
+  switch (a->op) {
+    case PG_EXPR_MUL: { double p = 1.0; p = p * va; p = p * dict_double(&cols[a->col_b], in->ids_b[d]); return p; }
+    case PG_EXPR_ADD: return va + dict_double(&cols[a->col_b], in->ids_b[d]);
+    case PG_EXPR_SUB: return va - dict_double(&cols[a->col_b], in->ids_b[d]);
+    default: return va;
+  }
+}
+
+static int is_integer_type(uint32_t t) { return t == PG_INT || t == PG_LONG; }
+
+/* Aggregation-only over the matching docs in blocks of MAX_DOC_PER_CALL, exactly as AggregationOperator
+ * (operator/query/AggregationOperator.java:60-89) drives DefaultAggregationExecutor.aggregate.  Per-block
+ * reductions follow each function's aggregate(): Sum (SumAggregationFunction.java:71-126), Min/Max
+ * (MinAggregationFunction.java:71-126 -- integer min within a block for INT/LONG inputs, then Math.min
+ * with the double holder), Avg (AvgAggregationFunction.java:76-82 -- block sum then AvgPair.apply),
+ * Count (CountAggregationFunction.java:87-111), CountMV (CountMVAggregationFunction.java:64-95),
+ * DistinctCount (DistinctCountAggregationFunction.java:66-128 -- RoaringBitmap of dictIds). */
+static void aggregate_only(const pg_plan *plan, const orc_column *cols, const uint32_t *docs, uint64_t n,
+                           agg_input *inputs, orc_segment_result *r) {
+  uint32_t A = plan->num_aggs;
+  r->num_groups = 1;
+  r->values = (double *)calloc(A ? A : 1, sizeof(double));
+  r->counts = (int64_t *)calloc(A ? A : 1, sizeof(int64_t));
+  uint8_t **distinct = (uint8_t **)calloc(A ? A : 1, sizeof(uint8_t *));
+  for (uint32_t a = 0; a < A; a++) {
+    const pg_agg *g = &plan->aggs[a];
+    if (g->fn == PG_AGG_MIN) r->values[a] = INFINITY;   /* DEFAULT_INITIAL_VALUE */
+    if (g->fn == PG_AGG_MAX) r->values[a] = -INFINITY;
+    if (g->fn == PG_AGG_DISTINCTCOUNT) distinct[a] = (uint8_t *)calloc(cols[g->col_a].cardinality + 1, 1);
+  }
+  for (uint64_t b0 = 0; b0 < n; b0 += MAX_DOC_PER_CALL) {
+    uint64_t b1 = b0 + MAX_DOC_PER_CALL < n ? b0 + MAX_DOC_PER_CALL : n;
+    uint64_t len = b1 - b0;
+    for (uint32_t a = 0; a < A; a++) {
+      const pg_agg *g = &plan->aggs[a];
+      agg_input *in = &inputs[a];
+      switch (g->fn) {
+        case PG_AGG_COUNT: r->values[a] += (double)len; break;
+        case PG_AGG_COUNTMV: {
+          double s = 0;
+          for (uint64_t i = b0; i < b1; i++) s += (double)(in->mv.offsets[docs[i] + 1] - in->mv.offsets[docs[i]]);
+          r->values[a] += s;
+          break;
+        }
+        case PG_AGG_SUM: { /* running double sum carried through the holder (SumAggregationFunction.java:82-124) */
+          double s = r->values[a];
+          for (uint64_t i = b0; i < b1; i++) s += agg_value(g, cols, in, docs[i]);
+          r->values[a] = s;
+          break;
+        }
+        case PG_AGG_AVG: { /* block-local sum, then AvgPair.apply (AvgAggregationFunction.java:76-82,132-139) */
+          double s = 0.0;
+          for (uint64_t i = b0; i < b1; i++) s += agg_value(g, cols, in, docs[i]);
+          r->values[a] += s;
+          r->counts[a] += (int64_t)len;
+          break;
+        }
+        case PG_AGG_MIN: case PG_AGG_MAX: {
+          int is_min = g->fn == PG_AGG_MIN;
+          double m;
+          if (g->op == PG_EXPR_COL && is_integer_type(cols[g->col_a].data_type)) {
+            /* integer path: Math.min over int/long values, then with the double holder */
+            double v0 = dict_double(&cols[g->col_a], in->ids_a[docs[b0]]);
+            m = v0;
+            for (uint64_t i = b0; i < b1; i++) {
+              double v = dict_double(&cols[g->col_a], in->ids_a[docs[i]]);
+              m = is_min ? (v < m ? v : m) : (v > m ? v : m);
+            }
+          } else {
+            m = agg_value(g, cols, in, docs[b0]);
+            for (uint64_t i = b0; i < b1; i++) {
+              double v = agg_value(g, cols, in, docs[i]);
+              m = is_min ? fmin(v, m) : fmax(v, m);
+            }
+          }
+          r->values[a] = is_min ? fmin(m, r->values[a]) : fmax(m, r->values[a]);
+          break;
+        }
+        case PG_AGG_DISTINCTCOUNT:
+          for (uint64_t i = b0; i < b1; i++) distinct[a][in->ids_a[docs[i]]] = 1;
+          break;
+      }
+    }
+  }
+  /* export DISTINCTCOUNT dictId sets */
+  uint64_t nd = 0;
+  for (uint32_t a = 0; a < A; a++)
+    if (distinct[a])
+      for (uint32_t id = 0; id < cols[plan->aggs[a].col_a].cardinality; id++) nd += distinct[a][id];
+  r->num_distinct = nd;
+  r->distinct_group_agg = (uint64_t *)malloc(sizeof(uint64_t) * (nd ? nd : 1));
+  r->distinct_dict_ids = (int32_t *)malloc(sizeof(int32_t) * (nd ? nd : 1));
+  nd = 0;
+  for (uint32_t a = 0; a < A; a++) {
+    if (!distinct[a]) continue;
+    uint32_t cnt = 0;
+    for (uint32_t id = 0; id < cols[plan->aggs[a].col_a].cardinality; id++)
+      if (distinct[a][id]) { r->distinct_group_agg[nd] = a; r->distinct_dict_ids[nd++] = (int32_t)id; cnt++; }
+    r->values[a] = (double)cnt;
+    free(distinct[a]);
+  }
+  free(distinct);
+}
+
+/* ---- group-by: DictionaryBasedGroupKeyGenerator (query/aggregation/groupby/DictionaryBasedGroupKeyGenerator.java)
+ * raw key = sum_k dictId_k * prod_{j<k} card_j (:280-322); ArrayBasedHolder when prod <= arrayBasedThreshold
+ * (group id = raw key, :253-382); otherwise map-based holders (:384-673, IntGroupIdMap :961-1110) that
+ * assign group ids in first-seen doc order and return INVALID_ID (-1, GroupKeyGenerator.java:30) once
+ * numGroupsLimit groups exist; DoubleGroupByResultHolder drops writes to INVALID_ID. */
+typedef struct { uint64_t *keys; int32_t *ids; uint64_t cap, n; } id_map; /* open addressing raw key -> group id */
+static uint64_t mix64(uint64_t x) { x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33; return x; }
+static int32_t map_get_or_put(id_map *m, uint64_t key, uint64_t limit) {
+  uint64_t mask = m->cap - 1, h = mix64(key) & mask;
+  while (m->ids[h] >= 0) {
+    if (m->keys[h] == key) return m->ids[h];
+    h = (h + 1) & mask;
+  }
+  if (m->n >= limit) return -1;
+  if ((m->n + 1) * 2 > m->cap) {  /* grow */
+    id_map nm = {0};
+    nm.cap = m->cap * 2;
+    nm.keys = (uint64_t *)malloc(nm.cap * 8);
+    nm.ids = (int32_t *)malloc(nm.cap * 4);
+    for (uint64_t i = 0; i < nm.cap; i++) nm.ids[i] = -1;
+    for (uint64_t i = 0; i < m->cap; i++)
+      if (m->ids[i] >= 0) {
+        uint64_t hh = mix64(m->keys[i]) & (nm.cap - 1);
+        while (nm.ids[hh] >= 0) hh = (hh + 1) & (nm.cap - 1);
+        nm.keys[hh] = m->keys[i];
+        nm.ids[hh] = m->ids[i];
+      }
+    nm.n = m->n;
+    free(m->keys); free(m->ids);
+    *m = nm;
+    mask = m->cap - 1;
+    h = mix64(key) & mask;
+    while (m->ids[h] >= 0) h = (h + 1) & mask;
+  }
+  m->keys[h] = key;
+  m->ids[h] = (int32_t)m->n;
+  return (int32_t)m->n++;
+}
+
+static void aggregate_group_by(const pg_plan *plan, const orc_column *cols, const uint32_t *docs, uint64_t n,
+                               agg_input *inputs, int32_t **key_ids, orc_segment_result *r,
+                               uint64_t array_based_threshold) {
+  uint32_t K = plan->num_keys, A = plan->num_aggs;
+  uint64_t card_prod = 1;
+  int overflow = 0;
+  uint64_t cards[64];
+  for (uint32_t k = 0; k < K; k++) {
+    cards[k] = cols[plan->keys[k].col_id].cardinality;
+    if (card_prod > UINT64_MAX / (cards[k] ? cards[k] : 1)) overflow = 1; else card_prod *= cards[k];
+  }
+  uint64_t limit = plan->num_groups_limit ? plan->num_groups_limit : 100000;
+  int array_based = !overflow && card_prod <= array_based_threshold;
+  uint64_t upper = array_based ? card_prod : limit;
+  id_map m = {0};
+  if (!array_based) {
+    m.cap = 1024;
+    m.keys = (uint64_t *)malloc(m.cap * 8);
+    m.ids = (int32_t *)malloc(m.cap * 4);
+    for (uint64_t i = 0; i < m.cap; i++) m.ids[i] = -1;
+  }
+  /* per-doc group ids in doc order (first-seen assignment) */
+  int32_t *gids = (int32_t *)malloc(sizeof(int32_t) * (n ? n : 1));
+  uint64_t *raw_of_gid = NULL;
+  uint8_t *seen = array_based ? (uint8_t *)calloc(upper ? upper : 1, 1) : NULL;
+  for (uint64_t i = 0; i < n; i++) {
+    uint32_t d = docs[i];
+    uint64_t raw = 0;
+    for (int k = (int)K - 1; k >= 0; k--) raw = raw * cards[k] + (uint64_t)key_ids[k][d];
+    if (array_based) { gids[i] = (int32_t)raw; seen[raw] = 1; }
+    else gids[i] = map_get_or_put(&m, raw, limit);
+  }
+  uint64_t G = array_based ? upper : m.n;
+  raw_of_gid = (uint64_t *)malloc(sizeof(uint64_t) * (G ? G : 1));
+  if (array_based) for (uint64_t g = 0; g < G; g++) raw_of_gid[g] = g;
+  else for (uint64_t i = 0; i < m.cap; i++) if (m.ids[i] >= 0) raw_of_gid[m.ids[i]] = m.keys[i];
+
+  double *vals = (double *)calloc((G ? G : 1) * (A ? A : 1), sizeof(double));
+  int64_t *cnts = (int64_t *)calloc((G ? G : 1) * (A ? A : 1), sizeof(int64_t));
+  uint8_t *dflags = NULL;
+  uint64_t dcard = 0;
+  for (uint32_t a = 0; a < A; a++) {
+    if (plan->aggs[a].fn == PG_AGG_MIN) for (uint64_t g = 0; g < G; g++) vals[g * A + a] = INFINITY;
+    if (plan->aggs[a].fn == PG_AGG_MAX) for (uint64_t g = 0; g < G; g++) vals[g * A + a] = -INFINITY;
+    if (plan->aggs[a].fn == PG_AGG_DISTINCTCOUNT && cols[plan->aggs[a].col_a].cardinality > dcard)
+      dcard = cols[plan->aggs[a].col_a].cardinality;
+  }
+  if (dcard) dflags = (uint8_t *)calloc((G ? G : 1) * A * dcard, 1);
+  /* aggregateGroupBySV: holder[groupId] op= value for each doc (e.g. SumAggregationFunction.java:205-237) */
+  for (uint64_t i = 0; i < n; i++) {
+    int32_t g = gids[i];
+    if (g < 0) continue;
+    uint32_t d = docs[i];
+    for (uint32_t a = 0; a < A; a++) {
+      const pg_agg *ag = &plan->aggs[a];
+      double *v = &vals[(uint64_t)g * A + a];
+      switch (ag->fn) {
+        case PG_AGG_COUNT: *v += 1.0; break;
+        case PG_AGG_COUNTMV: *v += (double)(inputs[a].mv.offsets[d + 1] - inputs[a].mv.offsets[d]); break;
+        case PG_AGG_SUM: *v += agg_value(ag, cols, &inputs[a], d); break;
+        case PG_AGG_AVG: *v += agg_value(ag, cols, &inputs[a], d); cnts[(uint64_t)g * A + a] += 1; break;
+        case PG_AGG_MIN: { double x = agg_value(ag, cols, &inputs[a], d); if (x < *v) *v = x; break; }
+        case PG_AGG_MAX: { double x = agg_value(ag, cols, &inputs[a], d); if (x > *v) *v = x; break; }
+        case PG_AGG_DISTINCTCOUNT: dflags[((uint64_t)g * A + a) * dcard + inputs[a].ids_a[d]] = 1; break;
+      }
+    }
+  }
+  /* export groups that received at least one doc */
+  uint8_t *present = (uint8_t *)calloc(G ? G : 1, 1);
+  for (uint64_t i = 0; i < n; i++) if (gids[i] >= 0) present[gids[i]] = 1;
+  uint64_t ng = 0;
+  for (uint64_t g = 0; g < G; g++) ng += present[g];
+  r->num_groups = ng;
+  r->key_dict_ids = (int32_t *)malloc(sizeof(int32_t) * (ng ? ng : 1) * (K ? K : 1));
+  r->values = (double *)malloc(sizeof(double) * (ng ? ng : 1) * (A ? A : 1));
+  r->counts = (int64_t *)malloc(sizeof(int64_t) * (ng ? ng : 1) * (A ? A : 1));
+  uint64_t nd = 0;
+  if (dflags)
+    for (uint64_t g = 0; g < G; g++)
+      if (present[g])
+        for (uint32_t a = 0; a < A; a++)
+          if (plan->aggs[a].fn == PG_AGG_DISTINCTCOUNT)
+            for (uint64_t x = 0; x < dcard; x++) nd += dflags[((uint64_t)g * A + a) * dcard + x];
+  r->num_distinct = nd;
+  r->distinct_group_agg = (uint64_t *)malloc(sizeof(uint64_t) * (nd ? nd : 1));
+  r->distinct_dict_ids = (int32_t *)malloc(sizeof(int32_t) * (nd ? nd : 1));
+  uint64_t o = 0, di = 0;
+  for (uint64_t g = 0; g < G; g++) {
+    if (!present[g]) continue;
+    uint64_t raw = raw_of_gid[g];
+    for (uint32_t k = 0; k < K; k++) { r->key_dict_ids[o * K + k] = (int32_t)(raw % cards[k]); raw /= cards[k]; }
+    for (uint32_t a = 0; a < A; a++) {
+      r->values[o * A + a] = vals[g * A + a];
+      r->counts[o * A + a] = cnts[g * A + a];
+      if (plan->aggs[a].fn == PG_AGG_DISTINCTCOUNT) {
+        uint32_t cnt = 0;
+        for (uint64_t x = 0; x < dcard; x++)
+          if (dflags[(g * A + a) * dcard + x]) {
+            r->distinct_group_agg[di] = o * A + a;
+            r->distinct_dict_ids[di++] = (int32_t)x;
+            cnt++;
+          }
+        r->values[o * A + a] = (double)cnt;
+      }
+    }
+    o++;
+  }
+  free(present); free(vals); free(cnts); free(dflags); free(gids); free(raw_of_gid); free(seen);
+  if (!array_based) { free(m.keys); free(m.ids); }
+}
+
+/* ------------------------------------------------------------------ entry points */
+
+/* Execute `plan` on ONE segment (segment index `seg` of the plan), columns indexed by col_id.
+ * array_based_threshold = InstancePlanMakerImplV2 max.init.group.holder.capacity (10 000). */
+int orc_execute_segment(const pg_plan *plan, uint32_t seg, const orc_column *cols, uint64_t array_based_threshold,
+                        orc_segment_result **out) {
+  const pg_segment_ref *s = &plan->segments[seg];
+  uint32_t nd = s->num_docs;
+  orc_segment_result *r = (orc_segment_result *)calloc(1, sizeof(orc_segment_result));
+  r->num_keys = plan->num_keys;
+  r->num_aggs = plan->num_aggs;
+  uint8_t *match = (uint8_t *)malloc(nd ? nd : 1);
+  uint64_t scanned = 0;
+  eval_filter(plan, s->leaves, cols, nd, match, &scanned);
+  uint64_t n = 0;
+  for (uint32_t d = 0; d < nd; d++) n += match[d];
+  uint32_t *docs = (uint32_t *)malloc(sizeof(uint32_t) * (n ? n : 1));
+  n = 0;
+  for (uint32_t d = 0; d < nd; d++) if (match[d]) docs[n++] = d;
+  free(match);
+
+  /* projection: decode the columns the aggregations / group-by read */
+  agg_input *inputs = (agg_input *)calloc(plan->num_aggs ? plan->num_aggs : 1, sizeof(agg_input));
+  uint32_t projected = 0;
+  uint8_t used[256] = {0};
+  for (uint32_t a = 0; a < plan->num_aggs; a++) {
+    const pg_agg *g = &plan->aggs[a];
+    if (g->fn == PG_AGG_COUNT) continue;
+    if (g->fn == PG_AGG_COUNTMV) { mv_open(&cols[g->col_a], &inputs[a].mv); inputs[a].has_mv = 1; used[g->col_a] = 1; continue; }
+    inputs[a].ids_a = sv_dict_ids(&cols[g->col_a]);
+    used[g->col_a] = 1;
+    if (g->op != PG_EXPR_COL) { inputs[a].ids_b = sv_dict_ids(&cols[g->col_b]); used[g->col_b] = 1; }
+  }
+  int32_t *key_ids[64] = {0};
+  for (uint32_t k = 0; k < plan->num_keys; k++) {
+    key_ids[k] = sv_dict_ids(&cols[plan->keys[k].col_id]);
+    used[plan->keys[k].col_id] = 1;
+  }
+  for (int i = 0; i < 256; i++) projected += used[i];
+
+  if (plan->num_keys == 0) aggregate_only(plan, cols, docs, n, inputs, r);
+  else aggregate_group_by(plan, cols, docs, n, inputs, key_ids, r, array_based_threshold);
+
+  r->stats.num_docs_scanned = n;
+  r->stats.num_entries_scanned_in_filter = scanned;
+  r->stats.num_entries_scanned_post_filter = n * projected; /* AggregationOperator.java:84-89 */
+  r->stats.num_total_docs = nd;
+  r->stats.num_segments_processed = 1;
+  r->stats.num_segments_matched = n > 0;
+  for (uint32_t a = 0; a < plan->num_aggs; a++) {
+    free(inputs[a].ids_a); free(inputs[a].ids_b);
+    if (inputs[a].has_mv) free(inputs[a].mv.offsets);
+  }
+  for (uint32_t k = 0; k < plan->num_keys; k++) free(key_ids[k]);
+  free(inputs);
+  free(docs);
+  *out = r;
+  return 0;
+}
+
+void orc_result_free(orc_segment_result *r) {
+  if (!r) return;
+  free(r->key_dict_ids); free(r->values); free(r->counts);
+  free(r->distinct_group_agg); free(r->distinct_dict_ids);
+  free(r);
+}
+
+/* Known-answer helpers for the format tests (FixedBitIntReaderTest / PinotDataBitSetTest style). */
+void orc_unpack(const uint8_t *buf, uint64_t start, uint64_t n, uint32_t b, int32_t *out) {
+  for (uint64_t i = 0; i < n; i++) out[i] = (int32_t)read_bits(buf, start + i, b);
+}
+void orc_roaring_decode(const uint8_t *buf, uint8_t *flags, uint32_t num_docs) { roaring_or_into(buf, flags, num_docs); }
+int orc_num_bits_per_value(int32_t max_value) { /* PinotDataBitSet.getNumBitsPerValue */
+  if (max_value <= 1) return 1;
+  int b = 0;
+  while (max_value > 0) { b++; max_value >>= 1; }
+  return b;
+}

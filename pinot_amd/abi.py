@@ -1,0 +1,123 @@
+"""ctypes mirror of include/pinot_gpu.h (the C ABI).  Shared by the GPU binding and the oracle."""
+import ctypes as C
+
+PG_ABI_VERSION = 1
+
+PG_OK, PG_E_INVALID, PG_E_HIP, PG_E_NOMEM, PG_E_NOTFOUND, PG_E_UNSUPPORTED, PG_E_CANCELLED, PG_E_TIMEOUT, \
+    PG_E_STATE = 0, -1, -2, -3, -4, -5, -6, -7, -8
+STATUS_NAMES = {0: "PG_OK", -1: "PG_E_INVALID", -2: "PG_E_HIP", -3: "PG_E_NOMEM", -4: "PG_E_NOTFOUND",
+                -5: "PG_E_UNSUPPORTED", -6: "PG_E_CANCELLED", -7: "PG_E_TIMEOUT", -8: "PG_E_STATE"}
+
+PG_IDX_DICT, PG_IDX_FWD_SV_BITPACKED, PG_IDX_FWD_SV_SORTED, PG_IDX_FWD_MV_BITPACKED, PG_IDX_INV_BITMAP, \
+    PG_IDX_KEYMAP = 1, 2, 3, 4, 5, 6
+PG_INT, PG_LONG, PG_FLOAT, PG_DOUBLE, PG_STRING, PG_BYTES = 0, 1, 2, 3, 4, 5
+DTYPE_CODES = {"INT": PG_INT, "LONG": PG_LONG, "FLOAT": PG_FLOAT, "DOUBLE": PG_DOUBLE, "STRING": PG_STRING,
+               "BYTES": PG_BYTES}
+PG_SRC_DEVICE = 1
+
+PG_LEAF_MATCH_ALL, PG_LEAF_EMPTY, PG_LEAF_SV_SCAN, PG_LEAF_SORTED, PG_LEAF_INVERTED, PG_LEAF_MV_SCAN = range(6)
+PG_OP_NOT = -1
+
+
+def PG_OP_AND(n):
+    return -(0x100 | n)
+
+
+def PG_OP_OR(n):
+    return -(0x200 | n)
+
+
+PG_AGG_COUNT, PG_AGG_SUM, PG_AGG_MIN, PG_AGG_MAX, PG_AGG_AVG, PG_AGG_DISTINCTCOUNT, PG_AGG_COUNTMV = range(7)
+AGG_CODES = {"COUNT": PG_AGG_COUNT, "SUM": PG_AGG_SUM, "MIN": PG_AGG_MIN, "MAX": PG_AGG_MAX, "AVG": PG_AGG_AVG,
+             "DISTINCTCOUNT": PG_AGG_DISTINCTCOUNT, "COUNTMV": PG_AGG_COUNTMV}
+PG_EXPR_COL, PG_EXPR_MUL, PG_EXPR_ADD, PG_EXPR_SUB = range(4)
+PG_KEY_VALUE_OFFSET, PG_KEY_KEYMAP = 0, 1
+
+
+class pg_col_desc(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("data_type", C.c_uint32), ("num_docs", C.c_uint32),
+                ("cardinality", C.c_uint32), ("bits_per_element", C.c_uint32), ("num_values", C.c_uint32),
+                ("entry_bytes", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class pg_leaf(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("col_id", C.c_uint32), ("exclusive", C.c_uint32), ("num_ids", C.c_uint32),
+                ("lo", C.c_int32), ("hi", C.c_int32), ("ids", C.POINTER(C.c_int32))]
+
+
+class pg_agg(C.Structure):
+    _fields_ = [("fn", C.c_uint32), ("op", C.c_uint32), ("col_a", C.c_uint32), ("col_b", C.c_uint32),
+                ("key_kind", C.c_uint32), ("key_cardinality", C.c_uint32), ("key_base", C.c_int64)]
+
+
+class pg_key(C.Structure):
+    _fields_ = [("col_id", C.c_uint32), ("kind", C.c_uint32), ("cardinality", C.c_uint32), ("pad", C.c_uint32),
+                ("base", C.c_int64)]
+
+
+class pg_segment_ref(C.Structure):
+    _fields_ = [("seg_key", C.c_uint64), ("num_docs", C.c_uint32), ("pad", C.c_uint32),
+                ("leaves", C.POINTER(pg_leaf))]
+
+
+class pg_plan(C.Structure):
+    _fields_ = [("abi_version", C.c_uint32), ("num_segments", C.c_uint32), ("segments", C.POINTER(pg_segment_ref)),
+                ("num_leaves", C.c_uint32), ("num_ops", C.c_uint32), ("ops", C.POINTER(C.c_int32)),
+                ("num_aggs", C.c_uint32), ("num_keys", C.c_uint32), ("aggs", C.POINTER(pg_agg)),
+                ("keys", C.POINTER(pg_key)), ("num_groups_limit", C.c_uint64), ("query_id", C.c_uint64),
+                ("deadline_ms", C.c_int64), ("stream", C.c_void_p)]
+
+
+class pg_stats(C.Structure):
+    _fields_ = [("num_docs_scanned", C.c_uint64), ("num_entries_scanned_in_filter", C.c_uint64),
+                ("num_entries_scanned_post_filter", C.c_uint64), ("num_total_docs", C.c_uint64),
+                ("num_segments_processed", C.c_uint64), ("num_segments_matched", C.c_uint64)]
+
+
+class pg_result(C.Structure):
+    _fields_ = [("stats", pg_stats), ("num_groups", C.c_uint64), ("num_keys", C.c_uint32), ("num_aggs", C.c_uint32),
+                ("keys", C.POINTER(C.c_uint32)), ("values", C.POINTER(C.c_double)),
+                ("counts", C.POINTER(C.c_int64))]
+
+
+class pg_partials(C.Structure):
+    _fields_ = [("stats", pg_stats), ("num_slots", C.c_uint64), ("n_i64", C.c_uint32), ("n_f64", C.c_uint32),
+                ("n_min", C.c_uint32), ("n_max", C.c_uint32), ("flag_bytes_per_slot", C.c_uint64),
+                ("i64", C.c_void_p), ("f64", C.c_void_p), ("mn", C.c_void_p), ("mx", C.c_void_p),
+                ("flags", C.c_void_p), ("impl", C.c_void_p)]
+
+
+class pg_timing(C.Structure):
+    _fields_ = [("prepass_ms", C.c_float), ("scan_ms", C.c_float), ("finalize_ms", C.c_float),
+                ("scan_launches", C.c_uint32), ("pad", C.c_uint32)]
+
+
+# every symbol declared in include/pinot_gpu.h (checked by tests/test_abi.py)
+EXPORTED = ["pg_init", "pg_last_error", "pg_resident_bytes", "pg_cancel", "pg_abi_version", "pg_column_upload",
+            "pg_segment_release", "pg_execute", "pg_result_free", "pg_execute_partial", "pg_partials_finalize",
+            "pg_partials_free", "pg_last_timing"]
+
+
+def declare(lib):
+    """Attach argtypes / restypes to a loaded libpinot_gpu."""
+    P = C.POINTER
+    sigs = {
+        "pg_init": ([C.c_int], C.c_int),
+        "pg_last_error": ([C.c_char_p, C.c_size_t], C.c_int),
+        "pg_resident_bytes": ([P(C.c_uint64)], C.c_int),
+        "pg_cancel": ([C.c_uint64], C.c_int),
+        "pg_abi_version": ([], C.c_int),
+        "pg_column_upload": ([C.c_uint64, C.c_uint32, P(pg_col_desc), C.c_void_p, C.c_uint64], C.c_int),
+        "pg_segment_release": ([C.c_uint64], C.c_int),
+        "pg_execute": ([P(pg_plan), P(P(pg_result))], C.c_int),
+        "pg_result_free": ([P(pg_result)], C.c_int),
+        "pg_execute_partial": ([P(pg_plan), P(P(pg_partials))], C.c_int),
+        "pg_partials_finalize": ([P(pg_partials), P(pg_plan), P(P(pg_result))], C.c_int),
+        "pg_partials_free": ([P(pg_partials)], C.c_int),
+        "pg_last_timing": ([P(pg_timing)], C.c_int),
+    }
+    for name, (args, res) in sigs.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = res
+    return lib

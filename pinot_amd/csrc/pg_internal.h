@@ -1,0 +1,144 @@
+// pg_internal.h -- device-side data layout and kernel interface of libpinot_gpu (gfx950 only).
+//
+// HBM layout of a resident segment column (built once by pg_column_upload):
+//   * bit-packed forward index   : the reference's big-endian stream re-laid as native uint32 words
+//                                  (byte-swapped per 32-bit word), so bit p of the stream is bit
+//                                  31-(p&31) of word p>>5.  +4 zero words of tail padding so a 64-bit
+//                                  window load of the last value never leaves the allocation.
+//                                  Sorted columns get the same packed stream synthesised from their
+//                                  (start,end) pairs, so every column is readable per doc.
+//   * dictionary                 : native typed array (int32 / int64 / float / double).
+//   * MV forward index           : packed values as above + uint32 row offsets[num_docs+1]
+//                                  (selected once from the start-of-row bitmap).
+//   * inverted index             : roaring bytes kept as-is (compressed in HBM) + a container
+//                                  directory (per dictId CSR of {key, type, card, offset}).
+// Per query, a parameter arena (one H2D copy) holds DevLeaf / DevCol tables indexed
+// [segment][leaf] and [segment][agg|key], LUTs for IN / NOT_IN leaves and sorted-index doc ranges.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pinot_gpu.h"
+
+namespace pg {
+
+constexpr int kBlock = 256;                          // 4 waves of 64
+constexpr int kDocsPerThread = 16;                   // docs of a thread in a tile: base + j*256 + tid
+constexpr int kTileDocs = kBlock * kDocsPerThread;   // 4096 docs per tile
+constexpr int kMaxAggs = 8;
+constexpr int kMaxKeys = 4;
+constexpr int kMaxLeaves = 24;
+constexpr int kMaxOps = 48;
+constexpr int kMaxStack = 8;
+constexpr int kLdsGroupBytes = 48 * 1024;            // LDS-privatised group table budget
+
+enum DevLeafKind : uint32_t {
+  DL_ALL = 0,        // match all
+  DL_NONE = 1,       // match none
+  DL_RANGE = 2,      // dictId in [lo,hi) decoded from a packed SV forward index
+  DL_LUT = 3,        // dictId in set: bit dictId of `lut` (native LSB-first words)
+  DL_DOCBITMAP = 4,  // precomputed doc bitmap (native LSB-first words)
+  DL_DOCRANGE = 5    // doc id in [lo,hi)
+};
+
+struct DevLeaf {
+  uint32_t kind;
+  uint32_t excl;
+  int32_t lo, hi;
+  const uint32_t* words;  // packed forward words (RANGE / LUT) or doc bitmap (DOCBITMAP)
+  const uint32_t* lut;    // LUT
+  uint32_t bits;
+  uint32_t pad;
+};
+
+// A column as read by aggregation inputs and group keys.
+struct DevCol {
+  const uint32_t* words;      // packed SV forward words
+  const void* dict;           // typed dictionary values
+  const int32_t* keymap;      // dictId -> global key (PG_KEY_KEYMAP)
+  const uint32_t* mv_offsets; // MV: row offsets [num_docs+1]
+  uint32_t bits;
+  uint32_t dtype;             // pg_data_type
+};
+
+enum SlotKind : uint32_t { SK_NONE = 0, SK_I64 = 1, SK_F64 = 2, SK_MIN = 3, SK_MAX = 4, SK_FLAG = 5 };
+
+struct AggSpec {
+  uint32_t fn;        // pg_agg_fn
+  uint32_t op;        // pg_expr_op
+  uint32_t kind;      // SlotKind of the primary slot
+  uint32_t slot;      // primary slot index within its array
+  uint32_t cnt_slot;  // AVG count slot (i64)
+  uint32_t integer;   // SUM/AVG inputs integer-exact -> i64 accumulate
+  uint32_t key_kind;  // DISTINCTCOUNT: pg_key_kind
+  uint32_t key_card;  // DISTINCTCOUNT: global key space size (flag bytes for this agg)
+  int64_t key_base;
+  uint64_t flag_off;  // DISTINCTCOUNT: byte offset of this agg's flags within a slot's flag row
+};
+
+struct QuerySpec {
+  uint32_t num_segments, num_leaves, num_ops, num_aggs, num_keys;
+  uint32_t use_lds;        // group table privatised in LDS
+  int32_t ops[kMaxOps];
+  AggSpec aggs[kMaxAggs];
+  uint32_t key_kind[kMaxKeys];
+  uint32_t key_card[kMaxKeys];
+  int64_t key_base[kMaxKeys];
+  uint64_t key_stride[kMaxKeys];
+  uint64_t num_slots;
+  uint32_t n_i64, n_f64, n_min, n_max;
+  uint64_t flag_bytes_per_slot;
+  unsigned long long* i64;
+  double* f64;
+  long long* mn;
+  long long* mx;
+  uint8_t* flags;
+  const DevLeaf* leaves;     // [seg][num_leaves]
+  const DevCol* aggcols;     // [seg][num_aggs][2]
+  const DevCol* keycols;     // [seg][num_keys]
+  const uint32_t* num_docs;  // [seg]
+  const uint64_t* tile_prefix;  // [seg+1]
+  uint64_t total_tiles;
+  unsigned long long* seg_matched;  // [seg]
+};
+
+// order-preserving int64 image of a double (for MIN/MAX slots)
+__host__ __device__ inline int64_t order_key(double v) {
+  int64_t b;
+  __builtin_memcpy(&b, &v, 8);
+  return b >= 0 ? b : (b ^ 0x7FFFFFFFFFFFFFFFLL);
+}
+__host__ __device__ inline double order_key_decode(int64_t k) {
+  int64_t b = k >= 0 ? k : (k ^ 0x7FFFFFFFFFFFFFFFLL);
+  double v;
+  __builtin_memcpy(&v, &b, 8);
+  return v;
+}
+
+// ---- kernel launchers (pg_kernels.hip)
+hipError_t launch_scan(const QuerySpec& q, uint32_t blocks, hipStream_t s);
+hipError_t launch_init_state(const QuerySpec& q, hipStream_t s);
+hipError_t launch_bswap_words(const uint8_t* src, uint32_t* dst, uint64_t nbytes, uint64_t nwords_out, hipStream_t s);
+hipError_t launch_be_to_native(const uint8_t* src, void* dst, uint64_t n, uint32_t width, hipStream_t s);
+hipError_t launch_sorted_to_packed(const int32_t* pairs, uint32_t card, uint32_t num_docs, uint32_t bits,
+                                   uint32_t* words, uint64_t nwords, hipStream_t s);
+hipError_t launch_mv_offsets(const uint32_t* bitmap_words, uint64_t num_values, uint32_t num_docs,
+                             uint32_t* offsets, void* scratch, size_t scratch_bytes, hipStream_t s);
+size_t mv_offsets_scratch_bytes(uint64_t num_values);
+hipError_t launch_fill_ranges(const int32_t* ranges /*[n][2] inclusive, sorted, disjoint*/, uint32_t n,
+                              uint32_t num_docs, uint32_t* bitmap, hipStream_t s);
+struct RoaringContainer {
+  uint32_t key;      // high 16 bits of the doc ids
+  uint32_t type;     // 0 array, 1 bitmap, 2 run
+  uint32_t card;     // array: cardinality; run: number of runs
+  uint32_t offset;   // byte offset of the payload within the column's roaring region
+};
+hipError_t launch_roaring_or(const uint8_t* roaring, const RoaringContainer* containers, const uint32_t* sel,
+                             uint32_t nsel, uint32_t num_docs, uint32_t* bitmap, hipStream_t s);
+hipError_t launch_bitmap_not(uint32_t* bitmap, uint32_t num_docs, hipStream_t s);
+hipError_t launch_mv_scan(const uint32_t* words, uint32_t bits, const uint32_t* offsets, uint32_t num_docs,
+                          int32_t lo, int32_t hi, const uint32_t* lut, uint32_t excl, uint32_t* bitmap,
+                          hipStream_t s);
+hipError_t launch_set_lut_bits(const int32_t* ids, uint32_t n, uint32_t* lut, hipStream_t s);
+
+}  // namespace pg

@@ -1,0 +1,1187 @@
+// pg_runtime.hip -- libpinot_gpu host runtime: device binding, segment residency, plan compilation,
+// launch sequencing and result decoding behind the C ABI of include/pinot_gpu.h.
+//
+// Mirrors on the device side what the reference does per query on the server:
+//   InstancePlanMakerImplV2.makeInstancePlan (plan/maker/InstancePlanMakerImplV2.java:153-187)
+//     -> per segment FilterPlanNode.constructPhysicalOperator (plan/FilterPlanNode.java:191-311)
+//        choosing scan / sorted / inverted leaves (operator/filter/FilterOperatorUtils.java:45-85)
+//     -> AggregationOperator / AggregationGroupByOrderByOperator
+//     -> AggregationOnlyCombineOperator / GroupByOrderByCombineOperator merge
+// but as ONE fused launch over all of the query's segments on this GPU (plus a small pre-pass for
+// index-backed leaves), with per-group state merged in device memory by global key id.
+#include <hip/hip_runtime.h>
+#include <time.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "pg_internal.h"
+
+using namespace pg;
+
+namespace {
+
+thread_local std::string t_err;
+thread_local pg_timing t_timing{};
+int g_device = -1;
+std::mutex g_init_mu;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  t_err = buf;
+  return code;
+}
+
+#define HIP_CHECK(expr)                                                                                  \
+  do {                                                                                                   \
+    hipError_t _e = (expr);                                                                              \
+    if (_e != hipSuccess) return fail(PG_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e),   \
+                                      __FILE__, __LINE__);                                               \
+  } while (0)
+
+int ensure_device() {
+  if (g_device < 0) return fail(PG_E_STATE, "pg_init has not been called");
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess || cur != g_device) {
+    if (hipSetDevice(g_device) != hipSuccess) return fail(PG_E_HIP, "hipSetDevice(%d) failed", g_device);
+  }
+  return PG_OK;
+}
+
+hipStream_t thread_stream() {
+  thread_local hipStream_t s = nullptr;
+  if (!s) hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  return s;
+}
+
+int64_t now_ms() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (int64_t)ts.tv_sec * 1000 + ts.tv_nsec / 1000000;
+}
+
+// ------------------------------------------------------------------------------------------ residency
+
+// Device buffer: resident buffers use hipMalloc; per-query buffers (async=true) use the stream-ordered
+// pool (hipMallocAsync / hipFreeAsync) so steady-state queries never call hipMalloc / hipFree.
+struct DevBuf {
+  void* p = nullptr;
+  uint64_t bytes = 0;
+  hipStream_t stream = nullptr;
+  bool async = false;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept { *this = std::move(o); }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    if (this != &o) {
+      reset();
+      p = o.p; bytes = o.bytes; stream = o.stream; async = o.async;
+      o.p = nullptr; o.bytes = 0;
+    }
+    return *this;
+  }
+  ~DevBuf() { reset(); }
+  void reset() {
+    if (p) {
+      if (async) hipFreeAsync(p, stream);
+      else hipFree(p);
+    }
+    p = nullptr;
+    bytes = 0;
+  }
+  int alloc(uint64_t n) {
+    reset();
+    if (n == 0) n = 16;
+    async = false;
+    if (hipMalloc(&p, n) != hipSuccess) {
+      p = nullptr;
+      return fail(PG_E_NOMEM, "hipMalloc(%llu) failed", (unsigned long long)n);
+    }
+    bytes = n;
+    return PG_OK;
+  }
+  int alloc_async(uint64_t n, hipStream_t s) {
+    reset();
+    if (n == 0) n = 16;
+    async = true;
+    stream = s;
+    if (hipMallocAsync(&p, n, s) != hipSuccess) {
+      p = nullptr;
+      return fail(PG_E_NOMEM, "hipMallocAsync(%llu) failed", (unsigned long long)n);
+    }
+    bytes = n;
+    return PG_OK;
+  }
+};
+
+enum FwdKind : uint32_t { FWD_NONE = 0, FWD_SV = 1, FWD_SORTED = 2, FWD_MV = 3 };
+
+struct ColumnRes {
+  // dictionary
+  bool has_dict = false;
+  uint32_t dtype = 0, card = 0, entry_bytes = 0;
+  DevBuf dict;
+  double dmin = 0, dmax = 0;  // dictionary min / max value (as double; integers exact below 2^53)
+  int64_t imin = 0, imax = 0;
+  // forward index
+  uint32_t fwd = FWD_NONE;
+  uint32_t num_docs = 0, bits = 0, num_values = 0;
+  DevBuf words;                       // packed dictIds (SV / synthesised for sorted / MV values)
+  DevBuf mv_offsets;                  // MV row offsets
+  std::vector<int32_t> sorted_pairs;  // host copy for leaf lowering (card x 2)
+  // inverted index
+  bool has_inv = false;
+  DevBuf roaring, containers;
+  std::vector<uint32_t> inv_dir;  // CSR: containers of dictId d are [inv_dir[d], inv_dir[d+1])
+  // keymap
+  bool has_keymap = false;
+  DevBuf keymap;
+};
+
+struct SegmentRes {
+  std::unordered_map<uint32_t, ColumnRes> cols;
+};
+
+std::shared_mutex g_seg_mu;
+std::unordered_map<uint64_t, SegmentRes*> g_segs;
+std::mutex g_cancel_mu;
+std::unordered_set<uint64_t> g_cancelled;
+
+bool is_cancelled(uint64_t qid) {
+  if (!qid) return false;
+  std::lock_guard<std::mutex> g(g_cancel_mu);
+  return g_cancelled.count(qid) != 0;
+}
+
+inline uint32_t rd_be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+inline uint64_t rd_be64(const uint8_t* p) { return ((uint64_t)rd_be32(p) << 32) | rd_be32(p + 4); }
+inline uint16_t rd_le16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+inline uint32_t rd_le32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+double be_value_as_double(const uint8_t* p, uint32_t dtype) {
+  switch (dtype) {
+    case PG_INT: return (double)(int32_t)rd_be32(p);
+    case PG_LONG: return (double)(int64_t)rd_be64(p);
+    case PG_FLOAT: { uint32_t u = rd_be32(p); float f; memcpy(&f, &u, 4); return f; }
+    case PG_DOUBLE: { uint64_t u = rd_be64(p); double d; memcpy(&d, &u, 8); return d; }
+    default: return 0;
+  }
+}
+int64_t be_value_as_i64(const uint8_t* p, uint32_t dtype) {
+  return dtype == PG_INT ? (int64_t)(int32_t)rd_be32(p) : (dtype == PG_LONG ? (int64_t)rd_be64(p) : 0);
+}
+
+// Copy `src` (host or device) into a fresh device staging buffer.
+int stage(const void* src, uint64_t nbytes, bool src_device, DevBuf& out, hipStream_t s) {
+  int rc = out.alloc(nbytes + 16);
+  if (rc) return rc;
+  HIP_CHECK(hipMemsetAsync(out.p, 0, nbytes + 16, s));
+  if (nbytes)
+    HIP_CHECK(hipMemcpyAsync(out.p, src, nbytes, src_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+  return PG_OK;
+}
+
+// Host copy of a (host or device) source range.
+int host_copy(const void* src, uint64_t nbytes, bool src_device, std::vector<uint8_t>& out) {
+  out.resize(nbytes);
+  if (!nbytes) return PG_OK;
+  if (src_device) HIP_CHECK(hipMemcpy(out.data(), src, nbytes, hipMemcpyDeviceToHost));
+  else memcpy(out.data(), src, nbytes);
+  return PG_OK;
+}
+
+// Parse a BitmapInvertedIndexWriter buffer: (card+1) BE uint32 offsets + portable roarings
+// (readers/BitmapInvertedIndexReader.java:45-63); re-lay every container payload 8-byte aligned.
+int parse_inverted(const std::vector<uint8_t>& b, uint32_t card, std::vector<uint32_t>& dir,
+                   std::vector<RoaringContainer>& cs, std::vector<uint8_t>& payload) {
+  if (b.size() < 4ull * (card + 1)) return fail(PG_E_INVALID, "inverted index too small");
+  const uint64_t base = 4ull * (card + 1);
+  const uint32_t first = rd_be32(&b[0]);
+  dir.assign(card + 1, 0);
+  for (uint32_t d = 0; d < card; d++) {
+    dir[d] = (uint32_t)cs.size();
+    const uint64_t s = base + (uint64_t)(rd_be32(&b[4ull * d]) - first);
+    const uint64_t e = base + (uint64_t)(rd_be32(&b[4ull * (d + 1)]) - first);
+    if (e > b.size() || s > e || e - s < 8) return fail(PG_E_INVALID, "bad roaring offsets for dictId %u", d);
+    const uint8_t* r = &b[s];
+    const uint32_t cookie = rd_le32(r);
+    uint32_t size, pos;
+    const uint8_t* run_flags = nullptr;
+    if ((cookie & 0xFFFF) == 12347) {
+      size = (cookie >> 16) + 1;
+      pos = 4;
+      run_flags = r + pos;
+      pos += (size + 7) / 8;
+    } else if (cookie == 12346) {
+      size = rd_le32(r + 4);
+      pos = 8;
+    } else {
+      return fail(PG_E_INVALID, "bad roaring cookie %u for dictId %u", cookie, d);
+    }
+    const uint32_t hdr = pos;
+    pos += 4 * size;
+    const bool has_off = !run_flags || size >= 4;
+    const uint32_t off_pos = pos;
+    if (has_off) pos += 4 * size;
+    uint32_t cur = pos;
+    for (uint32_t i = 0; i < size; i++) {
+      RoaringContainer c;
+      c.key = rd_le16(r + hdr + 4 * i);
+      const uint32_t cardm1 = rd_le16(r + hdr + 4 * i + 2);
+      if (has_off) cur = rd_le32(r + off_pos + 4 * i);
+      const bool is_run = run_flags && ((run_flags[i / 8] >> (i % 8)) & 1);
+      uint32_t len;
+      if (is_run) {
+        c.type = 2;
+        c.card = rd_le16(r + cur);
+        len = 2 + 4 * c.card;
+      } else if (cardm1 + 1 <= 4096) {
+        c.type = 0;
+        c.card = cardm1 + 1;
+        len = 2 * c.card;
+      } else {
+        c.type = 1;
+        c.card = cardm1 + 1;
+        len = 8192;
+      }
+      if (s + cur + len > e) return fail(PG_E_INVALID, "roaring container overruns dictId %u", d);
+      const uint64_t at = (payload.size() + 7) & ~7ull;
+      payload.resize(at + len);
+      memcpy(&payload[at], r + cur, len);
+      c.offset = (uint32_t)at;
+      cs.push_back(c);
+      cur += len;
+    }
+  }
+  dir[card] = (uint32_t)cs.size();
+  return PG_OK;
+}
+
+int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const void* src, uint64_t nbytes) {
+  const bool on_dev = (d->flags & PG_SRC_DEVICE) != 0;
+  hipStream_t s = thread_stream();
+  ColumnRes tmp;
+  DevBuf st;
+  int rc = PG_OK;
+  // Fill a fresh ColumnRes part, then swap it into the registry under the lock.
+  switch (d->kind) {
+    case PG_IDX_DICT: {
+      if (d->data_type > PG_BYTES) return fail(PG_E_INVALID, "bad dictionary data type %u", d->data_type);
+      const uint32_t w = d->data_type == PG_INT || d->data_type == PG_FLOAT ? 4 :
+                         (d->data_type == PG_LONG || d->data_type == PG_DOUBLE ? 8 : d->entry_bytes);
+      if ((uint64_t)w * d->cardinality > nbytes)
+        return fail(PG_E_INVALID, "dictionary: %llu bytes < card %u x %u", (unsigned long long)nbytes, d->cardinality, w);
+      tmp.has_dict = true;
+      tmp.dtype = d->data_type;
+      tmp.card = d->cardinality;
+      tmp.entry_bytes = w;
+      if (d->data_type <= PG_DOUBLE && d->cardinality) {
+        if ((rc = stage(src, nbytes, on_dev, st, s))) return rc;
+        if ((rc = tmp.dict.alloc((uint64_t)w * d->cardinality + 16))) return rc;
+        HIP_CHECK(launch_be_to_native((const uint8_t*)st.p, tmp.dict.p, d->cardinality, w, s));
+        std::vector<uint8_t> ends;
+        std::vector<uint8_t> lo(w), hi(w);
+        if (on_dev) {
+          HIP_CHECK(hipMemcpy(lo.data(), src, w, hipMemcpyDeviceToHost));
+          HIP_CHECK(hipMemcpy(hi.data(), (const uint8_t*)src + (uint64_t)w * (d->cardinality - 1), w, hipMemcpyDeviceToHost));
+        } else {
+          memcpy(lo.data(), src, w);
+          memcpy(hi.data(), (const uint8_t*)src + (uint64_t)w * (d->cardinality - 1), w);
+        }
+        tmp.dmin = be_value_as_double(lo.data(), d->data_type);
+        tmp.dmax = be_value_as_double(hi.data(), d->data_type);
+        tmp.imin = be_value_as_i64(lo.data(), d->data_type);
+        tmp.imax = be_value_as_i64(hi.data(), d->data_type);
+      }
+      break;
+    }
+    case PG_IDX_FWD_SV_BITPACKED: {
+      if (d->bits_per_element < 1 || d->bits_per_element > 32) return fail(PG_E_INVALID, "bad bitsPerElement");
+      const uint64_t need = ((uint64_t)d->num_docs * d->bits_per_element + 7) / 8;
+      if (nbytes < need) return fail(PG_E_INVALID, "forward index: %llu bytes < %llu", (unsigned long long)nbytes,
+                                     (unsigned long long)need);
+      tmp.fwd = FWD_SV;
+      tmp.num_docs = d->num_docs;
+      tmp.bits = d->bits_per_element;
+      tmp.card = d->cardinality;
+      tmp.num_values = d->num_docs;
+      const uint64_t nwords = (need + 3) / 4 + 4;
+      if ((rc = stage(src, need, on_dev, st, s))) return rc;
+      if ((rc = tmp.words.alloc(nwords * 4))) return rc;
+      HIP_CHECK(launch_bswap_words((const uint8_t*)st.p, (uint32_t*)tmp.words.p, need, nwords, s));
+      break;
+    }
+    case PG_IDX_FWD_SV_SORTED: {
+      if (nbytes < 8ull * d->cardinality) return fail(PG_E_INVALID, "sorted index too small");
+      tmp.fwd = FWD_SORTED;
+      tmp.num_docs = d->num_docs;
+      tmp.card = d->cardinality;
+      tmp.bits = d->bits_per_element ? d->bits_per_element : 1;
+      tmp.num_values = d->num_docs;
+      std::vector<uint8_t> hb;
+      if ((rc = host_copy(src, 8ull * d->cardinality, on_dev, hb))) return rc;
+      tmp.sorted_pairs.resize(2ull * d->cardinality);
+      for (uint64_t i = 0; i < 2ull * d->cardinality; i++) tmp.sorted_pairs[i] = (int32_t)rd_be32(&hb[4 * i]);
+      DevBuf pairs;
+      if ((rc = pairs.alloc(8ull * d->cardinality + 16))) return rc;
+      HIP_CHECK(hipMemcpyAsync(pairs.p, tmp.sorted_pairs.data(), 8ull * d->cardinality, hipMemcpyHostToDevice, s));
+      const uint64_t nwords = ((uint64_t)d->num_docs * tmp.bits + 31) / 32 + 4;
+      if ((rc = tmp.words.alloc(nwords * 4))) return rc;
+      HIP_CHECK(launch_sorted_to_packed((const int32_t*)pairs.p, d->cardinality, d->num_docs, tmp.bits,
+                                        (uint32_t*)tmp.words.p, nwords, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+      pairs.reset();
+      break;
+    }
+    case PG_IDX_FWD_MV_BITPACKED: {
+      const uint32_t nd = d->num_docs, nv = d->num_values, b = d->bits_per_element;
+      if (!nd || nv < nd) return fail(PG_E_INVALID, "MV column needs num_values >= num_docs > 0");
+      if (b < 1 || b > 32) return fail(PG_E_INVALID, "bad bitsPerElement");
+      // FixedBitMVForwardIndexReader.java:61-75
+      const uint32_t avg = nv / nd;
+      const uint32_t dpc = (uint32_t)ceilf(2048.0f / (float)avg);
+      const uint64_t nchunks = (nd + dpc - 1) / dpc;
+      const uint64_t hdr = 4 * nchunks, bm_bytes = ((uint64_t)nv + 7) / 8, raw = ((uint64_t)nv * b + 7) / 8;
+      if (nbytes < hdr + bm_bytes + raw) return fail(PG_E_INVALID, "MV forward index too small");
+      tmp.fwd = FWD_MV;
+      tmp.num_docs = nd;
+      tmp.num_values = nv;
+      tmp.bits = b;
+      tmp.card = d->cardinality;
+      if ((rc = stage(src, nbytes, on_dev, st, s))) return rc;
+      const uint64_t bm_words = (bm_bytes + 3) / 4 + 4, raw_words = (raw + 3) / 4 + 4;
+      DevBuf bm;
+      if ((rc = bm.alloc(bm_words * 4))) return rc;
+      if ((rc = tmp.words.alloc(raw_words * 4))) return rc;
+      HIP_CHECK(launch_bswap_words((const uint8_t*)st.p + hdr, (uint32_t*)bm.p, bm_bytes, bm_words, s));
+      HIP_CHECK(launch_bswap_words((const uint8_t*)st.p + hdr + bm_bytes, (uint32_t*)tmp.words.p, raw, raw_words, s));
+      if ((rc = tmp.mv_offsets.alloc(4ull * (nd + 1)))) return rc;
+      DevBuf scratch;
+      const size_t sb = mv_offsets_scratch_bytes(nv);
+      if ((rc = scratch.alloc(sb))) return rc;
+      HIP_CHECK(launch_mv_offsets((const uint32_t*)bm.p, nv, nd, (uint32_t*)tmp.mv_offsets.p, scratch.p, sb, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+      break;
+    }
+    case PG_IDX_INV_BITMAP: {
+      std::vector<uint8_t> hb;
+      if ((rc = host_copy(src, nbytes, on_dev, hb))) return rc;
+      std::vector<RoaringContainer> cs;
+      std::vector<uint8_t> payload;
+      if ((rc = parse_inverted(hb, d->cardinality, tmp.inv_dir, cs, payload))) return rc;
+      tmp.has_inv = true;
+      tmp.card = d->cardinality;
+      tmp.num_docs = d->num_docs;
+      if ((rc = tmp.roaring.alloc(payload.size() + 16))) return rc;
+      if ((rc = tmp.containers.alloc(cs.size() * sizeof(RoaringContainer) + 16))) return rc;
+      if (!payload.empty()) HIP_CHECK(hipMemcpyAsync(tmp.roaring.p, payload.data(), payload.size(), hipMemcpyHostToDevice, s));
+      if (!cs.empty())
+        HIP_CHECK(hipMemcpyAsync(tmp.containers.p, cs.data(), cs.size() * sizeof(RoaringContainer), hipMemcpyHostToDevice, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+      break;
+    }
+    case PG_IDX_KEYMAP: {
+      if (nbytes < 4ull * d->cardinality) return fail(PG_E_INVALID, "keymap too small");
+      tmp.has_keymap = true;
+      if ((rc = tmp.keymap.alloc(4ull * d->cardinality + 16))) return rc;
+      HIP_CHECK(hipMemcpyAsync(tmp.keymap.p, src, 4ull * d->cardinality,
+                               on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+      break;
+    }
+    default:
+      return fail(PG_E_INVALID, "unknown index kind %u", d->kind);
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
+  st.reset();
+
+  std::unique_lock<std::shared_mutex> lk(g_seg_mu);
+  SegmentRes*& seg = g_segs[seg_key];
+  if (!seg) seg = new SegmentRes();
+  ColumnRes& c = seg->cols[col_id];
+  switch (d->kind) {
+    case PG_IDX_DICT:
+      c.dict.reset();
+      c.has_dict = true; c.dtype = tmp.dtype; c.card = tmp.card; c.entry_bytes = tmp.entry_bytes;
+      c.dict = std::move(tmp.dict);
+      c.dmin = tmp.dmin; c.dmax = tmp.dmax; c.imin = tmp.imin; c.imax = tmp.imax;
+      break;
+    case PG_IDX_FWD_SV_BITPACKED: case PG_IDX_FWD_SV_SORTED: case PG_IDX_FWD_MV_BITPACKED:
+      c.words.reset(); c.mv_offsets.reset();
+      c.fwd = tmp.fwd; c.num_docs = tmp.num_docs; c.bits = tmp.bits; c.num_values = tmp.num_values;
+      if (!c.has_dict) c.card = tmp.card;
+      c.words = std::move(tmp.words);
+      c.mv_offsets = std::move(tmp.mv_offsets);
+      c.sorted_pairs.swap(tmp.sorted_pairs);
+      break;
+    case PG_IDX_INV_BITMAP:
+      c.roaring.reset(); c.containers.reset();
+      c.has_inv = true;
+      c.roaring = std::move(tmp.roaring);
+      c.containers = std::move(tmp.containers);
+      c.inv_dir.swap(tmp.inv_dir);
+      if (!c.num_docs) c.num_docs = tmp.num_docs;
+      break;
+    case PG_IDX_KEYMAP:
+      c.keymap.reset();
+      c.has_keymap = true;
+      c.keymap = std::move(tmp.keymap);
+      break;
+  }
+  return PG_OK;
+}
+
+// ------------------------------------------------------------------------------------------ execution
+
+struct Partials {
+  DevBuf i64, f64, mn, mx, flags, seg_matched;
+  std::vector<uint32_t> key_card;
+  std::vector<uint64_t> key_stride;
+  uint32_t projected_cols = 0;
+  uint64_t entries_in_filter = 0;
+  uint64_t total_docs = 0;
+  uint32_t num_segments = 0;
+  std::vector<AggSpec> aggs;
+};
+
+struct Arena {  // host image of the per-query parameter block, copied to the device in one transfer
+  std::vector<uint8_t> h;
+  uint64_t put(const void* p, uint64_t n, uint64_t align = 16) {
+    uint64_t at = (h.size() + align - 1) & ~(align - 1);
+    h.resize(at + n);
+    if (n) memcpy(&h[at], p, n);
+    return at;
+  }
+  uint64_t reserve(uint64_t n, uint64_t align = 16) {
+    uint64_t at = (h.size() + align - 1) & ~(align - 1);
+    h.resize(at + n, 0);
+    return at;
+  }
+};
+
+struct PrepassOp {  // filter materialisation work item
+  enum Kind { FILL_RANGES, ROARING, MV_SCAN, LUT } kind;
+  uint32_t seg, leaf;
+  uint64_t in_off = 0;   // arena offset of ranges / selected containers / ids
+  uint32_t n = 0;
+  uint32_t num_docs = 0;
+  uint64_t out_off = 0;  // scratch offset of the doc bitmap / LUT
+  uint64_t out_bytes = 0;
+  bool negate = false;
+  const ColumnRes* col = nullptr;
+  int32_t lo = 0, hi = 0;
+  uint64_t lut_off = 0;  // MV scan: scratch LUT offset (or ~0 for range)
+  uint32_t excl = 0;
+};
+
+int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
+  if (!plan) return fail(PG_E_INVALID, "null plan");
+  if (plan->abi_version != PG_ABI_VERSION) return fail(PG_E_INVALID, "ABI version %u != %u", plan->abi_version, PG_ABI_VERSION);
+  if (plan->num_aggs > (uint32_t)kMaxAggs) return fail(PG_E_UNSUPPORTED, "more than %d aggregations", kMaxAggs);
+  if (plan->num_keys > (uint32_t)kMaxKeys) return fail(PG_E_UNSUPPORTED, "more than %d group-by keys", kMaxKeys);
+  if (plan->num_leaves > (uint32_t)kMaxLeaves) return fail(PG_E_UNSUPPORTED, "more than %d filter leaves", kMaxLeaves);
+  if (plan->num_ops > (uint32_t)kMaxOps) return fail(PG_E_UNSUPPORTED, "filter program longer than %d", kMaxOps);
+  // validate program stack depth
+  {
+    int sp = 0, mx = 0;
+    for (uint32_t i = 0; i < plan->num_ops; i++) {
+      const int32_t op = plan->ops[i];
+      if (op >= 0) {
+        if ((uint32_t)op >= plan->num_leaves) return fail(PG_E_INVALID, "op %u references leaf %d", i, op);
+        sp++;
+      } else if (op == PG_OP_NOT) {
+        if (sp < 1) return fail(PG_E_INVALID, "NOT on empty stack");
+      } else {
+        const int n = (-op) & 0xFF;
+        if (n < 1 || sp < n || !((-op) & 0x300)) return fail(PG_E_INVALID, "bad AND/OR arity at op %u", i);
+        sp -= n - 1;
+      }
+      mx = std::max(mx, sp);
+    }
+    if (plan->num_ops && sp != 1) return fail(PG_E_INVALID, "filter program leaves %d values", sp);
+    if (mx > kMaxStack) return fail(PG_E_UNSUPPORTED, "filter nesting deeper than %d", kMaxStack);
+  }
+  if (plan->deadline_ms && now_ms() > plan->deadline_ms) return fail(PG_E_TIMEOUT, "deadline passed before launch");
+  if (is_cancelled(plan->query_id)) return fail(PG_E_CANCELLED, "query %llu cancelled", (unsigned long long)plan->query_id);
+
+  hipStream_t s = plan->stream ? (hipStream_t)plan->stream : thread_stream();
+  std::shared_lock<std::shared_mutex> lk(g_seg_mu);
+
+  const uint32_t S = plan->num_segments, L = plan->num_leaves, A = plan->num_aggs, K = plan->num_keys;
+  std::vector<const SegmentRes*> segs(S);
+  auto col = [&](uint32_t si, uint32_t cid) -> const ColumnRes* {
+    auto it = segs[si]->cols.find(cid);
+    return it == segs[si]->cols.end() ? nullptr : &it->second;
+  };
+  for (uint32_t si = 0; si < S; si++) {
+    auto it = g_segs.find(plan->segments[si].seg_key);
+    if (it == g_segs.end()) return fail(PG_E_NOTFOUND, "segment %llu not resident", (unsigned long long)plan->segments[si].seg_key);
+    segs[si] = it->second;
+  }
+
+  QuerySpec q;
+  memset(&q, 0, sizeof(q));
+  q.num_segments = S;
+  q.num_leaves = L;
+  q.num_ops = plan->num_ops;
+  q.num_aggs = A;
+  q.num_keys = K;
+  for (uint32_t i = 0; i < plan->num_ops; i++) q.ops[i] = plan->ops[i];
+
+  // ---- group key space (mixed radix, first key least significant: DictionaryBasedGroupKeyGenerator:280-322)
+  uint64_t G = 1;
+  P.key_card.assign(K, 0);
+  P.key_stride.assign(K, 0);
+  for (uint32_t k = 0; k < K; k++) {
+    const pg_key& key = plan->keys[k];
+    if (key.cardinality == 0) return fail(PG_E_INVALID, "group key %u has zero cardinality", k);
+    q.key_kind[k] = key.kind;
+    q.key_card[k] = key.cardinality;
+    q.key_base[k] = key.base;
+    q.key_stride[k] = G;
+    P.key_card[k] = key.cardinality;
+    P.key_stride[k] = G;
+    if (G > (1ull << 31) / key.cardinality) return fail(PG_E_UNSUPPORTED, "group key space exceeds 2^31 slots");
+    G *= key.cardinality;
+  }
+  // numGroupsLimit: the reference truncates per segment once the limit is hit (first-seen order,
+  // IntGroupIdMap :991-1016).  The device path only runs when no segment can reach the limit.
+  if (K) {
+    const uint64_t limit = plan->num_groups_limit ? plan->num_groups_limit : 100000;
+    for (uint32_t si = 0; si < S; si++) {
+      uint64_t prod = 1;
+      for (uint32_t k = 0; k < K; k++) {
+        const ColumnRes* c = col(si, plan->keys[k].col_id);
+        if (!c || !c->has_dict || c->fwd == FWD_NONE || c->fwd == FWD_MV)
+          return fail(c ? PG_E_UNSUPPORTED : PG_E_NOTFOUND, "group key column %u unusable in segment %u", plan->keys[k].col_id, si);
+        if (plan->keys[k].kind == PG_KEY_KEYMAP && !c->has_keymap) return fail(PG_E_NOTFOUND, "keymap missing for column %u", plan->keys[k].col_id);
+        if (plan->keys[k].kind == PG_KEY_VALUE_OFFSET && c->dtype != PG_INT && c->dtype != PG_LONG)
+          return fail(PG_E_INVALID, "VALUE_OFFSET key on non-integer column %u", plan->keys[k].col_id);
+        if (plan->keys[k].kind == PG_KEY_VALUE_OFFSET &&
+            (c->imin < plan->keys[k].base || (uint64_t)(c->imax - plan->keys[k].base) >= plan->keys[k].cardinality))
+          return fail(PG_E_INVALID, "column %u values outside the key range of key %u", plan->keys[k].col_id, k);
+        prod = prod > (1ull << 62) / (c->card ? c->card : 1) ? (1ull << 62) : prod * c->card;
+      }
+      if (prod > limit)
+        return fail(PG_E_UNSUPPORTED, "segment %u may exceed numGroupsLimit %llu (card product %llu)", si,
+                    (unsigned long long)limit, (unsigned long long)prod);
+    }
+  }
+
+  // ---- aggregation state slots
+  uint32_t n_i64 = 1, n_f64 = 0, n_min = 0, n_max = 0;
+  uint64_t flag_bytes = 0;
+  uint64_t total_docs = 0;
+  for (uint32_t si = 0; si < S; si++) total_docs += plan->segments[si].num_docs;
+  std::unordered_set<uint32_t> projected;
+  for (uint32_t a = 0; a < A; a++) {
+    const pg_agg& g = plan->aggs[a];
+    AggSpec& s2 = q.aggs[a];
+    memset(&s2, 0, sizeof(s2));
+    s2.fn = g.fn;
+    s2.op = g.op;
+    if (g.fn > PG_AGG_COUNTMV) return fail(PG_E_INVALID, "unknown aggregation %u", g.fn);
+    if (g.op > PG_EXPR_SUB) return fail(PG_E_INVALID, "unknown expression op %u", g.op);
+    if (g.fn == PG_AGG_COUNT) { s2.kind = SK_NONE; s2.slot = 0; continue; }
+    projected.insert(g.col_a);
+    const bool two = (g.fn == PG_AGG_SUM || g.fn == PG_AGG_MIN || g.fn == PG_AGG_MAX || g.fn == PG_AGG_AVG) && g.op != PG_EXPR_COL;
+    if (two) projected.insert(g.col_b);
+    // validate inputs in every segment, collect value bounds
+    double bound_a = 0, bound_b = 0;
+    bool all_int = true;
+    for (uint32_t si = 0; si < S; si++) {
+      const ColumnRes* ca = col(si, g.col_a);
+      if (!ca) return fail(PG_E_NOTFOUND, "aggregation %u: column %u not resident in segment %u", a, g.col_a, si);
+      if (g.fn == PG_AGG_COUNTMV) {
+        if (ca->fwd != FWD_MV) return fail(PG_E_INVALID, "COUNTMV on a single-value column %u", g.col_a);
+        continue;
+      }
+      if (ca->fwd == FWD_NONE || ca->fwd == FWD_MV || !ca->has_dict)
+        return fail(PG_E_UNSUPPORTED, "aggregation %u: column %u needs an SV forward index + dictionary", a, g.col_a);
+      if (g.fn == PG_AGG_DISTINCTCOUNT) {
+        if (g.key_kind == PG_KEY_KEYMAP && !ca->has_keymap) return fail(PG_E_NOTFOUND, "DISTINCTCOUNT keymap missing");
+        if (g.key_kind == PG_KEY_VALUE_OFFSET &&
+            (ca->dtype > PG_LONG || ca->imin < g.key_base || (uint64_t)(ca->imax - g.key_base) >= g.key_cardinality))
+          return fail(PG_E_INVALID, "DISTINCTCOUNT values outside the key range");
+        continue;
+      }
+      if (ca->dtype > PG_DOUBLE) return fail(PG_E_UNSUPPORTED, "numeric aggregation on non-numeric column %u", g.col_a);
+      all_int &= ca->dtype <= PG_LONG;
+      bound_a = std::max(bound_a, std::max(fabs(ca->dmin), fabs(ca->dmax)));
+      if (two) {
+        const ColumnRes* cb = col(si, g.col_b);
+        if (!cb || cb->fwd == FWD_NONE || cb->fwd == FWD_MV || !cb->has_dict || cb->dtype > PG_DOUBLE)
+          return fail(PG_E_UNSUPPORTED, "aggregation %u: second operand column %u unusable", a, g.col_b);
+        all_int &= cb->dtype <= PG_LONG;
+        bound_b = std::max(bound_b, std::max(fabs(cb->dmin), fabs(cb->dmax)));
+      }
+    }
+    switch (g.fn) {
+      case PG_AGG_COUNTMV: s2.kind = SK_I64; s2.slot = n_i64++; break;
+      case PG_AGG_SUM: case PG_AGG_AVG: {
+        double vb = bound_a;
+        if (two) vb = g.op == PG_EXPR_MUL ? bound_a * bound_b : bound_a + bound_b;
+        // integer-exact accumulation when every partial sum provably fits in int64 (2^62 margin)
+        s2.integer = all_int && vb * (double)(total_docs ? total_docs : 1) < 4.0e18;
+        if (s2.integer) { s2.kind = SK_I64; s2.slot = n_i64++; }
+        else { s2.kind = SK_F64; s2.slot = n_f64++; }
+        s2.cnt_slot = 0;
+        break;
+      }
+      case PG_AGG_MIN: s2.kind = SK_MIN; s2.slot = n_min++; break;
+      case PG_AGG_MAX: s2.kind = SK_MAX; s2.slot = n_max++; break;
+      case PG_AGG_DISTINCTCOUNT:
+        if (!g.key_cardinality) return fail(PG_E_INVALID, "DISTINCTCOUNT needs key_cardinality");
+        s2.kind = SK_FLAG;
+        s2.key_kind = g.key_kind;
+        s2.key_card = g.key_cardinality;
+        s2.key_base = g.key_base;
+        s2.flag_off = flag_bytes;
+        flag_bytes += g.key_cardinality;
+        break;
+    }
+  }
+  for (uint32_t k = 0; k < K; k++) projected.insert(plan->keys[k].col_id);
+  q.num_slots = G;
+  q.n_i64 = n_i64; q.n_f64 = n_f64; q.n_min = n_min; q.n_max = n_max;
+  q.flag_bytes_per_slot = flag_bytes;
+  const uint64_t state_bytes = G * 8ull * (n_i64 + n_f64 + n_min + n_max) + G * flag_bytes;
+  if (state_bytes > (64ull << 30)) return fail(PG_E_UNSUPPORTED, "group state of %llu bytes exceeds the 64 GiB budget", (unsigned long long)state_bytes);
+  q.use_lds = K > 0 && G * 8ull * (n_i64 + n_f64 + n_min + n_max) <= (uint64_t)kLdsGroupBytes;
+  P.projected_cols = (uint32_t)projected.size();
+  P.total_docs = total_docs;
+  P.num_segments = S;
+  P.aggs.assign(q.aggs, q.aggs + A);
+
+  // ---- per-segment tables + pre-pass work
+  Arena ar;
+  std::vector<DevLeaf> leaves((uint64_t)S * L);
+  std::vector<DevCol> aggcols((uint64_t)S * A * 2);
+  std::vector<DevCol> keycols((uint64_t)S * K);
+  std::vector<uint32_t> ndocs(S);
+  std::vector<uint64_t> tile_prefix(S + 1, 0);
+  std::vector<PrepassOp> pre;
+  uint64_t scratch_bytes = 0;
+  auto scratch_reserve = [&](uint64_t n) { uint64_t at = (scratch_bytes + 255) & ~255ull; scratch_bytes = at + n; return at; };
+  uint64_t entries_in_filter = 0;
+  // scratch pointers are patched after allocation: remember which leaf fields point into scratch
+  struct Patch { uint64_t leaf_index; uint64_t off; bool lut; };
+  std::vector<Patch> patches;
+
+  for (uint32_t si = 0; si < S; si++) {
+    const pg_segment_ref& sr = plan->segments[si];
+    ndocs[si] = sr.num_docs;
+    tile_prefix[si + 1] = tile_prefix[si] + (sr.num_docs + kTileDocs - 1) / kTileDocs;
+    for (uint32_t li = 0; li < L; li++) {
+      const pg_leaf& pl = sr.leaves[li];
+      DevLeaf& dl = leaves[(uint64_t)si * L + li];
+      memset(&dl, 0, sizeof(dl));
+      dl.excl = pl.exclusive ? 1 : 0;
+      if (pl.kind == PG_LEAF_MATCH_ALL) { dl.kind = DL_ALL; continue; }
+      if (pl.kind == PG_LEAF_EMPTY) { dl.kind = DL_NONE; continue; }
+      const ColumnRes* c = col(si, pl.col_id);
+      if (!c) return fail(PG_E_NOTFOUND, "leaf %u: column %u not resident in segment %u", li, pl.col_id, si);
+      if (pl.num_ids && !pl.ids) return fail(PG_E_INVALID, "leaf %u: null id list", li);
+      for (uint32_t i = 0; i < pl.num_ids; i++)
+        if (pl.ids[i] < 0 || (uint32_t)pl.ids[i] >= std::max(c->card, 1u) || (i && pl.ids[i] <= pl.ids[i - 1]))
+          return fail(PG_E_INVALID, "leaf %u: dictIds must be sorted, unique and < cardinality", li);
+      auto in_set = [&](int32_t id) {
+        if (!pl.num_ids) return id >= pl.lo && id < pl.hi;
+        return std::binary_search(pl.ids, pl.ids + pl.num_ids, id);
+      };
+      switch (pl.kind) {
+        case PG_LEAF_SV_SCAN: {
+          if (c->fwd != FWD_SV && c->fwd != FWD_SORTED) return fail(PG_E_INVALID, "SV scan on column %u without SV forward index", pl.col_id);
+          dl.words = (const uint32_t*)c->words.p;
+          dl.bits = c->bits;
+          entries_in_filter += sr.num_docs;
+          if (!pl.num_ids) {
+            dl.kind = DL_RANGE;
+            dl.lo = std::max(pl.lo, 0);
+            dl.hi = std::max(std::min(pl.hi, (int32_t)c->card), dl.lo);
+          } else {
+            dl.kind = DL_LUT;
+            PrepassOp op{PrepassOp::LUT, si, li};
+            op.in_off = ar.put(pl.ids, 4ull * pl.num_ids);
+            op.n = pl.num_ids;
+            op.out_bytes = 4ull * ((c->card + 31) / 32 + 1);
+            op.out_off = scratch_reserve(op.out_bytes);
+            patches.push_back({(uint64_t)si * L + li, op.out_off, true});
+            pre.push_back(op);
+          }
+          break;
+        }
+        case PG_LEAF_SORTED: {
+          if (c->fwd != FWD_SORTED) return fail(PG_E_INVALID, "sorted leaf on unsorted column %u", pl.col_id);
+          // SortedIndexBasedFilterOperator: matching dictIds -> merged [start,end] doc ranges
+          std::vector<int32_t> rg;
+          for (uint32_t id = 0; id < c->card; id++) {
+            if (!in_set((int32_t)id)) continue;
+            const int32_t s0 = c->sorted_pairs[2 * id], e0 = c->sorted_pairs[2 * id + 1];
+            if (e0 < s0) continue;
+            if (!rg.empty() && rg.back() + 1 >= s0) rg.back() = std::max(rg.back(), e0);
+            else { rg.push_back(s0); rg.push_back(e0); }
+          }
+          if (pl.exclusive) {  // complement within [0, num_docs)
+            std::vector<int32_t> cm;
+            int32_t next = 0;
+            for (size_t i = 0; i < rg.size(); i += 2) {
+              if (rg[i] > next) { cm.push_back(next); cm.push_back(rg[i] - 1); }
+              next = rg[i + 1] + 1;
+            }
+            if (next < (int32_t)sr.num_docs) { cm.push_back(next); cm.push_back((int32_t)sr.num_docs - 1); }
+            rg.swap(cm);
+            dl.excl = 0;
+          }
+          if (rg.empty()) { dl.kind = DL_NONE; break; }
+          if (rg.size() == 2) { dl.kind = DL_DOCRANGE; dl.lo = rg[0]; dl.hi = rg[1] + 1; break; }
+          dl.kind = DL_DOCBITMAP;
+          PrepassOp op{PrepassOp::FILL_RANGES, si, li};
+          op.in_off = ar.put(rg.data(), 4ull * rg.size());
+          op.n = (uint32_t)(rg.size() / 2);
+          op.num_docs = sr.num_docs;
+          op.out_bytes = 4ull * ((sr.num_docs + 31) / 32 + 1);
+          op.out_off = scratch_reserve(op.out_bytes);
+          patches.push_back({(uint64_t)si * L + li, op.out_off, false});
+          pre.push_back(op);
+          break;
+        }
+        case PG_LEAF_INVERTED: {
+          if (!c->has_inv) return fail(PG_E_INVALID, "inverted leaf on column %u without inverted index", pl.col_id);
+          std::vector<uint32_t> sel;
+          if (pl.num_ids) {
+            for (uint32_t i = 0; i < pl.num_ids; i++)
+              for (uint32_t x = c->inv_dir[pl.ids[i]]; x < c->inv_dir[pl.ids[i] + 1]; x++) sel.push_back(x);
+          } else {
+            const int32_t lo = std::max(pl.lo, 0), hi = std::min(pl.hi, (int32_t)c->card);
+            for (int32_t id = lo; id < hi; id++)
+              for (uint32_t x = c->inv_dir[id]; x < c->inv_dir[id + 1]; x++) sel.push_back(x);
+          }
+          dl.kind = DL_DOCBITMAP;
+          PrepassOp op{PrepassOp::ROARING, si, li};
+          op.in_off = ar.put(sel.data(), 4ull * sel.size());
+          op.n = (uint32_t)sel.size();
+          op.num_docs = sr.num_docs;
+          op.col = c;
+          op.negate = pl.exclusive != 0;
+          dl.excl = 0;
+          op.out_bytes = 4ull * ((sr.num_docs + 31) / 32 + 1);
+          op.out_off = scratch_reserve(op.out_bytes);
+          patches.push_back({(uint64_t)si * L + li, op.out_off, false});
+          pre.push_back(op);
+          break;
+        }
+        case PG_LEAF_MV_SCAN: {
+          if (c->fwd != FWD_MV) return fail(PG_E_INVALID, "MV scan on column %u without MV forward index", pl.col_id);
+          entries_in_filter += c->num_values;
+          dl.kind = DL_DOCBITMAP;
+          PrepassOp op{PrepassOp::MV_SCAN, si, li};
+          op.col = c;
+          op.num_docs = sr.num_docs;
+          op.excl = pl.exclusive ? 1 : 0;
+          dl.excl = 0;
+          op.lo = pl.lo;
+          op.hi = pl.hi;
+          op.lut_off = ~0ull;
+          if (pl.num_ids) {
+            PrepassOp lop{PrepassOp::LUT, si, li};
+            lop.in_off = ar.put(pl.ids, 4ull * pl.num_ids);
+            lop.n = pl.num_ids;
+            lop.out_bytes = 4ull * ((c->card + 31) / 32 + 1);
+            lop.out_off = scratch_reserve(lop.out_bytes);
+            pre.push_back(lop);
+            op.lut_off = lop.out_off;
+          }
+          op.out_bytes = 4ull * ((sr.num_docs + 31) / 32 + 1);
+          op.out_off = scratch_reserve(op.out_bytes);
+          patches.push_back({(uint64_t)si * L + li, op.out_off, false});
+          pre.push_back(op);
+          break;
+        }
+        default:
+          return fail(PG_E_INVALID, "unknown leaf kind %u", pl.kind);
+      }
+    }
+    for (uint32_t a = 0; a < A; a++) {
+      const pg_agg& g = plan->aggs[a];
+      if (g.fn == PG_AGG_COUNT) continue;
+      const uint32_t cids[2] = {g.col_a, g.col_b};
+      const int n = (g.op != PG_EXPR_COL && g.fn != PG_AGG_DISTINCTCOUNT && g.fn != PG_AGG_COUNTMV) ? 2 : 1;
+      for (int k = 0; k < n; k++) {
+        const ColumnRes* c = col(si, cids[k]);
+        DevCol& dc = aggcols[((uint64_t)si * A + a) * 2 + k];
+        dc.words = (const uint32_t*)c->words.p;
+        dc.dict = c->dict.p;
+        dc.keymap = (const int32_t*)c->keymap.p;
+        dc.mv_offsets = (const uint32_t*)c->mv_offsets.p;
+        dc.bits = c->bits;
+        dc.dtype = c->dtype;
+      }
+    }
+    for (uint32_t k = 0; k < K; k++) {
+      const ColumnRes* c = col(si, plan->keys[k].col_id);
+      DevCol& dc = keycols[(uint64_t)si * K + k];
+      dc.words = (const uint32_t*)c->words.p;
+      dc.dict = c->dict.p;
+      dc.keymap = (const int32_t*)c->keymap.p;
+      dc.bits = c->bits;
+      dc.dtype = c->dtype;
+    }
+  }
+  P.entries_in_filter = entries_in_filter;
+  q.total_tiles = tile_prefix[S];
+
+  // ---- device allocations (state + arena + scratch)
+  int rc;
+  if ((rc = P.i64.alloc_async(G * 8ull * n_i64, s))) return rc;
+  if (n_f64 && (rc = P.f64.alloc_async(G * 8ull * n_f64, s))) return rc;
+  if (n_min && (rc = P.mn.alloc_async(G * 8ull * n_min, s))) return rc;
+  if (n_max && (rc = P.mx.alloc_async(G * 8ull * n_max, s))) return rc;
+  if (flag_bytes && (rc = P.flags.alloc_async(G * flag_bytes, s))) return rc;
+  if ((rc = P.seg_matched.alloc_async(8ull * (S ? S : 1), s))) return rc;
+  q.i64 = (unsigned long long*)P.i64.p;
+  q.f64 = (double*)P.f64.p;
+  q.mn = (long long*)P.mn.p;
+  q.mx = (long long*)P.mx.p;
+  q.flags = (uint8_t*)P.flags.p;
+  q.seg_matched = (unsigned long long*)P.seg_matched.p;
+
+  const uint64_t off_leaves = ar.reserve(leaves.size() * sizeof(DevLeaf));
+  const uint64_t off_aggcols = ar.reserve(aggcols.size() * sizeof(DevCol));
+  const uint64_t off_keycols = ar.reserve(keycols.size() * sizeof(DevCol));
+  const uint64_t off_ndocs = ar.put(ndocs.data(), 4ull * S);
+  const uint64_t off_tiles = ar.put(tile_prefix.data(), 8ull * (S + 1));
+  DevBuf arena, scratch;
+  if ((rc = arena.alloc_async(ar.h.size() + 16, s))) return rc;
+  if (scratch_bytes && (rc = scratch.alloc_async(scratch_bytes, s))) return rc;
+  uint8_t* dA = (uint8_t*)arena.p;
+  uint8_t* dS = (uint8_t*)scratch.p;
+  for (const Patch& p : patches) {
+    DevLeaf& dl = leaves[p.leaf_index];
+    if (p.lut) dl.lut = (const uint32_t*)(dS + p.off);
+    else dl.words = (const uint32_t*)(dS + p.off);
+  }
+  memcpy(&ar.h[off_leaves], leaves.data(), leaves.size() * sizeof(DevLeaf));
+  memcpy(&ar.h[off_aggcols], aggcols.data(), aggcols.size() * sizeof(DevCol));
+  memcpy(&ar.h[off_keycols], keycols.data(), keycols.size() * sizeof(DevCol));
+  q.leaves = (const DevLeaf*)(dA + off_leaves);
+  q.aggcols = (const DevCol*)(dA + off_aggcols);
+  q.keycols = (const DevCol*)(dA + off_keycols);
+  q.num_docs = (const uint32_t*)(dA + off_ndocs);
+  q.tile_prefix = (const uint64_t*)(dA + off_tiles);
+
+  hipEvent_t ev[4];
+  for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+  struct EvGuard { hipEvent_t* e; ~EvGuard() { for (int i = 0; i < 4; i++) hipEventDestroy(e[i]); } } eg{ev};
+
+  HIP_CHECK(hipMemcpyAsync(arena.p, ar.h.data(), ar.h.size(), hipMemcpyHostToDevice, s));
+  HIP_CHECK(launch_init_state(q, s));
+  HIP_CHECK(hipEventRecord(ev[0], s));
+  if (scratch_bytes) HIP_CHECK(hipMemsetAsync(scratch.p, 0, scratch_bytes, s));
+  for (const PrepassOp& op : pre) {
+    switch (op.kind) {
+      case PrepassOp::LUT:
+        HIP_CHECK(launch_set_lut_bits((const int32_t*)(dA + op.in_off), op.n, (uint32_t*)(dS + op.out_off), s));
+        break;
+      case PrepassOp::FILL_RANGES:
+        HIP_CHECK(launch_fill_ranges((const int32_t*)(dA + op.in_off), op.n, op.num_docs, (uint32_t*)(dS + op.out_off), s));
+        break;
+      case PrepassOp::ROARING:
+        HIP_CHECK(launch_roaring_or((const uint8_t*)op.col->roaring.p, (const RoaringContainer*)op.col->containers.p,
+                                    (const uint32_t*)(dA + op.in_off), op.n, op.num_docs, (uint32_t*)(dS + op.out_off), s));
+        if (op.negate) HIP_CHECK(launch_bitmap_not((uint32_t*)(dS + op.out_off), op.num_docs, s));
+        break;
+      case PrepassOp::MV_SCAN:
+        HIP_CHECK(launch_mv_scan((const uint32_t*)op.col->words.p, op.col->bits, (const uint32_t*)op.col->mv_offsets.p,
+                                 op.num_docs, op.lo, op.hi,
+                                 op.lut_off == ~0ull ? nullptr : (const uint32_t*)(dS + op.lut_off), op.excl,
+                                 (uint32_t*)(dS + op.out_off), s));
+        break;
+    }
+  }
+  HIP_CHECK(hipEventRecord(ev[1], s));
+  if (is_cancelled(plan->query_id)) return fail(PG_E_CANCELLED, "query %llu cancelled", (unsigned long long)plan->query_id);
+  if (plan->deadline_ms && now_ms() > plan->deadline_ms) return fail(PG_E_TIMEOUT, "deadline passed");
+  uint32_t blocks = 0;
+  if (q.total_tiles) {
+    int dev_cus = 256;
+    hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g_device);
+    const uint64_t cap = (uint64_t)dev_cus * 8;
+    blocks = (uint32_t)std::min<uint64_t>(q.total_tiles, cap);
+    HIP_CHECK(launch_scan(q, blocks, s));
+  }
+  HIP_CHECK(hipEventRecord(ev[2], s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  float pre_ms = 0, scan_ms = 0;
+  hipEventElapsedTime(&pre_ms, ev[0], ev[1]);
+  hipEventElapsedTime(&scan_ms, ev[1], ev[2]);
+  t_timing.prepass_ms = pre_ms;
+  t_timing.scan_ms = scan_ms;
+  t_timing.scan_launches = blocks ? 1 : 0;
+  memset(&stats, 0, sizeof(stats));
+  stats.num_total_docs = total_docs;
+  stats.num_segments_processed = S;
+  stats.num_entries_scanned_in_filter = entries_in_filter;
+  return PG_OK;
+}
+
+struct PartialsImpl {
+  Partials P;
+  std::vector<uint64_t> seg_matched_host;
+};
+
+int finalize(pg_partials* pp, const pg_plan* plan, pg_result** out) {
+  PartialsImpl* impl = (PartialsImpl*)pp->impl;
+  Partials& P = impl->P;
+  const uint64_t G = pp->num_slots;
+  const uint32_t A = plan->num_aggs, K = plan->num_keys;
+  if (A != P.aggs.size()) return fail(PG_E_INVALID, "plan does not match partials");
+  hipEvent_t e0, e1;
+  HIP_CHECK(hipEventCreate(&e0));
+  HIP_CHECK(hipEventCreate(&e1));
+  hipStream_t s = thread_stream();
+  HIP_CHECK(hipEventRecord(e0, s));
+  std::vector<int64_t> hi64(G * pp->n_i64), hmn(G * pp->n_min), hmx(G * pp->n_max);
+  std::vector<double> hf64(G * pp->n_f64);
+  std::vector<uint8_t> hflags(G * pp->flag_bytes_per_slot);
+  std::vector<uint64_t> sm(P.num_segments);
+  HIP_CHECK(hipMemcpyAsync(hi64.data(), pp->i64, hi64.size() * 8, hipMemcpyDeviceToHost, s));
+  if (!hf64.empty()) HIP_CHECK(hipMemcpyAsync(hf64.data(), pp->f64, hf64.size() * 8, hipMemcpyDeviceToHost, s));
+  if (!hmn.empty()) HIP_CHECK(hipMemcpyAsync(hmn.data(), pp->mn, hmn.size() * 8, hipMemcpyDeviceToHost, s));
+  if (!hmx.empty()) HIP_CHECK(hipMemcpyAsync(hmx.data(), pp->mx, hmx.size() * 8, hipMemcpyDeviceToHost, s));
+  if (!hflags.empty()) HIP_CHECK(hipMemcpyAsync(hflags.data(), pp->flags, hflags.size(), hipMemcpyDeviceToHost, s));
+  if (!sm.empty()) HIP_CHECK(hipMemcpyAsync(sm.data(), P.seg_matched.p, sm.size() * 8, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipEventRecord(e1, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  float fm = 0;
+  hipEventElapsedTime(&fm, e0, e1);
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  t_timing.finalize_ms = fm;
+
+  pg_result* r = (pg_result*)calloc(1, sizeof(pg_result));
+  r->stats = pp->stats;
+  uint64_t matched = 0, segs_matched = 0;
+  for (uint64_t v : sm) { matched += v; segs_matched += v > 0; }
+  // pp->stats may have been merged by the caller across ranks; only fill what is still zero
+  if (!r->stats.num_docs_scanned) r->stats.num_docs_scanned = matched;
+  if (!r->stats.num_segments_matched) r->stats.num_segments_matched = segs_matched;
+  r->stats.num_entries_scanned_post_filter = r->stats.num_docs_scanned * P.projected_cols;
+  r->num_keys = K;
+  r->num_aggs = A;
+  std::vector<uint64_t> gl;
+  if (K == 0) gl.push_back(0);
+  else
+    for (uint64_t g = 0; g < G; g++)
+      if (hi64[g * pp->n_i64] > 0) gl.push_back(g);
+  r->num_groups = gl.size();
+  r->keys = (uint32_t*)calloc(gl.size() * (K ? K : 1), 4);
+  r->values = (double*)calloc(gl.size() * (A ? A : 1), 8);
+  r->counts = (int64_t*)calloc(gl.size() * (A ? A : 1), 8);
+  for (uint64_t o = 0; o < gl.size(); o++) {
+    const uint64_t g = gl[o];
+    for (uint32_t k = 0; k < K; k++) r->keys[o * K + k] = (uint32_t)((g / P.key_stride[k]) % P.key_card[k]);
+    const int64_t cnt = hi64[g * pp->n_i64];
+    for (uint32_t a = 0; a < A; a++) {
+      const AggSpec& s2 = P.aggs[a];
+      double v = 0;
+      int64_t c2 = 0;
+      switch (s2.fn) {
+        case PG_AGG_COUNT: v = (double)cnt; break;
+        case PG_AGG_COUNTMV: v = (double)hi64[g * pp->n_i64 + s2.slot]; break;
+        case PG_AGG_SUM: case PG_AGG_AVG:
+          v = s2.integer ? (double)hi64[g * pp->n_i64 + s2.slot] : hf64[g * pp->n_f64 + s2.slot];
+          if (s2.fn == PG_AGG_AVG) c2 = cnt;
+          break;
+        case PG_AGG_MIN: v = order_key_decode(hmn[g * pp->n_min + s2.slot]); break;
+        case PG_AGG_MAX: v = order_key_decode(hmx[g * pp->n_max + s2.slot]); break;
+        case PG_AGG_DISTINCTCOUNT: {
+          uint64_t n = 0;
+          const uint8_t* f = &hflags[g * pp->flag_bytes_per_slot + s2.flag_off];
+          for (uint64_t x = 0; x < s2.key_card; x++) n += f[x] != 0;
+          v = (double)n;
+          break;
+        }
+      }
+      r->values[o * A + a] = v;
+      r->counts[o * A + a] = c2;
+    }
+  }
+  *out = r;
+  return PG_OK;
+}
+
+}  // namespace
+
+// ============================================================================================ C ABI
+
+extern "C" {
+
+int pg_abi_version(void) { return PG_ABI_VERSION; }
+
+int pg_init(int device) {
+  std::lock_guard<std::mutex> g(g_init_mu);
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(PG_E_HIP, "no HIP device visible");
+  if (device < 0 || device >= n) return fail(PG_E_INVALID, "device %d out of range (%d visible)", device, n);
+  if (g_device >= 0 && g_device != device) return fail(PG_E_STATE, "already bound to device %d", g_device);
+  HIP_CHECK(hipSetDevice(device));
+  g_device = device;
+  return PG_OK;
+}
+
+int pg_last_error(char* buf, size_t n) {
+  if (buf && n) {
+    strncpy(buf, t_err.c_str(), n - 1);
+    buf[n - 1] = 0;
+  }
+  return (int)t_err.size();
+}
+
+int pg_resident_bytes(uint64_t* out) {
+  if (!out) return fail(PG_E_INVALID, "null out");
+  std::shared_lock<std::shared_mutex> lk(g_seg_mu);
+  uint64_t t = 0;
+  for (auto& kv : g_segs)
+    for (auto& c : kv.second->cols)
+      t += c.second.dict.bytes + c.second.words.bytes + c.second.mv_offsets.bytes + c.second.roaring.bytes +
+           c.second.containers.bytes + c.second.keymap.bytes;
+  *out = t;
+  return PG_OK;
+}
+
+int pg_cancel(uint64_t query_id) {
+  std::lock_guard<std::mutex> g(g_cancel_mu);
+  g_cancelled.insert(query_id);
+  return PG_OK;
+}
+
+int pg_column_upload(uint64_t seg_key, uint32_t col_id, const pg_col_desc* desc, const void* src, uint64_t nbytes) {
+  int rc = ensure_device();
+  if (rc) return rc;
+  if (!desc || (!src && nbytes)) return fail(PG_E_INVALID, "null descriptor or source");
+  try {
+    return upload_column(seg_key, col_id, desc, src, nbytes);
+  } catch (const std::exception& e) {
+    return fail(PG_E_NOMEM, "upload failed: %s", e.what());
+  }
+}
+
+int pg_segment_release(uint64_t seg_key) {
+  int rc = ensure_device();
+  if (rc) return rc;
+  std::unique_lock<std::shared_mutex> lk(g_seg_mu);
+  auto it = g_segs.find(seg_key);
+  if (it == g_segs.end()) return fail(PG_E_NOTFOUND, "segment %llu not resident", (unsigned long long)seg_key);
+  delete it->second;
+  g_segs.erase(it);
+  return PG_OK;
+}
+
+int pg_execute_partial(const pg_plan* plan, pg_partials** out) {
+  int rc = ensure_device();
+  if (rc) return rc;
+  if (!out) return fail(PG_E_INVALID, "null out");
+  *out = nullptr;
+  PartialsImpl* impl = new (std::nothrow) PartialsImpl();
+  if (!impl) return fail(PG_E_NOMEM, "out of host memory");
+  pg_stats st;
+  try {
+    rc = compile_and_run(plan, impl->P, st);
+  } catch (const std::exception& e) {
+    rc = fail(PG_E_NOMEM, "execute failed: %s", e.what());
+  }
+  if (rc) { delete impl; return rc; }
+  pg_partials* p = (pg_partials*)calloc(1, sizeof(pg_partials));
+  p->stats = st;
+  p->num_slots = 1;
+  for (uint32_t c : impl->P.key_card) p->num_slots *= c;
+  uint32_t n_i64 = 1, n_f64 = 0, n_min = 0, n_max = 0;
+  uint64_t fb = 0;
+  for (const AggSpec& a : impl->P.aggs) {
+    if (a.kind == SK_I64) n_i64 = std::max(n_i64, a.slot + 1);
+    if (a.kind == SK_F64) n_f64 = std::max(n_f64, a.slot + 1);
+    if (a.kind == SK_MIN) n_min = std::max(n_min, a.slot + 1);
+    if (a.kind == SK_MAX) n_max = std::max(n_max, a.slot + 1);
+    if (a.kind == SK_FLAG) fb = std::max<uint64_t>(fb, a.flag_off + a.key_card);
+  }
+  p->n_i64 = n_i64; p->n_f64 = n_f64; p->n_min = n_min; p->n_max = n_max;
+  p->flag_bytes_per_slot = fb;
+  p->i64 = (int64_t*)impl->P.i64.p;
+  p->f64 = (double*)impl->P.f64.p;
+  p->mn = (int64_t*)impl->P.mn.p;
+  p->mx = (int64_t*)impl->P.mx.p;
+  p->flags = (uint8_t*)impl->P.flags.p;
+  p->impl = impl;
+  *out = p;
+  return PG_OK;
+}
+
+int pg_partials_finalize(pg_partials* p, const pg_plan* plan, pg_result** out) {
+  int rc = ensure_device();
+  if (rc) return rc;
+  if (!p || !plan || !out) return fail(PG_E_INVALID, "null argument");
+  try {
+    return finalize(p, plan, out);
+  } catch (const std::exception& e) {
+    return fail(PG_E_NOMEM, "finalize failed: %s", e.what());
+  }
+}
+
+int pg_partials_free(pg_partials* p) {
+  if (!p) return PG_OK;
+  ensure_device();
+  PartialsImpl* impl = (PartialsImpl*)p->impl;
+  if (impl) {
+    impl->P.i64.reset(); impl->P.f64.reset(); impl->P.mn.reset(); impl->P.mx.reset();
+    impl->P.flags.reset(); impl->P.seg_matched.reset();
+    delete impl;
+  }
+  free(p);
+  return PG_OK;
+}
+
+int pg_execute(const pg_plan* plan, pg_result** out) {
+  if (!out) return fail(PG_E_INVALID, "null out");
+  pg_partials* p = nullptr;
+  int rc = pg_execute_partial(plan, &p);
+  if (rc) return rc;
+  rc = pg_partials_finalize(p, plan, out);
+  pg_partials_free(p);
+  return rc;
+}
+
+int pg_result_free(pg_result* r) {
+  if (!r) return PG_OK;
+  free(r->keys);
+  free(r->values);
+  free(r->counts);
+  free(r);
+  return PG_OK;
+}
+
+int pg_last_timing(pg_timing* out) {
+  if (!out) return fail(PG_E_INVALID, "null out");
+  *out = t_timing;
+  return PG_OK;
+}
+
+}  // extern "C"

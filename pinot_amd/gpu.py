@@ -1,0 +1,187 @@
+"""GPU engine: loads libpinot_gpu.so (in-tree, gfx950) and drives it through the C ABI.
+
+There is deliberately NO fallback here: if the HIP library is missing or the device is absent the
+engine raises.  Falling back to the CPU is the caller's (Pinot's) decision on PG_E_UNSUPPORTED.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import itertools
+import os
+import threading
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import abi
+from .plan import CPlan, ExecutionStats, IntermediateResult, Table, UnsupportedQuery
+from .query import QueryContext, parse
+from .segment import Column, ImmutableSegment
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpinot_gpu.so")
+_lib = None
+_lib_lock = threading.Lock()
+
+
+class PinotGpuError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{abi.STATUS_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libpinot_gpu.so; raises if it has not been built (python __graft_entry__.py build)."""
+    global _lib
+    with _lib_lock:
+        if _lib is None:
+            if not os.path.exists(path):
+                raise FileNotFoundError(f"{path} missing: build it with `make -C pinot_amd/csrc`")
+            _lib = abi.declare(C.CDLL(path))
+            if _lib.pg_abi_version() != abi.PG_ABI_VERSION:
+                raise RuntimeError("libpinot_gpu ABI version mismatch")
+        return _lib
+
+
+def check(rc: int):
+    if rc != abi.PG_OK:
+        lib = load_library()
+        buf = C.create_string_buffer(2048)
+        lib.pg_last_error(buf, 2048)
+        err = PinotGpuError(rc, buf.value.decode(errors="replace"))
+        if rc == abi.PG_E_UNSUPPORTED:
+            raise UnsupportedQuery(str(err))
+        raise err
+
+
+_seg_counter = itertools.count(1)
+
+
+def fwd_desc(col: Column) -> abi.pg_col_desc:
+    d = abi.pg_col_desc()
+    d.kind = {"sv": abi.PG_IDX_FWD_SV_BITPACKED, "sorted": abi.PG_IDX_FWD_SV_SORTED,
+              "mv": abi.PG_IDX_FWD_MV_BITPACKED}[col.fwd_kind]
+    d.data_type = abi.DTYPE_CODES[col.data_type]
+    d.num_docs = col.num_docs
+    d.cardinality = col.cardinality
+    d.bits_per_element = col.bits_per_element
+    d.num_values = col.num_values
+    d.entry_bytes = col.dictionary.entry_bytes
+    return d
+
+
+class GpuEngine:
+    """One engine per process, bound to one GPU (one process per GPU)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        check(self.lib.pg_init(device))
+        self.device = device
+        self._seg_keys: Dict[int, int] = {}      # id(segment) -> seg_key
+        self._keymaps_uploaded = set()
+
+    # ---- residency (IndexingOverrides reader-provider hook)
+    def upload_segment(self, seg: ImmutableSegment, table: Table) -> int:
+        key = self._seg_keys.get(id(seg))
+        if key is not None:
+            return key
+        key = next(_seg_counter)
+        for name, col in seg.columns.items():
+            cid = table.column_ids[name]
+            d = fwd_desc(col)
+            dict_bytes = col.dictionary.to_bytes()
+            dd = abi.pg_col_desc.from_buffer_copy(d)
+            dd.kind = abi.PG_IDX_DICT
+            self._upload(key, cid, dd, dict_bytes)
+            self._upload(key, cid, d, col.fwd)
+            if col.inverted is not None:
+                di = abi.pg_col_desc.from_buffer_copy(d)
+                di.kind = abi.PG_IDX_INV_BITMAP
+                self._upload(key, cid, di, col.inverted)
+        self._seg_keys[id(seg)] = key
+        return key
+
+    def _upload(self, key, cid, desc, data: bytes):
+        buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, dtype=np.uint8)
+        check(self.lib.pg_column_upload(key, cid, C.byref(desc), buf.ctypes.data_as(C.c_void_p), len(data)))
+
+    def upload_keymaps(self, table: Table, plan: CPlan, segments, seg_keys):
+        spaces = list(plan.key_spaces)
+        for ag in plan.aggs:
+            if ag.function == "DISTINCTCOUNT":
+                spaces.append(table.key_space(ag.arg.cols[0]))
+        for ks in spaces:
+            if ks.kind != abi.PG_KEY_KEYMAP:
+                continue
+            cid = table.column_ids[ks.column]
+            for seg, key in zip(segments, seg_keys):
+                if (key, cid) in self._keymaps_uploaded:
+                    continue
+                km = np.ascontiguousarray(ks.keymaps[table.segments.index(seg)], dtype=np.int32)
+                d = abi.pg_col_desc()
+                d.kind = abi.PG_IDX_KEYMAP
+                d.cardinality = len(km)
+                check(self.lib.pg_column_upload(key, cid, C.byref(d), km.ctypes.data_as(C.c_void_p), km.nbytes))
+                self._keymaps_uploaded.add((key, cid))
+
+    def release(self, seg: ImmutableSegment):
+        key = self._seg_keys.pop(id(seg), None)
+        if key is not None:
+            check(self.lib.pg_segment_release(key))
+
+    # ---- execution
+    def make_plan(self, table: Table, query: QueryContext, segments: Optional[Sequence[ImmutableSegment]] = None,
+                  num_groups_limit=None) -> CPlan:
+        segments = list(table.segments if segments is None else segments)
+        keys = [self.upload_segment(s, table) for s in segments]
+        plan = CPlan(table, query, segments, keys, num_groups_limit)
+        self.upload_keymaps(table, plan, segments, keys)
+        return plan
+
+    def run_plan(self, plan: CPlan) -> IntermediateResult:
+        res = C.POINTER(abi.pg_result)()
+        check(self.lib.pg_execute(C.byref(plan.plan), C.byref(res)))
+        try:
+            return self.decode(plan, res.contents)
+        finally:
+            self.lib.pg_result_free(res)
+
+    def execute(self, table: Table, query, segments=None, num_groups_limit=None) -> IntermediateResult:
+        if isinstance(query, str):
+            query = parse(query)
+        return self.run_plan(self.make_plan(table, query, segments, num_groups_limit))
+
+    def last_timing(self) -> abi.pg_timing:
+        t = abi.pg_timing()
+        check(self.lib.pg_last_timing(C.byref(t)))
+        return t
+
+    @staticmethod
+    def decode(plan: CPlan, r: abi.pg_result) -> IntermediateResult:
+        A = r.num_aggs
+        K = r.num_keys
+        G = r.num_groups
+        vals = np.ctypeslib.as_array(r.values, shape=(max(G * A, 1),))[:G * A].reshape(G, A) if G and A else \
+            np.zeros((G, A))
+        cnts = np.ctypeslib.as_array(r.counts, shape=(max(G * A, 1),))[:G * A].reshape(G, A) if G and A else \
+            np.zeros((G, A), dtype=np.int64)
+        keys = np.ctypeslib.as_array(r.keys, shape=(max(G * K, 1),))[:G * K].reshape(G, K) if G and K else \
+            np.zeros((G, K), dtype=np.uint32)
+        rows = {}
+        for g in range(G):
+            key = tuple(plan.key_spaces[k].value(int(keys[g, k])) for k in range(K))
+            row = []
+            for a, ag in enumerate(plan.aggs):
+                v = float(vals[g, a])
+                f = ag.function
+                if f in ("COUNT", "COUNTMV", "DISTINCTCOUNT"):
+                    row.append(int(round(v)))
+                elif f == "AVG":
+                    row.append((v, int(cnts[g, a])))
+                else:
+                    row.append(v)
+            rows[key] = row
+        s = r.stats
+        st = ExecutionStats(s.num_docs_scanned, s.num_entries_scanned_in_filter, s.num_entries_scanned_post_filter,
+                            s.num_total_docs, s.num_segments_processed, s.num_segments_matched)
+        return IntermediateResult(plan.aggs, list(plan.query.group_by), rows, st)

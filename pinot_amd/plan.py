@@ -1,0 +1,406 @@
+"""GpuPlanMaker: QueryContext + segments -> lowered pg_plan (C ABI), and the value-keyed results.
+
+Host-side mirror of the reference's planning for the hot path:
+  * predicate lowering to dictId space per segment -- PredicateEvaluatorProvider.getPredicateEvaluator
+    (operator/filter/predicate/PredicateEvaluatorProvider.java:38-90) with the dictionary-based
+    EQ / NOT_EQ / IN / NOT_IN / RANGE evaluators (EqualsPredicateEvaluatorFactory.java:85-110,
+    NotEqualsPredicateEvaluatorFactory.java:85-, InPredicateEvaluatorFactory.java:153-199,
+    NotInPredicateEvaluatorFactory.java:153-, RangePredicateEvaluatorFactory.java:115-210) and their
+    isAlwaysTrue / isAlwaysFalse shortcuts;
+  * leaf operator choice -- FilterOperatorUtils.getLeafFilterOperator (operator/filter/FilterOperatorUtils.java:45-85):
+    always-false -> Empty, always-true -> MatchAll, sorted -> SortedIndex, inverted (non-RANGE) -> Bitmap, else scan;
+  * group keys -- table-global key ids so that the device merges segments by VALUE the way
+    GroupByOrderByCombineOperator merges Key(Object[]) (operator/combine/GroupByOrderByCombineOperator.java:176-183).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import itertools
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import abi
+from .query import UNBOUNDED, Aggregation, FilterContext, Predicate, QueryContext
+from .segment import Column, ImmutableSegment
+
+MAX_VALUE_OFFSET_KEYS = 1 << 26   # integer key ranges up to this size use value offsets (no keymap)
+DEFAULT_NUM_GROUPS_LIMIT = 100_000          # InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT
+DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY = 10_000  # InstancePlanMakerImplV2 :73
+
+
+class UnsupportedQuery(Exception):
+    """The query shape is not served by the device path (the caller falls back to the CPU plan)."""
+
+
+# ------------------------------------------------------------------------------------------ lowering
+
+@dataclass
+class LoweredLeaf:
+    kind: int
+    col_id: int
+    exclusive: int = 0
+    lo: int = 0
+    hi: int = 0
+    ids: Optional[np.ndarray] = None   # sorted unique int32
+
+
+def lower_predicate(pred: Predicate, col: Column, col_id: int) -> LoweredLeaf:
+    """Dictionary-based predicate evaluator + leaf operator choice for one segment's column."""
+    d = col.dictionary
+    card = len(d)
+    excl = 0
+    ids = None
+    lo = hi = 0
+    always_true = always_false = False
+    t = pred.type
+    if t in ("EQ", "NOT_EQ"):
+        i = d.index_of(pred.values[0])
+        if t == "EQ":
+            if i >= 0:
+                ids = np.array([i], dtype=np.int32)
+                always_true = card == 1
+            else:
+                always_false = True
+        else:
+            excl = 1
+            if i >= 0:
+                ids = np.array([i], dtype=np.int32)
+                always_false = card == 1
+            else:
+                always_true = True
+    elif t in ("IN", "NOT_IN"):
+        s = sorted({i for i in (d.index_of(v) for v in pred.values) if i >= 0})   # PredicateUtils.getDictIdSet
+        ids = np.asarray(s, dtype=np.int32)
+        if t == "IN":
+            always_false = len(s) == 0
+            always_true = len(s) == card
+        else:
+            excl = 1
+            always_true = len(s) == 0
+            always_false = len(s) == card
+    elif t == "RANGE":
+        # SortedDictionaryBasedRangePredicateEvaluator (RangePredicateEvaluatorFactory.java:115-166)
+        if pred.lower == UNBOUNDED:
+            start = 0
+        else:
+            ii = d.insertion_index_of(pred.lower)
+            start = -(ii + 1) if ii < 0 else (ii if pred.lower_inclusive else ii + 1)
+        if pred.upper == UNBOUNDED:
+            end = card
+        else:
+            ii = d.insertion_index_of(pred.upper)
+            end = -(ii + 1) if ii < 0 else (ii + 1 if pred.upper_inclusive else ii)
+        lo, hi = start, end
+        if end - start <= 0:
+            always_false = True
+        elif end - start == card:
+            always_true = True
+    else:
+        raise UnsupportedQuery(f"predicate type {t}")
+    if always_false:
+        return LoweredLeaf(abi.PG_LEAF_EMPTY, col_id)
+    if always_true:
+        return LoweredLeaf(abi.PG_LEAF_MATCH_ALL, col_id)
+    if col.single_value and col.is_sorted:
+        kind = abi.PG_LEAF_SORTED
+    elif col.inverted is not None and t != "RANGE":
+        kind = abi.PG_LEAF_INVERTED
+    else:
+        kind = abi.PG_LEAF_SV_SCAN if col.single_value else abi.PG_LEAF_MV_SCAN
+    return LoweredLeaf(kind, col_id, excl, lo, hi, ids)
+
+
+def filter_program(f: Optional[FilterContext]) -> Tuple[List[int], List[Predicate]]:
+    """Postfix program over leaves (FilterPlanNode.constructPhysicalOperator's tree, in postfix)."""
+    ops: List[int] = []
+    leaves: List[Predicate] = []
+
+    def walk(n: FilterContext):
+        if n.type == "PREDICATE":
+            ops.append(len(leaves))
+            leaves.append(n.predicate)
+        elif n.type == "NOT":
+            walk(n.children[0])
+            ops.append(abi.PG_OP_NOT)
+        else:
+            for c in n.children:
+                walk(c)
+            ops.append(abi.PG_OP_AND(len(n.children)) if n.type == "AND" else abi.PG_OP_OR(len(n.children)))
+
+    if f is not None:
+        walk(f)
+    return ops, leaves
+
+
+# ------------------------------------------------------------------------------------------ table
+
+class Table:
+    """A set of immutable segments of one table + the table-global key spaces of its columns."""
+
+    def __init__(self, name: str, segments: Sequence[ImmutableSegment]):
+        self.name = name
+        self.segments = list(segments)
+        cols = []
+        for s in self.segments:
+            for c in s.columns:
+                if c not in cols:
+                    cols.append(c)
+        self.column_ids = {c: i for i, c in enumerate(cols)}
+        self._key_spaces: Dict[str, "KeySpace"] = {}
+
+    def data_type(self, column: str) -> str:
+        return self.segments[0].columns[column].data_type
+
+    def key_space(self, column: str) -> "KeySpace":
+        ks = self._key_spaces.get(column)
+        if ks is None:
+            ks = KeySpace.build(column, [s.columns[column] for s in self.segments])
+            self._key_spaces[column] = ks
+        return ks
+
+
+@dataclass
+class KeySpace:
+    """Table-global ids for the values of one column (group keys / DISTINCTCOUNT values)."""
+    column: str
+    kind: int                        # PG_KEY_VALUE_OFFSET or PG_KEY_KEYMAP
+    cardinality: int
+    base: int = 0
+    values: Optional[list] = None    # KEYMAP: global id -> value (sorted union)
+    keymaps: Optional[List[np.ndarray]] = None  # per segment dictId -> global id
+
+    @staticmethod
+    def build(column: str, cols: List[Column]) -> "KeySpace":
+        dt = cols[0].data_type
+        if dt in ("INT", "LONG"):
+            lo = min(int(c.dictionary.values[0]) for c in cols)
+            hi = max(int(c.dictionary.values[-1]) for c in cols)
+            if hi - lo + 1 <= MAX_VALUE_OFFSET_KEYS:
+                return KeySpace(column, abi.PG_KEY_VALUE_OFFSET, hi - lo + 1, lo)
+        if dt in ("INT", "LONG", "FLOAT", "DOUBLE"):
+            allv = np.unique(np.concatenate([np.asarray(c.dictionary.values) for c in cols]))
+            keymaps = [np.searchsorted(allv, np.asarray(c.dictionary.values)).astype(np.int32) for c in cols]
+            return KeySpace(column, abi.PG_KEY_KEYMAP, len(allv), 0, list(allv.tolist()), keymaps)
+        allv = sorted(set(itertools.chain.from_iterable(c.dictionary.values for c in cols)))
+        index = {v: i for i, v in enumerate(allv)}
+        keymaps = [np.asarray([index[v] for v in c.dictionary.values], dtype=np.int32) for c in cols]
+        return KeySpace(column, abi.PG_KEY_KEYMAP, len(allv), 0, allv, keymaps)
+
+    def value(self, gid: int):
+        if self.kind == abi.PG_KEY_VALUE_OFFSET:
+            return int(self.base + gid)
+        return self.values[gid]
+
+
+# ------------------------------------------------------------------------------------------ results
+
+@dataclass
+class ExecutionStats:
+    num_docs_scanned: int = 0
+    num_entries_scanned_in_filter: int = 0
+    num_entries_scanned_post_filter: int = 0
+    num_total_docs: int = 0
+    num_segments_processed: int = 0
+    num_segments_matched: int = 0
+
+
+@dataclass
+class IntermediateResult:
+    """Server-side combined result: aggregation-only -> one row under key (); group-by -> value-keyed rows.
+
+    Per aggregation the intermediate value follows the reference's intermediate types:
+    COUNT / COUNTMV int, SUM / MIN / MAX float, AVG (sum, count), DISTINCTCOUNT a set of values or
+    (device path) the distinct count as an int."""
+    aggregations: List[Aggregation]
+    group_by: List[str]
+    rows: Dict[tuple, list]
+    stats: ExecutionStats = field(default_factory=ExecutionStats)
+
+
+def merge_intermediate(aggs: List[Aggregation], a: list, b: list) -> list:
+    """AggregationFunction.merge for each function (e.g. SumAggregationFunction.java:268-278)."""
+    out = []
+    for ag, x, y in zip(aggs, a, b):
+        f = ag.function
+        if f in ("COUNT", "COUNTMV", "SUM"):
+            out.append(x + y)
+        elif f == "MIN":
+            out.append(min(x, y))
+        elif f == "MAX":
+            out.append(max(x, y))
+        elif f == "AVG":
+            out.append((x[0] + y[0], x[1] + y[1]))
+        elif f == "DISTINCTCOUNT":
+            if isinstance(x, set) and isinstance(y, set):
+                out.append(x | y)
+            else:
+                raise ValueError("cannot merge distinct counts without value sets")
+        else:
+            raise ValueError(f)
+    return out
+
+
+def final_value(ag: Aggregation, v):
+    """extractFinalResult of each function (e.g. AvgAggregationFunction.java:276-286)."""
+    f = ag.function
+    if f in ("COUNT", "COUNTMV"):
+        return int(round(v))
+    if f in ("SUM", "MIN", "MAX"):
+        return float(v)
+    if f == "AVG":
+        s, c = v
+        return float("-inf") if c == 0 else s / c
+    if f == "DISTINCTCOUNT":
+        return len(v) if isinstance(v, set) else int(v)
+    raise ValueError(f)
+
+
+def reduce_to_rows(query: QueryContext, res: IntermediateResult) -> Tuple[List[str], List[list]]:
+    """Broker reduce: final values, ORDER BY (with the remaining select columns as implicit tie-breakers
+    only when the ORDER BY names them), LIMIT (BrokerReduceService / GroupByDataTableReducer)."""
+    aggs = res.aggregations
+    agg_index = {a: i for i, a in enumerate(aggs)}
+    names = [s.name() for s in query.select]
+    rows_out = []
+    if not query.group_by:
+        vals = res.rows.get((), None)
+        row = []
+        for s in query.select:
+            row.append(final_value(s.agg, vals[agg_index[s.agg]]))
+        return names, [row]
+    keyed = []
+    for key, vals in res.rows.items():
+        finals = [final_value(a, v) for a, v in zip(aggs, vals)]
+        keyed.append((key, finals))
+
+    def sort_key(item):
+        key, finals = item
+        parts = []
+        for o in query.order_by:
+            if o.kind == "AGG":
+                v = finals[agg_index[o.agg]]
+            else:
+                v = key[query.group_by.index(o.column)]
+            parts.append(_Ord(v, o.asc))
+        return parts
+
+    if query.order_by:
+        keyed.sort(key=sort_key)
+    for key, finals in keyed[:query.limit]:
+        row = []
+        for s in query.select:
+            row.append(key[query.group_by.index(s.column)] if s.kind == "COL" else finals[agg_index[s.agg]])
+        rows_out.append(row)
+    return names, rows_out
+
+
+class _Ord:
+    __slots__ = ("v", "asc")
+
+    def __init__(self, v, asc):
+        self.v = v
+        self.asc = asc
+
+    def __lt__(self, other):
+        return self.v < other.v if self.asc else self.v > other.v
+
+    def __eq__(self, other):
+        return self.v == other.v
+
+
+# ------------------------------------------------------------------------------------------ C plan
+
+class CPlan:
+    """Owns every ctypes array a pg_plan points to (kept alive while the plan is in use)."""
+
+    def __init__(self, table: Table, query: QueryContext, segments: Sequence[ImmutableSegment],
+                 seg_keys: Sequence[int], num_groups_limit: Optional[int] = None):
+        self.table = table
+        self.query = query
+        self.aggs = query.aggregations
+        self._keep = []
+        cid = table.column_ids
+        ops, preds = filter_program(query.filter)
+        self.leaf_preds = preds
+        L = len(preds)
+        S = len(segments)
+        seg_arr = (abi.pg_segment_ref * max(S, 1))()
+        self.lowered: List[List[LoweredLeaf]] = []
+        for si, (seg, key) in enumerate(zip(segments, seg_keys)):
+            leaves = (abi.pg_leaf * max(L, 1))()
+            lows = []
+            for li, p in enumerate(preds):
+                if p.column not in seg.columns:
+                    raise UnsupportedQuery(f"unknown column {p.column}")
+                lw = lower_predicate(p, seg.columns[p.column], cid[p.column])
+                lows.append(lw)
+                leaves[li].kind = lw.kind
+                leaves[li].col_id = lw.col_id
+                leaves[li].exclusive = lw.exclusive
+                leaves[li].lo = lw.lo
+                leaves[li].hi = lw.hi
+                if lw.ids is not None and len(lw.ids):
+                    arr = np.ascontiguousarray(lw.ids, dtype=np.int32)
+                    self._keep.append(arr)
+                    leaves[li].num_ids = len(arr)
+                    leaves[li].ids = arr.ctypes.data_as(C.POINTER(C.c_int32))
+            self.lowered.append(lows)
+            self._keep.append(leaves)
+            seg_arr[si].seg_key = key
+            seg_arr[si].num_docs = seg.num_docs
+            seg_arr[si].leaves = leaves
+        self._keep.append(seg_arr)
+        ops_arr = (C.c_int32 * max(len(ops), 1))(*ops)
+        self._keep.append(ops_arr)
+
+        aggs = (abi.pg_agg * max(len(self.aggs), 1))()
+        for i, ag in enumerate(self.aggs):
+            aggs[i].fn = abi.AGG_CODES[ag.function]
+            e = ag.arg
+            if ag.function != "COUNT":
+                if e.op == "STAR":
+                    raise UnsupportedQuery(f"{ag.function}(*)")
+                aggs[i].col_a = cid[e.cols[0]]
+                aggs[i].op = {"COL": abi.PG_EXPR_COL, "MUL": abi.PG_EXPR_MUL, "ADD": abi.PG_EXPR_ADD,
+                              "SUB": abi.PG_EXPR_SUB}[e.op]
+                if e.op != "COL":
+                    if ag.function not in ("SUM", "MIN", "MAX", "AVG"):
+                        raise UnsupportedQuery(f"{ag.function} over an expression")
+                    aggs[i].col_b = cid[e.cols[1]]
+                for c in e.cols:
+                    if table.data_type(c) in ("STRING", "BYTES") and ag.function not in ("DISTINCTCOUNT",):
+                        raise UnsupportedQuery(f"{ag.function} on non-numeric column {c}")
+                if ag.function == "DISTINCTCOUNT":
+                    ks = table.key_space(e.cols[0])
+                    aggs[i].key_kind = ks.kind
+                    aggs[i].key_cardinality = ks.cardinality
+                    aggs[i].key_base = ks.base
+        self._keep.append(aggs)
+        keys = (abi.pg_key * max(len(query.group_by), 1))()
+        self.key_spaces = []
+        for k, col in enumerate(query.group_by):
+            ks = table.key_space(col)
+            self.key_spaces.append(ks)
+            keys[k].col_id = cid[col]
+            keys[k].kind = ks.kind
+            keys[k].cardinality = ks.cardinality
+            keys[k].base = ks.base
+        self._keep.append(keys)
+
+        p = abi.pg_plan()
+        p.abi_version = abi.PG_ABI_VERSION
+        p.num_segments = S
+        p.segments = seg_arr
+        p.num_leaves = L
+        p.num_ops = len(ops)
+        p.ops = ops_arr
+        p.num_aggs = len(self.aggs)
+        p.num_keys = len(query.group_by)
+        p.aggs = aggs
+        p.keys = keys
+        lim = num_groups_limit or int(query.options.get("numGroupsLimit", DEFAULT_NUM_GROUPS_LIMIT))
+        p.num_groups_limit = lim
+        self.plan = p
+        self.ops = ops

@@ -1,0 +1,328 @@
+"""QueryContext: the query IR the hot path consumes, built from the SQL subset Pinot's tests use.
+
+Mirrors pinot-core's QueryContext (core/query/request/context/QueryContext.java:73-122) and the
+FilterContext / Predicate types of pinot-common (request/context/FilterContext.java,
+request/context/predicate/*.java).  Comparison operators are rewritten into predicates the way
+RequestContextUtils does: `a > v` -> RANGE (v, *) exclusive, `a BETWEEN x AND y` -> RANGE [x, y],
+`a <> v` / `a != v` -> NOT_EQ.
+"""
+from __future__ import annotations
+
+import re
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple, Union
+
+UNBOUNDED = "*"  # RangePredicate.UNBOUNDED
+
+
+# ------------------------------------------------------------------------------------------ IR
+
+@dataclass(frozen=True)
+class Predicate:
+    type: str                 # EQ, NOT_EQ, IN, NOT_IN, RANGE
+    column: str
+    values: Tuple[str, ...] = ()
+    lower: str = UNBOUNDED
+    upper: str = UNBOUNDED
+    lower_inclusive: bool = False
+    upper_inclusive: bool = False
+
+    @property
+    def is_exclusive(self):
+        return self.type in ("NOT_EQ", "NOT_IN")
+
+
+@dataclass
+class FilterContext:
+    type: str                                   # AND, OR, NOT, PREDICATE
+    children: List["FilterContext"] = field(default_factory=list)
+    predicate: Optional[Predicate] = None
+
+    def leaves(self) -> List[Predicate]:
+        if self.type == "PREDICATE":
+            return [self.predicate]
+        out = []
+        for c in self.children:
+            out.extend(c.leaves())
+        return out
+
+
+@dataclass(frozen=True)
+class Expr:
+    """Aggregation input / group-by / order-by expression: a column, a binary op of columns, or '*'."""
+    op: str                       # COL, MUL, ADD, SUB, STAR
+    cols: Tuple[str, ...] = ()
+
+    def __str__(self):
+        if self.op == "STAR":
+            return "*"
+        if self.op == "COL":
+            return self.cols[0]
+        sym = {"MUL": "times", "ADD": "plus", "SUB": "minus"}[self.op]
+        return f"{sym}({self.cols[0]},{self.cols[1]})"
+
+
+@dataclass(frozen=True)
+class Aggregation:
+    function: str     # COUNT, SUM, MIN, MAX, AVG, DISTINCTCOUNT, COUNTMV
+    arg: Expr
+
+    def result_name(self):
+        return f"{self.function.lower()}({self.arg})"
+
+
+@dataclass
+class SelectItem:
+    kind: str                      # AGG or COL
+    agg: Optional[Aggregation] = None
+    column: Optional[str] = None
+    alias: Optional[str] = None
+
+    def name(self):
+        if self.alias:
+            return self.alias
+        return self.agg.result_name() if self.kind == "AGG" else self.column
+
+
+@dataclass
+class OrderBy:
+    kind: str                      # AGG, COL, ALIAS
+    agg: Optional[Aggregation] = None
+    column: Optional[str] = None
+    asc: bool = True
+
+
+@dataclass
+class QueryContext:
+    table: str
+    select: List[SelectItem]
+    filter: Optional[FilterContext]
+    group_by: List[str]
+    order_by: List[OrderBy]
+    limit: int
+    options: dict = field(default_factory=dict)
+
+    @property
+    def aggregations(self) -> List[Aggregation]:
+        """Distinct aggregations in first-seen order (QueryContext._aggregationFunctions)."""
+        out = []
+        for s in self.select:
+            if s.kind == "AGG" and s.agg not in out:
+                out.append(s.agg)
+        for o in self.order_by:
+            if o.kind == "AGG" and o.agg not in out:
+                out.append(o.agg)
+        return out
+
+
+# ------------------------------------------------------------------------------------------ parser
+
+_TOKEN = re.compile(r"\s*(?:(?P<num>-?\d+(?:\.\d+)?(?:[eE][-+]?\d+)?)|(?P<str>'(?:[^']|'')*')|"
+                    r"(?P<id>[A-Za-z_][A-Za-z0-9_.$]*)|(?P<op><>|!=|<=|>=|[=<>*+\-(),]))")
+_KEYWORDS = {"SELECT", "FROM", "WHERE", "GROUP", "BY", "ORDER", "LIMIT", "AND", "OR", "NOT", "IN", "BETWEEN",
+             "ASC", "DESC", "AS", "OPTION"}
+_AGGS = {"COUNT", "SUM", "MIN", "MAX", "AVG", "DISTINCTCOUNT", "COUNTMV"}
+
+
+def _tokenize(sql: str):
+    pos = 0
+    out = []
+    sql = sql.strip().rstrip(";")
+    while pos < len(sql):
+        m = _TOKEN.match(sql, pos)
+        if not m or m.end() == pos:
+            if sql[pos:].strip() == "":
+                break
+            raise ValueError(f"cannot tokenize at: {sql[pos:pos + 20]!r}")
+        pos = m.end()
+        if m.group("num") is not None:
+            out.append(("num", m.group("num")))
+        elif m.group("str") is not None:
+            out.append(("str", m.group("str")[1:-1].replace("''", "'")))
+        elif m.group("id") is not None:
+            v = m.group("id")
+            out.append(("kw", v.upper()) if v.upper() in _KEYWORDS else ("id", v))
+        else:
+            out.append(("op", m.group("op")))
+    return out
+
+
+class _Parser:
+    def __init__(self, sql):
+        self.t = _tokenize(sql)
+        self.i = 0
+
+    def peek(self, k=0):
+        return self.t[self.i + k] if self.i + k < len(self.t) else (None, None)
+
+    def next(self):
+        tok = self.peek()
+        self.i += 1
+        return tok
+
+    def accept(self, kind, val=None):
+        k, v = self.peek()
+        if k == kind and (val is None or v == val):
+            self.i += 1
+            return True
+        return False
+
+    def expect(self, kind, val=None):
+        k, v = self.next()
+        if k != kind or (val is not None and v != val):
+            raise ValueError(f"expected {val or kind}, got {v!r}")
+        return v
+
+    # expressions used inside aggregations: col | col op col | *
+    def expr(self) -> Expr:
+        if self.accept("op", "*"):
+            return Expr("STAR")
+        a = self.expect("id")
+        k, v = self.peek()
+        if k == "op" and v in ("*", "+", "-"):
+            self.next()
+            b = self.expect("id")
+            return Expr({"*": "MUL", "+": "ADD", "-": "SUB"}[v], (a, b))
+        return Expr("COL", (a,))
+
+    def agg_or_col(self):
+        k, v = self.peek()
+        if k == "id" and v.upper() in _AGGS and self.peek(1) == ("op", "("):
+            self.next()
+            self.expect("op", "(")
+            e = self.expr()
+            self.expect("op", ")")
+            fn = v.upper()
+            if fn == "COUNT":
+                e = Expr("STAR")
+            return "AGG", Aggregation(fn, e)
+        return "COL", self.expect("id")
+
+    def literal(self) -> str:
+        k, v = self.next()
+        if k in ("num", "str"):
+            return v
+        raise ValueError(f"expected literal, got {v!r}")
+
+    def predicate(self) -> FilterContext:
+        if self.accept("op", "("):
+            f = self.or_expr()
+            self.expect("op", ")")
+            return f
+        if self.accept("kw", "NOT"):
+            return FilterContext("NOT", [self.predicate()])
+        col = self.expect("id")
+        if self.accept("kw", "BETWEEN"):
+            lo = self.literal()
+            self.expect("kw", "AND")
+            hi = self.literal()
+            return FilterContext("PREDICATE", predicate=Predicate("RANGE", col, (), lo, hi, True, True))
+        neg = self.accept("kw", "NOT")
+        if self.accept("kw", "IN"):
+            self.expect("op", "(")
+            vals = [self.literal()]
+            while self.accept("op", ","):
+                vals.append(self.literal())
+            self.expect("op", ")")
+            return FilterContext("PREDICATE", predicate=Predicate("NOT_IN" if neg else "IN", col, tuple(vals)))
+        if neg:
+            raise ValueError("NOT must be followed by IN")
+        op = self.expect("op")
+        v = self.literal()
+        if op == "=":
+            p = Predicate("EQ", col, (v,))
+        elif op in ("!=", "<>"):
+            p = Predicate("NOT_EQ", col, (v,))
+        elif op == ">":
+            p = Predicate("RANGE", col, (), v, UNBOUNDED, False, False)
+        elif op == ">=":
+            p = Predicate("RANGE", col, (), v, UNBOUNDED, True, False)
+        elif op == "<":
+            p = Predicate("RANGE", col, (), UNBOUNDED, v, False, False)
+        elif op == "<=":
+            p = Predicate("RANGE", col, (), UNBOUNDED, v, False, True)
+        else:
+            raise ValueError(f"unsupported operator {op}")
+        return FilterContext("PREDICATE", predicate=p)
+
+    def and_expr(self) -> FilterContext:
+        parts = [self.predicate()]
+        while self.accept("kw", "AND"):
+            parts.append(self.predicate())
+        return parts[0] if len(parts) == 1 else FilterContext("AND", _flatten("AND", parts))
+
+    def or_expr(self) -> FilterContext:
+        parts = [self.and_expr()]
+        while self.accept("kw", "OR"):
+            parts.append(self.and_expr())
+        return parts[0] if len(parts) == 1 else FilterContext("OR", _flatten("OR", parts))
+
+
+def _flatten(kind, parts):
+    """FilterContext flattening of nested AND/AND and OR/OR (QueryOptimizer FlattenAndOrFilterOptimizer)."""
+    out = []
+    for p in parts:
+        out.extend(p.children if p.type == kind else [p])
+    return out
+
+
+def parse(sql: str) -> QueryContext:
+    p = _Parser(sql)
+    p.expect("kw", "SELECT")
+    select = []
+    while True:
+        kind, x = p.agg_or_col()
+        alias = None
+        if p.accept("kw", "AS"):
+            alias = p.expect("id")
+        select.append(SelectItem(kind, agg=x if kind == "AGG" else None, column=x if kind == "COL" else None,
+                                 alias=alias))
+        if not p.accept("op", ","):
+            break
+    p.expect("kw", "FROM")
+    table = p.expect("id")
+    filt = None
+    if p.accept("kw", "WHERE"):
+        filt = p.or_expr()
+    group_by = []
+    if p.accept("kw", "GROUP"):
+        p.expect("kw", "BY")
+        group_by.append(p.expect("id"))
+        while p.accept("op", ","):
+            group_by.append(p.expect("id"))
+    order_by = []
+    if p.accept("kw", "ORDER"):
+        p.expect("kw", "BY")
+        while True:
+            kind, x = p.agg_or_col()
+            asc = True
+            if p.accept("kw", "DESC"):
+                asc = False
+            else:
+                p.accept("kw", "ASC")
+            if kind == "AGG":
+                order_by.append(OrderBy("AGG", agg=x, asc=asc))
+            else:
+                aliases = {s.alias: s for s in select if s.alias}
+                if x in aliases and aliases[x].kind == "AGG":
+                    order_by.append(OrderBy("AGG", agg=aliases[x].agg, asc=asc))
+                else:
+                    order_by.append(OrderBy("COL", column=x, asc=asc))
+            if not p.accept("op", ","):
+                break
+    limit = 10  # SQL default LIMIT in Pinot
+    if p.accept("kw", "LIMIT"):
+        limit = int(p.expect("num"))
+    options = {}
+    if p.accept("kw", "OPTION"):
+        p.expect("op", "(")
+        while True:
+            k = p.expect("id")
+            p.expect("op", "=")
+            options[k] = p.literal()
+            if not p.accept("op", ","):
+                break
+        p.expect("op", ")")
+    if p.peek() != (None, None):
+        raise ValueError(f"trailing tokens: {p.t[p.i:]}")
+    return QueryContext(table, select, filt, group_by, order_by, limit, options)

@@ -1,0 +1,518 @@
+"""Pinot immutable-segment on-disk formats (host side): writer + reader.
+
+This is the segment-creation / segment-load side of the hot path.  It produces and parses
+exactly the byte layouts the reference writes, so the device path consumes real Pinot bytes:
+
+* bit packing        -- PinotDataBitSet / FixedBitIntReaderWriter: value i occupies bits
+                        [i*b, (i+1)*b) of a big-endian byte stream, MSB first
+                        (pinot-segment-local/.../io/util/PinotDataBitSet.java:59-135,
+                         io/writer/impl/FixedBitSVForwardIndexWriter.java:42-44).
+* bits per value     -- PinotDataBitSet.getNumBitsPerValue(cardinality - 1) (:59-70).
+* dictionary         -- sorted unique values, fixed width big-endian; strings padded with '\\0'
+                        to the longest UTF-8 length (segment/creator/impl/SegmentDictionaryCreator.java:73-250,
+                        readers/BaseImmutableDictionary.java).
+* sorted fwd index   -- per dictId big-endian int32 (startDocId, endDocId) inclusive
+                        (readers/sorted/SortedIndexReaderImpl.java:37-117).
+* MV fwd index       -- [chunk offsets BE int32][start-of-row bitmap][packed values]
+                        (readers/forward/FixedBitMVForwardIndexReader.java:33-75,
+                         io/writer/impl/FixedBitMVForwardIndexWriter.java:77-100).
+* inverted index     -- (card+1) BE uint32 offsets then portable RoaringBitmaps
+                        (segment/creator/impl/inv/BitmapInvertedIndexWriter.java:35-78,
+                         readers/BitmapInvertedIndexReader.java:45-63); roaring portable format of
+                         RoaringBitmap 0.9.28 (third-party, not vendored: restated from its published spec).
+* V1 directory       -- <col>.dict, <col>.sv.unsorted.fwd, <col>.sv.sorted.fwd, <col>.mv.fwd,
+                        <col>.bitmap.inv, metadata.properties (pinot-segment-spi/.../V1Constants.java).
+"""
+from __future__ import annotations
+
+import bisect
+import os
+import struct
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+DATA_TYPES = ("INT", "LONG", "FLOAT", "DOUBLE", "STRING", "BYTES")
+_NP_BE = {"INT": ">i4", "LONG": ">i8", "FLOAT": ">f4", "DOUBLE": ">f8"}
+_NP_NATIVE = {"INT": np.int32, "LONG": np.int64, "FLOAT": np.float32, "DOUBLE": np.float64}
+PREFERRED_NUM_VALUES_PER_CHUNK = 2048  # FixedBitMVForwardIndexWriter.java:52
+
+
+def num_bits_per_value(max_value: int) -> int:
+    """PinotDataBitSet.getNumBitsPerValue (PinotDataBitSet.java:59-70): at least one bit."""
+    if max_value <= 1:
+        return 1
+    return int(max_value).bit_length()
+
+
+# ----------------------------------------------------------------------------- bit packing
+
+def pack_bits(values: np.ndarray, b: int) -> bytes:
+    """Pack non-negative ints < 2**b MSB-first into ceil(n*b/8) bytes (FixedBitIntReaderWriter)."""
+    v = np.asarray(values, dtype=np.uint64)
+    n = v.size
+    nbytes = (n * b + 7) // 8
+    if n == 0:
+        return b""
+    out = np.zeros(nbytes, dtype=np.uint8)
+    # process in chunks to bound memory (n*b bools)
+    chunk = max(1, (1 << 22) // max(1, b)) // 8 * 8
+    shifts = np.arange(b - 1, -1, -1, dtype=np.uint64)
+    for s in range(0, n, chunk):
+        part = v[s:s + chunk]
+        bits = ((part[:, None] >> shifts[None, :]) & np.uint64(1)).astype(np.uint8).ravel()
+        packed = np.packbits(bits)  # MSB-first
+        start_bit = s * b
+        assert start_bit % 8 == 0
+        out[start_bit // 8: start_bit // 8 + packed.size] |= packed
+    return out.tobytes()
+
+
+def unpack_bits(buf: bytes, n: int, b: int, start: int = 0) -> np.ndarray:
+    """Inverse of pack_bits (PinotDataBitSet.readInt semantics) for values [start, start+n)."""
+    if n == 0:
+        return np.zeros(0, dtype=np.int64)
+    a = np.frombuffer(buf, dtype=np.uint8)
+    bits = np.unpackbits(a)
+    idx = (np.arange(start, start + n, dtype=np.int64)[:, None] * b + np.arange(b)[None, :])
+    sel = bits[idx].astype(np.int64)
+    weights = (1 << np.arange(b - 1, -1, -1, dtype=np.int64))
+    return (sel * weights[None, :]).sum(axis=1)
+
+
+def pack_bitmap(positions: np.ndarray, nbits: int) -> bytes:
+    """PinotDataBitSet bitmap: bit i set (MSB-first in each byte)."""
+    bits = np.zeros(((nbits + 7) // 8) * 8, dtype=np.uint8)
+    bits[np.asarray(positions, dtype=np.int64)] = 1
+    return np.packbits(bits).tobytes()
+
+
+# ----------------------------------------------------------------------------- roaring (portable)
+
+SERIAL_COOKIE_NO_RUNCONTAINER = 12346
+SERIAL_COOKIE = 12347
+NO_OFFSET_THRESHOLD = 4
+
+
+def roaring_serialize(doc_ids: np.ndarray, run_optimize: bool = True) -> bytes:
+    """Portable RoaringBitmap serialization of a sorted set of uint32 doc ids.
+
+    Container choice mirrors RoaringBitmap: array if card <= 4096, else bitmap; with run_optimize
+    a run container replaces either when it is strictly smaller (RoaringBitmap.runOptimize)."""
+    ids = np.unique(np.asarray(doc_ids, dtype=np.uint32))
+    keys = (ids >> 16).astype(np.uint16)
+    lows = (ids & 0xFFFF).astype(np.uint16)
+    ukeys, starts = np.unique(keys, return_index=True)
+    bounds = list(starts) + [ids.size]
+    containers = []
+    for ci, k in enumerate(ukeys):
+        lo = lows[bounds[ci]:bounds[ci + 1]]
+        card = lo.size
+        # runs
+        brk = np.nonzero(np.diff(lo.astype(np.int32)) != 1)[0]
+        run_starts = np.concatenate([[0], brk + 1])
+        run_ends = np.concatenate([brk, [card - 1]])
+        nruns = run_starts.size
+        run_size = 2 + 4 * nruns
+        plain_size = 2 * card if card <= 4096 else 8192
+        if run_optimize and run_size < plain_size:
+            payload = struct.pack("<H", nruns) + b"".join(
+                struct.pack("<HH", int(lo[s]), int(lo[e] - lo[s])) for s, e in zip(run_starts, run_ends))
+            containers.append((int(k), card, "run", payload))
+        elif card <= 4096:
+            containers.append((int(k), card, "array", lo.astype("<u2").tobytes()))
+        else:
+            words = np.zeros(1024, dtype=np.uint64)
+            np.bitwise_or.at(words, (lo >> 6).astype(np.int64), (np.uint64(1) << (lo & 63).astype(np.uint64)))
+            containers.append((int(k), card, "bitmap", words.astype("<u8").tobytes()))
+    size = len(containers)
+    has_run = any(c[2] == "run" for c in containers)
+    out = bytearray()
+    if has_run:
+        out += struct.pack("<HH", SERIAL_COOKIE, size - 1)
+        flags = bytearray((size + 7) // 8)
+        for i, c in enumerate(containers):
+            if c[2] == "run":
+                flags[i // 8] |= 1 << (i % 8)
+        out += flags
+    else:
+        out += struct.pack("<II", SERIAL_COOKIE_NO_RUNCONTAINER, size)
+    for k, card, _, _ in containers:
+        out += struct.pack("<HH", k, card - 1)
+    if (not has_run) or size >= NO_OFFSET_THRESHOLD:
+        off = len(out) + 4 * size
+        for c in containers:
+            out += struct.pack("<I", off)
+            off += len(c[3])
+    for c in containers:
+        out += c[3]
+    return bytes(out)
+
+
+def roaring_deserialize(buf: bytes) -> np.ndarray:
+    """Decode a portable RoaringBitmap into sorted uint32 ids."""
+    (cookie,) = struct.unpack_from("<I", buf, 0)
+    pos = 0
+    run_flags = None
+    if (cookie & 0xFFFF) == SERIAL_COOKIE:
+        size = (cookie >> 16) + 1
+        pos = 4
+        nb = (size + 7) // 8
+        run_flags = buf[pos:pos + nb]
+        pos += nb
+    elif cookie == SERIAL_COOKIE_NO_RUNCONTAINER:
+        (size,) = struct.unpack_from("<I", buf, 4)
+        pos = 8
+    else:
+        raise ValueError("bad roaring cookie %d" % cookie)
+    hdr = []
+    for i in range(size):
+        k, cm1 = struct.unpack_from("<HH", buf, pos)
+        pos += 4
+        hdr.append((k, cm1 + 1))
+    if run_flags is None or size >= NO_OFFSET_THRESHOLD:
+        pos += 4 * size  # offsets (we read sequentially)
+    out = []
+    for i, (k, card) in enumerate(hdr):
+        is_run = run_flags is not None and (run_flags[i // 8] >> (i % 8)) & 1
+        base = np.uint32(k) << np.uint32(16)
+        if is_run:
+            (nruns,) = struct.unpack_from("<H", buf, pos)
+            pos += 2
+            r = np.frombuffer(buf, dtype="<u2", count=2 * nruns, offset=pos).astype(np.uint32)
+            pos += 4 * nruns
+            vals = np.concatenate([np.arange(s, s + l + 1, dtype=np.uint32) for s, l in zip(r[0::2], r[1::2])])
+        elif card <= 4096:
+            vals = np.frombuffer(buf, dtype="<u2", count=card, offset=pos).astype(np.uint32)
+            pos += 2 * card
+        else:
+            words = np.frombuffer(buf, dtype="<u8", count=1024, offset=pos)
+            pos += 8192
+            bits = np.unpackbits(words.view(np.uint8), bitorder="little")
+            vals = np.nonzero(bits)[0].astype(np.uint32)
+        out.append(vals + base)
+    return np.concatenate(out) if out else np.zeros(0, dtype=np.uint32)
+
+
+# ----------------------------------------------------------------------------- dictionary
+
+class Dictionary:
+    """Immutable sorted dictionary (BaseImmutableDictionary + typed subclasses)."""
+
+    def __init__(self, data_type: str, values, entry_bytes: int = 0):
+        self.data_type = data_type
+        if data_type in _NP_NATIVE:
+            self.values = np.asarray(values, dtype=_NP_NATIVE[data_type])
+            self.entry_bytes = np.dtype(_NP_BE[data_type]).itemsize
+        else:
+            self.values = list(values)
+            self.entry_bytes = entry_bytes
+        self._list = None
+
+    def __len__(self):
+        return len(self.values)
+
+    length = __len__
+
+    def get(self, dict_id: int):
+        return self.values[dict_id]
+
+    def _coerce(self, value):
+        t = self.data_type
+        if t == "INT":
+            return int(value)
+        if t == "LONG":
+            return int(value)
+        if t == "FLOAT":
+            return float(np.float32(float(value)))
+        if t == "DOUBLE":
+            return float(value)
+        return str(value)
+
+    def insertion_index_of(self, value) -> int:
+        """BaseImmutableDictionary.binarySearch: index if found else -(insertion point) - 1."""
+        v = self._coerce(value)
+        if self.data_type in _NP_NATIVE:
+            i = int(np.searchsorted(self.values, v, side="left"))
+            if i < len(self.values) and self.values[i] == v:
+                return i
+            return -(i + 1)
+        if self._list is None:
+            self._list = list(self.values)
+        i = bisect.bisect_left(self._list, v)
+        if i < len(self._list) and self._list[i] == v:
+            return i
+        return -(i + 1)
+
+    def index_of(self, value) -> int:
+        """Dictionary.indexOf: dictId or NULL_VALUE_INDEX (-1)."""
+        try:
+            i = self.insertion_index_of(value)
+        except (ValueError, OverflowError):
+            return -1
+        return i if i >= 0 else -1
+
+    def to_bytes(self) -> bytes:
+        if self.data_type in _NP_BE:
+            return self.values.astype(_NP_BE[self.data_type]).tobytes()
+        out = bytearray()
+        for s in self.values:
+            b = s.encode("utf-8") if isinstance(s, str) else bytes(s)
+            out += b + b"\0" * (self.entry_bytes - len(b))
+        return bytes(out)
+
+    @staticmethod
+    def from_bytes(data_type: str, buf: bytes, cardinality: int, entry_bytes: int = 0,
+                   padding: bytes = b"\0") -> "Dictionary":
+        if data_type in _NP_BE:
+            vals = np.frombuffer(buf, dtype=_NP_BE[data_type], count=cardinality).astype(_NP_NATIVE[data_type])
+            return Dictionary(data_type, vals)
+        vals = []
+        for i in range(cardinality):
+            raw = buf[i * entry_bytes:(i + 1) * entry_bytes]
+            # StringDictionary strips the padding character from the right
+            vals.append(raw.rstrip(padding).decode("utf-8"))
+        return Dictionary(data_type, vals, entry_bytes)
+
+
+def build_dictionary(data_type: str, values) -> (Dictionary, np.ndarray):
+    """Sorted-unique dictionary + dictIds (SegmentDictionaryCreator + SegmentIndexCreationDriverImpl)."""
+    if data_type in _NP_NATIVE:
+        arr = np.asarray(values, dtype=_NP_NATIVE[data_type])
+        uniq, inv = np.unique(arr, return_inverse=True)
+        return Dictionary(data_type, uniq), inv.astype(np.int32)
+    arr = np.asarray(values, dtype=object).astype(str)
+    uniq, inv = np.unique(arr, return_inverse=True)
+    uniq = [str(u) for u in uniq]
+    eb = max((len(u.encode("utf-8")) for u in uniq), default=0)
+    return Dictionary(data_type, uniq, eb), inv.astype(np.int32)
+
+
+# ----------------------------------------------------------------------------- columns / segments
+
+@dataclass
+class Column:
+    name: str
+    data_type: str
+    single_value: bool
+    dictionary: Dictionary
+    num_docs: int
+    bits_per_element: int
+    is_sorted: bool
+    num_values: int                      # totalNumberOfEntries
+    max_num_multi_values: int = 0
+    fwd: bytes = b""                     # forward index bytes (sorted pairs / sv / mv layout)
+    inverted: Optional[bytes] = None     # bitmap inverted index bytes
+    field_type: str = "DIMENSION"
+    # decoded dictIds (host convenience; SV: int32[num_docs], MV: list of arrays)
+    dict_ids: Optional[np.ndarray] = None
+    mv_offsets: Optional[np.ndarray] = None  # MV: int64[num_docs+1]
+
+    @property
+    def cardinality(self) -> int:
+        return len(self.dictionary)
+
+    @property
+    def fwd_kind(self) -> str:
+        if not self.single_value:
+            return "mv"
+        return "sorted" if self.is_sorted else "sv"
+
+
+def sorted_index_bytes(dict_ids: np.ndarray, card: int) -> bytes:
+    """SingleValueSortedForwardIndexCreator: per dictId (start, end) inclusive doc ids, BE int32."""
+    d = np.asarray(dict_ids, dtype=np.int64)
+    starts = np.searchsorted(d, np.arange(card), side="left")
+    ends = np.searchsorted(d, np.arange(card), side="right") - 1
+    pairs = np.stack([starts, ends], axis=1).astype(">i4")
+    return pairs.tobytes()
+
+
+def mv_docs_per_chunk(num_docs: int, num_values: int) -> int:
+    """FixedBitMVForwardIndexReader.java:61 -- ceil((float) 2048 / (numValues / numDocs)) (int division inside)."""
+    avg = num_values // num_docs
+    return int(np.ceil(np.float32(PREFERRED_NUM_VALUES_PER_CHUNK) / np.float32(avg)))
+
+
+def mv_forward_bytes(lengths: np.ndarray, flat_dict_ids: np.ndarray, b: int) -> bytes:
+    num_docs = lengths.size
+    num_values = int(lengths.sum())
+    dpc = mv_docs_per_chunk(num_docs, num_values)
+    num_chunks = (num_docs + dpc - 1) // dpc
+    starts = np.concatenate([[0], np.cumsum(lengths)[:-1]]).astype(np.int64)
+    chunk_offsets = starts[::dpc][:num_chunks].astype(">i4").tobytes()
+    bitmap = pack_bitmap(starts, num_values)
+    raw = pack_bits(flat_dict_ids, b)
+    return chunk_offsets + bitmap + raw
+
+
+class ImmutableSegment:
+    """An in-memory immutable segment: per column the reference's index bytes + metadata."""
+
+    def __init__(self, name: str, num_docs: int, columns: Dict[str, Column]):
+        self.name = name
+        self.num_docs = num_docs
+        self.columns = columns
+
+    def column(self, name: str) -> Column:
+        return self.columns[name]
+
+    # -- creation (SegmentIndexCreationDriverImpl / SegmentColumnarIndexCreator semantics)
+    @staticmethod
+    def create(name: str, data: Dict[str, Sequence], schema: Dict[str, str],
+               inverted: Sequence[str] = (), field_types: Optional[Dict[str, str]] = None,
+               roaring_run_optimize: bool = True) -> "ImmutableSegment":
+        """schema: column -> data type.  MV columns are given as a list of sequences."""
+        cols = {}
+        num_docs = None
+        for cname, dtype in schema.items():
+            vals = data[cname]
+            sv = not (len(vals) > 0 and isinstance(vals[0], (list, tuple, np.ndarray)))
+            if sv:
+                dictionary, ids = build_dictionary(dtype, vals)
+                n = ids.size
+                card = len(dictionary)
+                b = num_bits_per_value(card - 1)
+                is_sorted = bool(np.all(np.diff(ids) >= 0)) if n > 1 else True
+                col = Column(cname, dtype, True, dictionary, n, b, is_sorted, n, 0,
+                             field_type=(field_types or {}).get(cname, "DIMENSION"), dict_ids=ids)
+                if is_sorted:
+                    col.fwd = sorted_index_bytes(ids, card)
+                else:
+                    col.fwd = pack_bits(ids, b)
+                    if cname in inverted:
+                        col.inverted = inverted_index_bytes_sv(ids, card, roaring_run_optimize)
+            else:
+                lengths = np.array([len(x) for x in vals], dtype=np.int64)
+                flat = np.concatenate([np.asarray(x) for x in vals]) if len(vals) else np.zeros(0)
+                dictionary, ids = build_dictionary(dtype, flat)
+                n = lengths.size
+                card = len(dictionary)
+                b = num_bits_per_value(card - 1)
+                offsets = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
+                col = Column(cname, dtype, False, dictionary, n, b, False, int(lengths.sum()),
+                             int(lengths.max()) if n else 0, dict_ids=ids, mv_offsets=offsets,
+                             field_type=(field_types or {}).get(cname, "DIMENSION"))
+                col.fwd = mv_forward_bytes(lengths, ids, b)
+                if cname in inverted:
+                    col.inverted = inverted_index_bytes_mv(ids, offsets, card, roaring_run_optimize)
+            if num_docs is None:
+                num_docs = n
+            assert n == num_docs, "ragged columns"
+            cols[cname] = col
+        return ImmutableSegment(name, num_docs or 0, cols)
+
+    # -- V1 directory (V1Constants file names + metadata.properties)
+    def write_v1(self, path: str) -> None:
+        os.makedirs(path, exist_ok=True)
+        props = [f"segment.name = {self.name}", f"segment.total.docs = {self.num_docs}",
+                 "segment.padding.character = \\\\u0000"]
+        for c in self.columns.values():
+            with open(os.path.join(path, c.name + ".dict"), "wb") as f:
+                f.write(c.dictionary.to_bytes())
+            ext = {"sv": ".sv.unsorted.fwd", "sorted": ".sv.sorted.fwd", "mv": ".mv.fwd"}[c.fwd_kind]
+            with open(os.path.join(path, c.name + ext), "wb") as f:
+                f.write(c.fwd)
+            if c.inverted is not None:
+                with open(os.path.join(path, c.name + ".bitmap.inv"), "wb") as f:
+                    f.write(c.inverted)
+            p = f"column.{c.name}."
+            props += [p + f"cardinality = {c.cardinality}", p + f"totalDocs = {c.num_docs}",
+                      p + f"dataType = {c.data_type}", p + f"bitsPerElement = {c.bits_per_element}",
+                      p + f"lengthOfEachEntry = {c.dictionary.entry_bytes if c.data_type == 'STRING' else 0}",
+                      p + f"columnType = {c.field_type}", p + f"isSorted = {str(c.is_sorted).lower()}",
+                      p + "hasDictionary = true", p + f"hasInvertedIndex = {str(c.inverted is not None).lower()}",
+                      p + f"isSingleValues = {str(c.single_value).lower()}",
+                      p + f"maxNumberOfMultiValues = {c.max_num_multi_values}",
+                      p + f"totalNumberOfEntries = {c.num_values}"]
+        with open(os.path.join(path, "metadata.properties"), "w") as f:
+            f.write("\n".join(props) + "\n")
+
+    @staticmethod
+    def load_v1(path: str) -> "ImmutableSegment":
+        """ImmutableSegmentLoader for the V1 layout (metadata.properties + per-index files)."""
+        props = {}
+        with open(os.path.join(path, "metadata.properties")) as f:
+            for line in f:
+                if "=" in line:
+                    k, v = line.split("=", 1)
+                    props[k.strip()] = v.strip()
+        num_docs = int(props["segment.total.docs"])
+        pad = props.get("segment.padding.character", "\\u0000")
+        padding = b"\0" if "0000" in pad else pad.encode()[-1:]
+        names = sorted({k.split(".")[1] for k in props if k.startswith("column.")})
+        cols = {}
+        for cname in names:
+            p = lambda k: props[f"column.{cname}.{k}"]
+            dtype = p("dataType")
+            card = int(p("cardinality"))
+            b = int(p("bitsPerElement"))
+            eb = int(p("lengthOfEachEntry")) if dtype == "STRING" else 0
+            with open(os.path.join(path, cname + ".dict"), "rb") as f:
+                dictionary = Dictionary.from_bytes(dtype, f.read(), card, eb, padding)
+            sv = p("isSingleValues") == "true"
+            is_sorted = p("isSorted") == "true"
+            nv = int(props.get(f"column.{cname}.totalNumberOfEntries", num_docs))
+            ext = (".sv.sorted.fwd" if is_sorted else ".sv.unsorted.fwd") if sv else ".mv.fwd"
+            with open(os.path.join(path, cname + ext), "rb") as f:
+                fwd = f.read()
+            inv = None
+            ip = os.path.join(path, cname + ".bitmap.inv")
+            if os.path.exists(ip):
+                with open(ip, "rb") as f:
+                    inv = f.read()
+            col = Column(cname, dtype, sv, dictionary, num_docs, b, is_sorted, nv,
+                         int(props.get(f"column.{cname}.maxNumberOfMultiValues", 0)), fwd, inv,
+                         props.get(f"column.{cname}.columnType", "DIMENSION"))
+            if sv and not is_sorted:
+                col.dict_ids = unpack_bits(fwd, num_docs, b).astype(np.int32)
+            elif sv:
+                pairs = np.frombuffer(fwd, dtype=">i4").reshape(-1, 2)
+                ids = np.zeros(num_docs, dtype=np.int32)
+                for d, (s, e) in enumerate(pairs):
+                    ids[s:e + 1] = d
+                col.dict_ids = ids
+            cols[cname] = col
+        return ImmutableSegment(props.get("segment.name", os.path.basename(path)), num_docs, cols)
+
+
+def inverted_index_bytes_sv(dict_ids: np.ndarray, card: int, run_optimize=True) -> bytes:
+    order = np.argsort(dict_ids, kind="stable")
+    sd = dict_ids[order]
+    bounds = np.searchsorted(sd, np.arange(card + 1), side="left")
+    bitmaps = [roaring_serialize(order[bounds[d]:bounds[d + 1]], run_optimize) for d in range(card)]
+    return _inverted_bytes(bitmaps)
+
+
+def inverted_index_bytes_mv(flat_ids: np.ndarray, offsets: np.ndarray, card: int, run_optimize=True) -> bytes:
+    docs = np.repeat(np.arange(offsets.size - 1), np.diff(offsets))
+    order = np.lexsort((docs, flat_ids))
+    sd = flat_ids[order]
+    sdocs = docs[order]
+    bounds = np.searchsorted(sd, np.arange(card + 1), side="left")
+    bitmaps = [roaring_serialize(np.unique(sdocs[bounds[d]:bounds[d + 1]]), run_optimize) for d in range(card)]
+    return _inverted_bytes(bitmaps)
+
+
+def _inverted_bytes(bitmaps: List[bytes]) -> bytes:
+    n = len(bitmaps)
+    off = (n + 1) * 4
+    offs = []
+    for bm in bitmaps:
+        offs.append(off)
+        off += len(bm)
+    offs.append(off)
+    return np.asarray(offs, dtype=">u4").tobytes() + b"".join(bitmaps)
+
+
+def inverted_docs(col: Column, dict_id: int) -> np.ndarray:
+    """BitmapInvertedIndexReader.getDocIds(dictId) -> sorted doc ids."""
+    buf = col.inverted
+    n = col.cardinality
+    offs = np.frombuffer(buf, dtype=">u4", count=n + 1).astype(np.int64)
+    first = offs[0]
+    base = (n + 1) * 4
+    s = base + offs[dict_id] - first
+    e = base + offs[dict_id + 1] - first
+    return roaring_deserialize(buf[s:e])
