@@ -257,6 +257,12 @@ int pg_execute_partial(const pg_plan *plan, pg_partials **out);
  * the partials were produced from (only its aggs / keys are read). */
 int pg_partials_finalize(pg_partials *p, const pg_plan *plan, pg_result **out);
 int pg_partials_free(pg_partials *p);
+/* Copy the partial-state arrays out to (PG_COPY_OUT) or back in from (PG_COPY_IN) caller-owned DEVICE buffers of
+ * the same sizes (e.g. torch tensors the ranks all-reduce over RCCL: SUM for i64 / f64, MIN for mn, MAX for mx and
+ * flags).  A NULL pointer skips that array.  `stream` NULL = the library's per-thread stream; synchronous. */
+#define PG_COPY_OUT 0
+#define PG_COPY_IN 1
+int pg_partials_copy(pg_partials *p, int dir, void *i64, void *f64, void *mn, void *mx, void *flags, void *stream);
 
 /* ---------------------------------------------------------------- measurement hooks */
 

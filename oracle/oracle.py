@@ -111,8 +111,8 @@ class OracleEngine:
     def columns(self, seg, table):
         k = (id(seg), id(table))
         if k not in self._cols:
-            self._cols[k] = _SegmentColumns(seg, table)
-        return self._cols[k]
+            self._cols[k] = (seg, table, _SegmentColumns(seg, table))  # refs keep the ids valid
+        return self._cols[k][2]
 
     def run_segment(self, plan: CPlan, si: int, seg: ImmutableSegment):
         cols = self.columns(seg, plan.table)

@@ -95,7 +95,8 @@ class pg_timing(C.Structure):
 # every symbol declared in include/pinot_gpu.h (checked by tests/test_abi.py)
 EXPORTED = ["pg_init", "pg_last_error", "pg_resident_bytes", "pg_cancel", "pg_abi_version", "pg_column_upload",
             "pg_segment_release", "pg_execute", "pg_result_free", "pg_execute_partial", "pg_partials_finalize",
-            "pg_partials_free", "pg_last_timing"]
+            "pg_partials_free", "pg_partials_copy", "pg_last_timing"]
+PG_COPY_OUT, PG_COPY_IN = 0, 1
 
 
 def declare(lib):
@@ -115,6 +116,8 @@ def declare(lib):
         "pg_partials_finalize": ([P(pg_partials), P(pg_plan), P(P(pg_result))], C.c_int),
         "pg_partials_free": ([P(pg_partials)], C.c_int),
         "pg_last_timing": ([P(pg_timing)], C.c_int),
+        "pg_partials_copy": ([P(pg_partials), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                              C.c_void_p], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(lib, name)

@@ -940,6 +940,12 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   stats.num_total_docs = total_docs;
   stats.num_segments_processed = S;
   stats.num_entries_scanned_in_filter = entries_in_filter;
+  if (S) {
+    std::vector<uint64_t> sm(S);
+    HIP_CHECK(hipMemcpy(sm.data(), P.seg_matched.p, 8ull * S, hipMemcpyDeviceToHost));
+    for (uint64_t v : sm) { stats.num_docs_scanned += v; stats.num_segments_matched += v > 0; }
+  }
+  stats.num_entries_scanned_post_filter = stats.num_docs_scanned * P.projected_cols;
   return PG_OK;
 }
 
@@ -962,13 +968,11 @@ int finalize(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   std::vector<int64_t> hi64(G * pp->n_i64), hmn(G * pp->n_min), hmx(G * pp->n_max);
   std::vector<double> hf64(G * pp->n_f64);
   std::vector<uint8_t> hflags(G * pp->flag_bytes_per_slot);
-  std::vector<uint64_t> sm(P.num_segments);
   HIP_CHECK(hipMemcpyAsync(hi64.data(), pp->i64, hi64.size() * 8, hipMemcpyDeviceToHost, s));
   if (!hf64.empty()) HIP_CHECK(hipMemcpyAsync(hf64.data(), pp->f64, hf64.size() * 8, hipMemcpyDeviceToHost, s));
   if (!hmn.empty()) HIP_CHECK(hipMemcpyAsync(hmn.data(), pp->mn, hmn.size() * 8, hipMemcpyDeviceToHost, s));
   if (!hmx.empty()) HIP_CHECK(hipMemcpyAsync(hmx.data(), pp->mx, hmx.size() * 8, hipMemcpyDeviceToHost, s));
   if (!hflags.empty()) HIP_CHECK(hipMemcpyAsync(hflags.data(), pp->flags, hflags.size(), hipMemcpyDeviceToHost, s));
-  if (!sm.empty()) HIP_CHECK(hipMemcpyAsync(sm.data(), P.seg_matched.p, sm.size() * 8, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipEventRecord(e1, s));
   HIP_CHECK(hipStreamSynchronize(s));
   float fm = 0;
@@ -978,12 +982,7 @@ int finalize(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   t_timing.finalize_ms = fm;
 
   pg_result* r = (pg_result*)calloc(1, sizeof(pg_result));
-  r->stats = pp->stats;
-  uint64_t matched = 0, segs_matched = 0;
-  for (uint64_t v : sm) { matched += v; segs_matched += v > 0; }
-  // pp->stats may have been merged by the caller across ranks; only fill what is still zero
-  if (!r->stats.num_docs_scanned) r->stats.num_docs_scanned = matched;
-  if (!r->stats.num_segments_matched) r->stats.num_segments_matched = segs_matched;
+  r->stats = pp->stats;  // local, or merged across ranks by the caller before finalize
   r->stats.num_entries_scanned_post_filter = r->stats.num_docs_scanned * P.projected_cols;
   r->num_keys = K;
   r->num_aggs = A;
@@ -1156,6 +1155,25 @@ int pg_partials_free(pg_partials* p) {
     delete impl;
   }
   free(p);
+  return PG_OK;
+}
+
+int pg_partials_copy(pg_partials* p, int dir, void* i64, void* f64, void* mn, void* mx, void* flags, void* stream) {
+  int rc = ensure_device();
+  if (rc) return rc;
+  if (!p || (dir != PG_COPY_OUT && dir != PG_COPY_IN)) return fail(PG_E_INVALID, "bad partials / direction");
+  hipStream_t s = stream ? (hipStream_t)stream : thread_stream();
+  void* mine[5] = {p->i64, p->f64, p->mn, p->mx, p->flags};
+  void* theirs[5] = {i64, f64, mn, mx, flags};
+  const uint64_t bytes[5] = {p->num_slots * 8ull * p->n_i64, p->num_slots * 8ull * p->n_f64,
+                             p->num_slots * 8ull * p->n_min, p->num_slots * 8ull * p->n_max,
+                             p->num_slots * p->flag_bytes_per_slot};
+  for (int i = 0; i < 5; i++) {
+    if (!theirs[i] || !bytes[i]) continue;
+    if (dir == PG_COPY_OUT) HIP_CHECK(hipMemcpyAsync(theirs[i], mine[i], bytes[i], hipMemcpyDeviceToDevice, s));
+    else HIP_CHECK(hipMemcpyAsync(mine[i], theirs[i], bytes[i], hipMemcpyDeviceToDevice, s));
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
   return PG_OK;
 }
 

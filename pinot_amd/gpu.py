@@ -77,14 +77,14 @@ class GpuEngine:
         self.lib = load_library()
         check(self.lib.pg_init(device))
         self.device = device
-        self._seg_keys: Dict[int, int] = {}      # id(segment) -> seg_key
+        self._seg_keys: Dict[int, tuple] = {}    # id(segment) -> (segment, seg_key); holds the segment alive
         self._keymaps_uploaded = set()
 
     # ---- residency (IndexingOverrides reader-provider hook)
     def upload_segment(self, seg: ImmutableSegment, table: Table) -> int:
-        key = self._seg_keys.get(id(seg))
-        if key is not None:
-            return key
+        hit = self._seg_keys.get(id(seg))
+        if hit is not None:
+            return hit[1]
         key = next(_seg_counter)
         for name, col in seg.columns.items():
             cid = table.column_ids[name]
@@ -98,7 +98,26 @@ class GpuEngine:
                 di = abi.pg_col_desc.from_buffer_copy(d)
                 di.kind = abi.PG_IDX_INV_BITMAP
                 self._upload(key, cid, di, col.inverted)
-        self._seg_keys[id(seg)] = key
+        self._seg_keys[id(seg)] = (seg, key)
+        return key
+
+    def register_device_segment(self, seg: ImmutableSegment, table: Table, dev_cols) -> int:
+        """Make a segment resident from DEVICE buffers in the reference's byte layout (PG_SRC_DEVICE): used for
+        synthetic segments generated on the GPU (pinot_amd.synth.DeviceColumn); `seg` carries the host metadata
+        and dictionaries, as the reference keeps them on heap."""
+        key = next(_seg_counter)
+        for dc in dev_cols:
+            col = seg.columns[dc.spec.name]
+            cid = table.column_ids[dc.spec.name]
+            d = fwd_desc(col)
+            d.flags = abi.PG_SRC_DEVICE
+            dd = abi.pg_col_desc.from_buffer_copy(d)
+            dd.kind = abi.PG_IDX_DICT
+            check(self.lib.pg_column_upload(key, cid, C.byref(dd), C.c_void_p(dc.dict_be.data_ptr()),
+                                            dc.dict_be.numel()))
+            check(self.lib.pg_column_upload(key, cid, C.byref(d), C.c_void_p(dc.fwd_be.data_ptr()),
+                                            dc.fwd_be.numel()))
+        self._seg_keys[id(seg)] = (seg, key)
         return key
 
     def _upload(self, key, cid, desc, data: bytes):
@@ -125,9 +144,10 @@ class GpuEngine:
                 self._keymaps_uploaded.add((key, cid))
 
     def release(self, seg: ImmutableSegment):
-        key = self._seg_keys.pop(id(seg), None)
-        if key is not None:
-            check(self.lib.pg_segment_release(key))
+        hit = self._seg_keys.pop(id(seg), None)
+        if hit is not None:
+            check(self.lib.pg_segment_release(hit[1]))
+            self._keymaps_uploaded = {k for k in self._keymaps_uploaded if k[0] != hit[1]}
 
     # ---- execution
     def make_plan(self, table: Table, query: QueryContext, segments: Optional[Sequence[ImmutableSegment]] = None,
@@ -141,6 +161,23 @@ class GpuEngine:
     def run_plan(self, plan: CPlan) -> IntermediateResult:
         res = C.POINTER(abi.pg_result)()
         check(self.lib.pg_execute(C.byref(plan.plan), C.byref(res)))
+        try:
+            return self.decode(plan, res.contents)
+        finally:
+            self.lib.pg_result_free(res)
+
+    def run_partial(self, plan: CPlan):
+        """pg_execute_partial: this device's dense partial state (for the cross-GPU merge, pinot_amd.combine)."""
+        p = C.POINTER(abi.pg_partials)()
+        check(self.lib.pg_execute_partial(C.byref(plan.plan), C.byref(p)))
+        return p
+
+    def finalize_partial(self, plan: CPlan, p) -> IntermediateResult:
+        res = C.POINTER(abi.pg_result)()
+        try:
+            check(self.lib.pg_partials_finalize(p, C.byref(plan.plan), C.byref(res)))
+        finally:
+            self.lib.pg_partials_free(p)
         try:
             return self.decode(plan, res.contents)
         finally:

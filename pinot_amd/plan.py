@@ -46,6 +46,20 @@ class LoweredLeaf:
     ids: Optional[np.ndarray] = None   # sorted unique int32
 
 
+def dict_id_set(d, values) -> np.ndarray:
+    """PredicateUtils.getDictIdSet: sorted unique dictIds of the literals present in the dictionary."""
+    if d.data_type in ("INT", "LONG", "FLOAT", "DOUBLE"):
+        try:
+            lit = np.asarray([d._coerce(v) for v in values], dtype=d.values.dtype)
+        except (ValueError, OverflowError):
+            return np.asarray(sorted({i for i in (d.index_of(v) for v in values) if i >= 0}), dtype=np.int32)
+        pos = np.searchsorted(d.values, lit, side="left")
+        ok = pos < len(d.values)
+        ok[ok] = d.values[pos[ok]] == lit[ok]
+        return np.unique(pos[ok]).astype(np.int32)
+    return np.asarray(sorted({i for i in (d.index_of(v) for v in values) if i >= 0}), dtype=np.int32)
+
+
 def lower_predicate(pred: Predicate, col: Column, col_id: int) -> LoweredLeaf:
     """Dictionary-based predicate evaluator + leaf operator choice for one segment's column."""
     d = col.dictionary
@@ -71,8 +85,8 @@ def lower_predicate(pred: Predicate, col: Column, col_id: int) -> LoweredLeaf:
             else:
                 always_true = True
     elif t in ("IN", "NOT_IN"):
-        s = sorted({i for i in (d.index_of(v) for v in pred.values) if i >= 0})   # PredicateUtils.getDictIdSet
-        ids = np.asarray(s, dtype=np.int32)
+        ids = dict_id_set(d, pred.values)   # PredicateUtils.getDictIdSet
+        s = ids
         if t == "IN":
             always_false = len(s) == 0
             always_true = len(s) == card

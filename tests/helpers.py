@@ -1,0 +1,78 @@
+"""Helpers shared by the parity tests: turn expected.json cases into queries and compare results."""
+import math
+
+from pinot_amd.plan import final_value, reduce_to_rows
+from pinot_amd.query import parse
+
+
+def with_filter(query: str, filt: str) -> str:
+    """Insert the shared FILTER where the case says `FILTER` (BaseSingleValueQueriesTest.java:73-77)."""
+    return query.replace(" FILTER", filt) if " FILTER" in query else query
+
+
+def inner_query(case, filt):
+    q = case.get("query") or "SELECT COUNT(*), SUM(column1), MAX(column3), MIN(column6), AVG(column7) FROM testTable"
+    if case.get("filtered"):
+        q += filt
+    if case.get("group_by"):
+        q += " GROUP BY " + ", ".join(case["group_by"])
+    return q
+
+
+def check_inner_values(res, case):
+    """QueriesTestUtils.testInnerSegmentAggregation(GroupBy)Result: longValue() of each result, AvgPair sum/count."""
+    key = tuple(case.get("key", ()))
+    assert key in res.rows, f"group key {key} missing"
+    row = res.rows[key]
+    exp = case["values"]
+    for a, (ag, v, e) in enumerate(zip(res.aggregations, row, exp)):
+        if ag.function == "AVG":
+            assert int(v[0]) == e[0] and int(v[1]) == e[1], (a, v, e)
+        else:
+            assert int(v) == e, (a, ag, v, e)
+    n_scanned, post, total = case["stats"]
+    assert res.stats.num_docs_scanned == n_scanned
+    assert res.stats.num_entries_scanned_post_filter == post
+    assert res.stats.num_total_docs == total
+
+
+def check_rows(got, exp, delta=None):
+    assert len(got) == len(exp), (got, exp)
+    for gr, er in zip(got, exp):
+        assert len(gr) == len(er)
+        for g, e in zip(gr, er):
+            if isinstance(e, str):
+                assert g == e, (gr, er)
+            elif delta is not None:
+                assert abs(float(g) - float(e)) <= delta * max(1.0, abs(float(e))), (gr, er)
+            else:
+                assert float(g) == float(e), (gr, er)
+
+
+def run_rows(engine, table, sql):
+    q = parse(sql)
+    res = engine.execute(table, q)
+    return q, res, reduce_to_rows(q, res)[1]
+
+
+def assert_same_result(a, b, rel=1e-9):
+    """Device result vs oracle result, both IntermediateResult.  Bit-exact for counts / integer sums / min / max /
+    distinct counts and keys; `rel` relative tolerance for double SUM / AVG sums (north_star: 1e-9)."""
+    assert set(a.rows) == set(b.rows), (sorted(a.rows)[:5], sorted(b.rows)[:5])
+    for k in a.rows:
+        for ag, x, y in zip(a.aggregations, a.rows[k], b.rows[k]):
+            if ag.function == "DISTINCTCOUNT":
+                x = final_value(ag, x)
+                y = final_value(ag, y)
+                assert x == y, (k, ag, x, y)
+            elif ag.function == "AVG":
+                assert x[1] == y[1], (k, ag, x, y)
+                assert math.isclose(x[0], y[0], rel_tol=rel, abs_tol=0), (k, ag, x, y)
+            elif ag.function in ("SUM",):
+                assert math.isclose(x, y, rel_tol=rel, abs_tol=0), (k, ag, x, y)
+            else:
+                assert x == y, (k, ag, x, y)
+    sa, sb = a.stats, b.stats
+    assert sa.num_docs_scanned == sb.num_docs_scanned
+    assert sa.num_entries_scanned_post_filter == sb.num_entries_scanned_post_filter
+    assert sa.num_total_docs == sb.num_total_docs

@@ -1,0 +1,206 @@
+"""Parity of the HIP path (libpinot_gpu.so through the C ABI) with the CPU oracle and the reference's known answers.
+
+Bar (north_star): bit-exact for COUNT, MIN, MAX, integer SUM, DISTINCTCOUNT and group keys; 1e-9 relative for
+double SUM / AVG sums.  Every test here runs on an MI355X (`-m gpu`)."""
+import numpy as np
+import pytest
+
+from helpers import assert_same_result, check_inner_values, check_rows, inner_query, run_rows, with_filter
+from pinot_amd.plan import Table, UnsupportedQuery
+from pinot_amd.query import parse
+from pinot_amd.segment import ImmutableSegment
+
+pytestmark = pytest.mark.gpu
+
+
+# ------------------------------------------------------------------ reference known answers (test_data-sv.avro)
+
+@pytest.mark.parametrize("i", range(2))
+def test_golden_inner_aggregation(i, expected, gpu_engine, sv_table_inner):
+    case = expected["inner_aggregation"][i]
+    res = gpu_engine.execute(sv_table_inner, inner_query(case, expected["filter"]))
+    check_inner_values(res, case)
+
+
+@pytest.mark.parametrize("i", range(4))
+def test_golden_inner_group_by(i, expected, gpu_engine, sv_table_inner):
+    case = expected["inner_group_by"][i]
+    res = gpu_engine.execute(sv_table_inner, inner_query(case, expected["filter"]))
+    check_inner_values(res, case)
+
+
+@pytest.mark.parametrize("i", range(24))
+def test_golden_inter_segment(i, expected, gpu_engine, sv_table_inter):
+    cases = expected["inter"]
+    if i >= len(cases):
+        pytest.skip("no case")
+    case = cases[i]
+    q, res, rows = run_rows(gpu_engine, sv_table_inter, with_filter(case["query"], expected["filter"]))
+    check_rows(rows, case["rows"], case.get("delta"))
+    n_scanned, post, total = case["stats"]
+    assert res.stats.num_docs_scanned == n_scanned
+    assert res.stats.num_total_docs == total
+
+
+# ------------------------------------------------------------------ device vs oracle, same inputs
+
+SV_QUERIES = [
+    "SELECT COUNT(*) FROM t",
+    "SELECT COUNT(*), SUM(column1), MIN(column3), MAX(column6), AVG(column7) FROM t",
+    "SELECT SUM(column1), SUM(column3) FROM t WHERE column6 < 500000000",
+    "SELECT COUNT(*) FROM t WHERE column11 IN ('P', 'o') AND column17 <> 5",
+    "SELECT COUNT(*), MAX(column18) FROM t WHERE NOT column11 = 'P'",
+    "SELECT COUNT(*) FROM t WHERE column7 IN (1, 2, 3, 4, 5, 6, 7, 8, 9, 10) OR column9 > 1000000000",
+    "SELECT MIN(column1), MAX(column1) FROM t WHERE daysSinceEpoch = 126164076",
+    "SELECT COUNT(*) FROM t WHERE daysSinceEpoch <> 126164076",
+    "SELECT COUNT(*) FROM t WHERE column1 > 3000000000",
+    "SELECT COUNT(*) FROM t WHERE column5 = 'nope'",
+    "SELECT DISTINCTCOUNT(column1), DISTINCTCOUNT(column11), DISTINCTCOUNT(column12) FROM t WHERE column3 > 1000000000",
+    "SELECT SUM(column1 * column3), SUM(column7 + column17), SUM(column7 - column18) FROM t",
+    "SELECT MIN(column6 * column7), MAX(column17 - column18), AVG(column1 * column17) FROM t WHERE column6 > 10",
+    "SELECT column11, COUNT(*), SUM(column1), MIN(column3), MAX(column3), AVG(column9) FROM t GROUP BY column11",
+    "SELECT column11, column12, SUM(column1) FROM t GROUP BY column11, column12",
+    "SELECT column9, COUNT(*) FROM t GROUP BY column9",
+    "SELECT daysSinceEpoch, column17, SUM(column18) FROM t WHERE column11 NOT IN ('t', 'P') GROUP BY daysSinceEpoch, column17",
+    "SELECT column12, DISTINCTCOUNT(column11), DISTINCTCOUNT(column7) FROM t GROUP BY column12",
+    "SELECT column7, COUNT(*), SUM(column3) FROM t WHERE (column6 < 500000000 OR column11 NOT IN ('t', 'P')) AND "
+    "NOT (column17 IN (1, 2) AND column18 > 100) GROUP BY column7",
+]
+
+
+@pytest.mark.parametrize("sql", SV_QUERIES)
+def test_sv_queries_match_oracle(sql, gpu_engine, oracle_engine, sv_table_inter):
+    q = parse(sql)
+    g = gpu_engine.execute(sv_table_inter, q)
+    o = oracle_engine.execute(sv_table_inter, q)
+    assert_same_result(g, o)
+
+
+def test_unsupported_shape_is_reported_not_crashed(gpu_engine, sv_table_inner):
+    """GROUP BY whose per-segment key space can exceed numGroupsLimit -> PG_E_UNSUPPORTED (caller falls back)."""
+    with pytest.raises(UnsupportedQuery):
+        gpu_engine.execute(sv_table_inner, "SELECT COUNT(*) FROM t GROUP BY column1, column6, column9")
+
+
+# ------------------------------------------------------------------ synthetic segments (config 2 shape + edges)
+
+def _seg(name, data, schema, **kw):
+    return ImmutableSegment.create(name, data, schema, **kw)
+
+
+def test_config2_shape_small(gpu_engine, oracle_engine):
+    from pinot_amd import synth
+    segs = [synth.make_segment_np(synth.ADANALYTICS, s, 150_001) for s in range(3)]
+    t = Table("adAnalytics", segs)
+    q = parse(synth.adanalytics_query(5000))
+    assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q))
+
+
+def test_device_generated_segments_match_host_bytes(gpu_engine, oracle_engine):
+    """Segments generated on the GPU (bench path) give the same results as their host copies through the oracle."""
+    import torch
+    from pinot_amd import synth
+    from pinot_amd.segment import ImmutableSegment as IS
+    segs, host_segs = [], []
+    n = 200_000
+    t_cols = {}
+    for s in range(2):
+        dcs = synth.make_columns_torch(synth.ADANALYTICS, s, n, torch.device("cuda"))
+        cols = {dc.spec.name: dc.host_column() for dc in dcs}
+        seg = IS(f"d{s}", n, cols)
+        segs.append((seg, dcs))
+    table = Table("adAnalytics", [s for s, _ in segs])
+    for seg, dcs in segs:
+        gpu_engine.register_device_segment(seg, table, dcs)
+    q = parse(synth.adanalytics_query(20000))
+    g = gpu_engine.execute(table, q)
+    o = oracle_engine.execute(table, q)
+    assert_same_result(g, o)
+    assert g.stats.num_docs_scanned > 0
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 4095, 4096, 4097, 10001, 70000])
+def test_ragged_sizes(n, gpu_engine, oracle_engine):
+    rng = np.random.default_rng(n)
+    data = {"a": rng.integers(0, 3, n), "b": rng.integers(-1000, 1000, n), "c": rng.integers(0, 2 ** 21, n),
+            "d": rng.normal(size=n)}
+    seg = _seg("r", data, {"a": "INT", "b": "LONG", "c": "INT", "d": "DOUBLE"})
+    t = Table("t", [seg, seg])
+    for sql in ["SELECT COUNT(*), SUM(b), MIN(c), MAX(d), AVG(d) FROM t WHERE c > 1000",
+                "SELECT a, COUNT(*), SUM(d), SUM(b), MIN(b) FROM t WHERE b BETWEEN -10 AND 500 GROUP BY a",
+                "SELECT DISTINCTCOUNT(b) FROM t WHERE a <> 1"]:
+        q = parse(sql)
+        assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q))
+
+
+def test_empty_and_all_filtered(gpu_engine, oracle_engine):
+    rng = np.random.default_rng(1)
+    seg = _seg("e", {"a": rng.integers(0, 10, 5000), "b": rng.integers(0, 100, 5000)}, {"a": "INT", "b": "INT"})
+    t = Table("t", [seg])
+    for sql in ["SELECT COUNT(*), SUM(b), MIN(b), MAX(b) FROM t WHERE a > 100",
+                "SELECT a, SUM(b) FROM t WHERE a = 77 GROUP BY a",
+                "SELECT COUNT(*) FROM t WHERE a IN (11, 12) OR b = 1000"]:
+        q = parse(sql)
+        g, o = gpu_engine.execute(t, q), oracle_engine.execute(t, q)
+        assert_same_result(g, o)
+        assert g.stats.num_docs_scanned == 0
+
+
+def test_per_segment_dictionaries_merge_by_value(gpu_engine, oracle_engine):
+    """dictIds are segment-local: different value sets per segment still merge by VALUE (IndexedTable keys)."""
+    rng = np.random.default_rng(2)
+    segs = []
+    for s in range(4):
+        n = 30000 + s * 777
+        data = {"k": rng.integers(s * 5, s * 5 + 20, n), "name": np.array(["x%d" % i for i in range(s, s + 7)],
+                                                                           dtype=object)[rng.integers(0, 7, n)],
+                "v": rng.integers(0, 10 ** 6, n), "f": rng.uniform(-5, 5, n).astype(np.float32)}
+        segs.append(_seg(f"s{s}", data, {"k": "INT", "name": "STRING", "v": "LONG", "f": "FLOAT"}))
+    t = Table("t", segs)
+    for sql in ["SELECT k, name, COUNT(*), SUM(v), MAX(f) FROM t GROUP BY k, name",
+                "SELECT name, DISTINCTCOUNT(k), AVG(f), MIN(f) FROM t WHERE v < 500000 GROUP BY name",
+                "SELECT f, COUNT(*) FROM t WHERE k < 3 GROUP BY f"]:
+        q = parse(sql)
+        assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q))
+
+
+def test_sorted_and_inverted_and_mv(gpu_engine, oracle_engine):
+    """Config-5 shape in miniature: sorted column, inverted-index leaves (incl. exclusive), MV COUNTMV + MV filter."""
+    rng = np.random.default_rng(3)
+    n = 50000
+    data = {"sortedCol": np.sort(rng.integers(0, 1000, n)), "inv1": rng.integers(0, 10, n),
+            "inv2": rng.integers(0, 100, n), "inv3": rng.integers(0, 1000, n), "inv4": rng.integers(0, 10000, n),
+            "mvTags": [list(rng.integers(0, 1000, rng.integers(1, 8))) for _ in range(n)]}
+    seg = _seg("idx", data, {k: "INT" for k in data}, inverted=["inv1", "inv2", "inv3", "inv4", "mvTags"])
+    seg2 = _seg("scan", data, {k: "INT" for k in data})  # same data, scan-only leaves
+    for segs in ([seg], [seg2], [seg, seg2]):
+        t = Table("t", segs)
+        for sql in [
+            "SELECT COUNT(*), COUNTMV(mvTags) FROM t WHERE sortedCol BETWEEN 100 AND 600 AND (inv1 = 3 OR inv2 IN "
+            "(1, 5, 9, 50)) AND inv3 <> 7 AND inv4 IN (1, 2, 3, 100, 200, 300, 4000, 5000)",
+            "SELECT COUNT(*), COUNTMV(mvTags) FROM t WHERE mvTags IN (5, 6, 7) AND NOT sortedCol < 200",
+            "SELECT COUNT(*) FROM t WHERE mvTags NOT IN (1, 2, 3, 4, 5, 6, 7, 8, 9, 10)",
+            "SELECT inv1, COUNTMV(mvTags), SUM(inv4) FROM t WHERE sortedCol IN (5, 77, 800) OR inv2 > 90 GROUP BY inv1",
+            "SELECT COUNT(*) FROM t WHERE sortedCol NOT IN (5, 6, 7) AND inv1 NOT IN (0, 1)",
+        ]:
+            q = parse(sql)
+            assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q))
+
+
+def test_partials_roundtrip_single_rank(gpu_engine, oracle_engine, sv_table_inter):
+    """pg_execute_partial -> pg_partials_copy out/in -> pg_partials_finalize == pg_execute (1-rank merge)."""
+    import ctypes as C
+    import torch
+    from pinot_amd import abi
+    q = parse("SELECT column11, COUNT(*), SUM(column1), MIN(column3), MAX(column6), DISTINCTCOUNT(column7) FROM t "
+              "GROUP BY column11")
+    plan = gpu_engine.make_plan(sv_table_inter, q)
+    p = gpu_engine.run_partial(plan)
+    pc = p.contents
+    bufs = [torch.empty(max(pc.num_slots * k, 1) * sz, dtype=torch.uint8, device="cuda")
+            for k, sz in ((pc.n_i64, 8), (pc.n_f64, 8), (pc.n_min, 8), (pc.n_max, 8), (pc.flag_bytes_per_slot, 1))]
+    ptrs = [C.c_void_p(b.data_ptr()) for b in bufs]
+    assert gpu_engine.lib.pg_partials_copy(p, abi.PG_COPY_OUT, *ptrs, None) == 0
+    assert gpu_engine.lib.pg_partials_copy(p, abi.PG_COPY_IN, *ptrs, None) == 0
+    g = gpu_engine.finalize_partial(plan, p)
+    assert_same_result(g, oracle_engine.execute(sv_table_inter, q))
