@@ -3,8 +3,8 @@
 // HBM layout of a resident segment column (built once by pg_column_upload):
 //   * bit-packed forward index   : the reference's big-endian stream re-laid as native uint32 words
 //                                  (byte-swapped per 32-bit word), so bit p of the stream is bit
-//                                  31-(p&31) of word p>>5.  +4 zero words of tail padding so a 64-bit
-//                                  window load of the last value never leaves the allocation.
+//                                  31-(p&31) of word p>>5.  +4 zero words of tail padding so the 64-bit
+//                                  window read of the last value never leaves the allocation.
 //                                  Sorted columns get the same packed stream synthesised from their
 //                                  (start,end) pairs, so every column is readable per doc.
 //   * dictionary                 : native typed array (int32 / int64 / float / double).
@@ -12,8 +12,9 @@
 //                                  (selected once from the start-of-row bitmap).
 //   * inverted index             : roaring bytes kept as-is (compressed in HBM) + a container
 //                                  directory (per dictId CSR of {key, type, card, offset}).
-// Per query, a parameter arena (one H2D copy) holds DevLeaf / DevCol tables indexed
-// [segment][leaf] and [segment][agg|key], LUTs for IN / NOT_IN leaves and sorted-index doc ranges.
+// Per query, ONE parameter arena (one pinned H2D copy) holds the per-segment tables the scan kernel
+// reads: SegDesc[seg], LeafDesc[seg][leaf], ColDesc[seg][agg*2 | key], WorkItem[item], the hash sets of
+// IN / NOT_IN leaves (staged into LDS by the kernel) and sorted-index doc ranges.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -23,42 +24,67 @@
 namespace pg {
 
 constexpr int kBlock = 256;                          // 4 waves of 64
-constexpr int kDocsPerThread = 16;                   // docs of a thread in a tile: base + j*256 + tid
-constexpr int kTileDocs = kBlock * kDocsPerThread;   // 4096 docs per tile
+constexpr int kRows = 16;                            // docs of a thread in a tile: base + j*256 + tid
+constexpr int kTileDocs = kBlock * kRows;            // 4096 docs per tile
+constexpr int kItemTiles = 8;                        // tiles per work item (32 768 docs), within one segment
 constexpr int kMaxAggs = 8;
 constexpr int kMaxKeys = 4;
 constexpr int kMaxLeaves = 24;
-constexpr int kMaxOps = 48;
-constexpr int kMaxStack = 8;
+constexpr int kMaxOps = 64;
+constexpr int kMaxDepth = 8;                         // filter tree nesting
 constexpr int kLdsGroupBytes = 48 * 1024;            // LDS-privatised group table budget
+constexpr int kLdsSetBytes = 32 * 1024;              // LDS hash sets of IN / NOT_IN leaves
 
-enum DevLeafKind : uint32_t {
-  DL_ALL = 0,        // match all
-  DL_NONE = 1,       // match none
-  DL_RANGE = 2,      // dictId in [lo,hi) decoded from a packed SV forward index
-  DL_LUT = 3,        // dictId in set: bit dictId of `lut` (native LSB-first words)
-  DL_DOCBITMAP = 4,  // precomputed doc bitmap (native LSB-first words)
-  DL_DOCRANGE = 5    // doc id in [lo,hi)
+// Filter program as the kernel runs it: a tree in prefix form (host-compiled from the ABI's postfix program,
+// AND children ordered most-selective first so later children are evaluated only on surviving docs).
+constexpr int32_t kOpAnd = -1, kOpOr = -2, kOpNot = -3, kOpEnd = -4;  // >= 0: leaf index
+
+enum LeafKind : uint32_t {
+  LK_ALL = 0,        // match all
+  LK_NONE = 1,       // match none
+  LK_RANGE = 2,      // dictId in [lo,hi), dictIds unpacked from a packed SV forward index
+  LK_SET_LDS = 3,    // dictId in set: open-addressing hash set staged in LDS (lds_off / set_log2)
+  LK_SET_LUT = 4,    // dictId in set: bit dictId of `aux` (global LSB-first words)
+  LK_DOCBITMAP = 5,  // precomputed doc bitmap `aux` (native LSB-first words)
+  LK_DOCRANGE = 6    // doc id in [lo,hi)
 };
 
-struct DevLeaf {
+struct LeafDesc {
   uint32_t kind;
-  uint32_t excl;
+  uint32_t excl;      // invert the leaf (NOT_EQ / NOT_IN on a scan)
   int32_t lo, hi;
-  const uint32_t* words;  // packed forward words (RANGE / LUT) or doc bitmap (DOCBITMAP)
-  const uint32_t* lut;    // LUT
+  const uint32_t* words;  // packed forward words (RANGE / SET_*)
+  const uint32_t* aux;    // SET_LUT bitmap / DOCBITMAP / SET_LDS source table (global)
   uint32_t bits;
+  uint32_t set_log2;      // SET_LDS: table has 1 << set_log2 int32 slots (empty = -1)
+  uint32_t lds_off;       // SET_LDS: int32 offset of the table in the block's LDS set region
   uint32_t pad;
 };
 
 // A column as read by aggregation inputs and group keys.
-struct DevCol {
+struct ColDesc {
   const uint32_t* words;      // packed SV forward words
   const void* dict;           // typed dictionary values
   const int32_t* keymap;      // dictId -> global key (PG_KEY_KEYMAP)
   const uint32_t* mv_offsets; // MV: row offsets [num_docs+1]
   uint32_t bits;
   uint32_t dtype;             // pg_data_type
+  uint32_t card;
+  uint32_t pad;
+};
+
+struct SegDesc {
+  uint32_t num_docs;
+  uint32_t pad;
+  const LeafDesc* leaves;   // [num_leaves]
+  const ColDesc* aggcols;   // [num_aggs][2]
+  const ColDesc* keycols;   // [num_keys]
+};
+
+struct WorkItem {
+  uint32_t seg;
+  uint32_t tile_begin, tile_end;  // tiles of kTileDocs docs within the segment
+  uint32_t pad;
 };
 
 enum SlotKind : uint32_t { SK_NONE = 0, SK_I64 = 1, SK_F64 = 2, SK_MIN = 3, SK_MAX = 4, SK_FLAG = 5 };
@@ -77,8 +103,9 @@ struct AggSpec {
 };
 
 struct QuerySpec {
-  uint32_t num_segments, num_leaves, num_ops, num_aggs, num_keys;
-  uint32_t use_lds;        // group table privatised in LDS
+  uint32_t num_segments, num_leaves, num_ops, num_aggs, num_keys, num_items;
+  uint32_t use_lds;          // group table privatised in LDS
+  uint32_t set_lds_ints;     // int32 slots of LDS hash sets per block
   int32_t ops[kMaxOps];
   AggSpec aggs[kMaxAggs];
   uint32_t key_kind[kMaxKeys];
@@ -93,13 +120,10 @@ struct QuerySpec {
   long long* mn;
   long long* mx;
   uint8_t* flags;
-  const DevLeaf* leaves;     // [seg][num_leaves]
-  const DevCol* aggcols;     // [seg][num_aggs][2]
-  const DevCol* keycols;     // [seg][num_keys]
-  const uint32_t* num_docs;  // [seg]
-  const uint64_t* tile_prefix;  // [seg+1]
-  uint64_t total_tiles;
+  const SegDesc* segs;       // [seg]
+  const WorkItem* items;     // [item]
   unsigned long long* seg_matched;  // [seg]
+  unsigned int* err;                // device-side bounds violations (bit 0 group key, bit 1 DISTINCTCOUNT key)
 };
 
 // order-preserving int64 image of a double (for MIN/MAX slots)
@@ -115,9 +139,14 @@ __host__ __device__ inline double order_key_decode(int64_t k) {
   return v;
 }
 
-// ---- kernel launchers (pg_kernels.hip)
-hipError_t launch_scan(const QuerySpec& q, uint32_t blocks, hipStream_t s);
-hipError_t launch_init_state(const QuerySpec& q, hipStream_t s);
+// IN-list hash: home slot of dictId `id` in a table of 2^log2 slots (shared by the host builder and the kernel)
+__host__ __device__ inline uint32_t set_hash(uint32_t id, uint32_t log2) {
+  return log2 ? (uint32_t)(id * 0x9E3779B1u) >> (32 - log2) : 0u;
+}
+
+// ---- kernel launchers
+hipError_t launch_scan(const QuerySpec& q, uint32_t blocks, hipStream_t s);                  // pg_scan.hip
+hipError_t launch_init_state(const QuerySpec& q, hipStream_t s);                             // pg_kernels.hip
 hipError_t launch_bswap_words(const uint8_t* src, uint32_t* dst, uint64_t nbytes, uint64_t nwords_out, hipStream_t s);
 hipError_t launch_be_to_native(const uint8_t* src, void* dst, uint64_t n, uint32_t width, hipStream_t s);
 hipError_t launch_sorted_to_packed(const int32_t* pairs, uint32_t card, uint32_t num_docs, uint32_t bits,
@@ -139,6 +168,12 @@ hipError_t launch_bitmap_not(uint32_t* bitmap, uint32_t num_docs, hipStream_t s)
 hipError_t launch_mv_scan(const uint32_t* words, uint32_t bits, const uint32_t* offsets, uint32_t num_docs,
                           int32_t lo, int32_t hi, const uint32_t* lut, uint32_t excl, uint32_t* bitmap,
                           hipStream_t s);
-hipError_t launch_set_lut_bits(const int32_t* ids, uint32_t n, uint32_t* lut, hipStream_t s);
+struct LutJob {            // set bits ids[0..n) in lut (one batched launch for every LUT of a query)
+  const int32_t* ids;
+  uint32_t* lut;
+  uint32_t n;
+  uint32_t pad;
+};
+hipError_t launch_set_lut_bits(const LutJob* jobs, uint32_t njobs, hipStream_t s);
 
 }  // namespace pg

@@ -1,16 +1,7 @@
-// pg_kernels.hip -- gfx950 kernels of the segment query hot path.
-//
-// scan_kernel is the fused hot loop that replaces, per tile of 4096 docs, Pinot's chain
-//   DocIdSetOperator (10 000-doc blocks, operator/DocIdSetOperator.java:58-83)
-//   -> SVScanDocIdIterator + PredicateEvaluator.applySV (dociditerators/SVScanDocIdIterator.java:67-125)
-//   -> FixedBitSVForwardIndexReaderV2.readDictIds / FixedBitIntReader (readers/forward/...V2.java:62-97)
-//   -> AND/OR/NOT doc-id algebra (docidsets/AndDocIdSet.java:60-150, OrDocIdSet.java:58-114)
-//   -> DataFetcher.readDoubleValues + Dictionary.readDoubleValues (common/DataFetcher.java:511-521)
-//   -> Sum/Count/Min/Max/Avg/DistinctCount/CountMV aggregate / aggregateGroupBySV
-//   -> DictionaryBasedGroupKeyGenerator mixed-radix keys (groupby/DictionaryBasedGroupKeyGenerator.java:280-322)
-// with no intermediate doc-id lists: each thread owns docs base + j*256 + tid (j < 16), so the 64 lanes
-// of a wave read 64 consecutive packed values (one contiguous run of 8*b bytes) per load instruction.
-// Nothing here is a dense contraction: there is no MFMA; the roofline is HBM bandwidth.
+// pg_kernels.hip -- gfx950 support kernels of the segment query hot path: upload-time re-layout (byte order,
+// sorted -> packed, MV row offsets), the filter pre-pass for index-backed leaves (sorted ranges, roaring
+// bitmaps, MV scans, IN-list LUTs) and state initialisation.  The fused scan itself is in pg_scan.hip.
+
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -18,371 +9,13 @@
 
 namespace pg {
 
-// ------------------------------------------------------------------------------------------ helpers
-
-// FixedBitIntReader.readUnchecked equivalent on the native-word image: value `idx` of `b` bits.
+// FixedBitIntReader.readUnchecked on the native-word image: value `idx` of `b` bits (MV value streams).
 __device__ __forceinline__ uint32_t unpack(const uint32_t* __restrict__ w, uint64_t idx, uint32_t b) {
   const uint64_t p = idx * b;
   const uint64_t wi = p >> 5;
   const uint32_t off = (uint32_t)p & 31u;
   const uint64_t win = ((uint64_t)w[wi] << 32) | (uint64_t)w[wi + 1];
-  const uint32_t mask = b >= 32 ? 0xFFFFFFFFu : ((1u << b) - 1u);
-  return (uint32_t)(win >> (64u - off - b)) & mask;
-}
-
-__device__ __forceinline__ double dict_double(const DevCol& c, uint32_t id) {
-  switch (c.dtype) {
-    case PG_INT: return (double)((const int32_t*)c.dict)[id];
-    case PG_LONG: return (double)((const int64_t*)c.dict)[id];
-    case PG_FLOAT: return (double)((const float*)c.dict)[id];
-    default: return ((const double*)c.dict)[id];
-  }
-}
-
-__device__ __forceinline__ int64_t dict_i64(const DevCol& c, uint32_t id) {
-  return c.dtype == PG_INT ? (int64_t)((const int32_t*)c.dict)[id] : ((const int64_t*)c.dict)[id];
-}
-
-// TransformFunction value of an aggregation input (double path).
-// MultiplicationTransformFunction.transformToDoubleValuesSV (transform/function/MultiplicationTransformFunction.java:91-111):
-// start from the literal product 1.0, multiply arguments in order; compiled with -ffp-contract=off.
-__device__ __forceinline__ double agg_value_f64(const AggSpec& a, const DevCol* c, uint32_t d) {
-  const double va = dict_double(c[0], unpack(c[0].words, d, c[0].bits));
-  if (a.op == PG_EXPR_COL) return va;
-  const double vb = dict_double(c[1], unpack(c[1].words, d, c[1].bits));
-  switch (a.op) {
-    case PG_EXPR_MUL: return (1.0 * va) * vb;
-    case PG_EXPR_ADD: return va + vb;
-    default: return va - vb;
-  }
-}
-
-// integer-exact path (host proved |result| bounds): identical value to the double path when < 2^53
-__device__ __forceinline__ int64_t agg_value_i64(const AggSpec& a, const DevCol* c, uint32_t d) {
-  const int64_t va = dict_i64(c[0], unpack(c[0].words, d, c[0].bits));
-  if (a.op == PG_EXPR_COL) return va;
-  const int64_t vb = dict_i64(c[1], unpack(c[1].words, d, c[1].bits));
-  switch (a.op) {
-    case PG_EXPR_MUL: return va * vb;
-    case PG_EXPR_ADD: return va + vb;
-    default: return va - vb;
-  }
-}
-
-__device__ __forceinline__ uint64_t col_key(uint32_t kind, int64_t base, const DevCol& c, uint32_t d) {
-  const uint32_t id = unpack(c.words, d, c.bits);
-  return kind == PG_KEY_KEYMAP ? (uint64_t)(uint32_t)c.keymap[id] : (uint64_t)(dict_i64(c, id) - base);
-}
-
-// One leaf over the thread's 16 docs -> 16-bit mask (bit j <-> doc base + j*256 + tid).
-__device__ __forceinline__ uint32_t eval_leaf(const DevLeaf& L, uint32_t base, uint32_t last_doc, int tid) {
-  uint32_t m = 0;
-  switch (L.kind) {
-    case DL_ALL: m = 0xFFFFu; break;
-    case DL_NONE: m = 0u; break;
-    case DL_RANGE: {
-      const uint32_t lo = (uint32_t)L.lo, span = (uint32_t)(L.hi - L.lo);
-#pragma unroll
-      for (int j = 0; j < kDocsPerThread; j++) {
-        const uint32_t d = min(base + (uint32_t)(j * kBlock + tid), last_doc);
-        const uint32_t v = unpack(L.words, d, L.bits);
-        m |= (uint32_t)((v - lo) < span) << j;
-      }
-      break;
-    }
-    case DL_LUT: {
-#pragma unroll
-      for (int j = 0; j < kDocsPerThread; j++) {
-        const uint32_t d = min(base + (uint32_t)(j * kBlock + tid), last_doc);
-        const uint32_t v = unpack(L.words, d, L.bits);
-        m |= ((L.lut[v >> 5] >> (v & 31u)) & 1u) << j;
-      }
-      break;
-    }
-    case DL_DOCBITMAP: {
-#pragma unroll
-      for (int j = 0; j < kDocsPerThread; j++) {
-        const uint32_t d = min(base + (uint32_t)(j * kBlock + tid), last_doc);
-        m |= ((L.words[d >> 5] >> (d & 31u)) & 1u) << j;
-      }
-      break;
-    }
-    default: {  // DL_DOCRANGE
-#pragma unroll
-      for (int j = 0; j < kDocsPerThread; j++) {
-        const uint32_t d = base + (uint32_t)(j * kBlock + tid);
-        m |= (uint32_t)(d >= (uint32_t)L.lo && d < (uint32_t)L.hi) << j;
-      }
-      break;
-    }
-  }
-  return L.excl ? (~m & 0xFFFFu) : m;
-}
-
-// Postfix filter program over 16-bit masks; the stack (<= 8 entries) lives in two 64-bit registers.
-__device__ __forceinline__ uint32_t eval_program(const QuerySpec& q, const DevLeaf* __restrict__ leaves,
-                                                 uint32_t base, uint32_t last_doc, int tid) {
-  uint64_t lo = 0, hi = 0;
-  for (uint32_t i = 0; i < q.num_ops; i++) {
-    const int32_t op = q.ops[i];
-    if (op >= 0) {
-      const uint32_t m = eval_leaf(leaves[op], base, last_doc, tid);
-      hi = (hi << 16) | (lo >> 48);
-      lo = (lo << 16) | m;
-    } else if (op == PG_OP_NOT) {
-      lo ^= 0xFFFFull;
-    } else {
-      const int n = (-op) & 0xFF;
-      const bool is_and = ((-op) & 0x100) != 0;
-      uint32_t acc = (uint32_t)(lo & 0xFFFFu);
-      lo = (lo >> 16) | (hi << 48);
-      hi >>= 16;
-      for (int k = 1; k < n; k++) {
-        const uint32_t m = (uint32_t)(lo & 0xFFFFu);
-        lo = (lo >> 16) | (hi << 48);
-        hi >>= 16;
-        acc = is_and ? (acc & m) : (acc | m);
-      }
-      hi = (hi << 16) | (lo >> 48);
-      lo = (lo << 16) | acc;
-    }
-  }
-  return q.num_ops ? (uint32_t)(lo & 0xFFFFu) : 0xFFFFu;
-}
-
-__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-__device__ __forceinline__ double wave_sum_f64(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) { int64_t x = __shfl_xor(v, o); v = x < v ? x : v; }
-  return v;
-}
-__device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) { int64_t x = __shfl_xor(v, o); v = x > v ? x : v; }
-  return v;
-}
-
-// ------------------------------------------------------------------------------------------ scan
-
-__global__ __launch_bounds__(kBlock) void scan_kernel(QuerySpec q) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tid = threadIdx.x;
-  const uint64_t T = q.total_tiles;
-  const uint64_t t0 = (uint64_t)blockIdx.x * T / gridDim.x;
-  const uint64_t t1 = ((uint64_t)blockIdx.x + 1) * T / gridDim.x;
-  const bool grouped = q.num_keys > 0;
-
-  // LDS-privatised group table: [G][n_i64] u64 | [G][n_f64] f64 | [G][n_min] i64 | [G][n_max] i64
-  unsigned long long* l_i64 = (unsigned long long*)smem;
-  double* l_f64 = (double*)(l_i64 + q.num_slots * q.n_i64);
-  long long* l_mn = (long long*)(l_f64 + q.num_slots * q.n_f64);
-  long long* l_mx = l_mn + q.num_slots * q.n_min;
-  if (grouped && q.use_lds) {
-    for (uint64_t i = tid; i < q.num_slots * q.n_i64; i += kBlock) l_i64[i] = 0;
-    for (uint64_t i = tid; i < q.num_slots * q.n_f64; i += kBlock) l_f64[i] = 0.0;
-    for (uint64_t i = tid; i < q.num_slots * q.n_min; i += kBlock) l_mn[i] = order_key(__builtin_inf());
-    for (uint64_t i = tid; i < q.num_slots * q.n_max; i += kBlock) l_mx[i] = order_key(-__builtin_inf());
-    __syncthreads();
-  }
-
-  // aggregation-only accumulators (registers; indices compile-time via unrolled agg loops)
-  uint64_t acc[kMaxAggs];
-#pragma unroll
-  for (int a = 0; a < kMaxAggs; a++) {
-    acc[a] = 0;
-    if (a < (int)q.num_aggs) {
-      if (q.aggs[a].kind == SK_MIN) acc[a] = (uint64_t)order_key(__builtin_inf());
-      if (q.aggs[a].kind == SK_MAX) acc[a] = (uint64_t)order_key(-__builtin_inf());
-    }
-  }
-  uint64_t doc_count = 0;  // matched docs of this thread (aggregation-only slot 0)
-
-  // segment of the first tile
-  uint32_t seg = 0;
-  if (t0 < t1) {
-    uint32_t lo = 0, hi = q.num_segments;  // last seg with tile_prefix[seg] <= t0
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (q.tile_prefix[mid] <= t0) lo = mid; else hi = mid;
-    }
-    seg = lo;
-  }
-  uint64_t seg_count = 0;
-
-  for (uint64_t t = t0; t < t1; t++) {
-    while (t >= q.tile_prefix[seg + 1]) {
-      const uint64_t c = wave_sum_u64(seg_count);
-      if ((tid & 63) == 0 && c) atomicAdd(&q.seg_matched[seg], (unsigned long long)c);
-      seg_count = 0;
-      seg++;
-    }
-    const uint32_t nd = q.num_docs[seg];
-    const uint32_t base = (uint32_t)(t - q.tile_prefix[seg]) * (uint32_t)kTileDocs;
-    const uint32_t last_doc = nd - 1;
-    uint32_t valid = 0;
-#pragma unroll
-    for (int j = 0; j < kDocsPerThread; j++) valid |= (uint32_t)(base + (uint32_t)(j * kBlock + tid) < nd) << j;
-
-    const DevLeaf* leaves = q.leaves + (uint64_t)seg * q.num_leaves;
-    uint32_t m = eval_program(q, leaves, base, last_doc, tid) & valid;
-    const uint32_t nm = __popc(m);
-    seg_count += nm;
-    if (m == 0) continue;
-
-    const DevCol* aggcols = q.aggcols + (uint64_t)seg * q.num_aggs * 2;
-    if (!grouped) {
-      doc_count += nm;
-      while (m) {
-        const int j = __ffs(m) - 1;
-        m &= m - 1;
-        const uint32_t d = base + (uint32_t)(j * kBlock + tid);
-#pragma unroll
-        for (int a = 0; a < kMaxAggs; a++) {
-          if (a >= (int)q.num_aggs) break;
-          const AggSpec& A = q.aggs[a];
-          const DevCol* c = aggcols + 2 * a;
-          switch (A.fn) {
-            case PG_AGG_COUNT: acc[a] += 1; break;
-            case PG_AGG_COUNTMV: acc[a] += c[0].mv_offsets[d + 1] - c[0].mv_offsets[d]; break;
-            case PG_AGG_SUM:
-            case PG_AGG_AVG:
-              if (A.integer) acc[a] += (uint64_t)agg_value_i64(A, c, d);
-              else acc[a] = __double_as_longlong(__longlong_as_double(acc[a]) + agg_value_f64(A, c, d));
-              break;  // AVG count == the group's doc count (slot 0)
-            case PG_AGG_MIN: {
-              const int64_t k = order_key(agg_value_f64(A, c, d));
-              if (k < (int64_t)acc[a]) acc[a] = (uint64_t)k;
-              break;
-            }
-            case PG_AGG_MAX: {
-              const int64_t k = order_key(agg_value_f64(A, c, d));
-              if (k > (int64_t)acc[a]) acc[a] = (uint64_t)k;
-              break;
-            }
-            case PG_AGG_DISTINCTCOUNT: {
-              const uint64_t key = col_key(A.key_kind, A.key_base, c[0], d);
-              q.flags[A.flag_off + key] = 1;
-              break;
-            }
-          }
-        }
-      }
-    } else {
-      const DevCol* keycols = q.keycols + (uint64_t)seg * q.num_keys;
-      while (m) {
-        const int j = __ffs(m) - 1;
-        m &= m - 1;
-        const uint32_t d = base + (uint32_t)(j * kBlock + tid);
-        uint64_t g = 0;
-#pragma unroll
-        for (int k = 0; k < kMaxKeys; k++) {
-          if (k >= (int)q.num_keys) break;
-          g += col_key(q.key_kind[k], q.key_base[k], keycols[k], d) * q.key_stride[k];
-        }
-        unsigned long long* gi = q.use_lds ? l_i64 : q.i64;
-        double* gf = q.use_lds ? l_f64 : q.f64;
-        long long* gmn = q.use_lds ? l_mn : q.mn;
-        long long* gmx = q.use_lds ? l_mx : q.mx;
-        atomicAdd(&gi[g * q.n_i64], 1ull);  // slot 0: doc count / presence
-#pragma unroll
-        for (int a = 0; a < kMaxAggs; a++) {
-          if (a >= (int)q.num_aggs) break;
-          const AggSpec& A = q.aggs[a];
-          const DevCol* c = aggcols + 2 * a;
-          switch (A.fn) {
-            case PG_AGG_COUNT: break;  // = slot 0
-            case PG_AGG_COUNTMV:
-              atomicAdd(&gi[g * q.n_i64 + A.slot],
-                        (unsigned long long)(c[0].mv_offsets[d + 1] - c[0].mv_offsets[d]));
-              break;
-            case PG_AGG_SUM:
-            case PG_AGG_AVG:
-              if (A.integer) atomicAdd(&gi[g * q.n_i64 + A.slot], (unsigned long long)agg_value_i64(A, c, d));
-              else atomicAdd(&gf[g * q.n_f64 + A.slot], agg_value_f64(A, c, d));
-              break;  // AVG count == slot 0
-            case PG_AGG_MIN:
-              atomicMin(&gmn[g * q.n_min + A.slot], (long long)order_key(agg_value_f64(A, c, d)));
-              break;
-            case PG_AGG_MAX:
-              atomicMax(&gmx[g * q.n_max + A.slot], (long long)order_key(agg_value_f64(A, c, d)));
-              break;
-            case PG_AGG_DISTINCTCOUNT: {
-              const uint64_t key = col_key(A.key_kind, A.key_base, c[0], d);
-              q.flags[g * q.flag_bytes_per_slot + A.flag_off + key] = 1;
-              break;
-            }
-          }
-        }
-      }
-    }
-  }
-  {
-    const uint64_t c = wave_sum_u64(seg_count);
-    if ((tid & 63) == 0 && c) atomicAdd(&q.seg_matched[seg], (unsigned long long)c);
-  }
-
-  if (!grouped) {
-    // wave-reduce then one global atomic per wave per slot
-    const uint64_t dc = wave_sum_u64(doc_count);
-    const bool lead = (tid & 63) == 0;
-    if (lead && dc) atomicAdd(&q.i64[0], (unsigned long long)dc);
-#pragma unroll
-    for (int a = 0; a < kMaxAggs; a++) {
-      if (a >= (int)q.num_aggs) break;
-      const AggSpec& A = q.aggs[a];
-      switch (A.kind) {
-        case SK_I64: {
-          const uint64_t v = wave_sum_u64(acc[a]);
-          if (lead && v) atomicAdd(&q.i64[A.slot], (unsigned long long)v);
-          break;
-        }
-        case SK_F64: {
-          const double v = wave_sum_f64(__longlong_as_double(acc[a]));
-          if (lead && v != 0.0) atomicAdd(&q.f64[A.slot], v);
-          break;
-        }
-        case SK_MIN: {
-          const int64_t v = wave_min_i64((int64_t)acc[a]);
-          if (lead) atomicMin(&q.mn[A.slot], (long long)v);
-          break;
-        }
-        case SK_MAX: {
-          const int64_t v = wave_max_i64((int64_t)acc[a]);
-          if (lead) atomicMax(&q.mx[A.slot], (long long)v);
-          break;
-        }
-        default: break;
-      }
-    }
-  } else if (q.use_lds) {
-    __syncthreads();
-    for (uint64_t g = tid; g < q.num_slots; g += kBlock) {
-      if (l_i64[g * q.n_i64] == 0) continue;
-      for (uint32_t s = 0; s < q.n_i64; s++) {
-        const unsigned long long v = l_i64[g * q.n_i64 + s];
-        if (v) atomicAdd(&q.i64[g * q.n_i64 + s], v);
-      }
-      for (uint32_t s = 0; s < q.n_f64; s++) atomicAdd(&q.f64[g * q.n_f64 + s], l_f64[g * q.n_f64 + s]);
-      for (uint32_t s = 0; s < q.n_min; s++) atomicMin(&q.mn[g * q.n_min + s], l_mn[g * q.n_min + s]);
-      for (uint32_t s = 0; s < q.n_max; s++) atomicMax(&q.mx[g * q.n_max + s], l_mx[g * q.n_max + s]);
-    }
-  }
-}
-
-hipError_t launch_scan(const QuerySpec& q, uint32_t blocks, hipStream_t s) {
-  size_t lds = 0;
-  if (q.num_keys && q.use_lds) lds = q.num_slots * 8ull * (q.n_i64 + q.n_f64 + q.n_min + q.n_max);
-  hipLaunchKernelGGL(scan_kernel, dim3(blocks), dim3(kBlock), lds, s, q);
-  return hipGetLastError();
+  return (uint32_t)(win >> (64u - off - b)) & (0xFFFFFFFFu >> (32u - b));
 }
 
 // ------------------------------------------------------------------------------------------ state init
@@ -400,7 +33,7 @@ hipError_t launch_init_state(const QuerySpec& q, hipStream_t s) {
   if (q.n_f64 && (e = hipMemsetAsync(q.f64, 0, q.num_slots * q.n_f64 * 8, s)) != hipSuccess) return e;
   if (q.flag_bytes_per_slot && (e = hipMemsetAsync(q.flags, 0, q.num_slots * q.flag_bytes_per_slot, s)) != hipSuccess)
     return e;
-  if ((e = hipMemsetAsync(q.seg_matched, 0, q.num_segments * 8ull, s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(q.seg_matched, 0, (q.num_segments ? q.num_segments : 1) * 8ull + 16, s)) != hipSuccess) return e;
   const uint64_t n = q.num_slots * (q.n_min > q.n_max ? q.n_min : q.n_max);
   if (n) {
     const uint32_t blocks = (uint32_t)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
@@ -680,15 +313,17 @@ hipError_t launch_mv_scan(const uint32_t* words, uint32_t bits, const uint32_t* 
   return hipGetLastError();
 }
 
-__global__ void set_lut_bits_kernel(const int32_t* __restrict__ ids, uint32_t n, uint32_t* __restrict__ lut) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    atomicOr(&lut[(uint32_t)ids[i] >> 5], 1u << ((uint32_t)ids[i] & 31u));
+// IN / NOT_IN dictId sets too large for an LDS hash set -> global bitmaps over dictIds; one launch for all
+// (segment, leaf) LUTs of a query: block b handles job b.
+__global__ void set_lut_bits_kernel(const LutJob* __restrict__ jobs) {
+  const LutJob J = jobs[blockIdx.x];
+  for (uint32_t i = threadIdx.x; i < J.n; i += blockDim.x)
+    atomicOr(&J.lut[(uint32_t)J.ids[i] >> 5], 1u << ((uint32_t)J.ids[i] & 31u));
 }
 
-hipError_t launch_set_lut_bits(const int32_t* ids, uint32_t n, uint32_t* lut, hipStream_t s) {
-  if (!n) return hipSuccess;
-  const uint32_t blocks = (n + 255) / 256;
-  hipLaunchKernelGGL(set_lut_bits_kernel, dim3(blocks < 4096 ? blocks : 4096), dim3(256), 0, s, ids, n, lut);
+hipError_t launch_set_lut_bits(const LutJob* jobs, uint32_t njobs, hipStream_t s) {
+  if (!njobs) return hipSuccess;
+  hipLaunchKernelGGL(set_lut_bits_kernel, dim3(njobs), dim3(256), 0, s, jobs);
   return hipGetLastError();
 }
 

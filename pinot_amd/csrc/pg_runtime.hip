@@ -76,13 +76,46 @@ int64_t now_ms() {
 
 // ------------------------------------------------------------------------------------------ residency
 
-// Device buffer: resident buffers use hipMalloc; per-query buffers (async=true) use the stream-ordered
-// pool (hipMallocAsync / hipFreeAsync) so steady-state queries never call hipMalloc / hipFree.
+// Caching device allocator for per-query buffers (parameter arena, filter scratch, partial state):
+// power-of-two buckets, hipMalloc on a miss, blocks parked for reuse instead of freed, so steady-state queries
+// make no hipMalloc / hipFree calls.  A block is returned only after the host has synchronised with every
+// launch that used it.
+class DevicePool {
+ public:
+  void* get(uint64_t bytes, uint64_t* cap) {
+    uint64_t c = 256;
+    while (c < bytes) c <<= 1;
+    *cap = c;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto& v = free_[c];
+      if (!v.empty()) {
+        void* p = v.back();
+        v.pop_back();
+        return p;
+      }
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, c) != hipSuccess) return nullptr;
+    return p;
+  }
+  void put(void* p, uint64_t cap) {
+    std::lock_guard<std::mutex> g(mu_);
+    free_[cap].push_back(p);
+  }
+
+ private:
+  std::mutex mu_;
+  std::unordered_map<uint64_t, std::vector<void*>> free_;
+};
+DevicePool g_pool;
+
+// Device buffer: resident index buffers own a hipMalloc allocation; per-query buffers borrow a pool block.
 struct DevBuf {
   void* p = nullptr;
   uint64_t bytes = 0;
-  hipStream_t stream = nullptr;
-  bool async = false;
+  uint64_t cap = 0;
+  bool pooled = false;
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
@@ -90,42 +123,60 @@ struct DevBuf {
   DevBuf& operator=(DevBuf&& o) noexcept {
     if (this != &o) {
       reset();
-      p = o.p; bytes = o.bytes; stream = o.stream; async = o.async;
-      o.p = nullptr; o.bytes = 0;
+      p = o.p; bytes = o.bytes; cap = o.cap; pooled = o.pooled;
+      o.p = nullptr; o.bytes = 0; o.cap = 0;
     }
     return *this;
   }
   ~DevBuf() { reset(); }
   void reset() {
     if (p) {
-      if (async) hipFreeAsync(p, stream);
-      else hipFree(p);
+      if (pooled) g_pool.put(p, cap);
+      else (void)hipFree(p);
     }
     p = nullptr;
-    bytes = 0;
+    bytes = cap = 0;
   }
   int alloc(uint64_t n) {
     reset();
     if (n == 0) n = 16;
-    async = false;
+    pooled = false;
     if (hipMalloc(&p, n) != hipSuccess) {
       p = nullptr;
       return fail(PG_E_NOMEM, "hipMalloc(%llu) failed", (unsigned long long)n);
     }
+    bytes = cap = n;
+    return PG_OK;
+  }
+  int alloc_pooled(uint64_t n) {
+    reset();
+    if (n == 0) n = 16;
+    pooled = true;
+    p = g_pool.get(n, &cap);
+    if (!p) return fail(PG_E_NOMEM, "device allocation of %llu bytes failed", (unsigned long long)n);
     bytes = n;
     return PG_OK;
   }
-  int alloc_async(uint64_t n, hipStream_t s) {
-    reset();
-    if (n == 0) n = 16;
-    async = true;
-    stream = s;
-    if (hipMallocAsync(&p, n, s) != hipSuccess) {
-      p = nullptr;
-      return fail(PG_E_NOMEM, "hipMallocAsync(%llu) failed", (unsigned long long)n);
+};
+
+// Pinned host staging for the per-query parameter arena (one H2D DMA, no pageable bounce).
+struct PinnedBuf {
+  void* p = nullptr;
+  uint64_t cap = 0;
+  ~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  void* get(uint64_t n) {
+    if (n > cap) {
+      if (p) (void)hipHostFree(p);
+      cap = 1;
+      while (cap < n) cap <<= 1;
+      if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess) {
+        p = nullptr;
+        cap = 0;
+      }
     }
-    bytes = n;
-    return PG_OK;
+    return p;
   }
 };
 
@@ -477,20 +528,107 @@ struct Arena {  // host image of the per-query parameter block, copied to the de
   }
 };
 
-struct PrepassOp {  // filter materialisation work item
-  enum Kind { FILL_RANGES, ROARING, MV_SCAN, LUT } kind;
+struct PrepassOp {  // filter materialisation of an index-backed leaf into a doc bitmap (scratch)
+  enum Kind { FILL_RANGES, ROARING, MV_SCAN } kind;
   uint32_t seg, leaf;
-  uint64_t in_off = 0;   // arena offset of ranges / selected containers / ids
+  uint64_t in_off = 0;   // arena offset of ranges / selected containers
   uint32_t n = 0;
   uint32_t num_docs = 0;
-  uint64_t out_off = 0;  // scratch offset of the doc bitmap / LUT
-  uint64_t out_bytes = 0;
+  uint64_t out_off = 0;  // scratch offset of the doc bitmap
   bool negate = false;
   const ColumnRes* col = nullptr;
   int32_t lo = 0, hi = 0;
-  uint64_t lut_off = 0;  // MV scan: scratch LUT offset (or ~0 for range)
+  uint64_t lut_off = ~0ull;  // MV scan: scratch LUT offset (or ~0 for a dictId range)
   uint32_t excl = 0;
 };
+
+// ---- filter program: ABI postfix -> tree -> prefix form for the kernel, AND / OR children reordered by
+// estimated pass fraction so that later children only see surviving docs (the device analogue of
+// FilterOperatorUtils.reorderAndFilterChildOperators, operator/filter/FilterOperatorUtils.java:160-200, plus
+// AndDocIdSet evaluating scan children only on the docs the earlier children accepted).
+struct FNode {
+  int kind;  // 0 leaf, 1 AND, 2 OR, 3 NOT
+  int leaf = -1;
+  std::vector<int> kids;
+  double pass = 1.0;  // estimated fraction of docs accepted
+  double cost = 0.0;  // estimated bytes / doc read when evaluated densely
+};
+
+int build_tree(const pg_plan* plan, const std::vector<double>& leaf_pass, const std::vector<double>& leaf_cost,
+               std::vector<FNode>& nodes, int& root) {
+  std::vector<int> st;
+  for (uint32_t i = 0; i < plan->num_ops; i++) {
+    const int32_t op = plan->ops[i];
+    if (op >= 0) {
+      FNode n;
+      n.kind = 0;
+      n.leaf = op;
+      n.pass = leaf_pass[op];
+      n.cost = leaf_cost[op];
+      nodes.push_back(n);
+      st.push_back((int)nodes.size() - 1);
+    } else if (op == PG_OP_NOT) {
+      FNode n;
+      n.kind = 3;
+      n.kids.push_back(st.back());
+      st.pop_back();
+      n.pass = 1.0 - nodes[n.kids[0]].pass;
+      n.cost = nodes[n.kids[0]].cost;
+      nodes.push_back(n);
+      st.push_back((int)nodes.size() - 1);
+    } else {
+      const int cnt = (-op) & 0xFF;
+      const int kind = ((-op) & 0x100) ? 1 : 2;
+      FNode n;
+      n.kind = kind;
+      std::vector<int> kids(st.end() - cnt, st.end());
+      st.resize(st.size() - cnt);
+      for (int k : kids) {  // flatten AND(AND(..)) / OR(OR(..))
+        if (nodes[k].kind == kind) n.kids.insert(n.kids.end(), nodes[k].kids.begin(), nodes[k].kids.end());
+        else n.kids.push_back(k);
+      }
+      // AND: cheapest-per-rejection first ~ ascending pass fraction, zero-cost leaves (doc ranges, bitmaps)
+      // before column scans; OR: descending pass fraction.  Results are order independent.
+      auto rank = [&](int k) {
+        const double p = kind == 1 ? nodes[k].pass : 1.0 - nodes[k].pass;
+        return nodes[k].cost <= 0.0 ? p - 2.0 : p + 1e-3 * nodes[k].cost;
+      };
+      std::stable_sort(n.kids.begin(), n.kids.end(), [&](int a, int b) { return rank(a) < rank(b); });
+      double pass = kind == 1 ? 1.0 : 0.0, cost = 0.0, reach = 1.0;
+      for (int k : n.kids) {
+        cost += reach * nodes[k].cost;
+        if (kind == 1) { pass *= nodes[k].pass; reach = pass; }
+        else { pass = 1.0 - (1.0 - pass) * (1.0 - nodes[k].pass); reach = 1.0 - pass; }
+      }
+      n.pass = pass;
+      n.cost = cost;
+      nodes.push_back(n);
+      st.push_back((int)nodes.size() - 1);
+    }
+  }
+  root = st.empty() ? -1 : st.back();
+  return PG_OK;
+}
+
+void emit_prefix(const std::vector<FNode>& nodes, int n, std::vector<int32_t>& out) {
+  const FNode& x = nodes[n];
+  if (x.kind == 0) { out.push_back(x.leaf); return; }
+  if (x.kind != 3 && x.kids.size() == 1) { emit_prefix(nodes, x.kids[0], out); return; }
+  out.push_back(x.kind == 1 ? kOpAnd : (x.kind == 2 ? kOpOr : kOpNot));
+  for (int k : x.kids) emit_prefix(nodes, k, out);
+  out.push_back(kOpEnd);
+}
+
+struct ThreadCtx {  // per calling thread: staging + events, created once
+  PinnedBuf pinned;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  int init() {
+    if (ev[0]) return PG_OK;
+    for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+    return PG_OK;
+  }
+};
+thread_local ThreadCtx t_ctx;
 
 int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   if (!plan) return fail(PG_E_INVALID, "null plan");
@@ -498,8 +636,10 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   if (plan->num_aggs > (uint32_t)kMaxAggs) return fail(PG_E_UNSUPPORTED, "more than %d aggregations", kMaxAggs);
   if (plan->num_keys > (uint32_t)kMaxKeys) return fail(PG_E_UNSUPPORTED, "more than %d group-by keys", kMaxKeys);
   if (plan->num_leaves > (uint32_t)kMaxLeaves) return fail(PG_E_UNSUPPORTED, "more than %d filter leaves", kMaxLeaves);
-  if (plan->num_ops > (uint32_t)kMaxOps) return fail(PG_E_UNSUPPORTED, "filter program longer than %d", kMaxOps);
-  // validate program stack depth
+  if (plan->num_segments && !plan->segments) return fail(PG_E_INVALID, "null segment list");
+  if ((plan->num_aggs && !plan->aggs) || (plan->num_keys && !plan->keys) || (plan->num_ops && !plan->ops))
+    return fail(PG_E_INVALID, "null aggregation / key / filter array");
+  // validate the postfix program
   {
     int sp = 0, mx = 0;
     for (uint32_t i = 0; i < plan->num_ops; i++) {
@@ -511,16 +651,18 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
         if (sp < 1) return fail(PG_E_INVALID, "NOT on empty stack");
       } else {
         const int n = (-op) & 0xFF;
-        if (n < 1 || sp < n || !((-op) & 0x300)) return fail(PG_E_INVALID, "bad AND/OR arity at op %u", i);
+        if (n < 1 || sp < n || !((-op) & 0x300) || ((-op) & ~0x3FF)) return fail(PG_E_INVALID, "bad AND/OR at op %u", i);
         sp -= n - 1;
       }
       mx = std::max(mx, sp);
     }
     if (plan->num_ops && sp != 1) return fail(PG_E_INVALID, "filter program leaves %d values", sp);
-    if (mx > kMaxStack) return fail(PG_E_UNSUPPORTED, "filter nesting deeper than %d", kMaxStack);
+    if (mx > 64) return fail(PG_E_UNSUPPORTED, "filter program too deep");
   }
   if (plan->deadline_ms && now_ms() > plan->deadline_ms) return fail(PG_E_TIMEOUT, "deadline passed before launch");
   if (is_cancelled(plan->query_id)) return fail(PG_E_CANCELLED, "query %llu cancelled", (unsigned long long)plan->query_id);
+  int rc = t_ctx.init();
+  if (rc) return rc;
 
   hipStream_t s = plan->stream ? (hipStream_t)plan->stream : thread_stream();
   std::shared_lock<std::shared_mutex> lk(g_seg_mu);
@@ -535,16 +677,15 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
     auto it = g_segs.find(plan->segments[si].seg_key);
     if (it == g_segs.end()) return fail(PG_E_NOTFOUND, "segment %llu not resident", (unsigned long long)plan->segments[si].seg_key);
     segs[si] = it->second;
+    if (L && !plan->segments[si].leaves) return fail(PG_E_INVALID, "segment %u has no leaves", si);
   }
 
   QuerySpec q;
   memset(&q, 0, sizeof(q));
   q.num_segments = S;
   q.num_leaves = L;
-  q.num_ops = plan->num_ops;
   q.num_aggs = A;
   q.num_keys = K;
-  for (uint32_t i = 0; i < plan->num_ops; i++) q.ops[i] = plan->ops[i];
 
   // ---- group key space (mixed radix, first key least significant: DictionaryBasedGroupKeyGenerator:280-322)
   uint64_t G = 1;
@@ -553,6 +694,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   for (uint32_t k = 0; k < K; k++) {
     const pg_key& key = plan->keys[k];
     if (key.cardinality == 0) return fail(PG_E_INVALID, "group key %u has zero cardinality", k);
+    if (key.kind > PG_KEY_KEYMAP) return fail(PG_E_INVALID, "group key %u: unknown kind %u", k, key.kind);
     q.key_kind[k] = key.kind;
     q.key_card[k] = key.cardinality;
     q.key_base[k] = key.base;
@@ -572,10 +714,12 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
         const ColumnRes* c = col(si, plan->keys[k].col_id);
         if (!c || !c->has_dict || c->fwd == FWD_NONE || c->fwd == FWD_MV)
           return fail(c ? PG_E_UNSUPPORTED : PG_E_NOTFOUND, "group key column %u unusable in segment %u", plan->keys[k].col_id, si);
+        if (c->dtype > PG_DOUBLE && plan->keys[k].kind != PG_KEY_KEYMAP)
+          return fail(PG_E_INVALID, "non-numeric key column %u needs a keymap", plan->keys[k].col_id);
         if (plan->keys[k].kind == PG_KEY_KEYMAP && !c->has_keymap) return fail(PG_E_NOTFOUND, "keymap missing for column %u", plan->keys[k].col_id);
         if (plan->keys[k].kind == PG_KEY_VALUE_OFFSET && c->dtype != PG_INT && c->dtype != PG_LONG)
           return fail(PG_E_INVALID, "VALUE_OFFSET key on non-integer column %u", plan->keys[k].col_id);
-        if (plan->keys[k].kind == PG_KEY_VALUE_OFFSET &&
+        if (plan->keys[k].kind == PG_KEY_VALUE_OFFSET && c->card &&
             (c->imin < plan->keys[k].base || (uint64_t)(c->imax - plan->keys[k].base) >= plan->keys[k].cardinality))
           return fail(PG_E_INVALID, "column %u values outside the key range of key %u", plan->keys[k].col_id, k);
         prod = prod > (1ull << 62) / (c->card ? c->card : 1) ? (1ull << 62) : prod * c->card;
@@ -604,7 +748,6 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
     projected.insert(g.col_a);
     const bool two = (g.fn == PG_AGG_SUM || g.fn == PG_AGG_MIN || g.fn == PG_AGG_MAX || g.fn == PG_AGG_AVG) && g.op != PG_EXPR_COL;
     if (two) projected.insert(g.col_b);
-    // validate inputs in every segment, collect value bounds
     double bound_a = 0, bound_b = 0;
     bool all_int = true;
     for (uint32_t si = 0; si < S; si++) {
@@ -618,7 +761,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
         return fail(PG_E_UNSUPPORTED, "aggregation %u: column %u needs an SV forward index + dictionary", a, g.col_a);
       if (g.fn == PG_AGG_DISTINCTCOUNT) {
         if (g.key_kind == PG_KEY_KEYMAP && !ca->has_keymap) return fail(PG_E_NOTFOUND, "DISTINCTCOUNT keymap missing");
-        if (g.key_kind == PG_KEY_VALUE_OFFSET &&
+        if (g.key_kind != PG_KEY_KEYMAP && g.key_kind != PG_KEY_VALUE_OFFSET) return fail(PG_E_INVALID, "bad key kind");
+        if (g.key_kind == PG_KEY_VALUE_OFFSET && ca->card &&
             (ca->dtype > PG_LONG || ca->imin < g.key_base || (uint64_t)(ca->imax - g.key_base) >= g.key_cardinality))
           return fail(PG_E_INVALID, "DISTINCTCOUNT values outside the key range");
         continue;
@@ -671,32 +815,95 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   P.num_segments = S;
   P.aggs.assign(q.aggs, q.aggs + A);
 
-  // ---- per-segment tables + pre-pass work
+  // ---- per (segment, leaf) lowering.  A leaf's dictId set becomes: a contiguous range -> RANGE; a small set
+  // -> LDS hash set (uniform table size per leaf across segments so the LDS layout is fixed); else a global
+  // bitmap over dictIds built on the device (one batched launch).
+  std::vector<uint32_t> set_log2(L, 0);  // per leaf: 0 = no LDS set
+  std::vector<double> leaf_pass(L, 0.0), leaf_cost(L, 0.0);
+  {
+    std::vector<uint32_t> max_ids(L, 0);
+    for (uint32_t si = 0; si < S; si++)
+      for (uint32_t li = 0; li < L; li++) {
+        const pg_leaf& pl = plan->segments[si].leaves[li];
+        if (pl.kind != PG_LEAF_SV_SCAN || pl.num_ids == 0) continue;
+        max_ids[li] = std::max(max_ids[li], pl.num_ids);
+      }
+    uint32_t budget = kLdsSetBytes / 4, used = 0;
+    for (uint32_t li = 0; li < L; li++) {
+      if (!max_ids[li] || max_ids[li] > 4096) continue;
+      uint32_t lg = 1;
+      while ((1u << lg) < 2 * max_ids[li]) lg++;
+      if (used + (1u << lg) > budget) continue;
+      set_log2[li] = lg;
+      used += 1u << lg;
+    }
+    q.set_lds_ints = used;
+  }
+  // pass-fraction / cost estimates (averaged over segments) for the AND / OR child order
+  for (uint32_t si = 0; si < S; si++) {
+    const double w = 1.0 / S;
+    for (uint32_t li = 0; li < L; li++) {
+      const pg_leaf& pl = plan->segments[si].leaves[li];
+      const ColumnRes* c = (pl.kind == PG_LEAF_MATCH_ALL || pl.kind == PG_LEAF_EMPTY) ? nullptr : col(si, pl.col_id);
+      double f = 1.0, cost = 0.0;
+      if (pl.kind == PG_LEAF_EMPTY) f = 0.0;
+      else if (c) {
+        const double card = std::max(1u, c->card);
+        const double nset = pl.num_ids ? pl.num_ids : std::max(0, std::min(pl.hi, (int32_t)c->card) - std::max(pl.lo, 0));
+        f = std::min(1.0, nset / card);
+        if (pl.exclusive) f = 1.0 - f;
+        if (pl.kind == PG_LEAF_SV_SCAN) cost = c->bits / 8.0;
+        if (pl.kind == PG_LEAF_MV_SCAN) cost = 0.0;  // materialised by the pre-pass
+      }
+      leaf_pass[li] += w * f;
+      leaf_cost[li] += w * cost;
+    }
+  }
+  {
+    std::vector<FNode> nodes;
+    int root = -1;
+    build_tree(plan, leaf_pass, leaf_cost, nodes, root);
+    std::vector<int32_t> pre;
+    if (root >= 0) emit_prefix(nodes, root, pre);
+    if (pre.size() > (size_t)kMaxOps) return fail(PG_E_UNSUPPORTED, "filter program longer than %d", kMaxOps);
+    int depth = 0, md = 0;
+    for (int32_t op : pre) {
+      if (op == kOpAnd || op == kOpOr || op == kOpNot) md = std::max(md, ++depth);
+      else if (op == kOpEnd) depth--;
+    }
+    if (md > kMaxDepth) return fail(PG_E_UNSUPPORTED, "filter nesting deeper than %d", kMaxDepth);
+    q.num_ops = (uint32_t)pre.size();
+    for (size_t i = 0; i < pre.size(); i++) q.ops[i] = pre[i];
+  }
+
   Arena ar;
-  std::vector<DevLeaf> leaves((uint64_t)S * L);
-  std::vector<DevCol> aggcols((uint64_t)S * A * 2);
-  std::vector<DevCol> keycols((uint64_t)S * K);
-  std::vector<uint32_t> ndocs(S);
-  std::vector<uint64_t> tile_prefix(S + 1, 0);
+  std::vector<LeafDesc> leaves((uint64_t)S * L);
+  std::vector<ColDesc> aggcols((uint64_t)S * A * 2);
+  std::vector<ColDesc> keycols((uint64_t)S * K);
+  std::vector<SegDesc> segd(S);
+  std::vector<WorkItem> items;
   std::vector<PrepassOp> pre;
+  struct LutReq { uint64_t ids_off; uint32_t n; uint64_t lut_off; };  // arena ids -> scratch LUT
+  std::vector<LutReq> luts;
   uint64_t scratch_bytes = 0;
   auto scratch_reserve = [&](uint64_t n) { uint64_t at = (scratch_bytes + 255) & ~255ull; scratch_bytes = at + n; return at; };
   uint64_t entries_in_filter = 0;
-  // scratch pointers are patched after allocation: remember which leaf fields point into scratch
-  struct Patch { uint64_t leaf_index; uint64_t off; bool lut; };
+  // device pointers into arena / scratch are patched once those are allocated
+  struct Patch { uint64_t leaf_index; uint64_t off; bool in_arena; };
   std::vector<Patch> patches;
 
   for (uint32_t si = 0; si < S; si++) {
     const pg_segment_ref& sr = plan->segments[si];
-    ndocs[si] = sr.num_docs;
-    tile_prefix[si + 1] = tile_prefix[si] + (sr.num_docs + kTileDocs - 1) / kTileDocs;
+    segd[si].num_docs = sr.num_docs;
+    const uint32_t tiles = (uint32_t)(((uint64_t)sr.num_docs + kTileDocs - 1) / kTileDocs);
+    for (uint32_t t = 0; t < tiles; t += kItemTiles) items.push_back({si, t, std::min(tiles, t + (uint32_t)kItemTiles), 0});
     for (uint32_t li = 0; li < L; li++) {
       const pg_leaf& pl = sr.leaves[li];
-      DevLeaf& dl = leaves[(uint64_t)si * L + li];
+      LeafDesc& dl = leaves[(uint64_t)si * L + li];
       memset(&dl, 0, sizeof(dl));
       dl.excl = pl.exclusive ? 1 : 0;
-      if (pl.kind == PG_LEAF_MATCH_ALL) { dl.kind = DL_ALL; continue; }
-      if (pl.kind == PG_LEAF_EMPTY) { dl.kind = DL_NONE; continue; }
+      if (pl.kind == PG_LEAF_MATCH_ALL) { dl.kind = LK_ALL; dl.excl = 0; continue; }
+      if (pl.kind == PG_LEAF_EMPTY) { dl.kind = LK_NONE; dl.excl = 0; continue; }
       const ColumnRes* c = col(si, pl.col_id);
       if (!c) return fail(PG_E_NOTFOUND, "leaf %u: column %u not resident in segment %u", li, pl.col_id, si);
       if (pl.num_ids && !pl.ids) return fail(PG_E_INVALID, "leaf %u: null id list", li);
@@ -710,22 +917,35 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
       switch (pl.kind) {
         case PG_LEAF_SV_SCAN: {
           if (c->fwd != FWD_SV && c->fwd != FWD_SORTED) return fail(PG_E_INVALID, "SV scan on column %u without SV forward index", pl.col_id);
+          if (c->num_docs < sr.num_docs) return fail(PG_E_INVALID, "column %u has %u docs < segment's %u", pl.col_id, c->num_docs, sr.num_docs);
           dl.words = (const uint32_t*)c->words.p;
           dl.bits = c->bits;
           entries_in_filter += sr.num_docs;
-          if (!pl.num_ids) {
-            dl.kind = DL_RANGE;
-            dl.lo = std::max(pl.lo, 0);
-            dl.hi = std::max(std::min(pl.hi, (int32_t)c->card), dl.lo);
+          const bool contiguous = pl.num_ids && (uint32_t)(pl.ids[pl.num_ids - 1] - pl.ids[0]) + 1 == pl.num_ids;
+          if (!pl.num_ids || contiguous) {
+            dl.kind = LK_RANGE;
+            const int32_t lo = pl.num_ids ? pl.ids[0] : pl.lo, hi = pl.num_ids ? pl.ids[pl.num_ids - 1] + 1 : pl.hi;
+            dl.lo = std::max(lo, 0);
+            dl.hi = std::max(std::min(hi, (int32_t)c->card), dl.lo);
+          } else if (set_log2[li]) {
+            dl.kind = LK_SET_LDS;
+            dl.set_log2 = set_log2[li];
+            const uint32_t n = 1u << set_log2[li];
+            std::vector<int32_t> tab(n, -1);
+            for (uint32_t i = 0; i < pl.num_ids; i++) {
+              uint32_t h = set_hash((uint32_t)pl.ids[i], dl.set_log2);
+              while (tab[h] >= 0) h = (h + 1) & (n - 1);
+              tab[h] = pl.ids[i];
+            }
+            uint32_t off = 0;
+            for (uint32_t l2 = 0; l2 < li; l2++) off += set_log2[l2] ? (1u << set_log2[l2]) : 0;
+            dl.lds_off = off;
+            patches.push_back({(uint64_t)si * L + li, ar.put(tab.data(), 4ull * n), true});
           } else {
-            dl.kind = DL_LUT;
-            PrepassOp op{PrepassOp::LUT, si, li};
-            op.in_off = ar.put(pl.ids, 4ull * pl.num_ids);
-            op.n = pl.num_ids;
-            op.out_bytes = 4ull * ((c->card + 31) / 32 + 1);
-            op.out_off = scratch_reserve(op.out_bytes);
-            patches.push_back({(uint64_t)si * L + li, op.out_off, true});
-            pre.push_back(op);
+            dl.kind = LK_SET_LUT;
+            const uint64_t lut_off = scratch_reserve(4ull * ((c->card + 31) / 32 + 1));
+            luts.push_back({ar.put(pl.ids, 4ull * pl.num_ids), pl.num_ids, lut_off});
+            patches.push_back({(uint64_t)si * L + li, lut_off, false});
           }
           break;
         }
@@ -735,7 +955,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
           std::vector<int32_t> rg;
           for (uint32_t id = 0; id < c->card; id++) {
             if (!in_set((int32_t)id)) continue;
-            const int32_t s0 = c->sorted_pairs[2 * id], e0 = c->sorted_pairs[2 * id + 1];
+            const int32_t s0 = c->sorted_pairs[2 * id], e0 = std::min(c->sorted_pairs[2 * id + 1], (int32_t)sr.num_docs - 1);
             if (e0 < s0) continue;
             if (!rg.empty() && rg.back() + 1 >= s0) rg.back() = std::max(rg.back(), e0);
             else { rg.push_back(s0); rg.push_back(e0); }
@@ -749,17 +969,16 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
             }
             if (next < (int32_t)sr.num_docs) { cm.push_back(next); cm.push_back((int32_t)sr.num_docs - 1); }
             rg.swap(cm);
-            dl.excl = 0;
           }
-          if (rg.empty()) { dl.kind = DL_NONE; break; }
-          if (rg.size() == 2) { dl.kind = DL_DOCRANGE; dl.lo = rg[0]; dl.hi = rg[1] + 1; break; }
-          dl.kind = DL_DOCBITMAP;
+          dl.excl = 0;
+          if (rg.empty()) { dl.kind = LK_NONE; break; }
+          if (rg.size() == 2) { dl.kind = LK_DOCRANGE; dl.lo = rg[0]; dl.hi = rg[1] + 1; break; }
+          dl.kind = LK_DOCBITMAP;
           PrepassOp op{PrepassOp::FILL_RANGES, si, li};
           op.in_off = ar.put(rg.data(), 4ull * rg.size());
           op.n = (uint32_t)(rg.size() / 2);
           op.num_docs = sr.num_docs;
-          op.out_bytes = 4ull * ((sr.num_docs + 31) / 32 + 1);
-          op.out_off = scratch_reserve(op.out_bytes);
+          op.out_off = scratch_reserve(4ull * ((sr.num_docs + 31) / 32 + 1));
           patches.push_back({(uint64_t)si * L + li, op.out_off, false});
           pre.push_back(op);
           break;
@@ -775,16 +994,15 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
             for (int32_t id = lo; id < hi; id++)
               for (uint32_t x = c->inv_dir[id]; x < c->inv_dir[id + 1]; x++) sel.push_back(x);
           }
-          dl.kind = DL_DOCBITMAP;
+          dl.kind = LK_DOCBITMAP;
+          dl.excl = 0;
           PrepassOp op{PrepassOp::ROARING, si, li};
           op.in_off = ar.put(sel.data(), 4ull * sel.size());
           op.n = (uint32_t)sel.size();
           op.num_docs = sr.num_docs;
           op.col = c;
           op.negate = pl.exclusive != 0;
-          dl.excl = 0;
-          op.out_bytes = 4ull * ((sr.num_docs + 31) / 32 + 1);
-          op.out_off = scratch_reserve(op.out_bytes);
+          op.out_off = scratch_reserve(4ull * ((sr.num_docs + 31) / 32 + 1));
           patches.push_back({(uint64_t)si * L + li, op.out_off, false});
           pre.push_back(op);
           break;
@@ -792,26 +1010,19 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
         case PG_LEAF_MV_SCAN: {
           if (c->fwd != FWD_MV) return fail(PG_E_INVALID, "MV scan on column %u without MV forward index", pl.col_id);
           entries_in_filter += c->num_values;
-          dl.kind = DL_DOCBITMAP;
+          dl.kind = LK_DOCBITMAP;
+          dl.excl = 0;
           PrepassOp op{PrepassOp::MV_SCAN, si, li};
           op.col = c;
           op.num_docs = sr.num_docs;
           op.excl = pl.exclusive ? 1 : 0;
-          dl.excl = 0;
           op.lo = pl.lo;
           op.hi = pl.hi;
-          op.lut_off = ~0ull;
           if (pl.num_ids) {
-            PrepassOp lop{PrepassOp::LUT, si, li};
-            lop.in_off = ar.put(pl.ids, 4ull * pl.num_ids);
-            lop.n = pl.num_ids;
-            lop.out_bytes = 4ull * ((c->card + 31) / 32 + 1);
-            lop.out_off = scratch_reserve(lop.out_bytes);
-            pre.push_back(lop);
-            op.lut_off = lop.out_off;
+            op.lut_off = scratch_reserve(4ull * ((c->card + 31) / 32 + 1));
+            luts.push_back({ar.put(pl.ids, 4ull * pl.num_ids), pl.num_ids, op.lut_off});
           }
-          op.out_bytes = 4ull * ((sr.num_docs + 31) / 32 + 1);
-          op.out_off = scratch_reserve(op.out_bytes);
+          op.out_off = scratch_reserve(4ull * ((sr.num_docs + 31) / 32 + 1));
           patches.push_back({(uint64_t)si * L + li, op.out_off, false});
           pre.push_back(op);
           break;
@@ -827,80 +1038,94 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
       const int n = (g.op != PG_EXPR_COL && g.fn != PG_AGG_DISTINCTCOUNT && g.fn != PG_AGG_COUNTMV) ? 2 : 1;
       for (int k = 0; k < n; k++) {
         const ColumnRes* c = col(si, cids[k]);
-        DevCol& dc = aggcols[((uint64_t)si * A + a) * 2 + k];
+        if (c->num_docs < sr.num_docs) return fail(PG_E_INVALID, "column %u has %u docs < segment's %u", cids[k], c->num_docs, sr.num_docs);
+        ColDesc& dc = aggcols[((uint64_t)si * A + a) * 2 + k];
         dc.words = (const uint32_t*)c->words.p;
         dc.dict = c->dict.p;
         dc.keymap = (const int32_t*)c->keymap.p;
         dc.mv_offsets = (const uint32_t*)c->mv_offsets.p;
         dc.bits = c->bits;
         dc.dtype = c->dtype;
+        dc.card = c->card;
       }
     }
     for (uint32_t k = 0; k < K; k++) {
       const ColumnRes* c = col(si, plan->keys[k].col_id);
-      DevCol& dc = keycols[(uint64_t)si * K + k];
+      if (c->num_docs < sr.num_docs) return fail(PG_E_INVALID, "key column %u has fewer docs than the segment", plan->keys[k].col_id);
+      ColDesc& dc = keycols[(uint64_t)si * K + k];
       dc.words = (const uint32_t*)c->words.p;
       dc.dict = c->dict.p;
       dc.keymap = (const int32_t*)c->keymap.p;
       dc.bits = c->bits;
       dc.dtype = c->dtype;
+      dc.card = c->card;
     }
   }
   P.entries_in_filter = entries_in_filter;
-  q.total_tiles = tile_prefix[S];
+  q.num_items = (uint32_t)items.size();
 
-  // ---- device allocations (state + arena + scratch)
-  int rc;
-  if ((rc = P.i64.alloc_async(G * 8ull * n_i64, s))) return rc;
-  if (n_f64 && (rc = P.f64.alloc_async(G * 8ull * n_f64, s))) return rc;
-  if (n_min && (rc = P.mn.alloc_async(G * 8ull * n_min, s))) return rc;
-  if (n_max && (rc = P.mx.alloc_async(G * 8ull * n_max, s))) return rc;
-  if (flag_bytes && (rc = P.flags.alloc_async(G * flag_bytes, s))) return rc;
-  if ((rc = P.seg_matched.alloc_async(8ull * (S ? S : 1), s))) return rc;
+  // ---- device buffers (state + arena + scratch) from the caching pool
+  if ((rc = P.i64.alloc_pooled(G * 8ull * n_i64))) return rc;
+  if (n_f64 && (rc = P.f64.alloc_pooled(G * 8ull * n_f64))) return rc;
+  if (n_min && (rc = P.mn.alloc_pooled(G * 8ull * n_min))) return rc;
+  if (n_max && (rc = P.mx.alloc_pooled(G * 8ull * n_max))) return rc;
+  if (flag_bytes && (rc = P.flags.alloc_pooled(G * flag_bytes))) return rc;
+  if ((rc = P.seg_matched.alloc_pooled(8ull * (S ? S : 1) + 16))) return rc;
   q.i64 = (unsigned long long*)P.i64.p;
   q.f64 = (double*)P.f64.p;
   q.mn = (long long*)P.mn.p;
   q.mx = (long long*)P.mx.p;
   q.flags = (uint8_t*)P.flags.p;
   q.seg_matched = (unsigned long long*)P.seg_matched.p;
+  q.err = (unsigned int*)(q.seg_matched + (S ? S : 1));
 
-  const uint64_t off_leaves = ar.reserve(leaves.size() * sizeof(DevLeaf));
-  const uint64_t off_aggcols = ar.reserve(aggcols.size() * sizeof(DevCol));
-  const uint64_t off_keycols = ar.reserve(keycols.size() * sizeof(DevCol));
-  const uint64_t off_ndocs = ar.put(ndocs.data(), 4ull * S);
-  const uint64_t off_tiles = ar.put(tile_prefix.data(), 8ull * (S + 1));
+  const uint64_t off_leaves = ar.reserve(leaves.size() * sizeof(LeafDesc));
+  const uint64_t off_aggcols = ar.reserve(aggcols.size() * sizeof(ColDesc));
+  const uint64_t off_keycols = ar.reserve(keycols.size() * sizeof(ColDesc));
+  const uint64_t off_segs = ar.reserve(segd.size() * sizeof(SegDesc));
+  const uint64_t off_items = ar.put(items.data(), items.size() * sizeof(WorkItem));
+  const uint64_t off_lutjobs = ar.reserve(luts.size() * sizeof(LutJob));
   DevBuf arena, scratch;
-  if ((rc = arena.alloc_async(ar.h.size() + 16, s))) return rc;
-  if (scratch_bytes && (rc = scratch.alloc_async(scratch_bytes, s))) return rc;
+  // declared after the buffers it protects: on any exit, wait for queued work before they return to the pool
+  struct SyncOnExit {
+    hipStream_t s;
+    ~SyncOnExit() { (void)hipStreamSynchronize(s); }
+  } sync_on_exit{s};
+  if ((rc = arena.alloc_pooled(ar.h.size() + 16))) return rc;
+  if (scratch_bytes && (rc = scratch.alloc_pooled(scratch_bytes))) return rc;
   uint8_t* dA = (uint8_t*)arena.p;
   uint8_t* dS = (uint8_t*)scratch.p;
   for (const Patch& p : patches) {
-    DevLeaf& dl = leaves[p.leaf_index];
-    if (p.lut) dl.lut = (const uint32_t*)(dS + p.off);
-    else dl.words = (const uint32_t*)(dS + p.off);
+    LeafDesc& dl = leaves[p.leaf_index];
+    dl.aux = (const uint32_t*)((p.in_arena ? dA : dS) + p.off);
   }
-  memcpy(&ar.h[off_leaves], leaves.data(), leaves.size() * sizeof(DevLeaf));
-  memcpy(&ar.h[off_aggcols], aggcols.data(), aggcols.size() * sizeof(DevCol));
-  memcpy(&ar.h[off_keycols], keycols.data(), keycols.size() * sizeof(DevCol));
-  q.leaves = (const DevLeaf*)(dA + off_leaves);
-  q.aggcols = (const DevCol*)(dA + off_aggcols);
-  q.keycols = (const DevCol*)(dA + off_keycols);
-  q.num_docs = (const uint32_t*)(dA + off_ndocs);
-  q.tile_prefix = (const uint64_t*)(dA + off_tiles);
+  for (uint32_t si = 0; si < S; si++) {
+    segd[si].leaves = (const LeafDesc*)(dA + off_leaves) + (uint64_t)si * L;
+    segd[si].aggcols = (const ColDesc*)(dA + off_aggcols) + (uint64_t)si * A * 2;
+    segd[si].keycols = (const ColDesc*)(dA + off_keycols) + (uint64_t)si * K;
+  }
+  std::vector<LutJob> lutjobs(luts.size());
+  for (size_t i = 0; i < luts.size(); i++)
+    lutjobs[i] = {(const int32_t*)(dA + luts[i].ids_off), (uint32_t*)(dS + luts[i].lut_off), luts[i].n, 0};
+  if (!leaves.empty()) memcpy(&ar.h[off_leaves], leaves.data(), leaves.size() * sizeof(LeafDesc));
+  if (!aggcols.empty()) memcpy(&ar.h[off_aggcols], aggcols.data(), aggcols.size() * sizeof(ColDesc));
+  if (!keycols.empty()) memcpy(&ar.h[off_keycols], keycols.data(), keycols.size() * sizeof(ColDesc));
+  if (!segd.empty()) memcpy(&ar.h[off_segs], segd.data(), segd.size() * sizeof(SegDesc));
+  if (!lutjobs.empty()) memcpy(&ar.h[off_lutjobs], lutjobs.data(), lutjobs.size() * sizeof(LutJob));
+  q.segs = (const SegDesc*)(dA + off_segs);
+  q.items = (const WorkItem*)(dA + off_items);
 
-  hipEvent_t ev[4];
-  for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
-  struct EvGuard { hipEvent_t* e; ~EvGuard() { for (int i = 0; i < 4; i++) hipEventDestroy(e[i]); } } eg{ev};
-
-  HIP_CHECK(hipMemcpyAsync(arena.p, ar.h.data(), ar.h.size(), hipMemcpyHostToDevice, s));
+  void* staging = t_ctx.pinned.get(ar.h.size());
+  if (!staging) return fail(PG_E_NOMEM, "pinned staging of %zu bytes failed", ar.h.size());
+  memcpy(staging, ar.h.data(), ar.h.size());
+  hipEvent_t* ev = t_ctx.ev;
+  HIP_CHECK(hipMemcpyAsync(arena.p, staging, ar.h.size(), hipMemcpyHostToDevice, s));
   HIP_CHECK(launch_init_state(q, s));
   HIP_CHECK(hipEventRecord(ev[0], s));
   if (scratch_bytes) HIP_CHECK(hipMemsetAsync(scratch.p, 0, scratch_bytes, s));
+  HIP_CHECK(launch_set_lut_bits((const LutJob*)(dA + off_lutjobs), (uint32_t)lutjobs.size(), s));
   for (const PrepassOp& op : pre) {
     switch (op.kind) {
-      case PrepassOp::LUT:
-        HIP_CHECK(launch_set_lut_bits((const int32_t*)(dA + op.in_off), op.n, (uint32_t*)(dS + op.out_off), s));
-        break;
       case PrepassOp::FILL_RANGES:
         HIP_CHECK(launch_fill_ranges((const int32_t*)(dA + op.in_off), op.n, op.num_docs, (uint32_t*)(dS + op.out_off), s));
         break;
@@ -918,21 +1143,22 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
     }
   }
   HIP_CHECK(hipEventRecord(ev[1], s));
-  if (is_cancelled(plan->query_id)) return fail(PG_E_CANCELLED, "query %llu cancelled", (unsigned long long)plan->query_id);
-  if (plan->deadline_ms && now_ms() > plan->deadline_ms) return fail(PG_E_TIMEOUT, "deadline passed");
+  if (is_cancelled(plan->query_id)) { (void)hipStreamSynchronize(s); return fail(PG_E_CANCELLED, "query %llu cancelled", (unsigned long long)plan->query_id); }
+  if (plan->deadline_ms && now_ms() > plan->deadline_ms) { (void)hipStreamSynchronize(s); return fail(PG_E_TIMEOUT, "deadline passed"); }
   uint32_t blocks = 0;
-  if (q.total_tiles) {
-    int dev_cus = 256;
-    hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g_device);
-    const uint64_t cap = (uint64_t)dev_cus * 8;
-    blocks = (uint32_t)std::min<uint64_t>(q.total_tiles, cap);
+  if (q.num_items) {
+    static int dev_cus = 0;
+    if (!dev_cus && hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g_device) != hipSuccess) dev_cus = 256;
+    static int per_cu = 0;
+    if (!per_cu) { const char* e = getenv("PG_SCAN_BLOCKS_PER_CU"); per_cu = e ? std::max(1, atoi(e)) : 8; }
+    blocks = (uint32_t)std::min<uint64_t>(q.num_items, (uint64_t)dev_cus * per_cu);
     HIP_CHECK(launch_scan(q, blocks, s));
   }
   HIP_CHECK(hipEventRecord(ev[2], s));
   HIP_CHECK(hipStreamSynchronize(s));
   float pre_ms = 0, scan_ms = 0;
-  hipEventElapsedTime(&pre_ms, ev[0], ev[1]);
-  hipEventElapsedTime(&scan_ms, ev[1], ev[2]);
+  (void)hipEventElapsedTime(&pre_ms, ev[0], ev[1]);
+  (void)hipEventElapsedTime(&scan_ms, ev[1], ev[2]);
   t_timing.prepass_ms = pre_ms;
   t_timing.scan_ms = scan_ms;
   t_timing.scan_launches = blocks ? 1 : 0;
@@ -940,10 +1166,12 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   stats.num_total_docs = total_docs;
   stats.num_segments_processed = S;
   stats.num_entries_scanned_in_filter = entries_in_filter;
-  if (S) {
-    std::vector<uint64_t> sm(S);
-    HIP_CHECK(hipMemcpy(sm.data(), P.seg_matched.p, 8ull * S, hipMemcpyDeviceToHost));
-    for (uint64_t v : sm) { stats.num_docs_scanned += v; stats.num_segments_matched += v > 0; }
+  {
+    std::vector<uint64_t> sm((S ? S : 1) + 2);
+    HIP_CHECK(hipMemcpy(sm.data(), P.seg_matched.p, 8ull * sm.size(), hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < S; i++) { stats.num_docs_scanned += sm[i]; stats.num_segments_matched += sm[i] > 0; }
+    const uint32_t err = (uint32_t)sm[S ? S : 1];
+    if (err) return fail(PG_E_INVALID, "device bounds check failed (code %u): a key fell outside the plan's key space", err);
   }
   stats.num_entries_scanned_post_filter = stats.num_docs_scanned * P.projected_cols;
   return PG_OK;
@@ -960,9 +1188,9 @@ int finalize(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   const uint64_t G = pp->num_slots;
   const uint32_t A = plan->num_aggs, K = plan->num_keys;
   if (A != P.aggs.size()) return fail(PG_E_INVALID, "plan does not match partials");
-  hipEvent_t e0, e1;
-  HIP_CHECK(hipEventCreate(&e0));
-  HIP_CHECK(hipEventCreate(&e1));
+  int rc = t_ctx.init();
+  if (rc) return rc;
+  hipEvent_t e0 = t_ctx.ev[3], e1 = t_ctx.ev[2];
   hipStream_t s = thread_stream();
   HIP_CHECK(hipEventRecord(e0, s));
   std::vector<int64_t> hi64(G * pp->n_i64), hmn(G * pp->n_min), hmx(G * pp->n_max);
@@ -976,9 +1204,7 @@ int finalize(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   HIP_CHECK(hipEventRecord(e1, s));
   HIP_CHECK(hipStreamSynchronize(s));
   float fm = 0;
-  hipEventElapsedTime(&fm, e0, e1);
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
+  (void)hipEventElapsedTime(&fm, e0, e1);
   t_timing.finalize_ms = fm;
 
   pg_result* r = (pg_result*)calloc(1, sizeof(pg_result));

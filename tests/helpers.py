@@ -22,7 +22,7 @@ def inner_query(case, filt):
 def check_inner_values(res, case):
     """QueriesTestUtils.testInnerSegmentAggregation(GroupBy)Result: longValue() of each result, AvgPair sum/count."""
     key = tuple(case.get("key", ()))
-    assert key in res.rows, f"group key {key} missing"
+    assert key in res.rows, f"group key {key} missing; {len(res.rows)} groups, e.g. {sorted(res.rows.items())[:3]}"
     row = res.rows[key]
     exp = case["values"]
     for a, (ag, v, e) in enumerate(zip(res.aggregations, row, exp)):
