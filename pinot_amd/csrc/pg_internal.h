@@ -24,9 +24,9 @@
 namespace pg {
 
 constexpr int kBlock = 256;                          // 4 waves of 64
-constexpr int kRows = 16;                            // docs of a thread in a tile: base + j*256 + tid
-constexpr int kTileDocs = kBlock * kRows;            // 4096 docs per tile
-constexpr int kItemTiles = 8;                        // tiles per work item (32 768 docs), within one segment
+constexpr int kRows = 8;                             // docs of a thread in a tile: base + j*256 + tid
+constexpr int kTileDocs = kBlock * kRows;            // 2048 docs per tile
+constexpr int kItemTiles = 16;                       // tiles per work item (32 768 docs), within one segment
 constexpr int kMaxAggs = 8;
 constexpr int kMaxKeys = 4;
 constexpr int kMaxLeaves = 24;
@@ -58,7 +58,7 @@ struct LeafDesc {
   uint32_t bits;
   uint32_t set_log2;      // SET_LDS: table has 1 << set_log2 int32 slots (empty = -1)
   uint32_t lds_off;       // SET_LDS: int32 offset of the table in the block's LDS set region
-  uint32_t pad;
+  uint32_t wbytes;        // bytes of `words` (buffer-descriptor range)
 };
 
 // A column as read by aggregation inputs and group keys.
@@ -70,7 +70,7 @@ struct ColDesc {
   uint32_t bits;
   uint32_t dtype;             // pg_data_type
   uint32_t card;
-  uint32_t pad;
+  uint32_t wbytes;            // bytes of `words` (buffer-descriptor range)
 };
 
 struct SegDesc {

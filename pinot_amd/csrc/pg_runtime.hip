@@ -831,9 +831,10 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
     uint32_t budget = kLdsSetBytes / 4, used = 0;
     for (uint32_t li = 0; li < L; li++) {
       if (!max_ids[li] || max_ids[li] > 4096) continue;
-      uint32_t lg = 1;
-      while ((1u << lg) < 2 * max_ids[li]) lg++;
-      if (used + (1u << lg) > budget) continue;
+      uint32_t lg = 1;  // load factor <= 1/4 when it fits (expected ~1.4 probes per miss), else <= 1/2
+      while ((1u << lg) < 4 * max_ids[li]) lg++;
+      if (used + (1u << lg) > budget) lg--;
+      if ((1u << lg) < 2 * max_ids[li] || used + (1u << lg) > budget) continue;
       set_log2[li] = lg;
       used += 1u << lg;
     }
@@ -919,6 +920,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
           if (c->fwd != FWD_SV && c->fwd != FWD_SORTED) return fail(PG_E_INVALID, "SV scan on column %u without SV forward index", pl.col_id);
           if (c->num_docs < sr.num_docs) return fail(PG_E_INVALID, "column %u has %u docs < segment's %u", pl.col_id, c->num_docs, sr.num_docs);
           dl.words = (const uint32_t*)c->words.p;
+          dl.wbytes = (uint32_t)std::min<uint64_t>(c->words.bytes, 0xFFFFFFF0ull);
           dl.bits = c->bits;
           entries_in_filter += sr.num_docs;
           const bool contiguous = pl.num_ids && (uint32_t)(pl.ids[pl.num_ids - 1] - pl.ids[0]) + 1 == pl.num_ids;
@@ -1041,6 +1043,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
         if (c->num_docs < sr.num_docs) return fail(PG_E_INVALID, "column %u has %u docs < segment's %u", cids[k], c->num_docs, sr.num_docs);
         ColDesc& dc = aggcols[((uint64_t)si * A + a) * 2 + k];
         dc.words = (const uint32_t*)c->words.p;
+        dc.wbytes = (uint32_t)std::min<uint64_t>(c->words.bytes, 0xFFFFFFF0ull);
         dc.dict = c->dict.p;
         dc.keymap = (const int32_t*)c->keymap.p;
         dc.mv_offsets = (const uint32_t*)c->mv_offsets.p;
@@ -1054,6 +1057,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
       if (c->num_docs < sr.num_docs) return fail(PG_E_INVALID, "key column %u has fewer docs than the segment", plan->keys[k].col_id);
       ColDesc& dc = keycols[(uint64_t)si * K + k];
       dc.words = (const uint32_t*)c->words.p;
+      dc.wbytes = (uint32_t)std::min<uint64_t>(c->words.bytes, 0xFFFFFFF0ull);
       dc.dict = c->dict.p;
       dc.keymap = (const int32_t*)c->keymap.p;
       dc.bits = c->bits;

@@ -11,25 +11,43 @@
 //      matching docs only (projection)
 //   -> Sum/Count/Min/Max/Avg/DistinctCount/CountMV aggregate / aggregateGroupBySV
 //   -> DictionaryBasedGroupKeyGenerator mixed-radix keys (groupby/DictionaryBasedGroupKeyGenerator.java:280-322)
-// with no intermediate doc-id lists.  Thread t of a block owns docs base + j*256 + t (j < 16), so for each j the
-// 64 lanes of a wave read 64 consecutive packed values (one contiguous run of 8*b bytes).  Every leaf and every
-// aggregation input is read only for the docs still needed (exec-masked loads), so a selective first leaf turns
-// the remaining columns into cache-line gathers: the HBM bytes actually moved are those of the most selective
-// leaf's column plus the lines that hold surviving docs.  Nothing here is a dense contraction: no MFMA; the
-// roofline is HBM bandwidth.
+// with no intermediate doc-id lists.  Thread t of a block owns docs base + j*256 + t (j < 8), so for each j the
+// 64 lanes of a wave read 64 consecutive packed values (one contiguous run of 8*b bytes).
+//
+// Memory-level parallelism: every gather of packed values is straight-line code -- docs a phase does not need
+// read the tile's first doc instead (one cache line for the whole wave) -- so all 2 x 8 window loads of a leaf
+// are in flight before the first is consumed.  Leaves after the first of an AND only need the docs that
+// survived, so after a selective first leaf the other columns move as a few cache lines, not as streams.
+// Packed columns are read through buffer descriptors: 32-bit offsets, and the hardware range check turns any
+// read past the column into 0 instead of a fault.  Nothing here is a dense contraction: no MFMA; the roofline
+// is HBM bandwidth.
 #include <hip/hip_runtime.h>
 
 #include "pg_internal.h"
 
 namespace pg {
+constexpr uint32_t kRowMask = (1u << kRows) - 1u;
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+// Buffer descriptor of a packed column; built from readfirstlane'd (wave-uniform) values so it lives in SGPRs.
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
 
 // FixedBitIntReader.readUnchecked on the native-word image: value `idx` of `b` (1..32) bits.
-__device__ __forceinline__ uint32_t unpack(const uint32_t* __restrict__ w, uint32_t idx, uint32_t b) {
+__device__ __forceinline__ uint32_t unpack(rsrc_t r, uint32_t idx, uint32_t b) {
   const uint64_t p = (uint64_t)idx * b;
-  const uint64_t wi = p >> 5;
-  const uint32_t off = (uint32_t)p & 31u;
-  const uint64_t win = ((uint64_t)w[wi] << 32) | (uint64_t)w[wi + 1];
-  return (uint32_t)(win >> (64u - off - b)) & (0xFFFFFFFFu >> (32u - b));
+  const uint32_t off = (uint32_t)(p >> 5) << 2;
+  const uint32_t sh = (uint32_t)p & 31u;
+  const uint32_t w0 = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+  const uint32_t w1 = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4u, 0, 0);
+  const uint64_t win = ((uint64_t)w0 << 32) | (uint64_t)w1;
+  return (uint32_t)(win >> (64u - sh - b)) & (0xFFFFFFFFu >> (32u - b));
 }
 
 // Dictionary reads clamp the dictId to the dictionary: valid data never needs it, and a corrupt forward index
@@ -49,13 +67,13 @@ __device__ __forceinline__ int64_t dict_i64(const ColDesc& c, uint32_t id) {
   return c.dtype == PG_INT ? (int64_t)((const int32_t*)c.dict)[id] : ((const int64_t*)c.dict)[id];
 }
 
-// TransformFunction value of an aggregation input (double path).
+// TransformFunction value of an aggregation input from its (already unpacked) dictIds.
 // MultiplicationTransformFunction.transformToDoubleValuesSV (transform/function/MultiplicationTransformFunction.java:91-111):
 // start from the literal product 1.0, multiply arguments in order; compiled with -ffp-contract=off.
-__device__ __forceinline__ double agg_value_f64(const AggSpec& a, const ColDesc* c, uint32_t d) {
-  const double va = dict_double(c[0], unpack(c[0].words, d, c[0].bits));
+__device__ __forceinline__ double value_f64(const AggSpec& a, const ColDesc* c, uint32_t ia, uint32_t ib) {
+  const double va = dict_double(c[0], ia);
   if (a.op == PG_EXPR_COL) return va;
-  const double vb = dict_double(c[1], unpack(c[1].words, d, c[1].bits));
+  const double vb = dict_double(c[1], ib);
   switch (a.op) {
     case PG_EXPR_MUL: return (1.0 * va) * vb;
     case PG_EXPR_ADD: return va + vb;
@@ -64,10 +82,10 @@ __device__ __forceinline__ double agg_value_f64(const AggSpec& a, const ColDesc*
 }
 
 // integer-exact path (host proved |partial sums| < 2^62): identical to the double path while < 2^53
-__device__ __forceinline__ int64_t agg_value_i64(const AggSpec& a, const ColDesc* c, uint32_t d) {
-  const int64_t va = dict_i64(c[0], unpack(c[0].words, d, c[0].bits));
+__device__ __forceinline__ int64_t value_i64(const AggSpec& a, const ColDesc* c, uint32_t ia, uint32_t ib) {
+  const int64_t va = dict_i64(c[0], ia);
   if (a.op == PG_EXPR_COL) return va;
-  const int64_t vb = dict_i64(c[1], unpack(c[1].words, d, c[1].bits));
+  const int64_t vb = dict_i64(c[1], ib);
   switch (a.op) {
     case PG_EXPR_MUL: return va * vb;
     case PG_EXPR_ADD: return va + vb;
@@ -75,17 +93,26 @@ __device__ __forceinline__ int64_t agg_value_i64(const AggSpec& a, const ColDesc
   }
 }
 
-__device__ __forceinline__ uint64_t col_key(uint32_t kind, int64_t base, const ColDesc& c, uint32_t d) {
-  const uint32_t id = unpack(c.words, d, c.bits);
-  if (id >= c.card) return ~0ull;  // corrupt input: rejected by the caller's range check
+// table-global key id of dictId `id` (~0 when the id is outside the dictionary: rejected by the caller)
+__device__ __forceinline__ uint64_t key_of(uint32_t kind, int64_t base, const ColDesc& c, uint32_t id) {
+  if (id >= c.card) return ~0ull;
   return kind == PG_KEY_KEYMAP ? (uint64_t)(uint32_t)c.keymap[id] : (uint64_t)(dict_i64(c, id) - base);
 }
 
-// IN-list membership in an LDS open-addressing table (<= 50 % full, empty = -1).
-__device__ __forceinline__ bool set_contains(const int32_t* tab, uint32_t log2, uint32_t id) {
+__device__ __forceinline__ uint32_t agg_ncols(const AggSpec& A) {
+  if (A.fn == PG_AGG_COUNT || A.fn == PG_AGG_COUNTMV) return 0;
+  if (A.fn == PG_AGG_DISTINCTCOUNT) return 1;
+  return A.op == PG_EXPR_COL ? 1u : 2u;
+}
+
+// IN-list membership in an LDS open-addressing table (<= 50 % full, empty = -1), given the home-slot entry `t0`
+// already read (the batched first probe).
+__device__ __forceinline__ bool set_resolve(const int32_t* tab, uint32_t log2, uint32_t id, int32_t t0) {
+  if (t0 == (int32_t)id) return true;
+  if (t0 < 0) return false;
   const uint32_t mask = (1u << log2) - 1u;
-  uint32_t h = set_hash(id, log2);
-  for (uint32_t probe = 0; probe <= mask; probe++) {
+  uint32_t h = (set_hash(id, log2) + 1) & mask;
+  for (uint32_t probe = 1; probe <= mask; probe++) {
     const int32_t v = tab[h];
     if (v == (int32_t)id) return true;
     if (v < 0) return false;
@@ -94,54 +121,71 @@ __device__ __forceinline__ bool set_contains(const int32_t* tab, uint32_t log2, 
   return false;
 }
 
-// One leaf over the thread's 16 docs, evaluated only for the docs in `need` -> 16-bit mask
+// Gather the dictIds of rows [0, N) of `need` starting at `base` (row r = doc base + r*256 + tid); rows outside
+// `need` read the doc `base` instead, keeping the loads straight-line.
+template <int N>
+__device__ __forceinline__ void gather_ids(rsrc_t r, uint32_t bits, uint32_t need, uint32_t base, int tid,
+                                           uint32_t (&v)[N]) {
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    const uint32_t d = ((need >> j) & 1u) ? base + (uint32_t)(j * kBlock + tid) : base;
+    v[j] = unpack(r, d, bits);
+  }
+}
+
+// One leaf over the thread's 8 docs, evaluated only for the docs in `need` -> 16-bit mask
 // (bit j <-> doc base + j*256 + tid).  Bits outside `need` are don't-care.
 __device__ __forceinline__ uint32_t eval_leaf(const LeafDesc& L, const int32_t* lds_sets, uint32_t need,
                                               uint32_t base, int tid) {
   uint32_t m = 0;
   switch (L.kind) {
-    case LK_ALL: m = 0xFFFFu; break;
+    case LK_ALL: m = kRowMask; break;
     case LK_NONE: break;
     case LK_RANGE: {
+      const rsrc_t r = make_rsrc(L.words, L.wbytes);
+      uint32_t v[kRows];
+      gather_ids<kRows>(r, L.bits, need, base, tid, v);
       const uint32_t lo = (uint32_t)L.lo, span = (uint32_t)(L.hi - L.lo);
 #pragma unroll
-      for (int j = 0; j < kRows; j++) {
-        if ((need >> j) & 1u) {
-          const uint32_t v = unpack(L.words, base + (uint32_t)(j * kBlock + tid), L.bits);
-          m |= (uint32_t)((v - lo) < span) << j;
-        }
-      }
+      for (int j = 0; j < kRows; j++) m |= (uint32_t)((v[j] - lo) < span) << j;
       break;
     }
     case LK_SET_LDS: {
+      const rsrc_t r = make_rsrc(L.words, L.wbytes);
+      uint32_t v[kRows];
+      gather_ids<kRows>(r, L.bits, need, base, tid, v);
       const int32_t* tab = lds_sets + L.lds_off;
+      int32_t t0[kRows];
+#pragma unroll
+      for (int j = 0; j < kRows; j++) t0[j] = tab[set_hash(v[j], L.set_log2)];
 #pragma unroll
       for (int j = 0; j < kRows; j++) {
-        if ((need >> j) & 1u) {
-          const uint32_t v = unpack(L.words, base + (uint32_t)(j * kBlock + tid), L.bits);
-          m |= (uint32_t)set_contains(tab, L.set_log2, v) << j;
-        }
+        const bool hit = t0[j] == (int32_t)v[j];
+        const bool decided = hit || t0[j] < 0;
+        m |= (uint32_t)(decided ? hit : set_resolve(tab, L.set_log2, v[j], t0[j])) << j;
       }
       break;
     }
     case LK_SET_LUT: {
+      const rsrc_t r = make_rsrc(L.words, L.wbytes);
+      uint32_t v[kRows];
+      gather_ids<kRows>(r, L.bits, need, base, tid, v);
+      uint32_t lw[kRows];
 #pragma unroll
-      for (int j = 0; j < kRows; j++) {
-        if ((need >> j) & 1u) {
-          const uint32_t v = unpack(L.words, base + (uint32_t)(j * kBlock + tid), L.bits);
-          m |= ((L.aux[v >> 5] >> (v & 31u)) & 1u) << j;
-        }
-      }
+      for (int j = 0; j < kRows; j++) lw[j] = L.aux[v[j] >> 5];
+#pragma unroll
+      for (int j = 0; j < kRows; j++) m |= ((lw[j] >> (v[j] & 31u)) & 1u) << j;
       break;
     }
     case LK_DOCBITMAP: {
+      uint32_t bw[kRows];
 #pragma unroll
       for (int j = 0; j < kRows; j++) {
-        if ((need >> j) & 1u) {
-          const uint32_t d = base + (uint32_t)(j * kBlock + tid);
-          m |= ((L.aux[d >> 5] >> (d & 31u)) & 1u) << j;
-        }
+        const uint32_t d = ((need >> j) & 1u) ? base + (uint32_t)(j * kBlock + tid) : base;
+        bw[j] = L.aux[d >> 5] >> (d & 31u);
       }
+#pragma unroll
+      for (int j = 0; j < kRows; j++) m |= (bw[j] & 1u) << j;
       break;
     }
     default: {  // LK_DOCRANGE
@@ -153,10 +197,10 @@ __device__ __forceinline__ uint32_t eval_leaf(const LeafDesc& L, const int32_t* 
       break;
     }
   }
-  return L.excl ? (~m & 0xFFFFu) : m;
+  return L.excl ? (~m & kRowMask) : m;
 }
 
-// Filter tree (prefix form) over 16-bit masks with short-circuit needs: an AND child only sees docs every
+// Filter tree (prefix form) over 8-bit masks with short-circuit needs: an AND child only sees docs every
 // earlier child accepted, an OR child only docs no earlier child accepted.  The group stack (<= 8 open groups)
 // lives in registers: 16-bit acc / need fields packed into 64-bit words, 2-bit types in one word.
 enum GroupType : uint32_t { GT_ROOT = 0, GT_AND = 1, GT_OR = 2, GT_NOT = 3 };
@@ -177,10 +221,10 @@ __device__ __forceinline__ uint32_t eval_filter(const QuerySpec& q, const LeafDe
         r = gtype == GT_NOT ? (~gacc & gneed) : gacc;
         gtype = stype & 3u;
         stype >>= 2;
-        gacc = (uint32_t)(sacc0 & 0xFFFFu);
+        gacc = (uint32_t)(sacc0 & kRowMask);
         sacc0 = (sacc0 >> 16) | (sacc1 << 48);
         sacc1 >>= 16;
-        gneed = (uint32_t)(sneed0 & 0xFFFFu);
+        gneed = (uint32_t)(sneed0 & kRowMask);
         sneed0 = (sneed0 >> 16) | (sneed1 << 48);
         sneed1 >>= 16;
       }
@@ -198,7 +242,7 @@ __device__ __forceinline__ uint32_t eval_filter(const QuerySpec& q, const LeafDe
       sneed0 = (sneed0 << 16) | gneed;
       gneed = need;
       gtype = op == kOpAnd ? GT_AND : (op == kOpOr ? GT_OR : GT_NOT);
-      gacc = gtype == GT_AND ? 0xFFFFu : 0u;
+      gacc = gtype == GT_AND ? kRowMask : 0u;
     }
   }
   return gacc & valid;
@@ -225,35 +269,213 @@ __device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
   return v;
 }
 
+// Group-state pointers: the block's LDS copy when the table is privatised, else the global arrays.
+struct GroupState {
+  unsigned long long* i64;
+  double* f64;
+  long long* mn;
+  long long* mx;
+};
+
+// Per-doc update of one aggregation in group slot g (aggregateGroupBySV of each function).
+__device__ __forceinline__ void group_update(const QuerySpec& q, const GroupState& S, const AggSpec& A,
+                                             const ColDesc* c, uint64_t g, uint32_t d, uint32_t ia, uint32_t ib) {
+  switch (A.fn) {
+    case PG_AGG_COUNT: break;  // = slot 0
+    case PG_AGG_COUNTMV:
+      atomicAdd(&S.i64[g * q.n_i64 + A.slot], (unsigned long long)(c[0].mv_offsets[d + 1] - c[0].mv_offsets[d]));
+      break;
+    case PG_AGG_SUM:
+    case PG_AGG_AVG:  // AVG count == slot 0
+      if (A.integer) atomicAdd(&S.i64[g * q.n_i64 + A.slot], (unsigned long long)value_i64(A, c, ia, ib));
+      else atomicAdd(&S.f64[g * q.n_f64 + A.slot], value_f64(A, c, ia, ib));
+      break;
+    case PG_AGG_MIN: atomicMin(&S.mn[g * q.n_min + A.slot], (long long)order_key(value_f64(A, c, ia, ib))); break;
+    case PG_AGG_MAX: atomicMax(&S.mx[g * q.n_max + A.slot], (long long)order_key(value_f64(A, c, ia, ib))); break;
+    case PG_AGG_DISTINCTCOUNT: {
+      const uint64_t key = key_of(A.key_kind, A.key_base, c[0], ia);
+      if (key < A.key_card) q.flags[g * q.flag_bytes_per_slot + A.flag_off + key] = 1;
+      else atomicOr(q.err, 2u);
+      break;
+    }
+  }
+}
+
+// Per-doc update of one aggregation-only accumulator (aggregate() of each function; COUNT = doc count).
+__device__ __forceinline__ void acc_update(const QuerySpec& q, const AggSpec& A, const ColDesc* c, uint64_t& acc,
+                                           uint32_t d, uint32_t ia, uint32_t ib) {
+  switch (A.fn) {
+    case PG_AGG_COUNT: break;
+    case PG_AGG_COUNTMV: acc += c[0].mv_offsets[d + 1] - c[0].mv_offsets[d]; break;
+    case PG_AGG_SUM:
+    case PG_AGG_AVG:
+      if (A.integer) acc += (uint64_t)value_i64(A, c, ia, ib);
+      else acc = __double_as_longlong(__longlong_as_double(acc) + value_f64(A, c, ia, ib));
+      break;
+    case PG_AGG_MIN: {
+      const int64_t k = order_key(value_f64(A, c, ia, ib));
+      if (k < (int64_t)acc) acc = (uint64_t)k;
+      break;
+    }
+    case PG_AGG_MAX: {
+      const int64_t k = order_key(value_f64(A, c, ia, ib));
+      if (k > (int64_t)acc) acc = (uint64_t)k;
+      break;
+    }
+    case PG_AGG_DISTINCTCOUNT: {
+      const uint64_t key = key_of(A.key_kind, A.key_base, c[0], ia);
+      if (key < A.key_card) q.flags[A.flag_off + key] = 1;
+      else atomicOr(q.err, 2u);
+      break;
+    }
+  }
+}
+
+constexpr int kHalf = kRows / 2;  // rows per batch of the dense aggregation path (bounds live registers)
+
+// Dense tiles (many matches): half a tile of rows at a time, every gather straight-line.
+template <bool GROUPED, int MAXA>
+__device__ __forceinline__ void aggregate_dense(const QuerySpec& q, const SegDesc& sd, const GroupState& S,
+                                                uint64_t (&acc)[MAXA], uint32_t m, uint32_t base, int tid) {
+#pragma unroll
+  for (int h = 0; h < kRows / kHalf; h++) {
+    const uint32_t mh = (m >> (h * kHalf)) & ((1u << kHalf) - 1u);
+    if (__ballot(mh != 0) == 0) continue;
+    const uint32_t hb = base + (uint32_t)(h * kHalf * kBlock);
+    uint32_t g[kHalf];  // slot index (< num_slots <= 2^31)
+    uint32_t live = mh;
+#pragma unroll
+    for (int r = 0; r < kHalf; r++) g[r] = 0;
+    if constexpr (GROUPED) {
+      for (uint32_t k = 0; k < q.num_keys; k++) {
+        const ColDesc& kc = sd.keycols[k];
+        uint32_t ids[kHalf];
+        gather_ids<kHalf>(make_rsrc(kc.words, kc.wbytes), kc.bits, mh, hb, tid, ids);
+        uint64_t kid[kHalf];
+#pragma unroll
+        for (int r = 0; r < kHalf; r++) kid[r] = key_of(q.key_kind[k], q.key_base[k], kc, ids[r]);
+#pragma unroll
+        for (int r = 0; r < kHalf; r++) {
+          if (kid[r] >= q.key_card[k]) live &= ~(1u << r);
+          else g[r] += (uint32_t)kid[r] * (uint32_t)q.key_stride[k];
+        }
+      }
+      if (live != mh) atomicOr(q.err, 1u);  // never expected: the host proved the key ranges
+#pragma unroll
+      for (int r = 0; r < kHalf; r++)
+        if ((live >> r) & 1u) atomicAdd(&S.i64[(uint64_t)g[r] * q.n_i64], 1ull);  // slot 0: doc count / presence
+    }
+    for (uint32_t a = 0; a < q.num_aggs; a++) {
+      const AggSpec& A = q.aggs[a];
+      if (A.fn == PG_AGG_COUNT) continue;
+      const ColDesc* c = sd.aggcols + 2 * a;
+      const uint32_t nc = agg_ncols(A);
+      uint32_t ia[kHalf], ib[kHalf];
+#pragma unroll
+      for (int r = 0; r < kHalf; r++) ia[r] = ib[r] = 0;
+      if (nc >= 1) gather_ids<kHalf>(make_rsrc(c[0].words, c[0].wbytes), c[0].bits, mh, hb, tid, ia);
+      if (nc >= 2) gather_ids<kHalf>(make_rsrc(c[1].words, c[1].wbytes), c[1].bits, mh, hb, tid, ib);
+#pragma unroll
+      for (int r = 0; r < kHalf; r++) {
+        if (!((live >> r) & 1u)) continue;
+        const uint32_t d = hb + (uint32_t)(r * kBlock + tid);
+        if constexpr (GROUPED) {
+          group_update(q, S, A, c, g[r], d, ia[r], ib[r]);
+        } else {
+#pragma unroll
+          for (int x = 0; x < MAXA; x++)
+            if ((uint32_t)x == a) acc_update(q, A, c, acc[x], d, ia[r], ib[r]);
+        }
+      }
+    }
+  }
+}
+
+// Sparse tiles (few matches): one matched doc per lane per round; the round's dictId loads for every key and
+// aggregation input are issued before any is consumed.
+template <bool GROUPED, int MAXA, int MAXK>
+__device__ __forceinline__ void aggregate_sparse(const QuerySpec& q, const SegDesc& sd, const GroupState& S,
+                                                 uint64_t (&acc)[MAXA], uint32_t m, uint32_t base, int tid) {
+  while (__ballot(m != 0)) {
+    const bool act = m != 0;
+    const int j = act ? __ffs(m) - 1 : 0;
+    m &= m - 1;
+    const uint32_t d = act ? base + (uint32_t)(j * kBlock + tid) : base;
+    uint32_t kidx[MAXK > 0 ? MAXK : 1], ia[MAXA], ib[MAXA];
+#pragma unroll
+    for (int k = 0; k < MAXK; k++) {
+      kidx[k] = 0;
+      if (GROUPED && k < (int)q.num_keys)
+        kidx[k] = unpack(make_rsrc(sd.keycols[k].words, sd.keycols[k].wbytes), d, sd.keycols[k].bits);
+    }
+#pragma unroll
+    for (int a = 0; a < MAXA; a++) {
+      ia[a] = ib[a] = 0;
+      if (a >= (int)q.num_aggs) continue;
+      const uint32_t nc = agg_ncols(q.aggs[a]);
+      const ColDesc* c = sd.aggcols + 2 * a;
+      if (nc >= 1) ia[a] = unpack(make_rsrc(c[0].words, c[0].wbytes), d, c[0].bits);
+      if (nc >= 2) ib[a] = unpack(make_rsrc(c[1].words, c[1].wbytes), d, c[1].bits);
+    }
+    if (!act) continue;
+    if constexpr (GROUPED) {
+      uint64_t g = 0;
+      bool in_range = true;
+#pragma unroll
+      for (int k = 0; k < MAXK; k++) {
+        if (k >= (int)q.num_keys) break;
+        const uint64_t kid = key_of(q.key_kind[k], q.key_base[k], sd.keycols[k], kidx[k]);
+        in_range &= kid < q.key_card[k];
+        g += kid * q.key_stride[k];
+      }
+      if (!in_range) {  // never expected: the host proved the key ranges; refuse rather than write out of bounds
+        atomicOr(q.err, 1u);
+        continue;
+      }
+      atomicAdd(&S.i64[g * q.n_i64], 1ull);
+#pragma unroll
+      for (int a = 0; a < MAXA; a++) {
+        if (a >= (int)q.num_aggs) break;
+        group_update(q, S, q.aggs[a], sd.aggcols + 2 * a, g, d, ia[a], ib[a]);
+      }
+    } else {
+#pragma unroll
+      for (int a = 0; a < MAXA; a++) {
+        if (a >= (int)q.num_aggs) break;
+        acc_update(q, q.aggs[a], sd.aggcols + 2 * a, acc[a], d, ia[a], ib[a]);
+      }
+    }
+  }
+}
+
+// MAXA / MAXK: compile-time bounds on the aggregations / group keys of the query (the smallest instantiation
+// that fits is launched), so registers are sized for the query shape, not for the ABI maximum.
+template <bool GROUPED, int MAXA, int MAXK>
 __global__ __launch_bounds__(kBlock) void scan_kernel(QuerySpec q) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   int32_t* lds_sets = (int32_t*)smem;
   unsigned char* lds_groups = smem + (uint64_t)q.set_lds_ints * 4;
   const int tid = threadIdx.x;
-  const bool grouped = q.num_keys > 0;
 
   // LDS-privatised group table: [G][n_i64] u64 | [G][n_f64] f64 | [G][n_min] i64 | [G][n_max] i64
   unsigned long long* l_i64 = (unsigned long long*)lds_groups;
   double* l_f64 = (double*)(l_i64 + q.num_slots * q.n_i64);
   long long* l_mn = (long long*)(l_f64 + q.num_slots * q.n_f64);
   long long* l_mx = l_mn + q.num_slots * q.n_min;
-  if (grouped && q.use_lds) {
+  if (GROUPED && q.use_lds) {
     for (uint64_t i = tid; i < q.num_slots * q.n_i64; i += kBlock) l_i64[i] = 0;
     for (uint64_t i = tid; i < q.num_slots * q.n_f64; i += kBlock) l_f64[i] = 0.0;
     for (uint64_t i = tid; i < q.num_slots * q.n_min; i += kBlock) l_mn[i] = order_key(__builtin_inf());
     for (uint64_t i = tid; i < q.num_slots * q.n_max; i += kBlock) l_mx[i] = order_key(-__builtin_inf());
   }
-  unsigned long long* gi = q.use_lds ? l_i64 : q.i64;
-  double* gf = q.use_lds ? l_f64 : q.f64;
-  long long* gmn = q.use_lds ? l_mn : q.mn;
-  long long* gmx = q.use_lds ? l_mx : q.mx;
+  const GroupState S = q.use_lds ? GroupState{l_i64, l_f64, l_mn, l_mx} : GroupState{q.i64, q.f64, q.mn, q.mx};
 
   // aggregation-only accumulators (registers; indices compile-time via unrolled agg loops)
-  uint64_t acc[kMaxAggs];
+  uint64_t acc[MAXA];
 #pragma unroll
-  for (int a = 0; a < kMaxAggs; a++) {
+  for (int a = 0; a < MAXA; a++) {
     acc[a] = 0;
-    if (a < (int)q.num_aggs) {
+    if (!GROUPED && a < (int)q.num_aggs) {
       if (q.aggs[a].kind == SK_MIN) acc[a] = (uint64_t)order_key(__builtin_inf());
       if (q.aggs[a].kind == SK_MAX) acc[a] = (uint64_t)order_key(-__builtin_inf());
     }
@@ -287,112 +509,28 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(QuerySpec q) {
       uint32_t valid = 0;
 #pragma unroll
       for (int j = 0; j < kRows; j++) valid |= (uint32_t)(base + (uint32_t)(j * kBlock + tid) < nd) << j;
-      uint32_t m = eval_filter(q, sd.leaves, lds_sets, valid, base, tid);
+      const uint32_t m = eval_filter(q, sd.leaves, lds_sets, valid, base, tid);
       const uint32_t nm = __popc(m);
       seg_count += nm;
-      if (__ballot(m != 0) == 0) continue;
-
-      if (!grouped) {
-        doc_count += nm;
-        while (m) {
-          const int j = __ffs(m) - 1;
-          m &= m - 1;
-          const uint32_t d = base + (uint32_t)(j * kBlock + tid);
-#pragma unroll
-          for (int a = 0; a < kMaxAggs; a++) {
-            if (a >= (int)q.num_aggs) break;
-            const AggSpec& A = q.aggs[a];
-            const ColDesc* c = sd.aggcols + 2 * a;
-            switch (A.fn) {
-              case PG_AGG_COUNT: break;  // = doc_count
-              case PG_AGG_COUNTMV: acc[a] += c[0].mv_offsets[d + 1] - c[0].mv_offsets[d]; break;
-              case PG_AGG_SUM:
-              case PG_AGG_AVG:
-                if (A.integer) acc[a] += (uint64_t)agg_value_i64(A, c, d);
-                else acc[a] = __double_as_longlong(__longlong_as_double(acc[a]) + agg_value_f64(A, c, d));
-                break;  // AVG count == doc_count
-              case PG_AGG_MIN: {
-                const int64_t k = order_key(agg_value_f64(A, c, d));
-                if (k < (int64_t)acc[a]) acc[a] = (uint64_t)k;
-                break;
-              }
-              case PG_AGG_MAX: {
-                const int64_t k = order_key(agg_value_f64(A, c, d));
-                if (k > (int64_t)acc[a]) acc[a] = (uint64_t)k;
-                break;
-              }
-              case PG_AGG_DISTINCTCOUNT: {
-                const uint64_t key = col_key(A.key_kind, A.key_base, c[0], d);
-                if (key < A.key_card) q.flags[A.flag_off + key] = 1;
-                else atomicOr(q.err, 2u);
-                break;
-              }
-            }
-          }
-        }
-      } else {
-        while (m) {
-          const int j = __ffs(m) - 1;
-          m &= m - 1;
-          const uint32_t d = base + (uint32_t)(j * kBlock + tid);
-          uint64_t g = 0;
-          bool in_range = true;
-#pragma unroll
-          for (int k = 0; k < kMaxKeys; k++) {
-            if (k >= (int)q.num_keys) break;
-            const uint64_t kid = col_key(q.key_kind[k], q.key_base[k], sd.keycols[k], d);
-            in_range &= kid < q.key_card[k];
-            g += kid * q.key_stride[k];
-          }
-          if (!in_range) {  // never expected (host proved the key ranges): refuse rather than write out of bounds
-            atomicOr(q.err, 1u);
-            continue;
-          }
-          atomicAdd(&gi[g * q.n_i64], 1ull);  // slot 0: doc count / presence
-#pragma unroll
-          for (int a = 0; a < kMaxAggs; a++) {
-            if (a >= (int)q.num_aggs) break;
-            const AggSpec& A = q.aggs[a];
-            const ColDesc* c = sd.aggcols + 2 * a;
-            switch (A.fn) {
-              case PG_AGG_COUNT: break;  // = slot 0
-              case PG_AGG_COUNTMV:
-                atomicAdd(&gi[g * q.n_i64 + A.slot],
-                          (unsigned long long)(c[0].mv_offsets[d + 1] - c[0].mv_offsets[d]));
-                break;
-              case PG_AGG_SUM:
-              case PG_AGG_AVG:
-                if (A.integer) atomicAdd(&gi[g * q.n_i64 + A.slot], (unsigned long long)agg_value_i64(A, c, d));
-                else atomicAdd(&gf[g * q.n_f64 + A.slot], agg_value_f64(A, c, d));
-                break;  // AVG count == slot 0
-              case PG_AGG_MIN:
-                atomicMin(&gmn[g * q.n_min + A.slot], (long long)order_key(agg_value_f64(A, c, d)));
-                break;
-              case PG_AGG_MAX:
-                atomicMax(&gmx[g * q.n_max + A.slot], (long long)order_key(agg_value_f64(A, c, d)));
-                break;
-              case PG_AGG_DISTINCTCOUNT: {
-                const uint64_t key = col_key(A.key_kind, A.key_base, c[0], d);
-                if (key < A.key_card) q.flags[g * q.flag_bytes_per_slot + A.flag_off + key] = 1;
-                else atomicOr(q.err, 2u);
-                break;
-              }
-            }
-          }
-        }
-      }
+      if (!GROUPED) doc_count += nm;
+      const uint64_t lanes = __ballot(m != 0);
+      if (lanes == 0) continue;
+      if (!GROUPED && q.num_aggs == 0) continue;
+      // dense when more than a quarter of the wave's lanes hold matches
+      if (__popcll(lanes) > 16) aggregate_dense<GROUPED, MAXA>(q, sd, S, acc, m, base, tid);
+      else aggregate_sparse<GROUPED, MAXA, MAXK>(q, sd, S, acc, m, base, tid);
     }
     const uint64_t c = wave_sum_u64(seg_count);
     if ((tid & 63) == 0 && c) atomicAdd(&q.seg_matched[it.seg], (unsigned long long)c);
   }
 
-  if (!grouped) {
+  if (!GROUPED) {
     // wave-reduce then one global atomic per wave per slot
     const uint64_t dc = wave_sum_u64(doc_count);
     const bool lead = (tid & 63) == 0;
     if (lead && dc) atomicAdd(&q.i64[0], (unsigned long long)dc);
 #pragma unroll
-    for (int a = 0; a < kMaxAggs; a++) {
+    for (int a = 0; a < MAXA; a++) {
       if (a >= (int)q.num_aggs) break;
       const AggSpec& A = q.aggs[a];
       switch (A.kind) {
@@ -434,10 +572,28 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(QuerySpec q) {
   }
 }
 
+template <bool G, int A, int K>
+static void launch_one(const QuerySpec& q, uint32_t blocks, size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL((scan_kernel<G, A, K>), dim3(blocks), dim3(kBlock), lds, s, q);
+}
+
 hipError_t launch_scan(const QuerySpec& q, uint32_t blocks, hipStream_t s) {
   size_t lds = (size_t)q.set_lds_ints * 4;
   if (q.num_keys && q.use_lds) lds += q.num_slots * 8ull * (q.n_i64 + q.n_f64 + q.n_min + q.n_max);
-  hipLaunchKernelGGL(scan_kernel, dim3(blocks), dim3(kBlock), lds, s, q);
+  const uint32_t na = q.num_aggs;
+  if (q.num_keys == 0) {
+    if (na <= 2) launch_one<false, 2, 0>(q, blocks, lds, s);
+    else if (na <= 4) launch_one<false, 4, 0>(q, blocks, lds, s);
+    else launch_one<false, kMaxAggs, 0>(q, blocks, lds, s);
+  } else if (q.num_keys == 1) {
+    if (na <= 2) launch_one<true, 2, 1>(q, blocks, lds, s);
+    else if (na <= 4) launch_one<true, 4, 1>(q, blocks, lds, s);
+    else launch_one<true, kMaxAggs, 1>(q, blocks, lds, s);
+  } else {
+    if (na <= 2) launch_one<true, 2, kMaxKeys>(q, blocks, lds, s);
+    else if (na <= 4) launch_one<true, 4, kMaxKeys>(q, blocks, lds, s);
+    else launch_one<true, kMaxAggs, kMaxKeys>(q, blocks, lds, s);
+  }
   return hipGetLastError();
 }
 
