@@ -24,16 +24,20 @@
 namespace pg {
 
 constexpr int kBlock = 256;                          // 4 waves of 64
-constexpr int kRows = 8;                             // docs of a thread in a tile: base + j*256 + tid
-constexpr int kTileDocs = kBlock * kRows;            // 2048 docs per tile
-constexpr int kItemTiles = 16;                       // tiles per work item (32 768 docs), within one segment
+constexpr int kRows = 32;                            // docs of a thread in a tile: base + j*256 + tid (32-bit masks)
+constexpr int kChunk = 8;                            // rows gathered per straight-line batch
+constexpr int kTileDocs = kBlock * kRows;            // 8192 docs per tile
+constexpr int kItemTiles = 4;                        // tiles per work item (32 768 docs), within one segment
 constexpr int kMaxAggs = 8;
 constexpr int kMaxKeys = 4;
 constexpr int kMaxLeaves = 24;
 constexpr int kMaxOps = 64;
-constexpr int kMaxDepth = 8;                         // filter tree nesting
-constexpr int kLdsGroupBytes = 48 * 1024;            // LDS-privatised group table budget
-constexpr int kLdsSetBytes = 32 * 1024;              // LDS hash sets of IN / NOT_IN leaves
+constexpr int kMaxDepth = 4;                         // filter tree nesting (open groups)
+constexpr int kLdsGroupBytes = 32 * 1024;            // LDS-privatised group table budget
+constexpr int kLdsSetBytes = 16 * 1024;              // LDS hash sets of IN / NOT_IN leaves
+constexpr int kLdsStageBytes = 32 * 1024;            // LDS tiles of densely read packed columns
+constexpr int kMaxStaged = 6;                        // packed columns staged per tile
+constexpr int kNoSlot = 255;
 
 // Filter program as the kernel runs it: a tree in prefix form (host-compiled from the ABI's postfix program,
 // AND children ordered most-selective first so later children are evaluated only on surviving docs).
@@ -43,9 +47,8 @@ enum LeafKind : uint32_t {
   LK_ALL = 0,        // match all
   LK_NONE = 1,       // match none
   LK_RANGE = 2,      // dictId in [lo,hi), dictIds unpacked from a packed SV forward index
-  LK_SET_LDS = 3,    // dictId in set: open-addressing hash set staged in LDS (lds_off / set_log2)
+  LK_SET_LDS = 3,    // dictId in set: LDS filter bitmap (+ exact hash table) staged per segment
   LK_SET_LUT = 4,    // dictId in set: bit dictId of `aux` (global LSB-first words)
-  LK_DOCBITMAP = 5,  // precomputed doc bitmap `aux` (native LSB-first words)
   LK_DOCRANGE = 6    // doc id in [lo,hi)
 };
 
@@ -53,12 +56,19 @@ struct LeafDesc {
   uint32_t kind;
   uint32_t excl;      // invert the leaf (NOT_EQ / NOT_IN on a scan)
   int32_t lo, hi;
-  const uint32_t* words;  // packed forward words (RANGE / SET_*)
-  const uint32_t* aux;    // SET_LUT bitmap / DOCBITMAP / SET_LDS source table (global)
+  const uint32_t* words;  // packed forward words (RANGE / SET_*); doc bitmaps are 1-bit columns
+  const uint32_t* aux;    // SET_LUT bitmap / SET_LDS source region (global)
   uint32_t bits;
-  uint32_t set_log2;      // SET_LDS: table has 1 << set_log2 int32 slots (empty = -1)
-  uint32_t lds_off;       // SET_LDS: int32 offset of the table in the block's LDS set region
   uint32_t wbytes;        // bytes of `words` (buffer-descriptor range)
+  // SET_LDS: an LDS region of `set_ints` words at `lds_off`: a filter bitmap of `nbw` words over dictId >> shift
+  // (LSB-first), followed, when shift > 0, by an exact open-addressing hash table of 1 << set_log2 int32 slots
+  // (empty = -1) that resolves the bitmap's candidates.  shift == 0: the bitmap is exact.
+  uint32_t lds_off;
+  uint32_t set_ints;
+  uint32_t shift;
+  uint32_t nbw;
+  uint32_t set_log2;
+  uint32_t pad;
 };
 
 // A column as read by aggregation inputs and group keys.
@@ -102,10 +112,26 @@ struct AggSpec {
   uint64_t flag_off;  // DISTINCTCOUNT: byte offset of this agg's flags within a slot's flag row
 };
 
+// A packed column staged per tile into LDS (coalesced 16-byte loads of the tile's whole word range) because
+// most of its cache lines are needed anyway; every other read of a packed column is a per-doc gather.
+// Source = the words of a leaf (role 0), an aggregation operand (role 1) or a group key (role 2) of the current
+// segment.  Slots are uniform across segments; `lds_words` is sized for the widest bitsPerElement.
+struct StagedCol {
+  uint32_t role, idx, operand;
+  uint32_t lds_word_off;     // offset of this slot in the staging region (uint32 words)
+};
+
 struct QuerySpec {
   uint32_t num_segments, num_leaves, num_ops, num_aggs, num_keys, num_items;
+  uint32_t agg_reads;        // some aggregation reads a column (else COUNT(*) only: matched-doc counts suffice)
   uint32_t use_lds;          // group table privatised in LDS
   uint32_t set_lds_ints;     // int32 slots of LDS hash sets per block
+  uint32_t num_staged;
+  uint32_t stage_lds_words;  // uint32 words of the staging region
+  StagedCol staged[kMaxStaged];
+  uint8_t leaf_slot[kMaxLeaves];     // staged slot of each leaf's column or kNoSlot
+  uint8_t agg_slot[kMaxAggs][2];     // staged slot of each aggregation operand or kNoSlot
+  uint8_t key_slot[kMaxKeys];        // staged slot of each group key column or kNoSlot
   int32_t ops[kMaxOps];
   AggSpec aggs[kMaxAggs];
   uint32_t key_kind[kMaxKeys];
@@ -146,6 +172,7 @@ __host__ __device__ inline uint32_t set_hash(uint32_t id, uint32_t log2) {
 
 // ---- kernel launchers
 hipError_t launch_scan(const QuerySpec& q, uint32_t blocks, hipStream_t s);                  // pg_scan.hip
+size_t scan_lds_bytes(const QuerySpec& q);
 hipError_t launch_init_state(const QuerySpec& q, hipStream_t s);                             // pg_kernels.hip
 hipError_t launch_bswap_words(const uint8_t* src, uint32_t* dst, uint64_t nbytes, uint64_t nwords_out, hipStream_t s);
 hipError_t launch_be_to_native(const uint8_t* src, void* dst, uint64_t n, uint32_t width, hipStream_t s);

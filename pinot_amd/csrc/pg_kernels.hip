@@ -182,6 +182,8 @@ hipError_t launch_mv_offsets(const uint32_t* bm, uint64_t num_values, uint32_t n
 
 // ------------------------------------------------------------------------------------------ filter pre-pass
 
+// Doc bitmaps produced by the pre-pass use the packed-column bit order (doc d = bit 31-(d&31) of word d>>5), so
+// the scan reads them as 1-bit packed columns (staged or gathered like any other column).
 // Doc ranges (inclusive, sorted, disjoint) -> doc bitmap: SortedIndexBasedFilterOperator's range list
 // (filter/SortedIndexBasedFilterOperator.java:51-138).  One thread per bitmap word.
 __global__ void fill_ranges_kernel(const int32_t* __restrict__ r, uint32_t n, uint32_t num_docs,
@@ -199,7 +201,7 @@ __global__ void fill_ranges_kernel(const int32_t* __restrict__ r, uint32_t n, ui
     for (uint32_t i = lo; i < n && r[2 * i] <= d1; i++) {
       const int64_t s = r[2 * i] > d0 ? r[2 * i] : d0;
       const int64_t e = r[2 * i + 1] < d1 ? r[2 * i + 1] : d1;
-      for (int64_t d = s; d <= e; d++) out |= 1u << (uint32_t)(d - d0);
+      for (int64_t d = s; d <= e; d++) out |= 0x80000000u >> (uint32_t)(d - d0);
     }
     bm[w] = out;
   }
@@ -228,14 +230,14 @@ __global__ void roaring_or_kernel(const uint8_t* __restrict__ roaring, const Roa
     const uint16_t* a = (const uint16_t*)p;
     for (uint32_t i = threadIdx.x; i < c.card; i += blockDim.x) {
       const uint32_t x = base + a[i];
-      if (x < num_docs) atomicOr(&bm[x >> 5], 1u << (x & 31u));
+      if (x < num_docs) atomicOr(&bm[x >> 5], 0x80000000u >> (x & 31u));
     }
   } else if (c.type == 1) {  // 1024 little-endian uint64 words
     const uint32_t* w32 = (const uint32_t*)p;
     for (uint32_t i = threadIdx.x; i < 2048; i += blockDim.x) {
       const uint32_t wi = (base >> 5) + i;
       const uint32_t v = w32[i];
-      if (v && wi < nwords) atomicOr(&bm[wi], v);
+      if (v && wi < nwords) atomicOr(&bm[wi], __builtin_bitreverse32(v));
     }
   } else {  // runs: uint16 nruns, then (start, length-1) pairs
     const uint16_t* r = (const uint16_t*)p + 1;
@@ -247,7 +249,7 @@ __global__ void roaring_or_kernel(const uint8_t* __restrict__ roaring, const Roa
         const uint32_t lo = w * 32 > s ? 0 : s - w * 32;
         const uint32_t hi = w * 32 + 31 < e ? 31 : e - w * 32;
         const uint32_t mask = (hi == 31 ? 0xFFFFFFFFu : ((1u << (hi + 1)) - 1u)) & ~((1u << lo) - 1u);
-        atomicOr(&bm[w], mask);
+        atomicOr(&bm[w], __builtin_bitreverse32(mask));
       }
     }
   }
@@ -265,7 +267,7 @@ __global__ void bitmap_not_kernel(uint32_t* bm, uint32_t num_docs) {
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += stride) {
     uint32_t v = ~bm[w];
-    if (w == nwords - 1 && (num_docs & 31u)) v &= (1u << (num_docs & 31u)) - 1u;
+    if (w == nwords - 1 && (num_docs & 31u)) v &= ~(0xFFFFFFFFu >> (num_docs & 31u));
     bm[w] = v;
   }
 }
@@ -297,8 +299,8 @@ __global__ void mv_scan_kernel(const uint32_t* __restrict__ words, uint32_t bits
     const uint64_t b = __ballot(match);
     if ((threadIdx.x & 63) == 0) {
       const uint32_t w = d >> 5;  // d is a multiple of 64 here
-      if (w < (num_docs + 31) / 32) bm[w] = (uint32_t)b;
-      if (w + 1 < (num_docs + 31) / 32) bm[w + 1] = (uint32_t)(b >> 32);
+      if (w < (num_docs + 31) / 32) bm[w] = __builtin_bitreverse32((uint32_t)b);
+      if (w + 1 < (num_docs + 31) / 32) bm[w + 1] = __builtin_bitreverse32((uint32_t)(b >> 32));
     }
   }
 }

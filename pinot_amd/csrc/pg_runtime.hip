@@ -619,6 +619,29 @@ void emit_prefix(const std::vector<FNode>& nodes, int n, std::vector<int32_t>& o
   out.push_back(kOpEnd);
 }
 
+// A pre-pass doc bitmap (packed-column bit order) read by the scan as a 1-bit column: doc matches iff bit == 1.
+void as_bitmap_leaf(LeafDesc& dl, uint32_t num_docs) {
+  dl.kind = LK_RANGE;
+  dl.bits = 1;
+  dl.lo = 1;
+  dl.hi = 2;
+  dl.excl = 0;
+  dl.wbytes = 4u * ((num_docs + 31) / 32 + 1);
+}
+
+// Probability that each leaf is evaluated for a doc (the root's children: 1; an AND child: the product of the
+// earlier siblings' pass fractions; an OR child: of their reject fractions).
+void assign_reach(const std::vector<FNode>& nodes, int n, double reach, std::vector<double>& leaf_reach) {
+  const FNode& x = nodes[n];
+  if (x.kind == 0) { leaf_reach[x.leaf] = std::max(leaf_reach[x.leaf], reach); return; }
+  double r = reach;
+  for (int k : x.kids) {
+    assign_reach(nodes, k, r, leaf_reach);
+    if (x.kind == 1) r *= nodes[k].pass;
+    else if (x.kind == 2) r *= 1.0 - nodes[k].pass;
+  }
+}
+
 struct ThreadCtx {  // per calling thread: staging + events, created once
   PinnedBuf pinned;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -629,6 +652,8 @@ struct ThreadCtx {  // per calling thread: staging + events, created once
   }
 };
 thread_local ThreadCtx t_ctx;
+
+bool pl_too_big(uint32_t ints) { return ints * 4ull > (uint64_t)kLdsSetBytes; }
 
 int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   if (!plan) return fail(PG_E_INVALID, "null plan");
@@ -804,6 +829,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
     }
   }
   for (uint32_t k = 0; k < K; k++) projected.insert(plan->keys[k].col_id);
+  for (uint32_t a = 0; a < A; a++) q.agg_reads |= plan->aggs[a].fn != PG_AGG_COUNT;
   q.num_slots = G;
   q.n_i64 = n_i64; q.n_f64 = n_f64; q.n_min = n_min; q.n_max = n_max;
   q.flag_bytes_per_slot = flag_bytes;
@@ -818,25 +844,40 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   // ---- per (segment, leaf) lowering.  A leaf's dictId set becomes: a contiguous range -> RANGE; a small set
   // -> LDS hash set (uniform table size per leaf across segments so the LDS layout is fixed); else a global
   // bitmap over dictIds built on the device (one batched launch).
-  std::vector<uint32_t> set_log2(L, 0);  // per leaf: 0 = no LDS set
-  std::vector<double> leaf_pass(L, 0.0), leaf_cost(L, 0.0);
+  // Per leaf: LDS words of its IN-set region (uniform across segments), 0 = gathered through a global LUT.
+  // Region = filter bitmap over dictId >> shift (<= 8 KB) + (shift > 0) an exact hash table (<= 50 % full).
+  auto set_geometry = [](uint32_t card, uint32_t n_ids, uint32_t& shift, uint32_t& nbw, uint32_t& lg) {
+    shift = 0;
+    while (((card + (1u << shift) - 1) >> shift) > 65536u) shift++;
+    nbw = (((card + (1u << shift) - 1) >> shift) + 31) / 32 + 1;
+    lg = 0;
+    if (shift) {
+      lg = 1;
+      while ((1u << lg) < 2 * n_ids) lg++;
+    }
+    return nbw + (shift ? (1u << lg) : 0u);
+  };
+  std::vector<uint32_t> set_ints(L, 0), set_off(L, 0);
+  std::vector<double> leaf_pass(L, 0.0), leaf_cost(L, 0.0), leaf_reach(L, 0.0);
+  double filter_pass = 1.0;
   {
-    std::vector<uint32_t> max_ids(L, 0);
     for (uint32_t si = 0; si < S; si++)
       for (uint32_t li = 0; li < L; li++) {
         const pg_leaf& pl = plan->segments[si].leaves[li];
         if (pl.kind != PG_LEAF_SV_SCAN || pl.num_ids == 0) continue;
-        max_ids[li] = std::max(max_ids[li], pl.num_ids);
+        const ColumnRes* c = col(si, pl.col_id);
+        if (!c) continue;
+        uint32_t sh, nbw, lg;
+        set_ints[li] = std::max(set_ints[li], set_geometry(std::max(c->card, 1u), pl.num_ids, sh, nbw, lg));
       }
-    uint32_t budget = kLdsSetBytes / 4, used = 0;
+    uint32_t used = 0;
     for (uint32_t li = 0; li < L; li++) {
-      if (!max_ids[li] || max_ids[li] > 4096) continue;
-      uint32_t lg = 1;  // load factor <= 1/4 when it fits (expected ~1.4 probes per miss), else <= 1/2
-      while ((1u << lg) < 4 * max_ids[li]) lg++;
-      if (used + (1u << lg) > budget) lg--;
-      if ((1u << lg) < 2 * max_ids[li] || used + (1u << lg) > budget) continue;
-      set_log2[li] = lg;
-      used += 1u << lg;
+      if (!set_ints[li] || pl_too_big(set_ints[li]) || (used + set_ints[li]) * 4ull > (uint64_t)kLdsSetBytes) {
+        set_ints[li] = 0;
+        continue;
+      }
+      set_off[li] = used;
+      used += (set_ints[li] + 3) & ~3u;
     }
     q.set_lds_ints = used;
   }
@@ -865,7 +906,11 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
     int root = -1;
     build_tree(plan, leaf_pass, leaf_cost, nodes, root);
     std::vector<int32_t> pre;
-    if (root >= 0) emit_prefix(nodes, root, pre);
+    if (root >= 0) {
+      emit_prefix(nodes, root, pre);
+      assign_reach(nodes, root, 1.0, leaf_reach);
+      filter_pass = nodes[root].pass;
+    }
     if (pre.size() > (size_t)kMaxOps) return fail(PG_E_UNSUPPORTED, "filter program longer than %d", kMaxOps);
     int depth = 0, md = 0;
     for (int32_t op : pre) {
@@ -890,7 +935,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   auto scratch_reserve = [&](uint64_t n) { uint64_t at = (scratch_bytes + 255) & ~255ull; scratch_bytes = at + n; return at; };
   uint64_t entries_in_filter = 0;
   // device pointers into arena / scratch are patched once those are allocated
-  struct Patch { uint64_t leaf_index; uint64_t off; bool in_arena; };
+  struct Patch { uint64_t leaf_index; uint64_t off; bool in_arena; bool words; };
   std::vector<Patch> patches;
 
   for (uint32_t si = 0; si < S; si++) {
@@ -929,25 +974,32 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
             const int32_t lo = pl.num_ids ? pl.ids[0] : pl.lo, hi = pl.num_ids ? pl.ids[pl.num_ids - 1] + 1 : pl.hi;
             dl.lo = std::max(lo, 0);
             dl.hi = std::max(std::min(hi, (int32_t)c->card), dl.lo);
-          } else if (set_log2[li]) {
+          } else if (set_ints[li]) {
             dl.kind = LK_SET_LDS;
-            dl.set_log2 = set_log2[li];
-            const uint32_t n = 1u << set_log2[li];
-            std::vector<int32_t> tab(n, -1);
+            const uint32_t n_region = set_geometry(std::max(c->card, 1u), pl.num_ids, dl.shift, dl.nbw, dl.set_log2);
+            std::vector<uint32_t> region(n_region, 0);
             for (uint32_t i = 0; i < pl.num_ids; i++) {
-              uint32_t h = set_hash((uint32_t)pl.ids[i], dl.set_log2);
-              while (tab[h] >= 0) h = (h + 1) & (n - 1);
-              tab[h] = pl.ids[i];
+              const uint32_t x = (uint32_t)pl.ids[i] >> dl.shift;
+              region[x >> 5] |= 1u << (x & 31u);
             }
-            uint32_t off = 0;
-            for (uint32_t l2 = 0; l2 < li; l2++) off += set_log2[l2] ? (1u << set_log2[l2]) : 0;
-            dl.lds_off = off;
-            patches.push_back({(uint64_t)si * L + li, ar.put(tab.data(), 4ull * n), true});
+            if (dl.shift) {
+              const uint32_t n = 1u << dl.set_log2;
+              int32_t* tab = (int32_t*)&region[dl.nbw];
+              for (uint32_t i = 0; i < n; i++) tab[i] = -1;
+              for (uint32_t i = 0; i < pl.num_ids; i++) {
+                uint32_t h = set_hash((uint32_t)pl.ids[i], dl.set_log2);
+                while (tab[h] >= 0) h = (h + 1) & (n - 1);
+                tab[h] = pl.ids[i];
+              }
+            }
+            dl.set_ints = n_region;
+            dl.lds_off = set_off[li];
+            patches.push_back({(uint64_t)si * L + li, ar.put(region.data(), 4ull * n_region), true, false});
           } else {
             dl.kind = LK_SET_LUT;
             const uint64_t lut_off = scratch_reserve(4ull * ((c->card + 31) / 32 + 1));
             luts.push_back({ar.put(pl.ids, 4ull * pl.num_ids), pl.num_ids, lut_off});
-            patches.push_back({(uint64_t)si * L + li, lut_off, false});
+            patches.push_back({(uint64_t)si * L + li, lut_off, false, false});
           }
           break;
         }
@@ -975,13 +1027,13 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
           dl.excl = 0;
           if (rg.empty()) { dl.kind = LK_NONE; break; }
           if (rg.size() == 2) { dl.kind = LK_DOCRANGE; dl.lo = rg[0]; dl.hi = rg[1] + 1; break; }
-          dl.kind = LK_DOCBITMAP;
+          as_bitmap_leaf(dl, sr.num_docs);
           PrepassOp op{PrepassOp::FILL_RANGES, si, li};
           op.in_off = ar.put(rg.data(), 4ull * rg.size());
           op.n = (uint32_t)(rg.size() / 2);
           op.num_docs = sr.num_docs;
           op.out_off = scratch_reserve(4ull * ((sr.num_docs + 31) / 32 + 1));
-          patches.push_back({(uint64_t)si * L + li, op.out_off, false});
+          patches.push_back({(uint64_t)si * L + li, op.out_off, false, true});
           pre.push_back(op);
           break;
         }
@@ -996,7 +1048,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
             for (int32_t id = lo; id < hi; id++)
               for (uint32_t x = c->inv_dir[id]; x < c->inv_dir[id + 1]; x++) sel.push_back(x);
           }
-          dl.kind = LK_DOCBITMAP;
+          as_bitmap_leaf(dl, sr.num_docs);
           dl.excl = 0;
           PrepassOp op{PrepassOp::ROARING, si, li};
           op.in_off = ar.put(sel.data(), 4ull * sel.size());
@@ -1005,14 +1057,14 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
           op.col = c;
           op.negate = pl.exclusive != 0;
           op.out_off = scratch_reserve(4ull * ((sr.num_docs + 31) / 32 + 1));
-          patches.push_back({(uint64_t)si * L + li, op.out_off, false});
+          patches.push_back({(uint64_t)si * L + li, op.out_off, false, true});
           pre.push_back(op);
           break;
         }
         case PG_LEAF_MV_SCAN: {
           if (c->fwd != FWD_MV) return fail(PG_E_INVALID, "MV scan on column %u without MV forward index", pl.col_id);
           entries_in_filter += c->num_values;
-          dl.kind = LK_DOCBITMAP;
+          as_bitmap_leaf(dl, sr.num_docs);
           dl.excl = 0;
           PrepassOp op{PrepassOp::MV_SCAN, si, li};
           op.col = c;
@@ -1025,7 +1077,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
             luts.push_back({ar.put(pl.ids, 4ull * pl.num_ids), pl.num_ids, op.lut_off});
           }
           op.out_off = scratch_reserve(4ull * ((sr.num_docs + 31) / 32 + 1));
-          patches.push_back({(uint64_t)si * L + li, op.out_off, false});
+          patches.push_back({(uint64_t)si * L + li, op.out_off, false, true});
           pre.push_back(op);
           break;
         }
@@ -1068,6 +1120,101 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   P.entries_in_filter = entries_in_filter;
   q.num_items = (uint32_t)items.size();
 
+  // ---- staging policy: a packed column is staged per tile (coalesced, every byte used) when the docs the query
+  // needs from it are dense enough that a gather would fetch most of its 128-byte lines anyway
+  // (reach * docs-per-line >= 1); the rest are gathered per needed doc.  Greedy by reach within the LDS budget.
+  {
+    struct Cand { uint32_t role, idx, operand; uint64_t key; double reach; uint32_t bmax; };
+    std::vector<Cand> cands;
+    auto add = [&](uint32_t role, uint32_t idx, uint32_t operand, uint64_t key, double reach, uint32_t bits) {
+      for (Cand& c : cands)
+        if (c.key == key) { c.reach = std::max(c.reach, reach); c.bmax = std::max(c.bmax, bits); return; }
+      cands.push_back({role, idx, operand, key, reach, bits});
+    };
+    for (uint32_t li = 0; li < L; li++) {
+      uint32_t bmax = 0;
+      bool bitmap = false, scan = false;
+      uint32_t cid = 0;
+      for (uint32_t si = 0; si < S; si++) {
+        const LeafDesc& dl = leaves[(uint64_t)si * L + li];
+        if (dl.kind != LK_RANGE && dl.kind != LK_SET_LDS && dl.kind != LK_SET_LUT) continue;
+        bmax = std::max(bmax, dl.bits);
+        const pg_leaf& pl = plan->segments[si].leaves[li];
+        if (pl.kind == PG_LEAF_SV_SCAN) { scan = true; cid = pl.col_id; } else bitmap = true;
+      }
+      if (!bmax || (scan && bitmap)) continue;  // mixed per-segment forms: gather
+      add(0, li, 0, scan ? (1ull << 32) | cid : (2ull << 32) | li, leaf_reach[li], bmax);
+    }
+    for (uint32_t a = 0; a < A; a++) {
+      const pg_agg& g = plan->aggs[a];
+      if (g.fn == PG_AGG_COUNT || g.fn == PG_AGG_COUNTMV) continue;
+      const int n = (g.op != PG_EXPR_COL && g.fn != PG_AGG_DISTINCTCOUNT) ? 2 : 1;
+      for (int k = 0; k < n; k++) {
+        const uint32_t cid = k ? g.col_b : g.col_a;
+        uint32_t bmax = 0;
+        for (uint32_t si = 0; si < S; si++) bmax = std::max(bmax, col(si, cid)->bits);
+        add(1, a, (uint32_t)k, (1ull << 32) | cid, filter_pass, bmax);
+      }
+    }
+    for (uint32_t k = 0; k < K; k++) {
+      uint32_t bmax = 0;
+      for (uint32_t si = 0; si < S; si++) bmax = std::max(bmax, col(si, plan->keys[k].col_id)->bits);
+      add(2, k, 0, (1ull << 32) | plan->keys[k].col_id, filter_pass, bmax);
+    }
+    std::stable_sort(cands.begin(), cands.end(), [](const Cand& x, const Cand& y) { return x.reach > y.reach; });
+    memset(q.leaf_slot, kNoSlot, sizeof(q.leaf_slot));
+    memset(q.agg_slot, kNoSlot, sizeof(q.agg_slot));
+    memset(q.key_slot, kNoSlot, sizeof(q.key_slot));
+    static const char* no_stage = getenv("PG_NO_STAGING");
+    uint32_t words = 0;
+    for (const Cand& c : cands) {
+      if (no_stage || q.num_staged >= (uint32_t)kMaxStaged) break;
+      if (c.reach * 1024.0 / c.bmax < 1.0) continue;
+      const uint32_t need = (uint32_t)(kTileDocs / 32) * c.bmax + 4;
+      if ((words + need) * 4ull > (uint64_t)kLdsStageBytes) continue;
+      const uint32_t slot = q.num_staged++;
+      q.staged[slot] = {c.role, c.idx, c.operand, words};
+      words += need;
+      // every use of the same column shares the slot
+      for (uint32_t li = 0; li < L; li++) {
+        bool match = false;
+        if ((c.key >> 32) == 2) match = li == (uint32_t)c.key;
+        else
+          for (uint32_t si = 0; si < S && !match; si++) {
+            const pg_leaf& pl = plan->segments[si].leaves[li];
+            match = pl.kind == PG_LEAF_SV_SCAN && (uint64_t)pl.col_id == (c.key & 0xFFFFFFFFull) &&
+                    leaves[(uint64_t)si * L + li].kind != LK_ALL && leaves[(uint64_t)si * L + li].kind != LK_NONE;
+          }
+        if (match && (c.key >> 32) == 2) q.leaf_slot[li] = (uint8_t)slot;
+        else if (match) {
+          // only when every segment's form of this leaf reads the column itself
+          bool all_col = true;
+          for (uint32_t si = 0; si < S; si++) {
+            const pg_leaf& pl = plan->segments[si].leaves[li];
+            const LeafDesc& dl = leaves[(uint64_t)si * L + li];
+            if ((dl.kind == LK_RANGE || dl.kind == LK_SET_LDS || dl.kind == LK_SET_LUT) && pl.kind != PG_LEAF_SV_SCAN)
+              all_col = false;
+          }
+          if (all_col) q.leaf_slot[li] = (uint8_t)slot;
+        }
+      }
+      if ((c.key >> 32) == 1) {
+        const uint32_t cid = (uint32_t)c.key;
+        for (uint32_t a = 0; a < A; a++) {
+          const pg_agg& g = plan->aggs[a];
+          if (g.fn == PG_AGG_COUNT || g.fn == PG_AGG_COUNTMV) continue;
+          if (g.col_a == cid) q.agg_slot[a][0] = (uint8_t)slot;
+          if (g.op != PG_EXPR_COL && g.fn != PG_AGG_DISTINCTCOUNT && g.col_b == cid) q.agg_slot[a][1] = (uint8_t)slot;
+        }
+        for (uint32_t k = 0; k < K; k++)
+          if (plan->keys[k].col_id == cid) q.key_slot[k] = (uint8_t)slot;
+      }
+    }
+    q.stage_lds_words = words;
+  }
+  const size_t lds_bytes = scan_lds_bytes(q);
+  if (lds_bytes > 160 * 1024) return fail(PG_E_UNSUPPORTED, "scan needs %zu bytes of LDS", lds_bytes);
+
   // ---- device buffers (state + arena + scratch) from the caching pool
   if ((rc = P.i64.alloc_pooled(G * 8ull * n_i64))) return rc;
   if (n_f64 && (rc = P.f64.alloc_pooled(G * 8ull * n_f64))) return rc;
@@ -1101,7 +1248,9 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   uint8_t* dS = (uint8_t*)scratch.p;
   for (const Patch& p : patches) {
     LeafDesc& dl = leaves[p.leaf_index];
-    dl.aux = (const uint32_t*)((p.in_arena ? dA : dS) + p.off);
+    const uint32_t* ptr = (const uint32_t*)((p.in_arena ? dA : dS) + p.off);
+    if (p.words) dl.words = ptr;
+    else dl.aux = ptr;
   }
   for (uint32_t si = 0; si < S; si++) {
     segd[si].leaves = (const LeafDesc*)(dA + off_leaves) + (uint64_t)si * L;

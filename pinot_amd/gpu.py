@@ -19,7 +19,7 @@ from .query import QueryContext, parse
 from .segment import Column, ImmutableSegment
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpinot_gpu.so")
+LIB_PATH = os.environ.get("PINOT_GPU_LIB", os.path.join(_HERE, "libpinot_gpu.so"))
 _lib = None
 _lib_lock = threading.Lock()
 

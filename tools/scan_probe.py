@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Dev tool: decompose scan-kernel time over query shapes on synthetic AdAnalytics segments (device-generated).
+
+usage: python tools/scan_probe.py [--segments 32] [--reps 5]
+Prints one line per query: scan kernel ms (HIP events), rows/s of the kernel, matched docs."""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--segments", type=int, default=32)
+    ap.add_argument("--rows", type=int, default=7_812_500)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    from pinot_amd import synth
+    from pinot_amd.gpu import GpuEngine
+    from pinot_amd.plan import Table
+    from pinot_amd.query import parse
+    from pinot_amd.segment import ImmutableSegment
+    eng = GpuEngine(0)
+    segs = []
+    table = None
+    for s in range(args.segments):
+        dcs = synth.make_columns_torch(synth.ADANALYTICS, s, args.rows, torch.device("cuda"))
+        seg = ImmutableSegment(f"a{s}", args.rows, {dc.spec.name: dc.meta_column() for dc in dcs})
+        segs.append(seg)
+        if table is None:
+            table = Table("adAnalytics", [seg])
+        eng.register_device_segment(seg, table, dcs)
+    table = Table("adAnalytics", segs)
+    ids = ", ".join(str((i * 7919 + 13) % 1_000_000) for i in range(1000))
+    qs = {
+        "count": "SELECT COUNT(*) FROM t",
+        "in_only": f"SELECT COUNT(*) FROM t WHERE accountId IN ({ids})",
+        "range_only": "SELECT COUNT(*) FROM t WHERE daysSinceEpoch BETWEEN 18000 AND 18089",
+        "range_acct": "SELECT COUNT(*) FROM t WHERE accountId BETWEEN 1000 AND 500000",
+        "sum_dense": "SELECT SUM(clicks) FROM t",
+        "gb_dense": "SELECT daysSinceEpoch, SUM(clicks) FROM t GROUP BY daysSinceEpoch",
+        "config2": synth.adanalytics_query(1000),
+    }
+    rows = args.segments * args.rows
+    for name, sql in qs.items():
+        if args.only and name not in args.only.split(","):
+            continue
+        plan = eng.make_plan(table, parse(sql))
+        r = eng.run_plan(plan)
+        ks = []
+        t0 = time.perf_counter()
+        for _ in range(args.reps):
+            r = eng.run_plan(plan)
+            ks.append(eng.last_timing().scan_ms)
+        wall = (time.perf_counter() - t0) / args.reps * 1e3
+        k = float(np.median(ks))
+        print(f"{name:12s} scan {k:8.3f} ms  {rows / k / 1e6:9.3f} Grows/s  wall {wall:8.3f} ms  "
+              f"matched {r.stats.num_docs_scanned}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
