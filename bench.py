@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--cpu-sample-segments", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "scan_traffic.json"),
+                    help="PMC HBM traffic of the scan kernel for this workload (tools/profile_bench.sh)")
     args = ap.parse_args()
 
     import numpy as np
@@ -150,6 +152,17 @@ def main():
         d = eng.run_plan(dplan)
         parity = bool(d.rows == o.rows and d.stats.num_docs_scanned == o.stats.num_docs_scanned)
 
+    traffic = traffic_bytes = None
+    try:  # measured by rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same command (tools/profile_bench.sh)
+        tj = json.load(open(args.traffic_file))
+        tc = tj.get("config") or {}
+        if (tc.get("rows_per_gpu") == args.segments * args.rows and tc.get("in_list_size") == args.in_ids
+                and tj.get("traffic_bytes_per_launch")):
+            traffic_bytes = float(tj["traffic_bytes_per_launch"])
+            traffic = traffic_bytes / (scan_avg_ms * 1e-3) / 1e9
+    except (OSError, ValueError):
+        pass
+
     if rank == 0:
         out = {
             "metric": "rows/sec for filter+group-by SUM over 1B rows; % of HBM roofline, 1–8 GPUs",
@@ -161,8 +174,9 @@ def main():
                        "rows_per_gpu": rows_per_gpu, "segments_per_gpu": args.segments,
                        "rows_per_segment": args.rows, "in_list_size": args.in_ids, "parallelism": f"segments x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "scan_kernel", "kernel_ms": scan_avg_ms, "algorithmic_bytes": alg_bytes},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "scan_kernel", "kernel_ms": scan_avg_ms, "algorithmic_bytes": alg_bytes,
+                         "traffic_bytes_per_launch": traffic_bytes},
             "cpu_baseline": cpu,
             "parity_sample": parity,
             "groups": len(res.rows), "docs_matched": res.stats.num_docs_scanned, "datagen_s": round(gen_s, 1),
