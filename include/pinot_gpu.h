@@ -266,13 +266,18 @@ int pg_partials_copy(pg_partials *p, int dir, void *i64, void *f64, void *mn, vo
 
 /* ---------------------------------------------------------------- measurement hooks */
 
-/* Device time (ms, HIP events on the execution stream) of the last pg_execute* on this thread,
- * split into the filter-materialisation pre-pass and the fused scan/aggregate kernel. */
+/* Timing of the last pg_execute* / pg_partials_finalize on this thread.  Device time (ms, HIP events on the
+ * execution stream): the filter-materialisation pre-pass, the fused scan/aggregate kernel, the state read-back.
+ * Host wall time (ms, steady clock): plan compile up to the scan launch, the whole execute call, the finalize
+ * (read-back + decode) call. */
 typedef struct pg_timing {
   float prepass_ms;
   float scan_ms;
   float finalize_ms;
   uint32_t scan_launches;
+  float host_compile_ms;
+  float execute_wall_ms;
+  float finalize_wall_ms;
   uint32_t pad;
 } pg_timing;
 int pg_last_timing(pg_timing *out);

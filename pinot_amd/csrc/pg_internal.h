@@ -34,20 +34,28 @@ constexpr int kMaxLeaves = 24;
 constexpr int kMaxOps = 64;
 constexpr int kMaxDepth = 4;                         // filter tree nesting (open groups)
 constexpr int kLdsGroupBytes = 32 * 1024;            // LDS-privatised group table budget
-constexpr int kLdsSetBytes = 16 * 1024;              // LDS hash sets of IN / NOT_IN leaves
-constexpr int kLdsStageBytes = 32 * 1024;            // LDS tiles of densely read packed columns
+constexpr int kLdsSetBytes = 16 * 1024;              // LDS filter bitmaps of IN / NOT_IN leaves
+constexpr int kLdsStageBytes = 32 * 1024;            // LDS tiles of densely read packed columns (per ring buffer)
 constexpr int kMaxStaged = 6;                        // packed columns staged per tile
 constexpr int kNoSlot = 255;
 
 // Filter program as the kernel runs it: a tree in prefix form (host-compiled from the ABI's postfix program,
 // AND children ordered most-selective first so later children are evaluated only on surviving docs).
 constexpr int32_t kOpAnd = -1, kOpOr = -2, kOpNot = -3, kOpEnd = -4;  // >= 0: leaf index
+enum GroupType : uint32_t { GT_ROOT = 0, GT_AND = 1, GT_OR = 2, GT_NOT = 3 };
+
+// Compaction queue (QuerySpec::queue_mode): docs that pass the staged (phase A) children of a root AND are appended
+// to a per-block LDS queue; the remaining children and the aggregation run over the queue once it holds at least
+// kQueueFlush docs (every lane busy) instead of over a few docs per tile.
+constexpr int kQueueRows = 4;
+constexpr int kQueueCap = kBlock * kQueueRows;       // 1024 docs
+constexpr int kQueueFlush = kBlock * 2;              // flush at >= 512 queued docs
 
 enum LeafKind : uint32_t {
   LK_ALL = 0,        // match all
   LK_NONE = 1,       // match none
   LK_RANGE = 2,      // dictId in [lo,hi), dictIds unpacked from a packed SV forward index
-  LK_SET_LDS = 3,    // dictId in set: LDS filter bitmap (+ exact hash table) staged per segment
+  LK_SET_LDS = 3,    // dictId in set: LDS filter bitmap staged per segment (+ exact global LUT when coarse)
   LK_SET_LUT = 4,    // dictId in set: bit dictId of `aux` (global LSB-first words)
   LK_DOCRANGE = 6    // doc id in [lo,hi)
 };
@@ -61,14 +69,13 @@ struct LeafDesc {
   uint32_t bits;
   uint32_t wbytes;        // bytes of `words` (buffer-descriptor range)
   // SET_LDS: an LDS region of `set_ints` words at `lds_off`: a filter bitmap of `nbw` words over dictId >> shift
-  // (LSB-first), followed, when shift > 0, by an exact open-addressing hash table of 1 << set_log2 int32 slots
-  // (empty = -1) that resolves the bitmap's candidates.  shift == 0: the bitmap is exact.
+  // (LSB-first).  shift == 0: the bitmap is exact; else its candidates are resolved by bit dictId of `lut`
+  // (global, LSB-first words, built per query by set_lut_bits).
   uint32_t lds_off;
   uint32_t set_ints;
   uint32_t shift;
   uint32_t nbw;
-  uint32_t set_log2;
-  uint32_t pad;
+  const uint32_t* lut;
 };
 
 // A column as read by aggregation inputs and group keys.
@@ -112,13 +119,13 @@ struct AggSpec {
   uint64_t flag_off;  // DISTINCTCOUNT: byte offset of this agg's flags within a slot's flag row
 };
 
-// A packed column staged per tile into LDS (coalesced 16-byte loads of the tile's whole word range) because
+// A packed column staged per tile into LDS (LDS-DMA of the tile's whole word range in 1 KiB pieces) because
 // most of its cache lines are needed anyway; every other read of a packed column is a per-doc gather.
 // Source = the words of a leaf (role 0), an aggregation operand (role 1) or a group key (role 2) of the current
 // segment.  Slots are uniform across segments; `lds_words` is sized for the widest bitsPerElement.
 struct StagedCol {
   uint32_t role, idx, operand;
-  uint32_t lds_word_off;     // offset of this slot in the staging region (uint32 words)
+  uint32_t lds_word_off;     // offset of this slot in a staging buffer (uint32 words, multiple of 256)
 };
 
 struct QuerySpec {
@@ -127,7 +134,11 @@ struct QuerySpec {
   uint32_t use_lds;          // group table privatised in LDS
   uint32_t set_lds_ints;     // int32 slots of LDS hash sets per block
   uint32_t num_staged;
-  uint32_t stage_lds_words;  // uint32 words of the staging region
+  uint32_t stage_lds_words;  // uint32 words of one staging buffer (a multiple of 256: 1 KiB DMA pieces)
+  uint32_t stage_ring;       // staging buffers (2: the next tile is copied while the current one is evaluated)
+  uint32_t queue_mode;       // phase A per tile -> LDS queue -> phase B per flush (see kQueueCap)
+  uint32_t opA_begin, opA_end, opA_type;  // phase A ops (the whole program as GT_ROOT when queue_mode == 0)
+  uint32_t opB_begin, opB_end;            // phase B ops: the root AND's remaining children
   StagedCol staged[kMaxStaged];
   uint8_t leaf_slot[kMaxLeaves];     // staged slot of each leaf's column or kNoSlot
   uint8_t agg_slot[kMaxAggs][2];     // staged slot of each aggregation operand or kNoSlot
@@ -165,14 +176,11 @@ __host__ __device__ inline double order_key_decode(int64_t k) {
   return v;
 }
 
-// IN-list hash: home slot of dictId `id` in a table of 2^log2 slots (shared by the host builder and the kernel)
-__host__ __device__ inline uint32_t set_hash(uint32_t id, uint32_t log2) {
-  return log2 ? (uint32_t)(id * 0x9E3779B1u) >> (32 - log2) : 0u;
-}
 
 // ---- kernel launchers
 hipError_t launch_scan(const QuerySpec& q, uint32_t blocks, hipStream_t s);                  // pg_scan.hip
 size_t scan_lds_bytes(const QuerySpec& q);
+uint32_t scan_min_blocks_per_cu();
 hipError_t launch_init_state(const QuerySpec& q, hipStream_t s);                             // pg_kernels.hip
 hipError_t launch_bswap_words(const uint8_t* src, uint32_t* dst, uint64_t nbytes, uint64_t nwords_out, hipStream_t s);
 hipError_t launch_be_to_native(const uint8_t* src, void* dst, uint64_t n, uint32_t width, hipStream_t s);

@@ -68,6 +68,12 @@ hipStream_t thread_stream() {
   return s;
 }
 
+double wall_ms() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
 int64_t now_ms() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -656,6 +662,7 @@ thread_local ThreadCtx t_ctx;
 bool pl_too_big(uint32_t ints) { return ints * 4ull > (uint64_t)kLdsSetBytes; }
 
 int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
+  const double t_enter = wall_ms();
   if (!plan) return fail(PG_E_INVALID, "null plan");
   if (plan->abi_version != PG_ABI_VERSION) return fail(PG_E_INVALID, "ABI version %u != %u", plan->abi_version, PG_ABI_VERSION);
   if (plan->num_aggs > (uint32_t)kMaxAggs) return fail(PG_E_UNSUPPORTED, "more than %d aggregations", kMaxAggs);
@@ -846,16 +853,12 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   // bitmap over dictIds built on the device (one batched launch).
   // Per leaf: LDS words of its IN-set region (uniform across segments), 0 = gathered through a global LUT.
   // Region = filter bitmap over dictId >> shift (<= 8 KB) + (shift > 0) an exact hash table (<= 50 % full).
-  auto set_geometry = [](uint32_t card, uint32_t n_ids, uint32_t& shift, uint32_t& nbw, uint32_t& lg) {
+  // LDS filter bitmap over dictId >> shift: at most kLdsSetBytes (shift > 0 adds an exact global LUT)
+  auto set_geometry = [](uint32_t card, uint32_t& shift, uint32_t& nbw) {
     shift = 0;
-    while (((card + (1u << shift) - 1) >> shift) > 65536u) shift++;
+    while (((card + (1u << shift) - 1) >> shift) > (uint32_t)(kLdsSetBytes * 8 - 32)) shift++;
     nbw = (((card + (1u << shift) - 1) >> shift) + 31) / 32 + 1;
-    lg = 0;
-    if (shift) {
-      lg = 1;
-      while ((1u << lg) < 2 * n_ids) lg++;
-    }
-    return nbw + (shift ? (1u << lg) : 0u);
+    return nbw;
   };
   std::vector<uint32_t> set_ints(L, 0), set_off(L, 0);
   std::vector<double> leaf_pass(L, 0.0), leaf_cost(L, 0.0), leaf_reach(L, 0.0);
@@ -867,8 +870,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
         if (pl.kind != PG_LEAF_SV_SCAN || pl.num_ids == 0) continue;
         const ColumnRes* c = col(si, pl.col_id);
         if (!c) continue;
-        uint32_t sh, nbw, lg;
-        set_ints[li] = std::max(set_ints[li], set_geometry(std::max(c->card, 1u), pl.num_ids, sh, nbw, lg));
+        uint32_t sh, nbw;
+        set_ints[li] = std::max(set_ints[li], set_geometry(std::max(c->card, 1u), sh, nbw));
       }
     uint32_t used = 0;
     for (uint32_t li = 0; li < L; li++) {
@@ -935,7 +938,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   auto scratch_reserve = [&](uint64_t n) { uint64_t at = (scratch_bytes + 255) & ~255ull; scratch_bytes = at + n; return at; };
   uint64_t entries_in_filter = 0;
   // device pointers into arena / scratch are patched once those are allocated
-  struct Patch { uint64_t leaf_index; uint64_t off; bool in_arena; bool words; };
+  enum PatchTarget { PT_AUX = 0, PT_WORDS = 1, PT_LUT = 2 };
+  struct Patch { uint64_t leaf_index; uint64_t off; bool in_arena; int target; };
   std::vector<Patch> patches;
 
   for (uint32_t si = 0; si < S; si++) {
@@ -976,30 +980,25 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
             dl.hi = std::max(std::min(hi, (int32_t)c->card), dl.lo);
           } else if (set_ints[li]) {
             dl.kind = LK_SET_LDS;
-            const uint32_t n_region = set_geometry(std::max(c->card, 1u), pl.num_ids, dl.shift, dl.nbw, dl.set_log2);
+            const uint32_t n_region = set_geometry(std::max(c->card, 1u), dl.shift, dl.nbw);
             std::vector<uint32_t> region(n_region, 0);
             for (uint32_t i = 0; i < pl.num_ids; i++) {
               const uint32_t x = (uint32_t)pl.ids[i] >> dl.shift;
               region[x >> 5] |= 1u << (x & 31u);
             }
-            if (dl.shift) {
-              const uint32_t n = 1u << dl.set_log2;
-              int32_t* tab = (int32_t*)&region[dl.nbw];
-              for (uint32_t i = 0; i < n; i++) tab[i] = -1;
-              for (uint32_t i = 0; i < pl.num_ids; i++) {
-                uint32_t h = set_hash((uint32_t)pl.ids[i], dl.set_log2);
-                while (tab[h] >= 0) h = (h + 1) & (n - 1);
-                tab[h] = pl.ids[i];
-              }
-            }
             dl.set_ints = n_region;
             dl.lds_off = set_off[li];
-            patches.push_back({(uint64_t)si * L + li, ar.put(region.data(), 4ull * n_region), true, false});
+            patches.push_back({(uint64_t)si * L + li, ar.put(region.data(), 4ull * n_region), true, PT_AUX});
+            if (dl.shift) {  // exact LUT resolving the bitmap's candidates
+              const uint64_t lut_off = scratch_reserve(4ull * ((c->card + 31) / 32 + 1));
+              luts.push_back({ar.put(pl.ids, 4ull * pl.num_ids), pl.num_ids, lut_off});
+              patches.push_back({(uint64_t)si * L + li, lut_off, false, PT_LUT});
+            }
           } else {
             dl.kind = LK_SET_LUT;
             const uint64_t lut_off = scratch_reserve(4ull * ((c->card + 31) / 32 + 1));
             luts.push_back({ar.put(pl.ids, 4ull * pl.num_ids), pl.num_ids, lut_off});
-            patches.push_back({(uint64_t)si * L + li, lut_off, false, false});
+            patches.push_back({(uint64_t)si * L + li, lut_off, false, PT_AUX});
           }
           break;
         }
@@ -1033,7 +1032,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
           op.n = (uint32_t)(rg.size() / 2);
           op.num_docs = sr.num_docs;
           op.out_off = scratch_reserve(4ull * ((sr.num_docs + 31) / 32 + 1));
-          patches.push_back({(uint64_t)si * L + li, op.out_off, false, true});
+          patches.push_back({(uint64_t)si * L + li, op.out_off, false, PT_WORDS});
           pre.push_back(op);
           break;
         }
@@ -1057,7 +1056,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
           op.col = c;
           op.negate = pl.exclusive != 0;
           op.out_off = scratch_reserve(4ull * ((sr.num_docs + 31) / 32 + 1));
-          patches.push_back({(uint64_t)si * L + li, op.out_off, false, true});
+          patches.push_back({(uint64_t)si * L + li, op.out_off, false, PT_WORDS});
           pre.push_back(op);
           break;
         }
@@ -1077,7 +1076,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
             luts.push_back({ar.put(pl.ids, 4ull * pl.num_ids), pl.num_ids, op.lut_off});
           }
           op.out_off = scratch_reserve(4ull * ((sr.num_docs + 31) / 32 + 1));
-          patches.push_back({(uint64_t)si * L + li, op.out_off, false, true});
+          patches.push_back({(uint64_t)si * L + li, op.out_off, false, PT_WORDS});
           pre.push_back(op);
           break;
         }
@@ -1170,7 +1169,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
     for (const Cand& c : cands) {
       if (no_stage || q.num_staged >= (uint32_t)kMaxStaged) break;
       if (c.reach * 1024.0 / c.bmax < 1.0) continue;
-      const uint32_t need = (uint32_t)(kTileDocs / 32) * c.bmax + 4;
+      const uint32_t need = (uint32_t)(kTileDocs / 32) * c.bmax;  // b DMA pieces of 1 KiB
       if ((words + need) * 4ull > (uint64_t)kLdsStageBytes) continue;
       const uint32_t slot = q.num_staged++;
       q.staged[slot] = {c.role, c.idx, c.operand, words};
@@ -1212,6 +1211,49 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
     }
     q.stage_lds_words = words;
   }
+  // ---- compaction queue: when the staged children of a root AND (phase A) pass few docs, the rest of the filter
+  // and the aggregation (phase B) run over an LDS queue of their survivors, a full block of docs at a time,
+  // instead of over the few survivors of each tile
+  q.opA_begin = 0;
+  q.opA_end = q.num_ops;
+  q.opA_type = GT_ROOT;
+  q.opB_begin = q.opB_end = 0;
+  q.queue_mode = 0;
+  if (q.num_ops && q.num_staged) {
+    uint32_t a0 = 0, a1 = 0, type = GT_ROOT, b0 = 0, b1 = 0;
+    double pass_a = 1.0;
+    if (q.ops[0] >= 0) {
+      if (q.leaf_slot[q.ops[0]] != kNoSlot) { a0 = 0; a1 = 1; pass_a = leaf_pass[q.ops[0]]; }
+    } else if (q.ops[0] == kOpAnd) {
+      uint32_t i = 1;
+      while (i + 1 < q.num_ops && q.ops[i] >= 0 && q.leaf_slot[q.ops[i]] != kNoSlot) pass_a *= leaf_pass[q.ops[i++]];
+      if (i > 1) { a0 = 1; a1 = i; type = GT_AND; b0 = i; b1 = q.num_ops - 1; }
+    }
+    bool agg_staged = false;
+    for (uint32_t a = 0; a < A; a++) agg_staged |= q.agg_slot[a][0] != kNoSlot || q.agg_slot[a][1] != kNoSlot;
+    for (uint32_t k = 0; k < K; k++) agg_staged |= q.key_slot[k] != kNoSlot;
+    const bool work_after = b1 > b0 || K > 0 || q.agg_reads;
+    static const char* queue_env = getenv("PG_QUEUE");
+    const bool want = queue_env ? atoi(queue_env) != 0 : pass_a <= 1.0 / 16;
+    if (a1 > a0 && !agg_staged && work_after && want) {
+      q.queue_mode = 1;
+      q.opA_begin = a0;
+      q.opA_end = a1;
+      q.opA_type = type;
+      q.opB_begin = b0;
+      q.opB_end = b1;
+      for (uint32_t i = b0; i < b1; i++)  // phase B reads queued docs by gather only
+        if (q.ops[i] >= 0) q.leaf_slot[q.ops[i]] = kNoSlot;
+    }
+  }
+  {
+    // two staging buffers (the copy of the next tile overlaps the current one) only when LDS still allows as many
+    // blocks per CU as the register budget does (PG_SCAN_MIN_WAVES); else one.  PG_STAGE_RING=1|2 overrides.
+    static const char* ring_env = getenv("PG_STAGE_RING");
+    q.stage_ring = 2;
+    const bool fits = q.num_staged && scan_lds_bytes(q) * (size_t)scan_min_blocks_per_cu() <= 160 * 1024;
+    q.stage_ring = ring_env ? (atoi(ring_env) > 1 ? 2 : 1) : (fits ? 2 : 1);
+  }
   const size_t lds_bytes = scan_lds_bytes(q);
   if (lds_bytes > 160 * 1024) return fail(PG_E_UNSUPPORTED, "scan needs %zu bytes of LDS", lds_bytes);
 
@@ -1249,7 +1291,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   for (const Patch& p : patches) {
     LeafDesc& dl = leaves[p.leaf_index];
     const uint32_t* ptr = (const uint32_t*)((p.in_arena ? dA : dS) + p.off);
-    if (p.words) dl.words = ptr;
+    if (p.target == PT_WORDS) dl.words = ptr;
+    else if (p.target == PT_LUT) dl.lut = ptr;
     else dl.aux = ptr;
   }
   for (uint32_t si = 0; si < S; si++) {
@@ -1305,6 +1348,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
     static int per_cu = 0;
     if (!per_cu) { const char* e = getenv("PG_SCAN_BLOCKS_PER_CU"); per_cu = e ? std::max(1, atoi(e)) : 8; }
     blocks = (uint32_t)std::min<uint64_t>(q.num_items, (uint64_t)dev_cus * per_cu);
+    t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
     HIP_CHECK(launch_scan(q, blocks, s));
   }
   HIP_CHECK(hipEventRecord(ev[2], s));
@@ -1336,6 +1380,11 @@ struct PartialsImpl {
 };
 
 int finalize(pg_partials* pp, const pg_plan* plan, pg_result** out) {
+  const double t0 = wall_ms();
+  struct Stamp {
+    double t0;
+    ~Stamp() { t_timing.finalize_wall_ms = (float)(wall_ms() - t0); }
+  } stamp{t0};
   PartialsImpl* impl = (PartialsImpl*)pp->impl;
   Partials& P = impl->P;
   const uint64_t G = pp->num_slots;
@@ -1482,8 +1531,11 @@ int pg_execute_partial(const pg_plan* plan, pg_partials** out) {
   PartialsImpl* impl = new (std::nothrow) PartialsImpl();
   if (!impl) return fail(PG_E_NOMEM, "out of host memory");
   pg_stats st;
+  const double t0 = wall_ms();
+  t_timing.host_compile_ms = 0;
   try {
     rc = compile_and_run(plan, impl->P, st);
+    t_timing.execute_wall_ms = (float)(wall_ms() - t0);
   } catch (const std::exception& e) {
     rc = fail(PG_E_NOMEM, "execute failed: %s", e.what());
   }

@@ -32,8 +32,24 @@
 namespace pg {
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+// The per-query descriptors (arena) are read-only for the whole launch: reading them through the constant address
+// space lets the compiler use scalar loads (the kernel's own atomics would otherwise force vector loads and full
+// vmcnt drains).  Per-doc data (dictionaries, LUTs, keymaps, MV offsets) is read through the global address space.
+#define PG_CONST __attribute__((address_space(4)))
+#define PG_GLOBAL __attribute__((address_space(1)))
+// p[i] of a read-only descriptor array, loaded word by word through the constant address space
+template <class T> __device__ __forceinline__ T ldc(const T* p, uint64_t i) {
+  static_assert(sizeof(T) % 4 == 0, "descriptor size");
+  const PG_CONST uint32_t* src = (const PG_CONST uint32_t*)(p + i);
+  T v;
+  uint32_t* dst = (uint32_t*)&v;
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(T) / 4); k++) dst[k] = src[k];
+  return v;
+}
+template <class T> __device__ __forceinline__ const PG_GLOBAL T* glb(const T* p) { return (const PG_GLOBAL T*)p; }
 constexpr uint32_t kRowMask = 0xFFFFFFFFu;                     // kRows == 32
-constexpr int kStageJobs = kLdsStageBytes / (16 * kBlock);      // 16-byte staging loads per thread per tile
 static_assert(kRows == 32, "masks are 32-bit");
 
 // Buffer descriptor of a packed column; built from readfirstlane'd (wave-uniform) values so it lives in SGPRs.
@@ -58,38 +74,42 @@ __device__ __forceinline__ uint32_t unpack(rsrc_t r, uint32_t idx, uint32_t b) {
   return (uint32_t)(win >> (64u - sh - b)) & bits_mask(b);
 }
 
-// The same from a staged tile in LDS: `rel` = doc - tile base.
+// The same from a staged tile in LDS, addressed by the value's LAST bit e = rel*b + b - 1: the 64-bit window
+// (st[k-1], st[k]) with k = e >> 5 holds the value in its low 32 + (e & 31) + 1 bits, so one v_alignbit by
+// 31 - (e & 31) (= ~e mod 32) right-aligns it.  st[-1] is readable (the ring starts 16 bytes into LDS) and
+// only ever contributes bits that the mask drops.
+__device__ __forceinline__ uint32_t unpack_end(const uint32_t* st, uint32_t e, uint32_t mask) {
+  const uint32_t k = e >> 5;
+  return __builtin_amdgcn_alignbit(st[k - 1], st[k], ~e) & mask;
+}
 __device__ __forceinline__ uint32_t unpack_lds(const uint32_t* st, uint32_t rel, uint32_t b) {
-  const uint32_t p = rel * b;
-  const uint32_t w = p >> 5, sh = p & 31u;
-  const uint64_t win = ((uint64_t)st[w] << 32) | (uint64_t)st[w + 1];
-  return (uint32_t)(win >> (64u - sh - b)) & bits_mask(b);
+  return unpack_end(st, rel * b + b - 1u, bits_mask(b));
 }
 
 // Dictionary reads clamp the dictId to the dictionary: valid data never needs it, and a corrupt forward index
 // then yields wrong values (caught by parity checks) instead of an out-of-bounds access.
-__device__ __forceinline__ double dict_double(const ColDesc& c, uint32_t id) {
+__device__ __forceinline__ double dict_double(const ColDesc c, uint32_t id) {
   id = min(id, c.card - 1u);
   switch (c.dtype) {
-    case PG_INT: return (double)((const int32_t*)c.dict)[id];
-    case PG_LONG: return (double)((const int64_t*)c.dict)[id];
-    case PG_FLOAT: return (double)((const float*)c.dict)[id];
-    default: return ((const double*)c.dict)[id];
+    case PG_INT: return (double)glb((const int32_t*)c.dict)[id];
+    case PG_LONG: return (double)glb((const int64_t*)c.dict)[id];
+    case PG_FLOAT: return (double)glb((const float*)c.dict)[id];
+    default: return glb((const double*)c.dict)[id];
   }
 }
 
-__device__ __forceinline__ int64_t dict_i64(const ColDesc& c, uint32_t id) {
+__device__ __forceinline__ int64_t dict_i64(const ColDesc c, uint32_t id) {
   id = min(id, c.card - 1u);
-  return c.dtype == PG_INT ? (int64_t)((const int32_t*)c.dict)[id] : ((const int64_t*)c.dict)[id];
+  return c.dtype == PG_INT ? (int64_t)glb((const int32_t*)c.dict)[id] : glb((const int64_t*)c.dict)[id];
 }
 
 // TransformFunction value of an aggregation input from its (already unpacked) dictIds.
 // MultiplicationTransformFunction.transformToDoubleValuesSV (transform/function/MultiplicationTransformFunction.java:91-111):
 // start from the literal product 1.0, multiply arguments in order; compiled with -ffp-contract=off.
 __device__ __forceinline__ double value_f64(const AggSpec& a, const ColDesc* c, uint32_t ia, uint32_t ib) {
-  const double va = dict_double(c[0], ia);
+  const double va = dict_double(ldc(c, 0), ia);
   if (a.op == PG_EXPR_COL) return va;
-  const double vb = dict_double(c[1], ib);
+  const double vb = dict_double(ldc(c, 1), ib);
   switch (a.op) {
     case PG_EXPR_MUL: return (1.0 * va) * vb;
     case PG_EXPR_ADD: return va + vb;
@@ -99,9 +119,9 @@ __device__ __forceinline__ double value_f64(const AggSpec& a, const ColDesc* c, 
 
 // integer-exact path (host proved |partial sums| < 2^62): identical to the double path while < 2^53
 __device__ __forceinline__ int64_t value_i64(const AggSpec& a, const ColDesc* c, uint32_t ia, uint32_t ib) {
-  const int64_t va = dict_i64(c[0], ia);
+  const int64_t va = dict_i64(ldc(c, 0), ia);
   if (a.op == PG_EXPR_COL) return va;
-  const int64_t vb = dict_i64(c[1], ib);
+  const int64_t vb = dict_i64(ldc(c, 1), ib);
   switch (a.op) {
     case PG_EXPR_MUL: return va * vb;
     case PG_EXPR_ADD: return va + vb;
@@ -110,9 +130,9 @@ __device__ __forceinline__ int64_t value_i64(const AggSpec& a, const ColDesc* c,
 }
 
 // table-global key id of dictId `id` (~0 when the id is outside the dictionary: rejected by the caller)
-__device__ __forceinline__ uint64_t key_of(uint32_t kind, int64_t base, const ColDesc& c, uint32_t id) {
+__device__ __forceinline__ uint64_t key_of(uint32_t kind, int64_t base, const ColDesc c, uint32_t id) {
   if (id >= c.card) return ~0ull;
-  return kind == PG_KEY_KEYMAP ? (uint64_t)(uint32_t)c.keymap[id] : (uint64_t)(dict_i64(c, id) - base);
+  return kind == PG_KEY_KEYMAP ? (uint64_t)(uint32_t)glb(c.keymap)[id] : (uint64_t)(dict_i64(c, id) - base);
 }
 
 __device__ __forceinline__ uint32_t agg_ncols(const AggSpec& A) {
@@ -121,133 +141,175 @@ __device__ __forceinline__ uint32_t agg_ncols(const AggSpec& A) {
   return A.op == PG_EXPR_COL ? 1u : 2u;
 }
 
-// IN-list membership in the exact LDS open-addressing table (<= 50 % full, empty = -1).
-__device__ __forceinline__ bool set_contains(const int32_t* tab, uint32_t log2, uint32_t id) {
-  const uint32_t mask = (1u << log2) - 1u;
-  uint32_t h = set_hash(id, log2);
-  int32_t v = tab[h];
-  for (uint32_t probe = 0; probe <= mask; probe++) {
-    if (v == (int32_t)id) return true;
-    if (v < 0) return false;
-    h = (h + 1) & mask;
-    v = tab[h];
-  }
-  return false;
-}
-
-// IN-set filter bitmap test (exact when shift == 0, else a candidate test resolved by set_contains).
+// IN-set filter bitmap test (exact when shift == 0, else a candidate test resolved by the global LUT).
 __device__ __forceinline__ uint32_t set_bit(const uint32_t* bm, uint32_t shift, uint32_t v) {
   const uint32_t x = v >> shift;
   return (bm[x >> 5] >> (x & 31u)) & 1u;
 }
 
 // Leaf predicate on a dictId (doc bitmaps: RANGE [1,2) on a 1-bit column).
-__device__ __forceinline__ bool leaf_pred(const LeafDesc& L, const int32_t* lds_sets, uint32_t v) {
+__device__ __forceinline__ bool leaf_pred(const LeafDesc L, const int32_t* lds_sets, uint32_t v) {
   switch (L.kind) {
     case LK_RANGE: return (v - (uint32_t)L.lo) < (uint32_t)(L.hi - L.lo);
     case LK_SET_LDS: {
       const uint32_t* bm = (const uint32_t*)(lds_sets + L.lds_off);
       if (!set_bit(bm, L.shift, v)) return false;
-      return L.shift == 0 || set_contains((const int32_t*)bm + L.nbw, L.set_log2, v);
+      return L.shift == 0 || ((glb(L.lut)[v >> 5] >> (v & 31u)) & 1u);
     }
-    default: return (L.aux[v >> 5] >> (v & 31u)) & 1u;  // LK_SET_LUT
+    default: return (glb(L.aux)[v >> 5] >> (v & 31u)) & 1u;  // LK_SET_LUT
   }
 }
 
-// Per-tile staging of the packed columns the host chose (QuerySpec::staged): coalesced 16-byte loads of each
-// column's word range for the tile into registers, then into LDS.  Slot geometry of the current segment.
-struct StageSrc {
-  const uint32_t* words[kMaxStaged];
-  uint32_t nwords[kMaxStaged];     // words in the column (loads past it read zeros)
-  uint32_t bits[kMaxStaged];
-};
+// LDS-DMA of 16 bytes per lane (buffer_load_dwordx4 ... lds): the wave's 64 lanes fill 1 KiB of LDS at `dst`
+// (wave-uniform) from byte offsets `voff` of the column; reads past the descriptor's range return zeros.
+__device__ __forceinline__ void dma16(rsrc_t r, uint32_t* dst, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)dst, 16, voff, 0, 0, 0);
+}
 
-__device__ __forceinline__ void stage_tile(const QuerySpec& q, const StageSrc& src, uint32_t tile, uint32_t* lds,
-                                           int tid) {  // `src` lives in LDS (keeps SGPRs free)
-  uint4 buf[kStageJobs];
-  uint32_t dst[kStageJobs];  // LDS word offset of each 16-byte job (~0: none)
-#pragma unroll
-  for (int k = 0; k < kStageJobs; k++) {
-    buf[k] = make_uint4(0, 0, 0, 0);
-    dst[k] = 0xFFFFFFFFu;
-    const uint32_t qi = (uint32_t)(tid + k * kBlock);  // quad index within the concatenated slot tiles
-    uint32_t q0 = 0;
-#pragma unroll
-    for (int s = 0; s < kMaxStaged; s++) {
-      if (s < (int)q.num_staged) {
-        const uint32_t nq = (uint32_t)(kTileDocs / 128) * src.bits[s] + 1;  // 16-byte quads of this slot's tile
-        if (qi >= q0 && qi < q0 + nq) {
-          const uint32_t local = qi - q0;
-          dst[k] = q.staged[s].lds_word_off + local * 4;
-          const uint32_t w = tile * (uint32_t)(kTileDocs / 32) * src.bits[s] + local * 4;
-          if (src.words[s] && w < src.nwords[s]) {
-            if (w + 4 <= src.nwords[s]) {
-              buf[k] = *(const uint4*)(src.words[s] + w);
-            } else {
-              uint32_t t[4] = {0, 0, 0, 0};
-              for (uint32_t x = 0; x < 4 && w + x < src.nwords[s]; x++) t[x] = src.words[s][w + x];
-              buf[k] = make_uint4(t[0], t[1], t[2], t[3]);
-            }
-          }
-        }
-        q0 += nq;
-      }
+// Words / bits of staged slot `s` in segment `sd` (nullptr: the segment's form of the leaf reads no column).
+__device__ __forceinline__ const uint32_t* staged_src(const QuerySpec& q, const SegDesc& sd, uint32_t s,
+                                                      uint32_t& bytes, uint32_t& bits) {
+  const StagedCol& sc = q.staged[s];
+  if (sc.role == 0) {
+    const LeafDesc L = ldc(sd.leaves, sc.idx);
+    bytes = L.wbytes;
+    bits = L.bits;
+    return (L.kind == LK_RANGE || L.kind == LK_SET_LDS || L.kind == LK_SET_LUT) ? L.words : nullptr;
+  }
+  const ColDesc c = sc.role == 1 ? ldc(sd.aggcols, 2 * sc.idx + sc.operand) : ldc(sd.keycols, sc.idx);
+  bytes = c.wbytes;
+  bits = c.bits;
+  return c.words;
+}
+
+// Issue the asynchronous copy of tile `tile` of every staged column into the LDS buffer `buf`: the tile's
+// 256*b words as b pieces of 1 KiB, pieces dealt round-robin to the 4 waves.  Control
+// flow is wave-uniform; nothing waits here (the consumer's barrier drains vmcnt).
+__device__ __forceinline__ void stage_issue(const QuerySpec& q, const SegDesc& sd, uint32_t tile, uint32_t* buf,
+                                            uint32_t wave, uint32_t lane) {
+  for (uint32_t s = 0; s < q.num_staged; s++) {
+    uint32_t bytes, bits;
+    const uint32_t* w = staged_src(q, sd, s, bytes, bits);
+    if (!w) continue;
+    const rsrc_t r = make_rsrc(w, bytes);
+    const uint32_t pieces = bits;  // the tile's 256*b words = b pieces of 1 KiB
+    const uint32_t tb = tile * (uint32_t)(kTileDocs / 8) * bits;  // byte offset of the tile's first word
+    uint32_t* dst = buf + q.staged[s].lds_word_off;
+    for (uint32_t c = wave; c < pieces; c += kBlock / 64) {
+      dma16(r, dst + c * 256, tb + (c * 64 + lane) * 16);
     }
   }
-  __syncthreads();  // every wave is done reading the previous tile's staged words
-#pragma unroll
-  for (int k = 0; k < kStageJobs; k++)
-    if (dst[k] != 0xFFFFFFFFu) *(uint4*)(lds + dst[k]) = buf[k];
-  __syncthreads();
 }
 
 // One leaf over the thread's 32 docs, evaluated for the docs in `need` -> 32-bit mask (bit j <-> doc
 // base + j*256 + tid).  Bits outside `need` are don't-care.
-__device__ __forceinline__ uint32_t eval_leaf(const QuerySpec& q, uint32_t li, const LeafDesc& L,
+// The docs a thread evaluates, as rows j of its 32-bit masks:
+//   TileRows  -- the tile's docs base + j*256 + tid (j < 32); staged columns are readable at rel = j*256 + tid.
+//   QueueRows -- docs compacted into the block's LDS queue: entry j*256 + tid (j < 4), gathers only.
+struct TileRows {
+  static constexpr bool kTile = true;
+  uint32_t base, tid;
+  __device__ __forceinline__ uint32_t doc(uint32_t j) const { return base + j * (uint32_t)kBlock + tid; }
+  __device__ __forceinline__ uint32_t rel(uint32_t d) const { return d - base; }
+};
+struct QueueRows {
+  static constexpr bool kTile = false;
+  const uint32_t* qd;
+  uint32_t n, tid;
+  __device__ __forceinline__ uint32_t doc(uint32_t j) const {
+    const uint32_t i = j * (uint32_t)kBlock + tid;
+    return i < n ? qd[i] : 0u;
+  }
+  __device__ __forceinline__ uint32_t rel(uint32_t) const { return 0u; }
+};
+
+template <class Rows>
+__device__ __forceinline__ uint32_t eval_leaf(const QuerySpec& q, uint32_t li, const LeafDesc L,
                                               const int32_t* lds_sets, const uint32_t* stage, uint32_t need,
-                                              uint32_t base, int tid) {
+                                              const Rows& rows, int tid) {
   uint32_t m = 0;
   switch (L.kind) {
     case LK_ALL: m = kRowMask; break;
     case LK_NONE: break;
     case LK_DOCRANGE: {
+      if constexpr (Rows::kTile) {
 #pragma unroll
-      for (int j = 0; j < kRows; j++) {
-        const uint32_t d = base + (uint32_t)(j * kBlock + tid);
-        m |= (uint32_t)(d >= (uint32_t)L.lo && d < (uint32_t)L.hi) << j;
+        for (int j = 0; j < kRows; j++) {
+          const uint32_t d = rows.doc((uint32_t)j);
+          m |= (uint32_t)(d >= (uint32_t)L.lo && d < (uint32_t)L.hi) << j;
+        }
+      } else {
+        uint32_t rem = need;
+        while (rem) {
+          const uint32_t j = (uint32_t)__ffs(rem) - 1u;
+          rem &= rem - 1u;
+          const uint32_t d = rows.doc(j);
+          m |= (uint32_t)(d >= (uint32_t)L.lo && d < (uint32_t)L.hi) << j;
+        }
       }
       break;
     }
     default: {  // packed column: RANGE / SET_LDS / SET_LUT
-      const uint32_t slot = q.leaf_slot[li];
+      const uint32_t slot = Rows::kTile ? q.leaf_slot[li] : (uint32_t)kNoSlot;
       if (slot != kNoSlot) {
+        // staged: all 32 rows from LDS, 8 rows per batch with the batch's LDS reads issued together
         const uint32_t* st = stage + q.staged[slot].lds_word_off;
-        const uint32_t b = L.bits;
+        const uint32_t b = L.bits, mask = bits_mask(b);
+        const uint32_t e0 = (uint32_t)tid * b + b - 1u, estep = (uint32_t)kBlock * b;
         if (L.kind == LK_RANGE) {
           const uint32_t lo = (uint32_t)L.lo, span = (uint32_t)(L.hi - L.lo);
-#pragma unroll 8
-          for (int j = 0; j < kRows; j++)
-            m |= (uint32_t)((unpack_lds(st, (uint32_t)(j * kBlock + tid), b) - lo) < span) << j;
+#pragma unroll
+          for (int j0 = 0; j0 < kRows; j0 += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int r = 0; r < 8; r++) v[r] = unpack_end(st, e0 + (uint32_t)(j0 + r) * estep, mask);
+#pragma unroll
+            for (int r = 0; r < 8; r++) m |= (uint32_t)((v[r] - lo) < span) << (j0 + r);
+          }
         } else if (L.kind == LK_SET_LDS) {
           const uint32_t* bm = (const uint32_t*)(lds_sets + L.lds_off);
           const uint32_t shift = L.shift;
-#pragma unroll 8
-          for (int j = 0; j < kRows; j++) m |= set_bit(bm, shift, unpack_lds(st, (uint32_t)(j * kBlock + tid), b)) << j;
-          if (shift) {  // resolve the (few) bitmap candidates exactly
+#pragma unroll
+          for (int j0 = 0; j0 < kRows; j0 += 8) {
+            uint32_t x[8], w[8];
+#pragma unroll
+            for (int r = 0; r < 8; r++) x[r] = unpack_end(st, e0 + (uint32_t)(j0 + r) * estep, mask) >> shift;
+#pragma unroll
+            for (int r = 0; r < 8; r++) w[r] = bm[x[r] >> 5];
+#pragma unroll
+            for (int r = 0; r < 8; r++) m |= __builtin_amdgcn_ubfe(w[r], x[r] & 31u, 1u) << (j0 + r);
+          }
+          if (shift) {  // resolve the (few) bitmap candidates exactly: LUT reads in rounds of 4 per lane
+            const PG_GLOBAL uint32_t* lut = glb(L.lut);
             uint32_t cand = m & need;
             m = 0;
-            while (cand) {
-              const uint32_t j = (uint32_t)__ffs(cand) - 1u;
-              cand &= cand - 1u;
-              if (set_contains((const int32_t*)bm + L.nbw, L.set_log2, unpack_lds(st, j * kBlock + (uint32_t)tid, b)))
-                m |= 1u << j;
+            while (__ballot(cand != 0)) {
+              uint32_t jj[4], v[4], w[4];
+#pragma unroll
+              for (int x = 0; x < 4; x++) {
+                jj[x] = cand ? (uint32_t)__ffs(cand) - 1u : 0u;
+                v[x] = cand ? unpack_end(st, e0 + jj[x] * estep, mask) : 0u;
+                jj[x] = cand ? jj[x] : 32u;
+                cand &= cand - 1u;
+              }
+#pragma unroll
+              for (int x = 0; x < 4; x++) w[x] = lut[v[x] >> 5];
+#pragma unroll
+              for (int x = 0; x < 4; x++)
+                if (jj[x] < 32u) m |= __builtin_amdgcn_ubfe(w[x], v[x] & 31u, 1u) << jj[x];
             }
           }
         } else {
-#pragma unroll 8
-          for (int j = 0; j < kRows; j++) {
-            const uint32_t v = unpack_lds(st, (uint32_t)(j * kBlock + tid), b);
-            m |= ((L.aux[v >> 5] >> (v & 31u)) & 1u) << j;
+          const PG_GLOBAL uint32_t* lut = glb(L.aux);
+#pragma unroll
+          for (int j0 = 0; j0 < kRows; j0 += 8) {
+            uint32_t v[8], w[8];
+#pragma unroll
+            for (int r = 0; r < 8; r++) v[r] = unpack_end(st, e0 + (uint32_t)(j0 + r) * estep, mask);
+#pragma unroll
+            for (int r = 0; r < 8; r++) w[r] = lut[v[r] >> 5];
+#pragma unroll
+            for (int r = 0; r < 8; r++) m |= __builtin_amdgcn_ubfe(w[r], v[r] & 31u, 1u) << (j0 + r);
           }
         }
       } else {
@@ -259,8 +321,7 @@ __device__ __forceinline__ uint32_t eval_leaf(const QuerySpec& q, uint32_t li, c
           for (int x = 0; x < 4; x++) {
             jj[x] = rem ? (uint32_t)__ffs(rem) - 1u : 32u;
             rem &= rem - 1u;
-            const uint32_t d = jj[x] < 32u ? base + jj[x] * (uint32_t)kBlock + (uint32_t)tid : base;
-            v[x] = unpack(r, d, L.bits);
+            v[x] = unpack(r, rows.doc(jj[x] < 32u ? jj[x] : 0u), L.bits);
           }
 #pragma unroll
           for (int x = 0; x < 4; x++)
@@ -276,21 +337,22 @@ __device__ __forceinline__ uint32_t eval_leaf(const QuerySpec& q, uint32_t li, c
 // Filter tree (prefix form) over 32-bit masks with short-circuit needs: an AND child only sees docs every
 // earlier child accepted, an OR child only docs no earlier child accepted.  Open groups (<= 4) are kept in
 // registers: 32-bit acc / need fields packed into 64-bit words, 2-bit types in one word.
-enum GroupType : uint32_t { GT_ROOT = 0, GT_AND = 1, GT_OR = 2, GT_NOT = 3 };
 
-__device__ __forceinline__ uint32_t eval_filter(const QuerySpec& q, const LeafDesc* __restrict__ leaves,
-                                                const int32_t* lds_sets, const uint32_t* stage, uint32_t valid,
-                                                uint32_t base, int tid) {
-  if (q.num_ops == 0) return valid;
-  uint32_t gtype = GT_ROOT, gacc = 0, gneed = valid, need = valid;
+// Ops [o0, o1) of the program as the children of a group of type `gtype0` (GT_ROOT: the whole program).
+template <class Rows>
+__device__ __forceinline__ uint32_t eval_filter(const QuerySpec& q, const LeafDesc* leaves, uint32_t o0, uint32_t o1,
+                                                uint32_t gtype0, const int32_t* lds_sets, const uint32_t* stage,
+                                                uint32_t valid, const Rows& rows, int tid) {
+  if (o0 >= o1) return valid;  // no program / no remaining children: every valid doc
+  uint32_t gtype = gtype0, gacc = gtype0 == GT_AND ? kRowMask : 0u, gneed = valid, need = valid;
   uint64_t sacc0 = 0, sacc1 = 0, sneed0 = 0, sneed1 = 0;
   uint32_t stype = 0;
-  for (uint32_t i = 0; i < q.num_ops; i++) {
+  for (uint32_t i = o0; i < o1; i++) {
     const int32_t op = q.ops[i];
     if (op >= 0 || op == kOpEnd) {
       uint32_t r;
       if (op >= 0) {
-        r = __ballot(need != 0) ? eval_leaf(q, (uint32_t)op, leaves[op], lds_sets, stage, need, base, tid) : 0u;
+        r = __ballot(need != 0) ? eval_leaf(q, (uint32_t)op, ldc(leaves, (uint32_t)op), lds_sets, stage, need, rows, tid) : 0u;
       } else {
         r = gtype == GT_NOT ? (~gacc & gneed) : gacc;
         gtype = stype & 3u;
@@ -357,7 +419,7 @@ __device__ __forceinline__ void group_update(const QuerySpec& q, const GroupStat
   switch (A.fn) {
     case PG_AGG_COUNT: break;  // = slot 0
     case PG_AGG_COUNTMV:
-      atomicAdd(&S.i64[g * q.n_i64 + A.slot], (unsigned long long)(c[0].mv_offsets[d + 1] - c[0].mv_offsets[d]));
+      atomicAdd(&S.i64[g * q.n_i64 + A.slot], (unsigned long long)(glb(ldc(c, 0).mv_offsets)[d + 1] - glb(ldc(c, 0).mv_offsets)[d]));
       break;
     case PG_AGG_SUM:
     case PG_AGG_AVG:  // AVG count == slot 0
@@ -367,7 +429,7 @@ __device__ __forceinline__ void group_update(const QuerySpec& q, const GroupStat
     case PG_AGG_MIN: atomicMin(&S.mn[g * q.n_min + A.slot], (long long)order_key(value_f64(A, c, ia, ib))); break;
     case PG_AGG_MAX: atomicMax(&S.mx[g * q.n_max + A.slot], (long long)order_key(value_f64(A, c, ia, ib))); break;
     case PG_AGG_DISTINCTCOUNT: {
-      const uint64_t key = key_of(A.key_kind, A.key_base, c[0], ia);
+      const uint64_t key = key_of(A.key_kind, A.key_base, ldc(c, 0), ia);
       if (key < A.key_card) q.flags[g * q.flag_bytes_per_slot + A.flag_off + key] = 1;
       else atomicOr(q.err, 2u);
       break;
@@ -380,7 +442,7 @@ __device__ __forceinline__ void acc_update(const QuerySpec& q, const AggSpec& A,
                                            uint32_t d, uint32_t ia, uint32_t ib) {
   switch (A.fn) {
     case PG_AGG_COUNT: break;
-    case PG_AGG_COUNTMV: acc += c[0].mv_offsets[d + 1] - c[0].mv_offsets[d]; break;
+    case PG_AGG_COUNTMV: acc += glb(ldc(c, 0).mv_offsets)[d + 1] - glb(ldc(c, 0).mv_offsets)[d]; break;
     case PG_AGG_SUM:
     case PG_AGG_AVG:
       if (A.integer) acc += (uint64_t)value_i64(A, c, ia, ib);
@@ -397,7 +459,7 @@ __device__ __forceinline__ void acc_update(const QuerySpec& q, const AggSpec& A,
       break;
     }
     case PG_AGG_DISTINCTCOUNT: {
-      const uint64_t key = key_of(A.key_kind, A.key_base, c[0], ia);
+      const uint64_t key = key_of(A.key_kind, A.key_base, ldc(c, 0), ia);
       if (key < A.key_card) q.flags[A.flag_off + key] = 1;
       else atomicOr(q.err, 2u);
       break;
@@ -407,7 +469,7 @@ __device__ __forceinline__ void acc_update(const QuerySpec& q, const AggSpec& A,
 
 // dictId of doc `d` (row offset `rel` in the tile) of a column read by an aggregation / key: from the staged
 // tile when the column is staged, else a gathered window.
-__device__ __forceinline__ uint32_t col_id(const QuerySpec& q, uint32_t slot, const ColDesc& c,
+__device__ __forceinline__ uint32_t col_id(const QuerySpec& q, uint32_t slot, const ColDesc c,
                                           const uint32_t* stage, uint32_t d, uint32_t rel) {
   if (slot != kNoSlot) return unpack_lds(stage + q.staged[slot].lds_word_off, rel, c.bits);
   return unpack(make_rsrc(c.words, c.wbytes), d, c.bits);
@@ -494,7 +556,7 @@ __device__ __forceinline__ void aggregate_dense(const QuerySpec& q, const SegDes
 #pragma unroll
       for (int k = 0; k < NK; k++) {
         if (k >= (int)q.num_keys) break;
-        const ColDesc& kc = sd.keycols[k];
+        const ColDesc kc = ldc(sd.keycols, k);
         uint32_t ids[8];
         uint64_t kid[8];
 #pragma unroll
@@ -522,8 +584,8 @@ __device__ __forceinline__ void aggregate_dense(const QuerySpec& q, const SegDes
       uint32_t ia[8], ib[8];
 #pragma unroll
       for (int r = 0; r < 8; r++) {
-        ia[r] = nc >= 1 ? col_id(q, q.agg_slot[a][0], c[0], stage, d[r], rel[r]) : 0u;
-        ib[r] = nc >= 2 ? col_id(q, q.agg_slot[a][1], c[1], stage, d[r], rel[r]) : 0u;
+        ia[r] = nc >= 1 ? col_id(q, q.agg_slot[a][0], ldc(c, 0), stage, d[r], rel[r]) : 0u;
+        ib[r] = nc >= 2 ? col_id(q, q.agg_slot[a][1], ldc(c, 1), stage, d[r], rel[r]) : 0u;
       }
       agg_rows8<GROUPED>(q, S, A, c, ia, ib, g, d, live, acc[a]);
     }
@@ -532,10 +594,10 @@ __device__ __forceinline__ void aggregate_dense(const QuerySpec& q, const SegDes
 
 // Aggregation over the matched docs `m` of a tile, in rounds of up to 2 docs per lane; a round's dictId reads for
 // every key and aggregation operand are issued before any is consumed.
-template <bool GROUPED, int MAXA, int MAXK>
+template <bool GROUPED, int MAXA, int MAXK, class Rows>
 __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc& sd, const GroupState& S,
                                                const uint32_t* stage, uint64_t (&acc)[MAXA], uint32_t m,
-                                               uint32_t base, int tid) {
+                                               const Rows& rows) {
   constexpr int R = 2;
   constexpr int NK = MAXK > 0 ? MAXK : 1;
   while (__ballot(m != 0)) {
@@ -544,16 +606,17 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
     for (int x = 0; x < R; x++) {
       jj[x] = m ? (uint32_t)__ffs(m) - 1u : 32u;
       m &= m - 1u;
-      d[x] = jj[x] < 32u ? base + jj[x] * (uint32_t)kBlock + (uint32_t)tid : base;
+      d[x] = rows.doc(jj[x] < 32u ? jj[x] : 0u);
     }
     uint32_t kidx[R][NK], ia[R][MAXA], ib[R][MAXA];
 #pragma unroll
     for (int x = 0; x < R; x++) {
-      const uint32_t rel = d[x] - base;
+      const uint32_t rel = rows.rel(d[x]);
 #pragma unroll
       for (int k = 0; k < NK; k++) {
         kidx[x][k] = 0;
-        if (GROUPED && k < (int)q.num_keys) kidx[x][k] = col_id(q, q.key_slot[k], sd.keycols[k], stage, d[x], rel);
+        if (GROUPED && k < (int)q.num_keys)
+          kidx[x][k] = col_id(q, Rows::kTile ? q.key_slot[k] : (uint32_t)kNoSlot, ldc(sd.keycols, k), stage, d[x], rel);
       }
 #pragma unroll
       for (int a = 0; a < MAXA; a++) {
@@ -561,8 +624,10 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
         if (a >= (int)q.num_aggs) continue;
         const uint32_t nc = agg_ncols(q.aggs[a]);
         const ColDesc* c = sd.aggcols + 2 * a;
-        if (nc >= 1) ia[x][a] = col_id(q, q.agg_slot[a][0], c[0], stage, d[x], rel);
-        if (nc >= 2) ib[x][a] = col_id(q, q.agg_slot[a][1], c[1], stage, d[x], rel);
+        const uint32_t s0 = Rows::kTile ? q.agg_slot[a][0] : (uint32_t)kNoSlot;
+        const uint32_t s1 = Rows::kTile ? q.agg_slot[a][1] : (uint32_t)kNoSlot;
+        if (nc >= 1) ia[x][a] = col_id(q, s0, ldc(c, 0), stage, d[x], rel);
+        if (nc >= 2) ib[x][a] = col_id(q, s1, ldc(c, 1), stage, d[x], rel);
       }
     }
 #pragma unroll
@@ -574,7 +639,7 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
 #pragma unroll
         for (int k = 0; k < NK; k++) {
           if (k >= (int)q.num_keys) break;
-          const uint64_t kid = key_of(q.key_kind[k], q.key_base[k], sd.keycols[k], kidx[x][k]);
+          const uint64_t kid = key_of(q.key_kind[k], q.key_base[k], ldc(sd.keycols, k), kidx[x][k]);
           in_range &= kid < q.key_card[k];
           g += kid * q.key_stride[k];
         }
@@ -605,15 +670,24 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
 #define PG_SCAN_MIN_WAVES 3  // waves per SIMD the register budget must allow (3 blocks of 256 threads per CU)
 #endif
 
+// LDS layout of a launch: [16 B][staging ring][IN sets][group table at a 16-byte boundary][queue]
+__host__ __device__ inline size_t scan_groups_off(const QuerySpec& q) {
+  return (16 + (size_t)q.stage_ring * q.stage_lds_words * 4 + (size_t)q.set_lds_ints * 4 + 15) & ~(size_t)15;
+}
+__host__ __device__ inline size_t scan_queue_off(const QuerySpec& q) {
+  const size_t g = (q.num_keys && q.use_lds) ? q.num_slots * 8ull * (q.n_i64 + q.n_f64 + q.n_min + q.n_max) : 0;
+  return scan_groups_off(q) + ((g + 15) & ~(size_t)15);
+}
+
 template <bool GROUPED, int MAXA, int MAXK>
 __global__ __launch_bounds__(kBlock, PG_SCAN_MIN_WAVES) void scan_kernel(QuerySpec q) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint32_t* stage = (uint32_t*)smem;                                   // staged tiles (16-byte aligned)
-  int32_t* lds_sets = (int32_t*)(stage + q.stage_lds_words);          // IN-list hash sets
-  unsigned char* lds_groups = (unsigned char*)(lds_sets + q.set_lds_ints);
+  uint32_t* stage = (uint32_t*)(smem + 16);                                   // staging ring (16 bytes in: st[-1])
+  int32_t* lds_sets = (int32_t*)(stage + q.stage_ring * q.stage_lds_words);  // IN-list filter bitmaps / hash sets
+  unsigned char* lds_groups = smem + scan_groups_off(q);                       // 16-byte aligned
   const int tid = threadIdx.x;
-  const uint64_t group_bytes = (GROUPED && q.use_lds) ? q.num_slots * 8ull * (q.n_i64 + q.n_f64 + q.n_min + q.n_max) : 0;
-  StageSrc& src = *(StageSrc*)(lds_groups + ((group_bytes + 15) & ~15ull));  // per-segment staging sources
+  const uint32_t lane = (uint32_t)tid & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
 
   // LDS-privatised group table: [G][n_i64] u64 | [G][n_f64] f64 | [G][n_min] i64 | [G][n_max] i64
   unsigned long long* l_i64 = (unsigned long long*)lds_groups;
@@ -640,95 +714,195 @@ __global__ __launch_bounds__(kBlock, PG_SCAN_MIN_WAVES) void scan_kernel(QuerySp
   }
   uint64_t doc_count = 0;  // matched docs of this thread (aggregation-only slot 0)
 
-  // contiguous item range of this block (consecutive items share a segment -> few per-segment reloads)
+  // The block walks the tiles of a contiguous item range (consecutive items share a segment) as one sequence;
+  // the staged columns of the next tile are copied HBM -> LDS while the current tile is evaluated (ring of 2
+  // buffers), or right after it (ring of 1, overlap across the CU's blocks only).
   const uint32_t i0 = (uint32_t)((uint64_t)blockIdx.x * q.num_items / gridDim.x);
   const uint32_t i1 = (uint32_t)(((uint64_t)blockIdx.x + 1) * q.num_items / gridDim.x);
-  uint32_t cur_seg = 0xFFFFFFFFu;
-  for (uint32_t item = i0; item < i1; item++) {
-    const WorkItem it = q.items[item];
-    const SegDesc sd = q.segs[it.seg];
-    if (it.seg != cur_seg) {
-      __syncthreads();  // every wave is done with the previous segment's LDS sets
-      if (q.set_lds_ints) {  // stage this segment's IN-list hash sets
-        for (uint32_t l = 0; l < q.num_leaves; l++) {
-          const LeafDesc L = sd.leaves[l];
-          if (L.kind != LK_SET_LDS) continue;
-          for (uint32_t k = tid; k < L.set_ints; k += kBlock) lds_sets[L.lds_off + k] = ((const int32_t*)L.aux)[k];
-        }
-      }
-      if (tid < kMaxStaged) {
-        const int s = tid;
-        src.words[s] = nullptr;
-        src.nwords[s] = 0;
-        src.bits[s] = 1;
-        if (s >= (int)q.num_staged) goto staged_done;
-        const StagedCol& sc = q.staged[s];
-        const uint32_t* w = nullptr;
-        uint32_t bytes = 0, bits = 1;
-        if (sc.role == 0) {
-          const LeafDesc& L = sd.leaves[sc.idx];
-          if (L.kind == LK_RANGE || L.kind == LK_SET_LDS || L.kind == LK_SET_LUT) { w = L.words; bytes = L.wbytes; bits = L.bits; }
-        } else {
-          const ColDesc& c = sc.role == 1 ? sd.aggcols[2 * sc.idx + sc.operand] : sd.keycols[sc.idx];
-          w = c.words; bytes = c.wbytes; bits = c.bits;
-        }
-        src.words[s] = w;
-        src.nwords[s] = bytes / 4;
-        src.bits[s] = bits;
-      }
-    staged_done:
-      __syncthreads();
-      cur_seg = it.seg;
-    }
-    const uint32_t nd = sd.num_docs;
+  // queue (queue_mode): [kQueueCap] doc ids + [4] wave totals of the compaction scan
+  uint32_t* queue = (uint32_t*)(smem + scan_queue_off(q));
+  uint32_t* scan_tmp = queue + kQueueCap;
+  uint32_t qn = 0;  // queued docs (block-uniform)
+
+  if (i0 < i1) {
+    const bool ring2 = q.stage_ring > 1;
+    uint32_t item = i0;
+    WorkItem it = ldc(q.items, item);
+    uint32_t tile = it.tile_begin;
+    uint32_t buf = 0;
+    uint32_t cur_seg = 0xFFFFFFFFu;
+    SegDesc cur_sd = ldc(q.segs, it.seg);
     uint64_t seg_count = 0;
-    for (uint32_t tile = it.tile_begin; tile < it.tile_end; tile++) {
-      const uint32_t base = tile * (uint32_t)kTileDocs;
-      if (q.num_staged) stage_tile(q, src, tile, stage, tid);
+
+    // phase B over the queued docs of segment `cur_sd`: the root AND's remaining children, then aggregation
+    auto flush = [&]() {
+      __syncthreads();  // queue entries visible
+      const QueueRows rows{queue, qn, (uint32_t)tid};
       uint32_t valid = 0;
 #pragma unroll
-      for (int j = 0; j < kRows; j++) valid |= (uint32_t)(base + (uint32_t)(j * kBlock + tid) < nd) << j;
-      const uint32_t m = eval_filter(q, sd.leaves, lds_sets, stage, valid, base, tid);
+      for (int j = 0; j < kQueueRows; j++) valid |= (uint32_t)((uint32_t)(j * kBlock + tid) < qn) << j;
+      const uint32_t m = eval_filter(q, cur_sd.leaves, q.opB_begin, q.opB_end, GT_AND, lds_sets, stage, valid, rows, tid);
       const uint32_t nm = __popc(m);
       seg_count += nm;
       if (!GROUPED) doc_count += nm;
-      if (!GROUPED && !q.agg_reads) continue;  // COUNT(*) only: the matched-doc count is the answer
-      // dense when at least a quarter of the lanes hold >= 8 matches: batched rows; else per-doc rounds
-      if (__popcll(__ballot(__popc(m) >= 8)) >= 16) aggregate_dense<GROUPED, MAXA, MAXK>(q, sd, S, stage, acc, m, base, tid);
-      else aggregate_tile<GROUPED, MAXA, MAXK>(q, sd, S, stage, acc, m, base, tid);
+      if (GROUPED || q.agg_reads) aggregate_tile<GROUPED, MAXA, MAXK>(q, cur_sd, S, stage, acc, m, rows);
+      __syncthreads();  // every lane is done reading the queue
+      qn = 0;
+    };
+
+    if (q.num_staged) stage_issue(q, cur_sd, tile, stage, wave, lane);
+    for (;;) {
+      // successor of (item, tile) in the block's sequence
+      uint32_t n_item = item, n_tile = tile + 1, n_seg = it.seg;
+      bool has_next = true;
+      WorkItem n_it = it;
+      if (n_tile >= it.tile_end) {
+        n_item = item + 1;
+        has_next = n_item < i1;
+        if (has_next) { n_it = ldc(q.items, n_item); n_tile = n_it.tile_begin; n_seg = n_it.seg; }
+      }
+      __builtin_amdgcn_s_waitcnt(0);  // this wave's copies of the current tile have landed
+      __syncthreads();                // ... and every wave's; every wave is done with the other buffer
+      if (it.seg != cur_seg) {
+        if (cur_seg != 0xFFFFFFFFu) {
+          if (qn) flush();  // the queue holds docs of the previous segment
+          const uint64_t c = wave_sum_u64(seg_count);
+          if (lane == 0 && c) atomicAdd(&q.seg_matched[cur_seg], (unsigned long long)c);
+          seg_count = 0;
+        }
+        cur_sd = ldc(q.segs, it.seg);
+        if (q.set_lds_ints) {  // this segment's IN-list filter bitmaps + hash tables
+          for (uint32_t l = 0; l < q.num_leaves; l++) {
+            const LeafDesc L = ldc(cur_sd.leaves, l);
+            if (L.kind != LK_SET_LDS) continue;
+            const PG_GLOBAL int32_t* src = glb((const int32_t*)L.aux);
+            int32_t* dst = lds_sets + L.lds_off;
+            for (uint32_t k = tid; k < L.set_ints; k += kBlock) dst[k] = src[k];
+          }
+          __syncthreads();
+        }
+        cur_seg = it.seg;
+      }
+      const SegDesc& sd = cur_sd;
+      if (ring2 && has_next && q.num_staged) stage_issue(q, ldc(q.segs, n_seg), n_tile, stage + (buf ^ 1u) * q.stage_lds_words, wave, lane);
+
+      const uint32_t* st = stage + buf * q.stage_lds_words;
+      const uint32_t base = tile * (uint32_t)kTileDocs;
+      const uint32_t nd = sd.num_docs;
+      uint32_t valid = kRowMask;
+      if (base + (uint32_t)kTileDocs > nd) {
+        valid = 0;
+#pragma unroll
+        for (int j = 0; j < kRows; j++) valid |= (uint32_t)(base + (uint32_t)(j * kBlock + tid) < nd) << j;
+      }
+      const TileRows rows{base, (uint32_t)tid};
+      uint32_t m = eval_filter(q, sd.leaves, q.opA_begin, q.opA_end, q.opA_type, lds_sets, st, valid, rows, tid);
+      bool direct = !q.queue_mode;
+      if (q.queue_mode) {
+        // compact the phase-A survivors into the queue (block-wide exclusive scan of per-thread counts)
+        const uint32_t cnt = __popc(m);
+        uint32_t x = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = __shfl_up(x, o);
+          if (lane >= (uint32_t)o) x += y;
+        }
+        if (lane == 63) scan_tmp[wave] = x;
+        __syncthreads();
+        uint32_t wbase = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; w++) {
+          const uint32_t t = scan_tmp[w];
+          wbase += (uint32_t)w < wave ? t : 0u;
+          tot += t;
+        }
+        if (tot > (uint32_t)kQueueCap) {
+          direct = true;  // a dense tile: finish it in place
+          m = eval_filter(q, sd.leaves, q.opB_begin, q.opB_end, GT_AND, lds_sets, st, m, rows, tid);
+        } else if (tot) {
+          if (qn + tot > (uint32_t)kQueueCap) flush();
+          uint32_t pos = qn + wbase + x - cnt;
+          for (uint32_t r = m; r; r &= r - 1u) queue[pos++] = rows.doc((uint32_t)__ffs(r) - 1u);
+          qn += tot;
+          if (qn >= (uint32_t)kQueueFlush) flush();
+        }
+      }
+      if (direct) {
+        const uint32_t nm = __popc(m);
+        seg_count += nm;
+        if (!GROUPED) doc_count += nm;
+        if (GROUPED || q.agg_reads) {
+          // dense when at least a quarter of the lanes hold >= 8 matches: batched rows; else per-doc rounds
+          if (__popcll(__ballot(nm >= 8)) >= 16) aggregate_dense<GROUPED, MAXA, MAXK>(q, sd, S, st, acc, m, base, tid);
+          else aggregate_tile<GROUPED, MAXA, MAXK>(q, sd, S, st, acc, m, rows);
+        }
+      }
+      if (!has_next) break;
+      if (!ring2 && q.num_staged) {
+        __syncthreads();  // every wave is done with the single buffer
+        stage_issue(q, ldc(q.segs, n_seg), n_tile, stage, wave, lane);
+      }
+      item = n_item;
+      it = n_it;
+      tile = n_tile;
+      if (ring2) buf ^= 1u;
     }
+    if (qn) flush();
     const uint64_t c = wave_sum_u64(seg_count);
-    if ((tid & 63) == 0 && c) atomicAdd(&q.seg_matched[it.seg], (unsigned long long)c);
+    if (lane == 0 && c) atomicAdd(&q.seg_matched[cur_seg], (unsigned long long)c);
   }
 
   if (!GROUPED) {
-    // wave-reduce then one global atomic per wave per slot
+    // wave-reduce, then the block's waves combine through LDS: one global atomic per block per slot
+    __syncthreads();  // the staging ring is free
+    uint64_t* red = (uint64_t*)stage;  // [wave][1 + MAXA]
     const uint64_t dc = wave_sum_u64(doc_count);
-    const bool lead = (tid & 63) == 0;
-    if (lead && dc) atomicAdd(&q.i64[0], (unsigned long long)dc);
+    if (lane == 0) red[wave * (1 + MAXA)] = dc;
 #pragma unroll
     for (int a = 0; a < MAXA; a++) {
       if (a >= (int)q.num_aggs) break;
+      uint64_t v = 0;
+      switch (q.aggs[a].kind) {
+        case SK_I64: v = wave_sum_u64(acc[a]); break;
+        case SK_F64: v = (uint64_t)__double_as_longlong(wave_sum_f64(__longlong_as_double(acc[a]))); break;
+        case SK_MIN: v = (uint64_t)wave_min_i64((int64_t)acc[a]); break;
+        case SK_MAX: v = (uint64_t)wave_max_i64((int64_t)acc[a]); break;
+        default: break;
+      }
+      if (lane == 0) red[wave * (1 + MAXA) + 1 + a] = v;
+    }
+    __syncthreads();
+    constexpr int NW = kBlock / 64;
+    if (tid == 0) {
+      uint64_t t = 0;
+      for (int w = 0; w < NW; w++) t += red[w * (1 + MAXA)];
+      if (t) atomicAdd(&q.i64[0], (unsigned long long)t);
+    } else if (tid <= MAXA && tid <= (int)q.num_aggs) {
+      const int a = tid - 1;
       const AggSpec& A = q.aggs[a];
       switch (A.kind) {
         case SK_I64: {
-          const uint64_t v = wave_sum_u64(acc[a]);
-          if (lead && v) atomicAdd(&q.i64[A.slot], (unsigned long long)v);
+          uint64_t t = 0;
+          for (int w = 0; w < NW; w++) t += red[w * (1 + MAXA) + 1 + a];
+          if (t) atomicAdd(&q.i64[A.slot], (unsigned long long)t);
           break;
         }
         case SK_F64: {
-          const double v = wave_sum_f64(__longlong_as_double(acc[a]));
-          if (lead && v != 0.0) atomicAdd(&q.f64[A.slot], v);
+          double t = 0.0;
+          for (int w = 0; w < NW; w++) t += __longlong_as_double((long long)red[w * (1 + MAXA) + 1 + a]);
+          if (t != 0.0) atomicAdd(&q.f64[A.slot], t);
           break;
         }
         case SK_MIN: {
-          const int64_t v = wave_min_i64((int64_t)acc[a]);
-          if (lead) atomicMin(&q.mn[A.slot], (long long)v);
+          int64_t t = (int64_t)red[1 + a];
+          for (int w = 1; w < NW; w++) t = min(t, (int64_t)red[w * (1 + MAXA) + 1 + a]);
+          atomicMin(&q.mn[A.slot], (long long)t);
           break;
         }
         case SK_MAX: {
-          const int64_t v = wave_max_i64((int64_t)acc[a]);
-          if (lead) atomicMax(&q.mx[A.slot], (long long)v);
+          int64_t t = (int64_t)red[1 + a];
+          for (int w = 1; w < NW; w++) t = max(t, (int64_t)red[w * (1 + MAXA) + 1 + a]);
+          atomicMax(&q.mx[A.slot], (long long)t);
           break;
         }
         default: break;
@@ -754,11 +928,16 @@ static void launch_one(const QuerySpec& q, uint32_t blocks, size_t lds, hipStrea
   hipLaunchKernelGGL((scan_kernel<G, A, K>), dim3(blocks), dim3(kBlock), lds, s, q);
 }
 
+// LDS of a launch: staging ring | IN sets | group table; at least the aggregation-only block reduction's
+// [4][1 + kMaxAggs] words, which reuses the ring.
 size_t scan_lds_bytes(const QuerySpec& q) {
-  size_t lds = (size_t)q.stage_lds_words * 4 + (size_t)q.set_lds_ints * 4;
-  if (q.num_keys && q.use_lds) lds += q.num_slots * 8ull * (q.n_i64 + q.n_f64 + q.n_min + q.n_max);
-  return ((lds + 15) & ~(size_t)15) + sizeof(StageSrc);
+  size_t lds = scan_queue_off(q) + (q.queue_mode ? (kQueueCap + 4) * 4 : 0);
+  const size_t red = 16 + (size_t)(kBlock / 64) * (1 + kMaxAggs) * 8;  // the IN sets are dead by then: may overlap
+  if (lds < red) lds = red;
+  return (lds + 15) & ~(size_t)15;
 }
+
+uint32_t scan_min_blocks_per_cu() { return PG_SCAN_MIN_WAVES; }  // 256-thread blocks: waves/SIMD == blocks/CU
 
 hipError_t launch_scan(const QuerySpec& q, uint32_t blocks, hipStream_t s) {
   const size_t lds = scan_lds_bytes(q);
