@@ -106,13 +106,17 @@ def main():
     for _ in range(args.warmup):
         res = step()
     scan_ms = []
+    parts = {k: [] for k in ("host_compile_ms", "prepass_ms", "scan_ms", "execute_wall_ms", "finalize_wall_ms")}
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = step()
-        scan_ms.append(eng.last_timing().scan_ms)
+        tm = eng.last_timing()
+        scan_ms.append(tm.scan_ms)
+        for k, v in parts.items():
+            v.append(getattr(tm, k))
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -179,6 +183,7 @@ def main():
                          "traffic_bytes_per_launch": traffic_bytes},
             "cpu_baseline": cpu,
             "parity_sample": parity,
+            "step_breakdown_ms": {k: round(float(np.mean(v)), 4) for k, v in parts.items()},
             "groups": len(res.rows), "docs_matched": res.stats.num_docs_scanned, "datagen_s": round(gen_s, 1),
         }
         print(json.dumps(out), flush=True)

@@ -924,9 +924,40 @@ __global__ __launch_bounds__(kBlock, PG_SCAN_MIN_WAVES) void scan_kernel(QuerySp
 }
 
 template <bool G, int A, int K>
-static void launch_one(const QuerySpec& q, uint32_t blocks, size_t lds, hipStream_t s) {
+void launch_one(const QuerySpec& q, uint32_t blocks, size_t lds, hipStream_t s) {
   hipLaunchKernelGGL((scan_kernel<G, A, K>), dim3(blocks), dim3(kBlock), lds, s, q);
 }
+
+// Each (grouped, aggs, keys) shape is compiled in its own translation unit (the Makefile builds this file once per
+// PG_SCAN_SHARD = 0..8 plus once without it for the dispatcher), so the nine kernel bodies build in parallel.
+#define PG_SCAN_SHAPES(X)                                                                                           \
+  X(0, false, 2, 0) X(1, false, 4, 0) X(2, false, kMaxAggs, 0) X(3, true, 2, 1) X(4, true, 4, 1)                    \
+  X(5, true, kMaxAggs, 1) X(6, true, 2, kMaxKeys) X(7, true, 4, kMaxKeys) X(8, true, kMaxAggs, kMaxKeys)
+
+#ifdef PG_SCAN_SHARD
+#if PG_SCAN_SHARD == 0
+template void launch_one<false, 2, 0>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+#elif PG_SCAN_SHARD == 1
+template void launch_one<false, 4, 0>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+#elif PG_SCAN_SHARD == 2
+template void launch_one<false, kMaxAggs, 0>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+#elif PG_SCAN_SHARD == 3
+template void launch_one<true, 2, 1>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+#elif PG_SCAN_SHARD == 4
+template void launch_one<true, 4, 1>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+#elif PG_SCAN_SHARD == 5
+template void launch_one<true, kMaxAggs, 1>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+#elif PG_SCAN_SHARD == 6
+template void launch_one<true, 2, kMaxKeys>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+#elif PG_SCAN_SHARD == 7
+template void launch_one<true, 4, kMaxKeys>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+#elif PG_SCAN_SHARD == 8
+template void launch_one<true, kMaxAggs, kMaxKeys>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+#endif
+#else
+#define PG_SCAN_EXTERN(i, G, A, K) \
+  extern template void launch_one<G, A, K>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+PG_SCAN_SHAPES(PG_SCAN_EXTERN)
 
 // LDS of a launch: staging ring | IN sets | group table; at least the aggregation-only block reduction's
 // [4][1 + kMaxAggs] words, which reuses the ring.
@@ -957,5 +988,6 @@ hipError_t launch_scan(const QuerySpec& q, uint32_t blocks, hipStream_t s) {
   }
   return hipGetLastError();
 }
+#endif  // PG_SCAN_SHARD
 
 }  // namespace pg
