@@ -203,11 +203,12 @@ hipError_t launch_bitmap_not(uint32_t* bitmap, uint32_t num_docs, hipStream_t s)
 hipError_t launch_mv_scan(const uint32_t* words, uint32_t bits, const uint32_t* offsets, uint32_t num_docs,
                           int32_t lo, int32_t hi, const uint32_t* lut, uint32_t excl, uint32_t* bitmap,
                           hipStream_t s);
-struct LutJob {            // set bits ids[0..n) in lut (one batched launch for every LUT of a query)
+struct LutJob {            // set bits ids[0..n) in lut and ids >> shift in region (one batched launch per query)
   const int32_t* ids;
-  uint32_t* lut;
+  uint32_t* lut;             // exact bitmap over dictIds, or null
+  uint32_t* region;          // LDS-set filter bitmap over dictId >> shift, or null
   uint32_t n;
-  uint32_t pad;
+  uint32_t shift;
 };
 hipError_t launch_set_lut_bits(const LutJob* jobs, uint32_t njobs, hipStream_t s);
 

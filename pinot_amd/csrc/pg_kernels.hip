@@ -315,12 +315,15 @@ hipError_t launch_mv_scan(const uint32_t* words, uint32_t bits, const uint32_t* 
   return hipGetLastError();
 }
 
-// IN / NOT_IN dictId sets too large for an LDS hash set -> global bitmaps over dictIds; one launch for all
-// (segment, leaf) LUTs of a query: block b handles job b.
+// IN / NOT_IN dictId sets -> global bitmaps over dictIds and the LDS filter bitmaps over dictId >> shift (both in
+// zeroed scratch); one launch for all (segment, leaf) sets of a query: block b handles job b.
 __global__ void set_lut_bits_kernel(const LutJob* __restrict__ jobs) {
   const LutJob J = jobs[blockIdx.x];
-  for (uint32_t i = threadIdx.x; i < J.n; i += blockDim.x)
-    atomicOr(&J.lut[(uint32_t)J.ids[i] >> 5], 1u << ((uint32_t)J.ids[i] & 31u));
+  for (uint32_t i = threadIdx.x; i < J.n; i += blockDim.x) {
+    const uint32_t id = (uint32_t)J.ids[i];
+    if (J.lut) atomicOr(&J.lut[id >> 5], 1u << (id & 31u));
+    if (J.region) atomicOr(&J.region[(id >> J.shift) >> 5], 1u << ((id >> J.shift) & 31u));
+  }
 }
 
 hipError_t launch_set_lut_bits(const LutJob* jobs, uint32_t njobs, hipStream_t s) {

@@ -520,7 +520,8 @@ struct Partials {
 };
 
 struct Arena {  // host image of the per-query parameter block, copied to the device in one transfer
-  std::vector<uint8_t> h;
+  std::vector<uint8_t>& h;  // the calling thread's buffer: its capacity persists, so steady-state queries touch no new pages
+  explicit Arena(std::vector<uint8_t>& buf) : h(buf) { h.clear(); }
   uint64_t put(const void* p, uint64_t n, uint64_t align = 16) {
     uint64_t at = (h.size() + align - 1) & ~(align - 1);
     h.resize(at + n);
@@ -650,6 +651,9 @@ void assign_reach(const std::vector<FNode>& nodes, int n, double reach, std::vec
 
 struct ThreadCtx {  // per calling thread: staging + events, created once
   PinnedBuf pinned;
+  PinnedBuf readback;
+  std::vector<uint8_t> arena;   // host image of the parameter arena (capacity reused across queries)
+  std::vector<WorkItem> items;  // work items of the current query (capacity reused across queries)  // per-segment match counts + error word, copied back before the one stream sync
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   int init() {
     if (ev[0]) return PG_OK;
@@ -925,14 +929,17 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
     for (size_t i = 0; i < pre.size(); i++) q.ops[i] = pre[i];
   }
 
-  Arena ar;
+  Arena ar(t_ctx.arena);
   std::vector<LeafDesc> leaves((uint64_t)S * L);
   std::vector<ColDesc> aggcols((uint64_t)S * A * 2);
   std::vector<ColDesc> keycols((uint64_t)S * K);
   std::vector<SegDesc> segd(S);
-  std::vector<WorkItem> items;
+  std::vector<WorkItem>& items = t_ctx.items;
+  items.clear();
   std::vector<PrepassOp> pre;
-  struct LutReq { uint64_t ids_off; uint32_t n; uint64_t lut_off; };  // arena ids -> scratch LUT
+  struct LutReq {  // arena ids -> scratch LUT and / or LDS-set region (~0 = none)
+    uint64_t ids_off; uint32_t n; uint64_t lut_off; uint64_t region_off = ~0ull; uint32_t shift = 0;
+  };
   std::vector<LutReq> luts;
   uint64_t scratch_bytes = 0;
   auto scratch_reserve = [&](uint64_t n) { uint64_t at = (scratch_bytes + 255) & ~255ull; scratch_bytes = at + n; return at; };
@@ -981,19 +988,14 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
           } else if (set_ints[li]) {
             dl.kind = LK_SET_LDS;
             const uint32_t n_region = set_geometry(std::max(c->card, 1u), dl.shift, dl.nbw);
-            std::vector<uint32_t> region(n_region, 0);
-            for (uint32_t i = 0; i < pl.num_ids; i++) {
-              const uint32_t x = (uint32_t)pl.ids[i] >> dl.shift;
-              region[x >> 5] |= 1u << (x & 31u);
-            }
             dl.set_ints = n_region;
             dl.lds_off = set_off[li];
-            patches.push_back({(uint64_t)si * L + li, ar.put(region.data(), 4ull * n_region), true, PT_AUX});
-            if (dl.shift) {  // exact LUT resolving the bitmap's candidates
-              const uint64_t lut_off = scratch_reserve(4ull * ((c->card + 31) / 32 + 1));
-              luts.push_back({ar.put(pl.ids, 4ull * pl.num_ids), pl.num_ids, lut_off});
-              patches.push_back({(uint64_t)si * L + li, lut_off, false, PT_LUT});
-            }
+            // filter bitmap (and, when shift > 0, the exact LUT resolving its candidates) built on the device
+            const uint64_t region_off = scratch_reserve(4ull * n_region);
+            const uint64_t lut_off = dl.shift ? scratch_reserve(4ull * ((c->card + 31) / 32 + 1)) : ~0ull;
+            luts.push_back({ar.put(pl.ids, 4ull * pl.num_ids), pl.num_ids, lut_off, region_off, dl.shift});
+            patches.push_back({(uint64_t)si * L + li, region_off, false, PT_AUX});
+            if (dl.shift) patches.push_back({(uint64_t)si * L + li, lut_off, false, PT_LUT});
           } else {
             dl.kind = LK_SET_LUT;
             const uint64_t lut_off = scratch_reserve(4ull * ((c->card + 31) / 32 + 1));
@@ -1302,7 +1304,9 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   }
   std::vector<LutJob> lutjobs(luts.size());
   for (size_t i = 0; i < luts.size(); i++)
-    lutjobs[i] = {(const int32_t*)(dA + luts[i].ids_off), (uint32_t*)(dS + luts[i].lut_off), luts[i].n, 0};
+    lutjobs[i] = {(const int32_t*)(dA + luts[i].ids_off),
+                  luts[i].lut_off == ~0ull ? nullptr : (uint32_t*)(dS + luts[i].lut_off),
+                  luts[i].region_off == ~0ull ? nullptr : (uint32_t*)(dS + luts[i].region_off), luts[i].n, luts[i].shift};
   if (!leaves.empty()) memcpy(&ar.h[off_leaves], leaves.data(), leaves.size() * sizeof(LeafDesc));
   if (!aggcols.empty()) memcpy(&ar.h[off_aggcols], aggcols.data(), aggcols.size() * sizeof(ColDesc));
   if (!keycols.empty()) memcpy(&ar.h[off_keycols], keycols.data(), keycols.size() * sizeof(ColDesc));
@@ -1352,6 +1356,10 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
     HIP_CHECK(launch_scan(q, blocks, s));
   }
   HIP_CHECK(hipEventRecord(ev[2], s));
+  const uint64_t n_sm = (S ? S : 1) + 2;
+  uint64_t* sm = (uint64_t*)t_ctx.readback.get(8ull * n_sm);
+  if (!sm) return fail(PG_E_NOMEM, "pinned readback of %llu bytes failed", (unsigned long long)(8ull * n_sm));
+  HIP_CHECK(hipMemcpyAsync(sm, P.seg_matched.p, 8ull * n_sm, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
   float pre_ms = 0, scan_ms = 0;
   (void)hipEventElapsedTime(&pre_ms, ev[0], ev[1]);
@@ -1364,8 +1372,6 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   stats.num_segments_processed = S;
   stats.num_entries_scanned_in_filter = entries_in_filter;
   {
-    std::vector<uint64_t> sm((S ? S : 1) + 2);
-    HIP_CHECK(hipMemcpy(sm.data(), P.seg_matched.p, 8ull * sm.size(), hipMemcpyDeviceToHost));
     for (uint32_t i = 0; i < S; i++) { stats.num_docs_scanned += sm[i]; stats.num_segments_matched += sm[i] > 0; }
     const uint32_t err = (uint32_t)sm[S ? S : 1];
     if (err) return fail(PG_E_INVALID, "device bounds check failed (code %u): a key fell outside the plan's key space", err);
