@@ -33,7 +33,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--segments", type=int, default=128, help="segments per GPU")
+    ap.add_argument("--workload", choices=("adanalytics", "ssb"), default="adanalytics",
+                    help="adanalytics = config 2 (the headline metric); ssb = config 3 (SSB Q1.1 shape, 96 segments/GPU)")
+    ap.add_argument("--segments", type=int, default=None, help="segments per GPU (default: the workload's)")
     ap.add_argument("--rows", type=int, default=7_812_500, help="rows per segment")
     ap.add_argument("--in-ids", type=int, default=1000)
     ap.add_argument("--cpu-sample-segments", type=int, default=2)
@@ -42,6 +44,9 @@ def main():
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "scan_traffic.json"),
                     help="PMC HBM traffic of the scan kernel for this workload (tools/profile_bench.sh)")
     args = ap.parse_args()
+    ssb = args.workload == "ssb"
+    if args.segments is None:
+        args.segments = 96 if ssb else 128
 
     import numpy as np
     import torch
@@ -66,32 +71,37 @@ def main():
     dev = torch.device("cuda", local)
     segs, dev_cols_sample = [], []
     t_gen = time.time()
-    table_cols = {s.name: i for i, s in enumerate(synth.ADANALYTICS)}
+    specs = synth.SSB_LINEORDER if ssb else synth.ADANALYTICS
+    tname = "lineorder" if ssb else "adAnalytics"
+    table_cols = {s.name: i for i, s in enumerate(specs)}
     fwd_bytes = 0
     dict_bytes = 0
     table = None
     for s in range(args.segments):
         gidx = rank * args.segments + s
-        dcs = synth.make_columns_torch(synth.ADANALYTICS, gidx, args.rows, dev)
-        seg = ImmutableSegment(f"adAnalytics_{gidx}", args.rows, {dc.spec.name: dc.meta_column() for dc in dcs})
+        dcs = synth.make_columns_torch(specs, gidx, args.rows, dev)
+        seg = ImmutableSegment(f"{tname}_{gidx}", args.rows, {dc.spec.name: dc.meta_column() for dc in dcs})
         segs.append(seg)
         if table is None:
-            table = Table("adAnalytics", [seg])
+            table = Table(tname, [seg])
         eng.register_device_segment(seg, table, dcs)
         fwd_bytes += sum((args.rows * dc.bits + 7) // 8 for dc in dcs)
-        dict_bytes += sum(4 * dc.cardinality for dc in dcs if dc.spec.name != "accountId")
+        # dictionaries the scan decodes: aggregated / grouped columns (config 2: all but accountId; config 3: the two
+        # SUM operands)
+        dec = ("lo_extendedprice", "lo_discount") if ssb else ("daysSinceEpoch", "clicks", "impressions")
+        dict_bytes += sum(4 * dc.cardinality for dc in dcs if dc.spec.name in dec)
         if s < args.cpu_sample_segments and rank == 0 and world == 1 and not args.no_cpu:
             dev_cols_sample.append((seg, [dc.host_column() for dc in dcs]))
         del dcs
     torch.cuda.synchronize()
-    table = Table("adAnalytics", segs)
+    table = Table(tname, segs)
     assert table.column_ids == table_cols
     gen_s = time.time() - t_gen
 
-    q = parse(synth.adanalytics_query(args.in_ids))
+    q = parse(synth.ssb_q11_query() if ssb else synth.adanalytics_query(args.in_ids))
     plan = eng.make_plan(table, q)
-    ks = plan.key_spaces[0]
-    if world > 1:  # the dense key space must be identical on every rank for the all-reduce
+    if world > 1 and plan.key_spaces:
+        ks = plan.key_spaces[0]  # the dense key space must be identical on every rank for the all-reduce
         kk = torch.tensor([ks.kind, ks.cardinality, ks.base], dtype=torch.int64, device=dev)
         allk = [torch.empty_like(kk) for _ in range(world)]
         dist.all_gather(allk, kk)
@@ -139,7 +149,7 @@ def main():
         from oracle.oracle import OracleEngine
         orc = OracleEngine(threads=1)
         hsegs = [ImmutableSegment(seg.name, args.rows, {c.name: c for c in cols}) for seg, cols in dev_cols_sample]
-        ht = Table("adAnalytics", hsegs)
+        ht = Table(tname, hsegs)
         o = orc.execute(ht, q)  # warm
         reps, tc0 = 0, time.perf_counter()
         while True:
@@ -160,7 +170,7 @@ def main():
     try:  # measured by rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same command (tools/profile_bench.sh)
         tj = json.load(open(args.traffic_file))
         tc = tj.get("config") or {}
-        if (tc.get("rows_per_gpu") == args.segments * args.rows and tc.get("in_list_size") == args.in_ids
+        if (not ssb and tc.get("rows_per_gpu") == args.segments * args.rows and tc.get("in_list_size") == args.in_ids
                 and tj.get("traffic_bytes_per_launch")):
             traffic_bytes = float(tj["traffic_bytes_per_launch"])
             traffic = traffic_bytes / (scan_avg_ms * 1e-3) / 1e9
@@ -169,14 +179,19 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": "rows/sec for filter+group-by SUM over 1B rows; % of HBM roofline, 1–8 GPUs",
+            "metric": ("rows/sec for filter + SUM(a*b) over SSB lineorder (config 3, secondary line)" if ssb else
+                       "rows/sec for filter+group-by SUM over 1B rows; % of HBM roofline, 1–8 GPUs"),
             "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "int64", "data": "synthetic (pinot_amd.synth, seed 42, Pinot segment format, device-generated)",
-            "config": {"workload": "AdAnalytics config 2: SUM(clicks), SUM(impressions) WHERE daysSinceEpoch BETWEEN "
-                                   "(90 of 365 days) AND accountId IN (1000 ids) GROUP BY daysSinceEpoch",
+            "config": {"workload": ("SSB config 3 (Q1.1 shape): SUM(lo_extendedprice * lo_discount) WHERE lo_orderdate "
+                                    "BETWEEN (365 of 2557 days) AND lo_discount BETWEEN 1 AND 3 AND lo_quantity < 25"
+                                    if ssb else
+                                    "AdAnalytics config 2: SUM(clicks), SUM(impressions) WHERE daysSinceEpoch BETWEEN "
+                                    "(90 of 365 days) AND accountId IN (1000 ids) GROUP BY daysSinceEpoch"),
                        "rows_per_gpu": rows_per_gpu, "segments_per_gpu": args.segments,
-                       "rows_per_segment": args.rows, "in_list_size": args.in_ids, "parallelism": f"segments x{world}"},
+                       "rows_per_segment": args.rows, "in_list_size": None if ssb else args.in_ids,
+                       "parallelism": f"segments x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "scan_kernel", "kernel_ms": scan_avg_ms, "algorithmic_bytes": alg_bytes,

@@ -651,9 +651,9 @@ void assign_reach(const std::vector<FNode>& nodes, int n, double reach, std::vec
 
 struct ThreadCtx {  // per calling thread: staging + events, created once
   PinnedBuf pinned;
-  PinnedBuf readback;
+  PinnedBuf readback;  // per-segment match counts + error word, copied back before the one stream sync
   std::vector<uint8_t> arena;   // host image of the parameter arena (capacity reused across queries)
-  std::vector<WorkItem> items;  // work items of the current query (capacity reused across queries)  // per-segment match counts + error word, copied back before the one stream sync
+  std::vector<WorkItem> items;  // work items of the current query (capacity reused across queries)
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   int init() {
     if (ev[0]) return PG_OK;

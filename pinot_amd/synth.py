@@ -50,6 +50,22 @@ def adanalytics_query(num_ids: int = 1000) -> str:
             "GROUP BY daysSinceEpoch ORDER BY daysSinceEpoch LIMIT 400")
 
 
+# Config 3: SSB-style lineorder; dates as day numbers (8035 = 1992-01-01), 2 557 days
+SSB_LINEORDER = [
+    ColSpec("lo_orderdate", 8035, 2557),
+    ColSpec("lo_discount", 0, 11),
+    ColSpec("lo_quantity", 1, 50),
+    ColSpec("lo_extendedprice", 90_000, 1 << 20),
+]
+SSB_SEGMENTS_PER_GPU = 96  # 768 segments of 7 812 500 rows = 6 B rows over 8 GPUs
+
+
+def ssb_q11_query() -> str:
+    """Config 3 query (SSB Q1.1 shape): one year of orders, discount 1..3, quantity < 25."""
+    return ("SELECT SUM(lo_extendedprice * lo_discount) FROM lineorder "
+            "WHERE lo_orderdate BETWEEN 8035 AND 8399 AND lo_discount BETWEEN 1 AND 3 AND lo_quantity < 25")
+
+
 def column_salt(name: str) -> int:
     return (zlib.crc32(name.encode()) ^ (SEED * 0x9E3779B1)) & M32
 

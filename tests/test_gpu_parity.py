@@ -96,6 +96,17 @@ def test_config2_shape_small(gpu_engine, oracle_engine):
     assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q))
 
 
+def test_config3_ssb_shape_small(gpu_engine, oracle_engine):
+    """Config 3 (SSB Q1.1 shape): three range filters + SUM(lo_extendedprice * lo_discount), integer-exact."""
+    from pinot_amd import synth
+    segs = [synth.make_segment_np(synth.SSB_LINEORDER, s, 120_007) for s in range(3)]
+    t = Table("lineorder", segs)
+    q = parse(synth.ssb_q11_query())
+    g, o = gpu_engine.execute(t, q), oracle_engine.execute(t, q)
+    assert g.stats.num_docs_scanned > 0
+    assert_same_result(g, o)
+
+
 def test_device_generated_segments_match_host_bytes(gpu_engine, oracle_engine):
     """Segments generated on the GPU (bench path) give the same results as their host copies through the oracle."""
     import torch

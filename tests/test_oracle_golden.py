@@ -74,3 +74,21 @@ def test_oracle_sees_filter_shortcuts(expected, sv_table_inner):
     assert kinds["column11"] == abi.PG_LEAF_INVERTED
     assert kinds["column1"] == abi.PG_LEAF_SV_SCAN
     assert kinds["column6"] == abi.PG_LEAF_SV_SCAN  # RANGE never uses the bitmap index
+
+
+def test_ssb_synthetic_oracle_matches_numpy():
+    """The oracle on a small config-3 (SSB Q1.1 shape) segment equals a direct numpy evaluation of the query."""
+    import numpy as np
+    from oracle.oracle import OracleEngine
+    from pinot_amd import synth
+    from pinot_amd.plan import Table
+    from pinot_amd.query import parse
+    n = 50_003
+    seg = synth.make_segment_np(synth.SSB_LINEORDER, 0, n)
+    v = {c.name: synth.values_np(c, 0, n) for c in synth.SSB_LINEORDER}
+    m = ((v["lo_orderdate"] >= 8035) & (v["lo_orderdate"] <= 8399) & (v["lo_discount"] >= 1)
+         & (v["lo_discount"] <= 3) & (v["lo_quantity"] < 25))
+    want = float((v["lo_extendedprice"][m] * v["lo_discount"][m]).sum())
+    r = OracleEngine(threads=1).execute(Table("lineorder", [seg]), parse(synth.ssb_q11_query()))
+    assert r.stats.num_docs_scanned == int(m.sum())
+    assert r.rows[()][0] == want
