@@ -1167,10 +1167,12 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
     memset(q.agg_slot, kNoSlot, sizeof(q.agg_slot));
     memset(q.key_slot, kNoSlot, sizeof(q.key_slot));
     static const char* no_stage = getenv("PG_NO_STAGING");
+    // minimum expected needed docs per 128-byte line for staging (PG_STAGE_MIN overrides)
+    static const double stage_min = getenv("PG_STAGE_MIN") ? atof(getenv("PG_STAGE_MIN")) : 1.0;
     uint32_t words = 0;
     for (const Cand& c : cands) {
       if (no_stage || q.num_staged >= (uint32_t)kMaxStaged) break;
-      if (c.reach * 1024.0 / c.bmax < 1.0) continue;
+      if (c.reach * 1024.0 / c.bmax < stage_min) continue;
       const uint32_t need = (uint32_t)(kTileDocs / 32) * c.bmax;  // b DMA pieces of 1 KiB
       if ((words + need) * 4ull > (uint64_t)kLdsStageBytes) continue;
       const uint32_t slot = q.num_staged++;
@@ -1350,7 +1352,12 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
     static int dev_cus = 0;
     if (!dev_cus && hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g_device) != hipSuccess) dev_cus = 256;
     static int per_cu = 0;
-    if (!per_cu) { const char* e = getenv("PG_SCAN_BLOCKS_PER_CU"); per_cu = e ? std::max(1, atoi(e)) : 8; }
+    // a whole number of resident rounds of blocks (3 resident per CU -> 6): no partial last round.  Measured on
+    // config 2 / config 3: 6 -> 0.94 / 1.75 ms, 8 -> 0.97 / 1.93 ms, 5 -> 1.01 / 1.99 ms, 7 -> 1.03 / 2.01 ms.
+    if (!per_cu) {
+      const char* e = getenv("PG_SCAN_BLOCKS_PER_CU");
+      per_cu = e ? std::max(1, atoi(e)) : 2 * (int)scan_min_blocks_per_cu();
+    }
     blocks = (uint32_t)std::min<uint64_t>(q.num_items, (uint64_t)dev_cus * per_cu);
     t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
     HIP_CHECK(launch_scan(q, blocks, s));
