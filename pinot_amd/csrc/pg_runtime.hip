@@ -654,6 +654,7 @@ struct ThreadCtx {  // per calling thread: staging + events, created once
   PinnedBuf readback;  // per-segment match counts + error word, copied back before the one stream sync
   std::vector<uint8_t> arena;   // host image of the parameter arena (capacity reused across queries)
   std::vector<WorkItem> items;  // work items of the current query (capacity reused across queries)
+  std::vector<WorkItem> items_perm;  // XCD-grouped order of the items (swapped with `items`)
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   int init() {
     if (ev[0]) return PG_OK;
@@ -1280,6 +1281,58 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   const uint64_t off_aggcols = ar.reserve(aggcols.size() * sizeof(ColDesc));
   const uint64_t off_keycols = ar.reserve(keycols.size() * sizeof(ColDesc));
   const uint64_t off_segs = ar.reserve(segd.size() * sizeof(SegDesc));
+  uint32_t blocks = 0;
+  if (!items.empty()) {
+    static int dev_cus = 0;
+    if (!dev_cus && hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g_device) != hipSuccess) dev_cus = 256;
+    static int per_cu = 0;
+    // a whole number of resident rounds of blocks (3 resident per CU -> 6): no partial last round.  Measured on
+    // config 2 / config 3: 6 -> 0.94 / 1.75 ms, 8 -> 0.97 / 1.93 ms, 5 -> 1.01 / 1.99 ms, 7 -> 1.03 / 2.01 ms.
+    if (!per_cu) {
+      const char* e = getenv("PG_SCAN_BLOCKS_PER_CU");
+      per_cu = e ? std::max(1, atoi(e)) : 2 * (int)scan_min_blocks_per_cu();
+    }
+    blocks = (uint32_t)std::min<uint64_t>(items.size(), (uint64_t)dev_cus * per_cu);
+    // XCD-grouped item order when the query decodes a large dictionary for many docs (> 16 decodes per
+    // 128-byte dictionary line per segment; SSB SUM(lo_extendedprice) over all rows: 13.2 -> 4.7 ms): workgroups are dispatched round-robin over the 8 XCDs (block b ->
+    // XCD b % 8), each with its own L2.  Give each XCD a contiguous run of segments and, within it, interleave
+    // the items step-major over the XCD's blocks, so at any moment the blocks of one XCD scan the same segment
+    // and share its dictionary lines in their L2 (instead of every XCD pulling every dictionary).
+    uint64_t dict_lines = 0;
+    for (uint32_t si = 0; si < S; si++) {
+      uint64_t seg_lines = 0;
+      for (uint32_t a = 0; a < A; a++)
+        for (int k = 0; k < 2; k++) {
+          const ColDesc& dc = aggcols[((uint64_t)si * A + a) * 2 + k];
+          if (dc.dict) seg_lines = std::max<uint64_t>(seg_lines, (uint64_t)dc.card * (dc.dtype == PG_INT || dc.dtype == PG_FLOAT ? 4 : 8) / 128);
+        }
+      for (uint32_t k = 0; k < K; k++) {
+        const ColDesc& dc = keycols[(uint64_t)si * K + k];
+        if (dc.dict && plan->keys[k].kind != PG_KEY_KEYMAP)
+          seg_lines = std::max<uint64_t>(seg_lines, (uint64_t)dc.card * (dc.dtype == PG_INT || dc.dtype == PG_FLOAT ? 4 : 8) / 128);
+      }
+      dict_lines = std::max(dict_lines, seg_lines);
+    }
+    const double decodes = filter_pass * (double)total_docs / std::max(1u, S);
+    static const char* xcd_env = getenv("PG_XCD_ORDER");
+    const bool want_xcd = xcd_env ? atoi(xcd_env) != 0 : (dict_lines >= 2048 && decodes > 16.0 * (double)dict_lines);
+    constexpr uint32_t kXcds = 8;
+    if (want_xcd && blocks % kXcds == 0 && blocks >= 2 * kXcds) {
+      const uint64_t N = items.size();
+      std::vector<WorkItem>& out = t_ctx.items_perm;
+      out.resize(N);
+      auto range_len = [&](uint32_t b) { return (uint32_t)(((uint64_t)b + 1) * N / blocks - (uint64_t)b * N / blocks); };
+      uint64_t next = 0;  // next item (segment order) to hand out
+      for (uint32_t x = 0; x < kXcds; x++) {
+        uint32_t max_r = 0;
+        for (uint32_t b = x; b < blocks; b += kXcds) max_r = std::max(max_r, range_len(b));
+        for (uint32_t j = 0; j < max_r; j++)
+          for (uint32_t b = x; b < blocks; b += kXcds)
+            if (j < range_len(b)) out[(uint64_t)b * N / blocks + j] = items[next++];
+      }
+      items.swap(out);
+    }
+  }
   const uint64_t off_items = ar.put(items.data(), items.size() * sizeof(WorkItem));
   const uint64_t off_lutjobs = ar.reserve(luts.size() * sizeof(LutJob));
   DevBuf arena, scratch;
@@ -1347,18 +1400,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   HIP_CHECK(hipEventRecord(ev[1], s));
   if (is_cancelled(plan->query_id)) { (void)hipStreamSynchronize(s); return fail(PG_E_CANCELLED, "query %llu cancelled", (unsigned long long)plan->query_id); }
   if (plan->deadline_ms && now_ms() > plan->deadline_ms) { (void)hipStreamSynchronize(s); return fail(PG_E_TIMEOUT, "deadline passed"); }
-  uint32_t blocks = 0;
   if (q.num_items) {
-    static int dev_cus = 0;
-    if (!dev_cus && hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g_device) != hipSuccess) dev_cus = 256;
-    static int per_cu = 0;
-    // a whole number of resident rounds of blocks (3 resident per CU -> 6): no partial last round.  Measured on
-    // config 2 / config 3: 6 -> 0.94 / 1.75 ms, 8 -> 0.97 / 1.93 ms, 5 -> 1.01 / 1.99 ms, 7 -> 1.03 / 2.01 ms.
-    if (!per_cu) {
-      const char* e = getenv("PG_SCAN_BLOCKS_PER_CU");
-      per_cu = e ? std::max(1, atoi(e)) : 2 * (int)scan_min_blocks_per_cu();
-    }
-    blocks = (uint32_t)std::min<uint64_t>(q.num_items, (uint64_t)dev_cus * per_cu);
     t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
     HIP_CHECK(launch_scan(q, blocks, s));
   }

@@ -107,6 +107,19 @@ def test_config3_ssb_shape_small(gpu_engine, oracle_engine):
     assert_same_result(g, o)
 
 
+def test_large_dictionary_dense_decode(gpu_engine, oracle_engine):
+    """Dense aggregation over a large-dictionary column: triggers the XCD-grouped work-item order (items of one
+    segment interleaved over one XCD's blocks); results must not depend on the order."""
+    from pinot_amd import synth
+    segs = [synth.make_segment_np(synth.SSB_LINEORDER, s, 300_000) for s in range(4)]
+    t = Table("lineorder", segs)
+    for sql in ["SELECT SUM(lo_extendedprice), MIN(lo_extendedprice), MAX(lo_extendedprice), COUNT(*) FROM t",
+                "SELECT lo_discount, SUM(lo_extendedprice), AVG(lo_extendedprice) FROM t GROUP BY lo_discount",
+                "SELECT DISTINCTCOUNT(lo_quantity), SUM(lo_extendedprice * lo_quantity) FROM t WHERE lo_quantity > 3"]:
+        q = parse(sql)
+        assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q))
+
+
 def test_device_generated_segments_match_host_bytes(gpu_engine, oracle_engine):
     """Segments generated on the GPU (bench path) give the same results as their host copies through the oracle."""
     import torch

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--rows", type=int, default=7_812_500)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only", default="")
+    ap.add_argument("--workload", choices=("adanalytics", "ssb"), default="adanalytics")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -29,7 +30,8 @@ def main():
     segs = []
     table = None
     for s in range(args.segments):
-        dcs = synth.make_columns_torch(synth.ADANALYTICS, s, args.rows, torch.device("cuda"))
+        specs = synth.SSB_LINEORDER if args.workload == "ssb" else synth.ADANALYTICS
+        dcs = synth.make_columns_torch(specs, s, args.rows, torch.device("cuda"))
         seg = ImmutableSegment(f"a{s}", args.rows, {dc.spec.name: dc.meta_column() for dc in dcs})
         segs.append(seg)
         if table is None:
@@ -37,7 +39,15 @@ def main():
         eng.register_device_segment(seg, table, dcs)
     table = Table("adAnalytics", segs)
     ids = ", ".join(str((i * 7919 + 13) % 1_000_000) for i in range(1000))
+    f3 = "lo_orderdate BETWEEN 8035 AND 8399 AND lo_discount BETWEEN 1 AND 3 AND lo_quantity < 25"
     qs = {
+        "ssb_count": f"SELECT COUNT(*) FROM t WHERE {f3}",
+        "ssb_date": "SELECT COUNT(*) FROM t WHERE lo_orderdate BETWEEN 8035 AND 8399",
+        "ssb_sum_small": f"SELECT SUM(lo_discount * lo_quantity) FROM t WHERE {f3}",
+        "ssb_sum_price": f"SELECT SUM(lo_extendedprice) FROM t WHERE {f3}",
+        "ssb_q11": synth.ssb_q11_query(),
+        "ssb_dense_price": "SELECT SUM(lo_extendedprice) FROM t",
+    } if args.workload == "ssb" else {
         "count": "SELECT COUNT(*) FROM t",
         "in_only": f"SELECT COUNT(*) FROM t WHERE accountId IN ({ids})",
         "range_only": "SELECT COUNT(*) FROM t WHERE daysSinceEpoch BETWEEN 18000 AND 18089",
