@@ -666,6 +666,22 @@ thread_local ThreadCtx t_ctx;
 
 bool pl_too_big(uint32_t ints) { return ints * 4ull > (uint64_t)kLdsSetBytes; }
 
+// Upper bound of the scan grid: a whole number of resident rounds of blocks (3 resident per CU -> 6 per CU, no
+// partial last round).  Measured on config 2 / config 3: 6 -> 0.94 / 1.75 ms, 8 -> 0.97 / 1.93 ms, 5 -> 1.01 /
+// 1.99 ms, 7 -> 1.03 / 2.01 ms.  PG_SCAN_BLOCKS_PER_CU overrides.
+uint64_t scan_grid_cap() {
+  static uint64_t cap = 0;
+  if (!cap) {
+    int dev_cus = 0;
+    if (hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g_device) != hipSuccess || dev_cus <= 0)
+      dev_cus = 256;
+    const char* e = getenv("PG_SCAN_BLOCKS_PER_CU");
+    const int per_cu = e ? std::max(1, atoi(e)) : 2 * (int)scan_min_blocks_per_cu();
+    cap = (uint64_t)dev_cus * per_cu;
+  }
+  return cap;
+}
+
 int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   const double t_enter = wall_ms();
   if (!plan) return fail(PG_E_INVALID, "null plan");
@@ -950,11 +966,11 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   struct Patch { uint64_t leaf_index; uint64_t off; bool in_arena; int target; };
   std::vector<Patch> patches;
 
+  std::vector<uint32_t> seg_tiles(S, 0);
   for (uint32_t si = 0; si < S; si++) {
     const pg_segment_ref& sr = plan->segments[si];
     segd[si].num_docs = sr.num_docs;
-    const uint32_t tiles = (uint32_t)(((uint64_t)sr.num_docs + kTileDocs - 1) / kTileDocs);
-    for (uint32_t t = 0; t < tiles; t += kItemTiles) items.push_back({si, t, std::min(tiles, t + (uint32_t)kItemTiles), 0});
+    seg_tiles[si] = (uint32_t)(((uint64_t)sr.num_docs + kTileDocs - 1) / kTileDocs);
     for (uint32_t li = 0; li < L; li++) {
       const pg_leaf& pl = sr.leaves[li];
       LeafDesc& dl = leaves[(uint64_t)si * L + li];
@@ -1120,6 +1136,63 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
     }
   }
   P.entries_in_filter = entries_in_filter;
+  uint64_t dict_lines = 0;
+  for (uint32_t si = 0; si < S; si++) {
+    uint64_t seg_lines = 0;
+    for (uint32_t a = 0; a < A; a++)
+      for (int k = 0; k < 2; k++) {
+        const ColDesc& dc = aggcols[((uint64_t)si * A + a) * 2 + k];
+        if (dc.dict) seg_lines = std::max<uint64_t>(seg_lines, (uint64_t)dc.card * (dc.dtype == PG_INT || dc.dtype == PG_FLOAT ? 4 : 8) / 128);
+      }
+    for (uint32_t k = 0; k < K; k++) {
+      const ColDesc& dc = keycols[(uint64_t)si * K + k];
+      if (dc.dict && plan->keys[k].kind != PG_KEY_KEYMAP)
+        seg_lines = std::max<uint64_t>(seg_lines, (uint64_t)dc.card * (dc.dtype == PG_INT || dc.dtype == PG_FLOAT ? 4 : 8) / 128);
+    }
+    dict_lines = std::max(dict_lines, seg_lines);
+  }
+  const double decodes = filter_pass * (double)total_docs / std::max(1u, S);
+  static const char* xcd_env = getenv("PG_XCD_ORDER");
+  const bool want_xcd = xcd_env ? atoi(xcd_env) != 0 : (dict_lines >= 2048 && decodes > 16.0 * (double)dict_lines);
+  // ---- work items.  Balanced form: the concatenated tile sequence of all segments is cut into G equal ranges, one
+  // per block, each given as exactly 2 items (split at the segment boundary it crosses, else halved), so the kernel's
+  // uniform [2b, 2b + 2) item ranges are tile-exact (+-1 tile per block) and the host emits 2G items instead of one
+  // per kItemTiles tiles.  Needs every non-empty segment to hold at least one block's range (so a range crosses at
+  // most one boundary); otherwise (and for the XCD-grouped order below, which wants fine items) items of kItemTiles
+  // tiles.
+  uint32_t grid = 0;
+  {
+    uint64_t T = 0;
+    uint32_t min_tiles = 0xFFFFFFFFu;
+    for (uint32_t si = 0; si < S; si++)
+      if (seg_tiles[si]) { T += seg_tiles[si]; min_tiles = std::min(min_tiles, seg_tiles[si]); }
+    const uint64_t G = std::min<uint64_t>(scan_grid_cap(), T / 2);
+    static const char* bal_env = getenv("PG_BALANCED_ITEMS");
+    const bool balanced = (bal_env ? atoi(bal_env) != 0 : !want_xcd) && G >= 1 && (T + G - 1) / G <= min_tiles;
+    if (balanced) {
+      items.resize(2 * G);
+      uint32_t si = 0;
+      uint64_t seg_first = 0;  // global index of segment si's first tile
+      auto advance = [&](uint64_t t) {  // move si to the segment holding global tile t
+        while (!seg_tiles[si] || t >= seg_first + seg_tiles[si]) { seg_first += seg_tiles[si]; si++; }
+      };
+      for (uint64_t b = 0; b < G; b++) {
+        const uint64_t t0 = b * T / G, t1 = (b + 1) * T / G;  // >= 2 tiles, since G <= T / 2
+        advance(t0);
+        const uint64_t seg_end = seg_first + seg_tiles[si];
+        const uint64_t cut = t1 > seg_end ? seg_end : t0 + (t1 - t0) / 2;
+        items[2 * b] = {si, (uint32_t)(t0 - seg_first), (uint32_t)(cut - seg_first), 0};
+        advance(cut);
+        items[2 * b + 1] = {si, (uint32_t)(cut - seg_first), (uint32_t)(t1 - seg_first), 0};
+      }
+      grid = (uint32_t)G;
+    } else {
+      for (uint32_t s2 = 0; s2 < S; s2++)
+        for (uint32_t t = 0; t < seg_tiles[s2]; t += kItemTiles)
+          items.push_back({s2, t, std::min(seg_tiles[s2], t + (uint32_t)kItemTiles), 0});
+      grid = (uint32_t)std::min<uint64_t>(items.size(), scan_grid_cap());
+    }
+  }
   q.num_items = (uint32_t)items.size();
 
   // ---- staging policy: a packed column is staged per tile (coalesced, every byte used) when the docs the query
@@ -1283,39 +1356,12 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   const uint64_t off_segs = ar.reserve(segd.size() * sizeof(SegDesc));
   uint32_t blocks = 0;
   if (!items.empty()) {
-    static int dev_cus = 0;
-    if (!dev_cus && hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g_device) != hipSuccess) dev_cus = 256;
-    static int per_cu = 0;
-    // a whole number of resident rounds of blocks (3 resident per CU -> 6): no partial last round.  Measured on
-    // config 2 / config 3: 6 -> 0.94 / 1.75 ms, 8 -> 0.97 / 1.93 ms, 5 -> 1.01 / 1.99 ms, 7 -> 1.03 / 2.01 ms.
-    if (!per_cu) {
-      const char* e = getenv("PG_SCAN_BLOCKS_PER_CU");
-      per_cu = e ? std::max(1, atoi(e)) : 2 * (int)scan_min_blocks_per_cu();
-    }
-    blocks = (uint32_t)std::min<uint64_t>(items.size(), (uint64_t)dev_cus * per_cu);
+    blocks = grid;
     // XCD-grouped item order when the query decodes a large dictionary for many docs (> 16 decodes per
     // 128-byte dictionary line per segment; SSB SUM(lo_extendedprice) over all rows: 13.2 -> 4.7 ms): workgroups are dispatched round-robin over the 8 XCDs (block b ->
     // XCD b % 8), each with its own L2.  Give each XCD a contiguous run of segments and, within it, interleave
     // the items step-major over the XCD's blocks, so at any moment the blocks of one XCD scan the same segment
     // and share its dictionary lines in their L2 (instead of every XCD pulling every dictionary).
-    uint64_t dict_lines = 0;
-    for (uint32_t si = 0; si < S; si++) {
-      uint64_t seg_lines = 0;
-      for (uint32_t a = 0; a < A; a++)
-        for (int k = 0; k < 2; k++) {
-          const ColDesc& dc = aggcols[((uint64_t)si * A + a) * 2 + k];
-          if (dc.dict) seg_lines = std::max<uint64_t>(seg_lines, (uint64_t)dc.card * (dc.dtype == PG_INT || dc.dtype == PG_FLOAT ? 4 : 8) / 128);
-        }
-      for (uint32_t k = 0; k < K; k++) {
-        const ColDesc& dc = keycols[(uint64_t)si * K + k];
-        if (dc.dict && plan->keys[k].kind != PG_KEY_KEYMAP)
-          seg_lines = std::max<uint64_t>(seg_lines, (uint64_t)dc.card * (dc.dtype == PG_INT || dc.dtype == PG_FLOAT ? 4 : 8) / 128);
-      }
-      dict_lines = std::max(dict_lines, seg_lines);
-    }
-    const double decodes = filter_pass * (double)total_docs / std::max(1u, S);
-    static const char* xcd_env = getenv("PG_XCD_ORDER");
-    const bool want_xcd = xcd_env ? atoi(xcd_env) != 0 : (dict_lines >= 2048 && decodes > 16.0 * (double)dict_lines);
     constexpr uint32_t kXcds = 8;
     if (want_xcd && blocks % kXcds == 0 && blocks >= 2 * kXcds) {
       const uint64_t N = items.size();
