@@ -205,16 +205,21 @@ class GpuEngine:
         keys = np.ctypeslib.as_array(r.keys, shape=(max(G * K, 1),))[:G * K].reshape(G, K) if G and K else \
             np.zeros((G, K), dtype=np.uint32)
         rows = {}
+        # plain Python lists: one conversion per array instead of a numpy scalar access per element
+        vals_l, cnts_l, keys_l = vals.tolist(), cnts.tolist(), keys.tolist()
+        kval = [plan.key_spaces[k].value for k in range(K)]
+        kinds = [0 if ag.function in ("COUNT", "COUNTMV", "DISTINCTCOUNT") else 1 if ag.function == "AVG" else 2
+                 for ag in plan.aggs]
         for g in range(G):
-            key = tuple(plan.key_spaces[k].value(int(keys[g, k])) for k in range(K))
+            kg, vg, cg = keys_l[g], vals_l[g], cnts_l[g]
+            key = tuple(kval[k](kg[k]) for k in range(K))
             row = []
-            for a, ag in enumerate(plan.aggs):
-                v = float(vals[g, a])
-                f = ag.function
-                if f in ("COUNT", "COUNTMV", "DISTINCTCOUNT"):
+            for a, kind in enumerate(kinds):
+                v = float(vg[a])
+                if kind == 0:
                     row.append(int(round(v)))
-                elif f == "AVG":
-                    row.append((v, int(cnts[g, a])))
+                elif kind == 1:
+                    row.append((v, int(cg[a])))
                 else:
                     row.append(v)
             rows[key] = row
