@@ -180,7 +180,7 @@ __host__ __device__ inline double order_key_decode(int64_t k) {
 // ---- kernel launchers
 hipError_t launch_scan(const QuerySpec& q, uint32_t blocks, hipStream_t s);                  // pg_scan.hip
 size_t scan_lds_bytes(const QuerySpec& q);
-uint32_t scan_min_blocks_per_cu();
+uint32_t scan_min_blocks_per_cu(bool grouped);
 hipError_t launch_init_state(const QuerySpec& q, hipStream_t s);                             // pg_kernels.hip
 hipError_t launch_bswap_words(const uint8_t* src, uint32_t* dst, uint64_t nbytes, uint64_t nwords_out, hipStream_t s);
 hipError_t launch_be_to_native(const uint8_t* src, void* dst, uint64_t n, uint32_t width, hipStream_t s);

@@ -666,17 +666,18 @@ thread_local ThreadCtx t_ctx;
 
 bool pl_too_big(uint32_t ints) { return ints * 4ull > (uint64_t)kLdsSetBytes; }
 
-// Upper bound of the scan grid: a whole number of resident rounds of blocks (3 resident per CU -> 6 per CU, no
+// Upper bound of the scan grid: a whole number of resident rounds of blocks (2 x the resident blocks per CU, no
 // partial last round).  Measured on config 2 / config 3: 6 -> 0.94 / 1.75 ms, 8 -> 0.97 / 1.93 ms, 5 -> 1.01 /
 // 1.99 ms, 7 -> 1.03 / 2.01 ms.  PG_SCAN_BLOCKS_PER_CU overrides.
-uint64_t scan_grid_cap() {
-  static uint64_t cap = 0;
+uint64_t scan_grid_cap(bool grouped) {
+  static uint64_t caps[2] = {0, 0};
+  uint64_t& cap = caps[grouped ? 1 : 0];
   if (!cap) {
     int dev_cus = 0;
     if (hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g_device) != hipSuccess || dev_cus <= 0)
       dev_cus = 256;
     const char* e = getenv("PG_SCAN_BLOCKS_PER_CU");
-    const int per_cu = e ? std::max(1, atoi(e)) : 2 * (int)scan_min_blocks_per_cu();
+    const int per_cu = e ? std::max(1, atoi(e)) : 2 * (int)scan_min_blocks_per_cu(grouped);
     cap = (uint64_t)dev_cus * per_cu;
   }
   return cap;
@@ -1166,7 +1167,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
     uint32_t min_tiles = 0xFFFFFFFFu;
     for (uint32_t si = 0; si < S; si++)
       if (seg_tiles[si]) { T += seg_tiles[si]; min_tiles = std::min(min_tiles, seg_tiles[si]); }
-    const uint64_t G = std::min<uint64_t>(scan_grid_cap(), T / 2);
+    const uint64_t G = std::min<uint64_t>(scan_grid_cap(K > 0), T / 2);
     static const char* bal_env = getenv("PG_BALANCED_ITEMS");
     const bool balanced = (bal_env ? atoi(bal_env) != 0 : !want_xcd) && G >= 1 && (T + G - 1) / G <= min_tiles;
     if (balanced) {
@@ -1190,7 +1191,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
       for (uint32_t s2 = 0; s2 < S; s2++)
         for (uint32_t t = 0; t < seg_tiles[s2]; t += kItemTiles)
           items.push_back({s2, t, std::min(seg_tiles[s2], t + (uint32_t)kItemTiles), 0});
-      grid = (uint32_t)std::min<uint64_t>(items.size(), scan_grid_cap());
+      grid = (uint32_t)std::min<uint64_t>(items.size(), scan_grid_cap(K > 0));
     }
   }
   q.num_items = (uint32_t)items.size();
@@ -1329,7 +1330,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
     // blocks per CU as the register budget does (PG_SCAN_MIN_WAVES); else one.  PG_STAGE_RING=1|2 overrides.
     static const char* ring_env = getenv("PG_STAGE_RING");
     q.stage_ring = 2;
-    const bool fits = q.num_staged && scan_lds_bytes(q) * (size_t)scan_min_blocks_per_cu() <= 160 * 1024;
+    const bool fits = q.num_staged && scan_lds_bytes(q) * (size_t)scan_min_blocks_per_cu(K > 0) <= 160 * 1024;
     q.stage_ring = ring_env ? (atoi(ring_env) > 1 ? 2 : 1) : (fits ? 2 : 1);
   }
   const size_t lds_bytes = scan_lds_bytes(q);
