@@ -668,16 +668,17 @@ bool pl_too_big(uint32_t ints) { return ints * 4ull > (uint64_t)kLdsSetBytes; }
 
 // Upper bound of the scan grid: a whole number of resident rounds of blocks (2 x the resident blocks per CU, no
 // partial last round).  Measured on config 2 / config 3: 6 -> 0.94 / 1.75 ms, 8 -> 0.97 / 1.93 ms, 5 -> 1.01 /
-// 1.99 ms, 7 -> 1.03 / 2.01 ms.  PG_SCAN_BLOCKS_PER_CU overrides.
-uint64_t scan_grid_cap(bool grouped) {
-  static uint64_t caps[2] = {0, 0};
-  uint64_t& cap = caps[grouped ? 1 : 0];
+// 1.99 ms, 7 -> 1.03 / 2.01 ms.  `one_round`: one resident round (the XCD-grouped order).  PG_SCAN_BLOCKS_PER_CU
+// overrides both.
+uint64_t scan_grid_cap(bool grouped, bool one_round = false) {
+  static uint64_t caps[4] = {0, 0, 0, 0};
+  uint64_t& cap = caps[(grouped ? 1 : 0) + (one_round ? 2 : 0)];
   if (!cap) {
     int dev_cus = 0;
     if (hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g_device) != hipSuccess || dev_cus <= 0)
       dev_cus = 256;
     const char* e = getenv("PG_SCAN_BLOCKS_PER_CU");
-    const int per_cu = e ? std::max(1, atoi(e)) : 2 * (int)scan_min_blocks_per_cu(grouped);
+    const int per_cu = e ? std::max(1, atoi(e)) : (one_round ? 1 : 2) * (int)scan_min_blocks_per_cu(grouped);
     cap = (uint64_t)dev_cus * per_cu;
   }
   return cap;
@@ -1191,7 +1192,9 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
       for (uint32_t s2 = 0; s2 < S; s2++)
         for (uint32_t t = 0; t < seg_tiles[s2]; t += kItemTiles)
           items.push_back({s2, t, std::min(seg_tiles[s2], t + (uint32_t)kItemTiles), 0});
-      grid = (uint32_t)std::min<uint64_t>(items.size(), scan_grid_cap(K > 0));
+      // the XCD-grouped order wants every block resident at once (one round), so the step-major interleave holds:
+      // dense SUM over a 4 MB dictionary 6.4 ms at 2 rounds -> 4.3 ms at 1 round
+      grid = (uint32_t)std::min<uint64_t>(items.size(), scan_grid_cap(K > 0, want_xcd));
     }
   }
   q.num_items = (uint32_t)items.size();
