@@ -157,6 +157,26 @@ def test_ragged_sizes(n, gpu_engine, oracle_engine):
         assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q))
 
 
+def test_balanced_split_over_ragged_segments(gpu_engine, oracle_engine):
+    """Unequal segments (13/31/22/4 tiles of 8 192 docs): the balanced work split cuts the concatenated tile sequence
+    into equal per-block ranges that straddle segment boundaries; per-segment state (match counts, IN sets, dictIds
+    per segment dictionary) must still land in the right segment."""
+    rng = np.random.default_rng(7)
+    segs = []
+    for i, n in enumerate([100_000, 250_001, 180_000, 8193 * 3]):
+        data = {"k": rng.integers(0, 40, n), "v": rng.integers(-5000, 5000, n), "w": rng.integers(0, 300_000, n)}
+        segs.append(_seg(f"b{i}", data, {"k": "INT", "v": "LONG", "w": "INT"}))
+    t = Table("t", segs)
+    ids = ", ".join(str(x) for x in range(0, 300_000, 97))
+    for sql in ["SELECT COUNT(*), SUM(v), MIN(w), MAX(v) FROM t",
+                f"SELECT k, COUNT(*), SUM(v) FROM t WHERE w IN ({ids}) GROUP BY k",
+                "SELECT k, AVG(v), DISTINCTCOUNT(w) FROM t WHERE v BETWEEN -100 AND 2500 GROUP BY k"]:
+        q = parse(sql)
+        g, o = gpu_engine.execute(t, q), oracle_engine.execute(t, q)
+        assert_same_result(g, o)
+        assert g.stats.num_segments_matched == o.stats.num_segments_matched
+
+
 def test_empty_and_all_filtered(gpu_engine, oracle_engine):
     rng = np.random.default_rng(1)
     seg = _seg("e", {"a": rng.integers(0, 10, 5000), "b": rng.integers(0, 100, 5000)}, {"a": "INT", "b": "INT"})
