@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 1
+#define PG_ABI_VERSION 2
 
 typedef enum pg_status {
   PG_OK = 0,
@@ -142,7 +142,7 @@ typedef enum pg_agg_fn {
   PG_AGG_MIN = 2,           /* MinAggregationFunction                              -> double         */
   PG_AGG_MAX = 3,           /* MaxAggregationFunction                              -> double         */
   PG_AGG_AVG = 4,           /* AvgAggregationFunction                              -> (sum, count)   */
-  PG_AGG_DISTINCTCOUNT = 5, /* DistinctCountAggregationFunction (dictionary path) -> #distinct keys  */
+  PG_AGG_DISTINCTCOUNT = 5, /* DistinctCountAggregationFunction (dictionary path) -> value set / size */
   PG_AGG_COUNTMV = 6        /* CountMVAggregationFunction                          -> sum numValues  */
 } pg_agg_fn;
 
@@ -184,6 +184,26 @@ typedef struct pg_segment_ref {
   const pg_leaf *leaves;    /* plan.num_leaves entries */
 } pg_segment_ref;
 
+/* ORDER BY item for the device-side trim of a group-by result (IndexedTable.finish ->
+ * TableResizer.getTopRecords, data/table/IndexedTable.java:147-158, TableResizer.java:248).  AGG items order
+ * by the aggregation's final value (AVG: sum / count, DISTINCTCOUNT: set size); KEY items by the key's
+ * table-global id, which is value order for both key kinds. */
+typedef enum pg_order_kind { PG_ORDER_AGG = 0, PG_ORDER_KEY = 1 } pg_order_kind;
+typedef struct pg_order {
+  uint32_t kind;            /* pg_order_kind */
+  uint32_t index;           /* aggregation index (AGG) or group-key index (KEY) */
+  uint32_t desc;            /* 1 = DESC */
+  uint32_t pad;
+} pg_order;
+
+#define PG_PLAN_VALUE_SETS 0x1u  /* return DISTINCTCOUNT value sets (the reference's Set intermediate,
+                                    DistinctCountAggregationFunction.java:252-310), not only their sizes */
+#define PG_PLAN_HASH_GROUPS 0x2u /* group in a hash table even when the key space is small enough to address
+                                    directly (same results; for tests and measurements) */
+#define PG_PLAN_F64_SUMS 0x4u    /* accumulate every SUM / AVG in double, as the reference does, instead of
+                                    integer-exact int64 for integer inputs; use when partial states of servers
+                                    or GPUs whose columns differ in range must merge (pg_partials.layout) */
+
 typedef struct pg_plan {
   uint32_t abi_version;     /* PG_ABI_VERSION */
   uint32_t num_segments;
@@ -195,10 +215,19 @@ typedef struct pg_plan {
   uint32_t num_keys;        /* 0 => aggregation-only query */
   const pg_agg *aggs;
   const pg_key *keys;       /* group-by expressions, in GROUP BY order */
-  uint64_t num_groups_limit;/* InstancePlanMakerImplV2 num.groups.limit (per segment)                 */
+  uint64_t num_groups_limit;/* InstancePlanMakerImplV2 num.groups.limit (per segment): as in the reference a
+                               segment keeps the first num_groups_limit distinct keys in doc order
+                               (IntGroupIdMap.getGroupId, DictionaryBasedGroupKeyGenerator.java:991-1016) and
+                               drops the docs of later keys; 0 = the reference default 100 000 */
   uint64_t query_id;        /* for pg_cancel */
   int64_t deadline_ms;      /* CLOCK_MONOTONIC ms; 0 = none (QueryContext.getEndTimeMs)              */
   void *stream;             /* hipStream_t to launch on; NULL = the library's per-thread stream      */
+  uint32_t flags;           /* PG_PLAN_* */
+  uint32_t num_order;       /* ORDER BY items (group-by only); 0 = no device-side trim */
+  const pg_order *order;
+  uint64_t limit;           /* with num_order > 0: keep the groups that rank within the first `limit` under
+                               the ORDER BY (every group tied with the limit-th is kept too, so any tie-break
+                               the caller applies stays exact); 0 = keep all groups */
 } pg_plan;
 
 /* ---------------------------------------------------------------- results */
@@ -213,10 +242,15 @@ typedef struct pg_stats {     /* ExecutionStatistics, summed over the plan's seg
 } pg_stats;
 
 /* Host-side final result of one plan (library-owned until pg_result_free).
- * Aggregation-only: num_groups = 1.  Group-by: one row per group with at least one matching doc.
+ * Aggregation-only: num_groups = 1.  Group-by: one row per group with at least one matching doc (after the
+ * plan's ORDER BY trim, sorted by it with ascending key ids as the final tie-break; unsorted without one).
  * keys[g*num_keys + k] = table-global key id of group g's k-th key.
- * values[g*num_aggs + a]: COUNT / COUNTMV count, SUM sum, MIN/MAX value, AVG sum, DISTINCTCOUNT count.
- * counts[g*num_aggs + a]: AVG count (0 for the others). */
+ * values[g*num_aggs + a]: COUNT / COUNTMV count, SUM sum, MIN/MAX value, AVG sum, DISTINCTCOUNT set size.
+ * counts[g*num_aggs + a]: AVG count (0 for the others).
+ * With PG_PLAN_VALUE_SETS, the value set of DISTINCTCOUNT aggregation a of group g is
+ *   distinct_ids[distinct_offsets[g*num_aggs + a] .. distinct_offsets[g*num_aggs + a + 1]),
+ * table-global value ids (the aggregation's key space) in ascending order; other aggregations have empty
+ * ranges.  Without the flag both pointers are NULL. */
 typedef struct pg_result {
   pg_stats stats;
   uint64_t num_groups;
@@ -225,6 +259,9 @@ typedef struct pg_result {
   uint32_t *keys;
   double *values;
   int64_t *counts;
+  uint64_t num_distinct;
+  uint64_t *distinct_offsets;
+  uint32_t *distinct_ids;
 } pg_result;
 
 int pg_execute(const pg_plan *plan, pg_result **out);
@@ -232,37 +269,72 @@ int pg_result_free(pg_result *res);
 
 /* ---------------------------------------------------------------- partial state (multi-GPU) */
 
-/* Dense partial state of one plan on this device, laid out per group slot g in [0, num_slots):
- *   i64 [num_slots][n_i64] : merged by SUM   (per-slot doc count, integer sums, AVG counts, COUNTMV)
- *   f64 [num_slots][n_f64] : merged by SUM   (floating-point sums)
- *   mn  [num_slots][n_min] : merged by MIN   (order-preserving int64 image of double MIN)
- *   mx  [num_slots][n_max] : merged by MAX   (order-preserving int64 image of double MAX)
- *   flags [num_slots][flag_bytes_per_slot] : merged by MAX (DISTINCTCOUNT presence bytes)
- * All pointers are device pointers owned by the handle; ranks all-reduce them in place. */
+/* Per-group partial state of one plan on this device.  Groups are identified by their packed key: the
+ * mixed-radix number of their table-global key ids, first key least significant (key k contributes
+ * id_k * prod_{j<k} keys[j].cardinality), as DictionaryBasedGroupKeyGenerator forms raw keys (:280-322)
+ * but over table-global ids so that segments, GPUs and servers merge by VALUE.
+ *   mode PG_STATE_DENSE: slot = packed key, num_slots = prod of the key cardinalities; keys == NULL.
+ *   mode PG_STATE_HASH : open-addressing table of num_slots entries; keys[slot] = packed key or
+ *                        PG_EMPTY_KEY (IntGroupIdMap / Long2IntOpenHashMap on the device).
+ * State arrays, per slot:
+ *   i64 [num_slots][n_i64]      merged by SUM (slot 0: doc count; integer sums, AVG counts, COUNTMV)
+ *   f64 [num_slots][n_f64]      merged by SUM (floating-point sums)
+ *   mn  [num_slots][n_min]      merged by MIN (order-preserving int64 image of double MIN)
+ *   mx  [num_slots][n_max]      merged by MAX (order-preserving int64 image of double MAX)
+ *   bitmaps [num_slots][bitmap_words] merged by OR: per DISTINCTCOUNT aggregation a bitmap over its
+ *                               table-global value ids (the per-group RoaringBitmap of the reference)
+ * All pointers are device pointers owned by the handle. */
+#define PG_STATE_DENSE 0
+#define PG_STATE_HASH 1
+#define PG_EMPTY_KEY 0xFFFFFFFFFFFFFFFFull
+
 typedef struct pg_partials {
   pg_stats stats;
   uint64_t num_slots;
+  uint32_t mode;            /* PG_STATE_* */
   uint32_t n_i64, n_f64, n_min, n_max;
-  uint64_t flag_bytes_per_slot;
+  uint32_t bitmap_words;    /* uint32 words of DISTINCTCOUNT bitmaps per slot */
+  uint32_t layout;          /* bit a: SUM / AVG aggregation a accumulates integer-exact in i64 (else f64); partial
+                               states merge only with equal layouts */
+  uint32_t pad;
+  uint64_t row_bytes;       /* bytes of one exchange row (pg_partials_export) */
+  uint64_t *keys;
   int64_t *i64;
   double *f64;
   int64_t *mn;
   int64_t *mx;
-  uint8_t *flags;
+  uint32_t *bitmaps;
   void *impl;
 } pg_partials;
 
 int pg_execute_partial(const pg_plan *plan, pg_partials **out);
-/* Decode (possibly all-reduced) partial state into a host pg_result.  `plan` must be the plan
- * the partials were produced from (only its aggs / keys are read). */
+/* Decode (possibly merged) partial state into a host pg_result, applying the plan's ORDER BY trim and
+ * PG_PLAN_VALUE_SETS.  `plan` must be the plan the partials were produced from (its aggs / keys / order are
+ * read). */
 int pg_partials_finalize(pg_partials *p, const pg_plan *plan, pg_result **out);
 int pg_partials_free(pg_partials *p);
-/* Copy the partial-state arrays out to (PG_COPY_OUT) or back in from (PG_COPY_IN) caller-owned DEVICE buffers of
- * the same sizes (e.g. torch tensors the ranks all-reduce over RCCL: SUM for i64 / f64, MIN for mn, MAX for mx and
- * flags).  A NULL pointer skips that array.  `stream` NULL = the library's per-thread stream; synchronous. */
+/* Dense merge: copy the state arrays out to (PG_COPY_OUT) or back in from (PG_COPY_IN) caller-owned DEVICE
+ * buffers of the same sizes (e.g. torch tensors the ranks all-reduce over RCCL: SUM for i64 / f64, MIN for mn,
+ * MAX for mx).  Bitmaps are not all-reducible (OR): plans with DISTINCTCOUNT use the row exchange below.  A NULL
+ * pointer skips that array.  `stream` NULL = the library's per-thread stream; synchronous. */
 #define PG_COPY_OUT 0
 #define PG_COPY_IN 1
-int pg_partials_copy(pg_partials *p, int dir, void *i64, void *f64, void *mn, void *mx, void *flags, void *stream);
+int pg_partials_copy(pg_partials *p, int dir, void *i64, void *f64, void *mn, void *mx, void *stream);
+/* Sparse merge (GroupByOrderByCombineOperator's value-keyed merge across GPUs): the groups of `p` as rows
+ *   { u64 packed key | i64[n_i64] | f64[n_f64] | i64 mn[n_min] | i64 mx[n_max] | u32 bitmaps[bitmap_words] }
+ * (row_bytes each, 8-byte aligned), bucketed by owner part = pg_key_owner(key, num_parts), buckets in part order.
+ * part_counts[num_parts] (host) receives the rows per bucket.  dst (DEVICE, dst_rows rows) may be NULL to only
+ * count.  Synchronous on `stream`. */
+int pg_partials_export(pg_partials *p, uint32_t num_parts, void *dst, uint64_t dst_rows, uint64_t *part_counts,
+                       void *stream);
+/* A fresh, empty PG_STATE_HASH partial state with the layout of `like` (its plan's aggregations and keys) and room
+ * for at least `capacity` groups; its stats are zero. */
+int pg_partials_create(const pg_partials *like, uint64_t capacity, pg_partials **out);
+/* Merge `n` exported rows (DEVICE buffer) into `p` (which must be PG_STATE_HASH): insert missing keys, then
+ * SUM / MIN / MAX / OR the state (AggregationFunction.merge of each function). */
+int pg_partials_merge(pg_partials *p, const void *rows, uint64_t n, void *stream);
+/* Owner part of a packed key among num_parts (the bucketing of pg_partials_export). */
+uint32_t pg_key_owner(uint64_t key, uint32_t num_parts);
 
 /* ---------------------------------------------------------------- measurement hooks */
 

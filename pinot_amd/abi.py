@@ -1,7 +1,7 @@
 """ctypes mirror of include/pinot_gpu.h (the C ABI).  Shared by the GPU binding and the oracle."""
 import ctypes as C
 
-PG_ABI_VERSION = 1
+PG_ABI_VERSION = 2
 
 PG_OK, PG_E_INVALID, PG_E_HIP, PG_E_NOMEM, PG_E_NOTFOUND, PG_E_UNSUPPORTED, PG_E_CANCELLED, PG_E_TIMEOUT, \
     PG_E_STATE = 0, -1, -2, -3, -4, -5, -6, -7, -8
@@ -32,6 +32,10 @@ AGG_CODES = {"COUNT": PG_AGG_COUNT, "SUM": PG_AGG_SUM, "MIN": PG_AGG_MIN, "MAX":
              "DISTINCTCOUNT": PG_AGG_DISTINCTCOUNT, "COUNTMV": PG_AGG_COUNTMV}
 PG_EXPR_COL, PG_EXPR_MUL, PG_EXPR_ADD, PG_EXPR_SUB = range(4)
 PG_KEY_VALUE_OFFSET, PG_KEY_KEYMAP = 0, 1
+PG_ORDER_AGG, PG_ORDER_KEY = 0, 1
+PG_PLAN_VALUE_SETS, PG_PLAN_HASH_GROUPS, PG_PLAN_F64_SUMS = 0x1, 0x2, 0x4
+PG_STATE_DENSE, PG_STATE_HASH = 0, 1
+PG_EMPTY_KEY = 0xFFFFFFFFFFFFFFFF
 
 
 class pg_col_desc(C.Structure):
@@ -60,12 +64,17 @@ class pg_segment_ref(C.Structure):
                 ("leaves", C.POINTER(pg_leaf))]
 
 
+class pg_order(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("index", C.c_uint32), ("desc", C.c_uint32), ("pad", C.c_uint32)]
+
+
 class pg_plan(C.Structure):
     _fields_ = [("abi_version", C.c_uint32), ("num_segments", C.c_uint32), ("segments", C.POINTER(pg_segment_ref)),
                 ("num_leaves", C.c_uint32), ("num_ops", C.c_uint32), ("ops", C.POINTER(C.c_int32)),
                 ("num_aggs", C.c_uint32), ("num_keys", C.c_uint32), ("aggs", C.POINTER(pg_agg)),
                 ("keys", C.POINTER(pg_key)), ("num_groups_limit", C.c_uint64), ("query_id", C.c_uint64),
-                ("deadline_ms", C.c_int64), ("stream", C.c_void_p)]
+                ("deadline_ms", C.c_int64), ("stream", C.c_void_p), ("flags", C.c_uint32),
+                ("num_order", C.c_uint32), ("order", C.POINTER(pg_order)), ("limit", C.c_uint64)]
 
 
 class pg_stats(C.Structure):
@@ -77,14 +86,16 @@ class pg_stats(C.Structure):
 class pg_result(C.Structure):
     _fields_ = [("stats", pg_stats), ("num_groups", C.c_uint64), ("num_keys", C.c_uint32), ("num_aggs", C.c_uint32),
                 ("keys", C.POINTER(C.c_uint32)), ("values", C.POINTER(C.c_double)),
-                ("counts", C.POINTER(C.c_int64))]
+                ("counts", C.POINTER(C.c_int64)), ("num_distinct", C.c_uint64),
+                ("distinct_offsets", C.POINTER(C.c_uint64)), ("distinct_ids", C.POINTER(C.c_uint32))]
 
 
 class pg_partials(C.Structure):
-    _fields_ = [("stats", pg_stats), ("num_slots", C.c_uint64), ("n_i64", C.c_uint32), ("n_f64", C.c_uint32),
-                ("n_min", C.c_uint32), ("n_max", C.c_uint32), ("flag_bytes_per_slot", C.c_uint64),
+    _fields_ = [("stats", pg_stats), ("num_slots", C.c_uint64), ("mode", C.c_uint32), ("n_i64", C.c_uint32),
+                ("n_f64", C.c_uint32), ("n_min", C.c_uint32), ("n_max", C.c_uint32), ("bitmap_words", C.c_uint32),
+                ("layout", C.c_uint32), ("pad", C.c_uint32), ("row_bytes", C.c_uint64), ("keys", C.c_void_p),
                 ("i64", C.c_void_p), ("f64", C.c_void_p), ("mn", C.c_void_p), ("mx", C.c_void_p),
-                ("flags", C.c_void_p), ("impl", C.c_void_p)]
+                ("bitmaps", C.c_void_p), ("impl", C.c_void_p)]
 
 
 class pg_timing(C.Structure):
@@ -96,7 +107,8 @@ class pg_timing(C.Structure):
 # every symbol declared in include/pinot_gpu.h (checked by tests/test_abi.py)
 EXPORTED = ["pg_init", "pg_last_error", "pg_resident_bytes", "pg_cancel", "pg_abi_version", "pg_column_upload",
             "pg_segment_release", "pg_execute", "pg_result_free", "pg_execute_partial", "pg_partials_finalize",
-            "pg_partials_free", "pg_partials_copy", "pg_last_timing"]
+            "pg_partials_free", "pg_partials_copy", "pg_partials_export", "pg_partials_create", "pg_partials_merge",
+            "pg_key_owner", "pg_last_timing"]
 PG_COPY_OUT, PG_COPY_IN = 0, 1
 
 
@@ -117,8 +129,13 @@ def declare(lib):
         "pg_partials_finalize": ([P(pg_partials), P(pg_plan), P(P(pg_result))], C.c_int),
         "pg_partials_free": ([P(pg_partials)], C.c_int),
         "pg_last_timing": ([P(pg_timing)], C.c_int),
-        "pg_partials_copy": ([P(pg_partials), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                              C.c_void_p], C.c_int),
+        "pg_partials_copy": ([P(pg_partials), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
+                             C.c_int),
+        "pg_partials_export": ([P(pg_partials), C.c_uint32, C.c_void_p, C.c_uint64, P(C.c_uint64), C.c_void_p],
+                               C.c_int),
+        "pg_partials_create": ([P(pg_partials), C.c_uint64, P(P(pg_partials))], C.c_int),
+        "pg_partials_merge": ([P(pg_partials), C.c_void_p, C.c_uint64, C.c_void_p], C.c_int),
+        "pg_key_owner": ([C.c_uint64, C.c_uint32], C.c_uint32),
     }
     for name, (args, res) in sigs.items():
         f = getattr(lib, name)

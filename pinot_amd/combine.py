@@ -5,72 +5,151 @@ AggregationOnlyCombineOperator.mergeResultsBlocks (operator/combine/AggregationO
 GroupByOrderByCombineOperator.processSegments -> IndexedTable.upsert (operator/combine/GroupByOrderByCombineOperator.java
 :127-214, data/table/IndexedTable.java:103-118).  Here segments are sharded over the GPUs of a node (one process per
 GPU); each GPU merges its own segments on device inside the fused scan (pg_execute_partial), and the ranks then merge
-their dense per-slot state with ONE collective per state array over RCCL / xGMI:
+their partial states over RCCL / xGMI in one of two ways:
 
-    i64   (doc counts, integer sums, AVG counts, COUNTMV)   all_reduce SUM
-    f64   (floating-point sums)                            all_reduce SUM
-    mn    (order-preserving int64 image of double MIN)      all_reduce MIN
-    mx    (order-preserving int64 image of double MAX)      all_reduce MAX
-    flags (DISTINCTCOUNT presence bytes)                    all_reduce MAX
-    stats (ExecutionStatistics)                            all_reduce SUM
+* dense all-reduce -- a small dense key space without DISTINCTCOUNT bitmaps: ONE collective per state array
+    i64 (doc counts, integer sums, AVG counts, COUNTMV) SUM, f64 SUM, mn (order-preserving int64 of MIN) MIN,
+    mx MAX, then every rank holds the merged state (config 2: 365 slots x 3 int64, latency-bound).
+* row exchange -- hash states, large key spaces, DISTINCTCOUNT (bitmaps merge by OR, which RCCL cannot reduce):
+    every rank exports its groups as rows bucketed by owner rank (pg_partials_export, owner = pg_key_owner(key)),
+    the buckets go to their owners in one all_to_all, each owner inserts-and-merges what it received into a fresh
+    table (pg_partials_merge: SUM / MIN / MAX / OR per state), finalizes ITS keys (ORDER BY trim included), and the
+    per-owner results -- disjoint key sets -- are gathered to every rank.  Per-link traffic is (N-1)/N of one
+    rank's groups instead of N copies of the key space.
 
-Sparse / high-cardinality keys use `gather_merge_results`: an all_gather of value-keyed partials merged with the
-reference's own AggregationFunction.merge semantics (pinot_amd.plan.merge_intermediate).
+Statistics (ExecutionStatistics) are summed with one all_reduce.  `gather_merge_results` merges value-keyed host
+results (oracle / DataTable-level) with the reference's AggregationFunction.merge (pinot_amd.plan.merge_intermediate).
 """
 from __future__ import annotations
 
 import ctypes as C
-from typing import Dict, Optional
+from typing import Optional
 
 import numpy as np
 
 from . import abi
-from .plan import ExecutionStats, IntermediateResult, merge_intermediate
+from .plan import ExecutionStats, IntermediateResult, default_row, merge_intermediate
 
 _STATS_FIELDS = ["num_docs_scanned", "num_entries_scanned_in_filter", "num_entries_scanned_post_filter",
                  "num_total_docs", "num_segments_processed", "num_segments_matched"]
+DENSE_ALLREDUCE_MAX_BYTES = 64 << 20
 
 
-def allreduce_state(state: Dict[str, "torch.Tensor"], group=None) -> None:
-    """In-place merge of a dense partial state across ranks (any backend: RCCL on GPU, gloo in CPU tests)."""
+def _is_gloo(group=None) -> bool:
+    import torch.distributed as dist
+    return dist.get_backend(group) == "gloo"
+
+
+def _comm(t, group):
+    """The tensor a collective runs on: the device tensor itself over RCCL, a host copy over gloo (CPU tests)."""
+    return t.cpu() if _is_gloo(group) else t
+
+
+def allreduce_state(state, group=None) -> None:
+    """In-place merge of a dense partial state across ranks."""
     import torch.distributed as dist
     ops = {"i64": dist.ReduceOp.SUM, "f64": dist.ReduceOp.SUM, "mn": dist.ReduceOp.MIN, "mx": dist.ReduceOp.MAX,
-           "flags": dist.ReduceOp.MAX, "stats": dist.ReduceOp.SUM}
-    for name in ("i64", "f64", "mn", "mx", "flags", "stats"):
+           "stats": dist.ReduceOp.SUM}
+    for name in ("i64", "f64", "mn", "mx", "stats"):
         t = state.get(name)
         if t is not None and t.numel():
-            dist.all_reduce(t, op=ops[name], group=group)
+            c = _comm(t, group)
+            dist.all_reduce(c, op=ops[name], group=group)
+            if c is not t:
+                t.copy_(c)
+
+
+def _all_gather_ints(vals, group, device):
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(vals, dtype=torch.int64, device=device)
+    c = _comm(t, group)
+    out = [torch.empty_like(c) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(out, c, group=group)
+    return [o.tolist() for o in out]
 
 
 def merge_partials_across_ranks(engine, plan, p, group=None) -> IntermediateResult:
-    """pg_execute_partial result `p` (this rank) -> all-reduced over the process group -> finalized result.
-
-    The state leaves the library through pg_partials_copy into torch device tensors (RCCL operates on those), is
-    reduced in place, and goes back with PG_COPY_IN before pg_partials_finalize decodes it."""
+    """pg_execute_partial result `p` (this rank) -> merged over the process group -> finalized result (every rank
+    returns the same merged result).  Consumes `p`."""
     import torch
+    import torch.distributed as dist
+    from .gpu import check
     pc = p.contents
     dev = torch.device("cuda", torch.cuda.current_device())
-    n = pc.num_slots
-    state = {
-        "i64": torch.empty(n * pc.n_i64, dtype=torch.int64, device=dev),
-        "f64": torch.empty(n * pc.n_f64, dtype=torch.float64, device=dev),
-        "mn": torch.empty(n * pc.n_min, dtype=torch.int64, device=dev),
-        "mx": torch.empty(n * pc.n_max, dtype=torch.int64, device=dev),
-        "flags": torch.empty(n * pc.flag_bytes_per_slot, dtype=torch.uint8, device=dev),
-    }
-    ptr = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None
+    world = dist.get_world_size(group)
+    layouts = _all_gather_ints([pc.mode, pc.num_slots, pc.n_i64, pc.n_f64, pc.n_min, pc.n_max, pc.bitmap_words,
+                                pc.layout], group, dev)
+    if any(l[2:] != layouts[0][2:] for l in layouts):
+        engine.lib.pg_partials_free(p)
+        raise ValueError(f"partial state layouts differ across ranks: {layouts} (plan with PG_PLAN_F64_SUMS)")
+    stats = torch.tensor([getattr(pc.stats, f) for f in _STATS_FIELDS], dtype=torch.int64, device=dev)
+    dense_ok = all(l[0] == abi.PG_STATE_DENSE and l[1] == layouts[0][1] for l in layouts) and pc.bitmap_words == 0 \
+        and pc.num_slots * 8 * (pc.n_i64 + pc.n_f64 + pc.n_min + pc.n_max) <= DENSE_ALLREDUCE_MAX_BYTES
+    if dense_ok:
+        n = pc.num_slots
+        state = {
+            "i64": torch.empty(n * pc.n_i64, dtype=torch.int64, device=dev),
+            "f64": torch.empty(n * pc.n_f64, dtype=torch.float64, device=dev),
+            "mn": torch.empty(n * pc.n_min, dtype=torch.int64, device=dev),
+            "mx": torch.empty(n * pc.n_max, dtype=torch.int64, device=dev),
+            "stats": stats,
+        }
+        ptr = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None
+        torch.cuda.synchronize()
+        check(engine.lib.pg_partials_copy(p, abi.PG_COPY_OUT, ptr(state["i64"]), ptr(state["f64"]), ptr(state["mn"]),
+                                          ptr(state["mx"]), None))
+        allreduce_state(state, group)
+        torch.cuda.synchronize()
+        check(engine.lib.pg_partials_copy(p, abi.PG_COPY_IN, ptr(state["i64"]), ptr(state["f64"]), ptr(state["mn"]),
+                                          ptr(state["mx"]), None))
+        for f, v in zip(_STATS_FIELDS, state["stats"].cpu().tolist()):
+            setattr(pc.stats, f, int(v))
+        return engine.finalize_partial(plan, p)
+    return _exchange_rows(engine, plan, p, stats, group, dev)
+
+
+def _exchange_rows(engine, plan, p, stats, group, dev) -> IntermediateResult:
+    import torch
+    import torch.distributed as dist
+    pc = p.contents
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    rb = pc.row_bytes
+    gloo = _is_gloo(group)
+    try:
+        counts = engine.export_rows(p, world)  # rows per owner rank
+        sc = torch.tensor(counts, dtype=torch.int64, device="cpu" if gloo else dev)
+        rcounts = torch.empty_like(sc)
+        dist.all_to_all_single(rcounts, sc, group=group)
+        rcounts = rcounts.tolist()
+        q = engine.create_like(p, max(sum(rcounts), 1))
+        send = torch.empty(max(sum(counts), 1) * rb, dtype=torch.uint8, device=dev)
+        engine.export_rows(p, world, C.c_void_p(send.data_ptr()), sum(counts))
+    finally:
+        engine.lib.pg_partials_free(p)
+    recv = torch.empty(max(sum(rcounts), 1) * rb, dtype=torch.uint8, device=dev)
+    s_in, r_in = (send.cpu(), torch.empty(recv.numel(), dtype=torch.uint8)) if gloo else (send, recv)
+    dist.all_to_all_single(r_in[:sum(rcounts) * rb], s_in[:sum(counts) * rb],
+                           output_split_sizes=[c * rb for c in rcounts], input_split_sizes=[c * rb for c in counts],
+                           group=group)
+    if gloo:
+        recv.copy_(r_in)
+    st = _comm(stats, group)
+    dist.all_reduce(st, op=dist.ReduceOp.SUM, group=group)
     torch.cuda.synchronize()
-    from .gpu import check
-    check(engine.lib.pg_partials_copy(p, abi.PG_COPY_OUT, ptr(state["i64"]), ptr(state["f64"]), ptr(state["mn"]),
-                                      ptr(state["mx"]), ptr(state["flags"]), None))
-    state["stats"] = torch.tensor([getattr(pc.stats, f) for f in _STATS_FIELDS], dtype=torch.int64, device=dev)
-    allreduce_state(state, group)
-    torch.cuda.synchronize()
-    check(engine.lib.pg_partials_copy(p, abi.PG_COPY_IN, ptr(state["i64"]), ptr(state["f64"]), ptr(state["mn"]),
-                                      ptr(state["mx"]), ptr(state["flags"]), None))
-    for f, v in zip(_STATS_FIELDS, state["stats"].cpu().tolist()):
-        setattr(pc.stats, f, int(v))
-    return engine.finalize_partial(plan, p)
+    engine.merge_rows(q, C.c_void_p(recv.data_ptr()), sum(rcounts))
+    for f, v in zip(_STATS_FIELDS, st.cpu().tolist()):
+        setattr(q.contents.stats, f, int(v))
+    mine = engine.finalize_partial(plan, q)  # this rank's keys (their ORDER BY trim included)
+    parts = [None] * world
+    dist.all_gather_object(parts, mine.rows, group=group)
+    rows = {}
+    for r in parts:  # owners hold disjoint key sets
+        rows.update(r)
+    if not plan.query.group_by and () not in rows:  # no rank matched a doc
+        rows[()] = default_row(mine.aggregations)
+    return IntermediateResult(mine.aggregations, mine.group_by, rows, mine.stats)
 
 
 def gather_merge_results(res: IntermediateResult, group=None) -> IntermediateResult:
@@ -84,11 +163,9 @@ def gather_merge_results(res: IntermediateResult, group=None) -> IntermediateRes
     stats = ExecutionStats()
     for rows, st in parts:
         for k, v in rows.items():
-            if v is None:
-                continue
             merged[k] = merge_intermediate(res.aggregations, merged[k], v) if k in merged else v
         for f in _STATS_FIELDS:
             setattr(stats, f, getattr(stats, f) + st[f])
     if not res.group_by and () not in merged:
-        merged[()] = None
+        merged[()] = default_row(res.aggregations)
     return IntermediateResult(res.aggregations, res.group_by, merged, stats)

@@ -1,0 +1,406 @@
+// pg_groups.hip -- group-state kernels of libpinot_gpu (gfx950): the device side of what the reference does after
+// the per-segment aggregation loop.
+//
+//   * numGroupsLimit truncation per segment (DictionaryBasedGroupKeyGenerator.IntGroupIdMap.getGroupId,
+//     query/aggregation/groupby/DictionaryBasedGroupKeyGenerator.java:991-1016: ids in first-seen doc order,
+//     INVALID_ID once the limit is reached): from a GM_HASH_SEG table every segment keeps the `limit` keys whose
+//     first matching doc comes first, then the kept (segment, key) entries are merged by key.
+//   * merge by VALUE key (GroupByOrderByCombineOperator.processSegments -> IndexedTable.upsert,
+//     operator/combine/GroupByOrderByCombineOperator.java:127-214, data/table/IndexedTable.java:103-118) as
+//     exchange rows inserted into an open-addressing table with each function's merge (SUM / MIN / MAX / OR).
+//   * finalisation: final values per group (extractFinalResult of each function; DISTINCTCOUNT = set size,
+//     DistinctCountAggregationFunction.java:252-310), the ORDER BY trim (TableResizer.getTopRecords,
+//     data/table/TableResizer.java:248) as a radix sort on the first ORDER BY item, and value-set extraction.
+// Everything here is HBM / atomic bound, O(groups); no MFMA.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "pg_internal.h"
+
+namespace pg {
+
+__host__ __device__ inline uint32_t key_owner(uint64_t key, uint32_t parts) {
+  // high bits of a second mix: independent of the table position bits (mix64(key) & mask) of the receiver
+  return (uint32_t)((mix64(key ^ 0x9E3779B97F4A7C15ull) >> 32) % parts);
+}
+
+__device__ __forceinline__ bool present(const StateView& v, uint64_t s) {
+  if (v.keys && v.keys[s] == kEmptyKey) return false;
+  return v.i64[s * v.n_i64] > 0;
+}
+
+// ------------------------------------------------------------------------------------------ slot selection
+
+struct SlotPred {
+  StateView v;
+  uint32_t kind, part, parts;
+  __device__ bool operator()(const uint32_t& s) const {
+    switch (kind) {
+      case SEL_OCCUPIED: return v.keys[s] != kEmptyKey;
+      case SEL_PRESENT_PART: return present(v, s) && key_owner(v.keys ? v.keys[s] : (uint64_t)s, parts) == part;
+      default: return present(v, s);
+    }
+  }
+};
+
+size_t select_temp_bytes(uint64_t n) {
+  size_t a = 0, b = 0, c = 0;
+  hipcub::CountingInputIterator<uint32_t> it(0);
+  hipcub::DeviceSelect::If(nullptr, a, it, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, SlotPred{});
+  hipcub::DeviceSelect::Flagged(nullptr, b, (uint32_t*)nullptr, (uint8_t*)nullptr, (uint32_t*)nullptr,
+                                (uint32_t*)nullptr, (int)n);
+  hipcub::DeviceScan::ExclusiveSum(nullptr, c, (uint64_t*)nullptr, (uint64_t*)nullptr, (int)n + 1);
+  return std::max(a, std::max(b, c)) + 256;
+}
+
+hipError_t launch_select_slots(const StateView& v, uint32_t kind, uint32_t part, uint32_t parts, uint32_t* out,
+                               uint32_t* d_num, void* temp, size_t temp_bytes, hipStream_t s) {
+  hipcub::CountingInputIterator<uint32_t> it(0);
+  return hipcub::DeviceSelect::If(temp, temp_bytes, it, out, d_num, (int)v.num_slots, SlotPred{v, kind, part, parts},
+                                  s);
+}
+
+hipError_t launch_select_flagged(const uint32_t* in, const uint8_t* flags, uint64_t n, uint32_t* out, uint32_t* d_num,
+                                 void* temp, size_t temp_bytes, hipStream_t s) {
+  return hipcub::DeviceSelect::Flagged(temp, temp_bytes, in, flags, out, d_num, (int)n, s);
+}
+
+hipError_t launch_exclusive_sum(const uint64_t* in, uint64_t* out, uint64_t n, void* temp, size_t temp_bytes,
+                                hipStream_t s) {
+  return hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n, s);
+}
+
+size_t sort_temp_bytes(uint64_t n) {
+  size_t t = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, t, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                     (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+  return t + 256;
+}
+
+hipError_t launch_sort_pairs(const uint64_t* kin, uint64_t* kout, const uint32_t* vin, uint32_t* vout, uint64_t n,
+                             void* temp, size_t temp_bytes, hipStream_t s) {
+  return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, kin, kout, vin, vout, (int)n, 0, 64, s);
+}
+
+// ------------------------------------------------------------------------------------------ finalisation
+
+__device__ __forceinline__ uint32_t bits_words(uint32_t card) { return (card + 31u) / 32u; }
+
+// Final value of every aggregation of the groups at `slots` (AggregationFunction.extractFinalResult; AVG keeps
+// its (sum, count) pair in vals / cnts, DISTINCTCOUNT its set size).  One thread per group.
+__global__ void final_values_kernel(StateView v, FinalSpec f, const uint32_t* __restrict__ slots, uint64_t n,
+                                    uint64_t* __restrict__ keys, double* __restrict__ vals,
+                                    int64_t* __restrict__ cnts) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t s = slots ? slots[i] : 0;
+    keys[i] = v.keys ? v.keys[s] : s;
+    const int64_t count = (int64_t)v.i64[s * v.n_i64];
+    for (uint32_t a = 0; a < f.num_aggs; a++) {
+      const AggSpec& A = f.aggs[a];
+      double x = 0;
+      int64_t c = 0;
+      switch (A.fn) {
+        case PG_AGG_COUNT: x = (double)count; break;
+        case PG_AGG_COUNTMV: x = (double)(int64_t)v.i64[s * v.n_i64 + A.slot]; break;
+        case PG_AGG_SUM:
+        case PG_AGG_AVG:
+          x = A.integer ? (double)(int64_t)v.i64[s * v.n_i64 + A.slot] : v.f64[s * v.n_f64 + A.slot];
+          if (A.fn == PG_AGG_AVG) c = count;
+          break;
+        case PG_AGG_MIN: x = order_key_decode(v.mn[s * v.n_min + A.slot]); break;
+        case PG_AGG_MAX: x = order_key_decode(v.mx[s * v.n_max + A.slot]); break;
+        case PG_AGG_DISTINCTCOUNT: {
+          const uint32_t* w = v.bits + s * v.bit_words + A.dc_word;
+          uint64_t pc = 0;
+          for (uint32_t k = 0; k < bits_words(A.key_card); k++) pc += __popc(w[k]);
+          x = (double)pc;
+          break;
+        }
+      }
+      vals[i * f.num_aggs + a] = x;
+      cnts[i * f.num_aggs + a] = c;
+    }
+  }
+}
+
+hipError_t launch_final_values(const StateView& v, const FinalSpec& f, const uint32_t* slots, uint64_t n,
+                               uint64_t* keys, double* vals, int64_t* cnts, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const uint64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(final_values_kernel, dim3((uint32_t)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, s, v, f,
+                     slots, n, keys, vals, cnts);
+  return hipGetLastError();
+}
+
+// Ascending u64 image of the first ORDER BY item (DESC = bit complement), for the radix-sort trim.
+__global__ void order_keys_kernel(FinalSpec f, const uint64_t* __restrict__ keys, const double* __restrict__ vals,
+                                  const int64_t* __restrict__ cnts, uint64_t n, uint64_t* __restrict__ out,
+                                  uint32_t* __restrict__ pos) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint64_t o;
+    if (f.order_kind == PG_ORDER_KEY) {
+      o = (keys[i] / f.key_stride[f.order_index]) % f.key_card[f.order_index];
+    } else {
+      const uint32_t a = f.order_index;
+      double x = vals[i * f.num_aggs + a];
+      if (f.aggs[a].fn == PG_AGG_AVG) {
+        const int64_t c = cnts[i * f.num_aggs + a];
+        x = c ? x / (double)c : -__builtin_inf();
+      }
+      int64_t b;
+      __builtin_memcpy(&b, &x, 8);
+      o = b >= 0 ? ((uint64_t)b | 0x8000000000000000ull) : ~(uint64_t)b;
+    }
+    out[i] = f.order_desc ? ~o : o;
+    pos[i] = (uint32_t)i;
+  }
+}
+
+hipError_t launch_order_keys(const FinalSpec& f, const uint64_t* keys, const double* vals, const int64_t* cnts,
+                             uint64_t n, uint64_t* out, uint32_t* pos, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const uint64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(order_keys_kernel, dim3((uint32_t)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, s, f, keys,
+                     vals, cnts, n, out, pos);
+  return hipGetLastError();
+}
+
+// Number of sorted entries that rank within the first `limit`, ties with the limit-th included.
+__global__ void cutoff_kernel(const uint64_t* __restrict__ sorted, uint64_t n, uint64_t limit, uint64_t* out) {
+  const uint64_t t = sorted[limit - 1];
+  uint64_t lo = limit, hi = n;  // first index with sorted > t
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (sorted[mid] <= t) lo = mid + 1;
+    else hi = mid;
+  }
+  *out = lo;
+}
+
+hipError_t launch_cutoff(const uint64_t* sorted, uint64_t n, uint64_t limit, uint64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(cutoff_kernel, dim3(1), dim3(1), 0, s, sorted, n, limit, out);
+  return hipGetLastError();
+}
+
+// out[i] = in[pos[i]] for the candidates (keys, per-agg values / counts, slots).
+__global__ void gather_final_kernel(uint32_t A, const uint32_t* __restrict__ pos, uint64_t n,
+                                    const uint64_t* __restrict__ keys, const double* __restrict__ vals,
+                                    const int64_t* __restrict__ cnts, const uint32_t* __restrict__ slots,
+                                    uint64_t* __restrict__ okeys, double* __restrict__ ovals,
+                                    int64_t* __restrict__ ocnts, uint32_t* __restrict__ oslots) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t p = pos[i];
+    okeys[i] = keys[p];
+    oslots[i] = slots ? slots[p] : 0u;
+    for (uint32_t a = 0; a < A; a++) {
+      ovals[i * A + a] = vals[(uint64_t)p * A + a];
+      ocnts[i * A + a] = cnts[(uint64_t)p * A + a];
+    }
+  }
+}
+
+hipError_t launch_gather_final(uint32_t A, const uint32_t* pos, uint64_t n, const uint64_t* keys, const double* vals,
+                               const int64_t* cnts, const uint32_t* slots, uint64_t* okeys, double* ovals,
+                               int64_t* ocnts, uint32_t* oslots, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const uint64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(gather_final_kernel, dim3((uint32_t)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, s, A, pos,
+                     n, keys, vals, cnts, slots, okeys, ovals, ocnts, oslots);
+  return hipGetLastError();
+}
+
+// Value sets: sizes[i*A + a] = |set| of DISTINCTCOUNT aggregation a of group slots[i] (0 for other functions).
+__global__ void set_sizes_kernel(StateView v, FinalSpec f, const uint32_t* __restrict__ slots, uint64_t n,
+                                 uint64_t* __restrict__ sizes) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t s = slots[i];
+    for (uint32_t a = 0; a < f.num_aggs; a++) {
+      uint64_t pc = 0;
+      if (f.aggs[a].fn == PG_AGG_DISTINCTCOUNT) {
+        const uint32_t* w = v.bits + s * v.bit_words + f.aggs[a].dc_word;
+        for (uint32_t k = 0; k < bits_words(f.aggs[a].key_card); k++) pc += __popc(w[k]);
+      }
+      sizes[i * f.num_aggs + a] = pc;
+    }
+  }
+}
+
+hipError_t launch_set_sizes(const StateView& v, const FinalSpec& f, const uint32_t* slots, uint64_t n,
+                            uint64_t* sizes, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const uint64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(set_sizes_kernel, dim3((uint32_t)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, s, v, f,
+                     slots, n, sizes);
+  return hipGetLastError();
+}
+
+// One wave per (group, DISTINCTCOUNT aggregation): the set bits of its bitmap, ascending, at offsets[i*A + a]
+// (an exclusive scan of set_sizes).  A lane takes one word per round; a wave prefix sum of the word popcounts
+// places its ids.
+__global__ void set_extract_kernel(StateView v, FinalSpec f, const uint32_t* __restrict__ slots, uint64_t n,
+                                   const uint64_t* __restrict__ offsets, uint32_t* __restrict__ ids) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  for (uint64_t job = wave; job < n * f.num_aggs; job += nwaves) {
+    const uint64_t i = job / f.num_aggs;
+    const uint32_t a = (uint32_t)(job % f.num_aggs);
+    if (f.aggs[a].fn != PG_AGG_DISTINCTCOUNT) continue;
+    const uint32_t* w = v.bits + (uint64_t)slots[i] * v.bit_words + f.aggs[a].dc_word;
+    const uint32_t nw = bits_words(f.aggs[a].key_card);
+    uint64_t out = offsets[job];
+    for (uint32_t k0 = 0; k0 < nw; k0 += 64) {
+      const uint32_t k = k0 + lane;
+      uint32_t x = k < nw ? w[k] : 0u;
+      const uint32_t c = __popc(x);
+      uint32_t incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= (uint32_t)o) incl += y;
+      }
+      uint64_t at = out + incl - c;
+      while (x) {
+        const uint32_t b = (uint32_t)__ffs(x) - 1u;
+        ids[at++] = k * 32u + b;
+        x &= x - 1u;
+      }
+      out += __shfl(incl, 63);
+    }
+  }
+}
+
+hipError_t launch_set_extract(const StateView& v, const FinalSpec& f, const uint32_t* slots, uint64_t n,
+                              const uint64_t* offsets, uint32_t* ids, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const uint64_t waves = n * f.num_aggs;
+  const uint64_t blocks = (waves + 3) / 4;
+  hipLaunchKernelGGL(set_extract_kernel, dim3((uint32_t)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, s, v, f,
+                     slots, n, offsets, ids);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------ exchange rows
+
+uint64_t row_bytes(const StateView& v) {
+  const uint64_t b = 8ull * (1 + v.n_i64 + v.n_f64 + v.n_min + v.n_max) + 4ull * v.bit_words;
+  return (b + 7) & ~7ull;
+}
+
+// rows[i] = { key / key_div | state of slots[i] } (GroupByOrderByCombineOperator's per-group record).
+__global__ void gather_rows_kernel(StateView v, const uint32_t* __restrict__ slots, uint64_t n, uint64_t key_div,
+                                   uint8_t* __restrict__ dst, uint64_t rb) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t s = slots[i];
+    uint64_t* r = (uint64_t*)(dst + i * rb);
+    r[0] = (v.keys ? v.keys[s] : s) / key_div;
+    uint64_t o = 1;
+    for (uint32_t k = 0; k < v.n_i64; k++) r[o++] = v.i64[s * v.n_i64 + k];
+    for (uint32_t k = 0; k < v.n_f64; k++) r[o++] = (uint64_t)__double_as_longlong(v.f64[s * v.n_f64 + k]);
+    for (uint32_t k = 0; k < v.n_min; k++) r[o++] = (uint64_t)v.mn[s * v.n_min + k];
+    for (uint32_t k = 0; k < v.n_max; k++) r[o++] = (uint64_t)v.mx[s * v.n_max + k];
+    uint32_t* b = (uint32_t*)(r + o);
+    for (uint32_t k = 0; k < v.bit_words; k++) b[k] = v.bits[s * v.bit_words + k];
+  }
+}
+
+hipError_t launch_gather_rows(const StateView& v, const uint32_t* slots, uint64_t n, uint64_t key_div, uint8_t* dst,
+                              hipStream_t s) {
+  if (!n) return hipSuccess;
+  const uint64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((uint32_t)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, s, v,
+                     slots, n, key_div, dst, row_bytes(v));
+  return hipGetLastError();
+}
+
+// Insert-merge rows into a GM_HASH table: AggregationFunction.merge per state kind.
+__global__ void merge_rows_kernel(StateView v, const uint8_t* __restrict__ src, uint64_t n, uint64_t rb) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t* r = (const uint64_t*)(src + i * rb);
+    const uint64_t key = r[0];
+    uint64_t h = mix64(key) & v.hmask, s = ~0ull;
+    for (uint64_t probe = 0; probe <= v.hmask; probe++) {
+      const unsigned long long cur = v.keys[h];
+      if (cur == key) { s = h; break; }
+      if (cur == kEmptyKey) {
+        if (__hip_atomic_load(v.fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= v.max_fill) break;
+        const unsigned long long prev = atomicCAS(&v.keys[h], kEmptyKey, (unsigned long long)key);
+        if (prev == kEmptyKey) { atomicAdd(v.fill, 1u); s = h; break; }
+        if (prev == key) { s = h; break; }
+      }
+      h = (h + 1) & v.hmask;
+    }
+    if (s == ~0ull) {
+      atomicOr(v.err, 4u);
+      continue;
+    }
+    uint64_t o = 1;
+    for (uint32_t k = 0; k < v.n_i64; k++) atomicAdd(&v.i64[s * v.n_i64 + k], (unsigned long long)r[o++]);
+    for (uint32_t k = 0; k < v.n_f64; k++) atomicAdd(&v.f64[s * v.n_f64 + k], __longlong_as_double((long long)r[o++]));
+    for (uint32_t k = 0; k < v.n_min; k++) atomicMin(&v.mn[s * v.n_min + k], (long long)r[o++]);
+    for (uint32_t k = 0; k < v.n_max; k++) atomicMax(&v.mx[s * v.n_max + k], (long long)r[o++]);
+    const uint32_t* b = (const uint32_t*)(r + o);
+    for (uint32_t k = 0; k < v.bit_words; k++)
+      if (b[k]) atomicOr(&v.bits[s * v.bit_words + k], b[k]);
+  }
+}
+
+hipError_t launch_merge_rows(const StateView& v, const uint8_t* rows, uint64_t n, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const uint64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(merge_rows_kernel, dim3((uint32_t)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, s, v, rows,
+                     n, row_bytes(v));
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------ numGroupsLimit
+
+// Sort key of an occupied GM_HASH_SEG entry: (segment, first matching doc) -> the segment's first-seen order.
+__global__ void seg_order_kernel(StateView v, const uint32_t* __restrict__ slots, uint64_t n, uint32_t num_segments,
+                                 uint64_t* __restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t s = slots[i];
+    const uint64_t seg = v.keys[s] % num_segments;
+    out[i] = (seg << 32) | v.first_doc[s];
+  }
+}
+
+// keep[i] = rank of sorted entry i within its segment < limit (seg_first: first sorted index of each segment).
+__global__ void seg_first_kernel(const uint64_t* __restrict__ sorted, uint64_t n, uint32_t* __restrict__ seg_first) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    if (i == 0 || (sorted[i] >> 32) != (sorted[i - 1] >> 32)) seg_first[sorted[i] >> 32] = (uint32_t)i;
+}
+__global__ void seg_keep_kernel(const uint64_t* __restrict__ sorted, uint64_t n, const uint32_t* __restrict__ seg_first,
+                                uint64_t limit, uint8_t* __restrict__ keep) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    keep[i] = (i - seg_first[sorted[i] >> 32]) < limit;
+}
+
+hipError_t launch_seg_truncate(const StateView& v, const uint32_t* slots, uint64_t n, uint32_t num_segments,
+                               uint64_t limit, uint64_t* tmp_keys, uint64_t* sorted_keys, uint32_t* sorted_slots,
+                               uint32_t* seg_first, uint8_t* keep, void* temp, size_t temp_bytes, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const uint64_t blocks = (n + 255) / 256;
+  const dim3 g((uint32_t)(blocks < 16384 ? blocks : 16384));
+  hipLaunchKernelGGL(seg_order_kernel, g, dim3(256), 0, s, v, slots, n, num_segments, tmp_keys);
+  hipError_t e = launch_sort_pairs(tmp_keys, sorted_keys, slots, sorted_slots, n, temp, temp_bytes, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(seg_first_kernel, g, dim3(256), 0, s, sorted_keys, n, seg_first);
+  hipLaunchKernelGGL(seg_keep_kernel, g, dim3(256), 0, s, sorted_keys, n, seg_first, limit, keep);
+  return hipGetLastError();
+}
+
+}  // namespace pg
+
+extern "C" uint32_t pg_key_owner(uint64_t key, uint32_t num_parts) {
+  return num_parts ? pg::key_owner(key, num_parts) : 0u;
+}

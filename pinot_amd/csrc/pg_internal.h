@@ -29,7 +29,7 @@ constexpr int kChunk = 8;                            // rows gathered per straig
 constexpr int kTileDocs = kBlock * kRows;            // 8192 docs per tile
 constexpr int kItemTiles = 4;                        // tiles per work item (32 768 docs), within one segment
 constexpr int kMaxAggs = 8;
-constexpr int kMaxKeys = 4;
+constexpr int kMaxKeys = 8;
 constexpr int kMaxLeaves = 24;
 constexpr int kMaxOps = 64;
 constexpr int kMaxDepth = 4;                         // filter tree nesting (open groups)
@@ -92,7 +92,7 @@ struct ColDesc {
 
 struct SegDesc {
   uint32_t num_docs;
-  uint32_t pad;
+  uint32_t index;           // segment index within the plan (GM_HASH_SEG keys)
   const LeafDesc* leaves;   // [num_leaves]
   const ColDesc* aggcols;   // [num_aggs][2]
   const ColDesc* keycols;   // [num_keys]
@@ -104,7 +104,28 @@ struct WorkItem {
   uint32_t pad;
 };
 
-enum SlotKind : uint32_t { SK_NONE = 0, SK_I64 = 1, SK_F64 = 2, SK_MIN = 3, SK_MAX = 4, SK_FLAG = 5 };
+enum SlotKind : uint32_t { SK_NONE = 0, SK_I64 = 1, SK_F64 = 2, SK_MIN = 3, SK_MAX = 4, SK_BITS = 5 };
+
+// Group state addressing (QuerySpec::group_mode):
+//   GM_NONE     aggregation-only: one slot (0).
+//   GM_DENSE    slot = packed key (mixed radix of table-global key ids, first key least significant);
+//               LDS-privatised per block when the whole table fits (use_lds).
+//   GM_HASH     open-addressing table of 2^k packed keys (linear probing, PG_EMPTY_KEY = free), slot = the
+//               key's table position; keys are claimed with one 64-bit CAS (IntGroupIdMap on the device).
+//   GM_HASH_SEG as GM_HASH over (packed key * num_segments + segment), with the first matching doc of every
+//               (segment, key) in first_doc: the per-segment table when numGroupsLimit can truncate a segment
+//               (the runtime then keeps, per segment, the limit keys seen first and merges them by key).
+enum GroupMode : uint32_t { GM_NONE = 0, GM_DENSE = 1, GM_HASH = 2, GM_HASH_SEG = 3 };
+constexpr unsigned long long kEmptyKey = 0xFFFFFFFFFFFFFFFFull;
+
+__host__ __device__ inline uint64_t mix64(uint64_t x) {  // murmur3 fmix64 (the HashCommon.mix role)
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
 
 struct AggSpec {
   uint32_t fn;        // pg_agg_fn
@@ -113,10 +134,11 @@ struct AggSpec {
   uint32_t slot;      // primary slot index within its array
   uint32_t cnt_slot;  // AVG count slot (i64)
   uint32_t integer;   // SUM/AVG inputs integer-exact -> i64 accumulate
-  uint32_t key_kind;  // DISTINCTCOUNT: pg_key_kind
-  uint32_t key_card;  // DISTINCTCOUNT: global key space size (flag bytes for this agg)
+  uint32_t key_kind;  // DISTINCTCOUNT: pg_key_kind of its value ids
+  uint32_t key_card;  // DISTINCTCOUNT: size of the table-global value id space (bits of its bitmap)
   int64_t key_base;
-  uint64_t flag_off;  // DISTINCTCOUNT: byte offset of this agg's flags within a slot's flag row
+  uint32_t dc_word;   // DISTINCTCOUNT: first uint32 word of this aggregation's bitmap within a slot's row
+  uint32_t pad;
 };
 
 // A packed column staged per tile into LDS (LDS-DMA of the tile's whole word range in 1 KiB pieces) because
@@ -149,18 +171,25 @@ struct QuerySpec {
   uint32_t key_card[kMaxKeys];
   int64_t key_base[kMaxKeys];
   uint64_t key_stride[kMaxKeys];
-  uint64_t num_slots;
+  uint32_t group_mode;       // GroupMode
+  uint32_t hmax_fill;        // GM_HASH*: keys claimed before the table reports overflow (err bit 4)
+  uint64_t num_slots;        // dense: key space size; hash: table capacity (a power of two)
+  uint64_t hmask;            // hash: num_slots - 1
   uint32_t n_i64, n_f64, n_min, n_max;
-  uint64_t flag_bytes_per_slot;
+  uint32_t dc_row_words;     // uint32 words of DISTINCTCOUNT bitmaps per slot
+  uint32_t pad2;
   unsigned long long* i64;
   double* f64;
   long long* mn;
   long long* mx;
-  uint8_t* flags;
+  uint32_t* dbits;           // [num_slots][dc_row_words]
+  unsigned long long* hkeys; // GM_HASH*: [num_slots] packed keys
+  unsigned int* hfill;       // GM_HASH*: claimed keys
+  unsigned int* first_doc;   // GM_HASH_SEG: [num_slots] first matching doc of the (segment, key)
   const SegDesc* segs;       // [seg]
   const WorkItem* items;     // [item]
   unsigned long long* seg_matched;  // [seg]
-  unsigned int* err;                // device-side bounds violations (bit 0 group key, bit 1 DISTINCTCOUNT key)
+  unsigned int* err;                // device-side violations: bit 0 group key, bit 1 DISTINCTCOUNT key, bit 2 hash table full
 };
 
 // order-preserving int64 image of a double (for MIN/MAX slots)
@@ -181,7 +210,6 @@ __host__ __device__ inline double order_key_decode(int64_t k) {
 hipError_t launch_scan(const QuerySpec& q, uint32_t blocks, hipStream_t s);                  // pg_scan.hip
 size_t scan_lds_bytes(const QuerySpec& q);
 uint32_t scan_min_blocks_per_cu(bool grouped);
-hipError_t launch_init_state(const QuerySpec& q, hipStream_t s);                             // pg_kernels.hip
 hipError_t launch_bswap_words(const uint8_t* src, uint32_t* dst, uint64_t nbytes, uint64_t nwords_out, hipStream_t s);
 hipError_t launch_be_to_native(const uint8_t* src, void* dst, uint64_t n, uint32_t width, hipStream_t s);
 hipError_t launch_sorted_to_packed(const int32_t* pairs, uint32_t card, uint32_t num_docs, uint32_t bits,
@@ -211,5 +239,58 @@ struct LutJob {            // set bits ids[0..n) in lut and ids >> shift in regi
   uint32_t shift;
 };
 hipError_t launch_set_lut_bits(const LutJob* jobs, uint32_t njobs, hipStream_t s);
+
+// ---- group state (pg_groups.hip)
+struct StateView {            // the device arrays of one partial state
+  uint64_t num_slots, hmask;
+  unsigned long long* keys;   // hash tables: [num_slots] packed keys (kEmptyKey = free); dense: null
+  unsigned long long* i64;
+  double* f64;
+  long long* mn;
+  long long* mx;
+  uint32_t* bits;
+  unsigned int* first_doc;    // GM_HASH_SEG tables
+  unsigned int* fill;         // hash tables: claimed keys
+  unsigned int* err;          // bit 2: table full
+  uint32_t n_i64, n_f64, n_min, n_max, bit_words, max_fill;
+};
+struct FinalSpec {            // what finalisation needs of the plan
+  uint32_t num_aggs, num_keys;
+  uint32_t order_kind, order_index, order_desc, pad;  // first ORDER BY item (pg_order)
+  AggSpec aggs[kMaxAggs];
+  uint32_t key_card[kMaxKeys];
+  uint64_t key_stride[kMaxKeys];
+};
+enum SelectKind : uint32_t { SEL_PRESENT = 0, SEL_OCCUPIED = 1, SEL_PRESENT_PART = 2 };
+size_t select_temp_bytes(uint64_t n);
+size_t sort_temp_bytes(uint64_t n);
+uint64_t row_bytes(const StateView& v);
+hipError_t launch_select_slots(const StateView& v, uint32_t kind, uint32_t part, uint32_t parts, uint32_t* out,
+                               uint32_t* d_num, void* temp, size_t temp_bytes, hipStream_t s);
+hipError_t launch_select_flagged(const uint32_t* in, const uint8_t* flags, uint64_t n, uint32_t* out, uint32_t* d_num,
+                                 void* temp, size_t temp_bytes, hipStream_t s);
+hipError_t launch_exclusive_sum(const uint64_t* in, uint64_t* out, uint64_t n, void* temp, size_t temp_bytes,
+                                hipStream_t s);
+hipError_t launch_sort_pairs(const uint64_t* kin, uint64_t* kout, const uint32_t* vin, uint32_t* vout, uint64_t n,
+                             void* temp, size_t temp_bytes, hipStream_t s);
+hipError_t launch_final_values(const StateView& v, const FinalSpec& f, const uint32_t* slots, uint64_t n,
+                               uint64_t* keys, double* vals, int64_t* cnts, hipStream_t s);
+hipError_t launch_order_keys(const FinalSpec& f, const uint64_t* keys, const double* vals, const int64_t* cnts,
+                             uint64_t n, uint64_t* out, uint32_t* pos, hipStream_t s);
+hipError_t launch_cutoff(const uint64_t* sorted, uint64_t n, uint64_t limit, uint64_t* out, hipStream_t s);
+hipError_t launch_gather_final(uint32_t A, const uint32_t* pos, uint64_t n, const uint64_t* keys, const double* vals,
+                               const int64_t* cnts, const uint32_t* slots, uint64_t* okeys, double* ovals,
+                               int64_t* ocnts, uint32_t* oslots, hipStream_t s);
+hipError_t launch_set_sizes(const StateView& v, const FinalSpec& f, const uint32_t* slots, uint64_t n,
+                            uint64_t* sizes, hipStream_t s);
+hipError_t launch_set_extract(const StateView& v, const FinalSpec& f, const uint32_t* slots, uint64_t n,
+                              const uint64_t* offsets, uint32_t* ids, hipStream_t s);
+hipError_t launch_gather_rows(const StateView& v, const uint32_t* slots, uint64_t n, uint64_t key_div, uint8_t* dst,
+                              hipStream_t s);
+hipError_t launch_merge_rows(const StateView& v, const uint8_t* rows, uint64_t n, hipStream_t s);
+hipError_t launch_init_view(const StateView& v, hipStream_t s);  // pg_kernels.hip: zero / empty / +-inf state
+hipError_t launch_seg_truncate(const StateView& v, const uint32_t* slots, uint64_t n, uint32_t num_segments,
+                               uint64_t limit, uint64_t* tmp_keys, uint64_t* sorted_keys, uint32_t* sorted_slots,
+                               uint32_t* seg_first, uint8_t* keep, void* temp, size_t temp_bytes, hipStream_t s);
 
 }  // namespace pg

@@ -27,18 +27,19 @@ __global__ void init_minmax_kernel(long long* mn, uint64_t nmn, long long* mx, u
   for (uint64_t k = i; k < nmx; k += stride) mx[k] = order_key(-__builtin_inf());
 }
 
-hipError_t launch_init_state(const QuerySpec& q, hipStream_t s) {
+hipError_t launch_init_view(const StateView& v, hipStream_t s) {
   hipError_t e;
-  if (q.n_i64 && (e = hipMemsetAsync(q.i64, 0, q.num_slots * q.n_i64 * 8, s)) != hipSuccess) return e;
-  if (q.n_f64 && (e = hipMemsetAsync(q.f64, 0, q.num_slots * q.n_f64 * 8, s)) != hipSuccess) return e;
-  if (q.flag_bytes_per_slot && (e = hipMemsetAsync(q.flags, 0, q.num_slots * q.flag_bytes_per_slot, s)) != hipSuccess)
-    return e;
-  if ((e = hipMemsetAsync(q.seg_matched, 0, (q.num_segments ? q.num_segments : 1) * 8ull + 16, s)) != hipSuccess) return e;
-  const uint64_t n = q.num_slots * (q.n_min > q.n_max ? q.n_min : q.n_max);
+  if (v.n_i64 && (e = hipMemsetAsync(v.i64, 0, v.num_slots * v.n_i64 * 8, s)) != hipSuccess) return e;
+  if (v.n_f64 && (e = hipMemsetAsync(v.f64, 0, v.num_slots * v.n_f64 * 8, s)) != hipSuccess) return e;
+  if (v.bit_words && (e = hipMemsetAsync(v.bits, 0, v.num_slots * v.bit_words * 4ull, s)) != hipSuccess) return e;
+  if (v.keys && (e = hipMemsetAsync(v.keys, 0xFF, v.num_slots * 8, s)) != hipSuccess) return e;
+  if (v.first_doc && (e = hipMemsetAsync(v.first_doc, 0xFF, v.num_slots * 4, s)) != hipSuccess) return e;
+  if (v.fill && (e = hipMemsetAsync(v.fill, 0, 8, s)) != hipSuccess) return e;  // fill + err
+  const uint64_t n = v.num_slots * (v.n_min > v.n_max ? v.n_min : v.n_max);
   if (n) {
     const uint32_t blocks = (uint32_t)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
-    hipLaunchKernelGGL(init_minmax_kernel, dim3(blocks), dim3(256), 0, s, q.mn, q.num_slots * q.n_min, q.mx,
-                       q.num_slots * q.n_max);
+    hipLaunchKernelGGL(init_minmax_kernel, dim3(blocks), dim3(256), 0, s, v.mn, v.num_slots * v.n_min, v.mx,
+                       v.num_slots * v.n_max);
   }
   return hipGetLastError();
 }

@@ -509,15 +509,57 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
 // ------------------------------------------------------------------------------------------ execution
 
 struct Partials {
-  DevBuf i64, f64, mn, mx, flags, seg_matched;
+  uint32_t mode = GM_NONE;      // GroupMode (GM_HASH_SEG only between the scan and the truncation merge)
+  uint64_t num_slots = 1;
+  uint32_t n_i64 = 1, n_f64 = 0, n_min = 0, n_max = 0, bit_words = 0, max_fill = 0;
+  DevBuf keys, i64, f64, mn, mx, bits, first_doc, misc /* [fill, err] */, seg_matched;
   std::vector<uint32_t> key_card;
   std::vector<uint64_t> key_stride;
   uint32_t projected_cols = 0;
   uint64_t entries_in_filter = 0;
   uint64_t total_docs = 0;
   uint32_t num_segments = 0;
+  uint32_t layout = 0;          // bit a: aggregation a accumulates integer-exact (i64) -- must agree across merges
   std::vector<AggSpec> aggs;
+
+  StateView view() {
+    StateView v;
+    memset(&v, 0, sizeof(v));
+    v.num_slots = num_slots;
+    v.hmask = mode == GM_HASH || mode == GM_HASH_SEG ? num_slots - 1 : 0;
+    v.keys = (unsigned long long*)keys.p;
+    v.i64 = (unsigned long long*)i64.p;
+    v.f64 = (double*)f64.p;
+    v.mn = (long long*)mn.p;
+    v.mx = (long long*)mx.p;
+    v.bits = (uint32_t*)bits.p;
+    v.first_doc = (unsigned int*)first_doc.p;
+    v.fill = (unsigned int*)misc.p;
+    v.err = misc.p ? (unsigned int*)misc.p + 1 : nullptr;
+    v.n_i64 = n_i64; v.n_f64 = n_f64; v.n_min = n_min; v.n_max = n_max; v.bit_words = bit_words;
+    v.max_fill = max_fill;
+    return v;
+  }
+  // device state for `num_slots` slots of the current layout (+ keys for hash modes), initialised
+  int alloc_state(hipStream_t s);
 };
+
+// Layout of the state arrays of a plan's aggregations (slot assignment, DISTINCTCOUNT bitmap words).  `integer`
+// bit a: SUM / AVG a accumulates integer-exact in i64.
+int agg_layout(const pg_plan* plan, uint32_t integer, std::vector<AggSpec>& aggs, uint32_t& n_i64, uint32_t& n_f64,
+               uint32_t& n_min, uint32_t& n_max, uint32_t& bit_words);
+
+// Pinot's default numGroupsLimit (InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT)
+constexpr uint64_t kDefaultNumGroupsLimit = 100000;
+constexpr uint64_t kDenseMaxSlots = 1ull << 26;      // dense key spaces up to 64 M slots
+constexpr uint64_t kStateBudget = 48ull << 30;       // bytes of group state one query may allocate
+constexpr uint64_t kMaxHashSlots = 1ull << 30;
+
+uint64_t pow2_at_least(uint64_t x) {
+  uint64_t c = 1;
+  while (c < x) c <<= 1;
+  return c;
+}
 
 struct Arena {  // host image of the per-query parameter block, copied to the device in one transfer
   std::vector<uint8_t>& h;  // the calling thread's buffer: its capacity persists, so steady-state queries touch no new pages
@@ -670,21 +712,173 @@ bool pl_too_big(uint32_t ints) { return ints * 4ull > (uint64_t)kLdsSetBytes; }
 // partial last round).  Measured on config 2 / config 3: 6 -> 0.94 / 1.75 ms, 8 -> 0.97 / 1.93 ms, 5 -> 1.01 /
 // 1.99 ms, 7 -> 1.03 / 2.01 ms.  `one_round`: one resident round (the XCD-grouped order).  PG_SCAN_BLOCKS_PER_CU
 // overrides both.
-uint64_t scan_grid_cap(bool grouped, bool one_round = false) {
-  static uint64_t caps[4] = {0, 0, 0, 0};
-  uint64_t& cap = caps[(grouped ? 1 : 0) + (one_round ? 2 : 0)];
-  if (!cap) {
-    int dev_cus = 0;
-    if (hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g_device) != hipSuccess || dev_cus <= 0)
-      dev_cus = 256;
-    const char* e = getenv("PG_SCAN_BLOCKS_PER_CU");
+uint64_t g_grid_caps[4] = {0, 0, 0, 0};
+void init_grid_caps() {  // under g_init_mu (pg_init), before any query reads them
+  int dev_cus = 0;
+  if (hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g_device) != hipSuccess || dev_cus <= 0)
+    dev_cus = 256;
+  const char* e = getenv("PG_SCAN_BLOCKS_PER_CU");
+  for (int i = 0; i < 4; i++) {
+    const bool grouped = i & 1, one_round = i & 2;
     const int per_cu = e ? std::max(1, atoi(e)) : (one_round ? 1 : 2) * (int)scan_min_blocks_per_cu(grouped);
-    cap = (uint64_t)dev_cus * per_cu;
+    g_grid_caps[i] = (uint64_t)dev_cus * per_cu;
   }
-  return cap;
+}
+uint64_t scan_grid_cap(bool grouped, bool one_round = false) {
+  return g_grid_caps[(grouped ? 1 : 0) + (one_round ? 2 : 0)];
 }
 
-int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
+int agg_layout(const pg_plan* plan, uint32_t integer, std::vector<AggSpec>& aggs, uint32_t& n_i64, uint32_t& n_f64,
+               uint32_t& n_min, uint32_t& n_max, uint32_t& bit_words) {
+  n_i64 = 1;  // slot 0: doc count (COUNT, AVG count, group presence)
+  n_f64 = n_min = n_max = bit_words = 0;
+  aggs.assign(plan->num_aggs, AggSpec{});
+  for (uint32_t a = 0; a < plan->num_aggs; a++) {
+    const pg_agg& g = plan->aggs[a];
+    AggSpec& s2 = aggs[a];
+    memset(&s2, 0, sizeof(s2));
+    s2.fn = g.fn;
+    s2.op = g.op;
+    if (g.fn > PG_AGG_COUNTMV) return fail(PG_E_INVALID, "unknown aggregation %u", g.fn);
+    if (g.op > PG_EXPR_SUB) return fail(PG_E_INVALID, "unknown expression op %u", g.op);
+    switch (g.fn) {
+      case PG_AGG_COUNT: s2.kind = SK_NONE; s2.slot = 0; break;
+      case PG_AGG_COUNTMV: s2.kind = SK_I64; s2.slot = n_i64++; break;
+      case PG_AGG_SUM: case PG_AGG_AVG:
+        s2.integer = (integer >> a) & 1u;
+        if (s2.integer) { s2.kind = SK_I64; s2.slot = n_i64++; }
+        else { s2.kind = SK_F64; s2.slot = n_f64++; }
+        s2.cnt_slot = 0;
+        break;
+      case PG_AGG_MIN: s2.kind = SK_MIN; s2.slot = n_min++; break;
+      case PG_AGG_MAX: s2.kind = SK_MAX; s2.slot = n_max++; break;
+      case PG_AGG_DISTINCTCOUNT:
+        if (!g.key_cardinality) return fail(PG_E_INVALID, "DISTINCTCOUNT needs key_cardinality");
+        s2.kind = SK_BITS;
+        s2.key_kind = g.key_kind;
+        s2.key_card = g.key_cardinality;
+        s2.key_base = g.key_base;
+        s2.dc_word = bit_words;
+        bit_words += (g.key_cardinality + 31) / 32;
+        break;
+    }
+  }
+  return PG_OK;
+}
+
+int Partials::alloc_state(hipStream_t s) {
+  const uint64_t G = num_slots;
+  int rc;
+  const bool hash = mode == GM_HASH || mode == GM_HASH_SEG;
+  if ((rc = i64.alloc_pooled(G * 8ull * n_i64))) return rc;
+  if (n_f64) { if ((rc = f64.alloc_pooled(G * 8ull * n_f64))) return rc; } else f64.reset();
+  if (n_min) { if ((rc = mn.alloc_pooled(G * 8ull * n_min))) return rc; } else mn.reset();
+  if (n_max) { if ((rc = mx.alloc_pooled(G * 8ull * n_max))) return rc; } else mx.reset();
+  if (bit_words) { if ((rc = bits.alloc_pooled(G * 4ull * bit_words))) return rc; } else bits.reset();
+  if (hash) { if ((rc = keys.alloc_pooled(G * 8ull))) return rc; } else keys.reset();
+  if (mode == GM_HASH_SEG) { if ((rc = first_doc.alloc_pooled(G * 4ull))) return rc; } else first_doc.reset();
+  if ((rc = misc.alloc_pooled(16))) return rc;
+  HIP_CHECK(launch_init_view(view(), s));
+  return PG_OK;
+}
+
+constexpr int kRetryLargerTable = 1;  // internal: the hash table overflowed its fill budget
+
+// Pooled device scratch of a host-side sequence of small launches (freed after the caller synchronises).
+struct Scratch {
+  hipStream_t s;
+  std::vector<DevBuf> bufs;
+  explicit Scratch(hipStream_t st) : s(st) {}
+  ~Scratch() { (void)hipStreamSynchronize(s); }  // before the blocks return to the pool
+  template <class T> T* get(uint64_t n, int& rc) {
+    bufs.emplace_back();
+    rc = bufs.back().alloc_pooled(n * sizeof(T) + 16);
+    return rc ? nullptr : (T*)bufs.back().p;
+  }
+};
+
+// Copy one device value to the host (synchronous on s).
+template <class T> int read_back(const T* d, T& h, hipStream_t s) {
+  HIP_CHECK(hipMemcpyAsync(&h, d, sizeof(T), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  return PG_OK;
+}
+
+// A fresh GM_HASH state with the layout of `src` and room for `groups` groups.
+int hash_like(const Partials& src, uint64_t groups, Partials& out, hipStream_t s) {
+  out.mode = GM_HASH;
+  out.num_slots = pow2_at_least(std::max<uint64_t>(1024, 2 * groups));
+  if (out.num_slots > kMaxHashSlots) return fail(PG_E_UNSUPPORTED, "merge table of %llu groups too large", (unsigned long long)groups);
+  out.max_fill = (uint32_t)(out.num_slots / 4 * 3);
+  out.n_i64 = src.n_i64; out.n_f64 = src.n_f64; out.n_min = src.n_min; out.n_max = src.n_max;
+  out.bit_words = src.bit_words;
+  out.key_card = src.key_card;
+  out.key_stride = src.key_stride;
+  out.projected_cols = src.projected_cols;
+  out.total_docs = src.total_docs;
+  out.num_segments = src.num_segments;
+  out.layout = src.layout;
+  out.aggs = src.aggs;
+  return out.alloc_state(s);
+}
+
+// numGroupsLimit (IntGroupIdMap.getGroupId, DictionaryBasedGroupKeyGenerator.java:991-1016): every segment of a
+// GM_HASH_SEG table keeps the `limit` keys whose first matching doc comes first (its group ids 0..limit-1; docs of
+// later keys got INVALID_ID and were dropped); the kept (segment, key) states are then merged by key
+// (GroupByOrderByCombineOperator) into a GM_HASH table that replaces P's state.
+int truncate_and_merge(Partials& P, uint64_t limit, hipStream_t s) {
+  const StateView v = P.view();
+  const uint64_t cap = P.num_slots;
+  Scratch sc(s);
+  int rc = PG_OK;
+  const size_t temp_bytes = std::max(select_temp_bytes(cap), sort_temp_bytes(cap));
+  uint32_t* slots = sc.get<uint32_t>(cap, rc);
+  uint32_t* d_num = sc.get<uint32_t>(2, rc);
+  void* temp = sc.get<uint8_t>(temp_bytes, rc);
+  if (rc) return rc;
+  HIP_CHECK(launch_select_slots(v, SEL_OCCUPIED, 0, 1, slots, d_num, temp, temp_bytes, s));
+  uint32_t n = 0;
+  if ((rc = read_back(d_num, n, s))) return rc;
+  uint64_t* tmp_keys = sc.get<uint64_t>(n + 1, rc);
+  uint64_t* sorted_keys = sc.get<uint64_t>(n + 1, rc);
+  uint32_t* sorted_slots = sc.get<uint32_t>(n + 1, rc);
+  uint32_t* seg_first = sc.get<uint32_t>(P.num_segments + 1, rc);
+  uint8_t* keep = sc.get<uint8_t>(n + 1, rc);
+  uint32_t* kept = sc.get<uint32_t>(n + 1, rc);
+  if (rc) return rc;
+  HIP_CHECK(launch_seg_truncate(v, slots, n, P.num_segments, limit, tmp_keys, sorted_keys, sorted_slots, seg_first,
+                                keep, temp, temp_bytes, s));
+  uint32_t nk = 0;
+  if (n) {
+    HIP_CHECK(launch_select_flagged(sorted_slots, keep, n, kept, d_num, temp, temp_bytes, s));
+    if ((rc = read_back(d_num, nk, s))) return rc;
+  }
+  const uint64_t rb = row_bytes(v);
+  uint8_t* rows = sc.get<uint8_t>(rb * (nk + 1), rc);
+  if (rc) return rc;
+  HIP_CHECK(launch_gather_rows(v, kept, nk, P.num_segments, rows, s));
+  Partials H;
+  if ((rc = hash_like(P, nk, H, s))) return rc;
+  HIP_CHECK(launch_merge_rows(H.view(), rows, nk, s));
+  uint32_t fe[2] = {0, 0};
+  HIP_CHECK(hipMemcpyAsync(fe, H.misc.p, 8, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  if (fe[1]) return fail(PG_E_INVALID, "truncation merge overflowed its table (code %u)", fe[1]);
+  P.mode = GM_HASH;
+  P.num_slots = H.num_slots;
+  P.max_fill = H.max_fill;
+  P.keys = std::move(H.keys);
+  P.i64 = std::move(H.i64);
+  P.f64 = std::move(H.f64);
+  P.mn = std::move(H.mn);
+  P.mx = std::move(H.mx);
+  P.bits = std::move(H.bits);
+  P.misc = std::move(H.misc);
+  P.first_doc.reset();
+  return PG_OK;
+}
+
+int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t hash_cap) {
   const double t_enter = wall_ms();
   if (!plan) return fail(PG_E_INVALID, "null plan");
   if (plan->abi_version != PG_ABI_VERSION) return fail(PG_E_INVALID, "ABI version %u != %u", plan->abi_version, PG_ABI_VERSION);
@@ -742,8 +936,10 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   q.num_aggs = A;
   q.num_keys = K;
 
-  // ---- group key space (mixed radix, first key least significant: DictionaryBasedGroupKeyGenerator:280-322)
+  // ---- group key space: packed key = mixed radix of the table-global key ids, first key least significant
+  // (DictionaryBasedGroupKeyGenerator raw keys, :280-322, over table-global ids so segments merge by value)
   uint64_t G = 1;
+  bool g_over = false;
   P.key_card.assign(K, 0);
   P.key_stride.assign(K, 0);
   for (uint32_t k = 0; k < K; k++) {
@@ -756,13 +952,18 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
     q.key_stride[k] = G;
     P.key_card[k] = key.cardinality;
     P.key_stride[k] = G;
-    if (G > (1ull << 31) / key.cardinality) return fail(PG_E_UNSUPPORTED, "group key space exceeds 2^31 slots");
-    G *= key.cardinality;
+    if (G > (~0ull) / key.cardinality) g_over = true;
+    else G *= key.cardinality;
   }
-  // numGroupsLimit: the reference truncates per segment once the limit is hit (first-seen order,
-  // IntGroupIdMap :991-1016).  The device path only runs when no segment can reach the limit.
+  if (K && (g_over || G >= (1ull << 62)))
+    return fail(PG_E_UNSUPPORTED, "packed group key of %u keys exceeds 62 bits", K);
+  // numGroupsLimit: a segment keeps the first `limit` distinct keys in doc order (IntGroupIdMap :991-1016).  It can
+  // only bite in a segment whose matching docs or key-cardinality product exceed the limit (the array-based holder,
+  // card product <= maxInitialResultHolderCapacity <= limit, never truncates).
+  const uint64_t limit = plan->num_groups_limit ? plan->num_groups_limit : kDefaultNumGroupsLimit;
+  uint64_t seg_groups = 0;  // sum over segments of an upper bound of the segment's distinct keys
+  bool truncating = false;
   if (K) {
-    const uint64_t limit = plan->num_groups_limit ? plan->num_groups_limit : 100000;
     for (uint32_t si = 0; si < S; si++) {
       uint64_t prod = 1;
       for (uint32_t k = 0; k < K; k++) {
@@ -779,27 +980,22 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
           return fail(PG_E_INVALID, "column %u values outside the key range of key %u", plan->keys[k].col_id, k);
         prod = prod > (1ull << 62) / (c->card ? c->card : 1) ? (1ull << 62) : prod * c->card;
       }
-      if (prod > limit)
-        return fail(PG_E_UNSUPPORTED, "segment %u may exceed numGroupsLimit %llu (card product %llu)", si,
-                    (unsigned long long)limit, (unsigned long long)prod);
+      const uint64_t ub = std::min<uint64_t>(prod, plan->segments[si].num_docs);
+      seg_groups += ub;
+      truncating |= ub > limit;
     }
   }
 
-  // ---- aggregation state slots
-  uint32_t n_i64 = 1, n_f64 = 0, n_min = 0, n_max = 0;
-  uint64_t flag_bytes = 0;
+  // ---- aggregation state layout
   uint64_t total_docs = 0;
   for (uint32_t si = 0; si < S; si++) total_docs += plan->segments[si].num_docs;
   std::unordered_set<uint32_t> projected;
+  uint32_t integer = 0;
   for (uint32_t a = 0; a < A; a++) {
     const pg_agg& g = plan->aggs[a];
-    AggSpec& s2 = q.aggs[a];
-    memset(&s2, 0, sizeof(s2));
-    s2.fn = g.fn;
-    s2.op = g.op;
     if (g.fn > PG_AGG_COUNTMV) return fail(PG_E_INVALID, "unknown aggregation %u", g.fn);
     if (g.op > PG_EXPR_SUB) return fail(PG_E_INVALID, "unknown expression op %u", g.op);
-    if (g.fn == PG_AGG_COUNT) { s2.kind = SK_NONE; s2.slot = 0; continue; }
+    if (g.fn == PG_AGG_COUNT) continue;
     projected.insert(g.col_a);
     const bool two = (g.fn == PG_AGG_SUM || g.fn == PG_AGG_MIN || g.fn == PG_AGG_MAX || g.fn == PG_AGG_AVG) && g.op != PG_EXPR_COL;
     if (two) projected.insert(g.col_b);
@@ -833,43 +1029,64 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
         bound_b = std::max(bound_b, std::max(fabs(cb->dmin), fabs(cb->dmax)));
       }
     }
-    switch (g.fn) {
-      case PG_AGG_COUNTMV: s2.kind = SK_I64; s2.slot = n_i64++; break;
-      case PG_AGG_SUM: case PG_AGG_AVG: {
-        double vb = bound_a;
-        if (two) vb = g.op == PG_EXPR_MUL ? bound_a * bound_b : bound_a + bound_b;
-        // integer-exact accumulation when every partial sum provably fits in int64 (2^62 margin)
-        s2.integer = all_int && vb * (double)(total_docs ? total_docs : 1) < 4.0e18;
-        if (s2.integer) { s2.kind = SK_I64; s2.slot = n_i64++; }
-        else { s2.kind = SK_F64; s2.slot = n_f64++; }
-        s2.cnt_slot = 0;
-        break;
-      }
-      case PG_AGG_MIN: s2.kind = SK_MIN; s2.slot = n_min++; break;
-      case PG_AGG_MAX: s2.kind = SK_MAX; s2.slot = n_max++; break;
-      case PG_AGG_DISTINCTCOUNT:
-        if (!g.key_cardinality) return fail(PG_E_INVALID, "DISTINCTCOUNT needs key_cardinality");
-        s2.kind = SK_FLAG;
-        s2.key_kind = g.key_kind;
-        s2.key_card = g.key_cardinality;
-        s2.key_base = g.key_base;
-        s2.flag_off = flag_bytes;
-        flag_bytes += g.key_cardinality;
-        break;
+    if (g.fn == PG_AGG_SUM || g.fn == PG_AGG_AVG) {
+      double vb = bound_a;
+      if (two) vb = g.op == PG_EXPR_MUL ? bound_a * bound_b : bound_a + bound_b;
+      // integer-exact accumulation when every partial sum provably fits in int64 (2^62 margin); identical to the
+      // reference's double accumulation while |sum| < 2^53, more exact beyond (within the 1e-9 tolerance)
+      const bool as_int = all_int && !(plan->flags & PG_PLAN_F64_SUMS) &&
+                          vb * (double)(total_docs ? total_docs : 1) < 4.0e18;
+      if (as_int) integer |= 1u << a;
     }
+  }
+  {
+    int rc2 = agg_layout(plan, integer, P.aggs, P.n_i64, P.n_f64, P.n_min, P.n_max, P.bit_words);
+    if (rc2) return rc2;
+    P.layout = integer;
+    for (uint32_t a = 0; a < A; a++) q.aggs[a] = P.aggs[a];
   }
   for (uint32_t k = 0; k < K; k++) projected.insert(plan->keys[k].col_id);
   for (uint32_t a = 0; a < A; a++) q.agg_reads |= plan->aggs[a].fn != PG_AGG_COUNT;
-  q.num_slots = G;
-  q.n_i64 = n_i64; q.n_f64 = n_f64; q.n_min = n_min; q.n_max = n_max;
-  q.flag_bytes_per_slot = flag_bytes;
-  const uint64_t state_bytes = G * 8ull * (n_i64 + n_f64 + n_min + n_max) + G * flag_bytes;
-  if (state_bytes > (64ull << 30)) return fail(PG_E_UNSUPPORTED, "group state of %llu bytes exceeds the 64 GiB budget", (unsigned long long)state_bytes);
-  q.use_lds = K > 0 && G * 8ull * (n_i64 + n_f64 + n_min + n_max) <= (uint64_t)kLdsGroupBytes;
+
+  // ---- group state addressing: dense key space, hash table of global keys, or (numGroupsLimit can truncate a
+  // segment) hash table of (segment, key) with first-seen docs
+  const uint64_t slot_bytes = 8ull * (P.n_i64 + P.n_f64 + P.n_min + P.n_max) + 4ull * P.bit_words;
+  if (K == 0) {
+    P.mode = GM_NONE;
+    P.num_slots = 1;
+  } else {
+    const bool dense = !(plan->flags & PG_PLAN_HASH_GROUPS) && G <= kDenseMaxSlots &&
+                       G * slot_bytes <= kStateBudget / 4 && G <= 4 * total_docs + 65536;
+    P.mode = truncating ? GM_HASH_SEG : (dense ? GM_DENSE : GM_HASH);
+    if (P.mode == GM_DENSE) {
+      P.num_slots = G;
+    } else {
+      if (P.mode == GM_HASH_SEG && (G - 1) > ((1ull << 62) - S) / std::max(1u, S))
+        return fail(PG_E_UNSUPPORTED, "per-segment group key (key space %llu x %u segments) exceeds 62 bits",
+                    (unsigned long long)G, S);
+      const uint64_t expect = P.mode == GM_HASH_SEG ? seg_groups : std::min(G, std::min(total_docs, seg_groups));
+      uint64_t cap = hash_cap ? hash_cap : pow2_at_least(std::max<uint64_t>(1024, 2 * expect));
+      // large bounds start smaller and grow on overflow (err bit 4 -> rerun with 8x the table)
+      if (!hash_cap && cap * (slot_bytes + 12) > (4ull << 30)) cap = std::max<uint64_t>(1024, pow2_at_least((4ull << 30) / (slot_bytes + 12)) / 2);
+      if (cap > kMaxHashSlots || cap * (slot_bytes + 12) > kStateBudget)
+        return fail(PG_E_UNSUPPORTED, "group-by hash table of %llu slots x %llu bytes exceeds the state budget",
+                    (unsigned long long)cap, (unsigned long long)slot_bytes);
+      P.num_slots = cap;
+      P.max_fill = (uint32_t)(cap / 4 * 3);
+    }
+  }
+  if (P.num_slots * slot_bytes > kStateBudget)
+    return fail(PG_E_UNSUPPORTED, "group state of %llu bytes exceeds the budget", (unsigned long long)(P.num_slots * slot_bytes));
+  q.group_mode = P.mode;
+  q.num_slots = P.num_slots;
+  q.hmask = P.mode == GM_HASH || P.mode == GM_HASH_SEG ? P.num_slots - 1 : 0;
+  q.hmax_fill = P.max_fill;
+  q.n_i64 = P.n_i64; q.n_f64 = P.n_f64; q.n_min = P.n_min; q.n_max = P.n_max;
+  q.dc_row_words = P.bit_words;
+  q.use_lds = P.mode == GM_DENSE && G * 8ull * (P.n_i64 + P.n_f64 + P.n_min + P.n_max) <= (uint64_t)kLdsGroupBytes;
   P.projected_cols = (uint32_t)projected.size();
   P.total_docs = total_docs;
   P.num_segments = S;
-  P.aggs.assign(q.aggs, q.aggs + A);
 
   // ---- per (segment, leaf) lowering.  A leaf's dictId set becomes: a contiguous range -> RANGE; a small set
   // -> LDS hash set (uniform table size per leaf across segments so the LDS layout is fixed); else a global
@@ -972,6 +1189,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   for (uint32_t si = 0; si < S; si++) {
     const pg_segment_ref& sr = plan->segments[si];
     segd[si].num_docs = sr.num_docs;
+    segd[si].index = si;
     seg_tiles[si] = (uint32_t)(((uint64_t)sr.num_docs + kTileDocs - 1) / kTileDocs);
     for (uint32_t li = 0; li < L; li++) {
       const pg_leaf& pl = sr.leaves[li];
@@ -1340,17 +1558,20 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   if (lds_bytes > 160 * 1024) return fail(PG_E_UNSUPPORTED, "scan needs %zu bytes of LDS", lds_bytes);
 
   // ---- device buffers (state + arena + scratch) from the caching pool
-  if ((rc = P.i64.alloc_pooled(G * 8ull * n_i64))) return rc;
-  if (n_f64 && (rc = P.f64.alloc_pooled(G * 8ull * n_f64))) return rc;
-  if (n_min && (rc = P.mn.alloc_pooled(G * 8ull * n_min))) return rc;
-  if (n_max && (rc = P.mx.alloc_pooled(G * 8ull * n_max))) return rc;
-  if (flag_bytes && (rc = P.flags.alloc_pooled(G * flag_bytes))) return rc;
+  if ((rc = P.alloc_state(s))) return rc;
   if ((rc = P.seg_matched.alloc_pooled(8ull * (S ? S : 1) + 16))) return rc;
-  q.i64 = (unsigned long long*)P.i64.p;
-  q.f64 = (double*)P.f64.p;
-  q.mn = (long long*)P.mn.p;
-  q.mx = (long long*)P.mx.p;
-  q.flags = (uint8_t*)P.flags.p;
+  HIP_CHECK(hipMemsetAsync(P.seg_matched.p, 0, 8ull * (S ? S : 1) + 16, s));
+  {
+    const StateView v = P.view();
+    q.i64 = v.i64;
+    q.f64 = v.f64;
+    q.mn = v.mn;
+    q.mx = v.mx;
+    q.dbits = v.bits;
+    q.hkeys = v.keys;
+    q.hfill = v.fill;
+    q.first_doc = v.first_doc;
+  }
   q.seg_matched = (unsigned long long*)P.seg_matched.p;
   q.err = (unsigned int*)(q.seg_matched + (S ? S : 1));
 
@@ -1425,7 +1646,6 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   memcpy(staging, ar.h.data(), ar.h.size());
   hipEvent_t* ev = t_ctx.ev;
   HIP_CHECK(hipMemcpyAsync(arena.p, staging, ar.h.size(), hipMemcpyHostToDevice, s));
-  HIP_CHECK(launch_init_state(q, s));
   HIP_CHECK(hipEventRecord(ev[0], s));
   if (scratch_bytes) HIP_CHECK(hipMemsetAsync(scratch.p, 0, scratch_bytes, s));
   HIP_CHECK(launch_set_lut_bits((const LutJob*)(dA + off_lutjobs), (uint32_t)lutjobs.size(), s));
@@ -1473,17 +1693,62 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats) {
   {
     for (uint32_t i = 0; i < S; i++) { stats.num_docs_scanned += sm[i]; stats.num_segments_matched += sm[i] > 0; }
     const uint32_t err = (uint32_t)sm[S ? S : 1];
+    if (err & 4u) return kRetryLargerTable;  // hash table over its fill budget: rerun with a larger one
     if (err) return fail(PG_E_INVALID, "device bounds check failed (code %u): a key fell outside the plan's key space", err);
   }
   stats.num_entries_scanned_post_filter = stats.num_docs_scanned * P.projected_cols;
+  if (P.mode == GM_HASH_SEG) {
+    const double t0 = wall_ms();
+    if ((rc = truncate_and_merge(P, limit, s))) return rc;
+    t_timing.finalize_wall_ms = (float)(wall_ms() - t0);
+  }
   return PG_OK;
 }
 
+
 struct PartialsImpl {
   Partials P;
-  std::vector<uint64_t> seg_matched_host;
 };
 
+void fill_handle(pg_partials* p, PartialsImpl* impl) {
+  Partials& P = impl->P;
+  p->num_slots = P.num_slots;
+  p->mode = P.mode == GM_HASH ? PG_STATE_HASH : PG_STATE_DENSE;
+  p->n_i64 = P.n_i64; p->n_f64 = P.n_f64; p->n_min = P.n_min; p->n_max = P.n_max;
+  p->bitmap_words = P.bit_words;
+  p->layout = P.layout;
+  p->row_bytes = row_bytes(P.view());
+  p->keys = (uint64_t*)P.keys.p;
+  p->i64 = (int64_t*)P.i64.p;
+  p->f64 = (double*)P.f64.p;
+  p->mn = (int64_t*)P.mn.p;
+  p->mx = (int64_t*)P.mx.p;
+  p->bitmaps = (uint32_t*)P.bits.p;
+  p->impl = impl;
+}
+
+FinalSpec make_final(const Partials& P, const pg_plan* plan) {
+  FinalSpec f;
+  memset(&f, 0, sizeof(f));
+  f.num_aggs = (uint32_t)P.aggs.size();
+  f.num_keys = (uint32_t)P.key_card.size();
+  for (uint32_t a = 0; a < f.num_aggs; a++) f.aggs[a] = P.aggs[a];
+  for (uint32_t k = 0; k < f.num_keys; k++) {
+    f.key_card[k] = P.key_card[k];
+    f.key_stride[k] = P.key_stride[k];
+  }
+  if (plan->num_order) {
+    f.order_kind = plan->order[0].kind;
+    f.order_index = plan->order[0].index;
+    f.order_desc = plan->order[0].desc;
+  }
+  return f;
+}
+
+// Partial state -> host result: the groups present (doc count > 0), their final values, the plan's ORDER BY trim
+// (IndexedTable.finish -> TableResizer.getTopRecords: a radix sort on the first ORDER BY item on the device, the
+// candidates -- every group that ranks within `limit`, ties included -- fully ordered on the host) and, on request,
+// the DISTINCTCOUNT value sets.
 int finalize(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   const double t0 = wall_ms();
   struct Stamp {
@@ -1492,70 +1757,178 @@ int finalize(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   } stamp{t0};
   PartialsImpl* impl = (PartialsImpl*)pp->impl;
   Partials& P = impl->P;
-  const uint64_t G = pp->num_slots;
   const uint32_t A = plan->num_aggs, K = plan->num_keys;
-  if (A != P.aggs.size()) return fail(PG_E_INVALID, "plan does not match partials");
+  if (A != P.aggs.size() || K != P.key_card.size()) return fail(PG_E_INVALID, "plan does not match partials");
+  if (plan->num_order && !plan->order) return fail(PG_E_INVALID, "null order list");
+  for (uint32_t i = 0; i < plan->num_order; i++) {
+    const pg_order& o = plan->order[i];
+    if (o.kind > PG_ORDER_KEY || (o.kind == PG_ORDER_AGG && o.index >= A) || (o.kind == PG_ORDER_KEY && o.index >= K))
+      return fail(PG_E_INVALID, "bad ORDER BY item %u", i);
+  }
   int rc = t_ctx.init();
   if (rc) return rc;
-  hipEvent_t e0 = t_ctx.ev[3], e1 = t_ctx.ev[2];
   hipStream_t s = thread_stream();
+  hipEvent_t e0 = t_ctx.ev[3], e1 = t_ctx.ev[2];
   HIP_CHECK(hipEventRecord(e0, s));
-  std::vector<int64_t> hi64(G * pp->n_i64), hmn(G * pp->n_min), hmx(G * pp->n_max);
-  std::vector<double> hf64(G * pp->n_f64);
-  std::vector<uint8_t> hflags(G * pp->flag_bytes_per_slot);
-  HIP_CHECK(hipMemcpyAsync(hi64.data(), pp->i64, hi64.size() * 8, hipMemcpyDeviceToHost, s));
-  if (!hf64.empty()) HIP_CHECK(hipMemcpyAsync(hf64.data(), pp->f64, hf64.size() * 8, hipMemcpyDeviceToHost, s));
-  if (!hmn.empty()) HIP_CHECK(hipMemcpyAsync(hmn.data(), pp->mn, hmn.size() * 8, hipMemcpyDeviceToHost, s));
-  if (!hmx.empty()) HIP_CHECK(hipMemcpyAsync(hmx.data(), pp->mx, hmx.size() * 8, hipMemcpyDeviceToHost, s));
-  if (!hflags.empty()) HIP_CHECK(hipMemcpyAsync(hflags.data(), pp->flags, hflags.size(), hipMemcpyDeviceToHost, s));
+  Scratch sc(s);
+  const StateView v = P.view();
+  const FinalSpec f = make_final(P, plan);
+  const uint32_t AA = A ? A : 1;
+
+  // 1. the groups
+  uint64_t n = 1;
+  // aggregation-only: slot 0 (always one row); a merged hash state holds key 0 only if some rank had matches
+  const bool single = K == 0 && P.mode != GM_HASH;
+  uint32_t* slots = sc.get<uint32_t>(single ? 1 : P.num_slots, rc);
+  uint32_t* d_num = sc.get<uint32_t>(2, rc);
+  if (rc) return rc;
+  if (single) {
+    HIP_CHECK(hipMemsetAsync(slots, 0, 4, s));
+  } else {
+    const size_t tb = select_temp_bytes(P.num_slots);
+    void* temp = sc.get<uint8_t>(tb, rc);
+    if (rc) return rc;
+    HIP_CHECK(launch_select_slots(v, SEL_PRESENT, 0, 1, slots, d_num, temp, tb, s));
+    uint32_t n32 = 0;
+    if ((rc = read_back(d_num, n32, s))) return rc;
+    n = n32;
+  }
+  // 2. final values
+  uint64_t* dkeys = sc.get<uint64_t>(n + 1, rc);
+  double* dvals = sc.get<double>((n + 1) * AA, rc);
+  int64_t* dcnts = sc.get<int64_t>((n + 1) * AA, rc);
+  if (rc) return rc;
+  HIP_CHECK(launch_final_values(v, f, slots, n, dkeys, dvals, dcnts, s));
+  // 3. ORDER BY trim
+  uint64_t nc = n;
+  const uint64_t* ck = dkeys;
+  const double* cv = dvals;
+  const int64_t* cc = dcnts;
+  const uint32_t* cs = slots;
+  if (K && plan->num_order && plan->limit && n > plan->limit) {
+    const size_t tb = sort_temp_bytes(n);
+    uint64_t* okeys = sc.get<uint64_t>(n, rc);
+    uint64_t* skeys = sc.get<uint64_t>(n, rc);
+    uint32_t* pos = sc.get<uint32_t>(n, rc);
+    uint32_t* spos = sc.get<uint32_t>(n, rc);
+    uint64_t* d_nc = sc.get<uint64_t>(1, rc);
+    void* temp = sc.get<uint8_t>(tb, rc);
+    if (rc) return rc;
+    HIP_CHECK(launch_order_keys(f, dkeys, dvals, dcnts, n, okeys, pos, s));
+    HIP_CHECK(launch_sort_pairs(okeys, skeys, pos, spos, n, temp, tb, s));
+    HIP_CHECK(launch_cutoff(skeys, n, plan->limit, d_nc, s));
+    if ((rc = read_back(d_nc, nc, s))) return rc;
+    uint64_t* gk = sc.get<uint64_t>(nc, rc);
+    double* gv = sc.get<double>(nc * AA, rc);
+    int64_t* gc = sc.get<int64_t>(nc * AA, rc);
+    uint32_t* gs = sc.get<uint32_t>(nc, rc);
+    if (rc) return rc;
+    HIP_CHECK(launch_gather_final(A, spos, nc, dkeys, dvals, dcnts, slots, gk, gv, gc, gs, s));
+    ck = gk; cv = gv; cc = gc; cs = gs;
+  }
+  std::vector<uint64_t> hk(nc);
+  std::vector<double> hv(nc * A);
+  std::vector<int64_t> hc(nc * A);
+  if (nc) {
+    HIP_CHECK(hipMemcpyAsync(hk.data(), ck, nc * 8, hipMemcpyDeviceToHost, s));
+    if (A) {
+      HIP_CHECK(hipMemcpyAsync(hv.data(), cv, nc * A * 8, hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipMemcpyAsync(hc.data(), cc, nc * A * 8, hipMemcpyDeviceToHost, s));
+    }
+  }
+  // 4. value sets
+  bool sets = false;
+  for (uint32_t a = 0; a < A; a++) sets |= (plan->flags & PG_PLAN_VALUE_SETS) && P.aggs[a].fn == PG_AGG_DISTINCTCOUNT;
+  std::vector<uint64_t> hoff;
+  std::vector<uint32_t> hids;
+  if (sets) {
+    const uint64_t m = nc * A;
+    uint64_t* sizes = sc.get<uint64_t>(m + 1, rc);
+    uint64_t* offs = sc.get<uint64_t>(m + 1, rc);
+    const size_t tb = select_temp_bytes(m + 1);
+    void* temp = sc.get<uint8_t>(tb, rc);
+    if (rc) return rc;
+    HIP_CHECK(hipMemsetAsync(sizes + m, 0, 8, s));
+    HIP_CHECK(launch_set_sizes(v, f, cs, nc, sizes, s));
+    HIP_CHECK(launch_exclusive_sum(sizes, offs, m + 1, temp, tb, s));
+    hoff.resize(m + 1);
+    HIP_CHECK(hipMemcpyAsync(hoff.data(), offs, (m + 1) * 8, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    uint32_t* ids = sc.get<uint32_t>(hoff[m] + 1, rc);
+    if (rc) return rc;
+    HIP_CHECK(launch_set_extract(v, f, cs, nc, offs, ids, s));
+    hids.resize(hoff[m]);
+    if (hoff[m]) HIP_CHECK(hipMemcpyAsync(hids.data(), ids, hoff[m] * 4, hipMemcpyDeviceToHost, s));
+  }
   HIP_CHECK(hipEventRecord(e1, s));
   HIP_CHECK(hipStreamSynchronize(s));
   float fm = 0;
   (void)hipEventElapsedTime(&fm, e0, e1);
   t_timing.finalize_ms = fm;
 
+  // 5. host order of the candidates: every ORDER BY item, then the packed key (a total order)
+  std::vector<uint64_t> perm(nc);
+  for (uint64_t i = 0; i < nc; i++) perm[i] = i;
+  if (K && plan->num_order) {
+    auto val = [&](uint64_t i, uint32_t a) {
+      double x = hv[i * A + a];
+      if (P.aggs[a].fn == PG_AGG_AVG) {
+        const int64_t c = hc[i * A + a];
+        x = c ? x / (double)c : -INFINITY;
+      }
+      return x;
+    };
+    std::sort(perm.begin(), perm.end(), [&](uint64_t i, uint64_t j) {
+      for (uint32_t o = 0; o < plan->num_order; o++) {
+        const pg_order& it = plan->order[o];
+        if (it.kind == PG_ORDER_AGG) {
+          const double x = val(i, it.index), y = val(j, it.index);
+          if (x != y) return it.desc ? x > y : x < y;
+        } else {
+          const uint64_t x = (hk[i] / P.key_stride[it.index]) % P.key_card[it.index];
+          const uint64_t y = (hk[j] / P.key_stride[it.index]) % P.key_card[it.index];
+          if (x != y) return it.desc ? x > y : x < y;
+        }
+      }
+      return hk[i] < hk[j];
+    });
+  }
+
   pg_result* r = (pg_result*)calloc(1, sizeof(pg_result));
+  if (!r) return fail(PG_E_NOMEM, "out of host memory");
   r->stats = pp->stats;  // local, or merged across ranks by the caller before finalize
   r->stats.num_entries_scanned_post_filter = r->stats.num_docs_scanned * P.projected_cols;
   r->num_keys = K;
   r->num_aggs = A;
-  std::vector<uint64_t> gl;
-  if (K == 0) gl.push_back(0);
-  else
-    for (uint64_t g = 0; g < G; g++)
-      if (hi64[g * pp->n_i64] > 0) gl.push_back(g);
-  r->num_groups = gl.size();
-  r->keys = (uint32_t*)calloc(gl.size() * (K ? K : 1), 4);
-  r->values = (double*)calloc(gl.size() * (A ? A : 1), 8);
-  r->counts = (int64_t*)calloc(gl.size() * (A ? A : 1), 8);
-  for (uint64_t o = 0; o < gl.size(); o++) {
-    const uint64_t g = gl[o];
-    for (uint32_t k = 0; k < K; k++) r->keys[o * K + k] = (uint32_t)((g / P.key_stride[k]) % P.key_card[k]);
-    const int64_t cnt = hi64[g * pp->n_i64];
+  r->num_groups = nc;
+  r->keys = (uint32_t*)calloc(nc * (K ? K : 1) + 1, 4);
+  r->values = (double*)calloc(nc * AA + 1, 8);
+  r->counts = (int64_t*)calloc(nc * AA + 1, 8);
+  if (!r->keys || !r->values || !r->counts) { pg_result_free(r); return fail(PG_E_NOMEM, "out of host memory"); }
+  for (uint64_t o = 0; o < nc; o++) {
+    const uint64_t i = perm[o];
+    for (uint32_t k = 0; k < K; k++) r->keys[o * K + k] = (uint32_t)((hk[i] / P.key_stride[k]) % P.key_card[k]);
     for (uint32_t a = 0; a < A; a++) {
-      const AggSpec& s2 = P.aggs[a];
-      double v = 0;
-      int64_t c2 = 0;
-      switch (s2.fn) {
-        case PG_AGG_COUNT: v = (double)cnt; break;
-        case PG_AGG_COUNTMV: v = (double)hi64[g * pp->n_i64 + s2.slot]; break;
-        case PG_AGG_SUM: case PG_AGG_AVG:
-          v = s2.integer ? (double)hi64[g * pp->n_i64 + s2.slot] : hf64[g * pp->n_f64 + s2.slot];
-          if (s2.fn == PG_AGG_AVG) c2 = cnt;
-          break;
-        case PG_AGG_MIN: v = order_key_decode(hmn[g * pp->n_min + s2.slot]); break;
-        case PG_AGG_MAX: v = order_key_decode(hmx[g * pp->n_max + s2.slot]); break;
-        case PG_AGG_DISTINCTCOUNT: {
-          uint64_t n = 0;
-          const uint8_t* f = &hflags[g * pp->flag_bytes_per_slot + s2.flag_off];
-          for (uint64_t x = 0; x < s2.key_card; x++) n += f[x] != 0;
-          v = (double)n;
-          break;
-        }
-      }
-      r->values[o * A + a] = v;
-      r->counts[o * A + a] = c2;
+      r->values[o * A + a] = hv[i * A + a];
+      r->counts[o * A + a] = hc[i * A + a];
     }
+  }
+  if (sets) {
+    const uint64_t m = nc * A;
+    r->num_distinct = hids.size();
+    r->distinct_offsets = (uint64_t*)malloc((m + 1) * 8);
+    r->distinct_ids = (uint32_t*)malloc(hids.size() * 4 + 4);
+    if (!r->distinct_offsets || !r->distinct_ids) { pg_result_free(r); return fail(PG_E_NOMEM, "out of host memory"); }
+    uint64_t at = 0;
+    for (uint64_t o = 0; o < nc; o++)
+      for (uint32_t a = 0; a < A; a++) {
+        const uint64_t src = perm[o] * A + a;
+        r->distinct_offsets[o * A + a] = at;
+        const uint64_t len = hoff[src + 1] - hoff[src];
+        if (len) memcpy(r->distinct_ids + at, hids.data() + hoff[src], len * 4);
+        at += len;
+      }
+    r->distinct_offsets[m] = at;
   }
   *out = r;
   return PG_OK;
@@ -1577,6 +1950,7 @@ int pg_init(int device) {
   if (g_device >= 0 && g_device != device) return fail(PG_E_STATE, "already bound to device %d", g_device);
   HIP_CHECK(hipSetDevice(device));
   g_device = device;
+  init_grid_caps();
   return PG_OK;
 }
 
@@ -1638,34 +2012,24 @@ int pg_execute_partial(const pg_plan* plan, pg_partials** out) {
   pg_stats st;
   const double t0 = wall_ms();
   t_timing.host_compile_ms = 0;
+  t_timing.finalize_wall_ms = 0;
   try {
-    rc = compile_and_run(plan, impl->P, st);
+    uint64_t cap = 0;
+    for (;;) {
+      rc = compile_and_run(plan, impl->P, st, cap);
+      if (rc != kRetryLargerTable) break;
+      cap = impl->P.num_slots * 8;  // the group-by hash table overflowed: rerun with 8x the slots
+      if (cap > kMaxHashSlots) { rc = fail(PG_E_UNSUPPORTED, "group-by needs more than %llu hash slots", (unsigned long long)kMaxHashSlots); break; }
+    }
     t_timing.execute_wall_ms = (float)(wall_ms() - t0);
   } catch (const std::exception& e) {
     rc = fail(PG_E_NOMEM, "execute failed: %s", e.what());
   }
   if (rc) { delete impl; return rc; }
   pg_partials* p = (pg_partials*)calloc(1, sizeof(pg_partials));
+  if (!p) { delete impl; return fail(PG_E_NOMEM, "out of host memory"); }
   p->stats = st;
-  p->num_slots = 1;
-  for (uint32_t c : impl->P.key_card) p->num_slots *= c;
-  uint32_t n_i64 = 1, n_f64 = 0, n_min = 0, n_max = 0;
-  uint64_t fb = 0;
-  for (const AggSpec& a : impl->P.aggs) {
-    if (a.kind == SK_I64) n_i64 = std::max(n_i64, a.slot + 1);
-    if (a.kind == SK_F64) n_f64 = std::max(n_f64, a.slot + 1);
-    if (a.kind == SK_MIN) n_min = std::max(n_min, a.slot + 1);
-    if (a.kind == SK_MAX) n_max = std::max(n_max, a.slot + 1);
-    if (a.kind == SK_FLAG) fb = std::max<uint64_t>(fb, a.flag_off + a.key_card);
-  }
-  p->n_i64 = n_i64; p->n_f64 = n_f64; p->n_min = n_min; p->n_max = n_max;
-  p->flag_bytes_per_slot = fb;
-  p->i64 = (int64_t*)impl->P.i64.p;
-  p->f64 = (double*)impl->P.f64.p;
-  p->mn = (int64_t*)impl->P.mn.p;
-  p->mx = (int64_t*)impl->P.mx.p;
-  p->flags = (uint8_t*)impl->P.flags.p;
-  p->impl = impl;
+  fill_handle(p, impl);
   *out = p;
   return PG_OK;
 }
@@ -1673,7 +2037,7 @@ int pg_execute_partial(const pg_plan* plan, pg_partials** out) {
 int pg_partials_finalize(pg_partials* p, const pg_plan* plan, pg_result** out) {
   int rc = ensure_device();
   if (rc) return rc;
-  if (!p || !plan || !out) return fail(PG_E_INVALID, "null argument");
+  if (!p || !plan || !out || !p->impl) return fail(PG_E_INVALID, "null argument");
   try {
     return finalize(p, plan, out);
   } catch (const std::exception& e) {
@@ -1684,32 +2048,98 @@ int pg_partials_finalize(pg_partials* p, const pg_plan* plan, pg_result** out) {
 int pg_partials_free(pg_partials* p) {
   if (!p) return PG_OK;
   ensure_device();
-  PartialsImpl* impl = (PartialsImpl*)p->impl;
-  if (impl) {
-    impl->P.i64.reset(); impl->P.f64.reset(); impl->P.mn.reset(); impl->P.mx.reset();
-    impl->P.flags.reset(); impl->P.seg_matched.reset();
-    delete impl;
-  }
+  delete (PartialsImpl*)p->impl;
   free(p);
   return PG_OK;
 }
 
-int pg_partials_copy(pg_partials* p, int dir, void* i64, void* f64, void* mn, void* mx, void* flags, void* stream) {
+int pg_partials_copy(pg_partials* p, int dir, void* i64, void* f64, void* mn, void* mx, void* stream) {
   int rc = ensure_device();
   if (rc) return rc;
-  if (!p || (dir != PG_COPY_OUT && dir != PG_COPY_IN)) return fail(PG_E_INVALID, "bad partials / direction");
+  if (!p || !p->impl || (dir != PG_COPY_OUT && dir != PG_COPY_IN)) return fail(PG_E_INVALID, "bad partials / direction");
+  if (p->mode != PG_STATE_DENSE) return fail(PG_E_INVALID, "pg_partials_copy needs a dense state (use pg_partials_export)");
   hipStream_t s = stream ? (hipStream_t)stream : thread_stream();
-  void* mine[5] = {p->i64, p->f64, p->mn, p->mx, p->flags};
-  void* theirs[5] = {i64, f64, mn, mx, flags};
-  const uint64_t bytes[5] = {p->num_slots * 8ull * p->n_i64, p->num_slots * 8ull * p->n_f64,
-                             p->num_slots * 8ull * p->n_min, p->num_slots * 8ull * p->n_max,
-                             p->num_slots * p->flag_bytes_per_slot};
-  for (int i = 0; i < 5; i++) {
+  void* mine[4] = {p->i64, p->f64, p->mn, p->mx};
+  void* theirs[4] = {i64, f64, mn, mx};
+  const uint64_t bytes[4] = {p->num_slots * 8ull * p->n_i64, p->num_slots * 8ull * p->n_f64,
+                             p->num_slots * 8ull * p->n_min, p->num_slots * 8ull * p->n_max};
+  for (int i = 0; i < 4; i++) {
     if (!theirs[i] || !bytes[i]) continue;
     if (dir == PG_COPY_OUT) HIP_CHECK(hipMemcpyAsync(theirs[i], mine[i], bytes[i], hipMemcpyDeviceToDevice, s));
     else HIP_CHECK(hipMemcpyAsync(mine[i], theirs[i], bytes[i], hipMemcpyDeviceToDevice, s));
   }
   HIP_CHECK(hipStreamSynchronize(s));
+  return PG_OK;
+}
+
+int pg_partials_export(pg_partials* p, uint32_t num_parts, void* dst, uint64_t dst_rows, uint64_t* part_counts,
+                       void* stream) {
+  int rc = ensure_device();
+  if (rc) return rc;
+  if (!p || !p->impl || !num_parts || !part_counts) return fail(PG_E_INVALID, "bad export arguments");
+  try {
+    Partials& P = ((PartialsImpl*)p->impl)->P;
+    hipStream_t s = stream ? (hipStream_t)stream : thread_stream();
+    Scratch sc(s);
+    const StateView v = P.view();
+    const size_t tb = select_temp_bytes(P.num_slots);
+    uint32_t* slots = sc.get<uint32_t>(P.num_slots, rc);
+    uint32_t* d_num = sc.get<uint32_t>(2, rc);
+    void* temp = sc.get<uint8_t>(tb, rc);
+    if (rc) return rc;
+    uint64_t at = 0;
+    for (uint32_t part = 0; part < num_parts; part++) {
+      HIP_CHECK(launch_select_slots(v, SEL_PRESENT_PART, part, num_parts, slots, d_num, temp, tb, s));
+      uint32_t n = 0;
+      if ((rc = read_back(d_num, n, s))) return rc;
+      part_counts[part] = n;
+      if (dst) {
+        if (at + n > dst_rows) return fail(PG_E_INVALID, "export buffer of %llu rows too small", (unsigned long long)dst_rows);
+        HIP_CHECK(launch_gather_rows(v, slots, n, 1, (uint8_t*)dst + at * p->row_bytes, s));
+      }
+      at += n;
+    }
+    HIP_CHECK(hipStreamSynchronize(s));
+    return PG_OK;
+  } catch (const std::exception& e) {
+    return fail(PG_E_NOMEM, "export failed: %s", e.what());
+  }
+}
+
+int pg_partials_create(const pg_partials* like, uint64_t capacity, pg_partials** out) {
+  int rc = ensure_device();
+  if (rc) return rc;
+  if (!like || !like->impl || !out) return fail(PG_E_INVALID, "null argument");
+  *out = nullptr;
+  PartialsImpl* impl = new (std::nothrow) PartialsImpl();
+  if (!impl) return fail(PG_E_NOMEM, "out of host memory");
+  try {
+    hipStream_t s = thread_stream();
+    rc = hash_like(((PartialsImpl*)like->impl)->P, capacity, impl->P, s);
+    if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = fail(PG_E_HIP, "state initialisation failed");
+  } catch (const std::exception& e) {
+    rc = fail(PG_E_NOMEM, "create failed: %s", e.what());
+  }
+  if (rc) { delete impl; return rc; }
+  pg_partials* p = (pg_partials*)calloc(1, sizeof(pg_partials));
+  if (!p) { delete impl; return fail(PG_E_NOMEM, "out of host memory"); }
+  fill_handle(p, impl);
+  *out = p;
+  return PG_OK;
+}
+
+int pg_partials_merge(pg_partials* p, const void* rows, uint64_t n, void* stream) {
+  int rc = ensure_device();
+  if (rc) return rc;
+  if (!p || !p->impl || (!rows && n)) return fail(PG_E_INVALID, "null argument");
+  Partials& P = ((PartialsImpl*)p->impl)->P;
+  if (P.mode != GM_HASH) return fail(PG_E_INVALID, "pg_partials_merge needs a hash state (pg_partials_create)");
+  hipStream_t s = stream ? (hipStream_t)stream : thread_stream();
+  HIP_CHECK(launch_merge_rows(P.view(), (const uint8_t*)rows, n, s));
+  uint32_t fe[2] = {0, 0};
+  HIP_CHECK(hipMemcpyAsync(fe, P.misc.p, 8, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  if (fe[1]) return fail(PG_E_NOMEM, "merge table of %llu slots is full", (unsigned long long)P.num_slots);
   return PG_OK;
 }
 
@@ -1728,6 +2158,8 @@ int pg_result_free(pg_result* r) {
   free(r->keys);
   free(r->values);
   free(r->counts);
+  free(r->distinct_offsets);
+  free(r->distinct_ids);
   free(r);
   return PG_OK;
 }

@@ -405,6 +405,39 @@ __device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
   return v;
 }
 
+// Hash-mode slot of packed key `key`: its table position, claimed with one 64-bit CAS on first sight (linear
+// probing; keys only ever change PG_EMPTY_KEY -> key, so a stale read of an empty entry just costs a failed CAS).
+// ~0 when the table is over its fill budget: err bit 4, and the runtime reruns the scan with a larger table.
+__device__ __forceinline__ uint64_t hash_slot(const QuerySpec& q, uint64_t key) {
+  uint64_t h = mix64(key) & q.hmask;
+  for (uint64_t n = 0; n <= q.hmask; n++) {
+    const unsigned long long cur = q.hkeys[h];
+    if (cur == key) return h;
+    if (cur == kEmptyKey) {
+      if (__hip_atomic_load(q.hfill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= q.hmax_fill) break;
+      const unsigned long long prev = atomicCAS(&q.hkeys[h], kEmptyKey, (unsigned long long)key);
+      if (prev == kEmptyKey) {
+        atomicAdd(q.hfill, 1u);
+        return h;
+      }
+      if (prev == key) return h;
+    }
+    h = (h + 1) & q.hmask;
+  }
+  atomicOr(q.err, 4u);
+  return ~0ull;
+}
+
+// State slot of a doc's group from its packed key (dense: the key itself).  GM_HASH_SEG keys carry the segment and
+// record the segment's first doc of the key (IntGroupIdMap assigns ids in first-seen doc order).
+__device__ __forceinline__ uint64_t group_slot(const QuerySpec& q, uint64_t packed, uint32_t seg, uint32_t doc) {
+  if (q.group_mode == GM_DENSE) return packed;
+  if (q.group_mode == GM_HASH) return hash_slot(q, packed);
+  const uint64_t h = hash_slot(q, packed * q.num_segments + seg);
+  if (h != ~0ull) atomicMin(&q.first_doc[h], doc);
+  return h;
+}
+
 // Group-state pointers: the block's LDS copy when the table is privatised, else the global arrays.
 struct GroupState {
   unsigned long long* i64;
@@ -430,7 +463,7 @@ __device__ __forceinline__ void group_update(const QuerySpec& q, const GroupStat
     case PG_AGG_MAX: atomicMax(&S.mx[g * q.n_max + A.slot], (long long)order_key(value_f64(A, c, ia, ib))); break;
     case PG_AGG_DISTINCTCOUNT: {
       const uint64_t key = key_of(A.key_kind, A.key_base, ldc(c, 0), ia);
-      if (key < A.key_card) q.flags[g * q.flag_bytes_per_slot + A.flag_off + key] = 1;
+      if (key < A.key_card) atomicOr(&q.dbits[g * q.dc_row_words + A.dc_word + (key >> 5)], 1u << (key & 31u));
       else atomicOr(q.err, 2u);
       break;
     }
@@ -460,7 +493,7 @@ __device__ __forceinline__ void acc_update(const QuerySpec& q, const AggSpec& A,
     }
     case PG_AGG_DISTINCTCOUNT: {
       const uint64_t key = key_of(A.key_kind, A.key_base, ldc(c, 0), ia);
-      if (key < A.key_card) q.flags[A.flag_off + key] = 1;
+      if (key < A.key_card) atomicOr(&q.dbits[A.dc_word + (key >> 5)], 1u << (key & 31u));
       else atomicOr(q.err, 2u);
       break;
     }
@@ -479,7 +512,7 @@ __device__ __forceinline__ uint32_t col_id(const QuerySpec& q, uint32_t slot, co
 // together (the switch on the function is outside the row loop so the 8 reads are straight-line).
 template <bool GROUPED>
 __device__ __forceinline__ void agg_rows8(const QuerySpec& q, const GroupState& S, const AggSpec& A, const ColDesc* c,
-                                          const uint32_t (&ia)[8], const uint32_t (&ib)[8], const uint32_t (&g)[8],
+                                          const uint32_t (&ia)[8], const uint32_t (&ib)[8], const uint64_t (&g)[8],
                                           const uint32_t (&d)[8], uint32_t live, uint64_t& acc) {
   switch (A.fn) {
     case PG_AGG_COUNT: break;
@@ -492,7 +525,7 @@ __device__ __forceinline__ void agg_rows8(const QuerySpec& q, const GroupState& 
 #pragma unroll
         for (int r = 0; r < 8; r++) {
           if (!((live >> r) & 1u)) continue;
-          if constexpr (GROUPED) atomicAdd(&S.i64[(uint64_t)g[r] * q.n_i64 + A.slot], (unsigned long long)v[r]);
+          if constexpr (GROUPED) atomicAdd(&S.i64[g[r] * q.n_i64 + A.slot], (unsigned long long)v[r]);
           else acc += (uint64_t)v[r];
         }
       } else {
@@ -502,7 +535,7 @@ __device__ __forceinline__ void agg_rows8(const QuerySpec& q, const GroupState& 
 #pragma unroll
         for (int r = 0; r < 8; r++) {
           if (!((live >> r) & 1u)) continue;
-          if constexpr (GROUPED) atomicAdd(&S.f64[(uint64_t)g[r] * q.n_f64 + A.slot], v[r]);
+          if constexpr (GROUPED) atomicAdd(&S.f64[g[r] * q.n_f64 + A.slot], v[r]);
           else acc = __double_as_longlong(__longlong_as_double(acc) + v[r]);
         }
       }
@@ -517,8 +550,8 @@ __device__ __forceinline__ void agg_rows8(const QuerySpec& q, const GroupState& 
       for (int r = 0; r < 8; r++) {
         if (!((live >> r) & 1u)) continue;
         if constexpr (GROUPED) {
-          if (is_min) atomicMin(&S.mn[(uint64_t)g[r] * q.n_min + A.slot], (long long)k[r]);
-          else atomicMax(&S.mx[(uint64_t)g[r] * q.n_max + A.slot], (long long)k[r]);
+          if (is_min) atomicMin(&S.mn[g[r] * q.n_min + A.slot], (long long)k[r]);
+          else atomicMax(&S.mx[g[r] * q.n_max + A.slot], (long long)k[r]);
         } else {
           if (is_min ? k[r] < (int64_t)acc : k[r] > (int64_t)acc) acc = (uint64_t)k[r];
         }
@@ -544,7 +577,8 @@ __device__ __forceinline__ void aggregate_dense(const QuerySpec& q, const SegDes
   for (int ch = 0; ch < kRows / 8; ch++) {
     const uint32_t mc = (m >> (8 * ch)) & 0xFFu;
     if (__ballot(mc != 0) == 0) continue;
-    uint32_t d[8], rel[8], g[8];
+    uint32_t d[8], rel[8];
+    uint64_t g[8];
     uint32_t live = mc;
 #pragma unroll
     for (int r = 0; r < 8; r++) {
@@ -566,13 +600,20 @@ __device__ __forceinline__ void aggregate_dense(const QuerySpec& q, const SegDes
 #pragma unroll
         for (int r = 0; r < 8; r++) {
           if (kid[r] >= q.key_card[k]) live &= ~(1u << r);
-          else g[r] += (uint32_t)kid[r] * (uint32_t)q.key_stride[k];
+          else g[r] += kid[r] * q.key_stride[k];
         }
       }
       if (live != mc) atomicOr(q.err, 1u);  // never expected: the host proved the key ranges
+      if (q.group_mode != GM_DENSE) {
+        for (int r = 0; r < 8; r++) {
+          if (!((live >> r) & 1u)) continue;
+          g[r] = group_slot(q, g[r], sd.index, d[r]);
+          if (g[r] == ~0ull) live &= ~(1u << r);
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 8; r++)
-        if ((live >> r) & 1u) atomicAdd(&S.i64[(uint64_t)g[r] * q.n_i64], 1ull);  // slot 0: doc count / presence
+        if ((live >> r) & 1u) atomicAdd(&S.i64[g[r] * q.n_i64], 1ull);  // slot 0: doc count / presence
     }
 #pragma unroll
     for (int a = 0; a < MAXA; a++) {
@@ -647,6 +688,8 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
           atomicOr(q.err, 1u);
           continue;
         }
+        g = group_slot(q, g, sd.index, d[x]);
+        if (g == ~0ull) continue;
         atomicAdd(&S.i64[g * q.n_i64], 1ull);  // slot 0: doc count / presence
 #pragma unroll
         for (int a = 0; a < MAXA; a++) {

@@ -151,10 +151,12 @@ class GpuEngine:
 
     # ---- execution
     def make_plan(self, table: Table, query: QueryContext, segments: Optional[Sequence[ImmutableSegment]] = None,
-                  num_groups_limit=None) -> CPlan:
+                  num_groups_limit=None, flags: int = abi.PG_PLAN_VALUE_SETS, trim: bool = False) -> CPlan:
+        """flags: PG_PLAN_* (default: DISTINCTCOUNT value sets, the reference's Set intermediate).  trim: the device
+        applies the query's ORDER BY / LIMIT (a final single-server answer; boundary ties kept)."""
         segments = list(table.segments if segments is None else segments)
         keys = [self.upload_segment(s, table) for s in segments]
-        plan = CPlan(table, query, segments, keys, num_groups_limit)
+        plan = CPlan(table, query, segments, keys, num_groups_limit, flags, trim)
         self.upload_keymaps(table, plan, segments, keys)
         return plan
 
@@ -167,26 +169,42 @@ class GpuEngine:
             self.lib.pg_result_free(res)
 
     def run_partial(self, plan: CPlan):
-        """pg_execute_partial: this device's dense partial state (for the cross-GPU merge, pinot_amd.combine)."""
+        """pg_execute_partial: this device's partial state (for the cross-GPU merge, pinot_amd.combine)."""
         p = C.POINTER(abi.pg_partials)()
         check(self.lib.pg_execute_partial(C.byref(plan.plan), C.byref(p)))
         return p
 
-    def finalize_partial(self, plan: CPlan, p) -> IntermediateResult:
+    def finalize_partial(self, plan: CPlan, p, free: bool = True) -> IntermediateResult:
         res = C.POINTER(abi.pg_result)()
         try:
             check(self.lib.pg_partials_finalize(p, C.byref(plan.plan), C.byref(res)))
         finally:
-            self.lib.pg_partials_free(p)
+            if free:
+                self.lib.pg_partials_free(p)
         try:
             return self.decode(plan, res.contents)
         finally:
             self.lib.pg_result_free(res)
 
-    def execute(self, table: Table, query, segments=None, num_groups_limit=None) -> IntermediateResult:
+    def export_rows(self, p, num_parts: int, dst_ptr=None, dst_rows: int = 0, stream=None):
+        """pg_partials_export: rows of the groups bucketed by owner part; returns the per-part row counts."""
+        counts = (C.c_uint64 * num_parts)()
+        check(self.lib.pg_partials_export(p, num_parts, dst_ptr, dst_rows, counts, stream))
+        return list(counts)
+
+    def create_like(self, p, capacity: int):
+        out = C.POINTER(abi.pg_partials)()
+        check(self.lib.pg_partials_create(p, capacity, C.byref(out)))
+        return out
+
+    def merge_rows(self, p, rows_ptr, n: int, stream=None):
+        check(self.lib.pg_partials_merge(p, rows_ptr, n, stream))
+
+    def execute(self, table: Table, query, segments=None, num_groups_limit=None, flags: int = abi.PG_PLAN_VALUE_SETS,
+                trim: bool = False) -> IntermediateResult:
         if isinstance(query, str):
             query = parse(query)
-        return self.run_plan(self.make_plan(table, query, segments, num_groups_limit))
+        return self.run_plan(self.make_plan(table, query, segments, num_groups_limit, flags, trim))
 
     def last_timing(self) -> abi.pg_timing:
         t = abi.pg_timing()
@@ -204,12 +222,19 @@ class GpuEngine:
             np.zeros((G, A), dtype=np.int64)
         keys = np.ctypeslib.as_array(r.keys, shape=(max(G * K, 1),))[:G * K].reshape(G, K) if G and K else \
             np.zeros((G, K), dtype=np.uint32)
+        sets = None
+        if r.distinct_offsets:
+            offs = np.ctypeslib.as_array(r.distinct_offsets, shape=(G * A + 1,)).copy()
+            ids = (np.ctypeslib.as_array(r.distinct_ids, shape=(max(int(r.num_distinct), 1),))[:r.num_distinct]
+                   .astype(np.int64))
+            sets = (offs, ids)
         rows = {}
         # plain Python lists: one conversion per array instead of a numpy scalar access per element
         vals_l, cnts_l, keys_l = vals.tolist(), cnts.tolist(), keys.tolist()
         kval = [plan.key_spaces[k].value for k in range(K)]
-        kinds = [0 if ag.function in ("COUNT", "COUNTMV", "DISTINCTCOUNT") else 1 if ag.function == "AVG" else 2
-                 for ag in plan.aggs]
+        kinds = [0 if ag.function in ("COUNT", "COUNTMV") else 3 if ag.function == "DISTINCTCOUNT" else
+                 1 if ag.function == "AVG" else 2 for ag in plan.aggs]
+        dspaces = [plan.table.key_space(ag.arg.cols[0]) if k == 3 else None for ag, k in zip(plan.aggs, kinds)]
         for g in range(G):
             kg, vg, cg = keys_l[g], vals_l[g], cnts_l[g]
             key = tuple(kval[k](kg[k]) for k in range(K))
@@ -220,6 +245,12 @@ class GpuEngine:
                     row.append(int(round(v)))
                 elif kind == 1:
                     row.append((v, int(cg[a])))
+                elif kind == 3:
+                    if sets is None:
+                        row.append(int(round(v)))  # size only (no PG_PLAN_VALUE_SETS)
+                    else:
+                        offs, ids = sets
+                        row.append(dspaces[a].values_of(ids[offs[g * A + a]:offs[g * A + a + 1]]))
                 else:
                     row.append(v)
             rows[key] = row

@@ -25,7 +25,8 @@ from . import abi
 from .query import UNBOUNDED, Aggregation, FilterContext, Predicate, QueryContext
 from .segment import Column, ImmutableSegment
 
-MAX_VALUE_OFFSET_KEYS = 1 << 26   # integer key ranges up to this size use value offsets (no keymap)
+MAX_VALUE_OFFSET_KEYS = 1 << 26   # integer key ranges up to this size may use value offsets (no keymap) ...
+VALUE_OFFSET_DENSITY = 4          # ... when the range is at most this many times the largest segment cardinality
 DEFAULT_NUM_GROUPS_LIMIT = 100_000          # InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT
 DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY = 10_000  # InstancePlanMakerImplV2 :73
 
@@ -184,6 +185,7 @@ class KeySpace:
     base: int = 0
     values: Optional[list] = None    # KEYMAP: global id -> value (sorted union)
     keymaps: Optional[List[np.ndarray]] = None  # per segment dictId -> global id
+    _values_np: Optional[np.ndarray] = None
 
     @staticmethod
     def build(column: str, cols: List[Column]) -> "KeySpace":
@@ -191,8 +193,12 @@ class KeySpace:
         if dt in ("INT", "LONG"):
             lo = min(int(c.dictionary.values[0]) for c in cols)
             hi = max(int(c.dictionary.values[-1]) for c in cols)
-            if hi - lo + 1 <= MAX_VALUE_OFFSET_KEYS:
-                return KeySpace(column, abi.PG_KEY_VALUE_OFFSET, hi - lo + 1, lo)
+            span = hi - lo + 1
+            # dense enough for direct ids: a sparse range (few values spread wide) would make every group-by state,
+            # DISTINCTCOUNT bitmap and merge scale with the range instead of the values
+            if span <= MAX_VALUE_OFFSET_KEYS and span <= max(1 << 16, VALUE_OFFSET_DENSITY *
+                                                             max(len(c.dictionary) for c in cols)):
+                return KeySpace(column, abi.PG_KEY_VALUE_OFFSET, span, lo)
         if dt in ("INT", "LONG", "FLOAT", "DOUBLE"):
             allv = np.unique(np.concatenate([np.asarray(c.dictionary.values) for c in cols]))
             keymaps = [np.searchsorted(allv, np.asarray(c.dictionary.values)).astype(np.int32) for c in cols]
@@ -206,6 +212,14 @@ class KeySpace:
         if self.kind == abi.PG_KEY_VALUE_OFFSET:
             return int(self.base + gid)
         return self.values[gid]
+
+    def values_of(self, gids: np.ndarray) -> set:
+        """The value set of an array of global ids (DISTINCTCOUNT's Set intermediate)."""
+        if self.kind == abi.PG_KEY_VALUE_OFFSET:
+            return set((np.asarray(gids, dtype=np.int64) + self.base).tolist())
+        if self._values_np is None:
+            self._values_np = np.asarray(self.values, dtype=object)
+        return set(self._values_np[np.asarray(gids, dtype=np.int64)].tolist())
 
 
 # ------------------------------------------------------------------------------------------ results
@@ -256,6 +270,14 @@ def merge_intermediate(aggs: List[Aggregation], a: list, b: list) -> list:
     return out
 
 
+def default_row(aggs: List[Aggregation]) -> list:
+    """Intermediate values of an aggregation over no docs (each function's initial holder value, e.g.
+    MinAggregationFunction DEFAULT_INITIAL_VALUE = +inf, AvgPair(0, 0), an empty DISTINCTCOUNT set)."""
+    init = {"COUNT": 0, "COUNTMV": 0, "SUM": 0.0, "MIN": float("inf"), "MAX": float("-inf")}
+    return [(0.0, 0) if a.function == "AVG" else set() if a.function == "DISTINCTCOUNT" else init[a.function]
+            for a in aggs]
+
+
 def final_value(ag: Aggregation, v):
     """extractFinalResult of each function (e.g. AvgAggregationFunction.java:276-286)."""
     f = ag.function
@@ -280,6 +302,8 @@ def reduce_to_rows(query: QueryContext, res: IntermediateResult) -> Tuple[List[s
     rows_out = []
     if not query.group_by:
         vals = res.rows.get((), None)
+        if vals is None:
+            vals = default_row(aggs)
         row = []
         for s in query.select:
             row.append(final_value(s.agg, vals[agg_index[s.agg]]))
@@ -330,7 +354,10 @@ class CPlan:
     """Owns every ctypes array a pg_plan points to (kept alive while the plan is in use)."""
 
     def __init__(self, table: Table, query: QueryContext, segments: Sequence[ImmutableSegment],
-                 seg_keys: Sequence[int], num_groups_limit: Optional[int] = None):
+                 seg_keys: Sequence[int], num_groups_limit: Optional[int] = None, flags: int = 0,
+                 trim: bool = False):
+        """flags: PG_PLAN_*.  trim: let the device apply the query's ORDER BY / LIMIT to the group-by result
+        (IndexedTable.finish + TableResizer; boundary ties kept) -- for a final, single-server answer."""
         self.table = table
         self.query = query
         self.aggs = query.aggregations
@@ -416,5 +443,20 @@ class CPlan:
         p.keys = keys
         lim = num_groups_limit or int(query.options.get("numGroupsLimit", DEFAULT_NUM_GROUPS_LIMIT))
         p.num_groups_limit = lim
+        p.flags = flags
+        if trim and query.group_by and query.order_by:
+            order = (abi.pg_order * len(query.order_by))()
+            for i, o in enumerate(query.order_by):
+                if o.kind == "AGG":
+                    order[i].kind, order[i].index = abi.PG_ORDER_AGG, self.aggs.index(o.agg)
+                elif o.column in query.group_by:
+                    order[i].kind, order[i].index = abi.PG_ORDER_KEY, query.group_by.index(o.column)
+                else:
+                    raise UnsupportedQuery(f"ORDER BY {o.column}")
+                order[i].desc = 0 if o.asc else 1
+            self._keep.append(order)
+            p.num_order = len(query.order_by)
+            p.order = order
+            p.limit = query.limit
         self.plan = p
         self.ops = ops

@@ -66,6 +66,20 @@ def ssb_q11_query() -> str:
             "WHERE lo_orderdate BETWEEN 8035 AND 8399 AND lo_discount BETWEEN 1 AND 3 AND lo_quantity < 25")
 
 
+# Config 4: high-cardinality group-by: 10 M users x 1 000 items, 128 segments of 7 812 500 rows
+def highcard_specs(users: int = 10_000_000, items: int = 1000) -> List[ColSpec]:
+    return [ColSpec("userId", 0, users), ColSpec("itemId", 0, items)]
+
+
+HIGHCARD = highcard_specs()
+
+
+def highcard_query(limit: int = 100) -> str:
+    """Config 4 query: distinct items per user, top users (a total order: userId breaks DISTINCTCOUNT ties)."""
+    return ("SELECT userId, DISTINCTCOUNT(itemId) FROM events GROUP BY userId "
+            f"ORDER BY DISTINCTCOUNT(itemId) DESC, userId LIMIT {limit}")
+
+
 def column_salt(name: str) -> int:
     return (zlib.crc32(name.encode()) ^ (SEED * 0x9E3779B1)) & M32
 

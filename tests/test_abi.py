@@ -18,7 +18,7 @@ LIB = os.path.join(ROOT, "pinot_amd", "libpinot_gpu.so")
 def header_functions():
     with open(HEADER) as f:
         src = f.read()
-    return sorted(set(re.findall(r"^int\s+(pg_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|uint32_t)\s+(pg_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_header_and_mirror_agree():
@@ -47,8 +47,8 @@ def test_library_is_gfx950_only():
         assert b"amdhsa--" + other not in blob
 
 
-STRUCTS = ["pg_col_desc", "pg_leaf", "pg_agg", "pg_key", "pg_segment_ref", "pg_plan", "pg_stats", "pg_result",
-           "pg_partials", "pg_timing"]
+STRUCTS = ["pg_col_desc", "pg_leaf", "pg_agg", "pg_key", "pg_segment_ref", "pg_order", "pg_plan", "pg_stats",
+           "pg_result", "pg_partials", "pg_timing"]
 
 
 def test_struct_layouts_match_header(tmp_path):

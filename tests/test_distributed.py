@@ -38,7 +38,7 @@ def _worker_state(rank, world, port, q):
     g = torch.Generator().manual_seed(rank)
     st = {"i64": torch.randint(0, 1000, (50,), generator=g), "f64": torch.rand(20, generator=g, dtype=torch.float64),
           "mn": torch.randint(-100, 100, (30,), generator=g), "mx": torch.randint(-100, 100, (30,), generator=g),
-          "flags": (torch.rand(64, generator=g) > 0.5).to(torch.uint8), "stats": torch.tensor([rank + 1] * 6)}
+          "stats": torch.tensor([rank + 1] * 6)}
     orig = {k: v.clone() for k, v in st.items()}
     allreduce_state(st)
     allg = {}
@@ -48,7 +48,6 @@ def _worker_state(rank, world, port, q):
         allg[k] = torch.stack(parts)
     ok = (torch.equal(st["i64"], allg["i64"].sum(0)) and torch.allclose(st["f64"], allg["f64"].sum(0))
           and torch.equal(st["mn"], allg["mn"].min(0).values) and torch.equal(st["mx"], allg["mx"].max(0).values)
-          and torch.equal(st["flags"], allg["flags"].max(0).values)
           and torch.equal(st["stats"], torch.tensor([world * (world + 1) // 2] * 6)))
     q.put((rank, ok))
     dist.destroy_process_group()

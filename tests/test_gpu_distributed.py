@@ -1,0 +1,90 @@
+"""Two ranks on one MI355X (gloo, world_size 2, both on cuda:0): each rank runs pg_execute_partial over half of the
+segments and pinot_amd.combine merges the DEVICE partial states -- the dense all-reduce path (small dense key space)
+and the row-exchange path (hash states, DISTINCTCOUNT bitmaps: all_to_all of rows by owner, pg_partials_merge) -- and
+the merged result must equal the CPU oracle over the whole table.  The same code runs over RCCL at N GPUs."""
+import os
+import socket
+import sys
+import traceback
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CASES = [
+    # (sql, force hash table)  -- dense all-reduce, then row exchange
+    ("SELECT daysSinceEpoch, SUM(clicks), SUM(impressions) FROM adAnalytics WHERE daysSinceEpoch BETWEEN 18000 AND "
+     "18089 AND accountId < 300000 GROUP BY daysSinceEpoch ORDER BY daysSinceEpoch LIMIT 400", False),
+    ("SELECT COUNT(*), SUM(clicks), MIN(impressions), MAX(accountId), AVG(clicks) FROM adAnalytics "
+     "WHERE accountId < 5000", False),
+    ("SELECT daysSinceEpoch, COUNT(*), SUM(clicks), MIN(impressions), MAX(impressions), AVG(clicks) FROM adAnalytics "
+     "WHERE clicks < 100 GROUP BY daysSinceEpoch", True),
+    ("SELECT daysSinceEpoch, DISTINCTCOUNT(clicks), SUM(impressions) FROM adAnalytics WHERE accountId < 20000 "
+     "GROUP BY daysSinceEpoch", False),
+    ("SELECT accountId, COUNT(*), SUM(impressions) FROM adAnalytics WHERE clicks < 5 GROUP BY accountId", False),
+    ("SELECT DISTINCTCOUNT(impressions), COUNT(*) FROM adAnalytics WHERE accountId < 1000", False),
+]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from helpers import assert_same_result
+        from oracle.oracle import OracleEngine
+        from pinot_amd import abi, synth
+        from pinot_amd.combine import merge_partials_across_ranks
+        from pinot_amd.gpu import GpuEngine
+        from pinot_amd.plan import Table
+        from pinot_amd.query import parse
+        eng = GpuEngine(0)
+        segs = [synth.make_segment_np(synth.ADANALYTICS, s, 60_001 + 777 * s) for s in range(4)]
+        table = Table("adAnalytics", segs)          # table-global key spaces: the same on every rank
+        mine = segs[rank::world]
+        paths = []
+        for sql, force_hash in CASES:
+            qc = parse(sql)
+            flags = abi.PG_PLAN_VALUE_SETS | (abi.PG_PLAN_HASH_GROUPS if force_hash else 0)
+            plan = eng.make_plan(table, qc, segments=mine, flags=flags)
+            p = eng.run_partial(plan)
+            pc = p.contents
+            paths.append("dense" if pc.mode == abi.PG_STATE_DENSE and pc.bitmap_words == 0 else "rows")
+            merged = merge_partials_across_ranks(eng, plan, p)
+            whole = OracleEngine().execute(table, qc)
+            assert_same_result(merged, whole, table=table)
+        q.put((rank, True, paths))
+        dist.destroy_process_group()
+    except Exception:
+        q.put((rank, False, traceback.format_exc()))
+
+
+def test_two_ranks_merge_device_partials():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, info in res:
+        assert ok, info
+    assert "dense" in res[0][2] and "rows" in res[0][2]

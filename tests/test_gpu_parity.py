@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 from helpers import assert_same_result, check_inner_values, check_rows, inner_query, run_rows, with_filter
-from pinot_amd.plan import Table, UnsupportedQuery
+from pinot_amd.plan import Table, UnsupportedQuery, reduce_to_rows
 from pinot_amd.query import parse
 from pinot_amd.segment import ImmutableSegment
 
@@ -22,7 +22,7 @@ def test_golden_inner_aggregation(i, expected, gpu_engine, sv_table_inner):
     check_inner_values(res, case)
 
 
-@pytest.mark.parametrize("i", range(4))
+@pytest.mark.parametrize("i", range(6))
 def test_golden_inner_group_by(i, expected, gpu_engine, sv_table_inner):
     case = expected["inner_group_by"][i]
     res = gpu_engine.execute(sv_table_inner, inner_query(case, expected["filter"]))
@@ -73,13 +73,115 @@ def test_sv_queries_match_oracle(sql, gpu_engine, oracle_engine, sv_table_inter)
     q = parse(sql)
     g = gpu_engine.execute(sv_table_inter, q)
     o = oracle_engine.execute(sv_table_inter, q)
-    assert_same_result(g, o)
+    assert_same_result(g, o, table=sv_table_inter)
 
 
 def test_unsupported_shape_is_reported_not_crashed(gpu_engine, sv_table_inner):
-    """GROUP BY whose per-segment key space can exceed numGroupsLimit -> PG_E_UNSUPPORTED (caller falls back)."""
+    """More group-by keys than the device path takes -> PG_E_UNSUPPORTED (the caller falls back to the CPU plan)."""
     with pytest.raises(UnsupportedQuery):
-        gpu_engine.execute(sv_table_inner, "SELECT COUNT(*) FROM t GROUP BY column1, column6, column9")
+        gpu_engine.execute(sv_table_inner, "SELECT COUNT(*) FROM t GROUP BY column1, column3, column5, column6, column7, "
+                                           "column9, column11, column12, column17")
+
+
+GROUP_QUERIES = [q for q in SV_QUERIES if "GROUP BY" in q] + [
+    "SELECT column1, column6, column9, column11, column12, COUNT(*), SUM(column1), MAX(column3), MIN(column6), "
+    "AVG(column7) FROM t GROUP BY column1, column6, column9, column11, column12",
+    "SELECT column9, DISTINCTCOUNT(column1), SUM(column17) FROM t WHERE column3 > 1000000000 GROUP BY column9",
+]
+
+
+@pytest.mark.parametrize("sql", GROUP_QUERIES)
+def test_group_by_hash_table_matches_oracle(sql, gpu_engine, oracle_engine, sv_table_inter):
+    """The same group-bys through the device hash table (IntGroupIdMap / Long2IntOpenHashMap on the device) instead of
+    direct addressing: identical results."""
+    from pinot_amd import abi
+    q = parse(sql)
+    g = gpu_engine.execute(sv_table_inter, q, flags=abi.PG_PLAN_VALUE_SETS | abi.PG_PLAN_HASH_GROUPS)
+    assert_same_result(g, oracle_engine.execute(sv_table_inter, q), table=sv_table_inter)
+
+
+@pytest.mark.parametrize("limit", [1, 37, 500, 1736, 1737])
+def test_num_groups_limit_truncation(limit, gpu_engine, oracle_engine):
+    """numGroupsLimit below the segment's distinct keys: each segment keeps the keys it sees first (doc order) and
+    drops the docs of later keys (IntGroupIdMap.getGroupId, DictionaryBasedGroupKeyGenerator.java:991-1016); the
+    segments then merge by value.  Segments hold different data so their kept key sets differ."""
+    rng = np.random.default_rng(limit)
+    segs = []
+    for s_ in range(3):
+        n = 20000 + 1111 * s_
+        data = {"k": rng.integers(0, 2000, n), "k2": rng.integers(0, 3, n), "v": rng.integers(-10 ** 6, 10 ** 6, n),
+                "d": rng.normal(size=n), "u": rng.integers(0, 300, n)}
+        segs.append(_seg(f"t{s_}", data, {"k": "INT", "k2": "INT", "v": "LONG", "d": "DOUBLE", "u": "INT"}))
+    t = Table("t", segs)
+    for sql in ["SELECT k, COUNT(*), SUM(v), MIN(d), MAX(v), AVG(d), DISTINCTCOUNT(u) FROM t GROUP BY k",
+                "SELECT k2, k, SUM(v) FROM t WHERE v > 0 GROUP BY k2, k"]:
+        q = parse(sql + f" OPTION(numGroupsLimit={limit})")
+        g, o = gpu_engine.execute(t, q), oracle_engine.execute(t, q)
+        assert_same_result(g, o, table=t)
+        assert len(g.rows) <= 3 * limit
+
+
+def test_order_by_trim_on_device(gpu_engine, oracle_engine, sv_table_inter):
+    """ORDER BY ... LIMIT applied on the device (TableResizer.getTopRecords): the kept candidates (boundary ties
+    included) give the reference's top rows."""
+    for sql in ["SELECT column9, SUM(column1) FROM t GROUP BY column9 ORDER BY SUM(column1) DESC, column9 LIMIT 7",
+                "SELECT column11, column12, AVG(column3), COUNT(*) FROM t GROUP BY column11, column12 "
+                "ORDER BY AVG(column3), column12 DESC, column11 LIMIT 5",
+                "SELECT column12, DISTINCTCOUNT(column7) FROM t GROUP BY column12 ORDER BY DISTINCTCOUNT(column7) DESC, "
+                "column12 LIMIT 3",
+                "SELECT column1, column6, COUNT(*) FROM t GROUP BY column1, column6 ORDER BY COUNT(*) DESC, column1, "
+                "column6 LIMIT 10"]:
+        q = parse(sql)
+        g = gpu_engine.execute(sv_table_inter, q, trim=True)
+        o = oracle_engine.execute(sv_table_inter, q)
+        assert reduce_to_rows(q, g)[1] == reduce_to_rows(q, o)[1], sql
+        assert len(g.rows) <= len(o.rows)
+
+
+def test_config4_shape_high_cardinality_distinctcount(gpu_engine, oracle_engine):
+    """Config 4 in miniature: userId of high cardinality x itemId 1 000, DISTINCTCOUNT per user, ORDER BY DISTINCTCOUNT
+    DESC, userId LIMIT 100, numGroupsLimit above the distinct users (as the reference must be run); plus the same
+    with the default limit, which truncates per segment."""
+    from pinot_amd import synth
+    segs = [synth.make_segment_np(synth.highcard_specs(users=150_000), s, 200_003) for s in range(3)]
+    t = Table("events", segs)
+    for sql in [synth.highcard_query() + " OPTION(numGroupsLimit=10000000)",
+                synth.highcard_query().replace("LIMIT 100", "LIMIT 20") + " OPTION(numGroupsLimit=40000)"]:
+        q = parse(sql)
+        g = gpu_engine.execute(t, q, trim=True)
+        o = oracle_engine.execute(t, q)
+        assert reduce_to_rows(q, g)[1] == reduce_to_rows(q, o)[1]
+        full = gpu_engine.execute(t, q)
+        assert_same_result(full, o, table=t)
+
+
+def test_partial_rows_export_merge_roundtrip(gpu_engine, oracle_engine, sv_table_inter):
+    """pg_partials_export (rows bucketed by owner) -> pg_partials_create + pg_partials_merge of every bucket ->
+    finalize == the direct result, for a dense and a hash state."""
+    import ctypes as C
+    import torch
+    from pinot_amd import abi
+    q = parse("SELECT column11, column12, COUNT(*), SUM(column1), MIN(column3), MAX(column6), AVG(column9), "
+              "DISTINCTCOUNT(column7) FROM t GROUP BY column11, column12")
+    o = oracle_engine.execute(sv_table_inter, q)
+    for flags in (abi.PG_PLAN_VALUE_SETS, abi.PG_PLAN_VALUE_SETS | abi.PG_PLAN_HASH_GROUPS):
+        plan = gpu_engine.make_plan(sv_table_inter, q, flags=flags)
+        p = gpu_engine.run_partial(plan)
+        counts = gpu_engine.export_rows(p, 3)
+        rb = p.contents.row_bytes
+        buf = torch.empty(sum(counts) * rb, dtype=torch.uint8, device="cuda")
+        assert gpu_engine.export_rows(p, 3, C.c_void_p(buf.data_ptr()), sum(counts)) == counts
+        keys = buf.view(-1, rb)[:, :8].contiguous().view(torch.int64).cpu().numpy().astype(np.uint64)
+        owners = [gpu_engine.lib.pg_key_owner(int(k), 3) for k in keys]
+        assert owners == sorted(owners)
+        qq = gpu_engine.create_like(p, sum(counts))
+        qq.contents.stats = p.contents.stats
+        at = 0
+        for c in counts:  # bucket by bucket, as the owners would receive them
+            gpu_engine.merge_rows(qq, C.c_void_p(buf.data_ptr() + at * rb), c)
+            at += c
+        gpu_engine.lib.pg_partials_free(p)
+        assert_same_result(gpu_engine.finalize_partial(plan, qq), o, table=sv_table_inter)
 
 
 # ------------------------------------------------------------------ synthetic segments (config 2 shape + edges)
@@ -93,7 +195,7 @@ def test_config2_shape_small(gpu_engine, oracle_engine):
     segs = [synth.make_segment_np(synth.ADANALYTICS, s, 150_001) for s in range(3)]
     t = Table("adAnalytics", segs)
     q = parse(synth.adanalytics_query(5000))
-    assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q))
+    assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q), table=t)
 
 
 def test_config3_ssb_shape_small(gpu_engine, oracle_engine):
@@ -104,7 +206,7 @@ def test_config3_ssb_shape_small(gpu_engine, oracle_engine):
     q = parse(synth.ssb_q11_query())
     g, o = gpu_engine.execute(t, q), oracle_engine.execute(t, q)
     assert g.stats.num_docs_scanned > 0
-    assert_same_result(g, o)
+    assert_same_result(g, o, table=t)
 
 
 def test_large_dictionary_dense_decode(gpu_engine, oracle_engine):
@@ -117,7 +219,7 @@ def test_large_dictionary_dense_decode(gpu_engine, oracle_engine):
                 "SELECT lo_discount, SUM(lo_extendedprice), AVG(lo_extendedprice) FROM t GROUP BY lo_discount",
                 "SELECT DISTINCTCOUNT(lo_quantity), SUM(lo_extendedprice * lo_quantity) FROM t WHERE lo_quantity > 3"]:
         q = parse(sql)
-        assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q))
+        assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q), table=t)
 
 
 def test_device_generated_segments_match_host_bytes(gpu_engine, oracle_engine):
@@ -139,7 +241,7 @@ def test_device_generated_segments_match_host_bytes(gpu_engine, oracle_engine):
     q = parse(synth.adanalytics_query(20000))
     g = gpu_engine.execute(table, q)
     o = oracle_engine.execute(table, q)
-    assert_same_result(g, o)
+    assert_same_result(g, o, table=table)
     assert g.stats.num_docs_scanned > 0
 
 
@@ -154,7 +256,7 @@ def test_ragged_sizes(n, gpu_engine, oracle_engine):
                 "SELECT a, COUNT(*), SUM(d), SUM(b), MIN(b) FROM t WHERE b BETWEEN -10 AND 500 GROUP BY a",
                 "SELECT DISTINCTCOUNT(b) FROM t WHERE a <> 1"]:
         q = parse(sql)
-        assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q))
+        assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q), table=t)
 
 
 def test_balanced_split_over_ragged_segments(gpu_engine, oracle_engine):
@@ -173,7 +275,7 @@ def test_balanced_split_over_ragged_segments(gpu_engine, oracle_engine):
                 "SELECT k, AVG(v), DISTINCTCOUNT(w) FROM t WHERE v BETWEEN -100 AND 2500 GROUP BY k"]:
         q = parse(sql)
         g, o = gpu_engine.execute(t, q), oracle_engine.execute(t, q)
-        assert_same_result(g, o)
+        assert_same_result(g, o, table=t)
         assert g.stats.num_segments_matched == o.stats.num_segments_matched
 
 
@@ -186,7 +288,7 @@ def test_empty_and_all_filtered(gpu_engine, oracle_engine):
                 "SELECT COUNT(*) FROM t WHERE a IN (11, 12) OR b = 1000"]:
         q = parse(sql)
         g, o = gpu_engine.execute(t, q), oracle_engine.execute(t, q)
-        assert_same_result(g, o)
+        assert_same_result(g, o, table=t)
         assert g.stats.num_docs_scanned == 0
 
 
@@ -205,7 +307,7 @@ def test_per_segment_dictionaries_merge_by_value(gpu_engine, oracle_engine):
                 "SELECT name, DISTINCTCOUNT(k), AVG(f), MIN(f) FROM t WHERE v < 500000 GROUP BY name",
                 "SELECT f, COUNT(*) FROM t WHERE k < 3 GROUP BY f"]:
         q = parse(sql)
-        assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q))
+        assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q), table=t)
 
 
 def test_sorted_and_inverted_and_mv(gpu_engine, oracle_engine):
@@ -228,23 +330,24 @@ def test_sorted_and_inverted_and_mv(gpu_engine, oracle_engine):
             "SELECT COUNT(*) FROM t WHERE sortedCol NOT IN (5, 6, 7) AND inv1 NOT IN (0, 1)",
         ]:
             q = parse(sql)
-            assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q))
+            assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q), table=t)
 
 
 def test_partials_roundtrip_single_rank(gpu_engine, oracle_engine, sv_table_inter):
-    """pg_execute_partial -> pg_partials_copy out/in -> pg_partials_finalize == pg_execute (1-rank merge)."""
+    """pg_execute_partial -> pg_partials_copy out/in -> pg_partials_finalize == pg_execute (1-rank dense merge)."""
     import ctypes as C
     import torch
     from pinot_amd import abi
-    q = parse("SELECT column11, COUNT(*), SUM(column1), MIN(column3), MAX(column6), DISTINCTCOUNT(column7) FROM t "
+    q = parse("SELECT column11, COUNT(*), SUM(column1), MIN(column3), MAX(column6), AVG(column7) FROM t "
               "GROUP BY column11")
     plan = gpu_engine.make_plan(sv_table_inter, q)
     p = gpu_engine.run_partial(plan)
     pc = p.contents
-    bufs = [torch.empty(max(pc.num_slots * k, 1) * sz, dtype=torch.uint8, device="cuda")
-            for k, sz in ((pc.n_i64, 8), (pc.n_f64, 8), (pc.n_min, 8), (pc.n_max, 8), (pc.flag_bytes_per_slot, 1))]
+    assert pc.mode == abi.PG_STATE_DENSE
+    bufs = [torch.empty(max(pc.num_slots * k, 1) * 8, dtype=torch.uint8, device="cuda")
+            for k in (pc.n_i64, pc.n_f64, pc.n_min, pc.n_max)]
     ptrs = [C.c_void_p(b.data_ptr()) for b in bufs]
     assert gpu_engine.lib.pg_partials_copy(p, abi.PG_COPY_OUT, *ptrs, None) == 0
     assert gpu_engine.lib.pg_partials_copy(p, abi.PG_COPY_IN, *ptrs, None) == 0
     g = gpu_engine.finalize_partial(plan, p)
-    assert_same_result(g, oracle_engine.execute(sv_table_inter, q))
+    assert_same_result(g, oracle_engine.execute(sv_table_inter, q), table=sv_table_inter)
