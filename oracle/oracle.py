@@ -128,6 +128,33 @@ class OracleEngine:
         finally:
             self.lib.orc_result_free(out)
 
+    def time_segments(self, plan: CPlan, segments: Sequence[ImmutableSegment], threads: int, seconds: float):
+        """Throughput of the per-segment operators alone (filter -> projection -> aggregation / group-by of every
+        segment, C, `threads` segments in flight as Pinot's combine worker tasks run them; the value-keyed merge is
+        excluded).  Runs the whole segment list repeatedly for at least `seconds`; returns (rows/s, runs)."""
+        cols = [self.columns(s, plan.table) for s in segments]
+        threshold = min(self.array_based_threshold, plan.plan.num_groups_limit or self.array_based_threshold)
+
+        def one(i):
+            out = C.POINTER(orc_segment_result)()
+            rc = self.lib.orc_execute_segment(C.byref(plan.plan), i, cols[i].arr, threshold, C.byref(out))
+            if rc:
+                raise RuntimeError(f"oracle failed rc={rc}")
+            self.lib.orc_result_free(out)
+
+        import time
+        rows = sum(s.num_docs for s in segments)
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(one, range(len(segments))))  # warm-up
+            runs, t0 = 0, time.perf_counter()
+            while True:
+                list(ex.map(one, range(len(segments))))
+                runs += 1
+                el = time.perf_counter() - t0
+                if el >= seconds:
+                    break
+        return runs * rows / el, runs
+
     def _to_value_rows(self, plan: CPlan, seg: ImmutableSegment, r: orc_segment_result):
         A, K, G = r.num_aggs, r.num_keys, r.num_groups
         aggs = plan.aggs

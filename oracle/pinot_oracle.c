@@ -452,6 +452,25 @@ static int32_t map_get_or_put(id_map *m, uint64_t key, uint64_t limit) {
   return (int32_t)m->n++;
 }
 
+/* LSD radix sort of u64 keys (8 passes of 8 bits) + in-place unique; returns the unique count. */
+static uint64_t sort_unique_u64(uint64_t *a, uint64_t n) {
+  uint64_t *tmp = (uint64_t *)malloc(sizeof(uint64_t) * (n ? n : 1));
+  for (int pass = 0; pass < 8; pass++) {
+    uint64_t cnt[257] = {0};
+    int sh = pass * 8;
+    for (uint64_t i = 0; i < n; i++) cnt[((a[i] >> sh) & 255) + 1]++;
+    if (cnt[1] == n) continue; /* every key has this digit = 0 */
+    for (int d = 0; d < 256; d++) cnt[d + 1] += cnt[d];
+    for (uint64_t i = 0; i < n; i++) tmp[cnt[(a[i] >> sh) & 255]++] = a[i];
+    memcpy(a, tmp, sizeof(uint64_t) * n);
+  }
+  free(tmp);
+  uint64_t u = 0;
+  for (uint64_t i = 0; i < n; i++)
+    if (u == 0 || a[u - 1] != a[i]) a[u++] = a[i];
+  return u;
+}
+
 static void aggregate_group_by(const pg_plan *plan, const orc_column *cols, const uint32_t *docs, uint64_t n,
                                agg_input *inputs, int32_t **key_ids, orc_segment_result *r,
                                uint64_t array_based_threshold) {
@@ -491,15 +510,16 @@ static void aggregate_group_by(const pg_plan *plan, const orc_column *cols, cons
 
   double *vals = (double *)calloc((G ? G : 1) * (A ? A : 1), sizeof(double));
   int64_t *cnts = (int64_t *)calloc((G ? G : 1) * (A ? A : 1), sizeof(int64_t));
-  uint8_t *dflags = NULL;
-  uint64_t dcard = 0;
+  /* DISTINCTCOUNT: the per-group RoaringBitmap of dictIds (DistinctCountAggregationFunction.aggregateGroupBySV,
+   * function/DistinctCountAggregationFunction.java:131-190) as sorted unique (group * A + agg, dictId) pairs */
+  uint32_t n_dc = 0;
   for (uint32_t a = 0; a < A; a++) {
     if (plan->aggs[a].fn == PG_AGG_MIN) for (uint64_t g = 0; g < G; g++) vals[g * A + a] = INFINITY;
     if (plan->aggs[a].fn == PG_AGG_MAX) for (uint64_t g = 0; g < G; g++) vals[g * A + a] = -INFINITY;
-    if (plan->aggs[a].fn == PG_AGG_DISTINCTCOUNT && cols[plan->aggs[a].col_a].cardinality > dcard)
-      dcard = cols[plan->aggs[a].col_a].cardinality;
+    n_dc += plan->aggs[a].fn == PG_AGG_DISTINCTCOUNT;
   }
-  if (dcard) dflags = (uint8_t *)calloc((G ? G : 1) * A * dcard, 1);
+  uint64_t *pairs = n_dc ? (uint64_t *)malloc(sizeof(uint64_t) * (n ? n : 1) * n_dc) : NULL;
+  uint64_t np = 0;
   /* aggregateGroupBySV: holder[groupId] op= value for each doc (e.g. SumAggregationFunction.java:205-237) */
   for (uint64_t i = 0; i < n; i++) {
     int32_t g = gids[i];
@@ -515,51 +535,48 @@ static void aggregate_group_by(const pg_plan *plan, const orc_column *cols, cons
         case PG_AGG_AVG: *v += agg_value(ag, cols, &inputs[a], d); cnts[(uint64_t)g * A + a] += 1; break;
         case PG_AGG_MIN: { double x = agg_value(ag, cols, &inputs[a], d); if (x < *v) *v = x; break; }
         case PG_AGG_MAX: { double x = agg_value(ag, cols, &inputs[a], d); if (x > *v) *v = x; break; }
-        case PG_AGG_DISTINCTCOUNT: dflags[((uint64_t)g * A + a) * dcard + inputs[a].ids_a[d]] = 1; break;
+        case PG_AGG_DISTINCTCOUNT:
+          pairs[np++] = (((uint64_t)g * A + a) << 32) | (uint32_t)inputs[a].ids_a[d];
+          break;
       }
     }
   }
+  np = pairs ? sort_unique_u64(pairs, np) : 0;
   /* export groups that received at least one doc */
   uint8_t *present = (uint8_t *)calloc(G ? G : 1, 1);
   for (uint64_t i = 0; i < n; i++) if (gids[i] >= 0) present[gids[i]] = 1;
   uint64_t ng = 0;
-  for (uint64_t g = 0; g < G; g++) ng += present[g];
+  uint64_t *out_row = (uint64_t *)malloc(sizeof(uint64_t) * (G ? G : 1));
+  for (uint64_t g = 0; g < G; g++) { out_row[g] = ng; ng += present[g]; }
   r->num_groups = ng;
   r->key_dict_ids = (int32_t *)malloc(sizeof(int32_t) * (ng ? ng : 1) * (K ? K : 1));
   r->values = (double *)malloc(sizeof(double) * (ng ? ng : 1) * (A ? A : 1));
   r->counts = (int64_t *)malloc(sizeof(int64_t) * (ng ? ng : 1) * (A ? A : 1));
-  uint64_t nd = 0;
-  if (dflags)
-    for (uint64_t g = 0; g < G; g++)
-      if (present[g])
-        for (uint32_t a = 0; a < A; a++)
-          if (plan->aggs[a].fn == PG_AGG_DISTINCTCOUNT)
-            for (uint64_t x = 0; x < dcard; x++) nd += dflags[((uint64_t)g * A + a) * dcard + x];
-  r->num_distinct = nd;
-  r->distinct_group_agg = (uint64_t *)malloc(sizeof(uint64_t) * (nd ? nd : 1));
-  r->distinct_dict_ids = (int32_t *)malloc(sizeof(int32_t) * (nd ? nd : 1));
-  uint64_t o = 0, di = 0;
+  r->num_distinct = np;
+  r->distinct_group_agg = (uint64_t *)malloc(sizeof(uint64_t) * (np ? np : 1));
+  r->distinct_dict_ids = (int32_t *)malloc(sizeof(int32_t) * (np ? np : 1));
+  uint64_t o = 0;
   for (uint64_t g = 0; g < G; g++) {
     if (!present[g]) continue;
     uint64_t raw = raw_of_gid[g];
     for (uint32_t k = 0; k < K; k++) { r->key_dict_ids[o * K + k] = (int32_t)(raw % cards[k]); raw /= cards[k]; }
     for (uint32_t a = 0; a < A; a++) {
-      r->values[o * A + a] = vals[g * A + a];
+      r->values[o * A + a] = plan->aggs[a].fn == PG_AGG_DISTINCTCOUNT ? 0.0 : vals[g * A + a];
       r->counts[o * A + a] = cnts[g * A + a];
-      if (plan->aggs[a].fn == PG_AGG_DISTINCTCOUNT) {
-        uint32_t cnt = 0;
-        for (uint64_t x = 0; x < dcard; x++)
-          if (dflags[(g * A + a) * dcard + x]) {
-            r->distinct_group_agg[di] = o * A + a;
-            r->distinct_dict_ids[di++] = (int32_t)x;
-            cnt++;
-          }
-        r->values[o * A + a] = (double)cnt;
-      }
     }
     o++;
   }
-  free(present); free(vals); free(cnts); free(dflags); free(gids); free(raw_of_gid); free(seen);
+  /* pairs are sorted by (group, agg): renumber groups to output rows and count the set sizes */
+  for (uint64_t i = 0; i < np; i++) {
+    const uint64_t ga = pairs[i] >> 32, g = ga / A, a = ga % A;
+    const uint64_t row = out_row[g] * A + a;
+    r->distinct_group_agg[i] = row;
+    r->distinct_dict_ids[i] = (int32_t)(uint32_t)pairs[i];
+    r->values[row] += 1.0;
+  }
+  free(pairs);
+  free(out_row);
+  free(present); free(vals); free(cnts); free(gids); free(raw_of_gid); free(seen);
   if (!array_based) { free(m.keys); free(m.ids); }
 }
 
