@@ -63,7 +63,9 @@ int pg_init(int device);
 int pg_last_error(char *buf, size_t n);
 /* Bytes of device memory held by resident segments. */
 int pg_resident_bytes(uint64_t *out);
-/* Request cancellation of an in-flight pg_execute carrying this query_id (checked between launches). */
+/* Cancel every pg_execute* carrying this query_id: one not yet launched fails before its launch, a running scan
+ * stops at its next tile of 8 192 docs (a host-coherent flag the kernel polls), both with PG_E_CANCELLED.  A
+ * plan's deadline_ms is enforced the same way (PG_E_TIMEOUT).  Callable from any thread. */
 int pg_cancel(uint64_t query_id);
 /* Library ABI version (PG_ABI_VERSION). */
 int pg_abi_version(void);

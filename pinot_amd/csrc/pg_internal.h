@@ -190,6 +190,7 @@ struct QuerySpec {
   const WorkItem* items;     // [item]
   unsigned long long* seg_matched;  // [seg]
   unsigned int* err;                // device-side violations: bit 0 group key, bit 1 DISTINCTCOUNT key, bit 2 hash table full
+  const unsigned int* cancel;       // host-mapped flag polled once per tile (nonzero: stop); null = not cancellable
 };
 
 // order-preserving int64 image of a double (for MIN/MAX slots)

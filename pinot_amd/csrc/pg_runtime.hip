@@ -10,6 +10,7 @@
 // but as ONE fused launch over all of the query's segments on this GPU (plus a small pre-pass for
 // index-backed leaves), with per-group state merged in device memory by global key id.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <time.h>
 
 #include <algorithm>
@@ -223,6 +224,51 @@ bool is_cancelled(uint64_t qid) {
   if (!qid) return false;
   std::lock_guard<std::mutex> g(g_cancel_mu);
   return g_cancelled.count(qid) != 0;
+}
+
+// In-flight cancellation: a slot of host-coherent pinned flags per running cancellable query (query_id or deadline),
+// polled by the scan kernel once per tile.  pg_cancel sets 1 (-> PG_E_CANCELLED); the executing thread sets 2 when the
+// deadline passes while it waits (-> PG_E_TIMEOUT).  Mirrors BaseOperator.nextBlock's interrupt check
+// (operator/BaseOperator.java:35-37) and the QueryContext deadline, at tile granularity inside the one launch.
+constexpr uint32_t kCancelSlots = 256;
+volatile uint32_t* g_flags = nullptr;        // [kCancelSlots], hipHostMalloc coherent + mapped
+std::vector<uint32_t> g_free_slots;           // under g_cancel_mu
+std::unordered_multimap<uint64_t, uint32_t> g_inflight;  // query_id -> slot, under g_cancel_mu
+
+struct CancelSlot {
+  int slot = -1;
+  uint64_t qid = 0;
+  CancelSlot(uint64_t q, bool want) : qid(q) {
+    if (!want || !g_flags) return;
+    std::lock_guard<std::mutex> g(g_cancel_mu);
+    if (g_free_slots.empty()) return;  // every slot busy: this query is only checked before launch
+    slot = (int)g_free_slots.back();
+    g_free_slots.pop_back();
+    g_flags[slot] = g_cancelled.count(qid) ? 1u : 0u;
+    if (qid) g_inflight.emplace(qid, (uint32_t)slot);
+  }
+  ~CancelSlot() {
+    if (slot < 0) return;
+    std::lock_guard<std::mutex> g(g_cancel_mu);
+    auto r = g_inflight.equal_range(qid);
+    for (auto it = r.first; it != r.second; ++it)
+      if (it->second == (uint32_t)slot) { g_inflight.erase(it); break; }
+    g_free_slots.push_back((uint32_t)slot);
+  }
+  const unsigned int* device_ptr() const { return slot < 0 ? nullptr : (const unsigned int*)(g_flags + slot); }
+  uint32_t state() const { return slot < 0 ? 0u : g_flags[slot]; }
+  void set(uint32_t v) { if (slot >= 0 && g_flags[slot] == 0) g_flags[slot] = v; }
+};
+
+int init_cancel_flags() {  // under g_init_mu
+  if (g_flags) return PG_OK;
+  void* p = nullptr;
+  HIP_CHECK(hipHostMalloc(&p, kCancelSlots * 4, hipHostMallocMapped | hipHostMallocCoherent));
+  memset(p, 0, kCancelSlots * 4);
+  std::lock_guard<std::mutex> g(g_cancel_mu);
+  for (uint32_t i = 0; i < kCancelSlots; i++) g_free_slots.push_back(kCancelSlots - 1 - i);
+  g_flags = (volatile uint32_t*)p;
+  return PG_OK;
 }
 
 inline uint32_t rd_be32(const uint8_t* p) {
@@ -1670,6 +1716,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   HIP_CHECK(hipEventRecord(ev[1], s));
   if (is_cancelled(plan->query_id)) { (void)hipStreamSynchronize(s); return fail(PG_E_CANCELLED, "query %llu cancelled", (unsigned long long)plan->query_id); }
   if (plan->deadline_ms && now_ms() > plan->deadline_ms) { (void)hipStreamSynchronize(s); return fail(PG_E_TIMEOUT, "deadline passed"); }
+  CancelSlot cancel(plan->query_id, plan->query_id != 0 || plan->deadline_ms != 0);
+  q.cancel = cancel.device_ptr();
   if (q.num_items) {
     t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
     HIP_CHECK(launch_scan(q, blocks, s));
@@ -1679,7 +1727,18 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   uint64_t* sm = (uint64_t*)t_ctx.readback.get(8ull * n_sm);
   if (!sm) return fail(PG_E_NOMEM, "pinned readback of %llu bytes failed", (unsigned long long)(8ull * n_sm));
   HIP_CHECK(hipMemcpyAsync(sm, P.seg_matched.p, 8ull * n_sm, hipMemcpyDeviceToHost, s));
+  if (plan->deadline_ms && q.cancel) {  // wait, turning a passed deadline into the kernel's stop flag
+    for (;;) {
+      const hipError_t e = hipStreamQuery(s);
+      if (e == hipSuccess) break;
+      if (e != hipErrorNotReady) HIP_CHECK(e);
+      if (now_ms() > plan->deadline_ms) cancel.set(2);
+      sched_yield();
+    }
+  }
   HIP_CHECK(hipStreamSynchronize(s));
+  if (cancel.state() == 1) return fail(PG_E_CANCELLED, "query %llu cancelled", (unsigned long long)plan->query_id);
+  if (cancel.state() == 2) return fail(PG_E_TIMEOUT, "deadline passed during the scan");
   float pre_ms = 0, scan_ms = 0;
   (void)hipEventElapsedTime(&pre_ms, ev[0], ev[1]);
   (void)hipEventElapsedTime(&scan_ms, ev[1], ev[2]);
@@ -1951,7 +2010,7 @@ int pg_init(int device) {
   HIP_CHECK(hipSetDevice(device));
   g_device = device;
   init_grid_caps();
-  return PG_OK;
+  return init_cancel_flags();
 }
 
 int pg_last_error(char* buf, size_t n) {
@@ -1977,6 +2036,8 @@ int pg_resident_bytes(uint64_t* out) {
 int pg_cancel(uint64_t query_id) {
   std::lock_guard<std::mutex> g(g_cancel_mu);
   g_cancelled.insert(query_id);
+  auto r = g_inflight.equal_range(query_id);
+  for (auto it = r.first; it != r.second; ++it) g_flags[it->second] = 1u;  // running launches stop at their next tile
   return PG_OK;
 }
 

@@ -772,6 +772,13 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
   uint32_t* queue = (uint32_t*)(smem + scan_queue_off(q));
   uint32_t* scan_tmp = queue + kQueueCap;
   uint32_t qn = 0;  // queued docs (block-uniform)
+  // cooperative cancellation (pg_cancel / deadline): thread 0 loads the query's host-visible flag during a tile and
+  // publishes it in LDS before the next tile's barrier; every wave reads the word of that tile's parity after the
+  // barrier, so the whole block leaves the loop at the same tile (the words live in the pad before the ring, whose
+  // st[-1] bits are always masked off)
+  volatile unsigned int* stop = (volatile unsigned int*)smem;
+  uint32_t iter = 0, pending = 0;
+  bool cancelled = false;
 
   if (i0 < i1) {
     const bool ring2 = q.stage_ring > 1;
@@ -811,7 +818,16 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
         if (has_next) { n_it = ldc(q.items, n_item); n_tile = n_it.tile_begin; n_seg = n_it.seg; }
       }
       __builtin_amdgcn_s_waitcnt(0);  // this wave's copies of the current tile have landed
+      if (q.cancel && tid == 0) stop[iter & 1u] = pending;
       __syncthreads();                // ... and every wave's; every wave is done with the other buffer
+      if (q.cancel) {
+        if (stop[iter & 1u]) {
+          cancelled = true;
+          break;
+        }
+        if (tid == 0) pending = __hip_atomic_load(q.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      iter++;
       if (it.seg != cur_seg) {
         if (cur_seg != 0xFFFFFFFFu) {
           if (qn) flush();  // the queue holds docs of the previous segment
@@ -896,7 +912,7 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
       tile = n_tile;
       if (ring2) buf ^= 1u;
     }
-    if (qn) flush();
+    if (qn && !cancelled) flush();
     const uint64_t c = wave_sum_u64(seg_count);
     if (lane == 0 && c) atomicAdd(&q.seg_matched[cur_seg], (unsigned long long)c);
   }

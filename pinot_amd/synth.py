@@ -80,6 +80,54 @@ def highcard_query(limit: int = 100) -> str:
             f"ORDER BY DISTINCTCOUNT(itemId) DESC, userId LIMIT {limit}")
 
 
+# Config 1: pinot-tools QuickStart baseballStats (CPU-reference scale).  The data CSV is not in the reference checkout
+# (.MISSING_LARGE_BLOBS), so rows follow the schema (pinot-tools/.../baseballStats/baseballStats_schema.json: 5 STRING /
+# INT dimensions, 20 INT metrics) with plausible ranges; inverted indexes on playerID and teamID as its table config.
+BASEBALL_METRICS = ["playerStint", "numberOfGames", "numberOfGamesAsBatter", "AtBatting", "runs", "hits", "doules",
+                    "tripples", "homeRuns", "runsBattedIn", "stolenBases", "caughtStealing", "baseOnBalls", "strikeouts",
+                    "intentionalWalks", "hitsByPitch", "sacrificeHits", "sacrificeFlies", "groundedIntoDoublePlays",
+                    "G_old"]
+
+
+def baseball_segment(rows: int = 97_889, players: int = 18_000, seed: int = SEED) -> ImmutableSegment:
+    rng = np.random.default_rng(seed)
+    pid = rng.integers(0, players, rows)
+    first = np.array(["John", "Bill", "Joe", "Jim", "Frank", "George", "Tom", "Charlie", "Ed", "Harry", "Mike",
+                      "Bob", "Dave", "Fred", "Jack", "Al", "Pete", "Sam", "Walter", "Lou"], dtype=object)
+    last = np.array([f"Player{i:05d}" for i in range(players // 3)], dtype=object)
+    # names collide across players (different playerIDs, one playerName), as in the real table
+    names = np.array([f"{first[i % len(first)]} {last[(i * 7919) % len(last)]}" for i in range(players)], dtype=object)
+    teams = np.array([f"T{i:03d}" for i in range(149)], dtype=object)
+    data = {"playerID": np.array([f"p{i:06d}" for i in range(players)], dtype=object)[pid],
+            "playerName": names[pid],
+            "yearID": rng.integers(1871, 2014, rows),
+            "teamID": teams[rng.integers(0, len(teams), rows)],
+            "league": np.array(["AL", "NL", "AA", "UA", "FL", "PL"], dtype=object)[rng.integers(0, 6, rows)]}
+    hi = {"playerStint": 5, "numberOfGames": 165, "numberOfGamesAsBatter": 165, "AtBatting": 716, "runs": 192,
+          "hits": 262, "doules": 67, "tripples": 36, "homeRuns": 73, "runsBattedIn": 191, "stolenBases": 138,
+          "caughtStealing": 42, "baseOnBalls": 232, "strikeouts": 223, "intentionalWalks": 120, "hitsByPitch": 51,
+          "sacrificeHits": 67, "sacrificeFlies": 19, "groundedIntoDoublePlays": 36, "G_old": 165}
+    for m in BASEBALL_METRICS:
+        data[m] = (rng.integers(0, hi[m] + 1, rows) * rng.random(rows) ** 2).astype(np.int64)
+    schema = {"playerID": "STRING", "playerName": "STRING", "yearID": "INT", "teamID": "STRING", "league": "STRING"}
+    schema.update({m: "INT" for m in BASEBALL_METRICS})
+    return ImmutableSegment.create("baseballStats_OFFLINE_0", data, schema, inverted=["playerID", "teamID"])
+
+
+# pinot-tools Quickstart.java:185-213 queries, LIMIT 10 with playerName as the tie-break of equal sums
+BASEBALL_QUERIES = [
+    "SELECT COUNT(*) FROM baseballStats",
+    "SELECT playerName, SUM(runs) FROM baseballStats GROUP BY playerName ORDER BY SUM(runs) DESC, playerName LIMIT 10",
+    "SELECT playerName, SUM(runs) FROM baseballStats WHERE yearID = 2000 GROUP BY playerName "
+    "ORDER BY SUM(runs) DESC, playerName LIMIT 10",
+    "SELECT playerName, SUM(runs) FROM baseballStats WHERE yearID >= 2000 GROUP BY playerName "
+    "ORDER BY SUM(runs) DESC, playerName LIMIT 10",
+    "SELECT teamID, COUNT(*), SUM(homeRuns), MAX(hits), AVG(runs) FROM baseballStats WHERE teamID IN ('T001', 'T017', "
+    "'T100') OR league = 'NL' GROUP BY teamID ORDER BY SUM(homeRuns) DESC, teamID LIMIT 10",
+    "SELECT league, DISTINCTCOUNT(playerID), SUM(runs) FROM baseballStats WHERE playerID <> 'p000007' GROUP BY league",
+]
+
+
 def column_salt(name: str) -> int:
     return (zlib.crc32(name.encode()) ^ (SEED * 0x9E3779B1)) & M32
 

@@ -351,3 +351,24 @@ def test_partials_roundtrip_single_rank(gpu_engine, oracle_engine, sv_table_inte
     assert gpu_engine.lib.pg_partials_copy(p, abi.PG_COPY_IN, *ptrs, None) == 0
     g = gpu_engine.finalize_partial(plan, p)
     assert_same_result(g, oracle_engine.execute(sv_table_inter, q), table=sv_table_inter)
+
+
+# ------------------------------------------------------------------ config 1: QuickStart baseballStats
+
+@pytest.fixture(scope="module")
+def baseball_table():
+    from pinot_amd import synth
+    return Table("baseballStats", [synth.baseball_segment()])
+
+
+@pytest.mark.parametrize("qi", range(6))
+def test_config1_baseball_quickstart(qi, gpu_engine, oracle_engine, baseball_table):
+    """BASELINE config 1: Quickstart.java:185-213's baseballStats queries (STRING playerName group key through a
+    keymap, inverted-index leaves on playerID / teamID) -- device vs oracle, plain and with the device ORDER BY trim."""
+    from pinot_amd import synth
+    q = parse(synth.BASEBALL_QUERIES[qi])
+    o = oracle_engine.execute(baseball_table, q)
+    g = gpu_engine.execute(baseball_table, q)
+    assert_same_result(g, o, table=baseball_table)
+    t = gpu_engine.execute(baseball_table, q, trim=True)
+    assert reduce_to_rows(q, t)[1] == reduce_to_rows(q, o)[1]

@@ -1,0 +1,113 @@
+"""Runtime behaviour of the C ABI on an MI355X: in-flight cancellation and deadlines (BaseOperator.nextBlock's
+interrupt check, QueryContext.getEndTimeMs), and re-entrancy (several host threads issuing pg_execute at once, as
+Pinot's combine worker threads and concurrent queries do)."""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from helpers import assert_same_result
+from pinot_amd.gpu import PinotGpuError
+from pinot_amd.plan import Table
+from pinot_amd.query import parse
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def long_scan(gpu_engine):
+    """~200 M rows of config-4 shape (random-atomic group-by: a scan of tens of ms)."""
+    import torch
+    from pinot_amd import synth
+    from pinot_amd.segment import ImmutableSegment
+    segs = []
+    table = None
+    for s in range(24):
+        dcs = synth.make_columns_torch(synth.HIGHCARD, s, 8_000_000, torch.device("cuda"))
+        seg = ImmutableSegment(f"ev{s}", 8_000_000, {dc.spec.name: dc.meta_column() for dc in dcs})
+        if table is None:
+            table = Table("events", [seg])
+        gpu_engine.register_device_segment(seg, table, dcs)
+        segs.append(seg)
+    table = Table("events", segs)
+    from pinot_amd import synth as sy
+    plan = gpu_engine.make_plan(table, parse(sy.highcard_query() + " OPTION(numGroupsLimit=10000000)"), flags=0,
+                                trim=True)
+    gpu_engine.run_plan(plan)
+    t0 = time.perf_counter()
+    ref = gpu_engine.run_plan(plan)
+    full = time.perf_counter() - t0
+    return plan, ref, full
+
+
+def _now_ms():
+    return int(time.clock_gettime(time.CLOCK_MONOTONIC) * 1000)
+
+
+def test_deadline_stops_running_scan(gpu_engine, long_scan):
+    from pinot_amd import abi
+    plan, ref, full = long_scan
+    assert full > 0.01, full
+    plan.plan.deadline_ms = _now_ms() + max(2, int(full * 1000 / 8))
+    t0 = time.perf_counter()
+    with pytest.raises(PinotGpuError) as e:
+        gpu_engine.run_plan(plan)
+    el = time.perf_counter() - t0
+    plan.plan.deadline_ms = 0
+    assert e.value.code == abi.PG_E_TIMEOUT
+    assert el < 0.7 * full, (el, full)
+    assert gpu_engine.run_plan(plan).rows == ref.rows  # the library is intact afterwards
+
+
+def test_cancel_from_another_thread(gpu_engine, long_scan):
+    from pinot_amd import abi
+    plan, ref, full = long_scan
+    plan.plan.query_id = 4242
+    out = {}
+
+    def run():
+        t0 = time.perf_counter()
+        try:
+            out["res"] = gpu_engine.run_plan(plan)
+        except PinotGpuError as ex:
+            out["err"] = ex.code
+        out["el"] = time.perf_counter() - t0
+
+    th = threading.Thread(target=run)
+    th.start()
+    time.sleep(full / 6)
+    assert gpu_engine.lib.pg_cancel(4242) == 0
+    th.join()
+    assert out.get("err") == abi.PG_E_CANCELLED, out
+    assert out["el"] < 0.8 * full, (out["el"], full)
+    plan.plan.query_id = 4243  # a fresh id runs to completion
+    assert gpu_engine.run_plan(plan).rows == ref.rows
+    plan.plan.query_id = 0
+
+
+def test_concurrent_executes_from_two_threads(gpu_engine, oracle_engine, sv_table_inter):
+    """Two host threads, each with its own stream and parameter arena, run different queries at once; every result
+    matches the oracle."""
+    queries = ["SELECT column11, COUNT(*), SUM(column1), MAX(column3) FROM t GROUP BY column11",
+               "SELECT COUNT(*), SUM(column7), MIN(column6) FROM t WHERE column6 < 500000000",
+               "SELECT column9, DISTINCTCOUNT(column7) FROM t WHERE column3 > 1000000000 GROUP BY column9",
+               "SELECT column12, AVG(column17) FROM t WHERE column11 NOT IN ('t', 'P') GROUP BY column12"]
+    expect = {sql: oracle_engine.execute(sv_table_inter, parse(sql)) for sql in queries}
+    plans = {sql: gpu_engine.make_plan(sv_table_inter, parse(sql)) for sql in queries}
+    errors = []
+
+    def worker(k):
+        try:
+            for i in range(12):
+                sql = queries[(i + k) % len(queries)]
+                assert_same_result(gpu_engine.run_plan(plans[sql]), expect[sql], table=sv_table_inter)
+        except Exception as ex:  # surfaced in the main thread
+            errors.append(repr(ex))
+
+    ths = [threading.Thread(target=worker, args=(k,)) for k in range(2)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errors, errors

@@ -92,3 +92,20 @@ def test_ssb_synthetic_oracle_matches_numpy():
     r = OracleEngine(threads=1).execute(Table("lineorder", [seg]), parse(synth.ssb_q11_query()))
     assert r.stats.num_docs_scanned == int(m.sum())
     assert r.rows[()][0] == want
+
+
+def test_baseball_oracle_matches_pandas():
+    """Config 1 (synthetic baseballStats): the oracle's top-10 run scorers equal a pandas evaluation of the query."""
+    import pandas as pd
+    from oracle.oracle import OracleEngine
+    from pinot_amd import synth
+    from pinot_amd.plan import Table, reduce_to_rows
+    seg = synth.baseball_segment(rows=20_011)
+    df = pd.DataFrame({c: [seg.columns[c].dictionary.values[i] for i in seg.columns[c].dict_ids]
+                       for c in ("playerName", "runs", "yearID")})
+    for qi, sub in ((1, df), (3, df[df.yearID >= 2000])):
+        q = parse(synth.BASEBALL_QUERIES[qi])
+        rows = reduce_to_rows(q, OracleEngine().execute(Table("baseballStats", [seg]), q))[1]
+        s = sub.groupby("playerName")["runs"].sum().reset_index()
+        s = s.sort_values(["runs", "playerName"], ascending=[False, True]).head(10)
+        assert rows == [[n, float(r)] for n, r in zip(s.playerName, s.runs)]
