@@ -15,9 +15,10 @@ query over all of this GPU's segments: host plan compile + filter pre-pass + fus
 finalize (+ at N > 1 the cross-GPU merge, pinot_amd.combine).  Weak scaling: every rank scans its own segments.
 `--gpus N` without a torchrun environment launches N rank processes (torch.distributed.run) before touching a GPU.
 
-`roofline`: the dominant kernel (scan_kernel): algorithmic bytes per launch (forward-index bytes of the touched columns
-+ dictionary bytes of the decoded columns) / its HIP-event duration on the stream it runs on; `traffic`
-from the rocprofv3 FETCH_SIZE / WRITE_SIZE passes of tools/profile_bench.sh (profiles/traffic_<workload>.json).
+`roofline`: the hot path's kernels (the streaming pre-filter of the selective filter leaves + the fused scan):
+algorithmic bytes per query (forward-index bytes of the touched columns + dictionary bytes of the decoded columns,
+SURVEY §8(d)) / their summed HIP-event durations on the stream they run on; `traffic` from the rocprofv3
+FETCH_SIZE / WRITE_SIZE passes of tools/profile_bench.sh (profiles/traffic_<workload>.json).
 `cpu_baseline`: the C restatement of the Pinot CPU operators (oracle/, "port") on a bounded sample of the same segments,
 at Pinot's default combine parallelism (CombineOperatorUtils.java:38-50) and at every core this process may use; rank 0
 at N = 1 only.
@@ -168,8 +169,8 @@ def main():
     for _ in range(args.warmup):
         res = step()
     scan_ms = []
-    parts = {k: [] for k in ("host_compile_ms", "prepass_ms", "scan_ms", "execute_wall_ms", "finalize_ms",
-                             "finalize_wall_ms")}
+    parts = {k: [] for k in ("host_compile_ms", "prepass_ms", "prefilter_ms", "scan_ms", "execute_wall_ms",
+                             "finalize_ms", "finalize_wall_ms")}
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -177,7 +178,7 @@ def main():
     for _ in range(args.steps):
         res = step()
         tm = eng.last_timing()
-        scan_ms.append(tm.scan_ms)
+        scan_ms.append(tm.prefilter_ms + tm.scan_ms)  # the hot path's two kernels: streaming pre-filter + fused scan
         for k, v in parts.items():
             v.append(getattr(tm, k))
     torch.cuda.synchronize()
@@ -244,7 +245,8 @@ def main():
                        "parallelism": f"segments x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "scan_kernel", "kernel_ms": scan_avg_ms, "algorithmic_bytes": alg_bytes,
+                         "kernel": "prefilter_kernel + scan_kernel", "kernel_ms": scan_avg_ms,
+                         "algorithmic_bytes": alg_bytes,
                          "traffic_bytes_per_launch": traffic_bytes},
             "cpu_baseline": cpu,
             "parity_sample": parity,

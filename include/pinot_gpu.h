@@ -341,9 +341,10 @@ uint32_t pg_key_owner(uint64_t key, uint32_t num_parts);
 /* ---------------------------------------------------------------- measurement hooks */
 
 /* Timing of the last pg_execute* / pg_partials_finalize on this thread.  Device time (ms, HIP events on the
- * execution stream): the filter-materialisation pre-pass, the fused scan/aggregate kernel, the state read-back.
- * Host wall time (ms, steady clock): plan compile up to the scan launch, the whole execute call, the finalize
- * (read-back + decode) call. */
+ * execution stream): the index pre-pass (IN-set LUTs, sorted / inverted / MV leaf bitmaps), the streaming
+ * pre-filter of the root AND's leaves, the fused scan/aggregate kernel, the finalize (group selection, ORDER BY
+ * trim, read-back).  Host wall time (ms, steady clock): plan compile up to the scan launch, the whole execute call,
+ * the finalize call. */
 typedef struct pg_timing {
   float prepass_ms;
   float scan_ms;
@@ -352,7 +353,7 @@ typedef struct pg_timing {
   float host_compile_ms;
   float execute_wall_ms;
   float finalize_wall_ms;
-  uint32_t pad;
+  float prefilter_ms;
 } pg_timing;
 int pg_last_timing(pg_timing *out);
 

@@ -101,7 +101,7 @@ class pg_partials(C.Structure):
 class pg_timing(C.Structure):
     _fields_ = [("prepass_ms", C.c_float), ("scan_ms", C.c_float), ("finalize_ms", C.c_float),
                 ("scan_launches", C.c_uint32), ("host_compile_ms", C.c_float), ("execute_wall_ms", C.c_float),
-                ("finalize_wall_ms", C.c_float), ("pad", C.c_uint32)]
+                ("finalize_wall_ms", C.c_float), ("prefilter_ms", C.c_float)]
 
 
 # every symbol declared in include/pinot_gpu.h (checked by tests/test_abi.py)

@@ -1,0 +1,180 @@
+// pg_filter.hip -- the streaming pre-filter of the segment query hot path (gfx950).
+//
+// The selective leaves of a query's root AND (ScanBasedFilterOperator leaves over bit-packed forward indexes, doc
+// ranges, index bitmaps) are evaluated here by a lean kernel into one doc bitmap per segment; the fused scan
+// (pg_scan.hip) then reads that bitmap as a 1-bit column and does projection / aggregation for the survivors only.
+// This is SVScanDocIdIterator (dociditerators/SVScanDocIdIterator.java:67-125) with AndDocIdSet's scan-children
+// order (docidsets/AndDocIdSet.java:60-150): each later leaf is tested only on docs the earlier ones accepted.
+//
+// Why a separate kernel: the fused scan carries every query shape's registers (3-4 waves/SIMD) and stages packed
+// columns through LDS-DMA, which streamed a 20-bit column at ~1.9 TB/s; this kernel holds ~60 VGPRs (8 waves/SIMD)
+// and loads each thread's 32 consecutive values straight into registers with 16-byte loads, the bit width a
+// template parameter so unpacking is static register arithmetic: 5.5-5.9 TB/s on the same column (tools/stream_probe).
+//
+// Thread t of a block takes 32-doc groups; group g of a segment = docs [32g, 32g+32) = packed words [g*b, (g+1)*b),
+// so the group's bits start word-aligned.  Output word g: bit 31-j <-> doc 32g+j (the packed 1-bit column order).
+#include <hip/hip_runtime.h>
+
+#include "pg_internal.h"
+
+namespace pg {
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+#define PG_CONST __attribute__((address_space(4)))
+
+template <class T> __device__ __forceinline__ T ldcf(const T* p, uint64_t i) {
+  const PG_CONST uint32_t* src = (const PG_CONST uint32_t*)(p + i);
+  T v;
+  uint32_t* dst = (uint32_t*)&v;
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(T) / 4); k++) dst[k] = src[k];
+  return v;
+}
+
+__device__ __forceinline__ rsrc_t rsrc_of(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// The B words of a 32-doc group into registers (buffer loads: reads past the column return 0).
+template <int B>
+__device__ __forceinline__ void load_group(rsrc_t r, uint64_t g, uint32_t (&w)[B + 1]) {
+  const uint32_t off = (uint32_t)(g * B * 4u);
+#pragma unroll
+  for (int k = 0; k + 4 <= B; k += 4) {
+    const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, off + 4u * k, 0, 0);
+    w[k] = x[0]; w[k + 1] = x[1]; w[k + 2] = x[2]; w[k + 3] = x[3];
+  }
+  constexpr int R = B & 3, K0 = B & ~3;
+  if constexpr (R == 1) {
+    w[K0] = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4u * K0, 0, 0);
+  } else if constexpr (R == 2) {
+    const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, off + 4u * K0, 0, 0);
+    w[K0] = x[0]; w[K0 + 1] = x[1];
+  } else if constexpr (R == 3) {
+    const auto x = __builtin_amdgcn_raw_buffer_load_b96(r, off + 4u * K0, 0, 0);
+    w[K0] = x[0]; w[K0 + 1] = x[1]; w[K0 + 2] = x[2];
+  }
+  w[B] = 0;
+}
+
+// value j (0..31) of the group: bits [j*B, j*B+B) of w, most significant first (FixedBitIntReader)
+template <int B>
+__device__ __forceinline__ uint32_t value_at(const uint32_t (&w)[B + 1], int j) {
+  constexpr uint32_t M = B == 32 ? 0xFFFFFFFFu : ((1u << B) - 1u);
+  const uint32_t s = (uint32_t)j * B, k = s >> 5, o = s & 31u;
+  if (o + B <= 32) return (w[k] >> (32u - o - B)) & M;
+  return __builtin_amdgcn_alignbit(w[k], w[k + 1], 64u - o - B) & M;
+}
+
+// One leaf over one group for the docs in `need`: bit j <-> doc 32g + j.
+template <int B>
+__device__ __forceinline__ uint32_t eval_group(const LeafDesc& L, const uint32_t* lds_sets, uint64_t g, uint32_t need) {
+  uint32_t w[B + 1];
+  load_group<B>(rsrc_of(L.words, L.wbytes), g, w);
+  uint32_t m = 0;
+  if (L.kind == LK_RANGE) {
+    const uint32_t lo = (uint32_t)L.lo, span = (uint32_t)(L.hi - L.lo);
+#pragma unroll
+    for (int j = 0; j < 32; j++) m |= (uint32_t)((value_at<B>(w, j) - lo) < span) << j;
+  } else if (L.kind == LK_SET_LDS) {
+    const uint32_t* bm = lds_sets + L.lds_off;
+    const uint32_t sh = L.shift;
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+      const uint32_t x = value_at<B>(w, j) >> sh;
+      m |= ((bm[x >> 5] >> (x & 31u)) & 1u) << j;
+    }
+    if (sh) {  // candidates of the coarse filter bitmap, resolved together through the exact LUT
+      uint32_t cand = m & need;
+      m = 0;
+      while (cand) {
+        const int j = __ffs(cand) - 1;
+        cand &= cand - 1u;
+        const uint32_t v = value_at<B>(w, j);
+        m |= ((L.lut[v >> 5] >> (v & 31u)) & 1u) << j;
+      }
+    }
+  } else {  // LK_SET_LUT: a global bitmap over dictIds, 8 lookups in flight at a time
+#pragma unroll
+    for (int j0 = 0; j0 < 32; j0 += 8) {
+      uint32_t lw[8];
+#pragma unroll
+      for (int r = 0; r < 8; r++) lw[r] = ((need >> (j0 + r)) & 1u) ? L.aux[value_at<B>(w, j0 + r) >> 5] : 0u;
+#pragma unroll
+      for (int r = 0; r < 8; r++) m |= ((lw[r] >> (value_at<B>(w, j0 + r) & 31u)) & 1u) << (j0 + r);
+    }
+  }
+  return m;
+}
+
+// One leaf of the root AND over the work items of the segments whose form of the leaf reads B-bit values (or a
+// doc range / constant): the first leaf writes each group's word, later ones AND into it and load their column
+// only for lanes whose word still has a doc.
+template <int B>
+__global__ __launch_bounds__(256) void prefilter_kernel(PreSpec p) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_sets[];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t i0 = (uint32_t)((uint64_t)blockIdx.x * p.num_items / gridDim.x);
+  const uint32_t i1 = (uint32_t)(((uint64_t)blockIdx.x + 1) * p.num_items / gridDim.x);
+  uint32_t cur_seg = 0xFFFFFFFFu;
+  LeafDesc L;
+  uint32_t nd = 0;
+  for (uint32_t it = i0; it < i1; it++) {
+    const WorkItem wi = ldcf(p.items, it);  // tile_begin / tile_end count 32-doc groups here
+    if (wi.seg != cur_seg) {
+      const SegDesc sd = ldcf(p.segs, wi.seg);
+      L = ldcf(sd.leaves, p.leaf);
+      nd = sd.num_docs;
+      if (L.kind == LK_SET_LDS) {
+        __syncthreads();  // every thread is done with the previous segment's set
+        for (uint32_t k = tid; k < L.set_ints; k += 256) lds_sets[L.lds_off + k] = L.aux[k];
+        __syncthreads();
+      }
+      cur_seg = wi.seg;
+    }
+    uint32_t* out = ldcf(p.out, wi.seg);
+    for (uint64_t g = wi.tile_begin + tid; g < wi.tile_end; g += 256) {
+      const uint64_t d0 = g * 32;
+      uint32_t m = d0 + 32 <= nd ? 0xFFFFFFFFu : (d0 < nd ? (0xFFFFFFFFu >> (32u - (uint32_t)(nd - d0))) : 0u);
+      if (!p.first) m &= __builtin_bitreverse32(out[g]);
+      uint32_t r = 0;
+      if (m) {
+        switch (L.kind) {
+          case LK_ALL: r = 0xFFFFFFFFu; break;
+          case LK_NONE: r = 0u; break;
+          case LK_DOCRANGE: {  // docs [lo, hi) within [d0, d0 + 32)
+            const int64_t lo = std::max<int64_t>((int64_t)L.lo - (int64_t)d0, 0);
+            const int64_t hi = std::min<int64_t>((int64_t)L.hi - (int64_t)d0, 32);
+            const uint32_t below_hi = hi >= 32 ? 0xFFFFFFFFu : (hi <= 0 ? 0u : ((1u << hi) - 1u));
+            r = lo >= 32 ? 0u : below_hi & ~((1u << lo) - 1u);
+            break;
+          }
+          default: r = eval_group<B>(L, lds_sets, g, m); break;
+        }
+        if (L.excl) r = ~r;
+      }
+      const uint32_t nm = m & r;
+      if (p.first || nm != m) out[g] = __builtin_bitreverse32(nm);
+    }
+  }
+}
+
+hipError_t launch_prefilter(const PreSpec& p, uint32_t bits, uint32_t blocks, hipStream_t s) {
+  if (!p.num_items || !blocks) return hipSuccess;
+  const size_t lds = (size_t)p.set_lds_ints * 4;
+  switch (bits) {
+#define PG_B(b) case b: hipLaunchKernelGGL(prefilter_kernel<b>, dim3(blocks), dim3(256), lds, s, p); break;
+    PG_B(1) PG_B(2) PG_B(3) PG_B(4) PG_B(5) PG_B(6) PG_B(7) PG_B(8) PG_B(9) PG_B(10) PG_B(11) PG_B(12) PG_B(13)
+    PG_B(14) PG_B(15) PG_B(16) PG_B(17) PG_B(18) PG_B(19) PG_B(20) PG_B(21) PG_B(22) PG_B(23) PG_B(24) PG_B(25)
+    PG_B(26) PG_B(27) PG_B(28) PG_B(29) PG_B(30) PG_B(31) PG_B(32)
+#undef PG_B
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace pg

@@ -241,6 +241,17 @@ struct LutJob {            // set bits ids[0..n) in lut and ids >> shift in regi
 };
 hipError_t launch_set_lut_bits(const LutJob* jobs, uint32_t njobs, hipStream_t s);
 
+// ---- streaming pre-filter (pg_filter.hip): one leaf of the root AND over the segments whose form of it reads
+// `bits`-bit values, into (first) or AND-ed into (later) one doc bitmap per segment
+constexpr uint32_t kPreItemGroups = 8192;   // 32-doc groups per pre-filter work item (262 144 docs)
+struct PreSpec {
+  uint32_t num_items, leaf, first, set_lds_ints;
+  const SegDesc* segs;
+  const WorkItem* items;          // tile_begin / tile_end in 32-doc groups
+  uint32_t* const* out;           // [seg] bitmap words, packed 1-bit column order
+};
+hipError_t launch_prefilter(const PreSpec& p, uint32_t bits, uint32_t blocks, hipStream_t s);
+
 // ---- group state (pg_groups.hip)
 struct StateView {            // the device arrays of one partial state
   uint64_t num_slots, hmask;

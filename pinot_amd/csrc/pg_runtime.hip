@@ -682,6 +682,13 @@ int build_tree(const pg_plan* plan, const std::vector<double>& leaf_pass, const 
         if (nodes[k].kind == kind) n.kids.insert(n.kids.end(), nodes[k].kids.begin(), nodes[k].kids.end());
         else n.kids.push_back(k);
       }
+      if (kind == 1) {  // AND: leaves that accept every doc at no cost (match-all, folded into the pre-filter) drop out
+        std::vector<int> keep;
+        for (int k : n.kids)
+          if (!(nodes[k].kind == 0 && nodes[k].pass >= 1.0 && nodes[k].cost <= 0.0)) keep.push_back(k);
+        if (keep.empty()) keep.push_back(n.kids[0]);
+        n.kids.swap(keep);
+      }
       // AND: cheapest-per-rejection first ~ ascending pass fraction, zero-cost leaves (doc ranges, bitmaps)
       // before column scans; OR: descending pass fraction.  Results are order independent.
       auto rank = [&](int k) {
@@ -743,7 +750,7 @@ struct ThreadCtx {  // per calling thread: staging + events, created once
   std::vector<uint8_t> arena;   // host image of the parameter arena (capacity reused across queries)
   std::vector<WorkItem> items;  // work items of the current query (capacity reused across queries)
   std::vector<WorkItem> items_perm;  // XCD-grouped order of the items (swapped with `items`)
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   int init() {
     if (ev[0]) return PG_OK;
     for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
@@ -759,10 +766,12 @@ bool pl_too_big(uint32_t ints) { return ints * 4ull > (uint64_t)kLdsSetBytes; }
 // 1.99 ms, 7 -> 1.03 / 2.01 ms.  `one_round`: one resident round (the XCD-grouped order).  PG_SCAN_BLOCKS_PER_CU
 // overrides both.
 uint64_t g_grid_caps[4] = {0, 0, 0, 0};
+uint32_t g_num_cus = 256;
 void init_grid_caps() {  // under g_init_mu (pg_init), before any query reads them
   int dev_cus = 0;
   if (hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g_device) != hipSuccess || dev_cus <= 0)
     dev_cus = 256;
+  g_num_cus = (uint32_t)dev_cus;
   const char* e = getenv("PG_SCAN_BLOCKS_PER_CU");
   for (int i = 0; i < 4; i++) {
     const bool grouped = i & 1, one_round = i & 2;
@@ -1190,10 +1199,37 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       leaf_cost[li] += w * cost;
     }
   }
+  // ---- streaming pre-filter (pg_filter.hip): the leaf children of a root AND (or a lone leaf) whose joint pass
+  // fraction is small are evaluated by lean per-bit-width kernels into one doc bitmap per segment; the fused scan
+  // then sees that bitmap as ONE 1-bit leaf and the other folded leaves as match-all.  PG_PREFILTER=0|1 overrides.
+  std::vector<uint32_t> pre_leaves;
   {
     std::vector<FNode> nodes;
     int root = -1;
     build_tree(plan, leaf_pass, leaf_cost, nodes, root);
+    if (root >= 0) {
+      const char* pf_env = getenv("PG_PREFILTER");
+      const int pf = pf_env ? atoi(pf_env) : -1;
+      std::vector<int> kids;
+      if (nodes[root].kind == 0) kids.push_back(root);
+      else if (nodes[root].kind == 1) kids = nodes[root].kids;
+      double pass = 1.0, cost = 0.0;
+      std::vector<uint32_t> cand;
+      for (int k : kids)
+        if (nodes[k].kind == 0) {
+          cand.push_back((uint32_t)nodes[k].leaf);
+          pass *= leaf_pass[nodes[k].leaf];
+          cost += leaf_cost[nodes[k].leaf];
+        }
+      if (!cand.empty() && pf != 0 && (pf == 1 || (pass <= 0.5 && cost > 0.0))) {
+        pre_leaves = cand;
+        leaf_pass[cand[0]] = pass;
+        leaf_cost[cand[0]] = 1.0 / 8;
+        for (size_t i = 1; i < cand.size(); i++) { leaf_pass[cand[i]] = 1.0; leaf_cost[cand[i]] = 0.0; }
+        nodes.clear();
+        build_tree(plan, leaf_pass, leaf_cost, nodes, root);
+      }
+    }
     std::vector<int32_t> pre;
     if (root >= 0) {
       emit_prefix(nodes, root, pre);
@@ -1228,7 +1264,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   uint64_t entries_in_filter = 0;
   // device pointers into arena / scratch are patched once those are allocated
   enum PatchTarget { PT_AUX = 0, PT_WORDS = 1, PT_LUT = 2 };
-  struct Patch { uint64_t leaf_index; uint64_t off; bool in_arena; int target; };
+  struct Patch { uint64_t leaf_index; uint64_t off; bool in_arena; int target; bool orig = false; };
   std::vector<Patch> patches;
 
   std::vector<uint32_t> seg_tiles(S, 0);
@@ -1402,6 +1438,64 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     }
   }
   P.entries_in_filter = entries_in_filter;
+
+  // ---- pre-filter launches: per folded leaf (in order), one launch per bit width its segments read (doc ranges
+  // and constants ride along as width 1); the fused scan's leaf list gets the bitmap leaf + match-all in their place,
+  // while the pre-filter reads the original descriptors (leaves_orig, patched like the others)
+  struct PreLaunch { uint32_t leaf, bits, first, n_items, set_ints; uint64_t items_off; };
+  std::vector<PreLaunch> pre_launches;
+  std::vector<LeafDesc> leaves_orig;
+  std::vector<uint64_t> pre_bitmap_off(pre_leaves.empty() ? 0 : S);
+  if (!pre_leaves.empty()) {
+    leaves_orig = leaves;
+    for (uint32_t si = 0; si < S; si++)
+      pre_bitmap_off[si] = scratch_reserve(4ull * (((uint64_t)plan->segments[si].num_docs + 31) / 32 + 2));
+    std::vector<WorkItem> pitems;
+    for (size_t k = 0; k < pre_leaves.size(); k++) {
+      const uint32_t li = pre_leaves[k];
+      std::vector<std::pair<uint32_t, uint32_t>> by_bits;  // (bits, segment)
+      for (uint32_t si = 0; si < S; si++) {
+        const LeafDesc& dl = leaves[(uint64_t)si * L + li];
+        const bool col = dl.kind == LK_RANGE || dl.kind == LK_SET_LDS || dl.kind == LK_SET_LUT;
+        by_bits.push_back({col ? dl.bits : 1u, si});
+      }
+      std::stable_sort(by_bits.begin(), by_bits.end(),
+                       [](const std::pair<uint32_t, uint32_t>& a, const std::pair<uint32_t, uint32_t>& b) { return a.first < b.first; });
+      for (size_t i = 0; i < by_bits.size();) {
+        const uint32_t b = by_bits[i].first;
+        pitems.clear();
+        uint32_t set_ints = 0;
+        for (; i < by_bits.size() && by_bits[i].first == b; i++) {
+          const uint32_t si = by_bits[i].second;
+          const LeafDesc& dl = leaves[(uint64_t)si * L + li];
+          if (dl.kind == LK_SET_LDS) set_ints = std::max(set_ints, dl.lds_off + dl.set_ints);
+          const uint32_t groups = (uint32_t)(((uint64_t)plan->segments[si].num_docs + 31) / 32);
+          for (uint32_t g0 = 0; g0 < groups; g0 += kPreItemGroups)
+            pitems.push_back({si, g0, std::min<uint32_t>(groups, g0 + kPreItemGroups), 0});
+        }
+        if (pitems.empty()) continue;
+        pre_launches.push_back({li, b, k == 0 ? 1u : 0u, (uint32_t)pitems.size(), set_ints,
+                                ar.put(pitems.data(), pitems.size() * sizeof(WorkItem))});
+      }
+    }
+    for (Patch& p : patches)
+      if (std::find(pre_leaves.begin(), pre_leaves.end(), (uint32_t)(p.leaf_index % L)) != pre_leaves.end()) p.orig = true;
+    for (uint32_t si = 0; si < S; si++)
+      for (size_t k = 0; k < pre_leaves.size(); k++) {
+        LeafDesc& dl = leaves[(uint64_t)si * L + pre_leaves[k]];
+        memset(&dl, 0, sizeof(dl));
+        if (k == 0) {
+          as_bitmap_leaf(dl, plan->segments[si].num_docs);
+          patches.push_back({(uint64_t)si * L + pre_leaves[k], pre_bitmap_off[si], false, PT_WORDS});
+        } else {
+          dl.kind = LK_ALL;
+        }
+      }
+    // the fused scan no longer reads the folded IN sets from LDS
+    bool set_lds = false;
+    for (const LeafDesc& dl : leaves) set_lds |= dl.kind == LK_SET_LDS;
+    if (!set_lds) q.set_lds_ints = 0;
+  }
   uint64_t dict_lines = 0;
   for (uint32_t si = 0; si < S; si++) {
     uint64_t seg_lines = 0;
@@ -1463,6 +1557,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   }
   q.num_items = (uint32_t)items.size();
 
+  auto is_pre = [&](uint32_t li) { return std::find(pre_leaves.begin(), pre_leaves.end(), li) != pre_leaves.end(); };
   // ---- staging policy: a packed column is staged per tile (coalesced, every byte used) when the docs the query
   // needs from it are dense enough that a gather would fetch most of its 128-byte lines anyway
   // (reach * docs-per-line >= 1); the rest are gathered per needed doc.  Greedy by reach within the LDS budget.
@@ -1483,7 +1578,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         if (dl.kind != LK_RANGE && dl.kind != LK_SET_LDS && dl.kind != LK_SET_LUT) continue;
         bmax = std::max(bmax, dl.bits);
         const pg_leaf& pl = plan->segments[si].leaves[li];
-        if (pl.kind == PG_LEAF_SV_SCAN) { scan = true; cid = pl.col_id; } else bitmap = true;
+        if (pl.kind == PG_LEAF_SV_SCAN && !is_pre(li)) { scan = true; cid = pl.col_id; } else bitmap = true;
       }
       if (!bmax || (scan && bitmap)) continue;  // mixed per-segment forms: gather
       add(0, li, 0, scan ? (1ull << 32) | cid : (2ull << 32) | li, leaf_reach[li], bmax);
@@ -1527,7 +1622,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         else
           for (uint32_t si = 0; si < S && !match; si++) {
             const pg_leaf& pl = plan->segments[si].leaves[li];
-            match = pl.kind == PG_LEAF_SV_SCAN && (uint64_t)pl.col_id == (c.key & 0xFFFFFFFFull) &&
+            match = pl.kind == PG_LEAF_SV_SCAN && !is_pre(li) && (uint64_t)pl.col_id == (c.key & 0xFFFFFFFFull) &&
                     leaves[(uint64_t)si * L + li].kind != LK_ALL && leaves[(uint64_t)si * L + li].kind != LK_NONE;
           }
         if (match && (c.key >> 32) == 2) q.leaf_slot[li] = (uint8_t)slot;
@@ -1537,7 +1632,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
           for (uint32_t si = 0; si < S; si++) {
             const pg_leaf& pl = plan->segments[si].leaves[li];
             const LeafDesc& dl = leaves[(uint64_t)si * L + li];
-            if ((dl.kind == LK_RANGE || dl.kind == LK_SET_LDS || dl.kind == LK_SET_LUT) && pl.kind != PG_LEAF_SV_SCAN)
+            if ((dl.kind == LK_RANGE || dl.kind == LK_SET_LDS || dl.kind == LK_SET_LUT) &&
+                (pl.kind != PG_LEAF_SV_SCAN || is_pre(li)))
               all_col = false;
           }
           if (all_col) q.leaf_slot[li] = (uint8_t)slot;
@@ -1625,6 +1721,10 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   const uint64_t off_aggcols = ar.reserve(aggcols.size() * sizeof(ColDesc));
   const uint64_t off_keycols = ar.reserve(keycols.size() * sizeof(ColDesc));
   const uint64_t off_segs = ar.reserve(segd.size() * sizeof(SegDesc));
+  // the pre-filter's view: the original (unfolded) leaves, their segment table, its output bitmaps
+  const uint64_t off_leaves_orig = ar.reserve(leaves_orig.size() * sizeof(LeafDesc));
+  const uint64_t off_segs_pre = ar.reserve(pre_leaves.empty() ? 0 : segd.size() * sizeof(SegDesc));
+  const uint64_t off_pre_out = ar.reserve(pre_leaves.empty() ? 0 : 8ull * S);
   uint32_t blocks = 0;
   if (!items.empty()) {
     blocks = grid;
@@ -1663,7 +1763,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   uint8_t* dA = (uint8_t*)arena.p;
   uint8_t* dS = (uint8_t*)scratch.p;
   for (const Patch& p : patches) {
-    LeafDesc& dl = leaves[p.leaf_index];
+    LeafDesc& dl = (p.orig ? leaves_orig : leaves)[p.leaf_index];
     const uint32_t* ptr = (const uint32_t*)((p.in_arena ? dA : dS) + p.off);
     if (p.target == PT_WORDS) dl.words = ptr;
     else if (p.target == PT_LUT) dl.lut = ptr;
@@ -1684,6 +1784,17 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   if (!keycols.empty()) memcpy(&ar.h[off_keycols], keycols.data(), keycols.size() * sizeof(ColDesc));
   if (!segd.empty()) memcpy(&ar.h[off_segs], segd.data(), segd.size() * sizeof(SegDesc));
   if (!lutjobs.empty()) memcpy(&ar.h[off_lutjobs], lutjobs.data(), lutjobs.size() * sizeof(LutJob));
+  if (!pre_leaves.empty()) {
+    memcpy(&ar.h[off_leaves_orig], leaves_orig.data(), leaves_orig.size() * sizeof(LeafDesc));
+    std::vector<SegDesc> segp(segd);
+    std::vector<uint32_t*> outs(S);
+    for (uint32_t si = 0; si < S; si++) {
+      segp[si].leaves = (const LeafDesc*)(dA + off_leaves_orig) + (uint64_t)si * L;
+      outs[si] = (uint32_t*)(dS + pre_bitmap_off[si]);
+    }
+    memcpy(&ar.h[off_segs_pre], segp.data(), segp.size() * sizeof(SegDesc));
+    memcpy(&ar.h[off_pre_out], outs.data(), outs.size() * 8);
+  }
   q.segs = (const SegDesc*)(dA + off_segs);
   q.items = (const WorkItem*)(dA + off_items);
 
@@ -1713,6 +1824,19 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         break;
     }
   }
+  HIP_CHECK(hipEventRecord(ev[4], s));
+  for (const PreLaunch& pl : pre_launches) {
+    PreSpec ps;
+    memset(&ps, 0, sizeof(ps));
+    ps.num_items = pl.n_items;
+    ps.leaf = pl.leaf;
+    ps.first = pl.first;
+    ps.set_lds_ints = pl.set_ints;
+    ps.segs = (const SegDesc*)(dA + off_segs_pre);
+    ps.items = (const WorkItem*)(dA + pl.items_off);
+    ps.out = (uint32_t* const*)(dA + off_pre_out);
+    HIP_CHECK(launch_prefilter(ps, pl.bits, (uint32_t)std::min<uint64_t>(pl.n_items, (uint64_t)g_num_cus * 8), s));
+  }
   HIP_CHECK(hipEventRecord(ev[1], s));
   if (is_cancelled(plan->query_id)) { (void)hipStreamSynchronize(s); return fail(PG_E_CANCELLED, "query %llu cancelled", (unsigned long long)plan->query_id); }
   if (plan->deadline_ms && now_ms() > plan->deadline_ms) { (void)hipStreamSynchronize(s); return fail(PG_E_TIMEOUT, "deadline passed"); }
@@ -1739,10 +1863,12 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   HIP_CHECK(hipStreamSynchronize(s));
   if (cancel.state() == 1) return fail(PG_E_CANCELLED, "query %llu cancelled", (unsigned long long)plan->query_id);
   if (cancel.state() == 2) return fail(PG_E_TIMEOUT, "deadline passed during the scan");
-  float pre_ms = 0, scan_ms = 0;
-  (void)hipEventElapsedTime(&pre_ms, ev[0], ev[1]);
+  float pre_ms = 0, filt_ms = 0, scan_ms = 0;
+  (void)hipEventElapsedTime(&pre_ms, ev[0], ev[4]);
+  (void)hipEventElapsedTime(&filt_ms, ev[4], ev[1]);
   (void)hipEventElapsedTime(&scan_ms, ev[1], ev[2]);
   t_timing.prepass_ms = pre_ms;
+  t_timing.prefilter_ms = filt_ms;
   t_timing.scan_ms = scan_ms;
   t_timing.scan_launches = blocks ? 1 : 0;
   memset(&stats, 0, sizeof(stats));

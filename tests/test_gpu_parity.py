@@ -76,6 +76,20 @@ def test_sv_queries_match_oracle(sql, gpu_engine, oracle_engine, sv_table_inter)
     assert_same_result(g, o, table=sv_table_inter)
 
 
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_streaming_prefilter_on_and_off(mode, monkeypatch, gpu_engine, oracle_engine, sv_table_inter):
+    """The same filters with the root AND's leaves folded into the streaming pre-filter (pg_filter.hip, forced on)
+    and evaluated by the fused scan alone (off): identical results and scan statistics."""
+    monkeypatch.setenv("PG_PREFILTER", mode)
+    for sql in [q for q in SV_QUERIES if "WHERE" in q] + [
+            "SELECT column9, SUM(column1), COUNT(*) FROM t WHERE column7 IN (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12) "
+            "AND column3 > 1000000 AND column17 NOT IN (5, 7) GROUP BY column9",
+            "SELECT COUNT(*), SUM(column3) FROM t WHERE daysSinceEpoch = 126164076 AND column6 < 900000000"]:
+        q = parse(sql)
+        assert_same_result(gpu_engine.execute(sv_table_inter, q), oracle_engine.execute(sv_table_inter, q),
+                           table=sv_table_inter)
+
+
 def test_unsupported_shape_is_reported_not_crashed(gpu_engine, sv_table_inner):
     """More group-by keys than the device path takes -> PG_E_UNSUPPORTED (the caller falls back to the CPU plan)."""
     with pytest.raises(UnsupportedQuery):

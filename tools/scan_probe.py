@@ -67,12 +67,13 @@ def main():
         for _ in range(args.reps):
             r = eng.run_plan(plan)
             t = eng.last_timing()
-            ks.append(t.scan_ms)
-            hs.append((t.host_compile_ms, t.prepass_ms, t.execute_wall_ms, t.finalize_wall_ms))
+            ks.append(t.prefilter_ms + t.scan_ms)
+            hs.append((t.host_compile_ms, t.prepass_ms, t.prefilter_ms, t.scan_ms, t.execute_wall_ms,
+                       t.finalize_wall_ms))
         wall = (time.perf_counter() - t0) / args.reps * 1e3
         k = float(np.median(ks))
         print(f"{name:12s} scan {k:8.3f} ms  {rows / k / 1e6:9.3f} Grows/s  wall {wall:8.3f} ms  "
-              f"matched {r.stats.num_docs_scanned}  host/pre/exec/fin ms "
+              f"matched {r.stats.num_docs_scanned}  host/pre/filt/scan/exec/fin ms "
               + "/".join(f"{x:.3f}" for x in np.median(np.array(hs), axis=0)), flush=True)
 
 
