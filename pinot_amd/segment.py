@@ -404,19 +404,10 @@ class ImmutableSegment:
         return ImmutableSegment(name, num_docs or 0, cols)
 
     # -- V1 directory (V1Constants file names + metadata.properties)
-    def write_v1(self, path: str) -> None:
-        os.makedirs(path, exist_ok=True)
+    def _metadata_lines(self) -> List[str]:
         props = [f"segment.name = {self.name}", f"segment.total.docs = {self.num_docs}",
                  "segment.padding.character = \\\\u0000"]
         for c in self.columns.values():
-            with open(os.path.join(path, c.name + ".dict"), "wb") as f:
-                f.write(c.dictionary.to_bytes())
-            ext = {"sv": ".sv.unsorted.fwd", "sorted": ".sv.sorted.fwd", "mv": ".mv.fwd"}[c.fwd_kind]
-            with open(os.path.join(path, c.name + ext), "wb") as f:
-                f.write(c.fwd)
-            if c.inverted is not None:
-                with open(os.path.join(path, c.name + ".bitmap.inv"), "wb") as f:
-                    f.write(c.inverted)
             p = f"column.{c.name}."
             props += [p + f"cardinality = {c.cardinality}", p + f"totalDocs = {c.num_docs}",
                       p + f"dataType = {c.data_type}", p + f"bitsPerElement = {c.bits_per_element}",
@@ -426,22 +417,70 @@ class ImmutableSegment:
                       p + f"isSingleValues = {str(c.single_value).lower()}",
                       p + f"maxNumberOfMultiValues = {c.max_num_multi_values}",
                       p + f"totalNumberOfEntries = {c.num_values}"]
+        return props
+
+    def write_v1(self, path: str) -> None:
+        os.makedirs(path, exist_ok=True)
+        for c in self.columns.values():
+            with open(os.path.join(path, c.name + ".dict"), "wb") as f:
+                f.write(c.dictionary.to_bytes())
+            ext = {"sv": ".sv.unsorted.fwd", "sorted": ".sv.sorted.fwd", "mv": ".mv.fwd"}[c.fwd_kind]
+            with open(os.path.join(path, c.name + ext), "wb") as f:
+                f.write(c.fwd)
+            if c.inverted is not None:
+                with open(os.path.join(path, c.name + ".bitmap.inv"), "wb") as f:
+                    f.write(c.inverted)
         with open(os.path.join(path, "metadata.properties"), "w") as f:
-            f.write("\n".join(props) + "\n")
+            f.write("\n".join(self._metadata_lines()) + "\n")
+
+    # -- V3 directory: <segment>/v3/{metadata.properties, creation.meta, index_map, columns.psf}
+    #    (SegmentDirectoryPaths.java:33-41, SingleFileIndexDirectory.java:71-74,164-188,214-320,452-465): every index
+    #    is appended to columns.psf as an 8-byte big-endian magic marker 0xdeadbeefdeafbead + its payload; index_map
+    #    holds `<column>.<indexName>.startOffset = <offset of the marker>` and `.size = <payload + 8>`; sorted columns
+    #    keep their (start, end) pairs as their forward_index (ColumnIndexType names).
+    V3_MAGIC = 0xDEADBEEFDEAFBEAD
+
+    def write_v3(self, path: str) -> None:
+        d = os.path.join(path, "v3")
+        os.makedirs(d, exist_ok=True)
+        entries = []
+        with open(os.path.join(d, "columns.psf"), "wb") as psf:
+            off = 0
+            for c in self.columns.values():
+                parts = [("dictionary", c.dictionary.to_bytes()), ("forward_index", c.fwd)]
+                if c.inverted is not None:
+                    parts.append(("inverted_index", c.inverted))
+                for idx, payload in parts:
+                    psf.write(struct.pack(">Q", self.V3_MAGIC))
+                    psf.write(payload)
+                    entries.append((c.name, idx, off, len(payload) + 8))
+                    off += len(payload) + 8
+        with open(os.path.join(d, "index_map"), "w") as f:
+            for col, idx, start, size in entries:
+                f.write(f"{col}.{idx}.startOffset = {start}\n{col}.{idx}.size = {size}\n")
+        with open(os.path.join(d, "metadata.properties"), "w") as f:
+            f.write("\n".join(self._metadata_lines()) + "\n")
+        with open(os.path.join(d, "creation.meta"), "wb") as f:  # SegmentIndexCreationDriverImpl: crc, creationTime
+            f.write(struct.pack(">qq", 0, 0))
 
     @staticmethod
-    def load_v1(path: str) -> "ImmutableSegment":
-        """ImmutableSegmentLoader for the V1 layout (metadata.properties + per-index files)."""
+    def _read_props(path: str) -> Dict[str, str]:
         props = {}
         with open(os.path.join(path, "metadata.properties")) as f:
             for line in f:
                 if "=" in line:
                     k, v = line.split("=", 1)
                     props[k.strip()] = v.strip()
+        return props
+
+    @staticmethod
+    def _from_parts(path: str, props: Dict[str, str], index_bytes) -> "ImmutableSegment":
+        """ImmutableSegmentLoader over either store: `index_bytes(column, kind)` returns the bytes of one index
+        (kind: dictionary / sorted / unsorted / mv / inverted) or None."""
         num_docs = int(props["segment.total.docs"])
         pad = props.get("segment.padding.character", "\\u0000")
         padding = b"\0" if "0000" in pad else pad.encode()[-1:]
-        names = sorted({k.split(".")[1] for k in props if k.startswith("column.")})
+        names = sorted({k[len("column."):].rsplit(".", 1)[0] for k in props if k.startswith("column.")})
         cols = {}
         for cname in names:
             p = lambda k: props[f"column.{cname}.{k}"]
@@ -449,19 +488,12 @@ class ImmutableSegment:
             card = int(p("cardinality"))
             b = int(p("bitsPerElement"))
             eb = int(p("lengthOfEachEntry")) if dtype == "STRING" else 0
-            with open(os.path.join(path, cname + ".dict"), "rb") as f:
-                dictionary = Dictionary.from_bytes(dtype, f.read(), card, eb, padding)
+            dictionary = Dictionary.from_bytes(dtype, index_bytes(cname, "dictionary"), card, eb, padding)
             sv = p("isSingleValues") == "true"
             is_sorted = p("isSorted") == "true"
             nv = int(props.get(f"column.{cname}.totalNumberOfEntries", num_docs))
-            ext = (".sv.sorted.fwd" if is_sorted else ".sv.unsorted.fwd") if sv else ".mv.fwd"
-            with open(os.path.join(path, cname + ext), "rb") as f:
-                fwd = f.read()
-            inv = None
-            ip = os.path.join(path, cname + ".bitmap.inv")
-            if os.path.exists(ip):
-                with open(ip, "rb") as f:
-                    inv = f.read()
+            fwd = index_bytes(cname, ("sorted" if is_sorted else "unsorted") if sv else "mv")
+            inv = index_bytes(cname, "inverted")
             col = Column(cname, dtype, sv, dictionary, num_docs, b, is_sorted, nv,
                          int(props.get(f"column.{cname}.maxNumberOfMultiValues", 0)), fwd, inv,
                          props.get(f"column.{cname}.columnType", "DIMENSION"))
@@ -475,6 +507,65 @@ class ImmutableSegment:
                 col.dict_ids = ids
             cols[cname] = col
         return ImmutableSegment(props.get("segment.name", os.path.basename(path)), num_docs, cols)
+
+    @staticmethod
+    def load_v1(path: str) -> "ImmutableSegment":
+        """ImmutableSegmentLoader for the V1 layout (metadata.properties + per-index files)."""
+        ext = {"dictionary": ".dict", "sorted": ".sv.sorted.fwd", "unsorted": ".sv.unsorted.fwd", "mv": ".mv.fwd",
+               "inverted": ".bitmap.inv"}
+
+        def index_bytes(col, kind):
+            fp = os.path.join(path, col + ext[kind])
+            if not os.path.exists(fp):
+                if kind == "inverted":
+                    return None
+                raise FileNotFoundError(fp)
+            with open(fp, "rb") as f:
+                return f.read()
+        return ImmutableSegment._from_parts(path, ImmutableSegment._read_props(path), index_bytes)
+
+    @staticmethod
+    def load_v3(path: str) -> "ImmutableSegment":
+        """ImmutableSegmentLoader for the V3 single-file store (SingleFileIndexDirectory.loadMap / mapBufferEntries):
+        index_map keys parsed from the right (column names may contain dots), every payload checked for its magic
+        marker."""
+        d = os.path.join(path, "v3") if os.path.isdir(os.path.join(path, "v3")) else path
+        entries: Dict[tuple, Dict[str, int]] = {}
+        with open(os.path.join(d, "index_map")) as f:
+            for line in f:
+                if "=" not in line:
+                    continue
+                k, v = (x.strip() for x in line.split("=", 1))
+                rest, prop = k.rsplit(".", 1)
+                col, idx = rest.rsplit(".", 1)
+                if prop not in ("startOffset", "size"):
+                    raise ValueError(f"invalid index_map key {k}")
+                entries.setdefault((col, idx.lower()), {})[prop] = int(v)
+        with open(os.path.join(d, "columns.psf"), "rb") as f:
+            psf = f.read()
+        names = {"dictionary": "dictionary", "sorted": "forward_index", "unsorted": "forward_index",
+                 "mv": "forward_index", "inverted": "inverted_index"}
+
+        def index_bytes(col, kind):
+            e = entries.get((col, names[kind]))
+            if e is None:
+                if kind == "inverted":
+                    return None
+                raise KeyError(f"{col}.{names[kind]} missing from index_map")
+            start, size = e["startOffset"], e["size"]
+            if size < 8 or start < 0 or start + size > len(psf):
+                raise ValueError(f"bad index_map entry for {col}.{names[kind]}")
+            if struct.unpack_from(">Q", psf, start)[0] != ImmutableSegment.V3_MAGIC:
+                raise ValueError(f"missing magic marker for {col}.{names[kind]} at {start}")
+            return psf[start + 8:start + size]
+        return ImmutableSegment._from_parts(d, ImmutableSegment._read_props(d), index_bytes)
+
+    @staticmethod
+    def load(path: str) -> "ImmutableSegment":
+        """SegmentDirectoryPaths.findSegmentDirectory: the v3 sub-directory when present, else V1 files."""
+        if os.path.isdir(os.path.join(path, "v3")) or os.path.exists(os.path.join(path, "columns.psf")):
+            return ImmutableSegment.load_v3(path)
+        return ImmutableSegment.load_v1(path)
 
 
 def inverted_index_bytes_sv(dict_ids: np.ndarray, card: int, run_optimize=True) -> bytes:

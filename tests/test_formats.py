@@ -153,3 +153,48 @@ def test_v1_roundtrip(tmp_path):
         assert np.array_equal(back.columns[c].dict_ids, seg.columns[c].dict_ids)
     assert back.columns["s"].is_sorted and back.columns["a"].inverted == seg.columns["a"].inverted
     assert back.columns["m"].fwd == seg.columns["m"].fwd
+
+
+def test_v3_roundtrip_and_layout(tmp_path):
+    """V3 single-file store (SingleFileIndexDirectory): columns.psf = per index an 8-byte BE magic marker + payload,
+    index_map offsets / sizes (size includes the marker), column names with dots parsed from the right."""
+    import struct
+    rng = np.random.default_rng(6)
+    n = 4000
+    data = {"a.b": rng.integers(0, 300, n), "s": np.sort(rng.integers(0, 40, n)),
+            "m": [list(rng.integers(0, 20, rng.integers(1, 5))) for _ in range(n)],
+            "t": np.array(["x", "yy", "zzz"], dtype=object)[rng.integers(0, 3, n)]}
+    seg = S.ImmutableSegment.create("seg3", data, {"a.b": "INT", "s": "LONG", "m": "INT", "t": "STRING"},
+                                    inverted=["a.b", "t"])
+    seg.write_v3(str(tmp_path))
+    d = tmp_path / "v3"
+    assert sorted(p.name for p in d.iterdir()) == ["columns.psf", "creation.meta", "index_map", "metadata.properties"]
+    psf = (d / "columns.psf").read_bytes()
+    keys = dict(l.split(" = ") for l in (d / "index_map").read_text().splitlines())
+    start, size = int(keys["a.b.forward_index.startOffset"]), int(keys["a.b.forward_index.size"])
+    assert struct.unpack_from(">Q", psf, start)[0] == 0xDEADBEEFDEAFBEAD
+    assert psf[start + 8:start + size] == seg.columns["a.b"].fwd
+    back = S.ImmutableSegment.load(str(tmp_path))
+    assert back.num_docs == n and set(back.columns) == set(seg.columns)
+    for c in seg.columns:
+        assert back.columns[c].fwd == seg.columns[c].fwd
+        assert back.columns[c].inverted == seg.columns[c].inverted
+        assert back.columns[c].dictionary.to_bytes() == seg.columns[c].dictionary.to_bytes()
+    # a corrupted marker is detected (validateMagicMarker)
+    bad = bytearray(psf)
+    bad[start] ^= 0xFF
+    (d / "columns.psf").write_bytes(bytes(bad))
+    with pytest.raises(ValueError):
+        S.ImmutableSegment.load_v3(str(tmp_path))
+
+
+def test_padding_null_converted_to_v3(tmp_path):
+    """The reference's own V1 bytes (paddingNull) converted to the V3 store load back identically."""
+    v1 = S.ImmutableSegment.load_v1(os.path.join(GOLDEN, "padding_null"))
+    v1.write_v3(str(tmp_path))
+    v3 = S.ImmutableSegment.load(str(tmp_path))
+    assert v3.num_docs == v1.num_docs and set(v3.columns) == set(v1.columns)
+    for c in v1.columns:
+        a, b = v1.columns[c], v3.columns[c]
+        assert a.fwd == b.fwd and a.inverted == b.inverted and a.data_type == b.data_type
+        assert list(a.dictionary.values) == list(b.dictionary.values)

@@ -386,3 +386,27 @@ def test_config1_baseball_quickstart(qi, gpu_engine, oracle_engine, baseball_tab
     assert_same_result(g, o, table=baseball_table)
     t = gpu_engine.execute(baseball_table, q, trim=True)
     assert reduce_to_rows(q, t)[1] == reduce_to_rows(q, o)[1]
+
+
+def test_v3_store_segments_on_device(tmp_path, gpu_engine, oracle_engine):
+    """Segments loaded from the V3 single-file store (SingleFileIndexDirectory) feed pg_column_upload unchanged:
+    a synthetic segment written as V3 and the reference's own paddingNull V1 bytes converted to V3."""
+    import os
+    rng = np.random.default_rng(11)
+    n = 60_000
+    data = {"k": rng.integers(0, 50, n), "v": rng.integers(-10 ** 6, 10 ** 6, n), "s": np.sort(rng.integers(0, 90, n)),
+            "t": np.array(["a", "bb", "ccc", "dd"], dtype=object)[rng.integers(0, 4, n)]}
+    seg = _seg("v3", data, {"k": "INT", "v": "LONG", "s": "INT", "t": "STRING"}, inverted=["t"])
+    seg.write_v3(str(tmp_path / "syn"))
+    back = ImmutableSegment.load(str(tmp_path / "syn"))
+    t_orig, t_v3 = Table("t", [seg]), Table("t", [back])
+    for sql in ["SELECT k, COUNT(*), SUM(v), MIN(v) FROM t WHERE t IN ('a', 'dd') AND s BETWEEN 10 AND 70 GROUP BY k",
+                "SELECT t, DISTINCTCOUNT(k), MAX(v) FROM t WHERE v > 0 GROUP BY t"]:
+        q = parse(sql)
+        assert_same_result(gpu_engine.execute(t_v3, q), oracle_engine.execute(t_orig, q), table=t_orig)
+    golden = os.path.join(os.path.dirname(__file__), "golden", "padding_null")
+    ImmutableSegment.load_v1(golden).write_v3(str(tmp_path / "pad"))
+    pad = Table("t", [ImmutableSegment.load(str(tmp_path / "pad"))])
+    q = parse("SELECT COUNT(*), MIN(age), MAX(age), SUM(age) FROM t")
+    g = gpu_engine.execute(pad, q)
+    assert g.rows[()][:4] == [5, 617.0, 1228.0, 617.0 + 824 + 837 + 1209 + 1228]
