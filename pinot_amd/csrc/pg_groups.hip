@@ -84,7 +84,7 @@ hipError_t launch_sort_pairs(const uint64_t* kin, uint64_t* kout, const uint32_t
 
 // ------------------------------------------------------------------------------------------ finalisation
 
-__device__ __forceinline__ uint32_t bits_words(uint32_t card) { return (card + 31u) / 32u; }
+__host__ __device__ __forceinline__ uint32_t bits_words(uint32_t card) { return (card + 31u) / 32u; }
 
 // Final value of every aggregation of the groups at `slots` (AggregationFunction.extractFinalResult; AVG keeps
 // its (sum, count) pair in vals / cnts, DISTINCTCOUNT its set size).  One thread per group.
@@ -110,16 +110,34 @@ __global__ void final_values_kernel(StateView v, FinalSpec f, const uint32_t* __
           break;
         case PG_AGG_MIN: x = order_key_decode(v.mn[s * v.n_min + A.slot]); break;
         case PG_AGG_MAX: x = order_key_decode(v.mx[s * v.n_max + A.slot]); break;
-        case PG_AGG_DISTINCTCOUNT: {
-          const uint32_t* w = v.bits + s * v.bit_words + A.dc_word;
-          uint64_t pc = 0;
-          for (uint32_t k = 0; k < bits_words(A.key_card); k++) pc += __popc(w[k]);
-          x = (double)pc;
-          break;
-        }
+        case PG_AGG_DISTINCTCOUNT: continue;  // set sizes: dc_sizes_kernel (coalesced bitmap rows)
       }
       vals[i * f.num_aggs + a] = x;
       cnts[i * f.num_aggs + a] = c;
+    }
+  }
+}
+
+// DISTINCTCOUNT a of the groups at `slots`: the popcount of each group's bitmap row (extractFinalResult = set size),
+// read coalesced: `lpg` lanes (a power of two covering the row's words, <= 64) share a row, 64 / lpg rows per wave.
+// One thread per row would read each 128-byte row alone (config 4: 10 M rows took 5.5 ms that way).
+__global__ void dc_sizes_kernel(StateView v, uint32_t dc_word, uint32_t words, uint32_t lpg, const uint32_t* __restrict__ slots,
+                                uint64_t n, uint32_t A, uint32_t a, double* __restrict__ vals, int64_t* __restrict__ cnts) {
+  const uint32_t lane = threadIdx.x & 63u, sub = lane & (lpg - 1u);
+  const uint64_t per_wave = 64u / lpg;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  for (uint64_t i0 = wave * per_wave; i0 < n; i0 += nwaves * per_wave) {
+    const uint64_t i = i0 + lane / lpg;
+    uint32_t pc = 0;
+    if (i < n) {
+      const uint32_t* w = v.bits + (uint64_t)slots[i] * v.bit_words + dc_word;
+      for (uint32_t k = sub; k < words; k += lpg) pc += __popc(w[k]);
+    }
+    for (uint32_t o = 1; o < lpg; o <<= 1) pc += __shfl_xor(pc, o);
+    if (i < n && sub == 0) {
+      vals[i * A + a] = (double)pc;
+      cnts[i * A + a] = 0;
     }
   }
 }
@@ -130,6 +148,15 @@ hipError_t launch_final_values(const StateView& v, const FinalSpec& f, const uin
   const uint64_t blocks = (n + 255) / 256;
   hipLaunchKernelGGL(final_values_kernel, dim3((uint32_t)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, s, v, f,
                      slots, n, keys, vals, cnts);
+  for (uint32_t a = 0; a < f.num_aggs; a++) {
+    if (f.aggs[a].fn != PG_AGG_DISTINCTCOUNT) continue;
+    const uint32_t words = bits_words(f.aggs[a].key_card);
+    uint32_t lpg = 1;
+    while (lpg < words && lpg < 64) lpg <<= 1;
+    const uint64_t waves = (n * lpg + 63) / 64, b2 = (waves + 3) / 4;
+    hipLaunchKernelGGL(dc_sizes_kernel, dim3((uint32_t)(b2 < 16384 ? b2 : 16384)), dim3(256), 0, s, v,
+                       f.aggs[a].dc_word, words, lpg, slots, n, f.num_aggs, a, vals, cnts);
+  }
   return hipGetLastError();
 }
 

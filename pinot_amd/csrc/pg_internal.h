@@ -38,6 +38,7 @@ constexpr int kLdsSetBytes = 16 * 1024;              // LDS filter bitmaps of IN
 constexpr int kLdsStageBytes = 32 * 1024;            // LDS tiles of densely read packed columns (per ring buffer)
 constexpr int kMaxStaged = 6;                        // packed columns staged per tile
 constexpr int kNoSlot = 255;
+constexpr uint32_t kPollTiles = 8;                   // scan tiles between polls of the cancel / deadline flag
 
 // Filter program as the kernel runs it: a tree in prefix form (host-compiled from the ABI's postfix program,
 // AND children ordered most-selective first so later children are evaluated only on surviving docs).
@@ -115,7 +116,13 @@ enum SlotKind : uint32_t { SK_NONE = 0, SK_I64 = 1, SK_F64 = 2, SK_MIN = 3, SK_M
 //   GM_HASH_SEG as GM_HASH over (packed key * num_segments + segment), with the first matching doc of every
 //               (segment, key) in first_doc: the per-segment table when numGroupsLimit can truncate a segment
 //               (the runtime then keeps, per segment, the limit keys seen first and merges them by key).
-enum GroupMode : uint32_t { GM_NONE = 0, GM_DENSE = 1, GM_HASH = 2, GM_HASH_SEG = 3 };
+//   GM_PART_COUNT / GM_PART_SCATTER  radix-partitioned dense group-by (pg_part.hip) for key spaces whose state is far
+//               larger than any cache: the scan only emits one 32-bit entry per matching doc -- (key low bits, value id)
+//               into the partition of its key's high bits -- with LDS-atomic positions, no global atomics:
+//               COUNT pass: per-(partition, block) entry counts; SCATTER pass (same grid, same docs): the entries at
+//               their block's range of each partition (exclusive scan of the counts).  Level-2 partitioning and the
+//               LDS-resident aggregation of each bucket follow in pg_part.hip; the state they write is GM_DENSE's.
+enum GroupMode : uint32_t { GM_NONE = 0, GM_DENSE = 1, GM_HASH = 2, GM_HASH_SEG = 3, GM_PART_COUNT = 4, GM_PART_SCATTER = 5 };
 constexpr unsigned long long kEmptyKey = 0xFFFFFFFFFFFFFFFFull;
 
 __host__ __device__ inline uint64_t mix64(uint64_t x) {  // murmur3 fmix64 (the HashCommon.mix role)
@@ -191,6 +198,13 @@ struct QuerySpec {
   unsigned long long* seg_matched;  // [seg]
   unsigned int* err;                // device-side violations: bit 0 group key, bit 1 DISTINCTCOUNT key, bit 2 hash table full
   const unsigned int* cancel;       // host-mapped flag polled once per tile (nonzero: stop); null = not cancellable
+  // GM_PART_*: level-1 partition of packed key g = g >> part_shift (< part_nparts); entry = ((g & part_lmask) <<
+  // part_vbits) | value id of aggregation part_dc (0 when part_dc == kNoSlot: COUNT only)
+  uint32_t part_shift, part_vbits, part_nparts, part_dc;
+  uint32_t part_lmask, pad3;
+  unsigned long long* part_hist;    // [part_nparts][gridDim.x]: COUNT pass writes counts; SCATTER pass reads offsets
+  uint32_t* part_out;               // SCATTER: level-1 entries
+  uint64_t part_cap;                // entries part_out can hold
 };
 
 // order-preserving int64 image of a double (for MIN/MAX slots)
@@ -251,6 +265,31 @@ struct PreSpec {
   uint32_t* const* out;           // [seg] bitmap words, packed 1-bit column order
 };
 hipError_t launch_prefilter(const PreSpec& p, uint32_t bits, uint32_t blocks, hipStream_t s);
+
+// ---- radix-partitioned group-by (pg_part.hip): level 2 + per-bucket aggregation, after the two scan passes
+constexpr uint32_t kPartL1 = 256;        // level-1 partitions (scan passes)
+constexpr uint32_t kPartNB = 32;         // level-2 blocks per level-1 partition
+constexpr uint32_t kPartLdsBytes = 72 * 1024;  // LDS state of one bucket (count + value bitmap per group)
+struct PartSpec {
+  uint32_t nparts1, nparts2;       // level-1 partitions, level-2 sub-partitions per level-1 partition
+  uint32_t vbits, shift2;          // value-id bits; key bits below the level-2 digit (log2 groups per bucket)
+  uint32_t dc_words;               // uint32 words of the value bitmap (0: COUNT only)
+  uint32_t row_words, dc_word;     // state bitmap row width / this aggregation's first word (StateView layout)
+  uint32_t n_i64;
+  uint32_t blocks1;                // level-1 blocks (the scan grid)
+  uint32_t pad;
+  uint64_t num_groups;             // G (packed key space)
+  const unsigned long long* off1;  // [nparts1 * blocks1 + 1] exclusive offsets of the level-1 counts
+  const uint32_t* in1;             // level-1 entries
+  unsigned long long* hist2;       // [nparts1 * nparts2 * kPartNB + 1] level-2 counts (last = 0)
+  const unsigned long long* off2;  // their exclusive scan: bucket b's entries start at off2[b * kPartNB]
+  uint32_t* out2;                  // level-2 entries, bucket-major
+  unsigned long long* i64;         // dense state written by the bucket pass
+  uint32_t* bits;
+};
+hipError_t launch_part_count2(const PartSpec& p, hipStream_t s);
+hipError_t launch_part_scatter2(const PartSpec& p, hipStream_t s);
+hipError_t launch_part_aggregate(const PartSpec& p, hipStream_t s);
 
 // ---- group state (pg_groups.hip)
 struct StateView {            // the device arrays of one partial state

@@ -587,7 +587,7 @@ struct Partials {
     return v;
   }
   // device state for `num_slots` slots of the current layout (+ keys for hash modes), initialised
-  int alloc_state(hipStream_t s);
+  int alloc_state(hipStream_t s, bool init = true);
 };
 
 // Layout of the state arrays of a plan's aggregations (slot assignment, DISTINCTCOUNT bitmap words).  `integer`
@@ -600,6 +600,12 @@ constexpr uint64_t kDefaultNumGroupsLimit = 100000;
 constexpr uint64_t kDenseMaxSlots = 1ull << 26;      // dense key spaces up to 64 M slots
 constexpr uint64_t kStateBudget = 48ull << 30;       // bytes of group state one query may allocate
 constexpr uint64_t kMaxHashSlots = 1ull << 30;
+constexpr uint64_t kPartMinStateBytes = 64ull << 20;  // radix-partitioned group-by above this much dense state
+
+struct PartPlan {  // GM_PART_* pipeline of one query (pg_part.hip)
+  bool on = false;
+  uint32_t shift1 = 0, shift2 = 0, vbits = 0, dc_words = 0, dc_word = 0, dc = 0, nparts1 = 0, nparts2 = 1;
+};
 
 uint64_t pow2_at_least(uint64_t x) {
   uint64_t c = 1;
@@ -821,7 +827,7 @@ int agg_layout(const pg_plan* plan, uint32_t integer, std::vector<AggSpec>& aggs
   return PG_OK;
 }
 
-int Partials::alloc_state(hipStream_t s) {
+int Partials::alloc_state(hipStream_t s, bool init) {
   const uint64_t G = num_slots;
   int rc;
   const bool hash = mode == GM_HASH || mode == GM_HASH_SEG;
@@ -833,7 +839,8 @@ int Partials::alloc_state(hipStream_t s) {
   if (hash) { if ((rc = keys.alloc_pooled(G * 8ull))) return rc; } else keys.reset();
   if (mode == GM_HASH_SEG) { if ((rc = first_doc.alloc_pooled(G * 4ull))) return rc; } else first_doc.reset();
   if ((rc = misc.alloc_pooled(16))) return rc;
-  HIP_CHECK(launch_init_view(view(), s));
+  if (init) HIP_CHECK(launch_init_view(view(), s));
+  else HIP_CHECK(hipMemsetAsync(misc.p, 0, 16, s));  // every slot is written by the producer (pg_part.hip)
   return PG_OK;
 }
 
@@ -1139,6 +1146,40 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   q.n_i64 = P.n_i64; q.n_f64 = P.n_f64; q.n_min = P.n_min; q.n_max = P.n_max;
   q.dc_row_words = P.bit_words;
   q.use_lds = P.mode == GM_DENSE && G * 8ull * (P.n_i64 + P.n_f64 + P.n_min + P.n_max) <= (uint64_t)kLdsGroupBytes;
+  // ---- radix-partitioned dense group-by (pg_part.hip) for a dense key space whose state is far larger than any
+  // cache, when the aggregations are COUNTs and at most one DISTINCTCOUNT (entries of key low bits | value id fit 32
+  // bits).  PG_PART=0|1 overrides the size threshold.
+  PartPlan part;
+  {
+    const char* part_env = getenv("PG_PART");
+    const int pe = part_env ? atoi(part_env) : -1;
+    uint32_t dc = (uint32_t)kNoSlot, ndc = 0;
+    bool ok = P.mode == GM_DENSE && !q.use_lds && K > 0 && P.n_i64 == 1 && !P.n_f64 && !P.n_min && !P.n_max &&
+              total_docs > 0 && total_docs < 0xFFFFFFF0ull && pe != 0;
+    for (uint32_t a = 0; a < A && ok; a++) {
+      if (P.aggs[a].fn == PG_AGG_DISTINCTCOUNT) { dc = a; ndc++; }
+      else if (P.aggs[a].fn != PG_AGG_COUNT) ok = false;
+    }
+    ok = ok && ndc <= 1 && (pe == 1 || G * slot_bytes >= kPartMinStateBytes);
+    if (ok) {
+      auto clog2 = [](uint64_t x) { uint32_t b = 0; while ((1ull << b) < x) b++; return b; };
+      const uint32_t gbits = clog2(G);
+      part.shift1 = gbits > 8 ? gbits - 8 : 0;
+      part.vbits = dc == (uint32_t)kNoSlot ? 0 : clog2(P.aggs[dc].key_card);
+      part.dc_words = dc == (uint32_t)kNoSlot ? 0 : (P.aggs[dc].key_card + 31) / 32;
+      const uint64_t per_group = 4ull * (1 + part.dc_words);
+      uint32_t sh2 = 0;
+      while ((per_group << (sh2 + 1)) <= (uint64_t)kPartLdsBytes) sh2++;
+      part.shift2 = std::min(sh2, part.shift1);
+      if (per_group <= (uint64_t)kPartLdsBytes && part.shift1 + part.vbits <= 32 && part.vbits < 32) {
+        part.on = true;
+        part.dc = dc;
+        part.dc_word = dc == (uint32_t)kNoSlot ? 0 : P.aggs[dc].dc_word;
+        part.nparts1 = (uint32_t)(((G - 1) >> part.shift1) + 1);
+        part.nparts2 = 1u << (part.shift1 - part.shift2);
+      }
+    }
+  }
   P.projected_cols = (uint32_t)projected.size();
   P.total_docs = total_docs;
   P.num_segments = S;
@@ -1201,7 +1242,9 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   }
   // ---- streaming pre-filter (pg_filter.hip): the leaf children of a root AND (or a lone leaf) whose joint pass
   // fraction is small are evaluated by lean per-bit-width kernels into one doc bitmap per segment; the fused scan
-  // then sees that bitmap as ONE 1-bit leaf and the other folded leaves as match-all.  PG_PREFILTER=0|1 overrides.
+  // then sees that bitmap as ONE 1-bit leaf and the other folded leaves as match-all.  Opt-in (PG_PREFILTER=1):
+  // measured slower than the fused scan alone on configs 2 and 3 (r02_v1: config 2 step 1.19 ->
+  // 1.90 ms, config 3 1.54 -> 2.80 ms), because the fused scan's short-circuit already skips most bytes.
   std::vector<uint32_t> pre_leaves;
   {
     std::vector<FNode> nodes;
@@ -1221,7 +1264,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
           pass *= leaf_pass[nodes[k].leaf];
           cost += leaf_cost[nodes[k].leaf];
         }
-      if (!cand.empty() && pf != 0 && (pf == 1 || (pass <= 0.5 && cost > 0.0))) {
+      if (!cand.empty() && pf == 1) {
         pre_leaves = cand;
         leaf_pass[cand[0]] = pass;
         leaf_cost[cand[0]] = 1.0 / 8;
@@ -1700,7 +1743,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   if (lds_bytes > 160 * 1024) return fail(PG_E_UNSUPPORTED, "scan needs %zu bytes of LDS", lds_bytes);
 
   // ---- device buffers (state + arena + scratch) from the caching pool
-  if ((rc = P.alloc_state(s))) return rc;
+  part.on = part.on && q.num_items > 0;
+  if ((rc = P.alloc_state(s, !part.on))) return rc;
   if ((rc = P.seg_matched.alloc_pooled(8ull * (S ? S : 1) + 16))) return rc;
   HIP_CHECK(hipMemsetAsync(P.seg_matched.p, 0, 8ull * (S ? S : 1) + 16, s));
   {
@@ -1753,6 +1797,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   const uint64_t off_items = ar.put(items.data(), items.size() * sizeof(WorkItem));
   const uint64_t off_lutjobs = ar.reserve(luts.size() * sizeof(LutJob));
   DevBuf arena, scratch;
+  DevBuf p_hist1, p_off1, p_ent1, p_hist2, p_off2, p_ent2, p_temp;  // GM_PART_* pipeline
   // declared after the buffers it protects: on any exit, wait for queued work before they return to the pool
   struct SyncOnExit {
     hipStream_t s;
@@ -1842,7 +1887,61 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   if (plan->deadline_ms && now_ms() > plan->deadline_ms) { (void)hipStreamSynchronize(s); return fail(PG_E_TIMEOUT, "deadline passed"); }
   CancelSlot cancel(plan->query_id, plan->query_id != 0 || plan->deadline_ms != 0);
   q.cancel = cancel.device_ptr();
-  if (q.num_items) {
+  if (q.num_items && part.on) {
+    // radix-partitioned group-by (pg_part.hip): count pass, exclusive scan, scatter pass, level 2, buckets
+    const uint64_t n1 = (uint64_t)part.nparts1 * blocks, n2 = (uint64_t)part.nparts1 * part.nparts2 * kPartNB;
+    const size_t tb = select_temp_bytes(std::max(n1, n2) + 1);
+    if ((rc = p_hist1.alloc_pooled(8 * (n1 + 1))) || (rc = p_off1.alloc_pooled(8 * (n1 + 1))) ||
+        (rc = p_ent1.alloc_pooled(4 * total_docs + 16)) || (rc = p_hist2.alloc_pooled(8 * (n2 + 1))) ||
+        (rc = p_off2.alloc_pooled(8 * (n2 + 1))) || (rc = p_ent2.alloc_pooled(4 * total_docs + 16)) ||
+        (rc = p_temp.alloc_pooled(tb)))
+      return rc;
+    unsigned long long* h1 = (unsigned long long*)p_hist1.p;
+    unsigned long long* o1 = (unsigned long long*)p_off1.p;
+    unsigned long long* h2 = (unsigned long long*)p_hist2.p;
+    unsigned long long* o2 = (unsigned long long*)p_off2.p;
+    HIP_CHECK(hipMemsetAsync(h1 + n1, 0, 8, s));
+    HIP_CHECK(hipMemsetAsync(h2 + n2, 0, 8, s));
+    q.part_shift = part.shift1;
+    q.part_vbits = part.vbits;
+    q.part_nparts = part.nparts1;
+    q.part_dc = part.dc;
+    q.part_lmask = part.shift1 >= 32 ? 0xFFFFFFFFu : (uint32_t)((1ull << part.shift1) - 1);
+    q.part_cap = total_docs;
+    q.part_out = (uint32_t*)p_ent1.p;
+    t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
+    q.group_mode = GM_PART_COUNT;
+    q.part_hist = h1;
+    HIP_CHECK(launch_scan(q, blocks, s));
+    HIP_CHECK(launch_exclusive_sum((const uint64_t*)h1, (uint64_t*)o1, n1 + 1, p_temp.p, tb, s));
+    HIP_CHECK(hipMemsetAsync(P.seg_matched.p, 0, 8ull * S, s));  // matched docs are counted by the second pass
+    q.group_mode = GM_PART_SCATTER;
+    q.part_hist = o1;
+    HIP_CHECK(launch_scan(q, blocks, s));
+    PartSpec ps;
+    memset(&ps, 0, sizeof(ps));
+    ps.nparts1 = part.nparts1;
+    ps.nparts2 = part.nparts2;
+    ps.vbits = part.vbits;
+    ps.shift2 = part.shift2;
+    ps.dc_words = part.dc_words;
+    ps.row_words = P.bit_words;
+    ps.dc_word = part.dc_word;
+    ps.n_i64 = P.n_i64;
+    ps.blocks1 = blocks;
+    ps.num_groups = G;
+    ps.off1 = o1;
+    ps.in1 = (const uint32_t*)p_ent1.p;
+    ps.hist2 = h2;
+    ps.off2 = o2;
+    ps.out2 = (uint32_t*)p_ent2.p;
+    ps.i64 = (unsigned long long*)P.i64.p;
+    ps.bits = (uint32_t*)P.bits.p;
+    HIP_CHECK(launch_part_count2(ps, s));
+    HIP_CHECK(launch_exclusive_sum((const uint64_t*)h2, (uint64_t*)o2, n2 + 1, p_temp.p, tb, s));
+    HIP_CHECK(launch_part_scatter2(ps, s));
+    HIP_CHECK(launch_part_aggregate(ps, s));
+  } else if (q.num_items) {
     t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
     HIP_CHECK(launch_scan(q, blocks, s));
   }

@@ -27,6 +27,8 @@
 // Nothing here is a dense contraction: no MFMA; the roofline is HBM bandwidth.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "pg_internal.h"
 
 namespace pg {
@@ -438,6 +440,25 @@ __device__ __forceinline__ uint64_t group_slot(const QuerySpec& q, uint64_t pack
   return h;
 }
 
+// GM_PART_*: the doc's entry instead of a state update.  COUNT pass: one more entry in the block's count of the
+// level-1 partition of key g; SCATTER pass (same grid and docs): the entry at the block's next position in that
+// partition (`cur` = the block's LDS cursors, loaded from the exclusive scan of the COUNT pass).
+__device__ __forceinline__ void part_emit(const QuerySpec& q, uint32_t* cur, uint64_t g, uint32_t vid) {
+  const uint32_t p = (uint32_t)(g >> q.part_shift);
+  if (q.group_mode == GM_PART_COUNT) {
+    atomicAdd(&cur[p], 1u);
+    return;
+  }
+  const uint32_t pos = atomicAdd(&cur[p], 1u);
+  if (pos < q.part_cap) q.part_out[pos] = (((uint32_t)g & q.part_lmask) << q.part_vbits) | vid;
+  else atomicOr(q.err, 8u);
+}
+
+// Packed group key / state slot of a doc: a single key's global id and every slot (dense <= 2^26, hash tables <=
+// 2^30) fit 32 bits; only a mixed-radix key of several columns needs 64 (and 32-bit keys keep the single-key shapes
+// free of scratch spills).
+template <int MAXK> using GKey = typename std::conditional<(MAXK > 1), uint64_t, uint32_t>::type;
+
 // Group-state pointers: the block's LDS copy when the table is privatised, else the global arrays.
 struct GroupState {
   unsigned long long* i64;
@@ -510,9 +531,9 @@ __device__ __forceinline__ uint32_t col_id(const QuerySpec& q, uint32_t slot, co
 
 // Dense tiles: the aggregation of 8 rows at a time with every dictionary / keymap read of the batch in flight
 // together (the switch on the function is outside the row loop so the 8 reads are straight-line).
-template <bool GROUPED>
+template <bool GROUPED, class GK>
 __device__ __forceinline__ void agg_rows8(const QuerySpec& q, const GroupState& S, const AggSpec& A, const ColDesc* c,
-                                          const uint32_t (&ia)[8], const uint32_t (&ib)[8], const uint64_t (&g)[8],
+                                          const uint32_t (&ia)[8], const uint32_t (&ib)[8], const GK (&g)[8],
                                           const uint32_t (&d)[8], uint32_t live, uint64_t& acc) {
   switch (A.fn) {
     case PG_AGG_COUNT: break;
@@ -525,7 +546,7 @@ __device__ __forceinline__ void agg_rows8(const QuerySpec& q, const GroupState& 
 #pragma unroll
         for (int r = 0; r < 8; r++) {
           if (!((live >> r) & 1u)) continue;
-          if constexpr (GROUPED) atomicAdd(&S.i64[g[r] * q.n_i64 + A.slot], (unsigned long long)v[r]);
+          if constexpr (GROUPED) atomicAdd(&S.i64[(uint64_t)g[r] * q.n_i64 + A.slot], (unsigned long long)v[r]);
           else acc += (uint64_t)v[r];
         }
       } else {
@@ -535,7 +556,7 @@ __device__ __forceinline__ void agg_rows8(const QuerySpec& q, const GroupState& 
 #pragma unroll
         for (int r = 0; r < 8; r++) {
           if (!((live >> r) & 1u)) continue;
-          if constexpr (GROUPED) atomicAdd(&S.f64[g[r] * q.n_f64 + A.slot], v[r]);
+          if constexpr (GROUPED) atomicAdd(&S.f64[(uint64_t)g[r] * q.n_f64 + A.slot], v[r]);
           else acc = __double_as_longlong(__longlong_as_double(acc) + v[r]);
         }
       }
@@ -550,8 +571,8 @@ __device__ __forceinline__ void agg_rows8(const QuerySpec& q, const GroupState& 
       for (int r = 0; r < 8; r++) {
         if (!((live >> r) & 1u)) continue;
         if constexpr (GROUPED) {
-          if (is_min) atomicMin(&S.mn[g[r] * q.n_min + A.slot], (long long)k[r]);
-          else atomicMax(&S.mx[g[r] * q.n_max + A.slot], (long long)k[r]);
+          if (is_min) atomicMin(&S.mn[(uint64_t)g[r] * q.n_min + A.slot], (long long)k[r]);
+          else atomicMax(&S.mx[(uint64_t)g[r] * q.n_max + A.slot], (long long)k[r]);
         } else {
           if (is_min ? k[r] < (int64_t)acc : k[r] > (int64_t)acc) acc = (uint64_t)k[r];
         }
@@ -578,7 +599,7 @@ __device__ __forceinline__ void aggregate_dense(const QuerySpec& q, const SegDes
     const uint32_t mc = (m >> (8 * ch)) & 0xFFu;
     if (__ballot(mc != 0) == 0) continue;
     uint32_t d[8], rel[8];
-    uint64_t g[8];
+    GKey<MAXK> g[8];
     uint32_t live = mc;
 #pragma unroll
     for (int r = 0; r < 8; r++) {
@@ -600,20 +621,44 @@ __device__ __forceinline__ void aggregate_dense(const QuerySpec& q, const SegDes
 #pragma unroll
         for (int r = 0; r < 8; r++) {
           if (kid[r] >= q.key_card[k]) live &= ~(1u << r);
-          else g[r] += kid[r] * q.key_stride[k];
+          else g[r] += (GKey<MAXK>)(kid[r] * q.key_stride[k]);
         }
       }
       if (live != mc) atomicOr(q.err, 1u);  // never expected: the host proved the key ranges
+      if (q.group_mode >= GM_PART_COUNT) {
+        uint32_t vid[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) vid[r] = 0;
+        if (q.group_mode == GM_PART_SCATTER && q.part_dc != (uint32_t)kNoSlot) {
+          const uint32_t a = q.part_dc;
+          const AggSpec& A = q.aggs[a];
+          const ColDesc c0 = ldc(sd.aggcols + 2 * a, 0);
+          uint32_t ids[8];
+#pragma unroll
+          for (int r = 0; r < 8; r++) ids[r] = col_id(q, q.agg_slot[a][0], c0, stage, d[r], rel[r]);
+#pragma unroll
+          for (int r = 0; r < 8; r++) {
+            const uint64_t k = key_of(A.key_kind, A.key_base, c0, ids[r]);
+            if (k < A.key_card) vid[r] = (uint32_t)k;
+            else if ((live >> r) & 1u) { atomicOr(q.err, 2u); live &= ~(1u << r); }
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 8; r++)
+          if ((live >> r) & 1u) part_emit(q, (uint32_t*)S.i64, g[r], vid[r]);
+        continue;
+      }
       if (q.group_mode != GM_DENSE) {
         for (int r = 0; r < 8; r++) {
           if (!((live >> r) & 1u)) continue;
-          g[r] = group_slot(q, g[r], sd.index, d[r]);
-          if (g[r] == ~0ull) live &= ~(1u << r);
+          const uint64_t slot = group_slot(q, (uint64_t)g[r], sd.index, d[r]);
+          if (slot == ~0ull) live &= ~(1u << r);
+          else g[r] = (GKey<MAXK>)slot;
         }
       }
 #pragma unroll
       for (int r = 0; r < 8; r++)
-        if ((live >> r) & 1u) atomicAdd(&S.i64[g[r] * q.n_i64], 1ull);  // slot 0: doc count / presence
+        if ((live >> r) & 1u) atomicAdd(&S.i64[(uint64_t)g[r] * q.n_i64], 1ull);  // slot 0: doc count / presence
     }
 #pragma unroll
     for (int a = 0; a < MAXA; a++) {
@@ -628,7 +673,7 @@ __device__ __forceinline__ void aggregate_dense(const QuerySpec& q, const SegDes
         ia[r] = nc >= 1 ? col_id(q, q.agg_slot[a][0], ldc(c, 0), stage, d[r], rel[r]) : 0u;
         ib[r] = nc >= 2 ? col_id(q, q.agg_slot[a][1], ldc(c, 1), stage, d[r], rel[r]) : 0u;
       }
-      agg_rows8<GROUPED>(q, S, A, c, ia, ib, g, d, live, acc[a]);
+      agg_rows8<GROUPED, GKey<MAXK>>(q, S, A, c, ia, ib, g, d, live, acc[a]);
     }
   }
 }
@@ -688,6 +733,20 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
           atomicOr(q.err, 1u);
           continue;
         }
+        if (q.group_mode >= GM_PART_COUNT) {
+          uint32_t vid = 0;
+          bool ok = true;
+#pragma unroll
+          for (int a = 0; a < MAXA; a++) {
+            if ((uint32_t)a != q.part_dc || q.group_mode != GM_PART_SCATTER) continue;
+            const AggSpec& A = q.aggs[a];
+            const uint64_t k = key_of(A.key_kind, A.key_base, ldc(sd.aggcols + 2 * a, 0), ia[x][a]);
+            if (k < A.key_card) vid = (uint32_t)k;
+            else { atomicOr(q.err, 2u); ok = false; }
+          }
+          if (ok) part_emit(q, (uint32_t*)S.i64, g, vid);
+          continue;
+        }
         g = group_slot(q, g, sd.index, d[x]);
         if (g == ~0ull) continue;
         atomicAdd(&S.i64[g * q.n_i64], 1ull);  // slot 0: doc count / presence
@@ -724,7 +783,8 @@ __host__ __device__ inline size_t scan_groups_off(const QuerySpec& q) {
   return (16 + (size_t)q.stage_ring * q.stage_lds_words * 4 + (size_t)q.set_lds_ints * 4 + 15) & ~(size_t)15;
 }
 __host__ __device__ inline size_t scan_queue_off(const QuerySpec& q) {
-  const size_t g = (q.num_keys && q.use_lds) ? q.num_slots * 8ull * (q.n_i64 + q.n_f64 + q.n_min + q.n_max) : 0;
+  const size_t g = (q.num_keys && q.group_mode >= GM_PART_COUNT) ? q.part_nparts * 4ull
+                   : (q.num_keys && q.use_lds) ? q.num_slots * 8ull * (q.n_i64 + q.n_f64 + q.n_min + q.n_max) : 0;
   return scan_groups_off(q) + ((g + 15) & ~(size_t)15);
 }
 
@@ -749,7 +809,15 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
     for (uint64_t i = tid; i < q.num_slots * q.n_min; i += kBlock) l_mn[i] = order_key(__builtin_inf());
     for (uint64_t i = tid; i < q.num_slots * q.n_max; i += kBlock) l_mx[i] = order_key(-__builtin_inf());
   }
-  const GroupState S = q.use_lds ? GroupState{l_i64, l_f64, l_mn, l_mx} : GroupState{q.i64, q.f64, q.mn, q.mx};
+  // GM_PART_*: the block's level-1 partition cursors (COUNT: counts from 0; SCATTER: this block's offsets)
+  const bool part = GROUPED && q.group_mode >= GM_PART_COUNT;
+  if (part) {
+    uint32_t* cur = (uint32_t*)lds_groups;
+    for (uint32_t p = tid; p < q.part_nparts; p += kBlock)
+      cur[p] = q.group_mode == GM_PART_COUNT ? 0u : (uint32_t)q.part_hist[(uint64_t)p * gridDim.x + blockIdx.x];
+    __syncthreads();
+  }
+  const GroupState S = (q.use_lds || part) ? GroupState{l_i64, l_f64, l_mn, l_mx} : GroupState{q.i64, q.f64, q.mn, q.mx};
 
   // aggregation-only accumulators (registers; indices compile-time via unrolled agg loops)
   uint64_t acc[MAXA];
@@ -776,9 +844,11 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
   // publishes it in LDS before the next tile's barrier; every wave reads the word of that tile's parity after the
   // barrier, so the whole block leaves the loop at the same tile (the words live in the pad before the ring, whose
   // st[-1] bits are always masked off)
+  // Polled every kPollTiles tiles into alternating words (no register stays live across a tile for it: at 4 waves
+  // per SIMD a per-tile poll state spilled 48 bytes per lane to scratch and slowed config 3 by 1.7x).
   volatile unsigned int* stop = (volatile unsigned int*)smem;
-  uint32_t iter = 0, pending = 0;
-  bool cancelled = false;
+  if (tid == 0) stop[0] = stop[1] = 0u;
+  uint32_t iter = 0;  // block-uniform tile counter
 
   if (i0 < i1) {
     const bool ring2 = q.stage_ring > 1;
@@ -818,14 +888,13 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
         if (has_next) { n_it = ldc(q.items, n_item); n_tile = n_it.tile_begin; n_seg = n_it.seg; }
       }
       __builtin_amdgcn_s_waitcnt(0);  // this wave's copies of the current tile have landed
-      if (q.cancel && tid == 0) stop[iter & 1u] = pending;
       __syncthreads();                // ... and every wave's; every wave is done with the other buffer
-      if (q.cancel) {
-        if (stop[iter & 1u]) {
-          cancelled = true;
-          break;
-        }
-        if (tid == 0) pending = __hip_atomic_load(q.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (q.cancel && (iter & (kPollTiles - 1u)) == 0) {
+        // word (k & 1) was written by thread 0 at poll k - 1, before this barrier; thread 0 now fills the other word
+        // for poll k + 1 (the host flag load may take a PCIe round trip; its LDS write lands before a later barrier)
+        const uint32_t k = iter / kPollTiles;
+        if (__builtin_amdgcn_readfirstlane(stop[k & 1u])) has_next = false;  // finish this tile, then leave
+        if (tid == 0) stop[(k + 1u) & 1u] = __hip_atomic_load(q.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       iter++;
       if (it.seg != cur_seg) {
@@ -912,7 +981,7 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
       tile = n_tile;
       if (ring2) buf ^= 1u;
     }
-    if (qn && !cancelled) flush();
+    if (qn && !(q.cancel && (stop[0] | stop[1]))) flush();
     const uint64_t c = wave_sum_u64(seg_count);
     if (lane == 0 && c) atomicAdd(&q.seg_matched[cur_seg], (unsigned long long)c);
   }
@@ -972,6 +1041,13 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
         }
         default: break;
       }
+    }
+  } else if (part) {
+    if (q.group_mode == GM_PART_COUNT) {
+      __syncthreads();
+      const uint32_t* cur = (const uint32_t*)lds_groups;
+      for (uint32_t p = tid; p < q.part_nparts; p += kBlock)
+        q.part_hist[(uint64_t)p * gridDim.x + blockIdx.x] = cur[p];
     }
   } else if (q.use_lds) {
     __syncthreads();

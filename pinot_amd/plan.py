@@ -47,12 +47,31 @@ class LoweredLeaf:
     ids: Optional[np.ndarray] = None   # sorted unique int32
 
 
+_LITERALS: dict = {}   # (id(values), data type) -> (values, coerced literal array): one coercion per predicate
+
+
+def _coerced_literals(d, values):
+    """The IN-list literals coerced to the dictionary's type once per predicate (not once per segment); None when a
+    literal does not convert (the per-value path then decides, as Dictionary.indexOf does)."""
+    key = (id(values), d.data_type, d.values.dtype.str)
+    hit = _LITERALS.get(key)
+    if hit is not None and hit[0] is values:
+        return hit[1]
+    try:
+        lit = np.unique(np.asarray([d._coerce(v) for v in values], dtype=d.values.dtype))  # sorted needles
+    except (ValueError, OverflowError):
+        lit = None
+    if len(_LITERALS) > 256:
+        _LITERALS.clear()
+    _LITERALS[key] = (values, lit)
+    return lit
+
+
 def dict_id_set(d, values) -> np.ndarray:
     """PredicateUtils.getDictIdSet: sorted unique dictIds of the literals present in the dictionary."""
     if d.data_type in ("INT", "LONG", "FLOAT", "DOUBLE"):
-        try:
-            lit = np.asarray([d._coerce(v) for v in values], dtype=d.values.dtype)
-        except (ValueError, OverflowError):
+        lit = _coerced_literals(d, values)
+        if lit is None:
             return np.asarray(sorted({i for i in (d.index_of(v) for v in values) if i >= 0}), dtype=np.int32)
         pos = np.searchsorted(d.values, lit, side="left")
         ok = pos < len(d.values)

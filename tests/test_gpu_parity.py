@@ -169,6 +169,28 @@ def test_config4_shape_high_cardinality_distinctcount(gpu_engine, oracle_engine)
         assert_same_result(full, o, table=t)
 
 
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_radix_partitioned_group_by(mode, monkeypatch, gpu_engine, oracle_engine):
+    """Dense group-by through the radix-partitioned pipeline (pg_part.hip: count pass, scatter pass, level 2, LDS
+    buckets; PG_PART=1 forces it below its state-size threshold) and through per-doc state updates (PG_PART=0):
+    identical to the oracle -- DISTINCTCOUNT value sets, COUNTs, the trimmed top rows, filters, ragged segments."""
+    from pinot_amd import abi, synth
+    monkeypatch.setenv("PG_PART", mode)
+    segs = [synth.make_segment_np(synth.highcard_specs(users=150_000), s, 200_003 + 977 * s) for s in range(3)]
+    t = Table("events", segs)
+    for sql in [synth.highcard_query() + " OPTION(numGroupsLimit=10000000)",
+                "SELECT userId, COUNT(*), DISTINCTCOUNT(itemId), COUNT(*) FROM events WHERE itemId < 700 "
+                "GROUP BY userId OPTION(numGroupsLimit=10000000)",
+                "SELECT itemId, COUNT(*) FROM events WHERE userId BETWEEN 1000 AND 90000 GROUP BY itemId",
+                "SELECT userId, COUNT(*) FROM events GROUP BY userId ORDER BY COUNT(*) DESC, userId LIMIT 10 "
+                "OPTION(numGroupsLimit=10000000)"]:
+        q = parse(sql)
+        o = oracle_engine.execute(t, q)
+        assert_same_result(gpu_engine.execute(t, q, flags=abi.PG_PLAN_VALUE_SETS), o, table=t)
+        if q.order_by:
+            assert reduce_to_rows(q, gpu_engine.execute(t, q, trim=True))[1] == reduce_to_rows(q, o)[1]
+
+
 def test_partial_rows_export_merge_roundtrip(gpu_engine, oracle_engine, sv_table_inter):
     """pg_partials_export (rows bucketed by owner) -> pg_partials_create + pg_partials_merge of every bucket ->
     finalize == the direct result, for a dense and a hash state."""
