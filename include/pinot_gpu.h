@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 2
+#define PG_ABI_VERSION 3
 
 typedef enum pg_status {
   PG_OK = 0,
@@ -78,8 +78,13 @@ typedef enum pg_index_kind {
   PG_IDX_FWD_SV_SORTED = 3,   /* sorted column: per dictId big-endian int32 [startDoc,endDoc] (`.sv.sorted.fwd`) */
   PG_IDX_FWD_MV_BITPACKED = 4,/* FixedBitMVForwardIndexWriter layout (`.mv.fwd`)                        */
   PG_IDX_INV_BITMAP = 5,      /* BitmapInvertedIndexWriter layout: (card+1) BE uint32 offsets + roaring */
-  PG_IDX_KEYMAP = 6           /* native int32[card]: dictId -> table-global key id (host-built, for
+  PG_IDX_KEYMAP = 6,          /* native int32[card]: dictId -> table-global key id (host-built, for
                                  group-by / DISTINCTCOUNT keys that are not integer value ranges)       */
+  PG_IDX_FWD_SV_RAW = 7       /* raw (no-dictionary) fixed-width chunked forward index (`.sv.raw.fwd`,
+                                 BaseChunkSVForwardIndexWriter v1-v4, PASS_THROUGH or SNAPPY chunks;
+                                 replaces FixedByteChunkSVForwardIndexReader /
+                                 FixedBytePower2ChunkSVForwardIndexReader, DefaultIndexReaderProvider.java:92-101);
+                                 data_type = stored type INT/LONG/FLOAT/DOUBLE                          */
 } pg_index_kind;
 
 typedef enum pg_data_type {
@@ -115,7 +120,9 @@ typedef enum pg_leaf_kind {
   PG_LEAF_SV_SCAN = 2,    /* ScanBasedFilterOperator over a bit-packed SV forward index                 */
   PG_LEAF_SORTED = 3,     /* SortedIndexBasedFilterOperator over PG_IDX_FWD_SV_SORTED                   */
   PG_LEAF_INVERTED = 4,   /* BitmapBasedFilterOperator over PG_IDX_INV_BITMAP                           */
-  PG_LEAF_MV_SCAN = 5     /* ScanBasedFilterOperator over a bit-packed MV forward index (any / all)     */
+  PG_LEAF_MV_SCAN = 5,    /* ScanBasedFilterOperator over a bit-packed MV forward index (any / all)     */
+  PG_LEAF_RAW_SCAN = 6    /* ScanBasedFilterOperator over a raw forward index with a raw-value predicate
+                             evaluator (predicate/...PredicateEvaluatorFactory.newRawValueBasedEvaluator)    */
 } pg_leaf_kind;
 
 /* A leaf matches dictIds in the set S, where S = [lo, hi) when num_ids == 0, else S = ids[0..num_ids).
@@ -130,6 +137,14 @@ typedef struct pg_leaf {
   uint32_t num_ids;
   int32_t lo, hi;
   const int32_t *ids;  /* host pointer, sorted ascending, no duplicates */
+  /* PG_LEAF_RAW_SCAN (values in the column's stored type): num_ids == 0 -> range; INT / LONG columns match
+   * ilo <= v <= ihi (bounds folded to closed on the host), FLOAT / DOUBLE columns dlo <(=) v <(=) dhi per
+   * lo_inclusive / hi_inclusive (+-inf = unbounded).  num_ids > 0 -> v in `values` (num_ids sorted unique values
+   * of the stored type: EQ / IN).  `exclusive` inverts (NOT_EQ / NOT_IN / NOT BETWEEN by the caller's NOT). */
+  int64_t ilo, ihi;
+  double dlo, dhi;
+  uint32_t lo_inclusive, hi_inclusive;
+  const void *values;  /* host pointer */
 } pg_leaf;
 
 /* Filter program: postfix over leaves.  op >= 0 pushes leaf `op`; PG_OP_AND(n)/PG_OP_OR(n) pop n

@@ -21,6 +21,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 from pinot_amd import abi
+from pinot_amd.segment import _NP_BE
 from pinot_amd.plan import (CPlan, DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY, ExecutionStats, IntermediateResult,
                             Table, default_row, merge_intermediate)
 from pinot_amd.query import QueryContext, parse
@@ -28,7 +29,7 @@ from pinot_amd.segment import ImmutableSegment
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(_HERE, "libpinot_oracle.so")
-ORC_FWD_SV, ORC_FWD_SORTED, ORC_FWD_MV = 0, 1, 2
+ORC_FWD_SV, ORC_FWD_SORTED, ORC_FWD_MV, ORC_FWD_RAW = 0, 1, 2, 3
 
 
 class orc_column(C.Structure):
@@ -80,7 +81,10 @@ class _SegmentColumns:
         self.keep = []
         for name, col in seg.columns.items():
             c = self.arr[table.column_ids[name]]
-            d = np.frombuffer(col.dictionary.to_bytes() or b"\0", dtype=np.uint8)
+            if col.dictionary is None:  # raw forward index: the decoded values stand in for the dictionary
+                d = np.frombuffer(col.raw_values.astype(_NP_BE[col.data_type]).tobytes() or b"\0", dtype=np.uint8)
+            else:
+                d = np.frombuffer(col.dictionary.to_bytes() or b"\0", dtype=np.uint8)
             f = np.frombuffer(col.fwd or b"\0", dtype=np.uint8)
             self.keep += [d, f]
             c.dict = d.ctypes.data
@@ -90,13 +94,14 @@ class _SegmentColumns:
                 self.keep.append(iv)
                 c.inv = iv.ctypes.data
                 c.inv_bytes = len(col.inverted)
-            c.fwd_kind = {"sv": ORC_FWD_SV, "sorted": ORC_FWD_SORTED, "mv": ORC_FWD_MV}[col.fwd_kind]
+            c.fwd_kind = {"sv": ORC_FWD_SV, "sorted": ORC_FWD_SORTED, "mv": ORC_FWD_MV, "raw": ORC_FWD_RAW}[col.fwd_kind]
             c.data_type = abi.DTYPE_CODES[col.data_type]
             c.num_docs = col.num_docs
-            c.cardinality = col.cardinality
+            c.cardinality = col.cardinality if col.dictionary is not None else col.num_docs
             c.bits = col.bits_per_element
             c.num_values = col.num_values
-            c.entry_bytes = col.dictionary.entry_bytes
+            c.entry_bytes = col.dictionary.entry_bytes if col.dictionary is not None else \
+                np.dtype(_NP_BE[col.data_type]).itemsize
 
 
 class OracleEngine:
@@ -182,8 +187,9 @@ class OracleEngine:
                 elif f == "AVG":
                     row.append((v, int(cnts[g, a])))
                 elif f == "DISTINCTCOUNT":
-                    dct = seg.columns[ag.arg.cols[0]].dictionary
-                    row.append({_py(dct.values[i]) for i in distinct.get(g * A + a, [])})
+                    col = seg.columns[ag.arg.cols[0]]
+                    dv = col.dictionary.values if col.dictionary is not None else col.raw_values  # raw: doc ids
+                    row.append({_py(dv[i]) for i in distinct.get(g * A + a, [])})
                 else:
                     row.append(v)
             rows[key] = row

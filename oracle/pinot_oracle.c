@@ -23,6 +23,8 @@
 #define ORC_FWD_SV 0
 #define ORC_FWD_SORTED 1
 #define ORC_FWD_MV 2
+#define ORC_FWD_RAW 3  /* raw forward index: `dict` holds the num_docs values (BE, decoded from the chunks), doc d's
+                          "dictId" is d itself (FixedByteChunkSVForwardIndexReader.getInt/.../getDouble(docId)) */
 
 typedef struct orc_column {
   const uint8_t *dict;   /* BE fixed-width values */
@@ -97,6 +99,8 @@ static int32_t *sv_dict_ids(const orc_column *c) {
   int32_t *ids = (int32_t *)malloc(sizeof(int32_t) * (c->num_docs ? c->num_docs : 1));
   if (c->fwd_kind == ORC_FWD_SV) {
     for (uint32_t d = 0; d < c->num_docs; d++) ids[d] = (int32_t)read_bits(c->fwd, d, c->bits);
+  } else if (c->fwd_kind == ORC_FWD_RAW) {
+    for (uint32_t d = 0; d < c->num_docs; d++) ids[d] = (int32_t)d;
   } else {
     for (uint32_t id = 0; id < c->cardinality; id++) {
       int32_t s = (int32_t)be32(c->fwd + 8ull * id), e = (int32_t)be32(c->fwd + 8ull * id + 4);
@@ -206,10 +210,35 @@ static int leaf_in_set(const pg_leaf *l, int32_t id) {
  * predicate/BaseDictionaryBasedPredicateEvaluator.java:133-150).  Sorted: SortedIndexBasedFilterOperator
  * (filter/SortedIndexBasedFilterOperator.java:51-138).  Inverted: BitmapBasedFilterOperator
  * (filter/BitmapBasedFilterOperator.java:66-115: OR of the matching dictIds' bitmaps, flip if exclusive). */
+/* Raw-value predicate evaluators (EqualsPredicateEvaluatorFactory / InPredicateEvaluatorFactory /
+ * RangePredicateEvaluatorFactory .newRawValueBasedEvaluator): the doc's value against the leaf's typed bounds or set. */
+static int raw_leaf_match(const pg_leaf *l, const orc_column *c, uint32_t d) {
+  if (c->data_type == PG_INT || c->data_type == PG_LONG) {
+    const int64_t v = c->data_type == PG_INT ? (int64_t)(int32_t)be32(c->dict + 4ull * d) : (int64_t)be64(c->dict + 8ull * d);
+    if (l->num_ids) {
+      const int64_t *set = (const int64_t *)l->values;
+      for (uint32_t i = 0; i < l->num_ids; i++) if (set[i] == v) return 1;
+      return 0;
+    }
+    return v >= l->ilo && v <= l->ihi;
+  }
+  const double v = dict_double(c, (int32_t)d);
+  if (l->num_ids) {
+    const double *set = (const double *)l->values;
+    for (uint32_t i = 0; i < l->num_ids; i++) if (set[i] == v) return 1;
+    return 0;
+  }
+  return (l->lo_inclusive ? v >= l->dlo : v > l->dlo) && (l->hi_inclusive ? v <= l->dhi : v < l->dhi);
+}
+
 static void eval_leaf(const pg_leaf *l, const orc_column *cols, uint32_t num_docs, uint8_t *out,
                       uint64_t *entries_scanned) {
   const orc_column *c = &cols[l->col_id];
   switch (l->kind) {
+    case PG_LEAF_RAW_SCAN:
+      for (uint32_t d = 0; d < num_docs; d++) out[d] = (uint8_t)(raw_leaf_match(l, c, d) ^ (l->exclusive != 0));
+      *entries_scanned += num_docs;
+      return;
     case PG_LEAF_MATCH_ALL: memset(out, 1, num_docs); return;
     case PG_LEAF_EMPTY: memset(out, 0, num_docs); return;
     case PG_LEAF_SV_SCAN: {
@@ -580,6 +609,97 @@ static void aggregate_group_by(const pg_plan *plan, const orc_column *cols, cons
   if (!array_based) { free(m.keys); free(m.ids); }
 }
 
+/* ------------------------------------------------------------------ metadata / dictionary route */
+
+/* The segment's filter is match-all after FilterPlanNode's pruning (plan/FilterPlanNode.java:191-311,
+ * FilterOperatorUtils.getAndFilterOperator / getOrFilterOperator / getNotFilterOperator drop match-all AND children,
+ * turn an OR with a match-all child into match-all and NOT(empty) into match-all): three-valued evaluation of the
+ * postfix program over MATCH_ALL (1) / EMPTY (0) / other (-1) leaves. */
+static int filter_is_match_all(const pg_plan *plan, const pg_leaf *leaves) {
+  if (!plan->num_ops) return 1;
+  int st[64], sp = 0;
+  for (uint32_t i = 0; i < plan->num_ops; i++) {
+    const int32_t op = plan->ops[i];
+    if (op >= 0) {
+      st[sp++] = leaves[op].kind == PG_LEAF_MATCH_ALL ? 1 : leaves[op].kind == PG_LEAF_EMPTY ? 0 : -1;
+    } else if (op == PG_OP_NOT) {
+      st[sp - 1] = st[sp - 1] < 0 ? -1 : !st[sp - 1];
+    } else {
+      const int n = (-op) & 0xFF, is_and = ((-op) & 0x300) == 0x100;
+      int v = is_and ? 1 : 0;
+      for (int k = 0; k < n; k++) {
+        const int x = st[sp - 1 - k];
+        if (is_and) v = (v == 0 || x == 0) ? 0 : (v < 0 || x < 0 ? -1 : 1);
+        else v = (v == 1 || x == 1) ? 1 : (v < 0 || x < 0 ? -1 : 0);
+      }
+      sp -= n;
+      st[sp++] = v;
+    }
+  }
+  return sp == 1 && st[0] == 1;
+}
+
+/* AggregationPlanNode.isFitForNonScanBasedPlan (plan/AggregationPlanNode.java:236-261): no group-by; every function is
+ * COUNT, or MIN / MAX / DISTINCTCOUNT of a plain column with a dictionary. */
+int orc_non_scan_fit(const pg_plan *plan) {
+  if (plan->num_keys) return 0;
+  for (uint32_t a = 0; a < plan->num_aggs; a++) {
+    const pg_agg *g = &plan->aggs[a];
+    if (g->fn == PG_AGG_COUNT) continue;
+    if (g->fn != PG_AGG_MIN && g->fn != PG_AGG_MAX && g->fn != PG_AGG_DISTINCTCOUNT) return 0;
+    if (g->op != PG_EXPR_COL) return 0;
+  }
+  return 1;
+}
+
+/* NonScanBasedAggregationOperator.getNextBlock (operator/query/NonScanBasedAggregationOperator.java:80-150): COUNT =
+ * numTotalDocs, MIN / MAX = the dictionary's first / last value, DISTINCTCOUNT = every dictionary value;
+ * ExecutionStatistics(numTotalDocs, 0, 0, numTotalDocs) (:253-256). */
+static void non_scan_aggregate(const pg_plan *plan, const orc_column *cols, uint32_t nd, orc_segment_result *r) {
+  const uint32_t A = plan->num_aggs;
+  r->num_groups = 1;
+  r->values = (double *)calloc(A ? A : 1, sizeof(double));
+  r->counts = (int64_t *)calloc(A ? A : 1, sizeof(int64_t));
+  uint64_t nd_pairs = 0;
+  for (uint32_t a = 0; a < A; a++)
+    if (plan->aggs[a].fn == PG_AGG_DISTINCTCOUNT) nd_pairs += cols[plan->aggs[a].col_a].cardinality;
+  r->distinct_group_agg = (uint64_t *)malloc(sizeof(uint64_t) * (nd_pairs ? nd_pairs : 1));
+  r->distinct_dict_ids = (int32_t *)malloc(sizeof(int32_t) * (nd_pairs ? nd_pairs : 1));
+  for (uint32_t a = 0; a < A; a++) {
+    const pg_agg *g = &plan->aggs[a];
+    const orc_column *c = &cols[g->col_a];
+    switch (g->fn) {
+      case PG_AGG_COUNT: r->values[a] = (double)nd; break;
+      case PG_AGG_MIN: case PG_AGG_MAX: {
+        /* dictionary: its first / last value; raw column: the column metadata's min / max (getMinValue/getMaxValue) */
+        const int is_min = g->fn == PG_AGG_MIN;
+        double m = is_min ? INFINITY : -INFINITY;
+        if (c->fwd_kind != ORC_FWD_RAW) {
+          if (c->cardinality) m = dict_double(c, is_min ? 0 : (int32_t)c->cardinality - 1);
+        } else {
+          for (uint32_t d = 0; d < c->num_docs; d++) {
+            const double v = dict_double(c, (int32_t)d);
+            m = is_min ? (v < m ? v : m) : (v > m ? v : m);
+          }
+        }
+        r->values[a] = m;
+        break;
+      }
+      default:
+        for (uint32_t id = 0; id < c->cardinality; id++) {
+          r->distinct_group_agg[r->num_distinct] = a;
+          r->distinct_dict_ids[r->num_distinct++] = (int32_t)id;
+        }
+        r->values[a] = (double)c->cardinality;
+        break;
+    }
+  }
+  r->stats.num_docs_scanned = nd;
+  r->stats.num_total_docs = nd;
+  r->stats.num_segments_processed = 1;
+  r->stats.num_segments_matched = nd > 0;
+}
+
 /* ------------------------------------------------------------------ entry points */
 
 /* Execute `plan` on ONE segment (segment index `seg` of the plan), columns indexed by col_id.
@@ -591,6 +711,14 @@ int orc_execute_segment(const pg_plan *plan, uint32_t seg, const orc_column *col
   orc_segment_result *r = (orc_segment_result *)calloc(1, sizeof(orc_segment_result));
   r->num_keys = plan->num_keys;
   r->num_aggs = plan->num_aggs;
+  int dict_ok = 1;  /* DISTINCTCOUNT needs the dictionary (DICTIONARY_BASED_FUNCTIONS) */
+  for (uint32_t a = 0; a < plan->num_aggs; a++)
+    if (plan->aggs[a].fn == PG_AGG_DISTINCTCOUNT && cols[plan->aggs[a].col_a].fwd_kind == ORC_FWD_RAW) dict_ok = 0;
+  if (dict_ok && orc_non_scan_fit(plan) && filter_is_match_all(plan, s->leaves)) {
+    non_scan_aggregate(plan, cols, nd, r);
+    *out = r;
+    return 0;
+  }
   uint8_t *match = (uint8_t *)malloc(nd ? nd : 1);
   uint64_t scanned = 0;
   eval_filter(plan, s->leaves, cols, nd, match, &scanned);

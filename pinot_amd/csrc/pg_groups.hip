@@ -121,7 +121,8 @@ __global__ void final_values_kernel(StateView v, FinalSpec f, const uint32_t* __
 // DISTINCTCOUNT a of the groups at `slots`: the popcount of each group's bitmap row (extractFinalResult = set size),
 // read coalesced: `lpg` lanes (a power of two covering the row's words, <= 64) share a row, 64 / lpg rows per wave.
 // One thread per row would read each 128-byte row alone (config 4: 10 M rows took 5.5 ms that way).
-__global__ void dc_sizes_kernel(StateView v, uint32_t dc_word, uint32_t words, uint32_t lpg, const uint32_t* __restrict__ slots,
+__global__ void dc_sizes_kernel(StateView v, uint32_t dc_word, uint32_t words, uint32_t lpg, uint32_t vec4,
+                                const uint32_t* __restrict__ slots,
                                 uint64_t n, uint32_t A, uint32_t a, double* __restrict__ vals, int64_t* __restrict__ cnts) {
   const uint32_t lane = threadIdx.x & 63u, sub = lane & (lpg - 1u);
   const uint64_t per_wave = 64u / lpg;
@@ -132,7 +133,14 @@ __global__ void dc_sizes_kernel(StateView v, uint32_t dc_word, uint32_t words, u
     uint32_t pc = 0;
     if (i < n) {
       const uint32_t* w = v.bits + (uint64_t)slots[i] * v.bit_words + dc_word;
-      for (uint32_t k = sub; k < words; k += lpg) pc += __popc(w[k]);
+      if (vec4) {  // 16-byte aligned rows: 4 words per lane per load
+        for (uint32_t k = 4 * sub; k < words; k += 4 * lpg) {
+          const uint4 x = *(const uint4*)(w + k);
+          pc += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+        }
+      } else {
+        for (uint32_t k = sub; k < words; k += lpg) pc += __popc(w[k]);
+      }
     }
     for (uint32_t o = 1; o < lpg; o <<= 1) pc += __shfl_xor(pc, o);
     if (i < n && sub == 0) {
@@ -151,11 +159,14 @@ hipError_t launch_final_values(const StateView& v, const FinalSpec& f, const uin
   for (uint32_t a = 0; a < f.num_aggs; a++) {
     if (f.aggs[a].fn != PG_AGG_DISTINCTCOUNT) continue;
     const uint32_t words = bits_words(f.aggs[a].key_card);
+    // whole uint4 loads when every row and this aggregation's words start 16-byte aligned and fill whole uint4s
+    const uint32_t vec4 = (v.bit_words % 4 == 0 && f.aggs[a].dc_word % 4 == 0 && words % 4 == 0) ? 1u : 0u;
+    const uint32_t per_lane = vec4 ? 4u : 1u;
     uint32_t lpg = 1;
-    while (lpg < words && lpg < 64) lpg <<= 1;
+    while (lpg * per_lane < words && lpg < 64) lpg <<= 1;
     const uint64_t waves = (n * lpg + 63) / 64, b2 = (waves + 3) / 4;
     hipLaunchKernelGGL(dc_sizes_kernel, dim3((uint32_t)(b2 < 16384 ? b2 : 16384)), dim3(256), 0, s, v,
-                       f.aggs[a].dc_word, words, lpg, slots, n, f.num_aggs, a, vals, cnts);
+                       f.aggs[a].dc_word, words, lpg, vec4, slots, n, f.num_aggs, a, vals, cnts);
   }
   return hipGetLastError();
 }

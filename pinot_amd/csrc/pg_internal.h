@@ -38,7 +38,7 @@ constexpr int kLdsSetBytes = 16 * 1024;              // LDS filter bitmaps of IN
 constexpr int kLdsStageBytes = 32 * 1024;            // LDS tiles of densely read packed columns (per ring buffer)
 constexpr int kMaxStaged = 6;                        // packed columns staged per tile
 constexpr int kNoSlot = 255;
-constexpr uint32_t kPollTiles = 8;                   // scan tiles between polls of the cancel / deadline flag
+constexpr uint32_t kPollTiles = 2;                   // scan tiles between polls of the cancel / deadline flag
 
 // Filter program as the kernel runs it: a tree in prefix form (host-compiled from the ABI's postfix program,
 // AND children ordered most-selective first so later children are evaluated only on surviving docs).
@@ -58,7 +58,8 @@ enum LeafKind : uint32_t {
   LK_RANGE = 2,      // dictId in [lo,hi), dictIds unpacked from a packed SV forward index
   LK_SET_LDS = 3,    // dictId in set: LDS filter bitmap staged per segment (+ exact global LUT when coarse)
   LK_SET_LUT = 4,    // dictId in set: bit dictId of `aux` (global LSB-first words)
-  LK_DOCRANGE = 6    // doc id in [lo,hi)
+  LK_DOCRANGE = 6,   // doc id in [lo,hi)
+  LK_RAW = 7         // raw value of the doc (`words` = typed values, rtype) in [ilo, ihi] / (dlo, dhi) / rvals set
 };
 
 struct LeafDesc {
@@ -77,9 +78,16 @@ struct LeafDesc {
   uint32_t shift;
   uint32_t nbw;
   const uint32_t* lut;
+  // LK_RAW: INT / LONG in [ilo, ihi]; FLOAT / DOUBLE in (dlo, dhi) with rflags bit 0 / 1 = inclusive lo / hi; with
+  // nvals > 0, membership in rvals (nvals sorted int64 for INT / LONG, double for FLOAT / DOUBLE)
+  int64_t ilo, ihi;
+  double dlo, dhi;
+  uint32_t rtype, rflags, nvals, pad;
+  const uint32_t* rvals;
 };
 
-// A column as read by aggregation inputs and group keys.
+// A column as read by aggregation inputs and group keys.  `decoded`: `words` is the column's decoded forward index
+// (value - vbase per doc, launch_decode_pack) instead of dictIds, and the "dictionary" is v -> vbase + v.
 struct ColDesc {
   const uint32_t* words;      // packed SV forward words
   const void* dict;           // typed dictionary values
@@ -89,6 +97,9 @@ struct ColDesc {
   uint32_t dtype;             // pg_data_type
   uint32_t card;
   uint32_t wbytes;            // bytes of `words` (buffer-descriptor range)
+  int64_t vbase;
+  uint32_t decoded;
+  uint32_t pad;
 };
 
 struct SegDesc {
@@ -116,13 +127,12 @@ enum SlotKind : uint32_t { SK_NONE = 0, SK_I64 = 1, SK_F64 = 2, SK_MIN = 3, SK_M
 //   GM_HASH_SEG as GM_HASH over (packed key * num_segments + segment), with the first matching doc of every
 //               (segment, key) in first_doc: the per-segment table when numGroupsLimit can truncate a segment
 //               (the runtime then keeps, per segment, the limit keys seen first and merges them by key).
-//   GM_PART_COUNT / GM_PART_SCATTER  radix-partitioned dense group-by (pg_part.hip) for key spaces whose state is far
-//               larger than any cache: the scan only emits one 32-bit entry per matching doc -- (key low bits, value id)
-//               into the partition of its key's high bits -- with LDS-atomic positions, no global atomics:
-//               COUNT pass: per-(partition, block) entry counts; SCATTER pass (same grid, same docs): the entries at
-//               their block's range of each partition (exclusive scan of the counts).  Level-2 partitioning and the
-//               LDS-resident aggregation of each bucket follow in pg_part.hip; the state they write is GM_DENSE's.
-enum GroupMode : uint32_t { GM_NONE = 0, GM_DENSE = 1, GM_HASH = 2, GM_HASH_SEG = 3, GM_PART_COUNT = 4, GM_PART_SCATTER = 5 };
+//   GM_PART     radix-partitioned dense group-by (pg_part.hip) for key spaces whose state is far larger than any
+//               cache: the scan only appends one 64-bit entry (packed key << part_vbits | value id) per matching doc to
+//               its block's region of an entry array (coalesced, LDS-atomic cursor) and counts it in the block's
+//               histogram of level-1 partitions; pg_part.hip partitions the entries twice (LDS counting sorts,
+//               coalesced runs) and aggregates each bucket in LDS into GM_DENSE's state layout.
+enum GroupMode : uint32_t { GM_NONE = 0, GM_DENSE = 1, GM_HASH = 2, GM_HASH_SEG = 3, GM_PART = 4 };
 constexpr unsigned long long kEmptyKey = 0xFFFFFFFFFFFFFFFFull;
 
 __host__ __device__ inline uint64_t mix64(uint64_t x) {  // murmur3 fmix64 (the HashCommon.mix role)
@@ -198,13 +208,13 @@ struct QuerySpec {
   unsigned long long* seg_matched;  // [seg]
   unsigned int* err;                // device-side violations: bit 0 group key, bit 1 DISTINCTCOUNT key, bit 2 hash table full
   const unsigned int* cancel;       // host-mapped flag polled once per tile (nonzero: stop); null = not cancellable
-  // GM_PART_*: level-1 partition of packed key g = g >> part_shift (< part_nparts); entry = ((g & part_lmask) <<
-  // part_vbits) | value id of aggregation part_dc (0 when part_dc == kNoSlot: COUNT only)
+  // GM_PART: level-1 partition of packed key g = g >> part_shift (< part_nparts); entry = g << part_vbits | value id
+  // of aggregation part_dc (0 when part_dc == kNoSlot: COUNTs only)
   uint32_t part_shift, part_vbits, part_nparts, part_dc;
-  uint32_t part_lmask, pad3;
-  unsigned long long* part_hist;    // [part_nparts][gridDim.x]: COUNT pass writes counts; SCATTER pass reads offsets
-  uint32_t* part_out;               // SCATTER: level-1 entries
-  uint64_t part_cap;                // entries part_out can hold
+  unsigned long long* part_hist;    // [part_nparts][gridDim.x] entries per (level-1 partition, block)
+  unsigned int* part_count;         // [gridDim.x] entries of each block
+  const unsigned long long* part_base;  // [gridDim.x] first entry of each block's region (its docs: an upper bound)
+  unsigned long long* part_out;     // the entry array
 };
 
 // order-preserving int64 image of a double (for MIN/MAX slots)
@@ -229,6 +239,11 @@ hipError_t launch_bswap_words(const uint8_t* src, uint32_t* dst, uint64_t nbytes
 hipError_t launch_be_to_native(const uint8_t* src, void* dst, uint64_t n, uint32_t width, hipStream_t s);
 hipError_t launch_sorted_to_packed(const int32_t* pairs, uint32_t card, uint32_t num_docs, uint32_t bits,
                                    uint32_t* words, uint64_t nwords, hipStream_t s);
+hipError_t launch_decode_pack(const uint32_t* ids, uint32_t bits, const void* dict, uint32_t dtype, uint32_t card,
+                              int64_t vmin, uint32_t vbits, uint32_t num_docs, uint32_t* out, uint64_t nwords,
+                              hipStream_t s);
+hipError_t launch_dict_bits(const void* dict, uint32_t dtype, uint32_t card, int64_t base, const int32_t* keymap,
+                            uint32_t key_card, uint32_t* bits, unsigned int* err, hipStream_t s);
 hipError_t launch_mv_offsets(const uint32_t* bitmap_words, uint64_t num_values, uint32_t num_docs,
                              uint32_t* offsets, void* scratch, size_t scratch_bytes, hipStream_t s);
 size_t mv_offsets_scratch_bytes(uint64_t num_values);
@@ -272,23 +287,26 @@ constexpr uint32_t kPartNB = 32;         // level-2 blocks per level-1 partition
 constexpr uint32_t kPartLdsBytes = 72 * 1024;  // LDS state of one bucket (count + value bitmap per group)
 struct PartSpec {
   uint32_t nparts1, nparts2;       // level-1 partitions, level-2 sub-partitions per level-1 partition
-  uint32_t vbits, shift2;          // value-id bits; key bits below the level-2 digit (log2 groups per bucket)
+  uint32_t vbits, shift1, shift2;  // value-id bits; key bits below the level-1 / level-2 digit (2^shift2 = bucket)
   uint32_t dc_words;               // uint32 words of the value bitmap (0: COUNT only)
   uint32_t row_words, dc_word;     // state bitmap row width / this aggregation's first word (StateView layout)
   uint32_t n_i64;
-  uint32_t blocks1;                // level-1 blocks (the scan grid)
-  uint32_t pad;
+  uint32_t blocks1;                // scan blocks (regions of the 64-bit entry array)
   uint64_t num_groups;             // G (packed key space)
-  const unsigned long long* off1;  // [nparts1 * blocks1 + 1] exclusive offsets of the level-1 counts
-  const uint32_t* in1;             // level-1 entries
+  const unsigned long long* in0;   // scan entries (64-bit), block b's at [base0[b], base0[b] + count0[b])
+  const unsigned long long* base0;
+  const unsigned int* count0;
+  const unsigned long long* off1;  // [nparts1 * blocks1 + 1] exclusive scan of the scan's (partition, block) counts
+  uint32_t* in1;                   // level-1 entries (32-bit: key below the level-1 digit << vbits | value id)
   unsigned long long* hist2;       // [nparts1 * nparts2 * kPartNB + 1] level-2 counts (last = 0)
   const unsigned long long* off2;  // their exclusive scan: bucket b's entries start at off2[b * kPartNB]
   uint32_t* out2;                  // level-2 entries, bucket-major
   unsigned long long* i64;         // dense state written by the bucket pass
   uint32_t* bits;
 };
+hipError_t launch_part_split1(const PartSpec& p, hipStream_t s);
 hipError_t launch_part_count2(const PartSpec& p, hipStream_t s);
-hipError_t launch_part_scatter2(const PartSpec& p, hipStream_t s);
+hipError_t launch_part_split2(const PartSpec& p, hipStream_t s);
 hipError_t launch_part_aggregate(const PartSpec& p, hipStream_t s);
 
 // ---- group state (pg_groups.hip)

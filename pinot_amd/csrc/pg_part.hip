@@ -6,25 +6,28 @@
 // -> DefaultGroupByExecutor.aggregate -> DistinctCountAggregationFunction.aggregateGroupBySV, :131-190: one
 // RoaringBitmap add per doc in the group's holder) is a random update of a huge table.  On MI355X a global atomic
 // executes at the memory side (MI355X_MICROARCH.md, Global atomics), so one random atomic per doc runs at the
-// atomic rate, not at HBM bandwidth (r02_v1: 90.7 ms for 1 B docs).  Instead the docs are radix-partitioned by key
-// with plain, coalescable stores and each bucket is aggregated in LDS:
+// atomic rate, not at HBM bandwidth (r02_v1: 90.7 ms for 1 B docs), and scattered 4-byte stores are bound by the
+// request rate the same way.  So every pass here moves whole runs:
 //
-//   scan pass 1 (pg_scan.hip, GM_PART_COUNT)   per (level-1 partition, block): matched-doc counts   (LDS atomics)
-//   exclusive scan                              -> every block's private range of every partition
-//   scan pass 2 (GM_PART_SCATTER)               32-bit entry (key low bits | value id) per matched doc, appended
-//                                               to its block's range of its partition (LDS-atomic cursor)
-//   part_count2 / exclusive scan / part_scatter2   the same one level down: kPartNB blocks per level-1 partition
-//   part_aggregate                              one workgroup per bucket of 2^shift2 groups: count + value bitmap
-//                                               in LDS (LDS atomics), then the bucket's rows of the dense state
-//                                               written once, coalesced (every slot, so no state memset is needed)
+//   scan (pg_scan.hip, GM_PART)  one 64-bit entry (key << vbits | value id) per matched doc appended to its block's
+//                                region (consecutive words per wave) + the block's level-1 histogram (LDS atomics)
+//   exclusive scan               -> each block's output range in every level-1 partition
+//   part_split1                  per scan block, chunks of kSplitChunk entries counting-sorted by level-1 digit in
+//                                LDS, each digit's run written at once (32-bit entries: key below the digit | value)
+//   part_count2 / scan / part_split2   the same one level down, kPartNB blocks per level-1 partition
+//   part_aggregate               one workgroup per bucket of 2^shift2 groups: count + value bitmap in LDS (LDS
+//                                atomics), then the bucket's rows of the dense state written once, coalesced (every
+//                                slot is written, so the state needs no memset)
 //
-// Bytes per matched doc: key + value columns once per scan pass (the key column twice), then 4 B written / 4 B read
-// per level, + the state rows once.  No global atomics anywhere; no MFMA (nothing is a contraction).
+// No global atomics anywhere; no MFMA (nothing is a contraction).  Bytes per matched doc: the key + value columns
+// once (scan) + 8 written / 8 read (scan entries) + 4 / 4 twice (levels 1, 2) + 4 read (count2) + state rows once.
 #include <hip/hip_runtime.h>
 
 #include "pg_internal.h"
 
 namespace pg {
+
+constexpr uint32_t kSplitChunk = 4096;  // entries counting-sorted per LDS round (16 per thread): longer runs per digit
 
 // Entries of level-1 partition p handled by level-2 block j (of kPartNB): [lo, hi).
 __device__ __forceinline__ void l2_range(const PartSpec& P, uint32_t p, uint32_t j, uint64_t& lo, uint64_t& hi) {
@@ -34,9 +37,90 @@ __device__ __forceinline__ void l2_range(const PartSpec& P, uint32_t p, uint32_t
   hi = s + n * (j + 1) / kPartNB;
 }
 
-// Level-2 digit of an entry: key bits [shift2, shift1) (the entry keeps the key below the level-1 digit).
+// Level-2 digit of a 32-bit entry: key bits [shift2, shift1).
 __device__ __forceinline__ uint32_t digit2(const PartSpec& P, uint32_t e) {
   return (e >> (P.vbits + P.shift2)) & (P.nparts2 - 1u);
+}
+
+// One LDS counting-sort round: the block's `n` (<= kSplitChunk) entries `e[k]` with digits `dg[k]` (thread t holds
+// chunk entries t + 256k) go to out[cur[digit]++] as one run per digit.  cur[] = the block's next output position per
+// digit (LDS, advanced here).  LDS: cnt/start [ndig] + sorted entries + their digits.
+template <class Out>
+__device__ __forceinline__ void split_round(uint32_t (&e)[kSplitChunk / 256], uint32_t (&dg)[kSplitChunk / 256],
+                                            uint32_t n, uint32_t ndig, uint32_t* cnt, uint32_t* start,
+                                            unsigned long long* cur, uint32_t* sbuf, uint16_t* sdig, Out* out) {
+  constexpr int E = kSplitChunk / 256;
+  const uint32_t tid = threadIdx.x;
+  uint32_t rank[E];
+#pragma unroll
+  for (int k = 0; k < E; k++) rank[k] = tid + 256u * k < n ? atomicAdd(&cnt[dg[k]], 1u) : 0u;
+  __syncthreads();
+  // exclusive scan of cnt over the digits (ndig <= 256: one per thread) -> start; reserve the runs
+  {
+    uint32_t c = tid < ndig ? cnt[tid] : 0u, x = c;
+    const uint32_t lane = tid & 63u, wave = tid >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    __shared__ uint32_t wsum[4];
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint32_t wb = 0;
+    for (uint32_t w = 0; w < wave; w++) wb += wsum[w];
+    if (tid < ndig) {
+      start[tid] = wb + x - c;
+      cnt[tid] = 0;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < E; k++)
+    if (tid + 256u * k < n) {
+      const uint32_t at = start[dg[k]] + rank[k];
+      sbuf[at] = e[k];
+      sdig[at] = (uint16_t)dg[k];
+    }
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += 256) {
+    const uint32_t d = sdig[i];
+    out[cur[d] + (i - start[d])] = (Out)sbuf[i];
+  }
+  __syncthreads();
+  // advance the cursors by this round's run lengths (start[d+1] - start[d])
+  if (tid < ndig) cur[tid] += (tid + 1 < ndig ? start[tid + 1] : n) - start[tid];
+  __syncthreads();
+}
+
+// Level 1: scan block b's entries -> level-1 partitions (its range of each starts at off1[p * blocks1 + b]).
+__global__ __launch_bounds__(256) void part_split1_kernel(PartSpec P) {
+  constexpr int E = kSplitChunk / 256;
+  __shared__ uint32_t cnt[kPartL1], start[kPartL1], sbuf[kSplitChunk];
+  __shared__ unsigned long long cur[kPartL1];
+  __shared__ uint16_t sdig[kSplitChunk];
+  const uint32_t b = blockIdx.x, tid = threadIdx.x;
+  if (tid < P.nparts1) {
+    cnt[tid] = 0;
+    cur[tid] = P.off1[(uint64_t)tid * P.blocks1 + b];
+  }
+  __syncthreads();
+  const unsigned long long* __restrict__ in = P.in0 + P.base0[b];
+  const uint32_t n = P.count0[b];
+  const uint32_t sh = P.vbits + P.shift1;
+  const uint64_t lmask = (1ull << P.shift1) - 1ull, vmask = (1ull << P.vbits) - 1ull;
+  for (uint32_t c0 = 0; c0 < n; c0 += kSplitChunk) {
+    const uint32_t m = min(kSplitChunk, n - c0);
+    uint32_t e[E], dg[E];
+#pragma unroll
+    for (int k = 0; k < E; k++) {
+      const uint32_t i = tid + 256u * k;
+      const uint64_t x = i < m ? in[c0 + i] : 0ull;
+      dg[k] = (uint32_t)(x >> sh);
+      e[k] = (uint32_t)((((x >> P.vbits) & lmask) << P.vbits) | (x & vmask));
+    }
+    split_round(e, dg, m, P.nparts1, cnt, start, cur, sbuf, sdig, P.in1);
+  }
 }
 
 // Counts of the level-2 digits in block (j, p)'s range -> hist2[(p * nparts2 + digit) * kPartNB + j].
@@ -61,28 +145,31 @@ __global__ __launch_bounds__(256) void part_count2_kernel(PartSpec P) {
   for (uint32_t d = tid; d < P.nparts2; d += 256) P.hist2[((uint64_t)p * P.nparts2 + d) * kPartNB + j] = h[d];
 }
 
-// The same ranges again: every entry to its block's next position of its bucket (offsets = exclusive scan of hist2).
-__global__ __launch_bounds__(256) void part_scatter2_kernel(PartSpec P) {
-  extern __shared__ uint32_t cur[];  // [nparts2]
+// Level 2: the same ranges, counting-sorted by level-2 digit into buckets (bucket p * nparts2 + d).
+__global__ __launch_bounds__(256) void part_split2_kernel(PartSpec P) {
+  constexpr int E = kSplitChunk / 256;
+  __shared__ uint32_t cnt[256], start[256], sbuf[kSplitChunk];
+  __shared__ unsigned long long cur[256];
+  __shared__ uint16_t sdig[kSplitChunk];
   const uint32_t j = blockIdx.x, p = blockIdx.y, tid = threadIdx.x;
-  for (uint32_t d = tid; d < P.nparts2; d += 256)
-    cur[d] = (uint32_t)P.off2[((uint64_t)p * P.nparts2 + d) * kPartNB + j];
+  if (tid < P.nparts2) {
+    cnt[tid] = 0;
+    cur[tid] = P.off2[((uint64_t)p * P.nparts2 + tid) * kPartNB + j];
+  }
   __syncthreads();
   uint64_t lo, hi;
   l2_range(P, p, j, lo, hi);
   const uint32_t* __restrict__ in = P.in1;
-  uint32_t* __restrict__ out = P.out2;
-  uint64_t i = lo + tid;
-  for (; i + 768 < hi; i += 1024) {
-    const uint32_t e0 = in[i], e1 = in[i + 256], e2 = in[i + 512], e3 = in[i + 768];
-    out[atomicAdd(&cur[digit2(P, e0)], 1u)] = e0;
-    out[atomicAdd(&cur[digit2(P, e1)], 1u)] = e1;
-    out[atomicAdd(&cur[digit2(P, e2)], 1u)] = e2;
-    out[atomicAdd(&cur[digit2(P, e3)], 1u)] = e3;
-  }
-  for (; i < hi; i += 256) {
-    const uint32_t e = in[i];
-    out[atomicAdd(&cur[digit2(P, e)], 1u)] = e;
+  for (uint64_t c0 = lo; c0 < hi; c0 += kSplitChunk) {
+    const uint32_t m = (uint32_t)min((uint64_t)kSplitChunk, hi - c0);
+    uint32_t e[E], dg[E];
+#pragma unroll
+    for (int k = 0; k < E; k++) {
+      const uint32_t i = tid + 256u * k;
+      e[k] = i < m ? in[c0 + i] : 0u;
+      dg[k] = digit2(P, e[k]);
+    }
+    split_round(e, dg, m, P.nparts2, cnt, start, cur, sbuf, sdig, P.out2);
   }
 }
 
@@ -101,13 +188,16 @@ __global__ __launch_bounds__(256) void part_aggregate_kernel(PartSpec P) {
   const uint32_t* __restrict__ in = P.out2;
   uint64_t i = lo + tid;
   if (dw) {
-    for (; i + 256 < hi; i += 512) {
-      const uint32_t e0 = in[i], e1 = in[i + 256];
-      const uint32_t g0 = (e0 >> vb) & gm, v0 = e0 & vm, g1 = (e1 >> vb) & gm, v1 = e1 & vm;
-      atomicAdd(&cnt[g0], 1u);
-      atomicOr(&bm[g0 * dw + (v0 >> 5)], 1u << (v0 & 31u));
-      atomicAdd(&cnt[g1], 1u);
-      atomicOr(&bm[g1 * dw + (v1 >> 5)], 1u << (v1 & 31u));
+    for (; i + 768 < hi; i += 1024) {  // four independent loads in flight per lane
+      uint32_t e[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) e[k] = in[i + 256 * k];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t g = (e[k] >> vb) & gm, v = e[k] & vm;
+        atomicAdd(&cnt[g], 1u);
+        atomicOr(&bm[g * dw + (v >> 5)], 1u << (v & 31u));
+      }
     }
     for (; i < hi; i += 256) {
       const uint32_t e = in[i];
@@ -132,12 +222,16 @@ __global__ __launch_bounds__(256) void part_aggregate_kernel(PartSpec P) {
   }
 }
 
+hipError_t launch_part_split1(const PartSpec& p, hipStream_t s) {
+  hipLaunchKernelGGL(part_split1_kernel, dim3(p.blocks1), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
 hipError_t launch_part_count2(const PartSpec& p, hipStream_t s) {
   hipLaunchKernelGGL(part_count2_kernel, dim3(kPartNB, p.nparts1), dim3(256), p.nparts2 * 4, s, p);
   return hipGetLastError();
 }
-hipError_t launch_part_scatter2(const PartSpec& p, hipStream_t s) {
-  hipLaunchKernelGGL(part_scatter2_kernel, dim3(kPartNB, p.nparts1), dim3(256), p.nparts2 * 4, s, p);
+hipError_t launch_part_split2(const PartSpec& p, hipStream_t s) {
+  hipLaunchKernelGGL(part_split2_kernel, dim3(kPartNB, p.nparts1), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 hipError_t launch_part_aggregate(const PartSpec& p, hipStream_t s) {

@@ -187,7 +187,7 @@ struct PinnedBuf {
   }
 };
 
-enum FwdKind : uint32_t { FWD_NONE = 0, FWD_SV = 1, FWD_SORTED = 2, FWD_MV = 3 };
+enum FwdKind : uint32_t { FWD_NONE = 0, FWD_SV = 1, FWD_SORTED = 2, FWD_MV = 3, FWD_RAW = 4 };
 
 struct ColumnRes {
   // dictionary
@@ -209,7 +209,41 @@ struct ColumnRes {
   // keymap
   bool has_keymap = false;
   DevBuf keymap;
+  // decoded forward index (value - imin, vbits bits per doc) of a large INT / LONG dictionary, built once both the
+  // dictionary and the SV forward index are resident (launch_decode_pack); read by group keys and aggregation
+  // inputs in place of dictId + dictionary gather
+  DevBuf vals;
+  uint32_t vbits = 0;
+  // raw (no-dictionary) forward index: the num_docs values, native typed (dtype), decoded from the chunks at upload
+  DevBuf rawv;
 };
+
+// Dictionaries at least this large get a decoded forward index (PG_DECODED=0 disables, =1 builds it for every
+// INT / LONG dictionary): below it the dictionary stays cache-resident and the gather is cheap.
+constexpr uint32_t kDecodeMinCard = 1u << 17;
+
+// Build c.vals when c has an INT / LONG dictionary of >= kDecodeMinCard values and an SV bit-packed forward index.
+int build_decoded(ColumnRes& c, hipStream_t s) {
+  static const char* env = getenv("PG_DECODED");
+  const int mode = env ? atoi(env) : -1;
+  c.vals.reset();
+  c.vbits = 0;
+  if (mode == 0 || !c.has_dict || c.fwd != FWD_SV || (c.dtype != PG_INT && c.dtype != PG_LONG) || !c.card ||
+      !c.num_docs || (mode != 1 && c.card < kDecodeMinCard))
+    return PG_OK;
+  const uint64_t span = (uint64_t)(c.imax - c.imin);
+  if (c.imax < c.imin || span >= (1ull << 32)) return PG_OK;
+  uint32_t vb = 1;
+  while (vb < 32 && (span >> vb)) vb++;
+  const uint64_t nwords = ((uint64_t)c.num_docs * vb + 31) / 32 + 4;
+  int rc;
+  if ((rc = c.vals.alloc(nwords * 4))) return rc;
+  HIP_CHECK(launch_decode_pack((const uint32_t*)c.words.p, c.bits, c.dict.p, c.dtype, c.card, c.imin, vb, c.num_docs,
+                               (uint32_t*)c.vals.p, nwords, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  c.vbits = vb;
+  return PG_OK;
+}
 
 struct SegmentRes {
   std::unordered_map<uint32_t, ColumnRes> cols;
@@ -379,6 +413,99 @@ int parse_inverted(const std::vector<uint8_t>& b, uint32_t card, std::vector<uin
   return PG_OK;
 }
 
+// Snappy block decompression (ChunkCompressionType.SNAPPY chunks): varint uncompressed length, then literal / copy
+// elements (copies may overlap their own output).  Upload-time format conversion, as the byte swaps above.
+int snappy_decode(const uint8_t* p, uint64_t n, std::vector<uint8_t>& out) {
+  uint64_t pos = 0, len = 0;
+  for (int shift = 0;; shift += 7) {
+    if (pos >= n || shift > 35) return fail(PG_E_INVALID, "snappy: bad length header");
+    const uint8_t b = p[pos++];
+    len |= (uint64_t)(b & 0x7F) << shift;
+    if (b < 0x80) break;
+  }
+  out.clear();
+  out.reserve(len);
+  while (pos < n) {
+    const uint8_t tag = p[pos++];
+    uint64_t ln, off = 0;
+    if ((tag & 3) == 0) {
+      ln = tag >> 2;
+      if (ln >= 60) {
+        const uint32_t nb = (uint32_t)ln - 59;
+        if (pos + nb > n) return fail(PG_E_INVALID, "snappy: truncated literal length");
+        ln = 0;
+        for (uint32_t k = 0; k < nb; k++) ln |= (uint64_t)p[pos + k] << (8 * k);
+        pos += nb;
+      }
+      ln += 1;
+      if (pos + ln > n) return fail(PG_E_INVALID, "snappy: truncated literal");
+      out.insert(out.end(), p + pos, p + pos + ln);
+      pos += ln;
+      continue;
+    }
+    if ((tag & 3) == 1) {
+      if (pos + 1 > n) return fail(PG_E_INVALID, "snappy: truncated copy");
+      ln = ((tag >> 2) & 7) + 4;
+      off = ((uint64_t)(tag >> 5) << 8) | p[pos];
+      pos += 1;
+    } else {
+      const uint32_t nb = (tag & 3) == 2 ? 2 : 4;
+      if (pos + nb > n) return fail(PG_E_INVALID, "snappy: truncated copy");
+      ln = (tag >> 2) + 1;
+      for (uint32_t k = 0; k < nb; k++) off |= (uint64_t)p[pos + k] << (8 * k);
+      pos += nb;
+    }
+    if (off == 0 || off > out.size()) return fail(PG_E_INVALID, "snappy: copy offset out of range");
+    for (uint64_t k = 0; k < ln; k++) out.push_back(out[out.size() - off]);
+  }
+  if (out.size() != len) return fail(PG_E_INVALID, "snappy: %zu bytes decoded, %llu expected", out.size(), (unsigned long long)len);
+  return PG_OK;
+}
+
+// A raw chunked forward index (BaseChunkForwardIndexReader.java:56-102 header; FixedByteChunkSVForwardIndexReader /
+// FixedBytePower2ChunkSVForwardIndexReader per-doc reads) -> the big-endian values of docs [0, num_docs).
+int raw_forward_values(const std::vector<uint8_t>& b, uint32_t width, uint32_t num_docs, std::vector<uint8_t>& out) {
+  if (b.size() < 16) return fail(PG_E_INVALID, "raw forward index: %zu-byte header", b.size());
+  const uint32_t version = rd_be32(&b[0]), num_chunks = rd_be32(&b[4]), per_chunk = rd_be32(&b[8]), entry = rd_be32(&b[12]);
+  if (entry != width) return fail(PG_E_INVALID, "raw forward index: entry size %u != %u", entry, width);
+  uint32_t comp = 1 /* SNAPPY */, data_start = 16;
+  if (version > 1) {
+    if (b.size() < 28) return fail(PG_E_INVALID, "raw forward index: short v%u header", version);
+    comp = rd_be32(&b[20]);
+    data_start = rd_be32(&b[24]);
+  }
+  if (version < 1 || version > 4) return fail(PG_E_UNSUPPORTED, "raw forward index version %u", version);
+  const uint32_t osz = version <= 2 ? 4 : 8;
+  const uint64_t raw_start = (uint64_t)data_start + (uint64_t)num_chunks * osz;
+  if (raw_start > b.size()) return fail(PG_E_INVALID, "raw forward index: chunk table past the buffer");
+  out.assign((uint64_t)num_docs * width, 0);
+  if (comp == 0) {  // PASS_THROUGH: the chunks are the contiguous values
+    if (raw_start + out.size() > b.size()) return fail(PG_E_INVALID, "raw forward index: %u docs past the buffer", num_docs);
+    memcpy(out.data(), &b[raw_start], out.size());
+    return PG_OK;
+  }
+  if (comp != 1) return fail(PG_E_UNSUPPORTED, "raw forward index: chunk compression %u (only PASS_THROUGH / SNAPPY)", comp);
+  std::vector<uint8_t> chunk;
+  uint64_t at = 0;
+  for (uint32_t k = 0; k < num_chunks && at < out.size(); k++) {
+    auto off = [&](uint32_t i) -> uint64_t {
+      const uint8_t* q = &b[data_start + (uint64_t)i * osz];
+      return osz == 4 ? rd_be32(q) : ((uint64_t)rd_be32(q) << 32) | rd_be32(q + 4);
+    };
+    const uint64_t s0 = off(k), e0 = k + 1 < num_chunks ? off(k + 1) : b.size();
+    if (s0 > e0 || e0 > b.size()) return fail(PG_E_INVALID, "raw forward index: bad chunk %u", k);
+    int rc = snappy_decode(&b[s0], e0 - s0, chunk);
+    if (rc) return rc;
+    const uint64_t take = std::min<uint64_t>(chunk.size(), out.size() - at);
+    if (chunk.size() < std::min<uint64_t>((uint64_t)per_chunk * width, out.size() - at))
+      return fail(PG_E_INVALID, "raw forward index: chunk %u holds %zu bytes", k, chunk.size());
+    memcpy(&out[at], chunk.data(), take);
+    at += take;
+  }
+  if (at < out.size()) return fail(PG_E_INVALID, "raw forward index: %llu of %u docs", (unsigned long long)(at / width), num_docs);
+  return PG_OK;
+}
+
 int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const void* src, uint64_t nbytes) {
   const bool on_dev = (d->flags & PG_SRC_DEVICE) != 0;
   hipStream_t s = thread_stream();
@@ -502,6 +629,38 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
       HIP_CHECK(hipStreamSynchronize(s));
       break;
     }
+    case PG_IDX_FWD_SV_RAW: {
+      if (d->data_type > PG_DOUBLE) return fail(PG_E_UNSUPPORTED, "raw forward index of type %u (fixed-width only)", d->data_type);
+      const uint32_t w = d->data_type == PG_INT || d->data_type == PG_FLOAT ? 4 : 8;
+      std::vector<uint8_t> hb, be;
+      if ((rc = host_copy(src, nbytes, on_dev, hb))) return rc;
+      if ((rc = raw_forward_values(hb, w, d->num_docs, be))) return rc;
+      tmp.fwd = FWD_RAW;
+      tmp.num_docs = d->num_docs;
+      tmp.num_values = d->num_docs;
+      tmp.dtype = d->data_type;
+      tmp.card = d->cardinality;
+      // column metadata min / max (ColumnMetadata.getMinValue / getMaxValue): integer-exact SUM bounds, non-scan MIN/MAX
+      tmp.dmin = INFINITY;
+      tmp.dmax = -INFINITY;
+      tmp.imin = INT64_MAX;
+      tmp.imax = INT64_MIN;
+      for (uint32_t i = 0; i < d->num_docs; i++) {
+        const double v = be_value_as_double(&be[(uint64_t)i * w], d->data_type);
+        tmp.dmin = std::min(tmp.dmin, v);
+        tmp.dmax = std::max(tmp.dmax, v);
+        if (d->data_type <= PG_LONG) {
+          const int64_t x = be_value_as_i64(&be[(uint64_t)i * w], d->data_type);
+          tmp.imin = std::min(tmp.imin, x);
+          tmp.imax = std::max(tmp.imax, x);
+        }
+      }
+      if ((rc = stage(be.data(), be.size(), false, st, s))) return rc;
+      if ((rc = tmp.rawv.alloc((uint64_t)w * d->num_docs + 16))) return rc;
+      HIP_CHECK(launch_be_to_native((const uint8_t*)st.p, tmp.rawv.p, d->num_docs, w, s));
+      HIP_CHECK(hipStreamSynchronize(s));  // `be` (pageable) is released at the end of this block
+      break;
+    }
     case PG_IDX_KEYMAP: {
       if (nbytes < 4ull * d->cardinality) return fail(PG_E_INVALID, "keymap too small");
       tmp.has_keymap = true;
@@ -548,7 +707,17 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
       c.has_keymap = true;
       c.keymap = std::move(tmp.keymap);
       break;
+    case PG_IDX_FWD_SV_RAW:
+      c.words.reset(); c.mv_offsets.reset(); c.rawv.reset(); c.vals.reset();
+      c.fwd = FWD_RAW; c.num_docs = tmp.num_docs; c.bits = 0; c.num_values = tmp.num_values;
+      c.dtype = tmp.dtype; c.card = tmp.card; c.has_dict = false;
+      c.dmin = tmp.dmin; c.dmax = tmp.dmax; c.imin = tmp.imin; c.imax = tmp.imax;
+      c.rawv = std::move(tmp.rawv);
+      break;
   }
+  if (d->kind == PG_IDX_DICT || d->kind == PG_IDX_FWD_SV_BITPACKED || d->kind == PG_IDX_FWD_SV_SORTED ||
+      d->kind == PG_IDX_FWD_MV_BITPACKED)
+    return build_decoded(c, s);
   return PG_OK;
 }
 
@@ -602,7 +771,7 @@ constexpr uint64_t kStateBudget = 48ull << 30;       // bytes of group state one
 constexpr uint64_t kMaxHashSlots = 1ull << 30;
 constexpr uint64_t kPartMinStateBytes = 64ull << 20;  // radix-partitioned group-by above this much dense state
 
-struct PartPlan {  // GM_PART_* pipeline of one query (pg_part.hip)
+struct PartPlan {  // GM_PART pipeline of one query (pg_part.hip)
   bool on = false;
   uint32_t shift1 = 0, shift2 = 0, vbits = 0, dc_words = 0, dc_word = 0, dc = 0, nparts1 = 0, nparts2 = 1;
 };
@@ -940,6 +1109,48 @@ int truncate_and_merge(Partials& P, uint64_t limit, hipStream_t s) {
   return PG_OK;
 }
 
+// The segment's filter is match-all after FilterPlanNode's pruning (FilterOperatorUtils: AND drops match-all children,
+// OR with a match-all child is match-all, NOT(empty) is match-all): three-valued evaluation of the postfix program.
+bool filter_is_match_all(const pg_plan* plan, const pg_leaf* leaves) {
+  if (!plan->num_ops) return true;
+  std::vector<int> st;
+  for (uint32_t i = 0; i < plan->num_ops; i++) {
+    const int32_t op = plan->ops[i];
+    if (op >= 0) {
+      st.push_back(leaves[op].kind == PG_LEAF_MATCH_ALL ? 1 : leaves[op].kind == PG_LEAF_EMPTY ? 0 : -1);
+    } else if (op == PG_OP_NOT) {
+      st.back() = st.back() < 0 ? -1 : !st.back();
+    } else {
+      const int n = (-op) & 0xFF;
+      const bool is_and = ((-op) & 0x300) == 0x100;
+      int v = is_and ? 1 : 0;
+      for (int k = 0; k < n; k++) {
+        const int x = st[st.size() - 1 - k];
+        if (is_and) v = (v == 0 || x == 0) ? 0 : (v < 0 || x < 0 ? -1 : 1);
+        else v = (v == 1 || x == 1) ? 1 : (v < 0 || x < 0 ? -1 : 0);
+      }
+      st.resize(st.size() - n);
+      st.push_back(v);
+    }
+  }
+  return st.size() == 1 && st[0] == 1;
+}
+
+// Aggregation inputs that only need dictionary VALUES (not dictIds) may read a column's decoded forward index.
+bool agg_decodes(const pg_agg& g) {
+  return g.fn == PG_AGG_SUM || g.fn == PG_AGG_MIN || g.fn == PG_AGG_MAX || g.fn == PG_AGG_AVG ||
+         (g.fn == PG_AGG_DISTINCTCOUNT && g.key_kind == PG_KEY_VALUE_OFFSET);
+}
+void use_decoded(ColDesc& dc, const ColumnRes* c) {
+  dc.words = (const uint32_t*)c->vals.p;
+  dc.wbytes = (uint32_t)std::min<uint64_t>(c->vals.bytes, 0xFFFFFFF0ull);
+  dc.bits = c->vbits;
+  dc.dict = nullptr;
+  dc.card = 0xFFFFFFFFu;
+  dc.vbase = c->imin;
+  dc.decoded = 1;
+}
+
 int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t hash_cap) {
   const double t_enter = wall_ms();
   if (!plan) return fail(PG_E_INVALID, "null plan");
@@ -1070,8 +1281,11 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         if (ca->fwd != FWD_MV) return fail(PG_E_INVALID, "COUNTMV on a single-value column %u", g.col_a);
         continue;
       }
-      if (ca->fwd == FWD_NONE || ca->fwd == FWD_MV || !ca->has_dict)
+      const bool raw_a = ca->fwd == FWD_RAW;
+      if (ca->fwd == FWD_NONE || ca->fwd == FWD_MV || (!ca->has_dict && !raw_a))
         return fail(PG_E_UNSUPPORTED, "aggregation %u: column %u needs an SV forward index + dictionary", a, g.col_a);
+      if (raw_a && g.fn == PG_AGG_DISTINCTCOUNT && g.key_kind != PG_KEY_VALUE_OFFSET)
+        return fail(PG_E_UNSUPPORTED, "DISTINCTCOUNT of raw column %u needs value-offset ids", g.col_a);
       if (g.fn == PG_AGG_DISTINCTCOUNT) {
         if (g.key_kind == PG_KEY_KEYMAP && !ca->has_keymap) return fail(PG_E_NOTFOUND, "DISTINCTCOUNT keymap missing");
         if (g.key_kind != PG_KEY_KEYMAP && g.key_kind != PG_KEY_VALUE_OFFSET) return fail(PG_E_INVALID, "bad key kind");
@@ -1085,7 +1299,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       bound_a = std::max(bound_a, std::max(fabs(ca->dmin), fabs(ca->dmax)));
       if (two) {
         const ColumnRes* cb = col(si, g.col_b);
-        if (!cb || cb->fwd == FWD_NONE || cb->fwd == FWD_MV || !cb->has_dict || cb->dtype > PG_DOUBLE)
+        if (!cb || cb->fwd == FWD_NONE || cb->fwd == FWD_MV || (!cb->has_dict && cb->fwd != FWD_RAW) || cb->dtype > PG_DOUBLE)
           return fail(PG_E_UNSUPPORTED, "aggregation %u: second operand column %u unusable", a, g.col_b);
         all_int &= cb->dtype <= PG_LONG;
         bound_b = std::max(bound_b, std::max(fabs(cb->dmin), fabs(cb->dmax)));
@@ -1171,7 +1385,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       uint32_t sh2 = 0;
       while ((per_group << (sh2 + 1)) <= (uint64_t)kPartLdsBytes) sh2++;
       part.shift2 = std::min(sh2, part.shift1);
-      if (per_group <= (uint64_t)kPartLdsBytes && part.shift1 + part.vbits <= 32 && part.vbits < 32) {
+      if (per_group <= (uint64_t)kPartLdsBytes && part.shift1 + part.vbits <= 32 && part.vbits < 32 &&
+          part.shift1 - part.shift2 <= 8 && gbits + part.vbits <= 64) {
         part.on = true;
         part.dc = dc;
         part.dc_word = dc == (uint32_t)kNoSlot ? 0 : P.aggs[dc].dc_word;
@@ -1228,7 +1443,17 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       const ColumnRes* c = (pl.kind == PG_LEAF_MATCH_ALL || pl.kind == PG_LEAF_EMPTY) ? nullptr : col(si, pl.col_id);
       double f = 1.0, cost = 0.0;
       if (pl.kind == PG_LEAF_EMPTY) f = 0.0;
-      else if (c) {
+      else if (c && pl.kind == PG_LEAF_RAW_SCAN) {
+        // uniform over [min, max] for a range, distinct values ~ cardinality for a set
+        if (pl.num_ids) f = std::min(1.0, pl.num_ids / (double)std::max(1u, c->card));
+        else {
+          const double lo = c->dtype <= PG_LONG ? (double)pl.ilo : pl.dlo, hi = c->dtype <= PG_LONG ? (double)pl.ihi : pl.dhi;
+          const double span = c->dmax - c->dmin;
+          f = span > 0 ? std::max(0.0, std::min(1.0, (std::min(hi, c->dmax) - std::max(lo, c->dmin)) / span)) : 1.0;
+        }
+        if (pl.exclusive) f = 1.0 - f;
+        cost = c->dtype == PG_INT || c->dtype == PG_FLOAT ? 4.0 : 8.0;
+      } else if (c) {
         const double card = std::max(1u, c->card);
         const double nset = pl.num_ids ? pl.num_ids : std::max(0, std::min(pl.hi, (int32_t)c->card) - std::max(pl.lo, 0));
         f = std::min(1.0, nset / card);
@@ -1264,7 +1489,10 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
           pass *= leaf_pass[nodes[k].leaf];
           cost += leaf_cost[nodes[k].leaf];
         }
-      if (!cand.empty() && pf == 1) {
+      bool raw_leaf = false;
+      for (uint32_t li : cand)
+        for (uint32_t si = 0; si < S; si++) raw_leaf |= plan->segments[si].leaves[li].kind == PG_LEAF_RAW_SCAN;
+      if (!cand.empty() && pf == 1 && !raw_leaf) {
         pre_leaves = cand;
         leaf_pass[cand[0]] = pass;
         leaf_cost[cand[0]] = 1.0 / 8;
@@ -1306,16 +1534,47 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   auto scratch_reserve = [&](uint64_t n) { uint64_t at = (scratch_bytes + 255) & ~255ull; scratch_bytes = at + n; return at; };
   uint64_t entries_in_filter = 0;
   // device pointers into arena / scratch are patched once those are allocated
-  enum PatchTarget { PT_AUX = 0, PT_WORDS = 1, PT_LUT = 2 };
+  enum PatchTarget { PT_AUX = 0, PT_WORDS = 1, PT_LUT = 2, PT_RVALS = 3 };
   struct Patch { uint64_t leaf_index; uint64_t off; bool in_arena; int target; bool orig = false; };
   std::vector<Patch> patches;
+
+  // ---- NonScanBasedAggregationOperator route (plan/AggregationPlanNode.java:185-197, :236-261): with no group-by,
+  // a segment whose filter matches all docs and functions that are COUNT or MIN / MAX / DISTINCTCOUNT of a column
+  // with a dictionary is answered from its dictionary instead of scanned (ExecutionStatistics(numTotalDocs, 0, 0,
+  // numTotalDocs), NonScanBasedAggregationOperator.java:253-256).  PG_NONSCAN=0 scans them instead.
+  std::vector<uint8_t> nonscan(S, 0);
+  uint64_t ns_docs = 0, ns_matched = 0;
+  {
+    const char* ns_env = getenv("PG_NONSCAN");
+    bool fit = K == 0 && !(ns_env && atoi(ns_env) == 0);
+    for (uint32_t a = 0; a < A && fit; a++) {
+      const pg_agg& g = plan->aggs[a];
+      if (g.fn == PG_AGG_COUNT) continue;
+      fit = (g.fn == PG_AGG_MIN || g.fn == PG_AGG_MAX || g.fn == PG_AGG_DISTINCTCOUNT) && g.op == PG_EXPR_COL;
+    }
+    for (uint32_t si = 0; si < S && fit; si++) {
+      bool ok = filter_is_match_all(plan, plan->segments[si].leaves);
+      for (uint32_t a = 0; a < A && ok; a++) {
+        const pg_agg& g = plan->aggs[a];
+        if (g.fn == PG_AGG_COUNT) continue;
+        const ColumnRes* c = col(si, g.col_a);
+        // MIN / MAX: dictionary or column metadata (a raw column's min / max); DISTINCTCOUNT: the dictionary
+        ok = c && ((c->has_dict && c->dict.p) || (c->fwd == FWD_RAW && g.fn != PG_AGG_DISTINCTCOUNT)) &&
+             (g.fn != PG_AGG_DISTINCTCOUNT || g.key_kind != PG_KEY_KEYMAP || c->has_keymap);
+      }
+      if (!ok) continue;
+      nonscan[si] = 1;
+      ns_docs += plan->segments[si].num_docs;
+      ns_matched += plan->segments[si].num_docs > 0;
+    }
+  }
 
   std::vector<uint32_t> seg_tiles(S, 0);
   for (uint32_t si = 0; si < S; si++) {
     const pg_segment_ref& sr = plan->segments[si];
     segd[si].num_docs = sr.num_docs;
     segd[si].index = si;
-    seg_tiles[si] = (uint32_t)(((uint64_t)sr.num_docs + kTileDocs - 1) / kTileDocs);
+    seg_tiles[si] = nonscan[si] ? 0u : (uint32_t)(((uint64_t)sr.num_docs + kTileDocs - 1) / kTileDocs);
     for (uint32_t li = 0; li < L; li++) {
       const pg_leaf& pl = sr.leaves[li];
       LeafDesc& dl = leaves[(uint64_t)si * L + li];
@@ -1325,6 +1584,24 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       if (pl.kind == PG_LEAF_EMPTY) { dl.kind = LK_NONE; dl.excl = 0; continue; }
       const ColumnRes* c = col(si, pl.col_id);
       if (!c) return fail(PG_E_NOTFOUND, "leaf %u: column %u not resident in segment %u", li, pl.col_id, si);
+      if (pl.kind == PG_LEAF_RAW_SCAN) {
+        // raw-value predicate over a raw forward index: values gathered per needed doc, compared in their type
+        if (c->fwd != FWD_RAW) return fail(PG_E_INVALID, "raw leaf on column %u without a raw forward index", pl.col_id);
+        if (c->num_docs < sr.num_docs) return fail(PG_E_INVALID, "column %u has %u docs < segment's %u", pl.col_id, c->num_docs, sr.num_docs);
+        if (pl.num_ids && !pl.values) return fail(PG_E_INVALID, "leaf %u: null value list", li);
+        dl.kind = LK_RAW;
+        dl.words = (const uint32_t*)c->rawv.p;
+        dl.rtype = c->dtype;
+        dl.ilo = pl.ilo; dl.ihi = pl.ihi; dl.dlo = pl.dlo; dl.dhi = pl.dhi;
+        dl.rflags = (pl.lo_inclusive ? 1u : 0u) | (pl.hi_inclusive ? 2u : 0u);
+        dl.nvals = pl.num_ids;
+        if (pl.num_ids) {  // int64 (INT / LONG) or double (FLOAT / DOUBLE), sorted: binary search on the device
+          const uint64_t off = ar.put(pl.values, 8ull * pl.num_ids);
+          patches.push_back({(uint64_t)si * L + li, off, true, PT_RVALS});
+        }
+        entries_in_filter += sr.num_docs;
+        continue;
+      }
       if (pl.num_ids && !pl.ids) return fail(PG_E_INVALID, "leaf %u: null id list", li);
       for (uint32_t i = 0; i < pl.num_ids; i++)
         if (pl.ids[i] < 0 || (uint32_t)pl.ids[i] >= std::max(c->card, 1u) || (i && pl.ids[i] <= pl.ids[i - 1]))
@@ -1465,6 +1742,15 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         dc.bits = c->bits;
         dc.dtype = c->dtype;
         dc.card = c->card;
+        if (c->fwd == FWD_RAW) {  // the values themselves: "dictId" = doc id (bits 0), "dictionary" = the values
+          dc.words = nullptr;
+          dc.wbytes = 0;
+          dc.bits = 0;
+          dc.dict = c->rawv.p;
+          dc.card = c->num_docs;
+        } else if (agg_decodes(g) && c->vals.p) {
+          use_decoded(dc, c);
+        }
       }
     }
     for (uint32_t k = 0; k < K; k++) {
@@ -1478,6 +1764,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       dc.bits = c->bits;
       dc.dtype = c->dtype;
       dc.card = c->card;
+      if (plan->keys[k].kind == PG_KEY_VALUE_OFFSET && c->vals.p) use_decoded(dc, c);
     }
   }
   P.entries_in_filter = entries_in_filter;
@@ -1545,7 +1832,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     for (uint32_t a = 0; a < A; a++)
       for (int k = 0; k < 2; k++) {
         const ColDesc& dc = aggcols[((uint64_t)si * A + a) * 2 + k];
-        if (dc.dict) seg_lines = std::max<uint64_t>(seg_lines, (uint64_t)dc.card * (dc.dtype == PG_INT || dc.dtype == PG_FLOAT ? 4 : 8) / 128);
+        if (dc.dict && dc.bits) seg_lines = std::max<uint64_t>(seg_lines, (uint64_t)dc.card * (dc.dtype == PG_INT || dc.dtype == PG_FLOAT ? 4 : 8) / 128);
       }
     for (uint32_t k = 0; k < K; k++) {
       const ColDesc& dc = keycols[(uint64_t)si * K + k];
@@ -1626,6 +1913,16 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       if (!bmax || (scan && bitmap)) continue;  // mixed per-segment forms: gather
       add(0, li, 0, scan ? (1ull << 32) | cid : (2ull << 32) | li, leaf_reach[li], bmax);
     }
+    // aggregation / key uses read the column's decoded forward index in some segment ("decoded" uses: their own
+    // slot, key type 3) or dictIds everywhere (key type 1, shared with scan leaves on the column)
+    auto agg_dec = [&](uint32_t a, int k) {
+      for (uint32_t si = 0; si < S; si++) if (aggcols[((uint64_t)si * A + a) * 2 + k].decoded) return true;
+      return false;
+    };
+    auto key_dec = [&](uint32_t k) {
+      for (uint32_t si = 0; si < S; si++) if (keycols[(uint64_t)si * K + k].decoded) return true;
+      return false;
+    };
     for (uint32_t a = 0; a < A; a++) {
       const pg_agg& g = plan->aggs[a];
       if (g.fn == PG_AGG_COUNT || g.fn == PG_AGG_COUNTMV) continue;
@@ -1633,14 +1930,14 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       for (int k = 0; k < n; k++) {
         const uint32_t cid = k ? g.col_b : g.col_a;
         uint32_t bmax = 0;
-        for (uint32_t si = 0; si < S; si++) bmax = std::max(bmax, col(si, cid)->bits);
-        add(1, a, (uint32_t)k, (1ull << 32) | cid, filter_pass, bmax);
+        for (uint32_t si = 0; si < S; si++) bmax = std::max(bmax, aggcols[((uint64_t)si * A + a) * 2 + k].bits);
+        add(1, a, (uint32_t)k, ((agg_dec(a, k) ? 3ull : 1ull) << 32) | cid, filter_pass, bmax);
       }
     }
     for (uint32_t k = 0; k < K; k++) {
       uint32_t bmax = 0;
-      for (uint32_t si = 0; si < S; si++) bmax = std::max(bmax, col(si, plan->keys[k].col_id)->bits);
-      add(2, k, 0, (1ull << 32) | plan->keys[k].col_id, filter_pass, bmax);
+      for (uint32_t si = 0; si < S; si++) bmax = std::max(bmax, keycols[(uint64_t)si * K + k].bits);
+      add(2, k, 0, ((key_dec(k) ? 3ull : 1ull) << 32) | plan->keys[k].col_id, filter_pass, bmax);
     }
     std::stable_sort(cands.begin(), cands.end(), [](const Cand& x, const Cand& y) { return x.reach > y.reach; });
     memset(q.leaf_slot, kNoSlot, sizeof(q.leaf_slot));
@@ -1652,14 +1949,15 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     uint32_t words = 0;
     for (const Cand& c : cands) {
       if (no_stage || q.num_staged >= (uint32_t)kMaxStaged) break;
+      if (!c.bmax) continue;  // raw values: read per doc (already consecutive words), never staged
       if (c.reach * 1024.0 / c.bmax < stage_min) continue;
       const uint32_t need = (uint32_t)(kTileDocs / 32) * c.bmax;  // b DMA pieces of 1 KiB
       if ((words + need) * 4ull > (uint64_t)kLdsStageBytes) continue;
       const uint32_t slot = q.num_staged++;
       q.staged[slot] = {c.role, c.idx, c.operand, words};
       words += need;
-      // every use of the same column shares the slot
-      for (uint32_t li = 0; li < L; li++) {
+      // every use of the same column (in the same form: dictIds or decoded values) shares the slot
+      for (uint32_t li = 0; li < L && (c.key >> 32) != 3; li++) {
         bool match = false;
         if ((c.key >> 32) == 2) match = li == (uint32_t)c.key;
         else
@@ -1682,16 +1980,18 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
           if (all_col) q.leaf_slot[li] = (uint8_t)slot;
         }
       }
-      if ((c.key >> 32) == 1) {
+      if ((c.key >> 32) == 1 || (c.key >> 32) == 3) {
         const uint32_t cid = (uint32_t)c.key;
+        const bool dec = (c.key >> 32) == 3;
         for (uint32_t a = 0; a < A; a++) {
           const pg_agg& g = plan->aggs[a];
           if (g.fn == PG_AGG_COUNT || g.fn == PG_AGG_COUNTMV) continue;
-          if (g.col_a == cid) q.agg_slot[a][0] = (uint8_t)slot;
-          if (g.op != PG_EXPR_COL && g.fn != PG_AGG_DISTINCTCOUNT && g.col_b == cid) q.agg_slot[a][1] = (uint8_t)slot;
+          if (g.col_a == cid && agg_dec(a, 0) == dec) q.agg_slot[a][0] = (uint8_t)slot;
+          if (g.op != PG_EXPR_COL && g.fn != PG_AGG_DISTINCTCOUNT && g.col_b == cid && agg_dec(a, 1) == dec)
+            q.agg_slot[a][1] = (uint8_t)slot;
         }
         for (uint32_t k = 0; k < K; k++)
-          if (plan->keys[k].col_id == cid) q.key_slot[k] = (uint8_t)slot;
+          if (plan->keys[k].col_id == cid && key_dec(k) == dec) q.key_slot[k] = (uint8_t)slot;
       }
     }
     q.stage_lds_words = words;
@@ -1745,6 +2045,37 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   // ---- device buffers (state + arena + scratch) from the caching pool
   part.on = part.on && q.num_items > 0;
   if ((rc = P.alloc_state(s, !part.on))) return rc;
+  if (ns_docs || ns_matched) {  // the non-scan segments' results seed the state the scan adds to
+    uint64_t* h = (uint64_t*)t_ctx.readback.get(8ull * (1 + 2 * A));
+    if (!h) return fail(PG_E_NOMEM, "pinned staging failed");
+    h[0] = ns_docs;
+    HIP_CHECK(hipMemcpyAsync(P.i64.p, &h[0], 8, hipMemcpyHostToDevice, s));
+    for (uint32_t a = 0; a < A; a++) {
+      const pg_agg& g = plan->aggs[a];
+      if (g.fn != PG_AGG_MIN && g.fn != PG_AGG_MAX) continue;
+      double m = g.fn == PG_AGG_MIN ? INFINITY : -INFINITY;
+      for (uint32_t si = 0; si < S; si++) {
+        if (!nonscan[si]) continue;
+        const ColumnRes* c = col(si, g.col_a);
+        if (c->card || c->fwd == FWD_RAW) m = g.fn == PG_AGG_MIN ? std::min(m, c->dmin) : std::max(m, c->dmax);
+      }
+      h[1 + a] = (uint64_t)order_key(m);
+      void* dst = g.fn == PG_AGG_MIN ? (void*)((long long*)P.mn.p + P.aggs[a].slot) : (void*)((long long*)P.mx.p + P.aggs[a].slot);
+      HIP_CHECK(hipMemcpyAsync(dst, &h[1 + a], 8, hipMemcpyHostToDevice, s));
+    }
+    for (uint32_t a = 0; a < A; a++) {
+      const pg_agg& g = plan->aggs[a];
+      if (g.fn != PG_AGG_DISTINCTCOUNT) continue;
+      for (uint32_t si = 0; si < S; si++) {
+        if (!nonscan[si]) continue;
+        const ColumnRes* c = col(si, g.col_a);
+        HIP_CHECK(launch_dict_bits(c->dict.p, c->dtype, c->card, g.key_base,
+                                   g.key_kind == PG_KEY_KEYMAP ? (const int32_t*)c->keymap.p : nullptr, g.key_cardinality,
+                                   (uint32_t*)P.bits.p + P.aggs[a].dc_word, (unsigned int*)P.misc.p + 1, s));
+      }
+    }
+    HIP_CHECK(hipStreamSynchronize(s));  // the pinned staging words are reused below
+  }
   if ((rc = P.seg_matched.alloc_pooled(8ull * (S ? S : 1) + 16))) return rc;
   HIP_CHECK(hipMemsetAsync(P.seg_matched.p, 0, 8ull * (S ? S : 1) + 16, s));
   {
@@ -1795,9 +2126,26 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     }
   }
   const uint64_t off_items = ar.put(items.data(), items.size() * sizeof(WorkItem));
+  // GM_PART: each block's region of the entry array = the docs of its items (the kernel's [i0, i1) item range)
+  uint64_t off_part_base = 0, part_entries = 0;
+  if (part.on && blocks) {
+    std::vector<uint64_t> base(blocks + 1, 0);
+    for (uint32_t b = 0; b < blocks; b++) {
+      const uint64_t i0 = (uint64_t)b * items.size() / blocks, i1 = (uint64_t)(b + 1) * items.size() / blocks;
+      uint64_t n = 0;
+      for (uint64_t i = i0; i < i1; i++) {
+        const WorkItem& it = items[i];
+        const uint64_t nd = plan->segments[it.seg].num_docs;
+        n += std::min<uint64_t>((uint64_t)it.tile_end * kTileDocs, nd) - std::min<uint64_t>((uint64_t)it.tile_begin * kTileDocs, nd);
+      }
+      base[b + 1] = base[b] + n;
+    }
+    part_entries = base[blocks];
+    off_part_base = ar.put(base.data(), base.size() * 8);
+  }
   const uint64_t off_lutjobs = ar.reserve(luts.size() * sizeof(LutJob));
   DevBuf arena, scratch;
-  DevBuf p_hist1, p_off1, p_ent1, p_hist2, p_off2, p_ent2, p_temp;  // GM_PART_* pipeline
+  DevBuf p_ent0, p_cnt0, p_hist1, p_off1, p_ent1, p_hist2, p_off2, p_ent2, p_temp;  // GM_PART pipeline
   // declared after the buffers it protects: on any exit, wait for queued work before they return to the pool
   struct SyncOnExit {
     hipStream_t s;
@@ -1812,6 +2160,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     const uint32_t* ptr = (const uint32_t*)((p.in_arena ? dA : dS) + p.off);
     if (p.target == PT_WORDS) dl.words = ptr;
     else if (p.target == PT_LUT) dl.lut = ptr;
+    else if (p.target == PT_RVALS) dl.rvals = ptr;
     else dl.aux = ptr;
   }
   for (uint32_t si = 0; si < S; si++) {
@@ -1888,12 +2237,14 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   CancelSlot cancel(plan->query_id, plan->query_id != 0 || plan->deadline_ms != 0);
   q.cancel = cancel.device_ptr();
   if (q.num_items && part.on) {
-    // radix-partitioned group-by (pg_part.hip): count pass, exclusive scan, scatter pass, level 2, buckets
+    // radix-partitioned group-by (pg_part.hip): scan appends entries + level-1 histogram, scan of the histogram,
+    // level-1 split, level-2 count / scan / split, per-bucket aggregation
     const uint64_t n1 = (uint64_t)part.nparts1 * blocks, n2 = (uint64_t)part.nparts1 * part.nparts2 * kPartNB;
     const size_t tb = select_temp_bytes(std::max(n1, n2) + 1);
-    if ((rc = p_hist1.alloc_pooled(8 * (n1 + 1))) || (rc = p_off1.alloc_pooled(8 * (n1 + 1))) ||
-        (rc = p_ent1.alloc_pooled(4 * total_docs + 16)) || (rc = p_hist2.alloc_pooled(8 * (n2 + 1))) ||
-        (rc = p_off2.alloc_pooled(8 * (n2 + 1))) || (rc = p_ent2.alloc_pooled(4 * total_docs + 16)) ||
+    if ((rc = p_ent0.alloc_pooled(8 * part_entries + 16)) || (rc = p_cnt0.alloc_pooled(4ull * blocks + 16)) ||
+        (rc = p_hist1.alloc_pooled(8 * (n1 + 1))) || (rc = p_off1.alloc_pooled(8 * (n1 + 1))) ||
+        (rc = p_ent1.alloc_pooled(4 * part_entries + 16)) || (rc = p_hist2.alloc_pooled(8 * (n2 + 1))) ||
+        (rc = p_off2.alloc_pooled(8 * (n2 + 1))) || (rc = p_ent2.alloc_pooled(4 * part_entries + 16)) ||
         (rc = p_temp.alloc_pooled(tb)))
       return rc;
     unsigned long long* h1 = (unsigned long long*)p_hist1.p;
@@ -1902,27 +2253,24 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     unsigned long long* o2 = (unsigned long long*)p_off2.p;
     HIP_CHECK(hipMemsetAsync(h1 + n1, 0, 8, s));
     HIP_CHECK(hipMemsetAsync(h2 + n2, 0, 8, s));
+    q.group_mode = GM_PART;
     q.part_shift = part.shift1;
     q.part_vbits = part.vbits;
     q.part_nparts = part.nparts1;
     q.part_dc = part.dc;
-    q.part_lmask = part.shift1 >= 32 ? 0xFFFFFFFFu : (uint32_t)((1ull << part.shift1) - 1);
-    q.part_cap = total_docs;
-    q.part_out = (uint32_t*)p_ent1.p;
-    t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
-    q.group_mode = GM_PART_COUNT;
     q.part_hist = h1;
+    q.part_count = (unsigned int*)p_cnt0.p;
+    q.part_base = (const unsigned long long*)(dA + off_part_base);
+    q.part_out = (unsigned long long*)p_ent0.p;
+    t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
     HIP_CHECK(launch_scan(q, blocks, s));
     HIP_CHECK(launch_exclusive_sum((const uint64_t*)h1, (uint64_t*)o1, n1 + 1, p_temp.p, tb, s));
-    HIP_CHECK(hipMemsetAsync(P.seg_matched.p, 0, 8ull * S, s));  // matched docs are counted by the second pass
-    q.group_mode = GM_PART_SCATTER;
-    q.part_hist = o1;
-    HIP_CHECK(launch_scan(q, blocks, s));
     PartSpec ps;
     memset(&ps, 0, sizeof(ps));
     ps.nparts1 = part.nparts1;
     ps.nparts2 = part.nparts2;
     ps.vbits = part.vbits;
+    ps.shift1 = part.shift1;
     ps.shift2 = part.shift2;
     ps.dc_words = part.dc_words;
     ps.row_words = P.bit_words;
@@ -1930,16 +2278,20 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     ps.n_i64 = P.n_i64;
     ps.blocks1 = blocks;
     ps.num_groups = G;
+    ps.in0 = (const unsigned long long*)p_ent0.p;
+    ps.base0 = (const unsigned long long*)(dA + off_part_base);
+    ps.count0 = (const unsigned int*)p_cnt0.p;
     ps.off1 = o1;
-    ps.in1 = (const uint32_t*)p_ent1.p;
+    ps.in1 = (uint32_t*)p_ent1.p;
     ps.hist2 = h2;
     ps.off2 = o2;
     ps.out2 = (uint32_t*)p_ent2.p;
     ps.i64 = (unsigned long long*)P.i64.p;
     ps.bits = (uint32_t*)P.bits.p;
+    HIP_CHECK(launch_part_split1(ps, s));
     HIP_CHECK(launch_part_count2(ps, s));
     HIP_CHECK(launch_exclusive_sum((const uint64_t*)h2, (uint64_t*)o2, n2 + 1, p_temp.p, tb, s));
-    HIP_CHECK(launch_part_scatter2(ps, s));
+    HIP_CHECK(launch_part_split2(ps, s));
     HIP_CHECK(launch_part_aggregate(ps, s));
   } else if (q.num_items) {
     t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
@@ -1976,11 +2328,13 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   stats.num_entries_scanned_in_filter = entries_in_filter;
   {
     for (uint32_t i = 0; i < S; i++) { stats.num_docs_scanned += sm[i]; stats.num_segments_matched += sm[i] > 0; }
+    stats.num_docs_scanned += ns_docs;  // NonScanBasedAggregationOperator: numDocsScanned = numTotalDocs
+    stats.num_segments_matched += ns_matched;
     const uint32_t err = (uint32_t)sm[S ? S : 1];
     if (err & 4u) return kRetryLargerTable;  // hash table over its fill budget: rerun with a larger one
     if (err) return fail(PG_E_INVALID, "device bounds check failed (code %u): a key fell outside the plan's key space", err);
   }
-  stats.num_entries_scanned_post_filter = stats.num_docs_scanned * P.projected_cols;
+  stats.num_entries_scanned_post_filter = (stats.num_docs_scanned - ns_docs) * P.projected_cols;
   if (P.mode == GM_HASH_SEG) {
     const double t0 = wall_ms();
     if ((rc = truncate_and_merge(P, limit, s))) return rc;
@@ -2181,7 +2535,6 @@ int finalize(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   pg_result* r = (pg_result*)calloc(1, sizeof(pg_result));
   if (!r) return fail(PG_E_NOMEM, "out of host memory");
   r->stats = pp->stats;  // local, or merged across ranks by the caller before finalize
-  r->stats.num_entries_scanned_post_filter = r->stats.num_docs_scanned * P.projected_cols;
   r->num_keys = K;
   r->num_aggs = A;
   r->num_groups = nc;
@@ -2253,7 +2606,7 @@ int pg_resident_bytes(uint64_t* out) {
   for (auto& kv : g_segs)
     for (auto& c : kv.second->cols)
       t += c.second.dict.bytes + c.second.words.bytes + c.second.mv_offsets.bytes + c.second.roaring.bytes +
-           c.second.containers.bytes + c.second.keymap.bytes;
+           c.second.containers.bytes + c.second.keymap.bytes + c.second.vals.bytes + c.second.rawv.bytes;
   *out = t;
   return PG_OK;
 }

@@ -91,6 +91,7 @@ __device__ __forceinline__ uint32_t unpack_lds(const uint32_t* st, uint32_t rel,
 // Dictionary reads clamp the dictId to the dictionary: valid data never needs it, and a corrupt forward index
 // then yields wrong values (caught by parity checks) instead of an out-of-bounds access.
 __device__ __forceinline__ double dict_double(const ColDesc c, uint32_t id) {
+  if (c.decoded) return (double)(c.vbase + (int64_t)id);
   id = min(id, c.card - 1u);
   switch (c.dtype) {
     case PG_INT: return (double)glb((const int32_t*)c.dict)[id];
@@ -101,6 +102,7 @@ __device__ __forceinline__ double dict_double(const ColDesc c, uint32_t id) {
 }
 
 __device__ __forceinline__ int64_t dict_i64(const ColDesc c, uint32_t id) {
+  if (c.decoded) return c.vbase + (int64_t)id;
   id = min(id, c.card - 1u);
   return c.dtype == PG_INT ? (int64_t)glb((const int32_t*)c.dict)[id] : glb((const int64_t*)c.dict)[id];
 }
@@ -141,6 +143,32 @@ __device__ __forceinline__ uint32_t agg_ncols(const AggSpec& A) {
   if (A.fn == PG_AGG_COUNT || A.fn == PG_AGG_COUNTMV) return 0;
   if (A.fn == PG_AGG_DISTINCTCOUNT) return 1;
   return A.op == PG_EXPR_COL ? 1u : 2u;
+}
+
+// Raw-value predicate of doc d (RawValueBasedPredicateEvaluator.applySV): the value in its stored type against the
+// leaf's closed integer range / floating range with inclusivity / sorted value set.
+__device__ __forceinline__ bool raw_pred(const LeafDesc& L, uint32_t d) {
+  if (L.rtype <= PG_LONG) {
+    const int64_t v = L.rtype == PG_INT ? (int64_t)glb((const int32_t*)L.words)[d] : glb((const int64_t*)L.words)[d];
+    if (!L.nvals) return v >= L.ilo && v <= L.ihi;
+    const PG_GLOBAL int64_t* set = glb((const int64_t*)L.rvals);
+    uint32_t lo = 0, hi = L.nvals;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (set[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return lo < L.nvals && set[lo] == v;
+  }
+  const double v = L.rtype == PG_FLOAT ? (double)glb((const float*)L.words)[d] : glb((const double*)L.words)[d];
+  if (!L.nvals)
+    return ((L.rflags & 1u) ? v >= L.dlo : v > L.dlo) && ((L.rflags & 2u) ? v <= L.dhi : v < L.dhi);
+  const PG_GLOBAL double* set = glb((const double*)L.rvals);
+  uint32_t lo = 0, hi = L.nvals;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (set[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo < L.nvals && set[lo] == v;
 }
 
 // IN-set filter bitmap test (exact when shift == 0, else a candidate test resolved by the global LUT).
@@ -233,6 +261,23 @@ __device__ __forceinline__ uint32_t eval_leaf(const QuerySpec& q, uint32_t li, c
   switch (L.kind) {
     case LK_ALL: m = kRowMask; break;
     case LK_NONE: break;
+    case LK_RAW: {  // per needed doc, rounds of up to 4 docs per lane with their loads in flight together
+      uint32_t rem = need;
+      while (__ballot(rem != 0)) {
+        uint32_t jj[4];
+        bool ok[4];
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+          jj[x] = rem ? (uint32_t)__ffs(rem) - 1u : 32u;
+          rem &= rem - 1u;
+          ok[x] = jj[x] < 32u && raw_pred(L, rows.doc(jj[x]));
+        }
+#pragma unroll
+        for (int x = 0; x < 4; x++)
+          if (ok[x]) m |= 1u << jj[x];
+      }
+      break;
+    }
     case LK_DOCRANGE: {
       if constexpr (Rows::kTile) {
 #pragma unroll
@@ -440,18 +485,49 @@ __device__ __forceinline__ uint64_t group_slot(const QuerySpec& q, uint64_t pack
   return h;
 }
 
-// GM_PART_*: the doc's entry instead of a state update.  COUNT pass: one more entry in the block's count of the
-// level-1 partition of key g; SCATTER pass (same grid and docs): the entry at the block's next position in that
-// partition (`cur` = the block's LDS cursors, loaded from the exclusive scan of the COUNT pass).
-__device__ __forceinline__ void part_emit(const QuerySpec& q, uint32_t* cur, uint64_t g, uint32_t vid) {
-  const uint32_t p = (uint32_t)(g >> q.part_shift);
-  if (q.group_mode == GM_PART_COUNT) {
-    atomicAdd(&cur[p], 1u);
-    return;
+// GM_PART: the doc's entry instead of a state update.  The lanes with `on` append (key << part_vbits | value id)
+// to the block's region of the entry array in lane order -- one LDS atomic per wave per call, and the wave's stores
+// are consecutive 8-byte words -- and count it in the block's histogram of level-1 partitions (key >> part_shift).
+// Called by every lane of the wave (it ballots).  lds[0] = the block's entry count, lds[1 + p] = its histogram.
+__device__ __forceinline__ void part_append(const QuerySpec& q, uint32_t* lds, unsigned long long* out, bool on,
+                                            uint64_t g, uint32_t vid) {
+  const uint64_t bal = __ballot(on);
+  if (!bal) return;
+  const uint32_t leader = (uint32_t)__builtin_ctzll(bal);
+  uint32_t base = 0;
+  if ((threadIdx.x & 63u) == leader) base = atomicAdd(&lds[0], (uint32_t)__popcll(bal));
+  base = __builtin_amdgcn_readlane(base, leader);
+  if (on) {
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+    out[base + rank] = (g << q.part_vbits) | vid;
+    atomicAdd(&lds[1 + (uint32_t)(g >> q.part_shift)], 1u);
   }
-  const uint32_t pos = atomicAdd(&cur[p], 1u);
-  if (pos < q.part_cap) q.part_out[pos] = (((uint32_t)g & q.part_lmask) << q.part_vbits) | vid;
-  else atomicOr(q.err, 8u);
+}
+
+// part_append for the 8 rows of a dense chunk at once: one LDS cursor atomic per wave for all of them (the cursor's
+// return latency is paid once per chunk, not once per row).
+template <class GK>
+__device__ __forceinline__ void part_append8(const QuerySpec& q, uint32_t* lds, unsigned long long* out, uint32_t live,
+                                             const GK (&g)[8], const uint32_t (&vid)[8]) {
+  uint64_t bal[8];
+  uint32_t pre[8], total = 0;
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    bal[r] = __ballot((live >> r) & 1u);
+    pre[r] = total;
+    total += (uint32_t)__popcll(bal[r]);
+  }
+  if (!total) return;
+  uint32_t base = 0;
+  if ((threadIdx.x & 63u) == 0) base = atomicAdd(&lds[0], total);
+  base = __builtin_amdgcn_readlane(base, 0);
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    if (!((live >> r) & 1u)) continue;
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[r] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[r], 0u));
+    out[base + pre[r] + rank] = ((uint64_t)g[r] << q.part_vbits) | vid[r];
+    atomicAdd(&lds[1 + (uint32_t)((uint64_t)g[r] >> q.part_shift)], 1u);
+  }
 }
 
 // Packed group key / state slot of a doc: a single key's global id and every slot (dense <= 2^26, hash tables <=
@@ -461,10 +537,11 @@ template <int MAXK> using GKey = typename std::conditional<(MAXK > 1), uint64_t,
 
 // Group-state pointers: the block's LDS copy when the table is privatised, else the global arrays.
 struct GroupState {
-  unsigned long long* i64;
+  unsigned long long* i64;   // GM_PART: the block's LDS entry count + level-1 histogram (uint32 words)
   double* f64;
   long long* mn;
   long long* mx;
+  unsigned long long* out;   // GM_PART: the block's region of the entry array
 };
 
 // Per-doc update of one aggregation in group slot g (aggregateGroupBySV of each function).
@@ -525,6 +602,7 @@ __device__ __forceinline__ void acc_update(const QuerySpec& q, const AggSpec& A,
 // tile when the column is staged, else a gathered window.
 __device__ __forceinline__ uint32_t col_id(const QuerySpec& q, uint32_t slot, const ColDesc c,
                                           const uint32_t* stage, uint32_t d, uint32_t rel) {
+  if (!c.bits) return d;  // raw forward index: the value array is indexed by doc id
   if (slot != kNoSlot) return unpack_lds(stage + q.staged[slot].lds_word_off, rel, c.bits);
   return unpack(make_rsrc(c.words, c.wbytes), d, c.bits);
 }
@@ -625,11 +703,11 @@ __device__ __forceinline__ void aggregate_dense(const QuerySpec& q, const SegDes
         }
       }
       if (live != mc) atomicOr(q.err, 1u);  // never expected: the host proved the key ranges
-      if (q.group_mode >= GM_PART_COUNT) {
+      if (q.group_mode == GM_PART) {
         uint32_t vid[8];
 #pragma unroll
         for (int r = 0; r < 8; r++) vid[r] = 0;
-        if (q.group_mode == GM_PART_SCATTER && q.part_dc != (uint32_t)kNoSlot) {
+        if (q.part_dc != (uint32_t)kNoSlot) {
           const uint32_t a = q.part_dc;
           const AggSpec& A = q.aggs[a];
           const ColDesc c0 = ldc(sd.aggcols + 2 * a, 0);
@@ -643,9 +721,7 @@ __device__ __forceinline__ void aggregate_dense(const QuerySpec& q, const SegDes
             else if ((live >> r) & 1u) { atomicOr(q.err, 2u); live &= ~(1u << r); }
           }
         }
-#pragma unroll
-        for (int r = 0; r < 8; r++)
-          if ((live >> r) & 1u) part_emit(q, (uint32_t*)S.i64, g[r], vid[r]);
+        part_append8(q, (uint32_t*)S.i64, S.out, live, g, vid);
         continue;
       }
       if (q.group_mode != GM_DENSE) {
@@ -718,6 +794,30 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
     }
 #pragma unroll
     for (int x = 0; x < R; x++) {
+      if constexpr (GROUPED) {
+        if (q.group_mode == GM_PART) {  // block-uniform: every lane takes part in the append
+          uint64_t g = 0;
+          bool on = jj[x] < 32u;
+#pragma unroll
+          for (int k = 0; k < NK; k++) {
+            if (k >= (int)q.num_keys) break;
+            const uint64_t kid = key_of(q.key_kind[k], q.key_base[k], ldc(sd.keycols, k), kidx[x][k]);
+            if (on && kid >= q.key_card[k]) { atomicOr(q.err, 1u); on = false; }
+            g += kid * q.key_stride[k];
+          }
+          uint32_t vid = 0;
+#pragma unroll
+          for (int a = 0; a < MAXA; a++) {
+            if ((uint32_t)a != q.part_dc) continue;
+            const AggSpec& A = q.aggs[a];
+            const uint64_t k = key_of(A.key_kind, A.key_base, ldc(sd.aggcols + 2 * a, 0), ia[x][a]);
+            if (k < A.key_card) vid = (uint32_t)k;
+            else if (on) { atomicOr(q.err, 2u); on = false; }
+          }
+          part_append(q, (uint32_t*)S.i64, S.out, on, g, vid);
+          continue;
+        }
+      }
       if (jj[x] >= 32u) continue;
       if constexpr (GROUPED) {
         uint64_t g = 0;
@@ -731,20 +831,6 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
         }
         if (!in_range) {  // never expected: the host proved the key ranges; refuse rather than write out of bounds
           atomicOr(q.err, 1u);
-          continue;
-        }
-        if (q.group_mode >= GM_PART_COUNT) {
-          uint32_t vid = 0;
-          bool ok = true;
-#pragma unroll
-          for (int a = 0; a < MAXA; a++) {
-            if ((uint32_t)a != q.part_dc || q.group_mode != GM_PART_SCATTER) continue;
-            const AggSpec& A = q.aggs[a];
-            const uint64_t k = key_of(A.key_kind, A.key_base, ldc(sd.aggcols + 2 * a, 0), ia[x][a]);
-            if (k < A.key_card) vid = (uint32_t)k;
-            else { atomicOr(q.err, 2u); ok = false; }
-          }
-          if (ok) part_emit(q, (uint32_t*)S.i64, g, vid);
           continue;
         }
         g = group_slot(q, g, sd.index, d[x]);
@@ -783,7 +869,7 @@ __host__ __device__ inline size_t scan_groups_off(const QuerySpec& q) {
   return (16 + (size_t)q.stage_ring * q.stage_lds_words * 4 + (size_t)q.set_lds_ints * 4 + 15) & ~(size_t)15;
 }
 __host__ __device__ inline size_t scan_queue_off(const QuerySpec& q) {
-  const size_t g = (q.num_keys && q.group_mode >= GM_PART_COUNT) ? q.part_nparts * 4ull
+  const size_t g = (q.num_keys && q.group_mode == GM_PART) ? (1 + q.part_nparts) * 4ull
                    : (q.num_keys && q.use_lds) ? q.num_slots * 8ull * (q.n_i64 + q.n_f64 + q.n_min + q.n_max) : 0;
   return scan_groups_off(q) + ((g + 15) & ~(size_t)15);
 }
@@ -809,15 +895,16 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
     for (uint64_t i = tid; i < q.num_slots * q.n_min; i += kBlock) l_mn[i] = order_key(__builtin_inf());
     for (uint64_t i = tid; i < q.num_slots * q.n_max; i += kBlock) l_mx[i] = order_key(-__builtin_inf());
   }
-  // GM_PART_*: the block's level-1 partition cursors (COUNT: counts from 0; SCATTER: this block's offsets)
-  const bool part = GROUPED && q.group_mode >= GM_PART_COUNT;
+  // GM_PART: the block's entry count and level-1 histogram (LDS), its region of the entry array
+  const bool part = GROUPED && q.group_mode == GM_PART;
   if (part) {
-    uint32_t* cur = (uint32_t*)lds_groups;
-    for (uint32_t p = tid; p < q.part_nparts; p += kBlock)
-      cur[p] = q.group_mode == GM_PART_COUNT ? 0u : (uint32_t)q.part_hist[(uint64_t)p * gridDim.x + blockIdx.x];
+    uint32_t* h = (uint32_t*)lds_groups;
+    for (uint32_t p = tid; p <= q.part_nparts; p += kBlock) h[p] = 0u;
     __syncthreads();
   }
-  const GroupState S = (q.use_lds || part) ? GroupState{l_i64, l_f64, l_mn, l_mx} : GroupState{q.i64, q.f64, q.mn, q.mx};
+  const GroupState S = (q.use_lds || part)
+                           ? GroupState{l_i64, l_f64, l_mn, l_mx, part ? q.part_out + q.part_base[blockIdx.x] : nullptr}
+                           : GroupState{q.i64, q.f64, q.mn, q.mx, nullptr};
 
   // aggregation-only accumulators (registers; indices compile-time via unrolled agg loops)
   uint64_t acc[MAXA];
@@ -844,11 +931,12 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
   // publishes it in LDS before the next tile's barrier; every wave reads the word of that tile's parity after the
   // barrier, so the whole block leaves the loop at the same tile (the words live in the pad before the ring, whose
   // st[-1] bits are always masked off)
-  // Polled every kPollTiles tiles into alternating words (no register stays live across a tile for it: at 4 waves
-  // per SIMD a per-tile poll state spilled 48 bytes per lane to scratch and slowed config 3 by 1.7x).
+  // Polled every kPollTiles tiles into alternating words; a raised flag ends the loop through has_next (a separate
+  // exit path out of the tile loop spilled 48 bytes per lane to scratch at 4 waves per SIMD: config 3 1.7x slower).
   volatile unsigned int* stop = (volatile unsigned int*)smem;
   if (tid == 0) stop[0] = stop[1] = 0u;
-  uint32_t iter = 0;  // block-uniform tile counter
+  uint32_t iter = 0;     // block-uniform tile counter
+  uint32_t pending = 0;  // thread 0: the flag loaded at the previous poll (arrived long before it is stored)
 
   if (i0 < i1) {
     const bool ring2 = q.stage_ring > 1;
@@ -888,13 +976,14 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
         if (has_next) { n_it = ldc(q.items, n_item); n_tile = n_it.tile_begin; n_seg = n_it.seg; }
       }
       __builtin_amdgcn_s_waitcnt(0);  // this wave's copies of the current tile have landed
+      const bool poll = q.cancel && (iter & (kPollTiles - 1u)) == 0;
+      const uint32_t k = iter / kPollTiles;
+      if (poll && tid == 0) stop[k & 1u] = pending;  // loaded at poll k - 1: no wait on the PCIe round trip here
       __syncthreads();                // ... and every wave's; every wave is done with the other buffer
-      if (q.cancel && (iter & (kPollTiles - 1u)) == 0) {
-        // word (k & 1) was written by thread 0 at poll k - 1, before this barrier; thread 0 now fills the other word
-        // for poll k + 1 (the host flag load may take a PCIe round trip; its LDS write lands before a later barrier)
-        const uint32_t k = iter / kPollTiles;
+      if (poll) {
+        // word (k & 1) is read by every wave after this barrier and rewritten only at poll k + 2
         if (__builtin_amdgcn_readfirstlane(stop[k & 1u])) has_next = false;  // finish this tile, then leave
-        if (tid == 0) stop[(k + 1u) & 1u] = __hip_atomic_load(q.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (tid == 0) pending = __hip_atomic_load(q.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       iter++;
       if (it.seg != cur_seg) {
@@ -1043,12 +1132,10 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
       }
     }
   } else if (part) {
-    if (q.group_mode == GM_PART_COUNT) {
-      __syncthreads();
-      const uint32_t* cur = (const uint32_t*)lds_groups;
-      for (uint32_t p = tid; p < q.part_nparts; p += kBlock)
-        q.part_hist[(uint64_t)p * gridDim.x + blockIdx.x] = cur[p];
-    }
+    __syncthreads();
+    const uint32_t* h = (const uint32_t*)lds_groups;
+    for (uint32_t p = tid; p < q.part_nparts; p += kBlock) q.part_hist[(uint64_t)p * gridDim.x + blockIdx.x] = h[1 + p];
+    if (tid == 0) q.part_count[blockIdx.x] = h[0];
   } else if (q.use_lds) {
     __syncthreads();
     for (uint64_t g = tid; g < q.num_slots; g += kBlock) {

@@ -60,13 +60,14 @@ _seg_counter = itertools.count(1)
 def fwd_desc(col: Column) -> abi.pg_col_desc:
     d = abi.pg_col_desc()
     d.kind = {"sv": abi.PG_IDX_FWD_SV_BITPACKED, "sorted": abi.PG_IDX_FWD_SV_SORTED,
-              "mv": abi.PG_IDX_FWD_MV_BITPACKED}[col.fwd_kind]
+              "mv": abi.PG_IDX_FWD_MV_BITPACKED, "raw": abi.PG_IDX_FWD_SV_RAW}[col.fwd_kind]
     d.data_type = abi.DTYPE_CODES[col.data_type]
     d.num_docs = col.num_docs
     d.cardinality = col.cardinality
     d.bits_per_element = col.bits_per_element
     d.num_values = col.num_values
-    d.entry_bytes = col.dictionary.entry_bytes
+    d.entry_bytes = col.dictionary.entry_bytes if col.dictionary is not None else \
+        {"INT": 4, "LONG": 8, "FLOAT": 4, "DOUBLE": 8}[col.data_type]
     return d
 
 
@@ -89,10 +90,10 @@ class GpuEngine:
         for name, col in seg.columns.items():
             cid = table.column_ids[name]
             d = fwd_desc(col)
-            dict_bytes = col.dictionary.to_bytes()
-            dd = abi.pg_col_desc.from_buffer_copy(d)
-            dd.kind = abi.PG_IDX_DICT
-            self._upload(key, cid, dd, dict_bytes)
+            if col.dictionary is not None:  # raw columns: the chunked forward index alone
+                dd = abi.pg_col_desc.from_buffer_copy(d)
+                dd.kind = abi.PG_IDX_DICT
+                self._upload(key, cid, dd, col.dictionary.to_bytes())
             self._upload(key, cid, d, col.fwd)
             if col.inverted is not None:
                 di = abi.pg_col_desc.from_buffer_copy(d)

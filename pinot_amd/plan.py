@@ -45,6 +45,7 @@ class LoweredLeaf:
     lo: int = 0
     hi: int = 0
     ids: Optional[np.ndarray] = None   # sorted unique int32
+    raw: Optional[dict] = None         # PG_LEAF_RAW_SCAN: dtype + values or bounds
 
 
 _LITERALS: dict = {}   # (id(values), data type) -> (values, coerced literal array): one coercion per predicate
@@ -80,8 +81,50 @@ def dict_id_set(d, values) -> np.ndarray:
     return np.asarray(sorted({i for i in (d.index_of(v) for v in values) if i >= 0}), dtype=np.int32)
 
 
+_RAW_CAST = {"INT": int, "LONG": int, "FLOAT": lambda v: float(np.float32(float(v))), "DOUBLE": float}
+
+
+def lower_raw_predicate(pred: Predicate, col: Column, col_id: int) -> LoweredLeaf:
+    """Raw-value predicate evaluators of a no-dictionary column (Equals / NotEquals / In / NotIn / Range
+    PredicateEvaluatorFactory.newRawValueBasedEvaluator): the literals in the column's stored type; an integer
+    range folded to closed bounds (exclusive x -> x + 1 / x - 1), a floating range with its inclusivity."""
+    t, dt = pred.type, col.data_type
+    cast = _RAW_CAST[dt]
+    lw = LoweredLeaf(abi.PG_LEAF_RAW_SCAN, col_id)
+    lw.raw = {"dtype": dt}
+    if t in ("EQ", "NOT_EQ", "IN", "NOT_IN"):
+        try:
+            vals = sorted({cast(v) for v in pred.values})
+        except ValueError:
+            raise UnsupportedQuery(f"literal of the wrong type for raw {dt} column {pred.column}")
+        lw.exclusive = 1 if t in ("NOT_EQ", "NOT_IN") else 0
+        lw.raw["values"] = vals
+        return lw
+    if t != "RANGE":
+        raise UnsupportedQuery(f"predicate type {t}")
+    integer = dt in ("INT", "LONG")
+    if integer:  # RangePredicateEvaluatorFactory: Integer / Long bounds, folded here to a closed range
+        lo, hi = -(1 << 63), (1 << 63) - 1
+        try:
+            if pred.lower != UNBOUNDED:
+                lo = int(pred.lower) + (0 if pred.lower_inclusive else 1)
+            if pred.upper != UNBOUNDED:
+                hi = int(pred.upper) - (0 if pred.upper_inclusive else 1)
+        except ValueError:
+            raise UnsupportedQuery(f"non-integer bound on raw {dt} column {pred.column}")
+        lw.raw.update(ilo=lo, ihi=hi)
+    else:
+        lw.raw.update(dlo=-np.inf if pred.lower == UNBOUNDED else cast(pred.lower),
+                      dhi=np.inf if pred.upper == UNBOUNDED else cast(pred.upper),
+                      lo_inc=1 if pred.lower == UNBOUNDED or pred.lower_inclusive else 0,
+                      hi_inc=1 if pred.upper == UNBOUNDED or pred.upper_inclusive else 0)
+    return lw
+
+
 def lower_predicate(pred: Predicate, col: Column, col_id: int) -> LoweredLeaf:
     """Dictionary-based predicate evaluator + leaf operator choice for one segment's column."""
+    if col.dictionary is None:
+        return lower_raw_predicate(pred, col, col_id)
     d = col.dictionary
     card = len(d)
     excl = 0
@@ -209,6 +252,18 @@ class KeySpace:
     @staticmethod
     def build(column: str, cols: List[Column]) -> "KeySpace":
         dt = cols[0].data_type
+        if any(c.dictionary is None for c in cols):
+            # raw (no-dictionary) columns: ids only as value offsets (a keymap needs dictIds)
+            if dt not in ("INT", "LONG"):
+                raise UnsupportedQuery(f"{column}: raw {dt} column as a key / DISTINCTCOUNT value")
+            vals = [c.raw_values if c.dictionary is None else np.asarray(c.dictionary.values) for c in cols]
+            vals = [v for v in vals if v.size]
+            lo = min((int(v.min()) for v in vals), default=0)
+            hi = max((int(v.max()) for v in vals), default=0)
+            span = hi - lo + 1
+            if span > MAX_VALUE_OFFSET_KEYS:
+                raise UnsupportedQuery(f"{column}: raw value range {span} too wide for value-offset ids")
+            return KeySpace(column, abi.PG_KEY_VALUE_OFFSET, span, lo)
         if dt in ("INT", "LONG"):
             lo = min(int(c.dictionary.values[0]) for c in cols)
             hi = max(int(c.dictionary.values[-1]) for c in cols)
@@ -406,6 +461,18 @@ class CPlan:
                     self._keep.append(arr)
                     leaves[li].num_ids = len(arr)
                     leaves[li].ids = arr.ctypes.data_as(C.POINTER(C.c_int32))
+                if lw.raw is not None:
+                    r = lw.raw
+                    if "values" in r:  # int64 for INT / LONG columns, float64 for FLOAT / DOUBLE
+                        arr = np.ascontiguousarray(r["values"], dtype=np.int64 if r["dtype"] in ("INT", "LONG")
+                                                   else np.float64)
+                        self._keep.append(arr)
+                        leaves[li].num_ids = len(arr)
+                        leaves[li].values = arr.ctypes.data
+                    else:
+                        leaves[li].ilo, leaves[li].ihi = r.get("ilo", 0), r.get("ihi", 0)
+                        leaves[li].dlo, leaves[li].dhi = r.get("dlo", 0.0), r.get("dhi", 0.0)
+                        leaves[li].lo_inclusive, leaves[li].hi_inclusive = r.get("lo_inc", 1), r.get("hi_inc", 1)
             self.lowered.append(lows)
             self._keep.append(leaves)
             seg_arr[si].seg_key = key
@@ -441,6 +508,8 @@ class CPlan:
         keys = (abi.pg_key * max(len(query.group_by), 1))()
         self.key_spaces = []
         for k, col in enumerate(query.group_by):
+            if any(s.columns[col].dictionary is None for s in segments if col in s.columns):
+                raise UnsupportedQuery(f"GROUP BY raw (no-dictionary) column {col}")
             ks = table.key_space(col)
             self.key_spaces.append(ks)
             keys[k].col_id = cid[col]

@@ -218,6 +218,12 @@ class _Parser:
             hi = self.literal()
             return FilterContext("PREDICATE", predicate=Predicate("RANGE", col, (), lo, hi, True, True))
         neg = self.accept("kw", "NOT")
+        if neg and self.accept("kw", "BETWEEN"):  # NOT BETWEEN -> NOT(RANGE) (CalciteSqlParser keeps the NOT)
+            lo = self.literal()
+            self.expect("kw", "AND")
+            hi = self.literal()
+            return FilterContext("NOT", [FilterContext("PREDICATE",
+                                                       predicate=Predicate("RANGE", col, (), lo, hi, True, True))])
         if self.accept("kw", "IN"):
             self.expect("op", "(")
             vals = [self.literal()]
@@ -226,7 +232,7 @@ class _Parser:
             self.expect("op", ")")
             return FilterContext("PREDICATE", predicate=Predicate("NOT_IN" if neg else "IN", col, tuple(vals)))
         if neg:
-            raise ValueError("NOT must be followed by IN")
+            raise ValueError("NOT must be followed by IN or BETWEEN")
         op = self.expect("op")
         v = self.literal()
         if op == "=":

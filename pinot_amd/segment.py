@@ -289,6 +289,105 @@ def build_dictionary(data_type: str, values) -> (Dictionary, np.ndarray):
     return Dictionary(data_type, uniq, eb), inv.astype(np.int32)
 
 
+# ----------------------------------------------------------------------------- raw (no-dictionary) forward index
+# Fixed-width chunked SV forward index of a noDictionaryColumn (SingleValueFixedByteRawIndexCreator, 1 000 docs per
+# chunk; BaseChunkSVForwardIndexWriter.writeHeader, io/writer/impl/BaseChunkSVForwardIndexWriter.java:129-161):
+#   version, numChunks, numDocsPerChunk, lengthOfLongestEntry [, totalDocs, compressionType, dataHeaderStart  (v >= 2)]
+#   chunk offsets (int32 for v1/v2, int64 for v3/v4; absolute file offsets), then the chunks (BE values, each chunk
+#   passed through its ChunkCompressionType; v1 is always SNAPPY).  FixedBytePower2ChunkSVForwardIndexReader (v4) only
+#   differs in a power-of-two docs per chunk.  Metrics default to PASS_THROUGH, dimensions to LZ4
+#   (SegmentColumnarIndexCreator.java:356-367).
+CHUNK_PASS_THROUGH, CHUNK_SNAPPY, CHUNK_ZSTANDARD, CHUNK_LZ4, CHUNK_LZ4_LENGTH_PREFIXED = 0, 1, 2, 3, 4
+RAW_DOCS_PER_CHUNK = 1000
+
+
+def raw_forward_bytes(values, data_type: str, version: int = 2, docs_per_chunk: int = RAW_DOCS_PER_CHUNK) -> bytes:
+    """PASS_THROUGH chunked raw forward index (FixedByteChunkSVForwardIndexWriter), version 2, 3 or 4."""
+    arr = np.asarray(values, dtype=_NP_BE[data_type])
+    n, size = arr.size, arr.dtype.itemsize
+    num_chunks = (n + docs_per_chunk - 1) // docs_per_chunk
+    off_size = 4 if version <= 2 else 8
+    header_size = 7 * 4 + num_chunks * off_size
+    head = struct.pack(">7i", version, num_chunks, docs_per_chunk, size, n, CHUNK_PASS_THROUGH, 28)
+    offs = np.arange(num_chunks, dtype=np.int64) * docs_per_chunk * size + header_size
+    return head + offs.astype(">i4" if off_size == 4 else ">i8").tobytes() + arr.tobytes()
+
+
+def snappy_decompress(src: bytes) -> bytes:
+    """The Snappy block format (ChunkCompressionType.SNAPPY, snappy-java 1.1.x; format: varint uncompressed length,
+    then literal / copy elements with 1-, 2- or 4-byte offsets)."""
+    pos, n, shift = 0, 0, 0
+    while True:
+        b = src[pos]
+        pos += 1
+        n |= (b & 0x7F) << shift
+        shift += 7
+        if b < 0x80:
+            break
+    out = bytearray()
+    while pos < len(src):
+        tag = src[pos]
+        pos += 1
+        kind = tag & 3
+        if kind == 0:  # literal
+            ln = tag >> 2
+            if ln >= 60:
+                nb = ln - 59
+                ln = int.from_bytes(src[pos:pos + nb], "little")
+                pos += nb
+            ln += 1
+            out += src[pos:pos + ln]
+            pos += ln
+            continue
+        if kind == 1:
+            ln = ((tag >> 2) & 7) + 4
+            off = ((tag >> 5) << 8) | src[pos]
+            pos += 1
+        elif kind == 2:
+            ln = (tag >> 2) + 1
+            off = int.from_bytes(src[pos:pos + 2], "little")
+            pos += 2
+        else:
+            ln = (tag >> 2) + 1
+            off = int.from_bytes(src[pos:pos + 4], "little")
+            pos += 4
+        if off == 0 or off > len(out):
+            raise ValueError("corrupt snappy stream")
+        for _ in range(ln):  # copies may overlap their own output
+            out.append(out[-off])
+    if len(out) != n:
+        raise ValueError(f"snappy: {len(out)} bytes decoded, {n} expected")
+    return bytes(out)
+
+
+def raw_forward_header(buf: bytes) -> dict:
+    """BaseChunkForwardIndexReader's constructor (readers/forward/BaseChunkForwardIndexReader.java:56-102)."""
+    version, num_chunks, docs_per_chunk, entry = struct.unpack_from(">4i", buf, 0)
+    if version > 1:
+        total, comp, data_start = struct.unpack_from(">3i", buf, 16)
+    else:
+        total, comp, data_start = None, CHUNK_SNAPPY, 16
+    off_size = 4 if version <= 2 else 8
+    offs = np.frombuffer(buf, dtype=">i4" if off_size == 4 else ">i8", count=num_chunks, offset=data_start)
+    return dict(version=version, num_chunks=num_chunks, docs_per_chunk=docs_per_chunk, entry=entry, total=total,
+                compression=comp, offsets=offs.astype(np.int64), raw_start=data_start + num_chunks * off_size)
+
+
+def raw_forward_values(buf: bytes, data_type: str, num_docs: Optional[int] = None) -> np.ndarray:
+    """All values of a fixed-width raw forward index (getInt / getLong / getFloat / getDouble per doc)."""
+    h = raw_forward_header(buf)
+    be = _NP_BE[data_type]
+    if h["compression"] == CHUNK_PASS_THROUGH:
+        data = buf[h["raw_start"]:]
+    elif h["compression"] == CHUNK_SNAPPY:
+        ends = list(h["offsets"][1:]) + [len(buf)]
+        data = b"".join(snappy_decompress(buf[s:e]) for s, e in zip(h["offsets"], ends))
+    else:
+        raise NotImplementedError(f"chunk compression {h['compression']}")
+    n = num_docs if num_docs is not None else (h["total"] if h["total"] is not None else len(data) // h["entry"])
+    return np.frombuffer(data, dtype=be, count=n).astype(_NP_NATIVE[data_type])
+
+
 # ----------------------------------------------------------------------------- columns / segments
 
 @dataclass
@@ -308,13 +407,22 @@ class Column:
     # decoded dictIds (host convenience; SV: int32[num_docs], MV: list of arrays)
     dict_ids: Optional[np.ndarray] = None
     mv_offsets: Optional[np.ndarray] = None  # MV: int64[num_docs+1]
+    # noDictionaryColumns: the values (host copy) of a raw chunked forward index (`fwd`); dictionary is None
+    raw_values: Optional[np.ndarray] = None
+    raw_cardinality: int = 0
+
+    @property
+    def has_dictionary(self) -> bool:
+        return self.dictionary is not None
 
     @property
     def cardinality(self) -> int:
-        return len(self.dictionary)
+        return len(self.dictionary) if self.dictionary is not None else self.raw_cardinality
 
     @property
     def fwd_kind(self) -> str:
+        if self.dictionary is None:
+            return "raw"
         if not self.single_value:
             return "mv"
         return "sorted" if self.is_sorted else "sv"
@@ -362,14 +470,25 @@ class ImmutableSegment:
     @staticmethod
     def create(name: str, data: Dict[str, Sequence], schema: Dict[str, str],
                inverted: Sequence[str] = (), field_types: Optional[Dict[str, str]] = None,
-               roaring_run_optimize: bool = True) -> "ImmutableSegment":
-        """schema: column -> data type.  MV columns are given as a list of sequences."""
+               roaring_run_optimize: bool = True, no_dictionary: Sequence[str] = (),
+               raw_version: int = 2) -> "ImmutableSegment":
+        """schema: column -> data type.  MV columns are given as a list of sequences.  `no_dictionary`: SV numeric
+        columns stored as raw PASS_THROUGH chunked forward indexes (tableIndexConfig.noDictionaryColumns)."""
         cols = {}
         num_docs = None
         for cname, dtype in schema.items():
             vals = data[cname]
             sv = not (len(vals) > 0 and isinstance(vals[0], (list, tuple, np.ndarray)))
-            if sv:
+            if cname in no_dictionary:
+                if not sv or dtype not in _NP_NATIVE:
+                    raise ValueError(f"raw forward index: {cname} must be a single-value numeric column")
+                arr = np.asarray(vals, dtype=_NP_NATIVE[dtype])
+                n = arr.size
+                col = Column(cname, dtype, True, None, n, 0, False, n, 0,
+                             field_type=(field_types or {}).get(cname, "METRIC"), raw_values=arr,
+                             raw_cardinality=int(np.unique(arr).size))
+                col.fwd = raw_forward_bytes(arr, dtype, raw_version)
+            elif sv:
                 dictionary, ids = build_dictionary(dtype, vals)
                 n = ids.size
                 card = len(dictionary)
@@ -409,11 +528,13 @@ class ImmutableSegment:
                  "segment.padding.character = \\\\u0000"]
         for c in self.columns.values():
             p = f"column.{c.name}."
+            eb = c.dictionary.entry_bytes if c.data_type == 'STRING' and c.dictionary is not None else 0
             props += [p + f"cardinality = {c.cardinality}", p + f"totalDocs = {c.num_docs}",
                       p + f"dataType = {c.data_type}", p + f"bitsPerElement = {c.bits_per_element}",
-                      p + f"lengthOfEachEntry = {c.dictionary.entry_bytes if c.data_type == 'STRING' else 0}",
+                      p + f"lengthOfEachEntry = {eb}",
                       p + f"columnType = {c.field_type}", p + f"isSorted = {str(c.is_sorted).lower()}",
-                      p + "hasDictionary = true", p + f"hasInvertedIndex = {str(c.inverted is not None).lower()}",
+                      p + f"hasDictionary = {str(c.dictionary is not None).lower()}",
+                      p + f"hasInvertedIndex = {str(c.inverted is not None).lower()}",
                       p + f"isSingleValues = {str(c.single_value).lower()}",
                       p + f"maxNumberOfMultiValues = {c.max_num_multi_values}",
                       p + f"totalNumberOfEntries = {c.num_values}"]
@@ -422,9 +543,10 @@ class ImmutableSegment:
     def write_v1(self, path: str) -> None:
         os.makedirs(path, exist_ok=True)
         for c in self.columns.values():
-            with open(os.path.join(path, c.name + ".dict"), "wb") as f:
-                f.write(c.dictionary.to_bytes())
-            ext = {"sv": ".sv.unsorted.fwd", "sorted": ".sv.sorted.fwd", "mv": ".mv.fwd"}[c.fwd_kind]
+            if c.dictionary is not None:
+                with open(os.path.join(path, c.name + ".dict"), "wb") as f:
+                    f.write(c.dictionary.to_bytes())
+            ext = {"sv": ".sv.unsorted.fwd", "sorted": ".sv.sorted.fwd", "mv": ".mv.fwd", "raw": ".sv.raw.fwd"}[c.fwd_kind]
             with open(os.path.join(path, c.name + ext), "wb") as f:
                 f.write(c.fwd)
             if c.inverted is not None:
@@ -447,7 +569,8 @@ class ImmutableSegment:
         with open(os.path.join(d, "columns.psf"), "wb") as psf:
             off = 0
             for c in self.columns.values():
-                parts = [("dictionary", c.dictionary.to_bytes()), ("forward_index", c.fwd)]
+                parts = ([("dictionary", c.dictionary.to_bytes())] if c.dictionary is not None else []) + \
+                    [("forward_index", c.fwd)]
                 if c.inverted is not None:
                     parts.append(("inverted_index", c.inverted))
                 for idx, payload in parts:
@@ -488,6 +611,14 @@ class ImmutableSegment:
             card = int(p("cardinality"))
             b = int(p("bitsPerElement"))
             eb = int(p("lengthOfEachEntry")) if dtype == "STRING" else 0
+            if props.get(f"column.{cname}.hasDictionary", "true") == "false":
+                # DefaultIndexReaderProvider.java:92-101: a raw chunked forward index
+                fwd = index_bytes(cname, "raw")
+                vals = raw_forward_values(fwd, dtype, num_docs)
+                cols[cname] = Column(cname, dtype, True, None, num_docs, b, False, num_docs, 0, fwd, None,
+                                     props.get(f"column.{cname}.columnType", "METRIC"), raw_values=vals,
+                                     raw_cardinality=card)
+                continue
             dictionary = Dictionary.from_bytes(dtype, index_bytes(cname, "dictionary"), card, eb, padding)
             sv = p("isSingleValues") == "true"
             is_sorted = p("isSorted") == "true"
@@ -512,7 +643,7 @@ class ImmutableSegment:
     def load_v1(path: str) -> "ImmutableSegment":
         """ImmutableSegmentLoader for the V1 layout (metadata.properties + per-index files)."""
         ext = {"dictionary": ".dict", "sorted": ".sv.sorted.fwd", "unsorted": ".sv.unsorted.fwd", "mv": ".mv.fwd",
-               "inverted": ".bitmap.inv"}
+               "inverted": ".bitmap.inv", "raw": ".sv.raw.fwd"}
 
         def index_bytes(col, kind):
             fp = os.path.join(path, col + ext[kind])
@@ -544,7 +675,7 @@ class ImmutableSegment:
         with open(os.path.join(d, "columns.psf"), "rb") as f:
             psf = f.read()
         names = {"dictionary": "dictionary", "sorted": "forward_index", "unsorted": "forward_index",
-                 "mv": "forward_index", "inverted": "inverted_index"}
+                 "mv": "forward_index", "inverted": "inverted_index", "raw": "forward_index"}
 
         def index_bytes(col, kind):
             e = entries.get((col, names[kind]))

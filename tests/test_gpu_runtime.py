@@ -17,7 +17,19 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def long_scan(gpu_engine):
-    """~200 M rows of config-4 shape (random-atomic group-by: a scan of tens of ms)."""
+    """~200 M rows of config-4 shape through the per-doc atomic group-by (PG_PART=0: one long scan launch of tens of
+    ms; the radix-partitioned pipeline finishes the same query in a few ms, mostly outside the scan kernel)."""
+    import os
+    old = os.environ.get("PG_PART")
+    os.environ["PG_PART"] = "0"
+    yield _long_scan(gpu_engine)
+    if old is None:
+        os.environ.pop("PG_PART", None)
+    else:
+        os.environ["PG_PART"] = old
+
+
+def _long_scan(gpu_engine):
     import torch
     from pinot_amd import synth
     from pinot_amd.segment import ImmutableSegment

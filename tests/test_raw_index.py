@@ -1,0 +1,223 @@
+"""Raw (no-dictionary) fixed-width forward index: the reference's chunked format
+(BaseChunkSVForwardIndexWriter / FixedByteChunkSVForwardIndexReader / FixedBytePower2ChunkSVForwardIndexReader),
+raw-value predicates and aggregations over it, on the oracle and the device.
+
+Pinned by the reference's own bytes: tests/golden/raw_fwd/ holds the three fixtures of
+FixedByteChunkSVForwardIndexTest.java:255-291 (fixedByteSVRDoubles.v1: v1 SNAPPY, 10 009 doubles i;
+fixedByteCompressed.v2: v2 SNAPPY, and fixedByteRaw.v2: v2 PASS_THROUGH, 2 000 doubles i + 100.2356)."""
+import os
+
+import numpy as np
+import pytest
+
+from pinot_amd.plan import Table, UnsupportedQuery, reduce_to_rows
+from pinot_amd.query import parse
+from pinot_amd.segment import (Column, ImmutableSegment, raw_forward_bytes, raw_forward_header, raw_forward_values)
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "raw_fwd")
+FIXTURES = [("fixedByteSVRDoubles.v1", 10009, 0.0, 1), ("fixedByteCompressed.v2", 2000, 100.2356, 1),
+            ("fixedByteRaw.v2", 2000, 100.2356, 0)]
+
+
+def _fixture(name):
+    with open(os.path.join(GOLDEN, name), "rb") as f:
+        return f.read()
+
+
+@pytest.mark.parametrize("name,n,start,compression", FIXTURES)
+def test_reference_fixtures_decode(name, n, start, compression):
+    b = _fixture(name)
+    assert raw_forward_header(b)["compression"] == compression
+    assert np.array_equal(raw_forward_values(b, "DOUBLE", n), np.arange(n) + start)
+
+
+@pytest.mark.parametrize("version", [2, 3, 4])
+@pytest.mark.parametrize("dtype", ["INT", "LONG", "FLOAT", "DOUBLE"])
+def test_writer_round_trip(version, dtype):
+    rng = np.random.default_rng(version)
+    vals = rng.integers(-10 ** 6, 10 ** 6, 2345).astype({"INT": np.int32, "LONG": np.int64, "FLOAT": np.float32,
+                                                          "DOUBLE": np.float64}[dtype])
+    b = raw_forward_bytes(vals, dtype, version, 1024 if version == 4 else 1000)
+    h = raw_forward_header(b)
+    assert (h["version"], h["total"], h["compression"]) == (version, 2345, 0)
+    assert np.array_equal(raw_forward_values(b, dtype), vals)
+
+
+def _raw_segments(n_segs=3, rows=50_000, seed=7):
+    rng = np.random.default_rng(seed)
+    segs = []
+    for s in range(n_segs):
+        n = rows + 1013 * s
+        data = {"k": rng.integers(0, 40, n), "m_int": rng.integers(-5000, 5000, n),
+                "m_long": rng.integers(-2 ** 40, 2 ** 40, n), "m_float": rng.normal(size=n).astype(np.float32),
+                "m_double": rng.normal(size=n) * 1e3, "u": rng.integers(0, 300, n)}
+        segs.append(ImmutableSegment.create(
+            f"r{s}", data, {"k": "INT", "m_int": "INT", "m_long": "LONG", "m_float": "FLOAT", "m_double": "DOUBLE",
+                            "u": "INT"},
+            no_dictionary=("m_int", "m_long", "m_float", "m_double", "u"), raw_version=2 + s % 3))
+    return segs
+
+
+RAW_QUERIES = [
+    "SELECT COUNT(*), SUM(m_int), MIN(m_long), MAX(m_double), AVG(m_float) FROM t",
+    "SELECT SUM(m_long), COUNT(*) FROM t WHERE m_int > 100 AND m_int <= 4000",
+    "SELECT MAX(m_int), MIN(m_double) FROM t WHERE m_double BETWEEN -200.5 AND 300.25",
+    "SELECT COUNT(*), SUM(m_double) FROM t WHERE m_float < 0 OR m_int IN (1, 2, 3, 4, 5, 6, 7)",
+    "SELECT COUNT(*) FROM t WHERE m_int NOT IN (0, 1, 2) AND NOT m_long < 0",
+    "SELECT COUNT(*), SUM(m_int) FROM t WHERE m_int = 42 OR m_int <> -42",
+    "SELECT k, SUM(m_int), MAX(m_double), COUNT(*) FROM t WHERE m_float >= 0.5 GROUP BY k",
+    "SELECT k, AVG(m_long), MIN(m_float) FROM t WHERE k < 20 AND m_int NOT BETWEEN -100 AND 100 GROUP BY k",
+    "SELECT SUM(m_int * m_double), SUM(m_int + k), MIN(m_long - m_int) FROM t WHERE m_double > 0",
+    "SELECT DISTINCTCOUNT(u), COUNT(*) FROM t WHERE m_int < 0",
+    "SELECT k, DISTINCTCOUNT(u) FROM t GROUP BY k",
+    "SELECT MIN(m_int), MAX(m_long), COUNT(*) FROM t",                     # non-scan: column metadata min / max
+]
+
+
+
+
+@pytest.fixture(scope="module")
+def raw_table():
+    return Table("t", _raw_segments())
+
+
+@pytest.mark.parametrize("sql", RAW_QUERIES)
+def test_raw_queries_oracle_vs_numpy(sql, oracle_engine, raw_table):
+    """The oracle's raw path against a numpy evaluation of the same query over the decoded values."""
+    q = parse(sql)
+    res = oracle_engine.execute(raw_table, q)
+    vals = {c: np.concatenate([s.columns[c].raw_values if s.columns[c].dictionary is None
+                               else s.columns[c].dictionary.values[s.columns[c].dict_ids] for s in raw_table.segments])
+            for c in raw_table.segments[0].columns}
+    mask = _np_filter(q.filter, vals)
+    if not q.group_by:
+        row = res.rows.get((), None)
+        for ag, v in zip(q.aggregations, row):
+            x = _np_agg(ag, vals, mask)
+            if ag.function == "AVG":
+                assert v[1] == x[1] and np.isclose(v[0], x[0], rtol=1e-9)
+            elif ag.function == "DISTINCTCOUNT":
+                assert v == x
+            else:
+                assert np.isclose(v, x, rtol=1e-9, atol=0) or v == x, (ag, v, x)
+    else:
+        keys = vals[q.group_by[0]][mask]
+        for key in np.unique(keys):
+            m2 = mask.copy()
+            m2[mask] = keys == key
+            for ag, v in zip(q.aggregations, res.rows[(int(key),)]):
+                x = _np_agg(ag, vals, m2)
+                if ag.function == "AVG":
+                    assert v[1] == x[1] and np.isclose(v[0], x[0], rtol=1e-9)
+                elif ag.function == "DISTINCTCOUNT":
+                    assert v == x
+                else:
+                    assert np.isclose(v, x, rtol=1e-9) or v == x, (ag, key, v, x)
+        assert len(res.rows) == len(np.unique(keys))
+
+
+def _np_filter(f, vals):
+    n = len(next(iter(vals.values())))
+    if f is None:
+        return np.ones(n, dtype=bool)
+    if f.type == "AND":
+        m = np.ones(n, dtype=bool)
+        for c in f.children:
+            m &= _np_filter(c, vals)
+        return m
+    if f.type == "OR":
+        m = np.zeros(n, dtype=bool)
+        for c in f.children:
+            m |= _np_filter(c, vals)
+        return m
+    if f.type == "NOT":
+        return ~_np_filter(f.children[0], vals)
+    p = f.predicate
+    v = vals[p.column]
+    conv = (lambda x: np.float32(float(x))) if v.dtype == np.float32 else float
+    if p.type in ("EQ", "IN"):
+        return np.isin(v, [conv(x) for x in p.values])
+    if p.type in ("NOT_EQ", "NOT_IN"):
+        return ~np.isin(v, [conv(x) for x in p.values])
+    m = np.ones(v.size, dtype=bool)
+    if p.lower != "*":
+        m &= (v >= conv(p.lower)) if p.lower_inclusive else (v > conv(p.lower))
+    if p.upper != "*":
+        m &= (v <= conv(p.upper)) if p.upper_inclusive else (v < conv(p.upper))
+    return m
+
+
+def _np_agg(ag, vals, mask):
+    f = ag.function
+    if f == "COUNT":
+        return int(mask.sum())
+    e = ag.arg
+    x = vals[e.cols[0]][mask].astype(np.float64)
+    if e.op == "MUL":
+        x = x * vals[e.cols[1]][mask]
+    elif e.op == "ADD":
+        x = x + vals[e.cols[1]][mask]
+    elif e.op == "SUB":
+        x = x - vals[e.cols[1]][mask]
+    if f == "SUM":
+        return float(np.sum(x))
+    if f == "MIN":
+        return float(x.min()) if x.size else float("inf")
+    if f == "MAX":
+        return float(x.max()) if x.size else float("-inf")
+    if f == "AVG":
+        return (float(np.sum(x)), int(x.size))
+    if f == "DISTINCTCOUNT":
+        return set(int(y) for y in vals[e.cols[0]][mask])
+    raise ValueError(f)
+
+
+def test_raw_store_round_trip(tmp_path):
+    """V1 (`<col>.sv.raw.fwd`, hasDictionary = false) and V3 (`forward_index` in columns.psf) stores load the raw
+    columns back unchanged."""
+    seg = _raw_segments(1, 5000)[0]
+    for writer, sub in ((seg.write_v1, "v1"), (seg.write_v3, "v3")):
+        writer(str(tmp_path / sub))
+        back = ImmutableSegment.load(str(tmp_path / sub))
+        for c in ("m_int", "m_long", "m_float", "m_double"):
+            assert back.columns[c].dictionary is None
+            assert np.array_equal(back.columns[c].raw_values, seg.columns[c].raw_values)
+        assert os.path.exists(tmp_path / "v1" / "m_int.sv.raw.fwd") if sub == "v1" else True
+
+
+def test_group_by_raw_column_is_unsupported(oracle_engine, raw_table):
+    with pytest.raises(UnsupportedQuery):
+        oracle_engine.execute(raw_table, parse("SELECT m_int, COUNT(*) FROM t GROUP BY m_int"))
+
+
+def _fixture_segment(name, n):
+    """A segment whose DOUBLE metric is the reference's fixture bytes as they are (its own chunks and codec)."""
+    b = _fixture(name)
+    vals = raw_forward_values(b, "DOUBLE", n)
+    col = Column("v", "DOUBLE", True, None, n, 0, False, n, 0, b, None, "METRIC", raw_values=vals,
+                 raw_cardinality=n)
+    seg = ImmutableSegment.create("f", {"k": np.arange(n) % 3}, {"k": "INT"})
+    seg.columns["v"] = col
+    return seg
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sql", RAW_QUERIES)
+def test_raw_queries_gpu(sql, gpu_engine, oracle_engine, raw_table):
+    from helpers import assert_same_result
+    q = parse(sql)
+    assert_same_result(gpu_engine.execute(raw_table, q), oracle_engine.execute(raw_table, q), table=raw_table)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,n,start,compression", FIXTURES)
+def test_reference_fixture_bytes_on_device(name, n, start, compression, gpu_engine):
+    """The reference's fixture bytes uploaded as they are (SNAPPY chunks decoded by the library): known answers."""
+    seg = _fixture_segment(name, n)
+    t = Table("f", [seg])
+    q = parse("SELECT COUNT(*), SUM(v), MIN(v), MAX(v) FROM f WHERE v >= 10")
+    exp = np.arange(n) + start
+    exp = exp[exp >= 10]
+    row = gpu_engine.execute(t, q).rows[()]
+    assert row[0] == exp.size and row[2] == exp.min() and row[3] == exp.max()
+    assert np.isclose(row[1], exp.sum(), rtol=1e-12)
