@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 3
+#define PG_ABI_VERSION 4
 
 typedef enum pg_status {
   PG_OK = 0,
@@ -80,11 +80,19 @@ typedef enum pg_index_kind {
   PG_IDX_INV_BITMAP = 5,      /* BitmapInvertedIndexWriter layout: (card+1) BE uint32 offsets + roaring */
   PG_IDX_KEYMAP = 6,          /* native int32[card]: dictId -> table-global key id (host-built, for
                                  group-by / DISTINCTCOUNT keys that are not integer value ranges)       */
-  PG_IDX_FWD_SV_RAW = 7       /* raw (no-dictionary) fixed-width chunked forward index (`.sv.raw.fwd`,
+  PG_IDX_FWD_SV_RAW = 7,      /* raw (no-dictionary) fixed-width chunked forward index (`.sv.raw.fwd`,
                                  BaseChunkSVForwardIndexWriter v1-v4, PASS_THROUGH or SNAPPY chunks;
                                  replaces FixedByteChunkSVForwardIndexReader /
                                  FixedBytePower2ChunkSVForwardIndexReader, DefaultIndexReaderProvider.java:92-101);
                                  data_type = stored type INT/LONG/FLOAT/DOUBLE                          */
+  PG_IDX_RANGE = 8            /* range index file (`.bitmap.range`): BitSlicedRangeIndexCreator v2 (BE int 2,
+                                 BE long min, RangeBitmap) or RangeIndexCreator v1 (BE int 1, value type, ranges,
+                                 roaring bitmaps); replaces BitSlicedRangeIndexReader / RangeIndexReaderImpl
+                                 (DefaultIndexReaderProvider.newRangeIndexReader).  Upload after the column's
+                                 forward index: the header is validated and the device form is derived from the
+                                 resident forward index (the index is a function of it) -- a dictionary column's
+                                 packed dictIds serve as is; a raw INT / LONG column gets (value - min) packed at
+                                 bits(max - min) bits per doc, which raw-column aggregations read too           */
 } pg_index_kind;
 
 typedef enum pg_data_type {
@@ -121,8 +129,12 @@ typedef enum pg_leaf_kind {
   PG_LEAF_SORTED = 3,     /* SortedIndexBasedFilterOperator over PG_IDX_FWD_SV_SORTED                   */
   PG_LEAF_INVERTED = 4,   /* BitmapBasedFilterOperator over PG_IDX_INV_BITMAP                           */
   PG_LEAF_MV_SCAN = 5,    /* ScanBasedFilterOperator over a bit-packed MV forward index (any / all)     */
-  PG_LEAF_RAW_SCAN = 6    /* ScanBasedFilterOperator over a raw forward index with a raw-value predicate
+  PG_LEAF_RAW_SCAN = 6,   /* ScanBasedFilterOperator over a raw forward index with a raw-value predicate
                              evaluator (predicate/...PredicateEvaluatorFactory.newRawValueBasedEvaluator)    */
+  PG_LEAF_RANGE_INDEX = 7 /* RangeIndexBasedFilterOperator (operator/filter/RangeIndexBasedFilterOperator.java
+                             :62-100) over PG_IDX_RANGE, RANGE predicates only: a dictionary column matches
+                             dictIds [lo, hi); a raw column takes the PG_LEAF_RAW_SCAN range fields (ilo / ihi,
+                             dlo / dhi + inclusivity).  Exact; counts no entries scanned in the filter        */
 } pg_leaf_kind;
 
 /* A leaf matches dictIds in the set S, where S = [lo, hi) when num_ids == 0, else S = ids[0..num_ids).

@@ -23,7 +23,7 @@ import numpy as np
 from pinot_amd import abi
 from pinot_amd.segment import _NP_BE
 from pinot_amd.plan import (CPlan, DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY, ExecutionStats, IntermediateResult,
-                            Table, default_row, merge_intermediate)
+                            Table, default_row, execute_filtered, has_filtered_aggregations, merge_intermediate)
 from pinot_amd.query import QueryContext, parse
 from pinot_amd.segment import ImmutableSegment
 
@@ -36,7 +36,8 @@ class orc_column(C.Structure):
     _fields_ = [("dict", C.c_void_p), ("fwd", C.c_void_p), ("inv", C.c_void_p), ("inv_bytes", C.c_uint64),
                 ("keymap", C.c_void_p), ("fwd_kind", C.c_uint32), ("data_type", C.c_uint32),
                 ("num_docs", C.c_uint32), ("cardinality", C.c_uint32), ("bits", C.c_uint32),
-                ("num_values", C.c_uint32), ("entry_bytes", C.c_uint32), ("pad", C.c_uint32)]
+                ("num_values", C.c_uint32), ("entry_bytes", C.c_uint32), ("pad", C.c_uint32),
+                ("range", C.c_void_p), ("range_bytes", C.c_uint64)]
 
 
 class orc_segment_result(C.Structure):
@@ -94,6 +95,11 @@ class _SegmentColumns:
                 self.keep.append(iv)
                 c.inv = iv.ctypes.data
                 c.inv_bytes = len(col.inverted)
+            if col.range_index is not None:
+                rg = np.frombuffer(col.range_index, dtype=np.uint8)
+                self.keep.append(rg)
+                c.range = rg.ctypes.data
+                c.range_bytes = len(col.range_index)
             c.fwd_kind = {"sv": ORC_FWD_SV, "sorted": ORC_FWD_SORTED, "mv": ORC_FWD_MV, "raw": ORC_FWD_RAW}[col.fwd_kind]
             c.data_type = abi.DTYPE_CODES[col.data_type]
             c.num_docs = col.num_docs
@@ -202,6 +208,8 @@ class OracleEngine:
                 num_groups_limit=None) -> IntermediateResult:
         if isinstance(query, str):
             query = parse(query)
+        if has_filtered_aggregations(query):  # FilteredAggregationOperator.java:70-98: one plan per filter
+            return execute_filtered(lambda q: self.execute(table, q, segments, num_groups_limit), query)
         segments = list(table.segments if segments is None else segments)
         plan = CPlan(table, query, segments, list(range(1, len(segments) + 1)), num_groups_limit)
         return self.run_plan(plan, segments)

@@ -40,6 +40,8 @@ typedef struct orc_column {
   uint32_t num_values;
   uint32_t entry_bytes;
   uint32_t pad;
+  const uint8_t *range;  /* `.bitmap.range` bytes (v1 or v2) or NULL */
+  uint64_t range_bytes;
 } orc_column;
 
 typedef struct orc_segment_result {
@@ -231,10 +233,75 @@ static int raw_leaf_match(const pg_leaf *l, const orc_column *c, uint32_t d) {
   return (l->lo_inclusive ? v >= l->dlo : v > l->dlo) && (l->hi_inclusive ? v <= l->dhi : v < l->dhi);
 }
 
+/* Range-index value as long double (exact for every INT / LONG / FLOAT / DOUBLE value). */
+static long double range_value(const uint8_t *p, int vt) {
+  switch (vt) {
+    case PG_INT: return (long double)(int32_t)be32(p);
+    case PG_LONG: return (long double)(int64_t)be64(p);
+    case PG_FLOAT: { uint32_t u = be32(p); float f; memcpy(&f, &u, 4); return (long double)f; }
+    default: { uint64_t u = be64(p); double d; memcpy(&d, &u, 8); return (long double)d; }
+  }
+}
+
+/* RangeIndexBasedFilterOperator (operator/filter/RangeIndexBasedFilterOperator.java:62-100).  Over a v1 index
+ * (RangeIndexReaderImpl.java:47-95, findRangeId :232-263, getMatchesInRange / getPartialMatchesInRange :270-300):
+ * docs of the ranges strictly inside the bound ranges match; docs of the two bound ranges are scanned with the exact
+ * predicate.  A v2 (bit-sliced) index is exact by construction: the predicate's docs, evaluated from the forward
+ * index (the RangeBitmap payload is not restated, see pinot_amd/segment.py).  No entries count as scanned in the
+ * filter for the index part; the v1 partial scan counts its docs. */
+static void eval_range_index(const pg_leaf *l, const orc_column *c, uint32_t num_docs, uint8_t *out,
+                             uint64_t *entries_scanned) {
+  const int raw = c->fwd_kind == ORC_FWD_RAW;
+  int32_t *ids = raw ? NULL : sv_dict_ids(c);
+  memset(out, 0, num_docs);
+  const uint8_t *b = c->range;
+  if (!b || c->range_bytes < 12 || be32(b) != 1) {  /* v2 / none: the exact set */
+    for (uint32_t d = 0; d < num_docs; d++) out[d] = (uint8_t)(raw ? raw_leaf_match(l, c, d) : leaf_in_set(l, ids[d]));
+    free(ids);
+    return;
+  }
+  const uint32_t len = be32(b + 4);
+  char name[8] = {0};
+  memcpy(name, b + 8, len < 7 ? len : 7);
+  const int vt = !strcmp(name, "INT") ? PG_INT : !strcmp(name, "LONG") ? PG_LONG : !strcmp(name, "FLOAT") ? PG_FLOAT
+                                                                                                      : PG_DOUBLE;
+  const uint32_t vsz = (vt == PG_INT || vt == PG_FLOAT) ? 4 : 8;
+  const uint8_t *q = b + 8 + len;
+  const uint32_t R = be32(q);
+  const uint8_t *starts = q + 4, *offs = starts + (uint64_t)(R + 1) * vsz;
+  long double lo, hi;
+  if (!raw) { lo = l->lo; hi = (long double)l->hi - 1; }
+  else if (c->data_type <= PG_LONG) { lo = l->ilo; hi = l->ihi; }
+  else { lo = l->dlo; hi = l->dhi; }
+  const long double last = range_value(starts + (uint64_t)R * vsz, vt);
+  int32_t ids_lohi[2];
+  for (int k = 0; k < 2; k++) {  /* findRangeId */
+    const long double x = k ? hi : lo;
+    int32_t r = -2;
+    for (uint32_t i = 0; i < R && r == -2; i++)
+      if (x < range_value(starts + (uint64_t)i * vsz, vt)) r = (int32_t)i - 1;
+    if (r == -2) r = x <= last ? (int32_t)R - 1 : (int32_t)R;
+    ids_lohi[k] = r;
+  }
+  const int32_t first = ids_lohi[0], lastr = ids_lohi[1];
+  for (int32_t r = first + 1; r < lastr; r++) roaring_or_into(b + be64(offs + 8ull * r), out, num_docs);
+  uint8_t *part = (uint8_t *)calloc(num_docs ? num_docs : 1, 1);
+  if (first >= 0 && first < (int32_t)R) roaring_or_into(b + be64(offs + 8ull * first), part, num_docs);
+  if (lastr >= 0 && lastr < (int32_t)R) roaring_or_into(b + be64(offs + 8ull * lastr), part, num_docs);
+  for (uint32_t d = 0; d < num_docs; d++)
+    if (part[d]) {
+      out[d] |= (uint8_t)(raw ? raw_leaf_match(l, c, d) : leaf_in_set(l, ids[d]));
+      (*entries_scanned)++;
+    }
+  free(part);
+  free(ids);
+}
+
 static void eval_leaf(const pg_leaf *l, const orc_column *cols, uint32_t num_docs, uint8_t *out,
                       uint64_t *entries_scanned) {
   const orc_column *c = &cols[l->col_id];
   switch (l->kind) {
+    case PG_LEAF_RANGE_INDEX: eval_range_index(l, c, num_docs, out, entries_scanned); return;
     case PG_LEAF_RAW_SCAN:
       for (uint32_t d = 0; d < num_docs; d++) out[d] = (uint8_t)(raw_leaf_match(l, c, d) ^ (l->exclusive != 0));
       *entries_scanned += num_docs;

@@ -1,7 +1,7 @@
 """ctypes mirror of include/pinot_gpu.h (the C ABI).  Shared by the GPU binding and the oracle."""
 import ctypes as C
 
-PG_ABI_VERSION = 3
+PG_ABI_VERSION = 4
 
 PG_OK, PG_E_INVALID, PG_E_HIP, PG_E_NOMEM, PG_E_NOTFOUND, PG_E_UNSUPPORTED, PG_E_CANCELLED, PG_E_TIMEOUT, \
     PG_E_STATE = 0, -1, -2, -3, -4, -5, -6, -7, -8
@@ -9,14 +9,14 @@ STATUS_NAMES = {0: "PG_OK", -1: "PG_E_INVALID", -2: "PG_E_HIP", -3: "PG_E_NOMEM"
                 -5: "PG_E_UNSUPPORTED", -6: "PG_E_CANCELLED", -7: "PG_E_TIMEOUT", -8: "PG_E_STATE"}
 
 PG_IDX_DICT, PG_IDX_FWD_SV_BITPACKED, PG_IDX_FWD_SV_SORTED, PG_IDX_FWD_MV_BITPACKED, PG_IDX_INV_BITMAP, \
-    PG_IDX_KEYMAP, PG_IDX_FWD_SV_RAW = 1, 2, 3, 4, 5, 6, 7
+    PG_IDX_KEYMAP, PG_IDX_FWD_SV_RAW, PG_IDX_RANGE = 1, 2, 3, 4, 5, 6, 7, 8
 PG_INT, PG_LONG, PG_FLOAT, PG_DOUBLE, PG_STRING, PG_BYTES = 0, 1, 2, 3, 4, 5
 DTYPE_CODES = {"INT": PG_INT, "LONG": PG_LONG, "FLOAT": PG_FLOAT, "DOUBLE": PG_DOUBLE, "STRING": PG_STRING,
                "BYTES": PG_BYTES}
 PG_SRC_DEVICE = 1
 
 PG_LEAF_MATCH_ALL, PG_LEAF_EMPTY, PG_LEAF_SV_SCAN, PG_LEAF_SORTED, PG_LEAF_INVERTED, PG_LEAF_MV_SCAN, \
-    PG_LEAF_RAW_SCAN = range(7)
+    PG_LEAF_RAW_SCAN, PG_LEAF_RANGE_INDEX = range(8)
 PG_OP_NOT = -1
 
 

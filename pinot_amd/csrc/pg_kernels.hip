@@ -136,7 +136,7 @@ __global__ void decode_pack_kernel(const uint32_t* __restrict__ ids, uint32_t bi
     if (d1 > num_docs) d1 = num_docs;
     uint32_t word = 0;
     for (uint64_t d = d0; d < d1; d++) {
-      uint32_t id = unpack(ids, d, bits);
+      uint32_t id = ids ? unpack(ids, d, bits) : (uint32_t)d;  // ids == nullptr: `dict` holds the doc values
       id = id < card ? id : card - 1u;
       const int64_t v = dtype == PG_INT ? (int64_t)((const int32_t*)dict)[id] : ((const int64_t*)dict)[id];
       const uint64_t x = (uint64_t)(v - vmin);

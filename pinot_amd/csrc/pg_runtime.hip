@@ -216,6 +216,8 @@ struct ColumnRes {
   uint32_t vbits = 0;
   // raw (no-dictionary) forward index: the num_docs values, native typed (dtype), decoded from the chunks at upload
   DevBuf rawv;
+  // range index (PG_IDX_RANGE): present; a raw INT / LONG column's device form is `vals` (value - imin, vbits bits)
+  bool has_range = false;
 };
 
 // Dictionaries at least this large get a decoded forward index (PG_DECODED=0 disables, =1 builds it for every
@@ -661,6 +663,29 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
       HIP_CHECK(hipStreamSynchronize(s));  // `be` (pageable) is released at the end of this block
       break;
     }
+    case PG_IDX_RANGE: {
+      // header only (readers/BitSlicedRangeIndexReader.java:44-52, RangeIndexReaderImpl.java:47-95); the body is
+      // not needed on the device (see PG_IDX_RANGE in pinot_gpu.h)
+      std::vector<uint8_t> hb;
+      if ((rc = host_copy(src, std::min<uint64_t>(nbytes, 64), on_dev, hb))) return rc;
+      if (hb.size() < 12) return fail(PG_E_INVALID, "range index: %llu bytes", (unsigned long long)nbytes);
+      const uint32_t version = rd_be32(&hb[0]);
+      if (version == 2) {
+        tmp.imin = (int64_t)(((uint64_t)rd_be32(&hb[4]) << 32) | rd_be32(&hb[8]));  // BitSliced min
+      } else if (version == 1) {
+        const uint32_t len = rd_be32(&hb[4]);
+        if (len < 3 || len > 6 || 12 + len > hb.size()) return fail(PG_E_INVALID, "range index v1: bad value type");
+        const std::string vt((const char*)&hb[8], len);
+        if (vt != "INT" && vt != "LONG" && vt != "FLOAT" && vt != "DOUBLE")
+          return fail(PG_E_INVALID, "range index v1: value type %s", vt.c_str());
+        tmp.imin = INT64_MIN;  // v1 keeps no min
+      } else {
+        return fail(PG_E_INVALID, "range index: unknown version %u", version);
+      }
+      tmp.has_range = true;
+      tmp.num_values = version;
+      break;
+    }
     case PG_IDX_KEYMAP: {
       if (nbytes < 4ull * d->cardinality) return fail(PG_E_INVALID, "keymap too small");
       tmp.has_keymap = true;
@@ -707,7 +732,29 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
       c.has_keymap = true;
       c.keymap = std::move(tmp.keymap);
       break;
+    case PG_IDX_RANGE: {
+      if (c.fwd != FWD_SV && c.fwd != FWD_SORTED && c.fwd != FWD_RAW)
+        return fail(PG_E_INVALID, "range index on column %u before its single-value forward index", col_id);
+      const bool raw = c.fwd == FWD_RAW;
+      // v2 min: 0 for dictIds (BitSlicedRangeIndexCreator.java:46-48), the column min for a raw INT / LONG column
+      if (tmp.num_values == 2 && (raw ? (c.dtype <= PG_LONG && tmp.imin != c.imin) : tmp.imin != 0))
+        return fail(PG_E_INVALID, "range index min %lld != column %u's", (long long)tmp.imin, col_id);
+      c.has_range = true;
+      if (raw && c.dtype <= PG_LONG && c.num_docs && c.imax >= c.imin && (uint64_t)(c.imax - c.imin) < (1ull << 30)) {
+        uint32_t vb = 1;
+        while (vb < 30 && ((uint64_t)(c.imax - c.imin) >> vb)) vb++;
+        const uint64_t nwords = ((uint64_t)c.num_docs * vb + 31) / 32 + 4;
+        c.vals.reset();
+        if ((rc = c.vals.alloc(nwords * 4))) return rc;
+        HIP_CHECK(launch_decode_pack(nullptr, 0, c.rawv.p, c.dtype, c.num_docs, c.imin, vb, c.num_docs,
+                                     (uint32_t*)c.vals.p, nwords, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        c.vbits = vb;
+      }
+      break;
+    }
     case PG_IDX_FWD_SV_RAW:
+      c.has_range = false; c.vbits = 0;
       c.words.reset(); c.mv_offsets.reset(); c.rawv.reset(); c.vals.reset();
       c.fwd = FWD_RAW; c.num_docs = tmp.num_docs; c.bits = 0; c.num_values = tmp.num_values;
       c.dtype = tmp.dtype; c.card = tmp.card; c.has_dict = false;
@@ -1202,6 +1249,47 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     if (L && !plan->segments[si].leaves) return fail(PG_E_INVALID, "segment %u has no leaves", si);
   }
 
+  // ---- RangeIndexBasedFilterOperator leaves (PG_LEAF_RANGE_INDEX): lowered onto the forms that evaluate them.  A
+  // dictionary column's range index answers dictIds [lo, hi) -> the packed forward index (SV scan form); a raw INT /
+  // LONG column's becomes a dictId-like range over its packed (value - min) offsets (kind kept RANGE_INDEX, its own
+  // staging slot); a raw FLOAT / DOUBLE column's is the raw compare.  All are exact index leaves: no entries
+  // scanned in the filter (BitSlicedRangeIndexReader.isExact, RangeIndexBasedFilterOperator.java:62-67).
+  pg_plan shadow;
+  std::vector<pg_segment_ref> shadow_segs;
+  std::vector<pg_leaf> shadow_leaves;
+  std::vector<uint8_t> index_leaf((uint64_t)S * L, 0);
+  {
+    bool any = false;
+    for (uint32_t si = 0; si < S && !any; si++)
+      for (uint32_t li = 0; li < L; li++) any |= plan->segments[si].leaves[li].kind == PG_LEAF_RANGE_INDEX;
+    if (any) {
+      shadow = *plan;
+      shadow_segs.assign(plan->segments, plan->segments + S);
+      shadow_leaves.resize((uint64_t)S * L);
+      for (uint32_t si = 0; si < S; si++) {
+        std::copy(plan->segments[si].leaves, plan->segments[si].leaves + L, &shadow_leaves[(uint64_t)si * L]);
+        shadow_segs[si].leaves = &shadow_leaves[(uint64_t)si * L];
+        for (uint32_t li = 0; li < L; li++) {
+          pg_leaf& pl = shadow_leaves[(uint64_t)si * L + li];
+          if (pl.kind != PG_LEAF_RANGE_INDEX) continue;
+          const ColumnRes* c = col(si, pl.col_id);
+          if (!c) return fail(PG_E_NOTFOUND, "leaf %u: column %u not resident in segment %u", li, pl.col_id, si);
+          if (!c->has_range) return fail(PG_E_INVALID, "range-index leaf on column %u without a range index", pl.col_id);
+          if (pl.num_ids) return fail(PG_E_INVALID, "range-index leaf %u with a value list (RANGE predicates only)", li);
+          index_leaf[(uint64_t)si * L + li] = 1;
+          if (c->fwd != FWD_RAW) { pl.kind = PG_LEAF_SV_SCAN; continue; }
+          if (!c->vals.p) { pl.kind = PG_LEAF_RAW_SCAN; continue; }
+          // closed [ilo, ihi] on the values -> [lo, hi) on the offsets (value - imin); vbits <= 30 keeps both in int32
+          const int64_t lo = std::max(pl.ilo, c->imin), hi = std::min(pl.ihi, c->imax);
+          pl.lo = lo > hi ? 0 : (int32_t)(lo - c->imin);
+          pl.hi = lo > hi ? 0 : (int32_t)(hi - c->imin + 1);
+        }
+      }
+      shadow.segments = shadow_segs.data();
+      plan = &shadow;
+    }
+  }
+
   QuerySpec q;
   memset(&q, 0, sizeof(q));
   q.num_segments = S;
@@ -1459,6 +1547,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         f = std::min(1.0, nset / card);
         if (pl.exclusive) f = 1.0 - f;
         if (pl.kind == PG_LEAF_SV_SCAN) cost = c->bits / 8.0;
+        if (pl.kind == PG_LEAF_RANGE_INDEX) cost = c->vbits / 8.0;
         if (pl.kind == PG_LEAF_MV_SCAN) cost = 0.0;  // materialised by the pre-pass
       }
       leaf_pass[li] += w * f;
@@ -1599,7 +1688,16 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
           const uint64_t off = ar.put(pl.values, 8ull * pl.num_ids);
           patches.push_back({(uint64_t)si * L + li, off, true, PT_RVALS});
         }
-        entries_in_filter += sr.num_docs;
+        if (!index_leaf[(uint64_t)si * L + li]) entries_in_filter += sr.num_docs;
+        continue;
+      }
+      if (pl.kind == PG_LEAF_RANGE_INDEX) {  // raw INT / LONG range index: offsets [lo, hi) of the packed values
+        dl.kind = LK_RANGE;
+        dl.words = (const uint32_t*)c->vals.p;
+        dl.wbytes = (uint32_t)std::min<uint64_t>(c->vals.bytes, 0xFFFFFFF0ull);
+        dl.bits = c->vbits;
+        dl.lo = pl.lo;
+        dl.hi = std::max(pl.hi, pl.lo);
         continue;
       }
       if (pl.num_ids && !pl.ids) return fail(PG_E_INVALID, "leaf %u: null id list", li);
@@ -1617,7 +1715,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
           dl.words = (const uint32_t*)c->words.p;
           dl.wbytes = (uint32_t)std::min<uint64_t>(c->words.bytes, 0xFFFFFFF0ull);
           dl.bits = c->bits;
-          entries_in_filter += sr.num_docs;
+          if (!index_leaf[(uint64_t)si * L + li]) entries_in_filter += sr.num_docs;
           const bool contiguous = pl.num_ids && (uint32_t)(pl.ids[pl.num_ids - 1] - pl.ids[0]) + 1 == pl.num_ids;
           if (!pl.num_ids || contiguous) {
             dl.kind = LK_RANGE;
@@ -1742,7 +1840,9 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         dc.bits = c->bits;
         dc.dtype = c->dtype;
         dc.card = c->card;
-        if (c->fwd == FWD_RAW) {  // the values themselves: "dictId" = doc id (bits 0), "dictionary" = the values
+        if (c->fwd == FWD_RAW && agg_decodes(g) && c->vals.p) {
+          use_decoded(dc, c);  // the range index's packed (value - min) offsets: fewer bytes than the values
+        } else if (c->fwd == FWD_RAW) {  // the values themselves: "dictId" = doc id (bits 0), "dictionary" = the values
           dc.words = nullptr;
           dc.wbytes = 0;
           dc.bits = 0;

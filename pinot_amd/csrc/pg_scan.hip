@@ -51,6 +51,32 @@ template <class T> __device__ __forceinline__ T ldc(const T* p, uint64_t i) {
   return v;
 }
 template <class T> __device__ __forceinline__ const PG_GLOBAL T* glb(const T* p) { return (const PG_GLOBAL T*)p; }
+#define PG_LDS __attribute__((address_space(3)))
+
+// Atomics through address-space-typed pointers: a generic pointer makes every atomic a FLAT atomic, which counts on
+// both the vector-memory and the LDS counters, so each LDS-privatised update waited for the wave's outstanding HBM
+// stores (config 4's entry append ran 4x slower that way).  g_*: global (agent scope), l_*: LDS (workgroup scope).
+template <class T> __device__ __forceinline__ T g_add(T* p, T v) {
+  return __hip_atomic_fetch_add((PG_GLOBAL T*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T> __device__ __forceinline__ T l_add(T* p, T v) {
+  return __hip_atomic_fetch_add((PG_LDS T*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <class T> __device__ __forceinline__ void g_min(T* p, T v) {
+  __hip_atomic_fetch_min((PG_GLOBAL T*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T> __device__ __forceinline__ void l_min(T* p, T v) {
+  __hip_atomic_fetch_min((PG_LDS T*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <class T> __device__ __forceinline__ void g_max(T* p, T v) {
+  __hip_atomic_fetch_max((PG_GLOBAL T*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T> __device__ __forceinline__ void l_max(T* p, T v) {
+  __hip_atomic_fetch_max((PG_LDS T*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void g_or(uint32_t* p, uint32_t v) {
+  __hip_atomic_fetch_or((PG_GLOBAL uint32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 constexpr uint32_t kRowMask = 0xFFFFFFFFu;                     // kRows == 32
 static_assert(kRows == 32, "masks are 32-bit");
 
@@ -495,12 +521,12 @@ __device__ __forceinline__ void part_append(const QuerySpec& q, uint32_t* lds, u
   if (!bal) return;
   const uint32_t leader = (uint32_t)__builtin_ctzll(bal);
   uint32_t base = 0;
-  if ((threadIdx.x & 63u) == leader) base = atomicAdd(&lds[0], (uint32_t)__popcll(bal));
+  if ((threadIdx.x & 63u) == leader) base = l_add(&lds[0], (uint32_t)__popcll(bal));
   base = __builtin_amdgcn_readlane(base, leader);
   if (on) {
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
     out[base + rank] = (g << q.part_vbits) | vid;
-    atomicAdd(&lds[1 + (uint32_t)(g >> q.part_shift)], 1u);
+    l_add(&lds[1 + (uint32_t)(g >> q.part_shift)], 1u);
   }
 }
 
@@ -519,14 +545,14 @@ __device__ __forceinline__ void part_append8(const QuerySpec& q, uint32_t* lds, 
   }
   if (!total) return;
   uint32_t base = 0;
-  if ((threadIdx.x & 63u) == 0) base = atomicAdd(&lds[0], total);
+  if ((threadIdx.x & 63u) == 0) base = l_add(&lds[0], total);
   base = __builtin_amdgcn_readlane(base, 0);
 #pragma unroll
   for (int r = 0; r < 8; r++) {
     if (!((live >> r) & 1u)) continue;
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[r] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[r], 0u));
     out[base + pre[r] + rank] = ((uint64_t)g[r] << q.part_vbits) | vid[r];
-    atomicAdd(&lds[1 + (uint32_t)((uint64_t)g[r] >> q.part_shift)], 1u);
+    l_add(&lds[1 + (uint32_t)((uint64_t)g[r] >> q.part_shift)], 1u);
   }
 }
 
@@ -542,7 +568,20 @@ struct GroupState {
   long long* mn;
   long long* mx;
   unsigned long long* out;   // GM_PART: the block's region of the entry array
+  bool lds;                  // the arrays are the block's LDS copy (block-uniform)
 };
+__device__ __forceinline__ void s_add(const GroupState& S, unsigned long long* p, unsigned long long v) {
+  if (S.lds) l_add(p, v); else g_add(p, v);
+}
+__device__ __forceinline__ void s_addf(const GroupState& S, double* p, double v) {
+  if (S.lds) l_add(p, v); else g_add(p, v);
+}
+__device__ __forceinline__ void s_min(const GroupState& S, long long* p, long long v) {
+  if (S.lds) l_min(p, v); else g_min(p, v);
+}
+__device__ __forceinline__ void s_max(const GroupState& S, long long* p, long long v) {
+  if (S.lds) l_max(p, v); else g_max(p, v);
+}
 
 // Per-doc update of one aggregation in group slot g (aggregateGroupBySV of each function).
 __device__ __forceinline__ void group_update(const QuerySpec& q, const GroupState& S, const AggSpec& A,
@@ -550,18 +589,18 @@ __device__ __forceinline__ void group_update(const QuerySpec& q, const GroupStat
   switch (A.fn) {
     case PG_AGG_COUNT: break;  // = slot 0
     case PG_AGG_COUNTMV:
-      atomicAdd(&S.i64[g * q.n_i64 + A.slot], (unsigned long long)(glb(ldc(c, 0).mv_offsets)[d + 1] - glb(ldc(c, 0).mv_offsets)[d]));
+      s_add(S, &S.i64[g * q.n_i64 + A.slot], (unsigned long long)(glb(ldc(c, 0).mv_offsets)[d + 1] - glb(ldc(c, 0).mv_offsets)[d]));
       break;
     case PG_AGG_SUM:
     case PG_AGG_AVG:  // AVG count == slot 0
-      if (A.integer) atomicAdd(&S.i64[g * q.n_i64 + A.slot], (unsigned long long)value_i64(A, c, ia, ib));
-      else atomicAdd(&S.f64[g * q.n_f64 + A.slot], value_f64(A, c, ia, ib));
+      if (A.integer) s_add(S, &S.i64[g * q.n_i64 + A.slot], (unsigned long long)value_i64(A, c, ia, ib));
+      else s_addf(S, &S.f64[g * q.n_f64 + A.slot], value_f64(A, c, ia, ib));
       break;
-    case PG_AGG_MIN: atomicMin(&S.mn[g * q.n_min + A.slot], (long long)order_key(value_f64(A, c, ia, ib))); break;
-    case PG_AGG_MAX: atomicMax(&S.mx[g * q.n_max + A.slot], (long long)order_key(value_f64(A, c, ia, ib))); break;
+    case PG_AGG_MIN: s_min(S, &S.mn[g * q.n_min + A.slot], (long long)order_key(value_f64(A, c, ia, ib))); break;
+    case PG_AGG_MAX: s_max(S, &S.mx[g * q.n_max + A.slot], (long long)order_key(value_f64(A, c, ia, ib))); break;
     case PG_AGG_DISTINCTCOUNT: {
       const uint64_t key = key_of(A.key_kind, A.key_base, ldc(c, 0), ia);
-      if (key < A.key_card) atomicOr(&q.dbits[g * q.dc_row_words + A.dc_word + (key >> 5)], 1u << (key & 31u));
+      if (key < A.key_card) g_or(&q.dbits[g * q.dc_row_words + A.dc_word + (key >> 5)], 1u << (key & 31u));
       else atomicOr(q.err, 2u);
       break;
     }
@@ -591,7 +630,7 @@ __device__ __forceinline__ void acc_update(const QuerySpec& q, const AggSpec& A,
     }
     case PG_AGG_DISTINCTCOUNT: {
       const uint64_t key = key_of(A.key_kind, A.key_base, ldc(c, 0), ia);
-      if (key < A.key_card) atomicOr(&q.dbits[A.dc_word + (key >> 5)], 1u << (key & 31u));
+      if (key < A.key_card) g_or(&q.dbits[A.dc_word + (key >> 5)], 1u << (key & 31u));
       else atomicOr(q.err, 2u);
       break;
     }
@@ -624,7 +663,7 @@ __device__ __forceinline__ void agg_rows8(const QuerySpec& q, const GroupState& 
 #pragma unroll
         for (int r = 0; r < 8; r++) {
           if (!((live >> r) & 1u)) continue;
-          if constexpr (GROUPED) atomicAdd(&S.i64[(uint64_t)g[r] * q.n_i64 + A.slot], (unsigned long long)v[r]);
+          if constexpr (GROUPED) s_add(S, &S.i64[(uint64_t)g[r] * q.n_i64 + A.slot], (unsigned long long)v[r]);
           else acc += (uint64_t)v[r];
         }
       } else {
@@ -634,7 +673,7 @@ __device__ __forceinline__ void agg_rows8(const QuerySpec& q, const GroupState& 
 #pragma unroll
         for (int r = 0; r < 8; r++) {
           if (!((live >> r) & 1u)) continue;
-          if constexpr (GROUPED) atomicAdd(&S.f64[(uint64_t)g[r] * q.n_f64 + A.slot], v[r]);
+          if constexpr (GROUPED) s_addf(S, &S.f64[(uint64_t)g[r] * q.n_f64 + A.slot], v[r]);
           else acc = __double_as_longlong(__longlong_as_double(acc) + v[r]);
         }
       }
@@ -649,8 +688,8 @@ __device__ __forceinline__ void agg_rows8(const QuerySpec& q, const GroupState& 
       for (int r = 0; r < 8; r++) {
         if (!((live >> r) & 1u)) continue;
         if constexpr (GROUPED) {
-          if (is_min) atomicMin(&S.mn[(uint64_t)g[r] * q.n_min + A.slot], (long long)k[r]);
-          else atomicMax(&S.mx[(uint64_t)g[r] * q.n_max + A.slot], (long long)k[r]);
+          if (is_min) s_min(S, &S.mn[(uint64_t)g[r] * q.n_min + A.slot], (long long)k[r]);
+          else s_max(S, &S.mx[(uint64_t)g[r] * q.n_max + A.slot], (long long)k[r]);
         } else {
           if (is_min ? k[r] < (int64_t)acc : k[r] > (int64_t)acc) acc = (uint64_t)k[r];
         }
@@ -734,7 +773,7 @@ __device__ __forceinline__ void aggregate_dense(const QuerySpec& q, const SegDes
       }
 #pragma unroll
       for (int r = 0; r < 8; r++)
-        if ((live >> r) & 1u) atomicAdd(&S.i64[(uint64_t)g[r] * q.n_i64], 1ull);  // slot 0: doc count / presence
+        if ((live >> r) & 1u) s_add(S, &S.i64[(uint64_t)g[r] * q.n_i64], 1ull);  // slot 0: doc count / presence
     }
 #pragma unroll
     for (int a = 0; a < MAXA; a++) {
@@ -835,7 +874,7 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
         }
         g = group_slot(q, g, sd.index, d[x]);
         if (g == ~0ull) continue;
-        atomicAdd(&S.i64[g * q.n_i64], 1ull);  // slot 0: doc count / presence
+        s_add(S, &S.i64[g * q.n_i64], 1ull);  // slot 0: doc count / presence
 #pragma unroll
         for (int a = 0; a < MAXA; a++) {
           if (a >= (int)q.num_aggs) break;
@@ -903,8 +942,8 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
     __syncthreads();
   }
   const GroupState S = (q.use_lds || part)
-                           ? GroupState{l_i64, l_f64, l_mn, l_mx, part ? q.part_out + q.part_base[blockIdx.x] : nullptr}
-                           : GroupState{q.i64, q.f64, q.mn, q.mx, nullptr};
+                           ? GroupState{l_i64, l_f64, l_mn, l_mx, part ? q.part_out + q.part_base[blockIdx.x] : nullptr, true}
+                           : GroupState{q.i64, q.f64, q.mn, q.mx, nullptr, false};
 
   // aggregation-only accumulators (registers; indices compile-time via unrolled agg loops)
   uint64_t acc[MAXA];
@@ -990,7 +1029,7 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
         if (cur_seg != 0xFFFFFFFFu) {
           if (qn) flush();  // the queue holds docs of the previous segment
           const uint64_t c = wave_sum_u64(seg_count);
-          if (lane == 0 && c) atomicAdd(&q.seg_matched[cur_seg], (unsigned long long)c);
+          if (lane == 0 && c) g_add(&q.seg_matched[cur_seg], (unsigned long long)c);
           seg_count = 0;
         }
         cur_sd = ldc(q.segs, it.seg);
@@ -1072,7 +1111,7 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
     }
     if (qn && !(q.cancel && (stop[0] | stop[1]))) flush();
     const uint64_t c = wave_sum_u64(seg_count);
-    if (lane == 0 && c) atomicAdd(&q.seg_matched[cur_seg], (unsigned long long)c);
+    if (lane == 0 && c) g_add(&q.seg_matched[cur_seg], (unsigned long long)c);
   }
 
   if (!GROUPED) {

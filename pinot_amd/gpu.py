@@ -14,7 +14,8 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from . import abi
-from .plan import CPlan, ExecutionStats, IntermediateResult, Table, UnsupportedQuery
+from .plan import (CPlan, ExecutionStats, IntermediateResult, Table, UnsupportedQuery, execute_filtered,
+                   has_filtered_aggregations)
 from .query import QueryContext, parse
 from .segment import Column, ImmutableSegment
 
@@ -99,6 +100,10 @@ class GpuEngine:
                 di = abi.pg_col_desc.from_buffer_copy(d)
                 di.kind = abi.PG_IDX_INV_BITMAP
                 self._upload(key, cid, di, col.inverted)
+            if col.range_index is not None:  # after the forward index: its device form derives from it
+                dr = abi.pg_col_desc.from_buffer_copy(d)
+                dr.kind = abi.PG_IDX_RANGE
+                self._upload(key, cid, dr, col.range_index)
         self._seg_keys[id(seg)] = (seg, key)
         return key
 
@@ -205,6 +210,8 @@ class GpuEngine:
                 trim: bool = False) -> IntermediateResult:
         if isinstance(query, str):
             query = parse(query)
+        if has_filtered_aggregations(query):  # FilteredAggregationOperator: one device plan per filter
+            return execute_filtered(lambda q: self.execute(table, q, segments, num_groups_limit, flags), query)
         return self.run_plan(self.make_plan(table, query, segments, num_groups_limit, flags, trim))
 
     def last_timing(self) -> abi.pg_timing:

@@ -8,7 +8,8 @@ Host-side mirror of the reference's planning for the hot path:
     NotInPredicateEvaluatorFactory.java:153-, RangePredicateEvaluatorFactory.java:115-210) and their
     isAlwaysTrue / isAlwaysFalse shortcuts;
   * leaf operator choice -- FilterOperatorUtils.getLeafFilterOperator (operator/filter/FilterOperatorUtils.java:45-85):
-    always-false -> Empty, always-true -> MatchAll, sorted -> SortedIndex, inverted (non-RANGE) -> Bitmap, else scan;
+    always-false -> Empty, always-true -> MatchAll, sorted -> SortedIndex, RANGE + range index -> RangeIndex,
+    inverted (non-RANGE) -> Bitmap, else scan;
   * group keys -- table-global key ids so that the device merges segments by VALUE the way
     GroupByOrderByCombineOperator merges Key(Object[]) (operator/combine/GroupByOrderByCombineOperator.java:176-183).
 """
@@ -22,7 +23,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import abi
-from .query import UNBOUNDED, Aggregation, FilterContext, Predicate, QueryContext
+from .query import (UNBOUNDED, Aggregation, Expr, FilterContext, Predicate, QueryContext, SelectItem,
+                    filter_str)
 from .segment import Column, ImmutableSegment
 
 MAX_VALUE_OFFSET_KEYS = 1 << 26   # integer key ranges up to this size may use value offsets (no keymap) ...
@@ -124,7 +126,10 @@ def lower_raw_predicate(pred: Predicate, col: Column, col_id: int) -> LoweredLea
 def lower_predicate(pred: Predicate, col: Column, col_id: int) -> LoweredLeaf:
     """Dictionary-based predicate evaluator + leaf operator choice for one segment's column."""
     if col.dictionary is None:
-        return lower_raw_predicate(pred, col, col_id)
+        lw = lower_raw_predicate(pred, col, col_id)
+        if pred.type == "RANGE" and col.range_index is not None:
+            lw.kind = abi.PG_LEAF_RANGE_INDEX   # FilterOperatorUtils.java:60-66: RANGE + range index
+        return lw
     d = col.dictionary
     card = len(d)
     excl = 0
@@ -182,6 +187,8 @@ def lower_predicate(pred: Predicate, col: Column, col_id: int) -> LoweredLeaf:
         return LoweredLeaf(abi.PG_LEAF_MATCH_ALL, col_id)
     if col.single_value and col.is_sorted:
         kind = abi.PG_LEAF_SORTED
+    elif t == "RANGE" and col.range_index is not None:
+        kind = abi.PG_LEAF_RANGE_INDEX         # RangeIndexBasedFilterOperator
     elif col.inverted is not None and t != "RANGE":
         kind = abi.PG_LEAF_INVERTED
     else:
@@ -408,6 +415,73 @@ def reduce_to_rows(query: QueryContext, res: IntermediateResult) -> Tuple[List[s
     return names, rows_out
 
 
+# ------------------------------------------------------------------------------------------ filtered aggregations
+
+def has_filtered_aggregations(query: QueryContext) -> bool:
+    """QueryContext.isHasFilteredAggregations (QueryContext.java:261, set at :531-533)."""
+    return any(a.filter is not None for a in query.aggregations)
+
+
+def filtered_aggregation_passes(query: QueryContext) -> List[Tuple[QueryContext, List[int]]]:
+    """AggregationPlanNode.buildFilteredAggOperator (plan/AggregationPlanNode.java:87-146): one pass per distinct
+    aggregation filter f, over CombinedFilterOperator(main, f) = main AND f (CombinedFilterOperator.java:56-61), plus
+    the main filter's pass for the non-filtered aggregations (always run, even with none: its docs count in the
+    statistics).  Returns [(pass query, indices into query.aggregations)], the main pass last.  A pass with no
+    aggregation of its own carries COUNT(*) so that the engines report its docs."""
+    aggs = query.aggregations
+    groups: Dict[str, Tuple[FilterContext, List[int]]] = {}
+    plain: List[int] = []
+    for i, a in enumerate(aggs):
+        if a.filter is None:
+            plain.append(i)
+            continue
+        groups.setdefault(filter_str(a.filter), (a.filter, []))[1].append(i)
+    out = []
+    for f, idx in groups.values():
+        combined = f if query.filter is None else FilterContext(
+            "AND", (query.filter.children if query.filter.type == "AND" else [query.filter]) +
+            (f.children if f.type == "AND" else [f]))
+        out.append((_pass_query(query, combined, [Aggregation(aggs[i].function, aggs[i].arg) for i in idx]), idx))
+    out.append((_pass_query(query, query.filter, [aggs[i] for i in plain] or [Aggregation("COUNT", Expr("STAR"))]),
+                plain))
+    return out
+
+
+def _pass_query(query: QueryContext, filt, aggs: List[Aggregation]) -> QueryContext:
+    return QueryContext(query.table, [SelectItem("AGG", agg=a) for a in aggs], filt, [], [], query.limit,
+                        dict(query.options))
+
+
+def assemble_filtered(query: QueryContext, passes, results: List["IntermediateResult"]) -> "IntermediateResult":
+    """FilteredAggregationOperator.getNextBlock (operator/query/FilteredAggregationOperator.java:70-98): each
+    function's result from its pass; numDocsScanned and numEntriesScannedInFilter summed over the passes,
+    numEntriesScannedPostFilter = sum of (pass docs x the columns of ALL the aggregations) -- every pass projects
+    the whole aggregation expression set (buildTransformOperatorForFilteredAggregates, :159-166); numTotalDocs and
+    the segment counts from the main pass (its docs contain every other pass's)."""
+    aggs = query.aggregations
+    row = [None] * len(aggs)
+    st = ExecutionStats()
+    projected = len({c for a in aggs if a.function != "COUNT" for c in a.arg.cols})
+    for (pq, idx), res in zip(passes, results):
+        vals = res.rows.get((), None) or default_row(pq.aggregations)
+        for k, i in enumerate(idx):
+            row[i] = vals[k]
+        st.num_docs_scanned += res.stats.num_docs_scanned
+        st.num_entries_scanned_in_filter += res.stats.num_entries_scanned_in_filter
+        st.num_entries_scanned_post_filter += res.stats.num_docs_scanned * projected
+    main = results[-1].stats
+    st.num_total_docs = main.num_total_docs
+    st.num_segments_processed = main.num_segments_processed
+    st.num_segments_matched = main.num_segments_matched
+    return IntermediateResult(aggs, [], {(): row}, st)
+
+
+def execute_filtered(run, query: QueryContext) -> "IntermediateResult":
+    """Runs the passes of a query with filtered aggregations through `run(pass_query) -> IntermediateResult`."""
+    passes = filtered_aggregation_passes(query)
+    return assemble_filtered(query, passes, [run(pq) for pq, _ in passes])
+
+
 class _Ord:
     __slots__ = ("v", "asc")
 
@@ -435,6 +509,8 @@ class CPlan:
         self.table = table
         self.query = query
         self.aggs = query.aggregations
+        if has_filtered_aggregations(query):
+            raise UnsupportedQuery("filtered aggregations run as one plan per filter (execute_filtered)")
         self._keep = []
         cid = table.column_ids
         ops, preds = filter_program(query.filter)

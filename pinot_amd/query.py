@@ -66,9 +66,13 @@ class Expr:
 class Aggregation:
     function: str     # COUNT, SUM, MIN, MAX, AVG, DISTINCTCOUNT, COUNTMV
     arg: Expr
+    # `AGG(x) FILTER (WHERE f)`: the aggregation's own filter, ANDed with the query's (QueryContext's
+    # filteredAggregationFunctions, QueryContext.java:512-560); part of equality, not of the hash
+    filter: Optional[FilterContext] = field(default=None, hash=False)
 
     def result_name(self):
-        return f"{self.function.lower()}({self.arg})"
+        base = f"{self.function.lower()}({self.arg})"
+        return base if self.filter is None else f"{base} FILTER(WHERE {filter_str(self.filter)})"
 
 
 @dataclass
@@ -195,7 +199,15 @@ class _Parser:
             fn = v.upper()
             if fn == "COUNT":
                 e = Expr("STAR")
-            return "AGG", Aggregation(fn, e)
+            filt = None
+            if self.peek()[0] == "id" and self.peek()[1].upper() == "FILTER" and self.peek(1) == ("op", "("):
+                # AGG(x) FILTER (WHERE f) -- CalciteSqlParser's FILTER clause -> FilterContext of the aggregation
+                self.next()
+                self.expect("op", "(")
+                self.expect("kw", "WHERE")
+                filt = self.or_expr()
+                self.expect("op", ")")
+            return "AGG", Aggregation(fn, e, filt)
         return "COL", self.expect("id")
 
     def literal(self) -> str:
@@ -262,6 +274,19 @@ class _Parser:
         while self.accept("kw", "OR"):
             parts.append(self.and_expr())
         return parts[0] if len(parts) == 1 else FilterContext("OR", _flatten("OR", parts))
+
+
+def filter_str(f: FilterContext) -> str:
+    """A canonical text of a filter tree (FilterContext.toString's role: equal filters, equal text)."""
+    if f.type == "PREDICATE":
+        p = f.predicate
+        if p.type == "RANGE":
+            return (f"{p.column} {'[' if p.lower_inclusive else '('}{p.lower},{p.upper}"
+                    f"{']' if p.upper_inclusive else ')'}")
+        return f"{p.column} {p.type} ({','.join(p.values)})"
+    if f.type == "NOT":
+        return f"NOT({filter_str(f.children[0])})"
+    return f"{f.type}(" + ", ".join(filter_str(c) for c in f.children) + ")"
 
 
 def _flatten(kind, parts):
@@ -331,4 +356,7 @@ def parse(sql: str) -> QueryContext:
         p.expect("op", ")")
     if p.peek() != (None, None):
         raise ValueError(f"trailing tokens: {p.t[p.i:]}")
+    if group_by and any(s.kind == "AGG" and s.agg.filter is not None for s in select):
+        # QueryContext.generateAggregationFunctions (QueryContext.java:531-533)
+        raise ValueError("GROUP BY with FILTER clauses is not supported")
     return QueryContext(table, select, filt, group_by, order_by, limit, options)

@@ -29,7 +29,7 @@ import bisect
 import os
 import struct
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -390,6 +390,96 @@ def raw_forward_values(buf: bytes, data_type: str, num_docs: Optional[int] = Non
 
 # ----------------------------------------------------------------------------- columns / segments
 
+# ------------------------------------------------------------------------------------------ range index
+# RangeIndexCreator v1 (segment/creator/impl/inv/RangeIndexCreator.java:248-400) file layout, big-endian:
+#   int VERSION (1) | int len, bytes of the value type name (INT/LONG/FLOAT/DOUBLE; dictIds of a dictionary column are
+#   INT, DefaultIndexCreatorProvider.java:285-287) | int R | R range start values + the last range's end value |
+#   (R + 1) long bitmap offsets from the file start (the last = file size) | R portable roaring bitmaps (not
+#   run-optimised) of the docs whose value falls in each range.
+# BitSlicedRangeIndexCreator v2 (:112-124): int VERSION (2) | long min (0 for dictIds; column min for INT / LONG;
+#   0 for FP ordinals) | RoaringBitmap 0.9.28's RangeBitmap.Appender serialization (not restated: the library is
+#   not vendored in the reference; the device derives the index from the forward index, see PG_IDX_RANGE).
+RANGE_V1, RANGE_V2 = 1, 2
+RANGE_DEFAULT_NUM_RANGES = 20
+_RANGE_TYPES = {"INT": ">i4", "LONG": ">i8", "FLOAT": ">f4", "DOUBLE": ">f8"}
+
+
+def range_index_v1_bytes(values: np.ndarray, value_type: str, num_ranges: int = RANGE_DEFAULT_NUM_RANGES) -> bytes:
+    """RangeIndexCreator.seal: sort the values (docIds alongside), cut a new range at the first value change after
+    more than numValuesPerRange = ceil(n / numRanges) values, one bitmap per range."""
+    v = np.asarray(values)
+    n = v.size
+    if n == 0:
+        raise ValueError("range index over no values")
+    per = (n + num_ranges - 1) // num_ranges
+    order = np.argsort(v, kind="stable")
+    sv = v[order]
+    change = np.flatnonzero(sv[1:] != sv[:-1]) + 1      # i with sv[i] != sv[i - 1]
+    ranges, start = [], 0
+    while True:  # `if (i > start + boundary && compare(i, i - 1) != 0)` over i ascending
+        j = np.searchsorted(change, start + per + 1)
+        if j >= change.size:
+            break
+        i = int(change[j])
+        ranges.append((start, i - 1))
+        start = i
+    ranges.append((start, n - 1))
+    vt = _RANGE_TYPES[value_type]
+    name = value_type.encode()
+    head = struct.pack(">ii", RANGE_V1, len(name)) + name + struct.pack(">i", len(ranges))
+    head += np.asarray([sv[a] for a, _ in ranges] + [sv[-1]], dtype=vt).tobytes()
+    bitmaps = [roaring_serialize(np.sort(order[a:b + 1]), run_optimize=False) for a, b in ranges]
+    off = len(head) + 8 * (len(ranges) + 1)
+    offs = [off]
+    for bm in bitmaps:
+        off += len(bm)
+        offs.append(off)
+    return head + np.asarray(offs, dtype=">i8").tobytes() + b"".join(bitmaps)
+
+
+def range_index_header(buf: bytes) -> dict:
+    """RangeIndexReaderImpl (readers/RangeIndexReaderImpl.java:47-95) / BitSlicedRangeIndexReader header."""
+    version = struct.unpack_from(">i", buf, 0)[0]
+    if version == RANGE_V2:
+        return {"version": 2, "min": struct.unpack_from(">q", buf, 4)[0]}
+    if version != RANGE_V1:
+        raise ValueError(f"unknown range index version {version}")
+    ln = struct.unpack_from(">i", buf, 4)[0]
+    vtype = buf[8:8 + ln].decode()
+    off = 8 + ln
+    r = struct.unpack_from(">i", buf, off)[0]
+    off += 4
+    vt = np.dtype(_RANGE_TYPES[vtype])
+    bounds = np.frombuffer(buf, dtype=vt, count=r + 1, offset=off)
+    off += (r + 1) * vt.itemsize
+    offs = np.frombuffer(buf, dtype=">i8", count=r + 1, offset=off).astype(np.int64)
+    if offs[-1] != len(buf):
+        raise ValueError(f"range index: last offset {offs[-1]} != size {len(buf)}")
+    return {"version": 1, "value_type": vtype, "starts": bounds[:r], "last_end": bounds[r], "offsets": offs}
+
+
+def range_index_v1_docs(buf: bytes, lo, hi) -> Tuple[np.ndarray, np.ndarray]:
+    """RangeIndexReaderImpl.getMatchingDocIds / getPartiallyMatchingDocIds (:146-229) for the closed value range
+    [lo, hi]: docs of the ranges strictly between the two bound ranges, and docs of the bound ranges themselves
+    (RangeIndexBasedFilterOperator scans those, :73-99)."""
+    h = range_index_header(buf)
+    starts, last_end, offs = h["starts"], h["last_end"], h["offsets"]
+
+    def find(x):  # findRangeId
+        for i, s0 in enumerate(starts):
+            if x < s0:
+                return i - 1
+        return len(starts) - 1 if x <= last_end else len(starts)
+
+    def docs(i):
+        return roaring_deserialize(buf[offs[i]:offs[i + 1]])
+    a, b = find(lo), find(hi)
+    full = [docs(i) for i in range(a + 1, b)]
+    part = [docs(i) for i in (a, b) if 0 <= i < len(starts)]
+    cat = lambda xs: np.unique(np.concatenate(xs)) if xs else np.zeros(0, dtype=np.int64)
+    return cat(full), cat(part)
+
+
 @dataclass
 class Column:
     name: str
@@ -410,6 +500,7 @@ class Column:
     # noDictionaryColumns: the values (host copy) of a raw chunked forward index (`fwd`); dictionary is None
     raw_values: Optional[np.ndarray] = None
     raw_cardinality: int = 0
+    range_index: Optional[bytes] = None  # `.bitmap.range` (v1 written here; v1 or v2 loaded)
 
     @property
     def has_dictionary(self) -> bool:
@@ -471,9 +562,11 @@ class ImmutableSegment:
     def create(name: str, data: Dict[str, Sequence], schema: Dict[str, str],
                inverted: Sequence[str] = (), field_types: Optional[Dict[str, str]] = None,
                roaring_run_optimize: bool = True, no_dictionary: Sequence[str] = (),
-               raw_version: int = 2) -> "ImmutableSegment":
+               raw_version: int = 2, range_index: Sequence[str] = ()) -> "ImmutableSegment":
         """schema: column -> data type.  MV columns are given as a list of sequences.  `no_dictionary`: SV numeric
-        columns stored as raw PASS_THROUGH chunked forward indexes (tableIndexConfig.noDictionaryColumns)."""
+        columns stored as raw PASS_THROUGH chunked forward indexes (tableIndexConfig.noDictionaryColumns).
+        `range_index`: SV numeric columns with a range index (tableIndexConfig.rangeIndexColumns), written in the
+        v1 layout (over dictIds for a dictionary column, over the values for a raw one)."""
         cols = {}
         num_docs = None
         for cname, dtype in schema.items():
@@ -516,6 +609,11 @@ class ImmutableSegment:
                 col.fwd = mv_forward_bytes(lengths, ids, b)
                 if cname in inverted:
                     col.inverted = inverted_index_bytes_mv(ids, offsets, card, roaring_run_optimize)
+            if cname in range_index:
+                if not sv or dtype not in _RANGE_TYPES:
+                    raise ValueError(f"range index: {cname} must be a single-value numeric column")
+                col.range_index = range_index_v1_bytes(col.raw_values if col.dictionary is None else ids,
+                                                       dtype if col.dictionary is None else "INT")
             if num_docs is None:
                 num_docs = n
             assert n == num_docs, "ragged columns"
@@ -552,6 +650,9 @@ class ImmutableSegment:
             if c.inverted is not None:
                 with open(os.path.join(path, c.name + ".bitmap.inv"), "wb") as f:
                     f.write(c.inverted)
+            if c.range_index is not None:  # V1Constants.Indexes.BITMAP_RANGE_INDEX_FILE_EXTENSION
+                with open(os.path.join(path, c.name + ".bitmap.range"), "wb") as f:
+                    f.write(c.range_index)
         with open(os.path.join(path, "metadata.properties"), "w") as f:
             f.write("\n".join(self._metadata_lines()) + "\n")
 
@@ -573,6 +674,8 @@ class ImmutableSegment:
                     [("forward_index", c.fwd)]
                 if c.inverted is not None:
                     parts.append(("inverted_index", c.inverted))
+                if c.range_index is not None:
+                    parts.append(("range_index", c.range_index))
                 for idx, payload in parts:
                     psf.write(struct.pack(">Q", self.V3_MAGIC))
                     psf.write(payload)
@@ -617,7 +720,7 @@ class ImmutableSegment:
                 vals = raw_forward_values(fwd, dtype, num_docs)
                 cols[cname] = Column(cname, dtype, True, None, num_docs, b, False, num_docs, 0, fwd, None,
                                      props.get(f"column.{cname}.columnType", "METRIC"), raw_values=vals,
-                                     raw_cardinality=card)
+                                     raw_cardinality=card, range_index=index_bytes(cname, "range"))
                 continue
             dictionary = Dictionary.from_bytes(dtype, index_bytes(cname, "dictionary"), card, eb, padding)
             sv = p("isSingleValues") == "true"
@@ -627,7 +730,8 @@ class ImmutableSegment:
             inv = index_bytes(cname, "inverted")
             col = Column(cname, dtype, sv, dictionary, num_docs, b, is_sorted, nv,
                          int(props.get(f"column.{cname}.maxNumberOfMultiValues", 0)), fwd, inv,
-                         props.get(f"column.{cname}.columnType", "DIMENSION"))
+                         props.get(f"column.{cname}.columnType", "DIMENSION"),
+                         range_index=index_bytes(cname, "range") if sv else None)
             if sv and not is_sorted:
                 col.dict_ids = unpack_bits(fwd, num_docs, b).astype(np.int32)
             elif sv:
@@ -643,12 +747,12 @@ class ImmutableSegment:
     def load_v1(path: str) -> "ImmutableSegment":
         """ImmutableSegmentLoader for the V1 layout (metadata.properties + per-index files)."""
         ext = {"dictionary": ".dict", "sorted": ".sv.sorted.fwd", "unsorted": ".sv.unsorted.fwd", "mv": ".mv.fwd",
-               "inverted": ".bitmap.inv", "raw": ".sv.raw.fwd"}
+               "inverted": ".bitmap.inv", "raw": ".sv.raw.fwd", "range": ".bitmap.range"}
 
         def index_bytes(col, kind):
             fp = os.path.join(path, col + ext[kind])
             if not os.path.exists(fp):
-                if kind == "inverted":
+                if kind in ("inverted", "range"):
                     return None
                 raise FileNotFoundError(fp)
             with open(fp, "rb") as f:
@@ -675,12 +779,13 @@ class ImmutableSegment:
         with open(os.path.join(d, "columns.psf"), "rb") as f:
             psf = f.read()
         names = {"dictionary": "dictionary", "sorted": "forward_index", "unsorted": "forward_index",
-                 "mv": "forward_index", "inverted": "inverted_index", "raw": "forward_index"}
+                 "mv": "forward_index", "inverted": "inverted_index", "raw": "forward_index",
+                 "range": "range_index"}
 
         def index_bytes(col, kind):
             e = entries.get((col, names[kind]))
             if e is None:
-                if kind == "inverted":
+                if kind in ("inverted", "range"):
                     return None
                 raise KeyError(f"{col}.{names[kind]} missing from index_map")
             start, size = e["startOffset"], e["size"]
