@@ -15,7 +15,8 @@ query over all of this GPU's segments: host plan compile + filter pre-pass + fus
 finalize (+ at N > 1 the cross-GPU merge, pinot_amd.combine).  Weak scaling: every rank scans its own segments.
 `--gpus N` without a torchrun environment launches N rank processes (torch.distributed.run) before touching a GPU.
 
-`roofline`: the hot path's kernels (the streaming pre-filter of the selective filter leaves + the fused scan):
+`roofline`: the hot path's kernels (the selective stream over the driving filter leaves + the fused scan over its
+survivors, or the fused scan alone when no leaf prefix is selective):
 algorithmic bytes per query (forward-index bytes of the touched columns + dictionary bytes of the decoded columns,
 SURVEY §8(d)) / their summed HIP-event durations on the stream they run on; `traffic` from the rocprofv3
 FETCH_SIZE / WRITE_SIZE passes of tools/profile_bench.sh (profiles/traffic_<workload>.json).
@@ -178,7 +179,7 @@ def main():
     for _ in range(args.steps):
         res = step()
         tm = eng.last_timing()
-        scan_ms.append(tm.prefilter_ms + tm.scan_ms)  # the hot path's two kernels: streaming pre-filter + fused scan
+        scan_ms.append(tm.prefilter_ms + tm.scan_ms)  # the hot path's kernels: selective stream + fused scan
         for k, v in parts.items():
             v.append(getattr(tm, k))
     torch.cuda.synchronize()
@@ -245,7 +246,8 @@ def main():
                        "parallelism": f"segments x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "prefilter_kernel + scan_kernel", "kernel_ms": scan_avg_ms,
+                         "kernel": "stream_kernel + scan_kernel" if tm.scan_launches > 1 else "scan_kernel",
+                         "kernel_ms": scan_avg_ms,
                          "algorithmic_bytes": alg_bytes,
                          "traffic_bytes_per_launch": traffic_bytes},
             "cpu_baseline": cpu,

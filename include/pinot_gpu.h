@@ -232,6 +232,8 @@ typedef struct pg_order {
 #define PG_PLAN_F64_SUMS 0x4u    /* accumulate every SUM / AVG in double, as the reference does, instead of
                                     integer-exact int64 for integer inputs; use when partial states of servers
                                     or GPUs whose columns differ in range must merge (pg_partials.layout) */
+#define PG_PLAN_NO_STREAM 0x8u   /* never use the selective stream (a lean kernel over the root AND's first,
+                                    selective scan leaf + the fused scan over its survivors); same results */
 
 typedef struct pg_plan {
   uint32_t abi_version;     /* PG_ABI_VERSION */
@@ -376,7 +378,7 @@ typedef struct pg_timing {
   float prepass_ms;
   float scan_ms;
   float finalize_ms;
-  uint32_t scan_launches;
+  uint32_t scan_launches;  /* hot-path kernels: the fused scan (1) + the selective stream (1) when it ran */
   float host_compile_ms;
   float execute_wall_ms;
   float finalize_wall_ms;

@@ -34,7 +34,7 @@ AGG_CODES = {"COUNT": PG_AGG_COUNT, "SUM": PG_AGG_SUM, "MIN": PG_AGG_MIN, "MAX":
 PG_EXPR_COL, PG_EXPR_MUL, PG_EXPR_ADD, PG_EXPR_SUB = range(4)
 PG_KEY_VALUE_OFFSET, PG_KEY_KEYMAP = 0, 1
 PG_ORDER_AGG, PG_ORDER_KEY = 0, 1
-PG_PLAN_VALUE_SETS, PG_PLAN_HASH_GROUPS, PG_PLAN_F64_SUMS = 0x1, 0x2, 0x4
+PG_PLAN_VALUE_SETS, PG_PLAN_HASH_GROUPS, PG_PLAN_F64_SUMS, PG_PLAN_NO_STREAM = 0x1, 0x2, 0x4, 0x8
 PG_STATE_DENSE, PG_STATE_HASH = 0, 1
 PG_EMPTY_KEY = 0xFFFFFFFFFFFFFFFF
 

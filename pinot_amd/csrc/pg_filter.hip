@@ -163,6 +163,153 @@ __global__ __launch_bounds__(256) void prefilter_kernel(PreSpec p) {
   }
 }
 
+// value `idx` of a `b`-bit packed column through its buffer descriptor (a 64-bit window of two words)
+__device__ __forceinline__ uint32_t unpack_win(rsrc_t r, uint32_t idx, uint32_t b) {
+  const uint64_t pbit = (uint64_t)idx * b;
+  const uint32_t off = (uint32_t)(pbit >> 5) << 2;
+  const uint32_t sh = (uint32_t)pbit & 31u;
+  const uint32_t w0 = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+  const uint32_t w1 = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4u, 0, 0);
+  const uint64_t win = ((uint64_t)w0 << 32) | (uint64_t)w1;
+  return (uint32_t)(win >> (64u - sh - b)) & (0xFFFFFFFFu >> (32u - b));
+}
+
+// A further leaf of the root AND on the docs `need` of the group at doc d0 (AndDocIdSet: later children see only the
+// survivors): per needed doc a window read, rounds of up to 4 docs per lane with their loads in flight together.
+__device__ __forceinline__ uint32_t eval_extra(const LeafDesc& X, const uint32_t* lds_sets, uint32_t d0, uint32_t need) {
+  uint32_t r = 0;
+  switch (X.kind) {
+    case LK_ALL: r = 0xFFFFFFFFu; break;
+    case LK_NONE: break;
+    case LK_DOCRANGE: {
+      const int64_t lo = std::max<int64_t>((int64_t)X.lo - (int64_t)d0, 0);
+      const int64_t hi = std::min<int64_t>((int64_t)X.hi - (int64_t)d0, 32);
+      const uint32_t below_hi = hi >= 32 ? 0xFFFFFFFFu : (hi <= 0 ? 0u : ((1u << hi) - 1u));
+      r = lo >= 32 ? 0u : below_hi & ~((1u << lo) - 1u);
+      break;
+    }
+    default: {  // RANGE / SET_LDS / SET_LUT on a packed column (doc bitmaps: RANGE [1, 2) on 1 bit)
+      const rsrc_t rs = rsrc_of(X.words, X.wbytes);
+      uint32_t rem = need;
+      while (__ballot(rem != 0)) {
+        uint32_t jj[4], v[4];
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+          jj[x] = rem ? (uint32_t)__ffs(rem) - 1u : 32u;
+          rem &= rem - 1u;
+          v[x] = unpack_win(rs, d0 + (jj[x] < 32u ? jj[x] : 0u), X.bits);
+        }
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+          if (jj[x] >= 32u) continue;
+          bool hit;
+          if (X.kind == LK_RANGE) {
+            hit = (v[x] - (uint32_t)X.lo) < (uint32_t)(X.hi - X.lo);
+          } else if (X.kind == LK_SET_LDS) {
+            const uint32_t y = v[x] >> X.shift;
+            hit = (lds_sets[X.lds_off + (y >> 5)] >> (y & 31u)) & 1u;
+            if (hit && X.shift) hit = (X.lut[v[x] >> 5] >> (v[x] & 31u)) & 1u;
+          } else {
+            hit = (X.aux[v[x] >> 5] >> (v[x] & 31u)) & 1u;
+          }
+          r |= (uint32_t)hit << jj[x];
+        }
+      }
+    }
+  }
+  return X.excl ? ~r : r;
+}
+
+// The selective stream: the driving leaf of the root AND over the block's items (32-doc groups, thread-contiguous
+// 16-byte loads, 6 waves per SIMD so ~120 KiB per CU are in flight), survivors appended to the item's region in group
+// order within each wave: one wave prefix sum + one LDS cursor atomic per wave and group round that has a survivor.
+// This is SVScanDocIdIterator over the first AND child, the compacted output playing the role of its docId batches.
+template <int B>
+__global__ __launch_bounds__(256, 6) void stream_kernel(StreamSpec p) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_sets[];
+  __shared__ uint32_t cursor;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t i0 = ldcf(p.block_first, blockIdx.x), i1 = ldcf(p.block_first, blockIdx.x + 1);
+  uint32_t cur_seg = 0xFFFFFFFFu;
+  LeafDesc L;
+  const LeafDesc* seg_leaves = nullptr;
+  uint32_t nd = 0;
+  for (uint32_t it = i0; it < i1; it++) {
+    const WorkItem wi = ldcf(p.items, it);
+    if (wi.seg != cur_seg) {
+      const SegDesc sd = ldcf(p.segs, wi.seg);
+      seg_leaves = sd.leaves;
+      L = ldcf(sd.leaves, p.leaf);
+      nd = sd.num_docs;
+      if (p.set_lds_ints) {
+        __syncthreads();  // every thread is done with the previous segment's sets
+        for (uint32_t x = 0; x <= p.num_extra; x++) {
+          const LeafDesc S = x ? ldcf(sd.leaves, p.extra[x - 1]) : L;
+          if (S.kind != LK_SET_LDS) continue;
+          for (uint32_t k = tid; k < S.set_ints; k += 256) lds_sets[S.lds_off + k] = S.aux[k];
+        }
+      }
+      cur_seg = wi.seg;
+    }
+    if (tid == 0) cursor = 0u;
+    __syncthreads();  // set staged, cursor reset
+    uint32_t* out = p.docs + (uint64_t)it * p.cap;
+    if (L.kind != LK_NONE) {
+      for (uint32_t g0 = wi.tile_begin; g0 < wi.tile_end; g0 += 256) {
+        const uint32_t g = g0 + tid;
+        const uint64_t d0 = (uint64_t)g * 32;
+        uint32_t m = 0;
+        if (g < wi.tile_end && d0 < nd) {
+          const uint32_t valid = d0 + 32 <= nd ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (32u - (uint32_t)(nd - d0)));
+          uint32_t r = eval_group<B>(L, lds_sets, g, valid);
+          if (L.excl) r = ~r;
+          m = r & valid;
+        }
+        for (uint32_t x = 0; x < p.num_extra; x++) {
+          if (__ballot(m != 0) == 0) break;
+          const LeafDesc X = ldcf(seg_leaves, p.extra[x]);
+          if (m) m &= eval_extra(X, lds_sets, (uint32_t)d0, m);
+        }
+        if (__ballot(m != 0) == 0) continue;
+        const uint32_t cnt = __popc(m);
+        uint32_t x = cnt;  // inclusive prefix over the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = __shfl_up(x, o);
+          if (lane >= (uint32_t)o) x += y;
+        }
+        uint32_t base = 0;
+        if (lane == 63) base = __hip_atomic_fetch_add((__attribute__((address_space(3))) uint32_t*)&cursor, x,
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        base = __builtin_amdgcn_readlane(base, 63);
+        uint32_t pos = base + x - cnt;
+        for (uint32_t r = m; r; r &= r - 1u, pos++)
+          if (pos < p.cap) out[pos] = (uint32_t)d0 + (uint32_t)(__ffs(r) - 1);
+      }
+    }
+    __syncthreads();  // every append of this item is counted
+    if (tid == 0) {
+      const uint32_t n = cursor;
+      p.counts[it] = n < p.cap ? n : p.cap;
+      if (n > p.cap) atomicOr(p.err, 8u);
+    }
+  }
+}
+
+hipError_t launch_stream(const StreamSpec& p, uint32_t bits, uint32_t blocks, hipStream_t s) {
+  if (!p.num_items || !blocks) return hipSuccess;
+  const size_t lds = (size_t)p.set_lds_ints * 4;
+  switch (bits) {
+#define PG_B(b) case b: hipLaunchKernelGGL(stream_kernel<b>, dim3(blocks), dim3(256), lds, s, p); break;
+    PG_B(1) PG_B(2) PG_B(3) PG_B(4) PG_B(5) PG_B(6) PG_B(7) PG_B(8) PG_B(9) PG_B(10) PG_B(11) PG_B(12) PG_B(13)
+    PG_B(14) PG_B(15) PG_B(16) PG_B(17) PG_B(18) PG_B(19) PG_B(20) PG_B(21) PG_B(22) PG_B(23) PG_B(24) PG_B(25)
+    PG_B(26) PG_B(27) PG_B(28) PG_B(29) PG_B(30) PG_B(31) PG_B(32)
+#undef PG_B
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_prefilter(const PreSpec& p, uint32_t bits, uint32_t blocks, hipStream_t s) {
   if (!p.num_items || !blocks) return hipSuccess;
   const size_t lds = (size_t)p.set_lds_ints * 4;

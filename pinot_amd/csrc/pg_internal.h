@@ -215,6 +215,12 @@ struct QuerySpec {
   unsigned int* part_count;         // [gridDim.x] entries of each block
   const unsigned long long* part_base;  // [gridDim.x] first entry of each block's region (its docs: an upper bound)
   unsigned long long* part_out;     // the entry array
+  // list mode (stream_kernel ran first): `items` are the stream's items and item i's survivors of the driving leaf
+  // are list_docs[i * list_cap, + list_counts[i]); the kernel feeds them to the LDS queue (phase B = the rest of the
+  // root AND, then aggregation) instead of walking tiles
+  uint32_t list_mode, list_cap;
+  const uint32_t* list_docs;
+  const uint32_t* list_counts;
 };
 
 // order-preserving int64 image of a double (for MIN/MAX slots)
@@ -280,6 +286,23 @@ struct PreSpec {
   uint32_t* const* out;           // [seg] bitmap words, packed 1-bit column order
 };
 hipError_t launch_prefilter(const PreSpec& p, uint32_t bits, uint32_t blocks, hipStream_t s);
+
+// ---- selective stream (pg_filter.hip): the driving leaf of the root AND (a packed scan leaf passing few docs) over
+// every segment, bit width a template parameter, values loaded straight into registers; the survivors' doc ids are
+// compacted into one region per item, which the scan kernel then consumes in list mode
+constexpr int kMaxStreamExtra = 3;
+struct StreamSpec {
+  uint32_t num_items, leaf, cap, set_lds_ints;
+  uint32_t num_extra;                 // further leaves of the root AND tested in the stream, on the survivors only
+  uint32_t extra[kMaxStreamExtra];    // (runtime bit width: per-doc windows, like the scan's gathered leaves)
+  const SegDesc* segs;
+  const WorkItem* items;          // tile_begin / tile_end in 32-doc groups
+  const uint32_t* block_first;    // [gridDim.x + 1]: block b streams items [block_first[b], block_first[b + 1])
+  uint32_t* docs;                 // [num_items][cap]
+  uint32_t* counts;               // [num_items] survivors written (<= cap)
+  unsigned int* err;              // bit 3: some item had more than `cap` survivors
+};
+hipError_t launch_stream(const StreamSpec& p, uint32_t bits, uint32_t blocks, hipStream_t s);
 
 // ---- radix-partitioned group-by (pg_part.hip): level 2 + per-bucket aggregation, after the two scan passes
 constexpr uint32_t kPartL1 = 256;        // level-1 partitions (scan passes)

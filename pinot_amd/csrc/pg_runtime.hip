@@ -18,6 +18,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <shared_mutex>
 #include <string>
@@ -784,7 +785,7 @@ struct Partials {
   uint32_t layout = 0;          // bit a: aggregation a accumulates integer-exact (i64) -- must agree across merges
   std::vector<AggSpec> aggs;
 
-  StateView view() {
+  StateView view() const {
     StateView v;
     memset(&v, 0, sizeof(v));
     v.num_slots = num_slots;
@@ -1061,6 +1062,7 @@ int Partials::alloc_state(hipStream_t s, bool init) {
 }
 
 constexpr int kRetryLargerTable = 1;  // internal: the hash table overflowed its fill budget
+constexpr int kRetryNoStream = 2;     // internal: a selective-stream region overflowed (more survivors than estimated)
 
 // Pooled device scratch of a host-side sequence of small launches (freed after the caller synchronises).
 struct Scratch {
@@ -1198,7 +1200,7 @@ void use_decoded(ColDesc& dc, const ColumnRes* c) {
   dc.decoded = 1;
 }
 
-int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t hash_cap) {
+int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t hash_cap, bool allow_stream) {
   const double t_enter = wall_ms();
   if (!plan) return fail(PG_E_INVALID, "null plan");
   if (plan->abi_version != PG_ABI_VERSION) return fail(PG_E_INVALID, "ABI version %u != %u", plan->abi_version, PG_ABI_VERSION);
@@ -1943,7 +1945,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   }
   const double decodes = filter_pass * (double)total_docs / std::max(1u, S);
   static const char* xcd_env = getenv("PG_XCD_ORDER");
-  const bool want_xcd = xcd_env ? atoi(xcd_env) != 0 : (dict_lines >= 2048 && decodes > 16.0 * (double)dict_lines);
+  bool want_xcd = xcd_env ? atoi(xcd_env) != 0 : (dict_lines >= 2048 && decodes > 16.0 * (double)dict_lines);
   // ---- work items.  Balanced form: the concatenated tile sequence of all segments is cut into G equal ranges, one
   // per block, each given as exactly 2 items (split at the segment boundary it crosses, else halved), so the kernel's
   // uniform [2b, 2b + 2) item ranges are tile-exact (+-1 tile per block) and the host emits 2G items instead of one
@@ -2139,6 +2141,115 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     const bool fits = q.num_staged && scan_lds_bytes(q) * (size_t)scan_min_blocks_per_cu(K > 0) <= 160 * 1024;
     q.stage_ring = ring_env ? (atoi(ring_env) > 1 ? 2 : 1) : (fits ? 2 : 1);
   }
+  // ---- selective stream (pg_filter.hip stream_kernel): when the root AND's first child (or the whole filter) is a
+  // packed scan leaf that passes few docs, a lean kernel streams that one column at full HBM rate and compacts its
+  // survivors; the scan kernel then runs in list mode over them (the rest of the AND + aggregation, gathers only).
+  // The fused tile loop pays a fixed cost per 8 192-doc tile that a 0.1 %-selective filter cannot amortise.
+  // Regions hold 4x the expected survivors (+ slack); an overflow reruns the query without the stream.
+  // PG_STREAM=0 disables, PG_STREAM_MAXPASS sets the pass-fraction bound (default 1/32).
+  struct StreamLaunch { uint32_t bits, blocks; uint64_t first_off; std::vector<uint32_t> first; };
+  struct StreamPlan {
+    bool on = false;
+    uint32_t leaf = 0, cap = 0;
+    std::vector<uint32_t> extra;  // further AND children tested in the stream (runtime bit width)
+    std::vector<StreamLaunch> launches;
+  } sp;
+  {
+    static const char* st_env = getenv("PG_STREAM");
+    static const double max_pass = getenv("PG_STREAM_MAXPASS") ? atof(getenv("PG_STREAM_MAXPASS")) : 1.0 / 32;
+    int32_t li = -1;
+    double pass = 1.0;
+    if (q.num_ops && q.ops[0] >= 0) {
+      li = q.ops[0];
+      pass = leaf_pass[li];
+    } else if (q.num_ops > 2 && q.ops[0] == kOpAnd && q.ops[1] >= 0) {
+      // the AND's leading leaf children while the joint pass is above 1/64: the first one streamed at its bit width,
+      // the others tested on its survivors (doc ranges, constants, packed columns incl. 1-bit doc bitmaps)
+      li = q.ops[1];
+      pass = leaf_pass[li];
+      for (uint32_t i = 2; i + 1 < q.num_ops && pass > 1.0 / 64 && sp.extra.size() < (size_t)kMaxStreamExtra; i++) {
+        const int32_t lx = q.ops[i];
+        if (lx < 0) break;
+        bool fits = true;
+        for (uint32_t si = 0; si < S && fits; si++) {
+          const uint32_t k = leaves[(uint64_t)si * L + lx].kind;
+          fits = k == LK_ALL || k == LK_NONE || k == LK_DOCRANGE || k == LK_RANGE || k == LK_SET_LDS || k == LK_SET_LUT;
+        }
+        if (!fits) break;
+        sp.extra.push_back((uint32_t)lx);
+        pass *= leaf_pass[lx];
+      }
+    }
+    bool ok = allow_stream && !(plan->flags & PG_PLAN_NO_STREAM) && !(st_env && atoi(st_env) == 0) && li >= 0 &&
+              !part.on && pre_leaves.empty() && pass <= max_pass && total_docs < 0xFFFFFFF0ull;
+    std::map<uint32_t, std::vector<uint32_t>> by_bits;  // bit width -> segments whose form of the leaf reads it
+    uint64_t T = 0;
+    std::vector<uint64_t> seg_groups(S, 0);
+    for (uint32_t si = 0; si < S && ok; si++) {
+      if (!seg_tiles[si]) continue;
+      const LeafDesc& dl = leaves[(uint64_t)si * L + li];
+      if (dl.kind == LK_NONE) continue;
+      ok = (dl.kind == LK_RANGE || dl.kind == LK_SET_LDS || dl.kind == LK_SET_LUT) && dl.bits >= 1 && dl.bits <= 32;
+      by_bits[dl.bits].push_back(si);
+      seg_groups[si] = ((uint64_t)plan->segments[si].num_docs + 31) / 32;
+      T += seg_groups[si];
+    }
+    if (ok && T) {
+      // items: per bit width, the concatenated 32-doc groups of its segments cut into one equal range per stream
+      // block (blocks in proportion to the groups), split at segment boundaries; one launch per bit width
+      const uint64_t NB = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)g_num_cus * 8, T / 64));
+      items.clear();
+      uint64_t max_groups = 0;
+      for (auto& bb : by_bits) {
+        const std::vector<uint32_t>& segs_b = bb.second;
+        uint64_t Tb = 0;
+        for (uint32_t si : segs_b) Tb += seg_groups[si];
+        const uint64_t nb = std::max<uint64_t>(1, std::min<uint64_t>(Tb, (NB * Tb + T - 1) / T));
+        StreamLaunch sl;
+        sl.bits = bb.first;
+        sl.blocks = (uint32_t)nb;
+        sl.first.assign(nb + 1, 0);
+        size_t k = 0;
+        uint64_t seg_first = 0;
+        for (uint64_t b = 0; b < nb; b++) {
+          sl.first[b] = (uint32_t)items.size();
+          uint64_t t0 = b * Tb / nb;
+          const uint64_t t1 = (b + 1) * Tb / nb;
+          while (t0 < t1) {
+            while (t0 >= seg_first + seg_groups[segs_b[k]]) { seg_first += seg_groups[segs_b[k]]; k++; }
+            const uint64_t e = std::min(t1, seg_first + seg_groups[segs_b[k]]);
+            items.push_back({segs_b[k], (uint32_t)(t0 - seg_first), (uint32_t)(e - seg_first), 0});
+            max_groups = std::max(max_groups, e - t0);
+            t0 = e;
+          }
+        }
+        sl.first[nb] = (uint32_t)items.size();
+        sp.launches.push_back(std::move(sl));
+      }
+      const double expect = pass * 32.0 * (double)max_groups;
+      const uint64_t cap = std::min<uint64_t>(32 * max_groups, ((uint64_t)(4.0 * expect) + 1024 + 63) & ~63ull);
+      sp.on = true;
+      sp.leaf = (uint32_t)li;
+      sp.cap = (uint32_t)cap;
+      q.num_items = (uint32_t)items.size();
+      grid = (uint32_t)std::min<uint64_t>(items.size(), scan_grid_cap(K > 0));
+      want_xcd = false;
+      // list mode: the driving leaf is done; phase B = the AND's remaining children, all read by gathers
+      q.list_mode = 1;
+      q.list_cap = sp.cap;
+      q.queue_mode = 1;
+      q.opA_begin = q.opA_end = 0;
+      q.opA_type = GT_ROOT;
+      if (q.ops[0] >= 0) { q.opB_begin = q.opB_end = 0; }
+      else { q.opB_begin = 2 + (uint32_t)sp.extra.size(); q.opB_end = q.num_ops - 1; }
+      q.num_staged = 0;
+      q.stage_lds_words = 0;
+      q.stage_ring = 1;
+      memset(q.leaf_slot, kNoSlot, sizeof(q.leaf_slot));
+      memset(q.agg_slot, kNoSlot, sizeof(q.agg_slot));
+      memset(q.key_slot, kNoSlot, sizeof(q.key_slot));
+    }
+  }
   const size_t lds_bytes = scan_lds_bytes(q);
   if (lds_bytes > 160 * 1024) return fail(PG_E_UNSUPPORTED, "scan needs %zu bytes of LDS", lds_bytes);
 
@@ -2226,6 +2337,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     }
   }
   const uint64_t off_items = ar.put(items.data(), items.size() * sizeof(WorkItem));
+  for (StreamLaunch& sl : sp.launches) sl.first_off = ar.put(sl.first.data(), sl.first.size() * 4);
   // GM_PART: each block's region of the entry array = the docs of its items (the kernel's [i0, i1) item range)
   uint64_t off_part_base = 0, part_entries = 0;
   if (part.on && blocks) {
@@ -2246,6 +2358,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   const uint64_t off_lutjobs = ar.reserve(luts.size() * sizeof(LutJob));
   DevBuf arena, scratch;
   DevBuf p_ent0, p_cnt0, p_hist1, p_off1, p_ent1, p_hist2, p_off2, p_ent2, p_temp;  // GM_PART pipeline
+  DevBuf l_docs, l_counts;  // selective stream: survivor regions + counts
   // declared after the buffers it protects: on any exit, wait for queued work before they return to the pool
   struct SyncOnExit {
     hipStream_t s;
@@ -2330,6 +2443,29 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     ps.items = (const WorkItem*)(dA + pl.items_off);
     ps.out = (uint32_t* const*)(dA + off_pre_out);
     HIP_CHECK(launch_prefilter(ps, pl.bits, (uint32_t)std::min<uint64_t>(pl.n_items, (uint64_t)g_num_cus * 8), s));
+  }
+  if (sp.on && q.num_items) {
+    if ((rc = l_docs.alloc_pooled(4ull * q.num_items * sp.cap + 16)) || (rc = l_counts.alloc_pooled(4ull * q.num_items + 16)))
+      return rc;
+    StreamSpec ss;
+    memset(&ss, 0, sizeof(ss));
+    ss.num_items = q.num_items;
+    ss.leaf = sp.leaf;
+    ss.cap = sp.cap;
+    ss.num_extra = (uint32_t)sp.extra.size();
+    for (size_t x = 0; x < sp.extra.size(); x++) ss.extra[x] = sp.extra[x];
+    ss.set_lds_ints = q.set_lds_ints;
+    ss.segs = q.segs;
+    ss.items = q.items;
+    ss.docs = (uint32_t*)l_docs.p;
+    ss.counts = (uint32_t*)l_counts.p;
+    ss.err = q.err;
+    for (const StreamLaunch& sl : sp.launches) {
+      ss.block_first = (const uint32_t*)(dA + sl.first_off);
+      HIP_CHECK(launch_stream(ss, sl.bits, sl.blocks, s));
+    }
+    q.list_docs = ss.docs;
+    q.list_counts = ss.counts;
   }
   HIP_CHECK(hipEventRecord(ev[1], s));
   if (is_cancelled(plan->query_id)) { (void)hipStreamSynchronize(s); return fail(PG_E_CANCELLED, "query %llu cancelled", (unsigned long long)plan->query_id); }
@@ -2421,7 +2557,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   t_timing.prepass_ms = pre_ms;
   t_timing.prefilter_ms = filt_ms;
   t_timing.scan_ms = scan_ms;
-  t_timing.scan_launches = blocks ? 1 : 0;
+  t_timing.scan_launches = (blocks ? 1 : 0) + (sp.on && q.num_items ? 1 : 0);  // + the selective stream
   memset(&stats, 0, sizeof(stats));
   stats.num_total_docs = total_docs;
   stats.num_segments_processed = S;
@@ -2431,6 +2567,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     stats.num_docs_scanned += ns_docs;  // NonScanBasedAggregationOperator: numDocsScanned = numTotalDocs
     stats.num_segments_matched += ns_matched;
     const uint32_t err = (uint32_t)sm[S ? S : 1];
+    if (err & 8u) return kRetryNoStream;     // more stream survivors than the regions hold: rerun without it
     if (err & 4u) return kRetryLargerTable;  // hash table over its fill budget: rerun with a larger one
     if (err) return fail(PG_E_INVALID, "device bounds check failed (code %u): a key fell outside the plan's key space", err);
   }
@@ -2483,6 +2620,101 @@ FinalSpec make_final(const Partials& P, const pg_plan* plan) {
   return f;
 }
 
+int build_result(pg_partials* pp, const pg_plan* plan, pg_result** out, const Partials& P, uint64_t nc,
+                 const std::vector<uint64_t>& hk, const std::vector<double>& hv, const std::vector<int64_t>& hc,
+                 bool sets, const std::vector<uint64_t>& hoff, const std::vector<uint32_t>& hids);
+
+// A dense state of at most this many bytes is finalised on the host from one D2H copy (config 2: 90 x 3 int64):
+// the device path's select / final-value / trim launches and its two stream round trips cost ~0.1 ms there.
+constexpr uint64_t kHostFinalBytes = 1ull << 20;
+
+// finalize() for small dense states without DISTINCTCOUNT: the same groups, final values and ORDER BY candidates
+// (ties with the limit-th on the first ORDER BY item included) as the device path, computed from a host copy.
+int finalize_small(pg_partials* pp, const pg_plan* plan, pg_result** out, const Partials& P, const FinalSpec& f,
+                   hipEvent_t e0, hipEvent_t e1, hipStream_t s) {
+  const StateView v = P.view();
+  const uint32_t A = plan->num_aggs, K = plan->num_keys;
+  const uint64_t G = P.num_slots;
+  const uint64_t b64 = G * 8ull * v.n_i64, bf = G * 8ull * v.n_f64, bmn = G * 8ull * v.n_min, bmx = G * 8ull * v.n_max;
+  uint8_t* h = (uint8_t*)t_ctx.readback.get(b64 + bf + bmn + bmx + 8);
+  if (!h) return fail(PG_E_NOMEM, "pinned readback failed");
+  HIP_CHECK(hipMemcpyAsync(h, v.i64, b64, hipMemcpyDeviceToHost, s));
+  if (bf) HIP_CHECK(hipMemcpyAsync(h + b64, v.f64, bf, hipMemcpyDeviceToHost, s));
+  if (bmn) HIP_CHECK(hipMemcpyAsync(h + b64 + bf, v.mn, bmn, hipMemcpyDeviceToHost, s));
+  if (bmx) HIP_CHECK(hipMemcpyAsync(h + b64 + bf + bmn, v.mx, bmx, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipEventRecord(e1, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  float fm = 0;
+  (void)hipEventElapsedTime(&fm, e0, e1);
+  t_timing.finalize_ms = fm;
+  const uint64_t* i64 = (const uint64_t*)h;
+  const double* f64 = (const double*)(h + b64);
+  const int64_t* mn = (const int64_t*)(h + b64 + bf);
+  const int64_t* mx = (const int64_t*)(h + b64 + bf + bmn);
+  // 1. the groups (aggregation-only: slot 0, always one row) and 2. their final values (final_values_kernel)
+  std::vector<uint64_t> hk;
+  std::vector<double> hv;
+  std::vector<int64_t> hc;
+  for (uint64_t sl = 0; sl < G; sl++) {
+    const int64_t count = (int64_t)i64[sl * v.n_i64];
+    if (K && count <= 0) continue;
+    hk.push_back(sl);
+    for (uint32_t a = 0; a < A; a++) {
+      const AggSpec& g = f.aggs[a];
+      double x = 0;
+      int64_t c = 0;
+      switch (g.fn) {
+        case PG_AGG_COUNT: x = (double)count; break;
+        case PG_AGG_COUNTMV: x = (double)(int64_t)i64[sl * v.n_i64 + g.slot]; break;
+        case PG_AGG_SUM:
+        case PG_AGG_AVG:
+          x = g.integer ? (double)(int64_t)i64[sl * v.n_i64 + g.slot] : f64[sl * v.n_f64 + g.slot];
+          if (g.fn == PG_AGG_AVG) c = count;
+          break;
+        case PG_AGG_MIN: x = order_key_decode(mn[sl * v.n_min + g.slot]); break;
+        case PG_AGG_MAX: x = order_key_decode(mx[sl * v.n_max + g.slot]); break;
+      }
+      hv.push_back(x);
+      hc.push_back(c);
+    }
+    if (!K) break;
+  }
+  uint64_t nc = hk.size();
+  // 3. ORDER BY trim: the candidates whose first-ORDER-BY image is <= the limit-th smallest (order_keys_kernel)
+  if (K && plan->num_order && plan->limit && nc > plan->limit) {
+    std::vector<uint64_t> ok(nc);
+    for (uint64_t i = 0; i < nc; i++) {
+      uint64_t o;
+      if (f.order_kind == PG_ORDER_KEY) {
+        o = (hk[i] / f.key_stride[f.order_index]) % f.key_card[f.order_index];
+      } else {
+        const uint32_t a = f.order_index;
+        double x = hv[i * A + a];
+        if (f.aggs[a].fn == PG_AGG_AVG) { const int64_t c = hc[i * A + a]; x = c ? x / (double)c : -INFINITY; }
+        int64_t b;
+        memcpy(&b, &x, 8);
+        o = b >= 0 ? ((uint64_t)b | 0x8000000000000000ull) : ~(uint64_t)b;
+      }
+      ok[i] = f.order_desc ? ~o : o;
+    }
+    std::vector<uint64_t> srt(ok);
+    std::nth_element(srt.begin(), srt.begin() + (plan->limit - 1), srt.end());
+    const uint64_t t = srt[plan->limit - 1];
+    uint64_t w = 0;
+    for (uint64_t i = 0; i < nc; i++) {
+      if (ok[i] > t) continue;
+      hk[w] = hk[i];
+      for (uint32_t a = 0; a < A; a++) { hv[w * A + a] = hv[i * A + a]; hc[w * A + a] = hc[i * A + a]; }
+      w++;
+    }
+    nc = w;
+    hk.resize(nc);
+    hv.resize(nc * A);
+    hc.resize(nc * A);
+  }
+  return build_result(pp, plan, out, P, nc, hk, hv, hc, false, {}, {});
+}
+
 // Partial state -> host result: the groups present (doc count > 0), their final values, the plan's ORDER BY trim
 // (IndexedTable.finish -> TableResizer.getTopRecords: a radix sort on the first ORDER BY item on the device, the
 // candidates -- every group that ranks within `limit`, ties included -- fully ordered on the host) and, on request,
@@ -2512,6 +2744,12 @@ int finalize(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   const StateView v = P.view();
   const FinalSpec f = make_final(P, plan);
   const uint32_t AA = A ? A : 1;
+
+  bool any_dc = false;
+  for (uint32_t a = 0; a < A; a++) any_dc |= P.aggs[a].fn == PG_AGG_DISTINCTCOUNT;
+  const uint64_t row_words = (uint64_t)v.n_i64 + v.n_f64 + v.n_min + v.n_max;
+  if ((P.mode == GM_DENSE || P.mode == GM_NONE) && !any_dc && P.num_slots * row_words * 8 <= kHostFinalBytes)
+    return finalize_small(pp, plan, out, P, f, e0, e1, s);
 
   // 1. the groups
   uint64_t n = 1;
@@ -2603,8 +2841,15 @@ int finalize(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   float fm = 0;
   (void)hipEventElapsedTime(&fm, e0, e1);
   t_timing.finalize_ms = fm;
+  return build_result(pp, plan, out, P, nc, hk, hv, hc, sets, hoff, hids);
+}
 
-  // 5. host order of the candidates: every ORDER BY item, then the packed key (a total order)
+// Host order of the candidates (every ORDER BY item, then the packed key: a total order) and the result rows.
+int build_result(pg_partials* pp, const pg_plan* plan, pg_result** out, const Partials& P, uint64_t nc,
+                 const std::vector<uint64_t>& hk, const std::vector<double>& hv, const std::vector<int64_t>& hc,
+                 bool sets, const std::vector<uint64_t>& hoff, const std::vector<uint32_t>& hids) {
+  const uint32_t A = plan->num_aggs, K = plan->num_keys;
+  const uint32_t AA = A ? A : 1;
   std::vector<uint64_t> perm(nc);
   for (uint64_t i = 0; i < nc; i++) perm[i] = i;
   if (K && plan->num_order) {
@@ -2754,8 +2999,10 @@ int pg_execute_partial(const pg_plan* plan, pg_partials** out) {
   t_timing.finalize_wall_ms = 0;
   try {
     uint64_t cap = 0;
+    bool allow_stream = true;
     for (;;) {
-      rc = compile_and_run(plan, impl->P, st, cap);
+      rc = compile_and_run(plan, impl->P, st, cap, allow_stream);
+      if (rc == kRetryNoStream) { allow_stream = false; continue; }
       if (rc != kRetryLargerTable) break;
       cap = impl->P.num_slots * 8;  // the group-by hash table overflowed: rerun with 8x the slots
       if (cap > kMaxHashSlots) { rc = fail(PG_E_UNSUPPORTED, "group-by needs more than %llu hash slots", (unsigned long long)kMaxHashSlots); break; }

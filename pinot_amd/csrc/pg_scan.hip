@@ -988,7 +988,7 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
     uint64_t seg_count = 0;
 
     // phase B over the queued docs of segment `cur_sd`: the root AND's remaining children, then aggregation
-    auto flush = [&]() {
+    auto flush = [&]() __attribute__((always_inline)) {
       __syncthreads();  // queue entries visible
       const QueueRows rows{queue, qn, (uint32_t)tid};
       uint32_t valid = 0;
@@ -1002,7 +1002,48 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
       __syncthreads();  // every lane is done reading the queue
       qn = 0;
     };
+    // a new segment: the previous one's queued docs and match count, then this one's IN-list sets in LDS
+    auto enter_segment = [&](uint32_t seg) __attribute__((always_inline)) {
+      if (cur_seg != 0xFFFFFFFFu) {
+        if (qn) flush();  // the queue holds docs of the previous segment
+        const uint64_t c = wave_sum_u64(seg_count);
+        if (lane == 0 && c) g_add(&q.seg_matched[cur_seg], (unsigned long long)c);
+        seg_count = 0;
+      }
+      cur_sd = ldc(q.segs, seg);
+      if (q.set_lds_ints) {  // this segment's IN-list filter bitmaps + hash tables
+        for (uint32_t l = 0; l < q.num_leaves; l++) {
+          const LeafDesc L = ldc(cur_sd.leaves, l);
+          if (L.kind != LK_SET_LDS) continue;
+          const PG_GLOBAL int32_t* src = glb((const int32_t*)L.aux);
+          int32_t* dst = lds_sets + L.lds_off;
+          for (uint32_t k = tid; k < L.set_ints; k += kBlock) dst[k] = src[k];
+        }
+        __syncthreads();
+      }
+      cur_seg = seg;
+    };
 
+    if (q.list_mode) {
+      // the stream kernel's survivors: item by item into the queue, phase B + aggregation per flush
+      for (;;) {
+        if (it.seg != cur_seg) enter_segment(it.seg);
+        const uint32_t n = __builtin_amdgcn_readfirstlane(min(glb(q.list_counts)[item], q.list_cap));
+        const PG_GLOBAL uint32_t* src = glb(q.list_docs + (uint64_t)item * q.list_cap);
+        for (uint32_t c0 = 0; c0 < n;) {
+          const uint32_t take = min(n - c0, (uint32_t)kQueueCap - qn);
+          for (uint32_t k = tid; k < take; k += kBlock) queue[qn + k] = src[c0 + k];
+          qn += take;
+          c0 += take;
+          if (qn >= (uint32_t)kQueueFlush) flush();
+        }
+        if (++item >= i1) break;
+        it = ldc(q.items, item);
+      }
+      if (qn) flush();
+      const uint64_t c = wave_sum_u64(seg_count);
+      if (lane == 0 && c) g_add(&q.seg_matched[cur_seg], (unsigned long long)c);
+    } else {
     if (q.num_staged) stage_issue(q, cur_sd, tile, stage, wave, lane);
     for (;;) {
       // successor of (item, tile) in the block's sequence
@@ -1025,26 +1066,7 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
         if (tid == 0) pending = __hip_atomic_load(q.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       iter++;
-      if (it.seg != cur_seg) {
-        if (cur_seg != 0xFFFFFFFFu) {
-          if (qn) flush();  // the queue holds docs of the previous segment
-          const uint64_t c = wave_sum_u64(seg_count);
-          if (lane == 0 && c) g_add(&q.seg_matched[cur_seg], (unsigned long long)c);
-          seg_count = 0;
-        }
-        cur_sd = ldc(q.segs, it.seg);
-        if (q.set_lds_ints) {  // this segment's IN-list filter bitmaps + hash tables
-          for (uint32_t l = 0; l < q.num_leaves; l++) {
-            const LeafDesc L = ldc(cur_sd.leaves, l);
-            if (L.kind != LK_SET_LDS) continue;
-            const PG_GLOBAL int32_t* src = glb((const int32_t*)L.aux);
-            int32_t* dst = lds_sets + L.lds_off;
-            for (uint32_t k = tid; k < L.set_ints; k += kBlock) dst[k] = src[k];
-          }
-          __syncthreads();
-        }
-        cur_seg = it.seg;
-      }
+      if (it.seg != cur_seg) enter_segment(it.seg);
       const SegDesc& sd = cur_sd;
       if (ring2 && has_next && q.num_staged) stage_issue(q, ldc(q.segs, n_seg), n_tile, stage + (buf ^ 1u) * q.stage_lds_words, wave, lane);
 
@@ -1112,6 +1134,7 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
     if (qn && !(q.cancel && (stop[0] | stop[1]))) flush();
     const uint64_t c = wave_sum_u64(seg_count);
     if (lane == 0 && c) g_add(&q.seg_matched[cur_seg], (unsigned long long)c);
+    }  // tile loop
   }
 
   if (!GROUPED) {

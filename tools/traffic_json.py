@@ -6,27 +6,33 @@ bytes of wide coalesced streaming reads, so the read count is doubled; WRITE_SIZ
 dispatches of each pass are warm-up launches and are kept (every launch of the bench runs the same query).
 
 usage: traffic_json.py <pmc summary txt> <bench json of the profiled command>"""
+import collections
 import json
 import statistics
 import sys
 
-fetch, write = [], []
+fetch, write = collections.defaultdict(list), collections.defaultdict(list)
 for line in open(sys.argv[1]):
-    for tok in line.split():
+    toks = line.split()
+    if len(toks) < 3:
+        continue
+    kern = toks[2]  # pmc_summary.py: <pass> <dispatch> <kernel> counters...
+    for tok in toks[3:]:
         if tok.startswith("FETCH_SIZE="):
-            fetch.append(float(tok.split("=")[1]))
+            fetch[kern].append(float(tok.split("=")[1]))
         if tok.startswith("WRITE_SIZE="):
-            write.append(float(tok.split("=")[1]))
+            write[kern].append(float(tok.split("=")[1]))
 bench = {}
 try:
     bench = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
 except Exception:
     pass
-rd = 2 * 1024 * statistics.median(fetch) if fetch else None
-wr = 1024 * statistics.median(write) if write else None
-print(json.dumps({"kernel": "pg::scan_kernel", "config": bench.get("config"),
-                  "fetch_size_kib_median": statistics.median(fetch) if fetch else None,
-                  "write_size_kib_median": statistics.median(write) if write else None,
+# one query launches each hot-path kernel once: per-query traffic = sum over kernels of the per-dispatch medians
+per = {k: {"fetch_size_kib_median": statistics.median(fetch[k]),
+           "write_size_kib_median": statistics.median(write[k]) if write.get(k) else 0.0} for k in fetch}
+rd = sum(2 * 1024 * v["fetch_size_kib_median"] for v in per.values()) if per else None
+wr = sum(1024 * v["write_size_kib_median"] for v in per.values()) if per else None
+print(json.dumps({"kernel": " + ".join(sorted(per)) or None, "config": bench.get("config"), "per_kernel": per,
                   "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
                   "traffic_bytes_per_launch": (rd or 0) + (wr or 0) if rd is not None else None,
                   "correction": "FETCH_SIZE x2 (gfx950 half-count of wide streaming reads), KiB -> bytes"}))
