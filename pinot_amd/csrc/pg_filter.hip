@@ -224,17 +224,21 @@ __device__ __forceinline__ uint32_t eval_extra(const LeafDesc& X, const uint32_t
 // 16-byte loads, 6 waves per SIMD so ~120 KiB per CU are in flight), survivors appended to the item's region in group
 // order within each wave: one wave prefix sum + one LDS cursor atomic per wave and group round that has a survivor.
 // This is SVScanDocIdIterator over the first AND child, the compacted output playing the role of its docId batches.
-template <int B>
-__global__ __launch_bounds__(256, 6) void stream_kernel(StreamSpec p) {
+// EXTRA: further AND leaves tested on the survivors (their code costs registers: 78 VGPRs / 6 waves per SIMD with,
+// 72 / 7 without).  Items: contiguous ranges per block (block_first), or with `interleave` item b + k * gridDim.x.
+template <int B, bool EXTRA>
+__global__ __launch_bounds__(256, EXTRA ? 6 : 7) void stream_kernel(StreamSpec p) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_sets[];
   __shared__ uint32_t cursor;
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  const uint32_t i0 = ldcf(p.block_first, blockIdx.x), i1 = ldcf(p.block_first, blockIdx.x + 1);
+  const uint32_t i0 = p.interleave ? ldcf(p.block_first, 0) + blockIdx.x : ldcf(p.block_first, blockIdx.x);
+  const uint32_t i1 = ldcf(p.block_first, p.interleave ? gridDim.x : blockIdx.x + 1);
+  const uint32_t istep = p.interleave ? gridDim.x : 1u;
   uint32_t cur_seg = 0xFFFFFFFFu;
   LeafDesc L;
   const LeafDesc* seg_leaves = nullptr;
   uint32_t nd = 0;
-  for (uint32_t it = i0; it < i1; it++) {
+  for (uint32_t it = i0; it < i1; it += istep) {
     const WorkItem wi = ldcf(p.items, it);
     if (wi.seg != cur_seg) {
       const SegDesc sd = ldcf(p.segs, wi.seg);
@@ -243,7 +247,7 @@ __global__ __launch_bounds__(256, 6) void stream_kernel(StreamSpec p) {
       nd = sd.num_docs;
       if (p.set_lds_ints) {
         __syncthreads();  // every thread is done with the previous segment's sets
-        for (uint32_t x = 0; x <= p.num_extra; x++) {
+        for (uint32_t x = 0; x <= (EXTRA ? p.num_extra : 0u); x++) {
           const LeafDesc S = x ? ldcf(sd.leaves, p.extra[x - 1]) : L;
           if (S.kind != LK_SET_LDS) continue;
           for (uint32_t k = tid; k < S.set_ints; k += 256) lds_sets[S.lds_off + k] = S.aux[k];
@@ -265,7 +269,7 @@ __global__ __launch_bounds__(256, 6) void stream_kernel(StreamSpec p) {
           if (L.excl) r = ~r;
           m = r & valid;
         }
-        for (uint32_t x = 0; x < p.num_extra; x++) {
+        for (uint32_t x = 0; x < (EXTRA ? p.num_extra : 0u); x++) {
           if (__ballot(m != 0) == 0) break;
           const LeafDesc X = ldcf(seg_leaves, p.extra[x]);
           if (m) m &= eval_extra(X, lds_sets, (uint32_t)d0, m);
@@ -300,7 +304,11 @@ hipError_t launch_stream(const StreamSpec& p, uint32_t bits, uint32_t blocks, hi
   if (!p.num_items || !blocks) return hipSuccess;
   const size_t lds = (size_t)p.set_lds_ints * 4;
   switch (bits) {
-#define PG_B(b) case b: hipLaunchKernelGGL(stream_kernel<b>, dim3(blocks), dim3(256), lds, s, p); break;
+#define PG_B(b)                                                                                \
+  case b:                                                                                      \
+    if (p.num_extra) hipLaunchKernelGGL((stream_kernel<b, true>), dim3(blocks), dim3(256), lds, s, p); \
+    else hipLaunchKernelGGL((stream_kernel<b, false>), dim3(blocks), dim3(256), lds, s, p);           \
+    break;
     PG_B(1) PG_B(2) PG_B(3) PG_B(4) PG_B(5) PG_B(6) PG_B(7) PG_B(8) PG_B(9) PG_B(10) PG_B(11) PG_B(12) PG_B(13)
     PG_B(14) PG_B(15) PG_B(16) PG_B(17) PG_B(18) PG_B(19) PG_B(20) PG_B(21) PG_B(22) PG_B(23) PG_B(24) PG_B(25)
     PG_B(26) PG_B(27) PG_B(28) PG_B(29) PG_B(30) PG_B(31) PG_B(32)

@@ -294,6 +294,8 @@ constexpr int kMaxStreamExtra = 3;
 struct StreamSpec {
   uint32_t num_items, leaf, cap, set_lds_ints;
   uint32_t num_extra;                 // further leaves of the root AND tested in the stream, on the survivors only
+  uint32_t interleave;                // block b streams items first + b + k * gridDim.x (first = block_first[0], end =
+                                      // block_first[gridDim.x]); else the range [block_first[b], block_first[b + 1])
   uint32_t extra[kMaxStreamExtra];    // (runtime bit width: per-doc windows, like the scan's gathered leaves)
   const SegDesc* segs;
   const WorkItem* items;          // tile_begin / tile_end in 32-doc groups

@@ -2151,6 +2151,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   struct StreamPlan {
     bool on = false;
     uint32_t leaf = 0, cap = 0;
+    bool interleave = false;      // items dealt round-robin to the blocks (PG_STREAM_ITEM_GROUPS)
+    uint32_t set_ints = 0;        // LDS IN-set words of the streamed leaves
     std::vector<uint32_t> extra;  // further AND children tested in the stream (runtime bit width)
     std::vector<StreamLaunch> launches;
   } sp;
@@ -2197,10 +2199,33 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     if (ok && T) {
       // items: per bit width, the concatenated 32-doc groups of its segments cut into one equal range per stream
       // block (blocks in proportion to the groups), split at segment boundaries; one launch per bit width
-      const uint64_t NB = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)g_num_cus * 8, T / 64));
+      static const char* ig_env = getenv("PG_STREAM_ITEM_GROUPS");  // > 0: interleaved items of this many groups
+      static const char* bpc_env = getenv("PG_STREAM_BLOCKS_PER_CU");
+      const uint64_t item_groups = ig_env ? (uint64_t)std::max(0, atoi(ig_env)) : 0;
+      const uint64_t per_cu = bpc_env ? (uint64_t)std::max(1, atoi(bpc_env)) : (sp.extra.empty() ? 7 : 6);
+      const uint64_t NB = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)g_num_cus * per_cu, T / 64));
       items.clear();
       uint64_t max_groups = 0;
+      sp.interleave = item_groups > 0;
       for (auto& bb : by_bits) {
+        if (sp.interleave) {  // items of item_groups groups in segment order, dealt round-robin to the blocks
+          StreamLaunch sl;
+          sl.bits = bb.first;
+          const uint32_t first = (uint32_t)items.size();
+          for (uint32_t si : bb.second)
+            for (uint64_t g0 = 0; g0 < seg_groups[si]; g0 += item_groups) {
+              const uint64_t e = std::min(seg_groups[si], g0 + item_groups);
+              items.push_back({si, (uint32_t)g0, (uint32_t)e, 0});
+              max_groups = std::max(max_groups, e - g0);
+            }
+          const uint64_t n_it = items.size() - first;
+          sl.blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_it, (NB * n_it + 1) / std::max<uint64_t>(1, T / item_groups)));
+          sl.first.assign(sl.blocks + 1, 0);
+          sl.first[0] = first;
+          sl.first[sl.blocks] = (uint32_t)items.size();
+          sp.launches.push_back(std::move(sl));
+          continue;
+        }
         const std::vector<uint32_t>& segs_b = bb.second;
         uint64_t Tb = 0;
         for (uint32_t si : segs_b) Tb += seg_groups[si];
@@ -2227,12 +2252,14 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         sp.launches.push_back(std::move(sl));
       }
       const double expect = pass * 32.0 * (double)max_groups;
-      const uint64_t cap = std::min<uint64_t>(32 * max_groups, ((uint64_t)(4.0 * expect) + 1024 + 63) & ~63ull);
+      const uint64_t slack = std::min<uint64_t>(1024, std::max<uint64_t>(64, 8 * max_groups));
+      const uint64_t cap = std::min<uint64_t>(32 * max_groups, ((uint64_t)(4.0 * expect) + slack + 63) & ~63ull);
       sp.on = true;
       sp.leaf = (uint32_t)li;
       sp.cap = (uint32_t)cap;
       q.num_items = (uint32_t)items.size();
-      grid = (uint32_t)std::min<uint64_t>(items.size(), scan_grid_cap(K > 0));
+      static const char* lb_env = getenv("PG_LIST_BLOCKS");
+      grid = (uint32_t)std::min<uint64_t>(items.size(), lb_env ? (uint64_t)std::max(1, atoi(lb_env)) : scan_grid_cap(K > 0));
       want_xcd = false;
       // list mode: the driving leaf is done; phase B = the AND's remaining children, all read by gathers
       q.list_mode = 1;
@@ -2248,6 +2275,13 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       memset(q.leaf_slot, kNoSlot, sizeof(q.leaf_slot));
       memset(q.agg_slot, kNoSlot, sizeof(q.agg_slot));
       memset(q.key_slot, kNoSlot, sizeof(q.key_slot));
+      // the list kernel stages only the IN sets its phase-B leaves read (the streamed leaves' sets are the stream's)
+      sp.set_ints = q.set_lds_ints;
+      bool b_sets = false;
+      for (uint32_t i = q.opB_begin; i < q.opB_end; i++)
+        for (uint32_t si = 0; si < S && q.ops[i] >= 0 && !b_sets; si++)
+          b_sets = leaves[(uint64_t)si * L + q.ops[i]].kind == LK_SET_LDS;
+      if (!b_sets) q.set_lds_ints = 0;
     }
   }
   const size_t lds_bytes = scan_lds_bytes(q);
@@ -2453,8 +2487,9 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     ss.leaf = sp.leaf;
     ss.cap = sp.cap;
     ss.num_extra = (uint32_t)sp.extra.size();
+    ss.interleave = sp.interleave ? 1u : 0u;
     for (size_t x = 0; x < sp.extra.size(); x++) ss.extra[x] = sp.extra[x];
-    ss.set_lds_ints = q.set_lds_ints;
+    ss.set_lds_ints = sp.set_ints;
     ss.segs = q.segs;
     ss.items = q.items;
     ss.docs = (uint32_t*)l_docs.p;
