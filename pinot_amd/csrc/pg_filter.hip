@@ -70,6 +70,17 @@ __device__ __forceinline__ uint32_t value_at(const uint32_t (&w)[B + 1], int j) 
   return __builtin_amdgcn_alignbit(w[k], w[k + 1], 64u - o - B) & M;
 }
 
+// value `idx` of a `b`-bit packed column through its buffer descriptor (a 64-bit window of two words)
+__device__ __forceinline__ uint32_t unpack_win(rsrc_t r, uint32_t idx, uint32_t b) {
+  const uint64_t pbit = (uint64_t)idx * b;
+  const uint32_t off = (uint32_t)(pbit >> 5) << 2;
+  const uint32_t sh = (uint32_t)pbit & 31u;
+  const uint32_t w0 = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+  const uint32_t w1 = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4u, 0, 0);
+  const uint64_t win = ((uint64_t)w0 << 32) | (uint64_t)w1;
+  return (uint32_t)(win >> (64u - sh - b)) & (0xFFFFFFFFu >> (32u - b));
+}
+
 // One leaf over one group for the docs in `need`: bit j <-> doc 32g + j.
 template <int B>
 __device__ __forceinline__ uint32_t eval_group(const LeafDesc& L, const uint32_t* lds_sets, uint64_t g, uint32_t need) {
@@ -88,14 +99,27 @@ __device__ __forceinline__ uint32_t eval_group(const LeafDesc& L, const uint32_t
       const uint32_t x = value_at<B>(w, j) >> sh;
       m |= ((bm[x >> 5] >> (x & 31u)) & 1u) << j;
     }
-    if (sh) {  // candidates of the coarse filter bitmap, resolved together through the exact LUT
+    if (sh) {
+      // candidates of the coarse filter bitmap, resolved through the exact LUT in rounds of up to 4 per lane with
+      // their loads in flight together.  The candidate's value is re-read from memory (its line was just loaded):
+      // picking it out of w[] by a per-lane index would be a waterfall loop over the lanes' indices.
+      const rsrc_t rs = rsrc_of(L.words, L.wbytes);
+      const uint32_t d0 = (uint32_t)(g * 32);
       uint32_t cand = m & need;
       m = 0;
-      while (cand) {
-        const int j = __ffs(cand) - 1;
-        cand &= cand - 1u;
-        const uint32_t v = value_at<B>(w, j);
-        m |= ((L.lut[v >> 5] >> (v & 31u)) & 1u) << j;
+      while (__ballot(cand != 0)) {
+        uint32_t jj[4], v[4], lw[4];
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+          jj[x] = cand ? (uint32_t)__ffs(cand) - 1u : 32u;
+          cand &= cand - 1u;
+          v[x] = jj[x] < 32u ? unpack_win(rs, d0 + jj[x], B) : 0u;
+        }
+#pragma unroll
+        for (int x = 0; x < 4; x++) lw[x] = jj[x] < 32u ? L.lut[v[x] >> 5] : 0u;
+#pragma unroll
+        for (int x = 0; x < 4; x++)
+          if (jj[x] < 32u) m |= ((lw[x] >> (v[x] & 31u)) & 1u) << jj[x];
       }
     }
   } else {  // LK_SET_LUT: a global bitmap over dictIds, 8 lookups in flight at a time
@@ -161,17 +185,6 @@ __global__ __launch_bounds__(256) void prefilter_kernel(PreSpec p) {
       if (p.first || nm != m) out[g] = __builtin_bitreverse32(nm);
     }
   }
-}
-
-// value `idx` of a `b`-bit packed column through its buffer descriptor (a 64-bit window of two words)
-__device__ __forceinline__ uint32_t unpack_win(rsrc_t r, uint32_t idx, uint32_t b) {
-  const uint64_t pbit = (uint64_t)idx * b;
-  const uint32_t off = (uint32_t)(pbit >> 5) << 2;
-  const uint32_t sh = (uint32_t)pbit & 31u;
-  const uint32_t w0 = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
-  const uint32_t w1 = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4u, 0, 0);
-  const uint64_t win = ((uint64_t)w0 << 32) | (uint64_t)w1;
-  return (uint32_t)(win >> (64u - sh - b)) & (0xFFFFFFFFu >> (32u - b));
 }
 
 // A further leaf of the root AND on the docs `need` of the group at doc d0 (AndDocIdSet: later children see only the

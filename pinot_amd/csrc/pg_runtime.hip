@@ -2259,7 +2259,11 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       sp.cap = (uint32_t)cap;
       q.num_items = (uint32_t)items.size();
       static const char* lb_env = getenv("PG_LIST_BLOCKS");
-      grid = (uint32_t)std::min<uint64_t>(items.size(), lb_env ? (uint64_t)std::max(1, atoi(lb_env)) : scan_grid_cap(K > 0));
+      // list grid: ~2 048 expected survivors per block (fewer blocks = fewer flushes of the block's group table;
+      // measured: config 2 (1 M survivors) 512 blocks 0.111 ms vs 1 536 0.166 ms, config 3 (14 M) flat 1 024-1 536)
+      const uint64_t want = std::max<uint64_t>(256, (uint64_t)(pass * 32.0 * (double)T) / 2048);
+      grid = (uint32_t)std::min<uint64_t>(items.size(), lb_env ? (uint64_t)std::max(1, atoi(lb_env))
+                                                                : std::min<uint64_t>(want, scan_grid_cap(K > 0)));
       want_xcd = false;
       // list mode: the driving leaf is done; phase B = the AND's remaining children, all read by gathers
       q.list_mode = 1;

@@ -52,6 +52,8 @@ def main():
         "in_only": f"SELECT COUNT(*) FROM t WHERE accountId IN ({ids})",
         "range_only": "SELECT COUNT(*) FROM t WHERE daysSinceEpoch BETWEEN 18000 AND 18089",
         "range_acct": "SELECT COUNT(*) FROM t WHERE accountId BETWEEN 1000 AND 500000",
+        "range_narrow": "SELECT COUNT(*) FROM t WHERE accountId BETWEEN 1000 AND 1999",
+        "in_100": "SELECT COUNT(*) FROM t WHERE accountId IN (" + ids.split(", 1")[0] + ")",
         "sum_dense": "SELECT SUM(clicks) FROM t",
         "gb_dense": "SELECT daysSinceEpoch, SUM(clicks) FROM t GROUP BY daysSinceEpoch",
         "config2": synth.adanalytics_query(1000),
