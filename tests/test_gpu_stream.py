@@ -114,3 +114,30 @@ def test_stream_multi_leaf_ssb_shape(gpu_engine, oracle_engine):
     assert_same_result(g, o, table=t)
     n = gpu_engine.execute(t, q, flags=abi.PG_PLAN_VALUE_SETS | abi.PG_PLAN_NO_STREAM)
     assert_same_result(g, n, table=t)
+
+
+@pytest.fixture(scope="module")
+def wide_table():
+    """acct cardinality ~290 K per segment: an IN list's LDS bitmap must be coarse (dictId >> shift), so lists of
+    <= 1 024 ids also get the exact LDS hash table, longer ones the global LUT."""
+    segs = []
+    for s, n in enumerate((300_000, 250_007)):
+        rng = np.random.default_rng(100 + s)
+        data = {"acct": rng.integers(0, 4_000_000, n), "day": rng.integers(0, 365, n),
+                "clicks": rng.integers(0, 1000, n)}
+        segs.append(ImmutableSegment.create(f"w{s}", data, {"acct": "INT", "day": "INT", "clicks": "INT"}))
+    return Table("t", segs)
+
+
+@pytest.mark.parametrize("k", [10, 1000, 3000])
+def test_stream_in_list_hash_table(k, wide_table, gpu_engine, oracle_engine):
+    ids = _in_list(k, seed=k, hi=4_000_000)
+    for sql in (f"SELECT COUNT(*), SUM(clicks) FROM t WHERE acct IN ({ids})",
+                # the IN list as a further AND leaf tested on the survivors of a selective range
+                f"SELECT day, COUNT(*) FROM t WHERE day < 10 AND acct IN ({ids}) GROUP BY day ORDER BY day LIMIT 20"):
+        q = parse(sql)
+        g = gpu_engine.execute(wide_table, q)
+        assert gpu_engine.last_timing().scan_launches == 2, "the selective stream did not run"
+        assert_same_result(g, oracle_engine.execute(wide_table, q), table=wide_table)
+        n = gpu_engine.execute(wide_table, q, flags=abi.PG_PLAN_VALUE_SETS | abi.PG_PLAN_NO_STREAM)
+        assert_same_result(g, n, table=wide_table)
