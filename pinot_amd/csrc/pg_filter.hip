@@ -91,22 +91,6 @@ __device__ __forceinline__ uint32_t eval_group(const LeafDesc& L, const uint32_t
     const uint32_t lo = (uint32_t)L.lo, span = (uint32_t)(L.hi - L.lo);
 #pragma unroll
     for (int j = 0; j < 32; j++) m |= (uint32_t)((value_at<B>(w, j) - lo) < span) << j;
-  } else if (L.kind == LK_SET_LDS && L.tbits) {
-    // coarse bitmap, then for its (rare) candidates the exact LDS hash table of the ids, value still in registers
-    const uint32_t* bm = lds_sets + L.lds_off;
-    const uint32_t* tab = bm + L.nbw;
-    const uint32_t sh = L.shift, tmask = (1u << L.tbits) - 1u, tb = L.tbits;
-#pragma unroll
-    for (int j = 0; j < 32; j++) {
-      const uint32_t v = value_at<B>(w, j), x = v >> sh;
-      if ((bm[x >> 5] >> (x & 31u)) & 1u) {
-        for (uint32_t h = set_hash_slot(v, tb);; h = (h + 1u) & tmask) {
-          const uint32_t k = tab[h];
-          if (k == v + 1u) { m |= 1u << j; break; }
-          if (!k) break;
-        }
-      }
-    }
   } else if (L.kind == LK_SET_LDS) {
     const uint32_t* bm = lds_sets + L.lds_off;
     const uint32_t sh = L.shift;
@@ -237,18 +221,7 @@ __device__ __forceinline__ uint32_t eval_extra(const LeafDesc& X, const uint32_t
           } else if (X.kind == LK_SET_LDS) {
             const uint32_t y = v[x] >> X.shift;
             hit = (lds_sets[X.lds_off + (y >> 5)] >> (y & 31u)) & 1u;
-            if (hit && X.tbits) {  // exact LDS hash table of the ids
-              const uint32_t* tab = lds_sets + X.lds_off + X.nbw;
-              const uint32_t tmask = (1u << X.tbits) - 1u;
-              hit = false;
-              for (uint32_t h = set_hash_slot(v[x], X.tbits);; h = (h + 1u) & tmask) {
-                const uint32_t k = tab[h];
-                if (k == v[x] + 1u) { hit = true; break; }
-                if (!k) break;
-              }
-            } else if (hit && X.shift) {
-              hit = (X.lut[v[x] >> 5] >> (v[x] & 31u)) & 1u;
-            }
+            if (hit && X.shift) hit = (X.lut[v[x] >> 5] >> (v[x] & 31u)) & 1u;
           } else {
             hit = (X.aux[v[x] >> 5] >> (v[x] & 31u)) & 1u;
           }

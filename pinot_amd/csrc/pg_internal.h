@@ -82,10 +82,7 @@ struct LeafDesc {
   // nvals > 0, membership in rvals (nvals sorted int64 for INT / LONG, double for FLOAT / DOUBLE)
   int64_t ilo, ihi;
   double dlo, dhi;
-  uint32_t rtype, rflags, nvals;
-  uint32_t tbits;         // SET_LDS with shift > 0: the region also holds an exact hash table of the ids after the bitmap,
-                          // 2^tbits words at lds_off + nbw (id + 1, 0 = empty; slot (id * 0x9E3779B1) >> (32 - tbits),
-                          // linear probing); 0 = none (candidates resolved by `lut`)
+  uint32_t rtype, rflags, nvals, pad;
   const uint32_t* rvals;
 };
 
@@ -276,11 +273,7 @@ struct LutJob {            // set bits ids[0..n) in lut and ids >> shift in regi
   uint32_t* region;          // LDS-set filter bitmap over dictId >> shift, or null
   uint32_t n;
   uint32_t shift;
-  uint32_t* table;           // exact hash table of the ids (LeafDesc::tbits), zeroed, or null
-  uint32_t tbits;
-  uint32_t pad;
 };
-__host__ __device__ inline uint32_t set_hash_slot(uint32_t id, uint32_t tbits) { return (id * 0x9E3779B1u) >> (32u - tbits); }
 hipError_t launch_set_lut_bits(const LutJob* jobs, uint32_t njobs, hipStream_t s);
 
 // ---- streaming pre-filter (pg_filter.hip): one leaf of the root AND over the segments whose form of it reads

@@ -385,11 +385,6 @@ __global__ void set_lut_bits_kernel(const LutJob* __restrict__ jobs) {
     const uint32_t id = (uint32_t)J.ids[i];
     if (J.lut) atomicOr(&J.lut[id >> 5], 1u << (id & 31u));
     if (J.region) atomicOr(&J.region[(id >> J.shift) >> 5], 1u << ((id >> J.shift) & 31u));
-    if (J.table) {  // ids are unique: claim the first free slot from the id's hash (linear probing, <= 50 % full)
-      const uint32_t mask = (1u << J.tbits) - 1u;
-      for (uint32_t h = set_hash_slot(id, J.tbits), k = 0; k <= mask; k++, h = (h + 1u) & mask)
-        if (atomicCAS(&J.table[h], 0u, id + 1u) == 0u) break;
-    }
   }
 }
 

@@ -1550,30 +1550,12 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   // Per leaf: LDS words of its IN-set region (uniform across segments), 0 = gathered through a global LUT.
   // Region = filter bitmap over dictId >> shift (<= 8 KB) + (shift > 0) an exact hash table (<= 50 % full).
   // LDS filter bitmap over dictId >> shift: at most kLdsSetBytes (shift > 0 adds an exact global LUT)
-  // When the bitmap cannot be exact (shift > 0) and the list is short (<= 1 024 ids), the region also holds an exact
-  // hash table of the ids (2^tbits words, <= 50 % full) after a correspondingly coarser bitmap: the selective stream
-  // then resolves candidates in LDS instead of by a global LUT read (config 2: 0.1 ms of its 0.54 ms).
-  auto set_geometry = [](uint32_t card, uint32_t max_ids, uint32_t& shift, uint32_t& nbw, uint32_t& tbits) {
-    auto fit = [&](uint32_t bits_budget) {
-      shift = 0;
-      while (((card + (1u << shift) - 1) >> shift) > bits_budget) shift++;
-      nbw = (((card + (1u << shift) - 1) >> shift) + 31) / 32 + 1;
-    };
-    tbits = 0;
-    fit((uint32_t)(kLdsSetBytes * 8 - 32));
-    if (shift && max_ids && max_ids <= 1024) {
-      tbits = 6;
-      while ((1u << tbits) < 2 * max_ids) tbits++;
-      fit((uint32_t)(kLdsSetBytes * 8 - 32) - (32u << tbits));
-    }
-    return nbw + (tbits ? (1u << tbits) : 0u);
+  auto set_geometry = [](uint32_t card, uint32_t& shift, uint32_t& nbw) {
+    shift = 0;
+    while (((card + (1u << shift) - 1) >> shift) > (uint32_t)(kLdsSetBytes * 8 - 32)) shift++;
+    nbw = (((card + (1u << shift) - 1) >> shift) + 31) / 32 + 1;
+    return nbw;
   };
-  std::vector<uint32_t> leaf_max_ids(L, 0);
-  for (uint32_t si = 0; si < S; si++)
-    for (uint32_t li = 0; li < L; li++) {
-      const pg_leaf& pl = plan->segments[si].leaves[li];
-      if (pl.kind == PG_LEAF_SV_SCAN) leaf_max_ids[li] = std::max(leaf_max_ids[li], pl.num_ids);
-    }
   std::vector<uint32_t> set_ints(L, 0), set_off(L, 0);
   std::vector<double> leaf_pass(L, 0.0), leaf_cost(L, 0.0), leaf_reach(L, 0.0);
   double filter_pass = 1.0;
@@ -1584,8 +1566,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         if (pl.kind != PG_LEAF_SV_SCAN || pl.num_ids == 0) continue;
         const ColumnRes* c = col(si, pl.col_id);
         if (!c) continue;
-        uint32_t sh, nbw, tb;
-        set_ints[li] = std::max(set_ints[li], set_geometry(std::max(c->card, 1u), leaf_max_ids[li], sh, nbw, tb));
+        uint32_t sh, nbw;
+        set_ints[li] = std::max(set_ints[li], set_geometry(std::max(c->card, 1u), sh, nbw));
       }
     uint32_t used = 0;
     for (uint32_t li = 0; li < L; li++) {
@@ -1693,7 +1675,6 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   std::vector<PrepassOp> pre;
   struct LutReq {  // arena ids -> scratch LUT and / or LDS-set region (~0 = none)
     uint64_t ids_off; uint32_t n; uint64_t lut_off; uint64_t region_off = ~0ull; uint32_t shift = 0;
-    uint32_t tbits = 0; uint64_t table_off = ~0ull;
   };
   std::vector<LutReq> luts;
   uint64_t scratch_bytes = 0;
@@ -1806,14 +1787,13 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
             dl.hi = std::max(std::min(hi, (int32_t)c->card), dl.lo);
           } else if (set_ints[li]) {
             dl.kind = LK_SET_LDS;
-            const uint32_t n_region = set_geometry(std::max(c->card, 1u), leaf_max_ids[li], dl.shift, dl.nbw, dl.tbits);
+            const uint32_t n_region = set_geometry(std::max(c->card, 1u), dl.shift, dl.nbw);
             dl.set_ints = n_region;
             dl.lds_off = set_off[li];
             // filter bitmap (and, when shift > 0, the exact LUT resolving its candidates) built on the device
             const uint64_t region_off = scratch_reserve(4ull * n_region);
             const uint64_t lut_off = dl.shift ? scratch_reserve(4ull * ((c->card + 31) / 32 + 1)) : ~0ull;
-            luts.push_back({ar.put(pl.ids, 4ull * pl.num_ids), pl.num_ids, lut_off, region_off, dl.shift, dl.tbits,
-                            dl.tbits ? region_off + 4ull * dl.nbw : ~0ull});
+            luts.push_back({ar.put(pl.ids, 4ull * pl.num_ids), pl.num_ids, lut_off, region_off, dl.shift});
             patches.push_back({(uint64_t)si * L + li, region_off, false, PT_AUX});
             if (dl.shift) patches.push_back({(uint64_t)si * L + li, lut_off, false, PT_LUT});
           } else {
@@ -2132,13 +2112,15 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     static const char* no_stage = getenv("PG_NO_STAGING");
     // minimum expected needed docs per 128-byte line for staging (PG_STAGE_MIN overrides)
     static const double stage_min = getenv("PG_STAGE_MIN") ? atof(getenv("PG_STAGE_MIN")) : 1.0;
+    // LDS bytes of one staging buffer (PG_STAGE_KB overrides kLdsStageBytes)
+    static const uint64_t stage_budget = getenv("PG_STAGE_KB") ? 1024ull * (uint64_t)atoi(getenv("PG_STAGE_KB")) : (uint64_t)kLdsStageBytes;
     uint32_t words = 0;
     for (const Cand& c : cands) {
       if (no_stage || q.num_staged >= (uint32_t)kMaxStaged) break;
       if (!c.bmax) continue;  // raw values: read per doc (already consecutive words), never staged
       if (c.reach * 1024.0 / c.bmax < stage_min) continue;
       const uint32_t need = (uint32_t)(kTileDocs / 32) * c.bmax;  // b DMA pieces of 1 KiB
-      if ((words + need) * 4ull > (uint64_t)kLdsStageBytes) continue;
+      if ((words + need) * 4ull > stage_budget) continue;
       const uint32_t slot = q.num_staged++;
       q.staged[slot] = {c.role, c.idx, c.operand, words};
       words += need;
@@ -2509,8 +2491,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   for (size_t i = 0; i < luts.size(); i++)
     lutjobs[i] = {(const int32_t*)(dA + luts[i].ids_off),
                   luts[i].lut_off == ~0ull ? nullptr : (uint32_t*)(dS + luts[i].lut_off),
-                  luts[i].region_off == ~0ull ? nullptr : (uint32_t*)(dS + luts[i].region_off), luts[i].n, luts[i].shift,
-                  luts[i].table_off == ~0ull ? nullptr : (uint32_t*)(dS + luts[i].table_off), luts[i].tbits, 0};
+                  luts[i].region_off == ~0ull ? nullptr : (uint32_t*)(dS + luts[i].region_off), luts[i].n, luts[i].shift};
   if (!leaves.empty()) memcpy(&ar.h[off_leaves], leaves.data(), leaves.size() * sizeof(LeafDesc));
   if (!aggcols.empty()) memcpy(&ar.h[off_aggcols], aggcols.data(), aggcols.size() * sizeof(ColDesc));
   if (!keycols.empty()) memcpy(&ar.h[off_keycols], keycols.data(), keycols.size() * sizeof(ColDesc));
