@@ -35,7 +35,7 @@ constexpr int kMaxOps = 64;
 constexpr int kMaxDepth = 4;                         // filter tree nesting (open groups)
 constexpr int kLdsGroupBytes = 32 * 1024;            // LDS-privatised group table budget
 constexpr int kLdsSetBytes = 16 * 1024;              // LDS filter bitmaps of IN / NOT_IN leaves
-constexpr int kLdsStageBytes = 32 * 1024;            // LDS tiles of densely read packed columns (per ring buffer)
+constexpr int kLdsStageBytes = 40 * 1024;            // LDS tiles of densely read packed columns (per ring buffer; config 4 stages 23 + 10 bits: 19.2 -> 16.3 ms)
 constexpr int kMaxStaged = 6;                        // packed columns staged per tile
 constexpr int kNoSlot = 255;
 constexpr uint32_t kPollTiles = 2;                   // scan tiles between polls of the cancel / deadline flag

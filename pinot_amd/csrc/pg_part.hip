@@ -48,7 +48,7 @@ __device__ __forceinline__ uint32_t digit2(const PartSpec& P, uint32_t e) {
 template <class Out>
 __device__ __forceinline__ void split_round(uint32_t (&e)[kSplitChunk / 256], uint32_t (&dg)[kSplitChunk / 256],
                                             uint32_t n, uint32_t ndig, uint32_t* cnt, uint32_t* start,
-                                            unsigned long long* cur, uint32_t* sbuf, uint16_t* sdig, Out* out) {
+                                            unsigned long long* cur, uint32_t* sbuf, uint8_t* sdig, Out* out) {
   constexpr int E = kSplitChunk / 256;
   const uint32_t tid = threadIdx.x;
   uint32_t rank[E];
@@ -80,7 +80,7 @@ __device__ __forceinline__ void split_round(uint32_t (&e)[kSplitChunk / 256], ui
     if (tid + 256u * k < n) {
       const uint32_t at = start[dg[k]] + rank[k];
       sbuf[at] = e[k];
-      sdig[at] = (uint16_t)dg[k];
+      sdig[at] = (uint8_t)dg[k];
     }
   __syncthreads();
   for (uint32_t i = tid; i < n; i += 256) {
@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256) void part_split1_kernel(PartSpec P) {
   constexpr int E = kSplitChunk / 256;
   __shared__ uint32_t cnt[kPartL1], start[kPartL1], sbuf[kSplitChunk];
   __shared__ unsigned long long cur[kPartL1];
-  __shared__ uint16_t sdig[kSplitChunk];
+  __shared__ uint8_t sdig[kSplitChunk];  // digits < 256: 4 KB, so 6 blocks fit a CU (the scan grid is 6 per CU)
   const uint32_t b = blockIdx.x, tid = threadIdx.x;
   if (tid < P.nparts1) {
     cnt[tid] = 0;
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void part_split2_kernel(PartSpec P) {
   constexpr int E = kSplitChunk / 256;
   __shared__ uint32_t cnt[256], start[256], sbuf[kSplitChunk];
   __shared__ unsigned long long cur[256];
-  __shared__ uint16_t sdig[kSplitChunk];
+  __shared__ uint8_t sdig[kSplitChunk];  // digits < 256: 4 KB, so 6 blocks fit a CU (the scan grid is 6 per CU)
   const uint32_t j = blockIdx.x, p = blockIdx.y, tid = threadIdx.x;
   if (tid < P.nparts2) {
     cnt[tid] = 0;
