@@ -57,6 +57,11 @@ def main():
         "sum_dense": "SELECT SUM(clicks) FROM t",
         "gb_dense": "SELECT daysSinceEpoch, SUM(clicks) FROM t GROUP BY daysSinceEpoch",
         "config2": synth.adanalytics_query(1000),
+        "c2_filter": f"SELECT COUNT(*) FROM t WHERE daysSinceEpoch BETWEEN 18000 AND 18089 AND accountId IN ({ids})",
+        "c2_gb_count": f"SELECT daysSinceEpoch, COUNT(*) FROM t WHERE daysSinceEpoch BETWEEN 18000 AND 18089 "
+                       f"AND accountId IN ({ids}) GROUP BY daysSinceEpoch",
+        "c2_sum": f"SELECT SUM(clicks), SUM(impressions) FROM t WHERE daysSinceEpoch BETWEEN 18000 AND 18089 "
+                  f"AND accountId IN ({ids})",
     }
     rows = args.segments * args.rows
     for name, sql in qs.items():
