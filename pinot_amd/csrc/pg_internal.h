@@ -328,27 +328,11 @@ struct PartSpec {
   uint32_t* out2;                  // level-2 entries, bucket-major
   unsigned long long* i64;         // dense state written by the bucket pass
   uint32_t* bits;
-  // fused level 1 (match-all filter, one key column, at most one DISTINCTCOUNT value column): no scan; block b reads
-  // the docs of fused items [ffirst[b], ffirst[b + 1]) (tile_begin / tile_end in 32-doc groups) twice: part_hist
-  // counts their level-1 digits into hist1 [nparts1][blocks1], part_fuse1 writes their level-1 entries into in1
-  const SegDesc* segs;
-  const WorkItem* fitems;
-  const uint32_t* ffirst;
-  unsigned long long* hist1;
-  unsigned long long* seg_matched;  // [seg] docs (every doc matches)
-  unsigned int* err;                // bit 0 / 1: a key / value id outside its key space
-  uint32_t key_kind, key_card;
-  int64_t key_base;
-  uint32_t val_kind, val_card;      // val_card 0: no DISTINCTCOUNT (COUNT only)
-  int64_t val_base;
-  uint32_t dc_agg, fpad;            // the DISTINCTCOUNT's aggregation index (its column: aggcols[2 * dc_agg])
 };
 hipError_t launch_part_split1(const PartSpec& p, hipStream_t s);
 hipError_t launch_part_count2(const PartSpec& p, hipStream_t s);
 hipError_t launch_part_split2(const PartSpec& p, hipStream_t s);
 hipError_t launch_part_aggregate(const PartSpec& p, hipStream_t s);
-hipError_t launch_part_hist(const PartSpec& p, hipStream_t s);   // fused level 1, pass 1
-hipError_t launch_part_fuse1(const PartSpec& p, hipStream_t s);  // fused level 1, pass 2 (replaces scan + split1)
 
 // ---- group state (pg_groups.hip)
 struct StateView {            // the device arrays of one partial state

@@ -123,125 +123,6 @@ __global__ __launch_bounds__(256) void part_split1_kernel(PartSpec P) {
   }
 }
 
-// ------------------------------------------------------------------ fused level 1 (no scan)
-// A match-all filter over one key column: every doc is an entry, so instead of the scan appending 64-bit entries to
-// block regions and part_split1 re-reading them (config 4: 8.1 + 3.8 ms, 8 GB written and read back), two lean
-// passes read the packed columns directly: part_hist counts each block's level-1 digits, part_fuse1 counting-sorts
-// 4 096-doc chunks in LDS and writes the 32-bit level-1 entries as runs.  Lane l of a wave handles consecutive docs,
-// so each column read (a 64-bit window per doc) is coalesced across the wave.
-
-typedef __amdgpu_buffer_rsrc_t prsrc_t;
-__device__ __forceinline__ prsrc_t p_rsrc(const void* p, uint32_t bytes) {
-  const uint64_t a = (uint64_t)p;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
-                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-__device__ __forceinline__ uint32_t p_unpack(prsrc_t r, uint32_t idx, uint32_t b) {
-  const uint64_t pb = (uint64_t)idx * b;
-  const uint32_t off = (uint32_t)(pb >> 5) << 2, sh = (uint32_t)pb & 31u;
-  const uint32_t w0 = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0), w1 = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4u, 0, 0);
-  return (uint32_t)((((uint64_t)w0 << 32) | w1) >> (64u - sh - b)) & (0xFFFFFFFFu >> (32u - b));
-}
-// table-global id of dictId `id` of column c (~0: outside the key space), as the scan's key_of
-__device__ __forceinline__ uint64_t p_key(uint32_t kind, int64_t base, const ColDesc& c, uint32_t id) {
-  if (id >= c.card) return ~0ull;
-  if (kind == PG_KEY_KEYMAP) return (uint64_t)(uint32_t)c.keymap[id];
-  const int64_t v = c.decoded ? c.vbase + (int64_t)id
-                              : (c.dtype == PG_INT ? (int64_t)((const int32_t*)c.dict)[id] : ((const int64_t*)c.dict)[id]);
-  return (uint64_t)(v - base);
-}
-
-// the docs of fused item `it`: [d0, d1) of segment `seg`
-__device__ __forceinline__ void fitem_docs(const PartSpec& P, uint32_t it, uint32_t& seg, uint32_t& d0, uint32_t& d1) {
-  const WorkItem w = P.fitems[it];
-  const uint32_t nd = P.segs[w.seg].num_docs;
-  seg = w.seg;
-  d0 = min(w.tile_begin * 32u, nd);
-  d1 = min(w.tile_end * 32u, nd);
-}
-
-__global__ __launch_bounds__(256) void part_hist_kernel(PartSpec P) {
-  __shared__ uint32_t h[kPartL1];
-  const uint32_t b = blockIdx.x, tid = threadIdx.x;
-  for (uint32_t i = tid; i < P.nparts1; i += 256) h[i] = 0;
-  __syncthreads();
-  const uint32_t sh = P.shift1;
-  uint32_t bad = 0;
-  for (uint32_t it = P.ffirst[b]; it < P.ffirst[b + 1]; it++) {
-    uint32_t seg, d0, d1;
-    fitem_docs(P, it, seg, d0, d1);
-    const ColDesc kc = P.segs[seg].keycols[0];
-    const prsrc_t kr = p_rsrc(kc.words, kc.wbytes);
-    if (tid == 0 && d1 > d0) atomicAdd(&P.seg_matched[seg], (unsigned long long)(d1 - d0));
-    for (uint32_t d = d0 + tid; d < d1; d += 1024) {  // four docs per lane in flight
-      uint32_t id[4];
-#pragma unroll
-      for (int k = 0; k < 4; k++) id[k] = d + 256u * k < d1 ? p_unpack(kr, d + 256u * k, kc.bits) : 0u;
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        if (d + 256u * k >= d1) continue;
-        const uint64_t g = p_key(P.key_kind, P.key_base, kc, id[k]);
-        if (g >= P.key_card) { bad = 1; continue; }
-        atomicAdd(&h[(uint32_t)(g >> sh)], 1u);
-      }
-    }
-  }
-  if (bad) atomicOr(P.err, 1u);
-  __syncthreads();
-  for (uint32_t p = tid; p < P.nparts1; p += 256) P.hist1[(uint64_t)p * P.blocks1 + b] = h[p];
-}
-
-__global__ __launch_bounds__(256) void part_fuse1_kernel(PartSpec P) {
-  constexpr int E = kSplitChunk / 256;
-  __shared__ uint32_t cnt[kPartL1], start[kPartL1], sbuf[kSplitChunk];
-  __shared__ unsigned long long cur[kPartL1];
-  __shared__ uint8_t sdig[kSplitChunk];
-  const uint32_t b = blockIdx.x, tid = threadIdx.x;
-  if (tid < P.nparts1) {
-    cnt[tid] = 0;
-    cur[tid] = P.off1[(uint64_t)tid * P.blocks1 + b];
-  }
-  __syncthreads();
-  const uint32_t sh = P.shift1, vb = P.vbits;
-  const uint64_t lmask = (1ull << P.shift1) - 1ull;
-  uint32_t bad = 0;
-  for (uint32_t it = P.ffirst[b]; it < P.ffirst[b + 1]; it++) {
-    uint32_t seg, d0, d1;
-    fitem_docs(P, it, seg, d0, d1);
-    const SegDesc sd = P.segs[seg];
-    const ColDesc kc = sd.keycols[0];
-    const prsrc_t kr = p_rsrc(kc.words, kc.wbytes);
-    ColDesc vc;
-    prsrc_t vr = kr;
-    if (P.val_card) {
-      vc = sd.aggcols[2 * P.dc_agg];
-      vr = p_rsrc(vc.words, vc.wbytes);
-    }
-    for (uint32_t c0 = d0; c0 < d1; c0 += kSplitChunk) {
-      const uint32_t m = min((uint32_t)kSplitChunk, d1 - c0);
-      uint32_t e[E], dg[E], kid[E], vid[E];
-#pragma unroll
-      for (int k = 0; k < E; k++) {
-        const uint32_t i = tid + 256u * k;
-        kid[k] = i < m ? p_unpack(kr, c0 + i, kc.bits) : 0u;
-        vid[k] = (P.val_card && i < m) ? p_unpack(vr, c0 + i, vc.bits) : 0u;
-      }
-#pragma unroll
-      for (int k = 0; k < E; k++) {
-        const uint32_t i = tid + 256u * k;
-        uint64_t g = i < m ? p_key(P.key_kind, P.key_base, kc, kid[k]) : 0ull;
-        uint64_t v = (P.val_card && i < m) ? p_key(P.val_kind, P.val_base, vc, vid[k]) : 0ull;
-        if (i < m && (g >= P.key_card || (P.val_card && v >= P.val_card))) { bad = 1; g = 0; v = 0; }
-        dg[k] = (uint32_t)(g >> sh);
-        e[k] = (uint32_t)(((g & lmask) << vb) | v);
-      }
-      split_round(e, dg, m, P.nparts1, cnt, start, cur, sbuf, sdig, P.in1);
-    }
-  }
-  if (bad) atomicOr(P.err, 1u);
-}
-
 // Counts of the level-2 digits in block (j, p)'s range -> hist2[(p * nparts2 + digit) * kPartNB + j].
 __global__ __launch_bounds__(256) void part_count2_kernel(PartSpec P) {
   extern __shared__ uint32_t h[];  // [nparts2]
@@ -343,14 +224,6 @@ __global__ __launch_bounds__(256) void part_aggregate_kernel(PartSpec P) {
 
 hipError_t launch_part_split1(const PartSpec& p, hipStream_t s) {
   hipLaunchKernelGGL(part_split1_kernel, dim3(p.blocks1), dim3(256), 0, s, p);
-  return hipGetLastError();
-}
-hipError_t launch_part_hist(const PartSpec& p, hipStream_t s) {
-  hipLaunchKernelGGL(part_hist_kernel, dim3(p.blocks1), dim3(256), 0, s, p);
-  return hipGetLastError();
-}
-hipError_t launch_part_fuse1(const PartSpec& p, hipStream_t s) {
-  hipLaunchKernelGGL(part_fuse1_kernel, dim3(p.blocks1), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 hipError_t launch_part_count2(const PartSpec& p, hipStream_t s) {

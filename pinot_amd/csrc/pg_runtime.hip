@@ -1508,7 +1508,6 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   // cache, when the aggregations are COUNTs and at most one DISTINCTCOUNT (entries of key low bits | value id fit 32
   // bits).  PG_PART=0|1 overrides the size threshold.
   PartPlan part;
-  uint64_t part_docs = 0;  // fused level 1: docs of the scanned segments (= entries)
   {
     const char* part_env = getenv("PG_PART");
     const int pe = part_env ? atoi(part_env) : -1;
@@ -2418,47 +2417,6 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   const uint64_t off_leaves_orig = ar.reserve(leaves_orig.size() * sizeof(LeafDesc));
   const uint64_t off_segs_pre = ar.reserve(pre_leaves.empty() ? 0 : segd.size() * sizeof(SegDesc));
   const uint64_t off_pre_out = ar.reserve(pre_leaves.empty() ? 0 : 8ull * S);
-  // ---- fused level 1 of the radix-partitioned group-by (pg_part.hip part_hist / part_fuse1): with no filter and one
-  // packed key column, the scan's 64-bit entries and part_split1 are replaced by two passes that read the columns
-  // directly (PG_PART_FUSED=0 disables).  Items: the 32-doc groups of the segments, one equal range per block.
-  struct { bool on = false; uint64_t first_off = 0; std::vector<uint32_t> first; } fz;
-  {
-    static const char* pf_env = getenv("PG_PART_FUSED");
-    bool ok = part.on && !items.empty() && q.num_ops == 0 && K == 1 && !(pf_env && atoi(pf_env) == 0);
-    uint64_t T = 0, docs = 0;
-    std::vector<uint64_t> sg(S, 0);
-    for (uint32_t si = 0; si < S && ok; si++) {
-      if (!seg_tiles[si]) continue;
-      ok = keycols[si].bits > 0 && (part.dc == (uint32_t)kNoSlot || aggcols[((uint64_t)si * A + part.dc) * 2].bits > 0);
-      sg[si] = ((uint64_t)plan->segments[si].num_docs + 31) / 32;
-      T += sg[si];
-      docs += plan->segments[si].num_docs;
-    }
-    if (ok && T) {
-      const uint64_t NB = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)g_num_cus * 6, T / 64));
-      items.clear();
-      fz.first.assign(NB + 1, 0);
-      uint32_t si = 0;
-      uint64_t seg_first = 0;
-      for (uint64_t b = 0; b < NB; b++) {
-        fz.first[b] = (uint32_t)items.size();
-        uint64_t t0 = b * T / NB;
-        const uint64_t t1 = (b + 1) * T / NB;
-        while (t0 < t1) {
-          while (!sg[si] || t0 >= seg_first + sg[si]) { seg_first += sg[si]; si++; }
-          const uint64_t e = std::min(t1, seg_first + sg[si]);
-          items.push_back({si, (uint32_t)(t0 - seg_first), (uint32_t)(e - seg_first), 0});
-          t0 = e;
-        }
-      }
-      fz.first[NB] = (uint32_t)items.size();
-      fz.on = true;
-      q.num_items = (uint32_t)items.size();
-      grid = (uint32_t)NB;
-      want_xcd = false;
-      part_docs = docs;
-    }
-  }
   uint32_t blocks = 0;
   if (!items.empty()) {
     blocks = grid;
@@ -2488,10 +2446,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   for (StreamLaunch& sl : sp.launches) sl.first_off = ar.put(sl.first.data(), sl.first.size() * 4);
   // GM_PART: each block's region of the entry array = the docs of its items (the kernel's [i0, i1) item range)
   uint64_t off_part_base = 0, part_entries = 0;
-  if (fz.on) {
-    fz.first_off = ar.put(fz.first.data(), fz.first.size() * 4);
-    part_entries = part_docs;
-  } else if (part.on && blocks) {
+  if (part.on && blocks) {
     std::vector<uint64_t> base(blocks + 1, 0);
     for (uint32_t b = 0; b < blocks; b++) {
       const uint64_t i0 = (uint64_t)b * items.size() / blocks, i1 = (uint64_t)(b + 1) * items.size() / blocks;
@@ -2628,7 +2583,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     // level-1 split, level-2 count / scan / split, per-bucket aggregation
     const uint64_t n1 = (uint64_t)part.nparts1 * blocks, n2 = (uint64_t)part.nparts1 * part.nparts2 * kPartNB;
     const size_t tb = select_temp_bytes(std::max(n1, n2) + 1);
-    if ((rc = p_ent0.alloc_pooled(fz.on ? 16 : 8 * part_entries + 16)) || (rc = p_cnt0.alloc_pooled(4ull * blocks + 16)) ||
+    if ((rc = p_ent0.alloc_pooled(8 * part_entries + 16)) || (rc = p_cnt0.alloc_pooled(4ull * blocks + 16)) ||
         (rc = p_hist1.alloc_pooled(8 * (n1 + 1))) || (rc = p_off1.alloc_pooled(8 * (n1 + 1))) ||
         (rc = p_ent1.alloc_pooled(4 * part_entries + 16)) || (rc = p_hist2.alloc_pooled(8 * (n2 + 1))) ||
         (rc = p_off2.alloc_pooled(8 * (n2 + 1))) || (rc = p_ent2.alloc_pooled(4 * part_entries + 16)) ||
@@ -2650,37 +2605,10 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     q.part_base = (const unsigned long long*)(dA + off_part_base);
     q.part_out = (unsigned long long*)p_ent0.p;
     t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
+    HIP_CHECK(launch_scan(q, blocks, s));
+    HIP_CHECK(launch_exclusive_sum((const uint64_t*)h1, (uint64_t*)o1, n1 + 1, p_temp.p, tb, s));
     PartSpec ps;
     memset(&ps, 0, sizeof(ps));
-    if (fz.on) {  // fused level 1: part_hist + scan of its counts + part_fuse1 (no scan kernel, no split1)
-      ps.nparts1 = part.nparts1;
-      ps.vbits = part.vbits;
-      ps.shift1 = part.shift1;
-      ps.blocks1 = blocks;
-      ps.segs = q.segs;
-      ps.fitems = q.items;
-      ps.ffirst = (const uint32_t*)(dA + fz.first_off);
-      ps.hist1 = h1;
-      ps.seg_matched = q.seg_matched;
-      ps.err = q.err;
-      ps.key_kind = q.key_kind[0];
-      ps.key_card = q.key_card[0];
-      ps.key_base = q.key_base[0];
-      if (part.dc != (uint32_t)kNoSlot) {
-        ps.val_kind = q.aggs[part.dc].key_kind;
-        ps.val_card = q.aggs[part.dc].key_card;
-        ps.val_base = q.aggs[part.dc].key_base;
-        ps.dc_agg = part.dc;
-      }
-      HIP_CHECK(launch_part_hist(ps, s));
-      HIP_CHECK(launch_exclusive_sum((const uint64_t*)h1, (uint64_t*)o1, n1 + 1, p_temp.p, tb, s));
-      ps.off1 = o1;
-      ps.in1 = (uint32_t*)p_ent1.p;
-      HIP_CHECK(launch_part_fuse1(ps, s));
-    } else {
-      HIP_CHECK(launch_scan(q, blocks, s));
-      HIP_CHECK(launch_exclusive_sum((const uint64_t*)h1, (uint64_t*)o1, n1 + 1, p_temp.p, tb, s));
-    }
     ps.nparts1 = part.nparts1;
     ps.nparts2 = part.nparts2;
     ps.vbits = part.vbits;
@@ -2702,7 +2630,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     ps.out2 = (uint32_t*)p_ent2.p;
     ps.i64 = (unsigned long long*)P.i64.p;
     ps.bits = (uint32_t*)P.bits.p;
-    if (!fz.on) HIP_CHECK(launch_part_split1(ps, s));
+    HIP_CHECK(launch_part_split1(ps, s));
     HIP_CHECK(launch_part_count2(ps, s));
     HIP_CHECK(launch_exclusive_sum((const uint64_t*)h2, (uint64_t*)o2, n2 + 1, p_temp.p, tb, s));
     HIP_CHECK(launch_part_split2(ps, s));
@@ -2736,7 +2664,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   t_timing.prepass_ms = pre_ms;
   t_timing.prefilter_ms = filt_ms;
   t_timing.scan_ms = scan_ms;
-  t_timing.scan_launches = (blocks && !fz.on ? 1 : 0) + (sp.on && q.num_items ? 1 : 0);  // + the selective stream
+  t_timing.scan_launches = (blocks ? 1 : 0) + (sp.on && q.num_items ? 1 : 0);  // + the selective stream
   memset(&stats, 0, sizeof(stats));
   stats.num_total_docs = total_docs;
   stats.num_segments_processed = S;
