@@ -99,7 +99,7 @@ struct ColDesc {
   uint32_t wbytes;            // bytes of `words` (buffer-descriptor range)
   int64_t vbase;
   uint32_t decoded;
-  uint32_t pad;
+  uint32_t identity;          // decoded from an identity dictionary: `words` are the column's dictIds (host-side flag)
 };
 
 struct SegDesc {

@@ -268,6 +268,9 @@ struct ColumnRes {
   DevBuf rawv;
   // range index (PG_IDX_RANGE): present; a raw INT / LONG column's device form is `vals` (value - imin, vbits bits)
   bool has_range = false;
+  // identity dictionary: INT / LONG values imin, imin + 1, ..., imin + card - 1 (every value of a dense range present),
+  // so value = imin + dictId and the packed dictIds serve as the decoded forward index (no dictionary reads)
+  bool identity = false;
 };
 
 // Dictionaries at least this large get a decoded forward index (PG_DECODED=0 disables, =1 builds it for every
@@ -280,6 +283,9 @@ int build_decoded(ColumnRes& c, hipStream_t s) {
   const int mode = env ? atoi(env) : -1;
   c.vals.reset();
   c.vbits = 0;
+  c.identity = mode != 0 && c.has_dict && c.fwd == FWD_SV && (c.dtype == PG_INT || c.dtype == PG_LONG) && c.card &&
+               c.imax >= c.imin && (uint64_t)(c.imax - c.imin) + 1 == (uint64_t)c.card;
+  if (c.identity) return PG_OK;
   if (mode == 0 || !c.has_dict || c.fwd != FWD_SV || (c.dtype != PG_INT && c.dtype != PG_LONG) || !c.card ||
       !c.num_docs || (mode != 1 && c.card < kDecodeMinCard))
     return PG_OK;
@@ -1241,13 +1247,15 @@ bool agg_decodes(const pg_agg& g) {
          (g.fn == PG_AGG_DISTINCTCOUNT && g.key_kind == PG_KEY_VALUE_OFFSET);
 }
 void use_decoded(ColDesc& dc, const ColumnRes* c) {
-  dc.words = (const uint32_t*)c->vals.p;
-  dc.wbytes = (uint32_t)std::min<uint64_t>(c->vals.bytes, 0xFFFFFFF0ull);
-  dc.bits = c->vbits;
+  const DevBuf& w = c->identity ? c->words : c->vals;
+  dc.words = (const uint32_t*)w.p;
+  dc.wbytes = (uint32_t)std::min<uint64_t>(w.bytes, 0xFFFFFFF0ull);
+  dc.bits = c->identity ? c->bits : c->vbits;
   dc.dict = nullptr;
   dc.card = 0xFFFFFFFFu;
   dc.vbase = c->imin;
   dc.decoded = 1;
+  dc.identity = c->identity ? 1u : 0u;
 }
 
 int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t hash_cap, bool allow_stream) {
@@ -1911,7 +1919,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
           dc.bits = 0;
           dc.dict = c->rawv.p;
           dc.card = c->num_docs;
-        } else if (agg_decodes(g) && c->vals.p) {
+        } else if (agg_decodes(g) && (c->vals.p || c->identity)) {
           use_decoded(dc, c);
         }
       }
@@ -1927,7 +1935,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       dc.bits = c->bits;
       dc.dtype = c->dtype;
       dc.card = c->card;
-      if (plan->keys[k].kind == PG_KEY_VALUE_OFFSET && c->vals.p) use_decoded(dc, c);
+      if (plan->keys[k].kind == PG_KEY_VALUE_OFFSET && (c->vals.p || c->identity)) use_decoded(dc, c);
     }
   }
   P.entries_in_filter = entries_in_filter;
@@ -2081,14 +2089,22 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     }
     // aggregation / key uses read the column's decoded forward index in some segment ("decoded" uses: their own
     // slot, key type 3) or dictIds everywhere (key type 1, shared with scan leaves on the column)
-    auto agg_dec = [&](uint32_t a, int k) {
-      for (uint32_t si = 0; si < S; si++) if (aggcols[((uint64_t)si * A + a) * 2 + k].decoded) return true;
-      return false;
-    };
-    auto key_dec = [&](uint32_t k) {
-      for (uint32_t si = 0; si < S; si++) if (keycols[(uint64_t)si * K + k].decoded) return true;
-      return false;
-    };
+    // (an identity dictionary's decoded form IS the dictId stream: it shares the dictIds' slot; an identity
+    // ColDesc reads the dictId words, so `words` tells the two decoded forms apart without a column lookup)
+    bool agg_dec_v[kMaxAggs][2] = {}, key_dec_v[kMaxKeys] = {};
+    for (uint32_t si = 0; si < S; si++) {
+      for (uint32_t a = 0; a < A && a < (uint32_t)kMaxAggs; a++)
+        for (int k = 0; k < 2; k++) {
+          const ColDesc& dc = aggcols[((uint64_t)si * A + a) * 2 + k];
+          agg_dec_v[a][k] |= dc.decoded && !dc.identity;
+        }
+      for (uint32_t k = 0; k < K && k < (uint32_t)kMaxKeys; k++) {
+        const ColDesc& dc = keycols[(uint64_t)si * K + k];
+        key_dec_v[k] |= dc.decoded && !dc.identity;
+      }
+    }
+    auto agg_dec = [&](uint32_t a, int k) { return agg_dec_v[a][k]; };
+    auto key_dec = [&](uint32_t k) { return key_dec_v[k]; };
     for (uint32_t a = 0; a < A; a++) {
       const pg_agg& g = plan->aggs[a];
       if (g.fn == PG_AGG_COUNT || g.fn == PG_AGG_COUNTMV) continue;
