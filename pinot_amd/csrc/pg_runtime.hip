@@ -831,6 +831,7 @@ struct Partials {
   uint64_t num_slots = 1;
   uint32_t n_i64 = 1, n_f64 = 0, n_min = 0, n_max = 0, bit_words = 0, max_fill = 0;
   DevBuf keys, i64, f64, mn, mx, bits, first_doc, misc /* [fill, err] */, seg_matched;
+  bool host_state = false;      // t_ctx.state_host holds a copy of the final state (queued before the scan's sync)
   std::vector<uint32_t> key_card;
   std::vector<uint64_t> key_stride;
   uint32_t projected_cols = 0;
@@ -1026,6 +1027,7 @@ void assign_reach(const std::vector<FNode>& nodes, int n, double reach, std::vec
 struct ThreadCtx {  // per calling thread: staging + events, created once
   PinnedBuf pinned;
   PinnedBuf readback;  // per-segment match counts + error word, copied back before the one stream sync
+  PinnedBuf state_host;  // small dense states copied back with them (pg_execute)
   PinnedVec arena;              // pinned host image of the parameter arena (capacity reused across queries)
   std::vector<WorkItem> items;  // work items of the current query (capacity reused across queries)
   std::vector<WorkItem> items_perm;  // XCD-grouped order of the items (swapped with `items`)
@@ -1116,6 +1118,12 @@ int Partials::alloc_state(hipStream_t s, bool init) {
   else HIP_CHECK(hipMemsetAsync(misc.p, 0, 16, s));  // every slot is written by the producer (pg_part.hip)
   return PG_OK;
 }
+
+// A dense state of at most this many bytes is finalised on the host from one D2H copy (config 2: 90 x 3 int64):
+// the device path's select / final-value / trim launches and its two stream round trips cost ~0.1 ms there.  Under
+// pg_execute (no cross-GPU merge in between) the copy is queued right behind the scan, before its one sync.
+constexpr uint64_t kHostFinalBytes = 1ull << 20;
+thread_local bool t_prefetch_state = false;  // set by pg_execute around its pg_execute_partial
 
 constexpr int kRetryLargerTable = 1;  // internal: the hash table overflowed its fill budget
 constexpr int kRetryNoStream = 2;     // internal: a selective-stream region overflowed (more survivors than estimated)
@@ -2660,6 +2668,20 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   uint64_t* sm = (uint64_t*)t_ctx.readback.get(8ull * n_sm);
   if (!sm) return fail(PG_E_NOMEM, "pinned readback of %llu bytes failed", (unsigned long long)(8ull * n_sm));
   HIP_CHECK(hipMemcpyAsync(sm, P.seg_matched.p, 8ull * n_sm, hipMemcpyDeviceToHost, s));
+  P.host_state = false;
+  if (t_prefetch_state && (P.mode == GM_DENSE || P.mode == GM_NONE) && !P.bit_words &&
+      P.num_slots * 8ull * (P.n_i64 + P.n_f64 + P.n_min + P.n_max) <= kHostFinalBytes) {
+    const uint64_t G = P.num_slots;
+    const uint64_t b64 = G * 8ull * P.n_i64, bf = G * 8ull * P.n_f64, bmn = G * 8ull * P.n_min, bmx = G * 8ull * P.n_max;
+    uint8_t* h = (uint8_t*)t_ctx.state_host.get(b64 + bf + bmn + bmx + 8);
+    if (h) {
+      HIP_CHECK(hipMemcpyAsync(h, P.i64.p, b64, hipMemcpyDeviceToHost, s));
+      if (bf) HIP_CHECK(hipMemcpyAsync(h + b64, P.f64.p, bf, hipMemcpyDeviceToHost, s));
+      if (bmn) HIP_CHECK(hipMemcpyAsync(h + b64 + bf, P.mn.p, bmn, hipMemcpyDeviceToHost, s));
+      if (bmx) HIP_CHECK(hipMemcpyAsync(h + b64 + bf + bmn, P.mx.p, bmx, hipMemcpyDeviceToHost, s));
+      P.host_state = true;
+    }
+  }
   if (plan->deadline_ms && q.cancel) {  // wait, turning a passed deadline into the kernel's stop flag
     for (;;) {
       const hipError_t e = hipStreamQuery(s);
@@ -2747,9 +2769,6 @@ int build_result(pg_partials* pp, const pg_plan* plan, pg_result** out, const Pa
                  const std::vector<uint64_t>& hk, const std::vector<double>& hv, const std::vector<int64_t>& hc,
                  bool sets, const std::vector<uint64_t>& hoff, const std::vector<uint32_t>& hids);
 
-// A dense state of at most this many bytes is finalised on the host from one D2H copy (config 2: 90 x 3 int64):
-// the device path's select / final-value / trim launches and its two stream round trips cost ~0.1 ms there.
-constexpr uint64_t kHostFinalBytes = 1ull << 20;
 
 // finalize() for small dense states without DISTINCTCOUNT: the same groups, final values and ORDER BY candidates
 // (ties with the limit-th on the first ORDER BY item included) as the device path, computed from a host copy.
@@ -2759,17 +2778,23 @@ int finalize_small(pg_partials* pp, const pg_plan* plan, pg_result** out, const 
   const uint32_t A = plan->num_aggs, K = plan->num_keys;
   const uint64_t G = P.num_slots;
   const uint64_t b64 = G * 8ull * v.n_i64, bf = G * 8ull * v.n_f64, bmn = G * 8ull * v.n_min, bmx = G * 8ull * v.n_max;
-  uint8_t* h = (uint8_t*)t_ctx.readback.get(b64 + bf + bmn + bmx + 8);
-  if (!h) return fail(PG_E_NOMEM, "pinned readback failed");
-  HIP_CHECK(hipMemcpyAsync(h, v.i64, b64, hipMemcpyDeviceToHost, s));
-  if (bf) HIP_CHECK(hipMemcpyAsync(h + b64, v.f64, bf, hipMemcpyDeviceToHost, s));
-  if (bmn) HIP_CHECK(hipMemcpyAsync(h + b64 + bf, v.mn, bmn, hipMemcpyDeviceToHost, s));
-  if (bmx) HIP_CHECK(hipMemcpyAsync(h + b64 + bf + bmn, v.mx, bmx, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipEventRecord(e1, s));
-  HIP_CHECK(hipStreamSynchronize(s));
-  float fm = 0;
-  (void)hipEventElapsedTime(&fm, e0, e1);
-  t_timing.finalize_ms = fm;
+  uint8_t* h;
+  if (P.host_state) {  // copied back with the scan's match counts (pg_execute): no device work left
+    h = (uint8_t*)t_ctx.state_host.p;
+    t_timing.finalize_ms = 0;
+  } else {
+    h = (uint8_t*)t_ctx.readback.get(b64 + bf + bmn + bmx + 8);
+    if (!h) return fail(PG_E_NOMEM, "pinned readback failed");
+    HIP_CHECK(hipMemcpyAsync(h, v.i64, b64, hipMemcpyDeviceToHost, s));
+    if (bf) HIP_CHECK(hipMemcpyAsync(h + b64, v.f64, bf, hipMemcpyDeviceToHost, s));
+    if (bmn) HIP_CHECK(hipMemcpyAsync(h + b64 + bf, v.mn, bmn, hipMemcpyDeviceToHost, s));
+    if (bmx) HIP_CHECK(hipMemcpyAsync(h + b64 + bf + bmn, v.mx, bmx, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipEventRecord(e1, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    float fm = 0;
+    (void)hipEventElapsedTime(&fm, e0, e1);
+    t_timing.finalize_ms = fm;
+  }
   const uint64_t* i64 = (const uint64_t*)h;
   const double* f64 = (const double*)(h + b64);
   const int64_t* mn = (const int64_t*)(h + b64 + bf);
@@ -3257,7 +3282,9 @@ int pg_execute(const pg_plan* plan, pg_result** out) {
   t_prof.n = 0;
   const double t_prof_start = wall_ms();
   pg_partials* p = nullptr;
+  t_prefetch_state = true;  // the state is finalised right after: copy a small one back with the scan's counts
   int rc = pg_execute_partial(plan, &p);
+  t_prefetch_state = false;
   if (rc) return rc;
   PG_PROF("execute");
   rc = pg_partials_finalize(p, plan, out);
