@@ -25,6 +25,8 @@ CASES = [
      "GROUP BY daysSinceEpoch", False),
     ("SELECT accountId, COUNT(*), SUM(impressions) FROM adAnalytics WHERE clicks < 5 GROUP BY accountId", False),
     ("SELECT DISTINCTCOUNT(impressions), COUNT(*) FROM adAnalytics WHERE accountId < 1000", False),
+    # the config-2 query itself: selective stream + list-mode scan on each rank, dense all-reduce
+    ("CONFIG2", False),
 ]
 
 
@@ -59,7 +61,7 @@ def _worker(rank, world, port, q):
         mine = segs[rank::world]
         paths = []
         for sql, force_hash in CASES:
-            qc = parse(sql)
+            qc = parse(synth.adanalytics_query(1000) if sql == "CONFIG2" else sql)
             flags = abi.PG_PLAN_VALUE_SETS | (abi.PG_PLAN_HASH_GROUPS if force_hash else 0)
             plan = eng.make_plan(table, qc, segments=mine, flags=flags)
             p = eng.run_partial(plan)
