@@ -2293,7 +2293,9 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       static const char* ig_env = getenv("PG_STREAM_ITEM_GROUPS");  // > 0: interleaved items of this many groups
       static const char* bpc_env = getenv("PG_STREAM_BLOCKS_PER_CU");
       const uint64_t item_groups = ig_env ? (uint64_t)std::max(0, atoi(ig_env)) : 0;
-      const uint64_t per_cu = bpc_env ? (uint64_t)std::max(1, atoi(bpc_env)) : (sp.extra.empty() ? 7 : 6);
+      // blocks per CU: 7 (one resident round at 7 waves/SIMD) without further leaves; with them 12 (two rounds of the
+      // 6-wave kernel: shorter ranges balance the survivors' gathers better; config 3 stream 0.639 -> 0.622 ms)
+      const uint64_t per_cu = bpc_env ? (uint64_t)std::max(1, atoi(bpc_env)) : (sp.extra.empty() ? 7 : 12);
       const uint64_t NB = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)g_num_cus * per_cu, T / 64));
       items.clear();
       uint64_t max_groups = 0;
@@ -2350,11 +2352,12 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       sp.cap = (uint32_t)cap;
       q.num_items = (uint32_t)items.size();
       static const char* lb_env = getenv("PG_LIST_BLOCKS");
-      // list grid: ~2 048 expected survivors per block (fewer blocks = fewer flushes of the block's group table;
-      // measured: config 2 (1 M survivors) 512 blocks 0.111 ms vs 1 536 0.166 ms, config 3 (14 M) flat 1 024-1 536)
+      // list grid: ~2 048 expected survivors per block, 256..4 x CUs blocks (fewer blocks = fewer flushes of the block
+      // group tables; measured: config 2 (1 M survivors) 512 blocks 0.099 ms vs 1 536 0.166 ms; config 3 (14 M)
+      // 768-1 024 blocks 0.297 ms vs 1 536 0.333 ms: tools/stream_sweep*.sh)
       const uint64_t want = std::max<uint64_t>(256, (uint64_t)(pass * 32.0 * (double)T) / 2048);
       grid = (uint32_t)std::min<uint64_t>(items.size(), lb_env ? (uint64_t)std::max(1, atoi(lb_env))
-                                                                : std::min<uint64_t>(want, scan_grid_cap(K > 0)));
+                                                                : std::min<uint64_t>(want, (uint64_t)g_num_cus * 4));
       want_xcd = false;
       // list mode: the driving leaf is done; phase B = the AND's remaining children, all read by gathers
       q.list_mode = 1;
