@@ -83,11 +83,18 @@ __device__ __forceinline__ uint32_t unpack_win(rsrc_t r, uint32_t idx, uint32_t 
 
 // One leaf over one group for the docs in `need`: bit j <-> doc 32g + j.
 template <int B>
-__device__ __forceinline__ uint32_t eval_group(const LeafDesc& L, const uint32_t* lds_sets, uint64_t g, uint32_t need) {
+__device__ __forceinline__ uint32_t eval_group(const LeafDesc& L, const uint32_t* lds_sets, uint64_t g, uint32_t need,
+                                               bool exact = false) {
   uint32_t w[B + 1];
   load_group<B>(rsrc_of(L.words, L.wbytes), g, w);
   uint32_t m = 0;
-  if (L.kind == LK_RANGE) {
+  if (exact) {  // SET_LDS with its exact LUT over dictIds staged at lds_sets[0]
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+      const uint32_t v = value_at<B>(w, j);
+      m |= ((lds_sets[v >> 5] >> (v & 31u)) & 1u) << j;
+    }
+  } else if (L.kind == LK_RANGE) {
     const uint32_t lo = (uint32_t)L.lo, span = (uint32_t)(L.hi - L.lo);
 #pragma unroll
     for (int j = 0; j < 32; j++) m |= (uint32_t)((value_at<B>(w, j) - lo) < span) << j;
@@ -239,10 +246,12 @@ __device__ __forceinline__ uint32_t eval_extra(const LeafDesc& X, const uint32_t
 // This is SVScanDocIdIterator over the first AND child, the compacted output playing the role of its docId batches.
 // EXTRA: further AND leaves tested on the survivors (their code costs registers: 78 VGPRs / 6 waves per SIMD with,
 // 72 / 7 without).  Items: contiguous ranges per block (block_first), or with `interleave` item b + k * gridDim.x.
-template <int B, bool EXTRA>
-__global__ __launch_bounds__(256, EXTRA ? 6 : 7) void stream_kernel(StreamSpec p) {
+// NT: threads per block.  NT = 1024 is exact mode (p.exact_nwords): one block per CU holding the exact LUT.
+template <int B, bool EXTRA, int NT>
+__global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? 6 : 7)) void stream_kernel(StreamSpec p) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_sets[];
   __shared__ uint32_t cursor;
+  constexpr bool EXACT = NT == 1024;
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t i0 = p.interleave ? ldcf(p.block_first, 0) + blockIdx.x : ldcf(p.block_first, blockIdx.x);
   const uint32_t i1 = ldcf(p.block_first, p.interleave ? gridDim.x : blockIdx.x + 1);
@@ -258,12 +267,18 @@ __global__ __launch_bounds__(256, EXTRA ? 6 : 7) void stream_kernel(StreamSpec p
       seg_leaves = sd.leaves;
       L = ldcf(sd.leaves, p.leaf);
       nd = sd.num_docs;
-      if (p.set_lds_ints) {
+      if (EXACT) {
+        __syncthreads();  // every thread is done with the previous segment's LUT
+        if (L.kind == LK_SET_LDS) {
+          const uint32_t nw = ldcf(p.exact_nwords, wi.seg);
+          for (uint32_t k = tid; k < nw; k += NT) lds_sets[k] = L.lut[k];
+        }
+      } else if (p.set_lds_ints) {
         __syncthreads();  // every thread is done with the previous segment's sets
         for (uint32_t x = 0; x <= (EXTRA ? p.num_extra : 0u); x++) {
           const LeafDesc S = x ? ldcf(sd.leaves, p.extra[x - 1]) : L;
           if (S.kind != LK_SET_LDS) continue;
-          for (uint32_t k = tid; k < S.set_ints; k += 256) lds_sets[S.lds_off + k] = S.aux[k];
+          for (uint32_t k = tid; k < S.set_ints; k += NT) lds_sets[S.lds_off + k] = S.aux[k];
         }
       }
       cur_seg = wi.seg;
@@ -272,13 +287,13 @@ __global__ __launch_bounds__(256, EXTRA ? 6 : 7) void stream_kernel(StreamSpec p
     __syncthreads();  // set staged, cursor reset
     uint32_t* out = p.docs + (uint64_t)it * p.cap;
     if (L.kind != LK_NONE) {
-      for (uint32_t g0 = wi.tile_begin; g0 < wi.tile_end; g0 += 256) {
+      for (uint32_t g0 = wi.tile_begin; g0 < wi.tile_end; g0 += NT) {
         const uint32_t g = g0 + tid;
         const uint64_t d0 = (uint64_t)g * 32;
         uint32_t m = 0;
         if (g < wi.tile_end && d0 < nd) {
           const uint32_t valid = d0 + 32 <= nd ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (32u - (uint32_t)(nd - d0)));
-          uint32_t r = eval_group<B>(L, lds_sets, g, valid);
+          uint32_t r = eval_group<B>(L, lds_sets, g, valid, EXACT && L.kind == LK_SET_LDS);
           if (L.excl) r = ~r;
           m = r & valid;
         }
@@ -315,12 +330,24 @@ __global__ __launch_bounds__(256, EXTRA ? 6 : 7) void stream_kernel(StreamSpec p
 
 hipError_t launch_stream(const StreamSpec& p, uint32_t bits, uint32_t blocks, hipStream_t s) {
   if (!p.num_items || !blocks) return hipSuccess;
-  const size_t lds = (size_t)p.set_lds_ints * 4;
+  const size_t lds = p.exact_nwords ? (size_t)128 * 1024 : (size_t)p.set_lds_ints * 4;
+  if (p.exact_nwords) {
+    static bool attr = false;  // >64 KiB of dynamic LDS must be opted into per kernel (once per process)
+    if (!attr) {
+#define PG_A(b) (void)hipFuncSetAttribute((const void*)stream_kernel<b, false, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+      PG_A(1) PG_A(2) PG_A(3) PG_A(4) PG_A(5) PG_A(6) PG_A(7) PG_A(8) PG_A(9) PG_A(10) PG_A(11) PG_A(12) PG_A(13)
+      PG_A(14) PG_A(15) PG_A(16) PG_A(17) PG_A(18) PG_A(19) PG_A(20) PG_A(21) PG_A(22) PG_A(23) PG_A(24) PG_A(25)
+      PG_A(26) PG_A(27) PG_A(28) PG_A(29) PG_A(30) PG_A(31) PG_A(32)
+#undef PG_A
+      attr = true;
+    }
+  }
   switch (bits) {
-#define PG_B(b)                                                                                \
-  case b:                                                                                      \
-    if (p.num_extra) hipLaunchKernelGGL((stream_kernel<b, true>), dim3(blocks), dim3(256), lds, s, p); \
-    else hipLaunchKernelGGL((stream_kernel<b, false>), dim3(blocks), dim3(256), lds, s, p);           \
+#define PG_B(b)                                                                                              \
+  case b:                                                                                                    \
+    if (p.exact_nwords) hipLaunchKernelGGL((stream_kernel<b, false, 1024>), dim3(blocks), dim3(1024), lds, s, p); \
+    else if (p.num_extra) hipLaunchKernelGGL((stream_kernel<b, true, 256>), dim3(blocks), dim3(256), lds, s, p); \
+    else hipLaunchKernelGGL((stream_kernel<b, false, 256>), dim3(blocks), dim3(256), lds, s, p);                \
     break;
     PG_B(1) PG_B(2) PG_B(3) PG_B(4) PG_B(5) PG_B(6) PG_B(7) PG_B(8) PG_B(9) PG_B(10) PG_B(11) PG_B(12) PG_B(13)
     PG_B(14) PG_B(15) PG_B(16) PG_B(17) PG_B(18) PG_B(19) PG_B(20) PG_B(21) PG_B(22) PG_B(23) PG_B(24) PG_B(25)

@@ -303,6 +303,9 @@ struct StreamSpec {
   uint32_t* docs;                 // [num_items][cap]
   uint32_t* counts;               // [num_items] survivors written (<= cap)
   unsigned int* err;              // bit 3: some item had more than `cap` survivors
+  // exact mode (1 024-thread blocks, one per CU): a coarse IN bitmap's exact LUT (exact_nwords[seg] words, <= 128 KiB)
+  // is staged whole in LDS, so no value is a candidate to resolve
+  const uint32_t* exact_nwords;
 };
 hipError_t launch_stream(const StreamSpec& p, uint32_t bits, uint32_t blocks, hipStream_t s);
 

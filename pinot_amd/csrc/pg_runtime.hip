@@ -2243,6 +2243,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     bool on = false;
     uint32_t leaf = 0, cap = 0;
     bool interleave = false;      // items dealt round-robin to the blocks (PG_STREAM_ITEM_GROUPS)
+    bool exact = false;           // exact mode: the driving IN leaf's exact LUT staged in LDS (1 024-thread blocks)
+    std::vector<uint32_t> exact_nwords;  // [seg] LUT words
     uint32_t set_ints = 0;        // LDS IN-set words of the streamed leaves
     std::vector<uint32_t> extra;  // further AND children tested in the stream (runtime bit width)
     std::vector<StreamLaunch> launches;
@@ -2295,7 +2297,19 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       const uint64_t item_groups = ig_env ? (uint64_t)std::max(0, atoi(ig_env)) : 0;
       // blocks per CU: 7 (one resident round at 7 waves/SIMD) without further leaves; with them 12 (two rounds of the
       // 6-wave kernel: shorter ranges balance the survivors' gathers better; config 3 stream 0.639 -> 0.622 ms)
-      const uint64_t per_cu = bpc_env ? (uint64_t)std::max(1, atoi(bpc_env)) : (sp.extra.empty() ? 7 : 12);
+      // exact mode (PG_STREAM_EXACT=0 disables): a coarse IN bitmap whose exact LUT fits 128 KiB of LDS is tested
+      // exactly by 1 024-thread blocks, one per CU, instead of resolving the coarse bitmap's candidates by global reads
+      static const char* ex_env = getenv("PG_STREAM_EXACT");
+      sp.exact = sp.extra.empty() && !(ex_env && atoi(ex_env) == 0);
+      sp.exact_nwords.assign(S, 0);
+      for (uint32_t si = 0; si < S && sp.exact; si++) {
+        if (!seg_groups[si]) continue;
+        const LeafDesc& dl = leaves[(uint64_t)si * L + li];
+        const ColumnRes* c = col(si, plan->segments[si].leaves[li].col_id);
+        sp.exact = dl.kind == LK_SET_LDS && dl.shift > 0 && !dl.excl && c && (c->card + 31) / 32 <= 32768u;  // shift > 0: its exact LUT exists
+        if (sp.exact) sp.exact_nwords[si] = (c->card + 31) / 32;
+      }
+      const uint64_t per_cu = sp.exact ? 1 : bpc_env ? (uint64_t)std::max(1, atoi(bpc_env)) : (sp.extra.empty() ? 7 : 12);
       const uint64_t NB = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)g_num_cus * per_cu, T / 64));
       items.clear();
       uint64_t max_groups = 0;
@@ -2471,6 +2485,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   }
   const uint64_t off_items = ar.put(items.data(), items.size() * sizeof(WorkItem));
   for (StreamLaunch& sl : sp.launches) sl.first_off = ar.put(sl.first.data(), sl.first.size() * 4);
+  const uint64_t off_exact = sp.exact ? ar.put(sp.exact_nwords.data(), 4ull * S) : 0;
   // GM_PART: each block's region of the entry array = the docs of its items (the kernel's [i0, i1) item range)
   uint64_t off_part_base = 0, part_entries = 0;
   if (part.on && blocks) {
@@ -2585,6 +2600,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     ss.leaf = sp.leaf;
     ss.cap = sp.cap;
     ss.num_extra = (uint32_t)sp.extra.size();
+    ss.exact_nwords = sp.exact ? (const uint32_t*)(dA + off_exact) : nullptr;
     ss.interleave = sp.interleave ? 1u : 0u;
     for (size_t x = 0; x < sp.extra.size(); x++) ss.extra[x] = sp.extra[x];
     ss.set_lds_ints = sp.set_ints;
