@@ -249,7 +249,9 @@ def main():
                          "kernel": "stream_kernel + scan_kernel" if tm.scan_launches > 1 else "scan_kernel",
                          "kernel_ms": scan_avg_ms,
                          "algorithmic_bytes": alg_bytes,
-                         "traffic_bytes_per_launch": traffic_bytes},
+                         "traffic_bytes_per_launch": traffic_bytes,
+                         # the bytes actually moved (PMC) over the same time: below `frac` when the AND short-circuits
+                         "traffic_frac": traffic / HBM_PEAK_GBS if traffic is not None else None},
             "cpu_baseline": cpu,
             "parity_sample": parity,
             "step_breakdown_ms": {k: round(float(np.mean(v)), 4) for k, v in parts.items()},
