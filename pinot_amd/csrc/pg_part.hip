@@ -27,7 +27,15 @@
 
 namespace pg {
 
-constexpr uint32_t kSplitChunk = 4096;  // entries counting-sorted per LDS round (16 per thread): longer runs per digit
+#ifndef PG_SPLIT_CHUNK
+#define PG_SPLIT_CHUNK 16384
+#endif
+#ifndef PG_SPLIT_THREADS
+#define PG_SPLIT_THREADS 1024
+#endif
+constexpr uint32_t kST = PG_SPLIT_THREADS;  // threads of a split block
+constexpr uint32_t kSplitChunk = PG_SPLIT_CHUNK;  // entries counting-sorted per LDS round (16 per thread): longer runs per digit
+// (16 384 x 1 024 threads, one block per CU: split1 4.08 -> 3.10 ms, split2 2.71 -> 2.15 ms on config 4 vs 4 096 x 256)
 
 // Entries of level-1 partition p handled by level-2 block j (of kPartNB): [lo, hi).
 __device__ __forceinline__ void l2_range(const PartSpec& P, uint32_t p, uint32_t j, uint64_t& lo, uint64_t& hi) {
@@ -43,19 +51,19 @@ __device__ __forceinline__ uint32_t digit2(const PartSpec& P, uint32_t e) {
 }
 
 // One LDS counting-sort round: the block's `n` (<= kSplitChunk) entries `e[k]` with digits `dg[k]` (thread t holds
-// chunk entries t + 256k) go to out[cur[digit]++] as one run per digit.  cur[] = the block's next output position per
+// chunk entries t + kST k) go to out[cur[digit]++] as one run per digit.  cur[] = the block's next output position per
 // digit (LDS, advanced here).  LDS: cnt/start [ndig] + sorted entries + their digits.
 template <class Out>
-__device__ __forceinline__ void split_round(uint32_t (&e)[kSplitChunk / 256], uint32_t (&dg)[kSplitChunk / 256],
+__device__ __forceinline__ void split_round(uint32_t (&e)[kSplitChunk / kST], uint32_t (&dg)[kSplitChunk / kST],
                                             uint32_t n, uint32_t ndig, uint32_t* cnt, uint32_t* start,
                                             unsigned long long* cur, uint32_t* sbuf, uint8_t* sdig, Out* out) {
-  constexpr int E = kSplitChunk / 256;
+  constexpr int E = kSplitChunk / kST;
   const uint32_t tid = threadIdx.x;
   uint32_t rank[E];
 #pragma unroll
-  for (int k = 0; k < E; k++) rank[k] = tid + 256u * k < n ? atomicAdd(&cnt[dg[k]], 1u) : 0u;
+  for (int k = 0; k < E; k++) rank[k] = tid + kST * k < n ? atomicAdd(&cnt[dg[k]], 1u) : 0u;
   __syncthreads();
-  // exclusive scan of cnt over the digits (ndig <= 256: one per thread) -> start; reserve the runs
+  // exclusive scan of cnt over the digits (ndig <= 256 <= kST: one per thread) -> start; reserve the runs
   {
     uint32_t c = tid < ndig ? cnt[tid] : 0u, x = c;
     const uint32_t lane = tid & 63u, wave = tid >> 6;
@@ -64,7 +72,7 @@ __device__ __forceinline__ void split_round(uint32_t (&e)[kSplitChunk / 256], ui
       const uint32_t y = __shfl_up(x, o);
       if (lane >= (uint32_t)o) x += y;
     }
-    __shared__ uint32_t wsum[4];
+    __shared__ uint32_t wsum[kST / 64];
     if (lane == 63) wsum[wave] = x;
     __syncthreads();
     uint32_t wb = 0;
@@ -77,13 +85,13 @@ __device__ __forceinline__ void split_round(uint32_t (&e)[kSplitChunk / 256], ui
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < E; k++)
-    if (tid + 256u * k < n) {
+    if (tid + kST * k < n) {
       const uint32_t at = start[dg[k]] + rank[k];
       sbuf[at] = e[k];
       sdig[at] = (uint8_t)dg[k];
     }
   __syncthreads();
-  for (uint32_t i = tid; i < n; i += 256) {
+  for (uint32_t i = tid; i < n; i += kST) {
     const uint32_t d = sdig[i];
     out[cur[d] + (i - start[d])] = (Out)sbuf[i];
   }
@@ -94,11 +102,11 @@ __device__ __forceinline__ void split_round(uint32_t (&e)[kSplitChunk / 256], ui
 }
 
 // Level 1: scan block b's entries -> level-1 partitions (its range of each starts at off1[p * blocks1 + b]).
-__global__ __launch_bounds__(256) void part_split1_kernel(PartSpec P) {
-  constexpr int E = kSplitChunk / 256;
+__global__ __launch_bounds__(kST) void part_split1_kernel(PartSpec P) {
+  constexpr int E = kSplitChunk / kST;
   __shared__ uint32_t cnt[kPartL1], start[kPartL1], sbuf[kSplitChunk];
   __shared__ unsigned long long cur[kPartL1];
-  __shared__ uint8_t sdig[kSplitChunk];  // digits < 256: 4 KB, so 6 blocks fit a CU (the scan grid is 6 per CU)
+  __shared__ uint8_t sdig[kSplitChunk];  // digits < 256: one byte each
   const uint32_t b = blockIdx.x, tid = threadIdx.x;
   if (tid < P.nparts1) {
     cnt[tid] = 0;
@@ -114,7 +122,7 @@ __global__ __launch_bounds__(256) void part_split1_kernel(PartSpec P) {
     uint32_t e[E], dg[E];
 #pragma unroll
     for (int k = 0; k < E; k++) {
-      const uint32_t i = tid + 256u * k;
+      const uint32_t i = tid + kST * k;
       const uint64_t x = i < m ? in[c0 + i] : 0ull;
       dg[k] = (uint32_t)(x >> sh);
       e[k] = (uint32_t)((((x >> P.vbits) & lmask) << P.vbits) | (x & vmask));
@@ -146,11 +154,11 @@ __global__ __launch_bounds__(256) void part_count2_kernel(PartSpec P) {
 }
 
 // Level 2: the same ranges, counting-sorted by level-2 digit into buckets (bucket p * nparts2 + d).
-__global__ __launch_bounds__(256) void part_split2_kernel(PartSpec P) {
-  constexpr int E = kSplitChunk / 256;
+__global__ __launch_bounds__(kST) void part_split2_kernel(PartSpec P) {
+  constexpr int E = kSplitChunk / kST;
   __shared__ uint32_t cnt[256], start[256], sbuf[kSplitChunk];
   __shared__ unsigned long long cur[256];
-  __shared__ uint8_t sdig[kSplitChunk];  // digits < 256: 4 KB, so 6 blocks fit a CU (the scan grid is 6 per CU)
+  __shared__ uint8_t sdig[kSplitChunk];  // digits < 256: one byte each
   const uint32_t j = blockIdx.x, p = blockIdx.y, tid = threadIdx.x;
   if (tid < P.nparts2) {
     cnt[tid] = 0;
@@ -165,7 +173,7 @@ __global__ __launch_bounds__(256) void part_split2_kernel(PartSpec P) {
     uint32_t e[E], dg[E];
 #pragma unroll
     for (int k = 0; k < E; k++) {
-      const uint32_t i = tid + 256u * k;
+      const uint32_t i = tid + kST * k;
       e[k] = i < m ? in[c0 + i] : 0u;
       dg[k] = digit2(P, e[k]);
     }
@@ -223,7 +231,7 @@ __global__ __launch_bounds__(256) void part_aggregate_kernel(PartSpec P) {
 }
 
 hipError_t launch_part_split1(const PartSpec& p, hipStream_t s) {
-  hipLaunchKernelGGL(part_split1_kernel, dim3(p.blocks1), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(part_split1_kernel, dim3(p.blocks1), dim3(kST), 0, s, p);
   return hipGetLastError();
 }
 hipError_t launch_part_count2(const PartSpec& p, hipStream_t s) {
@@ -231,7 +239,7 @@ hipError_t launch_part_count2(const PartSpec& p, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_part_split2(const PartSpec& p, hipStream_t s) {
-  hipLaunchKernelGGL(part_split2_kernel, dim3(kPartNB, p.nparts1), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(part_split2_kernel, dim3(kPartNB, p.nparts1), dim3(kST), 0, s, p);
   return hipGetLastError();
 }
 hipError_t launch_part_aggregate(const PartSpec& p, hipStream_t s) {

@@ -98,6 +98,19 @@ def test_cancel_from_another_thread(gpu_engine, long_scan):
     plan.plan.query_id = 0
 
 
+def test_partitioned_group_by_matches_atomic_at_scale(gpu_engine, long_scan):
+    """The radix-partitioned group-by (pg_part.hip) over the same 192 M rows gives the per-doc atomic path's result:
+    at this size every split block runs many LDS counting-sort rounds (the small parity cases run one partial round)."""
+    import os
+    plan, ref, full = long_scan
+    os.environ["PG_PART"] = "1"
+    try:
+        res = gpu_engine.run_plan(plan)
+    finally:
+        os.environ["PG_PART"] = "0"
+    assert res.rows == ref.rows
+
+
 def test_concurrent_executes_from_two_threads(gpu_engine, oracle_engine, sv_table_inter):
     """Two host threads, each with its own stream and parameter arena, run different queries at once; every result
     matches the oracle."""
