@@ -34,6 +34,13 @@ namespace pg {
 #define PG_SPLIT_THREADS 1024
 #endif
 constexpr uint32_t kST = PG_SPLIT_THREADS;  // threads of a split block
+#ifndef PG_SPLIT2_DIG
+#define PG_SPLIT2_DIG 0
+#endif
+#ifndef PG_AGG_THREADS
+#define PG_AGG_THREADS 1024
+#endif
+constexpr uint32_t kAT = PG_AGG_THREADS;  // threads of a part_aggregate block
 constexpr uint32_t kSplitChunk = PG_SPLIT_CHUNK;  // entries counting-sorted per LDS round (16 per thread): longer runs per digit
 // (16 384 x 1 024 threads, one block per CU: split1 4.08 -> 3.10 ms, split2 2.71 -> 2.15 ms on config 4 vs 4 096 x 256)
 
@@ -53,10 +60,12 @@ __device__ __forceinline__ uint32_t digit2(const PartSpec& P, uint32_t e) {
 // One LDS counting-sort round: the block's `n` (<= kSplitChunk) entries `e[k]` with digits `dg[k]` (thread t holds
 // chunk entries t + kST k) go to out[cur[digit]++] as one run per digit.  cur[] = the block's next output position per
 // digit (LDS, advanced here).  LDS: cnt/start [ndig] + sorted entries + their digits.
-template <class Out>
+// DIG = false: the digit is recomputable from the sorted entry itself, (e >> dsh) & (ndig - 1), so sdig is not used.
+template <class Out, bool DIG>
 __device__ __forceinline__ void split_round(uint32_t (&e)[kSplitChunk / kST], uint32_t (&dg)[kSplitChunk / kST],
                                             uint32_t n, uint32_t ndig, uint32_t* cnt, uint32_t* start,
-                                            unsigned long long* cur, uint32_t* sbuf, uint8_t* sdig, Out* out) {
+                                            unsigned long long* cur, uint32_t* sbuf, uint8_t* sdig, Out* out,
+                                            uint32_t dsh = 0) {
   constexpr int E = kSplitChunk / kST;
   const uint32_t tid = threadIdx.x;
   uint32_t rank[E];
@@ -88,12 +97,13 @@ __device__ __forceinline__ void split_round(uint32_t (&e)[kSplitChunk / kST], ui
     if (tid + kST * k < n) {
       const uint32_t at = start[dg[k]] + rank[k];
       sbuf[at] = e[k];
-      sdig[at] = (uint8_t)dg[k];
+      if (DIG) sdig[at] = (uint8_t)dg[k];
     }
   __syncthreads();
   for (uint32_t i = tid; i < n; i += kST) {
-    const uint32_t d = sdig[i];
-    out[cur[d] + (i - start[d])] = (Out)sbuf[i];
+    const uint32_t x = sbuf[i];
+    const uint32_t d = DIG ? (uint32_t)sdig[i] : (x >> dsh) & (ndig - 1u);
+    out[cur[d] + (i - start[d])] = (Out)x;
   }
   __syncthreads();
   // advance the cursors by this round's run lengths (start[d+1] - start[d])
@@ -127,7 +137,7 @@ __global__ __launch_bounds__(kST) void part_split1_kernel(PartSpec P) {
       dg[k] = (uint32_t)(x >> sh);
       e[k] = (uint32_t)((((x >> P.vbits) & lmask) << P.vbits) | (x & vmask));
     }
-    split_round(e, dg, m, P.nparts1, cnt, start, cur, sbuf, sdig, P.in1);
+    split_round<uint32_t, true>(e, dg, m, P.nparts1, cnt, start, cur, sbuf, sdig, P.in1);
   }
 }
 
@@ -158,7 +168,7 @@ __global__ __launch_bounds__(kST) void part_split2_kernel(PartSpec P) {
   constexpr int E = kSplitChunk / kST;
   __shared__ uint32_t cnt[256], start[256], sbuf[kSplitChunk];
   __shared__ unsigned long long cur[256];
-  __shared__ uint8_t sdig[kSplitChunk];  // digits < 256: one byte each
+  __shared__ uint8_t sdig[PG_SPLIT2_DIG ? kSplitChunk : 1];  // the digit is recomputed from the entry when !PG_SPLIT2_DIG
   const uint32_t j = blockIdx.x, p = blockIdx.y, tid = threadIdx.x;
   if (tid < P.nparts2) {
     cnt[tid] = 0;
@@ -177,29 +187,29 @@ __global__ __launch_bounds__(kST) void part_split2_kernel(PartSpec P) {
       e[k] = i < m ? in[c0 + i] : 0u;
       dg[k] = digit2(P, e[k]);
     }
-    split_round(e, dg, m, P.nparts2, cnt, start, cur, sbuf, sdig, P.out2);
+    split_round<uint32_t, PG_SPLIT2_DIG>(e, dg, m, P.nparts2, cnt, start, cur, sbuf, sdig, P.out2, P.vbits + P.shift2);
   }
 }
 
 // One workgroup per bucket b (groups g = b << shift2 | gl): doc count and value bitmap of each group in LDS, then the
 // bucket's slice of the dense state (i64 slot 0 = doc count, the bitmap row) written whole.
-__global__ __launch_bounds__(256) void part_aggregate_kernel(PartSpec P) {
+__global__ __launch_bounds__(kAT) void part_aggregate_kernel(PartSpec P) {
   extern __shared__ uint32_t lds[];
   const uint32_t b = blockIdx.x, tid = threadIdx.x;
   const uint32_t ng = 1u << P.shift2, dw = P.dc_words;
   uint32_t* cnt = lds;        // [ng]
   uint32_t* bm = lds + ng;    // [ng][dw]
-  for (uint32_t i = tid; i < ng * (1u + dw); i += 256) lds[i] = 0;
+  for (uint32_t i = tid; i < ng * (1u + dw); i += kAT) lds[i] = 0;
   __syncthreads();
   const uint64_t lo = P.off2[(uint64_t)b * kPartNB], hi = P.off2[(uint64_t)(b + 1) * kPartNB];
   const uint32_t gm = ng - 1u, vm = (1u << P.vbits) - 1u, vb = P.vbits;
   const uint32_t* __restrict__ in = P.out2;
   uint64_t i = lo + tid;
   if (dw) {
-    for (; i + 768 < hi; i += 1024) {  // four independent loads in flight per lane
+    for (; i + 3 * kAT < hi; i += 4 * kAT) {  // four independent loads in flight per lane
       uint32_t e[4];
 #pragma unroll
-      for (int k = 0; k < 4; k++) e[k] = in[i + 256 * k];
+      for (int k = 0; k < 4; k++) e[k] = in[i + kAT * k];
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const uint32_t g = (e[k] >> vb) & gm, v = e[k] & vm;
@@ -207,23 +217,23 @@ __global__ __launch_bounds__(256) void part_aggregate_kernel(PartSpec P) {
         atomicOr(&bm[g * dw + (v >> 5)], 1u << (v & 31u));
       }
     }
-    for (; i < hi; i += 256) {
+    for (; i < hi; i += kAT) {
       const uint32_t e = in[i];
       const uint32_t g = (e >> vb) & gm, v = e & vm;
       atomicAdd(&cnt[g], 1u);
       atomicOr(&bm[g * dw + (v >> 5)], 1u << (v & 31u));
     }
   } else {
-    for (; i < hi; i += 256) atomicAdd(&cnt[(in[i] >> vb) & gm], 1u);
+    for (; i < hi; i += kAT) atomicAdd(&cnt[(in[i] >> vb) & gm], 1u);
   }
   __syncthreads();
   const uint64_t g0 = (uint64_t)b << P.shift2;
   const uint32_t n = (uint32_t)(g0 + ng <= P.num_groups ? ng : (g0 < P.num_groups ? P.num_groups - g0 : 0));
-  for (uint32_t gl = tid; gl < n; gl += 256) P.i64[(g0 + gl) * P.n_i64] = cnt[gl];
+  for (uint32_t gl = tid; gl < n; gl += kAT) P.i64[(g0 + gl) * P.n_i64] = cnt[gl];
   if (P.row_words) {
     const uint32_t rw = P.row_words;
     uint32_t* __restrict__ dst = P.bits + g0 * rw;
-    for (uint32_t w = tid; w < n * rw; w += 256) {
+    for (uint32_t w = tid; w < n * rw; w += kAT) {
       const uint32_t gl = w / rw, k = w - gl * rw;
       dst[w] = (k >= P.dc_word && k < P.dc_word + dw) ? bm[gl * dw + (k - P.dc_word)] : 0u;
     }
@@ -244,7 +254,7 @@ hipError_t launch_part_split2(const PartSpec& p, hipStream_t s) {
 }
 hipError_t launch_part_aggregate(const PartSpec& p, hipStream_t s) {
   const size_t lds = (size_t)(1u << p.shift2) * (1u + p.dc_words) * 4u;
-  hipLaunchKernelGGL(part_aggregate_kernel, dim3(p.nparts1 * p.nparts2), dim3(256), lds, s, p);
+  hipLaunchKernelGGL(part_aggregate_kernel, dim3(p.nparts1 * p.nparts2), dim3(kAT), lds, s, p);
   return hipGetLastError();
 }
 
