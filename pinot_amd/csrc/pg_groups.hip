@@ -70,16 +70,19 @@ hipError_t launch_exclusive_sum(const uint64_t* in, uint64_t* out, uint64_t n, v
   return hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n, s);
 }
 
-size_t sort_temp_bytes(uint64_t n) {
+size_t sort_temp_bytes(uint64_t n, uint32_t begin_bit, uint32_t end_bit) {
   size_t t = 0;
   hipcub::DeviceRadixSort::SortPairs(nullptr, t, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                     (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+                                     (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, (int)begin_bit, (int)end_bit);
   return t + 256;
 }
 
+// Stable LSD radix sort of (key, pos) pairs on key bits [begin_bit, end_bit): when the other bits are equal in every
+// key (order_keys_kernel's span) the order is the full-width sort's, in fewer passes.
 hipError_t launch_sort_pairs(const uint64_t* kin, uint64_t* kout, const uint32_t* vin, uint32_t* vout, uint64_t n,
-                             void* temp, size_t temp_bytes, hipStream_t s) {
-  return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, kin, kout, vin, vout, (int)n, 0, 64, s);
+                             void* temp, size_t temp_bytes, hipStream_t s, uint32_t begin_bit, uint32_t end_bit) {
+  return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, kin, kout, vin, vout, (int)n, (int)begin_bit,
+                                            (int)end_bit, s);
 }
 
 // ------------------------------------------------------------------------------------------ finalisation
@@ -174,8 +177,9 @@ hipError_t launch_final_values(const StateView& v, const FinalSpec& f, const uin
 // Ascending u64 image of the first ORDER BY item (DESC = bit complement), for the radix-sort trim.
 __global__ void order_keys_kernel(FinalSpec f, const uint64_t* __restrict__ keys, const double* __restrict__ vals,
                                   const int64_t* __restrict__ cnts, uint64_t n, uint64_t* __restrict__ out,
-                                  uint32_t* __restrict__ pos) {
+                                  uint32_t* __restrict__ pos, unsigned long long* __restrict__ span) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t any = 0, anyz = 0;  // OR of the keys, OR of their complements
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     uint64_t o;
     if (f.order_kind == PG_ORDER_KEY) {
@@ -191,17 +195,39 @@ __global__ void order_keys_kernel(FinalSpec f, const uint64_t* __restrict__ keys
       __builtin_memcpy(&b, &x, 8);
       o = b >= 0 ? ((uint64_t)b | 0x8000000000000000ull) : ~(uint64_t)b;
     }
-    out[i] = f.order_desc ? ~o : o;
+    o = f.order_desc ? ~o : o;
+    out[i] = o;
     pos[i] = (uint32_t)i;
+    any |= o;
+    anyz |= ~o;
+  }
+  if (!span) return;
+  // block ORs -> one global atomic pair per block (the grid is capped, so a few thousand per launch)
+  for (int d = 1; d < 64; d <<= 1) {
+    any |= __shfl_xor(any, d);
+    anyz |= __shfl_xor(anyz, d);
+  }
+  __shared__ unsigned long long wa[4], wb[4];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  if (lane == 0) { wa[w] = any; wb[w] = anyz; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t k = 1; k < (blockDim.x >> 6); k++) { any |= wa[k]; anyz |= wb[k]; }
+    atomicOr(&span[0], (unsigned long long)any);
+    atomicOr(&span[1], (unsigned long long)anyz);
   }
 }
 
 hipError_t launch_order_keys(const FinalSpec& f, const uint64_t* keys, const double* vals, const int64_t* cnts,
-                             uint64_t n, uint64_t* out, uint32_t* pos, hipStream_t s) {
+                             uint64_t n, uint64_t* out, uint32_t* pos, hipStream_t s, uint64_t* span) {
   if (!n) return hipSuccess;
-  const uint64_t blocks = (n + 255) / 256;
-  hipLaunchKernelGGL(order_keys_kernel, dim3((uint32_t)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, s, f, keys,
-                     vals, cnts, n, out, pos);
+  const uint64_t blocks = (n + 255) / 256, cap = span ? 2048 : 16384;
+  if (span) {
+    const hipError_t e = hipMemsetAsync(span, 0, 16, s);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(order_keys_kernel, dim3((uint32_t)(blocks < cap ? blocks : cap)), dim3(256), 0, s, f, keys,
+                     vals, cnts, n, out, pos, (unsigned long long*)span);
   return hipGetLastError();
 }
 

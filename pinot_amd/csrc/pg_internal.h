@@ -360,7 +360,7 @@ struct FinalSpec {            // what finalisation needs of the plan
 };
 enum SelectKind : uint32_t { SEL_PRESENT = 0, SEL_OCCUPIED = 1, SEL_PRESENT_PART = 2 };
 size_t select_temp_bytes(uint64_t n);
-size_t sort_temp_bytes(uint64_t n);
+size_t sort_temp_bytes(uint64_t n, uint32_t begin_bit = 0, uint32_t end_bit = 64);
 uint64_t row_bytes(const StateView& v);
 hipError_t launch_select_slots(const StateView& v, uint32_t kind, uint32_t part, uint32_t parts, uint32_t* out,
                                uint32_t* d_num, void* temp, size_t temp_bytes, hipStream_t s);
@@ -369,11 +369,13 @@ hipError_t launch_select_flagged(const uint32_t* in, const uint8_t* flags, uint6
 hipError_t launch_exclusive_sum(const uint64_t* in, uint64_t* out, uint64_t n, void* temp, size_t temp_bytes,
                                 hipStream_t s);
 hipError_t launch_sort_pairs(const uint64_t* kin, uint64_t* kout, const uint32_t* vin, uint32_t* vout, uint64_t n,
-                             void* temp, size_t temp_bytes, hipStream_t s);
+                             void* temp, size_t temp_bytes, hipStream_t s, uint32_t begin_bit = 0, uint32_t end_bit = 64);
 hipError_t launch_final_values(const StateView& v, const FinalSpec& f, const uint32_t* slots, uint64_t n,
                                uint64_t* keys, double* vals, int64_t* cnts, hipStream_t s);
+// span (optional, 2 words, set here): the OR of every order key and the OR of their complements; the bits set in
+// both differ between keys, the others are equal in all of them and the sort can skip them
 hipError_t launch_order_keys(const FinalSpec& f, const uint64_t* keys, const double* vals, const int64_t* cnts,
-                             uint64_t n, uint64_t* out, uint32_t* pos, hipStream_t s);
+                             uint64_t n, uint64_t* out, uint32_t* pos, hipStream_t s, uint64_t* span = nullptr);
 hipError_t launch_cutoff(const uint64_t* sorted, uint64_t n, uint64_t limit, uint64_t* out, hipStream_t s);
 hipError_t launch_gather_final(uint32_t A, const uint32_t* pos, uint64_t n, const uint64_t* keys, const double* vals,
                                const int64_t* cnts, const uint32_t* slots, uint64_t* okeys, double* ovals,

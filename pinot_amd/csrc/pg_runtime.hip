@@ -1141,6 +1141,11 @@ struct Scratch {
   }
 };
 
+// OR of the order keys and OR of their complements (order_keys_kernel's span)
+struct KeySpan {
+  uint64_t any, anyz;
+};
+
 // Copy one device value to the host (synchronous on s).
 template <class T> int read_back(const T* d, T& h, hipStream_t s) {
   HIP_CHECK(hipMemcpyAsync(&h, d, sizeof(T), hipMemcpyDeviceToHost, s));
@@ -2949,16 +2954,24 @@ int finalize(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   const int64_t* cc = dcnts;
   const uint32_t* cs = slots;
   if (K && plan->num_order && plan->limit && n > plan->limit) {
-    const size_t tb = sort_temp_bytes(n);
     uint64_t* okeys = sc.get<uint64_t>(n, rc);
     uint64_t* skeys = sc.get<uint64_t>(n, rc);
     uint32_t* pos = sc.get<uint32_t>(n, rc);
     uint32_t* spos = sc.get<uint32_t>(n, rc);
     uint64_t* d_nc = sc.get<uint64_t>(1, rc);
+    KeySpan* d_span = sc.get<KeySpan>(1, rc);
+    if (rc) return rc;
+    // the sort covers only the key bits that differ between groups (config 4: a DISTINCTCOUNT <= 1 000 varies in
+    // 21 of the double image's 64 bits: 3 radix passes instead of 8)
+    HIP_CHECK(launch_order_keys(f, dkeys, dvals, dcnts, n, okeys, pos, s, (uint64_t*)d_span));
+    KeySpan span{};
+    if ((rc = read_back(d_span, span, s))) return rc;
+    const uint64_t diff = span.any & span.anyz;
+    const uint32_t b0 = diff ? (uint32_t)__builtin_ctzll(diff) : 0u, b1 = diff ? 64u - (uint32_t)__builtin_clzll(diff) : 1u;
+    const size_t tb = sort_temp_bytes(n, b0, b1);
     void* temp = sc.get<uint8_t>(tb, rc);
     if (rc) return rc;
-    HIP_CHECK(launch_order_keys(f, dkeys, dvals, dcnts, n, okeys, pos, s));
-    HIP_CHECK(launch_sort_pairs(okeys, skeys, pos, spos, n, temp, tb, s));
+    HIP_CHECK(launch_sort_pairs(okeys, skeys, pos, spos, n, temp, tb, s, b0, b1));
     HIP_CHECK(launch_cutoff(skeys, n, plan->limit, d_nc, s));
     if ((rc = read_back(d_nc, nc, s))) return rc;
     uint64_t* gk = sc.get<uint64_t>(nc, rc);
