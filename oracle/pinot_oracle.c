@@ -567,6 +567,48 @@ static uint64_t sort_unique_u64(uint64_t *a, uint64_t n) {
   return u;
 }
 
+/* ArrayMapBasedHolder (DictionaryBasedGroupKeyGenerator.java:777-860): when the product of the key cardinalities
+ * overflows a long (:117-131), the raw key is the array of the K dictIds (IntArray) and an Object2IntOpenHashMap
+ * assigns group ids in first-seen doc order, INVALID_ID once numGroupsLimit groups exist (getGroupId :812-819).
+ * Open addressing over tuples stored row-major in `tuples` ([n][K], grown with the map). */
+typedef struct { int32_t *tuples; int32_t *slots; uint64_t cap, n, tcap; uint32_t K; } tuple_map;
+static uint64_t tuple_hash(const int32_t *t, uint32_t K) {
+  uint64_t h = 0x9e3779b97f4a7c15ULL;
+  for (uint32_t k = 0; k < K; k++) h = mix64(h ^ ((uint64_t)(uint32_t)t[k] + 0x632be59bd9b4e019ULL * (k + 1)));
+  return h;
+}
+static int32_t tuple_get_or_put(tuple_map *m, const int32_t *t, uint64_t limit) {
+  uint64_t mask = m->cap - 1, h = tuple_hash(t, m->K) & mask;
+  while (m->slots[h] >= 0) {
+    if (!memcmp(&m->tuples[(uint64_t)m->slots[h] * m->K], t, 4ull * m->K)) return m->slots[h];
+    h = (h + 1) & mask;
+  }
+  if (m->n >= limit) return -1;
+  if ((m->n + 1) * 2 > m->cap) {  /* grow the slot table; ids index the tuple rows and do not move */
+    uint64_t nc = m->cap * 2;
+    int32_t *ns = (int32_t *)malloc(nc * 4);
+    for (uint64_t i = 0; i < nc; i++) ns[i] = -1;
+    for (uint64_t g = 0; g < m->n; g++) {
+      uint64_t hh = tuple_hash(&m->tuples[g * m->K], m->K) & (nc - 1);
+      while (ns[hh] >= 0) hh = (hh + 1) & (nc - 1);
+      ns[hh] = (int32_t)g;
+    }
+    free(m->slots);
+    m->slots = ns;
+    m->cap = nc;
+    mask = nc - 1;
+    h = tuple_hash(t, m->K) & mask;
+    while (m->slots[h] >= 0) h = (h + 1) & mask;
+  }
+  if (m->n == m->tcap) {
+    m->tcap = m->tcap ? m->tcap * 2 : 1024;
+    m->tuples = (int32_t *)realloc(m->tuples, m->tcap * 4ull * m->K);
+  }
+  memcpy(&m->tuples[m->n * m->K], t, 4ull * m->K);
+  m->slots[h] = (int32_t)m->n;
+  return (int32_t)m->n++;
+}
+
 static void aggregate_group_by(const pg_plan *plan, const orc_column *cols, const uint32_t *docs, uint64_t n,
                                agg_input *inputs, int32_t **key_ids, orc_segment_result *r,
                                uint64_t array_based_threshold) {
@@ -576,13 +618,20 @@ static void aggregate_group_by(const pg_plan *plan, const orc_column *cols, cons
   uint64_t cards[64];
   for (uint32_t k = 0; k < K; k++) {
     cards[k] = cols[plan->keys[k].col_id].cardinality;
-    if (card_prod > UINT64_MAX / (cards[k] ? cards[k] : 1)) overflow = 1; else card_prod *= cards[k];
+    /* cardinalityProduct > Long.MAX_VALUE / cardinality -> longOverflow (:117-131) */
+    if (overflow || card_prod > (uint64_t)INT64_MAX / (cards[k] ? cards[k] : 1)) overflow = 1; else card_prod *= cards[k];
   }
   uint64_t limit = plan->num_groups_limit ? plan->num_groups_limit : 100000;
   int array_based = !overflow && card_prod <= array_based_threshold;
   uint64_t upper = array_based ? card_prod : limit;
   id_map m = {0};
-  if (!array_based) {
+  tuple_map tm = {0};
+  if (overflow) {
+    tm.K = K;
+    tm.cap = 1024;
+    tm.slots = (int32_t *)malloc(tm.cap * 4);
+    for (uint64_t i = 0; i < tm.cap; i++) tm.slots[i] = -1;
+  } else if (!array_based) {
     m.cap = 1024;
     m.keys = (uint64_t *)malloc(m.cap * 8);
     m.ids = (int32_t *)malloc(m.cap * 4);
@@ -592,17 +641,23 @@ static void aggregate_group_by(const pg_plan *plan, const orc_column *cols, cons
   int32_t *gids = (int32_t *)malloc(sizeof(int32_t) * (n ? n : 1));
   uint64_t *raw_of_gid = NULL;
   uint8_t *seen = array_based ? (uint8_t *)calloc(upper ? upper : 1, 1) : NULL;
+  int32_t tuple[64];
   for (uint64_t i = 0; i < n; i++) {
     uint32_t d = docs[i];
+    if (overflow) {
+      for (uint32_t k = 0; k < K; k++) tuple[k] = key_ids[k][d];
+      gids[i] = tuple_get_or_put(&tm, tuple, limit);
+      continue;
+    }
     uint64_t raw = 0;
     for (int k = (int)K - 1; k >= 0; k--) raw = raw * cards[k] + (uint64_t)key_ids[k][d];
     if (array_based) { gids[i] = (int32_t)raw; seen[raw] = 1; }
     else gids[i] = map_get_or_put(&m, raw, limit);
   }
-  uint64_t G = array_based ? upper : m.n;
+  uint64_t G = array_based ? upper : overflow ? tm.n : m.n;
   raw_of_gid = (uint64_t *)malloc(sizeof(uint64_t) * (G ? G : 1));
   if (array_based) for (uint64_t g = 0; g < G; g++) raw_of_gid[g] = g;
-  else for (uint64_t i = 0; i < m.cap; i++) if (m.ids[i] >= 0) raw_of_gid[m.ids[i]] = m.keys[i];
+  else if (!overflow) for (uint64_t i = 0; i < m.cap; i++) if (m.ids[i] >= 0) raw_of_gid[m.ids[i]] = m.keys[i];
 
   double *vals = (double *)calloc((G ? G : 1) * (A ? A : 1), sizeof(double));
   int64_t *cnts = (int64_t *)calloc((G ? G : 1) * (A ? A : 1), sizeof(int64_t));
@@ -654,8 +709,12 @@ static void aggregate_group_by(const pg_plan *plan, const orc_column *cols, cons
   uint64_t o = 0;
   for (uint64_t g = 0; g < G; g++) {
     if (!present[g]) continue;
-    uint64_t raw = raw_of_gid[g];
-    for (uint32_t k = 0; k < K; k++) { r->key_dict_ids[o * K + k] = (int32_t)(raw % cards[k]); raw /= cards[k]; }
+    if (overflow) {
+      memcpy(&r->key_dict_ids[o * K], &tm.tuples[g * K], 4ull * K);
+    } else {
+      uint64_t raw = raw_of_gid[g];
+      for (uint32_t k = 0; k < K; k++) { r->key_dict_ids[o * K + k] = (int32_t)(raw % cards[k]); raw /= cards[k]; }
+    }
     for (uint32_t a = 0; a < A; a++) {
       r->values[o * A + a] = plan->aggs[a].fn == PG_AGG_DISTINCTCOUNT ? 0.0 : vals[g * A + a];
       r->counts[o * A + a] = cnts[g * A + a];
@@ -673,7 +732,8 @@ static void aggregate_group_by(const pg_plan *plan, const orc_column *cols, cons
   free(pairs);
   free(out_row);
   free(present); free(vals); free(cnts); free(gids); free(raw_of_gid); free(seen);
-  if (!array_based) { free(m.keys); free(m.ids); }
+  if (overflow) { free(tm.tuples); free(tm.slots); }
+  else if (!array_based) { free(m.keys); free(m.ids); }
 }
 
 /* ------------------------------------------------------------------ metadata / dictionary route */

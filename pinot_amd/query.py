@@ -19,7 +19,7 @@ UNBOUNDED = "*"  # RangePredicate.UNBOUNDED
 
 @dataclass(frozen=True)
 class Predicate:
-    type: str                 # EQ, NOT_EQ, IN, NOT_IN, RANGE
+    type: str                 # EQ, NOT_EQ, IN, NOT_IN, RANGE, IS_NULL, IS_NOT_NULL
     column: str
     values: Tuple[str, ...] = ()
     lower: str = UNBOUNDED
@@ -124,7 +124,7 @@ class QueryContext:
 _TOKEN = re.compile(r"\s*(?:(?P<num>-?\d+(?:\.\d+)?(?:[eE][-+]?\d+)?)|(?P<str>'(?:[^']|'')*')|"
                     r"(?P<id>[A-Za-z_][A-Za-z0-9_.$]*)|(?P<op><>|!=|<=|>=|[=<>*+\-(),]))")
 _KEYWORDS = {"SELECT", "FROM", "WHERE", "GROUP", "BY", "ORDER", "LIMIT", "AND", "OR", "NOT", "IN", "BETWEEN",
-             "ASC", "DESC", "AS", "OPTION"}
+             "ASC", "DESC", "AS", "OPTION", "IS", "NULL"}
 _AGGS = {"COUNT", "SUM", "MIN", "MAX", "AVG", "DISTINCTCOUNT", "COUNTMV"}
 
 
@@ -224,6 +224,10 @@ class _Parser:
         if self.accept("kw", "NOT"):
             return FilterContext("NOT", [self.predicate()])
         col = self.expect("id")
+        if self.accept("kw", "IS"):  # IsNullPredicate / IsNotNullPredicate (request/context/predicate/)
+            neg = self.accept("kw", "NOT")
+            self.expect("kw", "NULL")
+            return FilterContext("PREDICATE", predicate=Predicate("IS_NOT_NULL" if neg else "IS_NULL", col))
         if self.accept("kw", "BETWEEN"):
             lo = self.literal()
             self.expect("kw", "AND")
@@ -283,6 +287,8 @@ def filter_str(f: FilterContext) -> str:
         if p.type == "RANGE":
             return (f"{p.column} {'[' if p.lower_inclusive else '('}{p.lower},{p.upper}"
                     f"{']' if p.upper_inclusive else ')'}")
+        if p.type in ("IS_NULL", "IS_NOT_NULL"):
+            return f"{p.column} {p.type.replace('_', ' ')}"
         return f"{p.column} {p.type} ({','.join(p.values)})"
     if f.type == "NOT":
         return f"NOT({filter_str(f.children[0])})"

@@ -117,7 +117,10 @@ def _check(engine, table, sql, equivalent):
     i = np.arange(NUM_ROWS)
     vals = {"INT_COL": i, "NO_INDEX_COL": i, "STATIC_INT_COL": np.full(NUM_ROWS, 10)}
     from pinot_amd.plan import filtered_aggregation_passes
-    docs = sum(2 * int(_mask(pq.filter, vals).sum()) for pq, _ in filtered_aggregation_passes(q))
+    passes = filtered_aggregation_passes(q)
+    docs = sum(2 * int(_mask(pq.filter, vals).sum()) for pq, _ in passes)
+    if passes[-1][1]:  # non-filtered functions: a match-all pass over the main filter's docs besides the main pass
+        docs += 2 * int(main.sum())
     cols = len({c for a in q.aggregations for c in a.arg.cols})
     st = res.stats
     assert (st.num_docs_scanned, st.num_entries_scanned_post_filter, st.num_total_docs) == (docs, docs * cols,

@@ -18,11 +18,20 @@ def test_inner_aggregation(i, expected, oracle_engine, sv_table_inner):
     check_inner_values(res, case)
 
 
-@pytest.mark.parametrize("i", range(6))
+@pytest.mark.parametrize("i", range(8))
 def test_inner_group_by(i, expected, oracle_engine, sv_table_inner):
+    """ArrayBased / IntMap / LongMap / ArrayMap holders (cases 6-7: 9 keys whose cardinality product overflows a long)."""
     case = expected["inner_group_by"][i]
     res = oracle_engine.execute(sv_table_inner, inner_query(case, expected["filter"]))
     check_inner_values(res, case)
+
+
+@pytest.mark.parametrize("i", range(3))
+def test_inner_filtered_aggregation(i, expected, oracle_engine, sv_table_inner):
+    """InnerSegmentAggregationSingleValueQueriesTest.testFilteredAggregations: FILTER clauses with IS NOT NULL
+    (match-all without a null value vector) and the reference's pass statistics."""
+    case = expected["inner_filtered_aggregation"][i]
+    check_inner_values(oracle_engine.execute(sv_table_inner, case["query"]), case)
 
 
 def test_inner_group_by_array_vs_map_holders(oracle_engine, sv_table_inner):
