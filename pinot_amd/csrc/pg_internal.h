@@ -337,6 +337,26 @@ hipError_t launch_part_count2(const PartSpec& p, hipStream_t s);
 hipError_t launch_part_split2(const PartSpec& p, hipStream_t s);
 hipError_t launch_part_aggregate(const PartSpec& p, hipStream_t s);
 
+// ---- group keys wider than a packed 62-bit key (pg_wide.hip): ArrayMapBasedHolder as a device tuple table
+constexpr uint32_t kMaxWideKeys = 64;
+struct WideSpec {
+  uint32_t K, num_segments, max_fill, pad;
+  uint64_t mask;                    // table slots - 1 (a power of two)
+  unsigned long long* tags;         // [slots]: 0 free, 1 being written, else the tuple's hash | 2
+  uint32_t* tuples;                 // [slots][K] table-global key ids
+  unsigned int* fill;               // claimed slots
+  unsigned int* err;                // bit 0: key id outside its key space; bit 2: table over its fill budget
+  const ColDesc* keycols;           // [seg][K] (the scan's key column descriptors)
+  const uint32_t* num_docs;         // [seg]
+  uint32_t* const* out;             // [seg] -> uint32[num_docs]: tuple slot of each doc
+  const uint32_t* key_kind;         // [K]
+  const int64_t* key_base;          // [K]
+  const uint32_t* key_card;         // [K]
+};
+hipError_t launch_intern_tuples(const WideSpec& w, uint32_t max_docs, hipStream_t s);
+hipError_t launch_gather_tuples(const uint32_t* tuples, uint32_t K, const uint64_t* slots, uint64_t n, uint32_t* out,
+                                hipStream_t s);
+
 // ---- group state (pg_groups.hip)
 struct StateView {            // the device arrays of one partial state
   uint64_t num_slots, hmask;

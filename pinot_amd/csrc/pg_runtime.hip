@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <shared_mutex>
 #include <string>
@@ -826,7 +827,18 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
 
 // ------------------------------------------------------------------------------------------ execution
 
+// ArrayMapBasedHolder state of a wide-key plan (pg_wide.hip): the scan grouped by tuple slot; the tuples map the
+// slots back to the K table-global key ids.
+struct WideKeys {
+  uint32_t K = 0;
+  uint64_t cap = 0;
+  DevBuf tuples;                       // [cap][K]
+  pg_key key1{};                       // the scan's one key: the tuple slot (kWideColId)
+  const pg_plan* user_plan = nullptr;  // during finalize: the caller's plan (K keys, its ORDER BY)
+};
+
 struct Partials {
+  std::shared_ptr<WideKeys> wide;  // set for wide-key plans: packed keys are tuple slots, local to this state
   uint32_t mode = GM_NONE;      // GroupMode (GM_HASH_SEG only between the scan and the truncation merge)
   uint64_t num_slots = 1;
   uint32_t n_i64 = 1, n_f64 = 0, n_min = 0, n_max = 0, bit_words = 0, max_fill = 0;
@@ -1271,6 +1283,25 @@ void use_decoded(ColDesc& dc, const ColumnRes* c) {
   dc.identity = c->identity ? 1u : 0u;
 }
 
+// The scan's descriptor of group key column `c` (dictIds + dictionary / keymap, or the decoded forward index when the
+// key is a value offset of a column that has one).
+void key_coldesc(ColDesc& dc, const ColumnRes* c, const pg_key& key) {
+  memset(&dc, 0, sizeof(dc));
+  dc.words = (const uint32_t*)c->words.p;
+  dc.wbytes = (uint32_t)std::min<uint64_t>(c->words.bytes, 0xFFFFFFF0ull);
+  dc.dict = c->dict.p;
+  dc.keymap = (const int32_t*)c->keymap.p;
+  dc.bits = c->bits;
+  dc.dtype = c->dtype;
+  dc.card = c->card;
+  if (key.kind == PG_KEY_VALUE_OFFSET && (c->vals.p || c->identity)) use_decoded(dc, c);
+}
+
+// Wide group keys (pg_wide.hip): the plan is run with one key, the doc's tuple slot, read from a per-segment column
+// that exists only for this query; compile_and_run's column lookup finds it under kWideColId.
+constexpr uint32_t kWideColId = 0xFFFFFFF0u;
+thread_local const std::vector<ColumnRes>* t_wide_cols = nullptr;
+
 int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t hash_cap, bool allow_stream) {
   const double t_enter = wall_ms();
   if (!plan) return fail(PG_E_INVALID, "null plan");
@@ -1312,6 +1343,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   const uint32_t S = plan->num_segments, L = plan->num_leaves, A = plan->num_aggs, K = plan->num_keys;
   std::vector<const SegmentRes*> segs(S);
   auto col = [&](uint32_t si, uint32_t cid) -> const ColumnRes* {
+    if (cid == kWideColId && t_wide_cols) return &(*t_wide_cols)[si];
     auto it = segs[si]->cols.find(cid);
     return it == segs[si]->cols.end() ? nullptr : &it->second;
   };
@@ -1940,15 +1972,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     for (uint32_t k = 0; k < K; k++) {
       const ColumnRes* c = col(si, plan->keys[k].col_id);
       if (c->num_docs < sr.num_docs) return fail(PG_E_INVALID, "key column %u has fewer docs than the segment", plan->keys[k].col_id);
-      ColDesc& dc = keycols[(uint64_t)si * K + k];
-      dc.words = (const uint32_t*)c->words.p;
-      dc.wbytes = (uint32_t)std::min<uint64_t>(c->words.bytes, 0xFFFFFFF0ull);
-      dc.dict = c->dict.p;
-      dc.keymap = (const int32_t*)c->keymap.p;
-      dc.bits = c->bits;
-      dc.dtype = c->dtype;
-      dc.card = c->card;
-      if (plan->keys[k].kind == PG_KEY_VALUE_OFFSET && (c->vals.p || c->identity)) use_decoded(dc, c);
+      key_coldesc(keycols[(uint64_t)si * K + k], c, plan->keys[k]);
     }
   }
   P.entries_in_filter = entries_in_filter;
@@ -2750,6 +2774,189 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
 }
 
 
+// compile_and_run with its internal retries: a larger hash table after a fill overflow, no selective stream after a
+// survivor-region overflow.
+int run_with_retries(const pg_plan* plan, Partials& P, pg_stats& st) {
+  uint64_t cap = 0;
+  bool allow_stream = true;
+  for (;;) {
+    const int rc = compile_and_run(plan, P, st, cap, allow_stream);
+    if (rc == kRetryNoStream) { allow_stream = false; continue; }
+    if (rc != kRetryLargerTable) return rc;
+    cap = P.num_slots * 8;  // the group-by hash table overflowed: rerun with 8x the slots
+    if (cap > kMaxHashSlots) return fail(PG_E_UNSUPPORTED, "group-by needs more than %llu hash slots", (unsigned long long)kMaxHashSlots);
+  }
+}
+
+// A plan whose packed group key cannot be formed: more keys than the scan takes, or a key-space product >= 2^62
+// (DictionaryBasedGroupKeyGenerator's longOverflow, :117-131, over table-global key spaces).
+bool plan_needs_wide(const pg_plan* plan) {
+  if (!plan || plan->abi_version != PG_ABI_VERSION || !plan->num_keys || !plan->keys) return false;
+  if (plan->num_keys > (uint32_t)kMaxKeys) return true;
+  uint64_t G = 1;
+  for (uint32_t k = 0; k < plan->num_keys; k++) {
+    const uint64_t c = plan->keys[k].cardinality;
+    if (!c) return false;  // compile_and_run reports it
+    if (G > ((1ull << 62) - 1) / c) return true;
+    G *= c;
+  }
+  return false;
+}
+
+// ArrayMapBasedHolder (DictionaryBasedGroupKeyGenerator.java:777-860) on the device: intern every doc's key tuple
+// (pg_wide.hip), then run the plan grouped by the tuple slot.
+int run_wide(const pg_plan* plan, Partials& P, pg_stats& st) {
+  const uint32_t K = plan->num_keys, S = plan->num_segments;
+  if (K > kMaxWideKeys) return fail(PG_E_UNSUPPORTED, "more than %u group-by keys", kMaxWideKeys);
+  if (S && !plan->segments) return fail(PG_E_INVALID, "null segment list");
+  for (uint32_t k = 0; k < K; k++)
+    if (!plan->keys[k].cardinality || plan->keys[k].kind > PG_KEY_KEYMAP) return fail(PG_E_INVALID, "group key %u: bad key space", k);
+  int rc = t_ctx.init();
+  if (rc) return rc;
+  hipStream_t s = plan->stream ? (hipStream_t)plan->stream : thread_stream();
+  auto W = std::make_shared<WideKeys>();
+  W->K = K;
+  std::vector<ColumnRes> wcols(S);
+  uint64_t cap = 0;
+  {
+    std::shared_lock<std::shared_mutex> lk(g_seg_mu);
+    std::vector<ColDesc> kc((uint64_t)S * K);
+    std::vector<uint32_t> nd(S);
+    uint64_t expect = 0, max_docs = 0;
+    for (uint32_t si = 0; si < S; si++) {
+      auto it = g_segs.find(plan->segments[si].seg_key);
+      if (it == g_segs.end()) return fail(PG_E_NOTFOUND, "segment %llu not resident", (unsigned long long)plan->segments[si].seg_key);
+      nd[si] = plan->segments[si].num_docs;
+      max_docs = std::max<uint64_t>(max_docs, nd[si]);
+      uint64_t prod = 1;
+      for (uint32_t k = 0; k < K; k++) {
+        const pg_key& key = plan->keys[k];
+        auto ct = it->second->cols.find(key.col_id);
+        const ColumnRes* c = ct == it->second->cols.end() ? nullptr : &ct->second;
+        if (!c || !c->has_dict || (c->fwd != FWD_SV && c->fwd != FWD_SORTED))
+          return fail(c ? PG_E_UNSUPPORTED : PG_E_NOTFOUND, "group key column %u unusable in segment %u", key.col_id, si);
+        if (c->num_docs < nd[si]) return fail(PG_E_INVALID, "key column %u has fewer docs than the segment", key.col_id);
+        if (c->dtype > PG_DOUBLE && key.kind != PG_KEY_KEYMAP)
+          return fail(PG_E_INVALID, "non-numeric key column %u needs a keymap", key.col_id);
+        if (key.kind == PG_KEY_KEYMAP && !c->has_keymap) return fail(PG_E_NOTFOUND, "keymap missing for column %u", key.col_id);
+        if (key.kind == PG_KEY_VALUE_OFFSET && (c->dtype != PG_INT && c->dtype != PG_LONG))
+          return fail(PG_E_INVALID, "VALUE_OFFSET key on non-integer column %u", key.col_id);
+        if (key.kind == PG_KEY_VALUE_OFFSET && c->card &&
+            (c->imin < key.base || (uint64_t)(c->imax - key.base) >= key.cardinality))
+          return fail(PG_E_INVALID, "column %u values outside the key range of key %u", key.col_id, k);
+        key_coldesc(kc[(uint64_t)si * K + k], c, key);
+        prod = prod > nd[si] / std::max(1u, c->card) ? (uint64_t)nd[si] + 1 : prod * std::max(1u, c->card);
+      }
+      expect += std::min<uint64_t>(prod, nd[si]);
+      ColumnRes& w = wcols[si];
+      if ((rc = w.words.alloc_pooled(((uint64_t)nd[si] + 4) * 4))) return rc;
+      HIP_CHECK(hipMemsetAsync(w.words.p, 0, ((uint64_t)nd[si] + 4) * 4, s));
+    }
+    cap = pow2_at_least(std::max<uint64_t>(1024, 2 * expect));
+    cap = std::min<uint64_t>(cap, 1ull << 26);  // grows on overflow
+    std::vector<uint32_t*> outs(S);
+    for (uint32_t si = 0; si < S; si++) outs[si] = (uint32_t*)wcols[si].words.p;
+    std::vector<uint32_t> kkind(K), kcard(K);
+    std::vector<int64_t> kbase(K);
+    for (uint32_t k = 0; k < K; k++) {
+      kkind[k] = plan->keys[k].kind;
+      kcard[k] = plan->keys[k].cardinality;
+      kbase[k] = plan->keys[k].base;
+    }
+    // parameter block: [ColDesc S*K][num_docs S][out S][kind K][base K][card K]
+    std::vector<uint8_t> blob;
+    auto put = [&](const void* p, uint64_t n) {
+      const uint64_t at = (blob.size() + 15) & ~15ull;
+      blob.resize(at + n);
+      if (n) memcpy(&blob[at], p, n);
+      return at;
+    };
+    const uint64_t o_kc = put(kc.data(), kc.size() * sizeof(ColDesc)), o_nd = put(nd.data(), 4ull * S),
+                   o_out = put(outs.data(), 8ull * S), o_kind = put(kkind.data(), 4ull * K),
+                   o_base = put(kbase.data(), 8ull * K), o_card = put(kcard.data(), 4ull * K);
+    DevBuf params, tags, misc;
+    if ((rc = params.alloc_pooled(blob.size()))) return rc;
+    HIP_CHECK(hipMemcpyAsync(params.p, blob.data(), blob.size(), hipMemcpyHostToDevice, s));
+    const uint8_t* dp = (const uint8_t*)params.p;
+    if ((rc = misc.alloc_pooled(16))) return rc;
+    for (;;) {
+      if (cap > kMaxHashSlots || cap * (8ull + 4ull * K) > kStateBudget)
+        return fail(PG_E_UNSUPPORTED, "group key tuple table of %llu slots exceeds the state budget", (unsigned long long)cap);
+      if ((rc = tags.alloc_pooled(cap * 8))) return rc;
+      if ((rc = W->tuples.alloc_pooled(cap * 4ull * K))) return rc;
+      HIP_CHECK(hipMemsetAsync(tags.p, 0, cap * 8, s));
+      HIP_CHECK(hipMemsetAsync(misc.p, 0, 16, s));
+      WideSpec ws;
+      memset(&ws, 0, sizeof(ws));
+      ws.K = K;
+      ws.num_segments = S;
+      ws.max_fill = (uint32_t)(cap / 4 * 3);
+      ws.mask = cap - 1;
+      ws.tags = (unsigned long long*)tags.p;
+      ws.tuples = (uint32_t*)W->tuples.p;
+      ws.fill = (unsigned int*)misc.p;
+      ws.err = (unsigned int*)misc.p + 1;
+      ws.keycols = (const ColDesc*)(dp + o_kc);
+      ws.num_docs = (const uint32_t*)(dp + o_nd);
+      ws.out = (uint32_t* const*)(dp + o_out);
+      ws.key_kind = (const uint32_t*)(dp + o_kind);
+      ws.key_base = (const int64_t*)(dp + o_base);
+      ws.key_card = (const uint32_t*)(dp + o_card);
+      HIP_CHECK(launch_intern_tuples(ws, (uint32_t)max_docs, s));
+      uint32_t fe[2] = {0, 0};
+      HIP_CHECK(hipMemcpyAsync(fe, misc.p, 8, hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+      if (fe[1] & 1u) return fail(PG_E_INVALID, "device bounds check failed: a key fell outside the plan's key space");
+      if (!(fe[1] & 4u)) break;
+      cap *= 4;  // over the fill budget: a larger table
+    }
+  }
+  W->cap = cap;
+  for (uint32_t si = 0; si < S; si++) {  // the tuple-slot column: an identity "dictionary" over [0, cap)
+    ColumnRes& w = wcols[si];
+    w.has_dict = true;
+    w.dtype = PG_INT;
+    w.card = (uint32_t)cap;
+    w.imin = 0;
+    w.imax = (int64_t)cap - 1;
+    w.dmin = 0;
+    w.dmax = (double)(cap - 1);
+    w.fwd = FWD_SV;
+    w.num_docs = w.num_values = plan->segments[si].num_docs;
+    w.bits = 32;
+    w.identity = true;
+  }
+  W->key1.col_id = kWideColId;
+  W->key1.kind = PG_KEY_VALUE_OFFSET;
+  W->key1.cardinality = (uint32_t)cap;
+  W->key1.base = 0;
+  pg_plan sh = *plan;
+  sh.num_keys = 1;
+  sh.keys = &W->key1;
+  sh.num_order = 0;
+  sh.order = nullptr;
+  sh.limit = 0;
+  t_wide_cols = &wcols;
+  rc = run_with_retries(&sh, P, st);
+  t_wide_cols = nullptr;
+  if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = fail(PG_E_HIP, "stream failed");
+  if (rc) return rc;
+  P.wide = W;
+  // numEntriesScannedPostFilter counts the user's key columns, not the tuple column (AggregationOperator.java:84-89)
+  std::unordered_set<uint32_t> proj;
+  for (uint32_t a = 0; a < plan->num_aggs; a++) {
+    const pg_agg& g = plan->aggs[a];
+    if (g.fn == PG_AGG_COUNT) continue;
+    proj.insert(g.col_a);
+    if ((g.fn == PG_AGG_SUM || g.fn == PG_AGG_MIN || g.fn == PG_AGG_MAX || g.fn == PG_AGG_AVG) && g.op != PG_EXPR_COL)
+      proj.insert(g.col_b);
+  }
+  for (uint32_t k = 0; k < K; k++) proj.insert(plan->keys[k].col_id);
+  P.projected_cols = (uint32_t)proj.size();
+  st.num_entries_scanned_post_filter = st.num_docs_scanned * P.projected_cols;
+  return PG_OK;
+}
+
 struct PartialsImpl {
   Partials P;
 };
@@ -2891,7 +3098,42 @@ int finalize_small(pg_partials* pp, const pg_plan* plan, pg_result** out, const 
 // (IndexedTable.finish -> TableResizer.getTopRecords: a radix sort on the first ORDER BY item on the device, the
 // candidates -- every group that ranks within `limit`, ties included -- fully ordered on the host) and, on request,
 // the DISTINCTCOUNT value sets.
+int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out);
+
+// Wide-key partials: the state is keyed by tuple slot, so the device part runs on the plan's one-key form (a leading
+// ORDER BY on an aggregation still trims on the device; one on a key cannot, every group comes back) and build_result
+// maps slots to tuples and orders by the caller's full ORDER BY.
 int finalize(pg_partials* pp, const pg_plan* plan, pg_result** out) {
+  Partials& P = ((PartialsImpl*)pp->impl)->P;
+  if (!P.wide) return finalize_core(pp, plan, out);
+  if (plan->num_keys != P.wide->K) return fail(PG_E_INVALID, "plan does not match partials");
+  if (plan->num_order && !plan->order) return fail(PG_E_INVALID, "null order list");
+  for (uint32_t i = 0; i < plan->num_order; i++) {
+    const pg_order& o = plan->order[i];
+    if (o.kind > PG_ORDER_KEY || (o.kind == PG_ORDER_AGG && o.index >= plan->num_aggs) ||
+        (o.kind == PG_ORDER_KEY && o.index >= plan->num_keys))
+      return fail(PG_E_INVALID, "bad ORDER BY item %u", i);
+  }
+  pg_plan sh = *plan;
+  sh.num_keys = 1;
+  sh.keys = &P.wide->key1;
+  pg_order o0{};
+  if (plan->num_order && plan->order[0].kind == PG_ORDER_AGG) {
+    o0 = plan->order[0];
+    sh.num_order = 1;
+    sh.order = &o0;
+  } else {
+    sh.num_order = 0;
+    sh.order = nullptr;
+    sh.limit = 0;
+  }
+  P.wide->user_plan = plan;
+  const int rc = finalize_core(pp, &sh, out);
+  P.wide->user_plan = nullptr;
+  return rc;
+}
+
+int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   const double t0 = wall_ms();
   struct Stamp {
     double t0;
@@ -3028,8 +3270,27 @@ int finalize(pg_partials* pp, const pg_plan* plan, pg_result** out) {
 int build_result(pg_partials* pp, const pg_plan* plan, pg_result** out, const Partials& P, uint64_t nc,
                  const std::vector<uint64_t>& hk, const std::vector<double>& hv, const std::vector<int64_t>& hc,
                  bool sets, const std::vector<uint64_t>& hoff, const std::vector<uint32_t>& hids) {
+  if (P.wide && P.wide->user_plan) plan = P.wide->user_plan;  // the caller's K keys and ORDER BY
   const uint32_t A = plan->num_aggs, K = plan->num_keys;
   const uint32_t AA = A ? A : 1;
+  // key ids of candidate i: from the packed key, or (wide keys) from the tuple of its slot
+  std::vector<uint32_t> wk;
+  if (P.wide && nc) {
+    hipStream_t s = thread_stream();
+    Scratch sc(s);
+    int rc = PG_OK;
+    uint64_t* dk = sc.get<uint64_t>(nc, rc);
+    uint32_t* dt = sc.get<uint32_t>(nc * K, rc);
+    if (rc) return rc;
+    wk.resize(nc * K);
+    HIP_CHECK(hipMemcpyAsync(dk, hk.data(), nc * 8, hipMemcpyHostToDevice, s));
+    HIP_CHECK(launch_gather_tuples((const uint32_t*)P.wide->tuples.p, K, dk, nc, dt, s));
+    HIP_CHECK(hipMemcpyAsync(wk.data(), dt, nc * K * 4ull, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+  }
+  auto key_id = [&](uint64_t i, uint32_t k) -> uint64_t {
+    return P.wide ? (uint64_t)wk[i * K + k] : (hk[i] / P.key_stride[k]) % P.key_card[k];
+  };
   std::vector<uint64_t> perm(nc);
   for (uint64_t i = 0; i < nc; i++) perm[i] = i;
   if (K && plan->num_order) {
@@ -3048,10 +3309,14 @@ int build_result(pg_partials* pp, const pg_plan* plan, pg_result** out, const Pa
           const double x = val(i, it.index), y = val(j, it.index);
           if (x != y) return it.desc ? x > y : x < y;
         } else {
-          const uint64_t x = (hk[i] / P.key_stride[it.index]) % P.key_card[it.index];
-          const uint64_t y = (hk[j] / P.key_stride[it.index]) % P.key_card[it.index];
+          const uint64_t x = key_id(i, it.index), y = key_id(j, it.index);
           if (x != y) return it.desc ? x > y : x < y;
         }
+      }
+      if (P.wide) {  // ascending key ids, first key first
+        for (uint32_t k = 0; k < K; k++)
+          if (key_id(i, k) != key_id(j, k)) return key_id(i, k) < key_id(j, k);
+        return false;
       }
       return hk[i] < hk[j];
     });
@@ -3069,7 +3334,7 @@ int build_result(pg_partials* pp, const pg_plan* plan, pg_result** out, const Pa
   if (!r->keys || !r->values || !r->counts) { pg_result_free(r); return fail(PG_E_NOMEM, "out of host memory"); }
   for (uint64_t o = 0; o < nc; o++) {
     const uint64_t i = perm[o];
-    for (uint32_t k = 0; k < K; k++) r->keys[o * K + k] = (uint32_t)((hk[i] / P.key_stride[k]) % P.key_card[k]);
+    for (uint32_t k = 0; k < K; k++) r->keys[o * K + k] = (uint32_t)key_id(i, k);
     for (uint32_t a = 0; a < A; a++) {
       r->values[o * A + a] = hv[i * A + a];
       r->counts[o * A + a] = hc[i * A + a];
@@ -3178,15 +3443,7 @@ int pg_execute_partial(const pg_plan* plan, pg_partials** out) {
   t_timing.host_compile_ms = 0;
   t_timing.finalize_wall_ms = 0;
   try {
-    uint64_t cap = 0;
-    bool allow_stream = true;
-    for (;;) {
-      rc = compile_and_run(plan, impl->P, st, cap, allow_stream);
-      if (rc == kRetryNoStream) { allow_stream = false; continue; }
-      if (rc != kRetryLargerTable) break;
-      cap = impl->P.num_slots * 8;  // the group-by hash table overflowed: rerun with 8x the slots
-      if (cap > kMaxHashSlots) { rc = fail(PG_E_UNSUPPORTED, "group-by needs more than %llu hash slots", (unsigned long long)kMaxHashSlots); break; }
-    }
+    rc = plan_needs_wide(plan) ? run_wide(plan, impl->P, st) : run_with_retries(plan, impl->P, st);
     t_timing.execute_wall_ms = (float)(wall_ms() - t0);
   } catch (const std::exception& e) {
     rc = fail(PG_E_NOMEM, "execute failed: %s", e.what());
@@ -3224,6 +3481,8 @@ int pg_partials_copy(pg_partials* p, int dir, void* i64, void* f64, void* mn, vo
   if (rc) return rc;
   if (!p || !p->impl || (dir != PG_COPY_OUT && dir != PG_COPY_IN)) return fail(PG_E_INVALID, "bad partials / direction");
   if (p->mode != PG_STATE_DENSE) return fail(PG_E_INVALID, "pg_partials_copy needs a dense state (use pg_partials_export)");
+  if (((PartialsImpl*)p->impl)->P.wide)
+    return fail(PG_E_UNSUPPORTED, "wide group keys are tuple slots local to one state: no cross-state merge");
   hipStream_t s = stream ? (hipStream_t)stream : thread_stream();
   void* mine[4] = {p->i64, p->f64, p->mn, p->mx};
   void* theirs[4] = {i64, f64, mn, mx};
@@ -3245,6 +3504,7 @@ int pg_partials_export(pg_partials* p, uint32_t num_parts, void* dst, uint64_t d
   if (!p || !p->impl || !num_parts || !part_counts) return fail(PG_E_INVALID, "bad export arguments");
   try {
     Partials& P = ((PartialsImpl*)p->impl)->P;
+    if (P.wide) return fail(PG_E_UNSUPPORTED, "wide group keys are tuple slots local to one state: no cross-state merge");
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream();
     Scratch sc(s);
     const StateView v = P.view();
@@ -3277,6 +3537,8 @@ int pg_partials_create(const pg_partials* like, uint64_t capacity, pg_partials**
   if (rc) return rc;
   if (!like || !like->impl || !out) return fail(PG_E_INVALID, "null argument");
   *out = nullptr;
+  if (((PartialsImpl*)like->impl)->P.wide)
+    return fail(PG_E_UNSUPPORTED, "wide group keys are tuple slots local to one state: no cross-state merge");
   PartialsImpl* impl = new (std::nothrow) PartialsImpl();
   if (!impl) return fail(PG_E_NOMEM, "out of host memory");
   try {

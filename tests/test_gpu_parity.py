@@ -22,11 +22,19 @@ def test_golden_inner_aggregation(i, expected, gpu_engine, sv_table_inner):
     check_inner_values(res, case)
 
 
-@pytest.mark.parametrize("i", range(6))
+@pytest.mark.parametrize("i", range(8))
 def test_golden_inner_group_by(i, expected, gpu_engine, sv_table_inner):
+    """Cases 6-7 are the reference's ArrayMapBasedHolder answers (9 keys): the device tuple table of pg_wide.hip."""
     case = expected["inner_group_by"][i]
     res = gpu_engine.execute(sv_table_inner, inner_query(case, expected["filter"]))
     check_inner_values(res, case)
+
+
+@pytest.mark.parametrize("i", range(3))
+def test_golden_inner_filtered_aggregation(i, expected, gpu_engine, sv_table_inner):
+    """testFilteredAggregations (IS NOT NULL filters) through one device plan per filter."""
+    case = expected["inner_filtered_aggregation"][i]
+    check_inner_values(gpu_engine.execute(sv_table_inner, case["query"]), case)
 
 
 @pytest.mark.parametrize("i", range(24))
@@ -91,10 +99,46 @@ def test_streaming_prefilter_on_and_off(mode, monkeypatch, gpu_engine, oracle_en
 
 
 def test_unsupported_shape_is_reported_not_crashed(gpu_engine, sv_table_inner):
-    """More group-by keys than the device path takes -> PG_E_UNSUPPORTED (the caller falls back to the CPU plan)."""
+    """More aggregations than the device path takes -> PG_E_UNSUPPORTED (the caller falls back to the CPU plan)."""
     with pytest.raises(UnsupportedQuery):
-        gpu_engine.execute(sv_table_inner, "SELECT COUNT(*) FROM t GROUP BY column1, column3, column5, column6, column7, "
-                                           "column9, column11, column12, column17")
+        gpu_engine.execute(sv_table_inner, "SELECT COUNT(*), SUM(column1), SUM(column3), SUM(column6), SUM(column7), "
+                                           "SUM(column9), SUM(column17), SUM(column18), MAX(column1) FROM t")
+
+
+WIDE_KEYS = "column1, column3, column5, column6, column7, column9, column11, column12, column17"
+WIDE_QUERIES = [
+    f"SELECT COUNT(*), SUM(column18), MIN(column6), MAX(column3), AVG(column7) FROM t GROUP BY {WIDE_KEYS}",
+    f"SELECT COUNT(*), SUM(column1) FROM t WHERE column3 > 1000000000 AND column11 <> 'P' GROUP BY {WIDE_KEYS}, "
+    "column18, daysSinceEpoch",
+    f"SELECT DISTINCTCOUNT(column11), COUNT(*) FROM t WHERE column6 < 900000000 GROUP BY column1, column3, column6, "
+    "column7, column9",
+]
+
+
+@pytest.mark.parametrize("sql", WIDE_QUERIES)
+def test_wide_group_keys_match_oracle(sql, gpu_engine, oracle_engine, sv_table_inter):
+    """Group keys whose packed key exceeds 62 bits or that number more than 8 (ArrayMapBasedHolder,
+    DictionaryBasedGroupKeyGenerator.java:777-): device tuple interning over 4 segments merged by value, dense and hash
+    group states, the ORDER BY on the device (by an aggregation) and on the host (by a key)."""
+    from pinot_amd import abi
+    q = parse(sql)
+    o = oracle_engine.execute(sv_table_inter, q)
+    assert_same_result(gpu_engine.execute(sv_table_inter, q), o, table=sv_table_inter)
+    assert_same_result(gpu_engine.execute(sv_table_inter, q, flags=abi.PG_PLAN_VALUE_SETS | abi.PG_PLAN_HASH_GROUPS), o,
+                       table=sv_table_inter)
+    for order in ("ORDER BY COUNT(*) DESC, column1, column3, column6 LIMIT 7", "ORDER BY column3 DESC, column1 LIMIT 9"):
+        q2 = parse(sql.replace("SELECT ", "SELECT column1, column3, column6, ") + " " + order)
+        assert reduce_to_rows(q2, gpu_engine.execute(sv_table_inter, q2, trim=True))[1] == \
+            reduce_to_rows(q2, oracle_engine.execute(sv_table_inter, q2))[1]
+
+
+@pytest.mark.parametrize("limit", [1, 500, 29000])
+def test_wide_group_keys_num_groups_limit(limit, gpu_engine, oracle_engine, sv_table_inter):
+    """numGroupsLimit with the ArrayMapBasedHolder: per segment the first `limit` tuples in doc order (getGroupId
+    :812-819), then the value-keyed merge."""
+    q = parse(f"SELECT COUNT(*), SUM(column1) FROM t GROUP BY {WIDE_KEYS} OPTION(numGroupsLimit={limit})")
+    assert_same_result(gpu_engine.execute(sv_table_inter, q), oracle_engine.execute(sv_table_inter, q),
+                       table=sv_table_inter)
 
 
 GROUP_QUERIES = [q for q in SV_QUERIES if "GROUP BY" in q] + [
