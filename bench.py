@@ -16,16 +16,26 @@ finalize (+ at N > 1 the cross-GPU merge, pinot_amd.combine).  Weak scaling: eve
 `--gpus N` without a torchrun environment launches N rank processes (torch.distributed.run) before touching a GPU.
 
 `roofline`: the hot path's kernels (the selective stream over the driving filter leaves + the fused scan over its
-survivors, or the fused scan alone when no leaf prefix is selective):
-algorithmic bytes per query (forward-index bytes of the touched columns + dictionary bytes of the decoded columns,
-SURVEY §8(d)) / their summed HIP-event durations on the stream they run on; `traffic` from the rocprofv3
-FETCH_SIZE / WRITE_SIZE passes of tools/profile_bench.sh (profiles/traffic_<workload>.json).
-`cpu_baseline`: the C restatement of the Pinot CPU operators (oracle/, "port") on a bounded sample of the same segments,
-at Pinot's default combine parallelism (CombineOperatorUtils.java:38-50) and at every core this process may use; rank 0
-at N = 1 only.
+survivors, or the fused scan alone when no leaf prefix is selective), timed with HIP events on the stream they run on.
+`achieved` = the bytes the executed plan must read / that time: every column read for all docs in full (the streamed
+driving leaf, a full scan's columns) + for a column read only for the docs that passed earlier filter stages, the
+128-byte lines holding those docs' values (expected lines of uniformly spread survivors, with the survivor counts of the
+plan's own filter prefixes measured by COUNT(*) queries before timing), at the width the device reads (dictIds, or the
+decoded value image of a large dictionary).  SURVEY §8(d)'s algorithmic bytes (every touched column in full) are kept
+as `algorithmic_bytes` / `algorithmic_frac`: a short-circuiting AND never reads most of them, so that ratio is not
+bounded by the peak.  `traffic` = PMC bytes (FETCH_SIZE x 2 + WRITE_SIZE per query, tools/profile_bench.sh) from
+profiles/traffic_<workload>.json, used only when it was measured on this very libpinot_gpu.so (md5 stamp).
+`cpu_baseline`: the C restatement of the Pinot CPU operators (oracle/, "port": per-segment filter with later AND
+children on the survivors only, projection of the matching docs, aggregation) over min(#segments, 128, cores) of the
+same segments, at Pinot's default combine parallelism (CombineOperatorUtils.java:38-50) and at one thread per segment up
+to every core this process may use; rank 0 at N = 1 only.
+`--split-table`: the workload's table (128 segments for config 2 / 4) divided over the N ranks (16 per GPU
+at N = 8): strong scaling of the 1 B-row query.
 """
 import argparse
+import hashlib
 import json
+import math
 import os
 import socket
 import subprocess
@@ -40,27 +50,106 @@ HEADLINE_METRIC = "rows/sec for filter+group-by SUM over 1B rows; % of HBM roofl
 
 
 def workloads(args):
+    """`stages`: the executed plan's read pattern, in evaluation order: (filter the docs passed so far, or None = every
+    doc; [(column, "ids" | "values")] read for those docs).  "ids" = the packed dictIds; "values" = what an aggregation /
+    key reads (the decoded value image of a large non-identity dictionary, else the dictIds)."""
     from pinot_amd import synth
+    ids = ", ".join(str((i * 7919 + 13) % 1_000_000) for i in range(args.in_ids))
     return {
         "adanalytics": dict(
             specs=synth.ADANALYTICS, table="adAnalytics", segments=128, trim=False,
             query=synth.adanalytics_query(args.in_ids), decoded=("daysSinceEpoch", "clicks", "impressions"),
             metric=HEADLINE_METRIC,
             desc="AdAnalytics config 2: SUM(clicks), SUM(impressions) WHERE daysSinceEpoch BETWEEN (90 of 365 days) "
-                 f"AND accountId IN ({args.in_ids} ids) GROUP BY daysSinceEpoch"),
+                 f"AND accountId IN ({args.in_ids} ids) GROUP BY daysSinceEpoch",
+            stages=[(None, [("accountId", "ids")]),                       # the selective stream
+                    (f"accountId IN ({ids})", [("daysSinceEpoch", "ids")]),  # list scan: the range leaf + group key
+                    ("*", [("clicks", "values"), ("impressions", "values")])]),
         "ssb": dict(
             specs=synth.SSB_LINEORDER, table="lineorder", segments=96, trim=False, query=synth.ssb_q11_query(),
             decoded=("lo_extendedprice", "lo_discount"),
             metric="rows/sec for filter + SUM(a*b) over SSB lineorder (config 3, secondary line)",
             desc="SSB config 3 (Q1.1 shape): SUM(lo_extendedprice * lo_discount) WHERE lo_orderdate BETWEEN "
-                 "(365 of 2557 days) AND lo_discount BETWEEN 1 AND 3 AND lo_quantity < 25"),
+                 "(365 of 2557 days) AND lo_discount BETWEEN 1 AND 3 AND lo_quantity < 25",
+            stages=[(None, [("lo_orderdate", "ids")]),
+                    ("lo_orderdate BETWEEN 8035 AND 8399", [("lo_discount", "ids")]),
+                    ("lo_orderdate BETWEEN 8035 AND 8399 AND lo_discount BETWEEN 1 AND 3", [("lo_quantity", "ids")]),
+                    ("*", [("lo_extendedprice", "values")])]),
         "highcard": dict(
             specs=synth.HIGHCARD, table="events", segments=128, trim=True,
             query=synth.highcard_query() + " OPTION(numGroupsLimit=10000000)", decoded=("userId", "itemId"),
             metric="rows/sec for high-cardinality group-by DISTINCTCOUNT (config 4, secondary line)",
             desc="config 4: SELECT userId, DISTINCTCOUNT(itemId) GROUP BY userId (10 M users x 1 000 items) "
-                 "ORDER BY DISTINCTCOUNT(itemId) DESC, userId LIMIT 100, numGroupsLimit 10 M"),
+                 "ORDER BY DISTINCTCOUNT(itemId) DESC, userId LIMIT 100, numGroupsLimit 10 M",
+            stages=[(None, [("userId", "values"), ("itemId", "values")])]),
+        "index": dict(
+            specs=None, make=synth.make_index_columns_torch, table="idx", segments=synth.INDEX_SEGMENTS_PER_GPU,
+            trim=False, query=synth.index_query(), decoded=(),
+            metric="rows/sec for sorted + inverted index filters (5 predicates) + COUNTMV (config 5, secondary line)",
+            desc="config 5: COUNT(*), COUNTMV(mvTags) WHERE sortedCol BETWEEN (40 %) AND (inv1 = x OR inv2 IN (20)) "
+                 "AND inv3 <> y AND inv4 IN (2000) -- sorted index, 4 bitmap inverted indexes, MV column",
+            stages=None),
     }
+
+
+DECODE_MIN_CARD = 1 << 17  # pg_runtime.hip kDecodeMinCard: larger INT / LONG dictionaries get a decoded value image
+
+
+def read_width(dc, use):
+    """Bits per doc the device reads of synthetic column `dc` for a use (pg_runtime.hip build_decoded)."""
+    lo, hi = int(dc.dict_values[0]), int(dc.dict_values[-1])
+    identity = hi - lo + 1 == dc.cardinality
+    if use == "ids" or identity or dc.cardinality < DECODE_MIN_CARD:
+        return dc.bits
+    return max(1, (hi - lo).bit_length())
+
+
+def lines_bytes(num_docs, width, needed):
+    """Bytes of the 128-byte lines holding `needed` uniformly spread docs' values of a `width`-bit column."""
+    total = (num_docs * width + 7) // 8
+    if needed >= num_docs:
+        return total
+    lines = (total + 127) // 128
+    per_line = 1024.0 / width
+    p = 1.0 - (1.0 - needed / num_docs) ** per_line
+    return min(total, 128.0 * lines * p)
+
+
+def index_plan_bytes(eng, table, plan, index_meta, rows, sql):
+    """Config 5: the bytes its plan must move.  Per segment: the roaring bitmaps of the dictIds the inverted leaves
+    select (read once), each inverted leaf's doc bitmap (written by the pre-pass, re-read by the scan within the
+    sorted leaf's doc range; NOT_EQ also re-reads and re-writes it to flip it), and the MV row offsets of the matching
+    docs (COUNTMV).  The sorted leaf becomes a doc range on the host (no device bytes).  Returns (plan bytes, SURVEY
+    §8(d) algorithmic bytes = referenced roaring bytes + sorted pairs + the MV start-of-row bitmap over the sorted
+    range, [docs in the sorted range, matched docs])."""
+    import numpy as np
+    where = sql.split(" WHERE ")[1]
+    sp = [p for p in plan.query.filter.leaves() if p.column == "sortedCol"][0]
+    in_range = int(eng.execute(table, f"SELECT COUNT(*) FROM {table.name} WHERE sortedCol BETWEEN {sp.lower} AND "
+                                      f"{sp.upper}").rows[()][0])
+    matched = int(eng.execute(table, f"SELECT COUNT(*) FROM {table.name} WHERE {where}").rows[()][0])
+    S = len(index_meta)
+    frac_range = in_range / (S * rows)
+    total = alg = 0.0
+    bm = rows / 8
+    for si, meta in enumerate(index_meta):
+        ref = 0
+        for li, lw in enumerate(plan.lowered[si]):
+            offs = meta[plan.leaf_preds[li].column][0]
+            if offs is None or lw.ids is None:
+                continue
+            ids = np.asarray(lw.ids, dtype=np.int64)
+            ref += int((offs[ids + 1] - offs[ids]).sum())
+            total += bm + frac_range * bm + (2 * bm if lw.exclusive else 0)
+        total += ref + 2 * lines_bytes(rows + 1, 32, matched / S)  # offsets[d], offsets[d + 1] of matching docs
+        alg += ref + 8 * meta["sortedCol"][1] + frac_range * meta["mvTags"][2] / 8
+    return total, alg, [in_range, matched]
+
+
+def lib_md5():
+    from pinot_amd import gpu
+    with open(gpu.LIB_PATH, "rb") as f:
+        return hashlib.md5(f.read()).hexdigest()
 
 
 def launch_ranks(n):
@@ -89,14 +178,17 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=("adanalytics", "ssb", "highcard"), default="adanalytics")
+    ap.add_argument("--workload", choices=("adanalytics", "ssb", "highcard", "index"), default="adanalytics")
     ap.add_argument("--segments", type=int, default=None, help="segments per GPU (default: the workload's)")
+    ap.add_argument("--split-table", action="store_true",
+                    help="divide the workload's table (--table-segments) over the ranks: strong scaling")
+    ap.add_argument("--table-segments", type=int, default=None)
     ap.add_argument("--rows", type=int, default=7_812_500, help="rows per segment")
     ap.add_argument("--in-ids", type=int, default=1000)
     ap.add_argument("--cpu-sample-segments", type=int, default=None)
-    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="per CPU leg")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="per CPU leg")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--traffic-file", default=None, help="PMC HBM traffic of the scan kernel (tools/profile_bench.sh)")
+    ap.add_argument("--traffic-file", default=None, help="PMC HBM traffic of the hot-path kernels (tools/profile_bench.sh)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         launch_ranks(args.gpus)
@@ -105,11 +197,16 @@ def main():
     import torch
 
     W = workloads(args)[args.workload]
-    if args.segments is None:
-        args.segments = W["segments"]
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.split_table:
+        total = args.table_segments or W["segments"]
+        if total % world:
+            raise SystemExit(f"--split-table: {total} segments do not divide over {world} ranks")
+        args.segments = total // world
+    elif args.segments is None:
+        args.segments = W["segments"]
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -129,21 +226,31 @@ def main():
     cores = len(os.sched_getaffinity(0))
     nproc = os.cpu_count()
     pinot_threads = max(1, min(10, cores // 2))  # CombineOperatorUtils.MAX_NUM_THREADS_PER_QUERY on this host
-    n_sample = min(args.segments, args.cpu_sample_segments or max(4, min(16, cores)))
+    n_sample = min(args.segments, args.cpu_sample_segments or max(16, min(128, cores)))
     segs, host_sample = [], []
     t_gen = time.time()
     fwd_bytes = dict_bytes = 0
+    widths = {}  # column -> [(bits of dictIds, bits of values)] per segment
+    index_meta = []  # config 5: per segment {column: (inverted-index offsets, cardinality, num values)}
     table = None
     for s in range(args.segments):
         gidx = rank * args.segments + s
-        dcs = synth.make_columns_torch(W["specs"], gidx, args.rows, dev)
+        dcs = W["make"](gidx, args.rows, dev) if W.get("make") else \
+            synth.make_columns_torch(W["specs"], gidx, args.rows, dev)
         seg = ImmutableSegment(f"{W['table']}_{gidx}", args.rows, {dc.spec.name: dc.meta_column() for dc in dcs})
         segs.append(seg)
         if table is None:
             table = Table(W["table"], [seg])
         eng.register_device_segment(seg, table, dcs)
-        fwd_bytes += sum((args.rows * dc.bits + 7) // 8 for dc in dcs)
-        dict_bytes += sum(4 * dc.cardinality for dc in dcs if dc.spec.name in W["decoded"])
+        if W["stages"] is not None:
+            fwd_bytes += sum((args.rows * dc.bits + 7) // 8 for dc in dcs)
+            dict_bytes += sum(4 * dc.cardinality for dc in dcs if dc.spec.name in W["decoded"])
+            for dc in dcs:
+                widths.setdefault(dc.spec.name, []).append((read_width(dc, "ids"), read_width(dc, "values")))
+        else:  # index path: keep what the byte model needs (inverted-index offset headers, MV value counts)
+            index_meta.append({dc.spec.name: (dc.inv_be[:4 * (dc.cardinality + 1)].cpu().numpy().view(">u4")
+                                              .astype(np.int64) if dc.inv_be is not None else None,
+                                              dc.cardinality, dc.num_values) for dc in dcs})
         if want_cpu and s < n_sample:
             host_sample.append(ImmutableSegment(seg.name, args.rows, {dc.spec.name: dc.host_column() for dc in dcs}))
         del dcs
@@ -162,6 +269,25 @@ def main():
             dist.all_gather(allk, kk)
             assert all(torch.equal(kk, x) for x in allk), "key spaces differ across ranks"
 
+    # survivors of the plan's filter prefixes (outside the timed region): the bytes the executed plan must read
+    rows_per_gpu = args.segments * args.rows
+    plan_bytes, stage_docs, counted = 0.0, [], set()
+    if W["stages"] is None:
+        plan_bytes, fwd_bytes, stage_docs = index_plan_bytes(eng, table, plan, index_meta, args.rows, W["query"])
+    for filt, cols in W["stages"] or []:
+        if filt is None:
+            n = rows_per_gpu
+        else:
+            where = W["query"].split(" WHERE ")[1].split(" GROUP BY ")[0] if filt == "*" else filt
+            n = int(eng.execute(table, f"SELECT COUNT(*) FROM {W['table']} WHERE {where}").rows[()][0])
+        stage_docs.append(n)
+        for c, use in cols:
+            if c in counted:
+                continue
+            counted.add(c)
+            for w_ids, w_vals in widths[c]:
+                plan_bytes += lines_bytes(args.rows, w_ids if use == "ids" else w_vals, n / args.segments)
+
     def step():
         if world == 1:
             return eng.run_plan(plan)
@@ -179,7 +305,9 @@ def main():
     for _ in range(args.steps):
         res = step()
         tm = eng.last_timing()
-        scan_ms.append(tm.prefilter_ms + tm.scan_ms)  # the hot path's kernels: selective stream + fused scan
+        # the hot path's kernels: index pre-pass (IN-list LUTs, sorted / inverted / MV leaf bitmaps) + selective
+        # stream + fused scan (+ the radix-partitioned group-by's passes, reported in scan_ms)
+        scan_ms.append(tm.prepass_ms + tm.prefilter_ms + tm.scan_ms)
         for k, v in parts.items():
             v.append(getattr(tm, k))
     torch.cuda.synchronize()
@@ -191,18 +319,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
-    rows_per_gpu = args.segments * args.rows
     value = rows_per_gpu * world * args.steps / el
     scan_avg_ms = float(np.mean(scan_ms))
     alg_bytes = fwd_bytes + dict_bytes
-    achieved = alg_bytes / (scan_avg_ms * 1e-3) / 1e9
+    achieved = plan_bytes / (scan_avg_ms * 1e-3) / 1e9
+    alg_achieved = alg_bytes / (scan_avg_ms * 1e-3) / 1e9
 
     cpu = parity = None
     if want_cpu and host_sample:
         from oracle.oracle import OracleEngine
+        from pinot_amd.plan import CPlan
         ht = Table(W["table"], host_sample)
         hq = parse(W["query"])
-        from pinot_amd.plan import CPlan
         orc = OracleEngine()
         cplan = CPlan(ht, hq, host_sample, list(range(1, len(host_sample) + 1)))
         legs = {}
@@ -214,20 +342,36 @@ def main():
         cpu = {"value": best["value"], "unit": "rows/s", "cores": best["threads"], "kind": "port",
                "label": "restated Pinot CPU path (oracle/pinot_oracle.c, per-segment operators)",
                "sample": f"{len(host_sample)} of the {args.segments} segments ({len(host_sample) * args.rows} rows), "
-                         f"same query; per-segment filter -> projection -> aggregation in C, segments as parallel "
-                         f"combine tasks; the value-keyed merge of the per-segment results is not timed",
+                         f"same query; per-segment filter (later AND children on the survivors) -> projection of the "
+                         f"matching docs -> aggregation in C, segments as parallel combine tasks; the value-keyed merge "
+                         f"of the per-segment results is not timed",
                "legs": legs, "nproc": nproc, "cores_available": cores, "cpu_model": cpu_model()}
-        if W["table"] != "events":  # parity on the sample (config 4's 5 M groups per segment are tested smaller)
-            o = orc.execute(ht, hq)
-            d = eng.run_plan(eng.make_plan(table, q, segments=segs[:len(host_sample)], flags=0))
+        if W["table"] != "events":  # parity on up to 16 sampled segments (value-keyed merge in Python)
+            ps = host_sample[:16]
+            o = orc.execute(Table(W["table"], ps), hq)
+            d = eng.run_plan(eng.make_plan(table, q, segments=segs[:len(ps)], flags=0))
             parity = bool(d.rows == o.rows and d.stats.num_docs_scanned == o.stats.num_docs_scanned)
+        else:  # config 4 on 2 full segments: the oracle's per-segment value sets merged by value (numpy), top rows
+            from pinot_amd.plan import reduce_to_rows
+            ps = host_sample[:2]
+            pp = CPlan(Table(W["table"], ps), hq, ps, [1, 2])
+            pk, pv = zip(*(orc.distinct_pairs(pp, i, sg) for i, sg in enumerate(ps)))
+            pair = np.unique(np.concatenate(pk) * (1 << 20) + np.concatenate(pv))
+            users, counts = np.unique(pair >> 20, return_counts=True)
+            top = np.lexsort((users, -counts))[:q.limit]
+            want = [[int(users[i]), int(counts[i])] for i in top]
+            d = eng.run_plan(eng.make_plan(table, q, segments=segs[:2], flags=0, trim=True))
+            parity = bool(reduce_to_rows(q, d)[1] == want)
 
     traffic = traffic_bytes = None
+    traffic_note = None
     tf = args.traffic_file or os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
     try:  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same command (tools/profile_bench.sh)
         tj = json.load(open(tf))
         tc = tj.get("config") or {}
-        if tc.get("rows_per_gpu") == rows_per_gpu and tc.get("workload") == W["desc"] and \
+        if tj.get("lib_md5") != lib_md5():
+            traffic_note = f"{os.path.relpath(tf, ROOT)} measured on another build: not used"
+        elif tc.get("rows_per_gpu") == rows_per_gpu and tc.get("workload") == W["desc"] and \
                 tj.get("traffic_bytes_per_launch"):
             traffic_bytes = float(tj["traffic_bytes_per_launch"])
             traffic = traffic_bytes / (scan_avg_ms * 1e-3) / 1e9
@@ -237,26 +381,29 @@ def main():
     if rank == 0:
         out = {
             "metric": W["metric"], "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "strong" if args.split_table else "weak",
             "vs_baseline": None, "dtype": "int64",
             "data": "synthetic (pinot_amd.synth, seed 42, Pinot segment format, device-generated)",
             "config": {"workload": W["desc"], "rows_per_gpu": rows_per_gpu, "segments_per_gpu": args.segments,
                        "rows_per_segment": args.rows,
                        "in_list_size": args.in_ids if args.workload == "adanalytics" else None,
-                       "parallelism": f"segments x{world}"},
+                       "parallelism": f"segments x{world}" + (" (table split)" if args.split_table else "")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "stream_kernel + scan_kernel" if tm.scan_launches > 1 else "scan_kernel",
                          "kernel_ms": scan_avg_ms,
-                         "algorithmic_bytes": alg_bytes,
+                         "plan_bytes": plan_bytes, "stage_docs": stage_docs,
+                         "algorithmic_bytes": alg_bytes, "algorithmic_frac": alg_achieved / HBM_PEAK_GBS,
                          "traffic_bytes_per_launch": traffic_bytes,
-                         # the bytes actually moved (PMC) over the same time: below `frac` when the AND short-circuits
-                         "traffic_frac": traffic / HBM_PEAK_GBS if traffic is not None else None},
+                         "traffic_frac": traffic / HBM_PEAK_GBS if traffic is not None else None,
+                         "traffic_note": traffic_note},
             "cpu_baseline": cpu,
             "parity_sample": parity,
             "step_breakdown_ms": {k: round(float(np.mean(v)), 4) for k, v in parts.items()},
             "host_plan_lowering_ms": round(lowering_ms, 3),
             "groups": len(res.rows), "docs_matched": res.stats.num_docs_scanned, "datagen_s": round(gen_s, 1),
+            "lib_md5": lib_md5(),
         }
         print(json.dumps(out), flush=True)
     if dist:

@@ -139,6 +139,27 @@ class OracleEngine:
         finally:
             self.lib.orc_result_free(out)
 
+    def distinct_pairs(self, plan: CPlan, si: int, seg: ImmutableSegment):
+        """(group key value, distinct value) pairs of one segment for a one-key, one-DISTINCTCOUNT plan: the
+        segment's per-group value sets (DistinctCountAggregationFunction's Set intermediate) as two int64 arrays, so a
+        caller can merge many segments by value without a Python object per group."""
+        cols = self.columns(seg, plan.table)
+        out = C.POINTER(orc_segment_result)()
+        threshold = min(self.array_based_threshold, plan.plan.num_groups_limit or self.array_based_threshold)
+        if self.lib.orc_execute_segment(C.byref(plan.plan), si, cols.arr, threshold, C.byref(out)):
+            raise RuntimeError("oracle failed")
+        try:
+            r = out.contents
+            A, G, nd = r.num_aggs, r.num_groups, r.num_distinct
+            kd = np.ctypeslib.as_array(r.key_dict_ids, shape=(max(G, 1),))[:G].astype(np.int64)
+            ga = np.ctypeslib.as_array(r.distinct_group_agg, shape=(max(nd, 1),))[:nd].astype(np.int64)
+            di = np.ctypeslib.as_array(r.distinct_dict_ids, shape=(max(nd, 1),))[:nd].astype(np.int64)
+            kcol = seg.columns[plan.query.group_by[0]].dictionary.values
+            vcol = seg.columns[plan.aggs[0].arg.cols[0]].dictionary.values
+            return np.asarray(kcol, dtype=np.int64)[kd[ga // A]], np.asarray(vcol, dtype=np.int64)[di]
+        finally:
+            self.lib.orc_result_free(out)
+
     def time_segments(self, plan: CPlan, segments: Sequence[ImmutableSegment], threads: int, seconds: float):
         """Throughput of the per-segment operators alone (filter -> projection -> aggregation / group-by of every
         segment, C, `threads` segments in flight as Pinot's combine worker tasks run them; the value-keyed merge is

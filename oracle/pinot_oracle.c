@@ -112,6 +112,24 @@ static int32_t *sv_dict_ids(const orc_column *c) {
   return ids;
 }
 
+/* The dictIds of the matching docs only, in doc order (DataFetcher.ColumnValueReader.readDictIds over a block's docIds,
+ * common/DataFetcher.java:452-521: the projection reads the forward index at the filter's survivors). */
+static int32_t *sv_dict_ids_at(const orc_column *c, const uint32_t *docs, uint64_t n) {
+  int32_t *ids = (int32_t *)malloc(sizeof(int32_t) * (n ? n : 1));
+  if (c->fwd_kind == ORC_FWD_SV) {
+    for (uint64_t i = 0; i < n; i++) ids[i] = (int32_t)read_bits(c->fwd, docs[i], c->bits);
+  } else if (c->fwd_kind == ORC_FWD_RAW) {
+    for (uint64_t i = 0; i < n; i++) ids[i] = (int32_t)docs[i];
+  } else {  /* sorted: walk the (start, end) pairs alongside the ascending docs (SortedIndexReaderImpl.getDictId) */
+    uint32_t id = 0;
+    for (uint64_t i = 0; i < n; i++) {
+      while (id + 1 < c->cardinality && (int32_t)be32(c->fwd + 8ull * id + 4) < (int32_t)docs[i]) id++;
+      ids[i] = (int32_t)id;
+    }
+  }
+  return ids;
+}
+
 /* MV row offsets from the start-of-row bitmap (FixedBitMVForwardIndexReader.java:61-75, getNumValuesMV
  * :167-204): docsPerChunk = ceil((float) 2048 / (numValues / numDocs)); chunk offsets header, then a
  * bitmap of numValues bits with a set bit at each row start, then the packed values. */
@@ -297,33 +315,48 @@ static void eval_range_index(const pg_leaf *l, const orc_column *c, uint32_t num
   free(ids);
 }
 
-static void eval_leaf(const pg_leaf *l, const orc_column *cols, uint32_t num_docs, uint8_t *out,
+/* One leaf -> doc flags over the candidate docs `cand` (NULL = every doc; flags of other docs are 0).  Scan leaves
+ * read only the candidates' values: SVScanDocIdIterator.applyAnd (dociditerators/SVScanDocIdIterator.java:106-125)
+ * evaluates a later AND child on the docs the earlier children kept, and entries scanned count those docs. */
+static void eval_leaf(const pg_leaf *l, const orc_column *cols, uint32_t num_docs, const uint8_t *cand, uint8_t *out,
                       uint64_t *entries_scanned) {
   const orc_column *c = &cols[l->col_id];
+  const uint8_t ex = (uint8_t)(l->exclusive != 0);
   switch (l->kind) {
-    case PG_LEAF_RANGE_INDEX: eval_range_index(l, c, num_docs, out, entries_scanned); return;
+    case PG_LEAF_RANGE_INDEX: eval_range_index(l, c, num_docs, out, entries_scanned); break;
     case PG_LEAF_RAW_SCAN:
-      for (uint32_t d = 0; d < num_docs; d++) out[d] = (uint8_t)(raw_leaf_match(l, c, d) ^ (l->exclusive != 0));
-      *entries_scanned += num_docs;
+      for (uint32_t d = 0; d < num_docs; d++) {
+        if (cand && !cand[d]) { out[d] = 0; continue; }
+        out[d] = (uint8_t)(raw_leaf_match(l, c, d) ^ ex);
+        (*entries_scanned)++;
+      }
       return;
-    case PG_LEAF_MATCH_ALL: memset(out, 1, num_docs); return;
-    case PG_LEAF_EMPTY: memset(out, 0, num_docs); return;
-    case PG_LEAF_SV_SCAN: {
-      int32_t *ids = sv_dict_ids(c);
-      for (uint32_t d = 0; d < num_docs; d++) out[d] = (uint8_t)(leaf_in_set(l, ids[d]) ^ (l->exclusive != 0));
-      *entries_scanned += num_docs;
-      free(ids);
+    case PG_LEAF_MATCH_ALL: memset(out, 1, num_docs); break;
+    case PG_LEAF_EMPTY: memset(out, 0, num_docs); break;
+    case PG_LEAF_SV_SCAN:
+      if (c->fwd_kind == ORC_FWD_SORTED) {
+        int32_t *ids = sv_dict_ids(c);
+        for (uint32_t d = 0; d < num_docs; d++) out[d] = (uint8_t)((!cand || cand[d]) && (leaf_in_set(l, ids[d]) ^ ex));
+        *entries_scanned += num_docs;
+        free(ids);
+        return;
+      }
+      for (uint32_t d = 0; d < num_docs; d++) {
+        if (cand && !cand[d]) { out[d] = 0; continue; }
+        out[d] = (uint8_t)(leaf_in_set(l, (int32_t)read_bits(c->fwd, d, c->bits)) ^ ex);
+        (*entries_scanned)++;
+      }
       return;
-    }
     case PG_LEAF_MV_SCAN: {
       mv_view v;
       mv_open(c, &v);
       for (uint32_t d = 0; d < num_docs; d++) {
+        if (cand && !cand[d]) { out[d] = 0; continue; }
         int any = 0;
         for (uint64_t i = v.offsets[d]; i < v.offsets[d + 1]; i++) {
           if (leaf_in_set(l, (int32_t)read_bits(v.raw, i, c->bits))) { any = 1; break; }
         }
-        out[d] = (uint8_t)(any ^ (l->exclusive != 0));
+        out[d] = (uint8_t)(any ^ ex);
         *entries_scanned += v.offsets[d + 1] - v.offsets[d];
       }
       free(v.offsets);
@@ -336,9 +369,9 @@ static void eval_leaf(const pg_leaf *l, const orc_column *cols, uint32_t num_doc
         int32_t s = (int32_t)be32(c->fwd + 8ull * id), e = (int32_t)be32(c->fwd + 8ull * id + 4);
         for (int32_t d = s; d <= e; d++) out[d] = 1;
       }
-      if (l->exclusive)
+      if (ex)
         for (uint32_t d = 0; d < num_docs; d++) out[d] ^= 1;
-      return;
+      break;
     }
     case PG_LEAF_INVERTED: {
       memset(out, 0, num_docs);
@@ -350,45 +383,104 @@ static void eval_leaf(const pg_leaf *l, const orc_column *cols, uint32_t num_doc
         uint32_t o = be32(c->inv + 4ull * id);
         roaring_or_into(bitmaps + (o - first), out, num_docs);
       }
-      if (l->exclusive)
+      if (ex)
         for (uint32_t d = 0; d < num_docs; d++) out[d] ^= 1;
-      return;
+      break;
     }
+  }
+  if (cand)  /* index leaves are materialised whole (sorted ranges / roaring bitmaps), then intersected */
+    for (uint32_t d = 0; d < num_docs; d++) out[d] &= cand[d];
+}
+
+/* Filter tree from the postfix program: AndFilterOperator / OrFilterOperator / NotFilterOperator
+ * (filter/AndFilterOperator.java:42-49, OrFilterOperator.java:44-82, NotFilterOperator.java:53-77). */
+typedef struct { int kind; int leaf; int nk; int *kids; } orc_fnode;  /* kind 0 leaf, 1 AND, 2 OR, 3 NOT */
+
+/* FilterOperatorUtils.reorderAndFilterChildOperators (operator/filter/FilterOperatorUtils.java:160-224): sorted index 0,
+ * bitmap 1, range index 2, AND 3, OR 4, NOT as its child, SV scan 5, MV scan 6. */
+static int node_priority(const orc_fnode *nodes, int n, const pg_leaf *leaves) {
+  const orc_fnode *x = &nodes[n];
+  if (x->kind == 1) return 3;
+  if (x->kind == 2) return 4;
+  if (x->kind == 3) return node_priority(nodes, x->kids[0], leaves);
+  switch (leaves[x->leaf].kind) {
+    case PG_LEAF_SORTED: return 0;
+    case PG_LEAF_INVERTED: return 1;
+    case PG_LEAF_RANGE_INDEX: return 2;
+    case PG_LEAF_MV_SCAN: return 6;
+    case PG_LEAF_MATCH_ALL: case PG_LEAF_EMPTY: return -1;  /* removed from the AND / short-circuit it */
+    default: return 5;
   }
 }
 
-/* Postfix program over leaf doc-sets: AndFilterOperator / OrFilterOperator / NotFilterOperator
- * (filter/AndFilterOperator.java:42-49, OrFilterOperator.java:44-82, NotFilterOperator.java:53-77). */
+static void eval_node(const orc_fnode *nodes, int n, const pg_leaf *leaves, const orc_column *cols, uint32_t num_docs,
+                      const uint8_t *cand, uint8_t *out, uint64_t *entries_scanned) {
+  const orc_fnode *x = &nodes[n];
+  if (x->kind == 0) { eval_leaf(&leaves[x->leaf], cols, num_docs, cand, out, entries_scanned); return; }
+  if (x->kind == 3) {
+    uint8_t *t = (uint8_t *)malloc(num_docs ? num_docs : 1);
+    eval_node(nodes, x->kids[0], leaves, cols, num_docs, cand, t, entries_scanned);
+    for (uint32_t d = 0; d < num_docs; d++) out[d] = (uint8_t)((!cand || cand[d]) && !t[d]);
+    free(t);
+    return;
+  }
+  if (x->kind == 1) {  /* AND: children in priority order, each over the docs the earlier ones kept */
+    int order[64] = {0}, nk = x->nk < 64 ? x->nk : 64;
+    for (int i = 0; i < nk; i++) order[i] = x->kids[i];
+    for (int i = 1; i < nk; i++)  /* stable insertion sort by priority */
+      for (int j = i; j > 0 && node_priority(nodes, order[j], leaves) < node_priority(nodes, order[j - 1], leaves); j--) {
+        int t = order[j]; order[j] = order[j - 1]; order[j - 1] = t;
+      }
+    uint8_t *t = (uint8_t *)malloc(num_docs ? num_docs : 1);
+    eval_node(nodes, order[0], leaves, cols, num_docs, cand, out, entries_scanned);
+    for (int i = 1; i < nk; i++) {
+      eval_node(nodes, order[i], leaves, cols, num_docs, out, t, entries_scanned);
+      memcpy(out, t, num_docs);
+    }
+    free(t);
+    return;
+  }
+  /* OR: each child over the candidates, united */
+  uint8_t *t = (uint8_t *)malloc(num_docs ? num_docs : 1);
+  eval_node(nodes, x->kids[0], leaves, cols, num_docs, cand, out, entries_scanned);
+  for (int i = 1; i < x->nk; i++) {
+    eval_node(nodes, x->kids[i], leaves, cols, num_docs, cand, t, entries_scanned);
+    for (uint32_t d = 0; d < num_docs; d++) out[d] |= t[d];
+  }
+  free(t);
+}
+
 static int eval_filter(const pg_plan *plan, const pg_leaf *leaves, const orc_column *cols, uint32_t num_docs,
                        uint8_t *match, uint64_t *entries_scanned) {
   if (plan->num_ops == 0) { memset(match, 1, num_docs); return 0; }
-  uint8_t **stack = (uint8_t **)calloc(plan->num_ops + 1, sizeof(uint8_t *));
-  int sp = 0;
+  orc_fnode *nodes = (orc_fnode *)calloc(plan->num_ops, sizeof(orc_fnode));
+  int *kids = (int *)calloc(plan->num_ops * 2 + 1, sizeof(int));
+  int *st = (int *)calloc(plan->num_ops + 1, sizeof(int));
+  int nn = 0, sp = 0, nkids = 0;
   for (uint32_t i = 0; i < plan->num_ops; i++) {
     int32_t op = plan->ops[i];
+    orc_fnode *x = &nodes[nn];
     if (op >= 0) {
-      uint8_t *f = (uint8_t *)malloc(num_docs ? num_docs : 1);
-      eval_leaf(&leaves[op], cols, num_docs, f, entries_scanned);
-      stack[sp++] = f;
+      x->kind = 0;
+      x->leaf = op;
     } else if (op == PG_OP_NOT) {
-      uint8_t *f = stack[sp - 1];
-      for (uint32_t d = 0; d < num_docs; d++) f[d] ^= 1;
+      x->kind = 3;
+      x->nk = 1;
+      x->kids = kids + nkids;
+      kids[nkids++] = st[--sp];
     } else {
       int n = (-op) & 0xFF;
-      int is_and = ((-op) & 0x100) != 0;
-      uint8_t *dst = stack[sp - n];
-      for (int k = 1; k < n; k++) {
-        uint8_t *src = stack[sp - n + k];
-        if (is_and) for (uint32_t d = 0; d < num_docs; d++) dst[d] &= src[d];
-        else for (uint32_t d = 0; d < num_docs; d++) dst[d] |= src[d];
-        free(src);
-      }
-      sp -= n - 1;
+      x->kind = ((-op) & 0x100) ? 1 : 2;
+      x->nk = n;
+      x->kids = kids + nkids;
+      for (int k = 0; k < n; k++) kids[nkids + k] = st[sp - n + k];
+      nkids += n;
+      sp -= n;
     }
+    st[sp++] = nn++;
   }
-  memcpy(match, stack[0], num_docs);
-  free(stack[0]);
-  free(stack);
+  eval_node(nodes, st[0], leaves, cols, num_docs, NULL, match, entries_scanned);
+  free(st); free(kids); free(nodes);
   return 0;
 }
 
@@ -403,12 +495,12 @@ typedef struct agg_input {
 /* Transform value: TransformFunction.transformToDoubleValuesSV; MultiplicationTransformFunction
  * (transform/function/MultiplicationTransformFunction.java:91-111) starts from the literal product 1.0
  * and multiplies the arguments in order. */
-static inline double agg_value(const pg_agg *a, const orc_column *cols, const agg_input *in, uint32_t d) {
-  double va = dict_double(&cols[a->col_a], in->ids_a[d]);
+static inline double agg_value(const pg_agg *a, const orc_column *cols, const agg_input *in, uint64_t i) {
+  double va = dict_double(&cols[a->col_a], in->ids_a[i]);
   switch (a->op) {
-    case PG_EXPR_MUL: { double p = 1.0; p = p * va; p = p * dict_double(&cols[a->col_b], in->ids_b[d]); return p; }
-    case PG_EXPR_ADD: return va + dict_double(&cols[a->col_b], in->ids_b[d]);
-    case PG_EXPR_SUB: return va - dict_double(&cols[a->col_b], in->ids_b[d]);
+    case PG_EXPR_MUL: { double p = 1.0; p = p * va; p = p * dict_double(&cols[a->col_b], in->ids_b[i]); return p; }
+    case PG_EXPR_ADD: return va + dict_double(&cols[a->col_b], in->ids_b[i]);
+    case PG_EXPR_SUB: return va - dict_double(&cols[a->col_b], in->ids_b[i]);
     default: return va;
   }
 }
@@ -451,13 +543,13 @@ static void aggregate_only(const pg_plan *plan, const orc_column *cols, const ui
         }
         case PG_AGG_SUM: { /* running double sum carried through the holder (SumAggregationFunction.java:82-124) */
           double s = r->values[a];
-          for (uint64_t i = b0; i < b1; i++) s += agg_value(g, cols, in, docs[i]);
+          for (uint64_t i = b0; i < b1; i++) s += agg_value(g, cols, in, i);
           r->values[a] = s;
           break;
         }
         case PG_AGG_AVG: { /* block-local sum, then AvgPair.apply (AvgAggregationFunction.java:76-82,132-139) */
           double s = 0.0;
-          for (uint64_t i = b0; i < b1; i++) s += agg_value(g, cols, in, docs[i]);
+          for (uint64_t i = b0; i < b1; i++) s += agg_value(g, cols, in, i);
           r->values[a] += s;
           r->counts[a] += (int64_t)len;
           break;
@@ -467,16 +559,16 @@ static void aggregate_only(const pg_plan *plan, const orc_column *cols, const ui
           double m;
           if (g->op == PG_EXPR_COL && is_integer_type(cols[g->col_a].data_type)) {
             /* integer path: Math.min over int/long values, then with the double holder */
-            double v0 = dict_double(&cols[g->col_a], in->ids_a[docs[b0]]);
+            double v0 = dict_double(&cols[g->col_a], in->ids_a[b0]);
             m = v0;
             for (uint64_t i = b0; i < b1; i++) {
-              double v = dict_double(&cols[g->col_a], in->ids_a[docs[i]]);
+              double v = dict_double(&cols[g->col_a], in->ids_a[i]);
               m = is_min ? (v < m ? v : m) : (v > m ? v : m);
             }
           } else {
-            m = agg_value(g, cols, in, docs[b0]);
+            m = agg_value(g, cols, in, b0);
             for (uint64_t i = b0; i < b1; i++) {
-              double v = agg_value(g, cols, in, docs[i]);
+              double v = agg_value(g, cols, in, i);
               m = is_min ? fmin(v, m) : fmax(v, m);
             }
           }
@@ -484,7 +576,7 @@ static void aggregate_only(const pg_plan *plan, const orc_column *cols, const ui
           break;
         }
         case PG_AGG_DISTINCTCOUNT:
-          for (uint64_t i = b0; i < b1; i++) distinct[a][in->ids_a[docs[i]]] = 1;
+          for (uint64_t i = b0; i < b1; i++) distinct[a][in->ids_a[i]] = 1;
           break;
       }
     }
@@ -643,14 +735,13 @@ static void aggregate_group_by(const pg_plan *plan, const orc_column *cols, cons
   uint8_t *seen = array_based ? (uint8_t *)calloc(upper ? upper : 1, 1) : NULL;
   int32_t tuple[64];
   for (uint64_t i = 0; i < n; i++) {
-    uint32_t d = docs[i];
     if (overflow) {
-      for (uint32_t k = 0; k < K; k++) tuple[k] = key_ids[k][d];
+      for (uint32_t k = 0; k < K; k++) tuple[k] = key_ids[k][i];
       gids[i] = tuple_get_or_put(&tm, tuple, limit);
       continue;
     }
     uint64_t raw = 0;
-    for (int k = (int)K - 1; k >= 0; k--) raw = raw * cards[k] + (uint64_t)key_ids[k][d];
+    for (int k = (int)K - 1; k >= 0; k--) raw = raw * cards[k] + (uint64_t)key_ids[k][i];
     if (array_based) { gids[i] = (int32_t)raw; seen[raw] = 1; }
     else gids[i] = map_get_or_put(&m, raw, limit);
   }
@@ -682,12 +773,12 @@ static void aggregate_group_by(const pg_plan *plan, const orc_column *cols, cons
       switch (ag->fn) {
         case PG_AGG_COUNT: *v += 1.0; break;
         case PG_AGG_COUNTMV: *v += (double)(inputs[a].mv.offsets[d + 1] - inputs[a].mv.offsets[d]); break;
-        case PG_AGG_SUM: *v += agg_value(ag, cols, &inputs[a], d); break;
-        case PG_AGG_AVG: *v += agg_value(ag, cols, &inputs[a], d); cnts[(uint64_t)g * A + a] += 1; break;
-        case PG_AGG_MIN: { double x = agg_value(ag, cols, &inputs[a], d); if (x < *v) *v = x; break; }
-        case PG_AGG_MAX: { double x = agg_value(ag, cols, &inputs[a], d); if (x > *v) *v = x; break; }
+        case PG_AGG_SUM: *v += agg_value(ag, cols, &inputs[a], i); break;
+        case PG_AGG_AVG: *v += agg_value(ag, cols, &inputs[a], i); cnts[(uint64_t)g * A + a] += 1; break;
+        case PG_AGG_MIN: { double x = agg_value(ag, cols, &inputs[a], i); if (x < *v) *v = x; break; }
+        case PG_AGG_MAX: { double x = agg_value(ag, cols, &inputs[a], i); if (x > *v) *v = x; break; }
         case PG_AGG_DISTINCTCOUNT:
-          pairs[np++] = (((uint64_t)g * A + a) << 32) | (uint32_t)inputs[a].ids_a[d];
+          pairs[np++] = (((uint64_t)g * A + a) << 32) | (uint32_t)inputs[a].ids_a[i];
           break;
       }
     }
@@ -864,13 +955,13 @@ int orc_execute_segment(const pg_plan *plan, uint32_t seg, const orc_column *col
     const pg_agg *g = &plan->aggs[a];
     if (g->fn == PG_AGG_COUNT) continue;
     if (g->fn == PG_AGG_COUNTMV) { mv_open(&cols[g->col_a], &inputs[a].mv); inputs[a].has_mv = 1; used[g->col_a] = 1; continue; }
-    inputs[a].ids_a = sv_dict_ids(&cols[g->col_a]);
+    inputs[a].ids_a = sv_dict_ids_at(&cols[g->col_a], docs, n);
     used[g->col_a] = 1;
-    if (g->op != PG_EXPR_COL) { inputs[a].ids_b = sv_dict_ids(&cols[g->col_b]); used[g->col_b] = 1; }
+    if (g->op != PG_EXPR_COL) { inputs[a].ids_b = sv_dict_ids_at(&cols[g->col_b], docs, n); used[g->col_b] = 1; }
   }
   int32_t *key_ids[64] = {0};
   for (uint32_t k = 0; k < plan->num_keys; k++) {
-    key_ids[k] = sv_dict_ids(&cols[plan->keys[k].col_id]);
+    key_ids[k] = sv_dict_ids_at(&cols[plan->keys[k].col_id], docs, n);
     used[plan->keys[k].col_id] = 1;
   }
   for (int i = 0; i < 256; i++) projected += used[i];

@@ -111,7 +111,8 @@ class pg_timing(C.Structure):
 EXPORTED = ["pg_init", "pg_last_error", "pg_resident_bytes", "pg_cancel", "pg_abi_version", "pg_column_upload",
             "pg_segment_release", "pg_execute", "pg_result_free", "pg_execute_partial", "pg_partials_finalize",
             "pg_partials_free", "pg_partials_copy", "pg_partials_export", "pg_partials_create", "pg_partials_merge",
-            "pg_key_owner", "pg_last_timing"]
+            "pg_key_owner", "pg_last_timing", "pg_chunk_decompress"]
+PG_CODEC_PASS_THROUGH, PG_CODEC_SNAPPY, PG_CODEC_ZSTANDARD, PG_CODEC_LZ4, PG_CODEC_LZ4_LENGTH_PREFIXED = 0, 1, 2, 3, 4
 PG_COPY_OUT, PG_COPY_IN = 0, 1
 
 
@@ -139,6 +140,7 @@ def declare(lib):
         "pg_partials_create": ([P(pg_partials), C.c_uint64, P(P(pg_partials))], C.c_int),
         "pg_partials_merge": ([P(pg_partials), C.c_void_p, C.c_uint64, C.c_void_p], C.c_int),
         "pg_key_owner": ([C.c_uint64, C.c_uint32], C.c_uint32),
+        "pg_chunk_decompress": ([C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, P(C.c_uint64)], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(lib, name)

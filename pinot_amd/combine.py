@@ -14,8 +14,10 @@ their partial states over RCCL / xGMI in one of two ways:
     every rank exports its groups as rows bucketed by owner rank (pg_partials_export, owner = pg_key_owner(key)),
     the buckets go to their owners in one all_to_all, each owner inserts-and-merges what it received into a fresh
     table (pg_partials_merge: SUM / MIN / MAX / OR per state), finalizes ITS keys (ORDER BY trim included), and the
-    per-owner results -- disjoint key sets -- are gathered to every rank.  Per-link traffic is (N-1)/N of one
-    rank's groups instead of N copies of the key space.
+    per-owner results -- disjoint key sets, packed as flat byte buffers (keys, values, counts, value sets) -- are
+    all-gathered to every rank as device buffers.  Per-link traffic is (N-1)/N of one rank's groups instead of N
+    copies of the key space.  A library error on one rank (e.g. a merge table over the state budget) is agreed on by
+    an all-reduce before the next collective, so every rank raises instead of the others waiting forever.
 
 Statistics (ExecutionStatistics) are summed with one all_reduce.  `gather_merge_results` merges value-keyed host
 results (oracle / DataTable-level) with the reference's AggregationFunction.merge (pinot_amd.plan.merge_intermediate).
@@ -109,25 +111,84 @@ def merge_partials_across_ranks(engine, plan, p, group=None) -> IntermediateResu
     return _exchange_rows(engine, plan, p, stats, group, dev)
 
 
+def _agree(err, group, dev):
+    """MAX-all-reduce of an error flag: every rank learns that some rank's library call failed (then all raise)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if err is not None else 0], dtype=torch.int64, device=dev)
+    c = _comm(t, group)
+    dist.all_reduce(c, op=dist.ReduceOp.MAX, group=group)
+    if err is not None:
+        raise err
+    if int(c.item()):
+        raise RuntimeError("the cross-GPU merge failed on another rank")
+
+
+def _pack_result(ra) -> np.ndarray:
+    """One rank's finalized result arrays as a flat byte buffer: [G, K, A, num_distinct, has_sets, 6 stats] int64 |
+    keys uint32 | values float64 | counts int64 | offsets uint64 | ids uint32 (8-byte aligned sections)."""
+    has = ra["offsets"] is not None
+    nd = len(ra["ids"]) if has else 0
+    parts = [np.array([ra["G"], ra["K"], ra["A"], nd, int(has)], dtype=np.int64), ra["stats"].astype(np.int64),
+             ra["keys"].astype(np.uint32).ravel(), ra["values"].astype(np.float64).ravel(),
+             ra["counts"].astype(np.int64).ravel()]
+    if has:
+        parts += [ra["offsets"].astype(np.uint64), ra["ids"].astype(np.uint32)]
+    out = bytearray()
+    for a in parts:
+        b = a.tobytes()
+        out += b + bytes((-len(b)) % 8)
+    return np.frombuffer(bytes(out), dtype=np.uint8)
+
+
+def _unpack_result(buf: np.ndarray) -> dict:
+    b = buf.tobytes()
+    pos = 0
+
+    def take(dtype, n):
+        nonlocal pos
+        a = np.frombuffer(b, dtype=dtype, count=n, offset=pos).copy()
+        pos += -(-a.nbytes // 8) * 8
+        return a
+    G, K, A, nd, has = (int(x) for x in take(np.int64, 5))
+    stats = take(np.int64, 6)
+    keys = take(np.uint32, G * K).reshape(G, K)
+    vals = take(np.float64, G * A).reshape(G, A)
+    cnts = take(np.int64, G * A).reshape(G, A)
+    offs = take(np.uint64, G * A + 1) if has else None
+    ids = take(np.uint32, nd) if has else None
+    return {"G": G, "K": K, "A": A, "keys": keys, "values": vals, "counts": cnts, "offsets": offs, "ids": ids,
+            "stats": stats}
+
+
 def _exchange_rows(engine, plan, p, stats, group, dev) -> IntermediateResult:
     import torch
     import torch.distributed as dist
     pc = p.contents
     world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
     rb = pc.row_bytes
     gloo = _is_gloo(group)
+    err = q = None
+    counts, send = [0] * world, None
     try:
         counts = engine.export_rows(p, world)  # rows per owner rank
-        sc = torch.tensor(counts, dtype=torch.int64, device="cpu" if gloo else dev)
-        rcounts = torch.empty_like(sc)
-        dist.all_to_all_single(rcounts, sc, group=group)
-        rcounts = rcounts.tolist()
+    except Exception as e:  # noqa: BLE001 -- agreed on below, re-raised on every rank
+        err = e
+        engine.lib.pg_partials_free(p)
+    _agree(err, group, dev)
+    sc = torch.tensor(counts, dtype=torch.int64, device="cpu" if gloo else dev)
+    rcounts = torch.empty_like(sc)
+    dist.all_to_all_single(rcounts, sc, group=group)
+    rcounts = rcounts.tolist()
+    try:
         q = engine.create_like(p, max(sum(rcounts), 1))
         send = torch.empty(max(sum(counts), 1) * rb, dtype=torch.uint8, device=dev)
         engine.export_rows(p, world, C.c_void_p(send.data_ptr()), sum(counts))
+    except Exception as e:  # noqa: BLE001
+        err = e
     finally:
         engine.lib.pg_partials_free(p)
+    _agree(err, group, dev)
     recv = torch.empty(max(sum(rcounts), 1) * rb, dtype=torch.uint8, device=dev)
     s_in, r_in = (send.cpu(), torch.empty(recv.numel(), dtype=torch.uint8)) if gloo else (send, recv)
     dist.all_to_all_single(r_in[:sum(rcounts) * rb], s_in[:sum(counts) * rb],
@@ -138,18 +199,36 @@ def _exchange_rows(engine, plan, p, stats, group, dev) -> IntermediateResult:
     st = _comm(stats, group)
     dist.all_reduce(st, op=dist.ReduceOp.SUM, group=group)
     torch.cuda.synchronize()
-    engine.merge_rows(q, C.c_void_p(recv.data_ptr()), sum(rcounts))
-    for f, v in zip(_STATS_FIELDS, st.cpu().tolist()):
-        setattr(q.contents.stats, f, int(v))
-    mine = engine.finalize_partial(plan, q)  # this rank's keys (their ORDER BY trim included)
-    parts = [None] * world
-    dist.all_gather_object(parts, mine.rows, group=group)
+    ra = None
+    try:
+        engine.merge_rows(q, C.c_void_p(recv.data_ptr()), sum(rcounts))
+        for f, v in zip(_STATS_FIELDS, st.cpu().tolist()):
+            setattr(q.contents.stats, f, int(v))
+        ra = engine.finalize_arrays(plan, q)  # this rank's keys (their ORDER BY trim included); frees q
+        q = None
+    except Exception as e:  # noqa: BLE001
+        err = e
+    finally:
+        if q is not None:
+            engine.lib.pg_partials_free(q)
+    _agree(err, group, dev)
+    # the owners' results (disjoint key sets) to every rank: sizes, then one all_gather of padded byte buffers
+    mine = _pack_result(ra)
+    sizes = _all_gather_ints([mine.size], group, dev)
+    mx = max(s[0] for s in sizes)
+    buf = torch.zeros(mx, dtype=torch.uint8, device="cpu" if gloo else dev)
+    buf[:mine.size] = torch.from_numpy(mine.copy())
+    outs = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(outs, buf, group=group)
     rows = {}
-    for r in parts:  # owners hold disjoint key sets
-        rows.update(r)
+    res = None
+    for o, sz in zip(outs, sizes):
+        res = engine.decode(plan, _unpack_result(o[:sz[0]].cpu().numpy()))
+        rows.update(res.rows)
     if not plan.query.group_by and () not in rows:  # no rank matched a doc
-        rows[()] = default_row(mine.aggregations)
-    return IntermediateResult(mine.aggregations, mine.group_by, rows, mine.stats)
+        rows[()] = default_row(res.aggregations)
+    # every owner carries the statistics summed over the ranks
+    return IntermediateResult(res.aggregations, res.group_by, rows, ExecutionStats(*(int(x) for x in ra["stats"])))
 
 
 def gather_merge_results(res: IntermediateResult, group=None) -> IntermediateResult:

@@ -15,7 +15,7 @@
 // so the group's bits start word-aligned.  Output word g: bit 31-j <-> doc 32g+j (the packed 1-bit column order).
 #include <hip/hip_runtime.h>
 
-#include "pg_internal.h"
+#include "pg_aux.h"
 
 namespace pg {
 

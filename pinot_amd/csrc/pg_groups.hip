@@ -15,7 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
-#include "pg_internal.h"
+#include "pg_aux.h"
 
 namespace pg {
 

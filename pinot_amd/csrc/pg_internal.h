@@ -237,179 +237,10 @@ __host__ __device__ inline double order_key_decode(int64_t k) {
 }
 
 
-// ---- kernel launchers
+// ---- the fused scan (pg_scan.hip).  Everything else the runtime launches is declared in pg_aux.h, so that the scan's
+// nine shapes (a ~15 minute build) recompile only when this header changes.
 hipError_t launch_scan(const QuerySpec& q, uint32_t blocks, hipStream_t s);                  // pg_scan.hip
 size_t scan_lds_bytes(const QuerySpec& q);
 uint32_t scan_min_blocks_per_cu(bool grouped);
-hipError_t launch_bswap_words(const uint8_t* src, uint32_t* dst, uint64_t nbytes, uint64_t nwords_out, hipStream_t s);
-hipError_t launch_be_to_native(const uint8_t* src, void* dst, uint64_t n, uint32_t width, hipStream_t s);
-hipError_t launch_sorted_to_packed(const int32_t* pairs, uint32_t card, uint32_t num_docs, uint32_t bits,
-                                   uint32_t* words, uint64_t nwords, hipStream_t s);
-hipError_t launch_decode_pack(const uint32_t* ids, uint32_t bits, const void* dict, uint32_t dtype, uint32_t card,
-                              int64_t vmin, uint32_t vbits, uint32_t num_docs, uint32_t* out, uint64_t nwords,
-                              hipStream_t s);
-hipError_t launch_dict_bits(const void* dict, uint32_t dtype, uint32_t card, int64_t base, const int32_t* keymap,
-                            uint32_t key_card, uint32_t* bits, unsigned int* err, hipStream_t s);
-hipError_t launch_mv_offsets(const uint32_t* bitmap_words, uint64_t num_values, uint32_t num_docs,
-                             uint32_t* offsets, void* scratch, size_t scratch_bytes, hipStream_t s);
-size_t mv_offsets_scratch_bytes(uint64_t num_values);
-hipError_t launch_fill_ranges(const int32_t* ranges /*[n][2] inclusive, sorted, disjoint*/, uint32_t n,
-                              uint32_t num_docs, uint32_t* bitmap, hipStream_t s);
-struct RoaringContainer {
-  uint32_t key;      // high 16 bits of the doc ids
-  uint32_t type;     // 0 array, 1 bitmap, 2 run
-  uint32_t card;     // array: cardinality; run: number of runs
-  uint32_t offset;   // byte offset of the payload within the column's roaring region
-};
-hipError_t launch_roaring_or(const uint8_t* roaring, const RoaringContainer* containers, const uint32_t* sel,
-                             uint32_t nsel, uint32_t num_docs, uint32_t* bitmap, hipStream_t s);
-hipError_t launch_bitmap_not(uint32_t* bitmap, uint32_t num_docs, hipStream_t s);
-hipError_t launch_mv_scan(const uint32_t* words, uint32_t bits, const uint32_t* offsets, uint32_t num_docs,
-                          int32_t lo, int32_t hi, const uint32_t* lut, uint32_t excl, uint32_t* bitmap,
-                          hipStream_t s);
-struct LutJob {            // set bits ids[0..n) in lut and ids >> shift in region (one batched launch per query)
-  const int32_t* ids;
-  uint32_t* lut;             // exact bitmap over dictIds, or null
-  uint32_t* region;          // LDS-set filter bitmap over dictId >> shift, or null
-  uint32_t n;
-  uint32_t shift;
-};
-hipError_t launch_set_lut_bits(const LutJob* jobs, uint32_t njobs, hipStream_t s);
-
-// ---- streaming pre-filter (pg_filter.hip): one leaf of the root AND over the segments whose form of it reads
-// `bits`-bit values, into (first) or AND-ed into (later) one doc bitmap per segment
-constexpr uint32_t kPreItemGroups = 8192;   // 32-doc groups per pre-filter work item (262 144 docs)
-struct PreSpec {
-  uint32_t num_items, leaf, first, set_lds_ints;
-  const SegDesc* segs;
-  const WorkItem* items;          // tile_begin / tile_end in 32-doc groups
-  uint32_t* const* out;           // [seg] bitmap words, packed 1-bit column order
-};
-hipError_t launch_prefilter(const PreSpec& p, uint32_t bits, uint32_t blocks, hipStream_t s);
-
-// ---- selective stream (pg_filter.hip): the driving leaf of the root AND (a packed scan leaf passing few docs) over
-// every segment, bit width a template parameter, values loaded straight into registers; the survivors' doc ids are
-// compacted into one region per item, which the scan kernel then consumes in list mode
-constexpr int kMaxStreamExtra = 3;
-struct StreamSpec {
-  uint32_t num_items, leaf, cap, set_lds_ints;
-  uint32_t num_extra;                 // further leaves of the root AND tested in the stream, on the survivors only
-  uint32_t interleave;                // block b streams items first + b + k * gridDim.x (first = block_first[0], end =
-                                      // block_first[gridDim.x]); else the range [block_first[b], block_first[b + 1])
-  uint32_t extra[kMaxStreamExtra];    // (runtime bit width: per-doc windows, like the scan's gathered leaves)
-  const SegDesc* segs;
-  const WorkItem* items;          // tile_begin / tile_end in 32-doc groups
-  const uint32_t* block_first;    // [gridDim.x + 1]: block b streams items [block_first[b], block_first[b + 1])
-  uint32_t* docs;                 // [num_items][cap]
-  uint32_t* counts;               // [num_items] survivors written (<= cap)
-  unsigned int* err;              // bit 3: some item had more than `cap` survivors
-  // exact mode (1 024-thread blocks, one per CU): a coarse IN bitmap's exact LUT (exact_nwords[seg] words, <= 128 KiB)
-  // is staged whole in LDS, so no value is a candidate to resolve
-  const uint32_t* exact_nwords;
-};
-hipError_t launch_stream(const StreamSpec& p, uint32_t bits, uint32_t blocks, hipStream_t s);
-
-// ---- radix-partitioned group-by (pg_part.hip): level 2 + per-bucket aggregation, after the two scan passes
-constexpr uint32_t kPartL1 = 256;        // level-1 partitions (scan passes)
-constexpr uint32_t kPartNB = 32;         // level-2 blocks per level-1 partition
-constexpr uint32_t kPartLdsBytes = 72 * 1024;  // LDS state of one bucket (count + value bitmap per group)
-struct PartSpec {
-  uint32_t nparts1, nparts2;       // level-1 partitions, level-2 sub-partitions per level-1 partition
-  uint32_t vbits, shift1, shift2;  // value-id bits; key bits below the level-1 / level-2 digit (2^shift2 = bucket)
-  uint32_t dc_words;               // uint32 words of the value bitmap (0: COUNT only)
-  uint32_t row_words, dc_word;     // state bitmap row width / this aggregation's first word (StateView layout)
-  uint32_t n_i64;
-  uint32_t blocks1;                // scan blocks (regions of the 64-bit entry array)
-  uint64_t num_groups;             // G (packed key space)
-  const unsigned long long* in0;   // scan entries (64-bit), block b's at [base0[b], base0[b] + count0[b])
-  const unsigned long long* base0;
-  const unsigned int* count0;
-  const unsigned long long* off1;  // [nparts1 * blocks1 + 1] exclusive scan of the scan's (partition, block) counts
-  uint32_t* in1;                   // level-1 entries (32-bit: key below the level-1 digit << vbits | value id)
-  unsigned long long* hist2;       // [nparts1 * nparts2 * kPartNB + 1] level-2 counts (last = 0)
-  const unsigned long long* off2;  // their exclusive scan: bucket b's entries start at off2[b * kPartNB]
-  uint32_t* out2;                  // level-2 entries, bucket-major
-  unsigned long long* i64;         // dense state written by the bucket pass
-  uint32_t* bits;
-};
-hipError_t launch_part_split1(const PartSpec& p, hipStream_t s);
-hipError_t launch_part_count2(const PartSpec& p, hipStream_t s);
-hipError_t launch_part_split2(const PartSpec& p, hipStream_t s);
-hipError_t launch_part_aggregate(const PartSpec& p, hipStream_t s);
-
-// ---- group keys wider than a packed 62-bit key (pg_wide.hip): ArrayMapBasedHolder as a device tuple table
-constexpr uint32_t kMaxWideKeys = 64;
-struct WideSpec {
-  uint32_t K, num_segments, max_fill, pad;
-  uint64_t mask;                    // table slots - 1 (a power of two)
-  unsigned long long* tags;         // [slots]: 0 free, 1 being written, else the tuple's hash | 2
-  uint32_t* tuples;                 // [slots][K] table-global key ids
-  unsigned int* fill;               // claimed slots
-  unsigned int* err;                // bit 0: key id outside its key space; bit 2: table over its fill budget
-  const ColDesc* keycols;           // [seg][K] (the scan's key column descriptors)
-  const uint32_t* num_docs;         // [seg]
-  uint32_t* const* out;             // [seg] -> uint32[num_docs]: tuple slot of each doc
-  const uint32_t* key_kind;         // [K]
-  const int64_t* key_base;          // [K]
-  const uint32_t* key_card;         // [K]
-};
-hipError_t launch_intern_tuples(const WideSpec& w, uint32_t max_docs, hipStream_t s);
-hipError_t launch_gather_tuples(const uint32_t* tuples, uint32_t K, const uint64_t* slots, uint64_t n, uint32_t* out,
-                                hipStream_t s);
-
-// ---- group state (pg_groups.hip)
-struct StateView {            // the device arrays of one partial state
-  uint64_t num_slots, hmask;
-  unsigned long long* keys;   // hash tables: [num_slots] packed keys (kEmptyKey = free); dense: null
-  unsigned long long* i64;
-  double* f64;
-  long long* mn;
-  long long* mx;
-  uint32_t* bits;
-  unsigned int* first_doc;    // GM_HASH_SEG tables
-  unsigned int* fill;         // hash tables: claimed keys
-  unsigned int* err;          // bit 2: table full
-  uint32_t n_i64, n_f64, n_min, n_max, bit_words, max_fill;
-};
-struct FinalSpec {            // what finalisation needs of the plan
-  uint32_t num_aggs, num_keys;
-  uint32_t order_kind, order_index, order_desc, pad;  // first ORDER BY item (pg_order)
-  AggSpec aggs[kMaxAggs];
-  uint32_t key_card[kMaxKeys];
-  uint64_t key_stride[kMaxKeys];
-};
-enum SelectKind : uint32_t { SEL_PRESENT = 0, SEL_OCCUPIED = 1, SEL_PRESENT_PART = 2 };
-size_t select_temp_bytes(uint64_t n);
-size_t sort_temp_bytes(uint64_t n, uint32_t begin_bit = 0, uint32_t end_bit = 64);
-uint64_t row_bytes(const StateView& v);
-hipError_t launch_select_slots(const StateView& v, uint32_t kind, uint32_t part, uint32_t parts, uint32_t* out,
-                               uint32_t* d_num, void* temp, size_t temp_bytes, hipStream_t s);
-hipError_t launch_select_flagged(const uint32_t* in, const uint8_t* flags, uint64_t n, uint32_t* out, uint32_t* d_num,
-                                 void* temp, size_t temp_bytes, hipStream_t s);
-hipError_t launch_exclusive_sum(const uint64_t* in, uint64_t* out, uint64_t n, void* temp, size_t temp_bytes,
-                                hipStream_t s);
-hipError_t launch_sort_pairs(const uint64_t* kin, uint64_t* kout, const uint32_t* vin, uint32_t* vout, uint64_t n,
-                             void* temp, size_t temp_bytes, hipStream_t s, uint32_t begin_bit = 0, uint32_t end_bit = 64);
-hipError_t launch_final_values(const StateView& v, const FinalSpec& f, const uint32_t* slots, uint64_t n,
-                               uint64_t* keys, double* vals, int64_t* cnts, hipStream_t s);
-// span (optional, 2 words, set here): the OR of every order key and the OR of their complements; the bits set in
-// both differ between keys, the others are equal in all of them and the sort can skip them
-hipError_t launch_order_keys(const FinalSpec& f, const uint64_t* keys, const double* vals, const int64_t* cnts,
-                             uint64_t n, uint64_t* out, uint32_t* pos, hipStream_t s, uint64_t* span = nullptr);
-hipError_t launch_cutoff(const uint64_t* sorted, uint64_t n, uint64_t limit, uint64_t* out, hipStream_t s);
-hipError_t launch_gather_final(uint32_t A, const uint32_t* pos, uint64_t n, const uint64_t* keys, const double* vals,
-                               const int64_t* cnts, const uint32_t* slots, uint64_t* okeys, double* ovals,
-                               int64_t* ocnts, uint32_t* oslots, hipStream_t s);
-hipError_t launch_set_sizes(const StateView& v, const FinalSpec& f, const uint32_t* slots, uint64_t n,
-                            uint64_t* sizes, hipStream_t s);
-hipError_t launch_set_extract(const StateView& v, const FinalSpec& f, const uint32_t* slots, uint64_t n,
-                              const uint64_t* offsets, uint32_t* ids, hipStream_t s);
-hipError_t launch_gather_rows(const StateView& v, const uint32_t* slots, uint64_t n, uint64_t key_div, uint8_t* dst,
-                              hipStream_t s);
-hipError_t launch_merge_rows(const StateView& v, const uint8_t* rows, uint64_t n, hipStream_t s);
-hipError_t launch_init_view(const StateView& v, hipStream_t s);  // pg_kernels.hip: zero / empty / +-inf state
-hipError_t launch_seg_truncate(const StateView& v, const uint32_t* slots, uint64_t n, uint32_t num_segments,
-                               uint64_t limit, uint64_t* tmp_keys, uint64_t* sorted_keys, uint32_t* sorted_slots,
-                               uint32_t* seg_first, uint8_t* keep, void* temp, size_t temp_bytes, hipStream_t s);
 
 }  // namespace pg

@@ -23,7 +23,7 @@
 // once (scan) + 8 written / 8 read (scan entries) + 4 / 4 twice (levels 1, 2) + 4 read (count2) + state rows once.
 #include <hip/hip_runtime.h>
 
-#include "pg_internal.h"
+#include "pg_aux.h"
 
 namespace pg {
 
@@ -238,6 +238,123 @@ __global__ __launch_bounds__(kAT) void part_aggregate_kernel(PartSpec P) {
       dst[w] = (k >= P.dc_word && k < P.dc_word + dw) ? bm[gl * dw + (k - P.dc_word)] : 0u;
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------ level 1 from the columns
+
+// FixedBitIntReader.readUnchecked on the native-word image (columns keep 4 zero words of tail padding).
+__device__ __forceinline__ uint32_t col_unpack(const uint32_t* __restrict__ w, uint32_t idx, uint32_t b) {
+  const uint64_t p = (uint64_t)idx * b;
+  const uint64_t k = p >> 5;
+  const uint64_t win = ((uint64_t)w[k] << 32) | (uint64_t)w[k + 1];
+  return (uint32_t)(win >> (64u - ((uint32_t)p & 31u) - b)) & (0xFFFFFFFFu >> (32u - b));
+}
+
+// table-global id of dictId `id` (the scan's key_of): value offset through the dictionary / decoded image, or keymap
+__device__ __forceinline__ uint64_t col_key_of(uint32_t kind, int64_t base, const ColDesc& c, uint32_t id) {
+  if (id >= c.card) return ~0ull;
+  if (kind == PG_KEY_KEYMAP) return (uint64_t)(uint32_t)c.keymap[id];
+  int64_t v;
+  if (c.decoded) v = c.vbase + (int64_t)id;
+  else v = c.dtype == PG_INT ? (int64_t)((const int32_t*)c.dict)[id] : ((const int64_t*)c.dict)[id];
+  return (uint64_t)(v - base);
+}
+
+// The level-1 digit and 32-bit entry of doc d (keys / value of segment sd).  A key or value outside its space (never
+// expected: the host proved the ranges) reports an error bit and lands in partition 0; hist and scatter agree.
+__device__ __forceinline__ void part_entry(const PartScanSpec& P, const ColDesc* kc, const ColDesc& vc, uint32_t d,
+                                           uint32_t& digit, uint32_t& entry) {
+  uint64_t g = 0;
+  bool bad = false;
+  for (uint32_t k = 0; k < P.num_keys; k++) {
+    const uint64_t kid = col_key_of(P.key_kind[k], P.key_base[k], kc[k], col_unpack(kc[k].words, d, kc[k].bits));
+    bad |= kid >= P.key_card[k];
+    g += kid * P.key_stride[k];
+  }
+  uint32_t vid = 0;
+  if (P.val_agg != (uint32_t)kNoSlot) {
+    const uint64_t v = col_key_of(P.val.key_kind, P.val.key_base, vc, col_unpack(vc.words, d, vc.bits));
+    if (v >= P.val.key_card) atomicOr(P.err, 2u);
+    else vid = (uint32_t)v;
+  }
+  if (bad) {
+    atomicOr(P.err, 1u);
+    g = 0;
+  }
+  digit = (uint32_t)(g >> P.shift1);
+  entry = (uint32_t)(((g & ((1ull << P.shift1) - 1ull)) << P.vbits) | vid);
+}
+
+__global__ __launch_bounds__(kST) void part_hist_kernel(PartScanSpec P) {
+  __shared__ uint32_t h[kPartL1];
+  const uint32_t b = blockIdx.x, tid = threadIdx.x;
+  for (uint32_t i = tid; i < kPartL1; i += kST) h[i] = 0;
+  __syncthreads();
+  const uint64_t i0 = (uint64_t)b * P.num_items / P.blocks, i1 = (uint64_t)(b + 1) * P.num_items / P.blocks;
+  for (uint64_t it = i0; it < i1; it++) {
+    const WorkItem w = P.items[it];
+    const SegDesc sd = P.segs[w.seg];
+    const ColDesc* kc = sd.keycols;
+    const ColDesc vc = P.val_agg != (uint32_t)kNoSlot ? sd.aggcols[2 * P.val_agg] : kc[0];
+    const uint32_t d0 = w.tile_begin * (uint32_t)kTileDocs, d1 = min(w.tile_end * (uint32_t)kTileDocs, sd.num_docs);
+    for (uint32_t r0 = d0; r0 < d1; r0 += kSplitChunk) {  // the scatter's rounds: E docs per lane, loads in flight together
+      constexpr int E = kSplitChunk / kST;
+      const uint32_t m = min(kSplitChunk, d1 - r0);
+      uint32_t dg[E];
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        uint32_t e;
+        dg[k] = 0;
+        if (tid + kST * k < m) part_entry(P, kc, vc, r0 + tid + kST * k, dg[k], e);
+      }
+#pragma unroll
+      for (int k = 0; k < E; k++)
+        if (tid + kST * k < m) atomicAdd(&h[dg[k]], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t p = tid; p < P.nparts1; p += kST) P.hist1[(uint64_t)p * P.blocks + b] = h[p];
+}
+
+__global__ __launch_bounds__(kST) void part_scatter_kernel(PartScanSpec P) {
+  constexpr int E = kSplitChunk / kST;
+  __shared__ uint32_t cnt[kPartL1], start[kPartL1], sbuf[kSplitChunk];
+  __shared__ unsigned long long cur[kPartL1];
+  __shared__ uint8_t sdig[kSplitChunk];
+  const uint32_t b = blockIdx.x, tid = threadIdx.x;
+  if (tid < P.nparts1) {
+    cnt[tid] = 0;
+    cur[tid] = P.off1[(uint64_t)tid * P.blocks + b];
+  }
+  __syncthreads();
+  const uint64_t i0 = (uint64_t)b * P.num_items / P.blocks, i1 = (uint64_t)(b + 1) * P.num_items / P.blocks;
+  for (uint64_t it = i0; it < i1; it++) {
+    const WorkItem w = P.items[it];
+    const SegDesc sd = P.segs[w.seg];
+    const ColDesc* kc = sd.keycols;
+    const ColDesc vc = P.val_agg != (uint32_t)kNoSlot ? sd.aggcols[2 * P.val_agg] : kc[0];
+    const uint32_t d0 = w.tile_begin * (uint32_t)kTileDocs, d1 = min(w.tile_end * (uint32_t)kTileDocs, sd.num_docs);
+    for (uint32_t r0 = d0; r0 < d1; r0 += kSplitChunk) {
+      const uint32_t m = min(kSplitChunk, d1 - r0);
+      uint32_t e[E], dg[E];
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        const uint32_t i = tid + kST * k;
+        e[k] = dg[k] = 0;
+        if (i < m) part_entry(P, kc, vc, r0 + i, dg[k], e[k]);
+      }
+      split_round<uint32_t, true>(e, dg, m, P.nparts1, cnt, start, cur, sbuf, sdig, P.out1);
+    }
+  }
+}
+
+hipError_t launch_part_hist(const PartScanSpec& p, hipStream_t s) {
+  hipLaunchKernelGGL(part_hist_kernel, dim3(p.blocks), dim3(kST), 0, s, p);
+  return hipGetLastError();
+}
+hipError_t launch_part_scatter(const PartScanSpec& p, hipStream_t s) {
+  hipLaunchKernelGGL(part_scatter_kernel, dim3(p.blocks), dim3(kST), 0, s, p);
+  return hipGetLastError();
 }
 
 hipError_t launch_part_split1(const PartSpec& p, hipStream_t s) {

@@ -27,7 +27,8 @@
 #include <unordered_set>
 #include <vector>
 
-#include "pg_internal.h"
+#include "pg_aux.h"
+#include "../../include/pinot_codec.h"
 
 using namespace pg;
 
@@ -472,55 +473,6 @@ int parse_inverted(const std::vector<uint8_t>& b, uint32_t card, std::vector<uin
   return PG_OK;
 }
 
-// Snappy block decompression (ChunkCompressionType.SNAPPY chunks): varint uncompressed length, then literal / copy
-// elements (copies may overlap their own output).  Upload-time format conversion, as the byte swaps above.
-int snappy_decode(const uint8_t* p, uint64_t n, std::vector<uint8_t>& out) {
-  uint64_t pos = 0, len = 0;
-  for (int shift = 0;; shift += 7) {
-    if (pos >= n || shift > 35) return fail(PG_E_INVALID, "snappy: bad length header");
-    const uint8_t b = p[pos++];
-    len |= (uint64_t)(b & 0x7F) << shift;
-    if (b < 0x80) break;
-  }
-  out.clear();
-  out.reserve(len);
-  while (pos < n) {
-    const uint8_t tag = p[pos++];
-    uint64_t ln, off = 0;
-    if ((tag & 3) == 0) {
-      ln = tag >> 2;
-      if (ln >= 60) {
-        const uint32_t nb = (uint32_t)ln - 59;
-        if (pos + nb > n) return fail(PG_E_INVALID, "snappy: truncated literal length");
-        ln = 0;
-        for (uint32_t k = 0; k < nb; k++) ln |= (uint64_t)p[pos + k] << (8 * k);
-        pos += nb;
-      }
-      ln += 1;
-      if (pos + ln > n) return fail(PG_E_INVALID, "snappy: truncated literal");
-      out.insert(out.end(), p + pos, p + pos + ln);
-      pos += ln;
-      continue;
-    }
-    if ((tag & 3) == 1) {
-      if (pos + 1 > n) return fail(PG_E_INVALID, "snappy: truncated copy");
-      ln = ((tag >> 2) & 7) + 4;
-      off = ((uint64_t)(tag >> 5) << 8) | p[pos];
-      pos += 1;
-    } else {
-      const uint32_t nb = (tag & 3) == 2 ? 2 : 4;
-      if (pos + nb > n) return fail(PG_E_INVALID, "snappy: truncated copy");
-      ln = (tag >> 2) + 1;
-      for (uint32_t k = 0; k < nb; k++) off |= (uint64_t)p[pos + k] << (8 * k);
-      pos += nb;
-    }
-    if (off == 0 || off > out.size()) return fail(PG_E_INVALID, "snappy: copy offset out of range");
-    for (uint64_t k = 0; k < ln; k++) out.push_back(out[out.size() - off]);
-  }
-  if (out.size() != len) return fail(PG_E_INVALID, "snappy: %zu bytes decoded, %llu expected", out.size(), (unsigned long long)len);
-  return PG_OK;
-}
-
 // A raw chunked forward index (BaseChunkForwardIndexReader.java:56-102 header; FixedByteChunkSVForwardIndexReader /
 // FixedBytePower2ChunkSVForwardIndexReader per-doc reads) -> the big-endian values of docs [0, num_docs).
 int raw_forward_values(const std::vector<uint8_t>& b, uint32_t width, uint32_t num_docs, std::vector<uint8_t>& out) {
@@ -543,8 +495,8 @@ int raw_forward_values(const std::vector<uint8_t>& b, uint32_t width, uint32_t n
     memcpy(out.data(), &b[raw_start], out.size());
     return PG_OK;
   }
-  if (comp != 1) return fail(PG_E_UNSUPPORTED, "raw forward index: chunk compression %u (only PASS_THROUGH / SNAPPY)", comp);
-  std::vector<uint8_t> chunk;
+  if (comp > PG_CODEC_LZ4_LENGTH_PREFIXED) return fail(PG_E_UNSUPPORTED, "raw forward index: chunk compression %u", comp);
+  std::vector<uint8_t> chunk((uint64_t)per_chunk * width + 16);
   uint64_t at = 0;
   for (uint32_t k = 0; k < num_chunks && at < out.size(); k++) {
     auto off = [&](uint32_t i) -> uint64_t {
@@ -553,11 +505,14 @@ int raw_forward_values(const std::vector<uint8_t>& b, uint32_t width, uint32_t n
     };
     const uint64_t s0 = off(k), e0 = k + 1 < num_chunks ? off(k + 1) : b.size();
     if (s0 > e0 || e0 > b.size()) return fail(PG_E_INVALID, "raw forward index: bad chunk %u", k);
-    int rc = snappy_decode(&b[s0], e0 - s0, chunk);
-    if (rc) return rc;
-    const uint64_t take = std::min<uint64_t>(chunk.size(), out.size() - at);
-    if (chunk.size() < std::min<uint64_t>((uint64_t)per_chunk * width, out.size() - at))
-      return fail(PG_E_INVALID, "raw forward index: chunk %u holds %zu bytes", k, chunk.size());
+    // ChunkDecompressor.decompress of the chunk's codec (pg_codec.hip): at most docsPerChunk entries
+    uint64_t got = 0;
+    const char* why = "";
+    int rc = decompress_chunk(comp, &b[s0], e0 - s0, chunk.data(), (uint64_t)per_chunk * width, &got, &why);
+    if (rc) return fail(rc, "raw forward index chunk %u: %s", k, why);
+    const uint64_t take = std::min<uint64_t>(got, out.size() - at);
+    if (got < std::min<uint64_t>((uint64_t)per_chunk * width, out.size() - at))
+      return fail(PG_E_INVALID, "raw forward index: chunk %u holds %llu bytes", k, (unsigned long long)got);
     memcpy(&out[at], chunk.data(), take);
     at += take;
   }
@@ -1169,7 +1124,10 @@ template <class T> int read_back(const T* d, T& h, hipStream_t s) {
 int hash_like(const Partials& src, uint64_t groups, Partials& out, hipStream_t s) {
   out.mode = GM_HASH;
   out.num_slots = pow2_at_least(std::max<uint64_t>(1024, 2 * groups));
-  if (out.num_slots > kMaxHashSlots) return fail(PG_E_UNSUPPORTED, "merge table of %llu groups too large", (unsigned long long)groups);
+  const uint64_t slot_bytes = 8ull * (src.n_i64 + src.n_f64 + src.n_min + src.n_max) + 4ull * src.bit_words + 12;
+  if (out.num_slots > kMaxHashSlots || out.num_slots * slot_bytes > kStateBudget)  // compile_and_run's budget
+    return fail(PG_E_UNSUPPORTED, "merge table of %llu groups (%llu slots x %llu bytes) exceeds the state budget",
+                (unsigned long long)groups, (unsigned long long)out.num_slots, (unsigned long long)slot_bytes);
   out.max_fill = (uint32_t)(out.num_slots / 4 * 3);
   out.n_i64 = src.n_i64; out.n_f64 = src.n_f64; out.n_min = src.n_min; out.n_max = src.n_max;
   out.bit_words = src.bit_words;
@@ -2650,12 +2608,16 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   if (plan->deadline_ms && now_ms() > plan->deadline_ms) { (void)hipStreamSynchronize(s); return fail(PG_E_TIMEOUT, "deadline passed"); }
   CancelSlot cancel(plan->query_id, plan->query_id != 0 || plan->deadline_ms != 0);
   q.cancel = cancel.device_ptr();
+  std::vector<uint64_t> direct_matched;
   if (q.num_items && part.on) {
-    // radix-partitioned group-by (pg_part.hip): scan appends entries + level-1 histogram, scan of the histogram,
-    // level-1 split, level-2 count / scan / split, per-bucket aggregation
+    // radix-partitioned group-by (pg_part.hip).  Filter matching every doc: level-1 partitions straight from the
+    // columns (part_hist + scan + part_scatter).  Otherwise the fused scan appends 64-bit entries + the level-1
+    // histogram, then part_split1.  Both: level-2 count / scan / split, per-bucket aggregation.
+    bool direct = !getenv("PG_PART_SCAN");
+    for (uint32_t si = 0; si < S && direct; si++) direct = filter_is_match_all(plan, plan->segments[si].leaves);
     const uint64_t n1 = (uint64_t)part.nparts1 * blocks, n2 = (uint64_t)part.nparts1 * part.nparts2 * kPartNB;
     const size_t tb = select_temp_bytes(std::max(n1, n2) + 1);
-    if ((rc = p_ent0.alloc_pooled(8 * part_entries + 16)) || (rc = p_cnt0.alloc_pooled(4ull * blocks + 16)) ||
+    if ((!direct && ((rc = p_ent0.alloc_pooled(8 * part_entries + 16)) || (rc = p_cnt0.alloc_pooled(4ull * blocks + 16)))) ||
         (rc = p_hist1.alloc_pooled(8 * (n1 + 1))) || (rc = p_off1.alloc_pooled(8 * (n1 + 1))) ||
         (rc = p_ent1.alloc_pooled(4 * part_entries + 16)) || (rc = p_hist2.alloc_pooled(8 * (n2 + 1))) ||
         (rc = p_off2.alloc_pooled(8 * (n2 + 1))) || (rc = p_ent2.alloc_pooled(4 * part_entries + 16)) ||
@@ -2677,8 +2639,39 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     q.part_base = (const unsigned long long*)(dA + off_part_base);
     q.part_out = (unsigned long long*)p_ent0.p;
     t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
-    HIP_CHECK(launch_scan(q, blocks, s));
-    HIP_CHECK(launch_exclusive_sum((const uint64_t*)h1, (uint64_t*)o1, n1 + 1, p_temp.p, tb, s));
+    if (direct) {
+      PartScanSpec pss;
+      memset(&pss, 0, sizeof(pss));
+      pss.num_keys = K;
+      pss.blocks = blocks;
+      pss.num_items = q.num_items;
+      pss.nparts1 = part.nparts1;
+      pss.shift1 = part.shift1;
+      pss.vbits = part.vbits;
+      pss.val_agg = part.dc;
+      pss.segs = q.segs;
+      pss.items = q.items;
+      for (uint32_t k = 0; k < K; k++) {
+        pss.key_kind[k] = q.key_kind[k];
+        pss.key_card[k] = q.key_card[k];
+        pss.key_base[k] = q.key_base[k];
+        pss.key_stride[k] = q.key_stride[k];
+      }
+      if (part.dc != (uint32_t)kNoSlot) pss.val = q.aggs[part.dc];
+      pss.hist1 = h1;
+      pss.off1 = o1;
+      pss.out1 = (uint32_t*)p_ent1.p;
+      pss.err = q.err;
+      direct_matched.resize(S);  // every doc matches: the per-segment counts are the segments' sizes
+      for (uint32_t si = 0; si < S; si++) direct_matched[si] = plan->segments[si].num_docs;
+      if (S) HIP_CHECK(hipMemcpyAsync(P.seg_matched.p, direct_matched.data(), 8ull * S, hipMemcpyHostToDevice, s));
+      HIP_CHECK(launch_part_hist(pss, s));
+      HIP_CHECK(launch_exclusive_sum((const uint64_t*)h1, (uint64_t*)o1, n1 + 1, p_temp.p, tb, s));
+      HIP_CHECK(launch_part_scatter(pss, s));
+    } else {
+      HIP_CHECK(launch_scan(q, blocks, s));
+      HIP_CHECK(launch_exclusive_sum((const uint64_t*)h1, (uint64_t*)o1, n1 + 1, p_temp.p, tb, s));
+    }
     PartSpec ps;
     memset(&ps, 0, sizeof(ps));
     ps.nparts1 = part.nparts1;
@@ -2702,7 +2695,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     ps.out2 = (uint32_t*)p_ent2.p;
     ps.i64 = (unsigned long long*)P.i64.p;
     ps.bits = (uint32_t*)P.bits.p;
-    HIP_CHECK(launch_part_split1(ps, s));
+    if (!direct) HIP_CHECK(launch_part_split1(ps, s));
     HIP_CHECK(launch_part_count2(ps, s));
     HIP_CHECK(launch_exclusive_sum((const uint64_t*)h2, (uint64_t*)o2, n2 + 1, p_temp.p, tb, s));
     HIP_CHECK(launch_part_split2(ps, s));
@@ -3597,6 +3590,14 @@ int pg_result_free(pg_result* r) {
   free(r->distinct_ids);
   free(r);
   return PG_OK;
+}
+
+int pg_chunk_decompress(uint32_t codec, const void* src, uint64_t src_len, void* dst, uint64_t dst_cap,
+                        uint64_t* out_len) {
+  if ((!src && src_len) || (!dst && dst_cap) || !out_len) return fail(PG_E_INVALID, "null argument");
+  const char* why = "";
+  const int rc = decompress_chunk(codec, (const uint8_t*)src, src_len, (uint8_t*)dst, dst_cap, out_len, &why);
+  return rc ? fail(rc, "%s", why) : PG_OK;
 }
 
 int pg_last_timing(pg_timing* out) {

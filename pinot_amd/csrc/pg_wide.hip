@@ -19,7 +19,7 @@
 
 #include <algorithm>
 
-#include "pg_internal.h"
+#include "pg_aux.h"
 
 namespace pg {
 

@@ -123,6 +123,11 @@ class GpuEngine:
                                             dc.dict_be.numel()))
             check(self.lib.pg_column_upload(key, cid, C.byref(d), C.c_void_p(dc.fwd_be.data_ptr()),
                                             dc.fwd_be.numel()))
+            if getattr(dc, "inv_be", None) is not None:
+                di = abi.pg_col_desc.from_buffer_copy(d)
+                di.kind = abi.PG_IDX_INV_BITMAP
+                check(self.lib.pg_column_upload(key, cid, C.byref(di), C.c_void_p(dc.inv_be.data_ptr()),
+                                                dc.inv_be.numel()))
         self._seg_keys[id(seg)] = (seg, key)
         return key
 
@@ -219,23 +224,48 @@ class GpuEngine:
         check(self.lib.pg_last_timing(C.byref(t)))
         return t
 
+    def finalize_arrays(self, plan: CPlan, p) -> dict:
+        """pg_partials_finalize -> the result as plain arrays (result_arrays); frees `p`."""
+        res = C.POINTER(abi.pg_result)()
+        try:
+            check(self.lib.pg_partials_finalize(p, C.byref(plan.plan), C.byref(res)))
+        finally:
+            self.lib.pg_partials_free(p)
+        try:
+            return self.result_arrays(res.contents)
+        finally:
+            self.lib.pg_result_free(res)
+
     @staticmethod
-    def decode(plan: CPlan, r: abi.pg_result) -> IntermediateResult:
-        A = r.num_aggs
-        K = r.num_keys
-        G = r.num_groups
-        vals = np.ctypeslib.as_array(r.values, shape=(max(G * A, 1),))[:G * A].reshape(G, A) if G and A else \
+    def result_arrays(r: abi.pg_result) -> dict:
+        """Copies of a pg_result's arrays: stats (int64[6]), keys uint32[G, K], values float64[G, A], counts
+        int64[G, A] and, with value sets, distinct offsets uint64[G * A + 1] / ids uint32[num_distinct]."""
+        A, K, G = r.num_aggs, r.num_keys, r.num_groups
+        vals = np.ctypeslib.as_array(r.values, shape=(max(G * A, 1),))[:G * A].reshape(G, A).copy() if G and A else \
             np.zeros((G, A))
-        cnts = np.ctypeslib.as_array(r.counts, shape=(max(G * A, 1),))[:G * A].reshape(G, A) if G and A else \
+        cnts = np.ctypeslib.as_array(r.counts, shape=(max(G * A, 1),))[:G * A].reshape(G, A).copy() if G and A else \
             np.zeros((G, A), dtype=np.int64)
-        keys = np.ctypeslib.as_array(r.keys, shape=(max(G * K, 1),))[:G * K].reshape(G, K) if G and K else \
+        keys = np.ctypeslib.as_array(r.keys, shape=(max(G * K, 1),))[:G * K].reshape(G, K).copy() if G and K else \
             np.zeros((G, K), dtype=np.uint32)
-        sets = None
+        offs = ids = None
         if r.distinct_offsets:
             offs = np.ctypeslib.as_array(r.distinct_offsets, shape=(G * A + 1,)).copy()
-            ids = (np.ctypeslib.as_array(r.distinct_ids, shape=(max(int(r.num_distinct), 1),))[:r.num_distinct]
-                   .astype(np.int64))
-            sets = (offs, ids)
+            ids = np.ctypeslib.as_array(r.distinct_ids, shape=(max(int(r.num_distinct), 1),))[:r.num_distinct].copy()
+        s = r.stats
+        stats = np.array([s.num_docs_scanned, s.num_entries_scanned_in_filter, s.num_entries_scanned_post_filter,
+                          s.num_total_docs, s.num_segments_processed, s.num_segments_matched], dtype=np.int64)
+        return {"G": G, "K": K, "A": A, "keys": keys, "values": vals, "counts": cnts, "offsets": offs, "ids": ids,
+                "stats": stats}
+
+    @staticmethod
+    def decode(plan: CPlan, r) -> IntermediateResult:
+        """pg_result (or its result_arrays) -> value-keyed IntermediateResult."""
+        ra = r if isinstance(r, dict) else GpuEngine.result_arrays(r)
+        A, K, G = ra["A"], ra["K"], ra["G"]
+        vals, cnts, keys = ra["values"], ra["counts"], ra["keys"]
+        sets = None
+        if ra["offsets"] is not None:
+            sets = (ra["offsets"], ra["ids"].astype(np.int64))
         kinds = [0 if ag.function in ("COUNT", "COUNTMV") else 3 if ag.function == "DISTINCTCOUNT" else
                  1 if ag.function == "AVG" else 2 for ag in plan.aggs]
         dspaces = [plan.table.key_space(ag.arg.cols[0]) if k == 3 else None for ag, k in zip(plan.aggs, kinds)]
@@ -265,7 +295,5 @@ class GpuEngine:
             else:
                 acols.append(v.astype(np.float64).tolist())
         rows = dict(zip(keyt, (list(x) for x in zip(*acols)))) if A else {k: [] for k in keyt}
-        s = r.stats
-        st = ExecutionStats(s.num_docs_scanned, s.num_entries_scanned_in_filter, s.num_entries_scanned_post_filter,
-                            s.num_total_docs, s.num_segments_processed, s.num_segments_matched)
+        st = ExecutionStats(*(int(x) for x in ra["stats"]))
         return IntermediateResult(plan.aggs, list(plan.query.group_by), rows, st)

@@ -301,63 +301,104 @@ CHUNK_PASS_THROUGH, CHUNK_SNAPPY, CHUNK_ZSTANDARD, CHUNK_LZ4, CHUNK_LZ4_LENGTH_P
 RAW_DOCS_PER_CHUNK = 1000
 
 
-def raw_forward_bytes(values, data_type: str, version: int = 2, docs_per_chunk: int = RAW_DOCS_PER_CHUNK) -> bytes:
-    """PASS_THROUGH chunked raw forward index (FixedByteChunkSVForwardIndexWriter), version 2, 3 or 4."""
+CHUNK_CODECS = {"PASS_THROUGH": CHUNK_PASS_THROUGH, "SNAPPY": CHUNK_SNAPPY, "ZSTANDARD": CHUNK_ZSTANDARD,
+                "LZ4": CHUNK_LZ4, "LZ4_LENGTH_PREFIXED": CHUNK_LZ4_LENGTH_PREFIXED}
+
+
+def _native(name):
+    """A system compression library (the native codecs the reference's JNI wrappers bundle: liblz4, libzstd), used
+    by the segment WRITER only; reading goes through libpinot_gpu's own decoders (pg_chunk_decompress)."""
+    import ctypes as C
+    lib = C.CDLL(name)
+    return C, lib
+
+
+def chunk_compress(codec: int, data: bytes) -> bytes:
+    """ChunkCompressor.compress of one chunk (io/compression/*Compressor.java)."""
+    if codec == CHUNK_PASS_THROUGH:
+        return data
+    if codec == CHUNK_SNAPPY:  # a valid Snappy block of literal elements (SnappyDecompressor reads any encoder's)
+        out = bytearray()
+        n = len(data)
+        while True:
+            out.append((n & 0x7F) | (0x80 if n >= 0x80 else 0))
+            n >>= 7
+            if not n:
+                break
+        for i in range(0, len(data), 65536):
+            lit = data[i:i + 65536]
+            out += bytes([61 << 2]) + struct.pack("<H", len(lit) - 1) + lit
+        return bytes(out)
+    if codec in (CHUNK_LZ4, CHUNK_LZ4_LENGTH_PREFIXED):
+        C, lz = _native("liblz4.so.1")
+        cap = lz.LZ4_compressBound(C.c_int(len(data)))
+        buf = C.create_string_buffer(max(cap, 1))
+        n = lz.LZ4_compress_default(C.c_char_p(data), buf, C.c_int(len(data)), C.c_int(cap))
+        if n <= 0:
+            raise RuntimeError("LZ4 compression failed")
+        blk = buf.raw[:n]
+        # LZ4CompressorWithLength: the original length as a 4-byte little-endian prefix
+        return struct.pack("<i", len(data)) + blk if codec == CHUNK_LZ4_LENGTH_PREFIXED else blk
+    if codec == CHUNK_ZSTANDARD:
+        C, zs = _native("libzstd.so.1")
+        zs.ZSTD_compressBound.restype = C.c_size_t
+        zs.ZSTD_compress.restype = C.c_size_t
+        zs.ZSTD_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_int]
+        cap = zs.ZSTD_compressBound(C.c_size_t(len(data)))
+        buf = C.create_string_buffer(max(cap, 1))
+        n = zs.ZSTD_compress(buf, cap, data, len(data), 3)  # zstd-jni Zstd.compress default level (3)
+        if zs.ZSTD_isError(C.c_size_t(n)):
+            raise RuntimeError("Zstandard compression failed")
+        return buf.raw[:n]
+    raise ValueError(f"chunk compression {codec}")
+
+
+def chunk_decompress(codec: int, data: bytes, cap: int) -> bytes:
+    """ChunkDecompressor.decompress of one chunk through libpinot_gpu (pg_chunk_decompress, pinot_codec.h)."""
+    import ctypes as C
+    from .gpu import check, load_library
+    lib = load_library()
+    src = np.frombuffer(data, dtype=np.uint8) if data else np.zeros(1, dtype=np.uint8)
+    dst = np.empty(max(cap, 1), dtype=np.uint8)
+    n = C.c_uint64()
+    check(lib.pg_chunk_decompress(codec, src.ctypes.data, len(data), dst.ctypes.data, cap, C.byref(n)))
+    return dst[:n.value].tobytes()
+
+
+def raw_forward_bytes(values, data_type: str, version: int = 2, docs_per_chunk: int = RAW_DOCS_PER_CHUNK,
+                      compression: str = "PASS_THROUGH") -> bytes:
+    """Chunked raw forward index (FixedByteChunkSVForwardIndexWriter / BaseChunkSVForwardIndexWriter), version 2, 3 or 4
+    (v4: FixedBytePower2ChunkSVForwardIndexReader finds a doc's chunk as docId >>> numberOfTrailingZeros(docsPerChunk),
+    so its docs per chunk are rounded up to a power of two).  Each chunk of docsPerChunk values (the last one partial)
+    is compressed on its own; the header's chunk offsets point at the compressed chunks."""
+    if version >= 4:
+        docs_per_chunk = 1 << max(0, docs_per_chunk - 1).bit_length()
+    codec = CHUNK_CODECS[compression]
     arr = np.asarray(values, dtype=_NP_BE[data_type])
     n, size = arr.size, arr.dtype.itemsize
     num_chunks = (n + docs_per_chunk - 1) // docs_per_chunk
     off_size = 4 if version <= 2 else 8
     header_size = 7 * 4 + num_chunks * off_size
-    head = struct.pack(">7i", version, num_chunks, docs_per_chunk, size, n, CHUNK_PASS_THROUGH, 28)
-    offs = np.arange(num_chunks, dtype=np.int64) * docs_per_chunk * size + header_size
-    return head + offs.astype(">i4" if off_size == 4 else ">i8").tobytes() + arr.tobytes()
+    head = struct.pack(">7i", version, num_chunks, docs_per_chunk, size, n, codec, 28)
+    raw = arr.tobytes()
+    chunks = [chunk_compress(codec, raw[c * docs_per_chunk * size:(c + 1) * docs_per_chunk * size])
+              for c in range(num_chunks)]
+    offs = header_size + np.concatenate([[0], np.cumsum([len(c) for c in chunks])[:-1]]).astype(np.int64) \
+        if num_chunks else np.zeros(0, dtype=np.int64)
+    return head + offs.astype(">i4" if off_size == 4 else ">i8").tobytes() + b"".join(chunks)
 
 
 def snappy_decompress(src: bytes) -> bytes:
-    """The Snappy block format (ChunkCompressionType.SNAPPY, snappy-java 1.1.x; format: varint uncompressed length,
-    then literal / copy elements with 1-, 2- or 4-byte offsets)."""
-    pos, n, shift = 0, 0, 0
+    """Snappy block decompression through libpinot_gpu (SnappyDecompressor)."""
+    pos, length, shift = 0, 0, 0
     while True:
         b = src[pos]
         pos += 1
-        n |= (b & 0x7F) << shift
+        length |= (b & 0x7F) << shift
         shift += 7
         if b < 0x80:
             break
-    out = bytearray()
-    while pos < len(src):
-        tag = src[pos]
-        pos += 1
-        kind = tag & 3
-        if kind == 0:  # literal
-            ln = tag >> 2
-            if ln >= 60:
-                nb = ln - 59
-                ln = int.from_bytes(src[pos:pos + nb], "little")
-                pos += nb
-            ln += 1
-            out += src[pos:pos + ln]
-            pos += ln
-            continue
-        if kind == 1:
-            ln = ((tag >> 2) & 7) + 4
-            off = ((tag >> 5) << 8) | src[pos]
-            pos += 1
-        elif kind == 2:
-            ln = (tag >> 2) + 1
-            off = int.from_bytes(src[pos:pos + 2], "little")
-            pos += 2
-        else:
-            ln = (tag >> 2) + 1
-            off = int.from_bytes(src[pos:pos + 4], "little")
-            pos += 4
-        if off == 0 or off > len(out):
-            raise ValueError("corrupt snappy stream")
-        for _ in range(ln):  # copies may overlap their own output
-            out.append(out[-off])
-    if len(out) != n:
-        raise ValueError(f"snappy: {len(out)} bytes decoded, {n} expected")
-    return bytes(out)
+    return chunk_decompress(CHUNK_SNAPPY, src, length)
 
 
 def raw_forward_header(buf: bytes) -> dict:
@@ -367,6 +408,8 @@ def raw_forward_header(buf: bytes) -> dict:
         total, comp, data_start = struct.unpack_from(">3i", buf, 16)
     else:
         total, comp, data_start = None, CHUNK_SNAPPY, 16
+    if version >= 4 and docs_per_chunk & (docs_per_chunk - 1):
+        raise ValueError(f"v4 raw forward index with {docs_per_chunk} docs per chunk (a power of two is required)")
     off_size = 4 if version <= 2 else 8
     offs = np.frombuffer(buf, dtype=">i4" if off_size == 4 else ">i8", count=num_chunks, offset=data_start)
     return dict(version=version, num_chunks=num_chunks, docs_per_chunk=docs_per_chunk, entry=entry, total=total,
@@ -379,11 +422,12 @@ def raw_forward_values(buf: bytes, data_type: str, num_docs: Optional[int] = Non
     be = _NP_BE[data_type]
     if h["compression"] == CHUNK_PASS_THROUGH:
         data = buf[h["raw_start"]:]
-    elif h["compression"] == CHUNK_SNAPPY:
+    elif h["compression"] in CHUNK_CODECS.values():
         ends = list(h["offsets"][1:]) + [len(buf)]
-        data = b"".join(snappy_decompress(buf[s:e]) for s, e in zip(h["offsets"], ends))
+        cap = h["docs_per_chunk"] * h["entry"]
+        data = b"".join(chunk_decompress(h["compression"], buf[s:e], cap) for s, e in zip(h["offsets"], ends))
     else:
-        raise NotImplementedError(f"chunk compression {h['compression']}")
+        raise ValueError(f"chunk compression {h['compression']}")
     n = num_docs if num_docs is not None else (h["total"] if h["total"] is not None else len(data) // h["entry"])
     return np.frombuffer(data, dtype=be, count=n).astype(_NP_NATIVE[data_type])
 
@@ -562,9 +606,11 @@ class ImmutableSegment:
     def create(name: str, data: Dict[str, Sequence], schema: Dict[str, str],
                inverted: Sequence[str] = (), field_types: Optional[Dict[str, str]] = None,
                roaring_run_optimize: bool = True, no_dictionary: Sequence[str] = (),
-               raw_version: int = 2, range_index: Sequence[str] = ()) -> "ImmutableSegment":
+               raw_version: int = 2, range_index: Sequence[str] = (),
+               raw_compression: Optional[Dict[str, str]] = None) -> "ImmutableSegment":
         """schema: column -> data type.  MV columns are given as a list of sequences.  `no_dictionary`: SV numeric
-        columns stored as raw PASS_THROUGH chunked forward indexes (tableIndexConfig.noDictionaryColumns).
+        columns stored as raw chunked forward indexes (tableIndexConfig.noDictionaryColumns), compressed per
+        `raw_compression` (column -> ChunkCompressionType name), else PASS_THROUGH for metrics and LZ4 for dimensions.
         `range_index`: SV numeric columns with a range index (tableIndexConfig.rangeIndexColumns), written in the
         v1 layout (over dictIds for a dictionary column, over the values for a raw one)."""
         cols = {}
@@ -580,7 +626,10 @@ class ImmutableSegment:
                 col = Column(cname, dtype, True, None, n, 0, False, n, 0,
                              field_type=(field_types or {}).get(cname, "METRIC"), raw_values=arr,
                              raw_cardinality=int(np.unique(arr).size))
-                col.fwd = raw_forward_bytes(arr, dtype, raw_version)
+                # SegmentColumnarIndexCreator.getColumnCompressionType (:356-368): the spec's type, else PASS_THROUGH
+                # for metrics and LZ4 for dimensions
+                comp = (raw_compression or {}).get(cname) or ("PASS_THROUGH" if col.field_type == "METRIC" else "LZ4")
+                col.fwd = raw_forward_bytes(arr, dtype, raw_version, compression=comp)
             elif sv:
                 dictionary, ids = build_dictionary(dtype, vals)
                 n = ids.size

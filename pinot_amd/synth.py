@@ -80,6 +80,51 @@ def highcard_query(limit: int = 100) -> str:
             f"ORDER BY DISTINCTCOUNT(itemId) DESC, userId LIMIT {limit}")
 
 
+# Config 5: index path: 2 B rows = 256 segments (32 per GPU at N = 8).  sortedCol is sorted within
+# every segment over 100 000 values (sorted index: 800 KB of (start, end) pairs per segment); inv1..inv4 carry bitmap
+# inverted indexes; mvTags is multi-value (1-7 values per doc, 4 on average, over 1 000 tags).
+INDEX_SORTED = ColSpec("sortedCol", 0, 100_000)
+INDEX_INVERTED = [ColSpec("inv1", 0, 10), ColSpec("inv2", 0, 100), ColSpec("inv3", 0, 1000), ColSpec("inv4", 0, 10_000)]
+INDEX_MV = ColSpec("mvTags", 0, 1000)
+INDEX_SEGMENTS_PER_GPU = 32
+
+
+def index_query() -> str:
+    """Config 5 query: a 40 % sortedCol range AND (inv1 = x OR inv2 IN 20 of 100) AND inv3 <> y AND inv4 IN 2 000 of
+    10 000 -> about 2.2 % of the docs; COUNT(*) and COUNTMV over the multi-value column."""
+    ids = ", ".join(str(i * 5 + 1) for i in range(2000))
+    inv2 = ", ".join(str(i * 5) for i in range(20))
+    return ("SELECT COUNT(*), COUNTMV(mvTags) FROM idx WHERE sortedCol BETWEEN 20000 AND 59999 "
+            f"AND (inv1 = 3 OR inv2 IN ({inv2})) AND inv3 <> 7 AND inv4 IN ({ids})")
+
+
+def index_values_np(seg_index: int, n: int) -> Dict[str, object]:
+    """Values of one config-5 segment (numpy; identical to the device path)."""
+    row0 = seg_index * n
+    out = {"sortedCol": (np.arange(n, dtype=np.int64) * INDEX_SORTED.range) // n}
+    for c in INDEX_INVERTED:
+        out[c.name] = values_np(c, row0, n)
+    lengths, flat = mv_values_np(seg_index, n)
+    out["mvTags"] = np.split(flat, np.cumsum(lengths)[:-1])
+    return out
+
+
+def mv_values_np(seg_index: int, n: int):
+    """mvTags: per doc 1 + (hash % 7) values, each a hash of the value's global position."""
+    row0 = seg_index * n
+    lengths = 1 + (hash32_np(np.arange(row0, row0 + n, dtype=np.uint64), column_salt("mvTags.len")) % np.uint64(7))
+    lengths = lengths.astype(np.int64)
+    v0 = int(seg_index) * n * 8
+    flat = values_np(INDEX_MV, v0, int(lengths.sum()))
+    return lengths, flat
+
+
+def make_index_segment_np(seg_index: int, n: int) -> ImmutableSegment:
+    return ImmutableSegment.create(f"idx_{seg_index}", index_values_np(seg_index, n),
+                                   {"sortedCol": "INT", "inv1": "INT", "inv2": "INT", "inv3": "INT", "inv4": "INT",
+                                    "mvTags": "INT"}, inverted=[c.name for c in INDEX_INVERTED])
+
+
 # Config 1: pinot-tools QuickStart baseballStats (CPU-reference scale).  The data CSV is not in the reference checkout
 # (.MISSING_LARGE_BLOBS), so rows follow the schema (pinot-tools/.../baseballStats/baseballStats_schema.json: 5 STRING /
 # INT dimensions, 20 INT metrics) with plausible ranges; inverted indexes on playerID and teamID as its table config.
@@ -199,8 +244,9 @@ def be_int32_torch(v):
 
 @dataclass
 class DeviceColumn:
-    """A synthetic column generated on the device: BE dictionary bytes + BE forward bytes (device tensors) and the
-    host-side dictionary (needed for predicate lowering, as the reference keeps its Dictionary on heap)."""
+    """A synthetic column generated on the device: BE dictionary bytes + BE forward bytes (+ the bitmap inverted index
+    bytes) as device tensors and the host-side dictionary (needed for predicate lowering, as the reference keeps its
+    Dictionary on heap).  kind: "sv" (bit-packed), "sorted" ((start, end) pairs), "mv" (FixedBitMVForwardIndexWriter)."""
     spec: ColSpec
     num_docs: int
     cardinality: int
@@ -208,17 +254,29 @@ class DeviceColumn:
     dict_values: np.ndarray      # host, sorted unique
     dict_be: object              # torch uint8 (device)
     fwd_be: object               # torch uint8 (device)
+    kind: str = "sv"
+    num_values: int = 0          # MV: totalNumberOfEntries
+    max_mv: int = 0
+    inv_be: object = None        # torch uint8 (device): BitmapInvertedIndexWriter layout, or None
+
+    def _column(self) -> Column:
+        return Column(self.spec.name, self.spec.data_type, self.kind != "mv",
+                      Dictionary(self.spec.data_type, self.dict_values), self.num_docs, self.bits,
+                      self.kind == "sorted", self.num_values or self.num_docs, self.max_mv)
 
     def meta_column(self) -> Column:
-        """Host metadata + dictionary only (the forward index stays on the device)."""
-        return Column(self.spec.name, self.spec.data_type, True, Dictionary(self.spec.data_type, self.dict_values),
-                      self.num_docs, self.bits, False, self.num_docs)
+        """Host metadata + dictionary only (the indexes stay on the device); `inverted` marks an inverted index."""
+        col = self._column()
+        if self.inv_be is not None:
+            col.inverted = b"<device>"
+        return col
 
     def host_column(self) -> Column:
         """Copy to host as a reference-format Column (for the CPU oracle / baseline)."""
-        col = Column(self.spec.name, self.spec.data_type, True, Dictionary(self.spec.data_type, self.dict_values),
-                     self.num_docs, self.bits, False, self.num_docs)
+        col = self._column()
         col.fwd = self.fwd_be.cpu().numpy().tobytes()
+        if self.inv_be is not None:
+            col.inverted = self.inv_be.cpu().numpy().tobytes()
         return col
 
 
@@ -235,4 +293,122 @@ def make_columns_torch(specs: Sequence[ColSpec], seg_index: int, rows_per_segmen
         b = num_bits_per_value(card - 1)
         out.append(DeviceColumn(s, rows_per_segment, card, b, uniq.cpu().numpy().astype(np.int32),
                                 be_int32_torch(uniq), pack_bits_torch(inv.to(torch.int64), b)))
+    return out
+
+
+# ----------------------------------------------------------------------------------------- config 5 (device)
+
+def _le_bytes(x, nbytes: int):
+    """Little-endian bytes of int64 tensor x: [n, nbytes] uint8."""
+    import torch
+    sh = torch.arange(nbytes, device=x.device, dtype=torch.int64) * 8
+    return ((x.unsqueeze(1) >> sh) & 255).to(torch.uint8)
+
+
+def inverted_index_torch(ids, card: int, num_docs: int):
+    """BitmapInvertedIndexWriter bytes ((card + 1) BE uint32 offsets, then per dictId a portable RoaringBitmap of its
+    docs) built on the device for a column whose every dictId occurs.  Containers are arrays (<= 4 096 docs) or
+    bitmaps, as RoaringBitmap chooses without runOptimize gains (checked: no container here would shrink as runs)."""
+    import torch
+    dev = ids.device
+    n = ids.numel()
+    docs = torch.arange(n, device=dev, dtype=torch.int64)
+    sv, order = torch.sort(ids * (1 << 32) + docs)
+    sdoc = sv & 0xFFFFFFFF
+    sval = sv >> 32
+    nkeys = (num_docs + 65535) >> 16
+    cid = sval * nkeys + (sdoc >> 16)
+    cu, ccount = torch.unique_consecutive(cid, return_counts=True)
+    nc = cu.numel()
+    cval, ckey = cu // nkeys, cu % nkeys
+    # run containers would be chosen when 2 + 4 * runs < plain size (RoaringBitmap.runOptimize)
+    cstart = torch.cumsum(ccount, 0) - ccount
+    entry_c = torch.repeat_interleave(torch.arange(nc, device=dev), ccount)
+    low = sdoc & 0xFFFF
+    brk = torch.ones(n, dtype=torch.int64, device=dev)
+    brk[1:] = ((low[1:] - low[:-1]) != 1).to(torch.int64) | (entry_c[1:] != entry_c[:-1]).to(torch.int64)
+    runs = torch.zeros(nc, dtype=torch.int64, device=dev).index_add_(0, entry_c, brk)
+    is_bm = ccount > 4096
+    psize = torch.where(is_bm, torch.full_like(ccount, 8192), 2 * ccount)
+    if bool(((2 + 4 * runs) < psize).any()):
+        raise ValueError("a run container would be smaller: not generated on the device")
+    nv = torch.bincount(cval, minlength=card)
+    if bool((nv == 0).any()):
+        raise ValueError("every dictId must occur")
+    vstart_c = torch.cumsum(nv, 0) - nv                      # first container of each value
+    rank_c = torch.arange(nc, device=dev) - vstart_c[cval]   # container index within its bitmap
+    hdr = 8 + 8 * nv                                         # cookie + size + (key, card-1) pairs + offsets
+    pay = torch.zeros(card, dtype=torch.int64, device=dev).index_add_(0, cval, psize)
+    size_v = hdr + pay
+    base = 4 * (card + 1)
+    off_v = base + torch.cumsum(size_v, 0) - size_v          # absolute position of each bitmap in the file
+    total = base + int(size_v.sum())
+    out = torch.zeros(total, dtype=torch.uint8, device=dev)
+    head = torch.cat([off_v, torch.tensor([total], device=dev)])
+    out[:base] = torch.stack([(head >> 24) & 255, (head >> 16) & 255, (head >> 8) & 255, head & 255],
+                             dim=1).to(torch.uint8).reshape(-1)
+    p = off_v.unsqueeze(1) + torch.arange(8, device=dev)
+    out[p.reshape(-1)] = torch.cat([_le_bytes(torch.full_like(nv, 12346), 4), _le_bytes(nv, 4)], dim=1).reshape(-1)
+    pc = off_v[cval] + 8 + 4 * rank_c
+    out[(pc.unsqueeze(1) + torch.arange(4, device=dev)).reshape(-1)] = \
+        torch.cat([_le_bytes(ckey, 2), _le_bytes(ccount - 1, 2)], dim=1).reshape(-1)
+    # payload offsets (from the bitmap's start): header, then the payloads of the earlier containers of the value
+    pexcl = torch.cumsum(psize, 0) - psize
+    prel = hdr[cval] + pexcl - pexcl[vstart_c[cval]]
+    po = off_v[cval] + 8 + 4 * nv[cval] + 4 * rank_c
+    out[(po.unsqueeze(1) + torch.arange(4, device=dev)).reshape(-1)] = _le_bytes(prel, 4).reshape(-1)
+    pay_at = off_v[cval] + prel                              # absolute payload position of each container
+    arr = ~is_bm[entry_c]
+    erank = torch.arange(n, device=dev) - cstart[entry_c]
+    pa = pay_at[entry_c][arr] + 2 * erank[arr]
+    out[(pa.unsqueeze(1) + torch.arange(2, device=dev)).reshape(-1)] = _le_bytes(low[arr], 2).reshape(-1)
+    bm = ~arr
+    if bool(bm.any()):
+        pb = pay_at[entry_c][bm] + (low[bm] >> 3)
+        acc = torch.zeros(total, dtype=torch.int32, device=dev)
+        acc.index_add_(0, pb, (1 << (low[bm] & 7)).to(torch.int32))
+        out |= acc.to(torch.uint8)
+    return out
+
+
+def make_index_columns_torch(seg_index: int, n: int, device) -> List[DeviceColumn]:
+    """One config-5 segment on the device, in the reference's byte layouts (same values as index_values_np)."""
+    import torch
+    out = []
+    row0 = seg_index * n
+    # sortedCol: value = dictId (every value of [0, 100 000) occurs when n >= 100 000), (start, end) pairs
+    sv = (torch.arange(n, device=device, dtype=torch.int64) * INDEX_SORTED.range) // n
+    uniq, cnt = torch.unique_consecutive(sv, return_counts=True)
+    ends = torch.cumsum(cnt, 0) - 1
+    starts = ends - cnt + 1
+    card = uniq.numel()
+    pairs = torch.stack([starts, ends], dim=1).reshape(-1)
+    out.append(DeviceColumn(INDEX_SORTED, n, card, num_bits_per_value(card - 1), uniq.cpu().numpy().astype(np.int32),
+                            be_int32_torch(uniq), be_int32_torch(pairs), kind="sorted"))
+    rows = torch.arange(row0, row0 + n, dtype=torch.int64, device=device)
+    for s in INDEX_INVERTED:
+        h = hash32_torch(rows, column_salt(s.name))
+        v = s.lo + ((h * s.range) >> 32)
+        uq, inv = torch.unique(v, sorted=True, return_inverse=True)
+        c = uq.numel()
+        b = num_bits_per_value(c - 1)
+        out.append(DeviceColumn(s, n, c, b, uq.cpu().numpy().astype(np.int32), be_int32_torch(uq),
+                                pack_bits_torch(inv.to(torch.int64), b), inv_be=inverted_index_torch(inv, c, n)))
+    lengths = 1 + (hash32_torch(rows, column_salt("mvTags.len")) % 7)
+    nvals = int(lengths.sum())
+    vrows = torch.arange(seg_index * n * 8, seg_index * n * 8 + nvals, dtype=torch.int64, device=device)
+    v = INDEX_MV.lo + ((hash32_torch(vrows, column_salt(INDEX_MV.name)) * INDEX_MV.range) >> 32)
+    uq, inv = torch.unique(v, sorted=True, return_inverse=True)
+    c = uq.numel()
+    b = num_bits_per_value(c - 1)
+    starts = torch.cumsum(lengths, 0) - lengths
+    dpc = int(np.ceil(np.float32(2048) / np.float32(nvals // n)))  # FixedBitMVForwardIndexReader.java:61
+    nchunks = (n + dpc - 1) // dpc
+    chunk_offsets = be_int32_torch(starts[::dpc][:nchunks])
+    nbytes = (nvals + 7) // 8
+    bits = torch.zeros(nbytes, dtype=torch.int32, device=device)
+    bits.index_add_(0, starts >> 3, (128 >> (starts & 7)).to(torch.int32))  # MSB-first (PinotDataBitSet)
+    fwd = torch.cat([chunk_offsets, bits.to(torch.uint8), pack_bits_torch(inv.to(torch.int64), b)])
+    out.append(DeviceColumn(INDEX_MV, n, c, b, uq.cpu().numpy().astype(np.int32), be_int32_torch(uq), fwd, kind="mv",
+                            num_values=nvals, max_mv=int(lengths.max())))
     return out

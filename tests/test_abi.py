@@ -11,14 +11,18 @@ import pytest
 from pinot_amd import abi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "pinot_gpu.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in sorted(os.listdir(os.path.join(ROOT, "include")))
+           if h.endswith(".h")]
 LIB = os.path.join(ROOT, "pinot_amd", "libpinot_gpu.so")
 
 
 def header_functions():
-    with open(HEADER) as f:
-        src = f.read()
-    return sorted(set(re.findall(r"^(?:int|uint32_t)\s+(pg_\w+)\s*\(", src, flags=re.M)))
+    """Every entry point declared by include/*.h (pinot_gpu.h: the query path; pinot_codec.h: the chunk codecs)."""
+    names = set()
+    for h in HEADERS:
+        with open(h) as f:
+            names |= set(re.findall(r"^(?:int|uint32_t)\s+(pg_\w+)\s*\(", f.read(), flags=re.M))
+    return sorted(names)
 
 
 def test_header_and_mirror_agree():
@@ -53,7 +57,8 @@ STRUCTS = ["pg_col_desc", "pg_leaf", "pg_agg", "pg_key", "pg_segment_ref", "pg_o
 
 def test_struct_layouts_match_header(tmp_path):
     src = tmp_path / "sz.c"
-    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
+    header = os.path.join(ROOT, "include", "pinot_gpu.h")
+    lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{header}"', "int main(void){"]
     for s in STRUCTS:
         lines.append(f'printf("{s} %zu\\n", sizeof({s}));')
         for name, _ in getattr(abi, s)._fields_:

@@ -4,7 +4,11 @@ raw-value predicates and aggregations over it, on the oracle and the device.
 
 Pinned by the reference's own bytes: tests/golden/raw_fwd/ holds the three fixtures of
 FixedByteChunkSVForwardIndexTest.java:255-291 (fixedByteSVRDoubles.v1: v1 SNAPPY, 10 009 doubles i;
-fixedByteCompressed.v2: v2 SNAPPY, and fixedByteRaw.v2: v2 PASS_THROUGH, 2 000 doubles i + 100.2356)."""
+fixedByteCompressed.v2: v2 SNAPPY, and fixedByteRaw.v2: v2 PASS_THROUGH, 2 000 doubles i + 100.2356).
+
+The LZ4 / LZ4_LENGTH_PREFIXED / ZSTANDARD chunk decoders of libpinot_gpu (pg_codec.hip, pg_chunk_decompress) are pinned
+against independent encoders: the system liblz4 / libzstd (the native libraries lz4-java 1.8.0 and zstd-jni 1.4.9-5 wrap)
+compress the data, the library must return it unchanged.  The reference holds no LZ4 / ZSTD chunk bytes."""
 import os
 
 import numpy as np
@@ -12,7 +16,8 @@ import pytest
 
 from pinot_amd.plan import Table, UnsupportedQuery, reduce_to_rows
 from pinot_amd.query import parse
-from pinot_amd.segment import (Column, ImmutableSegment, raw_forward_bytes, raw_forward_header, raw_forward_values)
+from pinot_amd.segment import (CHUNK_CODECS, Column, ImmutableSegment, chunk_compress, chunk_decompress,
+                               raw_forward_bytes, raw_forward_header, raw_forward_values)
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "raw_fwd")
 FIXTURES = [("fixedByteSVRDoubles.v1", 10009, 0.0, 1), ("fixedByteCompressed.v2", 2000, 100.2356, 1),
@@ -43,7 +48,100 @@ def test_writer_round_trip(version, dtype):
     assert np.array_equal(raw_forward_values(b, dtype), vals)
 
 
-def _raw_segments(n_segs=3, rows=50_000, seed=7):
+def _codec_cases():
+    rng = np.random.default_rng(11)
+    cases = [b"", b"a", b"abc" * 1000, bytes(70000), rng.integers(0, 256, 5000, dtype=np.uint8).tobytes(),
+             np.arange(20000, dtype=">i4").tobytes(), rng.normal(size=9000).astype(">f8").tobytes(),
+             np.sort(rng.integers(0, 10 ** 9, 8000)).astype(">i8").tobytes(), b"The quick brown fox. " * 3000]
+    for _ in range(12):
+        n, k = int(rng.integers(1, 60000)), int(rng.integers(1, 300))
+        cases.append((rng.integers(0, k, n) * int(rng.integers(1, 1000))).astype(rng.choice([">i4", ">i8"])).tobytes())
+    return cases
+
+
+@pytest.mark.parametrize("codec", ["SNAPPY", "LZ4", "LZ4_LENGTH_PREFIXED", "ZSTANDARD"])
+def test_chunk_codecs_round_trip_independent_encoders(codec):
+    """ChunkDecompressor.decompress restated in C (pg_chunk_decompress) returns what an independent encoder packed:
+    liblz4 for LZ4 (block; length-prefixed = LZ4CompressorWithLength), libzstd level 3 (zstd-jni's default) and
+    further levels / strategies for ZSTANDARD."""
+    code = CHUNK_CODECS[codec]
+    for b in _codec_cases():
+        assert chunk_decompress(code, chunk_compress(code, b), len(b)) == b
+    if codec == "ZSTANDARD":  # other levels exercise other block / table modes (raw, RLE, repeat, 4-stream literals)
+        import ctypes as C
+        zs = C.CDLL("libzstd.so.1")
+        zs.ZSTD_compressBound.restype = C.c_size_t
+        zs.ZSTD_compress.restype = C.c_size_t
+        zs.ZSTD_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_int]
+        for lvl in (-5, 1, 9, 19):
+            for b in _codec_cases():
+                cap = zs.ZSTD_compressBound(C.c_size_t(len(b)))
+                buf = C.create_string_buffer(max(cap, 1))
+                n = zs.ZSTD_compress(buf, cap, b, len(b), lvl)
+                assert chunk_decompress(code, buf.raw[:n], len(b)) == b, (lvl, len(b))
+
+
+def test_chunk_codec_rejects_corrupt_input():
+    from pinot_amd.gpu import PinotGpuError
+    from pinot_amd.plan import UnsupportedQuery as U
+    data = np.arange(5000, dtype=">i8").tobytes()
+    for codec in ("LZ4", "ZSTANDARD", "SNAPPY"):
+        c = bytearray(chunk_compress(CHUNK_CODECS[codec], data))
+        c[len(c) // 2] ^= 0xFF
+        c = bytes(c[:len(c) - 3])
+        with pytest.raises((PinotGpuError, U)):
+            chunk_decompress(CHUNK_CODECS[codec], c, len(data))
+
+
+@pytest.mark.parametrize("codec", ["SNAPPY", "LZ4", "LZ4_LENGTH_PREFIXED", "ZSTANDARD"])
+@pytest.mark.parametrize("version", [2, 3, 4])
+def test_compressed_writer_round_trip(codec, version):
+    rng = np.random.default_rng(version)
+    vals = rng.integers(-10 ** 4, 10 ** 4, 23456).astype(np.int64)
+    b = raw_forward_bytes(vals, "LONG", version, 1000, compression=codec)
+    h = raw_forward_header(b)
+    assert (h["version"], h["total"], h["compression"]) == (version, 23456, CHUNK_CODECS[codec])
+    assert np.array_equal(raw_forward_values(b, "LONG"), vals)
+
+
+def test_v4_chunks_are_a_power_of_two():
+    """FixedBytePower2ChunkSVForwardIndexReader finds doc d in chunk d >>> numberOfTrailingZeros(numDocsPerChunk): a v4
+    file is written with a power-of-two chunk size, and that lookup finds every doc's value in its chunk."""
+    vals = np.arange(10_000, dtype=np.int32) * 3 - 7
+    b = raw_forward_bytes(vals, "INT", 4, 1000, compression="LZ4")
+    h = raw_forward_header(b)
+    dpc = h["docs_per_chunk"]
+    assert dpc == 1024 and dpc & (dpc - 1) == 0
+    shift = dpc.bit_length() - 1
+    ends = list(h["offsets"][1:]) + [len(b)]
+    for d in (0, 1, 1023, 1024, 5000, 9999):
+        c = d >> shift
+        chunk = chunk_decompress(h["compression"], b[h["offsets"][c]:ends[c]], dpc * 4)
+        assert np.frombuffer(chunk, dtype=">i4")[d & (dpc - 1)] == vals[d]
+    bad = bytearray(b)
+    bad[8:12] = (1000).to_bytes(4, "big")
+    with pytest.raises(ValueError):
+        raw_forward_header(bytes(bad))
+
+
+def test_default_raw_dimension_is_lz4(oracle_engine):
+    """SegmentColumnarIndexCreator.getColumnCompressionType (:356-368): a raw DIMENSION column is LZ4 by default, a
+    METRIC PASS_THROUGH; the LZ4 column loads (decoded by the library) and queries match numpy."""
+    rng = np.random.default_rng(3)
+    n = 30_011
+    d = rng.integers(-1000, 1000, n)
+    m = rng.integers(0, 50, n)
+    seg = ImmutableSegment.create("lz", {"d": d, "m": m}, {"d": "INT", "m": "LONG"}, no_dictionary=("d", "m"),
+                                  field_types={"d": "DIMENSION", "m": "METRIC"})
+    assert raw_forward_header(seg.columns["d"].fwd)["compression"] == CHUNK_CODECS["LZ4"]
+    assert raw_forward_header(seg.columns["m"].fwd)["compression"] == CHUNK_CODECS["PASS_THROUGH"]
+    assert np.array_equal(raw_forward_values(seg.columns["d"].fwd, "INT"), d)
+    r = oracle_engine.execute(Table("t", [seg]), "SELECT COUNT(*), SUM(m), MIN(d) FROM t WHERE d > 100")
+    k = d > 100
+    assert r.rows[()] == [int(k.sum()), float(m[k].sum()), float(d[k].min())]
+
+
+def _raw_segments(n_segs=3, rows=50_000, seed=7, codecs=None):
     rng = np.random.default_rng(seed)
     segs = []
     for s in range(n_segs):
@@ -54,7 +152,8 @@ def _raw_segments(n_segs=3, rows=50_000, seed=7):
         segs.append(ImmutableSegment.create(
             f"r{s}", data, {"k": "INT", "m_int": "INT", "m_long": "LONG", "m_float": "FLOAT", "m_double": "DOUBLE",
                             "u": "INT"},
-            no_dictionary=("m_int", "m_long", "m_float", "m_double", "u"), raw_version=2 + s % 3))
+            no_dictionary=("m_int", "m_long", "m_float", "m_double", "u"), raw_version=2 + s % 3,
+            raw_compression=codecs))
     return segs
 
 
@@ -221,3 +320,27 @@ def test_reference_fixture_bytes_on_device(name, n, start, compression, gpu_engi
     row = gpu_engine.execute(t, q).rows[()]
     assert row[0] == exp.size and row[2] == exp.min() and row[3] == exp.max()
     assert np.isclose(row[1], exp.sum(), rtol=1e-12)
+
+
+CODEC_MIX = {"m_int": "LZ4", "m_long": "ZSTANDARD", "m_float": "LZ4_LENGTH_PREFIXED", "m_double": "SNAPPY",
+             "u": "ZSTANDARD"}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sql", RAW_QUERIES)
+def test_compressed_raw_columns_gpu(sql, gpu_engine, oracle_engine):
+    """LZ4 / ZSTANDARD / LZ4_LENGTH_PREFIXED / SNAPPY chunks decoded by the library at upload: the device results equal
+    the oracle's over the same segments."""
+    from helpers import assert_same_result
+    t = _compressed_table()
+    q = parse(sql)
+    assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q), table=t)
+
+
+_COMPRESSED = []
+
+
+def _compressed_table():
+    if not _COMPRESSED:
+        _COMPRESSED.append(Table("t", _raw_segments(3, 40_000, seed=9, codecs=CODEC_MIX)))
+    return _COMPRESSED[0]

@@ -7,7 +7,9 @@ dispatches of each pass are warm-up launches and are kept (every launch of the b
 
 usage: traffic_json.py <pmc summary txt> <bench json of the profiled command>"""
 import collections
+import hashlib
 import json
+import os
 import statistics
 import sys
 
@@ -32,7 +34,9 @@ per = {k: {"fetch_size_kib_median": statistics.median(fetch[k]),
            "write_size_kib_median": statistics.median(write[k]) if write.get(k) else 0.0} for k in fetch}
 rd = sum(2 * 1024 * v["fetch_size_kib_median"] for v in per.values()) if per else None
 wr = sum(1024 * v["write_size_kib_median"] for v in per.values()) if per else None
+lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "pinot_amd", "libpinot_gpu.so")
 print(json.dumps({"kernel": " + ".join(sorted(per)) or None, "config": bench.get("config"), "per_kernel": per,
+                  "lib_md5": hashlib.md5(open(lib, "rb").read()).hexdigest(),
                   "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
                   "traffic_bytes_per_launch": (rd or 0) + (wr or 0) if rd is not None else None,
                   "correction": "FETCH_SIZE x2 (gfx950 half-count of wide streaming reads), KiB -> bytes"}))
