@@ -34,6 +34,20 @@ struct RoaringContainer {
 hipError_t launch_roaring_or(const uint8_t* roaring, const RoaringContainer* containers, const uint32_t* sel,
                              uint32_t nsel, uint32_t num_docs, uint32_t* bitmap, hipStream_t s);
 hipError_t launch_bitmap_not(uint32_t* bitmap, uint32_t num_docs, hipStream_t s);
+// Inverted-index leaves of a query, all segments in one launch (BitmapBasedFilterOperator: the OR of the selected
+// dictIds' roaring bitmaps, flipped when exclusive).  One workgroup per (job, 64 K-doc key): it ORs every selected
+// dictId's container of that key into an LDS chunk, then writes the chunk's words of the doc bitmap once (negated for
+// NOT_EQ / NOT_IN).  Keys [key0, key0 + nkeys) only: a root-AND doc range (sorted leaf) bounds the docs ever read.
+struct RoaringJob {
+  const uint8_t* roaring;          // container payloads (8-byte aligned)
+  const RoaringContainer* cs;      // container directory, per dictId sorted by key
+  const uint32_t* dir;             // [card + 1] first container of each dictId
+  const int32_t* ids;              // selected dictIds (sorted)
+  uint32_t nids, num_docs;
+  uint32_t* bm;                    // doc bitmap (packed 1-bit column order)
+  uint32_t negate, key0, nkeys, first_block;  // first_block: prefix of nkeys over the jobs
+};
+hipError_t launch_roaring_keys(const RoaringJob* jobs, uint32_t njobs, uint32_t blocks, hipStream_t s);
 hipError_t launch_mv_scan(const uint32_t* words, uint32_t bits, const uint32_t* offsets, uint32_t num_docs,
                           int32_t lo, int32_t hi, const uint32_t* lut, uint32_t excl, uint32_t* bitmap,
                           hipStream_t s);

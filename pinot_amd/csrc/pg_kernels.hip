@@ -324,6 +324,78 @@ hipError_t launch_roaring_or(const uint8_t* roaring, const RoaringContainer* con
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void roaring_keys_kernel(const RoaringJob* __restrict__ jobs, uint32_t njobs) {
+  __shared__ uint32_t chunk[2048];     // the key's 65 536 docs
+  __shared__ uint32_t bml[256];        // bitmap containers of this round, processed by the whole block
+  __shared__ uint32_t nbml;
+  uint32_t lo = 0, hi = njobs;         // the job whose block range holds this block
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (jobs[mid].first_block <= blockIdx.x) lo = mid; else hi = mid;
+  }
+  const RoaringJob J = jobs[lo];
+  const uint32_t key = J.key0 + (blockIdx.x - J.first_block), tid = threadIdx.x;
+  for (uint32_t w = tid; w < 2048; w += 256) chunk[w] = 0;
+  if (tid == 0) nbml = 0;
+  __syncthreads();
+  for (uint32_t r0 = 0; r0 < J.nids; r0 += 256) {
+    const uint32_t i = r0 + tid;
+    if (i < J.nids) {
+      const uint32_t id = (uint32_t)J.ids[i];
+      uint32_t a = J.dir[id], b = J.dir[id + 1];  // this dictId's containers, ascending keys: find `key`
+      while (a < b) {
+        const uint32_t m = (a + b) >> 1;
+        if (J.cs[m].key < key) a = m + 1; else b = m;
+      }
+      if (a < J.dir[id + 1] && J.cs[a].key == key) {
+        const RoaringContainer c = J.cs[a];
+        const uint8_t* p = J.roaring + c.offset;
+        if (c.type == 0) {  // array of uint16
+          const uint16_t* v = (const uint16_t*)p;
+          for (uint32_t e = 0; e < c.card; e++) atomicOr(&chunk[v[e] >> 5], 0x80000000u >> (v[e] & 31u));
+        } else if (c.type == 2) {  // runs: uint16 nruns, then (start, length - 1)
+          const uint16_t* rr = (const uint16_t*)p + 1;
+          for (uint32_t k = 0; k < c.card; k++) {
+            const uint32_t st = rr[2 * k], en = st + rr[2 * k + 1];
+            for (uint32_t w = st >> 5; w <= (en >> 5); w++) {
+              const uint32_t l = w * 32 > st ? 0 : st - w * 32, h = w * 32 + 31 < en ? 31 : en - w * 32;
+              const uint32_t mask = (h == 31 ? 0xFFFFFFFFu : ((1u << (h + 1)) - 1u)) & ~((1u << l) - 1u);
+              atomicOr(&chunk[w], __builtin_bitreverse32(mask));
+            }
+          }
+        } else {
+          bml[atomicAdd(&nbml, 1u)] = c.offset;
+        }
+      }
+    }
+    __syncthreads();
+    for (uint32_t k = 0; k < nbml; k++) {  // bitmap containers: 1 024 little-endian uint64 words each
+      const uint32_t* w32 = (const uint32_t*)(J.roaring + bml[k]);
+      for (uint32_t w = tid; w < 2048; w += 256) chunk[w] |= __builtin_bitreverse32(w32[w]);
+      __syncthreads();
+    }
+    if (tid == 0) nbml = 0;
+    __syncthreads();
+  }
+  const uint32_t nwords = (J.num_docs + 31) / 32, tail = J.num_docs & 31u;
+  for (uint32_t w = tid; w < 2048; w += 256) {
+    const uint32_t gw = key * 2048 + w;
+    if (gw >= nwords) break;
+    uint32_t v = chunk[w];
+    if (J.negate) {
+      v = ~v;
+      if (gw == nwords - 1 && tail) v &= ~(0xFFFFFFFFu >> tail);
+    }
+    J.bm[gw] = v;
+  }
+}
+
+hipError_t launch_roaring_keys(const RoaringJob* jobs, uint32_t njobs, uint32_t blocks, hipStream_t s) {
+  if (!njobs || !blocks) return hipSuccess;
+  hipLaunchKernelGGL(roaring_keys_kernel, dim3(blocks), dim3(256), 0, s, jobs, njobs);
+  return hipGetLastError();
+}
+
 __global__ void bitmap_not_kernel(uint32_t* bm, uint32_t num_docs) {
   const uint32_t nwords = (num_docs + 31) / 32;
   const uint32_t stride = gridDim.x * blockDim.x;

@@ -260,32 +260,66 @@ __device__ __forceinline__ uint64_t col_key_of(uint32_t kind, int64_t base, cons
   return (uint64_t)(v - base);
 }
 
-// The level-1 digit and 32-bit entry of doc d (keys / value of segment sd).  A key or value outside its space (never
+// The level-1 digits and 32-bit entries of the round's docs r0 + tid + kST * j (j < E, those < m valid), every key
+// and value column's window loads issued before any is consumed.  The segment's key / value descriptors are held in
+// registers for the whole item (NK: compile-time bound on the keys).  A key or value outside its space (never
 // expected: the host proved the ranges) reports an error bit and lands in partition 0; hist and scatter agree.
-__device__ __forceinline__ void part_entry(const PartScanSpec& P, const ColDesc* kc, const ColDesc& vc, uint32_t d,
-                                           uint32_t& digit, uint32_t& entry) {
-  uint64_t g = 0;
-  bool bad = false;
-  for (uint32_t k = 0; k < P.num_keys; k++) {
-    const uint64_t kid = col_key_of(P.key_kind[k], P.key_base[k], kc[k], col_unpack(kc[k].words, d, kc[k].bits));
-    bad |= kid >= P.key_card[k];
-    g += kid * P.key_stride[k];
+template <int NK, int E, int J0, int JN>  // docs j in [J0, J0 + JN) of the round's E
+__device__ __forceinline__ void part_entries(const PartScanSpec& P, const ColDesc (&kc)[NK], const ColDesc& vc,
+                                             uint32_t r0, uint32_t m, uint32_t (&dg)[E], uint32_t (&ent)[E]) {
+  const uint32_t tid = threadIdx.x;
+  const bool has_val = P.val_agg != (uint32_t)kNoSlot;
+  uint32_t raw[NK][JN], vraw[JN];
+#pragma unroll
+  for (int k = 0; k < NK; k++)
+#pragma unroll
+    for (int jj = 0; jj < JN; jj++) {
+      const uint32_t i = tid + kST * (J0 + jj);
+      raw[k][jj] = (i < m && (uint32_t)k < P.num_keys) ? col_unpack(kc[k].words, r0 + i, kc[k].bits) : 0u;
+    }
+#pragma unroll
+  for (int jj = 0; jj < JN; jj++) {
+    const uint32_t i = tid + kST * (J0 + jj);
+    vraw[jj] = (i < m && has_val) ? col_unpack(vc.words, r0 + i, vc.bits) : 0u;
   }
-  uint32_t vid = 0;
-  if (P.val_agg != (uint32_t)kNoSlot) {
-    const uint64_t v = col_key_of(P.val.key_kind, P.val.key_base, vc, col_unpack(vc.words, d, vc.bits));
-    if (v >= P.val.key_card) atomicOr(P.err, 2u);
-    else vid = (uint32_t)v;
+#pragma unroll
+  for (int jj = 0; jj < JN; jj++) {
+    const int j = J0 + jj;
+    uint64_t g = 0;
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < NK; k++) {
+      if ((uint32_t)k >= P.num_keys) break;
+      const uint64_t kid = col_key_of(P.key_kind[k], P.key_base[k], kc[k], raw[k][jj]);
+      bad |= kid >= P.key_card[k];
+      g += kid * P.key_stride[k];
+    }
+    uint32_t vid = 0;
+    if (has_val) {
+      const uint64_t v = col_key_of(P.val.key_kind, P.val.key_base, vc, vraw[jj]);
+      if (v < P.val.key_card) vid = (uint32_t)v;
+      else if (tid + kST * j < m) atomicOr(P.err, 2u);
+    }
+    if (bad) {
+      if (tid + kST * j < m) atomicOr(P.err, 1u);
+      g = 0;
+    }
+    dg[j] = (uint32_t)(g >> P.shift1);
+    ent[j] = (uint32_t)(((g & ((1ull << P.shift1) - 1ull)) << P.vbits) | vid);
   }
-  if (bad) {
-    atomicOr(P.err, 1u);
-    g = 0;
-  }
-  digit = (uint32_t)(g >> P.shift1);
-  entry = (uint32_t)(((g & ((1ull << P.shift1) - 1ull)) << P.vbits) | vid);
 }
 
+template <int NK>
+__device__ __forceinline__ void item_cols(const PartScanSpec& P, const SegDesc& sd, ColDesc (&kc)[NK], ColDesc& vc) {
+#pragma unroll
+  for (int k = 0; k < NK; k++)
+    if ((uint32_t)k < P.num_keys) kc[k] = sd.keycols[k];
+  if (P.val_agg != (uint32_t)kNoSlot) vc = sd.aggcols[2 * P.val_agg];
+}
+
+template <int NK>
 __global__ __launch_bounds__(kST) void part_hist_kernel(PartScanSpec P) {
+  constexpr int E = kSplitChunk / kST;
   __shared__ uint32_t h[kPartL1];
   const uint32_t b = blockIdx.x, tid = threadIdx.x;
   for (uint32_t i = tid; i < kPartL1; i += kST) h[i] = 0;
@@ -294,28 +328,24 @@ __global__ __launch_bounds__(kST) void part_hist_kernel(PartScanSpec P) {
   for (uint64_t it = i0; it < i1; it++) {
     const WorkItem w = P.items[it];
     const SegDesc sd = P.segs[w.seg];
-    const ColDesc* kc = sd.keycols;
-    const ColDesc vc = P.val_agg != (uint32_t)kNoSlot ? sd.aggcols[2 * P.val_agg] : kc[0];
+    ColDesc kc[NK], vc;
+    item_cols<NK>(P, sd, kc, vc);
     const uint32_t d0 = w.tile_begin * (uint32_t)kTileDocs, d1 = min(w.tile_end * (uint32_t)kTileDocs, sd.num_docs);
-    for (uint32_t r0 = d0; r0 < d1; r0 += kSplitChunk) {  // the scatter's rounds: E docs per lane, loads in flight together
-      constexpr int E = kSplitChunk / kST;
+    for (uint32_t r0 = d0; r0 < d1; r0 += kSplitChunk) {  // the scatter's rounds
       const uint32_t m = min(kSplitChunk, d1 - r0);
-      uint32_t dg[E];
+      uint32_t dg[E], e[E];
+      part_entries<NK, E, 0, E / 2>(P, kc, vc, r0, m, dg, e);
+      part_entries<NK, E, E / 2, E / 2>(P, kc, vc, r0, m, dg, e);
 #pragma unroll
-      for (int k = 0; k < E; k++) {
-        uint32_t e;
-        dg[k] = 0;
-        if (tid + kST * k < m) part_entry(P, kc, vc, r0 + tid + kST * k, dg[k], e);
-      }
-#pragma unroll
-      for (int k = 0; k < E; k++)
-        if (tid + kST * k < m) atomicAdd(&h[dg[k]], 1u);
+      for (int j = 0; j < E; j++)
+        if (tid + kST * j < m) atomicAdd(&h[dg[j]], 1u);
     }
   }
   __syncthreads();
   for (uint32_t p = tid; p < P.nparts1; p += kST) P.hist1[(uint64_t)p * P.blocks + b] = h[p];
 }
 
+template <int NK>
 __global__ __launch_bounds__(kST) void part_scatter_kernel(PartScanSpec P) {
   constexpr int E = kSplitChunk / kST;
   __shared__ uint32_t cnt[kPartL1], start[kPartL1], sbuf[kSplitChunk];
@@ -331,29 +361,27 @@ __global__ __launch_bounds__(kST) void part_scatter_kernel(PartScanSpec P) {
   for (uint64_t it = i0; it < i1; it++) {
     const WorkItem w = P.items[it];
     const SegDesc sd = P.segs[w.seg];
-    const ColDesc* kc = sd.keycols;
-    const ColDesc vc = P.val_agg != (uint32_t)kNoSlot ? sd.aggcols[2 * P.val_agg] : kc[0];
+    ColDesc kc[NK], vc;
+    item_cols<NK>(P, sd, kc, vc);
     const uint32_t d0 = w.tile_begin * (uint32_t)kTileDocs, d1 = min(w.tile_end * (uint32_t)kTileDocs, sd.num_docs);
     for (uint32_t r0 = d0; r0 < d1; r0 += kSplitChunk) {
       const uint32_t m = min(kSplitChunk, d1 - r0);
       uint32_t e[E], dg[E];
-#pragma unroll
-      for (int k = 0; k < E; k++) {
-        const uint32_t i = tid + kST * k;
-        e[k] = dg[k] = 0;
-        if (i < m) part_entry(P, kc, vc, r0 + i, dg[k], e[k]);
-      }
+      part_entries<NK, E, 0, E / 2>(P, kc, vc, r0, m, dg, e);
+      part_entries<NK, E, E / 2, E / 2>(P, kc, vc, r0, m, dg, e);
       split_round<uint32_t, true>(e, dg, m, P.nparts1, cnt, start, cur, sbuf, sdig, P.out1);
     }
   }
 }
 
 hipError_t launch_part_hist(const PartScanSpec& p, hipStream_t s) {
-  hipLaunchKernelGGL(part_hist_kernel, dim3(p.blocks), dim3(kST), 0, s, p);
+  if (p.num_keys <= 1) hipLaunchKernelGGL(part_hist_kernel<1>, dim3(p.blocks), dim3(kST), 0, s, p);
+  else hipLaunchKernelGGL(part_hist_kernel<kMaxKeys>, dim3(p.blocks), dim3(kST), 0, s, p);
   return hipGetLastError();
 }
 hipError_t launch_part_scatter(const PartScanSpec& p, hipStream_t s) {
-  hipLaunchKernelGGL(part_scatter_kernel, dim3(p.blocks), dim3(kST), 0, s, p);
+  if (p.num_keys <= 1) hipLaunchKernelGGL(part_scatter_kernel<1>, dim3(p.blocks), dim3(kST), 0, s, p);
+  else hipLaunchKernelGGL(part_scatter_kernel<kMaxKeys>, dim3(p.blocks), dim3(kST), 0, s, p);
   return hipGetLastError();
 }
 

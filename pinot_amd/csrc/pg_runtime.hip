@@ -256,8 +256,8 @@ struct ColumnRes {
   std::vector<int32_t> sorted_pairs;  // host copy for leaf lowering (card x 2)
   // inverted index
   bool has_inv = false;
-  DevBuf roaring, containers;
-  std::vector<uint32_t> inv_dir;  // CSR: containers of dictId d are [inv_dir[d], inv_dir[d+1])
+  DevBuf roaring, containers, inv_dir_dev;
+  std::vector<uint32_t> inv_dir;  // CSR: containers of dictId d are [inv_dir[d], inv_dir[d+1]) (+ a device copy)
   // keymap
   bool has_keymap = false;
   DevBuf keymap;
@@ -640,6 +640,8 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
       if (!payload.empty()) HIP_CHECK(hipMemcpyAsync(tmp.roaring.p, payload.data(), payload.size(), hipMemcpyHostToDevice, s));
       if (!cs.empty())
         HIP_CHECK(hipMemcpyAsync(tmp.containers.p, cs.data(), cs.size() * sizeof(RoaringContainer), hipMemcpyHostToDevice, s));
+      if ((rc = tmp.inv_dir_dev.alloc(4ull * tmp.inv_dir.size() + 16))) return rc;
+      HIP_CHECK(hipMemcpyAsync(tmp.inv_dir_dev.p, tmp.inv_dir.data(), 4ull * tmp.inv_dir.size(), hipMemcpyHostToDevice, s));
       HIP_CHECK(hipStreamSynchronize(s));
       break;
     }
@@ -736,6 +738,7 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
       c.has_inv = true;
       c.roaring = std::move(tmp.roaring);
       c.containers = std::move(tmp.containers);
+      c.inv_dir_dev = std::move(tmp.inv_dir_dev);
       c.inv_dir.swap(tmp.inv_dir);
       if (!c.num_docs) c.num_docs = tmp.num_docs;
       break;
@@ -882,6 +885,7 @@ struct PrepassOp {  // filter materialisation of an index-backed leaf into a doc
   int32_t lo = 0, hi = 0;
   uint64_t lut_off = ~0ull;  // MV scan: scratch LUT offset (or ~0 for a dictId range)
   uint32_t excl = 0;
+  uint32_t key0 = 0, nkeys = 0;  // ROARING: the 64 K-doc keys to build (a root-AND doc range bounds them)
 };
 
 // ---- filter program: ABI postfix -> tree -> prefix form for the kernel, AND / OR children reordered by
@@ -1818,13 +1822,26 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         case PG_LEAF_SORTED: {
           if (c->fwd != FWD_SORTED) return fail(PG_E_INVALID, "sorted leaf on unsorted column %u", pl.col_id);
           // SortedIndexBasedFilterOperator: matching dictIds -> merged [start,end] doc ranges
+          // (a sorted column's docs are ordered by dictId, so only the selected ids are visited: a dictId range is
+          // one doc range from its first to its last non-empty id)
           std::vector<int32_t> rg;
-          for (uint32_t id = 0; id < c->card; id++) {
-            if (!in_set((int32_t)id)) continue;
+          auto add_id = [&](int32_t id) {
             const int32_t s0 = c->sorted_pairs[2 * id], e0 = std::min(c->sorted_pairs[2 * id + 1], (int32_t)sr.num_docs - 1);
-            if (e0 < s0) continue;
+            if (e0 < s0) return;
             if (!rg.empty() && rg.back() + 1 >= s0) rg.back() = std::max(rg.back(), e0);
             else { rg.push_back(s0); rg.push_back(e0); }
+          };
+          if (pl.num_ids) {
+            for (uint32_t i = 0; i < pl.num_ids; i++) add_id(pl.ids[i]);
+          } else {
+            int32_t lo = std::max(pl.lo, 0), hi = std::min(pl.hi, (int32_t)c->card);
+            auto empty = [&](int32_t id) { return std::min(c->sorted_pairs[2 * id + 1], (int32_t)sr.num_docs - 1) < c->sorted_pairs[2 * id]; };
+            while (lo < hi && empty(lo)) lo++;
+            while (hi > lo && empty(hi - 1)) hi--;
+            if (lo < hi) {
+              rg.push_back(c->sorted_pairs[2 * lo]);
+              rg.push_back(std::min(c->sorted_pairs[2 * (hi - 1) + 1], (int32_t)sr.num_docs - 1));
+            }
           }
           if (pl.exclusive) {  // complement within [0, num_docs)
             std::vector<int32_t> cm;
@@ -1851,20 +1868,21 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         }
         case PG_LEAF_INVERTED: {
           if (!c->has_inv) return fail(PG_E_INVALID, "inverted leaf on column %u without inverted index", pl.col_id);
-          std::vector<uint32_t> sel;
-          if (pl.num_ids) {
-            for (uint32_t i = 0; i < pl.num_ids; i++)
-              for (uint32_t x = c->inv_dir[pl.ids[i]]; x < c->inv_dir[pl.ids[i] + 1]; x++) sel.push_back(x);
-          } else {
-            const int32_t lo = std::max(pl.lo, 0), hi = std::min(pl.hi, (int32_t)c->card);
-            for (int32_t id = lo; id < hi; id++)
-              for (uint32_t x = c->inv_dir[id]; x < c->inv_dir[id + 1]; x++) sel.push_back(x);
-          }
           as_bitmap_leaf(dl, sr.num_docs);
           dl.excl = 0;
           PrepassOp op{PrepassOp::ROARING, si, li};
-          op.in_off = ar.put(sel.data(), 4ull * sel.size());
-          op.n = (uint32_t)sel.size();
+          if (pl.num_ids) {  // the selected dictIds; the device finds their containers per 64 K-doc key
+            op.in_off = ar.put(pl.ids, 4ull * pl.num_ids);
+            op.n = pl.num_ids;
+          } else {
+            const int32_t lo = std::max(pl.lo, 0), hi = std::max(std::min(pl.hi, (int32_t)c->card), lo);
+            const uint64_t at = ar.reserve(4ull * (uint32_t)(hi - lo));
+            for (int32_t id = lo; id < hi; id++) memcpy(&ar.h[at + 4ull * (uint32_t)(id - lo)], &id, 4);
+            op.in_off = at;
+            op.n = (uint32_t)(hi - lo);
+          }
+          op.key0 = 0;
+          op.nkeys = (sr.num_docs + 65535) >> 16;
           op.num_docs = sr.num_docs;
           op.col = c;
           op.negate = pl.exclusive != 0;
@@ -1934,6 +1952,34 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     }
   }
   P.entries_in_filter = entries_in_filter;
+  // Inverted-leaf bitmaps are read only where the docs can match: a doc range among the root AND's direct children
+  // (a sorted-index leaf) bounds the 64 K-doc keys their roaring pre-pass builds.
+  if (std::any_of(pre.begin(), pre.end(), [](const PrepassOp& o) { return o.kind == PrepassOp::ROARING; }) &&
+      plan->num_ops && plan->ops[plan->num_ops - 1] < 0 && ((-plan->ops[plan->num_ops - 1]) & 0x300) == 0x100) {
+    std::vector<int> root_leaves;  // direct leaf children of the root AND (postfix: the operands on the stack)
+    std::vector<int> st;           // stack of leaf index or -1 (a subtree)
+    for (uint32_t i = 0; i < plan->num_ops; i++) {
+      const int32_t op = plan->ops[i];
+      if (op >= 0) { st.push_back(op); continue; }
+      const int n = op == PG_OP_NOT ? 1 : ((-op) & 0xFF);
+      if (i + 1 == plan->num_ops) root_leaves.assign(st.end() - n, st.end());
+      st.resize(st.size() - n);
+      st.push_back(-1);
+    }
+    for (PrepassOp& op : pre) {
+      if (op.kind != PrepassOp::ROARING) continue;
+      int64_t lo = 0, hi = op.num_docs;
+      for (int li : root_leaves) {
+        if (li < 0) continue;
+        const LeafDesc& dl = leaves[(uint64_t)op.seg * L + li];
+        if (dl.kind == LK_DOCRANGE) { lo = std::max<int64_t>(lo, dl.lo); hi = std::min<int64_t>(hi, dl.hi); }
+        else if (dl.kind == LK_NONE) hi = lo;
+      }
+      if (hi <= lo) { op.nkeys = 0; continue; }
+      op.key0 = (uint32_t)(lo >> 16);
+      op.nkeys = (uint32_t)(((hi - 1) >> 16) + 1) - op.key0;
+    }
+  }
 
   PG_PROF("leaves");
   // ---- pre-filter launches: per folded leaf (in order), one launch per bit width its segments read (doc ranges
@@ -2491,6 +2537,22 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     off_part_base = ar.put(base.data(), base.size() * 8);
   }
   const uint64_t off_lutjobs = ar.reserve(luts.size() * sizeof(LutJob));
+  std::vector<RoaringJob> rjobs;
+  uint32_t roaring_blocks = 0;
+  for (const PrepassOp& op : pre) {
+    if (op.kind != PrepassOp::ROARING || !op.nkeys) continue;
+    RoaringJob j;
+    memset(&j, 0, sizeof(j));
+    j.nids = op.n;
+    j.num_docs = op.num_docs;
+    j.negate = op.negate ? 1u : 0u;
+    j.key0 = op.key0;
+    j.nkeys = op.nkeys;
+    j.first_block = roaring_blocks;
+    roaring_blocks += op.nkeys;
+    rjobs.push_back(j);
+  }
+  const uint64_t off_rjobs = ar.reserve(rjobs.size() * sizeof(RoaringJob));
   DevBuf arena, scratch;
   DevBuf p_ent0, p_cnt0, p_hist1, p_off1, p_ent1, p_hist2, p_off2, p_ent2, p_temp;  // GM_PART pipeline
   DevBuf l_docs, l_counts;  // selective stream: survivor regions + counts
@@ -2526,6 +2588,19 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   if (!keycols.empty()) memcpy(&ar.h[off_keycols], keycols.data(), keycols.size() * sizeof(ColDesc));
   if (!segd.empty()) memcpy(&ar.h[off_segs], segd.data(), segd.size() * sizeof(SegDesc));
   if (!lutjobs.empty()) memcpy(&ar.h[off_lutjobs], lutjobs.data(), lutjobs.size() * sizeof(LutJob));
+  {
+    size_t k = 0;
+    for (const PrepassOp& op : pre) {
+      if (op.kind != PrepassOp::ROARING || !op.nkeys) continue;
+      RoaringJob& j = rjobs[k++];
+      j.roaring = (const uint8_t*)op.col->roaring.p;
+      j.cs = (const RoaringContainer*)op.col->containers.p;
+      j.dir = (const uint32_t*)op.col->inv_dir_dev.p;
+      j.ids = (const int32_t*)(dA + op.in_off);
+      j.bm = (uint32_t*)(dS + op.out_off);
+    }
+    if (!rjobs.empty()) memcpy(&ar.h[off_rjobs], rjobs.data(), rjobs.size() * sizeof(RoaringJob));
+  }
   if (!pre_leaves.empty()) {
     memcpy(&ar.h[off_leaves_orig], leaves_orig.data(), leaves_orig.size() * sizeof(LeafDesc));
     std::vector<SegDesc> segp(segd);
@@ -2552,10 +2627,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       case PrepassOp::FILL_RANGES:
         HIP_CHECK(launch_fill_ranges((const int32_t*)(dA + op.in_off), op.n, op.num_docs, (uint32_t*)(dS + op.out_off), s));
         break;
-      case PrepassOp::ROARING:
-        HIP_CHECK(launch_roaring_or((const uint8_t*)op.col->roaring.p, (const RoaringContainer*)op.col->containers.p,
-                                    (const uint32_t*)(dA + op.in_off), op.n, op.num_docs, (uint32_t*)(dS + op.out_off), s));
-        if (op.negate) HIP_CHECK(launch_bitmap_not((uint32_t*)(dS + op.out_off), op.num_docs, s));
+      case PrepassOp::ROARING:  // all of them in one launch below
         break;
       case PrepassOp::MV_SCAN:
         HIP_CHECK(launch_mv_scan((const uint32_t*)op.col->words.p, op.col->bits, (const uint32_t*)op.col->mv_offsets.p,
@@ -2565,6 +2637,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         break;
     }
   }
+  HIP_CHECK(launch_roaring_keys((const RoaringJob*)(dA + off_rjobs), (uint32_t)rjobs.size(), roaring_blocks, s));
   HIP_CHECK(hipEventRecord(ev[4], s));
   for (const PreLaunch& pl : pre_launches) {
     PreSpec ps;

@@ -73,7 +73,10 @@ _INTERMEDIATE_TYPE = {"COUNT": "LONG", "COUNTMV": "LONG", "SUM": "DOUBLE", "MIN"
 
 
 def column_name(ag: Aggregation) -> str:
-    """AggregationFunction.getColumnName(): "<type>_<expression>" (aggregation-only tables)."""
+    """AggregationFunction.getColumnName(): "<type>_<expression>" (aggregation-only tables); COUNT(*) is "count_star"
+    (CountAggregationFunction.java:37,62: COLUMN_NAME = "count_star")."""
+    if ag.function == "COUNT":
+        return "count_star"
     return f"{_TYPE_NAME[ag.function]}_{ag.arg}"
 
 

@@ -30,7 +30,7 @@ def _i(b, off):
 
 def test_layout_of_an_aggregation_table():
     """Header offsets, schema bytes, fixed-size row and variable-size objects exactly as DataTableImplV3 writes them."""
-    schema = dtm.DataSchema(["count_*", "sum_x", "avg_y", "distinctCount_z"], ["LONG", "DOUBLE", "OBJECT", "OBJECT"])
+    schema = dtm.DataSchema(["count_star", "sum_x", "avg_y", "distinctCount_z"], ["LONG", "DOUBLE", "OBJECT", "OBJECT"])
     dt = dtm.DataTable(schema, [[7, 2.5, (dtm.OBJ_AVG_PAIR, (10.0, 4)), (dtm.OBJ_INT_SET, {3, -1})]],
                        {"numDocsScanned": "7", "totalDocs": "100", "numSegmentsProcessed": "2"})
     b = dtm.to_bytes(dt)
