@@ -27,6 +27,9 @@ CASES = [
     ("SELECT DISTINCTCOUNT(impressions), COUNT(*) FROM adAnalytics WHERE accountId < 1000", False),
     # the config-2 query itself: selective stream + list-mode scan on each rank, dense all-reduce
     ("CONFIG2", False),
+    # untrimmed high-cardinality group-by (~10^5 groups with value sets): the owners' finalized rows come back as
+    # flat device byte buffers (no pickled objects)
+    ("SELECT accountId, COUNT(*), DISTINCTCOUNT(clicks) FROM adAnalytics WHERE clicks < 500 GROUP BY accountId", False),
 ]
 
 

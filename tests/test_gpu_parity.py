@@ -413,6 +413,37 @@ def test_sorted_and_inverted_and_mv(gpu_engine, oracle_engine):
             assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q), table=t)
 
 
+def test_config5_full_segment_matches_oracle(gpu_engine, oracle_engine):
+    """Config 5 at its stated scale: full 7 812 500-doc segments built on the device in the reference's byte layouts
+    (sorted pairs, portable-roaring inverted indexes, FixedBitMVForwardIndexWriter MV column: pinot_amd.synth), the
+    bench query and variants with NOT_IN / range / OR / NOT on the inverted and sorted indexes, GPU vs oracle."""
+    import torch
+    from pinot_amd import synth
+    dev = torch.device("cuda", 0)
+    segs, host = [], []
+    table = None
+    for si in range(2):
+        dcs = synth.make_index_columns_torch(si, 7_812_500, dev)
+        seg = ImmutableSegment(f"idx_{si}", 7_812_500, {dc.spec.name: dc.meta_column() for dc in dcs})
+        hs = ImmutableSegment(f"idx_{si}", 7_812_500, {dc.spec.name: dc.host_column() for dc in dcs})
+        if table is None:
+            table = Table("idx", [seg])
+        gpu_engine.register_device_segment(seg, table, dcs)
+        segs.append(seg)
+        host.append(hs)
+        del dcs
+    t, ht = Table("idx", segs), Table("idx", host)
+    for sql in [synth.index_query(),
+                "SELECT COUNT(*), COUNTMV(mvTags) FROM idx WHERE sortedCol NOT BETWEEN 1000 AND 90000 AND inv4 NOT IN "
+                "(3, 4, 5, 6, 7, 8) AND (inv2 < 20 OR inv1 = 9)",
+                "SELECT COUNT(*) FROM idx WHERE inv3 IN (10, 20, 30) OR NOT inv1 <> 4",
+                "SELECT inv1, COUNT(*), COUNTMV(mvTags) FROM idx WHERE sortedCol < 50000 AND inv2 = 42 GROUP BY inv1"]:
+        q = parse(sql)
+        assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(ht, q), table=t)
+    for seg in segs:
+        gpu_engine.release(seg)
+
+
 def test_partials_roundtrip_single_rank(gpu_engine, oracle_engine, sv_table_inter):
     """pg_execute_partial -> pg_partials_copy out/in -> pg_partials_finalize == pg_execute (1-rank dense merge)."""
     import ctypes as C
