@@ -120,6 +120,16 @@ int pg_column_upload(uint64_t seg_key, uint32_t col_id, const pg_col_desc *desc,
 /* Free every device buffer of a segment. */
 int pg_segment_release(uint64_t seg_key);
 
+/* IN / NOT_IN literal lowering against the resident dictionaries of many segments at once -- the device form of
+ * PredicateUtils.getDictIdSet (pinot-core/.../operator/filter/predicate/PredicateUtils.java:73-) as the
+ * dictionary-based In / NotIn evaluators call it per segment (InPredicateEvaluatorFactory.java:153-199,
+ * NotInPredicateEvaluatorFactory.java:153-).  `values`: num_values literals already converted to the column's stored
+ * type `data_type` (PG_INT int32, PG_LONG int64, PG_FLOAT float, PG_DOUBLE double), sorted ascending, unique.
+ * out_ids: [num_segments][num_values]; row s holds, in its first out_counts[s] entries, the dictIds (ascending) of the
+ * literals present in segment s's dictionary of column col_id.  Every segment's dictionary must hold data_type. */
+int pg_dict_id_sets(const uint64_t *seg_keys, uint32_t num_segments, uint32_t col_id, uint32_t data_type,
+                    const void *values, uint32_t num_values, int32_t *out_ids, uint32_t *out_counts);
+
 /* ---------------------------------------------------------------- query plan */
 
 typedef enum pg_leaf_kind {

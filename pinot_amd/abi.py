@@ -111,7 +111,7 @@ class pg_timing(C.Structure):
 EXPORTED = ["pg_init", "pg_last_error", "pg_resident_bytes", "pg_cancel", "pg_abi_version", "pg_column_upload",
             "pg_segment_release", "pg_execute", "pg_result_free", "pg_execute_partial", "pg_partials_finalize",
             "pg_partials_free", "pg_partials_copy", "pg_partials_export", "pg_partials_create", "pg_partials_merge",
-            "pg_key_owner", "pg_last_timing", "pg_chunk_decompress"]
+            "pg_key_owner", "pg_last_timing", "pg_chunk_decompress", "pg_dict_id_sets"]
 PG_CODEC_PASS_THROUGH, PG_CODEC_SNAPPY, PG_CODEC_ZSTANDARD, PG_CODEC_LZ4, PG_CODEC_LZ4_LENGTH_PREFIXED = 0, 1, 2, 3, 4
 PG_COPY_OUT, PG_COPY_IN = 0, 1
 
@@ -126,6 +126,8 @@ def declare(lib):
         "pg_cancel": ([C.c_uint64], C.c_int),
         "pg_abi_version": ([], C.c_int),
         "pg_column_upload": ([C.c_uint64, C.c_uint32, P(pg_col_desc), C.c_void_p, C.c_uint64], C.c_int),
+        "pg_dict_id_sets": ([P(C.c_uint64), C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, P(C.c_int32),
+                             P(C.c_uint32)], C.c_int),
         "pg_segment_release": ([C.c_uint64], C.c_int),
         "pg_execute": ([P(pg_plan), P(P(pg_result))], C.c_int),
         "pg_result_free": ([P(pg_result)], C.c_int),

@@ -60,6 +60,15 @@ struct LutJob {            // set bits ids[0..n) in lut and ids >> shift in regi
 };
 hipError_t launch_set_lut_bits(const LutJob* jobs, uint32_t njobs, hipStream_t s);
 
+// IN / NOT_IN literal lowering for many segments in one launch (PredicateUtils.getDictIdSet): out[s * n + i] = the
+// dictId of values[i] in segment s's dictionary, or -1
+struct DictLookupJob {
+  const void* dict;  // typed sorted dictionary values (dtype)
+  uint32_t card, pad;
+};
+hipError_t launch_dict_lookup(const DictLookupJob* jobs, uint32_t num_segments, const void* values, uint32_t n,
+                              uint32_t dtype, int32_t* out, hipStream_t s);
+
 // ---- streaming pre-filter (pg_filter.hip): one leaf of the root AND over the segments whose form of it reads
 // `bits`-bit values, into (first) or AND-ed into (later) one doc bitmap per segment
 constexpr uint32_t kPreItemGroups = 8192;   // 32-doc groups per pre-filter work item (262 144 docs)
@@ -115,7 +124,38 @@ struct PartSpec {
   uint32_t* out2;                  // level-2 entries, bucket-major
   unsigned long long* i64;         // dense state written by the bucket pass
   uint32_t* bits;
+  // speculative layout (fill1 != null; part_direct + part_split2s): level-1 partition p's entries at
+  // [p * cap1, p * cap1 + min(fill1[p], cap1)), bucket b's at [b * cap2, b * cap2 + min(fill2[b], cap2)); no histograms
+  const unsigned int* fill1;
+  unsigned int* fill2;
+  uint64_t cap1, cap2;
+  unsigned int* err;               // bit 4: a region over its capacity (the runtime reruns with exact offsets)
+  uint32_t* dc_pop;                // optional [num_groups]: each group's distinct-value count (its bitmap's popcount)
 };
+// Level 1 straight from the columns, speculative (filter matching every doc, one group key, at most one DISTINCTCOUNT
+// value column): 256-thread blocks take rounds of one 8 192-doc tile; the tile's packed words of the key / value column
+// are read coalesced (16-byte loads of the whole word range) into LDS, each thread unpacks 32 docs from there, and the
+// round's 32-bit entries are counting-sorted by level-1 digit in LDS and written as runs reserved in fixed-capacity
+// partition regions (split_round RES).  One read of each column, one write of the entries, no histogram pass.
+struct PartDirectSpec {
+  uint32_t blocks, num_items, nparts1, shift1;
+  uint32_t vbits, has_val, key_kind, val_kind;
+  uint64_t key_card, val_card;
+  int64_t key_base, val_base;
+  uint64_t cap1;                   // entries per level-1 partition region
+  uint32_t val_agg, pad;
+  const SegDesc* segs;
+  const WorkItem* items;           // tile ranges (kTileDocs docs)
+  unsigned int* fill1;             // [nparts1] entries reserved so far (zeroed before the launch)
+  uint32_t* out1;                  // level-1 regions
+  unsigned int* err;               // bit 0: key outside its space, bit 1: value outside, bit 4: a region overflowed
+};
+// Id modes (uniform over the segments, else the exact path): 0 decoded image (vbase + raw), 1 int32 gather (int32
+// dictionary or keymap); value mode -1 = no value column.  part_id_mode() gives a column's mode (2 = not direct).
+int part_id_mode(uint32_t key_kind, const ColDesc& c);
+hipError_t launch_part_direct(const PartDirectSpec& p, uint32_t key_bits, uint32_t val_bits, int key_mode, int val_mode,
+                              hipStream_t s);
+hipError_t launch_part_split2s(const PartSpec& p, hipStream_t s);
 // Level 1 straight from the columns when the filter matches every doc (no 64-bit scan entries, no split1): block b
 // walks the work items [b * num_items / blocks, (b + 1) * num_items / blocks) twice -- part_hist counts its docs'
 // level-1 digits, part_scatter counting-sorts them (LDS rounds of kSplitChunk) into its runs of the level-1
@@ -175,6 +215,8 @@ struct StateView {            // the device arrays of one partial state
   unsigned int* fill;         // hash tables: claimed keys
   unsigned int* err;          // bit 2: table full
   uint32_t n_i64, n_f64, n_min, n_max, bit_words, max_fill;
+  const uint32_t* dc_pop;     // optional: DISTINCTCOUNT dc_pop_agg's set size per slot (GM_PART's bucket pass)
+  uint32_t dc_pop_agg, pad;
 };
 struct FinalSpec {            // what finalisation needs of the plan
   uint32_t num_aggs, num_keys;

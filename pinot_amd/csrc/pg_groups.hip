@@ -153,6 +153,16 @@ __global__ void dc_sizes_kernel(StateView v, uint32_t dc_word, uint32_t words, u
   }
 }
 
+// DISTINCTCOUNT a from the set sizes the bucket pass recorded (StateView::dc_pop): 4 bytes per group read
+__global__ void dc_pop_kernel(const uint32_t* __restrict__ pop, const uint32_t* __restrict__ slots, uint64_t n,
+                              uint32_t A, uint32_t a, double* __restrict__ vals, int64_t* __restrict__ cnts) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    vals[i * A + a] = (double)pop[slots ? slots[i] : 0];
+    cnts[i * A + a] = 0;
+  }
+}
+
 hipError_t launch_final_values(const StateView& v, const FinalSpec& f, const uint32_t* slots, uint64_t n,
                                uint64_t* keys, double* vals, int64_t* cnts, hipStream_t s) {
   if (!n) return hipSuccess;
@@ -161,6 +171,11 @@ hipError_t launch_final_values(const StateView& v, const FinalSpec& f, const uin
                      slots, n, keys, vals, cnts);
   for (uint32_t a = 0; a < f.num_aggs; a++) {
     if (f.aggs[a].fn != PG_AGG_DISTINCTCOUNT) continue;
+    if (v.dc_pop && v.dc_pop_agg == a) {
+      hipLaunchKernelGGL(dc_pop_kernel, dim3((uint32_t)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, s, v.dc_pop,
+                         slots, n, f.num_aggs, a, vals, cnts);
+      continue;
+    }
     const uint32_t words = bits_words(f.aggs[a].key_card);
     // whole uint4 loads when every row and this aggregation's words start 16-byte aligned and fill whole uint4s
     const uint32_t vec4 = (v.bit_words % 4 == 0 && f.aggs[a].dc_word % 4 == 0 && words % 4 == 0) ? 1u : 0u;

@@ -466,4 +466,39 @@ hipError_t launch_set_lut_bits(const LutJob* jobs, uint32_t njobs, hipStream_t s
   return hipGetLastError();
 }
 
+// PredicateUtils.getDictIdSet over many segments at once: thread (segment s, literal i) binary-searches literal i
+// (already in the dictionary's stored type) in segment s's sorted dictionary -> its dictId, or -1 when absent.
+template <class T>
+__device__ __forceinline__ int32_t dict_find(const T* __restrict__ d, uint32_t card, T x) {
+  uint32_t lo = 0, n = card;
+  while (n > 0) {  // lower bound
+    const uint32_t h = n >> 1;
+    if (d[lo + h] < x) { lo += h + 1; n -= h + 1; } else n = h;
+  }
+  return lo < card && d[lo] == x ? (int32_t)lo : -1;
+}
+
+__global__ void dict_lookup_kernel(const DictLookupJob* __restrict__ jobs, const void* __restrict__ values, uint32_t n,
+                                   uint32_t dtype, int32_t* __restrict__ out) {
+  const uint32_t s = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const DictLookupJob j = jobs[s];
+  int32_t r;
+  switch (dtype) {
+    case PG_INT: r = dict_find((const int32_t*)j.dict, j.card, ((const int32_t*)values)[i]); break;
+    case PG_LONG: r = dict_find((const int64_t*)j.dict, j.card, ((const int64_t*)values)[i]); break;
+    case PG_FLOAT: r = dict_find((const float*)j.dict, j.card, ((const float*)values)[i]); break;
+    default: r = dict_find((const double*)j.dict, j.card, ((const double*)values)[i]); break;
+  }
+  out[(uint64_t)s * n + i] = r;
+}
+
+hipError_t launch_dict_lookup(const DictLookupJob* jobs, uint32_t num_segments, const void* values, uint32_t n,
+                              uint32_t dtype, int32_t* out, hipStream_t s) {
+  if (!n || !num_segments) return hipSuccess;
+  hipLaunchKernelGGL(dict_lookup_kernel, dim3((n + 255) / 256, num_segments), dim3(256), 0, s, jobs, values, n, dtype,
+                     out);
+  return hipGetLastError();
+}
+
 }  // namespace pg

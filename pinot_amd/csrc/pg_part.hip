@@ -23,9 +23,13 @@
 // once (scan) + 8 written / 8 read (scan entries) + 4 / 4 twice (levels 1, 2) + 4 read (count2) + state rows once.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "pg_aux.h"
 
 namespace pg {
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 #ifndef PG_SPLIT_CHUNK
 #define PG_SPLIT_CHUNK 16384
@@ -57,22 +61,27 @@ __device__ __forceinline__ uint32_t digit2(const PartSpec& P, uint32_t e) {
   return (e >> (P.vbits + P.shift2)) & (P.nparts2 - 1u);
 }
 
-// One LDS counting-sort round: the block's `n` (<= kSplitChunk) entries `e[k]` with digits `dg[k]` (thread t holds
-// chunk entries t + kST k) go to out[cur[digit]++] as one run per digit.  cur[] = the block's next output position per
-// digit (LDS, advanced here).  LDS: cnt/start [ndig] + sorted entries + their digits.
-// DIG = false: the digit is recomputable from the sorted entry itself, (e >> dsh) & (ndig - 1), so sdig is not used.
-template <class Out, bool DIG>
-__device__ __forceinline__ void split_round(uint32_t (&e)[kSplitChunk / kST], uint32_t (&dg)[kSplitChunk / kST],
-                                            uint32_t n, uint32_t ndig, uint32_t* cnt, uint32_t* start,
-                                            unsigned long long* cur, uint32_t* sbuf, uint8_t* sdig, Out* out,
-                                            uint32_t dsh = 0) {
-  constexpr int E = kSplitChunk / kST;
+// One LDS counting-sort round of an NT-thread block: the block's `n` (<= NT * E) entries `e[k]` with digits `dg[k]`
+// (thread t holds round entries t + NT k) go out as one run per digit.  LDS: cnt/start [ndig] + sorted entries + their
+// digits.  DIG = false: the digit is recomputable from the sorted entry itself, (e >> dsh) & (ndig - 1), so sdig is not
+// used.  Output cursors:
+//   RES = false: cur[d] = the block's next output position of digit d (exact offsets from a histogram; advanced here);
+//   RES = true:  each run is reserved in digit d's fixed-capacity region by one global atomic on fill[d]: the run lands
+//                at region0 + d * cap + (entries reserved before it); a run that would pass the region's capacity is
+//                dropped and raises err bit 4 (the runtime reruns the query with exact offsets).  Run order within a
+//                region is not deterministic; what is aggregated from it (counts, value sets) does not depend on it.
+template <int NT, int E, class Out, bool DIG, bool RES>
+__device__ __forceinline__ void split_round(uint32_t (&e)[E], uint32_t (&dg)[E], uint32_t n, uint32_t ndig,
+                                            uint32_t* cnt, uint32_t* start, unsigned long long* cur, uint32_t* sbuf,
+                                            uint8_t* sdig, Out* out, uint32_t dsh = 0, unsigned int* fill = nullptr,
+                                            uint64_t region0 = 0, uint64_t cap = 0, unsigned int* err = nullptr) {
+  constexpr unsigned long long kDrop = ~0ull;
   const uint32_t tid = threadIdx.x;
   uint32_t rank[E];
 #pragma unroll
-  for (int k = 0; k < E; k++) rank[k] = tid + kST * k < n ? atomicAdd(&cnt[dg[k]], 1u) : 0u;
+  for (int k = 0; k < E; k++) rank[k] = tid + NT * k < n ? atomicAdd(&cnt[dg[k]], 1u) : 0u;
   __syncthreads();
-  // exclusive scan of cnt over the digits (ndig <= 256 <= kST: one per thread) -> start; reserve the runs
+  // exclusive scan of cnt over the digits (ndig <= 256 <= NT: one per thread) -> start; reserve the runs
   {
     uint32_t c = tid < ndig ? cnt[tid] : 0u, x = c;
     const uint32_t lane = tid & 63u, wave = tid >> 6;
@@ -81,7 +90,7 @@ __device__ __forceinline__ void split_round(uint32_t (&e)[kSplitChunk / kST], ui
       const uint32_t y = __shfl_up(x, o);
       if (lane >= (uint32_t)o) x += y;
     }
-    __shared__ uint32_t wsum[kST / 64];
+    __shared__ uint32_t wsum[NT / 64];
     if (lane == 63) wsum[wave] = x;
     __syncthreads();
     uint32_t wb = 0;
@@ -89,26 +98,36 @@ __device__ __forceinline__ void split_round(uint32_t (&e)[kSplitChunk / kST], ui
     if (tid < ndig) {
       start[tid] = wb + x - c;
       cnt[tid] = 0;
+      if (RES && c) {
+        const uint32_t old = atomicAdd(&fill[tid], c);
+        if ((uint64_t)old + c <= cap) {
+          cur[tid] = region0 + (uint64_t)tid * cap + old;
+        } else {
+          cur[tid] = kDrop;
+          atomicOr(err, 16u);
+        }
+      }
     }
   }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < E; k++)
-    if (tid + kST * k < n) {
+    if (tid + NT * k < n) {
       const uint32_t at = start[dg[k]] + rank[k];
       sbuf[at] = e[k];
       if (DIG) sdig[at] = (uint8_t)dg[k];
     }
   __syncthreads();
-  for (uint32_t i = tid; i < n; i += kST) {
+  for (uint32_t i = tid; i < n; i += NT) {
     const uint32_t x = sbuf[i];
     const uint32_t d = DIG ? (uint32_t)sdig[i] : (x >> dsh) & (ndig - 1u);
-    out[cur[d] + (i - start[d])] = (Out)x;
+    if (!RES || cur[d] != kDrop) out[cur[d] + (i - start[d])] = (Out)x;
   }
   __syncthreads();
-  // advance the cursors by this round's run lengths (start[d+1] - start[d])
-  if (tid < ndig) cur[tid] += (tid + 1 < ndig ? start[tid + 1] : n) - start[tid];
-  __syncthreads();
+  if (!RES) {  // advance the cursors by this round's run lengths (start[d+1] - start[d])
+    if (tid < ndig) cur[tid] += (tid + 1 < ndig ? start[tid + 1] : n) - start[tid];
+    __syncthreads();
+  }
 }
 
 // Level 1: scan block b's entries -> level-1 partitions (its range of each starts at off1[p * blocks1 + b]).
@@ -137,7 +156,7 @@ __global__ __launch_bounds__(kST) void part_split1_kernel(PartSpec P) {
       dg[k] = (uint32_t)(x >> sh);
       e[k] = (uint32_t)((((x >> P.vbits) & lmask) << P.vbits) | (x & vmask));
     }
-    split_round<uint32_t, true>(e, dg, m, P.nparts1, cnt, start, cur, sbuf, sdig, P.in1);
+    split_round<kST, E, uint32_t, true, false>(e, dg, m, P.nparts1, cnt, start, cur, sbuf, sdig, P.in1);
   }
 }
 
@@ -187,7 +206,37 @@ __global__ __launch_bounds__(kST) void part_split2_kernel(PartSpec P) {
       e[k] = i < m ? in[c0 + i] : 0u;
       dg[k] = digit2(P, e[k]);
     }
-    split_round<uint32_t, PG_SPLIT2_DIG>(e, dg, m, P.nparts2, cnt, start, cur, sbuf, sdig, P.out2, P.vbits + P.shift2);
+    split_round<kST, E, uint32_t, PG_SPLIT2_DIG, false>(e, dg, m, P.nparts2, cnt, start, cur, sbuf, sdig, P.out2,
+                                                      P.vbits + P.shift2);
+  }
+}
+
+// Level 2, speculative layout: level-1 partition p's entries (min(fill1[p], cap1) of them) split over kPartNB blocks,
+// counting-sorted by level-2 digit, each run reserved in its bucket's fixed-capacity region (no count pass).
+__global__ __launch_bounds__(kST) void part_split2s_kernel(PartSpec P) {
+  constexpr int E = kSplitChunk / kST;
+  __shared__ uint32_t cnt[256], start[256], sbuf[kSplitChunk];
+  __shared__ unsigned long long cur[256];
+  __shared__ uint8_t sdig[1];
+  const uint32_t j = blockIdx.x, p = blockIdx.y, tid = threadIdx.x;
+  if (tid < P.nparts2) cnt[tid] = 0;
+  __syncthreads();
+  const uint64_t n = min((uint64_t)P.fill1[p], P.cap1), s0 = (uint64_t)p * P.cap1;
+  const uint64_t lo = s0 + n * j / kPartNB, hi = s0 + n * (j + 1) / kPartNB;
+  const uint32_t* __restrict__ in = P.in1;
+  unsigned int* fill = P.fill2 + (uint64_t)p * P.nparts2;
+  const uint64_t region0 = (uint64_t)p * P.nparts2 * P.cap2;
+  for (uint64_t c0 = lo; c0 < hi; c0 += kSplitChunk) {
+    const uint32_t m = (uint32_t)min((uint64_t)kSplitChunk, hi - c0);
+    uint32_t e[E], dg[E];
+#pragma unroll
+    for (int k = 0; k < E; k++) {
+      const uint32_t i = tid + kST * k;
+      e[k] = i < m ? in[c0 + i] : 0u;
+      dg[k] = digit2(P, e[k]);
+    }
+    split_round<kST, E, uint32_t, false, true>(e, dg, m, P.nparts2, cnt, start, cur, sbuf, sdig, P.out2,
+                                               P.vbits + P.shift2, fill, region0, P.cap2, P.err);
   }
 }
 
@@ -201,7 +250,14 @@ __global__ __launch_bounds__(kAT) void part_aggregate_kernel(PartSpec P) {
   uint32_t* bm = lds + ng;    // [ng][dw]
   for (uint32_t i = tid; i < ng * (1u + dw); i += kAT) lds[i] = 0;
   __syncthreads();
-  const uint64_t lo = P.off2[(uint64_t)b * kPartNB], hi = P.off2[(uint64_t)(b + 1) * kPartNB];
+  uint64_t lo, hi;
+  if (P.fill2) {
+    lo = (uint64_t)b * P.cap2;
+    hi = lo + min((uint64_t)P.fill2[b], P.cap2);
+  } else {
+    lo = P.off2[(uint64_t)b * kPartNB];
+    hi = P.off2[(uint64_t)(b + 1) * kPartNB];
+  }
   const uint32_t gm = ng - 1u, vm = (1u << P.vbits) - 1u, vb = P.vbits;
   const uint32_t* __restrict__ in = P.out2;
   uint64_t i = lo + tid;
@@ -229,7 +285,14 @@ __global__ __launch_bounds__(kAT) void part_aggregate_kernel(PartSpec P) {
   __syncthreads();
   const uint64_t g0 = (uint64_t)b << P.shift2;
   const uint32_t n = (uint32_t)(g0 + ng <= P.num_groups ? ng : (g0 < P.num_groups ? P.num_groups - g0 : 0));
-  for (uint32_t gl = tid; gl < n; gl += kAT) P.i64[(g0 + gl) * P.n_i64] = cnt[gl];
+  for (uint32_t gl = tid; gl < n; gl += kAT) {
+    P.i64[(g0 + gl) * P.n_i64] = cnt[gl];
+    if (P.dc_pop && dw) {  // the group's DISTINCTCOUNT (extractFinalResult = set size) while its bitmap is in LDS
+      uint32_t pc = 0;
+      for (uint32_t k = 0, r = gl % dw; k < dw; k++, r = r + 1 == dw ? 0 : r + 1) pc += __popc(bm[gl * dw + r]);  // lanes on distinct banks
+      P.dc_pop[g0 + gl] = pc;
+    }
+  }
   if (P.row_words) {
     const uint32_t rw = P.row_words;
     uint32_t* __restrict__ dst = P.bits + g0 * rw;
@@ -369,9 +432,214 @@ __global__ __launch_bounds__(kST) void part_scatter_kernel(PartScanSpec P) {
       uint32_t e[E], dg[E];
       part_entries<NK, E, 0, E / 2>(P, kc, vc, r0, m, dg, e);
       part_entries<NK, E, E / 2, E / 2>(P, kc, vc, r0, m, dg, e);
-      split_round<uint32_t, true>(e, dg, m, P.nparts1, cnt, start, cur, sbuf, sdig, P.out1);
+      split_round<kST, E, uint32_t, true, false>(e, dg, m, P.nparts1, cnt, start, cur, sbuf, sdig, P.out1);
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------ level 1, speculative
+
+#ifndef PG_DIRECT_THREADS
+#define PG_DIRECT_THREADS 1024
+#endif
+constexpr uint32_t kDT = PG_DIRECT_THREADS;   // threads of a part_direct block
+constexpr uint32_t kDE = kTileDocs / kDT;     // docs per thread per round (a round is one tile)
+static_assert(kDE * kDT == kTileDocs && kDT >= kPartL1, "one digit per thread in the run scan");
+
+// The tile's word range [w0, w0 + nw) of a packed column into LDS (16-byte loads; reads past the column return 0).
+// nw is a multiple of 4 plus the 4 words of padding the unpack's 64-bit window may touch.
+__device__ __forceinline__ void stage_words(rsrc_t r, uint32_t w0, uint32_t nw, uint32_t* lds) {
+  for (uint32_t q = threadIdx.x; q < nw / 4; q += kDT) {
+    const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, (w0 + 4u * q) * 4u, 0, 0);
+    *(uint4*)(lds + 4u * q) = make_uint4(x[0], x[1], x[2], x[3]);
+  }
+}
+
+// the b-bit value at bit p of a packed run staged at lds (FixedBitIntReader: MSB first)
+__device__ __forceinline__ uint32_t lds_unpack(const uint32_t* lds, uint32_t p, uint32_t b) {
+  const uint32_t k = p >> 5, o = p & 31u;
+  const uint64_t win = ((uint64_t)lds[k] << 32) | (uint64_t)lds[k + 1];
+  return (uint32_t)(win >> (64u - o - b)) & (0xFFFFFFFFu >> (32u - b));
+}
+
+__device__ __forceinline__ rsrc_t part_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// Table-global id of a raw (dictId / decoded) value: M = 0 decoded image (vbase + raw - base), 1 gather from an int32
+// array (`tab` = the int32 dictionary with `base`, or the keymap with base 0), 2 int64 dictionary (not taken by the
+// direct path: the runtime uses the exact one).  Ids outside [0, card) come back as ~0 (the caller's range check).
+template <int M>
+__device__ __forceinline__ uint64_t id_of(const ColDesc& c, const int32_t* tab, int64_t base, uint32_t raw) {
+  if (M == 0) return raw < c.card ? (uint64_t)(c.vbase + (int64_t)raw - base) : ~0ull;
+  return raw < c.card ? (uint64_t)((int64_t)tab[raw] - base) : ~0ull;
+}
+__host__ __device__ __forceinline__ int id_mode(uint32_t key_kind, const ColDesc& c) {
+  if (key_kind == PG_KEY_KEYMAP) return 1;
+  if (c.decoded) return 0;
+  return c.dtype == PG_INT ? 1 : 2;
+}
+
+// Round body: 32 docs per thread (doc tid + 256 j) -> level-1 digit + 32-bit entry, ranked within its digit right
+// away (LDS atomic; docs past the segment go to the spare digit kPartL1).  Returns the error bits seen.
+template <int KM, int VM>  // VM = -1: no value column (COUNTs only)
+__device__ __forceinline__ uint32_t direct_unpack(const PartDirectSpec& P, const ColDesc& kc, const ColDesc& vc,
+                                                  const int32_t* ktab, int64_t kbase, const int32_t* vtab, int64_t vbase,
+                                                  const uint32_t* stk, const uint32_t* stv, uint32_t kb, uint32_t vb,
+                                                  uint32_t m, uint32_t* cnt, uint32_t (&dr)[kDE], uint32_t (&e)[kDE]) {
+  const uint32_t tid = threadIdx.x;
+  const uint64_t lmask = (1ull << P.shift1) - 1ull;
+  uint32_t bad = 0;
+  // bit positions of doc tid, advanced by 256 docs per j; opaque to the optimiser so that the 64 positions are not
+  // hoisted out of the round loop as invariants (they would pin 64+ registers for the whole kernel)
+  uint32_t pk = tid * kb, pv = tid * vb;
+  asm volatile("" : "+v"(pk), "+v"(pv));
+  const uint32_t sk = kDT * kb, sv = kDT * vb;
+#pragma unroll
+  for (int j = 0; j < (int)kDE; j++) {
+    const uint32_t i = tid + kDT * j;
+    const bool ok = i < m;
+    uint64_t g = id_of<KM>(kc, ktab, kbase, lds_unpack(stk, pk + sk * j, kb));
+    uint32_t vid = 0;
+    if constexpr (VM >= 0) {
+      const uint64_t v = id_of<VM>(vc, vtab, vbase, lds_unpack(stv, pv + sv * j, vb));
+      const bool vbad = v >= P.val_card;
+      bad |= (ok && vbad) ? 2u : 0u;
+      vid = vbad ? 0u : (uint32_t)v;
+    }
+    const bool kbad = g >= P.key_card;
+    bad |= (ok && kbad) ? 1u : 0u;
+    g = kbad ? 0ull : g;
+    const uint32_t d = ok ? (uint32_t)(g >> P.shift1) : kPartL1;
+    e[j] = (uint32_t)(((g & lmask) << P.vbits) | vid);
+    dr[j] = (d << 16) | atomicAdd(&cnt[d], 1u);
+    if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // at most 8 docs' gathers in flight (their 64-bit addresses)
+  }
+  return bad;
+}
+
+// KM / VM: the id modes of the key / value column, uniform over the plan's segments (runtime-checked).  W: waves per
+// SIMD the register budget is cut for (PG_DIRECT_WAVES).
+template <int KM, int VM, int W>
+__global__ __launch_bounds__(kDT, W) void part_direct_kernel(PartDirectSpec P) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t dl[];  // stage (key | value words) / sort (sbuf | sdig)
+  __shared__ uint32_t cnt[kPartL1 + 1], start[kPartL1];
+  __shared__ unsigned long long cur[kPartL1];
+  const uint32_t b = blockIdx.x, tid = threadIdx.x;
+  if (tid < kPartL1) cnt[tid] = 0;
+  if (tid == 0) cnt[kPartL1] = 0;  // the spare digit of docs past the segment
+  __syncthreads();
+  uint32_t bad = 0;
+  const uint64_t i0 = (uint64_t)b * P.num_items / P.blocks, i1 = (uint64_t)(b + 1) * P.num_items / P.blocks;
+  for (uint64_t it = i0; it < i1; it++) {
+    const WorkItem w = P.items[it];
+    const SegDesc sd = P.segs[w.seg];
+    const ColDesc kc = sd.keycols[0];
+    ColDesc vc = kc;
+    if (P.has_val) vc = sd.aggcols[2 * P.val_agg];
+    const uint32_t kb = __builtin_amdgcn_readfirstlane(kc.bits);
+    const uint32_t vb = P.has_val ? __builtin_amdgcn_readfirstlane(vc.bits) : 0u;
+    const uint32_t nwk = 256u * kb + 4u, nwv = P.has_val ? 256u * vb + 4u : 0u;
+    const rsrc_t rk = part_rsrc(kc.words, kc.wbytes);
+    const rsrc_t rv = part_rsrc(vc.words, vc.wbytes);
+    const bool kmap = P.key_kind == PG_KEY_KEYMAP, vmap = P.val_kind == PG_KEY_KEYMAP;
+    const int32_t* ktab = kmap ? kc.keymap : (const int32_t*)kc.dict;
+    const int32_t* vtab = vmap ? vc.keymap : (const int32_t*)vc.dict;
+    const int64_t kbase = kmap ? 0 : P.key_base, vbase = vmap ? 0 : P.val_base;
+    const uint32_t num_docs = __builtin_amdgcn_readfirstlane(sd.num_docs);
+    for (uint32_t t = w.tile_begin; t < w.tile_end; t++) {
+      const uint32_t r0 = t * (uint32_t)kTileDocs;
+      if (r0 >= num_docs) break;
+      const uint32_t m = min((uint32_t)kTileDocs, num_docs - r0);
+      // 1. the tile's words of both columns, coalesced, into LDS
+      stage_words(rk, t * 256u * kb, nwk, dl);
+      if (P.has_val) stage_words(rv, t * 256u * vb, nwv, dl + nwk);
+      __syncthreads();
+      // 2. entries + ranks ((digit << 16 | rank) and the entry are all a thread keeps)
+      uint32_t dr[kDE], e[kDE];
+      bad |= direct_unpack<KM, VM>(P, kc, vc, ktab, kbase, vtab, vbase, dl, dl + nwk, kb, vb, m, cnt, dr, e);
+      __syncthreads();  // every rank taken; the stage is dead: its LDS becomes the sort buffer
+      // 3. run starts (exclusive scan of the digit counts) and one reservation per non-empty run
+      {
+        const uint32_t c = tid < P.nparts1 ? cnt[tid] : 0u;
+        uint32_t x = c;
+        const uint32_t lane = tid & 63u, wave = tid >> 6;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = __shfl_up(x, o);
+          if (lane >= (uint32_t)o) x += y;
+        }
+        __shared__ uint32_t wsum[kDT / 64];
+        if (lane == 63) wsum[wave] = x;
+        __syncthreads();
+        uint32_t wb = 0;
+        for (uint32_t w2 = 0; w2 < wave; w2++) wb += wsum[w2];
+        if (tid < P.nparts1) {
+          start[tid] = wb + x - c;
+          cnt[tid] = 0;
+          if (c) {
+            const uint32_t old = atomicAdd(&P.fill1[tid], c);
+            if ((uint64_t)old + c <= P.cap1) {
+              cur[tid] = (uint64_t)tid * P.cap1 + old;
+            } else {
+              cur[tid] = ~0ull;
+              atomicOr(P.err, 16u);
+            }
+          }
+        }
+        if (tid == 0) cnt[kPartL1] = 0;
+      }
+      __syncthreads();
+      uint32_t* sbuf = dl;
+      uint8_t* sdig = (uint8_t*)(dl + kTileDocs);
+#pragma unroll
+      for (int j = 0; j < (int)kDE; j++) {
+        const uint32_t d = dr[j] >> 16;
+        if (d < kPartL1) {
+          const uint32_t at = start[d] + (dr[j] & 0xFFFFu);
+          sbuf[at] = e[j];
+          sdig[at] = (uint8_t)d;
+        }
+      }
+      __syncthreads();
+      // 4. the runs, written out whole
+      for (uint32_t i = tid; i < m; i += kDT) {
+        const uint32_t d = sdig[i];
+        const unsigned long long c0 = cur[d];
+        if (c0 != ~0ull) P.out1[c0 + (i - start[d])] = sbuf[i];
+      }
+      __syncthreads();
+    }
+  }
+  if (bad) atomicOr(P.err, bad);
+}
+
+hipError_t launch_part_direct(const PartDirectSpec& p, uint32_t key_bits, uint32_t val_bits, int key_mode, int val_mode,
+                              hipStream_t s) {
+  const size_t stage = 4ull * ((256ull * key_bits + 4) + (p.has_val ? 256ull * val_bits + 4 : 0));
+  const size_t sort = 4ull * kTileDocs + kTileDocs;  // sbuf + sdig
+  const size_t lds = stage > sort ? stage : sort;
+  const dim3 g(p.blocks), b(kDT);
+  constexpr int kW0 = kDT / 256, kW1 = 2 * kDT / 256;  // one / two resident blocks' worth of waves per SIMD
+  static const int waves = getenv("PG_DIRECT_WAVES") ? atoi(getenv("PG_DIRECT_WAVES")) : kW0;
+#define PG_DIRECT(K, V)                                                                                 \
+  if (key_mode == (K) && val_mode == (V)) {                                                             \
+    if (waves == kW1) hipLaunchKernelGGL((part_direct_kernel<K, V, kW1>), g, b, lds, s, p);             \
+    else hipLaunchKernelGGL((part_direct_kernel<K, V, kW0>), g, b, lds, s, p);                          \
+    return hipGetLastError();                                                                           \
+  }
+  PG_DIRECT(0, -1) PG_DIRECT(0, 0) PG_DIRECT(0, 1) PG_DIRECT(1, -1) PG_DIRECT(1, 0) PG_DIRECT(1, 1)
+#undef PG_DIRECT
+  return hipErrorInvalidValue;
+}
+int part_id_mode(uint32_t key_kind, const ColDesc& c) { return id_mode(key_kind, c); }
+hipError_t launch_part_split2s(const PartSpec& p, hipStream_t s) {
+  hipLaunchKernelGGL(part_split2s_kernel, dim3(kPartNB, p.nparts1), dim3(kST), 0, s, p);
+  return hipGetLastError();
 }
 
 hipError_t launch_part_hist(const PartScanSpec& p, hipStream_t s) {

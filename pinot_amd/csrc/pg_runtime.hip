@@ -801,6 +801,8 @@ struct Partials {
   uint64_t num_slots = 1;
   uint32_t n_i64 = 1, n_f64 = 0, n_min = 0, n_max = 0, bit_words = 0, max_fill = 0;
   DevBuf keys, i64, f64, mn, mx, bits, first_doc, misc /* [fill, err] */, seg_matched;
+  DevBuf dc_pop;                // GM_PART under pg_execute: each group's DISTINCTCOUNT (aggregation dc_pop_agg)
+  int dc_pop_agg = -1;
   bool host_state = false;      // t_ctx.state_host holds a copy of the final state (queued before the scan's sync)
   std::vector<uint32_t> key_card;
   std::vector<uint64_t> key_stride;
@@ -827,6 +829,8 @@ struct Partials {
     v.err = misc.p ? (unsigned int*)misc.p + 1 : nullptr;
     v.n_i64 = n_i64; v.n_f64 = n_f64; v.n_min = n_min; v.n_max = n_max; v.bit_words = bit_words;
     v.max_fill = max_fill;
+    v.dc_pop = dc_pop_agg >= 0 ? (const uint32_t*)dc_pop.p : nullptr;
+    v.dc_pop_agg = (uint32_t)dc_pop_agg;
     return v;
   }
   // device state for `num_slots` slots of the current layout (+ keys for hash modes), initialised
@@ -1098,6 +1102,7 @@ thread_local bool t_prefetch_state = false;  // set by pg_execute around its pg_
 
 constexpr int kRetryLargerTable = 1;  // internal: the hash table overflowed its fill budget
 constexpr int kRetryNoStream = 2;     // internal: a selective-stream region overflowed (more survivors than estimated)
+constexpr int kRetryExactPart = 3;    // internal: a speculative GM_PART region overflowed (skewed keys): exact offsets
 
 // Pooled device scratch of a host-side sequence of small launches (freed after the caller synchronises).
 struct Scratch {
@@ -1264,7 +1269,8 @@ void key_coldesc(ColDesc& dc, const ColumnRes* c, const pg_key& key) {
 constexpr uint32_t kWideColId = 0xFFFFFFF0u;
 thread_local const std::vector<ColumnRes>* t_wide_cols = nullptr;
 
-int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t hash_cap, bool allow_stream) {
+int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t hash_cap, bool allow_stream,
+                    bool allow_spec) {
   const double t_enter = wall_ms();
   if (!plan) return fail(PG_E_INVALID, "null plan");
   if (plan->abi_version != PG_ABI_VERSION) return fail(PG_E_INVALID, "ABI version %u != %u", plan->abi_version, PG_ABI_VERSION);
@@ -2554,7 +2560,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   }
   const uint64_t off_rjobs = ar.reserve(rjobs.size() * sizeof(RoaringJob));
   DevBuf arena, scratch;
-  DevBuf p_ent0, p_cnt0, p_hist1, p_off1, p_ent1, p_hist2, p_off2, p_ent2, p_temp;  // GM_PART pipeline
+  DevBuf p_ent0, p_cnt0, p_hist1, p_off1, p_ent1, p_hist2, p_off2, p_ent2, p_temp, p_fill;  // GM_PART pipeline
   DevBuf l_docs, l_counts;  // selective stream: survivor regions + counts
   // declared after the buffers it protects: on any exit, wait for queued work before they return to the pool
   struct SyncOnExit {
@@ -2683,25 +2689,62 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   q.cancel = cancel.device_ptr();
   std::vector<uint64_t> direct_matched;
   if (q.num_items && part.on) {
-    // radix-partitioned group-by (pg_part.hip).  Filter matching every doc: level-1 partitions straight from the
-    // columns (part_hist + scan + part_scatter).  Otherwise the fused scan appends 64-bit entries + the level-1
-    // histogram, then part_split1.  Both: level-2 count / scan / split, per-bucket aggregation.
-    bool direct = !getenv("PG_PART_SCAN");
-    for (uint32_t si = 0; si < S && direct; si++) direct = filter_is_match_all(plan, plan->segments[si].leaves);
+    // radix-partitioned group-by (pg_part.hip).  Filter matching every doc and one group key: level-1 partitions
+    // straight from the columns into fixed-capacity regions (part_direct), level 2 likewise (part_split2s): no
+    // histogram or count pass; a region overflow (keys far from uniform over the digits) reruns the query with exact
+    // offsets.  Otherwise (a filter, several keys, or that rerun) the fused scan appends 64-bit entries + the level-1
+    // histogram, then part_split1 / count2 / split2 with exact offsets.  Both: per-bucket aggregation.
+    bool match_all = true;
+    for (uint32_t si = 0; si < S && match_all; si++) match_all = filter_is_match_all(plan, plan->segments[si].leaves);
+    const char* spec_env = getenv("PG_PART_SPEC");
+    // the key / value id modes of part_direct, uniform over the segments (else -2: not direct)
+    int kmode = -2, vmode = part.dc == (uint32_t)kNoSlot ? -1 : -2;
+    if (K == 1 && S) {
+      kmode = part_id_mode(q.key_kind[0], keycols[0]);
+      for (uint32_t si = 1; si < S; si++)
+        if (part_id_mode(q.key_kind[0], keycols[si]) != kmode) kmode = -2;
+      if (part.dc != (uint32_t)kNoSlot) {
+        const uint32_t vk = q.aggs[part.dc].key_kind;
+        vmode = part_id_mode(vk, aggcols[(uint64_t)part.dc * 2]);
+        for (uint32_t si = 1; si < S; si++)
+          if (part_id_mode(vk, aggcols[((uint64_t)si * A + part.dc) * 2]) != vmode) vmode = -2;
+      }
+    }
+    const bool modes_ok = (kmode == 0 || kmode == 1) && (vmode >= -1 && vmode <= 1);
+    const bool spec = match_all && allow_spec && K == 1 && modes_ok && !(spec_env && atoi(spec_env) == 0);
+    // PG_PART_DIRECT=1: the histogram + scatter form of level 1 from the columns (exact offsets; measured slower)
+    const bool direct = !spec && match_all && getenv("PG_PART_DIRECT") && atoi(getenv("PG_PART_DIRECT")) == 1;
     const uint64_t n1 = (uint64_t)part.nparts1 * blocks, n2 = (uint64_t)part.nparts1 * part.nparts2 * kPartNB;
+    const uint64_t nb = (uint64_t)part.nparts1 * part.nparts2;
+    // speculative capacities: 1.25x the uniform share of the docs + slack
+    const uint64_t cap1 = (part_entries + part_entries / 4) / part.nparts1 + 65536;
+    const uint64_t cap2 = (cap1 + part.nparts2 - 1) / part.nparts2 + 2048;
     const size_t tb = select_temp_bytes(std::max(n1, n2) + 1);
-    if ((!direct && ((rc = p_ent0.alloc_pooled(8 * part_entries + 16)) || (rc = p_cnt0.alloc_pooled(4ull * blocks + 16)))) ||
+    if (spec) {
+      if ((rc = p_fill.alloc_pooled(4ull * (part.nparts1 + nb) + 16)) ||
+          (rc = p_ent1.alloc_pooled(4ull * cap1 * part.nparts1 + 16)) || (rc = p_ent2.alloc_pooled(4ull * cap2 * nb + 16)))
+        return rc;
+      HIP_CHECK(hipMemsetAsync(p_fill.p, 0, 4ull * (part.nparts1 + nb), s));
+    } else if ((!direct && ((rc = p_ent0.alloc_pooled(8 * part_entries + 16)) || (rc = p_cnt0.alloc_pooled(4ull * blocks + 16)))) ||
         (rc = p_hist1.alloc_pooled(8 * (n1 + 1))) || (rc = p_off1.alloc_pooled(8 * (n1 + 1))) ||
         (rc = p_ent1.alloc_pooled(4 * part_entries + 16)) || (rc = p_hist2.alloc_pooled(8 * (n2 + 1))) ||
         (rc = p_off2.alloc_pooled(8 * (n2 + 1))) || (rc = p_ent2.alloc_pooled(4 * part_entries + 16)) ||
-        (rc = p_temp.alloc_pooled(tb)))
+        (rc = p_temp.alloc_pooled(tb))) {
       return rc;
+    }
+    P.dc_pop_agg = -1;
+    if (t_prefetch_state && part.dc != (uint32_t)kNoSlot) {  // finalised right after (pg_execute): keep the counts
+      if ((rc = P.dc_pop.alloc_pooled(4ull * G + 16))) return rc;
+      P.dc_pop_agg = (int)part.dc;
+    }
     unsigned long long* h1 = (unsigned long long*)p_hist1.p;
     unsigned long long* o1 = (unsigned long long*)p_off1.p;
     unsigned long long* h2 = (unsigned long long*)p_hist2.p;
     unsigned long long* o2 = (unsigned long long*)p_off2.p;
-    HIP_CHECK(hipMemsetAsync(h1 + n1, 0, 8, s));
-    HIP_CHECK(hipMemsetAsync(h2 + n2, 0, 8, s));
+    if (!spec) {
+      HIP_CHECK(hipMemsetAsync(h1 + n1, 0, 8, s));
+      HIP_CHECK(hipMemsetAsync(h2 + n2, 0, 8, s));
+    }
     q.group_mode = GM_PART;
     q.part_shift = part.shift1;
     q.part_vbits = part.vbits;
@@ -2712,7 +2755,41 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     q.part_base = (const unsigned long long*)(dA + off_part_base);
     q.part_out = (unsigned long long*)p_ent0.p;
     t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
-    if (direct) {
+    if (spec || direct) {
+      direct_matched.resize(S);  // every doc matches: the per-segment counts are the segments' sizes
+      for (uint32_t si = 0; si < S; si++) direct_matched[si] = plan->segments[si].num_docs;
+      if (S) HIP_CHECK(hipMemcpyAsync(P.seg_matched.p, direct_matched.data(), 8ull * S, hipMemcpyHostToDevice, s));
+    }
+    if (spec) {
+      PartDirectSpec pd;
+      memset(&pd, 0, sizeof(pd));
+      pd.blocks = blocks;
+      pd.num_items = q.num_items;
+      pd.nparts1 = part.nparts1;
+      pd.shift1 = part.shift1;
+      pd.vbits = part.vbits;
+      pd.has_val = part.dc != (uint32_t)kNoSlot;
+      pd.key_kind = q.key_kind[0];
+      pd.key_card = q.key_card[0];
+      pd.key_base = q.key_base[0];
+      pd.val_agg = part.dc;
+      uint32_t kbits = 1, vbits = 1;
+      for (uint32_t si = 0; si < S; si++) kbits = std::max(kbits, keycols[si].bits);
+      if (pd.has_val) {
+        const AggSpec& va = q.aggs[part.dc];
+        pd.val_kind = va.key_kind;
+        pd.val_card = va.key_card;
+        pd.val_base = va.key_base;
+        for (uint32_t si = 0; si < S; si++) vbits = std::max(vbits, aggcols[((uint64_t)si * A + part.dc) * 2].bits);
+      }
+      pd.cap1 = cap1;
+      pd.segs = q.segs;
+      pd.items = q.items;
+      pd.fill1 = (unsigned int*)p_fill.p;
+      pd.out1 = (uint32_t*)p_ent1.p;
+      pd.err = q.err;
+      HIP_CHECK(launch_part_direct(pd, kbits, vbits, kmode, vmode, s));
+    } else if (direct) {
       PartScanSpec pss;
       memset(&pss, 0, sizeof(pss));
       pss.num_keys = K;
@@ -2735,9 +2812,6 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       pss.off1 = o1;
       pss.out1 = (uint32_t*)p_ent1.p;
       pss.err = q.err;
-      direct_matched.resize(S);  // every doc matches: the per-segment counts are the segments' sizes
-      for (uint32_t si = 0; si < S; si++) direct_matched[si] = plan->segments[si].num_docs;
-      if (S) HIP_CHECK(hipMemcpyAsync(P.seg_matched.p, direct_matched.data(), 8ull * S, hipMemcpyHostToDevice, s));
       HIP_CHECK(launch_part_hist(pss, s));
       HIP_CHECK(launch_exclusive_sum((const uint64_t*)h1, (uint64_t*)o1, n1 + 1, p_temp.p, tb, s));
       HIP_CHECK(launch_part_scatter(pss, s));
@@ -2768,10 +2842,20 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     ps.out2 = (uint32_t*)p_ent2.p;
     ps.i64 = (unsigned long long*)P.i64.p;
     ps.bits = (uint32_t*)P.bits.p;
-    if (!direct) HIP_CHECK(launch_part_split1(ps, s));
-    HIP_CHECK(launch_part_count2(ps, s));
-    HIP_CHECK(launch_exclusive_sum((const uint64_t*)h2, (uint64_t*)o2, n2 + 1, p_temp.p, tb, s));
-    HIP_CHECK(launch_part_split2(ps, s));
+    ps.dc_pop = P.dc_pop_agg >= 0 ? (uint32_t*)P.dc_pop.p : nullptr;
+    ps.err = q.err;
+    if (spec) {
+      ps.fill1 = (const unsigned int*)p_fill.p;
+      ps.fill2 = (unsigned int*)p_fill.p + part.nparts1;
+      ps.cap1 = cap1;
+      ps.cap2 = cap2;
+      HIP_CHECK(launch_part_split2s(ps, s));
+    } else {
+      if (!direct) HIP_CHECK(launch_part_split1(ps, s));
+      HIP_CHECK(launch_part_count2(ps, s));
+      HIP_CHECK(launch_exclusive_sum((const uint64_t*)h2, (uint64_t*)o2, n2 + 1, p_temp.p, tb, s));
+      HIP_CHECK(launch_part_split2(ps, s));
+    }
     HIP_CHECK(launch_part_aggregate(ps, s));
   } else if (q.num_items) {
     t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
@@ -2827,6 +2911,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     stats.num_segments_matched += ns_matched;
     const uint32_t err = (uint32_t)sm[S ? S : 1];
     if (err & 8u) return kRetryNoStream;     // more stream survivors than the regions hold: rerun without it
+    if (err & 16u) return kRetryExactPart;   // a speculative partition region overflowed: rerun with exact offsets
     if (err & 4u) return kRetryLargerTable;  // hash table over its fill budget: rerun with a larger one
     if (err) return fail(PG_E_INVALID, "device bounds check failed (code %u): a key fell outside the plan's key space", err);
   }
@@ -2844,10 +2929,11 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
 // survivor-region overflow.
 int run_with_retries(const pg_plan* plan, Partials& P, pg_stats& st) {
   uint64_t cap = 0;
-  bool allow_stream = true;
+  bool allow_stream = true, allow_spec = true;
   for (;;) {
-    const int rc = compile_and_run(plan, P, st, cap, allow_stream);
+    const int rc = compile_and_run(plan, P, st, cap, allow_stream, allow_spec);
     if (rc == kRetryNoStream) { allow_stream = false; continue; }
+    if (rc == kRetryExactPart) { allow_spec = false; continue; }
     if (rc != kRetryLargerTable) return rc;
     cap = P.num_slots * 8;  // the group-by hash table overflowed: rerun with 8x the slots
     if (cap > kMaxHashSlots) return fail(PG_E_UNSUPPORTED, "group-by needs more than %llu hash slots", (unsigned long long)kMaxHashSlots);
@@ -3635,6 +3721,59 @@ int pg_partials_merge(pg_partials* p, const void* rows, uint64_t n, void* stream
   HIP_CHECK(hipStreamSynchronize(s));
   if (fe[1]) return fail(PG_E_NOMEM, "merge table of %llu slots is full", (unsigned long long)P.num_slots);
   return PG_OK;
+}
+
+int pg_dict_id_sets(const uint64_t* seg_keys, uint32_t num_segments, uint32_t col_id, uint32_t data_type,
+                    const void* values, uint32_t num_values, int32_t* out_ids, uint32_t* out_counts) {
+  int rc = ensure_device();
+  if (rc) return rc;
+  if ((!seg_keys && num_segments) || (!values && num_values) || (!out_ids && num_segments && num_values) ||
+      (!out_counts && num_segments))
+    return fail(PG_E_INVALID, "null argument");
+  if (data_type > PG_DOUBLE) return fail(PG_E_UNSUPPORTED, "dictIds of %u-typed literals", data_type);
+  const uint64_t S = num_segments, n = num_values;
+  if (!S) return PG_OK;
+  if (!n) { memset(out_counts, 0, 4 * S); return PG_OK; }
+  try {
+    std::vector<DictLookupJob> jobs(S);
+    {
+      std::shared_lock<std::shared_mutex> lk(g_seg_mu);
+      for (uint64_t si = 0; si < S; si++) {
+        auto it = g_segs.find(seg_keys[si]);
+        if (it == g_segs.end()) return fail(PG_E_NOTFOUND, "segment %llu not resident", (unsigned long long)seg_keys[si]);
+        auto c = it->second->cols.find(col_id);
+        if (c == it->second->cols.end() || !c->second.has_dict)
+          return fail(PG_E_NOTFOUND, "segment %llu has no dictionary for column %u", (unsigned long long)seg_keys[si], col_id);
+        if (c->second.dtype != data_type)
+          return fail(PG_E_INVALID, "column %u's dictionary holds type %u, the literals %u", col_id, c->second.dtype, data_type);
+        jobs[si].dict = c->second.dict.p;
+        jobs[si].card = c->second.card;
+      }
+    }
+    const uint64_t vb = n * (data_type == PG_INT || data_type == PG_FLOAT ? 4 : 8);
+    hipStream_t s = thread_stream();
+    Scratch sc(s);
+    DictLookupJob* dj = sc.get<DictLookupJob>(S, rc);
+    uint8_t* dv = sc.get<uint8_t>(vb, rc);
+    int32_t* dout = sc.get<int32_t>(S * n, rc);
+    if (rc) return rc;
+    HIP_CHECK(hipMemcpyAsync(dj, jobs.data(), S * sizeof(DictLookupJob), hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(dv, values, vb, hipMemcpyHostToDevice, s));
+    HIP_CHECK(launch_dict_lookup(dj, (uint32_t)S, dv, (uint32_t)n, data_type, dout, s));
+    HIP_CHECK(hipMemcpyAsync(out_ids, dout, S * n * 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    // compact each segment's row in place: the found ids, ascending (the literals and the dictionary are sorted)
+    for (uint64_t si = 0; si < S; si++) {
+      int32_t* row = out_ids + si * n;
+      uint32_t k = 0;
+      for (uint64_t i = 0; i < n; i++)
+        if (row[i] >= 0) row[k++] = row[i];
+      out_counts[si] = k;
+    }
+    return PG_OK;
+  } catch (const std::exception& e) {
+    return fail(PG_E_NOMEM, "dictionary lookup failed: %s", e.what());
+  }
 }
 
 int pg_execute(const pg_plan* plan, pg_result** out) {

@@ -154,6 +154,20 @@ class GpuEngine:
                 check(self.lib.pg_column_upload(key, cid, C.byref(d), km.ctypes.data_as(C.c_void_p), km.nbytes))
                 self._keymaps_uploaded.add((key, cid))
 
+    def dict_id_sets(self, col_id: int, data_type: str, literals: np.ndarray, seg_keys):
+        """pg_dict_id_sets: the literals' dictIds in every segment's resident dictionary (one device launch)."""
+        keys = np.ascontiguousarray(seg_keys, dtype=np.uint64)
+        literals = np.ascontiguousarray(literals, dtype={"INT": np.int32, "LONG": np.int64, "FLOAT": np.float32,
+                                                         "DOUBLE": np.float64}[data_type])
+        S, n = len(keys), len(literals)
+        ids = np.empty((S, max(n, 1)), dtype=np.int32)
+        counts = np.empty(max(S, 1), dtype=np.uint32)
+        check(self.lib.pg_dict_id_sets(keys.ctypes.data_as(C.POINTER(C.c_uint64)), S, col_id,
+                                       abi.DTYPE_CODES[data_type], literals.ctypes.data_as(C.c_void_p), n,
+                                       ids.ctypes.data_as(C.POINTER(C.c_int32)),
+                                       counts.ctypes.data_as(C.POINTER(C.c_uint32))))
+        return ids, counts
+
     def release(self, seg: ImmutableSegment):
         hit = self._seg_keys.pop(id(seg), None)
         if hit is not None:
@@ -167,7 +181,7 @@ class GpuEngine:
         applies the query's ORDER BY / LIMIT (a final single-server answer; boundary ties kept)."""
         segments = list(table.segments if segments is None else segments)
         keys = [self.upload_segment(s, table) for s in segments]
-        plan = CPlan(table, query, segments, keys, num_groups_limit, flags, trim)
+        plan = CPlan(table, query, segments, keys, num_groups_limit, flags, trim, id_sets=self.dict_id_sets)
         self.upload_keymaps(table, plan, segments, keys)
         return plan
 

@@ -123,8 +123,9 @@ def lower_raw_predicate(pred: Predicate, col: Column, col_id: int) -> LoweredLea
     return lw
 
 
-def lower_predicate(pred: Predicate, col: Column, col_id: int) -> LoweredLeaf:
-    """Dictionary-based predicate evaluator + leaf operator choice for one segment's column."""
+def lower_predicate(pred: Predicate, col: Column, col_id: int, in_ids: Optional[np.ndarray] = None) -> LoweredLeaf:
+    """Dictionary-based predicate evaluator + leaf operator choice for one segment's column.  in_ids: the IN / NOT_IN
+    literals' dictIds in this segment when already looked up for every segment at once (GpuEngine's pg_dict_id_sets)."""
     if pred.type in ("IS_NULL", "IS_NOT_NULL"):
         # FilterPlanNode.constructPhysicalOperator (plan/FilterPlanNode.java:285-298): without a null value vector
         # (segments built with null handling off, SegmentColumnarIndexCreator.java:291-294) IS NULL is an
@@ -160,7 +161,7 @@ def lower_predicate(pred: Predicate, col: Column, col_id: int) -> LoweredLeaf:
             else:
                 always_true = True
     elif t in ("IN", "NOT_IN"):
-        ids = dict_id_set(d, pred.values)   # PredicateUtils.getDictIdSet
+        ids = dict_id_set(d, pred.values) if in_ids is None else in_ids   # PredicateUtils.getDictIdSet
         s = ids
         if t == "IN":
             always_false = len(s) == 0
@@ -518,9 +519,12 @@ class CPlan:
 
     def __init__(self, table: Table, query: QueryContext, segments: Sequence[ImmutableSegment],
                  seg_keys: Sequence[int], num_groups_limit: Optional[int] = None, flags: int = 0,
-                 trim: bool = False):
+                 trim: bool = False, id_sets=None):
         """flags: PG_PLAN_*.  trim: let the device apply the query's ORDER BY / LIMIT to the group-by result
-        (IndexedTable.finish + TableResizer; boundary ties kept) -- for a final, single-server answer."""
+        (IndexedTable.finish + TableResizer; boundary ties kept) -- for a final, single-server answer.
+        id_sets(col_id, data_type, literals, seg_keys) -> (ids [S, n] int32, counts [S]): the IN / NOT_IN literals'
+        dictIds in every segment in one call (GpuEngine: pg_dict_id_sets on the resident dictionaries); None = per
+        segment on the host."""
         self.table = table
         self.query = query
         self.aggs = query.aggregations
@@ -534,13 +538,16 @@ class CPlan:
         S = len(segments)
         seg_arr = (abi.pg_segment_ref * max(S, 1))()
         self.lowered: List[List[LoweredLeaf]] = []
+        batch = self._batched_in_ids(preds, segments, seg_keys, cid, id_sets) if id_sets is not None and S > 1 else {}
         for si, (seg, key) in enumerate(zip(segments, seg_keys)):
             leaves = (abi.pg_leaf * max(L, 1))()
             lows = []
             for li, p in enumerate(preds):
                 if p.column not in seg.columns:
                     raise UnsupportedQuery(f"unknown column {p.column}")
-                lw = lower_predicate(p, seg.columns[p.column], cid[p.column])
+                b = batch.get(li)
+                lw = lower_predicate(p, seg.columns[p.column], cid[p.column],
+                                     None if b is None else b[0][si, :b[1][si]])
                 lows.append(lw)
                 leaves[li].kind = lw.kind
                 leaves[li].col_id = lw.col_id
@@ -639,3 +646,26 @@ class CPlan:
             p.limit = query.limit
         self.plan = p
         self.ops = ops
+
+    @staticmethod
+    def _batched_in_ids(preds, segments, seg_keys, cid, id_sets) -> dict:
+        """{leaf: (ids [S, n], counts [S])} for the IN / NOT_IN leaves over numeric dictionaries of one stored type in
+        every segment: the literals are coerced once (the first segment's dictionary type) and looked up in all
+        segments by one id_sets call."""
+        out = {}
+        for li, p in enumerate(preds):
+            if p.type not in ("IN", "NOT_IN"):
+                continue
+            cols = [s.columns.get(p.column) for s in segments]
+            if any(c is None or c.dictionary is None for c in cols):
+                continue
+            d0 = cols[0].dictionary
+            if d0.data_type not in ("INT", "LONG", "FLOAT", "DOUBLE") or \
+                    any(c.dictionary.data_type != d0.data_type or c.dictionary.values.dtype != d0.values.dtype
+                        for c in cols):
+                continue
+            lit = _coerced_literals(d0, p.values)
+            if lit is None:
+                continue
+            out[li] = id_sets(cid[p.column], d0.data_type, np.ascontiguousarray(lit), seg_keys)
+        return out

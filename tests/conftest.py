@@ -65,5 +65,9 @@ def oracle_engine():
 
 @pytest.fixture(scope="session")
 def gpu_engine():
+    # torch (device buffers of the synthetic segments, RCCL) carries its own HIP runtime beside the system one
+    # libpinot_gpu links; torch must open the device first or it reports no GPU afterwards (bench.py does the same)
+    import torch
+    torch.zeros(1, device="cuda")
     from pinot_amd.gpu import GpuEngine
     return GpuEngine(0)

@@ -235,6 +235,128 @@ def test_radix_partitioned_group_by(mode, monkeypatch, gpu_engine, oracle_engine
             assert reduce_to_rows(q, gpu_engine.execute(t, q, trim=True))[1] == reduce_to_rows(q, o)[1]
 
 
+def _skewed_events(seed: int, n: int, users: int, hot: int, items_scale: int = 1):
+    """Events whose userIds crowd into the first `hot` ids for 90 % of the docs (a level-1 partition far over its
+    uniform share), itemIds spread over [0, 1000) * items_scale."""
+    rng = np.random.default_rng(seed)
+    u = np.where(rng.random(n) < 0.9, rng.integers(0, hot, n), rng.integers(0, users, n)).astype(np.int64)
+    i = (rng.integers(0, 1000, n) * items_scale).astype(np.int64)
+    return {"userId": u, "itemId": i}
+
+
+@pytest.mark.parametrize("case", ["skewed", "keymap"])
+def test_radix_partitioned_speculative_regions(case, monkeypatch, gpu_engine, oracle_engine):
+    """The speculative level-1 / level-2 regions of the radix-partitioned group-by (part_direct + part_split2s): a
+    skewed key distribution overflows a region and the query reruns with exact offsets; sparse userIds (a keymap key
+    space) with non-identity itemIds (dictionary gathers) take the gather modes.  Both identical to the oracle."""
+    from pinot_amd import abi
+    from pinot_amd.segment import ImmutableSegment
+    monkeypatch.setenv("PG_PART", "1")
+    types = {"userId": "INT", "itemId": "INT"}
+    segs = []
+    for s in range(3):
+        if case == "skewed":
+            data = _skewed_events(s, 300_007 + 13 * s, users=150_000, hot=700)
+        else:
+            data = _skewed_events(s, 200_003, users=60_000, hot=60_000, items_scale=7)
+            data["userId"] = data["userId"] * 97 + 11  # span far above 4x the cardinality: a keymap key space
+        segs.append(ImmutableSegment.create(f"ev{s}", data, types))
+    t = Table("events", segs)
+    if case == "keymap":
+        assert t.key_space("userId").kind == abi.PG_KEY_KEYMAP
+    for sql in [synth_highcard() + " OPTION(numGroupsLimit=10000000)",
+                "SELECT userId, COUNT(*) FROM events GROUP BY userId ORDER BY COUNT(*) DESC, userId LIMIT 10 "
+                "OPTION(numGroupsLimit=10000000)"]:
+        q = parse(sql)
+        o = oracle_engine.execute(t, q)
+        assert_same_result(gpu_engine.execute(t, q, flags=abi.PG_PLAN_VALUE_SETS), o, table=t)
+        assert reduce_to_rows(q, gpu_engine.execute(t, q, trim=True))[1] == reduce_to_rows(q, o)[1]
+    monkeypatch.setenv("PG_PART_SPEC", "0")  # the exact-offset pipeline on the same data
+    q = parse(synth_highcard() + " OPTION(numGroupsLimit=10000000)")
+    assert_same_result(gpu_engine.execute(t, q, flags=abi.PG_PLAN_VALUE_SETS), oracle_engine.execute(t, q), table=t)
+
+
+def synth_highcard():
+    from pinot_amd import synth
+    return synth.highcard_query()
+
+
+def test_config4_full_segments_match_oracle(gpu_engine, oracle_engine):
+    """Config 4 at its stated scale: 4 full 7 812 500-row segments of the 10 M-user key space (device-generated, as the
+    bench), every group's DISTINCTCOUNT and COUNT-free result through the radix-partitioned pipeline against the
+    oracle's per-segment value sets merged by value, and the device-trimmed top 100 (ORDER BY DISTINCTCOUNT DESC,
+    userId) against the oracle's."""
+    import torch
+    from pinot_amd import abi, synth
+    from pinot_amd.plan import CPlan
+    dev = torch.device("cuda", 0)
+    rows = synth.ADANALYTICS_ROWS_PER_SEGMENT
+    segs, host = [], []
+    table = None
+    for si in range(4):
+        dcs = synth.make_columns_torch(synth.HIGHCARD, si, rows, dev)
+        seg = ImmutableSegment(f"ev_{si}", rows, {dc.spec.name: dc.meta_column() for dc in dcs})
+        host.append(ImmutableSegment(f"ev_{si}", rows, {dc.spec.name: dc.host_column() for dc in dcs}))
+        if table is None:
+            table = Table("events", [seg])
+        gpu_engine.register_device_segment(seg, table, dcs)
+        segs.append(seg)
+        del dcs
+    t = Table("events", segs)
+    q = parse(synth.highcard_query() + " OPTION(numGroupsLimit=10000000)")
+    # oracle: per-segment (user, item) value sets merged by value
+    ht = Table("events", host)
+    cp = CPlan(ht, q, host, list(range(1, len(host) + 1)))
+    pk, pv = zip(*(oracle_engine.distinct_pairs(cp, i, sg) for i, sg in enumerate(host)))
+    pair = np.unique(np.concatenate(pk) * (1 << 20) + np.concatenate(pv))
+    users, counts = np.unique(pair >> 20, return_counts=True)
+    # device: every group (keys, distinct counts) from the partial state
+    plan = gpu_engine.make_plan(t, q, flags=0)
+    ra = gpu_engine.finalize_arrays(plan, gpu_engine.run_partial(plan))
+    ks = plan.key_spaces[0]
+    assert ks.kind == abi.PG_KEY_VALUE_OFFSET
+    gk = ra["keys"][:, 0].astype(np.int64) + ks.base
+    order = np.argsort(gk)
+    assert np.array_equal(gk[order], users)
+    assert np.array_equal(ra["values"][order, 0].astype(np.int64), counts)
+    assert ra["stats"][0] == 4 * rows
+    # device-trimmed top rows (pg_execute: the bucket pass's set sizes feed the trim)
+    top = np.lexsort((users, -counts))[:q.limit]
+    want = [[int(users[i]), int(counts[i])] for i in top]
+    assert reduce_to_rows(q, gpu_engine.execute(t, q, flags=0, trim=True))[1] == want
+    for seg in segs:
+        gpu_engine.release(seg)
+
+
+@pytest.mark.parametrize("dtype", ["INT", "LONG", "FLOAT", "DOUBLE"])
+def test_dict_id_sets_on_device(dtype, gpu_engine, oracle_engine):
+    """pg_dict_id_sets (IN / NOT_IN literals looked up in every segment's resident dictionary in one launch) gives
+    PredicateUtils.getDictIdSet's per-segment dictIds (plan.dict_id_set on the host); the queries through it match
+    the oracle."""
+    from pinot_amd.plan import dict_id_set, _coerced_literals
+    rng = np.random.default_rng(7)
+    segs = []
+    for s in range(5):  # different dictionaries per segment (absent literals, ragged sizes)
+        n = 20_011 + 3_001 * s
+        v = rng.integers(-5_000, 5_000, n) * (3 if dtype in ("INT", "LONG") else 1)
+        data = {"k": v.astype(np.int64) if dtype in ("INT", "LONG") else v.astype(np.float64) / 4,
+                "m": rng.integers(0, 100, n).astype(np.int64)}
+        segs.append(ImmutableSegment.create(f"d{s}", data, {"k": dtype, "m": "INT"}))
+    t = Table("t", segs)
+    lits = [x * 3 for x in range(-300, 300, 7)] if dtype in ("INT", "LONG") else [x / 4 for x in range(-900, 900, 11)]
+    keys = [gpu_engine.upload_segment(s, t) for s in segs]
+    d0 = segs[0].columns["k"].dictionary
+    ids, counts = gpu_engine.dict_id_sets(t.column_ids["k"], dtype, _coerced_literals(d0, lits), keys)
+    for si, s in enumerate(segs):
+        want = dict_id_set(s.columns["k"].dictionary, lits)
+        assert np.array_equal(ids[si, :counts[si]], want), si
+    in_list = ", ".join(str(x) for x in lits)
+    for sql in [f"SELECT COUNT(*), SUM(m) FROM t WHERE k IN ({in_list})",
+                f"SELECT m, COUNT(*) FROM t WHERE k NOT IN ({in_list}) GROUP BY m"]:
+        q = parse(sql)
+        assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q), table=t)
+
+
 def test_partial_rows_export_merge_roundtrip(gpu_engine, oracle_engine, sv_table_inter):
     """pg_partials_export (rows bucketed by owner) -> pg_partials_create + pg_partials_merge of every bucket ->
     finalize == the direct result, for a dense and a hash state."""
