@@ -243,6 +243,13 @@ hipError_t launch_final_values(const StateView& v, const FinalSpec& f, const uin
 // both differ between keys, the others are equal in all of them and the sort can skip them
 hipError_t launch_order_keys(const FinalSpec& f, const uint64_t* keys, const double* vals, const int64_t* cnts,
                              uint64_t n, uint64_t* out, uint32_t* pos, hipStream_t s, uint64_t* span = nullptr);
+// ORDER BY trim by radix select (pg_groups.hip): histogram of key bits [lo, hi) of k' = (key >> b0) & (2^W - 1) over the
+// keys whose k' >> hi equals prefix (hist: 256 counters, zeroed by the caller); then the positions of every key with
+// k' <= tstar (count: zeroed by the caller)
+hipError_t launch_okey_hist(const uint64_t* keys, uint64_t n, uint32_t b0, uint32_t W, uint32_t lo, uint32_t hi,
+                            uint64_t prefix, unsigned int* hist, hipStream_t s);
+hipError_t launch_okey_select(const uint64_t* keys, uint64_t n, uint32_t b0, uint32_t W, uint64_t tstar, uint32_t* pos,
+                              unsigned long long* count, hipStream_t s);
 hipError_t launch_cutoff(const uint64_t* sorted, uint64_t n, uint64_t limit, uint64_t* out, hipStream_t s);
 hipError_t launch_gather_final(uint32_t A, const uint32_t* pos, uint64_t n, const uint64_t* keys, const double* vals,
                                const int64_t* cnts, const uint32_t* slots, uint64_t* okeys, double* ovals,

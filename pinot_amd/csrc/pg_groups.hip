@@ -13,6 +13,8 @@
 //     data/table/TableResizer.java:248) as a radix sort on the first ORDER BY item, and value-set extraction.
 // Everything here is HBM / atomic bound, O(groups); no MFMA.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <hipcub/hipcub.hpp>
 
 #include "pg_aux.h"
@@ -260,6 +262,65 @@ __global__ void cutoff_kernel(const uint64_t* __restrict__ sorted, uint64_t n, u
 
 hipError_t launch_cutoff(const uint64_t* sorted, uint64_t n, uint64_t limit, uint64_t* out, hipStream_t s) {
   hipLaunchKernelGGL(cutoff_kernel, dim3(1), dim3(1), 0, s, sorted, n, limit, out);
+  return hipGetLastError();
+}
+
+// ---- ORDER BY trim by radix select (instead of sorting every group): in the key space k' = (okey >> b0) & (2^W - 1)
+// (the only bits in which the order keys differ, order_keys_kernel's span), the limit-th smallest k' is found digit by
+// digit from the top: per pass a histogram of one <= 8-bit digit over the keys whose higher digits equal the prefix
+// chosen so far.  The candidates are then every key <= that value (the sorted cutoff's set: ties at the boundary
+// kept), compacted into a position list.
+__device__ __forceinline__ uint64_t kprime(uint64_t k, uint32_t b0, uint32_t W) {
+  const uint64_t x = k >> b0;
+  return W >= 64 ? x : (x & ((1ull << W) - 1ull));
+}
+
+__global__ void okey_hist_kernel(const uint64_t* __restrict__ keys, uint64_t n, uint32_t b0, uint32_t W, uint32_t lo,
+                                 uint32_t hi, uint64_t prefix, unsigned int* __restrict__ hist) {
+  __shared__ unsigned int h[256];
+  const uint32_t tid = threadIdx.x;
+  h[tid] = 0;
+  __syncthreads();
+  const uint64_t dmask = (1ull << (hi - lo)) - 1ull;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + tid; i < n; i += stride) {
+    const uint64_t k = kprime(keys[i], b0, W);
+    if (hi >= 64 || (k >> hi) == prefix) atomicAdd(&h[(k >> lo) & dmask], 1u);
+  }
+  __syncthreads();
+  if (h[tid]) atomicAdd(&hist[tid], h[tid]);
+}
+
+__global__ void okey_select_kernel(const uint64_t* __restrict__ keys, uint64_t n, uint32_t b0, uint32_t W,
+                                   uint64_t tstar, uint32_t* __restrict__ pos, unsigned long long* __restrict__ count) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
+    const uint64_t i = i0 + threadIdx.x;
+    const bool take = i < n && kprime(keys[i], b0, W) <= tstar;
+    const uint64_t m = __ballot(take);
+    if (!m) continue;
+    unsigned long long base = 0;
+    const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+    if (lane == leader) base = atomicAdd(count, (unsigned long long)__popcll(m));
+    base = __shfl(base, (int)leader);
+    if (take) pos[base + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)i;
+  }
+}
+
+hipError_t launch_okey_hist(const uint64_t* keys, uint64_t n, uint32_t b0, uint32_t W, uint32_t lo, uint32_t hi,
+                            uint64_t prefix, unsigned int* hist, hipStream_t s) {
+  const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(okey_hist_kernel, dim3((uint32_t)std::max<uint64_t>(blocks, 1)), dim3(256), 0, s, keys, n, b0, W,
+                     lo, hi, prefix, hist);
+  return hipGetLastError();
+}
+
+hipError_t launch_okey_select(const uint64_t* keys, uint64_t n, uint32_t b0, uint32_t W, uint64_t tstar, uint32_t* pos,
+                              unsigned long long* count, hipStream_t s) {
+  const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(okey_select_kernel, dim3((uint32_t)std::max<uint64_t>(blocks, 1)), dim3(256), 0, s, keys, n, b0,
+                     W, tstar, pos, count);
   return hipGetLastError();
 }
 

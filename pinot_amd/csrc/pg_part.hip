@@ -30,6 +30,17 @@
 namespace pg {
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+#define PG_CONST __attribute__((address_space(4)))
+
+// A wave-uniform struct read through the scalar cache (s_load: descriptors live in SGPRs, not 64 lanes' VGPRs).
+template <class T> __device__ __forceinline__ T ldcf(const T* p, uint64_t i) {
+  const PG_CONST uint32_t* src = (const PG_CONST uint32_t*)(p + i);
+  T v;
+  uint32_t* dst = (uint32_t*)&v;
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(T) / 4); k++) dst[k] = src[k];
+  return v;
+}
 
 #ifndef PG_SPLIT_CHUNK
 #define PG_SPLIT_CHUNK 16384
@@ -38,6 +49,9 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #define PG_SPLIT_THREADS 1024
 #endif
 constexpr uint32_t kST = PG_SPLIT_THREADS;  // threads of a split block
+#ifndef PG_SPLIT_WAVES
+#define PG_SPLIT_WAVES (PG_SPLIT_THREADS / 256)  // register budget: one resident block per CU
+#endif
 #ifndef PG_SPLIT2_DIG
 #define PG_SPLIT2_DIG 0
 #endif
@@ -47,6 +61,14 @@ constexpr uint32_t kST = PG_SPLIT_THREADS;  // threads of a split block
 constexpr uint32_t kAT = PG_AGG_THREADS;  // threads of a part_aggregate block
 constexpr uint32_t kSplitChunk = PG_SPLIT_CHUNK;  // entries counting-sorted per LDS round (16 per thread): longer runs per digit
 // (16 384 x 1 024 threads, one block per CU: split1 4.08 -> 3.10 ms, split2 2.71 -> 2.15 ms on config 4 vs 4 096 x 256)
+
+__device__ __forceinline__ rsrc_t part_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
 
 // Entries of level-1 partition p handled by level-2 block j (of kPartNB): [lo, hi).
 __device__ __forceinline__ void l2_range(const PartSpec& P, uint32_t p, uint32_t j, uint64_t& lo, uint64_t& hi) {
@@ -70,16 +92,25 @@ __device__ __forceinline__ uint32_t digit2(const PartSpec& P, uint32_t e) {
 //                at region0 + d * cap + (entries reserved before it); a run that would pass the region's capacity is
 //                dropped and raises err bit 4 (the runtime reruns the query with exact offsets).  Run order within a
 //                region is not deterministic; what is aggregated from it (counts, value sets) does not depend on it.
-template <int NT, int E, class Out, bool DIG, bool RES>
+// `after_reserve()` runs once the runs are reserved (the caller's prefetch of its next round: issued there, its loads
+// are not waited on by the reservations' returned values).
+struct NoPrefetch {
+  __device__ void operator()() const {}
+};
+template <int NT, int E, class Out, bool DIG, bool RES, class F = NoPrefetch>
 __device__ __forceinline__ void split_round(uint32_t (&e)[E], uint32_t (&dg)[E], uint32_t n, uint32_t ndig,
                                             uint32_t* cnt, uint32_t* start, unsigned long long* cur, uint32_t* sbuf,
                                             uint8_t* sdig, Out* out, uint32_t dsh = 0, unsigned int* fill = nullptr,
-                                            uint64_t region0 = 0, uint64_t cap = 0, unsigned int* err = nullptr) {
+                                            uint64_t region0 = 0, uint64_t cap = 0, unsigned int* err = nullptr,
+                                            F after_reserve = F()) {
   constexpr unsigned long long kDrop = ~0ull;
   const uint32_t tid = threadIdx.x;
   uint32_t rank[E];
 #pragma unroll
-  for (int k = 0; k < E; k++) rank[k] = tid + NT * k < n ? atomicAdd(&cnt[dg[k]], 1u) : 0u;
+  for (int k = 0; k < E; k++) {
+    const uint32_t d = DIG ? dg[k] : ((e[k] >> dsh) & (ndig - 1u));  // !DIG: recomputed, dg[] is never held
+    rank[k] = tid + NT * k < n ? atomicAdd(&cnt[d], 1u) : 0u;
+  }
   __syncthreads();
   // exclusive scan of cnt over the digits (ndig <= 256 <= NT: one per thread) -> start; reserve the runs
   {
@@ -110,10 +141,11 @@ __device__ __forceinline__ void split_round(uint32_t (&e)[E], uint32_t (&dg)[E],
     }
   }
   __syncthreads();
+  after_reserve();
 #pragma unroll
   for (int k = 0; k < E; k++)
     if (tid + NT * k < n) {
-      const uint32_t at = start[dg[k]] + rank[k];
+      const uint32_t at = start[DIG ? dg[k] : ((e[k] >> dsh) & (ndig - 1u))] + rank[k];
       sbuf[at] = e[k];
       if (DIG) sdig[at] = (uint8_t)dg[k];
     }
@@ -211,9 +243,12 @@ __global__ __launch_bounds__(kST) void part_split2_kernel(PartSpec P) {
   }
 }
 
+#ifndef PG_SPLIT2S_PREFETCH
+#define PG_SPLIT2S_PREFETCH 1  // the next chunk's loads issued while this one is sorted (registers: 1 block per CU)
+#endif
 // Level 2, speculative layout: level-1 partition p's entries (min(fill1[p], cap1) of them) split over kPartNB blocks,
 // counting-sorted by level-2 digit, each run reserved in its bucket's fixed-capacity region (no count pass).
-__global__ __launch_bounds__(kST) void part_split2s_kernel(PartSpec P) {
+__global__ __launch_bounds__(kST, PG_SPLIT_WAVES) void part_split2s_kernel(PartSpec P) {
   constexpr int E = kSplitChunk / kST;
   __shared__ uint32_t cnt[256], start[256], sbuf[kSplitChunk];
   __shared__ unsigned long long cur[256];
@@ -226,17 +261,32 @@ __global__ __launch_bounds__(kST) void part_split2s_kernel(PartSpec P) {
   const uint32_t* __restrict__ in = P.in1;
   unsigned int* fill = P.fill2 + (uint64_t)p * P.nparts2;
   const uint64_t region0 = (uint64_t)p * P.nparts2 * P.cap2;
-  for (uint64_t c0 = lo; c0 < hi; c0 += kSplitChunk) {
+  uint32_t e[E], ne[E];
+  // buffer loads relative to the partition (one 32-bit lane offset, the k stride as a scalar offset, reads past the
+  // block's range return 0): no 64-bit address per load in flight
+  const rsrc_t rin = part_rsrc(in + s0, (uint32_t)(4ull * n));
+  auto load = [&](uint64_t c0, uint32_t (&x)[E]) {
     const uint32_t m = (uint32_t)min((uint64_t)kSplitChunk, hi - c0);
-    uint32_t e[E], dg[E];
+    const uint32_t vo = 4u * (uint32_t)(c0 - s0 + tid);
 #pragma unroll
     for (int k = 0; k < E; k++) {
-      const uint32_t i = tid + kST * k;
-      e[k] = i < m ? in[c0 + i] : 0u;
-      dg[k] = digit2(P, e[k]);
+      const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rin, vo, 4u * kST * k, 0);
+      x[k] = tid + kST * k < m ? v : 0u;
     }
+  };
+  if (lo < hi) load(lo, e);
+  for (uint64_t c0 = lo; c0 < hi; c0 += kSplitChunk) {
+    const uint32_t m = (uint32_t)min((uint64_t)kSplitChunk, hi - c0);
+    uint32_t dg[E];
+#pragma unroll
+    for (int k = 0; k < E; k++) dg[k] = digit2(P, e[k]);
+    const uint64_t c1 = c0 + kSplitChunk;
     split_round<kST, E, uint32_t, false, true>(e, dg, m, P.nparts2, cnt, start, cur, sbuf, sdig, P.out2,
-                                               P.vbits + P.shift2, fill, region0, P.cap2, P.err);
+                                               P.vbits + P.shift2, fill, region0, P.cap2, P.err,
+                                               [&]() { if (PG_SPLIT2S_PREFETCH && c1 < hi) load(c1, ne); });
+    if (!PG_SPLIT2S_PREFETCH && c1 < hi) load(c1, ne);
+#pragma unroll
+    for (int k = 0; k < E; k++) e[k] = ne[k];
   }
 }
 
@@ -439,8 +489,10 @@ __global__ __launch_bounds__(kST) void part_scatter_kernel(PartScanSpec P) {
 
 // ------------------------------------------------------------------------------------------ level 1, speculative
 
+// 512 threads x 16 docs, two resident blocks per CU (their sort and write phases overlap each other's loads): 3.06 ms
+// on config 4 vs 3.65 for one 1 024-thread block per CU with the next tile prefetched into registers (r03_v3)
 #ifndef PG_DIRECT_THREADS
-#define PG_DIRECT_THREADS 1024
+#define PG_DIRECT_THREADS 512
 #endif
 constexpr uint32_t kDT = PG_DIRECT_THREADS;   // threads of a part_direct block
 constexpr uint32_t kDE = kTileDocs / kDT;     // docs per thread per round (a round is one tile)
@@ -455,6 +507,27 @@ __device__ __forceinline__ void stage_words(rsrc_t r, uint32_t w0, uint32_t nw, 
   }
 }
 
+// The same word range loaded into registers (thread t: uint4s t + kDT r) while the block sorts the previous tile, and
+// stored to LDS once the stage is free again: the next tile's HBM latency hides behind this tile's sort and writes.
+constexpr uint32_t kPreQ = ((256u * 32u + 4u) / 4u + kDT - 1u) / kDT;  // uint4s per thread for the widest column
+__device__ __forceinline__ void pre_load(rsrc_t r, uint32_t w0, uint32_t nw, uint4 (&x)[kPreQ]) {
+#pragma unroll
+  for (uint32_t k = 0; k < kPreQ; k++) {
+    const uint32_t q = threadIdx.x + kDT * k;
+    if (q < nw / 4) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (w0 + 4u * q) * 4u, 0, 0);
+      x[k] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  }
+}
+__device__ __forceinline__ void pre_store(uint32_t* lds, uint32_t nw, const uint4 (&x)[kPreQ]) {
+#pragma unroll
+  for (uint32_t k = 0; k < kPreQ; k++) {
+    const uint32_t q = threadIdx.x + kDT * k;
+    if (q < nw / 4) *(uint4*)(lds + 4u * q) = x[k];
+  }
+}
+
 // the b-bit value at bit p of a packed run staged at lds (FixedBitIntReader: MSB first)
 __device__ __forceinline__ uint32_t lds_unpack(const uint32_t* lds, uint32_t p, uint32_t b) {
   const uint32_t k = p >> 5, o = p & 31u;
@@ -462,13 +535,6 @@ __device__ __forceinline__ uint32_t lds_unpack(const uint32_t* lds, uint32_t p, 
   return (uint32_t)(win >> (64u - o - b)) & (0xFFFFFFFFu >> (32u - b));
 }
 
-__device__ __forceinline__ rsrc_t part_rsrc(const void* p, uint32_t bytes) {
-  const uint64_t a = (uint64_t)p;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
-                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
 
 // Table-global id of a raw (dictId / decoded) value: M = 0 decoded image (vbase + raw - base), 1 gather from an int32
 // array (`tab` = the int32 dictionary with `base`, or the keymap with base 0), 2 int64 dictionary (not taken by the
@@ -517,7 +583,7 @@ __device__ __forceinline__ uint32_t direct_unpack(const PartDirectSpec& P, const
     const uint32_t d = ok ? (uint32_t)(g >> P.shift1) : kPartL1;
     e[j] = (uint32_t)(((g & lmask) << P.vbits) | vid);
     dr[j] = (d << 16) | atomicAdd(&cnt[d], 1u);
-    if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // at most 8 docs' gathers in flight (their 64-bit addresses)
+    if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // at most 4 docs in flight (loads, 64-bit gather addresses)
   }
   return bad;
 }
@@ -536,11 +602,10 @@ __global__ __launch_bounds__(kDT, W) void part_direct_kernel(PartDirectSpec P) {
   uint32_t bad = 0;
   const uint64_t i0 = (uint64_t)b * P.num_items / P.blocks, i1 = (uint64_t)(b + 1) * P.num_items / P.blocks;
   for (uint64_t it = i0; it < i1; it++) {
-    const WorkItem w = P.items[it];
-    const SegDesc sd = P.segs[w.seg];
-    const ColDesc kc = sd.keycols[0];
-    ColDesc vc = kc;
-    if (P.has_val) vc = sd.aggcols[2 * P.val_agg];
+    const WorkItem w = ldcf(P.items, it);
+    const SegDesc sd = ldcf(P.segs, w.seg);
+    const ColDesc kc = ldcf(sd.keycols, 0);
+    const ColDesc vc = P.has_val ? ldcf(sd.aggcols, 2ull * P.val_agg) : kc;
     const uint32_t kb = __builtin_amdgcn_readfirstlane(kc.bits);
     const uint32_t vb = P.has_val ? __builtin_amdgcn_readfirstlane(vc.bits) : 0u;
     const uint32_t nwk = 256u * kb + 4u, nwv = P.has_val ? 256u * vb + 4u : 0u;
@@ -551,14 +616,17 @@ __global__ __launch_bounds__(kDT, W) void part_direct_kernel(PartDirectSpec P) {
     const int32_t* vtab = vmap ? vc.keymap : (const int32_t*)vc.dict;
     const int64_t kbase = kmap ? 0 : P.key_base, vbase = vmap ? 0 : P.val_base;
     const uint32_t num_docs = __builtin_amdgcn_readfirstlane(sd.num_docs);
-    for (uint32_t t = w.tile_begin; t < w.tile_end; t++) {
+    const uint32_t t_end = min(w.tile_end, (num_docs + (uint32_t)kTileDocs - 1u) / (uint32_t)kTileDocs);
+    bool staged = false;  // this tile's words already in LDS (prefetched during the previous round)
+    for (uint32_t t = w.tile_begin; t < t_end; t++) {
       const uint32_t r0 = t * (uint32_t)kTileDocs;
-      if (r0 >= num_docs) break;
       const uint32_t m = min((uint32_t)kTileDocs, num_docs - r0);
       // 1. the tile's words of both columns, coalesced, into LDS
-      stage_words(rk, t * 256u * kb, nwk, dl);
-      if (P.has_val) stage_words(rv, t * 256u * vb, nwv, dl + nwk);
-      __syncthreads();
+      if (!staged) {
+        stage_words(rk, t * 256u * kb, nwk, dl);
+        if (P.has_val) stage_words(rv, t * 256u * vb, nwv, dl + nwk);
+        __syncthreads();
+      }
       // 2. entries + ranks ((digit << 16 | rank) and the entry are all a thread keeps)
       uint32_t dr[kDE], e[kDE];
       bad |= direct_unpack<KM, VM>(P, kc, vc, ktab, kbase, vtab, vbase, dl, dl + nwk, kb, vb, m, cnt, dr, e);
@@ -594,6 +662,17 @@ __global__ __launch_bounds__(kDT, W) void part_direct_kernel(PartDirectSpec P) {
         if (tid == 0) cnt[kPartL1] = 0;
       }
       __syncthreads();
+      // the next tile of this item: its loads go out now (after the reservations, whose returned values wait on every
+      // outstanding vector load) and land in registers while this tile is sorted and written
+#ifndef PG_DIRECT_PREFETCH
+#define PG_DIRECT_PREFETCH 0  // 1: the next tile's words into registers during the sort (for one block per CU)
+#endif
+      const bool pre = PG_DIRECT_PREFETCH && t + 1 < t_end;
+      uint4 pk[kPreQ], pv[kPreQ];
+      if (pre) {
+        pre_load(rk, (t + 1) * 256u * kb, nwk, pk);
+        if (P.has_val) pre_load(rv, (t + 1) * 256u * vb, nwv, pv);
+      }
       uint32_t* sbuf = dl;
       uint8_t* sdig = (uint8_t*)(dl + kTileDocs);
 #pragma unroll
@@ -613,6 +692,12 @@ __global__ __launch_bounds__(kDT, W) void part_direct_kernel(PartDirectSpec P) {
         if (c0 != ~0ull) P.out1[c0 + (i - start[d])] = sbuf[i];
       }
       __syncthreads();
+      if (pre) {
+        pre_store(dl, nwk, pk);
+        if (P.has_val) pre_store(dl + nwk, nwv, pv);
+        __syncthreads();
+      }
+      staged = pre;
     }
   }
   if (bad) atomicOr(P.err, bad);
@@ -624,7 +709,11 @@ hipError_t launch_part_direct(const PartDirectSpec& p, uint32_t key_bits, uint32
   const size_t sort = 4ull * kTileDocs + kTileDocs;  // sbuf + sdig
   const size_t lds = stage > sort ? stage : sort;
   const dim3 g(p.blocks), b(kDT);
-  constexpr int kW0 = kDT / 256, kW1 = 2 * kDT / 256;  // one / two resident blocks' worth of waves per SIMD
+#ifndef PG_DIRECT_WAVES2
+#define PG_DIRECT_WAVES2 (3 * PG_DIRECT_THREADS / 256)
+#endif
+  // register budget: two resident blocks per CU (default) or PG_DIRECT_WAVES2 waves per SIMD
+  constexpr int kW0 = 2 * kDT / 256, kW1 = PG_DIRECT_WAVES2;
   static const int waves = getenv("PG_DIRECT_WAVES") ? atoi(getenv("PG_DIRECT_WAVES")) : kW0;
 #define PG_DIRECT(K, V)                                                                                 \
   if (key_mode == (K) && val_mode == (V)) {                                                             \

@@ -847,6 +847,7 @@ constexpr uint64_t kDefaultNumGroupsLimit = 100000;
 constexpr uint64_t kDenseMaxSlots = 1ull << 26;      // dense key spaces up to 64 M slots
 constexpr uint64_t kStateBudget = 48ull << 30;       // bytes of group state one query may allocate
 constexpr uint64_t kMaxHashSlots = 1ull << 30;
+constexpr uint64_t kTrimSelectMinGroups = 1ull << 16;  // ORDER BY trim by radix select from this many groups (else sort)
 constexpr uint64_t kPartMinStateBytes = 64ull << 20;  // radix-partitioned group-by above this much dense state
 
 struct PartPlan {  // GM_PART pipeline of one query (pg_part.hip)
@@ -3362,12 +3363,43 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
     if ((rc = read_back(d_span, span, s))) return rc;
     const uint64_t diff = span.any & span.anyz;
     const uint32_t b0 = diff ? (uint32_t)__builtin_ctzll(diff) : 0u, b1 = diff ? 64u - (uint32_t)__builtin_clzll(diff) : 1u;
-    const size_t tb = sort_temp_bytes(n, b0, b1);
-    void* temp = sc.get<uint8_t>(tb, rc);
-    if (rc) return rc;
-    HIP_CHECK(launch_sort_pairs(okeys, skeys, pos, spos, n, temp, tb, s, b0, b1));
-    HIP_CHECK(launch_cutoff(skeys, n, plan->limit, d_nc, s));
-    if ((rc = read_back(d_nc, nc, s))) return rc;
+    const char* sel_env = getenv("PG_TRIM_SELECT");  // 0: always sort, 1: always select (tests), else by size
+    const int sel = sel_env ? atoi(sel_env) : -1;
+    if (sel == 1 || (sel != 0 && n >= kTrimSelectMinGroups)) {
+      // radix select of the limit-th smallest key (a histogram readback per <= 8-bit digit of the differing bits),
+      // then the positions of every key up to it: no sort of all n groups
+      const uint32_t W = b1 - b0;
+      unsigned int* hist = sc.get<unsigned int>(256, rc);
+      unsigned int* hh = (unsigned int*)t_ctx.readback.get(1024);
+      if (rc) return rc;
+      if (!hh) return fail(PG_E_NOMEM, "pinned readback failed");
+      uint64_t need = plan->limit, prefix = 0;
+      for (uint32_t hi = W; hi > 0;) {
+        const uint32_t lo = hi > 8 ? hi - 8 : 0;
+        HIP_CHECK(hipMemsetAsync(hist, 0, 1024, s));
+        HIP_CHECK(launch_okey_hist(okeys, n, b0, W, lo, hi, prefix, hist, s));
+        HIP_CHECK(hipMemcpyAsync(hh, hist, 1024, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        uint64_t cum = 0;
+        uint32_t d = 0;
+        const uint32_t nd = 1u << (hi - lo);
+        for (; d + 1 < nd && cum + hh[d] < need; d++) cum += hh[d];
+        need -= cum;
+        prefix = (prefix << (hi - lo)) | d;
+        hi = lo;
+      }
+      unsigned long long* d_cnt = (unsigned long long*)d_nc;
+      HIP_CHECK(hipMemsetAsync(d_cnt, 0, 8, s));
+      HIP_CHECK(launch_okey_select(okeys, n, b0, W, prefix, spos, d_cnt, s));
+      if ((rc = read_back(d_nc, nc, s))) return rc;
+    } else {
+      const size_t tb = sort_temp_bytes(n, b0, b1);
+      void* temp = sc.get<uint8_t>(tb, rc);
+      if (rc) return rc;
+      HIP_CHECK(launch_sort_pairs(okeys, skeys, pos, spos, n, temp, tb, s, b0, b1));
+      HIP_CHECK(launch_cutoff(skeys, n, plan->limit, d_nc, s));
+      if ((rc = read_back(d_nc, nc, s))) return rc;
+    }
     uint64_t* gk = sc.get<uint64_t>(nc, rc);
     double* gv = sc.get<double>(nc * AA, rc);
     int64_t* gc = sc.get<int64_t>(nc * AA, rc);

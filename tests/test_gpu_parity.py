@@ -179,9 +179,12 @@ def test_num_groups_limit_truncation(limit, gpu_engine, oracle_engine):
         assert len(g.rows) <= 3 * limit
 
 
-def test_order_by_trim_on_device(gpu_engine, oracle_engine, sv_table_inter):
+@pytest.mark.parametrize("select", ["0", "1"])
+def test_order_by_trim_on_device(select, monkeypatch, gpu_engine, oracle_engine, sv_table_inter):
     """ORDER BY ... LIMIT applied on the device (TableResizer.getTopRecords): the kept candidates (boundary ties
-    included) give the reference's top rows."""
+    included) give the reference's top rows -- by a sort of every group's order key (PG_TRIM_SELECT=0) and by the
+    radix select of the limit-th key (=1; by default from 65 536 groups)."""
+    monkeypatch.setenv("PG_TRIM_SELECT", select)
     for sql in ["SELECT column9, SUM(column1) FROM t GROUP BY column9 ORDER BY SUM(column1) DESC, column9 LIMIT 7",
                 "SELECT column11, column12, AVG(column3), COUNT(*) FROM t GROUP BY column11, column12 "
                 "ORDER BY AVG(column3), column12 DESC, column11 LIMIT 5",

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Link a variant libpinot_gpu with pg_part.hip built under extra -D flags: tools/part_variant.sh <name> <flags...>
+# -> pinot_amd/libpinot_gpu_<name>.so (select it with PINOT_GPU_LIB).  Needs the main build's objects.
+set -e
+N=$1; shift
+cd "$(dirname "$0")/../pinot_amd/csrc"
+HIPCC=/opt/rocm/bin/hipcc
+FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -munsafe-fp-atomics -Wall -Wno-unused-function -Wno-unused-variable -Wno-unused-value -Wno-unused-result -I../../include"
+$HIPCC $FL "$@" -c pg_part.hip -o build/pg_part_$N.o
+OBJS=$(ls build/*.o | grep -v 'pg_part' | tr '\n' ' ')
+$HIPCC --offload-arch=gfx950 -shared -o ../libpinot_gpu_$N.so $OBJS build/pg_part_$N.o
+echo built ../libpinot_gpu_$N.so
