@@ -46,6 +46,8 @@ struct RoaringJob {
   uint32_t nids, num_docs;
   uint32_t* bm;                    // doc bitmap (packed 1-bit column order)
   uint32_t negate, key0, nkeys, first_block;  // first_block: prefix of nkeys over the jobs
+  const uint32_t* keydir;          // optional key-major directory: [key * card + dictId] = container or ~0
+  uint32_t card, pad;
 };
 hipError_t launch_roaring_keys(const RoaringJob* jobs, uint32_t njobs, uint32_t blocks, hipStream_t s);
 hipError_t launch_mv_scan(const uint32_t* words, uint32_t bits, const uint32_t* offsets, uint32_t num_docs,

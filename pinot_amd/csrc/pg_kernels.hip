@@ -342,12 +342,21 @@ __global__ __launch_bounds__(256) void roaring_keys_kernel(const RoaringJob* __r
     const uint32_t i = r0 + tid;
     if (i < J.nids) {
       const uint32_t id = (uint32_t)J.ids[i];
-      uint32_t a = J.dir[id], b = J.dir[id + 1];  // this dictId's containers, ascending keys: find `key`
-      while (a < b) {
-        const uint32_t m = (a + b) >> 1;
-        if (J.cs[m].key < key) a = m + 1; else b = m;
+      uint32_t a;
+      bool hit;
+      if (J.keydir) {  // one load: the key-major directory built at upload
+        a = J.keydir[(uint64_t)key * J.card + id];
+        hit = a != 0xFFFFFFFFu;
+      } else {
+        a = J.dir[id];
+        uint32_t b = J.dir[id + 1];  // this dictId's containers, ascending keys: find `key`
+        while (a < b) {
+          const uint32_t m = (a + b) >> 1;
+          if (J.cs[m].key < key) a = m + 1; else b = m;
+        }
+        hit = a < J.dir[id + 1] && J.cs[a].key == key;
       }
-      if (a < J.dir[id + 1] && J.cs[a].key == key) {
+      if (hit) {
         const RoaringContainer c = J.cs[a];
         const uint8_t* p = J.roaring + c.offset;
         if (c.type == 0) {  // array of uint16

@@ -258,6 +258,8 @@ struct ColumnRes {
   bool has_inv = false;
   DevBuf roaring, containers, inv_dir_dev;
   std::vector<uint32_t> inv_dir;  // CSR: containers of dictId d are [inv_dir[d], inv_dir[d+1]) (+ a device copy)
+  DevBuf inv_keydir;              // key-major: [key * card + dictId] = container index or ~0 (when small enough)
+  uint32_t inv_keydir_card = 0;
   // keymap
   bool has_keymap = false;
   DevBuf keymap;
@@ -278,6 +280,8 @@ struct ColumnRes {
 // Dictionaries at least this large get a decoded forward index (PG_DECODED=0 disables, =1 builds it for every
 // INT / LONG dictionary): below it the dictionary stays cache-resident and the gather is cheap.
 constexpr uint32_t kDecodeMinCard = 1u << 17;
+// key-major roaring container directories up to this many entries per column (64 M entries = 256 MB)
+constexpr uint64_t kKeyDirMaxEntries = 1ull << 26;
 
 // Build c.vals when c has an INT / LONG dictionary of >= kDecodeMinCard values and an SV bit-packed forward index.
 int build_decoded(ColumnRes& c, hipStream_t s) {
@@ -642,6 +646,19 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
         HIP_CHECK(hipMemcpyAsync(tmp.containers.p, cs.data(), cs.size() * sizeof(RoaringContainer), hipMemcpyHostToDevice, s));
       if ((rc = tmp.inv_dir_dev.alloc(4ull * tmp.inv_dir.size() + 16))) return rc;
       HIP_CHECK(hipMemcpyAsync(tmp.inv_dir_dev.p, tmp.inv_dir.data(), 4ull * tmp.inv_dir.size(), hipMemcpyHostToDevice, s));
+      // key-major directory (one load per (dictId, 64 K-doc key) in the pre-pass instead of a binary search over the
+      // dictId's containers), kept when it stays within kKeyDirMaxEntries
+      const uint64_t nkeys = ((uint64_t)d->num_docs + 65535) >> 16, card = d->cardinality;
+      std::vector<uint32_t> kd;
+      if (nkeys * card <= kKeyDirMaxEntries && nkeys * card) {
+        kd.assign(nkeys * card, 0xFFFFFFFFu);
+        for (uint32_t id = 0; id < card; id++)
+          for (uint32_t ci = tmp.inv_dir[id]; ci < tmp.inv_dir[id + 1]; ci++)
+            if (cs[ci].key < nkeys) kd[(uint64_t)cs[ci].key * card + id] = ci;
+        if ((rc = tmp.inv_keydir.alloc(4ull * kd.size() + 16))) return rc;
+        tmp.inv_keydir_card = (uint32_t)card;
+        HIP_CHECK(hipMemcpyAsync(tmp.inv_keydir.p, kd.data(), 4ull * kd.size(), hipMemcpyHostToDevice, s));
+      }
       HIP_CHECK(hipStreamSynchronize(s));
       break;
     }
@@ -739,6 +756,8 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
       c.roaring = std::move(tmp.roaring);
       c.containers = std::move(tmp.containers);
       c.inv_dir_dev = std::move(tmp.inv_dir_dev);
+      c.inv_keydir = std::move(tmp.inv_keydir);
+      c.inv_keydir_card = tmp.inv_keydir_card;
       c.inv_dir.swap(tmp.inv_dir);
       if (!c.num_docs) c.num_docs = tmp.num_docs;
       break;
@@ -1959,33 +1978,52 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     }
   }
   P.entries_in_filter = entries_in_filter;
-  // Inverted-leaf bitmaps are read only where the docs can match: a doc range among the root AND's direct children
-  // (a sorted-index leaf) bounds the 64 K-doc keys their roaring pre-pass builds.
-  if (std::any_of(pre.begin(), pre.end(), [](const PrepassOp& o) { return o.kind == PrepassOp::ROARING; }) &&
-      plan->num_ops && plan->ops[plan->num_ops - 1] < 0 && ((-plan->ops[plan->num_ops - 1]) & 0x300) == 0x100) {
+  // The docs that can match at all: the doc ranges among the root AND's direct children (sorted-index leaves; an
+  // empty leaf empties it).  They bound the 64 K-doc keys an inverted leaf's roaring pre-pass builds and the tiles
+  // the fused scan walks (SortedIndexBasedFilterOperator + AndDocIdSet: the other children are only asked about docs
+  // inside the range).
+  std::vector<std::pair<uint32_t, uint32_t>> root_range(S);
+  {
     std::vector<int> root_leaves;  // direct leaf children of the root AND (postfix: the operands on the stack)
-    std::vector<int> st;           // stack of leaf index or -1 (a subtree)
-    for (uint32_t i = 0; i < plan->num_ops; i++) {
-      const int32_t op = plan->ops[i];
-      if (op >= 0) { st.push_back(op); continue; }
-      const int n = op == PG_OP_NOT ? 1 : ((-op) & 0xFF);
-      if (i + 1 == plan->num_ops) root_leaves.assign(st.end() - n, st.end());
-      st.resize(st.size() - n);
-      st.push_back(-1);
+    if (plan->num_ops == 1 && plan->ops[0] >= 0) {
+      root_leaves.push_back(plan->ops[0]);  // a lone leaf
+    } else if (plan->num_ops && plan->ops[plan->num_ops - 1] < 0 && ((-plan->ops[plan->num_ops - 1]) & 0x300) == 0x100) {
+      std::vector<int> st;  // stack of leaf index or -1 (a subtree)
+      for (uint32_t i = 0; i < plan->num_ops; i++) {
+        const int32_t op = plan->ops[i];
+        if (op >= 0) { st.push_back(op); continue; }
+        const int n = op == PG_OP_NOT ? 1 : ((-op) & 0xFF);
+        if (i + 1 == plan->num_ops) root_leaves.assign(st.end() - n, st.end());
+        st.resize(st.size() - n);
+        st.push_back(-1);
+      }
     }
-    for (PrepassOp& op : pre) {
-      if (op.kind != PrepassOp::ROARING) continue;
-      int64_t lo = 0, hi = op.num_docs;
+    for (uint32_t si = 0; si < S; si++) {
+      int64_t lo = 0, hi = plan->segments[si].num_docs;
       for (int li : root_leaves) {
         if (li < 0) continue;
-        const LeafDesc& dl = leaves[(uint64_t)op.seg * L + li];
+        const LeafDesc& dl = leaves[(uint64_t)si * L + li];
         if (dl.kind == LK_DOCRANGE) { lo = std::max<int64_t>(lo, dl.lo); hi = std::min<int64_t>(hi, dl.hi); }
         else if (dl.kind == LK_NONE) hi = lo;
       }
-      if (hi <= lo) { op.nkeys = 0; continue; }
-      op.key0 = (uint32_t)(lo >> 16);
-      op.nkeys = (uint32_t)(((hi - 1) >> 16) + 1) - op.key0;
+      root_range[si] = hi > lo ? std::make_pair((uint32_t)lo, (uint32_t)hi) : std::make_pair(0u, 0u);
     }
+  }
+  for (PrepassOp& op : pre) {
+    if (op.kind != PrepassOp::ROARING) continue;
+    const uint32_t lo = root_range[op.seg].first, hi = std::min(root_range[op.seg].second, op.num_docs);
+    if (hi <= lo) { op.nkeys = 0; continue; }
+    op.key0 = lo >> 16;
+    op.nkeys = ((hi - 1) >> 16) + 1 - op.key0;
+  }
+  // the fused scan's tiles of each segment: those overlapping its root range
+  std::vector<uint32_t> seg_tile0(S, 0);
+  for (uint32_t si = 0; si < S; si++) {
+    if (!seg_tiles[si]) continue;
+    const uint32_t lo = root_range[si].first, hi = root_range[si].second;
+    if (hi <= lo) { seg_tiles[si] = 0; continue; }
+    seg_tile0[si] = lo / kTileDocs;
+    seg_tiles[si] = (hi + kTileDocs - 1) / kTileDocs - seg_tile0[si];
   }
 
   PG_PROF("leaves");
@@ -2092,15 +2130,15 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         advance(t0);
         const uint64_t seg_end = seg_first + seg_tiles[si];
         const uint64_t cut = t1 > seg_end ? seg_end : t0 + (t1 - t0) / 2;
-        items[2 * b] = {si, (uint32_t)(t0 - seg_first), (uint32_t)(cut - seg_first), 0};
+        items[2 * b] = {si, seg_tile0[si] + (uint32_t)(t0 - seg_first), seg_tile0[si] + (uint32_t)(cut - seg_first), 0};
         advance(cut);
-        items[2 * b + 1] = {si, (uint32_t)(cut - seg_first), (uint32_t)(t1 - seg_first), 0};
+        items[2 * b + 1] = {si, seg_tile0[si] + (uint32_t)(cut - seg_first), seg_tile0[si] + (uint32_t)(t1 - seg_first), 0};
       }
       grid = (uint32_t)G;
     } else {
       for (uint32_t s2 = 0; s2 < S; s2++)
         for (uint32_t t = 0; t < seg_tiles[s2]; t += kItemTiles)
-          items.push_back({s2, t, std::min(seg_tiles[s2], t + (uint32_t)kItemTiles), 0});
+          items.push_back({s2, seg_tile0[s2] + t, seg_tile0[s2] + std::min(seg_tiles[s2], t + (uint32_t)kItemTiles), 0});
       // the XCD-grouped order wants every block resident at once (one round), so the step-major interleave holds:
       // dense SUM over a 4 MB dictionary 6.4 ms at 2 rounds -> 4.3 ms at 1 round
       grid = (uint32_t)std::min<uint64_t>(items.size(), scan_grid_cap(K > 0, want_xcd));
@@ -2603,6 +2641,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       j.roaring = (const uint8_t*)op.col->roaring.p;
       j.cs = (const RoaringContainer*)op.col->containers.p;
       j.dir = (const uint32_t*)op.col->inv_dir_dev.p;
+      j.keydir = (const uint32_t*)op.col->inv_keydir.p;
+      j.card = op.col->inv_keydir_card;
       j.ids = (const int32_t*)(dA + op.in_off);
       j.bm = (uint32_t*)(dS + op.out_off);
     }
@@ -3580,7 +3620,7 @@ int pg_resident_bytes(uint64_t* out) {
   for (auto& kv : g_segs)
     for (auto& c : kv.second->cols)
       t += c.second.dict.bytes + c.second.words.bytes + c.second.mv_offsets.bytes + c.second.roaring.bytes +
-           c.second.containers.bytes + c.second.keymap.bytes + c.second.vals.bytes + c.second.rawv.bytes;
+           c.second.containers.bytes + c.second.inv_keydir.bytes + c.second.keymap.bytes + c.second.vals.bytes + c.second.rawv.bytes;
   *out = t;
   return PG_OK;
 }
