@@ -308,6 +308,6 @@ class GpuEngine:
                 acols.append([ds.values_of(ids[offs[g * A + a]:offs[g * A + a + 1]]) for g in range(G)])
             else:
                 acols.append(v.astype(np.float64).tolist())
-        rows = dict(zip(keyt, (list(x) for x in zip(*acols)))) if A else {k: [] for k in keyt}
-        st = ExecutionStats(*(int(x) for x in ra["stats"]))
+        rows = dict(zip(keyt, map(list, zip(*acols)))) if A else {k: [] for k in keyt}
+        st = ExecutionStats(*ra["stats"].tolist())
         return IntermediateResult(plan.aggs, list(plan.query.group_by), rows, st)
