@@ -101,7 +101,12 @@ struct StreamSpec {
   // exact mode (1 024-thread blocks, one per CU): a coarse IN bitmap's exact LUT (exact_nwords[seg] words, <= 128 KiB)
   // is staged whole in LDS, so no value is a candidate to resolve
   const uint32_t* exact_nwords;
+  // further leaves over packed columns of at most kStreamStageBits bits: a wave stages its 64 groups' words of the
+  // column into its LDS slice (16-byte coalesced loads) and tests its survivors from there instead of per-doc window
+  // reads.  stage_words: words per wave slice (0: off), placed after the IN-set words (set_lds_ints, a multiple of 4).
+  uint32_t stage_words, stage_pad;
 };
+constexpr uint32_t kStreamStageBits = 16;
 hipError_t launch_stream(const StreamSpec& p, uint32_t bits, uint32_t blocks, hipStream_t s);
 
 // ---- radix-partitioned group-by (pg_part.hip): level 2 + per-bucket aggregation, after the two scan passes

@@ -240,6 +240,46 @@ __device__ __forceinline__ uint32_t eval_extra(const LeafDesc& X, const uint32_t
   return X.excl ? ~r : r;
 }
 
+// The same test from the wave's LDS slice: the words of its 64 consecutive groups (lane l's group = words
+// [l * B, l * B + B) of the slice), staged by stage_slice.
+__device__ __forceinline__ uint32_t eval_staged(const LeafDesc& X, const uint32_t* lds_sets, const uint32_t* slice,
+                                                uint32_t lane, uint32_t need) {
+  const uint32_t b = X.bits, mask = 0xFFFFFFFFu >> (32u - b);
+  uint32_t r = 0;
+  for (uint32_t rem = need; rem; rem &= rem - 1u) {
+    const uint32_t j = (uint32_t)__ffs(rem) - 1u;
+    const uint32_t bit = (lane * 32u + j) * b, k = bit >> 5;
+    const uint64_t win = ((uint64_t)slice[k] << 32) | (uint64_t)slice[k + 1];
+    const uint32_t v = (uint32_t)(win >> (64u - (bit & 31u) - b)) & mask;
+    bool hit;
+    if (X.kind == LK_RANGE) {
+      hit = (v - (uint32_t)X.lo) < (uint32_t)(X.hi - X.lo);
+    } else if (X.kind == LK_SET_LDS) {
+      const uint32_t y = v >> X.shift;
+      hit = (lds_sets[X.lds_off + (y >> 5)] >> (y & 31u)) & 1u;
+      if (hit && X.shift) hit = (X.lut[v >> 5] >> (v & 31u)) & 1u;
+    } else {
+      hit = (X.aux[v >> 5] >> (v & 31u)) & 1u;
+    }
+    r |= (uint32_t)hit << j;
+  }
+  return X.excl ? ~r : r;
+}
+
+// The wave's 64 groups [wg0, wg0 + 64) of a b-bit column into its slice: 64 * b words + 4 of window padding, 16-byte
+// loads (reads past the column return 0).  Wave-local: the same wave reads the slice back.
+__device__ __forceinline__ void stage_slice(const LeafDesc& X, uint32_t wg0, uint32_t* slice, uint32_t lane) {
+  const rsrc_t rs = rsrc_of(X.words, X.wbytes);
+  const uint32_t nq = 16u * X.bits + 1u, w0 = wg0 * X.bits;
+  for (uint32_t q = lane; q < nq; q += 64u) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (w0 + 4u * q) * 4u, 0, 0);
+    *(uint4*)(slice + 4u * q) = make_uint4(v[0], v[1], v[2], v[3]);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // The selective stream: the driving leaf of the root AND over the block's items (32-doc groups, thread-contiguous
 // 16-byte loads, 6 waves per SIMD so ~120 KiB per CU are in flight), survivors appended to the item's region in group
 // order within each wave: one wave prefix sum + one LDS cursor atomic per wave and group round that has a survivor.
@@ -300,7 +340,14 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? 6 : 7)) void stream_k
         for (uint32_t x = 0; x < (EXTRA ? p.num_extra : 0u); x++) {
           if (__ballot(m != 0) == 0) break;
           const LeafDesc X = ldcf(seg_leaves, p.extra[x]);
-          if (m) m &= eval_extra(X, lds_sets, (uint32_t)d0, m);
+          const bool packed = X.kind == LK_RANGE || X.kind == LK_SET_LDS || X.kind == LK_SET_LUT;
+          if (EXTRA && p.stage_words && packed && X.bits * 64u + 4u <= p.stage_words) {
+            uint32_t* slice = lds_sets + p.set_lds_ints + (tid >> 6) * p.stage_words;
+            stage_slice(X, g0 + (tid & ~63u), slice, lane);
+            if (m) m &= eval_staged(X, lds_sets, slice, lane, m);
+          } else if (m) {
+            m &= eval_extra(X, lds_sets, (uint32_t)d0, m);
+          }
         }
         if (__ballot(m != 0) == 0) continue;
         const uint32_t cnt = __popc(m);
@@ -330,7 +377,8 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? 6 : 7)) void stream_k
 
 hipError_t launch_stream(const StreamSpec& p, uint32_t bits, uint32_t blocks, hipStream_t s) {
   if (!p.num_items || !blocks) return hipSuccess;
-  const size_t lds = p.exact_nwords ? (size_t)128 * 1024 : (size_t)p.set_lds_ints * 4;
+  const size_t lds = p.exact_nwords ? (size_t)128 * 1024
+                                    : (size_t)p.set_lds_ints * 4 + (p.num_extra ? (size_t)4 * 4 * p.stage_words : 0);
   if (p.exact_nwords) {
     static bool attr = false;  // >64 KiB of dynamic LDS must be opted into per kernel (once per process)
     if (!attr) {

@@ -2722,7 +2722,19 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     ss.exact_nwords = sp.exact ? (const uint32_t*)(dA + off_exact) : nullptr;
     ss.interleave = sp.interleave ? 1u : 0u;
     for (size_t x = 0; x < sp.extra.size(); x++) ss.extra[x] = sp.extra[x];
-    ss.set_lds_ints = sp.set_ints;
+    ss.set_lds_ints = (sp.set_ints + 3u) & ~3u;  // the wave slices start 16-byte aligned after the IN sets
+    {
+      // wave slices for the further leaves' columns of <= kStreamStageBits bits (PG_STREAM_STAGE=0: per-doc windows)
+      static const char* stg_env = getenv("PG_STREAM_STAGE");
+      uint32_t bmax = 0;
+      for (uint32_t x : sp.extra)
+        for (uint32_t si = 0; si < S; si++) {
+          const LeafDesc& dl = leaves[(uint64_t)si * L + x];
+          if ((dl.kind == LK_RANGE || dl.kind == LK_SET_LDS || dl.kind == LK_SET_LUT) && dl.bits <= kStreamStageBits)
+            bmax = std::max(bmax, dl.bits);
+        }
+      if (bmax && !sp.exact && !(stg_env && atoi(stg_env) == 0)) ss.stage_words = 64u * bmax + 4u;
+    }
     ss.segs = q.segs;
     ss.items = q.items;
     ss.docs = (uint32_t*)l_docs.p;
