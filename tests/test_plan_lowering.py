@@ -1,0 +1,74 @@
+"""Host lowering (pinot_amd/plan.py) without a GPU: the batched IN / NOT_IN lookup path of CPlan (one id_sets call per
+predicate over all segments, as GpuEngine does through pg_dict_id_sets) lowers every leaf exactly as the per-segment
+PredicateUtils.getDictIdSet restatement does."""
+import numpy as np
+import pytest
+
+from pinot_amd import abi
+from pinot_amd.plan import CPlan, Table, dict_id_set
+from pinot_amd.query import parse
+from pinot_amd.segment import ImmutableSegment
+
+
+def _host_id_sets(segments, calls):
+    """A host stand-in for pg_dict_id_sets: the same contract (ids [S, n] rows holding counts[s] ascending dictIds)."""
+    by_key = {}
+
+    def id_sets(col_id, data_type, literals, seg_keys):
+        calls.append((col_id, data_type, len(literals)))
+        n = len(literals)
+        ids = np.full((len(seg_keys), max(n, 1)), -7, dtype=np.int32)
+        counts = np.zeros(len(seg_keys), dtype=np.uint32)
+        for s, k in enumerate(seg_keys):
+            d = by_key[k]
+            found = dict_id_set(d, list(literals))
+            ids[s, :len(found)] = found
+            counts[s] = len(found)
+        return ids, counts
+
+    return id_sets, by_key
+
+
+@pytest.mark.parametrize("dtype", ["INT", "LONG", "FLOAT", "DOUBLE"])
+def test_batched_in_lowering_matches_per_segment(dtype):
+    rng = np.random.default_rng(3)
+    segs = []
+    for s in range(4):
+        n = 3_001 + 997 * s
+        v = rng.integers(-400, 400, n)
+        data = {"k": v.astype(np.int64) if dtype in ("INT", "LONG") else v.astype(np.float64) / 8,
+                "m": rng.integers(0, 50, n).astype(np.int64)}
+        segs.append(ImmutableSegment.create(f"s{s}", data, {"k": dtype, "m": "INT"}))
+    t = Table("t", segs)
+    lits = ", ".join(str(x) for x in (range(-500, 500, 13) if dtype in ("INT", "LONG") else
+                                      [x / 8 for x in range(-3_000, 3_000, 37)]))
+    calls = []
+    for sql in [f"SELECT COUNT(*) FROM t WHERE k IN ({lits})",
+                f"SELECT m, COUNT(*) FROM t WHERE k NOT IN ({lits}) AND m < 30 GROUP BY m",
+                "SELECT COUNT(*) FROM t WHERE k IN (123456789)"]:
+        q = parse(sql)
+        keys = list(range(1, len(segs) + 1))
+        id_sets, by_key = _host_id_sets(segs, calls)
+        by_key.update({k: s.columns["k"].dictionary for k, s in zip(keys, segs)})
+        batched = CPlan(t, q, segs, keys, id_sets=id_sets)
+        plain = CPlan(t, q, segs, keys)
+        for lb, lp in zip(batched.lowered, plain.lowered):
+            for a, b in zip(lb, lp):
+                assert (a.kind, a.col_id, a.exclusive, a.lo, a.hi) == (b.kind, b.col_id, b.exclusive, b.lo, b.hi)
+                assert (a.ids is None) == (b.ids is None)
+                if a.ids is not None:
+                    assert np.array_equal(np.asarray(a.ids, dtype=np.int32), np.asarray(b.ids, dtype=np.int32))
+    assert calls and all(c[1] == dtype for c in calls)
+
+
+def test_literal_absent_everywhere_is_empty_leaf():
+    rng = np.random.default_rng(0)  # unsorted columns: scan leaves (a sorted one would lower to a sorted-index leaf)
+    segs = [ImmutableSegment.create(f"s{s}", {"k": rng.permutation(np.arange(10 * s, 10 * s + 10, dtype=np.int64))},
+                                    {"k": "INT"}) for s in range(3)]
+    t = Table("t", segs)
+    calls = []
+    id_sets, by_key = _host_id_sets(segs, calls)
+    by_key.update({k: s.columns["k"].dictionary for k, s in zip([1, 2, 3], segs)})
+    p = CPlan(t, parse("SELECT COUNT(*) FROM t WHERE k IN (5, 15, 99)"), segs, [1, 2, 3], id_sets=id_sets)
+    kinds = [lw[0].kind for lw in p.lowered]
+    assert kinds == [abi.PG_LEAF_SV_SCAN, abi.PG_LEAF_SV_SCAN, abi.PG_LEAF_EMPTY]
