@@ -13,7 +13,7 @@ R=$(pwd)
 O=$R/gpurun_out
 T=${TAG}_${WL}
 # the hot-path kernels bench.py's roofline times (pre-pass + stream + scan / partition passes)
-HOT="(scan|stream|part_[a-z0-9]+|roaring_keys|set_lut_bits|fill_ranges|mv_scan|bitmap_not)_kernel"
+HOT="pg::(scan|stream|part_[a-z0-9]+|roaring_keys|set_lut_bits|fill_ranges|mv_scan|bitmap_not)_kernel"
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 420 python3 $R/bench.py --workload $WL $EXTRA > $O/${T}_bench.json 2> $O/${T}_bench.err || { echo "bench failed"; tail -20 $O/${T}_bench.err; exit 1; }
@@ -21,7 +21,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T
   python3 $R/bench.py --workload $WL $EXTRA --no-cpu --steps $STEPS --warmup 3 > $O/${T}_prof_bench.json 2> $O/${T}_prof.err \
   || { echo "kernel trace failed"; tail -20 $O/${T}_prof.err; exit 1; }
 cp $(find $O/${T}_prof -name '*kernel_stats.csv' | head -1) $O/${T}_kernel_stats.csv
-python3 $R/tools/trace_summary.py $O/${T}_prof "pg::$HOT" > $O/${T}_scan_trace.txt
+python3 $R/tools/trace_summary.py $O/${T}_prof "$HOT" > $O/${T}_scan_trace.txt
 rm -rf $O/${T}_prof
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 240 rocprofv3 --pmc $C --kernel-include-regex "$HOT" --output-format csv \
