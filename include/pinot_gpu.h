@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 4
+#define PG_ABI_VERSION 5
 
 typedef enum pg_status {
   PG_OK = 0,
@@ -167,6 +167,13 @@ typedef struct pg_leaf {
   double dlo, dhi;
   uint32_t lo_inclusive, hi_inclusive;
   const void *values;  /* host pointer */
+  /* Dictionary SV / MV scan leaves may carry their IN / NOT_IN literals instead of dictIds: ids == NULL, `values` =
+   * num_values sorted unique literals already converted to the column's stored type and widened (int64 for INT /
+   * LONG, double for FLOAT / DOUBLE), num_ids = how many of them this segment's dictionary holds (pg_dict_id_sets'
+   * count, > 0).  The device finds their dictIds in the resident dictionary itself (one launch for every such leaf of
+   * the query), so the per-segment id lists never cross the boundary.  num_values is 0 for every other leaf. */
+  uint32_t num_values;
+  uint32_t pad;
 } pg_leaf;
 
 /* Filter program: postfix over leaves.  op >= 0 pushes leaf `op`; PG_OP_AND(n)/PG_OP_OR(n) pop n

@@ -1,7 +1,7 @@
 """ctypes mirror of include/pinot_gpu.h (the C ABI).  Shared by the GPU binding and the oracle."""
 import ctypes as C
 
-PG_ABI_VERSION = 4
+PG_ABI_VERSION = 5
 
 PG_OK, PG_E_INVALID, PG_E_HIP, PG_E_NOMEM, PG_E_NOTFOUND, PG_E_UNSUPPORTED, PG_E_CANCELLED, PG_E_TIMEOUT, \
     PG_E_STATE = 0, -1, -2, -3, -4, -5, -6, -7, -8
@@ -49,7 +49,8 @@ class pg_leaf(C.Structure):
     _fields_ = [("kind", C.c_uint32), ("col_id", C.c_uint32), ("exclusive", C.c_uint32), ("num_ids", C.c_uint32),
                 ("lo", C.c_int32), ("hi", C.c_int32), ("ids", C.POINTER(C.c_int32)),
                 ("ilo", C.c_int64), ("ihi", C.c_int64), ("dlo", C.c_double), ("dhi", C.c_double),
-                ("lo_inclusive", C.c_uint32), ("hi_inclusive", C.c_uint32), ("values", C.c_void_p)]
+                ("lo_inclusive", C.c_uint32), ("hi_inclusive", C.c_uint32), ("values", C.c_void_p),
+                ("num_values", C.c_uint32), ("pad", C.c_uint32)]
 
 
 class pg_agg(C.Structure):

@@ -54,13 +54,16 @@ hipError_t launch_mv_scan(const uint32_t* words, uint32_t bits, const uint32_t* 
                           int32_t lo, int32_t hi, const uint32_t* lut, uint32_t excl, uint32_t* bitmap,
                           hipStream_t s);
 struct LutJob {            // set bits ids[0..n) in lut and ids >> shift in region (one batched launch per query)
-  const int32_t* ids;
+  const int32_t* ids;        // or null: the dictIds of the n literals `values` found in `dict` (values mode)
   uint32_t* lut;             // exact bitmap over dictIds, or null
   uint32_t* region;          // LDS-set filter bitmap over dictId >> shift, or null
   uint32_t n;
   uint32_t shift;
+  const void* values;        // values mode: n sorted literals of the dictionary's type (dtype)
+  const void* dict;          //   the segment's typed dictionary of `card` values
+  uint32_t card, dtype;
 };
-hipError_t launch_set_lut_bits(const LutJob* jobs, uint32_t njobs, hipStream_t s);
+hipError_t launch_set_lut_bits(const LutJob* jobs, uint32_t njobs, uint32_t max_n, hipStream_t s);
 
 // IN / NOT_IN literal lowering for many segments in one launch (PredicateUtils.getDictIdSet): out[s * n + i] = the
 // dictId of values[i] in segment s's dictionary, or -1

@@ -1731,10 +1731,46 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   std::vector<WorkItem>& items = t_ctx.items;
   items.clear();
   std::vector<PrepassOp> pre;
-  struct LutReq {  // arena ids -> scratch LUT and / or LDS-set region (~0 = none)
+  struct LutReq {  // arena ids (or literal values found in `dict`) -> scratch LUT and / or LDS-set region (~0 = none)
     uint64_t ids_off; uint32_t n; uint64_t lut_off; uint64_t region_off = ~0ull; uint32_t shift = 0;
+    uint64_t vals_off = ~0ull; const void* dict = nullptr; uint32_t card = 0, dtype = 0;
   };
   std::vector<LutReq> luts;
+  // values-mode leaves (pg_leaf.num_values): each literal list once in the arena per (host pointer, stored type)
+  std::map<std::pair<const void*, uint32_t>, uint64_t> lit_arena;
+  auto literals_off = [&](const pg_leaf& pl, uint32_t dtype) -> uint64_t {
+    auto it = lit_arena.find({pl.values, dtype});
+    if (it != lit_arena.end()) return it->second;
+    const uint32_t n = pl.num_values, w = dtype == PG_INT || dtype == PG_FLOAT ? 4 : 8;
+    const uint64_t at = ar.reserve((uint64_t)w * n);
+    for (uint32_t i = 0; i < n; i++) {
+      uint8_t* dst = &ar.h[at + (uint64_t)w * i];
+      if (dtype == PG_INT) { const int32_t v = (int32_t)((const int64_t*)pl.values)[i]; memcpy(dst, &v, 4); }
+      else if (dtype == PG_LONG) memcpy(dst, (const int64_t*)pl.values + i, 8);
+      else if (dtype == PG_FLOAT) { const float v = (float)((const double*)pl.values)[i]; memcpy(dst, &v, 4); }
+      else memcpy(dst, (const double*)pl.values + i, 8);
+    }
+    lit_arena[{pl.values, dtype}] = at;
+    return at;
+  };
+  auto lut_req = [&](const pg_leaf& pl, const ColumnRes* c, uint64_t lut_off, uint64_t region_off, uint32_t shift) {
+    LutReq r;
+    r.lut_off = lut_off;
+    r.region_off = region_off;
+    r.shift = shift;
+    if (pl.ids) {
+      r.ids_off = ar.put(pl.ids, 4ull * pl.num_ids);
+      r.n = pl.num_ids;
+    } else {  // values mode: the device finds the literals' dictIds
+      r.ids_off = ~0ull;
+      r.vals_off = literals_off(pl, c->dtype);
+      r.n = pl.num_values;
+      r.dict = c->dict.p;
+      r.card = c->card;
+      r.dtype = c->dtype;
+    }
+    luts.push_back(r);
+  };
   uint64_t scratch_bytes = 0;
   auto scratch_reserve = [&](uint64_t n) { uint64_t at = (scratch_bytes + 255) & ~255ull; scratch_bytes = at + n; return at; };
   uint64_t entries_in_filter = 0;
@@ -1817,8 +1853,13 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         dl.hi = std::max(pl.hi, pl.lo);
         continue;
       }
-      if (pl.num_ids && !pl.ids) return fail(PG_E_INVALID, "leaf %u: null id list", li);
-      if (!ids_valid(pl.ids, pl.num_ids, std::max(c->card, 1u)))
+      // values mode (pg_leaf.num_values): the literals themselves, for SV / MV scans over a resident dictionary
+      const bool vmode = pl.num_ids && !pl.ids && pl.num_values;
+      if (vmode && (!pl.values || (pl.kind != PG_LEAF_SV_SCAN && pl.kind != PG_LEAF_MV_SCAN) || !c->has_dict ||
+                    !c->dict.p || c->dtype > PG_DOUBLE))
+        return fail(PG_E_INVALID, "leaf %u: literal values need an SV / MV scan over a numeric dictionary", li);
+      if (pl.num_ids && !pl.ids && !vmode) return fail(PG_E_INVALID, "leaf %u: null id list", li);
+      if (!vmode && !ids_valid(pl.ids, pl.num_ids, std::max(c->card, 1u)))
         return fail(PG_E_INVALID, "leaf %u: dictIds must be sorted, unique and < cardinality", li);
       auto in_set = [&](int32_t id) {
         if (!pl.num_ids) return id >= pl.lo && id < pl.hi;
@@ -1832,7 +1873,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
           dl.wbytes = (uint32_t)std::min<uint64_t>(c->words.bytes, 0xFFFFFFF0ull);
           dl.bits = c->bits;
           if (!index_leaf[(uint64_t)si * L + li]) entries_in_filter += sr.num_docs;
-          const bool contiguous = pl.num_ids && (uint32_t)(pl.ids[pl.num_ids - 1] - pl.ids[0]) + 1 == pl.num_ids;
+          const bool contiguous = !vmode && pl.num_ids && (uint32_t)(pl.ids[pl.num_ids - 1] - pl.ids[0]) + 1 == pl.num_ids;
           if (!pl.num_ids || contiguous) {
             dl.kind = LK_RANGE;
             const int32_t lo = pl.num_ids ? pl.ids[0] : pl.lo, hi = pl.num_ids ? pl.ids[pl.num_ids - 1] + 1 : pl.hi;
@@ -1846,13 +1887,13 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
             // filter bitmap (and, when shift > 0, the exact LUT resolving its candidates) built on the device
             const uint64_t region_off = scratch_reserve(4ull * n_region);
             const uint64_t lut_off = dl.shift ? scratch_reserve(4ull * ((c->card + 31) / 32 + 1)) : ~0ull;
-            luts.push_back({ar.put(pl.ids, 4ull * pl.num_ids), pl.num_ids, lut_off, region_off, dl.shift});
+            lut_req(pl, c, lut_off, region_off, dl.shift);
             patches.push_back({(uint64_t)si * L + li, region_off, false, PT_AUX});
             if (dl.shift) patches.push_back({(uint64_t)si * L + li, lut_off, false, PT_LUT});
           } else {
             dl.kind = LK_SET_LUT;
             const uint64_t lut_off = scratch_reserve(4ull * ((c->card + 31) / 32 + 1));
-            luts.push_back({ar.put(pl.ids, 4ull * pl.num_ids), pl.num_ids, lut_off});
+            lut_req(pl, c, lut_off, ~0ull, 0);
             patches.push_back({(uint64_t)si * L + li, lut_off, false, PT_AUX});
           }
           break;
@@ -1942,7 +1983,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
           op.hi = pl.hi;
           if (pl.num_ids) {
             op.lut_off = scratch_reserve(4ull * ((c->card + 31) / 32 + 1));
-            luts.push_back({ar.put(pl.ids, 4ull * pl.num_ids), pl.num_ids, op.lut_off});
+            lut_req(pl, c, op.lut_off, ~0ull, 0);
           }
           op.out_off = scratch_reserve(4ull * ((sr.num_docs + 31) / 32 + 1));
           patches.push_back({(uint64_t)si * L + li, op.out_off, false, PT_WORDS});
@@ -2637,9 +2678,11 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   }
   std::vector<LutJob> lutjobs(luts.size());
   for (size_t i = 0; i < luts.size(); i++)
-    lutjobs[i] = {(const int32_t*)(dA + luts[i].ids_off),
+    lutjobs[i] = {luts[i].ids_off == ~0ull ? nullptr : (const int32_t*)(dA + luts[i].ids_off),
                   luts[i].lut_off == ~0ull ? nullptr : (uint32_t*)(dS + luts[i].lut_off),
-                  luts[i].region_off == ~0ull ? nullptr : (uint32_t*)(dS + luts[i].region_off), luts[i].n, luts[i].shift};
+                  luts[i].region_off == ~0ull ? nullptr : (uint32_t*)(dS + luts[i].region_off), luts[i].n, luts[i].shift,
+                  luts[i].vals_off == ~0ull ? nullptr : (const void*)(dA + luts[i].vals_off), luts[i].dict,
+                  luts[i].card, luts[i].dtype};
   if (!leaves.empty()) memcpy(&ar.h[off_leaves], leaves.data(), leaves.size() * sizeof(LeafDesc));
   if (!aggcols.empty()) memcpy(&ar.h[off_aggcols], aggcols.data(), aggcols.size() * sizeof(ColDesc));
   if (!keycols.empty()) memcpy(&ar.h[off_keycols], keycols.data(), keycols.size() * sizeof(ColDesc));
@@ -2680,7 +2723,11 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   HIP_CHECK(hipMemcpyAsync(arena.p, staging, ar.h.size(), hipMemcpyHostToDevice, s));
   HIP_CHECK(hipEventRecord(ev[0], s));
   if (scratch_bytes) HIP_CHECK(hipMemsetAsync(scratch.p, 0, scratch_bytes, s));
-  HIP_CHECK(launch_set_lut_bits((const LutJob*)(dA + off_lutjobs), (uint32_t)lutjobs.size(), s));
+  {
+    uint32_t max_n = 0;
+    for (const LutReq& r : luts) max_n = std::max(max_n, r.n);
+    HIP_CHECK(launch_set_lut_bits((const LutJob*)(dA + off_lutjobs), (uint32_t)lutjobs.size(), max_n, s));
+  }
   for (const PrepassOp& op : pre) {
     switch (op.kind) {
       case PrepassOp::FILL_RANGES:

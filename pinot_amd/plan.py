@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes as C
 import itertools
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -31,6 +32,8 @@ MAX_VALUE_OFFSET_KEYS = 1 << 26   # integer key ranges up to this size may use v
 VALUE_OFFSET_DENSITY = 4          # ... when the range is at most this many times the largest segment cardinality
 DEFAULT_NUM_GROUPS_LIMIT = 100_000          # InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT
 DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY = 10_000  # InstancePlanMakerImplV2 :73
+# batched IN / NOT_IN leaves cross as their literals (values mode, pg_leaf.num_values) unless PG_IN_VALUES=0 (ids)
+_IN_VALUES = os.environ.get("PG_IN_VALUES", "1") != "0"
 
 
 class UnsupportedQuery(Exception):
@@ -539,6 +542,7 @@ class CPlan:
         seg_arr = (abi.pg_segment_ref * max(S, 1))()
         self.lowered: List[List[LoweredLeaf]] = []
         batch = self._batched_in_ids(preds, segments, seg_keys, cid, id_sets) if id_sets is not None and S > 1 else {}
+        self._keep.extend(b[2] for b in batch.values())  # the literal arrays values-mode leaves point to
         for si, (seg, key) in enumerate(zip(segments, seg_keys)):
             leaves = (abi.pg_leaf * max(L, 1))()
             lows = []
@@ -556,9 +560,16 @@ class CPlan:
                 leaves[li].hi = lw.hi
                 if lw.ids is not None and len(lw.ids):
                     arr = np.ascontiguousarray(lw.ids, dtype=np.int32)
-                    self._keep.append(arr)
                     leaves[li].num_ids = len(arr)
-                    leaves[li].ids = arr.ctypes.data_as(C.POINTER(C.c_int32))
+                    if b is not None and _IN_VALUES and lw.kind in (abi.PG_LEAF_SV_SCAN, abi.PG_LEAF_MV_SCAN) and \
+                            int(arr[-1]) - int(arr[0]) + 1 != len(arr):
+                        # values mode: the predicate's literals (one array for every segment); the device finds their
+                        # dictIds in the resident dictionary (a contiguous id set still crosses as ids: a RANGE leaf)
+                        leaves[li].values = b[2].ctypes.data
+                        leaves[li].num_values = len(b[2])
+                    else:
+                        self._keep.append(arr)
+                        leaves[li].ids = arr.ctypes.data_as(C.POINTER(C.c_int32))
                 if lw.raw is not None:
                     r = lw.raw
                     if "values" in r:  # int64 for INT / LONG columns, float64 for FLOAT / DOUBLE
@@ -649,9 +660,9 @@ class CPlan:
 
     @staticmethod
     def _batched_in_ids(preds, segments, seg_keys, cid, id_sets) -> dict:
-        """{leaf: (ids [S, n], counts [S])} for the IN / NOT_IN leaves over numeric dictionaries of one stored type in
-        every segment: the literals are coerced once (the first segment's dictionary type) and looked up in all
-        segments by one id_sets call."""
+        """{leaf: (ids [S, n], counts [S], literals widened to int64 / float64)} for the IN / NOT_IN leaves over numeric
+        dictionaries of one stored type in every segment: the literals are coerced once (the first segment's dictionary
+        type) and looked up in all segments by one id_sets call."""
         out = {}
         for li, p in enumerate(preds):
             if p.type not in ("IN", "NOT_IN"):
@@ -667,5 +678,7 @@ class CPlan:
             lit = _coerced_literals(d0, p.values)
             if lit is None:
                 continue
-            out[li] = id_sets(cid[p.column], d0.data_type, np.ascontiguousarray(lit), seg_keys)
+            ids, counts = id_sets(cid[p.column], d0.data_type, np.ascontiguousarray(lit), seg_keys)
+            wide = np.ascontiguousarray(lit, dtype=np.int64 if d0.data_type in ("INT", "LONG") else np.float64)
+            out[li] = (ids, counts, wide)
         return out

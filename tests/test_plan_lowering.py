@@ -58,6 +58,13 @@ def test_batched_in_lowering_matches_per_segment(dtype):
                 assert (a.ids is None) == (b.ids is None)
                 if a.ids is not None:
                     assert np.array_equal(np.asarray(a.ids, dtype=np.int32), np.asarray(b.ids, dtype=np.int32))
+        # values mode on the C side: a non-contiguous IN / NOT_IN set crosses as the literals (ids left to the device)
+        for si in range(len(segs)):
+            leaf = batched.plan.segments[si].leaves[0]
+            if leaf.num_ids and leaf.kind in (abi.PG_LEAF_SV_SCAN, abi.PG_LEAF_MV_SCAN):
+                ids = batched.lowered[si][0].ids
+                contiguous = int(ids[-1]) - int(ids[0]) + 1 == len(ids)
+                assert bool(leaf.ids) == contiguous and (leaf.num_values > 0) != contiguous
     assert calls and all(c[1] == dtype for c in calls)
 
 
