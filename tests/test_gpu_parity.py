@@ -360,6 +360,25 @@ def test_dict_id_sets_on_device(dtype, gpu_engine, oracle_engine):
         assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q), table=t)
 
 
+def test_in_literals_on_mv_scan_leaves(gpu_engine, oracle_engine):
+    """IN / NOT_IN over an MV column without an inverted index, several segments: the leaves cross as their literals
+    (values mode) and the device finds each segment's dictIds while it builds the MV scan's LUT."""
+    rng = np.random.default_rng(11)
+    segs = []
+    for s in range(3):
+        n = 20_000 + 1_000 * s
+        data = {"tags": [list(rng.integers(0, 400 + 50 * s, rng.integers(1, 6))) for _ in range(n)],
+                "m": rng.integers(0, 30, n)}
+        segs.append(_seg(f"mv{s}", data, {"tags": "INT", "m": "INT"}))
+    t = Table("t", segs)
+    lits = ", ".join(str(x) for x in range(3, 420, 7))
+    for sql in [f"SELECT COUNT(*), COUNTMV(tags) FROM t WHERE tags IN ({lits})",
+                f"SELECT m, COUNT(*) FROM t WHERE tags NOT IN ({lits}) GROUP BY m",
+                f"SELECT COUNT(*) FROM t WHERE tags IN ({lits}) AND m < 10"]:
+        q = parse(sql)
+        assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q), table=t)
+
+
 def test_partial_rows_export_merge_roundtrip(gpu_engine, oracle_engine, sv_table_inter):
     """pg_partials_export (rows bucketed by owner) -> pg_partials_create + pg_partials_merge of every bucket ->
     finalize == the direct result, for a dense and a hash state."""
