@@ -73,42 +73,52 @@ def _all_gather_ints(vals, group, device):
 
 def merge_partials_across_ranks(engine, plan, p, group=None) -> IntermediateResult:
     """pg_execute_partial result `p` (this rank) -> merged over the process group -> finalized result (every rank
-    returns the same merged result).  Consumes `p`."""
+    returns the same merged result).  Consumes `p`.
+
+    Dense states take one collective per query step when they carry only SUMs (config 2): the i64 state and the six
+    statistics travel in ONE buffer (both SUM); MIN / MAX / f64 states add one all-reduce each.  The state layouts are
+    checked across ranks once per plan (they are a function of the plan) rather than every step."""
     import torch
     import torch.distributed as dist
     from .gpu import check
     pc = p.contents
     dev = torch.device("cuda", torch.cuda.current_device())
-    world = dist.get_world_size(group)
-    layouts = _all_gather_ints([pc.mode, pc.num_slots, pc.n_i64, pc.n_f64, pc.n_min, pc.n_max, pc.bitmap_words,
-                                pc.layout], group, dev)
-    if any(l[2:] != layouts[0][2:] for l in layouts):
-        engine.lib.pg_partials_free(p)
-        raise ValueError(f"partial state layouts differ across ranks: {layouts} (plan with PG_PLAN_F64_SUMS)")
-    stats = torch.tensor([getattr(pc.stats, f) for f in _STATS_FIELDS], dtype=torch.int64, device=dev)
-    dense_ok = all(l[0] == abi.PG_STATE_DENSE and l[1] == layouts[0][1] for l in layouts) and pc.bitmap_words == 0 \
-        and pc.num_slots * 8 * (pc.n_i64 + pc.n_f64 + pc.n_min + pc.n_max) <= DENSE_ALLREDUCE_MAX_BYTES
-    if dense_ok:
-        n = pc.num_slots
-        state = {
-            "i64": torch.empty(n * pc.n_i64, dtype=torch.int64, device=dev),
-            "f64": torch.empty(n * pc.n_f64, dtype=torch.float64, device=dev),
-            "mn": torch.empty(n * pc.n_min, dtype=torch.int64, device=dev),
-            "mx": torch.empty(n * pc.n_max, dtype=torch.int64, device=dev),
-            "stats": stats,
-        }
-        ptr = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None
+    mine = [pc.mode, pc.num_slots, pc.n_i64, pc.n_f64, pc.n_min, pc.n_max, pc.bitmap_words, pc.layout]
+    checked = getattr(plan, "_rank_layouts", None)
+    if checked is None or checked[0] != mine:
+        layouts = _all_gather_ints(mine, group, dev)
+        if any(l[2:] != layouts[0][2:] for l in layouts):
+            engine.lib.pg_partials_free(p)
+            raise ValueError(f"partial state layouts differ across ranks: {layouts} (plan with PG_PLAN_F64_SUMS)")
+        dense_all = all(l[0] == abi.PG_STATE_DENSE and l[1] == layouts[0][1] for l in layouts)
+        plan._rank_layouts = (mine, dense_all)
+    dense_all = plan._rank_layouts[1]
+    st_host = [getattr(pc.stats, f) for f in _STATS_FIELDS]
+    dense_ok = dense_all and pc.bitmap_words == 0 and \
+        pc.num_slots * 8 * (pc.n_i64 + pc.n_f64 + pc.n_min + pc.n_max) <= DENSE_ALLREDUCE_MAX_BYTES
+    if not dense_ok:
+        return _exchange_rows(engine, plan, p, torch.tensor(st_host, dtype=torch.int64, device=dev), group, dev)
+    n = pc.num_slots
+    ni = n * pc.n_i64
+    sums = torch.empty(ni + len(_STATS_FIELDS), dtype=torch.int64, device=dev)  # i64 state | statistics: one SUM
+    sums[ni:].copy_(torch.tensor(st_host, dtype=torch.int64), non_blocking=False)
+    state = {"i64": sums[:ni],
+             "f64": torch.empty(n * pc.n_f64, dtype=torch.float64, device=dev),
+             "mn": torch.empty(n * pc.n_min, dtype=torch.int64, device=dev),
+             "mx": torch.empty(n * pc.n_max, dtype=torch.int64, device=dev)}
+    ptr = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None
+    # the library's copies run on its own stream (torch carries its own HIP runtime, so streams do not cross) and
+    # return once done; the statistics' read-back after the collectives is the one host synchronisation between
+    check(engine.lib.pg_partials_copy(p, abi.PG_COPY_OUT, ptr(state["i64"]), ptr(state["f64"]), ptr(state["mn"]),
+                                      ptr(state["mx"]), None))
+    allreduce_state({"i64": sums, "f64": state["f64"], "mn": state["mn"], "mx": state["mx"]}, group)
+    for f, v in zip(_STATS_FIELDS, sums[ni:].cpu().tolist()):  # waits for the collectives
+        setattr(pc.stats, f, int(v))
+    if state["f64"].numel() or state["mn"].numel() or state["mx"].numel():
         torch.cuda.synchronize()
-        check(engine.lib.pg_partials_copy(p, abi.PG_COPY_OUT, ptr(state["i64"]), ptr(state["f64"]), ptr(state["mn"]),
-                                          ptr(state["mx"]), None))
-        allreduce_state(state, group)
-        torch.cuda.synchronize()
-        check(engine.lib.pg_partials_copy(p, abi.PG_COPY_IN, ptr(state["i64"]), ptr(state["f64"]), ptr(state["mn"]),
-                                          ptr(state["mx"]), None))
-        for f, v in zip(_STATS_FIELDS, state["stats"].cpu().tolist()):
-            setattr(pc.stats, f, int(v))
-        return engine.finalize_partial(plan, p)
-    return _exchange_rows(engine, plan, p, stats, group, dev)
+    check(engine.lib.pg_partials_copy(p, abi.PG_COPY_IN, ptr(state["i64"]), ptr(state["f64"]), ptr(state["mn"]),
+                                      ptr(state["mx"]), None))
+    return engine.finalize_partial(plan, p)
 
 
 def _agree(err, group, dev):
