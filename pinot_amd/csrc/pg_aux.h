@@ -241,6 +241,8 @@ size_t sort_temp_bytes(uint64_t n, uint32_t begin_bit = 0, uint32_t end_bit = 64
 uint64_t row_bytes(const StateView& v);
 hipError_t launch_select_slots(const StateView& v, uint32_t kind, uint32_t part, uint32_t parts, uint32_t* out,
                                uint32_t* d_num, void* temp, size_t temp_bytes, hipStream_t s);
+// The present slots of a state in no particular order (one pass, one atomic per wave): count must be zeroed
+hipError_t launch_select_present_unordered(const StateView& v, uint32_t* out, unsigned int* count, hipStream_t s);
 hipError_t launch_select_flagged(const uint32_t* in, const uint8_t* flags, uint64_t n, uint32_t* out, uint32_t* d_num,
                                  void* temp, size_t temp_bytes, hipStream_t s);
 hipError_t launch_exclusive_sum(const uint64_t* in, uint64_t* out, uint64_t n, void* temp, size_t temp_bytes,

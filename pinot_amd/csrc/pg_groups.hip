@@ -62,6 +62,52 @@ hipError_t launch_select_slots(const StateView& v, uint32_t kind, uint32_t part,
                                   s);
 }
 
+// Present slots of a large state in block-chunk order (order inside the output is irrelevant to the trim that
+// consumes it). Each block owns one contiguous chunk: it counts its present slots, reserves its output range with ONE
+// global atomic, then writes the chunk again in slot order. (A per-wave atomic on the single counter serialised 156K
+// atomics at L2 for 10M slots: 1.8 ms; hipcub's ordered select is 0.17 ms.)
+__global__ void __launch_bounds__(256) select_present_unordered_kernel(StateView v, uint32_t* __restrict__ out,
+                                                                       unsigned int* __restrict__ count,
+                                                                       uint32_t chunk) {
+  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t base_s;
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint64_t lo = (uint64_t)blockIdx.x * chunk;
+  const uint64_t hi = std::min<uint64_t>(lo + chunk, v.num_slots);
+  uint32_t mine = 0;
+  for (uint64_t s = lo + threadIdx.x; s < hi; s += 256) mine += present(v, s) ? 1u : 0u;
+  for (int o = 32; o; o >>= 1) mine += __shfl_xor(mine, o);
+  if (lane == 0) wsum[w] = mine;
+  __syncthreads();
+  if (threadIdx.x == 0) base_s = atomicAdd(count, wsum[0] + wsum[1] + wsum[2] + wsum[3]);
+  __syncthreads();
+  uint32_t run = base_s;
+  for (uint64_t t = lo; t < hi; t += 256) {
+    const uint64_t s = t + threadIdx.x;
+    const bool take = s < hi && present(v, s);
+    const uint64_t m = __ballot(take);
+    __syncthreads();  // wsum of the previous tile fully read
+    if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+    for (uint32_t i = 0; i < 4; ++i) {
+      pre += i < w ? wsum[i] : 0u;
+      tot += wsum[i];
+    }
+    if (take) out[run + pre + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)s;
+    run += tot;
+  }
+}
+
+hipError_t launch_select_present_unordered(const StateView& v, uint32_t* out, unsigned int* count, hipStream_t s) {
+  const uint64_t tiles = (v.num_slots + 255) / 256;
+  const uint64_t per = std::max<uint64_t>((tiles + 2047) / 2048, 1);  // ≤2048 blocks: ≤2048 atomics on the counter
+  const uint64_t blocks = std::max<uint64_t>((tiles + per - 1) / per, 1);
+  hipLaunchKernelGGL(select_present_unordered_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, v, out, count,
+                     (uint32_t)(per * 256));
+  return hipGetLastError();
+}
+
 hipError_t launch_select_flagged(const uint32_t* in, const uint8_t* flags, uint64_t n, uint32_t* out, uint32_t* d_num,
                                  void* temp, size_t temp_bytes, hipStream_t s) {
   return hipcub::DeviceSelect::Flagged(temp, temp_bytes, in, flags, out, d_num, (int)n, s);

@@ -2823,7 +2823,9 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       }
     }
     const bool modes_ok = (kmode == 0 || kmode == 1) && (vmode >= -1 && vmode <= 1);
-    const bool spec = match_all && allow_spec && K == 1 && modes_ok && !(spec_env && atoi(spec_env) == 0);
+    // (at least 16 level-1 partitions: fixed-capacity regions of 32-bit fill counters stay far below 2^32 entries)
+    const bool spec = match_all && allow_spec && K == 1 && modes_ok && part.nparts1 >= 16 &&
+                      !(spec_env && atoi(spec_env) == 0);
     // PG_PART_DIRECT=1: the histogram + scatter form of level 1 from the columns (exact offsets; measured slower)
     const bool direct = !spec && match_all && getenv("PG_PART_DIRECT") && atoi(getenv("PG_PART_DIRECT")) == 1;
     const uint64_t n1 = (uint64_t)part.nparts1 * blocks, n2 = (uint64_t)part.nparts1 * part.nparts2 * kPartNB;
@@ -3439,10 +3441,18 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   if (single) {
     HIP_CHECK(hipMemsetAsync(slots, 0, 4, s));
   } else {
-    const size_t tb = select_temp_bytes(P.num_slots);
-    void* temp = sc.get<uint8_t>(tb, rc);
-    if (rc) return rc;
-    HIP_CHECK(launch_select_slots(v, SEL_PRESENT, 0, 1, slots, d_num, temp, tb, s));
+    // an ORDER BY trim re-orders the candidates anyway (build_result): a large state's present slots may come in any
+    // order, by one pass with a wave-aggregated append instead of the ordered (two-pass) select
+    const bool trims = K && plan->num_order && plan->limit && P.num_slots >= kTrimSelectMinGroups;
+    if (trims) {
+      HIP_CHECK(hipMemsetAsync(d_num, 0, 4, s));
+      HIP_CHECK(launch_select_present_unordered(v, slots, (unsigned int*)d_num, s));
+    } else {
+      const size_t tb = select_temp_bytes(P.num_slots);
+      void* temp = sc.get<uint8_t>(tb, rc);
+      if (rc) return rc;
+      HIP_CHECK(launch_select_slots(v, SEL_PRESENT, 0, 1, slots, d_num, temp, tb, s));
+    }
     uint32_t n32 = 0;
     if ((rc = read_back(d_num, n32, s))) return rc;
     n = n32;
