@@ -258,6 +258,7 @@ hipError_t launch_order_keys(const FinalSpec& f, const uint64_t* keys, const dou
 // ORDER BY trim by radix select (pg_groups.hip): histogram of key bits [lo, hi) of k' = (key >> b0) & (2^W - 1) over the
 // keys whose k' >> hi equals prefix (hist: 256 counters, zeroed by the caller); then the positions of every key with
 // k' <= tstar (count: zeroed by the caller)
+constexpr uint32_t kOkeyDigitBits = 11;  // radix-select digit width: config 4's 21 differing bits in 2 passes, not 3
 hipError_t launch_okey_hist(const uint64_t* keys, uint64_t n, uint32_t b0, uint32_t W, uint32_t lo, uint32_t hi,
                             uint64_t prefix, unsigned int* hist, hipStream_t s);
 hipError_t launch_okey_select(const uint64_t* keys, uint64_t n, uint32_t b0, uint32_t W, uint64_t tstar, uint32_t* pos,

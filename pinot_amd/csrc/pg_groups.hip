@@ -313,7 +313,7 @@ hipError_t launch_cutoff(const uint64_t* sorted, uint64_t n, uint64_t limit, uin
 
 // ---- ORDER BY trim by radix select (instead of sorting every group): in the key space k' = (okey >> b0) & (2^W - 1)
 // (the only bits in which the order keys differ, order_keys_kernel's span), the limit-th smallest k' is found digit by
-// digit from the top: per pass a histogram of one <= 8-bit digit over the keys whose higher digits equal the prefix
+// digit from the top: per pass a histogram of one <= kOkeyDigitBits-bit digit over the keys whose higher digits equal the prefix
 // chosen so far.  The candidates are then every key <= that value (the sorted cutoff's set: ties at the boundary
 // kept), compacted into a position list.
 __device__ __forceinline__ uint64_t kprime(uint64_t k, uint32_t b0, uint32_t W) {
@@ -323,9 +323,9 @@ __device__ __forceinline__ uint64_t kprime(uint64_t k, uint32_t b0, uint32_t W) 
 
 __global__ void okey_hist_kernel(const uint64_t* __restrict__ keys, uint64_t n, uint32_t b0, uint32_t W, uint32_t lo,
                                  uint32_t hi, uint64_t prefix, unsigned int* __restrict__ hist) {
-  __shared__ unsigned int h[256];
-  const uint32_t tid = threadIdx.x;
-  h[tid] = 0;
+  __shared__ unsigned int h[1u << kOkeyDigitBits];
+  const uint32_t tid = threadIdx.x, nd = 1u << (hi - lo);
+  for (uint32_t d = tid; d < nd; d += blockDim.x) h[d] = 0;
   __syncthreads();
   const uint64_t dmask = (1ull << (hi - lo)) - 1ull;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -334,7 +334,8 @@ __global__ void okey_hist_kernel(const uint64_t* __restrict__ keys, uint64_t n, 
     if (hi >= 64 || (k >> hi) == prefix) atomicAdd(&h[(k >> lo) & dmask], 1u);
   }
   __syncthreads();
-  if (h[tid]) atomicAdd(&hist[tid], h[tid]);
+  for (uint32_t d = tid; d < nd; d += blockDim.x)
+    if (h[d]) atomicAdd(&hist[d], h[d]);
 }
 
 __global__ void okey_select_kernel(const uint64_t* __restrict__ keys, uint64_t n, uint32_t b0, uint32_t W,

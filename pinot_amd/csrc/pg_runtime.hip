@@ -1580,7 +1580,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     if (ok) {
       auto clog2 = [](uint64_t x) { uint32_t b = 0; while ((1ull << b) < x) b++; return b; };
       const uint32_t gbits = clog2(G);
-      part.shift1 = gbits > 8 ? gbits - 8 : 0;
+      static const uint32_t l1_bits = getenv("PG_PART_L1_BITS") ? (uint32_t)std::min(std::max(atoi(getenv("PG_PART_L1_BITS")), 1), 8) : 8u;
+      part.shift1 = gbits > l1_bits ? gbits - l1_bits : 0;
       part.vbits = dc == (uint32_t)kNoSlot ? 0 : clog2(P.aggs[dc].key_card);
       part.dc_words = dc == (uint32_t)kNoSlot ? 0 : (P.aggs[dc].key_card + 31) / 32;
       const uint64_t per_group = 4ull * (1 + part.dc_words);
@@ -3490,16 +3491,18 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
       // radix select of the limit-th smallest key (a histogram readback per <= 8-bit digit of the differing bits),
       // then the positions of every key up to it: no sort of all n groups
       const uint32_t W = b1 - b0;
-      unsigned int* hist = sc.get<unsigned int>(256, rc);
-      unsigned int* hh = (unsigned int*)t_ctx.readback.get(1024);
+      constexpr uint32_t kHB = 4u << kOkeyDigitBits;  // histogram bytes of the widest digit
+      unsigned int* hist = sc.get<unsigned int>(kHB / 4, rc);
+      unsigned int* hh = (unsigned int*)t_ctx.readback.get(kHB);
       if (rc) return rc;
       if (!hh) return fail(PG_E_NOMEM, "pinned readback failed");
       uint64_t need = plan->limit, prefix = 0;
       for (uint32_t hi = W; hi > 0;) {
-        const uint32_t lo = hi > 8 ? hi - 8 : 0;
-        HIP_CHECK(hipMemsetAsync(hist, 0, 1024, s));
+        const uint32_t lo = hi > kOkeyDigitBits ? hi - kOkeyDigitBits : 0;
+        const size_t hb = 4ull << (hi - lo);
+        HIP_CHECK(hipMemsetAsync(hist, 0, hb, s));
         HIP_CHECK(launch_okey_hist(okeys, n, b0, W, lo, hi, prefix, hist, s));
-        HIP_CHECK(hipMemcpyAsync(hh, hist, 1024, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipMemcpyAsync(hh, hist, hb, hipMemcpyDeviceToHost, s));
         HIP_CHECK(hipStreamSynchronize(s));
         uint64_t cum = 0;
         uint32_t d = 0;
