@@ -23,6 +23,11 @@ hipError_t launch_dict_bits(const void* dict, uint32_t dtype, uint32_t card, int
 hipError_t launch_mv_offsets(const uint32_t* bitmap_words, uint64_t num_values, uint32_t num_docs,
                              uint32_t* offsets, void* scratch, size_t scratch_bytes, hipStream_t s);
 size_t mv_offsets_scratch_bytes(uint64_t num_values);
+// The per-query parameter arena read by the device straight from its pinned (fine-grained, mapped) host image, and
+// the query's scratch zeroed, in ONE launch on the query stream (instead of an SDMA copy, whose completion the compute
+// queue waits on, plus a fill).
+hipError_t launch_arena_upload(const void* host_src, void* dst, uint64_t bytes, void* zero, uint64_t zero_bytes,
+                               hipStream_t s);
 hipError_t launch_fill_ranges(const int32_t* ranges /*[n][2] inclusive, sorted, disjoint*/, uint32_t n,
                               uint32_t num_docs, uint32_t* bitmap, hipStream_t s);
 struct RoaringContainer {

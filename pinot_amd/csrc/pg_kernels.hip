@@ -577,4 +577,27 @@ hipError_t launch_dict_lookup(const DictLookupJob* jobs, uint32_t num_segments, 
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------ parameter arena upload
+
+__global__ void __launch_bounds__(256) arena_upload_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                          uint64_t n16, uint8_t* __restrict__ z, uint64_t zbytes) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint64_t i = t; i < n16; i += stride) dst[i] = src[i];
+  const uint64_t z16 = zbytes / 16;
+  for (uint64_t i = t; i < z16; i += stride) ((uint4*)z)[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (uint64_t i = z16 * 16 + t; i < zbytes; i += stride) z[i] = 0;
+}
+
+hipError_t launch_arena_upload(const void* host_src, void* dst, uint64_t bytes, void* zero, uint64_t zero_bytes,
+                               hipStream_t s) {
+  // the source is read in whole 16-byte units: the pinned image's capacity is a multiple of 16 covering them
+  const uint64_t n16 = (bytes + 15) / 16, units = std::max<uint64_t>(n16, (zero_bytes + 15) / 16);
+  if (!units) return hipSuccess;
+  const uint64_t blocks = std::min<uint64_t>((units + 255) / 256, 1024);
+  hipLaunchKernelGGL(arena_upload_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, (const uint4*)host_src, (uint4*)dst,
+                     n16, (uint8_t*)zero, zero_bytes);
+  return hipGetLastError();
+}
+
 }  // namespace pg

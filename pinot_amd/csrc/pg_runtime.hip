@@ -216,6 +216,7 @@ struct PinnedBuf {
 // copied to the device from it (no staging memcpy).
 struct PinnedVec {
   uint8_t* p = nullptr;
+  void* dp = nullptr;  // the device's address of p
   uint64_t n = 0, cap = 0;
   ~PinnedVec() {
     if (p) (void)hipHostFree(p);
@@ -229,10 +230,17 @@ struct PinnedVec {
       uint64_t c = cap ? cap : 4096;
       while (c < m) c <<= 1;
       void* q = nullptr;
-      if (hipHostMalloc(&q, c, hipHostMallocDefault) != hipSuccess || !q) throw std::bad_alloc();
+      // fine-grained and mapped: the device reads it directly (launch_arena_upload), never a stale cached line
+      if (hipHostMalloc(&q, c, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess || !q) throw std::bad_alloc();
+      void* d = nullptr;
+      if (hipHostGetDevicePointer(&d, q, 0) != hipSuccess || !d) {
+        (void)hipHostFree(q);
+        throw std::bad_alloc();
+      }
       if (n) memcpy(q, p, n);
       if (p) (void)hipHostFree(p);
       p = (uint8_t*)q;
+      dp = d;
       cap = c;
     }
     n = m;
@@ -2718,12 +2726,11 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   q.segs = (const SegDesc*)(dA + off_segs);
   q.items = (const WorkItem*)(dA + off_items);
 
-  void* staging = ar.h.data();  // the arena is built in pinned memory: copied from where it was written
   hipEvent_t* ev = t_ctx.ev;
   PG_PROF("arena");
-  HIP_CHECK(hipMemcpyAsync(arena.p, staging, ar.h.size(), hipMemcpyHostToDevice, s));
+  // the arena was built in pinned memory: the device reads it from there
+  HIP_CHECK(launch_arena_upload(ar.h.dp, arena.p, ar.h.size(), scratch.p, scratch_bytes, s));
   HIP_CHECK(hipEventRecord(ev[0], s));
-  if (scratch_bytes) HIP_CHECK(hipMemsetAsync(scratch.p, 0, scratch_bytes, s));
   {
     uint32_t max_n = 0;
     for (const LutReq& r : luts) max_n = std::max(max_n, r.n);

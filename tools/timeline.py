@@ -13,6 +13,10 @@ rows = []
 for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
     with open(f) as fh:
         rows += [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in csv.DictReader(fh)]
+for f in glob.glob(f"{d}/**/*memory_copy_trace.csv", recursive=True):  # with --memory-copy-trace
+    with open(f) as fh:
+        rows += [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                  "copy " + r.get("Direction", "?") + " " + r.get("Size", r.get("Bytes", ""))) for r in csv.DictReader(fh)]
 rows.sort()
 rows = rows[-n:]
 t0, prev = rows[0][0], rows[0][0]
