@@ -8,7 +8,10 @@ Workloads (`--workload`; the default is the headline metric):
   ssb          config 3: SSB Q1.1 shape, SUM(lo_extendedprice * lo_discount) under 3 dictionary filters -- 96 segments
                per GPU (768 over 8 GPUs = 6 B rows)
   highcard     config 4: SELECT userId, DISTINCTCOUNT(itemId) ... GROUP BY userId ORDER BY DISTINCTCOUNT(itemId) DESC,
-               userId LIMIT 100 (10 M users x 1 000 items, numGroupsLimit 10 M) -- 128 segments per GPU
+               userId LIMIT 100 (10 M users x 1 000 items, numGroupsLimit 10 M) -- 128 segments per GPU; the step
+               returns the server's 5 000 top groups (GroupByOrderByCombineOperator's trim size)
+  index        config 5: COUNT(*), COUNTMV(mvTags) under a sorted-index range, an OR of two inverted-index leaves, an
+               inverted NOT_EQ and an inverted IN -- 32 segments per GPU (256 over 8 GPUs = 2 B rows)
 
 Segments are generated on the device (pinot_amd.synth) and resident in HBM before the timed region.  A step = one
 query over all of this GPU's segments: host plan compile + filter pre-pass + fused scan/aggregate kernel + device
@@ -50,14 +53,15 @@ HEADLINE_METRIC = "rows/sec for filter+group-by SUM over 1B rows; % of HBM roofl
 
 
 def workloads(args):
-    """`stages`: the executed plan's read pattern, in evaluation order: (filter the docs passed so far, or None = every
+    """`trim`: "server" = the group-by result a Pinot server returns (GroupByOrderByCombineOperator: the top
+    getTableCapacity(limit, 5 000) groups under the ORDER BY).  `stages`: the executed plan's read pattern, in evaluation order: (filter the docs passed so far, or None = every
     doc; [(column, "ids" | "values")] read for those docs).  "ids" = the packed dictIds; "values" = what an aggregation /
     key reads (the decoded value image of a large non-identity dictionary, else the dictIds)."""
     from pinot_amd import synth
     ids = ", ".join(str((i * 7919 + 13) % 1_000_000) for i in range(args.in_ids))
     return {
         "adanalytics": dict(
-            specs=synth.ADANALYTICS, table="adAnalytics", segments=128, trim=False,
+            specs=synth.ADANALYTICS, table="adAnalytics", segments=128, trim="server",
             query=synth.adanalytics_query(args.in_ids), decoded=("daysSinceEpoch", "clicks", "impressions"),
             metric=HEADLINE_METRIC,
             desc="AdAnalytics config 2: SUM(clicks), SUM(impressions) WHERE daysSinceEpoch BETWEEN (90 of 365 days) "
@@ -76,7 +80,7 @@ def workloads(args):
                     ("lo_orderdate BETWEEN 8035 AND 8399 AND lo_discount BETWEEN 1 AND 3", [("lo_quantity", "ids")]),
                     ("*", [("lo_extendedprice", "values")])]),
         "highcard": dict(
-            specs=synth.HIGHCARD, table="events", segments=128, trim=True,
+            specs=synth.HIGHCARD, table="events", segments=128, trim="server",
             query=synth.highcard_query() + " OPTION(numGroupsLimit=10000000)", decoded=("userId", "itemId"),
             metric="rows/sec for high-cardinality group-by DISTINCTCOUNT (config 4, secondary line)",
             desc="config 4: SELECT userId, DISTINCTCOUNT(itemId) GROUP BY userId (10 M users x 1 000 items) "

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 5
+#define PG_ABI_VERSION 6
 
 typedef enum pg_status {
   PG_OK = 0,
@@ -251,6 +251,13 @@ typedef struct pg_order {
                                     or GPUs whose columns differ in range must merge (pg_partials.layout) */
 #define PG_PLAN_NO_STREAM 0x8u   /* never use the selective stream (a lean kernel over the root AND's first,
                                     selective scan leaf + the fused scan over its survivors); same results */
+#define PG_PLAN_EXACT_LIMIT 0x10u /* keep exactly min(limit, #groups) groups: the first `limit` of the result order
+                                    (ORDER BY items, then ascending key ids, first key first -- the tie-break that
+                                    TableResizer.getTopRecords leaves arbitrary), or without ORDER BY the `limit`
+                                    groups of smallest key ids (an IndexedTable without ORDER BY keeps the first
+                                    `limit` keys it sees, IndexedTable.java:95-103).  The server-side result of
+                                    GroupByOrderByCombineOperator (:79-93, limit = GroupByUtils.getTableCapacity)
+                                    and the per-segment trim of AggregationGroupByOrderByOperator (:118-132). */
 
 typedef struct pg_plan {
   uint32_t abi_version;     /* PG_ABI_VERSION */
@@ -275,7 +282,8 @@ typedef struct pg_plan {
   const pg_order *order;
   uint64_t limit;           /* with num_order > 0: keep the groups that rank within the first `limit` under
                                the ORDER BY (every group tied with the limit-th is kept too, so any tie-break
-                               the caller applies stays exact); 0 = keep all groups */
+                               the caller applies stays exact -- or exactly `limit` with PG_PLAN_EXACT_LIMIT,
+                               which also applies without ORDER BY); 0 = keep all groups */
 } pg_plan;
 
 /* ---------------------------------------------------------------- results */
@@ -314,6 +322,7 @@ typedef struct pg_result {
 
 int pg_execute(const pg_plan *plan, pg_result **out);
 int pg_result_free(pg_result *res);
+
 
 /* ---------------------------------------------------------------- partial state (multi-GPU) */
 
@@ -383,6 +392,68 @@ int pg_partials_create(const pg_partials *like, uint64_t capacity, pg_partials *
 int pg_partials_merge(pg_partials *p, const void *rows, uint64_t n, void *stream);
 /* Owner part of a packed key among num_parts (the bucketing of pg_partials_export). */
 uint32_t pg_key_owner(uint64_t key, uint32_t num_parts);
+
+/* ---------------------------------------------------------------- relocatable plan image (JNI / FFI callers)
+ *
+ * The same plan as ONE self-contained byte buffer whose sub-arrays are byte offsets from the buffer's start instead
+ * of pointers, so a Java GpuPlanMaker (the PlanMaker.makeInstancePlan replacement, plan/maker/PlanMaker.java:42) fills
+ * a direct ByteBuffer (native byte order, 8-byte aligned: ByteBuffer.allocateDirect(n + 8).alignedSlice(8)) with
+ * putInt / putLong and hands its address and length over -- no Unsafe address arithmetic.
+ * Layout (every offset a multiple of the element's alignment, every array inside [0, n); offset 0 = no array):
+ *   pg_image_header at 0
+ *   pg_image_segment[num_segments] at segments_off, each pointing at its pg_image_leaf[num_leaves] (leaves_off)
+ *   int32 ops[num_ops], pg_agg[num_aggs], pg_key[num_keys], pg_order[num_order] at their offsets
+ *   leaf arrays: int32 dictIds[num_ids] at ids_off; 8-byte values at values_off (num_values literals in values mode,
+ *   else num_ids raw values) -- segments may share one array (the same offset).
+ * The image is validated in full before anything runs (PG_E_INVALID names the first bad field); it is borrowed for
+ * the call only.  The library's per-thread stream is used (a JNI caller has no HIP stream to pass). */
+#define PG_IMAGE_MAGIC 0x49504750u /* "PGPI" */
+
+typedef struct pg_image_header {
+  uint32_t magic;           /* PG_IMAGE_MAGIC */
+  uint32_t abi_version;     /* PG_ABI_VERSION */
+  uint64_t image_bytes;     /* the buffer length n */
+  uint32_t num_segments;
+  uint32_t num_leaves;
+  uint32_t num_ops;
+  uint32_t num_aggs;
+  uint32_t num_keys;
+  uint32_t num_order;
+  uint32_t flags;           /* PG_PLAN_* */
+  uint32_t pad;
+  uint64_t num_groups_limit;
+  uint64_t query_id;
+  int64_t deadline_ms;
+  uint64_t limit;
+  uint64_t segments_off;    /* pg_image_segment[num_segments] */
+  uint64_t ops_off;         /* int32_t[num_ops] */
+  uint64_t aggs_off;        /* pg_agg[num_aggs] */
+  uint64_t keys_off;        /* pg_key[num_keys] */
+  uint64_t order_off;       /* pg_order[num_order] */
+} pg_image_header;          /* 120 bytes */
+
+typedef struct pg_image_segment {
+  uint64_t seg_key;
+  uint32_t num_docs;
+  uint32_t pad;
+  uint64_t leaves_off;      /* pg_image_leaf[num_leaves] */
+} pg_image_segment;         /* 24 bytes */
+
+typedef struct pg_image_leaf { /* pg_leaf with its two host pointers replaced by offsets (same size, same fields) */
+  uint32_t kind, col_id, exclusive, num_ids;
+  int32_t lo, hi;
+  uint64_t ids_off;
+  int64_t ilo, ihi;
+  double dlo, dhi;
+  uint32_t lo_inclusive, hi_inclusive;
+  uint64_t values_off;
+  uint32_t num_values;
+  uint32_t pad;
+} pg_image_leaf;            /* 88 bytes */
+
+int pg_execute_image(const void *image, uint64_t n, pg_result **out);
+int pg_execute_partial_image(const void *image, uint64_t n, pg_partials **out);
+int pg_partials_finalize_image(pg_partials *p, const void *image, uint64_t n, pg_result **out);
 
 /* ---------------------------------------------------------------- measurement hooks */
 

@@ -23,7 +23,8 @@ import numpy as np
 from pinot_amd import abi
 from pinot_amd.segment import _NP_BE
 from pinot_amd.plan import (CPlan, DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY, ExecutionStats, IntermediateResult,
-                            Table, default_row, execute_filtered, has_filtered_aggregations, merge_intermediate)
+                            Table, default_row, execute_filtered, final_value, group_trim, has_filtered_aggregations,
+                            merge_intermediate)
 from pinot_amd.query import QueryContext, parse
 from pinot_amd.segment import ImmutableSegment
 
@@ -226,31 +227,87 @@ class OracleEngine:
         return rows, st
 
     def execute(self, table: Table, query, segments: Optional[Sequence[ImmutableSegment]] = None,
-                num_groups_limit=None) -> IntermediateResult:
+                num_groups_limit=None, server: bool = False, config=None) -> IntermediateResult:
+        """server=True: the reference server's combined result -- the per-segment trim when minSegmentGroupTrimSize
+        is on, the IndexedTable's result size (group_trim) -- instead of every merged group."""
         if isinstance(query, str):
             query = parse(query)
         if has_filtered_aggregations(query):  # FilteredAggregationOperator.java:70-98: one plan per filter
             return execute_filtered(lambda q: self.execute(table, q, segments, num_groups_limit), query)
         segments = list(table.segments if segments is None else segments)
         plan = CPlan(table, query, segments, list(range(1, len(segments) + 1)), num_groups_limit)
-        return self.run_plan(plan, segments)
+        trim = group_trim(query, config) if server and query.group_by else None
+        return self.run_plan(plan, segments, trim)
 
-    def run_plan(self, plan: CPlan, segments: Sequence[ImmutableSegment]) -> IntermediateResult:
+    def run_plan(self, plan: CPlan, segments: Sequence[ImmutableSegment], trim=None) -> IntermediateResult:
         if self.threads > 1:
             with ThreadPoolExecutor(self.threads) as ex:
                 parts = list(ex.map(lambda i: self.run_segment(plan, i, segments[i]), range(len(segments))))
         else:
             parts = [self.run_segment(plan, i, s) for i, s in enumerate(segments)]
+        q = plan.query
         merged = {}
         stats = ExecutionStats()
+        closed = False  # IndexedTable without ORDER BY: no new keys once it holds resultSize (ConcurrentIndexedTable:76-86)
         for rows, st in parts:
+            if trim is not None and trim.segment_size is not None and len(rows) > trim.segment_size:
+                rows = resizer_top(q, plan.aggs, rows, trim.segment_size)  # AggregationGroupByOrderByOperator:118-132
             for k, v in rows.items():
-                merged[k] = merge_intermediate(plan.aggs, merged[k], v) if k in merged else v
+                if k in merged:
+                    merged[k] = merge_intermediate(plan.aggs, merged[k], v)
+                elif not closed:
+                    merged[k] = v
+                    closed = trim is not None and not trim.ordered and trim.server_size is not None and \
+                        len(merged) >= trim.server_size
             for f in stats.__dataclass_fields__:
                 setattr(stats, f, getattr(stats, f) + getattr(st, f))
-        if not plan.query.group_by and () not in merged:
+        if trim is not None and trim.ordered and trim.server_size is not None and len(merged) > trim.server_size:
+            merged = resizer_top(q, plan.aggs, merged, trim.server_size)  # IndexedTable.finish
+        if not q.group_by and () not in merged:
             merged[()] = default_row(plan.aggs)
-        return IntermediateResult(plan.aggs, list(plan.query.group_by), merged, stats)
+        return IntermediateResult(plan.aggs, list(q.group_by), merged, stats)
+
+
+class _Rec:
+    """An IntermediateRecord under TableResizer's comparator REVERSED (TableResizer.java:100-115, :164-175): the
+    heap root is the kept record that ranks last."""
+    __slots__ = ("key", "row", "vals", "asc")
+
+    def __init__(self, key, row, vals, asc):
+        self.key, self.row, self.vals, self.asc = key, row, vals, asc
+
+    def cmp(self, other) -> int:  # the ORDER BY comparator: < 0 when self ranks before other
+        for x, y, a in zip(self.vals, other.vals, self.asc):
+            if x != y:
+                return (-1 if x < y else 1) if a else (1 if x < y else -1)
+        return 0
+
+    def __lt__(self, other):  # reversed: the record ranking later is "smaller" (sits at the heap root)
+        return self.cmp(other) > 0
+
+
+def resizer_top(query: QueryContext, aggs, rows: dict, size: int) -> dict:
+    """TableResizer.getTopRecords / trimInSegmentResults (data/table/TableResizer.java:160-310) restated: a heap of
+    `size` records whose root is the worst kept one; each further record replaces the root when it ranks before it.
+    Records the ORDER BY ties at the boundary are kept in arrival order (the reference's choice is arbitrary).  The
+    order-by values are the group-by values and extractFinalResult of the aggregations (:121-150)."""
+    import heapq
+    if len(rows) <= size:
+        return rows
+    asc = [o.asc for o in query.order_by]
+
+    def rec(k, v):
+        vals = [final_value(aggs[aggs.index(o.agg)], v[aggs.index(o.agg)]) if o.kind == "AGG"
+                else k[query.group_by.index(o.column)] for o in query.order_by]
+        return _Rec(k, v, vals, asc)
+    it = iter(rows.items())
+    heap = [rec(k, v) for k, v in (next(it) for _ in range(size))]
+    heapq.heapify(heap)
+    for k, v in it:
+        r = rec(k, v)
+        if r.cmp(heap[0]) < 0:
+            heapq.heapreplace(heap, r)
+    return {r.key: r.row for r in heap}
 
 
 def _py(v):

@@ -1,7 +1,7 @@
 """ctypes mirror of include/pinot_gpu.h (the C ABI).  Shared by the GPU binding and the oracle."""
 import ctypes as C
 
-PG_ABI_VERSION = 5
+PG_ABI_VERSION = 6
 
 PG_OK, PG_E_INVALID, PG_E_HIP, PG_E_NOMEM, PG_E_NOTFOUND, PG_E_UNSUPPORTED, PG_E_CANCELLED, PG_E_TIMEOUT, \
     PG_E_STATE = 0, -1, -2, -3, -4, -5, -6, -7, -8
@@ -35,6 +35,7 @@ PG_EXPR_COL, PG_EXPR_MUL, PG_EXPR_ADD, PG_EXPR_SUB = range(4)
 PG_KEY_VALUE_OFFSET, PG_KEY_KEYMAP = 0, 1
 PG_ORDER_AGG, PG_ORDER_KEY = 0, 1
 PG_PLAN_VALUE_SETS, PG_PLAN_HASH_GROUPS, PG_PLAN_F64_SUMS, PG_PLAN_NO_STREAM = 0x1, 0x2, 0x4, 0x8
+PG_PLAN_EXACT_LIMIT = 0x10
 PG_STATE_DENSE, PG_STATE_HASH = 0, 1
 PG_EMPTY_KEY = 0xFFFFFFFFFFFFFFFF
 
@@ -81,6 +82,30 @@ class pg_plan(C.Structure):
                 ("num_order", C.c_uint32), ("order", C.POINTER(pg_order)), ("limit", C.c_uint64)]
 
 
+PG_IMAGE_MAGIC = 0x49504750
+
+
+class pg_image_header(C.Structure):
+    _fields_ = [("magic", C.c_uint32), ("abi_version", C.c_uint32), ("image_bytes", C.c_uint64),
+                ("num_segments", C.c_uint32), ("num_leaves", C.c_uint32), ("num_ops", C.c_uint32),
+                ("num_aggs", C.c_uint32), ("num_keys", C.c_uint32), ("num_order", C.c_uint32), ("flags", C.c_uint32),
+                ("pad", C.c_uint32), ("num_groups_limit", C.c_uint64), ("query_id", C.c_uint64),
+                ("deadline_ms", C.c_int64), ("limit", C.c_uint64), ("segments_off", C.c_uint64),
+                ("ops_off", C.c_uint64), ("aggs_off", C.c_uint64), ("keys_off", C.c_uint64), ("order_off", C.c_uint64)]
+
+
+class pg_image_segment(C.Structure):
+    _fields_ = [("seg_key", C.c_uint64), ("num_docs", C.c_uint32), ("pad", C.c_uint32), ("leaves_off", C.c_uint64)]
+
+
+class pg_image_leaf(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("col_id", C.c_uint32), ("exclusive", C.c_uint32), ("num_ids", C.c_uint32),
+                ("lo", C.c_int32), ("hi", C.c_int32), ("ids_off", C.c_uint64),
+                ("ilo", C.c_int64), ("ihi", C.c_int64), ("dlo", C.c_double), ("dhi", C.c_double),
+                ("lo_inclusive", C.c_uint32), ("hi_inclusive", C.c_uint32), ("values_off", C.c_uint64),
+                ("num_values", C.c_uint32), ("pad", C.c_uint32)]
+
+
 class pg_stats(C.Structure):
     _fields_ = [("num_docs_scanned", C.c_uint64), ("num_entries_scanned_in_filter", C.c_uint64),
                 ("num_entries_scanned_post_filter", C.c_uint64), ("num_total_docs", C.c_uint64),
@@ -112,7 +137,8 @@ class pg_timing(C.Structure):
 EXPORTED = ["pg_init", "pg_last_error", "pg_resident_bytes", "pg_cancel", "pg_abi_version", "pg_column_upload",
             "pg_segment_release", "pg_execute", "pg_result_free", "pg_execute_partial", "pg_partials_finalize",
             "pg_partials_free", "pg_partials_copy", "pg_partials_export", "pg_partials_create", "pg_partials_merge",
-            "pg_key_owner", "pg_last_timing", "pg_chunk_decompress", "pg_dict_id_sets"]
+            "pg_key_owner", "pg_last_timing", "pg_chunk_decompress", "pg_dict_id_sets", "pg_execute_image",
+            "pg_execute_partial_image", "pg_partials_finalize_image"]
 PG_CODEC_PASS_THROUGH, PG_CODEC_SNAPPY, PG_CODEC_ZSTANDARD, PG_CODEC_LZ4, PG_CODEC_LZ4_LENGTH_PREFIXED = 0, 1, 2, 3, 4
 PG_COPY_OUT, PG_COPY_IN = 0, 1
 
@@ -144,9 +170,68 @@ def declare(lib):
         "pg_partials_merge": ([P(pg_partials), C.c_void_p, C.c_uint64, C.c_void_p], C.c_int),
         "pg_key_owner": ([C.c_uint64, C.c_uint32], C.c_uint32),
         "pg_chunk_decompress": ([C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, P(C.c_uint64)], C.c_int),
+        "pg_execute_image": ([C.c_void_p, C.c_uint64, P(P(pg_result))], C.c_int),
+        "pg_execute_partial_image": ([C.c_void_p, C.c_uint64, P(P(pg_partials))], C.c_int),
+        "pg_partials_finalize_image": ([P(pg_partials), C.c_void_p, C.c_uint64, P(P(pg_result))], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(lib, name)
         f.argtypes = args
         f.restype = res
     return lib
+
+
+def build_image(plan: pg_plan) -> "np.ndarray":
+    """The relocatable image (include/pinot_gpu.h, pg_image_header) of a pointer-form pg_plan: every array the plan
+    points to copied into one 8-byte-aligned buffer at a byte offset; an array several segments share (values-mode IN
+    literals) is stored once.  Returns a uint8 view of length image_bytes."""
+    import numpy as np
+    buf = bytearray(C.sizeof(pg_image_header))
+    placed = {}
+    keep = []  # temporaries stay alive while `placed` is keyed by their addresses
+
+    def put(addr, nbytes, align=8):
+        if not addr or not nbytes:
+            return 0
+        hit = placed.get((addr, nbytes))
+        if hit is not None:
+            return hit
+        buf.extend(bytes(-len(buf) % align))
+        off = len(buf)
+        buf.extend(C.string_at(addr, nbytes))
+        placed[(addr, nbytes)] = off
+        return off
+
+    def addr_of(ptr):
+        return C.cast(ptr, C.c_void_p).value
+
+    h = pg_image_header()
+    h.magic, h.abi_version = PG_IMAGE_MAGIC, plan.abi_version
+    for f in ("num_segments", "num_leaves", "num_ops", "num_aggs", "num_keys", "num_order", "flags",
+              "num_groups_limit", "query_id", "deadline_ms", "limit"):
+        setattr(h, f, getattr(plan, f))
+    h.ops_off = put(addr_of(plan.ops), 4 * plan.num_ops, 4)
+    h.aggs_off = put(addr_of(plan.aggs), C.sizeof(pg_agg) * plan.num_aggs)
+    h.keys_off = put(addr_of(plan.keys), C.sizeof(pg_key) * plan.num_keys)
+    h.order_off = put(addr_of(plan.order), C.sizeof(pg_order) * plan.num_order, 4)
+    segs = (pg_image_segment * max(plan.num_segments, 1))()
+    L = plan.num_leaves
+    for si in range(plan.num_segments):
+        sr = plan.segments[si]
+        leaves = (pg_image_leaf * max(L, 1))()
+        keep.append(leaves)
+        for li in range(L):
+            x = sr.leaves[li]
+            y = leaves[li]
+            C.memmove(C.addressof(y), C.addressof(x), C.sizeof(pg_leaf))
+            y.ids_off = put(addr_of(x.ids), 4 * x.num_ids, 4) if x.ids else 0
+            y.values_off = put(x.values, 8 * (x.num_values or x.num_ids)) if x.values else 0
+        segs[si].seg_key, segs[si].num_docs = sr.seg_key, sr.num_docs
+        segs[si].leaves_off = put(C.addressof(leaves), C.sizeof(pg_image_leaf) * L) if L else 0
+    h.segments_off = put(C.addressof(segs), C.sizeof(pg_image_segment) * plan.num_segments)
+    buf.extend(bytes(-len(buf) % 8))
+    h.image_bytes = len(buf)
+    buf[:C.sizeof(h)] = bytes(h)
+    out = np.empty(len(buf) // 8, dtype=np.uint64).view(np.uint8)
+    out[:] = np.frombuffer(bytes(buf), dtype=np.uint8)
+    return out

@@ -30,7 +30,7 @@ from typing import Optional
 import numpy as np
 
 from . import abi
-from .plan import ExecutionStats, IntermediateResult, default_row, merge_intermediate
+from .plan import ExecutionStats, IntermediateResult, default_row, merge_intermediate, top_groups
 
 _STATS_FIELDS = ["num_docs_scanned", "num_entries_scanned_in_filter", "num_entries_scanned_post_filter",
                  "num_total_docs", "num_segments_processed", "num_segments_matched"]
@@ -237,6 +237,9 @@ def _exchange_rows(engine, plan, p, stats, group, dev) -> IntermediateResult:
         rows.update(res.rows)
     if not plan.query.group_by and () not in rows:  # no rank matched a doc
         rows[()] = default_row(res.aggregations)
+    if plan.plan.flags & abi.PG_PLAN_EXACT_LIMIT and plan.plan.limit and len(rows) > plan.plan.limit:
+        # the server's result size over the union of the owners' kept rows (each owner kept its own top `limit`)
+        rows = top_groups(plan.query, res.aggregations, rows, plan.plan.limit)
     # every owner carries the statistics summed over the ranks
     return IntermediateResult(res.aggregations, res.group_by, rows, ExecutionStats(*(int(x) for x in ra["stats"])))
 

@@ -26,8 +26,23 @@ size_t mv_offsets_scratch_bytes(uint64_t num_values);
 // The per-query parameter arena read by the device straight from its pinned (fine-grained, mapped) host image, and
 // the query's scratch zeroed, in ONE launch on the query stream (instead of an SDMA copy, whose completion the compute
 // queue waits on, plus a fill).
+struct FillSpans {  // byte fills deferred into the arena-upload launch (a state's zero / empty initialisation)
+  static constexpr uint32_t kMax = 8;
+  void* p[kMax];
+  uint64_t n[kMax];
+  uint32_t byte[kMax];
+  uint32_t count;
+  bool add(void* ptr, uint32_t b, uint64_t bytes) {
+    if (count >= kMax) return false;
+    p[count] = ptr;
+    n[count] = bytes;
+    byte[count] = b;
+    count++;
+    return true;
+  }
+};
 hipError_t launch_arena_upload(const void* host_src, void* dst, uint64_t bytes, void* zero, uint64_t zero_bytes,
-                               hipStream_t s);
+                               const FillSpans& fills, hipStream_t s);
 hipError_t launch_fill_ranges(const int32_t* ranges /*[n][2] inclusive, sorted, disjoint*/, uint32_t n,
                               uint32_t num_docs, uint32_t* bitmap, hipStream_t s);
 struct RoaringContainer {
@@ -279,7 +294,7 @@ hipError_t launch_set_extract(const StateView& v, const FinalSpec& f, const uint
 hipError_t launch_gather_rows(const StateView& v, const uint32_t* slots, uint64_t n, uint64_t key_div, uint8_t* dst,
                               hipStream_t s);
 hipError_t launch_merge_rows(const StateView& v, const uint8_t* rows, uint64_t n, hipStream_t s);
-hipError_t launch_init_view(const StateView& v, hipStream_t s);  // pg_kernels.hip: zero / empty / +-inf state
+hipError_t launch_init_view(const StateView& v, hipStream_t s, FillSpans* defer = nullptr);  // pg_kernels.hip: zero / empty / +-inf state
 hipError_t launch_seg_truncate(const StateView& v, const uint32_t* slots, uint64_t n, uint32_t num_segments,
                                uint64_t limit, uint64_t* tmp_keys, uint64_t* sorted_keys, uint32_t* sorted_slots,
                                uint32_t* seg_first, uint8_t* keep, void* temp, size_t temp_bytes, hipStream_t s);

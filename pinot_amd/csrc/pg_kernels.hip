@@ -29,14 +29,19 @@ __global__ void init_minmax_kernel(long long* mn, uint64_t nmn, long long* mx, u
   for (uint64_t k = i; k < nmx; k += stride) mx[k] = order_key(-__builtin_inf());
 }
 
-hipError_t launch_init_view(const StateView& v, hipStream_t s) {
+// defer != null: the byte fills are appended there (applied by the query's arena-upload launch) while they fit
+hipError_t launch_init_view(const StateView& v, hipStream_t s, FillSpans* defer) {
   hipError_t e;
-  if (v.n_i64 && (e = hipMemsetAsync(v.i64, 0, v.num_slots * v.n_i64 * 8, s)) != hipSuccess) return e;
-  if (v.n_f64 && (e = hipMemsetAsync(v.f64, 0, v.num_slots * v.n_f64 * 8, s)) != hipSuccess) return e;
-  if (v.bit_words && (e = hipMemsetAsync(v.bits, 0, v.num_slots * v.bit_words * 4ull, s)) != hipSuccess) return e;
-  if (v.keys && (e = hipMemsetAsync(v.keys, 0xFF, v.num_slots * 8, s)) != hipSuccess) return e;
-  if (v.first_doc && (e = hipMemsetAsync(v.first_doc, 0xFF, v.num_slots * 4, s)) != hipSuccess) return e;
-  if (v.fill && (e = hipMemsetAsync(v.fill, 0, 8, s)) != hipSuccess) return e;  // fill + err
+  auto fill = [&](void* p, int b, uint64_t n) {
+    if (defer && defer->add(p, (uint32_t)b, n)) return hipSuccess;
+    return hipMemsetAsync(p, b, n, s);
+  };
+  if (v.n_i64 && (e = fill(v.i64, 0, v.num_slots * v.n_i64 * 8)) != hipSuccess) return e;
+  if (v.n_f64 && (e = fill(v.f64, 0, v.num_slots * v.n_f64 * 8)) != hipSuccess) return e;
+  if (v.bit_words && (e = fill(v.bits, 0, v.num_slots * v.bit_words * 4ull)) != hipSuccess) return e;
+  if (v.keys && (e = fill(v.keys, 0xFF, v.num_slots * 8)) != hipSuccess) return e;
+  if (v.first_doc && (e = fill(v.first_doc, 0xFF, v.num_slots * 4)) != hipSuccess) return e;
+  if (v.fill && (e = fill(v.fill, 0, 8)) != hipSuccess) return e;  // fill + err
   const uint64_t n = v.num_slots * (v.n_min > v.n_max ? v.n_min : v.n_max);
   if (n) {
     const uint32_t blocks = (uint32_t)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
@@ -579,24 +584,40 @@ hipError_t launch_dict_lookup(const DictLookupJob* jobs, uint32_t num_segments, 
 
 // ------------------------------------------------------------------------------------------ parameter arena upload
 
+// one byte value over [z, z + n) (z 16-byte aligned: pooled blocks), the grid's x dimension striding it
+__device__ __forceinline__ void fill_span(uint8_t* __restrict__ z, uint64_t n, uint32_t b, uint64_t t,
+                                          uint64_t stride) {
+  const uint32_t w = b * 0x01010101u;
+  const uint64_t n16 = n / 16;
+  for (uint64_t i = t; i < n16; i += stride) ((uint4*)z)[i] = make_uint4(w, w, w, w);
+  for (uint64_t i = n16 * 16 + t; i < n; i += stride) z[i] = (uint8_t)b;
+}
+
+// blockIdx.y == 0: the arena copy + the scratch zeroing; blockIdx.y == k + 1: deferred fill k
 __global__ void __launch_bounds__(256) arena_upload_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
-                                                          uint64_t n16, uint8_t* __restrict__ z, uint64_t zbytes) {
+                                                          uint64_t n16, uint8_t* __restrict__ z, uint64_t zbytes,
+                                                          FillSpans fills) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.y) {
+    const uint32_t k = blockIdx.y - 1;
+    fill_span((uint8_t*)fills.p[k], fills.n[k], fills.byte[k], t, stride);
+    return;
+  }
   for (uint64_t i = t; i < n16; i += stride) dst[i] = src[i];
-  const uint64_t z16 = zbytes / 16;
-  for (uint64_t i = t; i < z16; i += stride) ((uint4*)z)[i] = make_uint4(0u, 0u, 0u, 0u);
-  for (uint64_t i = z16 * 16 + t; i < zbytes; i += stride) z[i] = 0;
+  fill_span(z, zbytes, 0u, t, stride);
 }
 
 hipError_t launch_arena_upload(const void* host_src, void* dst, uint64_t bytes, void* zero, uint64_t zero_bytes,
-                               hipStream_t s) {
+                               const FillSpans& fills, hipStream_t s) {
   // the source is read in whole 16-byte units: the pinned image's capacity is a multiple of 16 covering them
-  const uint64_t n16 = (bytes + 15) / 16, units = std::max<uint64_t>(n16, (zero_bytes + 15) / 16);
+  const uint64_t n16 = (bytes + 15) / 16;
+  uint64_t units = std::max<uint64_t>(n16, (zero_bytes + 15) / 16);
+  for (uint32_t k = 0; k < fills.count; k++) units = std::max<uint64_t>(units, (fills.n[k] + 15) / 16);
   if (!units) return hipSuccess;
   const uint64_t blocks = std::min<uint64_t>((units + 255) / 256, 1024);
-  hipLaunchKernelGGL(arena_upload_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, (const uint4*)host_src, (uint4*)dst,
-                     n16, (uint8_t*)zero, zero_bytes);
+  hipLaunchKernelGGL(arena_upload_kernel, dim3((uint32_t)blocks, 1 + fills.count), dim3(256), 0, s,
+                     (const uint4*)host_src, (uint4*)dst, n16, (uint8_t*)zero, zero_bytes, fills);
   return hipGetLastError();
 }
 

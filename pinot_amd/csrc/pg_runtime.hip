@@ -861,7 +861,7 @@ struct Partials {
     return v;
   }
   // device state for `num_slots` slots of the current layout (+ keys for hash modes), initialised
-  int alloc_state(hipStream_t s, bool init = true);
+  int alloc_state(hipStream_t s, bool init = true, FillSpans* defer = nullptr);
 };
 
 // Layout of the state arrays of a plan's aggregations (slot assignment, DISTINCTCOUNT bitmap words).  `integer`
@@ -1105,7 +1105,7 @@ int agg_layout(const pg_plan* plan, uint32_t integer, std::vector<AggSpec>& aggs
   return PG_OK;
 }
 
-int Partials::alloc_state(hipStream_t s, bool init) {
+int Partials::alloc_state(hipStream_t s, bool init, FillSpans* defer) {
   const uint64_t G = num_slots;
   int rc;
   const bool hash = mode == GM_HASH || mode == GM_HASH_SEG;
@@ -1117,7 +1117,7 @@ int Partials::alloc_state(hipStream_t s, bool init) {
   if (hash) { if ((rc = keys.alloc_pooled(G * 8ull))) return rc; } else keys.reset();
   if (mode == GM_HASH_SEG) { if ((rc = first_doc.alloc_pooled(G * 4ull))) return rc; } else first_doc.reset();
   if ((rc = misc.alloc_pooled(16))) return rc;
-  if (init) HIP_CHECK(launch_init_view(view(), s));
+  if (init) HIP_CHECK(launch_init_view(view(), s, defer));
   else HIP_CHECK(hipMemsetAsync(misc.p, 0, 16, s));  // every slot is written by the producer (pg_part.hip)
   return PG_OK;
 }
@@ -2542,7 +2542,11 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   PG_PROF("stream");
   // ---- device buffers (state + arena + scratch) from the caching pool
   part.on = part.on && q.num_items > 0;
-  if ((rc = P.alloc_state(s, !part.on))) return rc;
+  // the state's byte fills ride on the arena-upload launch unless the non-scan seeding below writes the state first
+  FillSpans fills;
+  memset(&fills, 0, sizeof(fills));
+  const bool defer_fills = !(ns_docs || ns_matched);
+  if ((rc = P.alloc_state(s, !part.on, defer_fills ? &fills : nullptr))) return rc;
   if (ns_docs || ns_matched) {  // the non-scan segments' results seed the state the scan adds to
     uint64_t* h = (uint64_t*)t_ctx.readback.get(8ull * (1 + 2 * A));
     if (!h) return fail(PG_E_NOMEM, "pinned staging failed");
@@ -2575,7 +2579,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     HIP_CHECK(hipStreamSynchronize(s));  // the pinned staging words are reused below
   }
   if ((rc = P.seg_matched.alloc_pooled(8ull * (S ? S : 1) + 16))) return rc;
-  HIP_CHECK(hipMemsetAsync(P.seg_matched.p, 0, 8ull * (S ? S : 1) + 16, s));
+  if (!fills.add(P.seg_matched.p, 0, 8ull * (S ? S : 1) + 16))
+    HIP_CHECK(hipMemsetAsync(P.seg_matched.p, 0, 8ull * (S ? S : 1) + 16, s));
   {
     const StateView v = P.view();
     q.i64 = v.i64;
@@ -2729,7 +2734,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   hipEvent_t* ev = t_ctx.ev;
   PG_PROF("arena");
   // the arena was built in pinned memory: the device reads it from there
-  HIP_CHECK(launch_arena_upload(ar.h.dp, arena.p, ar.h.size(), scratch.p, scratch_bytes, s));
+  HIP_CHECK(launch_arena_upload(ar.h.dp, arena.p, ar.h.size(), scratch.p, scratch_bytes, fills, s));
   HIP_CHECK(hipEventRecord(ev[0], s));
   {
     uint32_t max_n = 0;
@@ -3628,14 +3633,20 @@ int build_result(pg_partials* pp, const pg_plan* plan, pg_result** out, const Pa
           if (x != y) return it.desc ? x > y : x < y;
         }
       }
-      if (P.wide) {  // ascending key ids, first key first
-        for (uint32_t k = 0; k < K; k++)
-          if (key_id(i, k) != key_id(j, k)) return key_id(i, k) < key_id(j, k);
-        return false;
-      }
-      return hk[i] < hk[j];
+      for (uint32_t k = 0; k < K; k++)  // ascending key ids, first key first
+        if (key_id(i, k) != key_id(j, k)) return key_id(i, k) < key_id(j, k);
+      return false;
+    });
+  } else if (K && (plan->flags & PG_PLAN_EXACT_LIMIT) && plan->limit && nc > plan->limit) {
+    // no ORDER BY: the `limit` groups of smallest key ids (first key first)
+    std::sort(perm.begin(), perm.end(), [&](uint64_t i, uint64_t j) {
+      for (uint32_t k = 0; k < K; k++)
+        if (key_id(i, k) != key_id(j, k)) return key_id(i, k) < key_id(j, k);
+      return false;
     });
   }
+  // PG_PLAN_EXACT_LIMIT: the first `limit` rows of that order (the server result / the per-segment trim)
+  if (K && (plan->flags & PG_PLAN_EXACT_LIMIT) && plan->limit && nc > plan->limit) nc = plan->limit;
 
   pg_result* r = (pg_result*)calloc(1, sizeof(pg_result));
   if (!r) return fail(PG_E_NOMEM, "out of host memory");
@@ -3671,8 +3682,108 @@ int build_result(pg_partials* pp, const pg_plan* plan, pg_result** out, const Pa
         at += len;
       }
     r->distinct_offsets[m] = at;
+    r->num_distinct = at;  // the kept groups' ids (an exact limit may drop candidates)
   }
   *out = r;
+  return PG_OK;
+}
+
+// ---------------------------------------------------------------------------------------- relocatable plan image
+
+static_assert(sizeof(pg_image_header) == 120 && sizeof(pg_image_segment) == 24 && sizeof(pg_image_leaf) == 88,
+              "pg_image_* layouts are part of the ABI");
+static_assert(sizeof(pg_image_leaf) == sizeof(pg_leaf) && offsetof(pg_image_leaf, ids_off) == offsetof(pg_leaf, ids) &&
+                  offsetof(pg_image_leaf, values_off) == offsetof(pg_leaf, values) &&
+                  offsetof(pg_image_leaf, num_values) == offsetof(pg_leaf, num_values),
+              "a pg_image_leaf is a pg_leaf with offsets for pointers");
+
+// A pg_plan whose pointers point into a validated image (pg_execute_image): the image is borrowed for the call.
+struct PlanImage {
+  pg_plan plan{};
+  std::vector<pg_segment_ref> segs;
+  std::vector<pg_leaf> leaves;
+};
+
+int decode_image(const void* image, uint64_t n, PlanImage& out) {
+  if (!image) return fail(PG_E_INVALID, "image: null buffer");
+  if ((uintptr_t)image & 7) return fail(PG_E_INVALID, "image: buffer not 8-byte aligned");
+  if (n < sizeof(pg_image_header)) return fail(PG_E_INVALID, "image: %llu bytes < header", (unsigned long long)n);
+  const uint8_t* base = (const uint8_t*)image;
+  const pg_image_header& h = *(const pg_image_header*)image;
+  if (h.magic != PG_IMAGE_MAGIC) return fail(PG_E_INVALID, "image: bad magic 0x%08x", h.magic);
+  if (h.abi_version != PG_ABI_VERSION) return fail(PG_E_INVALID, "image: ABI version %u != %u", h.abi_version, PG_ABI_VERSION);
+  if (h.image_bytes != n) return fail(PG_E_INVALID, "image: header says %llu bytes, buffer has %llu",
+                                      (unsigned long long)h.image_bytes, (unsigned long long)n);
+  // [off, off + count * size) inside the buffer, aligned; an empty array may carry any offset (it is never read)
+  auto span = [&](uint64_t off, uint64_t count, uint64_t size, uint64_t align, const char* what) -> const void* {
+    if (!count) return nullptr;
+    uint64_t bytes;
+    if (__builtin_mul_overflow(count, size, &bytes) || off < sizeof(pg_image_header) || off % align || off > n ||
+        bytes > n - off) {
+      fail(PG_E_INVALID, "image: %s (offset %llu, %llu x %llu bytes) outside the %llu-byte buffer or misaligned", what,
+           (unsigned long long)off, (unsigned long long)count, (unsigned long long)size, (unsigned long long)n);
+      return (const void*)1;  // sentinel: rejected
+    }
+    return base + off;
+  };
+  auto bad = [](const void* p) { return p == (const void*)1; };
+  if (h.num_segments > (1u << 24) || h.num_leaves > (1u << 16) || h.num_ops > (1u << 20) || h.num_aggs > 64 ||
+      h.num_keys > 64 || h.num_order > 64)
+    return fail(PG_E_INVALID, "image: counts out of range");
+  const pg_image_segment* segs = (const pg_image_segment*)span(h.segments_off, h.num_segments, sizeof(pg_image_segment), 8, "segments");
+  const int32_t* ops = (const int32_t*)span(h.ops_off, h.num_ops, 4, 4, "ops");
+  const pg_agg* aggs = (const pg_agg*)span(h.aggs_off, h.num_aggs, sizeof(pg_agg), 8, "aggs");
+  const pg_key* keys = (const pg_key*)span(h.keys_off, h.num_keys, sizeof(pg_key), 8, "keys");
+  const pg_order* order = (const pg_order*)span(h.order_off, h.num_order, sizeof(pg_order), 4, "order");
+  if (bad(segs) || bad(ops) || bad(aggs) || bad(keys) || bad(order)) return PG_E_INVALID;
+  out.segs.resize(h.num_segments);
+  out.leaves.resize((uint64_t)h.num_segments * h.num_leaves);
+  for (uint32_t si = 0; si < h.num_segments; si++) {
+    const pg_image_segment& is = segs[si];
+    const pg_image_leaf* il = (const pg_image_leaf*)span(is.leaves_off, h.num_leaves, sizeof(pg_image_leaf), 8, "leaves");
+    if (bad(il)) return PG_E_INVALID;
+    pg_leaf* dst = out.leaves.data() + (uint64_t)si * h.num_leaves;
+    for (uint32_t li = 0; li < h.num_leaves; li++) {
+      const pg_image_leaf& x = il[li];
+      pg_leaf& y = dst[li];
+      memcpy(&y, &x, sizeof(pg_leaf));  // same layout; the two offsets are replaced below
+      y.ids = nullptr;
+      y.values = nullptr;
+      if (x.ids_off) {
+        const void* p = span(x.ids_off, x.num_ids, 4, 4, "leaf ids");
+        if (bad(p) || !p) return bad(p) ? PG_E_INVALID : fail(PG_E_INVALID, "image: leaf %u ids_off with num_ids 0", li);
+        y.ids = (const int32_t*)p;
+      }
+      if (x.values_off) {
+        const uint64_t nv = x.num_values ? x.num_values : x.num_ids;
+        const void* p = span(x.values_off, nv, 8, 8, "leaf values");
+        if (bad(p) || !p) return bad(p) ? PG_E_INVALID : fail(PG_E_INVALID, "image: leaf %u values_off with no values", li);
+        y.values = p;
+      }
+    }
+    out.segs[si].seg_key = is.seg_key;
+    out.segs[si].num_docs = is.num_docs;
+    out.segs[si].leaves = dst;
+  }
+  pg_plan& p = out.plan;
+  p.abi_version = h.abi_version;
+  p.num_segments = h.num_segments;
+  p.segments = out.segs.data();
+  p.num_leaves = h.num_leaves;
+  p.num_ops = h.num_ops;
+  p.ops = ops;
+  p.num_aggs = h.num_aggs;
+  p.num_keys = h.num_keys;
+  p.aggs = aggs;
+  p.keys = keys;
+  p.num_groups_limit = h.num_groups_limit;
+  p.query_id = h.query_id;
+  p.deadline_ms = h.deadline_ms;
+  p.stream = nullptr;
+  p.flags = h.flags;
+  p.num_order = h.num_order;
+  p.order = order;
+  p.limit = h.limit;
   return PG_OK;
 }
 
@@ -3899,8 +4010,9 @@ int pg_dict_id_sets(const uint64_t* seg_keys, uint32_t num_segments, uint32_t co
   if (!n) { memset(out_counts, 0, 4 * S); return PG_OK; }
   try {
     std::vector<DictLookupJob> jobs(S);
+    // held until the lookup kernel has finished reading the dictionaries (a concurrent pg_segment_release frees them)
+    std::shared_lock<std::shared_mutex> lk(g_seg_mu);
     {
-      std::shared_lock<std::shared_mutex> lk(g_seg_mu);
       for (uint64_t si = 0; si < S; si++) {
         auto it = g_segs.find(seg_keys[si]);
         if (it == g_segs.end()) return fail(PG_E_NOTFOUND, "segment %llu not resident", (unsigned long long)seg_keys[si]);
@@ -3954,6 +4066,38 @@ int pg_execute(const pg_plan* plan, pg_result** out) {
   PG_PROF("finalize");
   host_prof_dump(t_prof.n ? t_prof_start : 0);
   return rc;
+}
+
+int pg_execute_image(const void* image, uint64_t n, pg_result** out) {
+  if (!out) return fail(PG_E_INVALID, "null out");
+  try {
+    PlanImage pi;
+    const int rc = decode_image(image, n, pi);
+    return rc ? rc : pg_execute(&pi.plan, out);
+  } catch (const std::exception& e) {
+    return fail(PG_E_NOMEM, "execute failed: %s", e.what());
+  }
+}
+
+int pg_execute_partial_image(const void* image, uint64_t n, pg_partials** out) {
+  if (!out) return fail(PG_E_INVALID, "null out");
+  try {
+    PlanImage pi;
+    const int rc = decode_image(image, n, pi);
+    return rc ? rc : pg_execute_partial(&pi.plan, out);
+  } catch (const std::exception& e) {
+    return fail(PG_E_NOMEM, "execute failed: %s", e.what());
+  }
+}
+
+int pg_partials_finalize_image(pg_partials* p, const void* image, uint64_t n, pg_result** out) {
+  try {
+    PlanImage pi;
+    const int rc = decode_image(image, n, pi);
+    return rc ? rc : pg_partials_finalize(p, &pi.plan, out);
+  } catch (const std::exception& e) {
+    return fail(PG_E_NOMEM, "finalize failed: %s", e.what());
+  }
 }
 
 int pg_result_free(pg_result* r) {

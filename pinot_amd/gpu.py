@@ -14,8 +14,8 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from . import abi
-from .plan import (CPlan, ExecutionStats, IntermediateResult, Table, UnsupportedQuery, execute_filtered,
-                   has_filtered_aggregations)
+from .plan import (CPlan, ExecutionStats, InstanceConfig, IntermediateResult, Table, UnsupportedQuery,
+                   execute_filtered, group_trim, has_filtered_aggregations, merge_intermediate, top_groups)
 from .query import QueryContext, parse
 from .segment import Column, ImmutableSegment
 
@@ -176,33 +176,50 @@ class GpuEngine:
 
     # ---- execution
     def make_plan(self, table: Table, query: QueryContext, segments: Optional[Sequence[ImmutableSegment]] = None,
-                  num_groups_limit=None, flags: int = abi.PG_PLAN_VALUE_SETS, trim: bool = False) -> CPlan:
-        """flags: PG_PLAN_* (default: DISTINCTCOUNT value sets, the reference's Set intermediate).  trim: the device
-        applies the query's ORDER BY / LIMIT (a final single-server answer; boundary ties kept)."""
+                  num_groups_limit=None, flags: int = abi.PG_PLAN_VALUE_SETS, trim=False,
+                  config: Optional[InstanceConfig] = None) -> CPlan:
+        """flags: PG_PLAN_* (default: DISTINCTCOUNT value sets, the reference's Set intermediate).  trim: see CPlan
+        (True: the query's ORDER BY / LIMIT with boundary ties, a final single-server answer; "server": the rows the
+        reference server's combine keeps under `config` and the query options)."""
         segments = list(table.segments if segments is None else segments)
         keys = [self.upload_segment(s, table) for s in segments]
-        plan = CPlan(table, query, segments, keys, num_groups_limit, flags, trim, id_sets=self.dict_id_sets)
+        plan = CPlan(table, query, segments, keys, num_groups_limit, flags, trim, id_sets=self.dict_id_sets,
+                     config=config)
         self.upload_keymaps(table, plan, segments, keys)
         return plan
 
-    def run_plan(self, plan: CPlan) -> IntermediateResult:
+    def run_plan(self, plan: CPlan, image: bool = True) -> IntermediateResult:
+        """pg_execute_image over the plan's relocatable image (the JNI form); image=False: pg_execute over the
+        pointer-form pg_plan (the in-process form)."""
         res = C.POINTER(abi.pg_result)()
-        check(self.lib.pg_execute(C.byref(plan.plan), C.byref(res)))
+        if image:
+            im = plan.image()
+            check(self.lib.pg_execute_image(im.ctypes.data, im.size, C.byref(res)))
+        else:
+            check(self.lib.pg_execute(C.byref(plan.plan), C.byref(res)))
         try:
             return self.decode(plan, res.contents)
         finally:
             self.lib.pg_result_free(res)
 
-    def run_partial(self, plan: CPlan):
-        """pg_execute_partial: this device's partial state (for the cross-GPU merge, pinot_amd.combine)."""
+    def run_partial(self, plan: CPlan, image: bool = True):
+        """pg_execute_partial(_image): this device's partial state (for the cross-GPU merge, pinot_amd.combine)."""
         p = C.POINTER(abi.pg_partials)()
-        check(self.lib.pg_execute_partial(C.byref(plan.plan), C.byref(p)))
+        if image:
+            im = plan.image()
+            check(self.lib.pg_execute_partial_image(im.ctypes.data, im.size, C.byref(p)))
+        else:
+            check(self.lib.pg_execute_partial(C.byref(plan.plan), C.byref(p)))
         return p
+
+    def _finalize(self, plan: CPlan, p, res):
+        im = plan.image()
+        check(self.lib.pg_partials_finalize_image(p, im.ctypes.data, im.size, C.byref(res)))
 
     def finalize_partial(self, plan: CPlan, p, free: bool = True) -> IntermediateResult:
         res = C.POINTER(abi.pg_result)()
         try:
-            check(self.lib.pg_partials_finalize(p, C.byref(plan.plan), C.byref(res)))
+            self._finalize(plan, p, res)
         finally:
             if free:
                 self.lib.pg_partials_free(p)
@@ -226,12 +243,35 @@ class GpuEngine:
         check(self.lib.pg_partials_merge(p, rows_ptr, n, stream))
 
     def execute(self, table: Table, query, segments=None, num_groups_limit=None, flags: int = abi.PG_PLAN_VALUE_SETS,
-                trim: bool = False) -> IntermediateResult:
+                trim=False, config: Optional[InstanceConfig] = None) -> IntermediateResult:
         if isinstance(query, str):
             query = parse(query)
         if has_filtered_aggregations(query):  # FilteredAggregationOperator: one device plan per filter
             return execute_filtered(lambda q: self.execute(table, q, segments, num_groups_limit, flags), query)
-        return self.run_plan(self.make_plan(table, query, segments, num_groups_limit, flags, trim))
+        if trim == "server" and query.group_by and group_trim(query, config).segment_size is not None:
+            return self._execute_segment_trimmed(table, query, segments, num_groups_limit, flags, config)
+        return self.run_plan(self.make_plan(table, query, segments, num_groups_limit, flags, trim, config))
+
+    def _execute_segment_trimmed(self, table, query, segments, num_groups_limit, flags, config) -> IntermediateResult:
+        """minSegmentGroupTrimSize > 0 with an ORDER BY: every segment's group-by result is trimmed to
+        getTableCapacity(limit, minSegmentGroupTrimSize) under the ORDER BY before the combine
+        (AggregationGroupByOrderByOperator.java:118-132, TableResizer.trimInSegmentResults), so each segment runs as its
+        own device plan with an exact limit, the value-keyed rows merge as IndexedTable.upsert merges them, and the
+        server keeps getTableCapacity(limit, minServerGroupTrimSize) rows (IndexedTable.finish)."""
+        gt = group_trim(query, config)
+        merged: dict = {}
+        stats = ExecutionStats()
+        aggs = None
+        for seg in (table.segments if segments is None else segments):
+            r = self.run_plan(self.make_plan(table, query, [seg], num_groups_limit, flags, gt.segment_size, config))
+            aggs = r.aggregations
+            for k, v in r.rows.items():
+                merged[k] = merge_intermediate(aggs, merged[k], v) if k in merged else v
+            for f in stats.__dataclass_fields__:
+                setattr(stats, f, getattr(stats, f) + getattr(r.stats, f))
+        if gt.server_size is not None:
+            merged = top_groups(query, aggs, merged, gt.server_size)
+        return IntermediateResult(aggs or query.aggregations, list(query.group_by), merged, stats)
 
     def last_timing(self) -> abi.pg_timing:
         t = abi.pg_timing()
@@ -242,7 +282,7 @@ class GpuEngine:
         """pg_partials_finalize -> the result as plain arrays (result_arrays); frees `p`."""
         res = C.POINTER(abi.pg_result)()
         try:
-            check(self.lib.pg_partials_finalize(p, C.byref(plan.plan), C.byref(res)))
+            self._finalize(plan, p, res)
         finally:
             self.lib.pg_partials_free(p)
         try:

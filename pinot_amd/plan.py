@@ -32,6 +32,10 @@ MAX_VALUE_OFFSET_KEYS = 1 << 26   # integer key ranges up to this size may use v
 VALUE_OFFSET_DENSITY = 4          # ... when the range is at most this many times the largest segment cardinality
 DEFAULT_NUM_GROUPS_LIMIT = 100_000          # InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT
 DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY = 10_000  # InstancePlanMakerImplV2 :73
+# group trim instance defaults (InstancePlanMakerImplV2.java:76-89; GroupByUtils.DEFAULT_MIN_NUM_GROUPS = 5000)
+DEFAULT_MIN_SEGMENT_GROUP_TRIM_SIZE = -1
+DEFAULT_MIN_SERVER_GROUP_TRIM_SIZE = 5000
+DEFAULT_GROUPBY_TRIM_THRESHOLD = 1_000_000
 # batched IN / NOT_IN leaves cross as their literals (values mode, pg_leaf.num_values) unless PG_IN_VALUES=0 (ids)
 _IN_VALUES = os.environ.get("PG_IN_VALUES", "1") != "0"
 
@@ -426,6 +430,91 @@ def reduce_to_rows(query: QueryContext, res: IntermediateResult) -> Tuple[List[s
     return names, rows_out
 
 
+# ------------------------------------------------------------------------------------------ group trim
+
+@dataclass
+class InstanceConfig:
+    """The pinot.server.query.executor.* settings InstancePlanMakerImplV2.init reads (plan/maker/
+    InstancePlanMakerImplV2.java:100-130): numGroupsLimit, min segment / server group trim sizes, trim threshold."""
+    num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT
+    min_segment_group_trim_size: int = DEFAULT_MIN_SEGMENT_GROUP_TRIM_SIZE
+    min_server_group_trim_size: int = DEFAULT_MIN_SERVER_GROUP_TRIM_SIZE
+    groupby_trim_threshold: int = DEFAULT_GROUPBY_TRIM_THRESHOLD
+
+
+@dataclass(frozen=True)
+class GroupTrim:
+    """What a server keeps of a group-by result.  segment_size: per-segment trim capacity (None = off); server_size:
+    rows of the server's combined result (None = every group); ordered: the kept rows are the top of the ORDER BY
+    (else `server_size` arbitrary groups -- here the smallest key ids); threshold: IndexedTable's trimThreshold."""
+    segment_size: Optional[int]
+    server_size: Optional[int]
+    ordered: bool
+    threshold: int
+
+
+def table_capacity(limit: int, min_num_groups: int) -> int:
+    """GroupByUtils.getTableCapacity (util/GroupByUtils.java:40-42): max(limit * 5, minNumGroups)."""
+    return max(limit * 5, min_num_groups)
+
+
+def _int_option(query: QueryContext, name: str) -> Optional[int]:
+    v = query.options.get(name)
+    return None if v is None else int(v)
+
+
+def group_trim(query: QueryContext, config: Optional[InstanceConfig] = None) -> GroupTrim:
+    """InstancePlanMakerImplV2.applyQueryOptions (:189-240: the minSegmentGroupTrimSize / minServerGroupTrimSize query
+    options override the instance config; groupTrimThreshold is instance-level) followed by the trims those settings
+    drive: AggregationGroupByOrderByOperator.getNextBlock (operator/query/AggregationGroupByOrderByOperator.java:
+    118-132: a segment with ORDER BY and more groups than getTableCapacity(limit, minSegmentGroupTrimSize) keeps that
+    many) and the GroupByOrderByCombineOperator constructor (operator/combine/GroupByOrderByCombineOperator.java:79-93:
+    ORDER BY -> getTableCapacity(limit, minServerGroupTrimSize), none -> limit, minServerGroupTrimSize <= 0 -> every
+    group), whose IndexedTable.finish keeps that many (data/table/IndexedTable.java:147-158)."""
+    cfg = config or InstanceConfig()
+    seg_min = _int_option(query, "minSegmentGroupTrimSize")
+    seg_min = cfg.min_segment_group_trim_size if seg_min is None else seg_min
+    srv_min = _int_option(query, "minServerGroupTrimSize")
+    srv_min = cfg.min_server_group_trim_size if srv_min is None else srv_min
+    ordered = bool(query.order_by)
+    seg = table_capacity(query.limit, seg_min) if ordered and seg_min > 0 else None
+    if srv_min > 0:
+        srv = table_capacity(query.limit, srv_min) if ordered else query.limit
+        threshold = cfg.groupby_trim_threshold
+    else:
+        srv, threshold = None, (1 << 31) - 1
+    return GroupTrim(seg, srv, ordered, threshold)
+
+
+def order_values(query: QueryContext, aggs: List[Aggregation], key: tuple, row: list) -> list:
+    """TableResizer's OrderByValueExtractors (data/table/TableResizer.java:121-150): a group-by expression's value or
+    the aggregation's final result (AggregationFunctionExtractor -> extractFinalResult)."""
+    out = []
+    for o in query.order_by:
+        if o.kind == "AGG":
+            i = aggs.index(o.agg)
+            out.append(final_value(aggs[i], row[i]))
+        else:
+            out.append(key[query.group_by.index(o.column)])
+    return out
+
+
+def top_groups(query: QueryContext, aggs: List[Aggregation], rows: Dict[tuple, list], size: int) -> Dict[tuple, list]:
+    """TableResizer.getTopRecords(recordsMap, size) (TableResizer.java:248-310) over value-keyed rows: the `size`
+    groups first under the ORDER BY; groups the ORDER BY ties at the boundary are taken in ascending key order (the
+    reference's heap leaves that choice arbitrary).  Without an ORDER BY: the `size` smallest keys (an IndexedTable
+    without ORDER BY keeps the first `size` keys it sees, IndexedTable.java:95-103)."""
+    if len(rows) <= size:
+        return rows
+    if query.order_by:
+        items = sorted(rows.items(), key=lambda kv: kv[0])
+        items.sort(key=lambda kv: [_Ord(v, o.asc) for v, o in zip(order_values(query, aggs, kv[0], kv[1]),
+                                                                   query.order_by)])
+    else:
+        items = sorted(rows.items(), key=lambda kv: kv[0])
+    return dict(items[:size])
+
+
 # ------------------------------------------------------------------------------------------ filtered aggregations
 
 def has_filtered_aggregations(query: QueryContext) -> bool:
@@ -522,9 +611,12 @@ class CPlan:
 
     def __init__(self, table: Table, query: QueryContext, segments: Sequence[ImmutableSegment],
                  seg_keys: Sequence[int], num_groups_limit: Optional[int] = None, flags: int = 0,
-                 trim: bool = False, id_sets=None):
-        """flags: PG_PLAN_*.  trim: let the device apply the query's ORDER BY / LIMIT to the group-by result
-        (IndexedTable.finish + TableResizer; boundary ties kept) -- for a final, single-server answer.
+                 trim=False, id_sets=None, config: Optional["InstanceConfig"] = None):
+        """flags: PG_PLAN_*.  trim (group-by only): True -- the device applies the query's ORDER BY / LIMIT (boundary
+        ties kept: a final, single-server answer); "server" -- the device keeps exactly the rows the reference server's
+        combine keeps (group_trim(query, config): getTableCapacity(limit, minServerGroupTrimSize) under the ORDER BY,
+        `limit` groups without one, all of them when the server trim is off); an int -- exactly that many under the
+        ORDER BY (the per-segment trim).
         id_sets(col_id, data_type, literals, seg_keys) -> (ids [S, n] int32, counts [S]): the IN / NOT_IN literals'
         dictIds in every segment in one call (GpuEngine: pg_dict_id_sets on the resident dictionaries); None = per
         segment on the host."""
@@ -641,7 +733,16 @@ class CPlan:
         lim = num_groups_limit or int(query.options.get("numGroupsLimit", DEFAULT_NUM_GROUPS_LIMIT))
         p.num_groups_limit = lim
         p.flags = flags
-        if trim and query.group_by and query.order_by:
+        size, exact = query.limit, False
+        if trim == "server":   # the reference server's IndexedTable result (group_trim); every group when trim is off
+            size, exact = group_trim(query, config).server_size, True
+        elif not isinstance(trim, bool) and isinstance(trim, int):   # an explicit exact size (per-segment trims)
+            size, exact = trim, True
+        if trim is not False and query.group_by and size is not None and (exact or query.order_by):
+            p.limit = size
+            if exact:
+                p.flags |= abi.PG_PLAN_EXACT_LIMIT
+        if trim is not False and query.group_by and query.order_by and size is not None:
             order = (abi.pg_order * len(query.order_by))()
             for i, o in enumerate(query.order_by):
                 if o.kind == "AGG":
@@ -654,9 +755,20 @@ class CPlan:
             self._keep.append(order)
             p.num_order = len(query.order_by)
             p.order = order
-            p.limit = query.limit
         self.plan = p
         self.ops = ops
+        self._image = None
+
+    def image(self) -> np.ndarray:
+        """The plan as one relocatable byte image (pg_image_header + arrays at offsets, include/pinot_gpu.h): what a
+        Java GpuPlanMaker fills in a direct ByteBuffer.  Built once per plan."""
+        if self._image is None:
+            self._image = abi.build_image(self.plan)
+            self._image_header = abi.pg_image_header.from_buffer(self._image)
+        h, p = self._image_header, self.plan  # the per-call scalars a caller may set on the plan (cancel id, deadline)
+        h.query_id, h.deadline_ms, h.flags, h.limit = p.query_id, p.deadline_ms, p.flags, p.limit
+        h.num_groups_limit = p.num_groups_limit
+        return self._image
 
     @staticmethod
     def _batched_in_ids(preds, segments, seg_keys, cid, id_sets) -> dict:

@@ -52,7 +52,7 @@ def test_library_is_gfx950_only():
 
 
 STRUCTS = ["pg_col_desc", "pg_leaf", "pg_agg", "pg_key", "pg_segment_ref", "pg_order", "pg_plan", "pg_stats",
-           "pg_result", "pg_partials", "pg_timing"]
+           "pg_result", "pg_partials", "pg_timing", "pg_image_header", "pg_image_segment", "pg_image_leaf"]
 
 
 def test_struct_layouts_match_header(tmp_path):
@@ -83,3 +83,93 @@ def test_oracle_is_not_linked_into_product():
     import pinot_amd.gpu as g
     with open(g.__file__) as f:
         assert "oracle" not in f.read().replace("no fallback", "")
+
+
+# ------------------------------------------------------------------ the relocatable plan image (pg_execute_image)
+
+def image_from_bytes(**over):
+    """A one-segment plan image written with struct.pack alone -- offsets, no pointers -- as a Java GpuPlanMaker fills a
+    direct ByteBuffer with putInt / putLong: SELECT COUNT(*) WHERE col0 IN (dictIds 1, 3) over segment key 7.
+    header @0 (120 B) | segment @120 (24 B) | leaf @144 (88 B) | ops @232 | agg @240 (32 B) | ids @272 (2 x int32)."""
+    import struct
+    f = dict(magic=abi.PG_IMAGE_MAGIC, abi=abi.PG_ABI_VERSION, n=280, segments_off=120, leaves_off=144, ops_off=232,
+             aggs_off=240, ids_off=272, num_ids=2, num_segments=1)
+    f.update(over)
+    b = struct.pack("<IIQ8I4Q5Q", f["magic"], f["abi"], f["n"], f["num_segments"], 1, 1, 1, 0, 0, 0, 0,
+                    0, 0, 0, 0, f["segments_off"], f["ops_off"], f["aggs_off"], 0, 0)
+    b += struct.pack("<QIIQ", 7, 1000, 0, f["leaves_off"])
+    b += struct.pack("<4I2iQ2q2d2IQ2I", abi.PG_LEAF_SV_SCAN, 0, 0, f["num_ids"], 0, 0, f["ids_off"], 0, 0, 0.0, 0.0,
+                     0, 0, 0, 0, 0)
+    b += struct.pack("<i", 0) + bytes(4)
+    b += struct.pack("<6Iq", abi.PG_AGG_COUNT, 0, 0, 0, 0, 0, 0)
+    b += struct.pack("<2i", 1, 3)
+    assert len(b) == 280
+    return b
+
+
+def _run_image(lib, b, shift=0):
+    import numpy as np
+    arr = np.zeros(len(b) // 8 + 2, dtype=np.uint64).view(np.uint8)
+    arr[shift:shift + len(b)] = np.frombuffer(b, dtype=np.uint8)
+    res = C.POINTER(abi.pg_result)()
+    rc = lib.pg_execute_image(arr.ctypes.data + shift, len(b), C.byref(res))
+    buf = C.create_string_buffer(512)
+    lib.pg_last_error(buf, 512)
+    return rc, buf.value.decode()
+
+
+def test_plan_image_from_python_bytes():
+    """The image parser accepts a well-formed image built from bytes alone (it then stops at the device: no pg_init
+    here -> PG_E_STATE) and names the first bad field of a malformed one (PG_E_INVALID) before touching a device."""
+    lib = abi.declare(C.CDLL(LIB))
+    rc, msg = _run_image(lib, image_from_bytes())
+    assert rc == abi.PG_E_STATE, msg
+    bad = [dict(magic=0x1234), dict(abi=abi.PG_ABI_VERSION - 1), dict(n=288), dict(segments_off=272),
+           dict(segments_off=121), dict(leaves_off=250), dict(ids_off=274), dict(ids_off=278),
+           dict(num_ids=0), dict(ops_off=4), dict(aggs_off=256), dict(num_segments=2)]
+    for over in bad:
+        b = image_from_bytes(**over)
+        if "n" in over:
+            b = b + bytes(over["n"] - len(b))
+            b = b[:len(b) - 8]  # header says 288, the buffer holds 280
+        rc, msg = _run_image(lib, b)
+        assert rc == abi.PG_E_INVALID and msg.startswith("image"), (over, rc, msg)
+    rc, msg = _run_image(lib, image_from_bytes(), shift=4)
+    assert rc == abi.PG_E_INVALID and "aligned" in msg
+    rc, msg = _run_image(lib, image_from_bytes()[:100])
+    assert rc == abi.PG_E_INVALID
+
+
+def test_plan_image_of_a_lowered_plan(sv_segment):
+    """CPlan.image(): the lowered config-style plan as an image (values-mode IN literals shared by the segments are
+    stored once) that the library's parser accepts."""
+    import numpy as np
+    from pinot_amd.plan import CPlan, Table
+    from pinot_amd.query import parse
+    t = Table("t", [sv_segment] * 3)
+    vals = sv_segment.columns["column9"].dictionary.values
+    lits = ", ".join(str(int(vals[i])) for i in (3, 7, 40, 41, 900))
+    q = parse(f"SELECT column11, SUM(column1) FROM t WHERE column9 IN ({lits}) AND column3 > 5 "
+              "GROUP BY column11 ORDER BY SUM(column1) DESC LIMIT 3")
+    ids = {}
+
+    def id_sets(col_id, dt, lit, keys):  # per-segment dictIds as the device lookup returns them
+        from pinot_amd.plan import dict_id_set
+        d = sv_segment.columns["column9"].dictionary
+        row = dict_id_set(d, list(lit))
+        out = np.zeros((len(keys), len(lit)), dtype=np.int32)
+        out[:, :len(row)] = row
+        return out, np.full(len(keys), len(row), dtype=np.uint32)
+    cp = CPlan(t, q, t.segments, [11, 12, 13], trim="server", id_sets=id_sets)
+    im = cp.image()
+    h = abi.pg_image_header.from_buffer_copy(im.tobytes()[:C.sizeof(abi.pg_image_header)])
+    assert (h.magic, h.num_segments, h.num_leaves, h.image_bytes) == (abi.PG_IMAGE_MAGIC, 3, 2, im.size)
+    assert h.flags & abi.PG_PLAN_EXACT_LIMIT and h.limit == 5000 and h.num_order == 1
+    segs = (abi.pg_image_segment * 3).from_buffer_copy(im.tobytes()[h.segments_off:h.segments_off + 72])
+    leaf_sets = [(abi.pg_image_leaf * 2).from_buffer_copy(im.tobytes()[s.leaves_off:s.leaves_off + 176]) for s in segs]
+    assert [s.seg_key for s in segs] == [11, 12, 13]
+    vo = {ls[0].values_off for ls in leaf_sets}
+    assert len(vo) == 1 and 0 not in vo   # one literal array for every segment
+    lib = abi.declare(C.CDLL(LIB))
+    rc, msg = _run_image(lib, im.tobytes())
+    assert rc == abi.PG_E_STATE, msg

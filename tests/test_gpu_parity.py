@@ -327,6 +327,14 @@ def test_config4_full_segments_match_oracle(gpu_engine, oracle_engine):
     top = np.lexsort((users, -counts))[:q.limit]
     want = [[int(users[i]), int(counts[i])] for i in top]
     assert reduce_to_rows(q, gpu_engine.execute(t, q, flags=0, trim=True))[1] == want
+    # the server's result (GroupByOrderByCombineOperator: getTableCapacity(100, minServerGroupTrimSize = 5 000) rows
+    # under the ORDER BY; the ORDER BY ends in the key, so the kept set is determined): exactly the oracle's top 5 000
+    srv = gpu_engine.execute(t, q, flags=0, trim="server")
+    top = np.lexsort((users, -counts))[:5000]
+    assert len(srv.rows) == 5000
+    assert sorted(k[0] for k in srv.rows) == sorted(users[top].tolist())
+    ku = np.asarray([k[0] for k in srv.rows], dtype=np.int64)
+    assert np.array_equal(np.asarray([v[0] for v in srv.rows.values()]), counts[np.searchsorted(users, ku)])
     for seg in segs:
         gpu_engine.release(seg)
 
@@ -651,3 +659,21 @@ def test_v3_store_segments_on_device(tmp_path, gpu_engine, oracle_engine):
     q = parse("SELECT COUNT(*), MIN(age), MAX(age), SUM(age) FROM t")
     g = gpu_engine.execute(pad, q)
     assert g.rows[()][:4] == [5, 617.0, 1228.0, 617.0 + 824 + 837 + 1209 + 1228]
+
+
+def test_plan_image_and_pointer_plan_agree(gpu_engine, sv_table_inter):
+    """pg_execute_image (the relocatable image a JNI caller passes) and pg_execute (the in-process pointer plan) give
+    identical results for the same lowered plan: every SV query, a values-mode IN over several segments, a server
+    trim; and the partial / finalize pair through images."""
+    from pinot_amd import synth
+    segs = [synth.make_segment_np(synth.ADANALYTICS, s, 100_003) for s in range(3)]
+    ad = Table("adAnalytics", segs)
+    cases = [(sv_table_inter, q) for q in SV_QUERIES] + [(ad, synth.adanalytics_query(20000))]
+    for t, sql in cases:
+        q = parse(sql)
+        for trim in (False, "server"):
+            plan = gpu_engine.make_plan(t, q, trim=trim)
+            a, b = gpu_engine.run_plan(plan, image=True), gpu_engine.run_plan(plan, image=False)
+            assert a.rows == b.rows and a.stats == b.stats, sql
+            c = gpu_engine.finalize_partial(plan, gpu_engine.run_partial(plan, image=True))
+            assert c.rows == a.rows, sql
