@@ -29,7 +29,8 @@ from pinot_amd.query import QueryContext, parse
 from pinot_amd.segment import ImmutableSegment
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(_HERE, "libpinot_oracle.so")
+# PINOT_ORACLE_LIB: the sanitizer build of the same source (tests/test_sanitizers.py)
+LIB = os.environ.get("PINOT_ORACLE_LIB") or os.path.join(_HERE, "libpinot_oracle.so")
 ORC_FWD_SV, ORC_FWD_SORTED, ORC_FWD_MV, ORC_FWD_RAW = 0, 1, 2, 3
 
 

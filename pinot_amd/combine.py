@@ -48,17 +48,29 @@ def _comm(t, group):
 
 
 def allreduce_state(state, group=None) -> None:
-    """In-place merge of a dense partial state across ranks."""
+    """In-place merge of a dense partial state across ranks: SUM of the integer state (and statistics), MIN / MAX of
+    the order-preserving images, and the double state summed in RANK ORDER on every rank (all_gather, then
+    ((r0 + r1) + r2) + ...): the same bits on every rank and in every run, whatever algorithm RCCL picks
+    (a fixed reduction order for reproducible double SUMs)."""
+    import torch
     import torch.distributed as dist
-    ops = {"i64": dist.ReduceOp.SUM, "f64": dist.ReduceOp.SUM, "mn": dist.ReduceOp.MIN, "mx": dist.ReduceOp.MAX,
-           "stats": dist.ReduceOp.SUM}
-    for name in ("i64", "f64", "mn", "mx", "stats"):
+    ops = {"i64": dist.ReduceOp.SUM, "mn": dist.ReduceOp.MIN, "mx": dist.ReduceOp.MAX, "stats": dist.ReduceOp.SUM}
+    for name in ("i64", "mn", "mx", "stats"):
         t = state.get(name)
         if t is not None and t.numel():
             c = _comm(t, group)
             dist.all_reduce(c, op=ops[name], group=group)
             if c is not t:
                 t.copy_(c)
+    f = state.get("f64")
+    if f is not None and f.numel():
+        c = _comm(f, group)
+        parts = [torch.empty_like(c) for _ in range(dist.get_world_size(group))]
+        dist.all_gather(parts, c, group=group)
+        acc = parts[0].clone()
+        for x in parts[1:]:
+            acc += x
+        f.copy_(acc)
 
 
 def _all_gather_ints(vals, group, device):
@@ -71,53 +83,78 @@ def _all_gather_ints(vals, group, device):
     return [o.tolist() for o in out]
 
 
+def _layout_header(err, fp, group, dev):
+    """ONE fixed-size MAX all-reduce every step: [error flag | fingerprint | -fingerprint].  Every rank then holds the
+    same maxima and minima, so every rank takes the same decision (raise, dense all-reduce or row exchange) even when one
+    rank's state layout changed since the last step (a hash table regrown, a DENSE / HASH switch)."""
+    import torch
+    import torch.distributed as dist
+    v = [1 if err is not None else 0] + fp + [-x for x in fp]
+    t = torch.tensor(v, dtype=torch.int64, device=dev)
+    c = _comm(t, group)
+    dist.all_reduce(c, op=dist.ReduceOp.MAX, group=group)
+    h = c.tolist()
+    n = len(fp)
+    return h[0], h[1:1 + n], [-x for x in h[1 + n:]]
+
+
 def merge_partials_across_ranks(engine, plan, p, group=None) -> IntermediateResult:
     """pg_execute_partial result `p` (this rank) -> merged over the process group -> finalized result (every rank
     returns the same merged result).  Consumes `p`.
 
-    Dense states take one collective per query step when they carry only SUMs (config 2): the i64 state and the six
-    statistics travel in ONE buffer (both SUM); MIN / MAX / f64 states add one all-reduce each.  The state layouts are
-    checked across ranks once per plan (they are a function of the plan) rather than every step."""
+    Per step: one MAX all-reduce of a fixed-size header (error flag + state-layout fingerprint, _layout_header), then
+    for dense states the i64 state and the six statistics in ONE SUM all-reduce (config 2: that is all), MIN / MAX
+    all-reduces for MIN / MAX states and an all_gather for double sums (summed in rank order); other states take the
+    row exchange."""
     import torch
-    import torch.distributed as dist
     from .gpu import check
     pc = p.contents
     dev = torch.device("cuda", torch.cuda.current_device())
-    mine = [pc.mode, pc.num_slots, pc.n_i64, pc.n_f64, pc.n_min, pc.n_max, pc.bitmap_words, pc.layout]
-    checked = getattr(plan, "_rank_layouts", None)
-    if checked is None or checked[0] != mine:
-        layouts = _all_gather_ints(mine, group, dev)
-        if any(l[2:] != layouts[0][2:] for l in layouts):
-            engine.lib.pg_partials_free(p)
-            raise ValueError(f"partial state layouts differ across ranks: {layouts} (plan with PG_PLAN_F64_SUMS)")
-        dense_all = all(l[0] == abi.PG_STATE_DENSE and l[1] == layouts[0][1] for l in layouts)
-        plan._rank_layouts = (mine, dense_all)
-    dense_all = plan._rank_layouts[1]
+    fp = [pc.mode, pc.num_slots, pc.n_i64, pc.n_f64, pc.n_min, pc.n_max, pc.bitmap_words, pc.layout]
     st_host = [getattr(pc.stats, f) for f in _STATS_FIELDS]
-    dense_ok = dense_all and pc.bitmap_words == 0 and \
-        pc.num_slots * 8 * (pc.n_i64 + pc.n_f64 + pc.n_min + pc.n_max) <= DENSE_ALLREDUCE_MAX_BYTES
-    if not dense_ok:
-        return _exchange_rows(engine, plan, p, torch.tensor(st_host, dtype=torch.int64, device=dev), group, dev)
     n = pc.num_slots
     ni = n * pc.n_i64
-    sums = torch.empty(ni + len(_STATS_FIELDS), dtype=torch.int64, device=dev)  # i64 state | statistics: one SUM
-    sums[ni:].copy_(torch.tensor(st_host, dtype=torch.int64), non_blocking=False)
-    state = {"i64": sums[:ni],
-             "f64": torch.empty(n * pc.n_f64, dtype=torch.float64, device=dev),
-             "mn": torch.empty(n * pc.n_min, dtype=torch.int64, device=dev),
-             "mx": torch.empty(n * pc.n_max, dtype=torch.int64, device=dev)}
+    dense_mine = pc.mode == abi.PG_STATE_DENSE and pc.bitmap_words == 0 and \
+        n * 8 * (pc.n_i64 + pc.n_f64 + pc.n_min + pc.n_max) <= DENSE_ALLREDUCE_MAX_BYTES
+    err = state = sums = None
     ptr = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None
-    # the library's copies run on its own stream (torch carries its own HIP runtime, so streams do not cross) and
-    # return once done; the statistics' read-back after the collectives is the one host synchronisation between
-    check(engine.lib.pg_partials_copy(p, abi.PG_COPY_OUT, ptr(state["i64"]), ptr(state["f64"]), ptr(state["mn"]),
-                                      ptr(state["mx"]), None))
+    if dense_mine:
+        # the library's copies run on its own stream (torch carries its own HIP runtime, so streams do not cross) and
+        # return once done
+        try:
+            sums = torch.empty(ni + len(_STATS_FIELDS), dtype=torch.int64, device=dev)  # i64 state | statistics
+            sums[ni:].copy_(torch.tensor(st_host, dtype=torch.int64), non_blocking=False)
+            state = {"i64": sums[:ni],
+                     "f64": torch.empty(n * pc.n_f64, dtype=torch.float64, device=dev),
+                     "mn": torch.empty(n * pc.n_min, dtype=torch.int64, device=dev),
+                     "mx": torch.empty(n * pc.n_max, dtype=torch.int64, device=dev)}
+            check(engine.lib.pg_partials_copy(p, abi.PG_COPY_OUT, ptr(state["i64"]), ptr(state["f64"]),
+                                              ptr(state["mn"]), ptr(state["mx"]), None))
+        except Exception as e:  # noqa: BLE001 -- agreed on below, raised on every rank
+            err = e
+    any_err, hi, lo = _layout_header(err, fp, group, dev)
+    if any_err:
+        engine.lib.pg_partials_free(p)
+        if err is not None:
+            raise err
+        raise RuntimeError("the cross-GPU merge failed on another rank")
+    if hi[2:] != lo[2:]:
+        engine.lib.pg_partials_free(p)
+        raise ValueError(f"partial state layouts differ across ranks: max {hi}, min {lo} (plan with PG_PLAN_F64_SUMS)")
+    dense_all = hi[:2] == lo[:2] and hi[0] == abi.PG_STATE_DENSE   # every rank dense over the same slots
+    if not (dense_all and dense_mine):  # dense_mine is a function of the (now known equal) layout: same on all ranks
+        return _exchange_rows(engine, plan, p, torch.tensor(st_host, dtype=torch.int64, device=dev), group, dev)
     allreduce_state({"i64": sums, "f64": state["f64"], "mn": state["mn"], "mx": state["mx"]}, group)
     for f, v in zip(_STATS_FIELDS, sums[ni:].cpu().tolist()):  # waits for the collectives
         setattr(pc.stats, f, int(v))
     if state["f64"].numel() or state["mn"].numel() or state["mx"].numel():
         torch.cuda.synchronize()
-    check(engine.lib.pg_partials_copy(p, abi.PG_COPY_IN, ptr(state["i64"]), ptr(state["f64"]), ptr(state["mn"]),
-                                      ptr(state["mx"]), None))
+    try:
+        check(engine.lib.pg_partials_copy(p, abi.PG_COPY_IN, ptr(state["i64"]), ptr(state["f64"]), ptr(state["mn"]),
+                                          ptr(state["mx"]), None))
+    except Exception:
+        engine.lib.pg_partials_free(p)
+        raise
     return engine.finalize_partial(plan, p)
 
 
@@ -196,6 +233,9 @@ def _exchange_rows(engine, plan, p, stats, group, dev) -> IntermediateResult:
         engine.export_rows(p, world, C.c_void_p(send.data_ptr()), sum(counts))
     except Exception as e:  # noqa: BLE001
         err = e
+        if q is not None:  # created, then the export failed: free the fresh table before every rank raises
+            engine.lib.pg_partials_free(q)
+            q = None
     finally:
         engine.lib.pg_partials_free(p)
     _agree(err, group, dev)

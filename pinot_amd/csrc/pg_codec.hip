@@ -321,6 +321,7 @@ static int huf_read_table(const uint8_t* p, uint64_t n, HufTable& H, uint64_t* u
     if (w[i]) sum += 1u << (w[i] - 1);
   }
   if (!sum) BAD("zstd: empty Huffman tree");
+  if (nw > 255) BAD("zstd: too many Huffman weights");  // the implied last weight is the 256th symbol at most
   const uint32_t max_bits = (uint32_t)highbit(sum) + 1;
   const uint32_t left = (1u << max_bits) - sum;
   if (left & (left - 1)) BAD("zstd: Huffman weights do not complete a tree");
@@ -572,16 +573,17 @@ static int zstd(const uint8_t* p, uint64_t n, uint8_t* dst, uint64_t cap, uint64
     const uint8_t fhd = p[pos++];
     const uint32_t fcs_flag = fhd >> 6, single = (fhd >> 5) & 1, checksum = (fhd >> 2) & 1, did_flag = fhd & 3;
     if (fhd & 8) BAD("zstd: reserved frame header bit");
-    if (!single) pos += 1;  // window descriptor (the whole chunk is decoded into one buffer)
     static const uint32_t did_size[4] = {0, 1, 2, 4};
+    static const uint32_t fcs_size[4] = {0, 2, 4, 8};
+    const uint32_t fs = fcs_flag == 0 ? (single ? 1 : 0) : fcs_size[fcs_flag];
+    // window descriptor + dictionary id + frame content size, all inside the chunk before any of them is read
+    if ((uint64_t)pos + (single ? 0 : 1) + did_size[did_flag] + fs > n) BAD("zstd: truncated frame header");
+    if (!single) pos += 1;  // window descriptor (the whole chunk is decoded into one buffer)
     uint64_t did = 0;
     for (uint32_t i = 0; i < did_size[did_flag]; i++) did |= (uint64_t)p[pos + i] << (8 * i);
     pos += did_size[did_flag];
     if (did) return PG_E_UNSUPPORTED;  // dictionaries: never written by Pinot
-    static const uint32_t fcs_size[4] = {0, 2, 4, 8};
-    const uint32_t fs = fcs_flag == 0 ? (single ? 1 : 0) : fcs_size[fcs_flag];
     pos += fs;
-    if (pos > n) BAD("zstd: truncated frame header");
     ZState Z;
     for (;;) {
       if (pos + 3 > n) BAD("zstd: truncated block header");

@@ -537,10 +537,12 @@ __device__ __forceinline__ int32_t dict_find(const T* __restrict__ d, uint32_t c
     // vlo = d[lo] <= x <= vhi = d[hi - 1]
     const double span = (double)vhi - (double)vlo;
     uint32_t pos = lo;
-    if (span > 0) {
+    if (span > 0 && span <= __DBL_MAX__) {  // finite: an infinite bound or a NaN literal takes the binary search
       const double f = ((double)x - (double)vlo) / span;
-      pos = lo + (uint32_t)(f * (double)(hi - 1 - lo));
-      pos = pos < lo ? lo : (pos > hi - 1 ? hi - 1 : pos);
+      if (f >= 0.0 && f <= 1.0) {  // (false for NaN) so the conversion below is defined
+        pos = lo + (uint32_t)(f * (double)(hi - 1 - lo));
+        pos = pos < lo ? lo : (pos > hi - 1 ? hi - 1 : pos);
+      }
     }
     const T v = d[pos];
     if (v == x) return (int32_t)pos;

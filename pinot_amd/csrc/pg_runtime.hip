@@ -3613,40 +3613,46 @@ int build_result(pg_partials* pp, const pg_plan* plan, pg_result** out, const Pa
   };
   std::vector<uint64_t> perm(nc);
   for (uint64_t i = 0; i < nc; i++) perm[i] = i;
-  if (K && plan->num_order) {
-    auto val = [&](uint64_t i, uint32_t a) {
-      double x = hv[i * A + a];
-      if (P.aggs[a].fn == PG_AGG_AVG) {
-        const int64_t c = hc[i * A + a];
-        x = c ? x / (double)c : -INFINITY;
-      }
-      return x;
-    };
-    std::sort(perm.begin(), perm.end(), [&](uint64_t i, uint64_t j) {
+  const bool exact = K && (plan->flags & PG_PLAN_EXACT_LIMIT) && plan->limit && nc > plan->limit;
+  if (K && (plan->num_order || exact)) {
+    // one row of order images per candidate (ascending = ranks first): the ORDER BY items, then the key ids (first key
+    // first); AGG items as the order-preserving image of the final double, DESC items complemented
+    const uint32_t W = plan->num_order + K;
+    std::vector<uint64_t> ok(nc * W);
+    for (uint64_t i = 0; i < nc; i++) {
+      uint64_t* row = ok.data() + i * W;
       for (uint32_t o = 0; o < plan->num_order; o++) {
         const pg_order& it = plan->order[o];
+        uint64_t x;
         if (it.kind == PG_ORDER_AGG) {
-          const double x = val(i, it.index), y = val(j, it.index);
-          if (x != y) return it.desc ? x > y : x < y;
+          double v = hv[i * A + it.index];
+          if (P.aggs[it.index].fn == PG_AGG_AVG) {
+            const int64_t c = hc[i * A + it.index];
+            v = c ? v / (double)c : -INFINITY;
+          }
+          if (v == 0) v = 0;  // -0.0 ties with 0.0, as the double comparison does
+          int64_t bits;
+          memcpy(&bits, &v, 8);
+          x = bits >= 0 ? ((uint64_t)bits | 0x8000000000000000ull) : ~(uint64_t)bits;
         } else {
-          const uint64_t x = key_id(i, it.index), y = key_id(j, it.index);
-          if (x != y) return it.desc ? x > y : x < y;
+          x = key_id(i, it.index);
         }
+        row[o] = it.desc ? ~x : x;
       }
-      for (uint32_t k = 0; k < K; k++)  // ascending key ids, first key first
-        if (key_id(i, k) != key_id(j, k)) return key_id(i, k) < key_id(j, k);
+      for (uint32_t k = 0; k < K; k++) row[plan->num_order + k] = key_id(i, k);
+    }
+    auto before = [&](uint64_t i, uint64_t j) {
+      const uint64_t *x = ok.data() + i * W, *y = ok.data() + j * W;
+      for (uint32_t w = 0; w < W; w++)
+        if (x[w] != y[w]) return x[w] < y[w];
       return false;
-    });
-  } else if (K && (plan->flags & PG_PLAN_EXACT_LIMIT) && plan->limit && nc > plan->limit) {
-    // no ORDER BY: the `limit` groups of smallest key ids (first key first)
-    std::sort(perm.begin(), perm.end(), [&](uint64_t i, uint64_t j) {
-      for (uint32_t k = 0; k < K; k++)
-        if (key_id(i, k) != key_id(j, k)) return key_id(i, k) < key_id(j, k);
-      return false;
-    });
+    };
+    // an exact limit needs only its first `limit` rows in order
+    if (exact) std::partial_sort(perm.begin(), perm.begin() + plan->limit, perm.end(), before);
+    else std::sort(perm.begin(), perm.end(), before);
   }
   // PG_PLAN_EXACT_LIMIT: the first `limit` rows of that order (the server result / the per-segment trim)
-  if (K && (plan->flags & PG_PLAN_EXACT_LIMIT) && plan->limit && nc > plan->limit) nc = plan->limit;
+  if (exact) nc = plan->limit;
 
   pg_result* r = (pg_result*)calloc(1, sizeof(pg_result));
   if (!r) return fail(PG_E_NOMEM, "out of host memory");

@@ -313,8 +313,15 @@ class GpuEngine:
 
     @staticmethod
     def decode(plan: CPlan, r) -> IntermediateResult:
-        """pg_result (or its result_arrays) -> value-keyed IntermediateResult."""
+        """pg_result (or its result_arrays) -> value-keyed IntermediateResult.  The arrays are copied out of the
+        library's result here; the value-keyed rows (Python objects, the form the tests and the DataTable writer read)
+        are built on first access to `.rows` (DeviceResult)."""
         ra = r if isinstance(r, dict) else GpuEngine.result_arrays(r)
+        st = ExecutionStats(*ra["stats"].tolist())
+        return DeviceResult(plan.aggs, list(plan.query.group_by), lambda: GpuEngine._rows(plan, ra), st, ra)
+
+    @staticmethod
+    def _rows(plan: CPlan, ra: dict) -> dict:
         A, K, G = ra["A"], ra["K"], ra["G"]
         vals, cnts, keys = ra["values"], ra["counts"], ra["keys"]
         sets = None
@@ -348,6 +355,26 @@ class GpuEngine:
                 acols.append([ds.values_of(ids[offs[g * A + a]:offs[g * A + a + 1]]) for g in range(G)])
             else:
                 acols.append(v.astype(np.float64).tolist())
-        rows = dict(zip(keyt, map(list, zip(*acols)))) if A else {k: [] for k in keyt}
-        st = ExecutionStats(*ra["stats"].tolist())
-        return IntermediateResult(plan.aggs, list(plan.query.group_by), rows, st)
+        return dict(zip(keyt, map(list, zip(*acols)))) if A else {k: [] for k in keyt}
+
+
+class DeviceResult(IntermediateResult):
+    """An IntermediateResult whose value-keyed rows are materialised from the device result's arrays (`arrays`:
+    GpuEngine.result_arrays) on first access."""
+
+    def __init__(self, aggregations, group_by, make_rows, stats, arrays):
+        self._make = make_rows
+        self._rows = None
+        self.arrays = arrays
+        super().__init__(aggregations, group_by, None, stats)
+
+    @property
+    def rows(self):
+        if self._make is not None:
+            self._rows, self._make = self._make(), None
+        return self._rows
+
+    @rows.setter
+    def rows(self, v):
+        if v is not None:
+            self._rows, self._make = v, None

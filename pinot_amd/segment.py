@@ -356,13 +356,32 @@ def chunk_compress(codec: int, data: bytes) -> bytes:
 def chunk_decompress(codec: int, data: bytes, cap: int) -> bytes:
     """ChunkDecompressor.decompress of one chunk through libpinot_gpu (pg_chunk_decompress, pinot_codec.h)."""
     import ctypes as C
-    from .gpu import check, load_library
-    lib = load_library()
+    from .gpu import PinotGpuError, check, load_library
+    alt = os.environ.get("PINOT_CODEC_LIB")  # the sanitizer build of the same decoders (tests/test_sanitizers.py)
+    lib = _codec_lib(alt) if alt else load_library()
     src = np.frombuffer(data, dtype=np.uint8) if data else np.zeros(1, dtype=np.uint8)
     dst = np.empty(max(cap, 1), dtype=np.uint8)
     n = C.c_uint64()
-    check(lib.pg_chunk_decompress(codec, src.ctypes.data, len(data), dst.ctypes.data, cap, C.byref(n)))
+    rc = lib.pg_chunk_decompress(codec, src.ctypes.data, len(data), dst.ctypes.data, cap, C.byref(n))
+    if alt and rc:
+        raise PinotGpuError(rc, "chunk decompression failed")
+    check(rc)
     return dst[:n.value].tobytes()
+
+
+_CODEC_LIBS: dict = {}
+
+
+def _codec_lib(path: str):
+    import ctypes as C
+    lib = _CODEC_LIBS.get(path)
+    if lib is None:
+        lib = C.CDLL(path)
+        lib.pg_chunk_decompress.argtypes = [C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                            C.POINTER(C.c_uint64)]
+        lib.pg_chunk_decompress.restype = C.c_int
+        _CODEC_LIBS[path] = lib
+    return lib
 
 
 def raw_forward_bytes(values, data_type: str, version: int = 2, docs_per_chunk: int = RAW_DOCS_PER_CHUNK,

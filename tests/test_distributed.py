@@ -46,11 +46,42 @@ def _worker_state(rank, world, port, q):
         parts = [torch.empty_like(v) for _ in range(world)]
         dist.all_gather(parts, v)
         allg[k] = torch.stack(parts)
-    ok = (torch.equal(st["i64"], allg["i64"].sum(0)) and torch.allclose(st["f64"], allg["f64"].sum(0))
+    ordered = allg["f64"][0].clone()
+    for r in range(1, world):
+        ordered += allg["f64"][r]
+    again = {"f64": orig["f64"].clone()}
+    allreduce_state(again)
+    ok = (torch.equal(st["i64"], allg["i64"].sum(0)) and torch.equal(st["f64"], ordered)
+          and torch.equal(again["f64"], st["f64"])
           and torch.equal(st["mn"], allg["mn"].min(0).values) and torch.equal(st["mx"], allg["mx"].max(0).values)
           and torch.equal(st["stats"], torch.tensor([world * (world + 1) // 2] * 6)))
     q.put((rank, ok))
     dist.destroy_process_group()
+
+
+def _worker_header(rank, world, port, q):
+    """The per-step layout header (combine._layout_header): every rank sees the same error flag and the same
+    fingerprint maxima / minima, so all of them take the same branch even when only one rank's layout changed."""
+    _init(rank, world, port)
+    from pinot_amd.combine import _layout_header
+    dev = torch.device("cpu")
+    same = [0, 365, 3, 0, 0, 0, 0, 3]
+    out = [_layout_header(None, list(same), None, dev)]
+    changed = list(same) if rank == 0 else [1, 1 << 20, 3, 0, 0, 0, 0, 3]   # rank 1 regrew into a hash table
+    out.append(_layout_header(None, changed, None, dev))
+    out.append(_layout_header(RuntimeError("x") if rank == 1 else None, list(same), None, dev))
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_layout_header_gives_every_rank_the_same_decision():
+    res = _run(_worker_header)
+    (_, a), (_, b) = res
+    assert a == b
+    eq, chg, err = a
+    assert eq[0] == 0 and eq[1] == eq[2]                       # no error, identical layouts: dense all-reduce
+    assert chg[0] == 0 and chg[1][:2] != chg[2][:2] and chg[1][2:] == chg[2][2:]   # mixed modes: row exchange
+    assert err[0] == 1                                         # one rank failed: every rank raises
 
 
 def _worker_sharded(rank, world, port, q):

@@ -73,6 +73,14 @@ def _worker(rank, world, port, q):
             merged = merge_partials_across_ranks(eng, plan, p)
             whole = OracleEngine().execute(table, qc)
             assert_same_result(merged, whole, table=table)
+        # the state layout of ONE rank changes between steps (rank 0 groups in a hash table at step 2): the per-step
+        # layout header gives both ranks the same decision (row exchange at step 2, dense all-reduce around it)
+        qc = parse(synth.adanalytics_query(1000))
+        whole = OracleEngine().execute(table, qc)
+        for hash_rank0 in (False, True, False):
+            flags = abi.PG_PLAN_VALUE_SETS | (abi.PG_PLAN_HASH_GROUPS if hash_rank0 and rank == 0 else 0)
+            plan = eng.make_plan(table, qc, segments=mine, flags=flags)
+            assert_same_result(merge_partials_across_ranks(eng, plan, eng.run_partial(plan)), whole, table=table)
         q.put((rank, True, paths))
         dist.destroy_process_group()
     except Exception:

@@ -366,6 +366,18 @@ def test_dict_id_sets_on_device(dtype, gpu_engine, oracle_engine):
                 f"SELECT m, COUNT(*) FROM t WHERE k NOT IN ({in_list}) GROUP BY m"]:
         q = parse(sql)
         assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q), table=t)
+    if dtype in ("FLOAT", "DOUBLE"):
+        # NaN / +-inf literals and a dictionary with infinite bounds: the lookup's interpolation step stays defined
+        # (finite span, 0 <= f <= 1) and the binary search finds exactly what the host finds
+        odd = [float("nan"), float("inf"), float("-inf"), 0.25, -1250.0]
+        inf_seg = ImmutableSegment.create("dinf", {"k": np.asarray([-np.inf, -3.5, 0.25, 7.0, np.inf] * 1000),
+                                                  "m": np.arange(5000, dtype=np.int64) % 7}, {"k": dtype, "m": "INT"})
+        t2 = Table("t", segs[:2] + [inf_seg])
+        keys2 = [gpu_engine.upload_segment(s, t2) for s in t2.segments]
+        lit = np.asarray(sorted(x for x in odd if x == x) + [float("nan")])
+        ids2, counts2 = gpu_engine.dict_id_sets(t2.column_ids["k"], dtype, lit, keys2)
+        for si, s in enumerate(t2.segments):
+            assert np.array_equal(ids2[si, :counts2[si]], dict_id_set(s.columns["k"].dictionary, list(lit))), si
 
 
 def test_in_literals_on_mv_scan_leaves(gpu_engine, oracle_engine):

@@ -344,3 +344,13 @@ def _compressed_table():
     if not _COMPRESSED:
         _COMPRESSED.append(Table("t", _raw_segments(3, 40_000, seed=9, codecs=CODEC_MIX)))
     return _COMPRESSED[0]
+
+
+def test_chunk_decoders_fuzzed_under_sanitizers(tmp_path):
+    """Malformed chunks (truncated, bit-flipped, overwritten, short output buffers; a few hundred per codec and chunk)
+    through the decoders built with -fsanitize=address,undefined: every one decodes or is rejected, none reads or
+    writes out of bounds (tests/test_sanitizers.py, tests/sanitize/codec_fuzz.cpp)."""
+    import subprocess
+    from test_sanitizers import SAN, test_chunk_decoders_under_sanitizers
+    subprocess.run(["make", "-s", "-C", SAN], check=True)
+    test_chunk_decoders_under_sanitizers(os.path.join(SAN, "build"), tmp_path)
