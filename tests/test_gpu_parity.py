@@ -689,3 +689,50 @@ def test_plan_image_and_pointer_plan_agree(gpu_engine, sv_table_inter):
             assert a.rows == b.rows and a.stats == b.stats, sql
             c = gpu_engine.finalize_partial(plan, gpu_engine.run_partial(plan, image=True))
             assert c.rows == a.rows, sql
+
+
+def _full_device_segments(gpu_engine, specs, table_name, n_segs, seg0=0):
+    """n_segs full 7 812 500-row segments generated on the device (as bench.py does) + their host copies."""
+    import torch
+    from pinot_amd import synth
+    dev = torch.device("cuda", 0)
+    rows = synth.ADANALYTICS_ROWS_PER_SEGMENT
+    segs, host, bits = [], [], []
+    table = None
+    for si in range(seg0, seg0 + n_segs):
+        dcs = synth.make_columns_torch(specs, si, rows, dev)
+        seg = ImmutableSegment(f"{table_name}_{si}", rows, {dc.spec.name: dc.meta_column() for dc in dcs})
+        host.append(ImmutableSegment(f"{table_name}_{si}", rows, {dc.spec.name: dc.host_column() for dc in dcs}))
+        bits.append({dc.spec.name: (dc.bits, dc.cardinality) for dc in dcs})
+        if table is None:
+            table = Table(table_name, [seg])
+        gpu_engine.register_device_segment(seg, table, dcs)
+        segs.append(seg)
+        del dcs
+    return Table(table_name, segs), Table(table_name, host), bits
+
+
+@pytest.mark.parametrize("config", ["adanalytics", "ssb"])
+def test_full_size_segments_match_oracle(config, gpu_engine):
+    """Configs 2 and 3 at their stated segment size: full 7 812 500-row device-generated segments (2 for config 2, 3 for
+    config 3), through the selective stream (scan_launches == 2: stream_kernel + the list-mode scan) -- for config 2 the
+    benchmark's own kernel instance, accountId at 20 bits with a <= 1 M-id exact LUT -- against the oracle over the
+    same segments' host bytes."""
+    from oracle.oracle import OracleEngine
+    from pinot_amd import synth
+    specs, name, n, sql = ((synth.ADANALYTICS, "adAnalytics", 2, synth.adanalytics_query(1000)) if config == "adanalytics"
+                           else (synth.SSB_LINEORDER, "lineorder", 3, synth.ssb_q11_query()))
+    t, ht, bits = _full_device_segments(gpu_engine, specs, name, n, seg0=5)
+    try:
+        if config == "adanalytics":
+            assert all(b["accountId"][0] == 20 and b["accountId"][1] <= 1 << 20 for b in bits)
+        q = parse(sql)
+        for trim in (False, "server"):
+            g = gpu_engine.execute(t, q, flags=0, trim=trim)
+            assert gpu_engine.last_timing().scan_launches == 2, "the selective stream did not run"
+            o = OracleEngine(threads=8).execute(ht, q)
+            assert_same_result(g, o, table=ht)
+            assert g.stats.num_docs_scanned > 0
+    finally:
+        for seg in t.segments:
+            gpu_engine.release(seg)

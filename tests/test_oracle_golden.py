@@ -118,3 +118,88 @@ def test_baseball_oracle_matches_pandas():
         s = sub.groupby("playerName")["runs"].sum().reset_index()
         s = s.sort_values(["runs", "playerName"], ascending=[False, True]).head(10)
         assert rows == [[n, float(r)] for n, r in zip(s.playerName, s.runs)]
+
+
+def _adanalytics_values(segs_n):
+    import numpy as np
+    from pinot_amd import synth
+    cols = {c.name: [] for c in synth.ADANALYTICS}
+    for s, n in segs_n:
+        for c in synth.ADANALYTICS:
+            cols[c.name].append(synth.values_np(c, s * n, n))
+    return {k: np.concatenate(v) for k, v in cols.items()}
+
+
+def test_adanalytics_lowering_pinned_by_numpy():
+    """Config 2's SQL evaluated directly in numpy over the generator's values == the oracle over the lowered plan:
+    pins plan.py's lowering (IN over a ~1 M-entry dictionary -> per-segment dictId sets, BETWEEN -> [lo, hi) on the
+    sorted dictionary, NOT IN -> exclusive sets) independently of the pg_plan the GPU and the oracle share."""
+    import numpy as np
+    from oracle.oracle import OracleEngine
+    from pinot_amd import synth
+    from pinot_amd.plan import Table
+    from pinot_amd.query import parse
+    segs_n = [(0, 150_001), (7, 120_007)]
+    segs = [synth.make_segment_np(synth.ADANALYTICS, s, n) for s, n in segs_n]
+    v = _adanalytics_values(segs_n)
+    t = Table("adAnalytics", segs)
+    orc = OracleEngine()
+    for num_ids in (1000, 20_000):
+        ids = np.asarray([(i * 7919 + 13) % 1_000_000 for i in range(num_ids)])
+        sql = synth.adanalytics_query(num_ids)
+        for neg in (False, True):
+            q = parse(sql.replace("accountId IN", "accountId NOT IN") if neg else sql)
+            m = (v["daysSinceEpoch"] >= 18000) & (v["daysSinceEpoch"] <= 18089) & (np.isin(v["accountId"], ids) ^ neg)
+            r = orc.execute(t, q)
+            assert r.stats.num_docs_scanned == int(m.sum())
+            days = np.unique(v["daysSinceEpoch"][m])
+            want = {(int(d),): [float(v["clicks"][m & (v["daysSinceEpoch"] == d)].sum()),
+                                float(v["impressions"][m & (v["daysSinceEpoch"] == d)].sum())] for d in days}
+            assert r.rows == want, (num_ids, neg)
+    # BETWEEN bounds that fall between dictionary values, and outside the value range
+    for lo, hi in ((17899, 17905), (18263, 19000), (18000, 18000), (17000, 17800)):
+        q = parse(f"SELECT COUNT(*), SUM(clicks) FROM adAnalytics WHERE daysSinceEpoch BETWEEN {lo} AND {hi}")
+        m = (v["daysSinceEpoch"] >= lo) & (v["daysSinceEpoch"] <= hi)
+        r = orc.execute(t, q)
+        assert r.rows[()] == [int(m.sum()), float(v["clicks"][m].sum())], (lo, hi)
+
+
+def test_index_path_lowering_pinned_by_numpy():
+    """Config 5's SQL (sorted-index range, an OR of an inverted EQ and IN, an inverted NOT_EQ, an inverted IN of 2 000
+    ids, COUNTMV) and variants with NOT IN / NOT BETWEEN / OR at the root, evaluated directly in numpy == the oracle
+    over the lowered plan (sorted ranges, inverted dictId sets and the NOT_EQ flip pinned independently)."""
+    import numpy as np
+    from oracle.oracle import OracleEngine
+    from pinot_amd import abi, synth
+    from pinot_amd.plan import Table
+    from pinot_amd.query import parse
+    segs_n = [(0, 60_001), (5, 70_003)]
+    segs = [synth.make_index_segment_np(s, n) for s, n in segs_n]
+    vals = [synth.index_values_np(s, n) for s, n in segs_n]
+    v = {k: np.concatenate([x[k] for x in vals]) for k in ("sortedCol", "inv1", "inv2", "inv3", "inv4")}
+    nvals = np.concatenate([np.asarray([len(t) for t in x["mvTags"]]) for x in vals])
+    t = Table("idx", segs)
+    inv4 = np.asarray([i * 5 + 1 for i in range(2000)])
+    inv2 = np.asarray([i * 5 for i in range(20)])
+    rest = ((v["sortedCol"] >= 20000) & (v["sortedCol"] <= 59999) & ((v["inv1"] == 3) | np.isin(v["inv2"], inv2))
+            & (v["inv3"] != 7))
+    base = rest & np.isin(v["inv4"], inv4)
+    ids = ", ".join(str(x) for x in inv4)
+    cases = [(synth.index_query(), base),
+             (synth.index_query().replace("inv4 IN", "inv4 NOT IN"), rest & ~np.isin(v["inv4"], inv4)),
+             ("SELECT COUNT(*), COUNTMV(mvTags) FROM idx WHERE NOT sortedCol BETWEEN 1000 AND 98999 OR inv3 = 999",
+              ~((v["sortedCol"] >= 1000) & (v["sortedCol"] <= 98999)) | (v["inv3"] == 999)),
+             (f"SELECT COUNT(*), COUNTMV(mvTags) FROM idx WHERE sortedCol <> 50000 AND inv2 NOT IN (0, 1, 2) "
+              f"AND inv4 IN ({ids})",
+              (v["sortedCol"] != 50000) & ~np.isin(v["inv2"], [0, 1, 2]) & np.isin(v["inv4"], inv4))]
+    orc = OracleEngine()
+    for sql, m in cases:
+        q = parse(sql)
+        r = orc.execute(t, q)
+        assert r.rows[()] == [int(m.sum()), int(nvals[m].sum())], sql[:120]
+    # and the leaf operators the lowering chose (FilterOperatorUtils.getLeafFilterOperator)
+    from pinot_amd.plan import CPlan
+    p = CPlan(t, parse(synth.index_query()), segs, [1, 2])
+    kinds = {pred.column: lw.kind for pred, lw in zip(p.leaf_preds, p.lowered[0])}
+    assert kinds == {"sortedCol": abi.PG_LEAF_SORTED, "inv1": abi.PG_LEAF_INVERTED, "inv2": abi.PG_LEAF_INVERTED,
+                     "inv3": abi.PG_LEAF_INVERTED, "inv4": abi.PG_LEAF_INVERTED}
