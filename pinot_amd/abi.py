@@ -133,12 +133,32 @@ class pg_timing(C.Structure):
                 ("finalize_wall_ms", C.c_float), ("prefilter_ms", C.c_float)]
 
 
-# every symbol declared in include/pinot_gpu.h (checked by tests/test_abi.py)
+# pinot_trace.h
+PG_TRACE_MAX_LEAVES = 16
+LEAF_FORMS = ["MATCH_ALL", "EMPTY", "SCAN_RANGE", "SCAN_SET_LDS", "SCAN_SET_LUT", "SORTED_RANGE", "SORTED_BITMAP",
+              "INVERTED", "MV_SCAN", "RAW_SCAN", "RANGE_INDEX"]
+PG_PATH_FUSED_SCAN, PG_PATH_STREAM, PG_PATH_PARTITIONED, PG_PATH_WIDE_KEYS, PG_PATH_NONSCAN, PG_PATH_PREPASS = \
+    0x1, 0x2, 0x4, 0x8, 0x10, 0x20
+PATH_NAMES = {PG_PATH_FUSED_SCAN: "fused_scan", PG_PATH_STREAM: "stream", PG_PATH_PARTITIONED: "partitioned",
+              PG_PATH_WIDE_KEYS: "wide_keys", PG_PATH_NONSCAN: "nonscan", PG_PATH_PREPASS: "prepass"}
+PG_RERUN_STREAM, PG_RERUN_PARTITION, PG_RERUN_HASH = 0x1, 0x2, 0x4
+
+
+class pg_trace(C.Structure):
+    _fields_ = [("query_id", C.c_uint64), ("path", C.c_uint32), ("group_mode", C.c_uint32), ("reruns", C.c_uint32),
+                ("rerun_reasons", C.c_uint32), ("num_leaves", C.c_uint32), ("stream_leaf", C.c_uint32),
+                ("leaf_forms", (C.c_uint32 * len(LEAF_FORMS)) * PG_TRACE_MAX_LEAVES), ("pad", C.c_uint32),
+                ("num_segments", C.c_uint64), ("num_segments_nonscan", C.c_uint64),
+                ("num_docs_matched", C.c_uint64), ("num_slots", C.c_uint64), ("device_ms", C.c_float),
+                ("wall_ms", C.c_float)]
+
+
+# every symbol declared in include/*.h (checked by tests/test_abi.py)
 EXPORTED = ["pg_init", "pg_last_error", "pg_resident_bytes", "pg_cancel", "pg_abi_version", "pg_column_upload",
             "pg_segment_release", "pg_execute", "pg_result_free", "pg_execute_partial", "pg_partials_finalize",
             "pg_partials_free", "pg_partials_copy", "pg_partials_export", "pg_partials_create", "pg_partials_merge",
             "pg_key_owner", "pg_last_timing", "pg_chunk_decompress", "pg_dict_id_sets", "pg_execute_image",
-            "pg_execute_partial_image", "pg_partials_finalize_image"]
+            "pg_execute_partial_image", "pg_partials_finalize_image", "pg_last_trace"]
 PG_CODEC_PASS_THROUGH, PG_CODEC_SNAPPY, PG_CODEC_ZSTANDARD, PG_CODEC_LZ4, PG_CODEC_LZ4_LENGTH_PREFIXED = 0, 1, 2, 3, 4
 PG_COPY_OUT, PG_COPY_IN = 0, 1
 
@@ -171,6 +191,7 @@ def declare(lib):
         "pg_key_owner": ([C.c_uint64, C.c_uint32], C.c_uint32),
         "pg_chunk_decompress": ([C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, P(C.c_uint64)], C.c_int),
         "pg_execute_image": ([C.c_void_p, C.c_uint64, P(P(pg_result))], C.c_int),
+        "pg_last_trace": ([P(pg_trace)], C.c_int),
         "pg_execute_partial_image": ([C.c_void_p, C.c_uint64, P(P(pg_partials))], C.c_int),
         "pg_partials_finalize_image": ([P(pg_partials), C.c_void_p, C.c_uint64, P(P(pg_result))], C.c_int),
     }

@@ -70,6 +70,17 @@ __device__ __forceinline__ uint32_t value_at(const uint32_t (&w)[B + 1], int j) 
   return __builtin_amdgcn_alignbit(w[k], w[k + 1], 64u - o - B) & M;
 }
 
+// value j of the group in the low B bits, with whatever bits precede it above them (no mask): for lookups that mask
+// the index themselves and bit tests whose offset is taken mod 32
+template <int B>
+__device__ __forceinline__ uint32_t value_raw(const uint32_t (&w)[B + 1], int j) {
+  const uint32_t s = (uint32_t)j * B, k = s >> 5, o = s & 31u;
+  if (o + B <= 32) return w[k] >> (32u - o - B);
+  return __builtin_amdgcn_alignbit(w[k], w[k + 1], 64u - o - B);
+}
+
+typedef const __attribute__((address_space(3))) uint32_t* lds_cptr;
+
 // value `idx` of a `b`-bit packed column through its buffer descriptor (a 64-bit window of two words)
 __device__ __forceinline__ uint32_t unpack_win(rsrc_t r, uint32_t idx, uint32_t b) {
   const uint64_t pbit = (uint64_t)idx * b;
@@ -88,11 +99,21 @@ __device__ __forceinline__ uint32_t eval_group(const LeafDesc& L, const uint32_t
   uint32_t w[B + 1];
   load_group<B>(rsrc_of(L.words, L.wbytes), g, w);
   uint32_t m = 0;
-  if (exact) {  // SET_LDS with its exact LUT over dictIds staged at lds_sets[0]
+  if (exact) {
+    // SET_LDS with its exact LUT over dictIds staged at lds_sets[0], which is LDS address 0 (stream_kernel has no
+    // static LDS; checked at its start): the word's byte address is the LDS address itself, and v_bfe_u32 takes the
+    // bit offset mod 32 -- per value one extract, two ops of address, the read, v_bfe_u32 and v_lshl_or_b32
+    constexpr uint32_t M = B == 32 ? 0xFFFFFFFFu : ((1u << B) - 1u);
 #pragma unroll
-    for (int j = 0; j < 32; j++) {
-      const uint32_t v = value_at<B>(w, j);
-      m |= ((lds_sets[v >> 5] >> (v & 31u)) & 1u) << j;
+    for (int j0 = 0; j0 < 32; j0 += 8) {  // 8 reads in flight per wait
+      uint32_t r[8], word[8];
+#pragma unroll
+      for (int x = 0; x < 8; x++) {
+        r[x] = value_raw<B>(w, j0 + x);
+        word[x] = *(lds_cptr)(uintptr_t)(((r[x] & M) >> 5) << 2);
+      }
+#pragma unroll
+      for (int x = 0; x < 8; x++) m |= __builtin_amdgcn_ubfe(word[x], r[x], 1u) << (j0 + x);
     }
   } else if (L.kind == LK_RANGE) {
     const uint32_t lo = (uint32_t)L.lo, span = (uint32_t)(L.hi - L.lo);
@@ -287,11 +308,21 @@ __device__ __forceinline__ void stage_slice(const LeafDesc& X, uint32_t wg0, uin
 // EXTRA: further AND leaves tested on the survivors (their code costs registers: 78 VGPRs / 6 waves per SIMD with,
 // 72 / 7 without).  Items: contiguous ranges per block (block_first), or with `interleave` item b + k * gridDim.x.
 // NT: threads per block.  NT = 1024 is exact mode (p.exact_nwords): one block per CU holding the exact LUT.
+constexpr uint32_t kExactLutWords = 32768;  // 128 KiB: the exact LUT of a <= 1 M-entry dictionary
+
+// Words of dynamic LDS the stream's sets / LUT / slices take; the block's append cursor is the word after them (no
+// static LDS in the kernel, so the exact LUT sits at LDS address 0).
+__host__ __device__ __forceinline__ uint32_t stream_lds_words(const StreamSpec& p, bool exact) {
+  return exact ? kExactLutWords : p.set_lds_ints + (p.num_extra ? 4u * p.stage_words : 0u);
+}
+
 template <int B, bool EXTRA, int NT>
 __global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? 6 : 7)) void stream_kernel(StreamSpec p) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_sets[];
-  __shared__ uint32_t cursor;
   constexpr bool EXACT = NT == 1024;
+  uint32_t& cursor = lds_sets[stream_lds_words(p, EXACT)];
+  // the exact LUT's lookups address LDS absolutely (eval_group): the dynamic LDS must start at address 0
+  if (EXACT && threadIdx.x == 0 && (uint32_t)(uintptr_t)(lds_cptr)lds_sets != 0u) atomicOr(p.err, 64u);
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t i0 = p.interleave ? ldcf(p.block_first, 0) + blockIdx.x : ldcf(p.block_first, blockIdx.x);
   const uint32_t i1 = ldcf(p.block_first, p.interleave ? gridDim.x : blockIdx.x + 1);
@@ -377,12 +408,11 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? 6 : 7)) void stream_k
 
 hipError_t launch_stream(const StreamSpec& p, uint32_t bits, uint32_t blocks, hipStream_t s) {
   if (!p.num_items || !blocks) return hipSuccess;
-  const size_t lds = p.exact_nwords ? (size_t)128 * 1024
-                                    : (size_t)p.set_lds_ints * 4 + (p.num_extra ? (size_t)4 * 4 * p.stage_words : 0);
+  const size_t lds = 4ull * stream_lds_words(p, p.exact_nwords != nullptr) + 16;  // + the cursor word
   if (p.exact_nwords) {
     static bool attr = false;  // >64 KiB of dynamic LDS must be opted into per kernel (once per process)
     if (!attr) {
-#define PG_A(b) (void)hipFuncSetAttribute((const void*)stream_kernel<b, false, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+#define PG_A(b) (void)hipFuncSetAttribute((const void*)stream_kernel<b, false, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kExactLutWords + 16);
       PG_A(1) PG_A(2) PG_A(3) PG_A(4) PG_A(5) PG_A(6) PG_A(7) PG_A(8) PG_A(9) PG_A(10) PG_A(11) PG_A(12) PG_A(13)
       PG_A(14) PG_A(15) PG_A(16) PG_A(17) PG_A(18) PG_A(19) PG_A(20) PG_A(21) PG_A(22) PG_A(23) PG_A(24) PG_A(25)
       PG_A(26) PG_A(27) PG_A(28) PG_A(29) PG_A(30) PG_A(31) PG_A(32)

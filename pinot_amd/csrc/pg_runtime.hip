@@ -29,6 +29,7 @@
 
 #include "pg_aux.h"
 #include "../../include/pinot_codec.h"
+#include "../../include/pinot_trace.h"
 
 using namespace pg;
 
@@ -36,6 +37,7 @@ namespace {
 
 thread_local std::string t_err;
 thread_local pg_timing t_timing{};
+thread_local pg_trace t_trace{};  // pg_last_trace: the calling thread's last device call (pinot_trace.h)
 int g_device = -1;
 std::mutex g_init_mu;
 
@@ -1314,10 +1316,31 @@ void key_coldesc(ColDesc& dc, const ColumnRes* c, const pg_key& key) {
 constexpr uint32_t kWideColId = 0xFFFFFFF0u;
 thread_local const std::vector<ColumnRes>* t_wide_cols = nullptr;
 
+// The physical form a compiled leaf took (pinot_trace.h pg_leaf_form).
+uint32_t leaf_form(const pg_leaf& pl, const LeafDesc& dl) {
+  if (dl.kind == LK_ALL) return PG_FORM_MATCH_ALL;
+  if (dl.kind == LK_NONE) return PG_FORM_EMPTY;
+  switch (pl.kind) {
+    case PG_LEAF_SV_SCAN:
+      return dl.kind == LK_SET_LDS ? PG_FORM_SCAN_SET_LDS : dl.kind == LK_SET_LUT ? PG_FORM_SCAN_SET_LUT : PG_FORM_SCAN_RANGE;
+    case PG_LEAF_SORTED: return dl.kind == LK_DOCRANGE ? PG_FORM_SORTED_RANGE : PG_FORM_SORTED_BITMAP;
+    case PG_LEAF_INVERTED: return PG_FORM_INVERTED;
+    case PG_LEAF_MV_SCAN: return PG_FORM_MV_SCAN;
+    case PG_LEAF_RAW_SCAN: return PG_FORM_RAW_SCAN;
+    case PG_LEAF_RANGE_INDEX: return PG_FORM_RANGE_INDEX;
+    default: return PG_FORM_EMPTY;
+  }
+}
+
 int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t hash_cap, bool allow_stream,
                     bool allow_spec) {
   const double t_enter = wall_ms();
   if (!plan) return fail(PG_E_INVALID, "null plan");
+  // this attempt's recording (a rerun starts over; the wide-key path's first pass is kept)
+  memset(t_trace.leaf_forms, 0, sizeof(t_trace.leaf_forms));
+  t_trace.path &= PG_PATH_WIDE_KEYS;
+  t_trace.num_leaves = plan->num_leaves;
+  t_trace.num_segments = plan->num_segments;
   if (plan->abi_version != PG_ABI_VERSION) return fail(PG_E_INVALID, "ABI version %u != %u", plan->abi_version, PG_ABI_VERSION);
   if (plan->num_aggs > (uint32_t)kMaxAggs) return fail(PG_E_UNSUPPORTED, "more than %d aggregations", kMaxAggs);
   if (plan->num_keys > (uint32_t)kMaxKeys) return fail(PG_E_UNSUPPORTED, "more than %d group-by keys", kMaxKeys);
@@ -2003,6 +2026,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
           return fail(PG_E_INVALID, "unknown leaf kind %u", pl.kind);
       }
     }
+    for (uint32_t li = 0; li < L && li < PG_TRACE_MAX_LEAVES; li++)  // the trace: the form each leaf took here
+      t_trace.leaf_forms[li][leaf_form(sr.leaves[li], leaves[(uint64_t)si * L + li])]++;
     for (uint32_t a = 0; a < A; a++) {
       const pg_agg& g = plan->aggs[a];
       if (g.fn == PG_AGG_COUNT) continue;
@@ -2954,7 +2979,10 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     ps.shift1 = part.shift1;
     ps.shift2 = part.shift2;
     ps.dc_words = part.dc_words;
-    ps.row_words = P.bit_words;
+    // the bitmap rows are state only a merge or value sets read: a call finalised right after (the set sizes kept in
+    // dc_pop) that returns no value sets and has no other bitmap aggregation skips their 1.28 GB (config 4) of writes
+    const bool rows_needed = !(P.dc_pop_agg >= 0 && !(plan->flags & PG_PLAN_VALUE_SETS) && P.bit_words == part.dc_words);
+    ps.row_words = rows_needed ? P.bit_words : 0u;
     ps.dc_word = part.dc_word;
     ps.n_i64 = P.n_i64;
     ps.blocks1 = blocks;
@@ -3028,6 +3056,15 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   t_timing.prefilter_ms = filt_ms;
   t_timing.scan_ms = scan_ms;
   t_timing.scan_launches = (blocks ? 1 : 0) + (sp.on && q.num_items ? 1 : 0);  // + the selective stream
+  t_trace.path |= (blocks ? PG_PATH_FUSED_SCAN : 0u) | (sp.on && q.num_items ? PG_PATH_STREAM : 0u) |
+                  (part.on ? PG_PATH_PARTITIONED : 0u) | (ns_docs || ns_matched ? PG_PATH_NONSCAN : 0u) |
+                  (!pre.empty() || !luts.empty() ? PG_PATH_PREPASS : 0u);
+  t_trace.stream_leaf = sp.on && q.num_items ? sp.leaf : 0xFFFFFFFFu;
+  t_trace.group_mode = (uint32_t)P.mode;
+  t_trace.num_slots = P.num_slots;
+  t_trace.num_segments_nonscan = 0;
+  for (uint32_t si = 0; si < S; si++) t_trace.num_segments_nonscan += nonscan[si];
+  t_trace.device_ms = pre_ms + filt_ms + scan_ms;
   memset(&stats, 0, sizeof(stats));
   stats.num_total_docs = total_docs;
   stats.num_segments_processed = S;
@@ -3059,9 +3096,11 @@ int run_with_retries(const pg_plan* plan, Partials& P, pg_stats& st) {
   bool allow_stream = true, allow_spec = true;
   for (;;) {
     const int rc = compile_and_run(plan, P, st, cap, allow_stream, allow_spec);
-    if (rc == kRetryNoStream) { allow_stream = false; continue; }
-    if (rc == kRetryExactPart) { allow_spec = false; continue; }
+    if (rc == kRetryNoStream || rc == kRetryExactPart || rc == kRetryLargerTable) t_trace.reruns++;
+    if (rc == kRetryNoStream) { allow_stream = false; t_trace.rerun_reasons |= PG_RERUN_STREAM; continue; }
+    if (rc == kRetryExactPart) { allow_spec = false; t_trace.rerun_reasons |= PG_RERUN_PARTITION; continue; }
     if (rc != kRetryLargerTable) return rc;
+    t_trace.rerun_reasons |= PG_RERUN_HASH;
     cap = P.num_slots * 8;  // the group-by hash table overflowed: rerun with 8x the slots
     if (cap > kMaxHashSlots) return fail(PG_E_UNSUPPORTED, "group-by needs more than %llu hash slots", (unsigned long long)kMaxHashSlots);
   }
@@ -3086,6 +3125,7 @@ bool plan_needs_wide(const pg_plan* plan) {
 // (pg_wide.hip), then run the plan grouped by the tuple slot.
 int run_wide(const pg_plan* plan, Partials& P, pg_stats& st) {
   const uint32_t K = plan->num_keys, S = plan->num_segments;
+  t_trace.path |= PG_PATH_WIDE_KEYS;
   if (K > kMaxWideKeys) return fail(PG_E_UNSUPPORTED, "more than %u group-by keys", kMaxWideKeys);
   if (S && !plan->segments) return fail(PG_E_INVALID, "null segment list");
   for (uint32_t k = 0; k < K; k++)
@@ -3874,12 +3914,17 @@ int pg_execute_partial(const pg_plan* plan, pg_partials** out) {
   const double t0 = wall_ms();
   t_timing.host_compile_ms = 0;
   t_timing.finalize_wall_ms = 0;
+  memset(&t_trace, 0, sizeof(t_trace));
+  t_trace.query_id = plan ? plan->query_id : 0;
+  t_trace.stream_leaf = 0xFFFFFFFFu;
   try {
     rc = plan_needs_wide(plan) ? run_wide(plan, impl->P, st) : run_with_retries(plan, impl->P, st);
     t_timing.execute_wall_ms = (float)(wall_ms() - t0);
   } catch (const std::exception& e) {
     rc = fail(PG_E_NOMEM, "execute failed: %s", e.what());
   }
+  t_trace.num_docs_matched = rc ? 0 : st.num_docs_scanned;
+  t_trace.wall_ms = (float)(wall_ms() - t0);
   if (rc) { delete impl; return rc; }
   pg_partials* p = (pg_partials*)calloc(1, sizeof(pg_partials));
   if (!p) { delete impl; return fail(PG_E_NOMEM, "out of host memory"); }
@@ -4123,6 +4168,12 @@ int pg_chunk_decompress(uint32_t codec, const void* src, uint64_t src_len, void*
   const char* why = "";
   const int rc = decompress_chunk(codec, (const uint8_t*)src, src_len, (uint8_t*)dst, dst_cap, out_len, &why);
   return rc ? fail(rc, "%s", why) : PG_OK;
+}
+
+int pg_last_trace(pg_trace* out) {
+  if (!out) return fail(PG_E_INVALID, "null out");
+  *out = t_trace;
+  return PG_OK;
 }
 
 int pg_last_timing(pg_timing* out) {

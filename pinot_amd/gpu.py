@@ -273,6 +273,24 @@ class GpuEngine:
             merged = top_groups(query, aggs, merged, gt.server_size)
         return IntermediateResult(aggs or query.aggregations, list(query.group_by), merged, stats)
 
+    def last_trace(self) -> dict:
+        """pg_last_trace: what the device did for this thread's last call -- the kernels that ran, the form each filter
+        leaf took in how many segments, re-runs after a speculative overflow, docs matched (the trace scope the
+        reference records per operator, BaseOperator.java:38, BitmapBasedFilterOperator.java:102-107)."""
+        t = abi.pg_trace()
+        check(self.lib.pg_last_trace(C.byref(t)))
+        forms = []
+        for li in range(min(t.num_leaves, abi.PG_TRACE_MAX_LEAVES)):
+            forms.append({abi.LEAF_FORMS[f]: int(n) for f, n in enumerate(t.leaf_forms[li]) if n})
+        return {"query_id": t.query_id, "path": [n for b, n in abi.PATH_NAMES.items() if t.path & b],
+                "group_mode": ["none", "dense", "hash", "hash_per_segment", "partitioned"][t.group_mode]
+                if t.group_mode < 5 else t.group_mode,
+                "reruns": t.reruns, "rerun_reasons": t.rerun_reasons,
+                "stream_leaf": None if t.stream_leaf == 0xFFFFFFFF else t.stream_leaf, "leaf_forms": forms,
+                "num_segments": t.num_segments, "num_segments_nonscan": t.num_segments_nonscan,
+                "num_docs_matched": t.num_docs_matched, "num_slots": t.num_slots, "device_ms": t.device_ms,
+                "wall_ms": t.wall_ms}
+
     def last_timing(self) -> abi.pg_timing:
         t = abi.pg_timing()
         check(self.lib.pg_last_timing(C.byref(t)))

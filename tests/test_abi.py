@@ -52,13 +52,12 @@ def test_library_is_gfx950_only():
 
 
 STRUCTS = ["pg_col_desc", "pg_leaf", "pg_agg", "pg_key", "pg_segment_ref", "pg_order", "pg_plan", "pg_stats",
-           "pg_result", "pg_partials", "pg_timing", "pg_image_header", "pg_image_segment", "pg_image_leaf"]
+           "pg_result", "pg_partials", "pg_timing", "pg_image_header", "pg_image_segment", "pg_image_leaf", "pg_trace"]
 
 
 def test_struct_layouts_match_header(tmp_path):
     src = tmp_path / "sz.c"
-    header = os.path.join(ROOT, "include", "pinot_gpu.h")
-    lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{header}"', "int main(void){"]
+    lines = ["#include <stdio.h>", "#include <stddef.h>"] + [f'#include "{h}"' for h in HEADERS] + ["int main(void){"]
     for s in STRUCTS:
         lines.append(f'printf("{s} %zu\\n", sizeof({s}));')
         for name, _ in getattr(abi, s)._fields_:

@@ -136,3 +136,30 @@ def test_concurrent_executes_from_two_threads(gpu_engine, oracle_engine, sv_tabl
     for t in ths:
         t.join()
     assert not errors, errors
+
+
+def test_trace_records_each_device_call(gpu_engine, sv_table_inter):
+    """pg_last_trace (pinot_trace.h): the per-call recording that stands for the reference's operator trace scopes --
+    the kernels that ran, each filter leaf's form per segment, the stream's driving leaf, docs matched."""
+    from pinot_amd import synth
+    from pinot_amd.plan import Table
+    segs = [synth.make_segment_np(synth.ADANALYTICS, s, 100_003) for s in range(3)]
+    t = Table("adAnalytics", segs)
+    r = gpu_engine.execute(t, synth.adanalytics_query(1000))
+    tr = gpu_engine.last_trace()
+    assert "stream" in tr["path"] and tr["stream_leaf"] == 1          # accountId IN drives the stream
+    assert tr["leaf_forms"][0] == {"SCAN_RANGE": 3}                   # daysSinceEpoch BETWEEN: a dictId range
+    assert tr["leaf_forms"][1] in ({"SCAN_SET_LDS": 3}, {"SCAN_SET_LUT": 3})
+    assert tr["num_docs_matched"] == r.stats.num_docs_scanned and tr["group_mode"] == "dense"
+    assert tr["reruns"] == 0 and tr["num_segments"] == 3 and tr["device_ms"] > 0
+    # the reference's test data: sorted daysSinceEpoch, inverted column11, a scan on column1
+    gpu_engine.execute(sv_table_inter, "SELECT COUNT(*) FROM t WHERE daysSinceEpoch = 126164076 AND "
+                                       "column11 IN ('P', 'o') AND column1 > 100000")
+    tr = gpu_engine.last_trace()
+    assert tr["leaf_forms"][0] == {"SORTED_RANGE": 4}
+    assert tr["leaf_forms"][1] == {"INVERTED": 4} and "prepass" in tr["path"]
+    assert tr["leaf_forms"][2] == {"SCAN_RANGE": 4}
+    # metadata answers: MIN / MAX / COUNT over match-all segments
+    gpu_engine.execute(sv_table_inter, "SELECT COUNT(*), MAX(column1) FROM t")
+    tr = gpu_engine.last_trace()
+    assert "nonscan" in tr["path"] and tr["num_segments_nonscan"] == 4

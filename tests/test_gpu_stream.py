@@ -95,6 +95,8 @@ def test_stream_overflow_reruns_without_it(gpu_engine, oracle_engine):
     q = parse("SELECT COUNT(*), SUM(clicks) FROM t WHERE acct IN (777)")
     g = gpu_engine.execute(t, q)
     assert gpu_engine.last_timing().scan_launches == 1, "expected the rerun without the stream"
+    tr = gpu_engine.last_trace()   # the recording names the re-run and its reason
+    assert tr["reruns"] == 1 and tr["rerun_reasons"] == 1 and "stream" not in tr["path"] and tr["stream_leaf"] is None
     o = oracle_engine.execute(t, q)
     assert_same_result(g, o, table=t)
     assert g.stats.num_docs_scanned == o.stats.num_docs_scanned > 0.7 * n
