@@ -127,14 +127,9 @@ struct StreamSpec {
   // further leaves over packed columns of at most kStreamStageBits bits: a wave stages its 64 groups' words of the
   // column into its LDS slice (16-byte coalesced loads) and tests its survivors from there instead of per-doc window
   // reads.  stage_words: words per wave slice (0: off), placed after the IN-set words (set_lds_ints, a multiple of 4).
-  uint32_t stage_words;
-  // dense_extra = 1: the driving leaf passes many docs (>= 1/16), so nearly every group of the further leaves' columns
-  // is needed anyway: a further packed leaf of <= kStreamDenseBits bits loads its group's words straight into
-  // registers (the driving leaf's 16-byte load path, static unpacking) instead of a wave slice or per-doc windows
-  uint32_t dense_extra;
+  uint32_t stage_words, stage_pad;
 };
 constexpr uint32_t kStreamStageBits = 16;
-constexpr uint32_t kStreamDenseBits = 16;
 hipError_t launch_stream(const StreamSpec& p, uint32_t bits, uint32_t blocks, hipStream_t s);
 
 // ---- radix-partitioned group-by (pg_part.hip): level 2 + per-bucket aggregation, after the two scan passes

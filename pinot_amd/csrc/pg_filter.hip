@@ -287,20 +287,6 @@ __device__ __forceinline__ uint32_t eval_staged(const LeafDesc& X, const uint32_
   return X.excl ? ~r : r;
 }
 
-// A further leaf over a whole group, its b-bit column's words loaded into registers (dense_extra): the static-width
-// eval_group of the driving leaf, dispatched once per group on the (wave-uniform) width.
-__device__ __forceinline__ uint32_t eval_dense(const LeafDesc& X, const uint32_t* lds_sets, uint32_t g, uint32_t need) {
-  uint32_t r = 0;
-  switch (X.bits) {
-#define PG_D(b) case b: r = eval_group<b>(X, lds_sets, g, need); break;
-    PG_D(1) PG_D(2) PG_D(3) PG_D(4) PG_D(5) PG_D(6) PG_D(7) PG_D(8) PG_D(9) PG_D(10) PG_D(11) PG_D(12) PG_D(13)
-    PG_D(14) PG_D(15) PG_D(16)
-#undef PG_D
-    default: break;
-  }
-  return X.excl ? ~r : r;
-}
-
 // The wave's 64 groups [wg0, wg0 + 64) of a b-bit column into its slice: 64 * b words + 4 of window padding, 16-byte
 // loads (reads past the column return 0).  Wave-local: the same wave reads the slice back.
 __device__ __forceinline__ void stage_slice(const LeafDesc& X, uint32_t wg0, uint32_t* slice, uint32_t lane) {
@@ -386,9 +372,7 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? 6 : 7)) void stream_k
           if (__ballot(m != 0) == 0) break;
           const LeafDesc X = ldcf(seg_leaves, p.extra[x]);
           const bool packed = X.kind == LK_RANGE || X.kind == LK_SET_LDS || X.kind == LK_SET_LUT;
-          if (EXTRA && p.dense_extra && packed && X.bits <= kStreamDenseBits) {
-            if (m) m &= eval_dense(X, lds_sets, g, m);
-          } else if (EXTRA && p.stage_words && packed && X.bits * 64u + 4u <= p.stage_words) {
+          if (EXTRA && p.stage_words && packed && X.bits * 64u + 4u <= p.stage_words) {
             uint32_t* slice = lds_sets + p.set_lds_ints + (tid >> 6) * p.stage_words;
             stage_slice(X, g0 + (tid & ~63u), slice, lane);
             if (m) m &= eval_staged(X, lds_sets, slice, lane, m);

@@ -2412,7 +2412,6 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     std::vector<uint32_t> exact_nwords;  // [seg] LUT words
     uint32_t set_ints = 0;        // LDS IN-set words of the streamed leaves
     std::vector<uint32_t> extra;  // further AND children tested in the stream (runtime bit width)
-    double lead_pass = 1.0;       // estimated pass fraction of the driving leaf alone
     std::vector<StreamLaunch> launches;
   } sp;
   {
@@ -2428,7 +2427,6 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       // the others tested on its survivors (doc ranges, constants, packed columns incl. 1-bit doc bitmaps)
       li = q.ops[1];
       pass = leaf_pass[li];
-      sp.lead_pass = pass;
       for (uint32_t i = 2; i + 1 < q.num_ops && pass > 1.0 / 64 && sp.extra.size() < (size_t)kMaxStreamExtra; i++) {
         const int32_t lx = q.ops[i];
         if (lx < 0) break;
@@ -2821,11 +2819,6 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
             bmax = std::max(bmax, dl.bits);
         }
       if (bmax && !sp.exact && !(stg_env && atoi(stg_env) == 0)) ss.stage_words = 64u * bmax + 4u;
-      // a driving leaf passing >= 1/16 of the docs needs nearly every line of the further leaves' columns: those load
-      // whole groups into registers (PG_STREAM_DENSE=0: slices / windows; =1: always)
-      static const char* dn_env = getenv("PG_STREAM_DENSE");
-      ss.dense_extra = !sp.extra.empty() && (dn_env ? atoi(dn_env) != 0 : sp.lead_pass >= 1.0 / 16) ? 1u : 0u;
-      if (ss.dense_extra) ss.stage_words = 0;  // every column a slice would hold is read densely instead
     }
     ss.segs = q.segs;
     ss.items = q.items;

@@ -152,10 +152,9 @@ def test_trace_records_each_device_call(gpu_engine, sv_table_inter):
     assert tr["leaf_forms"][1] in ({"SCAN_SET_LDS": 3}, {"SCAN_SET_LUT": 3})
     assert tr["num_docs_matched"] == r.stats.num_docs_scanned and tr["group_mode"] == "dense"
     assert tr["reruns"] == 0 and tr["num_segments"] == 3 and tr["device_ms"] > 0
-    # the reference's test data: sorted daysSinceEpoch, inverted column11, a range scan on column6 (a RANGE never
-    # takes the inverted index)
+    # the reference's test data: sorted daysSinceEpoch, inverted column11, a scan on column1
     gpu_engine.execute(sv_table_inter, "SELECT COUNT(*) FROM t WHERE daysSinceEpoch = 126164076 AND "
-                                       "column11 IN ('P', 'o') AND column6 < 500000000")
+                                       "column11 IN ('P', 'o') AND column1 > 100000")
     tr = gpu_engine.last_trace()
     assert tr["leaf_forms"][0] == {"SORTED_RANGE": 4}
     assert tr["leaf_forms"][1] == {"INVERTED": 4} and "prepass" in tr["path"]
