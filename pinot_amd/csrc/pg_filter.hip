@@ -94,10 +94,21 @@ __device__ __forceinline__ uint32_t unpack_win(rsrc_t r, uint32_t idx, uint32_t 
 
 // One leaf over one group for the docs in `need`: bit j <-> doc 32g + j.
 template <int B>
+__device__ __forceinline__ uint32_t test_group(const LeafDesc& L, const uint32_t* lds_sets, uint64_t g, uint32_t need,
+                                               bool exact, const uint32_t (&w)[B + 1]);
+
+template <int B>
 __device__ __forceinline__ uint32_t eval_group(const LeafDesc& L, const uint32_t* lds_sets, uint64_t g, uint32_t need,
                                                bool exact = false) {
   uint32_t w[B + 1];
   load_group<B>(rsrc_of(L.words, L.wbytes), g, w);
+  return test_group<B>(L, lds_sets, g, need, exact, w);
+}
+
+// The leaf's test over a group whose words `w` are in registers.
+template <int B>
+__device__ __forceinline__ uint32_t test_group(const LeafDesc& L, const uint32_t* lds_sets, uint64_t g, uint32_t need,
+                                               bool exact, const uint32_t (&w)[B + 1]) {
   uint32_t m = 0;
   if (exact) {
     // SET_LDS with its exact LUT over dictIds staged at lds_sets[0], which is LDS address 0 (stream_kernel has no
@@ -358,11 +369,28 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? 6 : 7)) void stream_k
     __syncthreads();  // set staged, cursor reset
     uint32_t* out = p.docs + (uint64_t)it * p.cap;
     if (L.kind != LK_NONE) {
+      // exact mode is software-pipelined: the next group's words are loaded before this group is tested, so each lane
+      // keeps two groups' loads in flight (160 KiB per CU at B = 20; 96 VGPRs of the 128 its 4 waves / SIMD allow --
+      // the 256-thread variants run 6-7 waves / SIMD and would spill)
+      const rsrc_t rs = rsrc_of(L.words, L.wbytes);
+      uint32_t w[B + 1];
+      if (EXACT && wi.tile_begin + tid < wi.tile_end) load_group<B>(rs, wi.tile_begin + tid, w);
       for (uint32_t g0 = wi.tile_begin; g0 < wi.tile_end; g0 += NT) {
         const uint32_t g = g0 + tid;
         const uint64_t d0 = (uint64_t)g * 32;
         uint32_t m = 0;
-        if (g < wi.tile_end && d0 < nd) {
+        if (EXACT) {
+          uint32_t wn[B + 1];
+          if (g + NT < wi.tile_end) load_group<B>(rs, g + NT, wn);
+          if (g < wi.tile_end && d0 < nd) {
+            const uint32_t valid = d0 + 32 <= nd ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (32u - (uint32_t)(nd - d0)));
+            uint32_t r = test_group<B>(L, lds_sets, g, valid, EXACT && L.kind == LK_SET_LDS, w);
+            if (L.excl) r = ~r;
+            m = r & valid;
+          }
+#pragma unroll
+          for (int k = 0; k <= B; k++) w[k] = wn[k];
+        } else if (g < wi.tile_end && d0 < nd) {
           const uint32_t valid = d0 + 32 <= nd ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (32u - (uint32_t)(nd - d0)));
           uint32_t r = eval_group<B>(L, lds_sets, g, valid, EXACT && L.kind == LK_SET_LDS);
           if (L.excl) r = ~r;

@@ -3315,6 +3315,52 @@ FinalSpec make_final(const Partials& P, const pg_plan* plan) {
   return f;
 }
 
+// The result order of nc candidates (plan's ORDER BY items, then ascending key ids, first key first) as a permutation
+// in `perm`; `exact`: only its first plan->limit entries are ordered (PG_PLAN_EXACT_LIMIT keeps just those).
+// key_id(i, k) = candidate i's k-th key id.
+template <class KeyId>
+void order_rows(const pg_plan* plan, const Partials& P, uint64_t nc, const std::vector<double>& hv,
+                const std::vector<int64_t>& hc, KeyId key_id, bool exact, std::vector<uint64_t>& perm) {
+  const uint32_t A = plan->num_aggs, K = plan->num_keys;
+  perm.resize(nc);
+  for (uint64_t i = 0; i < nc; i++) perm[i] = i;
+  if (!K || !(plan->num_order || exact)) return;
+  // one row of order images per candidate (ascending = ranks first): AGG items as the order-preserving image of the
+  // final double, DESC items complemented, then the key ids
+  const uint32_t W = plan->num_order + K;
+  std::vector<uint64_t> ok(nc * W);
+  for (uint64_t i = 0; i < nc; i++) {
+    uint64_t* row = ok.data() + i * W;
+    for (uint32_t o = 0; o < plan->num_order; o++) {
+      const pg_order& it = plan->order[o];
+      uint64_t x;
+      if (it.kind == PG_ORDER_AGG) {
+        double v = hv[i * A + it.index];
+        if (P.aggs[it.index].fn == PG_AGG_AVG) {
+          const int64_t c = hc[i * A + it.index];
+          v = c ? v / (double)c : -INFINITY;
+        }
+        if (v == 0) v = 0;  // -0.0 ties with 0.0, as the double comparison does
+        int64_t bits;
+        memcpy(&bits, &v, 8);
+        x = bits >= 0 ? ((uint64_t)bits | 0x8000000000000000ull) : ~(uint64_t)bits;
+      } else {
+        x = key_id(i, it.index);
+      }
+      row[o] = it.desc ? ~x : x;
+    }
+    for (uint32_t k = 0; k < K; k++) row[plan->num_order + k] = key_id(i, k);
+  }
+  auto before = [&](uint64_t i, uint64_t j) {
+    const uint64_t *x = ok.data() + i * W, *y = ok.data() + j * W;
+    for (uint32_t w = 0; w < W; w++)
+      if (x[w] != y[w]) return x[w] < y[w];
+    return false;
+  };
+  if (exact && nc > plan->limit) std::partial_sort(perm.begin(), perm.begin() + plan->limit, perm.end(), before);
+  else std::sort(perm.begin(), perm.end(), before);
+}
+
 int build_result(pg_partials* pp, const pg_plan* plan, pg_result** out, const Partials& P, uint64_t nc,
                  const std::vector<uint64_t>& hk, const std::vector<double>& hv, const std::vector<int64_t>& hc,
                  bool sets, const std::vector<uint64_t>& hoff, const std::vector<uint32_t>& hids);
@@ -3597,6 +3643,36 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   // 4. value sets
   bool sets = false;
   for (uint32_t a = 0; a < A; a++) sets |= (plan->flags & PG_PLAN_VALUE_SETS) && P.aggs[a].fn == PG_AGG_DISTINCTCOUNT;
+  if (sets && !P.wide && K && (plan->flags & PG_PLAN_EXACT_LIMIT) && plan->limit && nc > plan->limit) {
+    // an exact limit keeps `limit` of the candidates: order them now and extract the value sets of those only (the
+    // server trim of config 4 keeps 5 000 of the tens of thousands of groups tied at the boundary's set size)
+    std::vector<uint32_t> hs(nc);
+    HIP_CHECK(hipMemcpyAsync(hs.data(), cs, nc * 4, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    std::vector<uint64_t> perm;
+    order_rows(plan, P, nc, hv, hc, [&](uint64_t i, uint32_t k) { return (hk[i] / P.key_stride[k]) % P.key_card[k]; },
+               true, perm);
+    const uint64_t m = plan->limit;
+    std::vector<uint64_t> kk(m);
+    std::vector<double> kv(m * A);
+    std::vector<int64_t> kc(m * A);
+    std::vector<uint32_t> kslot(m);
+    for (uint64_t o = 0; o < m; o++) {
+      const uint64_t i = perm[o];
+      kk[o] = hk[i];
+      kslot[o] = hs[i];
+      for (uint32_t a = 0; a < A; a++) { kv[o * A + a] = hv[i * A + a]; kc[o * A + a] = hc[i * A + a]; }
+    }
+    uint32_t* ks = sc.get<uint32_t>(m, rc);
+    if (rc) return rc;
+    HIP_CHECK(hipMemcpyAsync(ks, kslot.data(), m * 4, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipStreamSynchronize(s));  // kslot is a local of this block
+    hk.swap(kk);
+    hv.swap(kv);
+    hc.swap(kc);
+    cs = ks;
+    nc = m;
+  }
   std::vector<uint64_t> hoff;
   std::vector<uint32_t> hids;
   if (sets) {
@@ -3651,46 +3727,9 @@ int build_result(pg_partials* pp, const pg_plan* plan, pg_result** out, const Pa
   auto key_id = [&](uint64_t i, uint32_t k) -> uint64_t {
     return P.wide ? (uint64_t)wk[i * K + k] : (hk[i] / P.key_stride[k]) % P.key_card[k];
   };
-  std::vector<uint64_t> perm(nc);
-  for (uint64_t i = 0; i < nc; i++) perm[i] = i;
   const bool exact = K && (plan->flags & PG_PLAN_EXACT_LIMIT) && plan->limit && nc > plan->limit;
-  if (K && (plan->num_order || exact)) {
-    // one row of order images per candidate (ascending = ranks first): the ORDER BY items, then the key ids (first key
-    // first); AGG items as the order-preserving image of the final double, DESC items complemented
-    const uint32_t W = plan->num_order + K;
-    std::vector<uint64_t> ok(nc * W);
-    for (uint64_t i = 0; i < nc; i++) {
-      uint64_t* row = ok.data() + i * W;
-      for (uint32_t o = 0; o < plan->num_order; o++) {
-        const pg_order& it = plan->order[o];
-        uint64_t x;
-        if (it.kind == PG_ORDER_AGG) {
-          double v = hv[i * A + it.index];
-          if (P.aggs[it.index].fn == PG_AGG_AVG) {
-            const int64_t c = hc[i * A + it.index];
-            v = c ? v / (double)c : -INFINITY;
-          }
-          if (v == 0) v = 0;  // -0.0 ties with 0.0, as the double comparison does
-          int64_t bits;
-          memcpy(&bits, &v, 8);
-          x = bits >= 0 ? ((uint64_t)bits | 0x8000000000000000ull) : ~(uint64_t)bits;
-        } else {
-          x = key_id(i, it.index);
-        }
-        row[o] = it.desc ? ~x : x;
-      }
-      for (uint32_t k = 0; k < K; k++) row[plan->num_order + k] = key_id(i, k);
-    }
-    auto before = [&](uint64_t i, uint64_t j) {
-      const uint64_t *x = ok.data() + i * W, *y = ok.data() + j * W;
-      for (uint32_t w = 0; w < W; w++)
-        if (x[w] != y[w]) return x[w] < y[w];
-      return false;
-    };
-    // an exact limit needs only its first `limit` rows in order
-    if (exact) std::partial_sort(perm.begin(), perm.begin() + plan->limit, perm.end(), before);
-    else std::sort(perm.begin(), perm.end(), before);
-  }
+  std::vector<uint64_t> perm;
+  order_rows(plan, P, nc, hv, hc, key_id, exact, perm);
   // PG_PLAN_EXACT_LIMIT: the first `limit` rows of that order (the server result / the per-segment trim)
   if (exact) nc = plan->limit;
 
