@@ -42,6 +42,8 @@ typedef enum pg_leaf_form {  /* the device form a filter leaf took in one segmen
 #define PG_PATH_WIDE_KEYS 0x8u   /* tuple-interned group keys (ArrayMapBasedHolder form)                            */
 #define PG_PATH_NONSCAN 0x10u    /* some segments answered from metadata (NonScanBasedAggregationOperator)          */
 #define PG_PATH_PREPASS 0x20u    /* index pre-pass kernels (IN-set LUTs, sorted / inverted / MV doc bitmaps)         */
+#define PG_PATH_INDEX_COUNT 0x40u /* the fused index count: inverted leaves decoded per 64 K-doc key in LDS, COUNT /
+                                     COUNTMV counted there (no doc bitmaps in HBM)                                    */
 
 #define PG_RERUN_STREAM 0x1u     /* the stream's survivor regions overflowed: re-ran without the stream            */
 #define PG_RERUN_PARTITION 0x2u  /* a speculative partition region overflowed: re-ran with exact offsets            */

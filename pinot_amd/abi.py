@@ -139,8 +139,10 @@ LEAF_FORMS = ["MATCH_ALL", "EMPTY", "SCAN_RANGE", "SCAN_SET_LDS", "SCAN_SET_LUT"
               "INVERTED", "MV_SCAN", "RAW_SCAN", "RANGE_INDEX"]
 PG_PATH_FUSED_SCAN, PG_PATH_STREAM, PG_PATH_PARTITIONED, PG_PATH_WIDE_KEYS, PG_PATH_NONSCAN, PG_PATH_PREPASS = \
     0x1, 0x2, 0x4, 0x8, 0x10, 0x20
+PG_PATH_INDEX_COUNT = 0x40
 PATH_NAMES = {PG_PATH_FUSED_SCAN: "fused_scan", PG_PATH_STREAM: "stream", PG_PATH_PARTITIONED: "partitioned",
-              PG_PATH_WIDE_KEYS: "wide_keys", PG_PATH_NONSCAN: "nonscan", PG_PATH_PREPASS: "prepass"}
+              PG_PATH_WIDE_KEYS: "wide_keys", PG_PATH_NONSCAN: "nonscan", PG_PATH_PREPASS: "prepass",
+              PG_PATH_INDEX_COUNT: "index_count"}
 PG_RERUN_STREAM, PG_RERUN_PARTITION, PG_RERUN_HASH = 0x1, 0x2, 0x4
 
 

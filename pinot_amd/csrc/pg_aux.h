@@ -70,6 +70,47 @@ struct RoaringJob {
   uint32_t card, pad;
 };
 hipError_t launch_roaring_keys(const RoaringJob* jobs, uint32_t njobs, uint32_t blocks, hipStream_t s);
+
+// ---- fused index count (pg_index.hip): an aggregation-only COUNT / COUNTMV query whose filter is index leaves only
+// (sorted doc ranges, inverted dictId sets, constants) in at most two levels of AND / OR / NOT.  One workgroup per
+// (segment, 64 K-doc key) of the segment's doc range decodes each inverted leaf's containers of that key into LDS,
+// evaluates the filter on the words and counts -- no doc bitmap goes through HBM.
+enum IdxLeafKind : uint32_t { IL_ALL = 0, IL_NONE = 1, IL_DOCRANGE = 2, IL_ROARING = 3 };
+struct IdxLeaf {                   // leaf l of segment s
+  uint32_t kind, negate;           // negate: NOT_EQ / NOT_IN over an inverted index (flip of the OR)
+  int32_t lo, hi;                  // IL_DOCRANGE: docs [lo, hi)
+  const uint8_t* roaring;          // IL_ROARING: the column's containers and the selected dictIds
+  const RoaringContainer* cs;
+  const uint32_t* dir;
+  const uint32_t* keydir;
+  const int32_t* ids;
+  uint32_t nids, card;
+};
+struct IdxSeg {
+  uint32_t num_docs, key0, first_block, pad;  // keys [key0, key0 + blocks) of the doc range; blocks prefix
+  const IdxLeaf* leaves;                      // [num_leaves]
+  const uint32_t* mv_cnt;                     // COUNTMV: 4-bit value counts per doc (packed, bit 31-4j.. <- doc 8w+j) or
+  const uint32_t* mv_offsets;                 //   the row offsets [num_docs + 1] when no count column exists
+};
+constexpr uint32_t kIdxMaxLeaves = 8, kIdxMaxItems = 16;
+struct IdxSpec {
+  uint32_t num_segs, num_leaves;
+  uint32_t root_or;                 // root combines its items by OR (else AND)
+  uint32_t num_items;
+  uint32_t item[kIdxMaxItems];      // bit 31 NOT, bit 30 group, else leaf index (low 8 bits)
+  uint32_t group_or[kIdxMaxItems];  // group g: OR (else AND) over gleaf[gfirst[g], gfirst[g] + gn[g])
+  uint32_t gfirst[kIdxMaxItems], gn[kIdxMaxItems];
+  uint32_t gleaf[kIdxMaxItems];     // bit 31 NOT, else leaf index
+  uint32_t chunk_of[kIdxMaxLeaves]; // LDS chunk slot of leaf l (~0: not an inverted leaf anywhere)
+  uint32_t num_chunks;
+  uint32_t cntmv_slot;              // i64 slot of COUNTMV (~0: none)
+  const IdxSeg* segs;
+  unsigned long long* i64;          // slot 0: doc count
+  unsigned long long* seg_matched;  // [num_segs]
+};
+hipError_t launch_index_count(const IdxSpec& p, uint32_t blocks, hipStream_t s);
+// COUNTMV's count column of an MV forward index: 4 bits per doc (min(count, 15)); *over set when a count exceeds 15
+hipError_t launch_mv_counts(const uint32_t* offsets, uint32_t num_docs, uint32_t* out, unsigned int* over, hipStream_t s);
 hipError_t launch_mv_scan(const uint32_t* words, uint32_t bits, const uint32_t* offsets, uint32_t num_docs,
                           int32_t lo, int32_t hi, const uint32_t* lut, uint32_t excl, uint32_t* bitmap,
                           hipStream_t s);

@@ -8,6 +8,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "pg_aux.h"
+#include "pg_roaring.h"
 
 namespace pg {
 
@@ -333,97 +334,16 @@ hipError_t launch_roaring_or(const uint8_t* roaring, const RoaringContainer* con
 
 __global__ __launch_bounds__(256) void roaring_keys_kernel(const RoaringJob* __restrict__ jobs, uint32_t njobs) {
   __shared__ uint32_t chunk[2048];     // the key's 65 536 docs
-  __shared__ uint32_t bml[256];        // bitmap containers of this round, processed by the whole block
-  __shared__ uint32_t nbml;
-  __shared__ uint32_t apre[257];       // array containers of this round: exclusive prefix of their cardinalities
-  __shared__ uint32_t aoff[256];       //   and their payload offsets (slot = the thread that found the container)
-  __shared__ uint32_t wsum[4];
+  __shared__ RoaringLds<256> S;
   uint32_t lo = 0, hi = njobs;         // the job whose block range holds this block
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
     if (jobs[mid].first_block <= blockIdx.x) lo = mid; else hi = mid;
   }
   const RoaringJob J = jobs[lo];
-  const uint32_t key = J.key0 + (blockIdx.x - J.first_block), tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t key = J.key0 + (blockIdx.x - J.first_block), tid = threadIdx.x;
   for (uint32_t w = tid; w < 2048; w += 256) chunk[w] = 0;
-  if (tid == 0) nbml = 0;
-  __syncthreads();
-  for (uint32_t r0 = 0; r0 < J.nids; r0 += 256) {
-    const uint32_t i = r0 + tid;
-    uint32_t alen = 0, aoffset = 0;  // this thread's array container (entries are spread over the block below)
-    if (i < J.nids) {
-      const uint32_t id = (uint32_t)J.ids[i];
-      uint32_t a;
-      bool hit;
-      if (J.keydir) {  // one load: the key-major directory built at upload
-        a = J.keydir[(uint64_t)key * J.card + id];
-        hit = a != 0xFFFFFFFFu;
-      } else {
-        a = J.dir[id];
-        uint32_t b = J.dir[id + 1];  // this dictId's containers, ascending keys: find `key`
-        while (a < b) {
-          const uint32_t m = (a + b) >> 1;
-          if (J.cs[m].key < key) a = m + 1; else b = m;
-        }
-        hit = a < J.dir[id + 1] && J.cs[a].key == key;
-      }
-      if (hit) {
-        const RoaringContainer c = J.cs[a];
-        const uint8_t* p = J.roaring + c.offset;
-        if (c.type == 0) {  // array of uint16: expanded by the whole block
-          alen = c.card;
-          aoffset = c.offset;
-        } else if (c.type == 2) {  // runs: uint16 nruns, then (start, length - 1)
-          const uint16_t* rr = (const uint16_t*)p + 1;
-          for (uint32_t k = 0; k < c.card; k++) {
-            const uint32_t st = rr[2 * k], en = st + rr[2 * k + 1];
-            for (uint32_t w = st >> 5; w <= (en >> 5); w++) {
-              const uint32_t l = w * 32 > st ? 0 : st - w * 32, h = w * 32 + 31 < en ? 31 : en - w * 32;
-              const uint32_t mask = (h == 31 ? 0xFFFFFFFFu : ((1u << (h + 1)) - 1u)) & ~((1u << l) - 1u);
-              atomicOr(&chunk[w], __builtin_bitreverse32(mask));
-            }
-          }
-        } else {
-          bml[atomicAdd(&nbml, 1u)] = c.offset;
-        }
-      }
-    }
-    // exclusive prefix of the array cardinalities over the block (wave scan + wave sums)
-    uint32_t x = alen;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o);
-      if (lane >= (uint32_t)o) x += y;
-    }
-    if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    uint32_t wb = 0;
-    for (uint32_t w = 0; w < wave; w++) wb += wsum[w];
-    apre[tid] = wb + x - alen;
-    aoff[tid] = aoffset;
-    if (tid == 255) apre[256] = wb + x;
-    __syncthreads();
-    // every array entry of the round, one per thread per step: container k = the last prefix <= e
-    const uint32_t total = apre[256];
-    for (uint32_t e = tid; e < total; e += 256) {
-      uint32_t a = 0, b = 256;
-      while (b - a > 1) {
-        const uint32_t m = (a + b) >> 1;
-        if (apre[m] <= e) a = m; else b = m;
-      }
-      const uint32_t v = ((const uint16_t*)(J.roaring + aoff[a]))[e - apre[a]];
-      atomicOr(&chunk[v >> 5], 0x80000000u >> (v & 31u));
-    }
-    __syncthreads();  // the bitmap containers below OR whole words without atomics
-    for (uint32_t k = 0; k < nbml; k++) {  // bitmap containers: 1 024 little-endian uint64 words each
-      const uint32_t* w32 = (const uint32_t*)(J.roaring + bml[k]);
-      for (uint32_t w = tid; w < 2048; w += 256) chunk[w] |= __builtin_bitreverse32(w32[w]);
-      __syncthreads();
-    }
-    __syncthreads();
-    if (tid == 0) nbml = 0;
-    __syncthreads();
-  }
+  roaring_key_chunk<256>(J.roaring, J.cs, J.dir, J.keydir, J.card, J.ids, J.nids, key, chunk, S);
   const uint32_t nwords = (J.num_docs + 31) / 32, tail = J.num_docs & 31u;
   for (uint32_t w = tid; w < 2048; w += 256) {
     const uint32_t gw = key * 2048 + w;

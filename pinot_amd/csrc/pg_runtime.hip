@@ -263,6 +263,7 @@ struct ColumnRes {
   uint32_t num_docs = 0, bits = 0, num_values = 0;
   DevBuf words;                       // packed dictIds (SV / synthesised for sorted / MV values)
   DevBuf mv_offsets;                  // MV row offsets
+  DevBuf mv_cnt;                      // MV values per doc, 4-bit packed (absent when a doc holds more than 15)
   std::vector<int32_t> sorted_pairs;  // host copy for leaf lowering (card x 2)
   // inverted index
   bool has_inv = false;
@@ -637,6 +638,17 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
       const size_t sb = mv_offsets_scratch_bytes(nv);
       if ((rc = scratch.alloc(sb))) return rc;
       HIP_CHECK(launch_mv_offsets((const uint32_t*)bm.p, nv, nd, (uint32_t*)tmp.mv_offsets.p, scratch.p, sb, s));
+      {  // COUNTMV's 4-bit count column (the fused index count reads 0.5 B per doc instead of two offsets)
+        const uint64_t cw = ((uint64_t)nd + 7) / 8 + 4;
+        DevBuf over;
+        if ((rc = tmp.mv_cnt.alloc(4 * cw)) || (rc = over.alloc(16))) return rc;
+        HIP_CHECK(hipMemsetAsync(over.p, 0, 4, s));
+        HIP_CHECK(launch_mv_counts((const uint32_t*)tmp.mv_offsets.p, nd, (uint32_t*)tmp.mv_cnt.p, (unsigned int*)over.p, s));
+        uint32_t big = 0;
+        HIP_CHECK(hipMemcpyAsync(&big, over.p, 4, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        if (big) tmp.mv_cnt.reset();  // a doc with more than 15 values: COUNTMV keeps the offsets
+      }
       HIP_CHECK(hipStreamSynchronize(s));
       break;
     }
@@ -753,11 +765,12 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
       c.dmin = tmp.dmin; c.dmax = tmp.dmax; c.imin = tmp.imin; c.imax = tmp.imax;
       break;
     case PG_IDX_FWD_SV_BITPACKED: case PG_IDX_FWD_SV_SORTED: case PG_IDX_FWD_MV_BITPACKED:
-      c.words.reset(); c.mv_offsets.reset();
+      c.words.reset(); c.mv_offsets.reset(); c.mv_cnt.reset();
       c.fwd = tmp.fwd; c.num_docs = tmp.num_docs; c.bits = tmp.bits; c.num_values = tmp.num_values;
       if (!c.has_dict) c.card = tmp.card;
       c.words = std::move(tmp.words);
       c.mv_offsets = std::move(tmp.mv_offsets);
+      c.mv_cnt = std::move(tmp.mv_cnt);
       c.sorted_pairs.swap(tmp.sorted_pairs);
       break;
     case PG_IDX_INV_BITMAP:
@@ -799,7 +812,7 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
     }
     case PG_IDX_FWD_SV_RAW:
       c.has_range = false; c.vbits = 0;
-      c.words.reset(); c.mv_offsets.reset(); c.rawv.reset(); c.vals.reset();
+      c.words.reset(); c.mv_offsets.reset(); c.mv_cnt.reset(); c.rawv.reset(); c.vals.reset();
       c.fwd = FWD_RAW; c.num_docs = tmp.num_docs; c.bits = 0; c.num_values = tmp.num_values;
       c.dtype = tmp.dtype; c.card = tmp.card; c.has_dict = false;
       c.dmin = tmp.dmin; c.dmax = tmp.dmax; c.imin = tmp.imin; c.imax = tmp.imax;
@@ -2565,6 +2578,148 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   if (lds_bytes > 160 * 1024) return fail(PG_E_UNSUPPORTED, "scan needs %zu bytes of LDS", lds_bytes);
 
   PG_PROF("stream");
+  // ---- fused index count (pg_index.hip): COUNT / COUNTMV with no group-by under a filter of index leaves only
+  // (inverted dictId sets, sorted doc ranges, constants) in at most two levels of AND / OR / NOT: one launch decodes
+  // each 64 K-doc key's containers into LDS, evaluates the filter there and counts -- instead of the roaring pre-pass
+  // writing doc bitmaps to HBM and the fused scan reading them back.  PG_INDEX_FUSED=0 disables.
+  struct IdxPlan {
+    bool on = false;
+    IdxSpec spec{};
+    std::vector<IdxLeaf> leaves;        // [S][L]
+    std::vector<IdxSeg> segs;           // [S]
+    std::vector<uint64_t> ids_off;      // [S][L] arena offset of a ROARING leaf's dictIds (~0: none)
+    uint32_t blocks = 0;
+  } ix;
+  {
+    const char* ix_env = getenv("PG_INDEX_FUSED");
+    bool ok = !(ix_env && atoi(ix_env) == 0) && K == 0 && A >= 1 && L <= kIdxMaxLeaves && !part.on && !sp.on &&
+              pre_leaves.empty();
+    uint32_t cntmv = 0xFFFFFFFFu, cntmv_col = 0;
+    for (uint32_t a = 0; a < A && ok; a++) {
+      const pg_agg& g = plan->aggs[a];
+      if (g.fn == PG_AGG_COUNT) continue;
+      ok = g.fn == PG_AGG_COUNTMV && cntmv == 0xFFFFFFFFu;
+      cntmv = P.aggs[a].slot;
+      cntmv_col = g.col_a;
+    }
+    std::vector<int> roar((uint64_t)S * L, -1);  // (segment, leaf) -> its ROARING pre-pass op
+    for (size_t k = 0; k < pre.size() && ok; k++) {
+      ok = pre[k].kind == PrepassOp::ROARING;
+      if (ok) roar[(uint64_t)pre[k].seg * L + pre[k].leaf] = (int)k;
+    }
+    // the filter as items of a root AND / OR, each a leaf or a group (AND / OR of leaves), any of them negated
+    IdxSpec& sp2 = ix.spec;
+    if (ok && plan->num_ops) {
+      struct N { int kind, leaf; std::vector<int> kids; };  // 0 leaf, 1 AND, 2 OR, 3 NOT
+      std::vector<N> nodes;
+      std::vector<int> st;
+      for (uint32_t i = 0; i < plan->num_ops; i++) {
+        const int32_t op = plan->ops[i];
+        N n{0, -1, {}};
+        if (op >= 0) { n.leaf = op; }
+        else {
+          const int cnt = op == PG_OP_NOT ? 1 : ((-op) & 0xFF);
+          n.kind = op == PG_OP_NOT ? 3 : (((-op) & 0x300) == 0x100 ? 1 : 2);
+          n.kids.assign(st.end() - cnt, st.end());
+          st.resize(st.size() - cnt);
+        }
+        nodes.push_back(n);
+        st.push_back((int)nodes.size() - 1);
+      }
+      uint32_t ng = 0, ngl = 0;
+      // a leaf or NOT leaf -> gleaf / item code; -1 if not a (negated) leaf
+      auto leaf_code = [&](int x) -> int64_t {
+        bool neg = false;
+        while (nodes[x].kind == 3) { neg = !neg; x = nodes[x].kids[0]; }
+        if (nodes[x].kind != 0) return -1;
+        return (int64_t)((uint32_t)nodes[x].leaf | (neg ? 0x80000000u : 0u));
+      };
+      auto item_code = [&](int x) -> int64_t {
+        const int64_t lc = leaf_code(x);
+        if (lc >= 0) return lc;
+        bool neg = false;
+        while (nodes[x].kind == 3) { neg = !neg; x = nodes[x].kids[0]; }
+        if (ng >= kIdxMaxItems) return -1;
+        const uint32_t g = ng++;
+        sp2.group_or[g] = nodes[x].kind == 2;
+        sp2.gfirst[g] = ngl;
+        sp2.gn[g] = (uint32_t)nodes[x].kids.size();
+        for (int k : nodes[x].kids) {
+          const int64_t c = leaf_code(k);
+          if (c < 0 || ngl >= kIdxMaxItems) return -1;
+          sp2.gleaf[ngl++] = (uint32_t)c;
+        }
+        return (int64_t)(g | 0x40000000u | (neg ? 0x80000000u : 0u));
+      };
+      const int root = st.back();
+      std::vector<int> items1;
+      if (nodes[root].kind == 1 || nodes[root].kind == 2) { sp2.root_or = nodes[root].kind == 2; items1 = nodes[root].kids; }
+      else { sp2.root_or = 0; items1.push_back(root); }
+      ok = items1.size() <= kIdxMaxItems;
+      for (size_t i = 0; i < items1.size() && ok; i++) {
+        const int64_t c = item_code(items1[i]);
+        ok = c >= 0;
+        if (ok) sp2.item[sp2.num_items++] = (uint32_t)c;
+      }
+    } else if (ok) {
+      sp2.root_or = 0;  // no filter: every doc
+      sp2.num_items = 0;
+    }
+    // the leaves of each segment: constants, doc ranges, inverted leaves (their LDS chunk slots)
+    if (ok) {
+      for (uint32_t l = 0; l < kIdxMaxLeaves; l++) sp2.chunk_of[l] = 0xFFFFFFFFu;
+      ix.leaves.assign((uint64_t)S * L, IdxLeaf{});
+      ix.ids_off.assign((uint64_t)S * L, ~0ull);
+      ix.segs.assign(S, IdxSeg{});
+      for (uint32_t si = 0; si < S && ok; si++) {
+        for (uint32_t li = 0; li < L && ok; li++) {
+          const LeafDesc& dl = leaves[(uint64_t)si * L + li];
+          IdxLeaf& x = ix.leaves[(uint64_t)si * L + li];
+          const int r = roar[(uint64_t)si * L + li];
+          if (r >= 0) {
+            const PrepassOp& op = pre[r];
+            x.kind = IL_ROARING;
+            x.negate = op.negate ? 1u : 0u;
+            x.roaring = (const uint8_t*)op.col->roaring.p;
+            x.cs = (const RoaringContainer*)op.col->containers.p;
+            x.dir = (const uint32_t*)op.col->inv_dir_dev.p;
+            x.keydir = (const uint32_t*)op.col->inv_keydir.p;
+            x.card = op.col->inv_keydir_card;
+            x.nids = op.n;
+            ix.ids_off[(uint64_t)si * L + li] = op.in_off;
+            if (sp2.chunk_of[li] == 0xFFFFFFFFu) sp2.chunk_of[li] = sp2.num_chunks++;
+          } else if (dl.kind == LK_ALL) { x.kind = IL_ALL; }
+          else if (dl.kind == LK_NONE) { x.kind = IL_NONE; }
+          else if (dl.kind == LK_DOCRANGE) { x.kind = IL_DOCRANGE; x.lo = dl.lo; x.hi = dl.hi; }
+          else ok = false;
+        }
+        IdxSeg& g = ix.segs[si];
+        g.num_docs = plan->segments[si].num_docs;
+        const uint32_t lo = root_range[si].first, hi = std::min(root_range[si].second, g.num_docs);
+        const uint32_t nk = (nonscan[si] || !seg_tiles[si] || hi <= lo) ? 0u : ((hi - 1) >> 16) + 1 - (lo >> 16);
+        g.key0 = nk ? lo >> 16 : 0u;
+        g.first_block = ix.blocks;
+        ix.blocks += nk;
+        if (cntmv != 0xFFFFFFFFu && nk) {
+          const ColumnRes* c = col(si, cntmv_col);
+          ok = c && c->fwd == FWD_MV && c->mv_offsets.p;
+          if (ok) {
+            g.mv_cnt = (const uint32_t*)c->mv_cnt.p;
+            g.mv_offsets = (const uint32_t*)c->mv_offsets.p;
+          }
+        }
+      }
+    }
+    if (ok) {
+      ix.on = true;
+      sp2.num_segs = S;
+      sp2.num_leaves = L;
+      sp2.cntmv_slot = cntmv;
+      q.num_items = 0;          // no fused scan
+      items.clear();
+      scratch_bytes = 0;        // nor doc bitmaps: the scratch would only hold the unused ones
+    }
+  }
   // ---- device buffers (state + arena + scratch) from the caching pool
   part.on = part.on && q.num_items > 0;
   // the state's byte fills ride on the arena-upload launch unless the non-scan seeding below writes the state first
@@ -2677,7 +2832,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   std::vector<RoaringJob> rjobs;
   uint32_t roaring_blocks = 0;
   for (const PrepassOp& op : pre) {
-    if (op.kind != PrepassOp::ROARING || !op.nkeys) continue;
+    if (ix.on || op.kind != PrepassOp::ROARING || !op.nkeys) continue;
     RoaringJob j;
     memset(&j, 0, sizeof(j));
     j.nids = op.n;
@@ -2690,6 +2845,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     rjobs.push_back(j);
   }
   const uint64_t off_rjobs = ar.reserve(rjobs.size() * sizeof(RoaringJob));
+  const uint64_t off_ixleaves = ar.reserve(ix.leaves.size() * sizeof(IdxLeaf));
+  const uint64_t off_ixsegs = ar.reserve(ix.segs.size() * sizeof(IdxSeg));
   DevBuf arena, scratch;
   DevBuf p_ent0, p_cnt0, p_hist1, p_off1, p_ent1, p_hist2, p_off2, p_ent2, p_temp, p_fill;  // GM_PART pipeline
   DevBuf l_docs, l_counts;  // selective stream: survivor regions + counts
@@ -2741,6 +2898,16 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       j.bm = (uint32_t*)(dS + op.out_off);
     }
     if (!rjobs.empty()) memcpy(&ar.h[off_rjobs], rjobs.data(), rjobs.size() * sizeof(RoaringJob));
+  }
+  if (ix.on) {  // the fused index count's leaf / segment tables (dictId lists already in the arena)
+    for (size_t k = 0; k < ix.leaves.size(); k++)
+      if (ix.ids_off[k] != ~0ull) ix.leaves[k].ids = (const int32_t*)(dA + ix.ids_off[k]);
+    for (uint32_t si = 0; si < S; si++) ix.segs[si].leaves = (const IdxLeaf*)(dA + off_ixleaves) + (uint64_t)si * L;
+    if (!ix.leaves.empty()) memcpy(&ar.h[off_ixleaves], ix.leaves.data(), ix.leaves.size() * sizeof(IdxLeaf));
+    if (!ix.segs.empty()) memcpy(&ar.h[off_ixsegs], ix.segs.data(), ix.segs.size() * sizeof(IdxSeg));
+    ix.spec.segs = (const IdxSeg*)(dA + off_ixsegs);
+    ix.spec.i64 = (unsigned long long*)P.i64.p;
+    ix.spec.seg_matched = (unsigned long long*)P.seg_matched.p;
   }
   if (!pre_leaves.empty()) {
     memcpy(&ar.h[off_leaves_orig], leaves_orig.data(), leaves_orig.size() * sizeof(LeafDesc));
@@ -3012,6 +3179,9 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       HIP_CHECK(launch_part_split2(ps, s));
     }
     HIP_CHECK(launch_part_aggregate(ps, s));
+  } else if (ix.on) {
+    t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
+    HIP_CHECK(launch_index_count(ix.spec, ix.blocks, s));
   } else if (q.num_items) {
     t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
     HIP_CHECK(launch_scan(q, blocks, s));
@@ -3055,8 +3225,9 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   t_timing.prepass_ms = pre_ms;
   t_timing.prefilter_ms = filt_ms;
   t_timing.scan_ms = scan_ms;
-  t_timing.scan_launches = (blocks ? 1 : 0) + (sp.on && q.num_items ? 1 : 0);  // + the selective stream
-  t_trace.path |= (blocks ? PG_PATH_FUSED_SCAN : 0u) | (sp.on && q.num_items ? PG_PATH_STREAM : 0u) |
+  t_timing.scan_launches = (blocks || (ix.on && ix.blocks) ? 1 : 0) + (sp.on && q.num_items ? 1 : 0);  // + the stream
+  t_trace.path |= (blocks && !ix.on ? PG_PATH_FUSED_SCAN : 0u) | (ix.on ? PG_PATH_INDEX_COUNT : 0u) |
+                  (sp.on && q.num_items ? PG_PATH_STREAM : 0u) |
                   (part.on ? PG_PATH_PARTITIONED : 0u) | (ns_docs || ns_matched ? PG_PATH_NONSCAN : 0u) |
                   (!pre.empty() || !luts.empty() ? PG_PATH_PREPASS : 0u);
   t_trace.stream_leaf = sp.on && q.num_items ? sp.leaf : 0xFFFFFFFFu;
@@ -3906,7 +4077,7 @@ int pg_resident_bytes(uint64_t* out) {
   uint64_t t = 0;
   for (auto& kv : g_segs)
     for (auto& c : kv.second->cols)
-      t += c.second.dict.bytes + c.second.words.bytes + c.second.mv_offsets.bytes + c.second.roaring.bytes +
+      t += c.second.dict.bytes + c.second.words.bytes + c.second.mv_offsets.bytes + c.second.mv_cnt.bytes + c.second.roaring.bytes +
            c.second.containers.bytes + c.second.inv_keydir.bytes + c.second.keymap.bytes + c.second.vals.bytes + c.second.rawv.bytes;
   *out = t;
   return PG_OK;

@@ -554,8 +554,12 @@ def test_per_segment_dictionaries_merge_by_value(gpu_engine, oracle_engine):
         assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q), table=t)
 
 
-def test_sorted_and_inverted_and_mv(gpu_engine, oracle_engine):
-    """Config-5 shape in miniature: sorted column, inverted-index leaves (incl. exclusive), MV COUNTMV + MV filter."""
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_sorted_and_inverted_and_mv(fused, monkeypatch, gpu_engine, oracle_engine):
+    """Config-5 shape in miniature: sorted column, inverted-index leaves (incl. exclusive), MV COUNTMV + MV filter --
+    through the fused index count (pg_index.hip: per-key LDS decode of the containers, no doc bitmaps) where the shape
+    allows it (fused=1, the default) and through the index pre-pass + fused scan (PG_INDEX_FUSED=0)."""
+    monkeypatch.setenv("PG_INDEX_FUSED", fused)
     rng = np.random.default_rng(3)
     n = 50000
     data = {"sortedCol": np.sort(rng.integers(0, 1000, n)), "inv1": rng.integers(0, 10, n),
@@ -572,9 +576,34 @@ def test_sorted_and_inverted_and_mv(gpu_engine, oracle_engine):
             "SELECT COUNT(*) FROM t WHERE mvTags NOT IN (1, 2, 3, 4, 5, 6, 7, 8, 9, 10)",
             "SELECT inv1, COUNTMV(mvTags), SUM(inv4) FROM t WHERE sortedCol IN (5, 77, 800) OR inv2 > 90 GROUP BY inv1",
             "SELECT COUNT(*) FROM t WHERE sortedCol NOT IN (5, 6, 7) AND inv1 NOT IN (0, 1)",
+            "SELECT COUNTMV(mvTags) FROM t",
+            "SELECT COUNT(*), COUNTMV(mvTags) FROM t WHERE NOT (inv1 IN (1, 2) AND inv3 < 500) OR inv4 = 77",
+            "SELECT COUNT(*) FROM t WHERE inv2 NOT IN (3, 4) AND NOT inv1 = 5 AND sortedCol >= 10",
         ]:
             q = parse(sql)
             assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q), table=t)
+    t = Table("t", [seg])
+    gpu_engine.execute(t, "SELECT COUNT(*), COUNTMV(mvTags) FROM t WHERE sortedCol BETWEEN 100 AND 600 AND inv1 = 3")
+    assert ("index_count" in gpu_engine.last_trace()["path"]) == (fused == "1")
+
+
+def test_fused_index_count_wide_mv_rows(gpu_engine, oracle_engine):
+    """COUNTMV through the fused index count when some doc holds more than 15 values (no 4-bit count column: the row
+    offsets), with segments whose inverted leaf is a constant (a dictId absent from one segment)."""
+    rng = np.random.default_rng(5)
+    segs = []
+    for s_ in range(3):
+        n = 40_000 + 999 * s_
+        data = {"inv": rng.integers(0, 50 + 10 * s_, n),
+                "tags": [list(rng.integers(0, 300, rng.integers(1, 40 if s_ == 1 else 6))) for _ in range(n)]}
+        segs.append(_seg(f"w{s_}", data, {"inv": "INT", "tags": "INT"}, inverted=["inv"]))
+    t = Table("t", segs)
+    for sql in ["SELECT COUNT(*), COUNTMV(tags) FROM t WHERE inv IN (1, 7, 55, 59)",
+                "SELECT COUNTMV(tags) FROM t WHERE inv <> 3",
+                "SELECT COUNT(*), COUNTMV(tags) FROM t WHERE inv = 58 OR inv = 2"]:
+        q = parse(sql)
+        assert_same_result(gpu_engine.execute(t, q), oracle_engine.execute(t, q), table=t)
+        assert "index_count" in gpu_engine.last_trace()["path"]
 
 
 def test_config5_full_segment_matches_oracle(gpu_engine, oracle_engine):
