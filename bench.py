@@ -120,12 +120,14 @@ def lines_bytes(num_docs, width, needed):
 
 
 def index_plan_bytes(eng, table, plan, index_meta, rows, sql):
-    """Config 5: the bytes its plan must move.  Per segment: the roaring bitmaps of the dictIds the inverted leaves
-    select (read once), each inverted leaf's doc bitmap (written by the pre-pass, re-read by the scan within the
-    sorted leaf's doc range; NOT_EQ also re-reads and re-writes it to flip it), and the MV row offsets of the matching
-    docs (COUNTMV).  The sorted leaf becomes a doc range on the host (no device bytes).  Returns (plan bytes, SURVEY
-    §8(d) algorithmic bytes = referenced roaring bytes + sorted pairs + the MV start-of-row bitmap over the sorted
-    range, [docs in the sorted range, matched docs])."""
+    """Config 5: the bytes its plan must read, on SURVEY §8(d)'s definition.  Per segment: the serialized roaring
+    bytes of the dictIds the inverted leaves select, within the 64 K-doc keys of the sorted leaf's doc range (the
+    fused index count decodes only those keys' containers; docs are uniform over the keys, so the range's share of
+    each bitmap), the sorted index's (start, end) pairs, and the value counts of the docs in that range at 4 bits per
+    doc (the count column COUNTMV reads, the device's form of the MV start-of-row bitmap, <= 0.5 B / doc).  No doc bitmap
+    is written or read: the leaves are decoded in LDS (pg_index.hip).  Returns (plan bytes, SURVEY §8(d) algorithmic
+    bytes = every referenced roaring byte + sorted pairs + the start-of-row bitmap over the sorted range,
+    [docs in the sorted range, matched docs])."""
     import numpy as np
     where = sql.split(" WHERE ")[1]
     sp = [p for p in plan.query.filter.leaves() if p.column == "sortedCol"][0]
@@ -135,7 +137,6 @@ def index_plan_bytes(eng, table, plan, index_meta, rows, sql):
     S = len(index_meta)
     frac_range = in_range / (S * rows)
     total = alg = 0.0
-    bm = rows / 8
     for si, meta in enumerate(index_meta):
         ref = 0
         for li, lw in enumerate(plan.lowered[si]):
@@ -144,9 +145,9 @@ def index_plan_bytes(eng, table, plan, index_meta, rows, sql):
                 continue
             ids = np.asarray(lw.ids, dtype=np.int64)
             ref += int((offs[ids + 1] - offs[ids]).sum())
-            total += bm + frac_range * bm + (2 * bm if lw.exclusive else 0)
-        total += ref + 2 * lines_bytes(rows + 1, 32, matched / S)  # offsets[d], offsets[d + 1] of matching docs
-        alg += ref + 8 * meta["sortedCol"][1] + frac_range * meta["mvTags"][2] / 8
+        pairs = 8 * meta["sortedCol"][1]
+        total += frac_range * ref + pairs + frac_range * rows / 2
+        alg += ref + pairs + frac_range * meta["mvTags"][2] / 8
     return total, alg, [in_range, matched]
 
 

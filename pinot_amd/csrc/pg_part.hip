@@ -62,6 +62,21 @@ constexpr uint32_t kAT = PG_AGG_THREADS;  // threads of a part_aggregate block
 constexpr uint32_t kSplitChunk = PG_SPLIT_CHUNK;  // entries counting-sorted per LDS round (16 per thread): longer runs per digit
 // (16 384 x 1 024 threads, one block per CU: split1 4.08 -> 3.10 ms, split2 2.71 -> 2.15 ms on config 4 vs 4 096 x 256)
 
+// The compile-time knobs (tools/part_variant.sh builds variants with -D) and what they size.  split_round scans the
+// digit counts with one thread per digit (<= 256 digits) in whole waves, each thread holds E = chunk / threads
+// entries in registers, and the chunk's sorted entries + digits live in the kernel's static LDS next to cnt / start /
+// cur; part_aggregate and part_direct stride their LDS tables by their thread counts.  A combination outside these
+// bounds would index past an LDS array (the r03 sweep's illegal access came from an ablation build whose flags were
+// not recorded: part_variant.sh now writes them next to the library).
+static_assert(kST % 64 == 0 && kST >= 256 && kST <= 1024, "split blocks: whole waves, one thread per digit (<= 256)");
+static_assert(kSplitChunk % kST == 0 && kSplitChunk / kST >= 1 && kSplitChunk / kST <= 32,
+              "split chunk: E = chunk / threads entries per thread, held in registers");
+static_assert(4ull * kSplitChunk + kSplitChunk + 2 * 4 * 256 + 8 * 256 <= 160 * 1024,
+              "split1's static LDS (sorted entries + digits + cnt / start / cur) must fit a CU");
+static_assert(PG_SPLIT_WAVES >= 1 && PG_SPLIT_WAVES * 256 >= kST / 4, "split register budget: >= one block per CU");
+static_assert(kAT % 64 == 0 && kAT >= 64 && kAT <= 1024, "part_aggregate blocks: whole waves");
+static_assert(kPartLdsBytes <= 160 * 1024, "one bucket's LDS state must fit a CU");
+
 __device__ __forceinline__ rsrc_t part_rsrc(const void* p, uint32_t bytes) {
   const uint64_t a = (uint64_t)p;
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
@@ -497,6 +512,7 @@ __global__ __launch_bounds__(kST) void part_scatter_kernel(PartScanSpec P) {
 constexpr uint32_t kDT = PG_DIRECT_THREADS;   // threads of a part_direct block
 constexpr uint32_t kDE = kTileDocs / kDT;     // docs per thread per round (a round is one tile)
 static_assert(kDE * kDT == kTileDocs && kDT >= kPartL1, "one digit per thread in the run scan");
+static_assert(kDT % 64 == 0 && kDT <= 1024 && kDE <= 32, "part_direct blocks: whole waves, <= 32 docs per thread");
 
 // The tile's word range [w0, w0 + nw) of a packed column into LDS (16-byte loads; reads past the column return 0).
 // nw is a multiple of 4 plus the 4 words of padding the unpack's 64-bit window may touch.

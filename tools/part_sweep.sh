@@ -5,6 +5,7 @@ mkdir -p gpurun_out
 for V in $VARIANTS; do
   N=${V%%:*}; E=${V#*:}; [ "$E" = "$V" ] && E=""
   L=pinot_amd/libpinot_gpu.so; [ "$N" != "main" ] && L=pinot_amd/libpinot_gpu_$N.so
+  [ -f "${L%.so}.flags" ] && echo "$N flags: $(cat ${L%.so}.flags)" | tee gpurun_out/sw_$N.flags
   env PINOT_GPU_LIB=$L ${E//,/ } timeout -k 10 300 python -u bench.py --workload highcard --steps 10 --warmup 3 --no-cpu > gpurun_out/sw_$N.json 2> gpurun_out/sw_$N.err \
     || { echo "bench $N failed"; tail -20 gpurun_out/sw_$N.err; exit 1; }
   echo "$V: $(python3 -c "import json;d=json.loads(open('gpurun_out/sw_$N.json').read().strip().splitlines()[-1]);print(round(d['ms_per_step'],3),d['step_breakdown_ms']['scan_ms'],d['step_breakdown_ms']['finalize_ms'])")"

@@ -9,4 +9,5 @@ FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -munsafe-fp-ato
 $HIPCC $FL "$@" -c pg_part.hip -o build/pg_part_$N.o
 OBJS=$(ls build/*.o | grep -v 'pg_part' | tr '\n' ' ')
 $HIPCC --offload-arch=gfx950 -shared -o ../libpinot_gpu_$N.so $OBJS build/pg_part_$N.o
-echo built ../libpinot_gpu_$N.so
+echo "$*" > ../libpinot_gpu_$N.flags  # the -D flags of this variant, read back by part_sweep.sh
+echo built ../libpinot_gpu_$N.so "($*)"
