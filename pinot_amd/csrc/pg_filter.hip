@@ -327,10 +327,15 @@ __host__ __device__ __forceinline__ uint32_t stream_lds_words(const StreamSpec& 
   return exact ? kExactLutWords : p.set_lds_ints + (p.num_extra ? 4u * p.stage_words : 0u);
 }
 
+#ifndef PG_STREAM_PIPE_EXTRA
+#define PG_STREAM_PIPE_EXTRA 1  // the variant with further leaves pipelines the driving leaf's loads too (5 waves / SIMD)
+#endif
+
 template <int B, bool EXTRA, int NT>
-__global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? 6 : 7)) void stream_kernel(StreamSpec p) {
+__global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? (PG_STREAM_PIPE_EXTRA && B <= 20 ? 5 : 6) : 7)) void stream_kernel(StreamSpec p) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_sets[];
   constexpr bool EXACT = NT == 1024;
+  constexpr bool PIPE = EXACT || (EXTRA && PG_STREAM_PIPE_EXTRA && B <= 20);
   uint32_t& cursor = lds_sets[stream_lds_words(p, EXACT)];
   // the exact LUT's lookups address LDS absolutely (eval_group): the dynamic LDS must start at address 0
   if (EXACT && threadIdx.x == 0 && (uint32_t)(uintptr_t)(lds_cptr)lds_sets != 0u) atomicOr(p.err, 64u);
@@ -374,12 +379,12 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? 6 : 7)) void stream_k
       // the 256-thread variants run 6-7 waves / SIMD and would spill)
       const rsrc_t rs = rsrc_of(L.words, L.wbytes);
       uint32_t w[B + 1];
-      if (EXACT && wi.tile_begin + tid < wi.tile_end) load_group<B>(rs, wi.tile_begin + tid, w);
+      if (PIPE && wi.tile_begin + tid < wi.tile_end) load_group<B>(rs, wi.tile_begin + tid, w);
       for (uint32_t g0 = wi.tile_begin; g0 < wi.tile_end; g0 += NT) {
         const uint32_t g = g0 + tid;
         const uint64_t d0 = (uint64_t)g * 32;
         uint32_t m = 0;
-        if (EXACT) {
+        if (PIPE) {
           uint32_t wn[B + 1];
           if (g + NT < wi.tile_end) load_group<B>(rs, g + NT, wn);
           if (g < wi.tile_end && d0 < nd) {
