@@ -10,7 +10,10 @@
 // but as ONE fused launch over all of the query's segments on this GPU (plus a small pre-pass for
 // index-backed leaves), with per-group state merged in device memory by global key id.
 #include <hip/hip_runtime.h>
+#include <execinfo.h>
 #include <sched.h>
+#include <signal.h>
+#include <unistd.h>
 #include <time.h>
 
 #include <algorithm>
@@ -2593,7 +2596,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   {
     const char* ix_env = getenv("PG_INDEX_FUSED");
     bool ok = !(ix_env && atoi(ix_env) == 0) && K == 0 && A >= 1 && L <= kIdxMaxLeaves && !part.on && !sp.on &&
-              pre_leaves.empty();
+              pre_leaves.empty() && luts.empty();  // the scratch (LUTs, bitmaps) is not allocated when fused
     uint32_t cntmv = 0xFFFFFFFFu, cntmv_col = 0;
     for (uint32_t a = 0; a < A && ok; a++) {
       const pg_agg& g = plan->aggs[a];
@@ -2887,7 +2890,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   {
     size_t k = 0;
     for (const PrepassOp& op : pre) {
-      if (op.kind != PrepassOp::ROARING || !op.nkeys) continue;
+      if (ix.on || op.kind != PrepassOp::ROARING || !op.nkeys) continue;  // the same selection as the job list above
       RoaringJob& j = rjobs[k++];
       j.roaring = (const uint8_t*)op.col->roaring.p;
       j.cs = (const RoaringContainer*)op.col->containers.p;
@@ -4051,8 +4054,20 @@ extern "C" {
 
 int pg_abi_version(void) { return PG_ABI_VERSION; }
 
+// PG_SEGV_TRACE=1: a host SIGSEGV prints the native frames (library offsets for addr2line) before the default action
+static void segv_trace(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  const char msg[] = "libpinot_gpu: fatal signal, native frames:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 int pg_init(int device) {
   std::lock_guard<std::mutex> g(g_init_mu);
+  if (getenv("PG_SEGV_TRACE") && atoi(getenv("PG_SEGV_TRACE"))) signal(SIGSEGV, segv_trace);
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(PG_E_HIP, "no HIP device visible");
   if (device < 0 || device >= n) return fail(PG_E_INVALID, "device %d out of range (%d visible)", device, n);
