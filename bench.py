@@ -335,6 +335,11 @@ def main():
         for k, v in parts.items():
             v.append(getattr(tm, k))
     value = rows_per_gpu * world * args.steps / el
+    # the kernels the last step ran (pg_last_trace), named for the roofline line
+    path = set(eng.last_trace()["path"]) if world == 1 else set()
+    kernels = [k for p, k in (("prepass", "prepass"), ("stream", "stream_kernel"), ("fused_scan", "scan_kernel"),
+                              ("partitioned", "part_direct + part_split2s + part_aggregate"),
+                              ("index_count", "index_count_kernel")) if p in path]
     scan_avg_ms = float(np.mean(scan_ms))
     alg_bytes = fwd_bytes + dict_bytes
     achieved = plan_bytes / (scan_avg_ms * 1e-3) / 1e9
@@ -406,7 +411,8 @@ def main():
                        "parallelism": f"segments x{world}" + (" (table split)" if args.split_table else "")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "stream_kernel + scan_kernel" if tm.scan_launches > 1 else "scan_kernel",
+                         "kernel": " + ".join(kernels) or ("stream_kernel + scan_kernel" if tm.scan_launches > 1
+                                                           else "scan_kernel"),
                          "kernel_ms": scan_avg_ms,
                          "plan_bytes": plan_bytes, "stage_docs": stage_docs,
                          "algorithmic_bytes": alg_bytes, "algorithmic_frac": alg_achieved / HBM_PEAK_GBS,

@@ -3008,6 +3008,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   CancelSlot cancel(plan->query_id, plan->query_id != 0 || plan->deadline_ms != 0);
   q.cancel = cancel.device_ptr();
   std::vector<uint64_t> direct_matched;
+  bool scan_ran = false;  // the fused scan (pg_scan.hip) was launched: the trace's FUSED_SCAN path
   if (q.num_items && part.on) {
     // radix-partitioned group-by (pg_part.hip).  Filter matching every doc and one group key: level-1 partitions
     // straight from the columns into fixed-capacity regions (part_direct), level 2 likewise (part_split2s): no
@@ -3139,6 +3140,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       HIP_CHECK(launch_part_scatter(pss, s));
     } else {
       HIP_CHECK(launch_scan(q, blocks, s));
+      scan_ran = true;
       HIP_CHECK(launch_exclusive_sum((const uint64_t*)h1, (uint64_t*)o1, n1 + 1, p_temp.p, tb, s));
     }
     PartSpec ps;
@@ -3188,6 +3190,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   } else if (q.num_items) {
     t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
     HIP_CHECK(launch_scan(q, blocks, s));
+    scan_ran = true;
   }
   HIP_CHECK(hipEventRecord(ev[2], s));
   const uint64_t n_sm = (S ? S : 1) + 2;
@@ -3229,10 +3232,10 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   t_timing.prefilter_ms = filt_ms;
   t_timing.scan_ms = scan_ms;
   t_timing.scan_launches = (blocks || (ix.on && ix.blocks) ? 1 : 0) + (sp.on && q.num_items ? 1 : 0);  // + the stream
-  t_trace.path |= (blocks && !ix.on ? PG_PATH_FUSED_SCAN : 0u) | (ix.on ? PG_PATH_INDEX_COUNT : 0u) |
+  t_trace.path |= (scan_ran ? PG_PATH_FUSED_SCAN : 0u) | (ix.on ? PG_PATH_INDEX_COUNT : 0u) |
                   (sp.on && q.num_items ? PG_PATH_STREAM : 0u) |
                   (part.on ? PG_PATH_PARTITIONED : 0u) | (ns_docs || ns_matched ? PG_PATH_NONSCAN : 0u) |
-                  (!pre.empty() || !luts.empty() ? PG_PATH_PREPASS : 0u);
+                  ((!pre.empty() && !ix.on) || !luts.empty() ? PG_PATH_PREPASS : 0u);
   t_trace.stream_leaf = sp.on && q.num_items ? sp.leaf : 0xFFFFFFFFu;
   t_trace.group_mode = (uint32_t)P.mode;
   t_trace.num_slots = P.num_slots;

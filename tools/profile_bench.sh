@@ -13,7 +13,7 @@ R=$(pwd)
 O=$R/gpurun_out
 T=${TAG}_${WL}
 # the hot-path kernels bench.py's roofline times (pre-pass + stream + scan / partition passes)
-HOT="pg::(scan|stream|part_[a-z0-9]+|roaring_keys|set_lut_bits|fill_ranges|mv_scan|bitmap_not)_kernel"
+HOT="pg::(scan|stream|part_[a-z0-9]+|roaring_keys|index_count|set_lut_bits|fill_ranges|mv_scan|bitmap_not)_kernel"
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 420 python3 $R/bench.py --workload $WL $EXTRA > $O/${T}_bench.json 2> $O/${T}_bench.err || { echo "bench failed"; tail -20 $O/${T}_bench.err; exit 1; }
