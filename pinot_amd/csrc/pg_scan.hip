@@ -914,7 +914,11 @@ __host__ __device__ inline size_t scan_queue_off(const QuerySpec& q) {
 }
 
 template <bool GROUPED, int MAXA, int MAXK>
-__global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_WAVES_AGG) void scan_kernel(QuerySpec q) {
+__global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_WAVES_AGG) void scan_kernel(QuerySpec qarg) {
+  // the spec is read where the launch put it (the kernel-argument segment, offset 0): bound by reference to the
+  // by-value parameter, a lane-varying index into it made the compiler copy all of it to scratch (1.4 KB per lane)
+  const QuerySpec& q = *(const QuerySpec*)__builtin_amdgcn_kernarg_segment_ptr();
+  (void)qarg;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* stage = (uint32_t*)(smem + 16);                                   // staging ring (16 bytes in: st[-1])
   int32_t* lds_sets = (int32_t*)(stage + q.stage_ring * q.stage_lds_words);  // IN-list filter bitmaps / hash sets
