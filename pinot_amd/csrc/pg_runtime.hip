@@ -2703,7 +2703,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         g.key0 = nk ? lo >> 16 : 0u;
         g.first_block = ix.blocks;
         ix.blocks += nk;
-        if (cntmv != 0xFFFFFFFFu && nk) {
+        if (ok && cntmv != 0xFFFFFFFFu && nk) {  // (ok: a leaf above may have ruled the fused count out)
           const ColumnRes* c = col(si, cntmv_col);
           ok = c && c->fwd == FWD_MV && c->mv_offsets.p;
           if (ok) {

@@ -585,6 +585,9 @@ def test_sorted_and_inverted_and_mv(fused, monkeypatch, gpu_engine, oracle_engin
     t = Table("t", [seg])
     gpu_engine.execute(t, "SELECT COUNT(*), COUNTMV(mvTags) FROM t WHERE sortedCol BETWEEN 100 AND 600 AND inv1 = 3")
     assert ("index_count" in gpu_engine.last_trace()["path"]) == (fused == "1")
+    # a scan leaf (inv3 < 500 is a dictId range: no range index) anywhere in the filter rules the fused count out
+    gpu_engine.execute(t, "SELECT COUNT(*), COUNTMV(mvTags) FROM t WHERE NOT (inv1 IN (1, 2) AND inv3 < 500)")
+    assert "index_count" not in gpu_engine.last_trace()["path"]
 
 
 def test_fused_index_count_wide_mv_rows(gpu_engine, oracle_engine):
