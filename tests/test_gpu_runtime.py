@@ -154,11 +154,17 @@ def test_trace_records_each_device_call(gpu_engine, sv_table_inter):
     assert tr["reruns"] == 0 and tr["num_segments"] == 3 and tr["device_ms"] > 0
     # the reference's test data: sorted daysSinceEpoch, inverted column11, a scan on column1
     gpu_engine.execute(sv_table_inter, "SELECT COUNT(*) FROM t WHERE daysSinceEpoch = 126164076 AND "
-                                       "column11 IN ('P', 'o') AND column1 > 100000")
+                                       "column11 IN ('P', 'o') AND column6 < 500000000")
     tr = gpu_engine.last_trace()
     assert tr["leaf_forms"][0] == {"SORTED_RANGE": 4}
     assert tr["leaf_forms"][1] == {"INVERTED": 4} and "prepass" in tr["path"]
-    assert tr["leaf_forms"][2] == {"SCAN_RANGE": 4}
+    assert "SCAN_RANGE" in tr["leaf_forms"][2] and "index_count" not in tr["path"]
+    # index leaves only (sorted range + inverted set) under COUNT(*): the fused index count, no pre-pass bitmaps
+    gpu_engine.execute(sv_table_inter, "SELECT COUNT(*) FROM t WHERE daysSinceEpoch = 126164076 AND "
+                                       "column11 IN ('P', 'o')")
+    tr = gpu_engine.last_trace()
+    assert tr["leaf_forms"][0] == {"SORTED_RANGE": 4} and tr["leaf_forms"][1] == {"INVERTED": 4}
+    assert tr["path"] == ["index_count"]
     # metadata answers: MIN / MAX / COUNT over match-all segments
     gpu_engine.execute(sv_table_inter, "SELECT COUNT(*), MAX(column1) FROM t")
     tr = gpu_engine.last_trace()
