@@ -328,7 +328,7 @@ __host__ __device__ __forceinline__ uint32_t stream_lds_words(const StreamSpec& 
 }
 
 #ifndef PG_STREAM_PIPE_EXTRA
-#define PG_STREAM_PIPE_EXTRA 1  // the variant with further leaves pipelines the driving leaf's loads too (5 waves / SIMD)
+#define PG_STREAM_PIPE_EXTRA 0  // 1: the variant with further leaves pipelines the driving leaf's loads too (5 waves / SIMD; config 3 stream 0.713 vs 0.596 ms, r04d)
 #endif
 
 template <int B, bool EXTRA, int NT>
