@@ -4,7 +4,8 @@
 //
 // Chunk word w, bit 31 - j <-> doc key * 65 536 + 32 w + j (the packed 1-bit column order).  Containers follow the
 // RoaringBitmap portable format (RoaringBitmap 0.9.28): array (sorted uint16), bitmap (1 024 little-endian uint64) and
-// run ((start, length - 1) uint16 pairs) containers, re-laid 8-byte aligned at upload (pg_runtime.hip).
+// run ((start, length - 1) uint16 pairs) containers, re-laid 8-byte aligned at upload, the payload region padded to
+// whole 8-byte words (pg_runtime.hip parse_inverted), so an array container is read as 8-byte quads of 4 entries.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -12,13 +13,19 @@
 
 namespace pg {
 
+// dictIds per thread per round: a round issues R directory loads, then R container loads, per thread before any is
+// consumed, and expands the round's array containers in one pass
+constexpr int kRoarR = 4;
+
 // LDS scratch of one chunk build (besides the chunk itself)
 template <int NT>
 struct RoaringLds {
-  uint32_t bml[NT];      // bitmap containers of this round, processed by the whole block
+  uint32_t bml[NT * kRoarR];  // bitmap containers of this round (payload offsets), OR-ed by the whole block
   uint32_t nbml;
-  uint32_t apre[NT + 1];  // array containers of this round: exclusive prefix of their cardinalities
-  uint32_t aoff[NT];      //   and their payload offsets (slot = the thread that found the container)
+  uint32_t tpre[NT + 1];      // exclusive prefix over the threads of their array containers' quads (4 entries each)
+  uint32_t aoff[kRoarR][NT];  // thread t's j-th array container of the round: payload offset,
+  uint16_t aq0[kRoarR][NT];   //   its first quad among t's quads (0xFFFF: no such container),
+  uint16_t acard[kRoarR][NT]; //   its cardinality
   uint32_t wsum[NT / 64];
 };
 
@@ -29,51 +36,65 @@ __device__ __forceinline__ void roaring_key_chunk(const uint8_t* __restrict__ ro
                                                   const uint32_t* __restrict__ dir, const uint32_t* __restrict__ keydir,
                                                   uint32_t card, const int32_t* __restrict__ ids, uint32_t nids,
                                                   uint32_t key, uint32_t* chunk, RoaringLds<NT>& S) {
+  constexpr int R = kRoarR;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   if (tid == 0) S.nbml = 0;
   __syncthreads();
-  for (uint32_t r0 = 0; r0 < nids; r0 += NT) {
-    const uint32_t i = r0 + tid;
-    uint32_t alen = 0, aoffset = 0;  // this thread's array container (entries are spread over the block below)
-    if (i < nids) {
-      const uint32_t id = (uint32_t)ids[i];
-      uint32_t a;
-      bool hit;
-      if (keydir) {  // one load: the key-major directory built at upload
-        a = keydir[(uint64_t)key * card + id];
-        hit = a != 0xFFFFFFFFu;
-      } else {
-        a = dir[id];
-        uint32_t b = dir[id + 1];  // this dictId's containers, ascending keys: find `key`
-        while (a < b) {
-          const uint32_t m = (a + b) >> 1;
-          if (cs[m].key < key) a = m + 1; else b = m;
-        }
-        hit = a < dir[id + 1] && cs[a].key == key;
-      }
-      if (hit) {
-        const RoaringContainer c = cs[a];
-        const uint8_t* p = roaring + c.offset;
-        if (c.type == 0) {  // array of uint16: expanded by the whole block
-          alen = c.card;
-          aoffset = c.offset;
-        } else if (c.type == 2) {  // runs: uint16 nruns, then (start, length - 1)
-          const uint16_t* rr = (const uint16_t*)p + 1;
-          for (uint32_t k = 0; k < c.card; k++) {
-            const uint32_t st = rr[2 * k], en = st + rr[2 * k + 1];
-            for (uint32_t w = st >> 5; w <= (en >> 5); w++) {
-              const uint32_t l = w * 32 > st ? 0 : st - w * 32, h = w * 32 + 31 < en ? 31 : en - w * 32;
-              const uint32_t mask = (h == 31 ? 0xFFFFFFFFu : ((1u << (h + 1)) - 1u)) & ~((1u << l) - 1u);
-              atomicOr(&chunk[w], __builtin_bitreverse32(mask));
-            }
+  for (uint32_t r0 = 0; r0 < nids; r0 += NT * R) {
+    // 1. the container of `key` of each of this thread's dictIds: all directory loads, then all container loads
+    uint32_t a[R];
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+      const uint32_t i = r0 + tid + NT * k;
+      a[k] = 0xFFFFFFFFu;
+      if (i < nids) {
+        const uint32_t id = (uint32_t)ids[i];
+        if (keydir) {  // one load: the key-major directory built at upload
+          a[k] = keydir[(uint64_t)key * card + id];
+        } else {  // this dictId's containers, ascending keys: find `key`
+          uint32_t lo = dir[id], hi = dir[id + 1];
+          const uint32_t end = hi;
+          while (lo < hi) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (cs[m].key < key) lo = m + 1; else hi = m;
           }
-        } else {
-          S.bml[atomicAdd(&S.nbml, 1u)] = c.offset;
+          a[k] = lo < end && cs[lo].key == key ? lo : 0xFFFFFFFFu;
         }
       }
     }
-    // exclusive prefix of the array cardinalities over the block (wave scan + wave sums)
-    uint32_t x = alen;
+    RoaringContainer c[R];
+#pragma unroll
+    for (int k = 0; k < R; k++) c[k] = a[k] != 0xFFFFFFFFu ? cs[a[k]] : RoaringContainer{0u, 3u, 0u, 0u};
+    // 2. classify: arrays -> this thread's quad list, bitmaps -> the block's list, runs expanded here
+    uint32_t nq = 0;
+    int na = 0;
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+      if (c[k].type == 0) {
+        S.aoff[na][tid] = c[k].offset;
+        S.aq0[na][tid] = (uint16_t)nq;
+        S.acard[na][tid] = (uint16_t)c[k].card;
+        nq += (c[k].card + 3u) >> 2;
+        na++;
+      } else if (c[k].type == 1) {
+        S.bml[atomicAdd(&S.nbml, 1u)] = c[k].offset;
+      } else if (c[k].type == 2) {  // runs: uint16 nruns, then (start, length - 1)
+        const uint16_t* rr = (const uint16_t*)(roaring + c[k].offset) + 1;
+        for (uint32_t q = 0; q < c[k].card; q++) {
+          const uint32_t st = rr[2 * q], en = st + rr[2 * q + 1];
+          for (uint32_t w = st >> 5; w <= (en >> 5); w++) {
+            const uint32_t l = w * 32 > st ? 0 : st - w * 32, h = w * 32 + 31 < en ? 31 : en - w * 32;
+            const uint32_t mask = (h == 31 ? 0xFFFFFFFFu : ((1u << (h + 1)) - 1u)) & ~((1u << l) - 1u);
+            atomicOr(&chunk[w], __builtin_bitreverse32(mask));
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < R; k++)
+      if (k >= na) S.aq0[k][tid] = 0xFFFFu;
+    // exclusive prefix of the threads' quad counts (wave scan + wave sums)
+    uint32_t x = nq;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t y = __shfl_up(x, o);
@@ -83,26 +104,52 @@ __device__ __forceinline__ void roaring_key_chunk(const uint8_t* __restrict__ ro
     __syncthreads();
     uint32_t wb = 0;
     for (uint32_t w = 0; w < wave; w++) wb += S.wsum[w];
-    S.apre[tid] = wb + x - alen;
-    S.aoff[tid] = aoffset;
-    if (tid == NT - 1) S.apre[NT] = wb + x;
+    S.tpre[tid] = wb + x - nq;
+    if (tid == NT - 1) S.tpre[NT] = wb + x;
     __syncthreads();
-    // every array entry of the round, one per thread per step: container k = the last prefix <= e
-    const uint32_t total = S.apre[NT];
-    for (uint32_t e = tid; e < total; e += NT) {
-      uint32_t a = 0, b = NT;
-      while (b - a > 1) {
-        const uint32_t m = (a + b) >> 1;
-        if (S.apre[m] <= e) a = m; else b = m;
+    // 3. every quad of the round's array containers, two per thread per step (both loads in flight): owner thread =
+    //    the last prefix <= e, then its container; 4 entries per 8-byte load
+    const uint32_t total = S.tpre[NT];
+    for (uint32_t e0 = tid; e0 < total; e0 += 2 * NT) {
+      uint2 w[2];
+      uint32_t n[2];
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const uint32_t e = e0 + (uint32_t)u * NT;
+        n[u] = 0;
+        w[u] = make_uint2(0u, 0u);
+        if (e < total) {
+          uint32_t lo = 0, hi = NT;
+          while (hi - lo > 1) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (S.tpre[m] <= e) lo = m; else hi = m;
+          }
+          const uint32_t local = e - S.tpre[lo];
+          int j = 0;
+#pragma unroll
+          for (int k = 1; k < R; k++)
+            if (S.aq0[k][lo] <= local) j = k;
+          const uint32_t q = local - S.aq0[j][lo];
+          const uint32_t left = (uint32_t)S.acard[j][lo] - 4u * q;
+          n[u] = left < 4u ? left : 4u;
+          w[u] = *(const uint2*)(roaring + S.aoff[j][lo] + 8u * q);
+        }
       }
-      const uint32_t v = ((const uint16_t*)(roaring + S.aoff[a]))[e - S.apre[a]];
-      atomicOr(&chunk[v >> 5], 0x80000000u >> (v & 31u));
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const uint32_t v4[4] = {w[u].x & 0xFFFFu, w[u].x >> 16, w[u].y & 0xFFFFu, w[u].y >> 16};
+#pragma unroll
+        for (int h = 0; h < 4; h++)
+          if ((uint32_t)h < n[u]) atomicOr(&chunk[v4[h] >> 5], 0x80000000u >> (v4[h] & 31u));
+      }
     }
     __syncthreads();  // the bitmap containers below OR whole words without atomics
-    for (uint32_t k = 0; k < S.nbml; k++) {  // bitmap containers: 1 024 little-endian uint64 words each
-      const uint32_t* w32 = (const uint32_t*)(roaring + S.bml[k]);
-      for (uint32_t w = tid; w < 2048; w += NT) chunk[w] |= __builtin_bitreverse32(w32[w]);
-      __syncthreads();
+    // 4. bitmap containers: 1 024 little-endian uint64 words each; a thread owns the same chunk words for all of them
+    const uint32_t nb = S.nbml;
+    for (uint32_t wd = tid; wd < 2048; wd += NT) {
+      uint32_t v = 0;
+      for (uint32_t k = 0; k < nb; k++) v |= ((const uint32_t*)(roaring + S.bml[k]))[wd];
+      if (nb) chunk[wd] |= __builtin_bitreverse32(v);
     }
     __syncthreads();
     if (tid == 0) S.nbml = 0;

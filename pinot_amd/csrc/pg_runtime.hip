@@ -488,6 +488,7 @@ int parse_inverted(const std::vector<uint8_t>& b, uint32_t card, std::vector<uin
     }
   }
   dir[card] = (uint32_t)cs.size();
+  payload.resize((payload.size() + 7) & ~7ull);  // whole 8-byte words: the device reads array entries 4 at a time
   return PG_OK;
 }
 
