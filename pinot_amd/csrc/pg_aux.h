@@ -51,6 +51,13 @@ struct RoaringContainer {
   uint32_t card;     // array: cardinality; run: number of runs
   uint32_t offset;   // byte offset of the payload within the column's roaring region
 };
+// Key-major directory entry (x = payload offset, y = type << 30 | card; ~0 ~0: the dictId has no container under the
+// key): the container's descriptor itself, so a key's lookup is one 8-byte load, not a directory load and then a
+// dependent descriptor load.
+__host__ __device__ inline uint2 keydir_entry(const RoaringContainer& c) {
+  return make_uint2(c.offset, (c.type << 30) | c.card);
+}
+constexpr uint32_t kKeyDirNone = 0xFFFFFFFFu;
 hipError_t launch_roaring_or(const uint8_t* roaring, const RoaringContainer* containers, const uint32_t* sel,
                              uint32_t nsel, uint32_t num_docs, uint32_t* bitmap, hipStream_t s);
 hipError_t launch_bitmap_not(uint32_t* bitmap, uint32_t num_docs, hipStream_t s);
@@ -66,7 +73,7 @@ struct RoaringJob {
   uint32_t nids, num_docs;
   uint32_t* bm;                    // doc bitmap (packed 1-bit column order)
   uint32_t negate, key0, nkeys, first_block;  // first_block: prefix of nkeys over the jobs
-  const uint32_t* keydir;          // optional key-major directory: [key * card + dictId] = container or ~0
+  const uint2* keydir;             // optional key-major directory: [key * card + dictId] = the container (KeyDirEntry)
   uint32_t card, pad;
 };
 hipError_t launch_roaring_keys(const RoaringJob* jobs, uint32_t njobs, uint32_t blocks, hipStream_t s);
@@ -82,7 +89,7 @@ struct IdxLeaf {                   // leaf l of segment s
   const uint8_t* roaring;          // IL_ROARING: the column's containers and the selected dictIds
   const RoaringContainer* cs;
   const uint32_t* dir;
-  const uint32_t* keydir;
+  const uint2* keydir;
   const int32_t* ids;
   uint32_t nids, card;
 };

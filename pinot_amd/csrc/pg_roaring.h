@@ -4,8 +4,9 @@
 //
 // Chunk word w, bit 31 - j <-> doc key * 65 536 + 32 w + j (the packed 1-bit column order).  Containers follow the
 // RoaringBitmap portable format (RoaringBitmap 0.9.28): array (sorted uint16), bitmap (1 024 little-endian uint64) and
-// run ((start, length - 1) uint16 pairs) containers, re-laid 8-byte aligned at upload, the payload region padded to
-// whole 8-byte words (pg_runtime.hip parse_inverted), so an array container is read as 8-byte quads of 4 entries.
+// run ((start, length - 1) uint16 pairs) containers, re-laid 8-byte aligned and key-major (by key, then dictId) at upload,
+// the payload region padded to whole 8-byte words (pg_runtime.hip parse_inverted), so an array container is read as
+// 8-byte quads of 4 entries.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -13,8 +14,8 @@
 
 namespace pg {
 
-// dictIds per thread per round: a round issues R directory loads, then R container loads, per thread before any is
-// consumed, and expands the round's array containers in one pass
+// dictIds per thread per round: a round issues its R container lookups per thread before any is consumed, and expands
+// the round's array containers in one pass
 constexpr int kRoarR = 4;
 
 // LDS scratch of one chunk build (besides the chunk itself)
@@ -30,10 +31,10 @@ struct RoaringLds {
 };
 
 // OR the containers of `key` of the nids selected dictIds into `chunk` (which the caller zeroed and synchronised).
-// Ends with a block barrier.  keydir (optional): [key * card + dictId] = container index or ~0.
+// Ends with a block barrier.  keydir (optional): [key * card + dictId] = keydir_entry of the container or ~0 ~0.
 template <int NT>
 __device__ __forceinline__ void roaring_key_chunk(const uint8_t* __restrict__ roaring, const RoaringContainer* __restrict__ cs,
-                                                  const uint32_t* __restrict__ dir, const uint32_t* __restrict__ keydir,
+                                                  const uint32_t* __restrict__ dir, const uint2* __restrict__ keydir,
                                                   uint32_t card, const int32_t* __restrict__ ids, uint32_t nids,
                                                   uint32_t key, uint32_t* chunk, RoaringLds<NT>& S) {
   constexpr int R = kRoarR;
@@ -41,30 +42,36 @@ __device__ __forceinline__ void roaring_key_chunk(const uint8_t* __restrict__ ro
   if (tid == 0) S.nbml = 0;
   __syncthreads();
   for (uint32_t r0 = 0; r0 < nids; r0 += NT * R) {
-    // 1. the container of `key` of each of this thread's dictIds: all directory loads, then all container loads
-    uint32_t a[R];
+    // 1. the container of `key` of each of this thread's dictIds, all R lookups issued before any is consumed: with the
+    //    key-major directory one 8-byte load each (the descriptor itself), else a search of the dictId's containers
+    RoaringContainer c[R];
+    if (keydir) {
+      uint2 e[R];
 #pragma unroll
-    for (int k = 0; k < R; k++) {
-      const uint32_t i = r0 + tid + NT * k;
-      a[k] = 0xFFFFFFFFu;
-      if (i < nids) {
-        const uint32_t id = (uint32_t)ids[i];
-        if (keydir) {  // one load: the key-major directory built at upload
-          a[k] = keydir[(uint64_t)key * card + id];
-        } else {  // this dictId's containers, ascending keys: find `key`
+      for (int k = 0; k < R; k++) {
+        const uint32_t i = r0 + tid + NT * k;
+        e[k] = make_uint2(kKeyDirNone, kKeyDirNone);
+        if (i < nids) e[k] = keydir[(uint64_t)key * card + (uint32_t)ids[i]];
+      }
+#pragma unroll
+      for (int k = 0; k < R; k++) c[k] = RoaringContainer{key, e[k].y >> 30, e[k].y & 0x3FFFFFFFu, e[k].x};
+    } else {
+#pragma unroll
+      for (int k = 0; k < R; k++) {
+        const uint32_t i = r0 + tid + NT * k;
+        c[k] = RoaringContainer{key, 3u, 0u, 0u};
+        if (i < nids) {  // this dictId's containers, ascending keys: find `key`
+          const uint32_t id = (uint32_t)ids[i];
           uint32_t lo = dir[id], hi = dir[id + 1];
           const uint32_t end = hi;
           while (lo < hi) {
             const uint32_t m = (lo + hi) >> 1;
             if (cs[m].key < key) lo = m + 1; else hi = m;
           }
-          a[k] = lo < end && cs[lo].key == key ? lo : 0xFFFFFFFFu;
+          if (lo < end && cs[lo].key == key) c[k] = cs[lo];
         }
       }
     }
-    RoaringContainer c[R];
-#pragma unroll
-    for (int k = 0; k < R; k++) c[k] = a[k] != 0xFFFFFFFFu ? cs[a[k]] : RoaringContainer{0u, 3u, 0u, 0u};
     // 2. classify: arrays -> this thread's quad list, bitmaps -> the block's list, runs expanded here
     uint32_t nq = 0;
     int na = 0;

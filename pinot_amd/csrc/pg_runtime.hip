@@ -272,7 +272,7 @@ struct ColumnRes {
   bool has_inv = false;
   DevBuf roaring, containers, inv_dir_dev;
   std::vector<uint32_t> inv_dir;  // CSR: containers of dictId d are [inv_dir[d], inv_dir[d+1]) (+ a device copy)
-  DevBuf inv_keydir;              // key-major: [key * card + dictId] = container index or ~0 (when small enough)
+  DevBuf inv_keydir;              // key-major: [key * card + dictId] = keydir_entry of the container (when small enough)
   uint32_t inv_keydir_card = 0;
   // keymap
   bool has_keymap = false;
@@ -488,7 +488,24 @@ int parse_inverted(const std::vector<uint8_t>& b, uint32_t card, std::vector<uin
     }
   }
   dir[card] = (uint32_t)cs.size();
-  payload.resize((payload.size() + 7) & ~7ull);  // whole 8-byte words: the device reads array entries 4 at a time
+  // payloads re-laid key-major (by 64 K-doc key, then dictId): a key's decode reads the selected dictIds' containers
+  // of that key from one contiguous region instead of one scattered line per container
+  std::vector<uint32_t> order(cs.size());
+  for (uint32_t i = 0; i < (uint32_t)cs.size(); i++) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return cs[x].key < cs[y].key; });
+  std::vector<uint8_t> km;
+  km.reserve(payload.size() + 8);
+  for (uint32_t i : order) {
+    RoaringContainer& c = cs[i];
+    const uint64_t len = c.type == 0 ? 2ull * c.card : (c.type == 1 ? 8192ull : 2ull + 4ull * c.card);
+    const uint64_t at = (km.size() + 7) & ~7ull;
+    if (at + len > 0xFFFFFFFFull) return fail(PG_E_UNSUPPORTED, "inverted index payload past 4 GiB");
+    km.resize(at + len);
+    memcpy(&km[at], &payload[c.offset], len);
+    c.offset = (uint32_t)at;
+  }
+  km.resize((km.size() + 7) & ~7ull);  // whole 8-byte words: the device reads array entries 4 at a time
+  payload.swap(km);
   return PG_OK;
 }
 
@@ -675,15 +692,15 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
       // key-major directory (one load per (dictId, 64 K-doc key) in the pre-pass instead of a binary search over the
       // dictId's containers), kept when it stays within kKeyDirMaxEntries
       const uint64_t nkeys = ((uint64_t)d->num_docs + 65535) >> 16, card = d->cardinality;
-      std::vector<uint32_t> kd;
+      std::vector<uint2> kd;
       if (nkeys * card <= kKeyDirMaxEntries && nkeys * card) {
-        kd.assign(nkeys * card, 0xFFFFFFFFu);
+        kd.assign(nkeys * card, make_uint2(kKeyDirNone, kKeyDirNone));
         for (uint32_t id = 0; id < card; id++)
           for (uint32_t ci = tmp.inv_dir[id]; ci < tmp.inv_dir[id + 1]; ci++)
-            if (cs[ci].key < nkeys) kd[(uint64_t)cs[ci].key * card + id] = ci;
-        if ((rc = tmp.inv_keydir.alloc(4ull * kd.size() + 16))) return rc;
+            if (cs[ci].key < nkeys) kd[(uint64_t)cs[ci].key * card + id] = keydir_entry(cs[ci]);
+        if ((rc = tmp.inv_keydir.alloc(8ull * kd.size() + 16))) return rc;
         tmp.inv_keydir_card = (uint32_t)card;
-        HIP_CHECK(hipMemcpyAsync(tmp.inv_keydir.p, kd.data(), 4ull * kd.size(), hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipMemcpyAsync(tmp.inv_keydir.p, kd.data(), 8ull * kd.size(), hipMemcpyHostToDevice, s));
       }
       HIP_CHECK(hipStreamSynchronize(s));
       break;
@@ -2687,7 +2704,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
             x.roaring = (const uint8_t*)op.col->roaring.p;
             x.cs = (const RoaringContainer*)op.col->containers.p;
             x.dir = (const uint32_t*)op.col->inv_dir_dev.p;
-            x.keydir = (const uint32_t*)op.col->inv_keydir.p;
+            x.keydir = (const uint2*)op.col->inv_keydir.p;
             x.card = op.col->inv_keydir_card;
             x.nids = op.n;
             ix.ids_off[(uint64_t)si * L + li] = op.in_off;
@@ -2896,7 +2913,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       j.roaring = (const uint8_t*)op.col->roaring.p;
       j.cs = (const RoaringContainer*)op.col->containers.p;
       j.dir = (const uint32_t*)op.col->inv_dir_dev.p;
-      j.keydir = (const uint32_t*)op.col->inv_keydir.p;
+      j.keydir = (const uint2*)op.col->inv_keydir.p;
       j.card = op.col->inv_keydir_card;
       j.ids = (const int32_t*)(dA + op.in_off);
       j.bm = (uint32_t*)(dS + op.out_off);
@@ -3734,6 +3751,7 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
     if ((rc = read_back(d_num, n32, s))) return rc;
     n = n32;
   }
+  PG_PROF("f_groups");
   // 2. final values
   uint64_t* dkeys = sc.get<uint64_t>(n + 1, rc);
   double* dvals = sc.get<double>((n + 1) * AA, rc);
@@ -3759,6 +3777,7 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
     HIP_CHECK(launch_order_keys(f, dkeys, dvals, dcnts, n, okeys, pos, s, (uint64_t*)d_span));
     KeySpan span{};
     if ((rc = read_back(d_span, span, s))) return rc;
+    PG_PROF("f_okeys");
     const uint64_t diff = span.any & span.anyz;
     const uint32_t b0 = diff ? (uint32_t)__builtin_ctzll(diff) : 0u, b1 = diff ? 64u - (uint32_t)__builtin_clzll(diff) : 1u;
     const char* sel_env = getenv("PG_TRIM_SELECT");  // 0: always sort, 1: always select (tests), else by size
@@ -3790,8 +3809,10 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
       }
       unsigned long long* d_cnt = (unsigned long long*)d_nc;
       HIP_CHECK(hipMemsetAsync(d_cnt, 0, 8, s));
+      PG_PROF("f_radix");
       HIP_CHECK(launch_okey_select(okeys, n, b0, W, prefix, spos, d_cnt, s));
       if ((rc = read_back(d_nc, nc, s))) return rc;
+      PG_PROF("f_cut");
     } else {
       const size_t tb = sort_temp_bytes(n, b0, b1);
       void* temp = sc.get<uint8_t>(tb, rc);
@@ -3827,6 +3848,7 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
     std::vector<uint32_t> hs(nc);
     HIP_CHECK(hipMemcpyAsync(hs.data(), cs, nc * 4, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
+    PG_PROF("f_cands");
     std::vector<uint64_t> perm;
     order_rows(plan, P, nc, hv, hc, [&](uint64_t i, uint32_t k) { return (hk[i] / P.key_stride[k]) % P.key_card[k]; },
                true, perm);
@@ -3850,6 +3872,7 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
     hc.swap(kc);
     cs = ks;
     nc = m;
+    PG_PROF("f_precut");
   }
   std::vector<uint64_t> hoff;
   std::vector<uint32_t> hids;
@@ -3874,6 +3897,7 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   }
   HIP_CHECK(hipEventRecord(e1, s));
   HIP_CHECK(hipStreamSynchronize(s));
+  PG_PROF("f_sets");
   float fm = 0;
   (void)hipEventElapsedTime(&fm, e0, e1);
   t_timing.finalize_ms = fm;
