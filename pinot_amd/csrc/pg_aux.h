@@ -323,6 +323,12 @@ hipError_t launch_final_values(const StateView& v, const FinalSpec& f, const uin
 // both differ between keys, the others are equal in all of them and the sort can skip them
 hipError_t launch_order_keys(const FinalSpec& f, const uint64_t* keys, const double* vals, const int64_t* cnts,
                              uint64_t n, uint64_t* out, uint32_t* pos, hipStream_t s, uint64_t* span = nullptr);
+// The order image straight from the state for the trim's candidate selection (no final values of every group);
+// order_keys_from_state_ok: the first ORDER BY item is a key or an aggregation whose final value is one state read
+bool order_keys_from_state_ok(const StateView& v, const FinalSpec& f);
+hipError_t launch_order_keys_state(const StateView& v, const FinalSpec& f, const uint32_t* slots, uint64_t n,
+                                   uint64_t* out, uint32_t* pos, uint64_t* span, hipStream_t s);
+hipError_t launch_gather_slots(const uint32_t* slots, const uint32_t* pos, uint64_t n, uint32_t* out, hipStream_t s);
 // ORDER BY trim by radix select (pg_groups.hip): histogram of key bits [lo, hi) of k' = (key >> b0) & (2^W - 1) over the
 // keys whose k' >> hi equals prefix (hist: 256 counters, zeroed by the caller); then the positions of every key with
 // k' <= tstar (count: zeroed by the caller)
