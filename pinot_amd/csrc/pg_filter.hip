@@ -445,7 +445,11 @@ hipError_t launch_stream(const StreamSpec& p, uint32_t bits, uint32_t blocks, hi
   if (p.exact_nwords) {
     static bool attr = false;  // >64 KiB of dynamic LDS must be opted into per kernel (once per process)
     if (!attr) {
-#define PG_A(b) (void)hipFuncSetAttribute((const void*)stream_kernel<b, false, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kExactLutWords + 16);
+#define PG_A(b)                                                                                                 \
+  (void)hipFuncSetAttribute((const void*)stream_kernel<b, false, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                            4 * kExactLutWords + 16);                                                            \
+  (void)hipFuncSetAttribute((const void*)stream_kernel<b, true, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize,  \
+                            4 * kExactLutWords + 16);
       PG_A(1) PG_A(2) PG_A(3) PG_A(4) PG_A(5) PG_A(6) PG_A(7) PG_A(8) PG_A(9) PG_A(10) PG_A(11) PG_A(12) PG_A(13)
       PG_A(14) PG_A(15) PG_A(16) PG_A(17) PG_A(18) PG_A(19) PG_A(20) PG_A(21) PG_A(22) PG_A(23) PG_A(24) PG_A(25)
       PG_A(26) PG_A(27) PG_A(28) PG_A(29) PG_A(30) PG_A(31) PG_A(32)
@@ -456,7 +460,8 @@ hipError_t launch_stream(const StreamSpec& p, uint32_t bits, uint32_t blocks, hi
   switch (bits) {
 #define PG_B(b)                                                                                              \
   case b:                                                                                                    \
-    if (p.exact_nwords) hipLaunchKernelGGL((stream_kernel<b, false, 1024>), dim3(blocks), dim3(1024), lds, s, p); \
+    if (p.exact_nwords && p.num_extra) hipLaunchKernelGGL((stream_kernel<b, true, 1024>), dim3(blocks), dim3(1024), lds, s, p); \
+    else if (p.exact_nwords) hipLaunchKernelGGL((stream_kernel<b, false, 1024>), dim3(blocks), dim3(1024), lds, s, p); \
     else if (p.num_extra) hipLaunchKernelGGL((stream_kernel<b, true, 256>), dim3(blocks), dim3(256), lds, s, p); \
     else hipLaunchKernelGGL((stream_kernel<b, false, 256>), dim3(blocks), dim3(256), lds, s, p);                \
     break;

@@ -2446,6 +2446,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     std::vector<uint32_t> exact_nwords;  // [seg] LUT words
     uint32_t set_ints = 0;        // LDS IN-set words of the streamed leaves
     std::vector<uint32_t> extra;  // further AND children tested in the stream (runtime bit width)
+    bool extra_lds_free = false;  // the further children need no LDS (allowed beside the exact mode's LUT)
     std::vector<StreamLaunch> launches;
   } sp;
   {
@@ -2473,6 +2474,26 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         sp.extra.push_back((uint32_t)lx);
         pass *= leaf_pass[lx];
       }
+      // a driving leaf that passes <= 1/64 alone (config 2's accountId IN: 0.1 %): the following AND children that need
+      // no LDS (doc ranges, constants, packed ranges, global-LUT sets) are still tested in the stream, on its few
+      // survivors by per-doc windows -- the list scan then gets the AND's survivors instead of re-reading those
+      // columns for every survivor of the driving leaf (PG_STREAM_EXACT_EXTRA=0: not)
+      static const char* xe_env = getenv("PG_STREAM_EXACT_EXTRA");
+      if (sp.extra.empty() && pass <= 1.0 / 64 && !(xe_env && atoi(xe_env) == 0)) {
+        for (uint32_t i = 2; i + 1 < q.num_ops && sp.extra.size() < (size_t)kMaxStreamExtra; i++) {
+          const int32_t lx = q.ops[i];
+          if (lx < 0) break;
+          bool fits = true;
+          for (uint32_t si = 0; si < S && fits; si++) {
+            const uint32_t k = leaves[(uint64_t)si * L + lx].kind;
+            fits = k == LK_ALL || k == LK_NONE || k == LK_DOCRANGE || k == LK_RANGE || k == LK_SET_LUT;
+          }
+          if (!fits) break;
+          sp.extra.push_back((uint32_t)lx);
+          sp.extra_lds_free = true;
+          pass *= leaf_pass[lx];
+        }
+      }
     }
     bool ok = allow_stream && !(plan->flags & PG_PLAN_NO_STREAM) && !(st_env && atoi(st_env) == 0) && li >= 0 &&
               !part.on && pre_leaves.empty() && pass <= max_pass && total_docs < 0xFFFFFFF0ull;
@@ -2499,7 +2520,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       // exact mode (PG_STREAM_EXACT=0 disables): a coarse IN bitmap whose exact LUT fits 128 KiB of LDS is tested
       // exactly by 1 024-thread blocks, one per CU, instead of resolving the coarse bitmap's candidates by global reads
       static const char* ex_env = getenv("PG_STREAM_EXACT");
-      sp.exact = sp.extra.empty() && !(ex_env && atoi(ex_env) == 0);
+      sp.exact = (sp.extra.empty() || sp.extra_lds_free) && !(ex_env && atoi(ex_env) == 0);
       sp.exact_nwords.assign(S, 0);
       for (uint32_t si = 0; si < S && sp.exact; si++) {
         if (!seg_groups[si]) continue;
