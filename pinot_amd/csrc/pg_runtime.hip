@@ -2477,9 +2477,11 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       // a driving leaf that passes <= 1/64 alone (config 2's accountId IN: 0.1 %): the following AND children that need
       // no LDS (doc ranges, constants, packed ranges, global-LUT sets) are still tested in the stream, on its few
       // survivors by per-doc windows -- the list scan then gets the AND's survivors instead of re-reading those
-      // columns for every survivor of the driving leaf (PG_STREAM_EXACT_EXTRA=0: not)
+      // columns for every survivor of the driving leaf.  PG_STREAM_EXACT_EXTRA=1 enables it; off by default: measured
+      // even on config 2 (stream 0.441 -> 0.492 ms, list scan 0.098 -> 0.050 ms, r04: the survivors' window reads stall
+      // the streaming waves as long as the list kernel's gathers take)
       static const char* xe_env = getenv("PG_STREAM_EXACT_EXTRA");
-      if (sp.extra.empty() && pass <= 1.0 / 64 && !(xe_env && atoi(xe_env) == 0)) {
+      if (sp.extra.empty() && pass <= 1.0 / 64 && xe_env && atoi(xe_env) == 1) {
         for (uint32_t i = 2; i + 1 < q.num_ops && sp.extra.size() < (size_t)kMaxStreamExtra; i++) {
           const int32_t lx = q.ops[i];
           if (lx < 0) break;
