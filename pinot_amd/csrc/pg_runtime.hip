@@ -2480,7 +2480,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       // columns for every survivor of the driving leaf.  PG_STREAM_EXACT_EXTRA=1 enables it; off by default: measured
       // even on config 2 (stream 0.441 -> 0.492 ms, list scan 0.098 -> 0.050 ms, r04: the survivors' window reads stall
       // the streaming waves as long as the list kernel's gathers take)
-      static const char* xe_env = getenv("PG_STREAM_EXACT_EXTRA");
+      const char* xe_env = getenv("PG_STREAM_EXACT_EXTRA");  // read per call (tests switch it)
       if (sp.extra.empty() && pass <= 1.0 / 64 && xe_env && atoi(xe_env) == 1) {
         for (uint32_t i = 2; i + 1 < q.num_ops && sp.extra.size() < (size_t)kMaxStreamExtra; i++) {
           const int32_t lx = q.ops[i];

@@ -74,6 +74,19 @@ def test_stream_matches_oracle_and_no_stream(sql, table, gpu_engine, oracle_engi
     assert g.stats.num_docs_scanned == n.stats.num_docs_scanned == o.stats.num_docs_scanned
 
 
+@pytest.mark.parametrize("qi", [0, 5, 6])
+def test_stream_exact_mode_further_leaves(qi, table, monkeypatch, gpu_engine, oracle_engine):
+    """PG_STREAM_EXACT_EXTRA=1: the exact-mode stream (stream_kernel<B, true, 1024>) also tests the AND's following
+    LDS-free leaves on the driving leaf's survivors; same answers as the oracle and as the plan without the stream."""
+    monkeypatch.setenv("PG_STREAM_EXACT_EXTRA", "1")
+    q = parse(STREAM_QUERIES[qi])
+    g = gpu_engine.execute(table, q)
+    assert gpu_engine.last_timing().scan_launches == 2, "the selective stream did not run"
+    assert_same_result(g, oracle_engine.execute(table, q), table=table)
+    n = gpu_engine.execute(table, q, flags=abi.PG_PLAN_VALUE_SETS | abi.PG_PLAN_NO_STREAM)
+    assert_same_result(g, n, table=table)
+
+
 def test_stream_not_used_for_unselective_filters(table, gpu_engine, oracle_engine):
     q = parse("SELECT SUM(clicks) FROM t WHERE day BETWEEN 18000 AND 18200 AND acct < 150000")
     g = gpu_engine.execute(table, q)
