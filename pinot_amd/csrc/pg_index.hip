@@ -32,7 +32,10 @@ __device__ __forceinline__ uint32_t word_range(int64_t a, int64_t b) {
 __global__ __launch_bounds__(kIdxNT) void index_count_kernel(IdxSpec p) {
   extern __shared__ __attribute__((aligned(16))) uint32_t chunks[];  // [num_chunks][2048]
   __shared__ RoaringLds<kIdxNT> S;
+  __shared__ RoarView V[kIdxMaxLeaves];
+  __shared__ uint32_t nv;
   __shared__ unsigned long long red[2][kIdxNT / 64];
+  static_assert(kIdxMaxLeaves <= kRoarMaxViews, "one view per inverted leaf");
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   uint32_t lo = 0, hi = p.num_segs;  // the segment whose block range holds this block
   while (hi - lo > 1) {
@@ -43,15 +46,32 @@ __global__ __launch_bounds__(kIdxNT) void index_count_kernel(IdxSpec p) {
   const IdxSeg G = p.segs[si];
   const uint32_t key = G.key0 + (blockIdx.x - G.first_block);
   for (uint32_t w = tid; w < p.num_chunks * 2048u; w += kIdxNT) chunks[w] = 0u;
-  for (uint32_t l = 0; l < p.num_leaves; l++) {  // each inverted leaf's containers of this key into its chunk
-    const IdxLeaf L = G.leaves[l];
-    if (L.kind == IL_ROARING)
-      roaring_key_chunk<kIdxNT>(L.roaring, L.cs, L.dir, L.keydir, L.card, L.ids, L.nids, key, chunks + p.chunk_of[l] * 2048u, S);
+  if (tid == 0) {  // every inverted leaf of the segment, decoded together into its chunk
+    uint32_t n = 0;
+    for (uint32_t l = 0; l < p.num_leaves; l++) {
+      const IdxLeaf& L = G.leaves[l];
+      if (L.kind == IL_ROARING && L.nids)
+        V[n++] = RoarView{L.roaring, L.cs, L.dir, L.keydir, L.ids, chunks + p.chunk_of[l] * 2048u, L.nids, L.card};
+    }
+    nv = n;
   }
   __syncthreads();
+  roaring_key_chunks<kIdxNT>(V, nv, key, S);
   const uint32_t nd = G.num_docs;
   unsigned long long cnt = 0, cmv = 0;
-  for (uint32_t w = tid; w < 2048u; w += kIdxNT) {
+  // COUNTMV from the 4-bit count column: this thread's count words of all its chunk words are loaded up front (one
+  // latency, not one per word; most words hold a match at config 5's 5.6 % pass)
+  constexpr uint32_t kWpt = 2048u / kIdxNT;
+  uint4 cwp[kWpt];
+  const bool pre_cnt = p.cntmv_slot != 0xFFFFFFFFu && G.mv_cnt;
+#pragma unroll
+  for (uint32_t k = 0; k < kWpt; k++) {
+    const uint64_t d0 = (uint64_t)key * 65536u + 32u * (tid + k * kIdxNT);
+    cwp[k] = pre_cnt && d0 < nd ? *(const uint4*)(G.mv_cnt + d0 / 8) : make_uint4(0u, 0u, 0u, 0u);
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kWpt; k++) {
+    const uint32_t w = tid + k * kIdxNT;
     const uint64_t d0 = (uint64_t)key * 65536u + 32u * w;
     if (d0 >= nd) break;
     const uint32_t valid = d0 + 32 <= nd ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (uint32_t)(nd - d0));
@@ -90,7 +110,7 @@ __global__ __launch_bounds__(kIdxNT) void index_count_kernel(IdxSpec p) {
     cnt += (uint32_t)__popc(m);
     if (p.cntmv_slot != 0xFFFFFFFFu && m) {
       if (G.mv_cnt) {  // 4-bit counts: docs d0 .. d0 + 31 are the 4 count words at d0 / 8
-        const uint4 cw = *(const uint4*)(G.mv_cnt + d0 / 8);
+        const uint4 cw = cwp[k];
         const uint32_t c4[4] = {cw.x, cw.y, cw.z, cw.w};
         for (uint32_t r = m; r; ) {
           const uint32_t j = (uint32_t)__builtin_clz(r);

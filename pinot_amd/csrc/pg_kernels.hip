@@ -335,6 +335,7 @@ hipError_t launch_roaring_or(const uint8_t* roaring, const RoaringContainer* con
 __global__ __launch_bounds__(256) void roaring_keys_kernel(const RoaringJob* __restrict__ jobs, uint32_t njobs) {
   __shared__ uint32_t chunk[2048];     // the key's 65 536 docs
   __shared__ RoaringLds<256> S;
+  __shared__ RoarView V;
   uint32_t lo = 0, hi = njobs;         // the job whose block range holds this block
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
@@ -343,7 +344,8 @@ __global__ __launch_bounds__(256) void roaring_keys_kernel(const RoaringJob* __r
   const RoaringJob J = jobs[lo];
   const uint32_t key = J.key0 + (blockIdx.x - J.first_block), tid = threadIdx.x;
   for (uint32_t w = tid; w < 2048; w += 256) chunk[w] = 0;
-  roaring_key_chunk<256>(J.roaring, J.cs, J.dir, J.keydir, J.card, J.ids, J.nids, key, chunk, S);
+  if (tid == 0) V = RoarView{J.roaring, J.cs, J.dir, J.keydir, J.ids, chunk, J.nids, J.card};
+  roaring_key_chunks<256>(&V, 1, key, S);  // (its first barrier publishes V and the zeroed chunk)
   const uint32_t nwords = (J.num_docs + 31) / 32, tail = J.num_docs & 31u;
   for (uint32_t w = tid; w < 2048; w += 256) {
     const uint32_t gw = key * 2048 + w;

@@ -1,6 +1,7 @@
-// pg_roaring.h -- device-side decoding of one 64 K-doc key of an inverted-index leaf (BitmapBasedFilterOperator's OR of
-// the selected dictIds' RoaringBitmaps, restricted to one high-16-bit key) into an LDS chunk of 2 048 words, shared by
-// the index pre-pass (pg_kernels.hip roaring_keys_kernel) and the fused index count (pg_index.hip).
+// pg_roaring.h -- device-side decoding of one 64 K-doc key of inverted-index leaves (BitmapBasedFilterOperator's OR of
+// the selected dictIds' RoaringBitmaps, restricted to one high-16-bit key) into LDS chunks of 2 048 words, shared by
+// the index pre-pass (pg_kernels.hip roaring_keys_kernel: one leaf) and the fused index count (pg_index.hip: every
+// inverted leaf of the filter at once).
 //
 // Chunk word w, bit 31 - j <-> doc key * 65 536 + 32 w + j (the packed 1-bit column order).  Containers follow the
 // RoaringBitmap portable format (RoaringBitmap 0.9.28): array (sorted uint16), bitmap (1 024 little-endian uint64) and
@@ -17,59 +18,77 @@ namespace pg {
 // dictIds per thread per round: a round issues its R container lookups per thread before any is consumed, and expands
 // the round's array containers in one pass
 constexpr int kRoarR = 4;
+constexpr uint32_t kRoarMaxViews = 8;
 
-// LDS scratch of one chunk build (besides the chunk itself)
-template <int NT>
-struct RoaringLds {
-  uint32_t bml[NT * kRoarR];  // bitmap containers of this round (payload offsets), OR-ed by the whole block
-  uint32_t nbml;
-  uint32_t tpre[NT + 1];      // exclusive prefix over the threads of their array containers' quads (4 entries each)
-  uint32_t aoff[kRoarR][NT];  // thread t's j-th array container of the round: payload offset,
-  uint16_t aq0[kRoarR][NT];   //   its first quad among t's quads (0xFFFF: no such container),
-  uint16_t acard[kRoarR][NT]; //   its cardinality
-  uint32_t wsum[NT / 64];
+// One inverted leaf to decode: its column's containers, the selected dictIds, the LDS chunk it is OR-ed into.
+struct RoarView {
+  const uint8_t* roaring;
+  const RoaringContainer* cs;
+  const uint32_t* dir;
+  const uint2* keydir;      // optional key-major directory: [key * card + dictId] = keydir_entry or ~0 ~0
+  const int32_t* ids;
+  uint32_t* chunk;          // LDS
+  uint32_t nids, card;
 };
 
-// OR the containers of `key` of the nids selected dictIds into `chunk` (which the caller zeroed and synchronised).
-// Ends with a block barrier.  keydir (optional): [key * card + dictId] = keydir_entry of the container or ~0 ~0.
+// LDS scratch of one decode (besides the chunks and the views)
 template <int NT>
-__device__ __forceinline__ void roaring_key_chunk(const uint8_t* __restrict__ roaring, const RoaringContainer* __restrict__ cs,
-                                                  const uint32_t* __restrict__ dir, const uint2* __restrict__ keydir,
-                                                  uint32_t card, const int32_t* __restrict__ ids, uint32_t nids,
-                                                  uint32_t key, uint32_t* chunk, RoaringLds<NT>& S) {
+struct RoaringLds {
+  uint32_t bml[NT * kRoarR];   // bitmap containers of this round (payload offsets), OR-ed by the whole block
+  uint8_t bview[NT * kRoarR];  //   and their views
+  uint32_t nbml;
+  uint32_t tpre[NT + 1];       // exclusive prefix over the threads of their array containers' quads (4 entries each)
+  uint32_t aoff[kRoarR][NT];   // thread t's j-th array container of the round: payload offset,
+  uint16_t aq0[kRoarR][NT];    //   its first quad among t's quads (0xFFFF: no such container),
+  uint16_t acard[kRoarR][NT];  //   its cardinality,
+  uint8_t aview[kRoarR][NT];   //   its view
+  uint32_t wsum[NT / 64];
+  uint32_t vpre[kRoarMaxViews + 1];  // prefix of the views' dictId counts
+};
+
+// OR the containers of `key` of every view's selected dictIds into the view's chunk (zeroed by the caller).  The views'
+// dictIds are taken as one list, so a round's lookups span the leaves (config 5: 4 leaves of 1 + 20 + 1 + 2 000 ids
+// decode in 2 rounds, not 5).  `V` (nv <= kRoarMaxViews entries) is visible to the whole block; starts and ends with a
+// block barrier.
+template <int NT>
+__device__ __forceinline__ void roaring_key_chunks(const RoarView* V, uint32_t nv, uint32_t key, RoaringLds<NT>& S) {
   constexpr int R = kRoarR;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  if (tid == 0) S.nbml = 0;
+  if (tid == 0) {
+    S.nbml = 0;
+    uint32_t a = 0;
+    for (uint32_t l = 0; l < nv; l++) { S.vpre[l] = a; a += V[l].nids; }
+    S.vpre[nv] = a;
+  }
   __syncthreads();
+  const uint32_t nids = S.vpre[nv];
   for (uint32_t r0 = 0; r0 < nids; r0 += NT * R) {
     // 1. the container of `key` of each of this thread's dictIds, all R lookups issued before any is consumed: with the
     //    key-major directory one 8-byte load each (the descriptor itself), else a search of the dictId's containers
     RoaringContainer c[R];
-    if (keydir) {
-      uint2 e[R];
+    uint32_t vw[R];
 #pragma unroll
-      for (int k = 0; k < R; k++) {
-        const uint32_t i = r0 + tid + NT * k;
-        e[k] = make_uint2(kKeyDirNone, kKeyDirNone);
-        if (i < nids) e[k] = keydir[(uint64_t)key * card + (uint32_t)ids[i]];
-      }
-#pragma unroll
-      for (int k = 0; k < R; k++) c[k] = RoaringContainer{key, e[k].y >> 30, e[k].y & 0x3FFFFFFFu, e[k].x};
-    } else {
-#pragma unroll
-      for (int k = 0; k < R; k++) {
-        const uint32_t i = r0 + tid + NT * k;
-        c[k] = RoaringContainer{key, 3u, 0u, 0u};
-        if (i < nids) {  // this dictId's containers, ascending keys: find `key`
-          const uint32_t id = (uint32_t)ids[i];
-          uint32_t lo = dir[id], hi = dir[id + 1];
-          const uint32_t end = hi;
-          while (lo < hi) {
-            const uint32_t m = (lo + hi) >> 1;
-            if (cs[m].key < key) lo = m + 1; else hi = m;
-          }
-          if (lo < end && cs[lo].key == key) c[k] = cs[lo];
+    for (int k = 0; k < R; k++) {
+      const uint32_t i = r0 + tid + NT * k;
+      c[k] = RoaringContainer{key, 3u, 0u, 0u};
+      vw[k] = 0;
+      if (i >= nids) continue;
+      uint32_t l = 0;
+      while (l + 1 < nv && S.vpre[l + 1] <= i) l++;
+      vw[k] = l;
+      const RoarView& v = V[l];
+      const uint32_t id = (uint32_t)v.ids[i - S.vpre[l]];
+      if (v.keydir) {
+        const uint2 e = v.keydir[(uint64_t)key * v.card + id];
+        c[k] = RoaringContainer{key, e.y >> 30, e.y & 0x3FFFFFFFu, e.x};
+      } else {  // this dictId's containers, ascending keys: find `key`
+        uint32_t lo = v.dir[id], hi = v.dir[id + 1];
+        const uint32_t end = hi;
+        while (lo < hi) {
+          const uint32_t m = (lo + hi) >> 1;
+          if (v.cs[m].key < key) lo = m + 1; else hi = m;
         }
+        if (lo < end && v.cs[lo].key == key) c[k] = v.cs[lo];
       }
     }
     // 2. classify: arrays -> this thread's quad list, bitmaps -> the block's list, runs expanded here
@@ -81,12 +100,16 @@ __device__ __forceinline__ void roaring_key_chunk(const uint8_t* __restrict__ ro
         S.aoff[na][tid] = c[k].offset;
         S.aq0[na][tid] = (uint16_t)nq;
         S.acard[na][tid] = (uint16_t)c[k].card;
+        S.aview[na][tid] = (uint8_t)vw[k];
         nq += (c[k].card + 3u) >> 2;
         na++;
       } else if (c[k].type == 1) {
-        S.bml[atomicAdd(&S.nbml, 1u)] = c[k].offset;
+        const uint32_t b = atomicAdd(&S.nbml, 1u);
+        S.bml[b] = c[k].offset;
+        S.bview[b] = (uint8_t)vw[k];
       } else if (c[k].type == 2) {  // runs: uint16 nruns, then (start, length - 1)
-        const uint16_t* rr = (const uint16_t*)(roaring + c[k].offset) + 1;
+        const uint16_t* rr = (const uint16_t*)(V[vw[k]].roaring + c[k].offset) + 1;
+        uint32_t* chunk = V[vw[k]].chunk;
         for (uint32_t q = 0; q < c[k].card; q++) {
           const uint32_t st = rr[2 * q], en = st + rr[2 * q + 1];
           for (uint32_t w = st >> 5; w <= (en >> 5); w++) {
@@ -114,17 +137,20 @@ __device__ __forceinline__ void roaring_key_chunk(const uint8_t* __restrict__ ro
     S.tpre[tid] = wb + x - nq;
     if (tid == NT - 1) S.tpre[NT] = wb + x;
     __syncthreads();
-    // 3. every quad of the round's array containers, two per thread per step (both loads in flight): owner thread =
-    //    the last prefix <= e, then its container; 4 entries per 8-byte load
+    // 3. every quad of the round's array containers, kQ per thread per step (their loads in flight together): owner
+    //    thread = the last prefix <= e, then its container; 4 entries per 8-byte load
+    constexpr int kQ = 4;
     const uint32_t total = S.tpre[NT];
-    for (uint32_t e0 = tid; e0 < total; e0 += 2 * NT) {
-      uint2 w[2];
-      uint32_t n[2];
+    for (uint32_t e0 = tid; e0 < total; e0 += kQ * NT) {
+      uint2 w[kQ];
+      uint32_t n[kQ];
+      uint32_t* dst[kQ];
 #pragma unroll
-      for (int u = 0; u < 2; u++) {
+      for (int u = 0; u < kQ; u++) {
         const uint32_t e = e0 + (uint32_t)u * NT;
         n[u] = 0;
         w[u] = make_uint2(0u, 0u);
+        dst[u] = nullptr;
         if (e < total) {
           uint32_t lo = 0, hi = NT;
           while (hi - lo > 1) {
@@ -138,25 +164,27 @@ __device__ __forceinline__ void roaring_key_chunk(const uint8_t* __restrict__ ro
             if (S.aq0[k][lo] <= local) j = k;
           const uint32_t q = local - S.aq0[j][lo];
           const uint32_t left = (uint32_t)S.acard[j][lo] - 4u * q;
+          const RoarView& v = V[S.aview[j][lo]];
           n[u] = left < 4u ? left : 4u;
-          w[u] = *(const uint2*)(roaring + S.aoff[j][lo] + 8u * q);
+          dst[u] = v.chunk;
+          w[u] = *(const uint2*)(v.roaring + S.aoff[j][lo] + 8u * q);
         }
       }
 #pragma unroll
-      for (int u = 0; u < 2; u++) {
+      for (int u = 0; u < kQ; u++) {
         const uint32_t v4[4] = {w[u].x & 0xFFFFu, w[u].x >> 16, w[u].y & 0xFFFFu, w[u].y >> 16};
 #pragma unroll
         for (int h = 0; h < 4; h++)
-          if ((uint32_t)h < n[u]) atomicOr(&chunk[v4[h] >> 5], 0x80000000u >> (v4[h] & 31u));
+          if ((uint32_t)h < n[u]) atomicOr(&dst[u][v4[h] >> 5], 0x80000000u >> (v4[h] & 31u));
       }
     }
     __syncthreads();  // the bitmap containers below OR whole words without atomics
-    // 4. bitmap containers: 1 024 little-endian uint64 words each; a thread owns the same chunk words for all of them
+    // 4. bitmap containers: 1 024 little-endian uint64 words each; a thread owns the same words of every chunk
     const uint32_t nb = S.nbml;
-    for (uint32_t wd = tid; wd < 2048; wd += NT) {
-      uint32_t v = 0;
-      for (uint32_t k = 0; k < nb; k++) v |= ((const uint32_t*)(roaring + S.bml[k]))[wd];
-      if (nb) chunk[wd] |= __builtin_bitreverse32(v);
+    for (uint32_t k = 0; k < nb; k++) {
+      const uint32_t* src = (const uint32_t*)(V[S.bview[k]].roaring + S.bml[k]);
+      uint32_t* chunk = V[S.bview[k]].chunk;
+      for (uint32_t wd = tid; wd < 2048; wd += NT) chunk[wd] |= __builtin_bitreverse32(src[wd]);
     }
     __syncthreads();
     if (tid == 0) S.nbml = 0;
