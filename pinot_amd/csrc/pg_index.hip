@@ -17,7 +17,11 @@
 
 namespace pg {
 
-constexpr int kIdxNT = 256;
+#ifndef PG_IDX_NT
+#define PG_IDX_NT 256
+#endif
+constexpr int kIdxNT = PG_IDX_NT;  // threads per (segment, key) block
+static_assert(kIdxNT % 64 == 0 && 2048 % kIdxNT == 0 && kIdxNT <= 1024, "whole waves, whole chunk words per thread");
 
 // docs [a, b) of a 32-doc word (bit 31 - j <-> doc j), clamped to the word
 __device__ __forceinline__ uint32_t word_range(int64_t a, int64_t b) {

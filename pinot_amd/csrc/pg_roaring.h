@@ -184,7 +184,12 @@ __device__ __forceinline__ void roaring_key_chunks(const RoarView* V, uint32_t n
     for (uint32_t k = 0; k < nb; k++) {
       const uint32_t* src = (const uint32_t*)(V[S.bview[k]].roaring + S.bml[k]);
       uint32_t* chunk = V[S.bview[k]].chunk;
-      for (uint32_t wd = tid; wd < 2048; wd += NT) chunk[wd] |= __builtin_bitreverse32(src[wd]);
+      constexpr uint32_t kWpt = 2048u / NT;  // this thread's words of the container, loaded together
+      uint32_t bw[kWpt];
+#pragma unroll
+      for (uint32_t j = 0; j < kWpt; j++) bw[j] = src[tid + j * NT];
+#pragma unroll
+      for (uint32_t j = 0; j < kWpt; j++) chunk[tid + j * NT] |= __builtin_bitreverse32(bw[j]);
     }
     __syncthreads();
     if (tid == 0) S.nbml = 0;

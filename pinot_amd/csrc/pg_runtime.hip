@@ -2754,6 +2754,37 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         }
       }
     }
+    if (ok && sp2.num_chunks > 1) {
+      // the positive inverted leaves of one OR (a group, or the root's leaf items) decode into ONE chunk: the OR of
+      // their containers is the union either of them then reads (a constant or doc-range form in some segment still
+      // ORs in correctly) -- fewer LDS chunks per block, more blocks per CU
+      bool neg[kIdxMaxLeaves] = {};
+      for (uint64_t k = 0; k < ix.leaves.size(); k++)
+        if (ix.leaves[k].kind == IL_ROARING && ix.leaves[k].negate) neg[k % L] = true;
+      uint32_t rep[kIdxMaxLeaves];
+      for (uint32_t l = 0; l < kIdxMaxLeaves; l++) rep[l] = l;
+      auto share = [&](const uint32_t* codes, uint32_t n) {
+        int first = -1;
+        for (uint32_t k = 0; k < n; k++) {
+          const uint32_t c = codes[k];
+          if (c & 0xC0000000u) continue;  // a group or a negated item
+          const uint32_t l = c & 0xFFu;
+          if (l >= L || neg[l] || sp2.chunk_of[l] == 0xFFFFFFFFu) continue;
+          if (first < 0) first = (int)l; else rep[l] = (uint32_t)first;
+        }
+      };
+      for (uint32_t gi = 0; gi < kIdxMaxItems; gi++)
+        if (sp2.group_or[gi] && sp2.gn[gi]) share(sp2.gleaf + sp2.gfirst[gi], sp2.gn[gi]);
+      if (sp2.root_or) share(sp2.item, sp2.num_items);
+      uint32_t newc[kIdxMaxLeaves];
+      for (uint32_t l = 0; l < kIdxMaxLeaves; l++) newc[l] = 0xFFFFFFFFu;
+      sp2.num_chunks = 0;
+      for (uint32_t l = 0; l < L; l++) {
+        if (sp2.chunk_of[l] == 0xFFFFFFFFu) continue;
+        if (newc[rep[l]] == 0xFFFFFFFFu) newc[rep[l]] = sp2.num_chunks++;
+        sp2.chunk_of[l] = newc[rep[l]];
+      }
+    }
     if (ok) {
       ix.on = true;
       sp2.num_segs = S;
