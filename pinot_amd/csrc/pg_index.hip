@@ -50,14 +50,18 @@ __global__ __launch_bounds__(kIdxNT) void index_count_kernel(IdxSpec p) {
   const IdxSeg G = p.segs[si];
   const uint32_t key = G.key0 + (blockIdx.x - G.first_block);
   for (uint32_t w = tid; w < p.num_chunks * 2048u; w += kIdxNT) chunks[w] = 0u;
-  if (tid == 0) {  // every inverted leaf of the segment, decoded together into its chunk
-    uint32_t n = 0;
-    for (uint32_t l = 0; l < p.num_leaves; l++) {
-      const IdxLeaf& L = G.leaves[l];
-      if (L.kind == IL_ROARING && L.nids)
-        V[n++] = RoarView{L.roaring, L.cs, L.dir, L.keydir, L.ids, chunks + p.chunk_of[l] * 2048u, L.nids, L.card};
+  // every inverted leaf of the segment, decoded together into its chunk: leaf l's descriptor read by lane l (one
+  // latency), the views compacted by wave 0
+  if (tid < 64) {
+    IdxLeaf L{};
+    if (tid < p.num_leaves) L = G.leaves[tid];
+    const bool on = tid < p.num_leaves && L.kind == IL_ROARING && L.nids;
+    const unsigned long long b = __ballot(on);
+    if (on) {
+      const uint32_t at = (uint32_t)__popcll(b & ((1ull << tid) - 1ull));
+      V[at] = RoarView{L.roaring, L.cs, L.dir, L.keydir, L.ids, chunks + p.chunk_of[tid] * 2048u, L.nids, L.card};
     }
-    nv = n;
+    if (tid == 0) nv = (uint32_t)__popcll(b);
   }
   __syncthreads();
   roaring_key_chunks<kIdxNT>(V, nv, key, S);

@@ -17,8 +17,16 @@ namespace pg {
 
 // dictIds per thread per round: a round issues its R container lookups per thread before any is consumed, and expands
 // the round's array containers in one pass
-constexpr int kRoarR = 4;
+#ifndef PG_ROAR_R
+#define PG_ROAR_R 4
+#endif
+#ifndef PG_ROAR_Q
+#define PG_ROAR_Q 4
+#endif
+constexpr int kRoarR = PG_ROAR_R;
+constexpr int kRoarQ = PG_ROAR_Q;  // array-container quads per thread per expansion step (loads in flight together)
 constexpr uint32_t kRoarMaxViews = 8;
+static_assert(kRoarR >= 1 && kRoarR <= 16 && kRoarQ >= 1 && kRoarQ <= 16, "roaring decode knobs");
 
 // One inverted leaf to decode: its column's containers, the selected dictIds, the LDS chunk it is OR-ed into.
 struct RoarView {
@@ -34,8 +42,8 @@ struct RoarView {
 // LDS scratch of one decode (besides the chunks and the views)
 template <int NT>
 struct RoaringLds {
-  uint32_t bml[NT * kRoarR];   // bitmap containers of this round (payload offsets), OR-ed by the whole block
-  uint8_t bview[NT * kRoarR];  //   and their views
+  uint32_t bml[NT];            // bitmap containers of this round (payload offsets), OR-ed by the whole block
+  uint8_t bview[NT];           //   and their views (more than NT in a round: the finder ORs it in by itself)
   uint32_t nbml;
   uint32_t tpre[NT + 1];       // exclusive prefix over the threads of their array containers' quads (4 entries each)
   uint32_t aoff[kRoarR][NT];   // thread t's j-th array container of the round: payload offset,
@@ -105,8 +113,15 @@ __device__ __forceinline__ void roaring_key_chunks(const RoarView* V, uint32_t n
         na++;
       } else if (c[k].type == 1) {
         const uint32_t b = atomicAdd(&S.nbml, 1u);
-        S.bml[b] = c[k].offset;
-        S.bview[b] = (uint8_t)vw[k];
+        if (b < NT) {
+          S.bml[b] = c[k].offset;
+          S.bview[b] = (uint8_t)vw[k];
+        } else {  // list full (more than NT bitmap containers in one round): this thread ORs it in word by word
+          const uint32_t* src = (const uint32_t*)(V[vw[k]].roaring + c[k].offset);
+          uint32_t* chunk = V[vw[k]].chunk;
+          for (uint32_t wd = 0; wd < 2048; wd++)
+            if (src[wd]) atomicOr(&chunk[wd], __builtin_bitreverse32(src[wd]));
+        }
       } else if (c[k].type == 2) {  // runs: uint16 nruns, then (start, length - 1)
         const uint16_t* rr = (const uint16_t*)(V[vw[k]].roaring + c[k].offset) + 1;
         uint32_t* chunk = V[vw[k]].chunk;
@@ -139,7 +154,7 @@ __device__ __forceinline__ void roaring_key_chunks(const RoarView* V, uint32_t n
     __syncthreads();
     // 3. every quad of the round's array containers, kQ per thread per step (their loads in flight together): owner
     //    thread = the last prefix <= e, then its container; 4 entries per 8-byte load
-    constexpr int kQ = 4;
+    constexpr int kQ = kRoarQ;
     const uint32_t total = S.tpre[NT];
     for (uint32_t e0 = tid; e0 < total; e0 += kQ * NT) {
       uint2 w[kQ];
@@ -180,7 +195,7 @@ __device__ __forceinline__ void roaring_key_chunks(const RoarView* V, uint32_t n
     }
     __syncthreads();  // the bitmap containers below OR whole words without atomics
     // 4. bitmap containers: 1 024 little-endian uint64 words each; a thread owns the same words of every chunk
-    const uint32_t nb = S.nbml;
+    const uint32_t nb = S.nbml < NT ? S.nbml : NT;
     for (uint32_t k = 0; k < nb; k++) {
       const uint32_t* src = (const uint32_t*)(V[S.bview[k]].roaring + S.bml[k]);
       uint32_t* chunk = V[S.bview[k]].chunk;
