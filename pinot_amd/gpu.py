@@ -313,16 +313,17 @@ class GpuEngine:
         """Copies of a pg_result's arrays: stats (int64[6]), keys uint32[G, K], values float64[G, A], counts
         int64[G, A] and, with value sets, distinct offsets uint64[G * A + 1] / ids uint32[num_distinct]."""
         A, K, G = r.num_aggs, r.num_keys, r.num_groups
-        vals = np.ctypeslib.as_array(r.values, shape=(max(G * A, 1),))[:G * A].reshape(G, A).copy() if G and A else \
-            np.zeros((G, A))
-        cnts = np.ctypeslib.as_array(r.counts, shape=(max(G * A, 1),))[:G * A].reshape(G, A).copy() if G and A else \
-            np.zeros((G, A), dtype=np.int64)
-        keys = np.ctypeslib.as_array(r.keys, shape=(max(G * K, 1),))[:G * K].reshape(G, K).copy() if G and K else \
-            np.zeros((G, K), dtype=np.uint32)
+
+        def copy(ptr, n, dt, shape):  # one bytes copy out of the library's buffer, viewed read-only (the cheapest
+            return np.frombuffer(C.string_at(ptr, n * np.dtype(dt).itemsize), dtype=dt).reshape(shape)  # ctypes path)
+        vals = copy(r.values, G * A, np.float64, (G, A)) if G and A else np.zeros((G, A))
+        cnts = copy(r.counts, G * A, np.int64, (G, A)) if G and A else np.zeros((G, A), dtype=np.int64)
+        keys = copy(r.keys, G * K, np.uint32, (G, K)) if G and K else np.zeros((G, K), dtype=np.uint32)
         offs = ids = None
         if r.distinct_offsets:
-            offs = np.ctypeslib.as_array(r.distinct_offsets, shape=(G * A + 1,)).copy()
-            ids = np.ctypeslib.as_array(r.distinct_ids, shape=(max(int(r.num_distinct), 1),))[:r.num_distinct].copy()
+            offs = copy(r.distinct_offsets, G * A + 1, np.uint64, (G * A + 1,))
+            nd = int(r.num_distinct)
+            ids = copy(r.distinct_ids, nd, np.uint32, (nd,)) if nd else np.zeros(0, dtype=np.uint32)
         s = r.stats
         stats = np.array([s.num_docs_scanned, s.num_entries_scanned_in_filter, s.num_entries_scanned_post_filter,
                           s.num_total_docs, s.num_segments_processed, s.num_segments_matched], dtype=np.int64)
