@@ -1173,7 +1173,7 @@ struct Scratch {
   hipStream_t s;
   std::vector<DevBuf> bufs;
   explicit Scratch(hipStream_t st) : s(st) {}
-  ~Scratch() { (void)hipStreamSynchronize(s); }  // before the blocks return to the pool
+  ~Scratch() { if (!bufs.empty()) (void)hipStreamSynchronize(s); }  // before the blocks return to the pool
   template <class T> T* get(uint64_t n, int& rc) {
     bufs.emplace_back();
     rc = bufs.back().alloc_pooled(n * sizeof(T) + 16);
@@ -3803,8 +3803,6 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   if (rc) return rc;
   hipStream_t s = thread_stream();
   hipEvent_t e0 = t_ctx.ev[3], e1 = t_ctx.ev[2];
-  HIP_CHECK(hipEventRecord(e0, s));
-  Scratch sc(s);
   const StateView v = P.view();
   const FinalSpec f = make_final(P, plan);
   const uint32_t AA = A ? A : 1;
@@ -3812,8 +3810,12 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   bool any_dc = false;
   for (uint32_t a = 0; a < A; a++) any_dc |= P.aggs[a].fn == PG_AGG_DISTINCTCOUNT;
   const uint64_t row_words = (uint64_t)v.n_i64 + v.n_f64 + v.n_min + v.n_max;
-  if ((P.mode == GM_DENSE || P.mode == GM_NONE) && !any_dc && P.num_slots * row_words * 8 <= kHostFinalBytes)
+  if ((P.mode == GM_DENSE || P.mode == GM_NONE) && !any_dc && P.num_slots * row_words * 8 <= kHostFinalBytes) {
+    if (!P.host_state) HIP_CHECK(hipEventRecord(e0, s));  // (a state already on the host needs no device time)
     return finalize_small(pp, plan, out, P, f, e0, e1, s);
+  }
+  HIP_CHECK(hipEventRecord(e0, s));
+  Scratch sc(s);
 
   // 1. the groups
   uint64_t n = 1;
