@@ -239,7 +239,9 @@ __host__ __device__ inline double order_key_decode(int64_t k) {
 
 // ---- the fused scan (pg_scan.hip).  Everything else the runtime launches is declared in pg_aux.h, so that the scan's
 // nine shapes (a ~15 minute build) recompile only when this header changes.
-hipError_t launch_scan(const QuerySpec& q, uint32_t blocks, hipStream_t s);                  // pg_scan.hip
+hipError_t launch_scan(const QuerySpec& q, uint32_t blocks, hipStream_t s, bool co = false);  // pg_scan.hip
+// co: the 128-VGPR variant that runs beside the exact-mode stream kernel (scan_co_resident shapes)
+bool scan_co_resident(const QuerySpec& q);
 size_t scan_lds_bytes(const QuerySpec& q);
 uint32_t scan_min_blocks_per_cu(bool grouped);
 

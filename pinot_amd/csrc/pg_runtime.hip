@@ -1071,9 +1071,15 @@ struct ThreadCtx {  // per calling thread: staging + events, created once
   std::vector<WorkItem> items;  // work items of the current query (capacity reused across queries)
   std::vector<WorkItem> items_perm;  // XCD-grouped order of the items (swapped with `items`)
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  // the overlapped list scan (stream plan's `split`): its first half runs on s2 beside the stream's second half
+  hipStream_t s2 = nullptr;
+  hipEvent_t ev_a = nullptr, ev_l = nullptr;
   int init() {
     if (ev[0]) return PG_OK;
     for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_a, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_l, hipEventDisableTiming));
+    HIP_CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
     return PG_OK;
   }
 };
@@ -2448,6 +2454,9 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     std::vector<uint32_t> extra;  // further AND children tested in the stream (runtime bit width)
     bool extra_lds_free = false;  // the further children need no LDS (allowed beside the exact mode's LUT)
     std::vector<StreamLaunch> launches;
+    // overlapped list scan: launches [0, split_launch) stream the items [0, split) (the first half of the segments);
+    // their list scan runs on a second stream while the remaining launches stream the rest (0: no overlap)
+    uint32_t split = 0, split_launch = 0;
   } sp;
   {
     static const char* st_env = getenv("PG_STREAM");
@@ -2555,30 +2564,52 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
           sp.launches.push_back(std::move(sl));
           continue;
         }
-        const std::vector<uint32_t>& segs_b = bb.second;
-        uint64_t Tb = 0;
-        for (uint32_t si : segs_b) Tb += seg_groups[si];
-        const uint64_t nb = std::max<uint64_t>(1, std::min<uint64_t>(Tb, (NB * Tb + T - 1) / T));
-        StreamLaunch sl;
-        sl.bits = bb.first;
-        sl.blocks = (uint32_t)nb;
-        sl.first.assign(nb + 1, 0);
-        size_t k = 0;
-        uint64_t seg_first = 0;
-        for (uint64_t b = 0; b < nb; b++) {
-          sl.first[b] = (uint32_t)items.size();
-          uint64_t t0 = b * Tb / nb;
-          const uint64_t t1 = (b + 1) * Tb / nb;
-          while (t0 < t1) {
-            while (t0 >= seg_first + seg_groups[segs_b[k]]) { seg_first += seg_groups[segs_b[k]]; k++; }
-            const uint64_t e = std::min(t1, seg_first + seg_groups[segs_b[k]]);
-            items.push_back({segs_b[k], (uint32_t)(t0 - seg_first), (uint32_t)(e - seg_first), 0});
-            max_groups = std::max(max_groups, e - t0);
-            t0 = e;
+        // overlapped list scan (exact mode, one bit width, >= 2 segments, a shape that fits beside the stream):
+        // two launches over the two halves of the segments, each on the whole chip.  PG_LIST_OVERLAP=0 disables.
+        const char* ov_env = getenv("PG_LIST_OVERLAP");
+        std::vector<std::vector<uint32_t>> parts;
+        if (sp.exact && by_bits.size() == 1 && bb.second.size() >= 2 && scan_co_resident(q) &&
+            !(ov_env && atoi(ov_env) == 0)) {
+          uint64_t acc = 0;
+          size_t cut = 0;
+          while (cut + 1 < bb.second.size() && 2 * (acc + seg_groups[bb.second[cut]]) <= T) acc += seg_groups[bb.second[cut++]];
+          if (cut == 0) cut = 1;
+          parts.emplace_back(bb.second.begin(), bb.second.begin() + cut);
+          parts.emplace_back(bb.second.begin() + cut, bb.second.end());
+        } else {
+          parts.push_back(bb.second);
+        }
+        for (size_t pi = 0; pi < parts.size(); pi++) {
+          const std::vector<uint32_t>& segs_b = parts[pi];
+          uint64_t Tb = 0;
+          for (uint32_t si : segs_b) Tb += seg_groups[si];
+          const uint64_t nb = parts.size() > 1 ? std::max<uint64_t>(1, std::min<uint64_t>(Tb, NB))
+                                               : std::max<uint64_t>(1, std::min<uint64_t>(Tb, (NB * Tb + T - 1) / T));
+          StreamLaunch sl;
+          sl.bits = bb.first;
+          sl.blocks = (uint32_t)nb;
+          sl.first.assign(nb + 1, 0);
+          size_t k = 0;
+          uint64_t seg_first = 0;
+          for (uint64_t b = 0; b < nb; b++) {
+            sl.first[b] = (uint32_t)items.size();
+            uint64_t t0 = b * Tb / nb;
+            const uint64_t t1 = (b + 1) * Tb / nb;
+            while (t0 < t1) {
+              while (t0 >= seg_first + seg_groups[segs_b[k]]) { seg_first += seg_groups[segs_b[k]]; k++; }
+              const uint64_t e = std::min(t1, seg_first + seg_groups[segs_b[k]]);
+              items.push_back({segs_b[k], (uint32_t)(t0 - seg_first), (uint32_t)(e - seg_first), 0});
+              max_groups = std::max(max_groups, e - t0);
+              t0 = e;
+            }
+          }
+          sl.first[nb] = (uint32_t)items.size();
+          sp.launches.push_back(std::move(sl));
+          if (parts.size() > 1 && pi == 0) {
+            sp.split = (uint32_t)items.size();
+            sp.split_launch = (uint32_t)sp.launches.size();
           }
         }
-        sl.first[nb] = (uint32_t)items.size();
-        sp.launches.push_back(std::move(sl));
       }
       const double expect = pass * 32.0 * (double)max_groups;
       const uint64_t slack = std::min<uint64_t>(1024, std::max<uint64_t>(64, 8 * max_groups));
@@ -2928,7 +2959,11 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   // declared after the buffers it protects: on any exit, wait for queued work before they return to the pool
   struct SyncOnExit {
     hipStream_t s;
-    ~SyncOnExit() { (void)hipStreamSynchronize(s); }
+    bool s2 = false;  // an overlapped list-scan half was launched on the second stream
+    ~SyncOnExit() {
+      if (s2) (void)hipStreamSynchronize(t_ctx.s2);
+      (void)hipStreamSynchronize(s);
+    }
   } sync_on_exit{s};
   if ((rc = arena.alloc_pooled(ar.h.size() + 16))) return rc;
   if (scratch_bytes && (rc = scratch.alloc_pooled(scratch_bytes))) return rc;
@@ -3067,9 +3102,11 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     ss.docs = (uint32_t*)l_docs.p;
     ss.counts = (uint32_t*)l_counts.p;
     ss.err = q.err;
-    for (const StreamLaunch& sl : sp.launches) {
+    for (size_t k = 0; k < sp.launches.size(); k++) {
+      const StreamLaunch& sl = sp.launches[k];
       ss.block_first = (const uint32_t*)(dA + sl.first_off);
       HIP_CHECK(launch_stream(ss, sl.bits, sl.blocks, s));
+      if (sp.split && k + 1 == sp.split_launch) HIP_CHECK(hipEventRecord(t_ctx.ev_a, s));  // the first half's survivors
     }
     q.list_docs = ss.docs;
     q.list_counts = ss.counts;
@@ -3259,6 +3296,25 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   } else if (ix.on) {
     t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
     HIP_CHECK(launch_index_count(ix.spec, ix.blocks, s));
+  } else if (q.num_items && sp.on && sp.split && sp.split < q.num_items) {
+    // overlapped list scan: the first half's items on the second stream as soon as their stream launch is done (its
+    // blocks share the CUs with the second stream launch: 128-VGPR variant), the second half's after the stream
+    t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
+    QuerySpec qa = q, qb = q;
+    qa.num_items = sp.split;
+    qb.items = q.items + sp.split;
+    qb.num_items = q.num_items - sp.split;
+    qb.list_docs = q.list_docs + (uint64_t)sp.split * q.list_cap;
+    qb.list_counts = q.list_counts + sp.split;
+    const uint32_t ga = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(qa.num_items, (uint64_t)blocks * sp.split / q.num_items));
+    const uint32_t gb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(qb.num_items, blocks > ga ? blocks - ga : 1));
+    sync_on_exit.s2 = true;
+    HIP_CHECK(hipStreamWaitEvent(t_ctx.s2, t_ctx.ev_a, 0));
+    HIP_CHECK(launch_scan(qa, ga, t_ctx.s2, true));
+    HIP_CHECK(hipEventRecord(t_ctx.ev_l, t_ctx.s2));
+    HIP_CHECK(launch_scan(qb, gb, s, true));
+    HIP_CHECK(hipStreamWaitEvent(s, t_ctx.ev_l, 0));  // everything after (readbacks, finalize) sees both halves
+    scan_ran = true;
   } else if (q.num_items) {
     t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
     HIP_CHECK(launch_scan(q, blocks, s));

@@ -914,11 +914,10 @@ __host__ __device__ inline size_t scan_queue_off(const QuerySpec& q) {
 }
 
 template <bool GROUPED, int MAXA, int MAXK>
-__global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_WAVES_AGG) void scan_kernel(QuerySpec qarg) {
+__device__ __forceinline__ void scan_body() {
   // the spec is read where the launch put it (the kernel-argument segment, offset 0): bound by reference to the
   // by-value parameter, a lane-varying index into it made the compiler copy all of it to scratch (1.4 KB per lane)
   const QuerySpec& q = *(const QuerySpec*)__builtin_amdgcn_kernarg_segment_ptr();
-  (void)qarg;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* stage = (uint32_t*)(smem + 16);                                   // staging ring (16 bytes in: st[-1])
   int32_t* lds_sets = (int32_t*)(stage + q.stage_ring * q.stage_lds_words);  // IN-list filter bitmaps / hash sets
@@ -1217,8 +1216,27 @@ __global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_W
   }
 }
 
+template <bool GROUPED, int MAXA, int MAXK>
+__global__ __launch_bounds__(kBlock, GROUPED ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_WAVES_AGG) void scan_kernel(QuerySpec qarg) {
+  (void)qarg;
+  scan_body<GROUPED, MAXA, MAXK>();
+}
+// The same body under a 128-VGPR budget (4 waves / SIMD): a list-mode launch that runs beside the exact-mode stream
+// kernel (4 waves x 96 VGPRs per SIMD) fits the SIMD's remaining 128 registers, so the two overlap on every CU.
+template <bool GROUPED, int MAXA, int MAXK>
+__global__ __launch_bounds__(kBlock, 4) void scan_kernel_co(QuerySpec qarg) {
+  (void)qarg;
+  scan_body<GROUPED, MAXA, MAXK>();
+}
+
 template <bool G, int A, int K>
-void launch_one(const QuerySpec& q, uint32_t blocks, size_t lds, hipStream_t s) {
+void launch_one(const QuerySpec& q, uint32_t blocks, size_t lds, hipStream_t s, bool co) {
+  if constexpr (G && A == 2 && K == 1) {  // the one grouped shape with a co-resident variant (config 2's list scan)
+    if (co) {
+      hipLaunchKernelGGL((scan_kernel_co<G, A, K>), dim3(blocks), dim3(kBlock), lds, s, q);
+      return;
+    }
+  }
   hipLaunchKernelGGL((scan_kernel<G, A, K>), dim3(blocks), dim3(kBlock), lds, s, q);
 }
 
@@ -1230,28 +1248,33 @@ void launch_one(const QuerySpec& q, uint32_t blocks, size_t lds, hipStream_t s) 
 
 #ifdef PG_SCAN_SHARD
 #if PG_SCAN_SHARD == 0
-template void launch_one<false, 2, 0>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+template void launch_one<false, 2, 0>(const QuerySpec&, uint32_t, size_t, hipStream_t, bool);
 #elif PG_SCAN_SHARD == 1
-template void launch_one<false, 4, 0>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+template void launch_one<false, 4, 0>(const QuerySpec&, uint32_t, size_t, hipStream_t, bool);
 #elif PG_SCAN_SHARD == 2
-template void launch_one<false, kMaxAggs, 0>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+template void launch_one<false, kMaxAggs, 0>(const QuerySpec&, uint32_t, size_t, hipStream_t, bool);
 #elif PG_SCAN_SHARD == 3
-template void launch_one<true, 2, 1>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+template void launch_one<true, 2, 1>(const QuerySpec&, uint32_t, size_t, hipStream_t, bool);
 #elif PG_SCAN_SHARD == 4
-template void launch_one<true, 4, 1>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+template void launch_one<true, 4, 1>(const QuerySpec&, uint32_t, size_t, hipStream_t, bool);
 #elif PG_SCAN_SHARD == 5
-template void launch_one<true, kMaxAggs, 1>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+template void launch_one<true, kMaxAggs, 1>(const QuerySpec&, uint32_t, size_t, hipStream_t, bool);
 #elif PG_SCAN_SHARD == 6
-template void launch_one<true, 2, kMaxKeys>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+template void launch_one<true, 2, kMaxKeys>(const QuerySpec&, uint32_t, size_t, hipStream_t, bool);
 #elif PG_SCAN_SHARD == 7
-template void launch_one<true, 4, kMaxKeys>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+template void launch_one<true, 4, kMaxKeys>(const QuerySpec&, uint32_t, size_t, hipStream_t, bool);
 #elif PG_SCAN_SHARD == 8
-template void launch_one<true, kMaxAggs, kMaxKeys>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+template void launch_one<true, kMaxAggs, kMaxKeys>(const QuerySpec&, uint32_t, size_t, hipStream_t, bool);
 #endif
 #else
 #define PG_SCAN_EXTERN(i, G, A, K) \
-  extern template void launch_one<G, A, K>(const QuerySpec&, uint32_t, size_t, hipStream_t);
+  extern template void launch_one<G, A, K>(const QuerySpec&, uint32_t, size_t, hipStream_t, bool);
 PG_SCAN_SHAPES(PG_SCAN_EXTERN)
+
+bool scan_co_resident(const QuerySpec& q) {  // shapes whose launch fits beside the exact-mode stream kernel
+  static_assert(PG_SCAN_MIN_WAVES_AGG >= 4, "the aggregation-only 2-aggregation shape runs within 128 VGPRs as is");
+  return q.num_aggs <= 2 && q.num_keys <= 1;
+}
 
 // LDS of a launch: staging ring | IN sets | group table; at least the aggregation-only block reduction's
 // [4][1 + kMaxAggs] words, which reuses the ring.
@@ -1266,21 +1289,21 @@ uint32_t scan_min_blocks_per_cu(bool grouped) {  // 256-thread blocks: waves/SIM
   return grouped ? PG_SCAN_MIN_WAVES : PG_SCAN_MIN_WAVES_AGG;
 }
 
-hipError_t launch_scan(const QuerySpec& q, uint32_t blocks, hipStream_t s) {
+hipError_t launch_scan(const QuerySpec& q, uint32_t blocks, hipStream_t s, bool co) {
   const size_t lds = scan_lds_bytes(q);
   const uint32_t na = q.num_aggs;
   if (q.num_keys == 0) {
-    if (na <= 2) launch_one<false, 2, 0>(q, blocks, lds, s);
-    else if (na <= 4) launch_one<false, 4, 0>(q, blocks, lds, s);
-    else launch_one<false, kMaxAggs, 0>(q, blocks, lds, s);
+    if (na <= 2) launch_one<false, 2, 0>(q, blocks, lds, s, co);
+    else if (na <= 4) launch_one<false, 4, 0>(q, blocks, lds, s, co);
+    else launch_one<false, kMaxAggs, 0>(q, blocks, lds, s, co);
   } else if (q.num_keys == 1) {
-    if (na <= 2) launch_one<true, 2, 1>(q, blocks, lds, s);
-    else if (na <= 4) launch_one<true, 4, 1>(q, blocks, lds, s);
-    else launch_one<true, kMaxAggs, 1>(q, blocks, lds, s);
+    if (na <= 2) launch_one<true, 2, 1>(q, blocks, lds, s, co);
+    else if (na <= 4) launch_one<true, 4, 1>(q, blocks, lds, s, co);
+    else launch_one<true, kMaxAggs, 1>(q, blocks, lds, s, co);
   } else {
-    if (na <= 2) launch_one<true, 2, kMaxKeys>(q, blocks, lds, s);
-    else if (na <= 4) launch_one<true, 4, kMaxKeys>(q, blocks, lds, s);
-    else launch_one<true, kMaxAggs, kMaxKeys>(q, blocks, lds, s);
+    if (na <= 2) launch_one<true, 2, kMaxKeys>(q, blocks, lds, s, co);
+    else if (na <= 4) launch_one<true, 4, kMaxKeys>(q, blocks, lds, s, co);
+    else launch_one<true, kMaxAggs, kMaxKeys>(q, blocks, lds, s, co);
   }
   return hipGetLastError();
 }

@@ -87,6 +87,22 @@ def test_stream_exact_mode_further_leaves(qi, table, monkeypatch, gpu_engine, or
     assert_same_result(g, n, table=table)
 
 
+@pytest.mark.parametrize("qi", [0, 1, 5])
+def test_stream_overlapped_list_scan(qi, table, monkeypatch, gpu_engine, oracle_engine):
+    """The list scan split in two halves, the first on a second HIP stream beside the stream kernel's second launch
+    (exact mode, >= 2 segments, <= 2 aggregations and <= 1 key): same answers as the oracle and as PG_LIST_OVERLAP=0."""
+    q = parse(STREAM_QUERIES[qi])
+    g = gpu_engine.execute(table, q)
+    assert gpu_engine.last_timing().scan_launches == 2, "the selective stream did not run"
+    o = oracle_engine.execute(table, q)
+    assert_same_result(g, o, table=table)
+    assert g.stats.num_docs_scanned == o.stats.num_docs_scanned
+    monkeypatch.setenv("PG_LIST_OVERLAP", "0")
+    n = gpu_engine.execute(table, q)
+    assert_same_result(g, n, table=table)
+    assert g.stats.num_docs_scanned == n.stats.num_docs_scanned
+
+
 def test_stream_not_used_for_unselective_filters(table, gpu_engine, oracle_engine):
     q = parse("SELECT SUM(clicks) FROM t WHERE day BETWEEN 18000 AND 18200 AND acct < 150000")
     g = gpu_engine.execute(table, q)
