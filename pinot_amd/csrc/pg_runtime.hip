@@ -2565,11 +2565,14 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
           continue;
         }
         // overlapped list scan (exact mode, one bit width, >= 2 segments, a shape that fits beside the stream):
-        // two launches over the two halves of the segments, each on the whole chip.  PG_LIST_OVERLAP=0 disables.
+        // two launches over the two halves of the segments, each on the whole chip.  PG_LIST_OVERLAP=1 enables it
+        // (read per call); off by default: config 2 measured 0.714 vs 0.644 ms per query -- the two stream launches
+        // took 0.514 ms instead of 0.445 (the first half's list scan, running beside the second launch, slows it by
+        // as much as it saves)
         const char* ov_env = getenv("PG_LIST_OVERLAP");
         std::vector<std::vector<uint32_t>> parts;
-        if (sp.exact && by_bits.size() == 1 && bb.second.size() >= 2 && scan_co_resident(q) &&
-            !(ov_env && atoi(ov_env) == 0)) {
+        if (sp.exact && by_bits.size() == 1 && bb.second.size() >= 2 && scan_co_resident(q) && ov_env &&
+            atoi(ov_env) == 1) {
           uint64_t acc = 0;
           size_t cut = 0;
           while (cut + 1 < bb.second.size() && 2 * (acc + seg_groups[bb.second[cut]]) <= T) acc += seg_groups[bb.second[cut++]];

@@ -90,8 +90,10 @@ def test_stream_exact_mode_further_leaves(qi, table, monkeypatch, gpu_engine, or
 @pytest.mark.parametrize("qi", [0, 1, 5])
 def test_stream_overlapped_list_scan(qi, table, monkeypatch, gpu_engine, oracle_engine):
     """The list scan split in two halves, the first on a second HIP stream beside the stream kernel's second launch
-    (exact mode, >= 2 segments, <= 2 aggregations and <= 1 key): same answers as the oracle and as PG_LIST_OVERLAP=0."""
+    (exact mode, >= 2 segments, <= 2 aggregations and <= 1 key; PG_LIST_OVERLAP=1, off by default): same answers as
+    the oracle and as PG_LIST_OVERLAP=0."""
     q = parse(STREAM_QUERIES[qi])
+    monkeypatch.setenv("PG_LIST_OVERLAP", "1")
     g = gpu_engine.execute(table, q)
     assert gpu_engine.last_timing().scan_launches == 2, "the selective stream did not run"
     o = oracle_engine.execute(table, q)
