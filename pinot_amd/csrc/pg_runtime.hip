@@ -1067,6 +1067,7 @@ struct ThreadCtx {  // per calling thread: staging + events, created once
   PinnedBuf pinned;
   PinnedBuf readback;  // per-segment match counts + error word, copied back before the one stream sync
   PinnedBuf state_host;  // small dense states copied back with them (pg_execute)
+  PinnedBuf ids_host;    // value-set ids of a finalize
   PinnedVec arena;              // pinned host image of the parameter arena (capacity reused across queries)
   std::vector<WorkItem> items;  // work items of the current query (capacity reused across queries)
   std::vector<WorkItem> items_perm;  // XCD-grouped order of the items (swapped with `items`)
@@ -3707,7 +3708,7 @@ void order_rows(const pg_plan* plan, const Partials& P, uint64_t nc, const std::
 
 int build_result(pg_partials* pp, const pg_plan* plan, pg_result** out, const Partials& P, uint64_t nc,
                  const std::vector<uint64_t>& hk, const std::vector<double>& hv, const std::vector<int64_t>& hc,
-                 bool sets, const std::vector<uint64_t>& hoff, const std::vector<uint32_t>& hids);
+                 bool sets, const std::vector<uint64_t>& hoff, const uint32_t* hids, uint64_t n_ids);
 
 
 // finalize() for small dense states without DISTINCTCOUNT: the same groups, final values and ORDER BY candidates
@@ -3800,7 +3801,7 @@ int finalize_small(pg_partials* pp, const pg_plan* plan, pg_result** out, const 
     hv.resize(nc * A);
     hc.resize(nc * A);
   }
-  return build_result(pp, plan, out, P, nc, hk, hv, hc, false, {}, {});
+  return build_result(pp, plan, out, P, nc, hk, hv, hc, false, {}, nullptr, 0);
 }
 
 // Partial state -> host result: the groups present (doc count > 0), their final values, the plan's ORDER BY trim
@@ -4041,7 +4042,8 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
     PG_PROF("f_precut");
   }
   std::vector<uint64_t> hoff;
-  std::vector<uint32_t> hids;
+  const uint32_t* hids = nullptr;  // the value sets' ids, copied back into pinned memory (config 4: 2.5 MB)
+  uint64_t n_ids = 0;
   if (sets) {
     const uint64_t m = nc * A;
     uint64_t* sizes = sc.get<uint64_t>(m + 1, rc);
@@ -4058,8 +4060,11 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
     uint32_t* ids = sc.get<uint32_t>(hoff[m] + 1, rc);
     if (rc) return rc;
     HIP_CHECK(launch_set_extract(v, f, cs, nc, offs, ids, s));
-    hids.resize(hoff[m]);
-    if (hoff[m]) HIP_CHECK(hipMemcpyAsync(hids.data(), ids, hoff[m] * 4, hipMemcpyDeviceToHost, s));
+    n_ids = hoff[m];
+    uint32_t* h = (uint32_t*)t_ctx.ids_host.get(n_ids * 4 + 4);
+    if (!h) return fail(PG_E_NOMEM, "pinned readback of %llu set ids failed", (unsigned long long)n_ids);
+    if (n_ids) HIP_CHECK(hipMemcpyAsync(h, ids, n_ids * 4, hipMemcpyDeviceToHost, s));
+    hids = h;
   }
   HIP_CHECK(hipEventRecord(e1, s));
   HIP_CHECK(hipStreamSynchronize(s));
@@ -4067,13 +4072,13 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   float fm = 0;
   (void)hipEventElapsedTime(&fm, e0, e1);
   t_timing.finalize_ms = fm;
-  return build_result(pp, plan, out, P, nc, hk, hv, hc, sets, hoff, hids);
+  return build_result(pp, plan, out, P, nc, hk, hv, hc, sets, hoff, hids, n_ids);
 }
 
 // Host order of the candidates (every ORDER BY item, then the packed key: a total order) and the result rows.
 int build_result(pg_partials* pp, const pg_plan* plan, pg_result** out, const Partials& P, uint64_t nc,
                  const std::vector<uint64_t>& hk, const std::vector<double>& hv, const std::vector<int64_t>& hc,
-                 bool sets, const std::vector<uint64_t>& hoff, const std::vector<uint32_t>& hids) {
+                 bool sets, const std::vector<uint64_t>& hoff, const uint32_t* hids, uint64_t n_ids) {
   if (P.wide && P.wide->user_plan) plan = P.wide->user_plan;  // the caller's K keys and ORDER BY
   const uint32_t A = plan->num_aggs, K = plan->num_keys;
   const uint32_t AA = A ? A : 1;
@@ -4121,9 +4126,9 @@ int build_result(pg_partials* pp, const pg_plan* plan, pg_result** out, const Pa
   }
   if (sets) {
     const uint64_t m = nc * A;
-    r->num_distinct = hids.size();
+    r->num_distinct = n_ids;
     r->distinct_offsets = (uint64_t*)malloc((m + 1) * 8);
-    r->distinct_ids = (uint32_t*)malloc(hids.size() * 4 + 4);
+    r->distinct_ids = (uint32_t*)malloc(n_ids * 4 + 4);
     if (!r->distinct_offsets || !r->distinct_ids) { pg_result_free(r); return fail(PG_E_NOMEM, "out of host memory"); }
     uint64_t at = 0;
     for (uint64_t o = 0; o < nc; o++)
@@ -4131,7 +4136,7 @@ int build_result(pg_partials* pp, const pg_plan* plan, pg_result** out, const Pa
         const uint64_t src = perm[o] * A + a;
         r->distinct_offsets[o * A + a] = at;
         const uint64_t len = hoff[src + 1] - hoff[src];
-        if (len) memcpy(r->distinct_ids + at, hids.data() + hoff[src], len * 4);
+        if (len) memcpy(r->distinct_ids + at, hids + hoff[src], len * 4);
         at += len;
       }
     r->distinct_offsets[m] = at;
