@@ -357,8 +357,22 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? (PG_STREAM_PIPE_EXTRA
       if (EXACT) {
         __syncthreads();  // every thread is done with the previous segment's LUT
         if (L.kind == LK_SET_LDS) {
-          const uint32_t nw = ldcf(p.exact_nwords, wi.seg);
-          for (uint32_t k = tid; k < nw; k += NT) lds_sets[k] = L.lut[k];
+          // the segment's exact LUT (up to 128 KiB) into LDS: 16-byte buffer loads, 8 per thread issued before any is
+          // stored (one load latency per segment change instead of one per word; reads past the LUT return 0)
+          const uint32_t nw = ldcf(p.exact_nwords, wi.seg), nq = (nw + 3u) / 4u;
+          const rsrc_t rl = rsrc_of(L.lut, 4u * nw);
+          constexpr uint32_t kU = 8;
+          for (uint32_t q0 = tid; q0 < nq; q0 += NT * kU) {
+            uint4 v[kU];
+#pragma unroll
+            for (uint32_t u = 0; u < kU; u++) {
+              const auto x = __builtin_amdgcn_raw_buffer_load_b128(rl, (q0 + u * NT) * 16u, 0, 0);
+              v[u] = make_uint4(x[0], x[1], x[2], x[3]);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kU; u++)
+              if (q0 + u * NT < nq) ((uint4*)lds_sets)[q0 + u * NT] = v[u];
+          }
         }
       } else if (p.set_lds_ints) {
         __syncthreads();  // every thread is done with the previous segment's sets
