@@ -14,8 +14,11 @@ Workloads (`--workload`; the default is the headline metric):
                inverted NOT_EQ and an inverted IN -- 32 segments per GPU (256 over 8 GPUs = 2 B rows)
 
 Segments are generated on the device (pinot_amd.synth) and resident in HBM before the timed region.  A step = one
-query over all of this GPU's segments: host plan compile + filter pre-pass + fused scan/aggregate kernel + device
-finalize (+ at N > 1 the cross-GPU merge, pinot_amd.combine).  Weak scaling: every rank scans its own segments.
+query over all of this GPU's segments through the relocatable plan image (pg_execute_image): host plan compile +
+filter pre-pass + fused scan/aggregate kernel + device finalize + the result's arrays (keys, values, counts, value
+sets: what the server's DataTable holds) copied into numpy (+ at N > 1 the cross-GPU merge, pinot_amd.combine).  The
+value-keyed Python dict view of those arrays (DeviceResult.rows) is built on first access, outside the step: the parity
+check after the timed region reads it.  Weak scaling: every rank scans its own segments.
 `--gpus N` without a torchrun environment launches N rank processes (torch.distributed.run) before touching a GPU.
 
 `roofline`: the hot path's kernels (the selective stream over the driving filter leaves + the fused scan over its
