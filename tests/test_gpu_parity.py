@@ -380,6 +380,43 @@ def test_dict_id_sets_on_device(dtype, gpu_engine, oracle_engine):
             assert np.array_equal(ids2[si, :counts2[si]], dict_id_set(s.columns["k"].dictionary, list(lit))), si
 
 
+def test_dict_id_sets_concurrent_with_release(gpu_engine):
+    """pg_dict_id_sets on one thread while another releases the segments it looks up (pg_segment_release): the
+    lookup holds the segment lock through its device work, so each call either sees the segment (the host's dictIds)
+    or reports it unknown -- never a read of freed dictionaries."""
+    import threading
+    from pinot_amd.gpu import PinotGpuError
+    from pinot_amd.plan import dict_id_set
+    rng = np.random.default_rng(19)
+    for rnd in range(4):
+        segs = [ImmutableSegment.create(f"r{rnd}_{s}", {"k": rng.integers(0, 200_000, 150_000).astype(np.int64)},
+                                        {"k": "LONG"}) for s in range(4)]
+        t = Table("t", segs)
+        keys = [gpu_engine.upload_segment(s, t) for s in segs]
+        lits = np.arange(0, 200_000, 7, dtype=np.int64)
+        want = [dict_id_set(s.columns["k"].dictionary, lits.tolist()) for s in segs]
+        outcomes, errors = [], []
+
+        def lookup():
+            for _ in range(20):
+                try:
+                    ids, counts = gpu_engine.dict_id_sets(t.column_ids["k"], "LONG", lits, keys)
+                    for si in range(len(segs)):
+                        if not np.array_equal(ids[si, :counts[si]], want[si]):
+                            errors.append(si)
+                    outcomes.append("ok")
+                except PinotGpuError as e:  # a released segment: refused, not read
+                    outcomes.append(str(e)[:40])
+
+        th = threading.Thread(target=lookup)
+        th.start()
+        for s in segs:
+            gpu_engine.release(s)
+        th.join()
+        assert not errors, errors
+        assert len(outcomes) == 20
+
+
 def test_in_literals_on_mv_scan_leaves(gpu_engine, oracle_engine):
     """IN / NOT_IN over an MV column without an inverted index, several segments: the leaves cross as their literals
     (values mode) and the device finds each segment's dictIds while it builds the MV scan's LUT."""
