@@ -311,6 +311,12 @@ hipError_t launch_select_slots(const StateView& v, uint32_t kind, uint32_t part,
                                uint32_t* d_num, void* temp, size_t temp_bytes, hipStream_t s);
 // The present slots of a state in no particular order (one pass, one atomic per wave): count must be zeroed
 hipError_t launch_select_present_unordered(const StateView& v, uint32_t* out, unsigned int* count, hipStream_t s);
+// DISTINCTCOUNT-ordered trim from the bucket pass's set sizes (StateView::dc_pop): a histogram of the present groups'
+// sizes (maxv + 1 bins, hist zeroed), then the present groups with size >= t (at_least) or <= t, unordered (count
+// zeroed)
+hipError_t launch_pop_hist(const StateView& v, uint32_t maxv, unsigned int* hist, hipStream_t s);
+hipError_t launch_select_pop(const StateView& v, uint32_t t, uint32_t maxv, bool at_least, uint32_t* out,
+                             unsigned int* count, hipStream_t s);
 hipError_t launch_select_flagged(const uint32_t* in, const uint8_t* flags, uint64_t n, uint32_t* out, uint32_t* d_num,
                                  void* temp, size_t temp_bytes, hipStream_t s);
 hipError_t launch_exclusive_sum(const uint64_t* in, uint64_t* out, uint64_t n, void* temp, size_t temp_bytes,

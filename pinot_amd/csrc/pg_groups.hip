@@ -66,16 +66,26 @@ hipError_t launch_select_slots(const StateView& v, uint32_t kind, uint32_t part,
 // consumes it). Each block owns one contiguous chunk: it counts its present slots, reserves its output range with ONE
 // global atomic, then writes the chunk again in slot order. (A per-wave atomic on the single counter serialised 156K
 // atomics at L2 for 10M slots: 1.8 ms; hipcub's ordered select is 0.17 ms.)
+// MODE 0: every present slot; 1 / 2: present slots whose DISTINCTCOUNT set size (dc_pop) is >= / <= t
+template <int MODE>
+__device__ __forceinline__ bool take_slot(const StateView& v, uint64_t s, uint32_t t, uint32_t maxv) {
+  if (!present(v, s)) return false;
+  if (MODE == 1) return min(v.dc_pop[s], maxv) >= t;  // (clamped as pop_hist_kernel bins it: the counts agree)
+  if (MODE == 2) return min(v.dc_pop[s], maxv) <= t;
+  return true;
+}
+
+template <int MODE>
 __global__ void __launch_bounds__(256) select_present_unordered_kernel(StateView v, uint32_t* __restrict__ out,
                                                                        unsigned int* __restrict__ count,
-                                                                       uint32_t chunk) {
+                                                                       uint32_t chunk, uint32_t t, uint32_t maxv) {
   __shared__ uint32_t wsum[4];
   __shared__ uint32_t base_s;
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   const uint64_t lo = (uint64_t)blockIdx.x * chunk;
   const uint64_t hi = std::min<uint64_t>(lo + chunk, v.num_slots);
   uint32_t mine = 0;
-  for (uint64_t s = lo + threadIdx.x; s < hi; s += 256) mine += present(v, s) ? 1u : 0u;
+  for (uint64_t s = lo + threadIdx.x; s < hi; s += 256) mine += take_slot<MODE>(v, s, t, maxv) ? 1u : 0u;
   for (int o = 32; o; o >>= 1) mine += __shfl_xor(mine, o);
   if (lane == 0) wsum[w] = mine;
   __syncthreads();
@@ -84,7 +94,7 @@ __global__ void __launch_bounds__(256) select_present_unordered_kernel(StateView
   uint32_t run = base_s;
   for (uint64_t t = lo; t < hi; t += 256) {
     const uint64_t s = t + threadIdx.x;
-    const bool take = s < hi && present(v, s);
+    const bool take = s < hi && take_slot<MODE>(v, s, t, maxv);
     const uint64_t m = __ballot(take);
     __syncthreads();  // wsum of the previous tile fully read
     if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
@@ -103,8 +113,43 @@ hipError_t launch_select_present_unordered(const StateView& v, uint32_t* out, un
   const uint64_t tiles = (v.num_slots + 255) / 256;
   const uint64_t per = std::max<uint64_t>((tiles + 2047) / 2048, 1);  // ≤2048 blocks: ≤2048 atomics on the counter
   const uint64_t blocks = std::max<uint64_t>((tiles + per - 1) / per, 1);
-  hipLaunchKernelGGL(select_present_unordered_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, v, out, count,
-                     (uint32_t)(per * 256));
+  hipLaunchKernelGGL(select_present_unordered_kernel<0>, dim3((uint32_t)blocks), dim3(256), 0, s, v, out, count,
+                     (uint32_t)(per * 256), 0u, 0u);
+  return hipGetLastError();
+}
+
+// The trim of a DISTINCTCOUNT-ordered state whose set sizes the bucket pass kept (dc_pop): a histogram of the present
+// groups' set sizes (<= maxv + 1 bins) in one pass, then the groups at or beyond the limit-th size in a second --
+// instead of present slots + order images + a radix select over every group.
+__global__ void __launch_bounds__(256) pop_hist_kernel(StateView v, uint32_t maxv, unsigned int* __restrict__ hist) {
+  extern __shared__ unsigned int lh[];
+  for (uint32_t i = threadIdx.x; i <= maxv; i += 256) lh[i] = 0;
+  __syncthreads();
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < v.num_slots; s += stride)
+    if (present(v, s)) atomicAdd(&lh[min(v.dc_pop[s], maxv)], 1u);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i <= maxv; i += 256)
+    if (lh[i]) atomicAdd(&hist[i], lh[i]);
+}
+
+hipError_t launch_pop_hist(const StateView& v, uint32_t maxv, unsigned int* hist, hipStream_t s) {
+  const uint64_t blocks = std::min<uint64_t>((v.num_slots + 255) / 256, 2048);
+  hipLaunchKernelGGL(pop_hist_kernel, dim3((uint32_t)(blocks ? blocks : 1)), dim3(256), 4ull * (maxv + 1), s, v, maxv, hist);
+  return hipGetLastError();
+}
+
+hipError_t launch_select_pop(const StateView& v, uint32_t t, uint32_t maxv, bool at_least, uint32_t* out,
+                             unsigned int* count, hipStream_t s) {
+  const uint64_t per = 16;  // 4 096 slots per block
+  const uint64_t blocks = (v.num_slots + per * 256 - 1) / (per * 256);
+  if (!blocks) return hipSuccess;
+  if (at_least)
+    hipLaunchKernelGGL(select_present_unordered_kernel<1>, dim3((uint32_t)blocks), dim3(256), 0, s, v, out, count,
+                       (uint32_t)(per * 256), t, maxv);
+  else
+    hipLaunchKernelGGL(select_present_unordered_kernel<2>, dim3((uint32_t)blocks), dim3(256), 0, s, v, out, count,
+                       (uint32_t)(per * 256), t, maxv);
   return hipGetLastError();
 }
 

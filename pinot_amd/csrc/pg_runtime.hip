@@ -3877,124 +3877,176 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   HIP_CHECK(hipEventRecord(e0, s));
   Scratch sc(s);
 
-  // 1. the groups
-  uint64_t n = 1;
-  // aggregation-only: slot 0 (always one row); a merged hash state holds key 0 only if some rank had matches
-  const bool single = K == 0 && P.mode != GM_HASH;
-  uint32_t* slots = sc.get<uint32_t>(single ? 1 : P.num_slots, rc);
-  uint32_t* d_num = sc.get<uint32_t>(2, rc);
-  if (rc) return rc;
-  if (single) {
-    HIP_CHECK(hipMemsetAsync(slots, 0, 4, s));
-  } else {
-    // an ORDER BY trim re-orders the candidates anyway (build_result): a large state's present slots may come in any
-    // order, by one pass with a wave-aggregated append instead of the ordered (two-pass) select
-    const bool trims = K && plan->num_order && plan->limit && P.num_slots >= kTrimSelectMinGroups;
-    if (trims) {
-      HIP_CHECK(hipMemsetAsync(d_num, 0, 4, s));
-      HIP_CHECK(launch_select_present_unordered(v, slots, (unsigned int*)d_num, s));
-    } else {
-      const size_t tb = select_temp_bytes(P.num_slots);
-      void* temp = sc.get<uint8_t>(tb, rc);
-      if (rc) return rc;
-      HIP_CHECK(launch_select_slots(v, SEL_PRESENT, 0, 1, slots, d_num, temp, tb, s));
-    }
-    uint32_t n32 = 0;
-    if ((rc = read_back(d_num, n32, s))) return rc;
-    n = n32;
-  }
-  PG_PROF("f_groups");
-  // 2. final values (a radix-select trim orders the groups by an image read straight from the state, and computes the
-  // final values of its candidates only)
-  const bool trim = K && plan->num_order && plan->limit && n > plan->limit;
-  const char* sel_env = getenv("PG_TRIM_SELECT");  // 0: always sort, 1: always select (tests), else by size
-  const int sel = sel_env ? atoi(sel_env) : -1;
-  const bool select = trim && (sel == 1 || (sel != 0 && n >= kTrimSelectMinGroups));
-  const bool late_values = select && order_keys_from_state_ok(v, f);
-  uint64_t* dkeys = nullptr;
-  double* dvals = nullptr;
-  int64_t* dcnts = nullptr;
-  if (!late_values) {
-    dkeys = sc.get<uint64_t>(n + 1, rc);
-    dvals = sc.get<double>((n + 1) * AA, rc);
-    dcnts = sc.get<int64_t>((n + 1) * AA, rc);
+  // 0. a trim ordered by a DISTINCTCOUNT whose set sizes the bucket pass kept (config 4's server trim): the candidates
+  // straight from a histogram of the sizes and one select pass, their final values, then on to the value sets
+  // (PG_TRIM_POP=0: the general path below)
+  const char* tp_env = getenv("PG_TRIM_POP");
+  const bool pop_trim = K && plan->num_order && plan->limit && P.num_slots >= kTrimSelectMinGroups && v.dc_pop &&
+                        f.order_kind == PG_ORDER_AGG && f.order_index < A && v.dc_pop_agg == f.order_index &&
+                        f.aggs[f.order_index].fn == PG_AGG_DISTINCTCOUNT && f.aggs[f.order_index].key_card < 8192 &&
+                        !(tp_env && atoi(tp_env) == 0);
+  uint64_t nc = 0;
+  const uint64_t* ck = nullptr;
+  const double* cv = nullptr;
+  const int64_t* cc = nullptr;
+  const uint32_t* cs = nullptr;
+  bool have_candidates = false;
+  if (pop_trim) {
+    const uint32_t maxv = f.aggs[f.order_index].key_card;  // set sizes are <= the value space
+    unsigned int* hist = sc.get<unsigned int>(maxv + 2, rc);
+    unsigned int* d_cnt = sc.get<unsigned int>(2, rc);
     if (rc) return rc;
-    HIP_CHECK(launch_final_values(v, f, slots, n, dkeys, dvals, dcnts, s));
-  }
-  // 3. ORDER BY trim
-  uint64_t nc = n;
-  const uint64_t* ck = dkeys;
-  const double* cv = dvals;
-  const int64_t* cc = dcnts;
-  const uint32_t* cs = slots;
-  if (trim) {
-    uint64_t* okeys = sc.get<uint64_t>(n, rc);
-    uint64_t* skeys = sc.get<uint64_t>(n, rc);
-    uint32_t* pos = sc.get<uint32_t>(n, rc);
-    uint32_t* spos = sc.get<uint32_t>(n, rc);
-    uint64_t* d_nc = sc.get<uint64_t>(1, rc);
-    KeySpan* d_span = sc.get<KeySpan>(1, rc);
-    if (rc) return rc;
-    // the sort covers only the key bits that differ between groups (config 4: a DISTINCTCOUNT <= 1 000 varies in
-    // 21 of the double image's 64 bits: 3 radix passes instead of 8)
-    if (late_values) HIP_CHECK(launch_order_keys_state(v, f, slots, n, okeys, pos, (uint64_t*)d_span, s));
-    else HIP_CHECK(launch_order_keys(f, dkeys, dvals, dcnts, n, okeys, pos, s, (uint64_t*)d_span));
-    KeySpan span{};
-    if ((rc = read_back(d_span, span, s))) return rc;
-    PG_PROF("f_okeys");
-    const uint64_t diff = span.any & span.anyz;
-    const uint32_t b0 = diff ? (uint32_t)__builtin_ctzll(diff) : 0u, b1 = diff ? 64u - (uint32_t)__builtin_clzll(diff) : 1u;
-    if (select) {
-      // radix select of the limit-th smallest key (a histogram readback per <= 8-bit digit of the differing bits),
-      // then the positions of every key up to it: no sort of all n groups
-      const uint32_t W = b1 - b0;
-      constexpr uint32_t kHB = 4u << kOkeyDigitBits;  // histogram bytes of the widest digit
-      unsigned int* hist = sc.get<unsigned int>(kHB / 4, rc);
-      unsigned int* hh = (unsigned int*)t_ctx.readback.get(kHB);
-      if (rc) return rc;
-      if (!hh) return fail(PG_E_NOMEM, "pinned readback failed");
-      uint64_t need = plan->limit, prefix = 0;
-      for (uint32_t hi = W; hi > 0;) {
-        const uint32_t lo = hi > kOkeyDigitBits ? hi - kOkeyDigitBits : 0;
-        const size_t hb = 4ull << (hi - lo);
-        HIP_CHECK(hipMemsetAsync(hist, 0, hb, s));
-        HIP_CHECK(launch_okey_hist(okeys, n, b0, W, lo, hi, prefix, hist, s));
-        HIP_CHECK(hipMemcpyAsync(hh, hist, hb, hipMemcpyDeviceToHost, s));
-        HIP_CHECK(hipStreamSynchronize(s));
-        uint64_t cum = 0;
-        uint32_t d = 0;
-        const uint32_t nd = 1u << (hi - lo);
-        for (; d + 1 < nd && cum + hh[d] < need; d++) cum += hh[d];
-        need -= cum;
-        prefix = (prefix << (hi - lo)) | d;
-        hi = lo;
+    unsigned int* hh = (unsigned int*)t_ctx.readback.get(4ull * (maxv + 1));
+    if (!hh) return fail(PG_E_NOMEM, "pinned readback failed");
+    HIP_CHECK(hipMemsetAsync(hist, 0, 4ull * (maxv + 1), s));
+    HIP_CHECK(hipMemsetAsync(d_cnt, 0, 4, s));
+    HIP_CHECK(launch_pop_hist(v, maxv, hist, s));
+    HIP_CHECK(hipMemcpyAsync(hh, hist, 4ull * (maxv + 1), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    uint64_t present = 0;
+    for (uint32_t x = 0; x <= maxv; x++) present += hh[x];
+    if (present > plan->limit) {
+      // the limit-th group's size in the ORDER BY direction; every group tied with it stays a candidate
+      uint64_t cum = 0;
+      uint32_t t = 0;
+      if (f.order_desc) {
+        for (uint32_t x = maxv + 1; x-- > 0;) { cum += hh[x]; if (cum >= plan->limit) { t = x; break; } }
+      } else {
+        for (uint32_t x = 0; x <= maxv; x++) { cum += hh[x]; if (cum >= plan->limit) { t = x; break; } }
       }
-      unsigned long long* d_cnt = (unsigned long long*)d_nc;
-      HIP_CHECK(hipMemsetAsync(d_cnt, 0, 8, s));
-      PG_PROF("f_radix");
-      HIP_CHECK(launch_okey_select(okeys, n, b0, W, prefix, spos, d_cnt, s));
-      if ((rc = read_back(d_nc, nc, s))) return rc;
-      PG_PROF("f_cut");
-    } else {
-      const size_t tb = sort_temp_bytes(n, b0, b1);
-      void* temp = sc.get<uint8_t>(tb, rc);
+      uint32_t* gs = sc.get<uint32_t>(cum + 1, rc);
+      uint64_t* gk = sc.get<uint64_t>(cum + 1, rc);
+      double* gv = sc.get<double>((cum + 1) * AA, rc);
+      int64_t* gc = sc.get<int64_t>((cum + 1) * AA, rc);
       if (rc) return rc;
-      HIP_CHECK(launch_sort_pairs(okeys, skeys, pos, spos, n, temp, tb, s, b0, b1));
-      HIP_CHECK(launch_cutoff(skeys, n, plan->limit, d_nc, s));
-      if ((rc = read_back(d_nc, nc, s))) return rc;
+      HIP_CHECK(launch_select_pop(v, t, maxv, f.order_desc != 0, gs, d_cnt, s));
+      HIP_CHECK(launch_final_values(v, f, gs, cum, gk, gv, gc, s));
+      nc = cum;
+      ck = gk; cv = gv; cc = gc; cs = gs;
+      have_candidates = true;
+      PG_PROF("f_pop");
     }
-    uint64_t* gk = sc.get<uint64_t>(nc + 1, rc);
-    double* gv = sc.get<double>((nc + 1) * AA, rc);
-    int64_t* gc = sc.get<int64_t>((nc + 1) * AA, rc);
-    uint32_t* gs = sc.get<uint32_t>(nc + 1, rc);
+  }
+  if (!have_candidates) {
+    // 1. the groups
+    uint64_t n = 1;
+    // aggregation-only: slot 0 (always one row); a merged hash state holds key 0 only if some rank had matches
+    const bool single = K == 0 && P.mode != GM_HASH;
+    uint32_t* slots = sc.get<uint32_t>(single ? 1 : P.num_slots, rc);
+    uint32_t* d_num = sc.get<uint32_t>(2, rc);
     if (rc) return rc;
-    if (late_values) {  // the candidates' slots, then their final values
-      HIP_CHECK(launch_gather_slots(slots, spos, nc, gs, s));
-      HIP_CHECK(launch_final_values(v, f, gs, nc, gk, gv, gc, s));
+    if (single) {
+      HIP_CHECK(hipMemsetAsync(slots, 0, 4, s));
     } else {
-      HIP_CHECK(launch_gather_final(A, spos, nc, dkeys, dvals, dcnts, slots, gk, gv, gc, gs, s));
+      // an ORDER BY trim re-orders the candidates anyway (build_result): a large state's present slots may come in any
+      // order, by one pass with a wave-aggregated append instead of the ordered (two-pass) select
+      const bool trims = K && plan->num_order && plan->limit && P.num_slots >= kTrimSelectMinGroups;
+      if (trims) {
+        HIP_CHECK(hipMemsetAsync(d_num, 0, 4, s));
+        HIP_CHECK(launch_select_present_unordered(v, slots, (unsigned int*)d_num, s));
+      } else {
+        const size_t tb = select_temp_bytes(P.num_slots);
+        void* temp = sc.get<uint8_t>(tb, rc);
+        if (rc) return rc;
+        HIP_CHECK(launch_select_slots(v, SEL_PRESENT, 0, 1, slots, d_num, temp, tb, s));
+      }
+      uint32_t n32 = 0;
+      if ((rc = read_back(d_num, n32, s))) return rc;
+      n = n32;
     }
-    ck = gk; cv = gv; cc = gc; cs = gs;
+    PG_PROF("f_groups");
+    // 2. final values (a radix-select trim orders the groups by an image read straight from the state, and computes the
+    // final values of its candidates only)
+    const bool trim = K && plan->num_order && plan->limit && n > plan->limit;
+    const char* sel_env = getenv("PG_TRIM_SELECT");  // 0: always sort, 1: always select (tests), else by size
+    const int sel = sel_env ? atoi(sel_env) : -1;
+    const bool select = trim && (sel == 1 || (sel != 0 && n >= kTrimSelectMinGroups));
+    const bool late_values = select && order_keys_from_state_ok(v, f);
+    uint64_t* dkeys = nullptr;
+    double* dvals = nullptr;
+    int64_t* dcnts = nullptr;
+    if (!late_values) {
+      dkeys = sc.get<uint64_t>(n + 1, rc);
+      dvals = sc.get<double>((n + 1) * AA, rc);
+      dcnts = sc.get<int64_t>((n + 1) * AA, rc);
+      if (rc) return rc;
+      HIP_CHECK(launch_final_values(v, f, slots, n, dkeys, dvals, dcnts, s));
+    }
+    // 3. ORDER BY trim
+    nc = n;
+    ck = dkeys;
+    cv = dvals;
+    cc = dcnts;
+    cs = slots;
+    if (trim) {
+      uint64_t* okeys = sc.get<uint64_t>(n, rc);
+      uint64_t* skeys = sc.get<uint64_t>(n, rc);
+      uint32_t* pos = sc.get<uint32_t>(n, rc);
+      uint32_t* spos = sc.get<uint32_t>(n, rc);
+      uint64_t* d_nc = sc.get<uint64_t>(1, rc);
+      KeySpan* d_span = sc.get<KeySpan>(1, rc);
+      if (rc) return rc;
+      // the sort covers only the key bits that differ between groups (config 4: a DISTINCTCOUNT <= 1 000 varies in
+      // 21 of the double image's 64 bits: 3 radix passes instead of 8)
+      if (late_values) HIP_CHECK(launch_order_keys_state(v, f, slots, n, okeys, pos, (uint64_t*)d_span, s));
+      else HIP_CHECK(launch_order_keys(f, dkeys, dvals, dcnts, n, okeys, pos, s, (uint64_t*)d_span));
+      KeySpan span{};
+      if ((rc = read_back(d_span, span, s))) return rc;
+      PG_PROF("f_okeys");
+      const uint64_t diff = span.any & span.anyz;
+      const uint32_t b0 = diff ? (uint32_t)__builtin_ctzll(diff) : 0u, b1 = diff ? 64u - (uint32_t)__builtin_clzll(diff) : 1u;
+      if (select) {
+        // radix select of the limit-th smallest key (a histogram readback per <= 8-bit digit of the differing bits),
+        // then the positions of every key up to it: no sort of all n groups
+        const uint32_t W = b1 - b0;
+        constexpr uint32_t kHB = 4u << kOkeyDigitBits;  // histogram bytes of the widest digit
+        unsigned int* hist = sc.get<unsigned int>(kHB / 4, rc);
+        unsigned int* hh = (unsigned int*)t_ctx.readback.get(kHB);
+        if (rc) return rc;
+        if (!hh) return fail(PG_E_NOMEM, "pinned readback failed");
+        uint64_t need = plan->limit, prefix = 0;
+        for (uint32_t hi = W; hi > 0;) {
+          const uint32_t lo = hi > kOkeyDigitBits ? hi - kOkeyDigitBits : 0;
+          const size_t hb = 4ull << (hi - lo);
+          HIP_CHECK(hipMemsetAsync(hist, 0, hb, s));
+          HIP_CHECK(launch_okey_hist(okeys, n, b0, W, lo, hi, prefix, hist, s));
+          HIP_CHECK(hipMemcpyAsync(hh, hist, hb, hipMemcpyDeviceToHost, s));
+          HIP_CHECK(hipStreamSynchronize(s));
+          uint64_t cum = 0;
+          uint32_t d = 0;
+          const uint32_t nd = 1u << (hi - lo);
+          for (; d + 1 < nd && cum + hh[d] < need; d++) cum += hh[d];
+          need -= cum;
+          prefix = (prefix << (hi - lo)) | d;
+          hi = lo;
+        }
+        unsigned long long* d_cnt = (unsigned long long*)d_nc;
+        HIP_CHECK(hipMemsetAsync(d_cnt, 0, 8, s));
+        PG_PROF("f_radix");
+        HIP_CHECK(launch_okey_select(okeys, n, b0, W, prefix, spos, d_cnt, s));
+        if ((rc = read_back(d_nc, nc, s))) return rc;
+        PG_PROF("f_cut");
+      } else {
+        const size_t tb = sort_temp_bytes(n, b0, b1);
+        void* temp = sc.get<uint8_t>(tb, rc);
+        if (rc) return rc;
+        HIP_CHECK(launch_sort_pairs(okeys, skeys, pos, spos, n, temp, tb, s, b0, b1));
+        HIP_CHECK(launch_cutoff(skeys, n, plan->limit, d_nc, s));
+        if ((rc = read_back(d_nc, nc, s))) return rc;
+      }
+      uint64_t* gk = sc.get<uint64_t>(nc + 1, rc);
+      double* gv = sc.get<double>((nc + 1) * AA, rc);
+      int64_t* gc = sc.get<int64_t>((nc + 1) * AA, rc);
+      uint32_t* gs = sc.get<uint32_t>(nc + 1, rc);
+      if (rc) return rc;
+      if (late_values) {  // the candidates' slots, then their final values
+        HIP_CHECK(launch_gather_slots(slots, spos, nc, gs, s));
+        HIP_CHECK(launch_final_values(v, f, gs, nc, gk, gv, gc, s));
+      } else {
+        HIP_CHECK(launch_gather_final(A, spos, nc, dkeys, dvals, dcnts, slots, gk, gv, gc, gs, s));
+      }
+      ck = gk; cv = gv; cc = gc; cs = gs;
+    }
   }
   std::vector<uint64_t> hk(nc);
   std::vector<double> hv(nc * A);

@@ -236,6 +236,13 @@ def test_radix_partitioned_group_by(mode, monkeypatch, gpu_engine, oracle_engine
         assert_same_result(gpu_engine.execute(t, q, flags=abi.PG_PLAN_VALUE_SETS), o, table=t)
         if q.order_by:
             assert reduce_to_rows(q, gpu_engine.execute(t, q, trim=True))[1] == reduce_to_rows(q, o)[1]
+            # the trim of a DISTINCTCOUNT-ordered state from its set-size histogram (finalize_core step 0) and the
+            # general order-image radix select give the same server rows
+            srv = gpu_engine.execute(t, q, trim="server")
+            monkeypatch.setenv("PG_TRIM_POP", "0")
+            gen = gpu_engine.execute(t, q, trim="server")
+            monkeypatch.delenv("PG_TRIM_POP")
+            assert srv.rows == gen.rows
 
 
 def _skewed_events(seed: int, n: int, users: int, hot: int, items_scale: int = 1):
