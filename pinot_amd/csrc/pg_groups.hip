@@ -78,14 +78,14 @@ __device__ __forceinline__ bool take_slot(const StateView& v, uint64_t s, uint32
 template <int MODE>
 __global__ void __launch_bounds__(256) select_present_unordered_kernel(StateView v, uint32_t* __restrict__ out,
                                                                        unsigned int* __restrict__ count,
-                                                                       uint32_t chunk, uint32_t t, uint32_t maxv) {
+                                                                       uint32_t chunk, uint32_t thr, uint32_t maxv) {
   __shared__ uint32_t wsum[4];
   __shared__ uint32_t base_s;
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   const uint64_t lo = (uint64_t)blockIdx.x * chunk;
   const uint64_t hi = std::min<uint64_t>(lo + chunk, v.num_slots);
   uint32_t mine = 0;
-  for (uint64_t s = lo + threadIdx.x; s < hi; s += 256) mine += take_slot<MODE>(v, s, t, maxv) ? 1u : 0u;
+  for (uint64_t s = lo + threadIdx.x; s < hi; s += 256) mine += take_slot<MODE>(v, s, thr, maxv) ? 1u : 0u;
   for (int o = 32; o; o >>= 1) mine += __shfl_xor(mine, o);
   if (lane == 0) wsum[w] = mine;
   __syncthreads();
@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(256) select_present_unordered_kernel(StateView
   uint32_t run = base_s;
   for (uint64_t t = lo; t < hi; t += 256) {
     const uint64_t s = t + threadIdx.x;
-    const bool take = s < hi && take_slot<MODE>(v, s, t, maxv);
+    const bool take = s < hi && take_slot<MODE>(v, s, thr, maxv);
     const uint64_t m = __ballot(take);
     __syncthreads();  // wsum of the previous tile fully read
     if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
