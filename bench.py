@@ -215,11 +215,18 @@ def main():
         args.segments = total // world
     elif args.segments is None:
         args.segments = W["segments"]
+    # PG_BENCH_SHARE_GPU=1 (rehearsal of the N-rank path on a one-GPU box): every rank on device 0, gloo collectives
+    share = os.environ.get("PG_BENCH_SHARE_GPU") == "1"
+    if share:
+        local = 0
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import ctypes as C
 
@@ -327,7 +334,7 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device="cpu" if share else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
