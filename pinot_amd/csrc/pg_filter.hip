@@ -316,7 +316,7 @@ __device__ __forceinline__ void stage_slice(const LeafDesc& X, uint32_t wg0, uin
 // 16-byte loads, 6 waves per SIMD so ~120 KiB per CU are in flight), survivors appended to the item's region in group
 // order within each wave: one wave prefix sum + one LDS cursor atomic per wave and group round that has a survivor.
 // This is SVScanDocIdIterator over the first AND child, the compacted output playing the role of its docId batches.
-// EXTRA: further AND leaves tested on the survivors (their code costs registers: 78 VGPRs / 6 waves per SIMD with,
+// EXTRA: further AND leaves tested on the survivors (their code costs registers: 71 VGPRs at 7 waves per SIMD with,
 // 72 / 7 without).  Items: contiguous ranges per block (block_first), or with `interleave` item b + k * gridDim.x.
 // NT: threads per block.  NT = 1024 is exact mode (p.exact_nwords): one block per CU holding the exact LUT.
 constexpr uint32_t kExactLutWords = 32768;  // 128 KiB: the exact LUT of a <= 1 M-entry dictionary
@@ -332,7 +332,10 @@ __host__ __device__ __forceinline__ uint32_t stream_lds_words(const StreamSpec& 
 #endif
 
 template <int B, bool EXTRA, int NT>
-__global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? (PG_STREAM_PIPE_EXTRA && B <= 20 ? 5 : 6) : 7)) void stream_kernel(StreamSpec p) {
+#ifndef PG_STREAM_EXTRA_WAVES
+#define PG_STREAM_EXTRA_WAVES 7  // waves / SIMD the further-leaf variant's register budget allows (71 VGPRs, no scratch; config 3 stream 0.579 vs 0.595 ms at 6, 0.631 at 8)
+#endif
+__global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? (PG_STREAM_PIPE_EXTRA && B <= 20 ? 5 : PG_STREAM_EXTRA_WAVES) : 7)) void stream_kernel(StreamSpec p) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_sets[];
   constexpr bool EXACT = NT == 1024;
   constexpr bool PIPE = EXACT || (EXTRA && PG_STREAM_PIPE_EXTRA && B <= 20);
