@@ -1,9 +1,14 @@
 #!/bin/bash
-# kernel timeline of the last query of one bench workload (dev tool; see tools/timeline.py)
+# per-step GPU timeline (kernel + memory-copy trace) of a few bench steps per workload, for the gaps between the
+# hot path's dispatches and the host's part of a step; analysed by tools/timeline.py
 set -o pipefail
-WL=${1:-highcard}; N=${2:-40}; R=$(pwd); O=$R/gpurun_out; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace ${COPIES:+--memory-copy-trace} --output-format csv -d $O/tl_$WL -o run -- python3 $R/bench.py --workload $WL --no-cpu --steps 3 --warmup 1 $BENCH_ARGS > $O/tl_$WL.log 2>&1 || { echo "trace failed"; tail -5 $O/tl_$WL.log; exit 1; }
-python3 $R/tools/timeline.py $O/tl_$WL $N > $O/tl_$WL.txt
-rm -rf $O/tl_$WL
-cat $O/tl_$WL.txt
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+TAG=${TAG:-tl}
+for w in ${WORKLOADS:-adanalytics index}; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/${TAG}_$w -o run \
+    -- python3 bench.py --workload $w --no-cpu --steps 6 --warmup 2 $BENCH_ARGS > gpurun_out/${TAG}_$w.json \
+    2> gpurun_out/${TAG}_$w.err || { echo "$w failed"; tail -20 gpurun_out/${TAG}_$w.err; exit 1; }
+  echo "$w ok"
+done
