@@ -43,6 +43,20 @@ struct FillSpans {  // byte fills deferred into the arena-upload launch (a state
 };
 hipError_t launch_arena_upload(const void* host_src, void* dst, uint64_t bytes, void* zero, uint64_t zero_bytes,
                                const FillSpans& fills, hipStream_t s);
+struct CopySpans {  // device -> mapped host spans of 8-byte words copied by one launch (the end-of-query readback)
+  static constexpr uint32_t kMax = 5;
+  const void* src[kMax];
+  void* dst[kMax];
+  uint64_t words[kMax];
+  uint32_t count;
+  void add(const void* from, void* to, uint64_t bytes) {  // bytes: a multiple of 8
+    src[count] = from;
+    dst[count] = to;
+    words[count] = bytes / 8;
+    count++;
+  }
+};
+hipError_t launch_copy_spans(const CopySpans& c, hipStream_t s);
 hipError_t launch_fill_ranges(const int32_t* ranges /*[n][2] inclusive, sorted, disjoint*/, uint32_t n,
                               uint32_t num_docs, uint32_t* bitmap, hipStream_t s);
 struct RoaringContainer {

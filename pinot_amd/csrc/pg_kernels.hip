@@ -545,4 +545,23 @@ hipError_t launch_arena_upload(const void* host_src, void* dst, uint64_t bytes, 
   return hipGetLastError();
 }
 
+// blockIdx.y == k: span k, 8-byte words, the grid's x dimension striding it (the destinations are mapped host memory:
+// the end-of-query readback in one dispatch instead of one blit per span)
+__global__ void __launch_bounds__(256) copy_spans_kernel(CopySpans c) {
+  const uint32_t k = blockIdx.y;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const unsigned long long* __restrict__ src = (const unsigned long long*)c.src[k];
+  unsigned long long* __restrict__ dst = (unsigned long long*)c.dst[k];
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < c.words[k]; i += stride) dst[i] = src[i];
+}
+
+hipError_t launch_copy_spans(const CopySpans& c, hipStream_t s) {
+  uint64_t w = 0;
+  for (uint32_t k = 0; k < c.count; k++) w = std::max<uint64_t>(w, c.words[k]);
+  if (!w) return hipSuccess;
+  const uint64_t blocks = std::min<uint64_t>((w + 255) / 256, 256);
+  hipLaunchKernelGGL(copy_spans_kernel, dim3((uint32_t)blocks, c.count), dim3(256), 0, s, c);
+  return hipGetLastError();
+}
+
 }  // namespace pg

@@ -197,8 +197,10 @@ struct DevBuf {
 };
 
 // Pinned host staging for the per-query parameter arena (one H2D DMA, no pageable bounce).
+// Fine-grained and mapped (`dp`: the device's address of p), so a kernel can write it directly (launch_copy_spans).
 struct PinnedBuf {
   void* p = nullptr;
+  void* dp = nullptr;
   uint64_t cap = 0;
   ~PinnedBuf() {
     if (p) (void)hipHostFree(p);
@@ -206,15 +208,19 @@ struct PinnedBuf {
   void* get(uint64_t n) {
     if (n > cap) {
       if (p) (void)hipHostFree(p);
+      p = dp = nullptr;
       cap = 1;
       while (cap < n) cap <<= 1;
-      if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess) {
-        p = nullptr;
+      if (hipHostMalloc(&p, cap, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess || !p ||
+          hipHostGetDevicePointer(&dp, p, 0) != hipSuccess || !dp) {
+        if (p) (void)hipHostFree(p);
+        p = dp = nullptr;
         cap = 0;
       }
     }
     return p;
   }
+  void* dev(const void* host) const { return (uint8_t*)dp + ((const uint8_t*)host - (const uint8_t*)p); }
 };
 
 // Growable pinned host buffer whose capacity persists across queries: the parameter arena is built in it directly and
@@ -2253,8 +2259,14 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       auto advance = [&](uint64_t t) {  // move si to the segment holding global tile t
         while (!seg_tiles[si] || t >= seg_first + seg_tiles[si]) { seg_first += seg_tiles[si]; si++; }
       };
+      // block b's range [b T / G, (b + 1) T / G), the bounds stepped by quotient + remainder (no divisions)
+      const uint64_t dq = T / G, dr = T % G;
+      uint64_t t1 = 0, rem = 0;
       for (uint64_t b = 0; b < G; b++) {
-        const uint64_t t0 = b * T / G, t1 = (b + 1) * T / G;  // >= 2 tiles, since G <= T / 2
+        const uint64_t t0 = t1;  // >= 2 tiles per block, since G <= T / 2
+        t1 += dq;
+        rem += dr;
+        if (rem >= G) { t1++; rem -= G; }
         advance(t0);
         const uint64_t seg_end = seg_first + seg_tiles[si];
         const uint64_t cut = t1 > seg_end ? seg_end : t0 + (t1 - t0) / 2;
@@ -2595,10 +2607,15 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
           sl.first.assign(nb + 1, 0);
           size_t k = 0;
           uint64_t seg_first = 0;
+          // block b's groups [b Tb / nb, (b + 1) Tb / nb), stepped by quotient + remainder (no divisions)
+          const uint64_t dq = Tb / nb, dr = Tb % nb;
+          uint64_t t1 = 0, rem = 0;
           for (uint64_t b = 0; b < nb; b++) {
             sl.first[b] = (uint32_t)items.size();
-            uint64_t t0 = b * Tb / nb;
-            const uint64_t t1 = (b + 1) * Tb / nb;
+            uint64_t t0 = t1;
+            t1 += dq;
+            rem += dr;
+            if (rem >= nb) { t1++; rem -= nb; }
             while (t0 < t1) {
               while (t0 >= seg_first + seg_groups[segs_b[k]]) { seg_first += seg_groups[segs_b[k]]; k++; }
               const uint64_t e = std::min(t1, seg_first + seg_groups[segs_b[k]]);
@@ -3328,7 +3345,10 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   const uint64_t n_sm = (S ? S : 1) + 2;
   uint64_t* sm = (uint64_t*)t_ctx.readback.get(8ull * n_sm);
   if (!sm) return fail(PG_E_NOMEM, "pinned readback of %llu bytes failed", (unsigned long long)(8ull * n_sm));
-  HIP_CHECK(hipMemcpyAsync(sm, P.seg_matched.p, 8ull * n_sm, hipMemcpyDeviceToHost, s));
+  // the match counts + error word, and a small final state, written into mapped host memory by one launch
+  CopySpans rb;
+  memset(&rb, 0, sizeof(rb));
+  rb.add(P.seg_matched.p, t_ctx.readback.dev(sm), 8ull * n_sm);
   P.host_state = false;
   if (t_prefetch_state && (P.mode == GM_DENSE || P.mode == GM_NONE) && !P.bit_words &&
       P.num_slots * 8ull * (P.n_i64 + P.n_f64 + P.n_min + P.n_max) <= kHostFinalBytes) {
@@ -3336,13 +3356,15 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     const uint64_t b64 = G * 8ull * P.n_i64, bf = G * 8ull * P.n_f64, bmn = G * 8ull * P.n_min, bmx = G * 8ull * P.n_max;
     uint8_t* h = (uint8_t*)t_ctx.state_host.get(b64 + bf + bmn + bmx + 8);
     if (h) {
-      HIP_CHECK(hipMemcpyAsync(h, P.i64.p, b64, hipMemcpyDeviceToHost, s));
-      if (bf) HIP_CHECK(hipMemcpyAsync(h + b64, P.f64.p, bf, hipMemcpyDeviceToHost, s));
-      if (bmn) HIP_CHECK(hipMemcpyAsync(h + b64 + bf, P.mn.p, bmn, hipMemcpyDeviceToHost, s));
-      if (bmx) HIP_CHECK(hipMemcpyAsync(h + b64 + bf + bmn, P.mx.p, bmx, hipMemcpyDeviceToHost, s));
+      const PinnedBuf& sh = t_ctx.state_host;
+      if (b64) rb.add(P.i64.p, sh.dev(h), b64);
+      if (bf) rb.add(P.f64.p, sh.dev(h + b64), bf);
+      if (bmn) rb.add(P.mn.p, sh.dev(h + b64 + bf), bmn);
+      if (bmx) rb.add(P.mx.p, sh.dev(h + b64 + bf + bmn), bmx);
       P.host_state = true;
     }
   }
+  HIP_CHECK(launch_copy_spans(rb, s));
   if (plan->deadline_ms && q.cancel) {  // wait, turning a passed deadline into the kernel's stop flag
     for (;;) {
       const hipError_t e = hipStreamQuery(s);

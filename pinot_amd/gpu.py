@@ -314,16 +314,16 @@ class GpuEngine:
         int64[G, A] and, with value sets, distinct offsets uint64[G * A + 1] / ids uint32[num_distinct]."""
         A, K, G = r.num_aggs, r.num_keys, r.num_groups
 
-        def copy(ptr, n, dt, shape):  # one bytes copy out of the library's buffer, viewed read-only (the cheapest
-            return np.frombuffer(C.string_at(ptr, n * np.dtype(dt).itemsize), dtype=dt).reshape(shape)  # ctypes path)
-        vals = copy(r.values, G * A, np.float64, (G, A)) if G and A else np.zeros((G, A))
-        cnts = copy(r.counts, G * A, np.int64, (G, A)) if G and A else np.zeros((G, A), dtype=np.int64)
-        keys = copy(r.keys, G * K, np.uint32, (G, K)) if G and K else np.zeros((G, K), dtype=np.uint32)
+        def copy(ptr, n, dt, size, shape):  # one bytes copy out of the library's buffer, viewed read-only (the
+            return np.frombuffer(C.string_at(ptr, n * size), dtype=dt).reshape(shape)  # cheapest ctypes path)
+        vals = copy(r.values, G * A, np.float64, 8, (G, A)) if G and A else np.zeros((G, A))
+        cnts = copy(r.counts, G * A, np.int64, 8, (G, A)) if G and A else np.zeros((G, A), dtype=np.int64)
+        keys = copy(r.keys, G * K, np.uint32, 4, (G, K)) if G and K else np.zeros((G, K), dtype=np.uint32)
         offs = ids = None
         if r.distinct_offsets:
-            offs = copy(r.distinct_offsets, G * A + 1, np.uint64, (G * A + 1,))
+            offs = copy(r.distinct_offsets, G * A + 1, np.uint64, 8, (G * A + 1,))
             nd = int(r.num_distinct)
-            ids = copy(r.distinct_ids, nd, np.uint32, (nd,)) if nd else np.zeros(0, dtype=np.uint32)
+            ids = copy(r.distinct_ids, nd, np.uint32, 4, (nd,)) if nd else np.zeros(0, dtype=np.uint32)
         s = r.stats
         stats = np.array([s.num_docs_scanned, s.num_entries_scanned_in_filter, s.num_entries_scanned_post_filter,
                           s.num_total_docs, s.num_segments_processed, s.num_segments_matched], dtype=np.int64)
