@@ -194,7 +194,7 @@ class GpuEngine:
         res = C.POINTER(abi.pg_result)()
         if image:
             im = plan.image()
-            check(self.lib.pg_execute_image(im.ctypes.data, im.size, C.byref(res)))
+            check(self.lib.pg_execute_image(plan.image_addr, im.size, C.byref(res)))
         else:
             check(self.lib.pg_execute(C.byref(plan.plan), C.byref(res)))
         try:
@@ -207,14 +207,14 @@ class GpuEngine:
         p = C.POINTER(abi.pg_partials)()
         if image:
             im = plan.image()
-            check(self.lib.pg_execute_partial_image(im.ctypes.data, im.size, C.byref(p)))
+            check(self.lib.pg_execute_partial_image(plan.image_addr, im.size, C.byref(p)))
         else:
             check(self.lib.pg_execute_partial(C.byref(plan.plan), C.byref(p)))
         return p
 
     def _finalize(self, plan: CPlan, p, res):
         im = plan.image()
-        check(self.lib.pg_partials_finalize_image(p, im.ctypes.data, im.size, C.byref(res)))
+        check(self.lib.pg_partials_finalize_image(p, plan.image_addr, im.size, C.byref(res)))
 
     def finalize_partial(self, plan: CPlan, p, free: bool = True) -> IntermediateResult:
         res = C.POINTER(abi.pg_result)()

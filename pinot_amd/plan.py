@@ -765,6 +765,7 @@ class CPlan:
         if self._image is None:
             self._image = abi.build_image(self.plan)
             self._image_header = abi.pg_image_header.from_buffer(self._image)
+            self.image_addr = self._image.ctypes.data  # stable while _image lives (ndarray.ctypes costs ~3 us a call)
         h, p = self._image_header, self.plan  # the per-call scalars a caller may set on the plan (cancel id, deadline)
         h.query_id, h.deadline_ms, h.flags, h.limit = p.query_id, p.deadline_ms, p.flags, p.limit
         h.num_groups_limit = p.num_groups_limit
