@@ -580,6 +580,20 @@ def test_empty_and_all_filtered(gpu_engine, oracle_engine):
         assert g.stats.num_docs_scanned == 0
 
 
+def test_no_segments(gpu_engine, oracle_engine):
+    """A query over an empty segment list (a server whose segments were all pruned): the readback of the match
+    counts / error word and the small final state still runs (one launch into mapped host memory), stats all zero."""
+    rng = np.random.default_rng(3)
+    seg = _seg("z", {"a": rng.integers(0, 10, 3000), "b": rng.integers(0, 100, 3000)}, {"a": "INT", "b": "INT"})
+    t = Table("t", [seg])
+    for sql in ["SELECT COUNT(*), SUM(b), MIN(b), MAX(b) FROM t WHERE a > 3",
+                "SELECT a, SUM(b) FROM t WHERE b < 50 GROUP BY a"]:
+        q = parse(sql)
+        g, o = gpu_engine.execute(t, q, segments=[]), oracle_engine.execute(t, q, segments=[])
+        assert_same_result(g, o, table=t)
+        assert g.stats.num_docs_scanned == 0 and g.stats.num_segments_processed == 0
+
+
 def test_per_segment_dictionaries_merge_by_value(gpu_engine, oracle_engine):
     """dictIds are segment-local: different value sets per segment still merge by VALUE (IndexedTable keys)."""
     rng = np.random.default_rng(2)
