@@ -8,8 +8,10 @@ Workloads (`--workload`; the default is the headline metric):
   ssb          config 3: SSB Q1.1 shape, SUM(lo_extendedprice * lo_discount) under 3 dictionary filters -- 96 segments
                per GPU (768 over 8 GPUs = 6 B rows)
   highcard     config 4: SELECT userId, DISTINCTCOUNT(itemId) ... GROUP BY userId ORDER BY DISTINCTCOUNT(itemId) DESC,
-               userId LIMIT 100 (10 M users x 1 000 items, numGroupsLimit 10 M) -- 128 segments per GPU; the step
-               returns the server's 5 000 top groups (GroupByOrderByCombineOperator's trim size)
+               userId LIMIT 100 (10 M users x 1 000 items) -- 128 segments per GPU, under the server instance config
+               SURVEY §8(d) prescribes for the reference: num.groups.limit 10 M (no per-segment truncation) and
+               groupby.trim.threshold = MAX_TRIM_THRESHOLD (no lossy resize during the combine); the step returns the
+               server's result, the top getTableCapacity(100, 5 000) = 5 000 groups with their value sets
   index        config 5: COUNT(*), COUNTMV(mvTags) under a sorted-index range, an OR of two inverted-index leaves, an
                inverted NOT_EQ and an inverted IN -- 32 segments per GPU (256 over 8 GPUs = 2 B rows)
 
@@ -35,6 +37,8 @@ profiles/traffic_<workload>.json, used only when it was measured on this very li
 children on the survivors only, projection of the matching docs, aggregation) over min(#segments, 128, cores) of the
 same segments, at Pinot's default combine parallelism (CombineOperatorUtils.java:38-50) and at one thread per segment up
 to every core this process may use; rank 0 at N = 1 only.
+`parity_full`: the last timed step's result itself (same plan, flags and trim) against the oracle over EVERY segment of
+the line (the server's combined result under the same instance config); `parity_sample` re-plans 16 segments.
 `--split-table`: the workload's table (128 segments for config 2 / 4) divided over the N ranks (16 per GPU
 at N = 8): strong scaling of the 1 B-row query.
 """
@@ -57,10 +61,12 @@ HEADLINE_METRIC = "rows/sec for filter+group-by SUM over 1B rows; % of HBM roofl
 
 def workloads(args):
     """`trim`: "server" = the group-by result a Pinot server returns (GroupByOrderByCombineOperator: the top
-    getTableCapacity(limit, 5 000) groups under the ORDER BY).  `stages`: the executed plan's read pattern, in evaluation order: (filter the docs passed so far, or None = every
+    getTableCapacity(limit, 5 000) groups under the ORDER BY).  `config`: the server instance's settings
+    (InstanceConfig; default = InstancePlanMakerImplV2's defaults).  `stages`: the executed plan's read pattern, in evaluation order: (filter the docs passed so far, or None = every
     doc; [(column, "ids" | "values")] read for those docs).  "ids" = the packed dictIds; "values" = what an aggregation /
     key reads (the decoded value image of a large non-identity dictionary, else the dictIds)."""
     from pinot_amd import synth
+    from pinot_amd.plan import MAX_TRIM_THRESHOLD, InstanceConfig
     ids = ", ".join(str((i * 7919 + 13) % 1_000_000) for i in range(args.in_ids))
     return {
         "adanalytics": dict(
@@ -84,7 +90,8 @@ def workloads(args):
                     ("*", [("lo_extendedprice", "values")])]),
         "highcard": dict(
             specs=synth.HIGHCARD, table="events", segments=128, trim="server", flags="VALUE_SETS",
-            query=synth.highcard_query() + " OPTION(numGroupsLimit=10000000)", decoded=("userId", "itemId"),
+            query=synth.highcard_query(), decoded=("userId", "itemId"),
+            config=InstanceConfig(num_groups_limit=10_000_000, groupby_trim_threshold=MAX_TRIM_THRESHOLD),
             metric="rows/sec for high-cardinality group-by DISTINCTCOUNT (config 4, secondary line)",
             desc="config 4: SELECT userId, DISTINCTCOUNT(itemId) GROUP BY userId (10 M users x 1 000 items) "
                  "ORDER BY DISTINCTCOUNT(itemId) DESC, userId LIMIT 100, numGroupsLimit 10 M",
@@ -154,6 +161,41 @@ def index_plan_bytes(eng, table, plan, index_meta, rows, sql):
     return total, alg, [in_range, matched]
 
 
+def full_parity(W, q, res, host_all, cfg, threads) -> bool:
+    """The timed plan's own result (`res`: same flags, trim and instance config) against the oracle over every segment
+    of the line: the server's combined result (GroupByOrderByCombineOperator / AggregationOnlyCombineOperator under
+    `cfg`), rows and docs scanned.  Config 4 (~10 M users with value sets): the oracle's per-segment (user, item) pairs
+    merged by value in a bitmap of every (user, item), then the server's top getTableCapacity rows under the ORDER BY
+    with their item sets."""
+    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle.oracle import OracleEngine
+    from pinot_amd.plan import CPlan, Table, group_trim
+    orc = OracleEngine(threads=threads)
+    table = Table(W["table"], host_all)
+    if W["table"] != "events":
+        o = orc.execute(table, q, server=W["trim"] == "server", config=cfg)
+        return bool(res.rows == o.rows and res.stats.num_docs_scanned == o.stats.num_docs_scanned)
+    cp = CPlan(table, q, host_all, list(range(1, len(host_all) + 1)), config=cfg)
+    users_card = table.key_space("userId")
+    items = table.key_space("itemId")
+    from pinot_amd import abi
+    assert users_card.kind == items.kind == abi.PG_KEY_VALUE_OFFSET
+    ub, ib = users_card.base, items.base
+    seen = np.zeros((users_card.cardinality, items.cardinality), dtype=bool)
+    with ThreadPoolExecutor(threads) as ex:
+        for u, v in ex.map(lambda i: orc.distinct_pairs(cp, i, host_all[i]), range(len(host_all))):
+            seen[u - ub, v - ib] = True
+    counts = seen.sum(axis=1)
+    users = np.nonzero(counts)[0]
+    size = group_trim(q, cfg).server_size
+    top = users[np.lexsort((users, -counts[users]))[:size]]
+    want = {(int(x + ub),): {int(i + ib) for i in np.nonzero(seen[x])[0]} for x in top}
+    got = res.rows
+    return bool(got.keys() == want.keys() and all(got[k][0] == want[k] for k in want) and
+                res.stats.num_docs_scanned == sum(sg.num_docs for sg in host_all))
+
+
 def lib_md5():
     from pinot_amd import gpu
     with open(gpu.LIB_PATH, "rb") as f:
@@ -196,6 +238,8 @@ def main():
     ap.add_argument("--cpu-sample-segments", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="per CPU leg")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-full-parity", action="store_true",
+                    help="skip the oracle check of the timed result over every segment (parity_full)")
     ap.add_argument("--traffic-file", default=None, help="PMC HBM traffic of the hot-path kernels (tools/profile_bench.sh)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -244,7 +288,7 @@ def main():
     nproc = os.cpu_count()
     pinot_threads = max(1, min(10, cores // 2))  # CombineOperatorUtils.MAX_NUM_THREADS_PER_QUERY on this host
     n_sample = min(args.segments, args.cpu_sample_segments or max(16, min(128, cores)))
-    segs, host_sample = [], []
+    segs, host_all = [], []  # host copies of every segment (rank 0, N = 1): the CPU leg's sample and the full parity
     t_gen = time.time()
     fwd_bytes = dict_bytes = 0
     widths = {}  # column -> [(bits of dictIds, bits of values)] per segment
@@ -268,8 +312,8 @@ def main():
             index_meta.append({dc.spec.name: (dc.inv_be[:4 * (dc.cardinality + 1)].cpu().numpy().view(">u4")
                                               .astype(np.int64) if dc.inv_be is not None else None,
                                               dc.cardinality, dc.num_values) for dc in dcs})
-        if want_cpu and s < n_sample:
-            host_sample.append(ImmutableSegment(seg.name, args.rows, {dc.spec.name: dc.host_column() for dc in dcs}))
+        if want_cpu and (s < n_sample or not args.no_full_parity):
+            host_all.append(ImmutableSegment(seg.name, args.rows, {dc.spec.name: dc.host_column() for dc in dcs}))
         del dcs
     torch.cuda.synchronize()
     table = Table(W["table"], segs)
@@ -280,7 +324,8 @@ def main():
     # config 4's server result carries the DISTINCTCOUNT intermediate as the reference's Set of values per kept group
     # (what GroupByOrderByCombineOperator hands the broker); the other workloads have no DISTINCTCOUNT
     flags = abi.PG_PLAN_VALUE_SETS if W.get("flags") == "VALUE_SETS" else 0
-    plan = eng.make_plan(table, q, flags=flags, trim=W["trim"])
+    cfg = W.get("config")
+    plan = eng.make_plan(table, q, flags=flags, trim=W["trim"], config=cfg)
     lowering_ms = (time.perf_counter() - t_low) * 1e3
     if world > 1:
         for ks in plan.key_spaces:  # packed keys merge across ranks only over identical key spaces
@@ -355,14 +400,15 @@ def main():
     achieved = plan_bytes / (scan_avg_ms * 1e-3) / 1e9
     alg_achieved = alg_bytes / (scan_avg_ms * 1e-3) / 1e9
 
-    cpu = parity = None
+    cpu = parity = parity_full = None
+    host_sample = host_all[:n_sample]
     if want_cpu and host_sample:
         from oracle.oracle import OracleEngine
         from pinot_amd.plan import CPlan
         ht = Table(W["table"], host_sample)
         hq = parse(W["query"])
         orc = OracleEngine()
-        cplan = CPlan(ht, hq, host_sample, list(range(1, len(host_sample) + 1)))
+        cplan = CPlan(ht, hq, host_sample, list(range(1, len(host_sample) + 1)), config=cfg)
         legs = {}
         for name, threads in (("pinot_default", min(len(host_sample), pinot_threads)),
                               ("all_cores", min(len(host_sample), cores))):
@@ -378,20 +424,24 @@ def main():
                "legs": legs, "nproc": nproc, "cores_available": cores, "cpu_model": cpu_model()}
         if W["table"] != "events":  # parity on up to 16 sampled segments (value-keyed merge in Python)
             ps = host_sample[:16]
-            o = orc.execute(Table(W["table"], ps), hq)
-            d = eng.run_plan(eng.make_plan(table, q, segments=segs[:len(ps)], flags=0))
+            o = orc.execute(Table(W["table"], ps), hq, config=cfg)
+            d = eng.run_plan(eng.make_plan(table, q, segments=segs[:len(ps)], flags=0, config=cfg))
             parity = bool(d.rows == o.rows and d.stats.num_docs_scanned == o.stats.num_docs_scanned)
         else:  # config 4 on 2 full segments: the oracle's per-segment value sets merged by value (numpy), top rows
             from pinot_amd.plan import reduce_to_rows
             ps = host_sample[:2]
-            pp = CPlan(Table(W["table"], ps), hq, ps, [1, 2])
+            pp = CPlan(Table(W["table"], ps), hq, ps, [1, 2], config=cfg)
             pk, pv = zip(*(orc.distinct_pairs(pp, i, sg) for i, sg in enumerate(ps)))
             pair = np.unique(np.concatenate(pk) * (1 << 20) + np.concatenate(pv))
             users, counts = np.unique(pair >> 20, return_counts=True)
             top = np.lexsort((users, -counts))[:q.limit]
             want = [[int(users[i]), int(counts[i])] for i in top]
-            d = eng.run_plan(eng.make_plan(table, q, segments=segs[:2], flags=0, trim=True))
+            d = eng.run_plan(eng.make_plan(table, q, segments=segs[:2], flags=0, trim=True, config=cfg))
             parity = bool(reduce_to_rows(q, d)[1] == want)
+        if not args.no_full_parity and len(host_all) == args.segments:
+            t_par = time.perf_counter()
+            parity_full = full_parity(W, q, res, host_all, cfg, min(cores, 64))
+            parity_full_s = time.perf_counter() - t_par
 
     traffic = traffic_bytes = None
     traffic_note = None
@@ -430,6 +480,10 @@ def main():
                          "traffic_frac": traffic / HBM_PEAK_GBS if traffic is not None else None,
                          "traffic_note": traffic_note},
             "cpu_baseline": cpu,
+            "parity_full": parity_full,
+            "parity_full_scope": None if parity_full is None else
+            f"the last timed step's result vs the oracle over all {args.segments} segments "
+            f"({round(parity_full_s, 1)} s)",
             "parity_sample": parity,
             "step_breakdown_ms": {k: round(float(np.mean(v)), 4) for k, v in parts.items()},
             "host_plan_lowering_ms": round(lowering_ms, 3),

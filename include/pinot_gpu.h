@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 6
+#define PG_ABI_VERSION 7
 
 typedef enum pg_status {
   PG_OK = 0,
@@ -208,7 +208,15 @@ typedef struct pg_agg {
   uint32_t key_kind;
   uint32_t key_cardinality;
   int64_t key_base;
+  /* SUM / AVG accumulated exactly in fixed point (every input that is not provably an integer, or all of them with
+   * PG_PLAN_F64_SUMS): e != 0 states 2^e >= |every finite input value| over the whole table (from the columns'
+   * metadata min / max), so every GPU and server that merges this plan's partial states uses the same fixed-point
+   * unit; 0 = derive the bound from the plan's resident segments.  Ignored by the other functions. */
+  int32_t sum_exp;
+  uint32_t sum_flags;  /* SUM / AVG: PG_SUM_NONFINITE = some input of the table may be +-inf / NaN (a FLOAT / DOUBLE column
+                          holding them, or a product / sum that overflows), so every GPU keeps the same slots for them */
 } pg_agg;
+#define PG_SUM_NONFINITE 0x1u
 
 typedef enum pg_key_kind {
   PG_KEY_VALUE_OFFSET = 0,  /* INT/LONG dictionary: global id = value - base                         */
@@ -246,9 +254,11 @@ typedef struct pg_order {
                                     DistinctCountAggregationFunction.java:252-310), not only their sizes */
 #define PG_PLAN_HASH_GROUPS 0x2u /* group in a hash table even when the key space is small enough to address
                                     directly (same results; for tests and measurements) */
-#define PG_PLAN_F64_SUMS 0x4u    /* accumulate every SUM / AVG in double, as the reference does, instead of
-                                    integer-exact int64 for integer inputs; use when partial states of servers
-                                    or GPUs whose columns differ in range must merge (pg_partials.layout) */
+#define PG_PLAN_F64_SUMS 0x4u    /* accumulate every SUM / AVG as an exact 128-bit fixed-point sum (as the sums of
+                                    non-integer inputs always are) instead of integer-exact int64 for integer
+                                    inputs: the reference's double SUM, rounded once at the end; use when partial
+                                    states of servers or GPUs whose columns differ in range must merge
+                                    (pg_partials.layout) */
 #define PG_PLAN_NO_STREAM 0x8u   /* never use the selective stream (a lean kernel over the root AND's first,
                                     selective scan leaf + the fused scan over its survivors); same results */
 #define PG_PLAN_EXACT_LIMIT 0x10u /* keep exactly min(limit, #groups) groups: the first `limit` of the result order
@@ -284,6 +294,13 @@ typedef struct pg_plan {
                                the ORDER BY (every group tied with the limit-th is kept too, so any tie-break
                                the caller applies stays exact -- or exactly `limit` with PG_PLAN_EXACT_LIMIT,
                                which also applies without ORDER BY); 0 = keep all groups */
+  uint64_t trim_threshold;  /* the server's IndexedTable trimThreshold (InstancePlanMakerImplV2 groupby.trim.threshold,
+                               GroupByOrderByCombineOperator.java:79-93) for a group-by with ORDER BY and the server trim
+                               on; 0 = none.  The reference's ConcurrentIndexedTable resizes to min(trimSize,
+                               threshold / 2) records whenever it holds >= threshold of them during the merge
+                               (ConcurrentIndexedTable.java:61-65, IndexedTable.java:77-80): a lossy, schedule-dependent
+                               answer.  The device merges every group exactly and reports it:
+                               PG_RESULT_TRIM_THRESHOLD_REACHED. */
 } pg_plan;
 
 /* ---------------------------------------------------------------- results */
@@ -307,6 +324,11 @@ typedef struct pg_stats {     /* ExecutionStatistics, summed over the plan's seg
  *   distinct_ids[distinct_offsets[g*num_aggs + a] .. distinct_offsets[g*num_aggs + a + 1]),
  * table-global value ids (the aggregation's key space) in ascending order; other aggregations have empty
  * ranges.  Without the flag both pointers are NULL. */
+#define PG_RESULT_GROUPS_LIMIT_REACHED 0x1u  /* some segment reached num_groups_limit groups (its later keys dropped):
+                                                IntermediateResultsBlock.isNumGroupsLimitReached, set as
+                                                AggregationGroupByOrderByOperator.java:112-113 does */
+#define PG_RESULT_TRIM_THRESHOLD_REACHED 0x2u /* the merged groups reached the plan's trim_threshold: the reference
+                                                server would have resized its table mid-merge (numResizes > 0) */
 typedef struct pg_result {
   pg_stats stats;
   uint64_t num_groups;
@@ -318,6 +340,9 @@ typedef struct pg_result {
   uint64_t num_distinct;
   uint64_t *distinct_offsets;
   uint32_t *distinct_ids;
+  uint64_t num_groups_merged; /* groups of the merged (combined) table before the ORDER BY / limit trim */
+  uint32_t flags;             /* PG_RESULT_* */
+  uint32_t pad;
 } pg_result;
 
 int pg_execute(const pg_plan *plan, pg_result **out);
@@ -335,7 +360,9 @@ int pg_result_free(pg_result *res);
  *                        PG_EMPTY_KEY (IntGroupIdMap / Long2IntOpenHashMap on the device).
  * State arrays, per slot:
  *   i64 [num_slots][n_i64]      merged by SUM (slot 0: doc count; integer sums, AVG counts, COUNTMV)
- *   f64 [num_slots][n_f64]      merged by SUM (floating-point sums)
+ *   fx  [num_slots][n_fx][2]    merged by 128-bit SUM: the exact fixed-point sums of SUM / AVG inputs that are not
+ *                               provably integers, (lo, hi) two's-complement words (the low word's carry goes to the
+ *                               high word: a word-wise SUM all-reduce is NOT a merge -- split the words into limbs)
  *   mn  [num_slots][n_min]      merged by MIN (order-preserving int64 image of double MIN)
  *   mx  [num_slots][n_max]      merged by MAX (order-preserving int64 image of double MAX)
  *   bitmaps [num_slots][bitmap_words] merged by OR: per DISTINCTCOUNT aggregation a bitmap over its
@@ -349,19 +376,21 @@ typedef struct pg_partials {
   pg_stats stats;
   uint64_t num_slots;
   uint32_t mode;            /* PG_STATE_* */
-  uint32_t n_i64, n_f64, n_min, n_max;
+  uint32_t n_i64, n_fx, n_min, n_max;
   uint32_t bitmap_words;    /* uint32 words of DISTINCTCOUNT bitmaps per slot */
-  uint32_t layout;          /* bit a: SUM / AVG aggregation a accumulates integer-exact in i64 (else f64); partial
+  uint32_t layout;          /* bit a: SUM / AVG aggregation a accumulates integer-exact in i64 (else in fx); partial
                                states merge only with equal layouts */
-  uint32_t pad;
+  uint32_t fx_sig;          /* signature of the fx sums' fixed-point units: partial states merge only when it agrees */
   uint64_t row_bytes;       /* bytes of one exchange row (pg_partials_export) */
   uint64_t *keys;
   int64_t *i64;
-  double *f64;
+  int64_t *fx;
   int64_t *mn;
   int64_t *mx;
   uint32_t *bitmaps;
   void *impl;
+  uint32_t flags;           /* PG_RESULT_* seen producing this state (the caller ORs the ranks' flags before finalize) */
+  uint32_t pad;
 } pg_partials;
 
 int pg_execute_partial(const pg_plan *plan, pg_partials **out);
@@ -371,14 +400,16 @@ int pg_execute_partial(const pg_plan *plan, pg_partials **out);
 int pg_partials_finalize(pg_partials *p, const pg_plan *plan, pg_result **out);
 int pg_partials_free(pg_partials *p);
 /* Dense merge: copy the state arrays out to (PG_COPY_OUT) or back in from (PG_COPY_IN) caller-owned DEVICE
- * buffers of the same sizes (e.g. torch tensors the ranks all-reduce over RCCL: SUM for i64 / f64, MIN for mn,
- * MAX for mx).  Bitmaps are not all-reducible (OR): plans with DISTINCTCOUNT use the row exchange below.  A NULL
+ * buffers (e.g. torch tensors the ranks all-reduce over RCCL: SUM for i64, MIN for mn, MAX for mx).  i64 / mn / mx keep
+ * their layout and size; fx travels as 4 int64 limbs per sum (num_slots * n_fx * 4 words: limb k = bits [32k, 32k+32)
+ * of the 128-bit pair), so a plain SUM all-reduce over up to 2^31 ranks merges it exactly -- PG_COPY_IN folds the
+ * limbs' carries back into the pairs.  Bitmaps are not all-reducible (OR): plans with DISTINCTCOUNT use the row exchange below.  A NULL
  * pointer skips that array.  `stream` NULL = the library's per-thread stream; synchronous. */
 #define PG_COPY_OUT 0
 #define PG_COPY_IN 1
-int pg_partials_copy(pg_partials *p, int dir, void *i64, void *f64, void *mn, void *mx, void *stream);
+int pg_partials_copy(pg_partials *p, int dir, void *i64, void *fx, void *mn, void *mx, void *stream);
 /* Sparse merge (GroupByOrderByCombineOperator's value-keyed merge across GPUs): the groups of `p` as rows
- *   { u64 packed key | i64[n_i64] | f64[n_f64] | i64 mn[n_min] | i64 mx[n_max] | u32 bitmaps[bitmap_words] }
+ *   { u64 packed key | i64[n_i64] | i64 fx[n_fx][2] | i64 mn[n_min] | i64 mx[n_max] | u32 bitmaps[bitmap_words] }
  * (row_bytes each, 8-byte aligned), bucketed by owner part = pg_key_owner(key, num_parts), buckets in part order.
  * part_counts[num_parts] (host) receives the rows per bucket.  dst (DEVICE, dst_rows rows) may be NULL to only
  * count.  Synchronous on `stream`. */
@@ -420,7 +451,7 @@ typedef struct pg_image_header {
   uint32_t num_keys;
   uint32_t num_order;
   uint32_t flags;           /* PG_PLAN_* */
-  uint32_t pad;
+  uint32_t trim_threshold;  /* pg_plan.trim_threshold (an int on the reference's side) */
   uint64_t num_groups_limit;
   uint64_t query_id;
   int64_t deadline_ms;

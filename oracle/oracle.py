@@ -22,9 +22,8 @@ import numpy as np
 
 from pinot_amd import abi
 from pinot_amd.segment import _NP_BE
-from pinot_amd.plan import (CPlan, DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY, ExecutionStats, IntermediateResult,
-                            Table, default_row, execute_filtered, final_value, group_trim, has_filtered_aggregations,
-                            merge_intermediate)
+from pinot_amd.plan import (MAX_TRIM_THRESHOLD, CPlan, ExecutionStats, IntermediateResult, Table, default_row,
+                            execute_filtered, final_value, group_trim, has_filtered_aggregations, merge_intermediate)
 from pinot_amd.query import QueryContext, parse
 from pinot_amd.segment import ImmutableSegment
 
@@ -115,11 +114,16 @@ class _SegmentColumns:
 class OracleEngine:
     """Runs plans on the CPU restatement.  `threads` parallelises over segments (ctypes drops the GIL)."""
 
-    def __init__(self, threads: int = 1, array_based_threshold: int = DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY):
+    def __init__(self, threads: int = 1):
         self.lib = load()
         self.threads = threads
-        self.array_based_threshold = array_based_threshold
         self._cols = {}
+
+    @staticmethod
+    def _array_threshold(plan: CPlan) -> int:
+        """DictionaryBasedGroupKeyGenerator's array-based holder bound: the instance's maxInitialResultHolderCapacity
+        (<= its numGroupsLimit, InstancePlanMakerImplV2.java:138-140)."""
+        return min(plan.config.max_init_group_holder_capacity, plan.config.num_groups_limit)
 
     def columns(self, seg, table):
         k = (id(seg), id(table))
@@ -130,10 +134,7 @@ class OracleEngine:
     def run_segment(self, plan: CPlan, si: int, seg: ImmutableSegment):
         cols = self.columns(seg, plan.table)
         out = C.POINTER(orc_segment_result)()
-        # InstancePlanMakerImplV2 keeps maxInitialResultHolderCapacity <= numGroupsLimit
-        # (DictionaryBasedGroupKeyGenerator asserts numGroupsLimit >= arrayBasedThreshold, :102)
-        threshold = min(self.array_based_threshold, plan.plan.num_groups_limit or self.array_based_threshold)
-        rc = self.lib.orc_execute_segment(C.byref(plan.plan), si, cols.arr, threshold, C.byref(out))
+        rc = self.lib.orc_execute_segment(C.byref(plan.plan), si, cols.arr, self._array_threshold(plan), C.byref(out))
         if rc:
             raise RuntimeError(f"oracle failed rc={rc}")
         try:
@@ -147,8 +148,7 @@ class OracleEngine:
         caller can merge many segments by value without a Python object per group."""
         cols = self.columns(seg, plan.table)
         out = C.POINTER(orc_segment_result)()
-        threshold = min(self.array_based_threshold, plan.plan.num_groups_limit or self.array_based_threshold)
-        if self.lib.orc_execute_segment(C.byref(plan.plan), si, cols.arr, threshold, C.byref(out)):
+        if self.lib.orc_execute_segment(C.byref(plan.plan), si, cols.arr, self._array_threshold(plan), C.byref(out)):
             raise RuntimeError("oracle failed")
         try:
             r = out.contents
@@ -167,7 +167,7 @@ class OracleEngine:
         segment, C, `threads` segments in flight as Pinot's combine worker tasks run them; the value-keyed merge is
         excluded).  Runs the whole segment list repeatedly for at least `seconds`; returns (rows/s, runs)."""
         cols = [self.columns(s, plan.table) for s in segments]
-        threshold = min(self.array_based_threshold, plan.plan.num_groups_limit or self.array_based_threshold)
+        threshold = self._array_threshold(plan)
 
         def one(i):
             out = C.POINTER(orc_segment_result)()
@@ -228,15 +228,16 @@ class OracleEngine:
         return rows, st
 
     def execute(self, table: Table, query, segments: Optional[Sequence[ImmutableSegment]] = None,
-                num_groups_limit=None, server: bool = False, config=None) -> IntermediateResult:
-        """server=True: the reference server's combined result -- the per-segment trim when minSegmentGroupTrimSize
-        is on, the IndexedTable's result size (group_trim) -- instead of every merged group."""
+                server: bool = False, config=None) -> IntermediateResult:
+        """config: the server instance's settings (InstanceConfig: numGroupsLimit, maxInitialResultHolderCapacity, trim
+        sizes / threshold).  server=True: the reference server's combined result -- the per-segment trim when
+        minSegmentGroupTrimSize is on, the IndexedTable's result size (group_trim) -- instead of every merged group."""
         if isinstance(query, str):
             query = parse(query)
         if has_filtered_aggregations(query):  # FilteredAggregationOperator.java:70-98: one plan per filter
-            return execute_filtered(lambda q: self.execute(table, q, segments, num_groups_limit), query)
+            return execute_filtered(lambda q: self.execute(table, q, segments, config=config), query)
         segments = list(table.segments if segments is None else segments)
-        plan = CPlan(table, query, segments, list(range(1, len(segments) + 1)), num_groups_limit)
+        plan = CPlan(table, query, segments, list(range(1, len(segments) + 1)), config=config)
         trim = group_trim(query, config) if server and query.group_by else None
         return self.run_plan(plan, segments, trim)
 
@@ -249,6 +250,9 @@ class OracleEngine:
         q = plan.query
         merged = {}
         stats = ExecutionStats()
+        limit = plan.config.num_groups_limit
+        # AggregationGroupByOrderByOperator.java:112-113: numGroupsLimitReached when a segment's generator holds >= limit
+        limit_reached = bool(q.group_by) and any(len(rows) >= limit for rows, _ in parts)
         closed = False  # IndexedTable without ORDER BY: no new keys once it holds resultSize (ConcurrentIndexedTable:76-86)
         for rows, st in parts:
             if trim is not None and trim.segment_size is not None and len(rows) > trim.segment_size:
@@ -262,11 +266,18 @@ class OracleEngine:
                         len(merged) >= trim.server_size
             for f in stats.__dataclass_fields__:
                 setattr(stats, f, getattr(stats, f) + getattr(st, f))
+        n_merged = len(merged)
+        # ConcurrentIndexedTable.upsertWithOrderBy (:61-65) resizes whenever the map holds >= trimThreshold records;
+        # until its first resize the map holds every merged key, so it resizes iff the merged keys reach the threshold
+        # (the resize itself is lossy and depends on thread scheduling: it is reported, not reproduced)
+        resized = trim is not None and trim.ordered and trim.server_size is not None and \
+            trim.threshold < MAX_TRIM_THRESHOLD and n_merged >= trim.threshold
         if trim is not None and trim.ordered and trim.server_size is not None and len(merged) > trim.server_size:
             merged = resizer_top(q, plan.aggs, merged, trim.server_size)  # IndexedTable.finish
         if not q.group_by and () not in merged:
             merged[()] = default_row(plan.aggs)
-        return IntermediateResult(plan.aggs, list(q.group_by), merged, stats)
+        return IntermediateResult(plan.aggs, list(q.group_by), merged, stats, limit_reached, resized,
+                                  n_merged if q.group_by else None)
 
 
 class _Rec:

@@ -1,7 +1,7 @@
 """ctypes mirror of include/pinot_gpu.h (the C ABI).  Shared by the GPU binding and the oracle."""
 import ctypes as C
 
-PG_ABI_VERSION = 6
+PG_ABI_VERSION = 7
 
 PG_OK, PG_E_INVALID, PG_E_HIP, PG_E_NOMEM, PG_E_NOTFOUND, PG_E_UNSUPPORTED, PG_E_CANCELLED, PG_E_TIMEOUT, \
     PG_E_STATE = 0, -1, -2, -3, -4, -5, -6, -7, -8
@@ -37,6 +37,8 @@ PG_ORDER_AGG, PG_ORDER_KEY = 0, 1
 PG_PLAN_VALUE_SETS, PG_PLAN_HASH_GROUPS, PG_PLAN_F64_SUMS, PG_PLAN_NO_STREAM = 0x1, 0x2, 0x4, 0x8
 PG_PLAN_EXACT_LIMIT = 0x10
 PG_STATE_DENSE, PG_STATE_HASH = 0, 1
+PG_RESULT_GROUPS_LIMIT_REACHED, PG_RESULT_TRIM_THRESHOLD_REACHED = 0x1, 0x2
+PG_SUM_NONFINITE = 0x1
 PG_EMPTY_KEY = 0xFFFFFFFFFFFFFFFF
 
 
@@ -56,7 +58,8 @@ class pg_leaf(C.Structure):
 
 class pg_agg(C.Structure):
     _fields_ = [("fn", C.c_uint32), ("op", C.c_uint32), ("col_a", C.c_uint32), ("col_b", C.c_uint32),
-                ("key_kind", C.c_uint32), ("key_cardinality", C.c_uint32), ("key_base", C.c_int64)]
+                ("key_kind", C.c_uint32), ("key_cardinality", C.c_uint32), ("key_base", C.c_int64),
+                ("sum_exp", C.c_int32), ("sum_flags", C.c_uint32)]
 
 
 class pg_key(C.Structure):
@@ -79,7 +82,8 @@ class pg_plan(C.Structure):
                 ("num_aggs", C.c_uint32), ("num_keys", C.c_uint32), ("aggs", C.POINTER(pg_agg)),
                 ("keys", C.POINTER(pg_key)), ("num_groups_limit", C.c_uint64), ("query_id", C.c_uint64),
                 ("deadline_ms", C.c_int64), ("stream", C.c_void_p), ("flags", C.c_uint32),
-                ("num_order", C.c_uint32), ("order", C.POINTER(pg_order)), ("limit", C.c_uint64)]
+                ("num_order", C.c_uint32), ("order", C.POINTER(pg_order)), ("limit", C.c_uint64),
+                ("trim_threshold", C.c_uint64)]
 
 
 PG_IMAGE_MAGIC = 0x49504750
@@ -89,7 +93,7 @@ class pg_image_header(C.Structure):
     _fields_ = [("magic", C.c_uint32), ("abi_version", C.c_uint32), ("image_bytes", C.c_uint64),
                 ("num_segments", C.c_uint32), ("num_leaves", C.c_uint32), ("num_ops", C.c_uint32),
                 ("num_aggs", C.c_uint32), ("num_keys", C.c_uint32), ("num_order", C.c_uint32), ("flags", C.c_uint32),
-                ("pad", C.c_uint32), ("num_groups_limit", C.c_uint64), ("query_id", C.c_uint64),
+                ("trim_threshold", C.c_uint32), ("num_groups_limit", C.c_uint64), ("query_id", C.c_uint64),
                 ("deadline_ms", C.c_int64), ("limit", C.c_uint64), ("segments_off", C.c_uint64),
                 ("ops_off", C.c_uint64), ("aggs_off", C.c_uint64), ("keys_off", C.c_uint64), ("order_off", C.c_uint64)]
 
@@ -116,15 +120,16 @@ class pg_result(C.Structure):
     _fields_ = [("stats", pg_stats), ("num_groups", C.c_uint64), ("num_keys", C.c_uint32), ("num_aggs", C.c_uint32),
                 ("keys", C.POINTER(C.c_uint32)), ("values", C.POINTER(C.c_double)),
                 ("counts", C.POINTER(C.c_int64)), ("num_distinct", C.c_uint64),
-                ("distinct_offsets", C.POINTER(C.c_uint64)), ("distinct_ids", C.POINTER(C.c_uint32))]
+                ("distinct_offsets", C.POINTER(C.c_uint64)), ("distinct_ids", C.POINTER(C.c_uint32)),
+                ("num_groups_merged", C.c_uint64), ("flags", C.c_uint32), ("pad", C.c_uint32)]
 
 
 class pg_partials(C.Structure):
     _fields_ = [("stats", pg_stats), ("num_slots", C.c_uint64), ("mode", C.c_uint32), ("n_i64", C.c_uint32),
-                ("n_f64", C.c_uint32), ("n_min", C.c_uint32), ("n_max", C.c_uint32), ("bitmap_words", C.c_uint32),
-                ("layout", C.c_uint32), ("pad", C.c_uint32), ("row_bytes", C.c_uint64), ("keys", C.c_void_p),
-                ("i64", C.c_void_p), ("f64", C.c_void_p), ("mn", C.c_void_p), ("mx", C.c_void_p),
-                ("bitmaps", C.c_void_p), ("impl", C.c_void_p)]
+                ("n_fx", C.c_uint32), ("n_min", C.c_uint32), ("n_max", C.c_uint32), ("bitmap_words", C.c_uint32),
+                ("layout", C.c_uint32), ("fx_sig", C.c_uint32), ("row_bytes", C.c_uint64), ("keys", C.c_void_p),
+                ("i64", C.c_void_p), ("fx", C.c_void_p), ("mn", C.c_void_p), ("mx", C.c_void_p),
+                ("bitmaps", C.c_void_p), ("impl", C.c_void_p), ("flags", C.c_uint32), ("pad", C.c_uint32)]
 
 
 class pg_timing(C.Structure):
@@ -233,6 +238,7 @@ def build_image(plan: pg_plan) -> "np.ndarray":
     for f in ("num_segments", "num_leaves", "num_ops", "num_aggs", "num_keys", "num_order", "flags",
               "num_groups_limit", "query_id", "deadline_ms", "limit"):
         setattr(h, f, getattr(plan, f))
+    h.trim_threshold = min(plan.trim_threshold, 0xFFFFFFFF)
     h.ops_off = put(addr_of(plan.ops), 4 * plan.num_ops, 4)
     h.aggs_off = put(addr_of(plan.aggs), C.sizeof(pg_agg) * plan.num_aggs)
     h.keys_off = put(addr_of(plan.keys), C.sizeof(pg_key) * plan.num_keys)

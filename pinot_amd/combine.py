@@ -7,9 +7,11 @@ GroupByOrderByCombineOperator.processSegments -> IndexedTable.upsert (operator/c
 GPU); each GPU merges its own segments on device inside the fused scan (pg_execute_partial), and the ranks then merge
 their partial states over RCCL / xGMI in one of two ways:
 
-* dense all-reduce -- a small dense key space without DISTINCTCOUNT bitmaps: ONE collective per state array
-    i64 (doc counts, integer sums, AVG counts, COUNTMV) SUM, f64 SUM, mn (order-preserving int64 of MIN) MIN,
-    mx MAX, then every rank holds the merged state (config 2: 365 slots x 3 int64, latency-bound).
+* dense all-reduce -- a small dense key space without DISTINCTCOUNT bitmaps: ONE SUM all-reduce of i64 (doc counts,
+    integer sums, AVG counts, COUNTMV), the exact fixed-point sums as 32-bit limbs (pg_partials_copy) and the
+    statistics, then MIN / MAX all-reduces of the order-preserving images; every rank holds the merged state (config 2:
+    365 slots x 3 int64, latency-bound).  Double sums are exact integers in fixed point (SK_FX), so the merged sum has
+    the same bits for every run, every rank count and every collective algorithm.
 * row exchange -- hash states, large key spaces, DISTINCTCOUNT (bitmaps merge by OR, which RCCL cannot reduce):
     every rank exports its groups as rows bucketed by owner rank (pg_partials_export, owner = pg_key_owner(key)),
     the buckets go to their owners in one all_to_all, each owner inserts-and-merges what it received into a fresh
@@ -48,11 +50,10 @@ def _comm(t, group):
 
 
 def allreduce_state(state, group=None) -> None:
-    """In-place merge of a dense partial state across ranks: SUM of the integer state (and statistics), MIN / MAX of
-    the order-preserving images, and the double state summed in RANK ORDER on every rank (all_gather, then
-    ((r0 + r1) + r2) + ...): the same bits on every rank and in every run, whatever algorithm RCCL picks
-    (a fixed reduction order for reproducible double SUMs)."""
-    import torch
+    """In-place merge of a dense partial state across ranks: SUM of the integer words (i64 state, the exact sums'
+    32-bit limbs, statistics -- one buffer), MIN / MAX of the order-preserving images.  Every merge is an integer
+    operation, so the result is the same bits on every rank, in every run, whatever algorithm RCCL picks (SURVEY.md
+    §8(e): reproducible double SUMs)."""
     import torch.distributed as dist
     ops = {"i64": dist.ReduceOp.SUM, "mn": dist.ReduceOp.MIN, "mx": dist.ReduceOp.MAX, "stats": dist.ReduceOp.SUM}
     for name in ("i64", "mn", "mx", "stats"):
@@ -62,15 +63,6 @@ def allreduce_state(state, group=None) -> None:
             dist.all_reduce(c, op=ops[name], group=group)
             if c is not t:
                 t.copy_(c)
-    f = state.get("f64")
-    if f is not None and f.numel():
-        c = _comm(f, group)
-        parts = [torch.empty_like(c) for _ in range(dist.get_world_size(group))]
-        dist.all_gather(parts, c, group=group)
-        acc = parts[0].clone()
-        for x in parts[1:]:
-            acc += x
-        f.copy_(acc)
 
 
 def _all_gather_ints(vals, group, device):
@@ -83,56 +75,62 @@ def _all_gather_ints(vals, group, device):
     return [o.tolist() for o in out]
 
 
-def _layout_header(err, fp, group, dev):
-    """ONE fixed-size MAX all-reduce every step: [error flag | fingerprint | -fingerprint].  Every rank then holds the
-    same maxima and minima, so every rank takes the same decision (raise, dense all-reduce or row exchange) even when one
-    rank's state layout changed since the last step (a hash table regrown, a DENSE / HASH switch)."""
+_FLAG_BITS = (abi.PG_RESULT_GROUPS_LIMIT_REACHED, abi.PG_RESULT_TRIM_THRESHOLD_REACHED)
+
+
+def _layout_header(err, fp, flags, group, dev):
+    """ONE fixed-size MAX all-reduce every step: [error flag | result flag bits | fingerprint | -fingerprint].  Every
+    rank then holds the same maxima and minima, so every rank takes the same decision (raise, dense all-reduce or row
+    exchange) even when one rank's state layout changed since the last step (a hash table regrown, a DENSE / HASH
+    switch), and the OR of the ranks' PG_RESULT_* flags (the combined block's numGroupsLimitReached)."""
     import torch
     import torch.distributed as dist
-    v = [1 if err is not None else 0] + fp + [-x for x in fp]
+    v = [1 if err is not None else 0] + [1 if flags & b else 0 for b in _FLAG_BITS] + fp + [-x for x in fp]
     t = torch.tensor(v, dtype=torch.int64, device=dev)
     c = _comm(t, group)
     dist.all_reduce(c, op=dist.ReduceOp.MAX, group=group)
     h = c.tolist()
-    n = len(fp)
-    return h[0], h[1:1 + n], [-x for x in h[1 + n:]]
+    n, nb = len(fp), len(_FLAG_BITS)
+    merged_flags = sum(b for b, x in zip(_FLAG_BITS, h[1:1 + nb]) if x)
+    return h[0], merged_flags, h[1 + nb:1 + nb + n], [-x for x in h[1 + nb + n:]]
 
 
 def merge_partials_across_ranks(engine, plan, p, group=None) -> IntermediateResult:
     """pg_execute_partial result `p` (this rank) -> merged over the process group -> finalized result (every rank
     returns the same merged result).  Consumes `p`.
 
-    Per step: one MAX all-reduce of a fixed-size header (error flag + state-layout fingerprint, _layout_header), then
-    for dense states the i64 state and the six statistics in ONE SUM all-reduce (config 2: that is all), MIN / MAX
-    all-reduces for MIN / MAX states and an all_gather for double sums (summed in rank order); other states take the
-    row exchange."""
+    Per step: one MAX all-reduce of a fixed-size header (error flag, result flags, state-layout fingerprint,
+    _layout_header), then for dense states the i64 state, the exact sums' limbs and the six statistics in ONE SUM
+    all-reduce (config 2: that is all) and MIN / MAX all-reduces for MIN / MAX states; other states take the row
+    exchange."""
     import torch
     from .gpu import check
     pc = p.contents
     dev = torch.device("cuda", torch.cuda.current_device())
-    fp = [pc.mode, pc.num_slots, pc.n_i64, pc.n_f64, pc.n_min, pc.n_max, pc.bitmap_words, pc.layout]
+    fp = [pc.mode, pc.num_slots, pc.n_i64, pc.n_fx, pc.n_min, pc.n_max, pc.bitmap_words, pc.layout, pc.fx_sig]
     st_host = [getattr(pc.stats, f) for f in _STATS_FIELDS]
     n = pc.num_slots
     ni = n * pc.n_i64
+    nf = n * pc.n_fx * 4  # the exact sums as 32-bit limbs (pg_partials_copy)
     dense_mine = pc.mode == abi.PG_STATE_DENSE and pc.bitmap_words == 0 and \
-        n * 8 * (pc.n_i64 + pc.n_f64 + pc.n_min + pc.n_max) <= DENSE_ALLREDUCE_MAX_BYTES
+        n * 8 * (pc.n_i64 + 4 * pc.n_fx + pc.n_min + pc.n_max) <= DENSE_ALLREDUCE_MAX_BYTES
     err = state = sums = None
     ptr = lambda t: C.c_void_p(t.data_ptr()) if t.numel() else None
     if dense_mine:
         # the library's copies run on its own stream (torch carries its own HIP runtime, so streams do not cross) and
         # return once done
         try:
-            sums = torch.empty(ni + len(_STATS_FIELDS), dtype=torch.int64, device=dev)  # i64 state | statistics
-            sums[ni:].copy_(torch.tensor(st_host, dtype=torch.int64), non_blocking=False)
-            state = {"i64": sums[:ni],
-                     "f64": torch.empty(n * pc.n_f64, dtype=torch.float64, device=dev),
+            # i64 state | fx limbs | statistics: one SUM all-reduce
+            sums = torch.empty(ni + nf + len(_STATS_FIELDS), dtype=torch.int64, device=dev)
+            sums[ni + nf:].copy_(torch.tensor(st_host, dtype=torch.int64), non_blocking=False)
+            state = {"i64": sums[:ni], "fx": sums[ni:ni + nf],
                      "mn": torch.empty(n * pc.n_min, dtype=torch.int64, device=dev),
                      "mx": torch.empty(n * pc.n_max, dtype=torch.int64, device=dev)}
-            check(engine.lib.pg_partials_copy(p, abi.PG_COPY_OUT, ptr(state["i64"]), ptr(state["f64"]),
+            check(engine.lib.pg_partials_copy(p, abi.PG_COPY_OUT, ptr(state["i64"]), ptr(state["fx"]),
                                               ptr(state["mn"]), ptr(state["mx"]), None))
         except Exception as e:  # noqa: BLE001 -- agreed on below, raised on every rank
             err = e
-    any_err, hi, lo = _layout_header(err, fp, group, dev)
+    any_err, flags, hi, lo = _layout_header(err, fp, pc.flags, group, dev)
     if any_err:
         engine.lib.pg_partials_free(p)
         if err is not None:
@@ -140,17 +138,19 @@ def merge_partials_across_ranks(engine, plan, p, group=None) -> IntermediateResu
         raise RuntimeError("the cross-GPU merge failed on another rank")
     if hi[2:] != lo[2:]:
         engine.lib.pg_partials_free(p)
-        raise ValueError(f"partial state layouts differ across ranks: max {hi}, min {lo} (plan with PG_PLAN_F64_SUMS)")
+        raise ValueError(f"partial state layouts differ across ranks: max {hi}, min {lo} (a plan with PG_PLAN_F64_SUMS "
+                         f"and table-global sum bounds, pg_agg.sum_exp)")
+    pc.flags = flags
     dense_all = hi[:2] == lo[:2] and hi[0] == abi.PG_STATE_DENSE   # every rank dense over the same slots
     if not (dense_all and dense_mine):  # dense_mine is a function of the (now known equal) layout: same on all ranks
-        return _exchange_rows(engine, plan, p, torch.tensor(st_host, dtype=torch.int64, device=dev), group, dev)
-    allreduce_state({"i64": sums, "f64": state["f64"], "mn": state["mn"], "mx": state["mx"]}, group)
-    for f, v in zip(_STATS_FIELDS, sums[ni:].cpu().tolist()):  # waits for the collectives
+        return _exchange_rows(engine, plan, p, torch.tensor(st_host, dtype=torch.int64, device=dev), flags, group, dev)
+    allreduce_state({"i64": sums, "mn": state["mn"], "mx": state["mx"]}, group)
+    for f, v in zip(_STATS_FIELDS, sums[ni + nf:].cpu().tolist()):  # waits for the collectives
         setattr(pc.stats, f, int(v))
-    if state["f64"].numel() or state["mn"].numel() or state["mx"].numel():
+    if state["mn"].numel() or state["mx"].numel():
         torch.cuda.synchronize()
     try:
-        check(engine.lib.pg_partials_copy(p, abi.PG_COPY_IN, ptr(state["i64"]), ptr(state["f64"]), ptr(state["mn"]),
+        check(engine.lib.pg_partials_copy(p, abi.PG_COPY_IN, ptr(state["i64"]), ptr(state["fx"]), ptr(state["mn"]),
                                           ptr(state["mx"]), None))
     except Exception:
         engine.lib.pg_partials_free(p)
@@ -172,11 +172,13 @@ def _agree(err, group, dev):
 
 
 def _pack_result(ra) -> np.ndarray:
-    """One rank's finalized result arrays as a flat byte buffer: [G, K, A, num_distinct, has_sets, 6 stats] int64 |
-    keys uint32 | values float64 | counts int64 | offsets uint64 | ids uint32 (8-byte aligned sections)."""
+    """One rank's finalized result arrays as a flat byte buffer: [G, K, A, num_distinct, has_sets, flags, merged,
+    6 stats] int64 | keys uint32 | values float64 | counts int64 | offsets uint64 | ids uint32 (8-byte aligned
+    sections)."""
     has = ra["offsets"] is not None
     nd = len(ra["ids"]) if has else 0
-    parts = [np.array([ra["G"], ra["K"], ra["A"], nd, int(has)], dtype=np.int64), ra["stats"].astype(np.int64),
+    parts = [np.array([ra["G"], ra["K"], ra["A"], nd, int(has), ra.get("flags", 0), ra.get("merged", 0)],
+                      dtype=np.int64), ra["stats"].astype(np.int64),
              ra["keys"].astype(np.uint32).ravel(), ra["values"].astype(np.float64).ravel(),
              ra["counts"].astype(np.int64).ravel()]
     if has:
@@ -197,7 +199,7 @@ def _unpack_result(buf: np.ndarray) -> dict:
         a = np.frombuffer(b, dtype=dtype, count=n, offset=pos).copy()
         pos += -(-a.nbytes // 8) * 8
         return a
-    G, K, A, nd, has = (int(x) for x in take(np.int64, 5))
+    G, K, A, nd, has, flags, merged = (int(x) for x in take(np.int64, 7))
     stats = take(np.int64, 6)
     keys = take(np.uint32, G * K).reshape(G, K)
     vals = take(np.float64, G * A).reshape(G, A)
@@ -205,10 +207,10 @@ def _unpack_result(buf: np.ndarray) -> dict:
     offs = take(np.uint64, G * A + 1) if has else None
     ids = take(np.uint32, nd) if has else None
     return {"G": G, "K": K, "A": A, "keys": keys, "values": vals, "counts": cnts, "offsets": offs, "ids": ids,
-            "stats": stats}
+            "stats": stats, "flags": flags, "merged": merged}
 
 
-def _exchange_rows(engine, plan, p, stats, group, dev) -> IntermediateResult:
+def _exchange_rows(engine, plan, p, stats, flags, group, dev) -> IntermediateResult:
     import torch
     import torch.distributed as dist
     pc = p.contents
@@ -254,6 +256,7 @@ def _exchange_rows(engine, plan, p, stats, group, dev) -> IntermediateResult:
         engine.merge_rows(q, C.c_void_p(recv.data_ptr()), sum(rcounts))
         for f, v in zip(_STATS_FIELDS, st.cpu().tolist()):
             setattr(q.contents.stats, f, int(v))
+        q.contents.flags = flags & abi.PG_RESULT_GROUPS_LIMIT_REACHED  # the threshold is judged on the union below
         ra = engine.finalize_arrays(plan, q)  # this rank's keys (their ORDER BY trim included); frees q
         q = None
     except Exception as e:  # noqa: BLE001
@@ -272,8 +275,11 @@ def _exchange_rows(engine, plan, p, stats, group, dev) -> IntermediateResult:
     dist.all_gather(outs, buf, group=group)
     rows = {}
     res = None
+    n_merged = 0  # the owners' key sets are disjoint: the combined table holds their sum
     for o, sz in zip(outs, sizes):
-        res = engine.decode(plan, _unpack_result(o[:sz[0]].cpu().numpy()))
+        ra_o = _unpack_result(o[:sz[0]].cpu().numpy())
+        n_merged += ra_o["merged"]
+        res = engine.decode(plan, ra_o)
         rows.update(res.rows)
     if not plan.query.group_by and () not in rows:  # no rank matched a doc
         rows[()] = default_row(res.aggregations)
@@ -281,7 +287,11 @@ def _exchange_rows(engine, plan, p, stats, group, dev) -> IntermediateResult:
         # the server's result size over the union of the owners' kept rows (each owner kept its own top `limit`)
         rows = top_groups(plan.query, res.aggregations, rows, plan.plan.limit)
     # every owner carries the statistics summed over the ranks
-    return IntermediateResult(res.aggregations, res.group_by, rows, ExecutionStats(*(int(x) for x in ra["stats"])))
+    thr = plan.plan.trim_threshold
+    return IntermediateResult(res.aggregations, res.group_by, rows, ExecutionStats(*(int(x) for x in ra["stats"])),
+                              bool(flags & abi.PG_RESULT_GROUPS_LIMIT_REACHED),
+                              bool(plan.query.group_by and plan.query.order_by and thr and n_merged >= thr),
+                              n_merged if plan.query.group_by else None)
 
 
 def gather_merge_results(res: IntermediateResult, group=None) -> IntermediateResult:

@@ -299,14 +299,14 @@ struct StateView {            // the device arrays of one partial state
   uint64_t num_slots, hmask;
   unsigned long long* keys;   // hash tables: [num_slots] packed keys (kEmptyKey = free); dense: null
   unsigned long long* i64;
-  double* f64;
+  unsigned long long* fx;     // [num_slots][n_fx][2]: SK_FX (lo, hi) pairs
   long long* mn;
   long long* mx;
   uint32_t* bits;
   unsigned int* first_doc;    // GM_HASH_SEG tables
   unsigned int* fill;         // hash tables: claimed keys
   unsigned int* err;          // bit 2: table full
-  uint32_t n_i64, n_f64, n_min, n_max, bit_words, max_fill;
+  uint32_t n_i64, n_fx, n_min, n_max, bit_words, max_fill;
   const uint32_t* dc_pop;     // optional: DISTINCTCOUNT dc_pop_agg's set size per slot (GM_PART's bucket pass)
   uint32_t dc_pop_agg, pad;
 };
@@ -368,9 +368,12 @@ hipError_t launch_set_extract(const StateView& v, const FinalSpec& f, const uint
 hipError_t launch_gather_rows(const StateView& v, const uint32_t* slots, uint64_t n, uint64_t key_div, uint8_t* dst,
                               hipStream_t s);
 hipError_t launch_merge_rows(const StateView& v, const uint8_t* rows, uint64_t n, hipStream_t s);
+// SK_FX pairs <-> 4 x 32-bit limbs per pair (in: fold the limbs' carries back into the pairs)
+hipError_t launch_fx_limbs(unsigned long long* pairs, long long* limbs, uint64_t n, bool in, hipStream_t s);
 hipError_t launch_init_view(const StateView& v, hipStream_t s, FillSpans* defer = nullptr);  // pg_kernels.hip: zero / empty / +-inf state
 hipError_t launch_seg_truncate(const StateView& v, const uint32_t* slots, uint64_t n, uint32_t num_segments,
                                uint64_t limit, uint64_t* tmp_keys, uint64_t* sorted_keys, uint32_t* sorted_slots,
-                               uint32_t* seg_first, uint8_t* keep, void* temp, size_t temp_bytes, hipStream_t s);
+                               uint32_t* seg_first, uint8_t* keep, unsigned int* reached, void* temp, size_t temp_bytes,
+                               hipStream_t s);
 
 }  // namespace pg

@@ -182,6 +182,15 @@ hipError_t launch_sort_pairs(const uint64_t* kin, uint64_t* kout, const uint32_t
 
 __host__ __device__ __forceinline__ uint32_t bits_words(uint32_t card) { return (card + 31u) / 32u; }
 
+// The final SUM of SK_FX aggregation A in slot s (fx_final: the exact fixed-point sum, or IEEE's sum of the
+// non-finite inputs seen)
+__device__ __forceinline__ double fx_value(const StateView& v, const AggSpec& A, uint64_t s) {
+  const unsigned long long* p = v.fx + (s * v.n_fx + A.slot) * 2;
+  const int64_t smn = A.sp_min != kNoSp ? (int64_t)v.mn[s * v.n_min + A.sp_min] : 0;
+  const int64_t smx = A.sp_max != kNoSp ? (int64_t)v.mx[s * v.n_max + A.sp_max] : 0;
+  return fx_final(A, p[0], p[1], smn, smx);
+}
+
 // Final value of every aggregation of the groups at `slots` (AggregationFunction.extractFinalResult; AVG keeps
 // its (sum, count) pair in vals / cnts, DISTINCTCOUNT its set size).  One thread per group.
 __global__ void final_values_kernel(StateView v, FinalSpec f, const uint32_t* __restrict__ slots, uint64_t n,
@@ -201,7 +210,7 @@ __global__ void final_values_kernel(StateView v, FinalSpec f, const uint32_t* __
         case PG_AGG_COUNTMV: x = (double)(int64_t)v.i64[s * v.n_i64 + A.slot]; break;
         case PG_AGG_SUM:
         case PG_AGG_AVG:
-          x = A.integer ? (double)(int64_t)v.i64[s * v.n_i64 + A.slot] : v.f64[s * v.n_f64 + A.slot];
+          x = A.integer ? (double)(int64_t)v.i64[s * v.n_i64 + A.slot] : fx_value(v, A, s);
           if (A.fn == PG_AGG_AVG) c = count;
           break;
         case PG_AGG_MIN: x = order_key_decode(v.mn[s * v.n_min + A.slot]); break;
@@ -362,7 +371,7 @@ __global__ void order_keys_state_kernel(StateView v, FinalSpec f, const uint32_t
         case PG_AGG_COUNTMV: x = (double)(int64_t)v.i64[s * v.n_i64 + A.slot]; break;
         case PG_AGG_SUM:
         case PG_AGG_AVG:
-          x = A.integer ? (double)(int64_t)v.i64[s * v.n_i64 + A.slot] : v.f64[s * v.n_f64 + A.slot];
+          x = A.integer ? (double)(int64_t)v.i64[s * v.n_i64 + A.slot] : fx_value(v, A, s);
           if (A.fn == PG_AGG_AVG) x = count ? x / (double)count : -__builtin_inf();
           break;
         case PG_AGG_MIN: x = order_key_decode(v.mn[s * v.n_min + A.slot]); break;
@@ -605,7 +614,7 @@ hipError_t launch_set_extract(const StateView& v, const FinalSpec& f, const uint
 // ------------------------------------------------------------------------------------------ exchange rows
 
 uint64_t row_bytes(const StateView& v) {
-  const uint64_t b = 8ull * (1 + v.n_i64 + v.n_f64 + v.n_min + v.n_max) + 4ull * v.bit_words;
+  const uint64_t b = 8ull * (1 + v.n_i64 + 2ull * v.n_fx + v.n_min + v.n_max) + 4ull * v.bit_words;
   return (b + 7) & ~7ull;
 }
 
@@ -619,7 +628,7 @@ __global__ void gather_rows_kernel(StateView v, const uint32_t* __restrict__ slo
     r[0] = (v.keys ? v.keys[s] : s) / key_div;
     uint64_t o = 1;
     for (uint32_t k = 0; k < v.n_i64; k++) r[o++] = v.i64[s * v.n_i64 + k];
-    for (uint32_t k = 0; k < v.n_f64; k++) r[o++] = (uint64_t)__double_as_longlong(v.f64[s * v.n_f64 + k]);
+    for (uint32_t k = 0; k < 2 * v.n_fx; k++) r[o++] = v.fx[s * v.n_fx * 2 + k];
     for (uint32_t k = 0; k < v.n_min; k++) r[o++] = (uint64_t)v.mn[s * v.n_min + k];
     for (uint32_t k = 0; k < v.n_max; k++) r[o++] = (uint64_t)v.mx[s * v.n_max + k];
     uint32_t* b = (uint32_t*)(r + o);
@@ -660,7 +669,12 @@ __global__ void merge_rows_kernel(StateView v, const uint8_t* __restrict__ src, 
     }
     uint64_t o = 1;
     for (uint32_t k = 0; k < v.n_i64; k++) atomicAdd(&v.i64[s * v.n_i64 + k], (unsigned long long)r[o++]);
-    for (uint32_t k = 0; k < v.n_f64; k++) atomicAdd(&v.f64[s * v.n_f64 + k], __longlong_as_double((long long)r[o++]));
+    for (uint32_t k = 0; k < v.n_fx; k++, o += 2) {  // 128-bit add: the low word's carry-out goes to the high word
+      unsigned long long* p = v.fx + (s * v.n_fx + k) * 2;
+      const uint64_t lo = r[o], old = atomicAdd(p, (unsigned long long)lo);
+      const uint64_t hi = r[o + 1] + (old + lo < old ? 1ull : 0ull);
+      if (hi) atomicAdd(p + 1, (unsigned long long)hi);
+    }
     for (uint32_t k = 0; k < v.n_min; k++) atomicMin(&v.mn[s * v.n_min + k], (long long)r[o++]);
     for (uint32_t k = 0; k < v.n_max; k++) atomicMax(&v.mx[s * v.n_max + k], (long long)r[o++]);
     const uint32_t* b = (const uint32_t*)(r + o);
@@ -696,16 +710,21 @@ __global__ void seg_first_kernel(const uint64_t* __restrict__ sorted, uint64_t n
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
     if (i == 0 || (sorted[i] >> 32) != (sorted[i - 1] >> 32)) seg_first[sorted[i] >> 32] = (uint32_t)i;
 }
+// reached: set when some segment holds >= limit keys (its rank limit - 1 exists: numGroupsLimitReached)
 __global__ void seg_keep_kernel(const uint64_t* __restrict__ sorted, uint64_t n, const uint32_t* __restrict__ seg_first,
-                                uint64_t limit, uint8_t* __restrict__ keep) {
+                                uint64_t limit, uint8_t* __restrict__ keep, unsigned int* __restrict__ reached) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-    keep[i] = (i - seg_first[sorted[i] >> 32]) < limit;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t rank = i - seg_first[sorted[i] >> 32];
+    keep[i] = rank < limit;
+    if (rank + 1 == limit) atomicOr(reached, 1u);
+  }
 }
 
 hipError_t launch_seg_truncate(const StateView& v, const uint32_t* slots, uint64_t n, uint32_t num_segments,
                                uint64_t limit, uint64_t* tmp_keys, uint64_t* sorted_keys, uint32_t* sorted_slots,
-                               uint32_t* seg_first, uint8_t* keep, void* temp, size_t temp_bytes, hipStream_t s) {
+                               uint32_t* seg_first, uint8_t* keep, unsigned int* reached, void* temp, size_t temp_bytes,
+                               hipStream_t s) {
   if (!n) return hipSuccess;
   const uint64_t blocks = (n + 255) / 256;
   const dim3 g((uint32_t)(blocks < 16384 ? blocks : 16384));
@@ -713,7 +732,7 @@ hipError_t launch_seg_truncate(const StateView& v, const uint32_t* slots, uint64
   hipError_t e = launch_sort_pairs(tmp_keys, sorted_keys, slots, sorted_slots, n, temp, temp_bytes, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(seg_first_kernel, g, dim3(256), 0, s, sorted_keys, n, seg_first);
-  hipLaunchKernelGGL(seg_keep_kernel, g, dim3(256), 0, s, sorted_keys, n, seg_first, limit, keep);
+  hipLaunchKernelGGL(seg_keep_kernel, g, dim3(256), 0, s, sorted_keys, n, seg_first, limit, keep, reached);
   return hipGetLastError();
 }
 

@@ -116,7 +116,11 @@ struct WorkItem {
   uint32_t pad;
 };
 
-enum SlotKind : uint32_t { SK_NONE = 0, SK_I64 = 1, SK_F64 = 2, SK_MIN = 3, SK_MAX = 4, SK_BITS = 5 };
+// SK_FX: a SUM / AVG whose inputs are not provably integer accumulates EXACTLY, as a 128-bit two's-complement
+// fixed-point number (lo, hi words of the `fx` state array) in units of 2^fx_shift (see fx_from_double): integer adds
+// are associative, so the sum has the same bits whatever the order of the atomics, the grid, the number of GPUs or the
+// merge order -- the reference's double sum depends on its thread scheduling.
+enum SlotKind : uint32_t { SK_NONE = 0, SK_I64 = 1, SK_FX = 2, SK_MIN = 3, SK_MAX = 4, SK_BITS = 5 };
 
 // Group state addressing (QuerySpec::group_mode):
 //   GM_NONE     aggregation-only: one slot (0).
@@ -155,8 +159,12 @@ struct AggSpec {
   uint32_t key_card;  // DISTINCTCOUNT: size of the table-global value id space (bits of its bitmap)
   int64_t key_base;
   uint32_t dc_word;   // DISTINCTCOUNT: first uint32 word of this aggregation's bitmap within a slot's row
-  uint32_t pad;
+  int32_t fx_shift;   // SK_FX: the fixed-point unit is 2^fx_shift
+  // SK_FX over a column that may hold +-inf / NaN: mn / mx slots that receive the order images of the non-finite
+  // inputs (the fixed-point sum skips them), so that finalisation gives IEEE's sum of them (fx_final); else kNoSp
+  uint32_t sp_min, sp_max;
 };
+constexpr uint32_t kNoSp = 0xFFFFFFFFu;
 
 // A packed column staged per tile into LDS (LDS-DMA of the tile's whole word range in 1 KiB pieces) because
 // most of its cache lines are needed anyway; every other read of a packed column is a per-doc gather.
@@ -192,11 +200,11 @@ struct QuerySpec {
   uint32_t hmax_fill;        // GM_HASH*: keys claimed before the table reports overflow (err bit 4)
   uint64_t num_slots;        // dense: key space size; hash: table capacity (a power of two)
   uint64_t hmask;            // hash: num_slots - 1
-  uint32_t n_i64, n_f64, n_min, n_max;
+  uint32_t n_i64, n_fx, n_min, n_max;  // n_fx: SK_FX slots, 2 words each
   uint32_t dc_row_words;     // uint32 words of DISTINCTCOUNT bitmaps per slot
   uint32_t pad2;
   unsigned long long* i64;
-  double* f64;
+  unsigned long long* fx;    // [num_slots][n_fx][2] (lo, hi)
   long long* mn;
   long long* mx;
   uint32_t* dbits;           // [num_slots][dc_row_words]
@@ -234,6 +242,96 @@ __host__ __device__ inline double order_key_decode(int64_t k) {
   double v;
   __builtin_memcpy(&v, &b, 8);
   return v;
+}
+
+// ---- exact fixed-point sums (SK_FX)
+// The unit 2^fx_shift is chosen by the host from a bound 2^e >= |every input| of the plan: fx_shift = e + 40 - 126, so a
+// single input needs at most 87 bits and 2^40 inputs sum within 127 bits (no overflow for any table this library can
+// hold).  Inputs of magnitude >= 2^(e - 34) convert exactly; smaller ones round to the nearest unit (2^-86 of the bound:
+// far below a double sum's own rounding error).
+constexpr int kFxSumBits = 126;
+constexpr int kFxCountBits = 40;
+__host__ __device__ inline int32_t fx_shift_for(int32_t bound_exp) { return bound_exp + kFxCountBits - kFxSumBits; }
+
+// x / 2^shift rounded to nearest (ties to even) as a 128-bit two's-complement integer; 0 for +-inf / NaN (those are
+// tracked apart, AggSpec::sp_min / sp_max)
+__host__ __device__ inline void fx_from_double(double x, int32_t shift, uint64_t& lo, uint64_t& hi) {
+  uint64_t b;
+  __builtin_memcpy(&b, &x, 8);
+  int e = (int)((b >> 52) & 0x7FF);
+  uint64_t m = b & ((1ull << 52) - 1);
+  lo = hi = 0;
+  if (e == 0x7FF) return;
+  if (e == 0) e = 1; else m |= 1ull << 52;
+  if (!m) return;
+  const int sh = e - 1075 - shift;  // x = m * 2^(e - 1075) = m * 2^sh units
+  if (sh >= 0) {
+    if (sh >= 128) return;  // outside the range the host's bound allows (never for valid plans)
+    if (sh >= 64) { hi = m << (sh - 64); }
+    else if (sh == 0) { lo = m; }
+    else { lo = m << sh; hi = m >> (64 - sh); }
+  } else {
+    const int r = -sh;
+    if (r > 54) return;  // below half a unit: m < 2^53 <= 2^(r - 1)
+    uint64_t q = m >> r;
+    const uint64_t rem = m & ((1ull << r) - 1), half = 1ull << (r - 1);
+    if (rem > half || (rem == half && (q & 1))) q++;
+    lo = q;
+  }
+  if (b >> 63) {  // negate
+    lo = ~lo + 1;
+    hi = ~hi + (lo == 0 ? 1 : 0);
+  }
+}
+
+// (lo, hi) * 2^shift as the nearest double (ties to even; exact integer rounding of the 128-bit value, then one exact
+// scaling -- the same bits on the host and on the device)
+__host__ __device__ inline double fx_to_double(uint64_t lo, uint64_t hi, int32_t shift) {
+  const bool neg = (int64_t)hi < 0;
+  if (neg) {
+    lo = ~lo + 1;
+    hi = ~hi + (lo == 0 ? 1 : 0);
+  }
+  if (!hi && !lo) return 0.0;
+  const int nb = hi ? 128 - __builtin_clzll(hi) : 64 - __builtin_clzll(lo);  // significant bits
+  uint64_t mant;
+  int exp2 = 0;
+  if (nb <= 53) {
+    mant = lo;
+  } else {
+    const int r = nb - 53;  // 1..75 bits dropped
+    mant = r >= 64 ? hi >> (r - 64) : ((lo >> r) | (hi << (64 - r)));
+    const int rb = r - 1;   // the rounding bit; sticky = any bit below it
+    const uint64_t round = rb >= 64 ? (hi >> (rb - 64)) & 1 : (lo >> rb) & 1;
+    bool sticky;
+    if (rb >= 64) sticky = lo != 0 || (rb > 64 && (hi & ((1ull << (rb - 64)) - 1)) != 0);
+    else sticky = rb > 0 && (lo & ((1ull << rb) - 1)) != 0;
+    if (round && (sticky || (mant & 1))) mant++;  // may carry to 2^53: still exact as a double
+    exp2 = r;
+  }
+  const double d = __builtin_ldexp((double)mant, exp2 + shift);
+  return neg ? -d : d;
+}
+
+// 128-bit add of (blo, bhi) into (lo, hi)
+__host__ __device__ inline void fx_add(uint64_t& lo, uint64_t& hi, uint64_t blo, uint64_t bhi) {
+  const uint64_t t = lo + blo;
+  hi += bhi + (t < lo ? 1 : 0);
+  lo = t;
+}
+
+// The final SUM of an SK_FX aggregation: the fixed-point sum of the finite inputs, unless non-finite inputs were seen
+// (their order images in the sp_min / sp_max slots): IEEE 754 addition gives NaN for any NaN or for +inf with -inf,
+// else the infinity -- whatever the order, so the special cases stay exact too.
+__host__ __device__ inline double fx_final(const AggSpec& A, uint64_t lo, uint64_t hi, int64_t sp_mn, int64_t sp_mx) {
+  if (A.sp_min != kNoSp) {
+    const int64_t kpinf = order_key(__builtin_inf()), kninf = order_key(-__builtin_inf());
+    const bool nan = sp_mx > kpinf || sp_mn < kninf, pinf = sp_mx == kpinf, ninf = sp_mn == kninf;
+    if (nan || (pinf && ninf)) return __builtin_nan("");
+    if (pinf) return __builtin_inf();
+    if (ninf) return -__builtin_inf();
+  }
+  return fx_to_double(lo, hi, A.fx_shift);
 }
 
 

@@ -23,6 +23,39 @@ __device__ __forceinline__ uint32_t unpack(const uint32_t* __restrict__ w, uint6
 
 // ------------------------------------------------------------------------------------------ state init
 
+// SK_FX sums <-> 32-bit limbs (pg_partials_copy): out, each (lo, hi) pair as 4 int64 limbs of 32 bits (limb k = bits
+// [32k, 32k + 32)), so that a plain SUM all-reduce of the limbs over up to 2^31 ranks is exact; in, the limbs'
+// carries folded back into the 128-bit pair (mod 2^128, the pair's own wrap-around).
+__global__ void fx_limbs_kernel(unsigned long long* pairs, long long* limbs, uint64_t n, int in) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    if (!in) {
+      const uint64_t lo = pairs[2 * i], hi = pairs[2 * i + 1];
+      limbs[4 * i] = (long long)(lo & 0xFFFFFFFFull);
+      limbs[4 * i + 1] = (long long)(lo >> 32);
+      limbs[4 * i + 2] = (long long)(hi & 0xFFFFFFFFull);
+      limbs[4 * i + 3] = (long long)(hi >> 32);
+    } else {
+      uint64_t w[4], c = 0;
+      for (int k = 0; k < 4; k++) {  // each limb is a sum of 32-bit values: < 2^63, carry its excess upward
+        const uint64_t t = (uint64_t)limbs[4 * i + k] + c;
+        w[k] = t & 0xFFFFFFFFull;
+        c = t >> 32;
+      }
+      pairs[2 * i] = w[0] | (w[1] << 32);
+      pairs[2 * i + 1] = w[2] | (w[3] << 32);
+    }
+  }
+}
+
+hipError_t launch_fx_limbs(unsigned long long* pairs, long long* limbs, uint64_t n, bool in, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const uint64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(fx_limbs_kernel, dim3((uint32_t)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, pairs, limbs, n,
+                     in ? 1 : 0);
+  return hipGetLastError();
+}
+
 __global__ void init_minmax_kernel(long long* mn, uint64_t nmn, long long* mx, uint64_t nmx) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -38,7 +71,7 @@ hipError_t launch_init_view(const StateView& v, hipStream_t s, FillSpans* defer)
     return hipMemsetAsync(p, b, n, s);
   };
   if (v.n_i64 && (e = fill(v.i64, 0, v.num_slots * v.n_i64 * 8)) != hipSuccess) return e;
-  if (v.n_f64 && (e = fill(v.f64, 0, v.num_slots * v.n_f64 * 8)) != hipSuccess) return e;
+  if (v.n_fx && (e = fill(v.fx, 0, v.num_slots * v.n_fx * 16)) != hipSuccess) return e;
   if (v.bit_words && (e = fill(v.bits, 0, v.num_slots * v.bit_words * 4ull)) != hipSuccess) return e;
   if (v.keys && (e = fill(v.keys, 0xFF, v.num_slots * 8)) != hipSuccess) return e;
   if (v.first_doc && (e = fill(v.first_doc, 0xFF, v.num_slots * 4)) != hipSuccess) return e;

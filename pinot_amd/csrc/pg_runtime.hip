@@ -18,6 +18,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cfloat>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -267,6 +269,8 @@ struct ColumnRes {
   DevBuf dict;
   double dmin = 0, dmax = 0;  // dictionary min / max value (as double; integers exact below 2^53)
   int64_t imin = 0, imax = 0;
+  double fin_abs = 0;         // largest |value| among the finite values (the SK_FX unit's bound)
+  bool nonfinite = false;     // some value is +-inf or NaN (FLOAT / DOUBLE)
   // forward index
   uint32_t fwd = FWD_NONE;
   uint32_t num_docs = 0, bits = 0, num_values = 0;
@@ -597,6 +601,17 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
         tmp.dmax = be_value_as_double(hi.data(), d->data_type);
         tmp.imin = be_value_as_i64(lo.data(), d->data_type);
         tmp.imax = be_value_as_i64(hi.data(), d->data_type);
+        if (std::isfinite(tmp.dmin) && std::isfinite(tmp.dmax)) {
+          tmp.fin_abs = std::max(fabs(tmp.dmin), fabs(tmp.dmax));
+        } else {  // a FLOAT / DOUBLE dictionary with +-inf / NaN (sorted as Double.compare: NaN last): scan it once
+          std::vector<uint8_t> all;
+          if ((rc = host_copy(src, (uint64_t)w * d->cardinality, on_dev, all))) return rc;
+          for (uint32_t i = 0; i < d->cardinality; i++) {
+            const double v = be_value_as_double(&all[(uint64_t)i * w], d->data_type);
+            if (std::isfinite(v)) tmp.fin_abs = std::max(tmp.fin_abs, fabs(v));
+            else tmp.nonfinite = true;
+          }
+        }
       }
       break;
     }
@@ -731,6 +746,8 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
         const double v = be_value_as_double(&be[(uint64_t)i * w], d->data_type);
         tmp.dmin = std::min(tmp.dmin, v);
         tmp.dmax = std::max(tmp.dmax, v);
+        if (std::isfinite(v)) tmp.fin_abs = std::max(tmp.fin_abs, fabs(v));
+        else tmp.nonfinite = true;
         if (d->data_type <= PG_LONG) {
           const int64_t x = be_value_as_i64(&be[(uint64_t)i * w], d->data_type);
           tmp.imin = std::min(tmp.imin, x);
@@ -790,6 +807,7 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
       c.has_dict = true; c.dtype = tmp.dtype; c.card = tmp.card; c.entry_bytes = tmp.entry_bytes;
       c.dict = std::move(tmp.dict);
       c.dmin = tmp.dmin; c.dmax = tmp.dmax; c.imin = tmp.imin; c.imax = tmp.imax;
+      c.fin_abs = tmp.fin_abs; c.nonfinite = tmp.nonfinite;
       break;
     case PG_IDX_FWD_SV_BITPACKED: case PG_IDX_FWD_SV_SORTED: case PG_IDX_FWD_MV_BITPACKED:
       c.words.reset(); c.mv_offsets.reset(); c.mv_cnt.reset();
@@ -843,6 +861,7 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
       c.fwd = FWD_RAW; c.num_docs = tmp.num_docs; c.bits = 0; c.num_values = tmp.num_values;
       c.dtype = tmp.dtype; c.card = tmp.card; c.has_dict = false;
       c.dmin = tmp.dmin; c.dmax = tmp.dmax; c.imin = tmp.imin; c.imax = tmp.imax;
+      c.fin_abs = tmp.fin_abs; c.nonfinite = tmp.nonfinite;
       c.rawv = std::move(tmp.rawv);
       break;
   }
@@ -868,8 +887,8 @@ struct Partials {
   std::shared_ptr<WideKeys> wide;  // set for wide-key plans: packed keys are tuple slots, local to this state
   uint32_t mode = GM_NONE;      // GroupMode (GM_HASH_SEG only between the scan and the truncation merge)
   uint64_t num_slots = 1;
-  uint32_t n_i64 = 1, n_f64 = 0, n_min = 0, n_max = 0, bit_words = 0, max_fill = 0;
-  DevBuf keys, i64, f64, mn, mx, bits, first_doc, misc /* [fill, err] */, seg_matched;
+  uint32_t n_i64 = 1, n_fx = 0, n_min = 0, n_max = 0, bit_words = 0, max_fill = 0;
+  DevBuf keys, i64, fx, mn, mx, bits, first_doc, misc /* [fill, err] */, seg_matched;
   DevBuf dc_pop;                // GM_PART under pg_execute: each group's DISTINCTCOUNT (aggregation dc_pop_agg)
   int dc_pop_agg = -1;
   bool host_state = false;      // t_ctx.state_host holds a copy of the final state (queued before the scan's sync)
@@ -880,7 +899,15 @@ struct Partials {
   uint64_t total_docs = 0;
   uint32_t num_segments = 0;
   uint32_t layout = 0;          // bit a: aggregation a accumulates integer-exact (i64) -- must agree across merges
+  uint32_t flags = 0;           // PG_RESULT_* seen while producing this state (a segment reached numGroupsLimit)
   std::vector<AggSpec> aggs;
+  // signature of the SK_FX units and special slots: states merge only when it agrees (as `layout`)
+  uint32_t fx_sig() const {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    for (const AggSpec& a : aggs)
+      if (a.kind == SK_FX) h = mix64(h ^ ((uint64_t)(uint32_t)a.fx_shift << 32) ^ (a.sp_min != kNoSp ? 1u : 0u) ^ ((uint64_t)a.slot << 8));
+    return (uint32_t)(h >> 33);  // 31 bits: a non-negative int64 in the ranks' fingerprint all-reduce
+  }
 
   StateView view() const {
     StateView v;
@@ -889,14 +916,14 @@ struct Partials {
     v.hmask = mode == GM_HASH || mode == GM_HASH_SEG ? num_slots - 1 : 0;
     v.keys = (unsigned long long*)keys.p;
     v.i64 = (unsigned long long*)i64.p;
-    v.f64 = (double*)f64.p;
+    v.fx = (unsigned long long*)fx.p;
     v.mn = (long long*)mn.p;
     v.mx = (long long*)mx.p;
     v.bits = (uint32_t*)bits.p;
     v.first_doc = (unsigned int*)first_doc.p;
     v.fill = (unsigned int*)misc.p;
     v.err = misc.p ? (unsigned int*)misc.p + 1 : nullptr;
-    v.n_i64 = n_i64; v.n_f64 = n_f64; v.n_min = n_min; v.n_max = n_max; v.bit_words = bit_words;
+    v.n_i64 = n_i64; v.n_fx = n_fx; v.n_min = n_min; v.n_max = n_max; v.bit_words = bit_words;
     v.max_fill = max_fill;
     v.dc_pop = dc_pop_agg >= 0 ? (const uint32_t*)dc_pop.p : nullptr;
     v.dc_pop_agg = (uint32_t)dc_pop_agg;
@@ -907,9 +934,11 @@ struct Partials {
 };
 
 // Layout of the state arrays of a plan's aggregations (slot assignment, DISTINCTCOUNT bitmap words).  `integer`
-// bit a: SUM / AVG a accumulates integer-exact in i64.
-int agg_layout(const pg_plan* plan, uint32_t integer, std::vector<AggSpec>& aggs, uint32_t& n_i64, uint32_t& n_f64,
-               uint32_t& n_min, uint32_t& n_max, uint32_t& bit_words);
+// bit a: SUM / AVG a accumulates integer-exact in i64, else exactly as SK_FX in units of 2^fx_shift[a], with special
+// slots for non-finite inputs when bit a of `special` is set.
+int agg_layout(const pg_plan* plan, uint32_t integer, const std::vector<int32_t>& fx_shift, uint32_t special,
+               std::vector<AggSpec>& aggs, uint32_t& n_i64, uint32_t& n_fx, uint32_t& n_min, uint32_t& n_max,
+               uint32_t& bit_words);
 
 // Pinot's default numGroupsLimit (InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT)
 constexpr uint64_t kDefaultNumGroupsLimit = 100000;
@@ -1116,10 +1145,11 @@ uint64_t scan_grid_cap(bool grouped, bool one_round = false) {
   return g_grid_caps[(grouped ? 1 : 0) + (one_round ? 2 : 0)];
 }
 
-int agg_layout(const pg_plan* plan, uint32_t integer, std::vector<AggSpec>& aggs, uint32_t& n_i64, uint32_t& n_f64,
-               uint32_t& n_min, uint32_t& n_max, uint32_t& bit_words) {
+int agg_layout(const pg_plan* plan, uint32_t integer, const std::vector<int32_t>& fx_shift, uint32_t special,
+               std::vector<AggSpec>& aggs, uint32_t& n_i64, uint32_t& n_fx, uint32_t& n_min, uint32_t& n_max,
+               uint32_t& bit_words) {
   n_i64 = 1;  // slot 0: doc count (COUNT, AVG count, group presence)
-  n_f64 = n_min = n_max = bit_words = 0;
+  n_fx = n_min = n_max = bit_words = 0;
   aggs.assign(plan->num_aggs, AggSpec{});
   for (uint32_t a = 0; a < plan->num_aggs; a++) {
     const pg_agg& g = plan->aggs[a];
@@ -1127,6 +1157,7 @@ int agg_layout(const pg_plan* plan, uint32_t integer, std::vector<AggSpec>& aggs
     memset(&s2, 0, sizeof(s2));
     s2.fn = g.fn;
     s2.op = g.op;
+    s2.sp_min = s2.sp_max = kNoSp;
     if (g.fn > PG_AGG_COUNTMV) return fail(PG_E_INVALID, "unknown aggregation %u", g.fn);
     if (g.op > PG_EXPR_SUB) return fail(PG_E_INVALID, "unknown expression op %u", g.op);
     switch (g.fn) {
@@ -1134,8 +1165,15 @@ int agg_layout(const pg_plan* plan, uint32_t integer, std::vector<AggSpec>& aggs
       case PG_AGG_COUNTMV: s2.kind = SK_I64; s2.slot = n_i64++; break;
       case PG_AGG_SUM: case PG_AGG_AVG:
         s2.integer = (integer >> a) & 1u;
-        if (s2.integer) { s2.kind = SK_I64; s2.slot = n_i64++; }
-        else { s2.kind = SK_F64; s2.slot = n_f64++; }
+        if (s2.integer) {
+          s2.kind = SK_I64;
+          s2.slot = n_i64++;
+        } else {
+          s2.kind = SK_FX;
+          s2.slot = n_fx++;
+          s2.fx_shift = a < fx_shift.size() ? fx_shift[a] : fx_shift_for(1024);
+          if ((special >> a) & 1u) { s2.sp_min = n_min++; s2.sp_max = n_max++; }
+        }
         s2.cnt_slot = 0;
         break;
       case PG_AGG_MIN: s2.kind = SK_MIN; s2.slot = n_min++; break;
@@ -1159,7 +1197,7 @@ int Partials::alloc_state(hipStream_t s, bool init, FillSpans* defer) {
   int rc;
   const bool hash = mode == GM_HASH || mode == GM_HASH_SEG;
   if ((rc = i64.alloc_pooled(G * 8ull * n_i64))) return rc;
-  if (n_f64) { if ((rc = f64.alloc_pooled(G * 8ull * n_f64))) return rc; } else f64.reset();
+  if (n_fx) { if ((rc = fx.alloc_pooled(G * 16ull * n_fx))) return rc; } else fx.reset();
   if (n_min) { if ((rc = mn.alloc_pooled(G * 8ull * n_min))) return rc; } else mn.reset();
   if (n_max) { if ((rc = mx.alloc_pooled(G * 8ull * n_max))) return rc; } else mx.reset();
   if (bit_words) { if ((rc = bits.alloc_pooled(G * 4ull * bit_words))) return rc; } else bits.reset();
@@ -1210,12 +1248,12 @@ template <class T> int read_back(const T* d, T& h, hipStream_t s) {
 int hash_like(const Partials& src, uint64_t groups, Partials& out, hipStream_t s) {
   out.mode = GM_HASH;
   out.num_slots = pow2_at_least(std::max<uint64_t>(1024, 2 * groups));
-  const uint64_t slot_bytes = 8ull * (src.n_i64 + src.n_f64 + src.n_min + src.n_max) + 4ull * src.bit_words + 12;
+  const uint64_t slot_bytes = 8ull * (src.n_i64 + 2ull * src.n_fx + src.n_min + src.n_max) + 4ull * src.bit_words + 12;
   if (out.num_slots > kMaxHashSlots || out.num_slots * slot_bytes > kStateBudget)  // compile_and_run's budget
     return fail(PG_E_UNSUPPORTED, "merge table of %llu groups (%llu slots x %llu bytes) exceeds the state budget",
                 (unsigned long long)groups, (unsigned long long)out.num_slots, (unsigned long long)slot_bytes);
   out.max_fill = (uint32_t)(out.num_slots / 4 * 3);
-  out.n_i64 = src.n_i64; out.n_f64 = src.n_f64; out.n_min = src.n_min; out.n_max = src.n_max;
+  out.n_i64 = src.n_i64; out.n_fx = src.n_fx; out.n_min = src.n_min; out.n_max = src.n_max;
   out.bit_words = src.bit_words;
   out.key_card = src.key_card;
   out.key_stride = src.key_stride;
@@ -1223,6 +1261,7 @@ int hash_like(const Partials& src, uint64_t groups, Partials& out, hipStream_t s
   out.total_docs = src.total_docs;
   out.num_segments = src.num_segments;
   out.layout = src.layout;
+  out.flags = src.flags;
   out.aggs = src.aggs;
   return out.alloc_state(s);
 }
@@ -1250,9 +1289,14 @@ int truncate_and_merge(Partials& P, uint64_t limit, hipStream_t s) {
   uint32_t* seg_first = sc.get<uint32_t>(P.num_segments + 1, rc);
   uint8_t* keep = sc.get<uint8_t>(n + 1, rc);
   uint32_t* kept = sc.get<uint32_t>(n + 1, rc);
+  unsigned int* reached = sc.get<unsigned int>(1, rc);
   if (rc) return rc;
+  HIP_CHECK(hipMemsetAsync(reached, 0, 4, s));
   HIP_CHECK(launch_seg_truncate(v, slots, n, P.num_segments, limit, tmp_keys, sorted_keys, sorted_slots, seg_first,
-                                keep, temp, temp_bytes, s));
+                                keep, reached, temp, temp_bytes, s));
+  uint32_t hit = 0;
+  if ((rc = read_back((uint32_t*)reached, hit, s))) return rc;
+  if (hit) P.flags |= PG_RESULT_GROUPS_LIMIT_REACHED;
   uint32_t nk = 0;
   if (n) {
     HIP_CHECK(launch_select_flagged(sorted_slots, keep, n, kept, d_num, temp, temp_bytes, s));
@@ -1274,7 +1318,7 @@ int truncate_and_merge(Partials& P, uint64_t limit, hipStream_t s) {
   P.max_fill = H.max_fill;
   P.keys = std::move(H.keys);
   P.i64 = std::move(H.i64);
-  P.f64 = std::move(H.f64);
+  P.fx = std::move(H.fx);
   P.mn = std::move(H.mn);
   P.mx = std::move(H.mx);
   P.bits = std::move(H.bits);
@@ -1533,7 +1577,9 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       }
       const uint64_t ub = std::min<uint64_t>(prod, plan->segments[si].num_docs);
       seg_groups += ub;
-      truncating |= ub > limit;
+      // >=: a segment holding exactly `limit` keys reports numGroupsLimitReached (getNumGroups() >= limit,
+      // AggregationGroupByOrderByOperator.java:112-113), which the per-segment table counts
+      truncating |= ub >= limit;
     }
   }
 
@@ -1542,7 +1588,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   uint64_t total_docs = 0;
   for (uint32_t si = 0; si < S; si++) total_docs += plan->segments[si].num_docs;
   std::unordered_set<uint32_t> projected;
-  uint32_t integer = 0;
+  uint32_t integer = 0, special = 0;
+  std::vector<int32_t> fx_shift(A, 0);
   for (uint32_t a = 0; a < A; a++) {
     const pg_agg& g = plan->aggs[a];
     if (g.fn > PG_AGG_COUNTMV) return fail(PG_E_INVALID, "unknown aggregation %u", g.fn);
@@ -1551,8 +1598,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     projected.insert(g.col_a);
     const bool two = (g.fn == PG_AGG_SUM || g.fn == PG_AGG_MIN || g.fn == PG_AGG_MAX || g.fn == PG_AGG_AVG) && g.op != PG_EXPR_COL;
     if (two) projected.insert(g.col_b);
-    double bound_a = 0, bound_b = 0;
-    bool all_int = true;
+    double bound_a = 0, bound_b = 0, fin_a = 0, fin_b = 0;  // |value| bounds: all values / the finite ones
+    bool all_int = true, nonfinite = false;
     for (uint32_t si = 0; si < S; si++) {
       const ColumnRes* ca = col(si, g.col_a);
       if (!ca) return fail(PG_E_NOTFOUND, "aggregation %u: column %u not resident in segment %u", a, g.col_a, si);
@@ -1576,12 +1623,16 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       if (ca->dtype > PG_DOUBLE) return fail(PG_E_UNSUPPORTED, "numeric aggregation on non-numeric column %u", g.col_a);
       all_int &= ca->dtype <= PG_LONG;
       bound_a = std::max(bound_a, std::max(fabs(ca->dmin), fabs(ca->dmax)));
+      fin_a = std::max(fin_a, ca->fin_abs);
+      nonfinite |= ca->nonfinite;
       if (two) {
         const ColumnRes* cb = col(si, g.col_b);
         if (!cb || cb->fwd == FWD_NONE || cb->fwd == FWD_MV || (!cb->has_dict && cb->fwd != FWD_RAW) || cb->dtype > PG_DOUBLE)
           return fail(PG_E_UNSUPPORTED, "aggregation %u: second operand column %u unusable", a, g.col_b);
         all_int &= cb->dtype <= PG_LONG;
         bound_b = std::max(bound_b, std::max(fabs(cb->dmin), fabs(cb->dmax)));
+        fin_b = std::max(fin_b, cb->fin_abs);
+        nonfinite |= cb->nonfinite;
       }
     }
     if (g.fn == PG_AGG_SUM || g.fn == PG_AGG_AVG) {
@@ -1591,11 +1642,29 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       // reference's double accumulation while |sum| < 2^53, more exact beyond (within the 1e-9 tolerance)
       const bool as_int = all_int && !(plan->flags & PG_PLAN_F64_SUMS) &&
                           vb * (double)(total_docs ? total_docs : 1) < 4.0e18;
-      if (as_int) integer |= 1u << a;
+      if (as_int) {
+        integer |= 1u << a;
+      } else {
+        // SK_FX: the unit from a power-of-two bound of the finite inputs (an expression of finite operands can still
+        // overflow to +-inf: then the bound is DBL_MAX's and the non-finite results go to the special slots)
+        double fb = fin_a;
+        if (two) fb = g.op == PG_EXPR_MUL ? fin_a * fin_b : fin_a + fin_b;
+        if (!std::isfinite(fb)) { fb = DBL_MAX; nonfinite = true; }
+        int e = 0;
+        if (fb > 0) (void)frexp(fb, &e);  // fb <= 2^e
+        if (g.sum_exp) {  // the caller's table-global bound (the same unit on every GPU / server that merges)
+          if (e > g.sum_exp)
+            return fail(PG_E_INVALID, "aggregation %u: inputs up to 2^%d exceed the plan's sum_exp %d", a, e, g.sum_exp);
+          e = g.sum_exp;
+        }
+        if (e < -1000 || e > 1024) return fail(PG_E_INVALID, "aggregation %u: sum_exp %d out of range", a, e);
+        fx_shift[a] = fx_shift_for(e);
+        if (nonfinite || (g.sum_flags & PG_SUM_NONFINITE)) special |= 1u << a;
+      }
     }
   }
   {
-    int rc2 = agg_layout(plan, integer, P.aggs, P.n_i64, P.n_f64, P.n_min, P.n_max, P.bit_words);
+    int rc2 = agg_layout(plan, integer, fx_shift, special, P.aggs, P.n_i64, P.n_fx, P.n_min, P.n_max, P.bit_words);
     if (rc2) return rc2;
     P.layout = integer;
     for (uint32_t a = 0; a < A; a++) q.aggs[a] = P.aggs[a];
@@ -1606,7 +1675,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   PG_PROF("state");
   // ---- group state addressing: dense key space, hash table of global keys, or (numGroupsLimit can truncate a
   // segment) hash table of (segment, key) with first-seen docs
-  const uint64_t slot_bytes = 8ull * (P.n_i64 + P.n_f64 + P.n_min + P.n_max) + 4ull * P.bit_words;
+  const uint64_t slot_bytes = 8ull * (P.n_i64 + 2ull * P.n_fx + P.n_min + P.n_max) + 4ull * P.bit_words;
   if (K == 0) {
     P.mode = GM_NONE;
     P.num_slots = 1;
@@ -1637,9 +1706,11 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   q.num_slots = P.num_slots;
   q.hmask = P.mode == GM_HASH || P.mode == GM_HASH_SEG ? P.num_slots - 1 : 0;
   q.hmax_fill = P.max_fill;
-  q.n_i64 = P.n_i64; q.n_f64 = P.n_f64; q.n_min = P.n_min; q.n_max = P.n_max;
+  q.n_i64 = P.n_i64; q.n_fx = P.n_fx; q.n_min = P.n_min; q.n_max = P.n_max;
   q.dc_row_words = P.bit_words;
-  q.use_lds = P.mode == GM_DENSE && G * 8ull * (P.n_i64 + P.n_f64 + P.n_min + P.n_max) <= (uint64_t)kLdsGroupBytes;
+  // aggregation-only plans with SK_FX sums use a one-slot LDS table for them (pg_scan.hip acc_update)
+  q.use_lds = (P.mode == GM_DENSE || (P.mode == GM_NONE && P.n_fx)) &&
+              P.num_slots * 8ull * (P.n_i64 + 2ull * P.n_fx + P.n_min + P.n_max) <= (uint64_t)kLdsGroupBytes;
   // ---- radix-partitioned dense group-by (pg_part.hip) for a dense key space whose state is far larger than any
   // cache, when the aggregations are COUNTs and at most one DISTINCTCOUNT (entries of key low bits | value id fit 32
   // bits).  PG_PART=0|1 overrides the size threshold.
@@ -1648,7 +1719,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     const char* part_env = getenv("PG_PART");
     const int pe = part_env ? atoi(part_env) : -1;
     uint32_t dc = (uint32_t)kNoSlot, ndc = 0;
-    bool ok = P.mode == GM_DENSE && !q.use_lds && K > 0 && P.n_i64 == 1 && !P.n_f64 && !P.n_min && !P.n_max &&
+    bool ok = P.mode == GM_DENSE && !q.use_lds && K > 0 && P.n_i64 == 1 && !P.n_fx && !P.n_min && !P.n_max &&
               total_docs > 0 && total_docs < 0xFFFFFFF0ull && pe != 0;
     for (uint32_t a = 0; a < A && ok; a++) {
       if (P.aggs[a].fn == PG_AGG_DISTINCTCOUNT) { dc = a; ndc++; }
@@ -2824,6 +2895,11 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       bool neg[kIdxMaxLeaves] = {};
       for (uint64_t k = 0; k < ix.leaves.size(); k++)
         if (ix.leaves[k].kind == IL_ROARING && ix.leaves[k].negate) neg[k % L] = true;
+      // only a leaf the program references ONCE may read the OR's union: `a AND (a OR c)` references leaf a twice,
+      // and its AND must see a's own docs
+      uint32_t refs[kIdxMaxLeaves] = {};
+      for (uint32_t i = 0; i < plan->num_ops; i++)
+        if (plan->ops[i] >= 0 && (uint32_t)plan->ops[i] < kIdxMaxLeaves) refs[plan->ops[i]]++;
       uint32_t rep[kIdxMaxLeaves];
       for (uint32_t l = 0; l < kIdxMaxLeaves; l++) rep[l] = l;
       auto share = [&](const uint32_t* codes, uint32_t n) {
@@ -2832,7 +2908,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
           const uint32_t c = codes[k];
           if (c & 0xC0000000u) continue;  // a group or a negated item
           const uint32_t l = c & 0xFFu;
-          if (l >= L || neg[l] || sp2.chunk_of[l] == 0xFFFFFFFFu) continue;
+          if (l >= L || neg[l] || refs[l] != 1 || sp2.chunk_of[l] == 0xFFFFFFFFu) continue;
           if (first < 0) first = (int)l; else rep[l] = (uint32_t)first;
         }
       };
@@ -2902,7 +2978,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   {
     const StateView v = P.view();
     q.i64 = v.i64;
-    q.f64 = v.f64;
+    q.fx = v.fx;
     q.mn = v.mn;
     q.mx = v.mx;
     q.dbits = v.bits;
@@ -3362,14 +3438,14 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   rb.add(P.seg_matched.p, t_ctx.readback.dev(sm), 8ull * n_sm);
   P.host_state = false;
   if (t_prefetch_state && (P.mode == GM_DENSE || P.mode == GM_NONE) && !P.bit_words &&
-      P.num_slots * 8ull * (P.n_i64 + P.n_f64 + P.n_min + P.n_max) <= kHostFinalBytes) {
+      P.num_slots * 8ull * (P.n_i64 + 2ull * P.n_fx + P.n_min + P.n_max) <= kHostFinalBytes) {
     const uint64_t G = P.num_slots;
-    const uint64_t b64 = G * 8ull * P.n_i64, bf = G * 8ull * P.n_f64, bmn = G * 8ull * P.n_min, bmx = G * 8ull * P.n_max;
+    const uint64_t b64 = G * 8ull * P.n_i64, bf = G * 16ull * P.n_fx, bmn = G * 8ull * P.n_min, bmx = G * 8ull * P.n_max;
     uint8_t* h = (uint8_t*)t_ctx.state_host.get(b64 + bf + bmn + bmx + 8);
     if (h) {
       const PinnedBuf& sh = t_ctx.state_host;
       if (b64) rb.add(P.i64.p, sh.dev(h), b64);
-      if (bf) rb.add(P.f64.p, sh.dev(h + b64), bf);
+      if (bf) rb.add(P.fx.p, sh.dev(h + b64), bf);
       if (bmn) rb.add(P.mn.p, sh.dev(h + b64 + bf), bmn);
       if (bmx) rb.add(P.mx.p, sh.dev(h + b64 + bf + bmn), bmx);
       P.host_state = true;
@@ -3419,7 +3495,10 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     if (err & 8u) return kRetryNoStream;     // more stream survivors than the regions hold: rerun without it
     if (err & 16u) return kRetryExactPart;   // a speculative partition region overflowed: rerun with exact offsets
     if (err & 4u) return kRetryLargerTable;  // hash table over its fill budget: rerun with a larger one
-    if (err) return fail(PG_E_INVALID, "device bounds check failed (code %u): a key fell outside the plan's key space", err);
+    if (err & 64u)  // pg_filter.hip: the exact-mode stream kernel found its LDS LUT at a nonzero base address
+      return fail(PG_E_INVALID, "stream kernel LDS layout check failed (code %u): the exact LUT is not at LDS offset 0", err);
+    if (err) return fail(PG_E_INVALID, "device bounds check failed (code %u): a %s fell outside the plan's key space", err,
+                         (err & 2u) && !(err & 1u) ? "DISTINCTCOUNT value" : "group key");
   }
   stats.num_entries_scanned_post_filter = (stats.num_docs_scanned - ns_docs) * P.projected_cols;
   if (P.mode == GM_HASH_SEG) {
@@ -3626,13 +3705,15 @@ void fill_handle(pg_partials* p, PartialsImpl* impl) {
   Partials& P = impl->P;
   p->num_slots = P.num_slots;
   p->mode = P.mode == GM_HASH ? PG_STATE_HASH : PG_STATE_DENSE;
-  p->n_i64 = P.n_i64; p->n_f64 = P.n_f64; p->n_min = P.n_min; p->n_max = P.n_max;
+  p->n_i64 = P.n_i64; p->n_fx = P.n_fx; p->n_min = P.n_min; p->n_max = P.n_max;
   p->bitmap_words = P.bit_words;
   p->layout = P.layout;
+  p->fx_sig = P.fx_sig();
+  p->flags = P.flags;
   p->row_bytes = row_bytes(P.view());
   p->keys = (uint64_t*)P.keys.p;
   p->i64 = (int64_t*)P.i64.p;
-  p->f64 = (double*)P.f64.p;
+  p->fx = (int64_t*)P.fx.p;
   p->mn = (int64_t*)P.mn.p;
   p->mx = (int64_t*)P.mx.p;
   p->bitmaps = (uint32_t*)P.bits.p;
@@ -3741,7 +3822,7 @@ void order_rows(const pg_plan* plan, const Partials& P, uint64_t nc, const std::
 
 int build_result(pg_partials* pp, const pg_plan* plan, pg_result** out, const Partials& P, uint64_t nc,
                  const std::vector<uint64_t>& hk, const std::vector<double>& hv, const std::vector<int64_t>& hc,
-                 bool sets, const std::vector<uint64_t>& hoff, const uint32_t* hids, uint64_t n_ids);
+                 bool sets, const std::vector<uint64_t>& hoff, const uint32_t* hids, uint64_t n_ids, uint64_t merged);
 
 
 // finalize() for small dense states without DISTINCTCOUNT: the same groups, final values and ORDER BY candidates
@@ -3751,7 +3832,7 @@ int finalize_small(pg_partials* pp, const pg_plan* plan, pg_result** out, const 
   const StateView v = P.view();
   const uint32_t A = plan->num_aggs, K = plan->num_keys;
   const uint64_t G = P.num_slots;
-  const uint64_t b64 = G * 8ull * v.n_i64, bf = G * 8ull * v.n_f64, bmn = G * 8ull * v.n_min, bmx = G * 8ull * v.n_max;
+  const uint64_t b64 = G * 8ull * v.n_i64, bf = G * 16ull * v.n_fx, bmn = G * 8ull * v.n_min, bmx = G * 8ull * v.n_max;
   uint8_t* h;
   if (P.host_state) {  // copied back with the scan's match counts (pg_execute): no device work left
     h = (uint8_t*)t_ctx.state_host.p;
@@ -3760,7 +3841,7 @@ int finalize_small(pg_partials* pp, const pg_plan* plan, pg_result** out, const 
     h = (uint8_t*)t_ctx.readback.get(b64 + bf + bmn + bmx + 8);
     if (!h) return fail(PG_E_NOMEM, "pinned readback failed");
     HIP_CHECK(hipMemcpyAsync(h, v.i64, b64, hipMemcpyDeviceToHost, s));
-    if (bf) HIP_CHECK(hipMemcpyAsync(h + b64, v.f64, bf, hipMemcpyDeviceToHost, s));
+    if (bf) HIP_CHECK(hipMemcpyAsync(h + b64, v.fx, bf, hipMemcpyDeviceToHost, s));
     if (bmn) HIP_CHECK(hipMemcpyAsync(h + b64 + bf, v.mn, bmn, hipMemcpyDeviceToHost, s));
     if (bmx) HIP_CHECK(hipMemcpyAsync(h + b64 + bf + bmn, v.mx, bmx, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipEventRecord(e1, s));
@@ -3770,7 +3851,7 @@ int finalize_small(pg_partials* pp, const pg_plan* plan, pg_result** out, const 
     t_timing.finalize_ms = fm;
   }
   const uint64_t* i64 = (const uint64_t*)h;
-  const double* f64 = (const double*)(h + b64);
+  const uint64_t* fx = (const uint64_t*)(h + b64);
   const int64_t* mn = (const int64_t*)(h + b64 + bf);
   const int64_t* mx = (const int64_t*)(h + b64 + bf + bmn);
   // 1. the groups (aggregation-only: slot 0, always one row) and 2. their final values (final_values_kernel)
@@ -3790,7 +3871,13 @@ int finalize_small(pg_partials* pp, const pg_plan* plan, pg_result** out, const 
         case PG_AGG_COUNTMV: x = (double)(int64_t)i64[sl * v.n_i64 + g.slot]; break;
         case PG_AGG_SUM:
         case PG_AGG_AVG:
-          x = g.integer ? (double)(int64_t)i64[sl * v.n_i64 + g.slot] : f64[sl * v.n_f64 + g.slot];
+          if (g.integer) {
+            x = (double)(int64_t)i64[sl * v.n_i64 + g.slot];
+          } else {
+            const uint64_t* w = fx + (sl * v.n_fx + g.slot) * 2;
+            x = fx_final(g, w[0], w[1], g.sp_min != kNoSp ? mn[sl * v.n_min + g.sp_min] : 0,
+                         g.sp_max != kNoSp ? mx[sl * v.n_max + g.sp_max] : 0);
+          }
           if (g.fn == PG_AGG_AVG) c = count;
           break;
         case PG_AGG_MIN: x = order_key_decode(mn[sl * v.n_min + g.slot]); break;
@@ -3802,6 +3889,7 @@ int finalize_small(pg_partials* pp, const pg_plan* plan, pg_result** out, const 
     if (!K) break;
   }
   uint64_t nc = hk.size();
+  const uint64_t merged = nc;
   // 3. ORDER BY trim: the candidates whose first-ORDER-BY image is <= the limit-th smallest (order_keys_kernel)
   if (K && plan->num_order && plan->limit && nc > plan->limit) {
     std::vector<uint64_t> ok(nc);
@@ -3834,7 +3922,7 @@ int finalize_small(pg_partials* pp, const pg_plan* plan, pg_result** out, const 
     hv.resize(nc * A);
     hc.resize(nc * A);
   }
-  return build_result(pp, plan, out, P, nc, hk, hv, hc, false, {}, nullptr, 0);
+  return build_result(pp, plan, out, P, nc, hk, hv, hc, false, {}, nullptr, 0, merged);
 }
 
 // Partial state -> host result: the groups present (doc count > 0), their final values, the plan's ORDER BY trim
@@ -3902,7 +3990,7 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
 
   bool any_dc = false;
   for (uint32_t a = 0; a < A; a++) any_dc |= P.aggs[a].fn == PG_AGG_DISTINCTCOUNT;
-  const uint64_t row_words = (uint64_t)v.n_i64 + v.n_f64 + v.n_min + v.n_max;
+  const uint64_t row_words = (uint64_t)v.n_i64 + 2ull * v.n_fx + v.n_min + v.n_max;
   if ((P.mode == GM_DENSE || P.mode == GM_NONE) && !any_dc && P.num_slots * row_words * 8 <= kHostFinalBytes) {
     if (!P.host_state) HIP_CHECK(hipEventRecord(e0, s));  // (a state already on the host needs no device time)
     return finalize_small(pp, plan, out, P, f, e0, e1, s);
@@ -3918,7 +4006,7 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
                         f.order_kind == PG_ORDER_AGG && f.order_index < A && v.dc_pop_agg == f.order_index &&
                         f.aggs[f.order_index].fn == PG_AGG_DISTINCTCOUNT && f.aggs[f.order_index].key_card < 8192 &&
                         !(tp_env && atoi(tp_env) == 0);
-  uint64_t nc = 0;
+  uint64_t nc = 0, merged = 0;  // merged: the groups present before the trim
   const uint64_t* ck = nullptr;
   const double* cv = nullptr;
   const int64_t* cc = nullptr;
@@ -3938,6 +4026,7 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
     HIP_CHECK(hipStreamSynchronize(s));
     uint64_t present = 0;
     for (uint32_t x = 0; x <= maxv; x++) present += hh[x];
+    merged = present;
     if (present > plan->limit) {
       // the limit-th group's size in the ORDER BY direction; every group tied with it stays a candidate
       uint64_t cum = 0;
@@ -3987,6 +4076,7 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
       if ((rc = read_back(d_num, n32, s))) return rc;
       n = n32;
     }
+    merged = n;
     PG_PROF("f_groups");
     // 2. final values (a radix-select trim orders the groups by an image read straight from the state, and computes the
     // final values of its candidates only)
@@ -4157,7 +4247,7 @@ int finalize_core(pg_partials* pp, const pg_plan* plan, pg_result** out) {
   float fm = 0;
   (void)hipEventElapsedTime(&fm, e0, e1);
   t_timing.finalize_ms = fm;
-  return build_result(pp, plan, out, P, nc, hk, hv, hc, sets, hoff, hids, n_ids);
+  return build_result(pp, plan, out, P, nc, hk, hv, hc, sets, hoff, hids, n_ids, merged);
 }
 
 // Host order of the candidates (every ORDER BY item, then the packed key: a total order) and the result rows.
@@ -4197,7 +4287,7 @@ void res_free(void* p) {
 
 int build_result(pg_partials* pp, const pg_plan* plan, pg_result** out, const Partials& P, uint64_t nc,
                  const std::vector<uint64_t>& hk, const std::vector<double>& hv, const std::vector<int64_t>& hc,
-                 bool sets, const std::vector<uint64_t>& hoff, const uint32_t* hids, uint64_t n_ids) {
+                 bool sets, const std::vector<uint64_t>& hoff, const uint32_t* hids, uint64_t n_ids, uint64_t merged) {
   if (P.wide && P.wide->user_plan) plan = P.wide->user_plan;  // the caller's K keys and ORDER BY
   const uint32_t A = plan->num_aggs, K = plan->num_keys;
   const uint32_t AA = A ? A : 1;
@@ -4228,6 +4318,12 @@ int build_result(pg_partials* pp, const pg_plan* plan, pg_result** out, const Pa
   pg_result* r = (pg_result*)calloc(1, sizeof(pg_result));
   if (!r) return fail(PG_E_NOMEM, "out of host memory");
   r->stats = pp->stats;  // local, or merged across ranks by the caller before finalize
+  r->num_groups_merged = K ? merged : nc;
+  r->flags = pp->flags & (PG_RESULT_GROUPS_LIMIT_REACHED | PG_RESULT_TRIM_THRESHOLD_REACHED);
+  // the reference's ConcurrentIndexedTable resizes whenever it holds >= trimThreshold records: before its first resize
+  // it holds every merged key, so a resize happened iff the merged groups reach the threshold
+  if (K && plan->num_order && plan->trim_threshold && merged >= plan->trim_threshold)
+    r->flags |= PG_RESULT_TRIM_THRESHOLD_REACHED;
   r->num_keys = K;
   r->num_aggs = A;
   r->num_groups = nc;
@@ -4361,6 +4457,7 @@ int decode_image(const void* image, uint64_t n, PlanImage& out) {
   p.num_order = h.num_order;
   p.order = order;
   p.limit = h.limit;
+  p.trim_threshold = h.trim_threshold;
   return PG_OK;
 }
 
@@ -4496,7 +4593,7 @@ int pg_partials_free(pg_partials* p) {
   return PG_OK;
 }
 
-int pg_partials_copy(pg_partials* p, int dir, void* i64, void* f64, void* mn, void* mx, void* stream) {
+int pg_partials_copy(pg_partials* p, int dir, void* i64, void* fx, void* mn, void* mx, void* stream) {
   int rc = ensure_device();
   if (rc) return rc;
   if (!p || !p->impl || (dir != PG_COPY_OUT && dir != PG_COPY_IN)) return fail(PG_E_INVALID, "bad partials / direction");
@@ -4504,12 +4601,14 @@ int pg_partials_copy(pg_partials* p, int dir, void* i64, void* f64, void* mn, vo
   if (((PartialsImpl*)p->impl)->P.wide)
     return fail(PG_E_UNSUPPORTED, "wide group keys are tuple slots local to one state: no cross-state merge");
   hipStream_t s = stream ? (hipStream_t)stream : thread_stream();
-  void* mine[4] = {p->i64, p->f64, p->mn, p->mx};
-  void* theirs[4] = {i64, f64, mn, mx};
-  const uint64_t bytes[4] = {p->num_slots * 8ull * p->n_i64, p->num_slots * 8ull * p->n_f64,
+  void* mine[4] = {p->i64, p->fx, p->mn, p->mx};
+  void* theirs[4] = {i64, fx, mn, mx};
+  const uint64_t bytes[4] = {p->num_slots * 8ull * p->n_i64, p->num_slots * 16ull * p->n_fx,
                              p->num_slots * 8ull * p->n_min, p->num_slots * 8ull * p->n_max};
+  if (fx && p->n_fx)  // the exact sums travel as 32-bit limbs (4 per sum): a word-wise SUM merges those
+    HIP_CHECK(launch_fx_limbs((unsigned long long*)p->fx, (long long*)fx, p->num_slots * p->n_fx, dir == PG_COPY_IN, s));
   for (int i = 0; i < 4; i++) {
-    if (!theirs[i] || !bytes[i]) continue;
+    if (i == 1 || !theirs[i] || !bytes[i]) continue;
     if (dir == PG_COPY_OUT) HIP_CHECK(hipMemcpyAsync(theirs[i], mine[i], bytes[i], hipMemcpyDeviceToDevice, s));
     else HIP_CHECK(hipMemcpyAsync(mine[i], theirs[i], bytes[i], hipMemcpyDeviceToDevice, s));
   }

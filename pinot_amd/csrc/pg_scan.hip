@@ -462,10 +462,13 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
 }
-__device__ __forceinline__ double wave_sum_f64(double v) {
+// exact 128-bit wave sum of (lo, hi) fixed-point partials (SK_FX): integer adds, so the butterfly's order is irrelevant
+__device__ __forceinline__ void wave_sum_fx(uint64_t& lo, uint64_t& hi) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t xl = __shfl_xor(lo, o), xh = __shfl_xor(hi, o);
+    fx_add(lo, hi, xl, xh);
+  }
 }
 __device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
 #pragma unroll
@@ -564,7 +567,7 @@ template <int MAXK> using GKey = typename std::conditional<(MAXK > 1), uint64_t,
 // Group-state pointers: the block's LDS copy when the table is privatised, else the global arrays.
 struct GroupState {
   unsigned long long* i64;   // GM_PART: the block's LDS entry count + level-1 histogram (uint32 words)
-  double* f64;
+  unsigned long long* fx;    // SK_FX pairs (lo, hi)
   long long* mn;
   long long* mx;
   unsigned long long* out;   // GM_PART: the block's region of the entry array
@@ -573,16 +576,41 @@ struct GroupState {
 __device__ __forceinline__ void s_add(const GroupState& S, unsigned long long* p, unsigned long long v) {
   if (S.lds) l_add(p, v); else g_add(p, v);
 }
-__device__ __forceinline__ void s_addf(const GroupState& S, double* p, double v) {
-  if (S.lds) l_add(p, v); else g_add(p, v);
-}
 __device__ __forceinline__ void s_min(const GroupState& S, long long* p, long long v) {
   if (S.lds) l_min(p, v); else g_min(p, v);
 }
 __device__ __forceinline__ void s_max(const GroupState& S, long long* p, long long v) {
   if (S.lds) l_max(p, v); else g_max(p, v);
 }
-
+// 128-bit atomic add of (lo, hi) at p[0], p[1]: the low word's carry-out (seen in its old value) goes to the high word,
+// which makes the pair's final value the exact sum in any interleaving of the atomics
+__device__ __forceinline__ void g_addfx(unsigned long long* p, uint64_t lo, uint64_t hi) {
+  const uint64_t old = g_add(p, (unsigned long long)lo);
+  const uint64_t h = hi + (old + lo < old ? 1ull : 0ull);
+  if (h) g_add(p + 1, (unsigned long long)h);
+}
+__device__ __forceinline__ void s_addfx(const GroupState& S, unsigned long long* p, uint64_t lo, uint64_t hi) {
+  if (S.lds) {
+    const uint64_t old = l_add(p, (unsigned long long)lo);
+    const uint64_t h = hi + (old + lo < old ? 1ull : 0ull);
+    if (h) l_add(p + 1, (unsigned long long)h);
+  } else {
+    g_addfx(p, lo, hi);
+  }
+}
+// One SK_FX input: its exact fixed-point value into the pair, or (+-inf / NaN) its order image into the special slots
+__device__ __forceinline__ void fx_update(const QuerySpec& q, const GroupState& S, const AggSpec& A, uint64_t g,
+                                          double v) {
+  if (__builtin_isfinite(v)) {
+    uint64_t lo, hi;
+    fx_from_double(v, A.fx_shift, lo, hi);
+    s_addfx(S, &S.fx[(g * q.n_fx + A.slot) * 2], lo, hi);
+  } else if (A.sp_min != kNoSp) {
+    const long long k = (long long)order_key(v);
+    s_min(S, &S.mn[g * q.n_min + A.sp_min], k);
+    s_max(S, &S.mx[g * q.n_max + A.sp_max], k);
+  }
+}
 // Per-doc update of one aggregation in group slot g (aggregateGroupBySV of each function).
 __device__ __forceinline__ void group_update(const QuerySpec& q, const GroupState& S, const AggSpec& A,
                                              const ColDesc* c, uint64_t g, uint32_t d, uint32_t ia, uint32_t ib) {
@@ -594,7 +622,7 @@ __device__ __forceinline__ void group_update(const QuerySpec& q, const GroupStat
     case PG_AGG_SUM:
     case PG_AGG_AVG:  // AVG count == slot 0
       if (A.integer) s_add(S, &S.i64[g * q.n_i64 + A.slot], (unsigned long long)value_i64(A, c, ia, ib));
-      else s_addf(S, &S.f64[g * q.n_f64 + A.slot], value_f64(A, c, ia, ib));
+      else fx_update(q, S, A, g, value_f64(A, c, ia, ib));
       break;
     case PG_AGG_MIN: s_min(S, &S.mn[g * q.n_min + A.slot], (long long)order_key(value_f64(A, c, ia, ib))); break;
     case PG_AGG_MAX: s_max(S, &S.mx[g * q.n_max + A.slot], (long long)order_key(value_f64(A, c, ia, ib))); break;
@@ -608,15 +636,17 @@ __device__ __forceinline__ void group_update(const QuerySpec& q, const GroupStat
 }
 
 // Per-doc update of one aggregation-only accumulator (aggregate() of each function; COUNT = doc count).
-__device__ __forceinline__ void acc_update(const QuerySpec& q, const AggSpec& A, const ColDesc* c, uint64_t& acc,
-                                           uint32_t d, uint32_t ia, uint32_t ib) {
+// SK_FX sums go to the block's one-slot LDS table S (use_lds): a 128-bit accumulator per thread would cost the
+// aggregation-only shapes registers they do not have.
+__device__ __forceinline__ void acc_update(const QuerySpec& q, const GroupState& S, const AggSpec& A, const ColDesc* c,
+                                           uint64_t& acc, uint32_t d, uint32_t ia, uint32_t ib) {
   switch (A.fn) {
     case PG_AGG_COUNT: break;
     case PG_AGG_COUNTMV: acc += glb(ldc(c, 0).mv_offsets)[d + 1] - glb(ldc(c, 0).mv_offsets)[d]; break;
     case PG_AGG_SUM:
     case PG_AGG_AVG:
       if (A.integer) acc += (uint64_t)value_i64(A, c, ia, ib);
-      else acc = __double_as_longlong(__longlong_as_double(acc) + value_f64(A, c, ia, ib));
+      else fx_update(q, S, A, 0, value_f64(A, c, ia, ib));
       break;
     case PG_AGG_MIN: {
       const int64_t k = order_key(value_f64(A, c, ia, ib));
@@ -673,8 +703,7 @@ __device__ __forceinline__ void agg_rows8(const QuerySpec& q, const GroupState& 
 #pragma unroll
         for (int r = 0; r < 8; r++) {
           if (!((live >> r) & 1u)) continue;
-          if constexpr (GROUPED) s_addf(S, &S.f64[(uint64_t)g[r] * q.n_f64 + A.slot], v[r]);
-          else acc = __double_as_longlong(__longlong_as_double(acc) + v[r]);
+          fx_update(q, S, A, GROUPED ? (uint64_t)g[r] : 0ull, v[r]);
         }
       }
       break;
@@ -701,7 +730,7 @@ __device__ __forceinline__ void agg_rows8(const QuerySpec& q, const GroupState& 
       for (int r = 0; r < 8; r++) {
         if (!((live >> r) & 1u)) continue;
         if constexpr (GROUPED) group_update(q, S, A, c, g[r], d[r], ia[r], ib[r]);
-        else acc_update(q, A, c, acc, d[r], ia[r], ib[r]);
+        else acc_update(q, S, A, c, acc, d[r], ia[r], ib[r]);
       }
       break;
   }
@@ -884,7 +913,7 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
 #pragma unroll
         for (int a = 0; a < MAXA; a++) {
           if (a >= (int)q.num_aggs) break;
-          acc_update(q, q.aggs[a], sd.aggcols + 2 * a, acc[a], d[x], ia[x][a], ib[x][a]);
+          acc_update(q, S, q.aggs[a], sd.aggcols + 2 * a, acc[a], d[x], ia[x][a], ib[x][a]);
         }
       }
     }
@@ -905,11 +934,15 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
 
 // LDS layout of a launch: [16 B][staging ring][IN sets][group table at a 16-byte boundary][queue]
 __host__ __device__ inline size_t scan_groups_off(const QuerySpec& q) {
-  return (16 + (size_t)q.stage_ring * q.stage_lds_words * 4 + (size_t)q.set_lds_ints * 4 + 15) & ~(size_t)15;
+  size_t off = 16 + (size_t)q.stage_ring * q.stage_lds_words * 4 + (size_t)q.set_lds_ints * 4;
+  // aggregation-only with a one-slot table (SK_FX sums): past the block reduction's words, which reuse the ring
+  const size_t red = 16 + (size_t)(kBlock / 64) * (1 + kMaxAggs) * 8;
+  if (!q.num_keys && q.use_lds && off < red) off = red;
+  return (off + 15) & ~(size_t)15;
 }
 __host__ __device__ inline size_t scan_queue_off(const QuerySpec& q) {
   const size_t g = (q.num_keys && q.group_mode == GM_PART) ? (1 + q.part_nparts) * 4ull
-                   : (q.num_keys && q.use_lds) ? q.num_slots * 8ull * (q.n_i64 + q.n_f64 + q.n_min + q.n_max) : 0;
+                   : q.use_lds ? q.num_slots * 8ull * (q.n_i64 + 2 * q.n_fx + q.n_min + q.n_max) : 0;
   return scan_groups_off(q) + ((g + 15) & ~(size_t)15);
 }
 
@@ -926,14 +959,14 @@ __device__ __forceinline__ void scan_body() {
   const uint32_t lane = (uint32_t)tid & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
 
-  // LDS-privatised group table: [G][n_i64] u64 | [G][n_f64] f64 | [G][n_min] i64 | [G][n_max] i64
+  // LDS-privatised group table: [G][n_i64] u64 | [G][n_fx][2] u64 | [G][n_min] i64 | [G][n_max] i64
   unsigned long long* l_i64 = (unsigned long long*)lds_groups;
-  double* l_f64 = (double*)(l_i64 + q.num_slots * q.n_i64);
-  long long* l_mn = (long long*)(l_f64 + q.num_slots * q.n_f64);
+  unsigned long long* l_fx = l_i64 + q.num_slots * q.n_i64;
+  long long* l_mn = (long long*)(l_fx + q.num_slots * q.n_fx * 2);
   long long* l_mx = l_mn + q.num_slots * q.n_min;
-  if (GROUPED && q.use_lds) {
+  if (q.use_lds) {  // (aggregation-only: one slot for SK_FX sums and their special slots)
     for (uint64_t i = tid; i < q.num_slots * q.n_i64; i += kBlock) l_i64[i] = 0;
-    for (uint64_t i = tid; i < q.num_slots * q.n_f64; i += kBlock) l_f64[i] = 0.0;
+    for (uint64_t i = tid; i < q.num_slots * q.n_fx * 2; i += kBlock) l_fx[i] = 0;
     for (uint64_t i = tid; i < q.num_slots * q.n_min; i += kBlock) l_mn[i] = order_key(__builtin_inf());
     for (uint64_t i = tid; i < q.num_slots * q.n_max; i += kBlock) l_mx[i] = order_key(-__builtin_inf());
   }
@@ -945,8 +978,8 @@ __device__ __forceinline__ void scan_body() {
     __syncthreads();
   }
   const GroupState S = (q.use_lds || part)
-                           ? GroupState{l_i64, l_f64, l_mn, l_mx, part ? q.part_out + q.part_base[blockIdx.x] : nullptr, true}
-                           : GroupState{q.i64, q.f64, q.mn, q.mx, nullptr, false};
+                           ? GroupState{l_i64, l_fx, l_mn, l_mx, part ? q.part_out + q.part_base[blockIdx.x] : nullptr, true}
+                           : GroupState{q.i64, q.fx, q.mn, q.mx, nullptr, false};
 
   // aggregation-only accumulators (registers; indices compile-time via unrolled agg loops)
   uint64_t acc[MAXA];
@@ -1144,26 +1177,26 @@ __device__ __forceinline__ void scan_body() {
     // wave-reduce, then the block's waves combine through LDS: one global atomic per block per slot
     __syncthreads();  // the staging ring is free
     uint64_t* red = (uint64_t*)stage;  // [wave][1 + MAXA]
+    constexpr int RW = 1 + MAXA;
     const uint64_t dc = wave_sum_u64(doc_count);
-    if (lane == 0) red[wave * (1 + MAXA)] = dc;
+    if (lane == 0) red[wave * RW] = dc;
 #pragma unroll
     for (int a = 0; a < MAXA; a++) {
       if (a >= (int)q.num_aggs) break;
       uint64_t v = 0;
       switch (q.aggs[a].kind) {
         case SK_I64: v = wave_sum_u64(acc[a]); break;
-        case SK_F64: v = (uint64_t)__double_as_longlong(wave_sum_f64(__longlong_as_double(acc[a]))); break;
         case SK_MIN: v = (uint64_t)wave_min_i64((int64_t)acc[a]); break;
         case SK_MAX: v = (uint64_t)wave_max_i64((int64_t)acc[a]); break;
-        default: break;
+        default: break;  // SK_FX: the LDS slot below
       }
-      if (lane == 0) red[wave * (1 + MAXA) + 1 + a] = v;
+      if (lane == 0) red[wave * RW + 1 + a] = v;
     }
     __syncthreads();
     constexpr int NW = kBlock / 64;
     if (tid == 0) {
       uint64_t t = 0;
-      for (int w = 0; w < NW; w++) t += red[w * (1 + MAXA)];
+      for (int w = 0; w < NW; w++) t += red[w * RW];
       if (t) atomicAdd(&q.i64[0], (unsigned long long)t);
     } else if (tid <= MAXA && tid <= (int)q.num_aggs) {
       const int a = tid - 1;
@@ -1171,30 +1204,30 @@ __device__ __forceinline__ void scan_body() {
       switch (A.kind) {
         case SK_I64: {
           uint64_t t = 0;
-          for (int w = 0; w < NW; w++) t += red[w * (1 + MAXA) + 1 + a];
+          for (int w = 0; w < NW; w++) t += red[w * RW + 1 + a];
           if (t) atomicAdd(&q.i64[A.slot], (unsigned long long)t);
-          break;
-        }
-        case SK_F64: {
-          double t = 0.0;
-          for (int w = 0; w < NW; w++) t += __longlong_as_double((long long)red[w * (1 + MAXA) + 1 + a]);
-          if (t != 0.0) atomicAdd(&q.f64[A.slot], t);
           break;
         }
         case SK_MIN: {
           int64_t t = (int64_t)red[1 + a];
-          for (int w = 1; w < NW; w++) t = min(t, (int64_t)red[w * (1 + MAXA) + 1 + a]);
+          for (int w = 1; w < NW; w++) t = min(t, (int64_t)red[w * RW + 1 + a]);
           atomicMin(&q.mn[A.slot], (long long)t);
           break;
         }
         case SK_MAX: {
           int64_t t = (int64_t)red[1 + a];
-          for (int w = 1; w < NW; w++) t = max(t, (int64_t)red[w * (1 + MAXA) + 1 + a]);
+          for (int w = 1; w < NW; w++) t = max(t, (int64_t)red[w * RW + 1 + a]);
           atomicMax(&q.mx[A.slot], (long long)t);
           break;
         }
         default: break;
       }
+    }
+    if (q.use_lds && tid == 0) {  // the one-slot LDS table: SK_FX sums and their special slots
+      for (uint32_t s = 0; s < q.n_fx; s++)
+        if (l_fx[2 * s] | l_fx[2 * s + 1]) g_addfx(&q.fx[2 * s], l_fx[2 * s], l_fx[2 * s + 1]);
+      for (uint32_t s = 0; s < q.n_min; s++) atomicMin(&q.mn[s], l_mn[s]);
+      for (uint32_t s = 0; s < q.n_max; s++) atomicMax(&q.mx[s], l_mx[s]);
     }
   } else if (part) {
     __syncthreads();
@@ -1209,7 +1242,10 @@ __device__ __forceinline__ void scan_body() {
         const unsigned long long v = l_i64[g * q.n_i64 + s];
         if (v) atomicAdd(&q.i64[g * q.n_i64 + s], v);
       }
-      for (uint32_t s = 0; s < q.n_f64; s++) atomicAdd(&q.f64[g * q.n_f64 + s], l_f64[g * q.n_f64 + s]);
+      for (uint32_t s = 0; s < q.n_fx; s++) {
+        const uint64_t lo = l_fx[(g * q.n_fx + s) * 2], hi = l_fx[(g * q.n_fx + s) * 2 + 1];
+        if (lo | hi) g_addfx(&q.fx[(g * q.n_fx + s) * 2], lo, hi);
+      }
       for (uint32_t s = 0; s < q.n_min; s++) atomicMin(&q.mn[g * q.n_min + s], l_mn[g * q.n_min + s]);
       for (uint32_t s = 0; s < q.n_max; s++) atomicMax(&q.mx[g * q.n_max + s], l_mx[g * q.n_max + s]);
     }

@@ -14,8 +14,9 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from . import abi
-from .plan import (CPlan, ExecutionStats, InstanceConfig, IntermediateResult, Table, UnsupportedQuery,
-                   execute_filtered, group_trim, has_filtered_aggregations, merge_intermediate, top_groups)
+from .plan import (MAX_TRIM_THRESHOLD, CPlan, ExecutionStats, InstanceConfig, IntermediateResult, Table,
+                   UnsupportedQuery, execute_filtered, group_trim, has_filtered_aggregations, merge_intermediate,
+                   top_groups)
 from .query import QueryContext, parse
 from .segment import Column, ImmutableSegment
 
@@ -176,15 +177,14 @@ class GpuEngine:
 
     # ---- execution
     def make_plan(self, table: Table, query: QueryContext, segments: Optional[Sequence[ImmutableSegment]] = None,
-                  num_groups_limit=None, flags: int = abi.PG_PLAN_VALUE_SETS, trim=False,
-                  config: Optional[InstanceConfig] = None) -> CPlan:
+                  flags: int = abi.PG_PLAN_VALUE_SETS, trim=False, config: Optional[InstanceConfig] = None) -> CPlan:
         """flags: PG_PLAN_* (default: DISTINCTCOUNT value sets, the reference's Set intermediate).  trim: see CPlan
         (True: the query's ORDER BY / LIMIT with boundary ties, a final single-server answer; "server": the rows the
-        reference server's combine keeps under `config` and the query options)."""
+        reference server's combine keeps under `config` and the query options).  config: the server instance's
+        settings (numGroupsLimit comes only from there, as in the reference)."""
         segments = list(table.segments if segments is None else segments)
         keys = [self.upload_segment(s, table) for s in segments]
-        plan = CPlan(table, query, segments, keys, num_groups_limit, flags, trim, id_sets=self.dict_id_sets,
-                     config=config)
+        plan = CPlan(table, query, segments, keys, flags, trim, id_sets=self.dict_id_sets, config=config)
         self.upload_keymaps(table, plan, segments, keys)
         return plan
 
@@ -242,17 +242,19 @@ class GpuEngine:
     def merge_rows(self, p, rows_ptr, n: int, stream=None):
         check(self.lib.pg_partials_merge(p, rows_ptr, n, stream))
 
-    def execute(self, table: Table, query, segments=None, num_groups_limit=None, flags: int = abi.PG_PLAN_VALUE_SETS,
-                trim=False, config: Optional[InstanceConfig] = None) -> IntermediateResult:
+    def execute(self, table: Table, query, segments=None, flags: int = abi.PG_PLAN_VALUE_SETS, trim=False,
+                config: Optional[InstanceConfig] = None) -> IntermediateResult:
         if isinstance(query, str):
             query = parse(query)
         if has_filtered_aggregations(query):  # FilteredAggregationOperator: one device plan per filter
-            return execute_filtered(lambda q: self.execute(table, q, segments, num_groups_limit, flags), query)
+            if query.group_by:  # the passes are aggregation-only (FilteredAggregationOperator); no group trim applies
+                raise UnsupportedQuery("filtered aggregations with GROUP BY")
+            return execute_filtered(lambda q: self.execute(table, q, segments, flags, config=config), query)
         if trim == "server" and query.group_by and group_trim(query, config).segment_size is not None:
-            return self._execute_segment_trimmed(table, query, segments, num_groups_limit, flags, config)
-        return self.run_plan(self.make_plan(table, query, segments, num_groups_limit, flags, trim, config))
+            return self._execute_segment_trimmed(table, query, segments, flags, config)
+        return self.run_plan(self.make_plan(table, query, segments, flags, trim, config))
 
-    def _execute_segment_trimmed(self, table, query, segments, num_groups_limit, flags, config) -> IntermediateResult:
+    def _execute_segment_trimmed(self, table, query, segments, flags, config) -> IntermediateResult:
         """minSegmentGroupTrimSize > 0 with an ORDER BY: every segment's group-by result is trimmed to
         getTableCapacity(limit, minSegmentGroupTrimSize) under the ORDER BY before the combine
         (AggregationGroupByOrderByOperator.java:118-132, TableResizer.trimInSegmentResults), so each segment runs as its
@@ -262,16 +264,21 @@ class GpuEngine:
         merged: dict = {}
         stats = ExecutionStats()
         aggs = None
+        limit_reached = False
         for seg in (table.segments if segments is None else segments):
-            r = self.run_plan(self.make_plan(table, query, [seg], num_groups_limit, flags, gt.segment_size, config))
+            r = self.run_plan(self.make_plan(table, query, [seg], flags, gt.segment_size, config))
             aggs = r.aggregations
+            limit_reached |= r.groups_limit_reached
             for k, v in r.rows.items():
                 merged[k] = merge_intermediate(aggs, merged[k], v) if k in merged else v
             for f in stats.__dataclass_fields__:
                 setattr(stats, f, getattr(stats, f) + getattr(r.stats, f))
+        n_merged = len(merged)
         if gt.server_size is not None:
             merged = top_groups(query, aggs, merged, gt.server_size)
-        return IntermediateResult(aggs or query.aggregations, list(query.group_by), merged, stats)
+        return IntermediateResult(aggs or query.aggregations, list(query.group_by), merged, stats, limit_reached,
+                                  bool(gt.ordered and gt.server_size is not None and gt.threshold < MAX_TRIM_THRESHOLD
+                                       and n_merged >= gt.threshold), n_merged)
 
     def last_trace(self) -> dict:
         """pg_last_trace: what the device did for this thread's last call -- the kernels that ran, the form each filter
@@ -328,7 +335,7 @@ class GpuEngine:
         stats = np.array([s.num_docs_scanned, s.num_entries_scanned_in_filter, s.num_entries_scanned_post_filter,
                           s.num_total_docs, s.num_segments_processed, s.num_segments_matched], dtype=np.int64)
         return {"G": G, "K": K, "A": A, "keys": keys, "values": vals, "counts": cnts, "offsets": offs, "ids": ids,
-                "stats": stats}
+                "stats": stats, "flags": int(r.flags), "merged": int(r.num_groups_merged)}
 
     @staticmethod
     def decode(plan: CPlan, r) -> IntermediateResult:
@@ -337,7 +344,12 @@ class GpuEngine:
         are built on first access to `.rows` (DeviceResult)."""
         ra = r if isinstance(r, dict) else GpuEngine.result_arrays(r)
         st = ExecutionStats(*ra["stats"].tolist())
-        return DeviceResult(plan.aggs, list(plan.query.group_by), lambda: GpuEngine._rows(plan, ra), st, ra)
+        out = DeviceResult(plan.aggs, list(plan.query.group_by), lambda: GpuEngine._rows(plan, ra), st, ra)
+        fl = ra.get("flags", 0)
+        out.groups_limit_reached = bool(fl & abi.PG_RESULT_GROUPS_LIMIT_REACHED)
+        out.trim_threshold_reached = bool(fl & abi.PG_RESULT_TRIM_THRESHOLD_REACHED)
+        out.num_groups_merged = ra.get("merged")
+        return out
 
     @staticmethod
     def _rows(plan: CPlan, ra: dict) -> dict:

@@ -17,7 +17,9 @@ from __future__ import annotations
 
 import ctypes as C
 import itertools
+import math
 import os
+import threading
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -36,6 +38,7 @@ DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY = 10_000  # InstancePlanMakerImplV2 :73
 DEFAULT_MIN_SEGMENT_GROUP_TRIM_SIZE = -1
 DEFAULT_MIN_SERVER_GROUP_TRIM_SIZE = 5000
 DEFAULT_GROUPBY_TRIM_THRESHOLD = 1_000_000
+MAX_TRIM_THRESHOLD = 1_000_000_000   # GroupByOrderByCombineOperator.MAX_TRIM_THRESHOLD: at or above, no resize at all
 # batched IN / NOT_IN leaves cross as their literals (values mode, pg_leaf.num_values) unless PG_IN_VALUES=0 (ids)
 _IN_VALUES = os.environ.get("PG_IN_VALUES", "1") != "0"
 
@@ -211,6 +214,19 @@ def lower_predicate(pred: Predicate, col: Column, col_id: int, in_ids: Optional[
     return LoweredLeaf(kind, col_id, excl, lo, hi, ids)
 
 
+def sum_bound(table: "Table", e: Expr) -> Tuple[int, bool]:
+    """(pg_agg.sum_exp, PG_SUM_NONFINITE) of a SUM / AVG input: e with 2^e >= |every finite value| of the expression
+    over the table (a*b: the product of the operand bounds, a+b / a-b their sum; an overflow to inf bounds it by
+    DBL_MAX), so every GPU that merges the plan's partial states sums in the same fixed-point unit (e = 0, "let the
+    device derive it", only when every value is 0), and whether some input may be +-inf / NaN."""
+    b = [table.abs_bound(c) for c in e.cols]
+    nonfinite = any(table.has_nonfinite(c) for c in e.cols)
+    v = b[0] if e.op == "COL" else (b[0] * b[1] if e.op == "MUL" else b[0] + b[1])
+    if not math.isfinite(v):
+        v, nonfinite = float(np.finfo(np.float64).max), True
+    return (math.frexp(v)[1] if v > 0 else 0), nonfinite
+
+
 def filter_program(f: Optional[FilterContext]) -> Tuple[List[int], List[Predicate]]:
     """Postfix program over leaves (FilterPlanNode.constructPhysicalOperator's tree, in postfix)."""
     ops: List[int] = []
@@ -248,6 +264,32 @@ class Table:
                     cols.append(c)
         self.column_ids = {c: i for i, c in enumerate(cols)}
         self._key_spaces: Dict[str, "KeySpace"] = {}
+        self._abs_bounds: Dict[str, Tuple[float, bool]] = {}
+
+    def has_nonfinite(self, column: str) -> bool:
+        self.abs_bound(column)
+        return self._abs_bounds[column][1]
+
+    def abs_bound(self, column: str) -> float:
+        """The largest |finite value| of a numeric column over every segment of the table (ColumnMetadata min / max:
+        the dictionary's ends, or a raw column's values) -- the table-global bound of pg_agg.sum_exp."""
+        hit = self._abs_bounds.get(column)
+        if hit is None:
+            b, nonfinite = 0.0, False
+            for seg in self.segments:
+                c = seg.columns.get(column)
+                if c is None:
+                    continue
+                v = np.asarray(c.raw_values if c.dictionary is None else c.dictionary.values)
+                if v.size and v.dtype.kind in "iuf":
+                    a = np.abs(v.astype(np.float64))
+                    fin = np.isfinite(a)
+                    nonfinite |= not bool(fin.all())
+                    a = a[fin]
+                    if a.size:
+                        b = max(b, float(a.max()))
+            hit = self._abs_bounds[column] = (b, nonfinite)
+        return hit[0]
 
     def data_type(self, column: str) -> str:
         return self.segments[0].columns[column].data_type
@@ -341,6 +383,11 @@ class IntermediateResult:
     group_by: List[str]
     rows: Dict[tuple, list]
     stats: ExecutionStats = field(default_factory=ExecutionStats)
+    # IntermediateResultsBlock.isNumGroupsLimitReached: a segment reached the instance's numGroupsLimit
+    groups_limit_reached: bool = False
+    # the server's combine would have resized its IndexedTable mid-merge (groupTrimThreshold; numResizes > 0)
+    trim_threshold_reached: bool = False
+    num_groups_merged: Optional[int] = None   # groups of the combined table before the ORDER BY / limit trim
 
 
 def merge_intermediate(aggs: List[Aggregation], a: list, b: list) -> list:
@@ -434,12 +481,34 @@ def reduce_to_rows(query: QueryContext, res: IntermediateResult) -> Tuple[List[s
 
 @dataclass
 class InstanceConfig:
-    """The pinot.server.query.executor.* settings InstancePlanMakerImplV2.init reads (plan/maker/
-    InstancePlanMakerImplV2.java:100-130): numGroupsLimit, min segment / server group trim sizes, trim threshold."""
+    """The pinot.server.query.executor.* settings InstancePlanMakerImplV2 reads (plan/maker/
+    InstancePlanMakerImplV2.java:67-89 keys, :132-150 the QueryExecutorConfig constructor): num.groups.limit,
+    max.init.group.holder.capacity, min.segment / min.server group trim sizes, groupby.trim.threshold.
+
+    numGroupsLimit is an INSTANCE setting only: applyQueryOptions (:223) sets queryContext.setNumGroupsLimit from it, and
+    QueryOptionsUtils has no such query option -- an OPTION(numGroupsLimit=...) in the SQL changes nothing (as in
+    Pinot 0.11).  The constructor's preconditions hold here too (:138-140, :144-145)."""
     num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT
     min_segment_group_trim_size: int = DEFAULT_MIN_SEGMENT_GROUP_TRIM_SIZE
     min_server_group_trim_size: int = DEFAULT_MIN_SERVER_GROUP_TRIM_SIZE
     groupby_trim_threshold: int = DEFAULT_GROUPBY_TRIM_THRESHOLD
+    max_init_group_holder_capacity: int = DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY
+
+    def __post_init__(self):
+        if self.max_init_group_holder_capacity > self.num_groups_limit:
+            raise ValueError(f"Invalid configuration: maxInitialResultHolderCapacity: "
+                             f"{self.max_init_group_holder_capacity} must be smaller or equal to numGroupsLimit: "
+                             f"{self.num_groups_limit}")
+        if self.groupby_trim_threshold <= 0:
+            raise ValueError(f"Invalid configurable: groupByTrimThreshold: {self.groupby_trim_threshold} must be "
+                             f"positive")
+
+    @staticmethod
+    def with_groups_limit(limit: int, **kw) -> "InstanceConfig":
+        """An instance whose num.groups.limit is `limit` (and max.init.group.holder.capacity lowered to it when it is
+        below the 10 000 default, as the precondition requires)."""
+        return InstanceConfig(num_groups_limit=limit,
+                              max_init_group_holder_capacity=min(DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY, limit), **kw)
 
 
 @dataclass(frozen=True)
@@ -610,9 +679,10 @@ class CPlan:
     """Owns every ctypes array a pg_plan points to (kept alive while the plan is in use)."""
 
     def __init__(self, table: Table, query: QueryContext, segments: Sequence[ImmutableSegment],
-                 seg_keys: Sequence[int], num_groups_limit: Optional[int] = None, flags: int = 0,
-                 trim=False, id_sets=None, config: Optional["InstanceConfig"] = None):
-        """flags: PG_PLAN_*.  trim (group-by only): True -- the device applies the query's ORDER BY / LIMIT (boundary
+                 seg_keys: Sequence[int], flags: int = 0, trim=False, id_sets=None,
+                 config: Optional["InstanceConfig"] = None):
+        """config: the server instance's settings (InstanceConfig; numGroupsLimit, trim sizes, trim threshold).
+        flags: PG_PLAN_*.  trim (group-by only): True -- the device applies the query's ORDER BY / LIMIT (boundary
         ties kept: a final, single-server answer); "server" -- the device keeps exactly the rows the reference server's
         combine keeps (group_trim(query, config): getTableCapacity(limit, minServerGroupTrimSize) under the ORDER BY,
         `limit` groups without one, all of them when the server trim is off); an int -- exactly that many under the
@@ -622,6 +692,7 @@ class CPlan:
         segment on the host."""
         self.table = table
         self.query = query
+        self.config = config or InstanceConfig()
         self.aggs = query.aggregations
         if has_filtered_aggregations(query):
             raise UnsupportedQuery("filtered aggregations run as one plan per filter (execute_filtered)")
@@ -705,6 +776,9 @@ class CPlan:
                     aggs[i].key_kind = ks.kind
                     aggs[i].key_cardinality = ks.cardinality
                     aggs[i].key_base = ks.base
+                if ag.function in ("SUM", "AVG"):
+                    aggs[i].sum_exp, nonfinite = sum_bound(table, e)
+                    aggs[i].sum_flags = abi.PG_SUM_NONFINITE if nonfinite else 0
         self._keep.append(aggs)
         keys = (abi.pg_key * max(len(query.group_by), 1))()
         self.key_spaces = []
@@ -730,9 +804,12 @@ class CPlan:
         p.num_keys = len(query.group_by)
         p.aggs = aggs
         p.keys = keys
-        lim = num_groups_limit or int(query.options.get("numGroupsLimit", DEFAULT_NUM_GROUPS_LIMIT))
-        p.num_groups_limit = lim
+        # InstancePlanMakerImplV2.applyQueryOptions (:223): the instance's num.groups.limit, never a query option
+        p.num_groups_limit = self.config.num_groups_limit
         p.flags = flags
+        gt = group_trim(query, self.config) if query.group_by else None
+        if gt is not None and gt.ordered and gt.server_size is not None and gt.threshold < MAX_TRIM_THRESHOLD:
+            p.trim_threshold = gt.threshold   # flags PG_RESULT_TRIM_THRESHOLD_REACHED when the merge reaches it
         size, exact = query.limit, False
         if trim == "server":   # the reference server's IndexedTable result (group_trim); every group when trim is off
             size, exact = group_trim(query, config).server_size, True
@@ -761,15 +838,26 @@ class CPlan:
 
     def image(self) -> np.ndarray:
         """The plan as one relocatable byte image (pg_image_header + arrays at offsets, include/pinot_gpu.h): what a
-        Java GpuPlanMaker fills in a direct ByteBuffer.  Built once per plan."""
+        Java GpuPlanMaker fills in a direct ByteBuffer.  Built once per plan; each calling thread gets its own copy, whose
+        header carries the per-call scalars (query id, deadline, flags, limits) -- two threads running the same plan
+        with different query ids or deadlines never see each other's values.  `image_addr` is the calling thread's."""
         if self._image is None:
             self._image = abi.build_image(self.plan)
-            self._image_header = abi.pg_image_header.from_buffer(self._image)
-            self.image_addr = self._image.ctypes.data  # stable while _image lives (ndarray.ctypes costs ~3 us a call)
-        h, p = self._image_header, self.plan  # the per-call scalars a caller may set on the plan (cancel id, deadline)
+            self._tls = threading.local()
+        t = self._tls
+        if getattr(t, "image", None) is None:
+            t.image = self._image.copy()
+            t.header = abi.pg_image_header.from_buffer(t.image)
+            t.addr = t.image.ctypes.data  # stable while the copy lives (ndarray.ctypes costs ~3 us a call)
+        h, p = t.header, self.plan  # the per-call scalars a caller may set on the plan (cancel id, deadline)
         h.query_id, h.deadline_ms, h.flags, h.limit = p.query_id, p.deadline_ms, p.flags, p.limit
         h.num_groups_limit = p.num_groups_limit
-        return self._image
+        h.trim_threshold = min(p.trim_threshold, 0xFFFFFFFF)
+        return t.image
+
+    @property
+    def image_addr(self) -> int:
+        return self._tls.addr
 
     @staticmethod
     def _batched_in_ids(preds, segments, seg_keys, cid, id_sets) -> dict:

@@ -63,6 +63,14 @@ def _integer_input(ag, table):
         all(table.data_type(c) in INTEGER_TYPES for c in ag.arg.cols)
 
 
+def _close(x, y, rel):
+    """A double sum within `rel` of the oracle's; NaN matches NaN and an infinity the same infinity (IEEE sums of
+    non-finite inputs are exact in any order)."""
+    if math.isnan(y) or math.isinf(y):
+        return (math.isnan(x) and math.isnan(y)) or x == y
+    return math.isclose(x, y, rel_tol=rel, abs_tol=0)
+
+
 def assert_same_result(a, b, rel=1e-9, table=None):
     """Device result vs oracle result, both IntermediateResult.  Bit-exact for counts / min / max / distinct value sets
     and keys, and for SUM / AVG sums of integer inputs (given `table`) while |sum| < 2^53 (the reference accumulates
@@ -81,12 +89,12 @@ def assert_same_result(a, b, rel=1e-9, table=None):
                 if exact_sum and abs(y[0]) < 2 ** 53:
                     assert x[0] == y[0], (k, ag, x, y)
                 else:
-                    assert math.isclose(x[0], y[0], rel_tol=rel, abs_tol=0), (k, ag, x, y)
+                    assert _close(x[0], y[0], rel), (k, ag, x, y)
             elif ag.function in ("SUM",):
                 if exact_sum and abs(y) < 2 ** 53:
                     assert x == y, (k, ag, x, y)
                 else:
-                    assert math.isclose(x, y, rel_tol=rel, abs_tol=0), (k, ag, x, y)
+                    assert _close(x, y, rel), (k, ag, x, y)
             else:
                 assert x == y, (k, ag, x, y)
     sa, sb = a.stats, b.stats

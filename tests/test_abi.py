@@ -89,10 +89,10 @@ def test_oracle_is_not_linked_into_product():
 def image_from_bytes(**over):
     """A one-segment plan image written with struct.pack alone -- offsets, no pointers -- as a Java GpuPlanMaker fills a
     direct ByteBuffer with putInt / putLong: SELECT COUNT(*) WHERE col0 IN (dictIds 1, 3) over segment key 7.
-    header @0 (120 B) | segment @120 (24 B) | leaf @144 (88 B) | ops @232 | agg @240 (32 B) | ids @272 (2 x int32)."""
+    header @0 (120 B) | segment @120 (24 B) | leaf @144 (88 B) | ops @232 | agg @240 (40 B) | ids @280 (2 x int32)."""
     import struct
-    f = dict(magic=abi.PG_IMAGE_MAGIC, abi=abi.PG_ABI_VERSION, n=280, segments_off=120, leaves_off=144, ops_off=232,
-             aggs_off=240, ids_off=272, num_ids=2, num_segments=1)
+    f = dict(magic=abi.PG_IMAGE_MAGIC, abi=abi.PG_ABI_VERSION, n=288, segments_off=120, leaves_off=144, ops_off=232,
+             aggs_off=240, ids_off=280, num_ids=2, num_segments=1)
     f.update(over)
     b = struct.pack("<IIQ8I4Q5Q", f["magic"], f["abi"], f["n"], f["num_segments"], 1, 1, 1, 0, 0, 0, 0,
                     0, 0, 0, 0, f["segments_off"], f["ops_off"], f["aggs_off"], 0, 0)
@@ -100,9 +100,9 @@ def image_from_bytes(**over):
     b += struct.pack("<4I2iQ2q2d2IQ2I", abi.PG_LEAF_SV_SCAN, 0, 0, f["num_ids"], 0, 0, f["ids_off"], 0, 0, 0.0, 0.0,
                      0, 0, 0, 0, 0)
     b += struct.pack("<i", 0) + bytes(4)
-    b += struct.pack("<6Iq", abi.PG_AGG_COUNT, 0, 0, 0, 0, 0, 0)
+    b += struct.pack("<6Iqi4x", abi.PG_AGG_COUNT, 0, 0, 0, 0, 0, 0, 0)
     b += struct.pack("<2i", 1, 3)
-    assert len(b) == 280
+    assert len(b) == 288
     return b
 
 
@@ -123,14 +123,14 @@ def test_plan_image_from_python_bytes():
     lib = abi.declare(C.CDLL(LIB))
     rc, msg = _run_image(lib, image_from_bytes())
     assert rc == abi.PG_E_STATE, msg
-    bad = [dict(magic=0x1234), dict(abi=abi.PG_ABI_VERSION - 1), dict(n=288), dict(segments_off=272),
-           dict(segments_off=121), dict(leaves_off=250), dict(ids_off=274), dict(ids_off=278),
+    bad = [dict(magic=0x1234), dict(abi=abi.PG_ABI_VERSION - 1), dict(n=296), dict(segments_off=272),
+           dict(segments_off=121), dict(leaves_off=250), dict(ids_off=282), dict(ids_off=284),
            dict(num_ids=0), dict(ops_off=4), dict(aggs_off=256), dict(num_segments=2)]
     for over in bad:
         b = image_from_bytes(**over)
         if "n" in over:
             b = b + bytes(over["n"] - len(b))
-            b = b[:len(b) - 8]  # header says 288, the buffer holds 280
+            b = b[:len(b) - 8]  # header says 296, the buffer holds 288
         rc, msg = _run_image(lib, b)
         assert rc == abi.PG_E_INVALID and msg.startswith("image"), (over, rc, msg)
     rc, msg = _run_image(lib, image_from_bytes(), shift=4)

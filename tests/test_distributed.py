@@ -1,6 +1,8 @@
 """Multi-rank combine on CPU (gloo, world_size 2): the collective logic pinot_amd.combine runs over RCCL on GPUs.
 
-* allreduce_state: SUM / MIN / MAX semantics per dense state array (the device partials' merge).
+* allreduce_state: SUM / MIN / MAX semantics per dense state array (the device partials' merge), including the exact
+  fixed-point double sums as 32-bit limbs (pg_partials_copy's form): one SUM all-reduce, then the carries folded, gives
+  the exact 128-bit sum on every rank.
 * gather_merge_results: sparse value-keyed merge; segments sharded over ranks merge to the single-process answer
   (checked against the CPU oracle over the whole table and the reference's known answers)."""
 import os
@@ -36,7 +38,12 @@ def _worker_state(rank, world, port, q):
     _init(rank, world, port)
     from pinot_amd.combine import allreduce_state
     g = torch.Generator().manual_seed(rank)
-    st = {"i64": torch.randint(0, 1000, (50,), generator=g), "f64": torch.rand(20, generator=g, dtype=torch.float64),
+    rng = np.random.default_rng(100 + rank)
+    # 20 signed 128-bit sums per rank (SK_FX pairs), in pg_partials_copy's limb form: limb k = bits [32k, 32k + 32)
+    vals = [int(x) for x in rng.integers(-(1 << 62), 1 << 62, 20)]
+    vals = [v * (1 << 60) + int(w) for v, w in zip(vals, rng.integers(0, 1 << 60, 20))]
+    limbs = [((v % (1 << 128)) >> (32 * k)) & 0xFFFFFFFF for v in vals for k in range(4)]
+    st = {"i64": torch.cat([torch.randint(0, 1000, (50,), generator=g), torch.tensor(limbs, dtype=torch.int64)]),
           "mn": torch.randint(-100, 100, (30,), generator=g), "mx": torch.randint(-100, 100, (30,), generator=g),
           "stats": torch.tensor([rank + 1] * 6)}
     orig = {k: v.clone() for k, v in st.items()}
@@ -46,13 +53,19 @@ def _worker_state(rank, world, port, q):
         parts = [torch.empty_like(v) for _ in range(world)]
         dist.all_gather(parts, v)
         allg[k] = torch.stack(parts)
-    ordered = allg["f64"][0].clone()
-    for r in range(1, world):
-        ordered += allg["f64"][r]
-    again = {"f64": orig["f64"].clone()}
-    allreduce_state(again)
-    ok = (torch.equal(st["i64"], allg["i64"].sum(0)) and torch.equal(st["f64"], ordered)
-          and torch.equal(again["f64"], st["f64"])
+    every = [None] * world
+    dist.all_gather_object(every, vals)
+    summed = st["i64"][50:].tolist()
+    folded = []  # fx_limbs_kernel's fold: carry each limb's excess upward, mod 2^128, as a signed value
+    for i in range(20):
+        c, w = 0, 0
+        for k in range(4):
+            t = summed[4 * i + k] + c
+            w |= (t & 0xFFFFFFFF) << (32 * k)
+            c = t >> 32
+        folded.append(w - (1 << 128) if w >> 127 else w)
+    exact = [sum(vs[i] for vs in every) for i in range(20)]
+    ok = (torch.equal(st["i64"], allg["i64"].sum(0)) and folded == exact
           and torch.equal(st["mn"], allg["mn"].min(0).values) and torch.equal(st["mx"], allg["mx"].max(0).values)
           and torch.equal(st["stats"], torch.tensor([world * (world + 1) // 2] * 6)))
     q.put((rank, ok))
@@ -64,12 +77,15 @@ def _worker_header(rank, world, port, q):
     fingerprint maxima / minima, so all of them take the same branch even when only one rank's layout changed."""
     _init(rank, world, port)
     from pinot_amd.combine import _layout_header
+    from pinot_amd import abi
     dev = torch.device("cpu")
-    same = [0, 365, 3, 0, 0, 0, 0, 3]
-    out = [_layout_header(None, list(same), None, dev)]
-    changed = list(same) if rank == 0 else [1, 1 << 20, 3, 0, 0, 0, 0, 3]   # rank 1 regrew into a hash table
-    out.append(_layout_header(None, changed, None, dev))
-    out.append(_layout_header(RuntimeError("x") if rank == 1 else None, list(same), None, dev))
+    same = [0, 365, 3, 0, 0, 0, 0, 3, 0]
+    out = [_layout_header(None, list(same), 0, None, dev)]
+    changed = list(same) if rank == 0 else [1, 1 << 20, 3, 0, 0, 0, 0, 3, 0]   # rank 1 regrew into a hash table
+    out.append(_layout_header(None, changed, 0, None, dev))
+    out.append(_layout_header(RuntimeError("x") if rank == 1 else None, list(same), 0, None, dev))
+    # one rank's segment reached numGroupsLimit: every rank's combined result reports it
+    out.append(_layout_header(None, list(same), abi.PG_RESULT_GROUPS_LIMIT_REACHED if rank == 1 else 0, None, dev))
     q.put((rank, out))
     dist.destroy_process_group()
 
@@ -77,11 +93,13 @@ def _worker_header(rank, world, port, q):
 def test_layout_header_gives_every_rank_the_same_decision():
     res = _run(_worker_header)
     (_, a), (_, b) = res
+    from pinot_amd import abi
     assert a == b
-    eq, chg, err = a
-    assert eq[0] == 0 and eq[1] == eq[2]                       # no error, identical layouts: dense all-reduce
-    assert chg[0] == 0 and chg[1][:2] != chg[2][:2] and chg[1][2:] == chg[2][2:]   # mixed modes: row exchange
+    eq, chg, err, lim = a
+    assert eq[0] == 0 and eq[1] == 0 and eq[2] == eq[3]        # no error, identical layouts: dense all-reduce
+    assert chg[0] == 0 and chg[2][:2] != chg[3][:2] and chg[2][2:] == chg[3][2:]   # mixed modes: row exchange
     assert err[0] == 1                                         # one rank failed: every rank raises
+    assert lim[1] == abi.PG_RESULT_GROUPS_LIMIT_REACHED        # the OR of the ranks' result flags
 
 
 def _worker_sharded(rank, world, port, q):

@@ -1,7 +1,12 @@
 """Two ranks on one MI355X (gloo, world_size 2, both on cuda:0): each rank runs pg_execute_partial over half of the
 segments and pinot_amd.combine merges the DEVICE partial states -- the dense all-reduce path (small dense key space)
 and the row-exchange path (hash states, DISTINCTCOUNT bitmaps: all_to_all of rows by owner, pg_partials_merge) -- and
-the merged result must equal the CPU oracle over the whole table.  The same code runs over RCCL at N GPUs."""
+the merged result must equal the CPU oracle over the whole table.  The same code runs over RCCL at N GPUs.
+
+Double sums (test_two_ranks_double_sums_are_bit_identical): SUM / AVG over DOUBLE / FLOAT columns and expressions
+accumulate as exact fixed-point integers (SK_FX), so the device result is the same bits in two runs, on 1 rank and on
+2 ranks (dense all-reduce of 32-bit limbs, and the row exchange), and within 1e-9 of the oracle's sequential double
+sum; +-inf / NaN inputs give IEEE's sum exactly."""
 import os
 import socket
 import sys
@@ -101,3 +106,105 @@ def test_two_ranks_merge_device_partials():
     for rank, ok, info in res:
         assert ok, info
     assert "dense" in res[0][2] and "rows" in res[0][2]
+
+
+DOUBLE_CASES = [
+    # (sql, force hash table)
+    ("SELECT SUM(d), AVG(w), SUM(f), COUNT(*), SUM(d * w) FROM t", False),            # aggregation-only: LDS slot
+    ("SELECT g, SUM(d), AVG(f), SUM(d * w), SUM(i), MIN(d) FROM t GROUP BY g", False),  # dense table
+    ("SELECT g, SUM(d), AVG(f), SUM(d * w), SUM(i), MIN(d) FROM t GROUP BY g", True),   # hash table: row exchange
+    ("SELECT g, SUM(w), AVG(d + w) FROM t WHERE i < 500 GROUP BY g", False),
+    ("SELECT g, SUM(s), AVG(s) FROM t GROUP BY g", False),                               # +-inf / NaN inputs
+    ("SELECT SUM(s), SUM(d - w) FROM t WHERE g < 20", False),
+]
+
+
+def _double_segments():
+    import numpy as np
+    from pinot_amd.segment import ImmutableSegment
+    rng = np.random.default_rng(2024)
+    segs = []
+    for si in range(4):
+        n = 50_000 + 3_331 * si
+        s_col = rng.normal(size=n) * 1e3
+        if si == 0:
+            s_col[rng.integers(0, n, 5)] = np.inf      # +inf in some groups
+        if si == 2:
+            s_col[rng.integers(0, n, 5)] = -np.inf     # -inf in others (NaN where both meet)
+        if si == 1:
+            s_col[7] = np.nan
+        data = {"g": rng.integers(0, 40, n), "i": rng.integers(0, 1000, n),
+                "d": np.round(rng.normal(size=n) * 1e6, 3), "f": rng.normal(size=n).astype(np.float32),
+                "w": rng.lognormal(0, 6, n) * rng.choice([-1.0, 1.0], n), "s": s_col}
+        segs.append(ImmutableSegment.create(f"dbl{si}", data, {"g": "INT", "i": "INT", "d": "DOUBLE", "f": "FLOAT",
+                                                              "w": "DOUBLE", "s": "DOUBLE"}))
+    return segs
+
+
+def _bits(rows):
+    """The rows with every float replaced by its IEEE bits (so NaN compares equal to the same NaN)."""
+    import struct
+
+    def conv(v):
+        if isinstance(v, float):
+            return struct.unpack("<Q", struct.pack("<d", v))[0]
+        if isinstance(v, tuple):
+            return tuple(conv(x) for x in v)
+        return v
+    return {k: [conv(v) for v in row] for k, row in rows.items()}
+
+
+def _worker_double(rank, world, port, q):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from helpers import assert_same_result
+        from oracle.oracle import OracleEngine
+        from pinot_amd import abi
+        from pinot_amd.combine import merge_partials_across_ranks
+        from pinot_amd.gpu import GpuEngine
+        from pinot_amd.plan import Table
+        from pinot_amd.query import parse
+        eng = GpuEngine(0)
+        segs = _double_segments()
+        table = Table("t", segs)
+        mine = segs[rank::world]
+        n_fx = []
+        for sql, force_hash in DOUBLE_CASES:
+            qc = parse(sql)
+            flags = abi.PG_PLAN_HASH_GROUPS if force_hash else 0
+            one = eng.run_plan(eng.make_plan(table, qc, flags=flags))           # 1 rank: every segment
+            again = eng.run_plan(eng.make_plan(table, qc, flags=flags))
+            assert _bits(one.rows) == _bits(again.rows), sql                    # run to run: the same bits
+            plan = eng.make_plan(table, qc, segments=mine, flags=flags)
+            p = eng.run_partial(plan)
+            n_fx.append(int(p.contents.n_fx))
+            two = merge_partials_across_ranks(eng, plan, p)                      # 2 ranks: half the segments each
+            assert _bits(two.rows) == _bits(one.rows), (sql, sorted(two.rows.items())[:2], sorted(one.rows.items())[:2])
+            assert_same_result(one, OracleEngine().execute(table, qc), table=table)
+        q.put((rank, True, n_fx))
+        dist.destroy_process_group()
+    except Exception:
+        q.put((rank, False, traceback.format_exc()))
+
+
+def test_two_ranks_double_sums_are_bit_identical():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_double, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, info in res:
+        assert ok, info
+    assert all(n > 0 for n in res[0][2])   # every case has exact fixed-point sums (SK_FX)

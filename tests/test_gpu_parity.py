@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 from helpers import assert_same_result, check_inner_values, check_rows, inner_query, run_rows, with_filter
-from pinot_amd.plan import Table, UnsupportedQuery, reduce_to_rows
+from pinot_amd.plan import MAX_TRIM_THRESHOLD, InstanceConfig, Table, UnsupportedQuery, reduce_to_rows
 from pinot_amd.query import parse
 from pinot_amd.segment import ImmutableSegment
 
@@ -134,11 +134,13 @@ def test_wide_group_keys_match_oracle(sql, gpu_engine, oracle_engine, sv_table_i
 
 @pytest.mark.parametrize("limit", [1, 500, 29000])
 def test_wide_group_keys_num_groups_limit(limit, gpu_engine, oracle_engine, sv_table_inter):
-    """numGroupsLimit with the ArrayMapBasedHolder: per segment the first `limit` tuples in doc order (getGroupId
-    :812-819), then the value-keyed merge."""
-    q = parse(f"SELECT COUNT(*), SUM(column1) FROM t GROUP BY {WIDE_KEYS} OPTION(numGroupsLimit={limit})")
-    assert_same_result(gpu_engine.execute(sv_table_inter, q), oracle_engine.execute(sv_table_inter, q),
-                       table=sv_table_inter)
+    """The instance's numGroupsLimit with the ArrayMapBasedHolder: per segment the first `limit` tuples in doc order
+    (getGroupId :812-819), then the value-keyed merge; numGroupsLimitReached as the oracle reports it."""
+    q = parse(f"SELECT COUNT(*), SUM(column1) FROM t GROUP BY {WIDE_KEYS}")
+    cfg = InstanceConfig.with_groups_limit(limit)
+    g, o = gpu_engine.execute(sv_table_inter, q, config=cfg), oracle_engine.execute(sv_table_inter, q, config=cfg)
+    assert_same_result(g, o, table=sv_table_inter)
+    assert g.groups_limit_reached == o.groups_limit_reached
 
 
 GROUP_QUERIES = [q for q in SV_QUERIES if "GROUP BY" in q] + [
@@ -160,9 +162,11 @@ def test_group_by_hash_table_matches_oracle(sql, gpu_engine, oracle_engine, sv_t
 
 @pytest.mark.parametrize("limit", [1, 37, 500, 1736, 1737])
 def test_num_groups_limit_truncation(limit, gpu_engine, oracle_engine):
-    """numGroupsLimit below the segment's distinct keys: each segment keeps the keys it sees first (doc order) and
-    drops the docs of later keys (IntGroupIdMap.getGroupId, DictionaryBasedGroupKeyGenerator.java:991-1016); the
-    segments then merge by value.  Segments hold different data so their kept key sets differ."""
+    """The instance's numGroupsLimit below the segment's distinct keys: each segment keeps the keys it sees first (doc
+    order) and drops the docs of later keys (IntGroupIdMap.getGroupId, DictionaryBasedGroupKeyGenerator.java:991-1016);
+    the segments then merge by value.  Segments hold different data so their kept key sets differ.  The result
+    reports numGroupsLimitReached exactly when a segment holds >= limit keys (AggregationGroupByOrderByOperator
+    .java:112-113); an OPTION(numGroupsLimit=...) in the SQL is ignored, as Pinot 0.11 ignores it."""
     rng = np.random.default_rng(limit)
     segs = []
     for s_ in range(3):
@@ -173,10 +177,14 @@ def test_num_groups_limit_truncation(limit, gpu_engine, oracle_engine):
     t = Table("t", segs)
     for sql in ["SELECT k, COUNT(*), SUM(v), MIN(d), MAX(v), AVG(d), DISTINCTCOUNT(u) FROM t GROUP BY k",
                 "SELECT k2, k, SUM(v) FROM t WHERE v > 0 GROUP BY k2, k"]:
-        q = parse(sql + f" OPTION(numGroupsLimit={limit})")
-        g, o = gpu_engine.execute(t, q), oracle_engine.execute(t, q)
+        q = parse(sql)
+        cfg = InstanceConfig.with_groups_limit(limit)
+        g, o = gpu_engine.execute(t, q, config=cfg), oracle_engine.execute(t, q, config=cfg)
         assert_same_result(g, o, table=t)
         assert len(g.rows) <= 3 * limit
+        assert g.groups_limit_reached == o.groups_limit_reached
+        q_opt = parse(sql + " OPTION(numGroupsLimit=10000000)")   # not an instance setting: no effect
+        assert_same_result(gpu_engine.execute(t, q_opt, config=cfg), o, table=t)
 
 
 @pytest.mark.parametrize("select", ["0", "1"])
@@ -201,19 +209,20 @@ def test_order_by_trim_on_device(select, monkeypatch, gpu_engine, oracle_engine,
 
 def test_config4_shape_high_cardinality_distinctcount(gpu_engine, oracle_engine):
     """Config 4 in miniature: userId of high cardinality x itemId 1 000, DISTINCTCOUNT per user, ORDER BY DISTINCTCOUNT
-    DESC, userId LIMIT 100, numGroupsLimit above the distinct users (as the reference must be run); plus the same
-    with the default limit, which truncates per segment."""
+    DESC, userId LIMIT 100, with an instance numGroupsLimit above the distinct users (as the reference must be run);
+    plus the same under a 40 000 limit, which truncates per segment."""
     from pinot_amd import synth
     segs = [synth.make_segment_np(synth.highcard_specs(users=150_000), s, 200_003) for s in range(3)]
     t = Table("events", segs)
-    for sql in [synth.highcard_query() + " OPTION(numGroupsLimit=10000000)",
-                synth.highcard_query().replace("LIMIT 100", "LIMIT 20") + " OPTION(numGroupsLimit=40000)"]:
+    for sql, cfg in [(synth.highcard_query(), InstanceConfig(num_groups_limit=10_000_000)),
+                     (synth.highcard_query().replace("LIMIT 100", "LIMIT 20"), InstanceConfig(num_groups_limit=40_000))]:
         q = parse(sql)
-        g = gpu_engine.execute(t, q, trim=True)
-        o = oracle_engine.execute(t, q)
+        g = gpu_engine.execute(t, q, trim=True, config=cfg)
+        o = oracle_engine.execute(t, q, config=cfg)
         assert reduce_to_rows(q, g)[1] == reduce_to_rows(q, o)[1]
-        full = gpu_engine.execute(t, q)
+        full = gpu_engine.execute(t, q, config=cfg)
         assert_same_result(full, o, table=t)
+        assert full.groups_limit_reached == o.groups_limit_reached == (cfg.num_groups_limit == 40_000)
 
 
 @pytest.mark.parametrize("mode", ["0", "1"])
@@ -225,22 +234,22 @@ def test_radix_partitioned_group_by(mode, monkeypatch, gpu_engine, oracle_engine
     monkeypatch.setenv("PG_PART", mode)
     segs = [synth.make_segment_np(synth.highcard_specs(users=150_000), s, 200_003 + 977 * s) for s in range(3)]
     t = Table("events", segs)
-    for sql in [synth.highcard_query() + " OPTION(numGroupsLimit=10000000)",
+    cfg = InstanceConfig(num_groups_limit=10_000_000)
+    for sql in [synth.highcard_query(),
                 "SELECT userId, COUNT(*), DISTINCTCOUNT(itemId), COUNT(*) FROM events WHERE itemId < 700 "
-                "GROUP BY userId OPTION(numGroupsLimit=10000000)",
+                "GROUP BY userId",
                 "SELECT itemId, COUNT(*) FROM events WHERE userId BETWEEN 1000 AND 90000 GROUP BY itemId",
-                "SELECT userId, COUNT(*) FROM events GROUP BY userId ORDER BY COUNT(*) DESC, userId LIMIT 10 "
-                "OPTION(numGroupsLimit=10000000)"]:
+                "SELECT userId, COUNT(*) FROM events GROUP BY userId ORDER BY COUNT(*) DESC, userId LIMIT 10"]:
         q = parse(sql)
-        o = oracle_engine.execute(t, q)
-        assert_same_result(gpu_engine.execute(t, q, flags=abi.PG_PLAN_VALUE_SETS), o, table=t)
+        o = oracle_engine.execute(t, q, config=cfg)
+        assert_same_result(gpu_engine.execute(t, q, flags=abi.PG_PLAN_VALUE_SETS, config=cfg), o, table=t)
         if q.order_by:
-            assert reduce_to_rows(q, gpu_engine.execute(t, q, trim=True))[1] == reduce_to_rows(q, o)[1]
+            assert reduce_to_rows(q, gpu_engine.execute(t, q, trim=True, config=cfg))[1] == reduce_to_rows(q, o)[1]
             # the trim of a DISTINCTCOUNT-ordered state from its set-size histogram (finalize_core step 0) and the
             # general order-image radix select give the same server rows
-            srv = gpu_engine.execute(t, q, trim="server")
+            srv = gpu_engine.execute(t, q, trim="server", config=cfg)
             monkeypatch.setenv("PG_TRIM_POP", "0")
-            gen = gpu_engine.execute(t, q, trim="server")
+            gen = gpu_engine.execute(t, q, trim="server", config=cfg)
             monkeypatch.delenv("PG_TRIM_POP")
             assert srv.rows == gen.rows
 
@@ -274,16 +283,17 @@ def test_radix_partitioned_speculative_regions(case, monkeypatch, gpu_engine, or
     t = Table("events", segs)
     if case == "keymap":
         assert t.key_space("userId").kind == abi.PG_KEY_KEYMAP
-    for sql in [synth_highcard() + " OPTION(numGroupsLimit=10000000)",
-                "SELECT userId, COUNT(*) FROM events GROUP BY userId ORDER BY COUNT(*) DESC, userId LIMIT 10 "
-                "OPTION(numGroupsLimit=10000000)"]:
+    cfg = InstanceConfig(num_groups_limit=10_000_000)
+    for sql in [synth_highcard(),
+                "SELECT userId, COUNT(*) FROM events GROUP BY userId ORDER BY COUNT(*) DESC, userId LIMIT 10"]:
         q = parse(sql)
-        o = oracle_engine.execute(t, q)
-        assert_same_result(gpu_engine.execute(t, q, flags=abi.PG_PLAN_VALUE_SETS), o, table=t)
-        assert reduce_to_rows(q, gpu_engine.execute(t, q, trim=True))[1] == reduce_to_rows(q, o)[1]
+        o = oracle_engine.execute(t, q, config=cfg)
+        assert_same_result(gpu_engine.execute(t, q, flags=abi.PG_PLAN_VALUE_SETS, config=cfg), o, table=t)
+        assert reduce_to_rows(q, gpu_engine.execute(t, q, trim=True, config=cfg))[1] == reduce_to_rows(q, o)[1]
     monkeypatch.setenv("PG_PART_SPEC", "0")  # the exact-offset pipeline on the same data
-    q = parse(synth_highcard() + " OPTION(numGroupsLimit=10000000)")
-    assert_same_result(gpu_engine.execute(t, q, flags=abi.PG_PLAN_VALUE_SETS), oracle_engine.execute(t, q), table=t)
+    q = parse(synth_highcard())
+    assert_same_result(gpu_engine.execute(t, q, flags=abi.PG_PLAN_VALUE_SETS, config=cfg),
+                       oracle_engine.execute(t, q, config=cfg), table=t)
 
 
 def synth_highcard():
@@ -295,7 +305,10 @@ def test_config4_full_segments_match_oracle(gpu_engine, oracle_engine):
     """Config 4 at its stated scale: 4 full 7 812 500-row segments of the 10 M-user key space (device-generated, as the
     bench), every group's DISTINCTCOUNT and COUNT-free result through the radix-partitioned pipeline against the
     oracle's per-segment value sets merged by value, and the device-trimmed top 100 (ORDER BY DISTINCTCOUNT DESC,
-    userId) against the oracle's."""
+    userId) against the oracle's.  The instance is configured as SURVEY §8(d) states the reference must be run:
+    num.groups.limit 10 M (above the ~5.4 M users of a segment) and groupby.trim.threshold at MAX_TRIM_THRESHOLD (no
+    lossy resize during the merge); at the default threshold (1 M) the result reports that the reference server would
+    have resized its table mid-merge."""
     import torch
     from pinot_amd import abi, synth
     from pinot_amd.plan import CPlan
@@ -313,15 +326,16 @@ def test_config4_full_segments_match_oracle(gpu_engine, oracle_engine):
         segs.append(seg)
         del dcs
     t = Table("events", segs)
-    q = parse(synth.highcard_query() + " OPTION(numGroupsLimit=10000000)")
+    q = parse(synth.highcard_query())
+    cfg = InstanceConfig(num_groups_limit=10_000_000, groupby_trim_threshold=MAX_TRIM_THRESHOLD)
     # oracle: per-segment (user, item) value sets merged by value
     ht = Table("events", host)
-    cp = CPlan(ht, q, host, list(range(1, len(host) + 1)))
+    cp = CPlan(ht, q, host, list(range(1, len(host) + 1)), config=cfg)
     pk, pv = zip(*(oracle_engine.distinct_pairs(cp, i, sg) for i, sg in enumerate(host)))
     pair = np.unique(np.concatenate(pk) * (1 << 20) + np.concatenate(pv))
     users, counts = np.unique(pair >> 20, return_counts=True)
     # device: every group (keys, distinct counts) from the partial state
-    plan = gpu_engine.make_plan(t, q, flags=0)
+    plan = gpu_engine.make_plan(t, q, flags=0, config=cfg)
     ra = gpu_engine.finalize_arrays(plan, gpu_engine.run_partial(plan))
     ks = plan.key_spaces[0]
     assert ks.kind == abi.PG_KEY_VALUE_OFFSET
@@ -333,12 +347,22 @@ def test_config4_full_segments_match_oracle(gpu_engine, oracle_engine):
     # device-trimmed top rows (pg_execute: the bucket pass's set sizes feed the trim)
     top = np.lexsort((users, -counts))[:q.limit]
     want = [[int(users[i]), int(counts[i])] for i in top]
-    assert reduce_to_rows(q, gpu_engine.execute(t, q, flags=0, trim=True))[1] == want
+    assert reduce_to_rows(q, gpu_engine.execute(t, q, flags=0, trim=True, config=cfg))[1] == want
     # the server's result (GroupByOrderByCombineOperator: getTableCapacity(100, minServerGroupTrimSize = 5 000) rows
-    # under the ORDER BY; the ORDER BY ends in the key, so the kept set is determined): exactly the oracle's top 5 000
-    srv = gpu_engine.execute(t, q, flags=0, trim="server")
+    # under the ORDER BY; the ORDER BY ends in the key, so the kept set is determined; no mid-merge resize under this
+    # instance config): exactly the oracle's top 5 000
+    srv = gpu_engine.execute(t, q, flags=0, trim="server", config=cfg)
     top = np.lexsort((users, -counts))[:5000]
     assert len(srv.rows) == 5000
+    assert not srv.trim_threshold_reached and not srv.groups_limit_reached
+    assert srv.num_groups_merged == len(users)
+    # two segments under the default groupby.trim.threshold (1 M): the ~8 M merged users would have made the reference's
+    # ConcurrentIndexedTable resize mid-merge (lossy); the device merges exactly and reports it.  Raised: no resize.
+    two_users = np.unique(np.concatenate(pk[:2])).size
+    for c2, hit in ((InstanceConfig(num_groups_limit=10_000_000), True), (cfg, False)):
+        r2 = gpu_engine.execute(t, q, segments=segs[:2], flags=0, trim="server", config=c2)
+        assert r2.trim_threshold_reached == hit and r2.num_groups_merged == two_users > 1_000_000
+        assert len(r2.rows) == 5000
     assert sorted(k[0] for k in srv.rows) == sorted(users[top].tolist())
     ku = np.asarray([k[0] for k in srv.rows], dtype=np.int64)
     assert np.array_equal(np.asarray([v[0] for v in srv.rows.values()]), counts[np.searchsorted(users, ku)])
@@ -460,7 +484,7 @@ def test_partial_rows_export_merge_roundtrip(gpu_engine, oracle_engine, sv_table
         buf = torch.empty(sum(counts) * rb, dtype=torch.uint8, device="cuda")
         assert gpu_engine.export_rows(p, 3, C.c_void_p(buf.data_ptr()), sum(counts)) == counts
         keys = buf.view(-1, rb)[:, :8].contiguous().view(torch.int64).cpu().numpy().astype(np.uint64)
-        owners = [gpu_engine.lib.pg_key_owner(int(k), 3) for k in keys]
+        owners = [gpu_engine.lib.pg_key_owner(int(k), 3) for k in keys.ravel()]
         assert owners == sorted(owners)
         qq = gpu_engine.create_like(p, sum(counts))
         qq.contents.stats = p.contents.stats
@@ -705,17 +729,23 @@ def test_partials_roundtrip_single_rank(gpu_engine, oracle_engine, sv_table_inte
     from pinot_amd import abi
     q = parse("SELECT column11, COUNT(*), SUM(column1), MIN(column3), MAX(column6), AVG(column7) FROM t "
               "GROUP BY column11")
-    plan = gpu_engine.make_plan(sv_table_inter, q)
-    p = gpu_engine.run_partial(plan)
-    pc = p.contents
-    assert pc.mode == abi.PG_STATE_DENSE
-    bufs = [torch.empty(max(pc.num_slots * k, 1) * 8, dtype=torch.uint8, device="cuda")
-            for k in (pc.n_i64, pc.n_f64, pc.n_min, pc.n_max)]
-    ptrs = [C.c_void_p(b.data_ptr()) for b in bufs]
-    assert gpu_engine.lib.pg_partials_copy(p, abi.PG_COPY_OUT, *ptrs, None) == 0
-    assert gpu_engine.lib.pg_partials_copy(p, abi.PG_COPY_IN, *ptrs, None) == 0
-    g = gpu_engine.finalize_partial(plan, p)
-    assert_same_result(g, oracle_engine.execute(sv_table_inter, q), table=sv_table_inter)
+    o = oracle_engine.execute(sv_table_inter, q)
+    # integer-exact i64 sums, then every sum as an exact fixed-point sum (its 128-bit pairs travel as 4 limbs each)
+    for flags in (0, abi.PG_PLAN_F64_SUMS):
+        plan = gpu_engine.make_plan(sv_table_inter, q, flags=flags)
+        p = gpu_engine.run_partial(plan)
+        pc = p.contents
+        assert pc.mode == abi.PG_STATE_DENSE and (pc.n_fx == 2) == bool(flags)
+        bufs = [torch.empty(max(pc.num_slots * k, 1) * 8, dtype=torch.uint8, device="cuda")
+                for k in (pc.n_i64, 4 * pc.n_fx, pc.n_min, pc.n_max)]
+        ptrs = [C.c_void_p(b.data_ptr()) for b in bufs]
+        assert gpu_engine.lib.pg_partials_copy(p, abi.PG_COPY_OUT, *ptrs, None) == 0
+        if flags:  # the limbs are 32-bit values: a SUM of them over ranks cannot overflow
+            limbs = bufs[1].view(torch.int64)
+            assert int(limbs.min()) >= 0 and int(limbs.max()) < (1 << 32)
+        assert gpu_engine.lib.pg_partials_copy(p, abi.PG_COPY_IN, *ptrs, None) == 0
+        g = gpu_engine.finalize_partial(plan, p)
+        assert_same_result(g, o, table=sv_table_inter)
 
 
 # ------------------------------------------------------------------ config 1: QuickStart baseballStats

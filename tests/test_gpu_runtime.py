@@ -44,8 +44,9 @@ def _long_scan(gpu_engine):
         segs.append(seg)
     table = Table("events", segs)
     from pinot_amd import synth as sy
-    plan = gpu_engine.make_plan(table, parse(sy.highcard_query() + " OPTION(numGroupsLimit=10000000)"), flags=0,
-                                trim=True)
+    from pinot_amd.plan import InstanceConfig
+    plan = gpu_engine.make_plan(table, parse(sy.highcard_query()), flags=0, trim=True,
+                                config=InstanceConfig(num_groups_limit=10_000_000))
     gpu_engine.run_plan(plan)
     t0 = time.perf_counter()
     ref = gpu_engine.run_plan(plan)

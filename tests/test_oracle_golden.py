@@ -36,10 +36,11 @@ def test_inner_filtered_aggregation(i, expected, oracle_engine, sv_table_inner):
 
 def test_inner_group_by_array_vs_map_holders(oracle_engine, sv_table_inner):
     """ArrayBased (card product <= 10 000) vs map-based holders give the same groups (DictionaryBasedGroupKeyGenerator)."""
-    from oracle.oracle import OracleEngine
+    from pinot_amd.plan import InstanceConfig
     q = "SELECT COUNT(*), SUM(column1) FROM testTable GROUP BY column11, column12"
     a = oracle_engine.execute(sv_table_inner, q)
-    b = OracleEngine(array_based_threshold=1).execute(sv_table_inner, q)
+    # max.init.group.holder.capacity = 1: every card product exceeds it, so the map-based holders run
+    b = oracle_engine.execute(sv_table_inner, q, config=InstanceConfig(max_init_group_holder_capacity=1))
     assert a.rows == b.rows
 
 

@@ -79,3 +79,66 @@ def test_literal_absent_everywhere_is_empty_leaf():
     p = CPlan(t, parse("SELECT COUNT(*) FROM t WHERE k IN (5, 15, 99)"), segs, [1, 2, 3], id_sets=id_sets)
     kinds = [lw[0].kind for lw in p.lowered]
     assert kinds == [abi.PG_LEAF_SV_SCAN, abi.PG_LEAF_SV_SCAN, abi.PG_LEAF_EMPTY]
+
+
+# ------------------------------------------------------------------ the instance's group-by settings
+
+
+def test_num_groups_limit_is_an_instance_setting(oracle_engine):
+    """numGroupsLimit comes from the server instance only (InstancePlanMakerImplV2.java:223; QueryOptionsUtils has no
+    such option): an OPTION(numGroupsLimit=...) changes neither the plan nor the result, and the instance's limit
+    truncates each segment to the first `limit` keys in doc order (IntGroupIdMap.getGroupId,
+    DictionaryBasedGroupKeyGenerator.java:991-1016) -- checked against numpy -- with numGroupsLimitReached set."""
+    from pinot_amd.plan import DEFAULT_NUM_GROUPS_LIMIT, InstanceConfig
+    rng = np.random.default_rng(11)
+    segs, raw = [], []
+    for s in range(3):
+        n = 5_000 + 777 * s
+        data = {"k": rng.integers(0, 400, n).astype(np.int64), "v": rng.integers(-1000, 1000, n).astype(np.int64)}
+        raw.append(data)
+        segs.append(ImmutableSegment.create(f"n{s}", data, {"k": "INT", "v": "LONG"}))
+    t = Table("t", segs)
+    sql = "SELECT k, COUNT(*), SUM(v) FROM t GROUP BY k"
+    assert CPlan(t, parse(sql + " OPTION(numGroupsLimit=5)"), segs, [1, 2, 3]).plan.num_groups_limit == \
+        DEFAULT_NUM_GROUPS_LIMIT
+    cfg = InstanceConfig.with_groups_limit(37)
+    assert CPlan(t, parse(sql), segs, [1, 2, 3], config=cfg).plan.num_groups_limit == 37
+    want = {}
+    for d in raw:   # numpy: each segment keeps its first 37 distinct keys (doc order), then the merge by value
+        keys, first = np.unique(d["k"], return_index=True)
+        kept = keys[np.argsort(first)][:37]
+        for k in kept.tolist():
+            m = d["k"] == k
+            c, sm = want.get((k,), [0, 0.0])
+            want[(k,)] = [c + int(m.sum()), sm + float(d["v"][m].sum())]
+    for extra in ("", " OPTION(numGroupsLimit=1000000)", " OPTION(numGroupsLimit=2)"):
+        r = oracle_engine.execute(t, sql + extra, config=cfg)
+        assert r.rows == want and r.groups_limit_reached
+    full = oracle_engine.execute(t, sql + " OPTION(numGroupsLimit=2)")   # default instance: every group, no limit hit
+    assert len(full.rows) == 400 and not full.groups_limit_reached
+    with pytest.raises(ValueError):   # the constructor's precondition (InstancePlanMakerImplV2.java:138-140)
+        InstanceConfig(num_groups_limit=100)
+    with pytest.raises(ValueError):
+        InstanceConfig(groupby_trim_threshold=0)
+
+
+def test_trim_threshold_flag_in_the_oracle(oracle_engine):
+    """groupTrimThreshold: the reference server's table (ORDER BY, server trim on) resizes whenever it holds >=
+    threshold records (ConcurrentIndexedTable.java:61-65); the oracle reports that instead of reproducing the lossy,
+    schedule-dependent resize, and the plan carries the threshold to the device (pg_plan.trim_threshold)."""
+    from pinot_amd.plan import MAX_TRIM_THRESHOLD, InstanceConfig
+    rng = np.random.default_rng(12)
+    segs = [ImmutableSegment.create(f"m{s}", {"k": rng.integers(0, 3000, 20_000).astype(np.int64)}, {"k": "INT"})
+            for s in range(2)]
+    t = Table("t", segs)
+    sql = "SELECT k, COUNT(*) FROM t GROUP BY k ORDER BY COUNT(*) DESC, k LIMIT 10"
+    for thr, hit in ((1000, True), (2999, True), (3001, False), (MAX_TRIM_THRESHOLD, False)):
+        cfg = InstanceConfig(groupby_trim_threshold=thr)
+        r = oracle_engine.execute(t, sql, server=True, config=cfg)
+        assert r.trim_threshold_reached == hit and r.num_groups_merged == 3000 and len(r.rows) == 5000 - 2000
+        assert CPlan(t, parse(sql), segs, [1, 2], trim="server", config=cfg).plan.trim_threshold == \
+            (thr if thr < MAX_TRIM_THRESHOLD else 0)
+    # no ORDER BY: no resize at all (the table stops taking keys at its result size instead)
+    r = oracle_engine.execute(t, "SELECT k, COUNT(*) FROM t GROUP BY k LIMIT 10", server=True,
+                              config=InstanceConfig(groupby_trim_threshold=1000))
+    assert not r.trim_threshold_reached
