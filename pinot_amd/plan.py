@@ -281,13 +281,19 @@ class Table:
                 if c is None:
                     continue
                 v = np.asarray(c.raw_values if c.dictionary is None else c.dictionary.values)
-                if v.size and v.dtype.kind in "iuf":
-                    a = np.abs(v.astype(np.float64))
-                    fin = np.isfinite(a)
-                    nonfinite |= not bool(fin.all())
-                    a = a[fin]
-                    if a.size:
-                        b = max(b, float(a.max()))
+                if not v.size or v.dtype.kind not in "iuf":
+                    continue
+                if c.dictionary is not None:  # a sorted dictionary: its ends bound it, unless they are not finite
+                    ends = np.abs(v[[0, -1]].astype(np.float64))
+                    if np.isfinite(ends).all():
+                        b = max(b, float(ends.max()))
+                        continue
+                a = np.abs(v.astype(np.float64))
+                fin = np.isfinite(a)
+                nonfinite |= not bool(fin.all())
+                a = a[fin]
+                if a.size:
+                    b = max(b, float(a.max()))
             hit = self._abs_bounds[column] = (b, nonfinite)
         return hit[0]
 
