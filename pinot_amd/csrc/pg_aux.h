@@ -223,6 +223,8 @@ struct PartSpec {
   uint64_t cap1, cap2;
   unsigned int* err;               // bit 4: a region over its capacity (the runtime reruns with exact offsets)
   uint32_t* dc_pop;                // optional [num_groups]: each group's distinct-value count (its bitmap's popcount)
+  uint32_t count_docs;             // 1: i64 slot 0 = doc count (a COUNT reads it); 0: the value set's size (presence)
+  uint32_t pad2;
 };
 // Level 1 straight from the columns, speculative (filter matching every doc, one group key, at most one DISTINCTCOUNT
 // value column): 256-thread blocks take rounds of one 8 192-doc tile; the tile's packed words of the key / value column
@@ -235,7 +237,7 @@ struct PartDirectSpec {
   uint64_t key_card, val_card;
   int64_t key_base, val_base;
   uint64_t cap1;                   // entries per level-1 partition region
-  uint32_t val_agg, pad;
+  uint32_t val_agg, stage_words;   // stage_words: set by launch_part_direct (LDS words of the widest tile stage)
   const SegDesc* segs;
   const WorkItem* items;           // tile ranges (kTileDocs docs)
   unsigned int* fill1;             // [nparts1] entries reserved so far (zeroed before the launch)

@@ -23,7 +23,10 @@
 // once (scan) + 8 written / 8 read (scan entries) + 4 / 4 twice (levels 1, 2) + 4 read (count2) + state rows once.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include "pg_aux.h"
 
@@ -59,7 +62,11 @@ constexpr uint32_t kST = PG_SPLIT_THREADS;  // threads of a split block
 #define PG_AGG_THREADS 1024
 #endif
 constexpr uint32_t kAT = PG_AGG_THREADS;  // threads of a part_aggregate block
-constexpr uint32_t kSplitChunk = PG_SPLIT_CHUNK;  // entries counting-sorted per LDS round (16 per thread): longer runs per digit
+constexpr uint32_t kSplitChunk = PG_SPLIT_CHUNK;
+#ifndef PG_AGG_BATCH
+#define PG_AGG_BATCH 16
+#endif
+constexpr int kAggB = PG_AGG_BATCH;  // entries per lane per load batch of the bucket pass  // entries counting-sorted per LDS round (16 per thread): longer runs per digit
 // (16 384 x 1 024 threads, one block per CU: split1 4.08 -> 3.10 ms, split2 2.71 -> 2.15 ms on config 4 vs 4 096 x 256)
 
 // The compile-time knobs (tools/part_variant.sh builds variants with -D) and what they size.  split_round scans the
@@ -84,6 +91,32 @@ __device__ __forceinline__ rsrc_t part_rsrc(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
                                            (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
+
+// ---- dev instrumentation (PG_PART_PROF=1 variant builds only: tools/part_variant.sh): lane 0 of every block sums
+// clock64() deltas per phase in registers and adds them to g_part_prof[kernel][phase] once at its end; the launch
+// functions synchronise and print the per-block averages to stderr.  Kernels: 0 part_direct, 1 split2s, 2 aggregate.
+#ifndef PG_PART_PROF
+#define PG_PART_PROF 0
+#endif
+#if PG_PART_PROF
+__device__ unsigned long long g_part_prof[3][8];
+#define PROF_NOW() (threadIdx.x == 0 ? (uint64_t)clock64() : 0ull)
+#define PROF_LAP(acc, ph, t) do { if (threadIdx.x == 0) { const uint64_t n_ = clock64(); (acc)[ph] += n_ - (t); (t) = n_; } } while (0)
+#define PROF_FLUSH(k, acc) do { if (threadIdx.x == 0) for (int i_ = 0; i_ < 8; i_++) atomicAdd(&g_part_prof[k][i_], (acc)[i_]); } while (0)
+static void prof_report(const char* name, int k, uint64_t blocks) {
+  unsigned long long h[3][8];
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(h, HIP_SYMBOL(g_part_prof), sizeof(h)) != hipSuccess) return;
+  fprintf(stderr, "[part_prof] %s blocks=%llu per-block kcycles:", name, (unsigned long long)blocks);
+  for (int i = 0; i < 8; i++) fprintf(stderr, " %.1f", h[k][i] / 1e3 / (double)blocks);
+  fprintf(stderr, "\n");
+  memset(h, 0, sizeof(h));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_part_prof), h, sizeof(h));
+}
+#else
+#define PROF_NOW() 0ull
+#define PROF_LAP(acc, ph, t) do { } while (0)
+#define PROF_FLUSH(k, acc) do { } while (0)
+#endif
 
 // Entries of level-1 partition p handled by level-2 block j (of kPartNB): [lo, hi).
 __device__ __forceinline__ void l2_range(const PartSpec& P, uint32_t p, uint32_t j, uint64_t& lo, uint64_t& hi) {
@@ -117,8 +150,10 @@ __device__ __forceinline__ void split_round(uint32_t (&e)[E], uint32_t (&dg)[E],
                                             uint32_t* cnt, uint32_t* start, unsigned long long* cur, uint32_t* sbuf,
                                             uint8_t* sdig, Out* out, uint32_t dsh = 0, unsigned int* fill = nullptr,
                                             uint64_t region0 = 0, uint64_t cap = 0, unsigned int* err = nullptr,
-                                            F after_reserve = F()) {
-  constexpr unsigned long long kDrop = ~0ull;
+                                            F after_reserve = F(), uint64_t* prof = nullptr) {
+  // a dropped run's cursor: never a (run start - sort position) value, which lies in (-2^15, 2^40) mod 2^64
+  constexpr unsigned long long kDrop = 1ull << 63;
+  [[maybe_unused]] uint64_t pt = PROF_NOW();
   const uint32_t tid = threadIdx.x;
   uint32_t rank[E];
 #pragma unroll
@@ -127,6 +162,7 @@ __device__ __forceinline__ void split_round(uint32_t (&e)[E], uint32_t (&dg)[E],
     rank[k] = tid + NT * k < n ? atomicAdd(&cnt[d], 1u) : 0u;
   }
   __syncthreads();
+  if (prof) PROF_LAP(prof, 1, pt);
   // exclusive scan of cnt over the digits (ndig <= 256 <= NT: one per thread) -> start; reserve the runs
   {
     uint32_t c = tid < ndig ? cnt[tid] : 0u, x = c;
@@ -147,7 +183,7 @@ __device__ __forceinline__ void split_round(uint32_t (&e)[E], uint32_t (&dg)[E],
       if (RES && c) {
         const uint32_t old = atomicAdd(&fill[tid], c);
         if ((uint64_t)old + c <= cap) {
-          cur[tid] = region0 + (uint64_t)tid * cap + old;
+          cur[tid] = region0 + (uint64_t)tid * cap + old - (wb + x - c);  // run start - its sort position
         } else {
           cur[tid] = kDrop;
           atomicOr(err, 16u);
@@ -156,6 +192,7 @@ __device__ __forceinline__ void split_round(uint32_t (&e)[E], uint32_t (&dg)[E],
     }
   }
   __syncthreads();
+  if (prof) PROF_LAP(prof, 2, pt);
   after_reserve();
 #pragma unroll
   for (int k = 0; k < E; k++)
@@ -165,12 +202,18 @@ __device__ __forceinline__ void split_round(uint32_t (&e)[E], uint32_t (&dg)[E],
       if (DIG) sdig[at] = (uint8_t)dg[k];
     }
   __syncthreads();
+  if (prof) PROF_LAP(prof, 3, pt);
   for (uint32_t i = tid; i < n; i += NT) {
     const uint32_t x = sbuf[i];
     const uint32_t d = DIG ? (uint32_t)sdig[i] : (x >> dsh) & (ndig - 1u);
-    if (!RES || cur[d] != kDrop) out[cur[d] + (i - start[d])] = (Out)x;
+    // RES: cur[d] holds the run's start minus its sort position (one LDS read per entry); else the cursor
+    const unsigned long long c0 = cur[d];
+    if (!RES || c0 != kDrop) {
+      out[RES ? c0 + i : c0 + (i - start[d])] = (Out)x;
+    }
   }
   __syncthreads();
+  if (prof) PROF_LAP(prof, 4, pt);
   if (!RES) {  // advance the cursors by this round's run lengths (start[d+1] - start[d])
     if (tid < ndig) cur[tid] += (tid + 1 < ndig ? start[tid + 1] : n) - start[tid];
     __syncthreads();
@@ -261,60 +304,162 @@ __global__ __launch_bounds__(kST) void part_split2_kernel(PartSpec P) {
 #ifndef PG_SPLIT2S_PREFETCH
 #define PG_SPLIT2S_PREFETCH 1  // the next chunk's loads issued while this one is sorted (registers: 1 block per CU)
 #endif
-// Level 2, speculative layout: level-1 partition p's entries (min(fill1[p], cap1) of them) split over kPartNB blocks,
-// counting-sorted by level-2 digit, each run reserved in its bucket's fixed-capacity region (no count pass).
-__global__ __launch_bounds__(kST, PG_SPLIT_WAVES) void part_split2s_kernel(PartSpec P) {
+// Level 2, speculative layout: entries [lo, hi) of level-1 partition p (its region starts at s0 and holds n entries),
+// counting-sorted by level-2 digit in LDS rounds of kSplitChunk, each run reserved in its bucket's fixed-capacity
+// region (bucket d at region0 + d * cap2, reservations on fill[d]; no count pass).  cnt must be zero on entry (it is
+// again on exit).
+__device__ __forceinline__ void split2s_range(const PartSpec& P, uint64_t s0, uint64_t n, uint64_t lo, uint64_t hi,
+                                              unsigned int* fill, uint64_t region0, uint32_t* cnt, uint32_t* start,
+                                              unsigned long long* cur, uint32_t* sbuf, uint64_t* prof = nullptr) {
   constexpr int E = kSplitChunk / kST;
-  __shared__ uint32_t cnt[256], start[256], sbuf[kSplitChunk];
-  __shared__ unsigned long long cur[256];
-  __shared__ uint8_t sdig[1];
-  const uint32_t j = blockIdx.x, p = blockIdx.y, tid = threadIdx.x;
-  if (tid < P.nparts2) cnt[tid] = 0;
-  __syncthreads();
-  const uint64_t n = min((uint64_t)P.fill1[p], P.cap1), s0 = (uint64_t)p * P.cap1;
-  const uint64_t lo = s0 + n * j / kPartNB, hi = s0 + n * (j + 1) / kPartNB;
-  const uint32_t* __restrict__ in = P.in1;
-  unsigned int* fill = P.fill2 + (uint64_t)p * P.nparts2;
-  const uint64_t region0 = (uint64_t)p * P.nparts2 * P.cap2;
+  const uint32_t tid = threadIdx.x;
   uint32_t e[E], ne[E];
   // buffer loads relative to the partition (one 32-bit lane offset, the k stride as a scalar offset, reads past the
   // block's range return 0): no 64-bit address per load in flight
-  const rsrc_t rin = part_rsrc(in + s0, (uint32_t)(4ull * n));
+  const rsrc_t rin = part_rsrc(P.in1 + s0, (uint32_t)(4ull * n));
+  // (no select on the loaded value: split_round skips the round's entries past n itself, so the loads stay in flight
+  // until the round that consumes them -- a `cond ? v : 0` here waited for them where they were issued)
   auto load = [&](uint64_t c0, uint32_t (&x)[E]) {
-    const uint32_t m = (uint32_t)min((uint64_t)kSplitChunk, hi - c0);
     const uint32_t vo = 4u * (uint32_t)(c0 - s0 + tid);
 #pragma unroll
-    for (int k = 0; k < E; k++) {
-      const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rin, vo, 4u * kST * k, 0);
-      x[k] = tid + kST * k < m ? v : 0u;
-    }
+    for (int k = 0; k < E; k++) x[k] = __builtin_amdgcn_raw_buffer_load_b32(rin, vo, 4u * kST * k, 0);
   };
   if (lo < hi) load(lo, e);
   for (uint64_t c0 = lo; c0 < hi; c0 += kSplitChunk) {
     const uint32_t m = (uint32_t)min((uint64_t)kSplitChunk, hi - c0);
+    [[maybe_unused]] uint64_t pt = PROF_NOW();
     uint32_t dg[E];
 #pragma unroll
     for (int k = 0; k < E; k++) dg[k] = digit2(P, e[k]);
+    if (prof) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (profile build only: the loads' wait shows up here)
+      PROF_LAP(prof, 0, pt);
+      if (threadIdx.x == 0) prof[7]++;
+    }
     const uint64_t c1 = c0 + kSplitChunk;
-    split_round<kST, E, uint32_t, false, true>(e, dg, m, P.nparts2, cnt, start, cur, sbuf, sdig, P.out2,
-                                               P.vbits + P.shift2, fill, region0, P.cap2, P.err,
-                                               [&]() { if (PG_SPLIT2S_PREFETCH && c1 < hi) load(c1, ne); });
+    auto pre = [&]() { if (PG_SPLIT2S_PREFETCH && c1 < hi) load(c1, ne); };
+    split_round<kST, E, uint32_t, false, true>(e, dg, m, P.nparts2, cnt, start, cur, sbuf, nullptr, P.out2,
+                                               P.vbits + P.shift2, fill, region0, P.cap2, P.err, pre, prof);
     if (!PG_SPLIT2S_PREFETCH && c1 < hi) load(c1, ne);
 #pragma unroll
     for (int k = 0; k < E; k++) e[k] = ne[k];
   }
 }
 
-// One workgroup per bucket b (groups g = b << shift2 | gl): doc count and value bitmap of each group in LDS, then the
-// bucket's slice of the dense state (i64 slot 0 = doc count, the bitmap row) written whole.
-__global__ __launch_bounds__(kAT) void part_aggregate_kernel(PartSpec P) {
-  extern __shared__ uint32_t lds[];
-  const uint32_t b = blockIdx.x, tid = threadIdx.x;
+// Level 2 as its own launch: level-1 partition p's entries (min(fill1[p], cap1) of them) split over kPartNB blocks,
+// buckets at b * cap2 for every bucket b of the plan.
+__global__ __launch_bounds__(kST, PG_SPLIT_WAVES) void part_split2s_kernel(PartSpec P) {
+  __shared__ uint32_t cnt[256], start[256], sbuf[kSplitChunk];
+  __shared__ unsigned long long cur[256];
+  const uint32_t j = blockIdx.x, p = blockIdx.y, tid = threadIdx.x;
+  if (tid < P.nparts2) cnt[tid] = 0;
+  __syncthreads();
+  const uint64_t n = min((uint64_t)P.fill1[p], P.cap1), s0 = (uint64_t)p * P.cap1;
+  uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  split2s_range(P, s0, n, s0 + n * j / kPartNB, s0 + n * (j + 1) / kPartNB, P.fill2 + (uint64_t)p * P.nparts2,
+                (uint64_t)p * P.nparts2 * P.cap2, cnt, start, cur, sbuf, PG_PART_PROF ? prof : nullptr);
+  PROF_FLUSH(1, prof);
+}
+
+// Bucket b (groups g = b << shift2 | gl), entries [lo, hi) of out2: doc count and value bitmap of each group in LDS
+// (lds: (1 + dc_words) words per group, zeroed here), then the bucket's slice of the dense state (i64 slot 0 = doc
+// count, the bitmap row) written whole.
+template <uint32_t NT>  // threads of the workgroup
+__device__ __forceinline__ void aggregate_bucket(const PartSpec& P, uint32_t b, uint64_t lo, uint64_t hi, uint32_t* lds) {
+  const uint32_t tid = threadIdx.x;
   const uint32_t ng = 1u << P.shift2, dw = P.dc_words;
   uint32_t* cnt = lds;        // [ng]
   uint32_t* bm = lds + ng;    // [ng][dw]
-  for (uint32_t i = tid; i < ng * (1u + dw); i += kAT) lds[i] = 0;
+  [[maybe_unused]] uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  [[maybe_unused]] uint64_t pt = PROF_NOW();
+  for (uint32_t i = tid; i < ng * (1u + dw); i += NT) lds[i] = 0;
   __syncthreads();
+  PROF_LAP(prof, 0, pt);
+  const uint32_t gm = ng - 1u, vm = (1u << P.vbits) - 1u, vb = P.vbits;
+  // the bucket's entries by buffer loads relative to lo (reads past the bucket's region return 0), kAggB per lane in
+  // flight and the next batch issued before this one is counted: the pass is bound by load latency otherwise
+  // (4 loads per lane: 66k cycles per 51k-entry bucket on config 4, r05 PG_PART_PROF)
+  constexpr int B = kAggB;
+  const uint64_t n = hi - lo;
+  const rsrc_t rin = part_rsrc(P.out2 + lo, (uint32_t)(4ull * n));
+  uint32_t e[B], ne[B];
+  auto load = [&](uint32_t base, uint32_t (&x)[B]) {
+#pragma unroll
+    for (int k = 0; k < B; k++) x[k] = __builtin_amdgcn_raw_buffer_load_b32(rin, 4u * (base + tid), 4u * NT * k, 0);
+  };
+  load(0, e);
+  for (uint32_t base = 0; base < n; base += B * NT) {
+    // issued whatever remains (reads past the region return 0): a conditional load here made the compiler wait for
+    // every outstanding load at the first use below, which undid the prefetch
+    load(base + B * NT, ne);
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+      if (base + tid + NT * k < n) {
+        const uint32_t g = (e[k] >> vb) & gm;
+        if (P.count_docs) atomicAdd(&cnt[g], 1u);
+        if (dw) {
+          const uint32_t v = e[k] & vm;
+          atomicOr(&bm[g * dw + (v >> 5)], 1u << (v & 31u));
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < B; k++) e[k] = ne[k];
+  }
+  __syncthreads();
+  PROF_LAP(prof, 1, pt);
+  const uint64_t g0 = (uint64_t)b << P.shift2;
+  const uint32_t ng_out = (uint32_t)(g0 + ng <= P.num_groups ? ng : (g0 < P.num_groups ? P.num_groups - g0 : 0));
+  const bool want_pop = dw && (P.dc_pop || !P.count_docs);
+  if (want_pop && dw == 32 && NT >= 2 * 512 && ng <= NT / 2) {
+    // the group's set size (extractFinalResult) while its bitmap is in LDS: two lanes per group, 16 words each as four
+    // 16-B reads (a wave reads 32 whole rows per instruction), halves combined across the lane pair
+    const uint32_t gl = tid >> 1, h = tid & 1u;
+    uint32_t pc = 0;
+    if (gl < ng) {
+      const uint4* row = (const uint4*)(bm + gl * 32u + h * 16u);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint4 x = row[k];
+        pc += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+      }
+    }
+    pc += __shfl_xor(pc, 1);
+    if (gl < ng_out && h == 0) {
+      // slot 0: the doc count, or with no COUNT aggregation (count_docs 0) the set size -- nonzero exactly for the
+      // groups that have a doc, which is all a DISTINCTCOUNT-only state reads from it
+      P.i64[(g0 + gl) * P.n_i64] = P.count_docs ? cnt[gl] : pc;
+      if (P.dc_pop) P.dc_pop[g0 + gl] = pc;
+    }
+  } else {
+    for (uint32_t gl = tid; gl < ng_out; gl += NT) {
+      uint32_t pc = 0;
+      if (want_pop)
+        for (uint32_t k = 0, r = gl % dw; k < dw; k++, r = r + 1 == dw ? 0 : r + 1) pc += __popc(bm[gl * dw + r]);  // lanes on distinct banks
+      P.i64[(g0 + gl) * P.n_i64] = P.count_docs ? cnt[gl] : pc;
+      if (P.dc_pop && dw) P.dc_pop[g0 + gl] = pc;
+    }
+  }
+  if (P.row_words) {
+    const uint32_t rw = P.row_words;
+    uint32_t* __restrict__ dst = P.bits + g0 * rw;
+    for (uint32_t w = tid; w < ng_out * rw; w += NT) {
+      const uint32_t gl = w / rw, k = w - gl * rw;
+      dst[w] = (k >= P.dc_word && k < P.dc_word + dw) ? bm[gl * dw + (k - P.dc_word)] : 0u;
+    }
+  }
+  if (PG_PART_PROF) {
+    __syncthreads();
+    PROF_LAP(prof, 2, pt);
+    PROF_FLUSH(2, prof);
+  }
+}
+
+// One workgroup per bucket b: its entries at [off2[b * kPartNB], off2[(b + 1) * kPartNB]) (exact layout) or
+// [b * cap2, b * cap2 + min(fill2[b], cap2)) (speculative).
+__global__ __launch_bounds__(kAT) void part_aggregate_kernel(PartSpec P) {
+  extern __shared__ uint32_t lds[];
+  const uint32_t b = blockIdx.x;
   uint64_t lo, hi;
   if (P.fill2) {
     lo = (uint64_t)b * P.cap2;
@@ -323,49 +468,7 @@ __global__ __launch_bounds__(kAT) void part_aggregate_kernel(PartSpec P) {
     lo = P.off2[(uint64_t)b * kPartNB];
     hi = P.off2[(uint64_t)(b + 1) * kPartNB];
   }
-  const uint32_t gm = ng - 1u, vm = (1u << P.vbits) - 1u, vb = P.vbits;
-  const uint32_t* __restrict__ in = P.out2;
-  uint64_t i = lo + tid;
-  if (dw) {
-    for (; i + 3 * kAT < hi; i += 4 * kAT) {  // four independent loads in flight per lane
-      uint32_t e[4];
-#pragma unroll
-      for (int k = 0; k < 4; k++) e[k] = in[i + kAT * k];
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const uint32_t g = (e[k] >> vb) & gm, v = e[k] & vm;
-        atomicAdd(&cnt[g], 1u);
-        atomicOr(&bm[g * dw + (v >> 5)], 1u << (v & 31u));
-      }
-    }
-    for (; i < hi; i += kAT) {
-      const uint32_t e = in[i];
-      const uint32_t g = (e >> vb) & gm, v = e & vm;
-      atomicAdd(&cnt[g], 1u);
-      atomicOr(&bm[g * dw + (v >> 5)], 1u << (v & 31u));
-    }
-  } else {
-    for (; i < hi; i += kAT) atomicAdd(&cnt[(in[i] >> vb) & gm], 1u);
-  }
-  __syncthreads();
-  const uint64_t g0 = (uint64_t)b << P.shift2;
-  const uint32_t n = (uint32_t)(g0 + ng <= P.num_groups ? ng : (g0 < P.num_groups ? P.num_groups - g0 : 0));
-  for (uint32_t gl = tid; gl < n; gl += kAT) {
-    P.i64[(g0 + gl) * P.n_i64] = cnt[gl];
-    if (P.dc_pop && dw) {  // the group's DISTINCTCOUNT (extractFinalResult = set size) while its bitmap is in LDS
-      uint32_t pc = 0;
-      for (uint32_t k = 0, r = gl % dw; k < dw; k++, r = r + 1 == dw ? 0 : r + 1) pc += __popc(bm[gl * dw + r]);  // lanes on distinct banks
-      P.dc_pop[g0 + gl] = pc;
-    }
-  }
-  if (P.row_words) {
-    const uint32_t rw = P.row_words;
-    uint32_t* __restrict__ dst = P.bits + g0 * rw;
-    for (uint32_t w = tid; w < n * rw; w += kAT) {
-      const uint32_t gl = w / rw, k = w - gl * rw;
-      dst[w] = (k >= P.dc_word && k < P.dc_word + dw) ? bm[gl * dw + (k - P.dc_word)] : 0u;
-    }
-  }
+  aggregate_bucket<kAT>(P, b, lo, hi, lds);
 }
 
 // ------------------------------------------------------------------------------------------ level 1 from the columns
@@ -516,32 +619,32 @@ static_assert(kDT % 64 == 0 && kDT <= 1024 && kDE <= 32, "part_direct blocks: wh
 
 // The tile's word range [w0, w0 + nw) of a packed column into LDS (16-byte loads; reads past the column return 0).
 // nw is a multiple of 4 plus the 4 words of padding the unpack's 64-bit window may touch.
+// Every pass's load is issued before the first is stored (a load-store loop waited for each load in turn); passes are
+// skipped by a block-uniform test, lanes past nw load a few words they do not store.
+constexpr uint32_t kStageQ = ((256u * 32u + 4u) / 4u + kDT - 1u) / kDT;  // uint4 passes for a 32-bit column
 __device__ __forceinline__ void stage_words(rsrc_t r, uint32_t w0, uint32_t nw, uint32_t* lds) {
-  for (uint32_t q = threadIdx.x; q < nw / 4; q += kDT) {
-    const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, (w0 + 4u * q) * 4u, 0, 0);
-    *(uint4*)(lds + 4u * q) = make_uint4(x[0], x[1], x[2], x[3]);
-  }
-}
-
-// The same word range loaded into registers (thread t: uint4s t + kDT r) while the block sorts the previous tile, and
-// stored to LDS once the stage is free again: the next tile's HBM latency hides behind this tile's sort and writes.
-constexpr uint32_t kPreQ = ((256u * 32u + 4u) / 4u + kDT - 1u) / kDT;  // uint4s per thread for the widest column
-__device__ __forceinline__ void pre_load(rsrc_t r, uint32_t w0, uint32_t nw, uint4 (&x)[kPreQ]) {
+  uint4 x[kStageQ];
 #pragma unroll
-  for (uint32_t k = 0; k < kPreQ; k++) {
-    const uint32_t q = threadIdx.x + kDT * k;
-    if (q < nw / 4) {
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (w0 + 4u * q) * 4u, 0, 0);
+  for (uint32_t k = 0; k < kStageQ; k++)
+    if (kDT * k < nw / 4) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (w0 + 4u * (threadIdx.x + kDT * k)) * 4u, 0, 0);
       x[k] = make_uint4(v[0], v[1], v[2], v[3]);
     }
-  }
-}
-__device__ __forceinline__ void pre_store(uint32_t* lds, uint32_t nw, const uint4 (&x)[kPreQ]) {
 #pragma unroll
-  for (uint32_t k = 0; k < kPreQ; k++) {
+  for (uint32_t k = 0; k < kStageQ; k++) {
     const uint32_t q = threadIdx.x + kDT * k;
     if (q < nw / 4) *(uint4*)(lds + 4u * q) = x[k];
   }
+}
+
+// The same word range into LDS by LDS-DMA (buffer_load_dwordx4 ... lds: no registers, reads past the column return 0):
+// wave v's pass r covers uint4s q = r * kDT + 64 v + lane, landing at lds + 4 q.  Waited for by vmcnt, not lgkmcnt.
+__device__ __forceinline__ void dma_words(rsrc_t r, uint32_t w0, uint32_t nw, uint32_t* lds) {
+  const uint32_t lane = threadIdx.x & 63u, q0w = (threadIdx.x >> 6) * 64u;
+  for (uint32_t q0 = q0w; q0 < nw / 4; q0 += kDT)
+    if (q0 + lane < nw / 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(lds + 4u * q0), 16,
+                                               (w0 + 4u * (q0 + lane)) * 4u, 0, 0, 0);
 }
 
 // the b-bit value at bit p of a packed run staged at lds (FixedBitIntReader: MSB first)
@@ -605,17 +708,31 @@ __device__ __forceinline__ uint32_t direct_unpack(const PartDirectSpec& P, const
 }
 
 // KM / VM: the id modes of the key / value column, uniform over the plan's segments (runtime-checked).  W: waves per
-// SIMD the register budget is cut for (PG_DIRECT_WAVES).
-template <int KM, int VM, int W>
+// SIMD the register budget is cut for (PG_DIRECT_WAVES).  PRE: the stage has LDS of its own, and the next tile's words
+// are DMA'd into it while this tile is sorted and written (issued after the reservations -- a returned atomic waits
+// for every older vector-memory op -- and carried across raw barriers, which do not drain vmcnt); else the stage and
+// the sort buffer share LDS and each tile's words are loaded when it starts.
+//
+// LDS (one dynamic array, 16-B aligned carve): stage [stage_words] | sort: sbuf [kTileDocs] + sdig [kTileDocs bytes]
+// (PRE: after the stage; else over it) | cnt [kPartL1 + 4] | start [kPartL1] | cur [kPartL1] (8 B) | wsum [16].
+template <int KM, int VM, int W, bool PRE>
 __global__ __launch_bounds__(kDT, W) void part_direct_kernel(PartDirectSpec P) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t dl[];  // stage (key | value words) / sort (sbuf | sdig)
-  __shared__ uint32_t cnt[kPartL1 + 1], start[kPartL1];
-  __shared__ unsigned long long cur[kPartL1];
+  extern __shared__ __attribute__((aligned(16))) uint32_t dl[];
+  const uint32_t sw = P.stage_words;
+  const uint32_t so = PRE ? sw : 0u, sort_words = kTileDocs + kTileDocs / 4;
+  const uint32_t mo = PRE ? sw + sort_words : (sw > sort_words ? sw : sort_words);
+  uint32_t* sbuf = dl + so;
+  uint8_t* sdig = (uint8_t*)(dl + so + kTileDocs);
+  uint32_t* cnt = dl + mo;                   // [kPartL1 + 1] (+ pad)
+  uint32_t* start = cnt + kPartL1 + 4;       // [kPartL1]
+  unsigned long long* cur = (unsigned long long*)(start + kPartL1);  // [kPartL1]
+  uint32_t* wsum = (uint32_t*)(cur + kPartL1);                       // [kDT / 64]
   const uint32_t b = blockIdx.x, tid = threadIdx.x;
   if (tid < kPartL1) cnt[tid] = 0;
   if (tid == 0) cnt[kPartL1] = 0;  // the spare digit of docs past the segment
   __syncthreads();
   uint32_t bad = 0;
+  [[maybe_unused]] uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const uint64_t i0 = (uint64_t)b * P.num_items / P.blocks, i1 = (uint64_t)(b + 1) * P.num_items / P.blocks;
   for (uint64_t it = i0; it < i1; it++) {
     const WorkItem w = ldcf(P.items, it);
@@ -633,20 +750,26 @@ __global__ __launch_bounds__(kDT, W) void part_direct_kernel(PartDirectSpec P) {
     const int64_t kbase = kmap ? 0 : P.key_base, vbase = vmap ? 0 : P.val_base;
     const uint32_t num_docs = __builtin_amdgcn_readfirstlane(sd.num_docs);
     const uint32_t t_end = min(w.tile_end, (num_docs + (uint32_t)kTileDocs - 1u) / (uint32_t)kTileDocs);
-    bool staged = false;  // this tile's words already in LDS (prefetched during the previous round)
+    bool staged = false;  // this tile's words already DMA'd into the stage during the previous tile (PRE)
     for (uint32_t t = w.tile_begin; t < t_end; t++) {
       const uint32_t r0 = t * (uint32_t)kTileDocs;
       const uint32_t m = min((uint32_t)kTileDocs, num_docs - r0);
+      [[maybe_unused]] uint64_t pt = PROF_NOW();
       // 1. the tile's words of both columns, coalesced, into LDS
-      if (!staged) {
+      if (staged) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed; the barrier: every wave's
+        __syncthreads();
+      } else {
         stage_words(rk, t * 256u * kb, nwk, dl);
         if (P.has_val) stage_words(rv, t * 256u * vb, nwv, dl + nwk);
         __syncthreads();
       }
+      PROF_LAP(prof, 0, pt);
       // 2. entries + ranks ((digit << 16 | rank) and the entry are all a thread keeps)
       uint32_t dr[kDE], e[kDE];
       bad |= direct_unpack<KM, VM>(P, kc, vc, ktab, kbase, vtab, vbase, dl, dl + nwk, kb, vb, m, cnt, dr, e);
-      __syncthreads();  // every rank taken; the stage is dead: its LDS becomes the sort buffer
+      __syncthreads();  // every rank taken; the stage is dead (!PRE: its LDS becomes the sort buffer)
+      PROF_LAP(prof, 1, pt);
       // 3. run starts (exclusive scan of the digit counts) and one reservation per non-empty run
       {
         const uint32_t c = tid < P.nparts1 ? cnt[tid] : 0u;
@@ -657,7 +780,6 @@ __global__ __launch_bounds__(kDT, W) void part_direct_kernel(PartDirectSpec P) {
           const uint32_t y = __shfl_up(x, o);
           if (lane >= (uint32_t)o) x += y;
         }
-        __shared__ uint32_t wsum[kDT / 64];
         if (lane == 63) wsum[wave] = x;
         __syncthreads();
         uint32_t wb = 0;
@@ -668,9 +790,9 @@ __global__ __launch_bounds__(kDT, W) void part_direct_kernel(PartDirectSpec P) {
           if (c) {
             const uint32_t old = atomicAdd(&P.fill1[tid], c);
             if ((uint64_t)old + c <= P.cap1) {
-              cur[tid] = (uint64_t)tid * P.cap1 + old;
+              cur[tid] = (uint64_t)tid * P.cap1 + old - (wb + x - c);  // run start - its sort position
             } else {
-              cur[tid] = ~0ull;
+              cur[tid] = 1ull << 63;  // dropped (never a run start - sort position value)
               atomicOr(P.err, 16u);
             }
           }
@@ -678,19 +800,13 @@ __global__ __launch_bounds__(kDT, W) void part_direct_kernel(PartDirectSpec P) {
         if (tid == 0) cnt[kPartL1] = 0;
       }
       __syncthreads();
-      // the next tile of this item: its loads go out now (after the reservations, whose returned values wait on every
-      // outstanding vector load) and land in registers while this tile is sorted and written
-#ifndef PG_DIRECT_PREFETCH
-#define PG_DIRECT_PREFETCH 0  // 1: the next tile's words into registers during the sort (for one block per CU)
-#endif
-      const bool pre = PG_DIRECT_PREFETCH && t + 1 < t_end;
-      uint4 pk[kPreQ], pv[kPreQ];
+      PROF_LAP(prof, 2, pt);
+      // PRE: the next tile's words go out now, into the stage (dead since step 2's barrier)
+      const bool pre = PRE && t + 1 < t_end;
       if (pre) {
-        pre_load(rk, (t + 1) * 256u * kb, nwk, pk);
-        if (P.has_val) pre_load(rv, (t + 1) * 256u * vb, nwv, pv);
+        dma_words(rk, (t + 1) * 256u * kb, nwk, dl);
+        if (P.has_val) dma_words(rv, (t + 1) * 256u * vb, nwv, dl + nwk);
       }
-      uint32_t* sbuf = dl;
-      uint8_t* sdig = (uint8_t*)(dl + kTileDocs);
 #pragma unroll
       for (int j = 0; j < (int)kDE; j++) {
         const uint32_t d = dr[j] >> 16;
@@ -700,30 +816,46 @@ __global__ __launch_bounds__(kDT, W) void part_direct_kernel(PartDirectSpec P) {
           sdig[at] = (uint8_t)d;
         }
       }
-      __syncthreads();
-      // 4. the runs, written out whole
-      for (uint32_t i = tid; i < m; i += kDT) {
-        const uint32_t d = sdig[i];
-        const unsigned long long c0 = cur[d];
-        if (c0 != ~0ull) P.out1[c0 + (i - start[d])] = sbuf[i];
-      }
-      __syncthreads();
-      if (pre) {
-        pre_store(dl, nwk, pk);
-        if (P.has_val) pre_store(dl + nwk, nwv, pv);
+      if (PRE) {  // a raw barrier: __syncthreads() would drain the DMA in flight (vmcnt(0))
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      } else {
         __syncthreads();
       }
+      PROF_LAP(prof, 3, pt);
+      // 4. the runs, written out whole
+      for (uint32_t i = tid; i < m; i += kDT) {  // cur[d] already holds the run's start minus its sort position
+        const unsigned long long c0 = cur[sdig[i]];
+        if (c0 != (1ull << 63)) P.out1[c0 + i] = sbuf[i];
+      }
+      // PRE: the next tile's first barrier (or the next item's stage barrier) orders these reads before the sort
+      // buffer's next writes; !PRE: the next stage overwrites the sort buffer
+      if (!PRE) __syncthreads();
+      else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      PROF_LAP(prof, 4, pt);
+      if (PG_PART_PROF && tid == 0) prof[7]++;
       staged = pre;
     }
   }
   if (bad) atomicOr(P.err, bad);
+  PROF_FLUSH(0, prof);
 }
 
-hipError_t launch_part_direct(const PartDirectSpec& p, uint32_t key_bits, uint32_t val_bits, int key_mode, int val_mode,
+static void prof_report_direct(uint64_t blocks) {
+#if PG_PART_PROF
+  prof_report("part_direct", 0, blocks);
+#endif
+}
+hipError_t launch_part_direct(const PartDirectSpec& p_in, uint32_t key_bits, uint32_t val_bits, int key_mode, int val_mode,
                               hipStream_t s) {
-  const size_t stage = 4ull * ((256ull * key_bits + 4) + (p.has_val ? 256ull * val_bits + 4 : 0));
-  const size_t sort = 4ull * kTileDocs + kTileDocs;  // sbuf + sdig
-  const size_t lds = stage > sort ? stage : sort;
+  PartDirectSpec p = p_in;
+  // stage words of the widest key / value column (a multiple of 4: 16-B aligned carve)
+  p.stage_words = (uint32_t)((256ull * key_bits + 4) + (p.has_val ? 256ull * val_bits + 4 : 0));
+  const uint32_t sort_words = kTileDocs + kTileDocs / 4, misc_words = (kPartL1 + 4) + kPartL1 + 2 * kPartL1 + 16;
+  // PRE when stage + sort + misc leave two resident blocks per CU (config 4: 79.9 KB per block); PG_DIRECT_PRE=0 off
+  const size_t pre_bytes = 4ull * (p.stage_words + sort_words + misc_words);
+  const char* pe = getenv("PG_DIRECT_PRE");
+  const bool pre = pre_bytes <= 80 * 1024 && !(pe && atoi(pe) == 0);
+  const size_t lds = pre ? pre_bytes : 4ull * (std::max(p.stage_words, sort_words) + misc_words);
   const dim3 g(p.blocks), b(kDT);
 #ifndef PG_DIRECT_WAVES2
 #define PG_DIRECT_WAVES2 (3 * PG_DIRECT_THREADS / 256)
@@ -733,8 +865,10 @@ hipError_t launch_part_direct(const PartDirectSpec& p, uint32_t key_bits, uint32
   static const int waves = getenv("PG_DIRECT_WAVES") ? atoi(getenv("PG_DIRECT_WAVES")) : kW0;
 #define PG_DIRECT(K, V)                                                                                 \
   if (key_mode == (K) && val_mode == (V)) {                                                             \
-    if (waves == kW1) hipLaunchKernelGGL((part_direct_kernel<K, V, kW1>), g, b, lds, s, p);             \
-    else hipLaunchKernelGGL((part_direct_kernel<K, V, kW0>), g, b, lds, s, p);                          \
+    if (pre) hipLaunchKernelGGL((part_direct_kernel<K, V, kW0, true>), g, b, lds, s, p);                \
+    else if (waves == kW1) hipLaunchKernelGGL((part_direct_kernel<K, V, kW1, false>), g, b, lds, s, p); \
+    else hipLaunchKernelGGL((part_direct_kernel<K, V, kW0, false>), g, b, lds, s, p);                   \
+    if (PG_PART_PROF) prof_report_direct(p.blocks);                                                     \
     return hipGetLastError();                                                                           \
   }
   PG_DIRECT(0, -1) PG_DIRECT(0, 0) PG_DIRECT(0, 1) PG_DIRECT(1, -1) PG_DIRECT(1, 0) PG_DIRECT(1, 1)
@@ -744,9 +878,11 @@ hipError_t launch_part_direct(const PartDirectSpec& p, uint32_t key_bits, uint32
 int part_id_mode(uint32_t key_kind, const ColDesc& c) { return id_mode(key_kind, c); }
 hipError_t launch_part_split2s(const PartSpec& p, hipStream_t s) {
   hipLaunchKernelGGL(part_split2s_kernel, dim3(kPartNB, p.nparts1), dim3(kST), 0, s, p);
+#if PG_PART_PROF
+  prof_report("split2s", 1, (uint64_t)kPartNB * p.nparts1);
+#endif
   return hipGetLastError();
 }
-
 hipError_t launch_part_hist(const PartScanSpec& p, hipStream_t s) {
   if (p.num_keys <= 1) hipLaunchKernelGGL(part_hist_kernel<1>, dim3(p.blocks), dim3(kST), 0, s, p);
   else hipLaunchKernelGGL(part_hist_kernel<kMaxKeys>, dim3(p.blocks), dim3(kST), 0, s, p);
@@ -773,6 +909,9 @@ hipError_t launch_part_split2(const PartSpec& p, hipStream_t s) {
 hipError_t launch_part_aggregate(const PartSpec& p, hipStream_t s) {
   const size_t lds = (size_t)(1u << p.shift2) * (1u + p.dc_words) * 4u;
   hipLaunchKernelGGL(part_aggregate_kernel, dim3(p.nparts1 * p.nparts2), dim3(kAT), lds, s, p);
+#if PG_PART_PROF
+  prof_report("aggregate", 2, (uint64_t)p.nparts1 * p.nparts2);
+#endif
   return hipGetLastError();
 }
 

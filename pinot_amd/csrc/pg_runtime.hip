@@ -3387,6 +3387,10 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     ps.i64 = (unsigned long long*)P.i64.p;
     ps.bits = (uint32_t*)P.bits.p;
     ps.dc_pop = P.dc_pop_agg >= 0 ? (uint32_t*)P.dc_pop.p : nullptr;
+    // slot 0 holds the doc count only when a COUNT reads it (or there is no value set to mark presence with)
+    ps.count_docs = part.dc == (uint32_t)kNoSlot ? 1u : 0u;
+    for (uint32_t a = 0; a < A; a++)
+      if (P.aggs[a].fn == PG_AGG_COUNT) ps.count_docs = 1u;
     ps.err = q.err;
     if (spec) {
       ps.fill1 = (const unsigned int*)p_fill.p;
@@ -3394,13 +3398,14 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       ps.cap1 = cap1;
       ps.cap2 = cap2;
       HIP_CHECK(launch_part_split2s(ps, s));
+      HIP_CHECK(launch_part_aggregate(ps, s));
     } else {
       if (!direct) HIP_CHECK(launch_part_split1(ps, s));
       HIP_CHECK(launch_part_count2(ps, s));
       HIP_CHECK(launch_exclusive_sum((const uint64_t*)h2, (uint64_t*)o2, n2 + 1, p_temp.p, tb, s));
       HIP_CHECK(launch_part_split2(ps, s));
+      HIP_CHECK(launch_part_aggregate(ps, s));
     }
-    HIP_CHECK(launch_part_aggregate(ps, s));
   } else if (ix.on) {
     t_timing.host_compile_ms = (float)(wall_ms() - t_enter);
     HIP_CHECK(launch_index_count(ix.spec, ix.blocks, s));
