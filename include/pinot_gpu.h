@@ -370,6 +370,10 @@ int pg_result_free(pg_result *res);
  * All pointers are device pointers owned by the handle. */
 #define PG_STATE_DENSE 0
 #define PG_STATE_HASH 1
+/* wide group keys (more than kMaxKeys keys, or a key-cardinality product of 2^62 and more: DictionaryBasedGroupKeyGenerator's
+ * ArrayMapBasedHolder): the packed key is a slot of the state's own tuple table, local to it.  Such states merge only
+ * through the row exchange, whose rows carry the tuple (pg_partials_export). */
+#define PG_STATE_TUPLES 2
 #define PG_EMPTY_KEY 0xFFFFFFFFFFFFFFFFull
 
 typedef struct pg_partials {
@@ -411,6 +415,9 @@ int pg_partials_copy(pg_partials *p, int dir, void *i64, void *fx, void *mn, voi
 /* Sparse merge (GroupByOrderByCombineOperator's value-keyed merge across GPUs): the groups of `p` as rows
  *   { u64 packed key | i64[n_i64] | i64 fx[n_fx][2] | i64 mn[n_min] | i64 mx[n_max] | u32 bitmaps[bitmap_words] }
  * (row_bytes each, 8-byte aligned), bucketed by owner part = pg_key_owner(key, num_parts), buckets in part order.
+ * PG_STATE_TUPLES: each row is followed by its K table-global key ids (u32, padded to 8 bytes; row_bytes includes
+ * them) and the owner part is a hash of those ids, so a group has one owner on every GPU; the merge target re-interns
+ * them (IndexedTable.upsert of a Key(Object[]), IndexedTable.java:103-117).
  * part_counts[num_parts] (host) receives the rows per bucket.  dst (DEVICE, dst_rows rows) may be NULL to only
  * count.  Synchronous on `stream`. */
 int pg_partials_export(pg_partials *p, uint32_t num_parts, void *dst, uint64_t dst_rows, uint64_t *part_counts,

@@ -203,10 +203,12 @@ class OracleEngine:
             di = np.ctypeslib.as_array(r.distinct_dict_ids, shape=(r.num_distinct,))
             for g_a, d in zip(ga.tolist(), di.tolist()):
                 distinct.setdefault(g_a, []).append(d)
-        key_dicts = [seg.columns[c].dictionary for c in plan.query.group_by]
+        # a raw key column's "dictId" is a doc holding the value (orc_execute_segment's no-dictionary generator)
+        key_vals = [seg.columns[c].dictionary.values if seg.columns[c].dictionary is not None
+                    else seg.columns[c].raw_values for c in plan.query.group_by]
         rows = {}
         for g in range(G):
-            key = tuple(_py(key_dicts[k].values[int(keys[g, k])]) for k in range(K))
+            key = tuple(_py(key_vals[k][int(keys[g, k])]) for k in range(K))
             row = []
             for a, ag in enumerate(aggs):
                 f = ag.function

@@ -701,20 +701,63 @@ static int32_t tuple_get_or_put(tuple_map *m, const int32_t *t, uint64_t limit) 
   return (int32_t)m->n++;
 }
 
+/* NoDictionarySingleColumnGroupKeyGenerator / NoDictionaryMultiColumnGroupKeyGenerator (DefaultGroupByExecutor.java:
+ * 85-94 pick them when any group-by column has no dictionary): the single-column generator maps each raw value to a
+ * group id in first-seen doc order (getKeyForValue :416-424, INVALID_ID once numGroupsLimit ids exist); the
+ * multi-column one gives each raw column's values ids in first-seen order (its on-the-fly dictionaries) and maps the id
+ * tuples the same way (getGroupIdForKey :318-328).  Both assign group ids in first-seen order of the value tuples, so
+ * here a raw key column's per-doc ids are replaced by first-seen value ids (raw_key_ids) and the tuple -> group id map
+ * below runs with the array-based holder off.  The map key of a value: INT / LONG the value, FLOAT / DOUBLE
+ * Float.floatToIntBits / Double.doubleToLongBits (fastutil's Float2IntOpenHashMap equality: one NaN, -0.0 != 0.0). */
+static uint64_t raw_key_bits(const orc_column *c, uint32_t doc) {
+  const uint8_t *p = c->dict + (uint64_t)doc * c->entry_bytes;
+  switch (c->data_type) {
+    case PG_INT: return (uint64_t)(int64_t)(int32_t)be32(p);
+    case PG_LONG: return be64(p);
+    case PG_FLOAT: { uint32_t u = be32(p); if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) u = 0x7fc00000u; return u; }
+    case PG_DOUBLE: {
+      uint64_t u = be64(p);
+      if (((u >> 52) & 0x7ff) == 0x7ff && (u & 0xfffffffffffffULL)) u = 0x7ff8000000000000ULL;
+      return u;
+    }
+    default: return 0;
+  }
+}
+/* ids[i] (in: the doc of match i, a raw column's "dictId") -> the value's first-seen id; rep[id] = the first doc holding
+ * the value (the output's "dictId" for it).  Returns the number of distinct values. */
+static uint64_t raw_key_ids(const orc_column *c, int32_t *ids, uint64_t n, int32_t **rep_out) {
+  id_map m = {0};
+  m.cap = 1024;
+  m.keys = (uint64_t *)malloc(m.cap * 8);
+  m.ids = (int32_t *)malloc(m.cap * 4);
+  for (uint64_t i = 0; i < m.cap; i++) m.ids[i] = -1;
+  int32_t *rep = (int32_t *)malloc(sizeof(int32_t) * (n ? n : 1));
+  for (uint64_t i = 0; i < n; i++) {
+    const uint64_t before = m.n;
+    const int32_t id = map_get_or_put(&m, raw_key_bits(c, (uint32_t)ids[i]), UINT64_MAX);
+    if (m.n > before) rep[id] = ids[i];
+    ids[i] = id;
+  }
+  free(m.keys); free(m.ids);
+  *rep_out = rep;
+  return m.n;
+}
+
 static void aggregate_group_by(const pg_plan *plan, const orc_column *cols, const uint32_t *docs, uint64_t n,
                                agg_input *inputs, int32_t **key_ids, orc_segment_result *r,
-                               uint64_t array_based_threshold) {
+                               uint64_t array_based_threshold, int32_t *const *raw_rep, const uint64_t *raw_cards) {
   uint32_t K = plan->num_keys, A = plan->num_aggs;
   uint64_t card_prod = 1;
-  int overflow = 0;
+  int overflow = 0, nodict = 0;
   uint64_t cards[64];
   for (uint32_t k = 0; k < K; k++) {
-    cards[k] = cols[plan->keys[k].col_id].cardinality;
+    nodict |= raw_rep[k] != NULL;
+    cards[k] = raw_rep[k] ? raw_cards[k] : cols[plan->keys[k].col_id].cardinality;
     /* cardinalityProduct > Long.MAX_VALUE / cardinality -> longOverflow (:117-131) */
     if (overflow || card_prod > (uint64_t)INT64_MAX / (cards[k] ? cards[k] : 1)) overflow = 1; else card_prod *= cards[k];
   }
   uint64_t limit = plan->num_groups_limit ? plan->num_groups_limit : 100000;
-  int array_based = !overflow && card_prod <= array_based_threshold;
+  int array_based = !nodict && !overflow && card_prod <= array_based_threshold;  /* dictionary keys only */
   uint64_t upper = array_based ? card_prod : limit;
   id_map m = {0};
   tuple_map tm = {0};
@@ -806,6 +849,8 @@ static void aggregate_group_by(const pg_plan *plan, const orc_column *cols, cons
       uint64_t raw = raw_of_gid[g];
       for (uint32_t k = 0; k < K; k++) { r->key_dict_ids[o * K + k] = (int32_t)(raw % cards[k]); raw /= cards[k]; }
     }
+    for (uint32_t k = 0; k < K; k++)  /* a raw key's value id -> a doc holding the value */
+      if (raw_rep[k]) r->key_dict_ids[o * K + k] = raw_rep[k][r->key_dict_ids[o * K + k]];
     for (uint32_t a = 0; a < A; a++) {
       r->values[o * A + a] = plan->aggs[a].fn == PG_AGG_DISTINCTCOUNT ? 0.0 : vals[g * A + a];
       r->counts[o * A + a] = cnts[g * A + a];
@@ -959,15 +1004,18 @@ int orc_execute_segment(const pg_plan *plan, uint32_t seg, const orc_column *col
     used[g->col_a] = 1;
     if (g->op != PG_EXPR_COL) { inputs[a].ids_b = sv_dict_ids_at(&cols[g->col_b], docs, n); used[g->col_b] = 1; }
   }
-  int32_t *key_ids[64] = {0};
+  int32_t *key_ids[64] = {0}, *raw_rep[64] = {0};
+  uint64_t raw_cards[64] = {0};
   for (uint32_t k = 0; k < plan->num_keys; k++) {
-    key_ids[k] = sv_dict_ids_at(&cols[plan->keys[k].col_id], docs, n);
+    const orc_column *kc = &cols[plan->keys[k].col_id];
+    key_ids[k] = sv_dict_ids_at(kc, docs, n);
+    if (kc->fwd_kind == ORC_FWD_RAW) raw_cards[k] = raw_key_ids(kc, key_ids[k], n, &raw_rep[k]);
     used[plan->keys[k].col_id] = 1;
   }
   for (int i = 0; i < 256; i++) projected += used[i];
 
   if (plan->num_keys == 0) aggregate_only(plan, cols, docs, n, inputs, r);
-  else aggregate_group_by(plan, cols, docs, n, inputs, key_ids, r, array_based_threshold);
+  else aggregate_group_by(plan, cols, docs, n, inputs, key_ids, r, array_based_threshold, raw_rep, raw_cards);
 
   r->stats.num_docs_scanned = n;
   r->stats.num_entries_scanned_in_filter = scanned;
@@ -979,7 +1027,7 @@ int orc_execute_segment(const pg_plan *plan, uint32_t seg, const orc_column *col
     free(inputs[a].ids_a); free(inputs[a].ids_b);
     if (inputs[a].has_mv) free(inputs[a].mv.offsets);
   }
-  for (uint32_t k = 0; k < plan->num_keys; k++) free(key_ids[k]);
+  for (uint32_t k = 0; k < plan->num_keys; k++) { free(key_ids[k]); free(raw_rep[k]); }
   free(inputs);
   free(docs);
   *out = r;

@@ -36,7 +36,7 @@ PG_KEY_VALUE_OFFSET, PG_KEY_KEYMAP = 0, 1
 PG_ORDER_AGG, PG_ORDER_KEY = 0, 1
 PG_PLAN_VALUE_SETS, PG_PLAN_HASH_GROUPS, PG_PLAN_F64_SUMS, PG_PLAN_NO_STREAM = 0x1, 0x2, 0x4, 0x8
 PG_PLAN_EXACT_LIMIT = 0x10
-PG_STATE_DENSE, PG_STATE_HASH = 0, 1
+PG_STATE_DENSE, PG_STATE_HASH, PG_STATE_TUPLES = 0, 1, 2
 PG_RESULT_GROUPS_LIMIT_REACHED, PG_RESULT_TRIM_THRESHOLD_REACHED = 0x1, 0x2
 PG_SUM_NONFINITE = 0x1
 PG_EMPTY_KEY = 0xFFFFFFFFFFFFFFFF

@@ -295,6 +295,15 @@ struct WideSpec {
 hipError_t launch_intern_tuples(const WideSpec& w, uint32_t max_docs, hipStream_t s);
 hipError_t launch_gather_tuples(const uint32_t* tuples, uint32_t K, const uint64_t* slots, uint64_t n, uint32_t* out,
                                 hipStream_t s);
+// cross-state merge of wide keys (rows gathered with key_div 1: the key word is the tuple slot): owner part of each
+// row's tuple; rows widened with their tuples (rbw = rb + K uint32
+// padded to 8 bytes); exchanged rows' tuples interned into `w` (err bit 2: table full), out = rows keyed by the slot
+hipError_t launch_wide_owner(const uint32_t* tuples, uint32_t K, const uint8_t* rows, uint64_t rb, uint64_t n,
+                             uint32_t parts, uint32_t* owner, hipStream_t s);
+hipError_t launch_widen_rows(const uint8_t* rows, uint64_t rb, const uint32_t* tuples, uint32_t K, uint64_t n,
+                             uint8_t* dst, uint64_t rbw, hipStream_t s);
+hipError_t launch_intern_rows(const WideSpec& w, const uint8_t* rows, uint64_t n, uint64_t rb, uint64_t rbw,
+                              uint8_t* out, hipStream_t s);
 
 // ---- group state (pg_groups.hip)
 struct StateView {            // the device arrays of one partial state

@@ -879,6 +879,7 @@ struct WideKeys {
   uint32_t K = 0;
   uint64_t cap = 0;
   DevBuf tuples;                       // [cap][K]
+  DevBuf tags, misc;                   // a merge target's (pg_partials_create) intern table tags and [fill, err]
   pg_key key1{};                       // the scan's one key: the tuple slot (kWideColId)
   const pg_plan* user_plan = nullptr;  // during finalize: the caller's plan (K keys, its ORDER BY)
 };
@@ -1392,6 +1393,16 @@ void use_decoded(ColDesc& dc, const ColumnRes* c) {
 // key is a value offset of a column that has one).
 void key_coldesc(ColDesc& dc, const ColumnRes* c, const pg_key& key) {
   memset(&dc, 0, sizeof(dc));
+  if (c->fwd == FWD_RAW) {  // a raw INT / LONG key (value offsets): the range index's packed offsets, else the values
+    dc.dtype = c->dtype;
+    if (c->vals.p) {
+      use_decoded(dc, c);
+    } else {  // "dictId" = doc id (bits 0), "dictionary" = the values, as for a raw aggregation input
+      dc.dict = c->rawv.p;
+      dc.card = c->num_docs;
+    }
+    return;
+  }
   dc.words = (const uint32_t*)c->words.p;
   dc.wbytes = (uint32_t)std::min<uint64_t>(c->words.bytes, 0xFFFFFFF0ull);
   dc.dict = c->dict.p;
@@ -1400,6 +1411,28 @@ void key_coldesc(ColDesc& dc, const ColumnRes* c, const pg_key& key) {
   dc.dtype = c->dtype;
   dc.card = c->card;
   if (key.kind == PG_KEY_VALUE_OFFSET && (c->vals.p || c->identity)) use_decoded(dc, c);
+}
+
+// A group key column usable in segment si: SV dictIds + dictionary (any key kind), or a raw INT / LONG forward index
+// as value offsets (NoDictionarySingleColumnGroupKeyGenerator.java:51 / NoDictionaryMultiColumnGroupKeyGenerator.java:49
+// key raw values; here the value offset is the key id, so segments and GPUs merge by value as for dictionary keys).
+int check_key_column(const ColumnRes* c, const pg_key& key, uint32_t k, uint32_t si) {
+  if (!c) return fail(PG_E_NOTFOUND, "group key column %u not resident in segment %u", key.col_id, si);
+  const bool raw = c->fwd == FWD_RAW;
+  if ((!c->has_dict && !raw) || c->fwd == FWD_NONE || c->fwd == FWD_MV)
+    return fail(PG_E_UNSUPPORTED, "group key column %u unusable in segment %u", key.col_id, si);
+  if (raw && (key.kind != PG_KEY_VALUE_OFFSET || c->dtype > PG_LONG))
+    return fail(PG_E_UNSUPPORTED, "raw group key column %u: value-offset INT / LONG keys only", key.col_id);
+  if (c->dtype > PG_DOUBLE && key.kind != PG_KEY_KEYMAP)
+    return fail(PG_E_INVALID, "non-numeric key column %u needs a keymap", key.col_id);
+  if (key.kind == PG_KEY_KEYMAP && !c->has_keymap) return fail(PG_E_NOTFOUND, "keymap missing for column %u", key.col_id);
+  if (key.kind == PG_KEY_VALUE_OFFSET && c->dtype != PG_INT && c->dtype != PG_LONG)
+    return fail(PG_E_INVALID, "VALUE_OFFSET key on non-integer column %u", key.col_id);
+  const bool has_values = raw ? c->num_docs > 0 : c->card > 0;
+  if (key.kind == PG_KEY_VALUE_OFFSET && has_values &&
+      (c->imin < key.base || (uint64_t)(c->imax - key.base) >= key.cardinality))
+    return fail(PG_E_INVALID, "column %u values outside the key range of key %u", key.col_id, k);
+  return PG_OK;
 }
 
 // Wide group keys (pg_wide.hip): the plan is run with one key, the doc's tuple slot, read from a per-segment column
@@ -1563,17 +1596,10 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       uint64_t prod = 1;
       for (uint32_t k = 0; k < K; k++) {
         const ColumnRes* c = col(si, plan->keys[k].col_id);
-        if (!c || !c->has_dict || c->fwd == FWD_NONE || c->fwd == FWD_MV)
-          return fail(c ? PG_E_UNSUPPORTED : PG_E_NOTFOUND, "group key column %u unusable in segment %u", plan->keys[k].col_id, si);
-        if (c->dtype > PG_DOUBLE && plan->keys[k].kind != PG_KEY_KEYMAP)
-          return fail(PG_E_INVALID, "non-numeric key column %u needs a keymap", plan->keys[k].col_id);
-        if (plan->keys[k].kind == PG_KEY_KEYMAP && !c->has_keymap) return fail(PG_E_NOTFOUND, "keymap missing for column %u", plan->keys[k].col_id);
-        if (plan->keys[k].kind == PG_KEY_VALUE_OFFSET && c->dtype != PG_INT && c->dtype != PG_LONG)
-          return fail(PG_E_INVALID, "VALUE_OFFSET key on non-integer column %u", plan->keys[k].col_id);
-        if (plan->keys[k].kind == PG_KEY_VALUE_OFFSET && c->card &&
-            (c->imin < plan->keys[k].base || (uint64_t)(c->imax - plan->keys[k].base) >= plan->keys[k].cardinality))
-          return fail(PG_E_INVALID, "column %u values outside the key range of key %u", plan->keys[k].col_id, k);
-        prod = prod > (1ull << 62) / (c->card ? c->card : 1) ? (1ull << 62) : prod * c->card;
+        if ((rc = check_key_column(c, plan->keys[k], k, si))) return rc;
+        // distinct values in the segment: the dictionary's size, or (raw) at most its docs and the key range
+        const uint64_t kc = c->fwd == FWD_RAW ? std::min<uint64_t>(c->num_docs, plan->keys[k].cardinality) : c->card;
+        prod = prod > (1ull << 62) / (kc ? kc : 1) ? (1ull << 62) : prod * kc;
       }
       const uint64_t ub = std::min<uint64_t>(prod, plan->segments[si].num_docs);
       seg_groups += ub;
@@ -3578,19 +3604,11 @@ int run_wide(const pg_plan* plan, Partials& P, pg_stats& st) {
         const pg_key& key = plan->keys[k];
         auto ct = it->second->cols.find(key.col_id);
         const ColumnRes* c = ct == it->second->cols.end() ? nullptr : &ct->second;
-        if (!c || !c->has_dict || (c->fwd != FWD_SV && c->fwd != FWD_SORTED))
-          return fail(c ? PG_E_UNSUPPORTED : PG_E_NOTFOUND, "group key column %u unusable in segment %u", key.col_id, si);
+        if ((rc = check_key_column(c, key, k, si))) return rc;
         if (c->num_docs < nd[si]) return fail(PG_E_INVALID, "key column %u has fewer docs than the segment", key.col_id);
-        if (c->dtype > PG_DOUBLE && key.kind != PG_KEY_KEYMAP)
-          return fail(PG_E_INVALID, "non-numeric key column %u needs a keymap", key.col_id);
-        if (key.kind == PG_KEY_KEYMAP && !c->has_keymap) return fail(PG_E_NOTFOUND, "keymap missing for column %u", key.col_id);
-        if (key.kind == PG_KEY_VALUE_OFFSET && (c->dtype != PG_INT && c->dtype != PG_LONG))
-          return fail(PG_E_INVALID, "VALUE_OFFSET key on non-integer column %u", key.col_id);
-        if (key.kind == PG_KEY_VALUE_OFFSET && c->card &&
-            (c->imin < key.base || (uint64_t)(c->imax - key.base) >= key.cardinality))
-          return fail(PG_E_INVALID, "column %u values outside the key range of key %u", key.col_id, k);
         key_coldesc(kc[(uint64_t)si * K + k], c, key);
-        prod = prod > nd[si] / std::max(1u, c->card) ? (uint64_t)nd[si] + 1 : prod * std::max(1u, c->card);
+        const uint32_t kcard = c->fwd == FWD_RAW ? std::max(1u, nd[si]) : std::max(1u, c->card);
+        prod = prod > nd[si] / kcard ? (uint64_t)nd[si] + 1 : prod * kcard;
       }
       expect += std::min<uint64_t>(prod, nd[si]);
       ColumnRes& w = wcols[si];
@@ -3706,16 +3724,19 @@ struct PartialsImpl {
   Partials P;
 };
 
+// wide-key exchange rows carry their tuple after the state row: K uint32 table-global key ids, padded to 8 bytes
+uint64_t wide_tuple_bytes(uint32_t K) { return (4ull * K + 7) & ~7ull; }
+
 void fill_handle(pg_partials* p, PartialsImpl* impl) {
   Partials& P = impl->P;
   p->num_slots = P.num_slots;
-  p->mode = P.mode == GM_HASH ? PG_STATE_HASH : PG_STATE_DENSE;
+  p->mode = P.wide ? PG_STATE_TUPLES : P.mode == GM_HASH ? PG_STATE_HASH : PG_STATE_DENSE;
   p->n_i64 = P.n_i64; p->n_fx = P.n_fx; p->n_min = P.n_min; p->n_max = P.n_max;
   p->bitmap_words = P.bit_words;
   p->layout = P.layout;
   p->fx_sig = P.fx_sig();
   p->flags = P.flags;
-  p->row_bytes = row_bytes(P.view());
+  p->row_bytes = row_bytes(P.view()) + (P.wide ? wide_tuple_bytes(P.wide->K) : 0);
   p->keys = (uint64_t*)P.keys.p;
   p->i64 = (int64_t*)P.i64.p;
   p->fx = (int64_t*)P.fx.p;
@@ -4621,6 +4642,49 @@ int pg_partials_copy(pg_partials* p, int dir, void* i64, void* fx, void* mn, voi
   return PG_OK;
 }
 
+// Wide keys (the state's packed keys are slots of its own tuple table): rows { state row | tuple }, the owner part from
+// the tuple (table-global key ids), so the same group goes to the same owner from every GPU.
+int export_wide(Partials& P, uint32_t num_parts, void* dst, uint64_t dst_rows, uint64_t* part_counts, hipStream_t s) {
+  const WideKeys& W = *P.wide;
+  Scratch sc(s);
+  int rc = PG_OK;
+  const StateView v = P.view();
+  const size_t tb = select_temp_bytes(P.num_slots);
+  uint32_t* slots = sc.get<uint32_t>(P.num_slots, rc);
+  uint32_t* d_num = sc.get<uint32_t>(2, rc);
+  void* temp = sc.get<uint8_t>(tb, rc);
+  if (rc) return rc;
+  HIP_CHECK(launch_select_slots(v, SEL_PRESENT, 0, 1, slots, d_num, temp, tb, s));
+  uint32_t n = 0;
+  if ((rc = read_back(d_num, n, s))) return rc;
+  const uint64_t rb = row_bytes(v), rbw = rb + wide_tuple_bytes(W.K);
+  uint32_t* owner = sc.get<uint32_t>((uint64_t)n + 1, rc);
+  uint8_t* rows = sc.get<uint8_t>(rb * n + 8, rc);
+  if (rc) return rc;
+  // the rows (key word = tuple slot: a hash state's key, a dense state's slot), their owners from the tuples
+  HIP_CHECK(launch_gather_rows(v, slots, n, 1, rows, s));
+  HIP_CHECK(launch_wide_owner((const uint32_t*)W.tuples.p, W.K, rows, rb, n, num_parts, owner, s));
+  std::vector<uint32_t> own(n), sl(n);
+  if (n) {
+    HIP_CHECK(hipMemcpyAsync(own.data(), owner, 4ull * n, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(sl.data(), slots, 4ull * n, hipMemcpyDeviceToHost, s));
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
+  std::vector<uint64_t> at(num_parts + 1, 0);
+  for (uint32_t i = 0; i < n; i++) at[own[i] + 1]++;
+  for (uint32_t q = 0; q < num_parts; q++) part_counts[q] = at[q + 1];
+  if (!dst) return PG_OK;
+  if (n > dst_rows) return fail(PG_E_INVALID, "export buffer of %llu rows too small", (unsigned long long)dst_rows);
+  for (uint32_t q = 0; q < num_parts; q++) at[q + 1] += at[q];
+  std::vector<uint32_t> order(n);  // state slots bucketed by owner part, stable
+  for (uint32_t i = 0; i < n; i++) order[at[own[i]]++] = sl[i];
+  if (n) HIP_CHECK(hipMemcpyAsync(slots, order.data(), 4ull * n, hipMemcpyHostToDevice, s));
+  HIP_CHECK(launch_gather_rows(v, slots, n, 1, rows, s));
+  HIP_CHECK(launch_widen_rows(rows, rb, (const uint32_t*)W.tuples.p, W.K, n, (uint8_t*)dst, rbw, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  return PG_OK;
+}
+
 int pg_partials_export(pg_partials* p, uint32_t num_parts, void* dst, uint64_t dst_rows, uint64_t* part_counts,
                        void* stream) {
   int rc = ensure_device();
@@ -4628,8 +4692,8 @@ int pg_partials_export(pg_partials* p, uint32_t num_parts, void* dst, uint64_t d
   if (!p || !p->impl || !num_parts || !part_counts) return fail(PG_E_INVALID, "bad export arguments");
   try {
     Partials& P = ((PartialsImpl*)p->impl)->P;
-    if (P.wide) return fail(PG_E_UNSUPPORTED, "wide group keys are tuple slots local to one state: no cross-state merge");
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream();
+    if (P.wide) return export_wide(P, num_parts, dst, dst_rows, part_counts, s);
     Scratch sc(s);
     const StateView v = P.view();
     const size_t tb = select_temp_bytes(P.num_slots);
@@ -4661,13 +4725,29 @@ int pg_partials_create(const pg_partials* like, uint64_t capacity, pg_partials**
   if (rc) return rc;
   if (!like || !like->impl || !out) return fail(PG_E_INVALID, "null argument");
   *out = nullptr;
-  if (((PartialsImpl*)like->impl)->P.wide)
-    return fail(PG_E_UNSUPPORTED, "wide group keys are tuple slots local to one state: no cross-state merge");
   PartialsImpl* impl = new (std::nothrow) PartialsImpl();
   if (!impl) return fail(PG_E_NOMEM, "out of host memory");
   try {
     hipStream_t s = thread_stream();
-    rc = hash_like(((PartialsImpl*)like->impl)->P, capacity, impl->P, s);
+    const Partials& L = ((PartialsImpl*)like->impl)->P;
+    rc = hash_like(L, capacity, impl->P, s);
+    if (!rc && L.wide) {  // a wide-key merge target: a fresh tuple table; its slots are the hash state's one key
+      auto W = std::make_shared<WideKeys>();
+      W->K = L.wide->K;
+      W->cap = pow2_at_least(std::max<uint64_t>(1024, 2 * capacity));
+      if (W->cap > (1ull << 31) || W->cap * (8ull + 4ull * W->K) > kStateBudget) {
+        rc = fail(PG_E_UNSUPPORTED, "tuple table of %llu slots exceeds the state budget", (unsigned long long)W->cap);
+      } else if (!(rc = W->tags.alloc(W->cap * 8)) && !(rc = W->tuples.alloc(W->cap * 4ull * W->K)) &&
+                 !(rc = W->misc.alloc(16))) {
+        HIP_CHECK(hipMemsetAsync(W->tags.p, 0, W->cap * 8, s));
+        HIP_CHECK(hipMemsetAsync(W->misc.p, 0, 16, s));
+        W->key1 = L.wide->key1;
+        W->key1.cardinality = (uint32_t)W->cap;
+        impl->P.key_card.assign(1, (uint32_t)W->cap);
+        impl->P.key_stride.assign(1, 1);
+        impl->P.wide = W;
+      }
+    }
     if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = fail(PG_E_HIP, "state initialisation failed");
   } catch (const std::exception& e) {
     rc = fail(PG_E_NOMEM, "create failed: %s", e.what());
@@ -4687,7 +4767,31 @@ int pg_partials_merge(pg_partials* p, const void* rows, uint64_t n, void* stream
   Partials& P = ((PartialsImpl*)p->impl)->P;
   if (P.mode != GM_HASH) return fail(PG_E_INVALID, "pg_partials_merge needs a hash state (pg_partials_create)");
   hipStream_t s = stream ? (hipStream_t)stream : thread_stream();
-  HIP_CHECK(launch_merge_rows(P.view(), (const uint8_t*)rows, n, s));
+  const void* merged = rows;
+  Scratch sc(s);
+  if (P.wide) {  // wide keys: re-intern each row's tuple here, then merge the rows keyed by this table's slots
+    WideKeys& W = *P.wide;
+    if (!W.tags.p) return fail(PG_E_INVALID, "pg_partials_merge needs a merge target (pg_partials_create)");
+    const uint64_t rb = row_bytes(P.view());
+    uint8_t* keyed = sc.get<uint8_t>(rb * n + 8, rc);
+    if (rc) return rc;
+    WideSpec ws;
+    memset(&ws, 0, sizeof(ws));
+    ws.K = W.K;
+    ws.max_fill = (uint32_t)(W.cap / 4 * 3);
+    ws.mask = W.cap - 1;
+    ws.tags = (unsigned long long*)W.tags.p;
+    ws.tuples = (uint32_t*)W.tuples.p;
+    ws.fill = (unsigned int*)W.misc.p;
+    ws.err = (unsigned int*)W.misc.p + 1;
+    HIP_CHECK(launch_intern_rows(ws, (const uint8_t*)rows, n, rb, rb + wide_tuple_bytes(W.K), keyed, s));
+    uint32_t we[2] = {0, 0};
+    HIP_CHECK(hipMemcpyAsync(we, W.misc.p, 8, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (we[1]) return fail(PG_E_NOMEM, "merge tuple table of %llu slots is full", (unsigned long long)W.cap);
+    merged = keyed;
+  }
+  HIP_CHECK(launch_merge_rows(P.view(), (const uint8_t*)merged, n, s));
   uint32_t fe[2] = {0, 0};
   HIP_CHECK(hipMemcpyAsync(fe, P.misc.p, 8, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));

@@ -331,8 +331,10 @@ class KeySpace:
             lo = min((int(v.min()) for v in vals), default=0)
             hi = max((int(v.max()) for v in vals), default=0)
             span = hi - lo + 1
-            if span > MAX_VALUE_OFFSET_KEYS:
-                raise UnsupportedQuery(f"{column}: raw value range {span} too wide for value-offset ids")
+            # value offsets are 32-bit key ids (pg_key.cardinality): a group key may span up to 2^32 - 1 values (the
+            # device state then hashes them); a DISTINCTCOUNT value set also needs a dense bitmap (checked at its use)
+            if span >= 1 << 32:
+                raise UnsupportedQuery(f"{column}: raw value range {span} too wide for 32-bit value-offset ids")
             return KeySpace(column, abi.PG_KEY_VALUE_OFFSET, span, lo)
         if dt in ("INT", "LONG"):
             lo = min(int(c.dictionary.values[0]) for c in cols)
@@ -779,6 +781,9 @@ class CPlan:
                         raise UnsupportedQuery(f"{ag.function} on non-numeric column {c}")
                 if ag.function == "DISTINCTCOUNT":
                     ks = table.key_space(e.cols[0])
+                    if ks.kind == abi.PG_KEY_VALUE_OFFSET and ks.cardinality > MAX_VALUE_OFFSET_KEYS:
+                        raise UnsupportedQuery(f"DISTINCTCOUNT({e.cols[0]}): raw value range {ks.cardinality} too wide "
+                                               "for a value bitmap")
                     aggs[i].key_kind = ks.kind
                     aggs[i].key_cardinality = ks.cardinality
                     aggs[i].key_base = ks.base
@@ -789,8 +794,12 @@ class CPlan:
         keys = (abi.pg_key * max(len(query.group_by), 1))()
         self.key_spaces = []
         for k, col in enumerate(query.group_by):
-            if any(s.columns[col].dictionary is None for s in segments if col in s.columns):
-                raise UnsupportedQuery(f"GROUP BY raw (no-dictionary) column {col}")
+            # a raw (no-dictionary) INT / LONG key groups by value offset (NoDictionarySingleColumnGroupKeyGenerator /
+            # NoDictionaryMultiColumnGroupKeyGenerator, DefaultGroupByExecutor.java:85-94); other raw types are not
+            # handled on the device
+            if any(s.columns[col].dictionary is None for s in segments if col in s.columns) and \
+                    table.data_type(col) not in ("INT", "LONG"):
+                raise UnsupportedQuery(f"GROUP BY raw (no-dictionary) {table.data_type(col)} column {col}")
             ks = table.key_space(col)
             self.key_spaces.append(ks)
             keys[k].col_id = cid[col]

@@ -208,3 +208,107 @@ def test_two_ranks_double_sums_are_bit_identical():
     for rank, ok, info in res:
         assert ok, info
     assert all(n > 0 for n in res[0][2])   # every case has exact fixed-point sums (SK_FX)
+
+
+WIDE_KEYS = "column1, column3, column5, column6, column7, column9, column11, column12, column17"
+WIDE_CASES = [
+    # 9 keys (more than a packed key takes): tuple states, merged by the row exchange with their tuples re-interned
+    f"SELECT COUNT(*), SUM(column18), MIN(column6), MAX(column3), AVG(column7) FROM t GROUP BY {WIDE_KEYS}",
+    f"SELECT COUNT(*), SUM(column1) FROM t WHERE column3 > 1000000000 AND column11 <> 'P' GROUP BY {WIDE_KEYS}, "
+    "column18, daysSinceEpoch",
+    f"SELECT column1, column3, column6, COUNT(*), DISTINCTCOUNT(column11) FROM t GROUP BY {WIDE_KEYS} "
+    "ORDER BY COUNT(*) DESC, column1, column3, column6 LIMIT 7",
+]
+RAW_CASES = [
+    # raw (no-dictionary) group keys (NoDictionarySingleColumnGroupKeyGenerator / ...MultiColumn...)
+    "SELECT ts, COUNT(*), SUM(m_long) FROM t WHERE m_int > 3000 GROUP BY ts",
+    "SELECT u, k, COUNT(*), MAX(m_double) FROM t GROUP BY u, k",
+]
+
+
+def _wide_segments():
+    """4 segments of the reference's SV test data (BaseSingleValueQueriesTest), segment i without every fourth row
+    starting at i: most tuples sit on both ranks, some on one only."""
+    import numpy as np
+    from conftest import GOLDEN, SV_SCHEMA
+    from pinot_amd.segment import ImmutableSegment
+    z = np.load(os.path.join(GOLDEN, "test_data_sv.npz"))
+    full = {k: (z[k] if z[k].dtype.kind != "U" else z[k].astype(object)) for k in SV_SCHEMA}
+    n = len(full["column1"])
+    segs = []
+    for si in range(4):
+        keep = (np.arange(n) % 4) != si
+        segs.append(ImmutableSegment.create(f"sv{si}", {k: v[keep] for k, v in full.items()},
+                                            {k: v[0] for k, v in SV_SCHEMA.items()},
+                                            inverted=("column6", "column7", "column11", "column17", "column18"),
+                                            field_types={k: v[1] for k, v in SV_SCHEMA.items()}))
+    return segs
+
+
+def _worker_wide(rank, world, port, q):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from helpers import assert_same_result
+        from oracle.oracle import OracleEngine
+        from pinot_amd import abi
+        from pinot_amd.combine import merge_partials_across_ranks
+        from pinot_amd.gpu import GpuEngine
+        from pinot_amd.plan import InstanceConfig, Table, reduce_to_rows
+        from pinot_amd.query import parse
+        from test_raw_index import _raw_segments
+        eng = GpuEngine(0)
+        modes = []
+        for segs, cases in ((_wide_segments(), WIDE_CASES), (_raw_segments(4, 30_000, seed=5), RAW_CASES)):
+            table = Table("t", segs)
+            mine = segs[rank::world]
+            for sql in cases:
+                qc = parse(sql)
+                for flags in (abi.PG_PLAN_VALUE_SETS, abi.PG_PLAN_VALUE_SETS | abi.PG_PLAN_HASH_GROUPS):
+                    plan = eng.make_plan(table, qc, segments=mine, flags=flags)
+                    p = eng.run_partial(plan)
+                    modes.append(int(p.contents.mode))
+                    merged = merge_partials_across_ranks(eng, plan, p)
+                    whole = OracleEngine().execute(table, qc)
+                    if qc.order_by:
+                        assert reduce_to_rows(qc, merged)[1] == reduce_to_rows(qc, whole)[1], sql
+                    else:
+                        assert_same_result(merged, whole, table=table)
+        # numGroupsLimit with tuple keys: each segment keeps its first tuples; the flag is the OR over the ranks
+        table = Table("t", _wide_segments())
+        qc = parse(f"SELECT COUNT(*), SUM(column1) FROM t GROUP BY {WIDE_KEYS}")
+        cfg = InstanceConfig.with_groups_limit(500)
+        plan = eng.make_plan(table, qc, segments=table.segments[rank::world], config=cfg)
+        merged = merge_partials_across_ranks(eng, plan, eng.run_partial(plan))
+        whole = OracleEngine().execute(table, qc, config=cfg)
+        assert_same_result(merged, whole, table=table)
+        assert merged.groups_limit_reached == whole.groups_limit_reached
+        q.put((rank, True, modes))
+        dist.destroy_process_group()
+    except Exception:
+        q.put((rank, False, traceback.format_exc()))
+
+
+def test_two_ranks_merge_wide_and_raw_keys():
+    """A 9-key group-by (and raw-key group-bys) over 2 ranks: tuple states exported with their key tuples, re-interned
+    on the owner (PG_STATE_TUPLES rows), equal to the oracle over all segments."""
+    import torch.multiprocessing as mp
+    from pinot_amd import abi
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_wide, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, info in res:
+        assert ok, info
+    assert abi.PG_STATE_TUPLES in res[0][2]

@@ -148,11 +148,13 @@ def _raw_segments(n_segs=3, rows=50_000, seed=7, codecs=None):
         n = rows + 1013 * s
         data = {"k": rng.integers(0, 40, n), "m_int": rng.integers(-5000, 5000, n),
                 "m_long": rng.integers(-2 ** 40, 2 ** 40, n), "m_float": rng.normal(size=n).astype(np.float32),
-                "m_double": rng.normal(size=n) * 1e3, "u": rng.integers(0, 300, n)}
+                "m_double": rng.normal(size=n) * 1e3, "u": rng.integers(0, 300, n),
+                # a raw LONG key of a timestamp-like range (~1e9 values: hashed device state)
+                "ts": 1_600_000_000_000 + rng.integers(0, 10 ** 9, n) // 997 * 997}
         segs.append(ImmutableSegment.create(
             f"r{s}", data, {"k": "INT", "m_int": "INT", "m_long": "LONG", "m_float": "FLOAT", "m_double": "DOUBLE",
-                            "u": "INT"},
-            no_dictionary=("m_int", "m_long", "m_float", "m_double", "u"), raw_version=2 + s % 3,
+                            "u": "INT", "ts": "LONG"},
+            no_dictionary=("m_int", "m_long", "m_float", "m_double", "u", "ts"), raw_version=2 + s % 3,
             raw_compression=codecs))
     return segs
 
@@ -170,6 +172,13 @@ RAW_QUERIES = [
     "SELECT DISTINCTCOUNT(u), COUNT(*) FROM t WHERE m_int < 0",
     "SELECT k, DISTINCTCOUNT(u) FROM t GROUP BY k",
     "SELECT MIN(m_int), MAX(m_long), COUNT(*) FROM t",                     # non-scan: column metadata min / max
+    # raw (no-dictionary) group keys: NoDictionarySingleColumnGroupKeyGenerator / NoDictionaryMultiColumnGroupKeyGenerator
+    "SELECT u, COUNT(*), SUM(m_int), MAX(m_double) FROM t GROUP BY u",
+    "SELECT m_int, COUNT(*), MIN(m_long) FROM t WHERE k < 10 GROUP BY m_int",
+    "SELECT k, u, COUNT(*), AVG(m_float) FROM t WHERE m_double > 0 GROUP BY k, u",
+    "SELECT ts, COUNT(*), SUM(m_long) FROM t WHERE m_int > 3000 GROUP BY ts",
+    "SELECT u, m_int, COUNT(*) FROM t WHERE m_int BETWEEN -50 AND 50 GROUP BY u, m_int",
+    "SELECT u, DISTINCTCOUNT(k), COUNT(*) FROM t GROUP BY u",
 ]
 
 
@@ -200,19 +209,24 @@ def test_raw_queries_oracle_vs_numpy(sql, oracle_engine, raw_table):
             else:
                 assert np.isclose(v, x, rtol=1e-9, atol=0) or v == x, (ag, v, x)
     else:
-        keys = vals[q.group_by[0]][mask]
-        for key in np.unique(keys):
-            m2 = mask.copy()
-            m2[mask] = keys == key
-            for ag, v in zip(q.aggregations, res.rows[(int(key),)]):
+        kv = np.stack([vals[c][mask] for c in q.group_by], axis=1)
+        uniq, inv = np.unique(kv, axis=0, return_inverse=True)
+        inv = inv.reshape(-1)
+        order = np.argsort(inv, kind="stable")
+        bounds = np.searchsorted(inv[order], np.arange(len(uniq) + 1))
+        sel = np.flatnonzero(mask)
+        for gi in range(len(uniq)):
+            m2 = np.zeros_like(mask)
+            m2[sel[order[bounds[gi]:bounds[gi + 1]]]] = True
+            for ag, v in zip(q.aggregations, res.rows[tuple(int(x) for x in uniq[gi])]):
                 x = _np_agg(ag, vals, m2)
                 if ag.function == "AVG":
                     assert v[1] == x[1] and np.isclose(v[0], x[0], rtol=1e-9)
                 elif ag.function == "DISTINCTCOUNT":
                     assert v == x
                 else:
-                    assert np.isclose(v, x, rtol=1e-9) or v == x, (ag, key, v, x)
-        assert len(res.rows) == len(np.unique(keys))
+                    assert np.isclose(v, x, rtol=1e-9) or v == x, (ag, uniq[gi], v, x)
+        assert len(res.rows) == len(uniq)
 
 
 def _np_filter(f, vals):
@@ -284,9 +298,58 @@ def test_raw_store_round_trip(tmp_path):
         assert os.path.exists(tmp_path / "v1" / "m_int.sv.raw.fwd") if sub == "v1" else True
 
 
-def test_group_by_raw_column_is_unsupported(oracle_engine, raw_table):
+def _first_seen_groups(table, cols, where, limit):
+    """NoDictionarySingleColumnGroupKeyGenerator.getKeyForValue (:416-424) / NoDictionaryMultiColumnGroupKeyGenerator
+    .getGroupIdForKey (:318-328) restated in Python: per segment, the value tuples of the matching docs get group ids in
+    first-seen doc order until numGroupsLimit exist; later new tuples are dropped (INVALID_ID).  -> {tuple: doc count}
+    merged over the segments by value."""
+    out = {}
+    for s in table.segments:
+        v = [s.columns[c].raw_values if s.columns[c].dictionary is None
+             else np.asarray(s.columns[c].dictionary.values)[s.columns[c].dict_ids] for c in cols]
+        m = where(s)
+        seen = {}
+        for row in zip(*(x[m].tolist() for x in v)):
+            if row in seen:
+                seen[row] += 1
+            elif len(seen) < limit:
+                seen[row] = 1
+        for key, c in seen.items():
+            out[key] = out.get(key, 0) + c
+    return out
+
+
+@pytest.mark.parametrize("cols,limit", [(("m_int",), 700), (("u", "k"), 1500), (("ts",), 2000)])
+def test_raw_group_by_limit_is_first_seen(cols, limit, oracle_engine, raw_table):
+    """A raw key's groups under an instance numGroupsLimit: the first `limit` distinct keys in doc order per segment
+    (the reference's no-dictionary generators have no array-based holder, so a small key range truncates too), then
+    merged by value; numGroupsLimitReached when a segment reached the limit."""
+    from pinot_amd.plan import InstanceConfig
+    cfg = InstanceConfig(num_groups_limit=limit, max_init_group_holder_capacity=min(limit, 10_000))
+    q = parse(f"SELECT {', '.join(cols)}, COUNT(*) FROM t WHERE m_double > -500 GROUP BY {', '.join(cols)}")
+    res = oracle_engine.execute(raw_table, q, config=cfg)
+    want = _first_seen_groups(raw_table, cols, lambda s: s.columns["m_double"].raw_values > -500, limit)
+    assert {k: v[0] for k, v in res.rows.items()} == want
+    assert res.groups_limit_reached
+
+
+def test_group_by_raw_float_column_is_unsupported(oracle_engine, raw_table):
+    """Raw FLOAT / DOUBLE keys (the generators' Float2Int / Double2Int maps) are not handled on the device."""
     with pytest.raises(UnsupportedQuery):
-        oracle_engine.execute(raw_table, parse("SELECT m_int, COUNT(*) FROM t GROUP BY m_int"))
+        oracle_engine.execute(raw_table, parse("SELECT m_float, COUNT(*) FROM t GROUP BY m_float"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cols,limit", [(("m_int",), 700), (("u", "k"), 1500), (("ts",), 2000)])
+def test_raw_group_by_limit_gpu(cols, limit, gpu_engine, oracle_engine, raw_table):
+    """The device's per-segment truncation of raw keys equals the oracle's first-seen groups (and the limit flag)."""
+    from helpers import assert_same_result
+    from pinot_amd.plan import InstanceConfig
+    cfg = InstanceConfig(num_groups_limit=limit, max_init_group_holder_capacity=min(limit, 10_000))
+    q = parse(f"SELECT {', '.join(cols)}, COUNT(*), SUM(m_int) FROM t WHERE m_double > -500 GROUP BY {', '.join(cols)}")
+    g, o = gpu_engine.execute(raw_table, q, config=cfg), oracle_engine.execute(raw_table, q, config=cfg)
+    assert_same_result(g, o, table=raw_table)
+    assert g.groups_limit_reached == o.groups_limit_reached
 
 
 def _fixture_segment(name, n):
