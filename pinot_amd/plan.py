@@ -477,12 +477,77 @@ def reduce_to_rows(query: QueryContext, res: IntermediateResult) -> Tuple[List[s
 
     if query.order_by:
         keyed.sort(key=sort_key)
+    if query.having is not None:
+        # GroupByDataTableReducer.reduceToResultTable (:148-165): the broker's table keeps getTableCapacity(limit)
+        # records (resultSize = trimSize under HAVING, :232-237); its sorted records are taken in order while fewer
+        # than LIMIT rows passed HAVING (HavingFilterHandler.isMatch over the final values)
+        keyed = [kf for kf in keyed[:table_capacity(query.limit, 5000)]  # getTableCapacity(limit), GroupByUtils:31
+                 if having_match(query.having, query, agg_index, kf[0], kf[1])]
     for key, finals in keyed[:query.limit]:
         row = []
         for s in query.select:
             row.append(key[query.group_by.index(s.column)] if s.kind == "COL" else finals[agg_index[s.agg]])
         rows_out.append(row)
     return names, rows_out
+
+
+def having_value(e, query: QueryContext, agg_index: dict, key: tuple, finals: list):
+    """A HAVING operand's value (PostAggregationHandler.getValueExtractor): an aggregation's final result, a group
+    key, a literal; + - * / of them in double arithmetic (the arithmetic transform functions)."""
+    if e.kind == "AGG":
+        return finals[agg_index[e.agg]]
+    if e.kind == "COL":
+        return key[query.group_by.index(e.column)]
+    if e.kind == "LIT":
+        if e.op == "STR":
+            return e.value
+        return float(e.value) if any(c in e.value for c in ".eE") else int(e.value)
+    a, b = (float(having_value(x, query, agg_index, key, finals)) for x in e.args)
+    if e.op == "+":
+        return a + b
+    if e.op == "-":
+        return a - b
+    if e.op == "*":
+        return a * b
+    return a / b if b != 0 else (math.copysign(math.inf, a) if a != 0 else math.nan)
+
+
+def _having_cmp(v, lit: str):
+    """(value, literal) in one comparable type: strings compare as strings; an integer value against an integral
+    literal exactly; otherwise as doubles (the predicate evaluator of the value column's data type)."""
+    if isinstance(v, str):
+        return v, lit
+    if isinstance(v, int) and not any(c in lit for c in ".eE"):
+        return v, int(lit)
+    return float(v), float(lit)
+
+
+def having_match(h, query: QueryContext, agg_index: dict, key: tuple, finals: list) -> bool:
+    """HavingFilterHandler.isMatch (query/reduce/HavingFilterHandler.java): AND / OR / NOT of the predicates on the
+    row's post-aggregation values (no null handling: IS NULL never matches)."""
+    if h.type == "AND":
+        return all(having_match(c, query, agg_index, key, finals) for c in h.children)
+    if h.type == "OR":
+        return any(having_match(c, query, agg_index, key, finals) for c in h.children)
+    if h.type == "NOT":
+        return not having_match(h.children[0], query, agg_index, key, finals)
+    p = h.predicate
+    v = having_value(h.lhs, query, agg_index, key, finals)
+    if p.type in ("IS_NULL", "IS_NOT_NULL"):
+        return p.type == "IS_NOT_NULL"
+    if isinstance(v, float) and math.isnan(v):
+        return p.type in ("NOT_EQ", "NOT_IN")
+    if p.type in ("EQ", "IN", "NOT_EQ", "NOT_IN"):
+        hit = any(a == b for a, b in (_having_cmp(v, x) for x in p.values))
+        return hit if p.type in ("EQ", "IN") else not hit
+    ok = True
+    if p.lower != UNBOUNDED:
+        a, b = _having_cmp(v, p.lower)
+        ok &= a >= b if p.lower_inclusive else a > b
+    if p.upper != UNBOUNDED:
+        a, b = _having_cmp(v, p.upper)
+        ok &= a <= b if p.upper_inclusive else a < b
+    return ok
 
 
 # ------------------------------------------------------------------------------------------ group trim
@@ -556,7 +621,8 @@ def group_trim(query: QueryContext, config: Optional[InstanceConfig] = None) -> 
     ordered = bool(query.order_by)
     seg = table_capacity(query.limit, seg_min) if ordered and seg_min > 0 else None
     if srv_min > 0:
-        srv = table_capacity(query.limit, srv_min) if ordered else query.limit
+        # ORDER BY or HAVING -> getTableCapacity(limit, minServerGroupTrimSize) (:82-84); neither -> LIMIT
+        srv = table_capacity(query.limit, srv_min) if ordered or query.having is not None else query.limit
         threshold = cfg.groupby_trim_threshold
     else:
         srv, threshold = None, (1 << 31) - 1

@@ -96,6 +96,44 @@ class OrderBy:
     asc: bool = True
 
 
+@dataclass(frozen=True)
+class HavingExpr:
+    """A HAVING operand (PostAggregationHandler's value extractors, query/reduce/PostAggregationHandler.java): an
+    aggregation's final result, a group-by key, a numeric literal, or + - * / of those."""
+    kind: str                              # AGG, COL, LIT, ARITH
+    agg: Optional[Aggregation] = None
+    column: Optional[str] = None
+    value: Optional[str] = None
+    op: Optional[str] = None               # ARITH: + - * /
+    args: Tuple["HavingExpr", ...] = ()
+
+    def aggregations(self) -> List[Aggregation]:
+        if self.kind == "AGG":
+            return [self.agg]
+        out = []
+        for a in self.args:
+            out.extend(a.aggregations())
+        return out
+
+
+@dataclass
+class HavingFilter:
+    """The HAVING clause (QueryContext._havingFilter): AND / OR / NOT of predicates whose left-hand side is a
+    HavingExpr; `lhs <op> rhs` with a non-literal rhs is `lhs - rhs <op> 0`, as CalciteSqlParser rewrites it."""
+    type: str                                       # AND, OR, NOT, PREDICATE
+    children: List["HavingFilter"] = field(default_factory=list)
+    lhs: Optional[HavingExpr] = None
+    predicate: Optional[Predicate] = None           # its column is unused ("")
+
+    def aggregations(self) -> List[Aggregation]:
+        if self.type == "PREDICATE":
+            return self.lhs.aggregations()
+        out = []
+        for c in self.children:
+            out.extend(c.aggregations())
+        return out
+
+
 @dataclass
 class QueryContext:
     table: str
@@ -105,14 +143,19 @@ class QueryContext:
     order_by: List[OrderBy]
     limit: int
     options: dict = field(default_factory=dict)
+    having: Optional[HavingFilter] = None
 
     @property
     def aggregations(self) -> List[Aggregation]:
-        """Distinct aggregations in first-seen order (QueryContext._aggregationFunctions)."""
+        """Distinct aggregations in first-seen order: the select list, the HAVING filter, the ORDER BY
+        (QueryContext.generateAggregationFunctions, QueryContext.java:514-560)."""
         out = []
         for s in self.select:
             if s.kind == "AGG" and s.agg not in out:
                 out.append(s.agg)
+        for a in (self.having.aggregations() if self.having is not None else []):
+            if a not in out:
+                out.append(a)
         for o in self.order_by:
             if o.kind == "AGG" and o.agg not in out:
                 out.append(o.agg)
@@ -122,9 +165,9 @@ class QueryContext:
 # ------------------------------------------------------------------------------------------ parser
 
 _TOKEN = re.compile(r"\s*(?:(?P<num>-?\d+(?:\.\d+)?(?:[eE][-+]?\d+)?)|(?P<str>'(?:[^']|'')*')|"
-                    r"(?P<id>[A-Za-z_][A-Za-z0-9_.$]*)|(?P<op><>|!=|<=|>=|[=<>*+\-(),]))")
+                    r"(?P<id>[A-Za-z_][A-Za-z0-9_.$]*)|(?P<op><>|!=|<=|>=|[=<>*+\-/(),]))")
 _KEYWORDS = {"SELECT", "FROM", "WHERE", "GROUP", "BY", "ORDER", "LIMIT", "AND", "OR", "NOT", "IN", "BETWEEN",
-             "ASC", "DESC", "AS", "OPTION", "IS", "NULL"}
+             "ASC", "DESC", "AS", "OPTION", "IS", "NULL", "HAVING"}
 _AGGS = {"COUNT", "SUM", "MIN", "MAX", "AVG", "DISTINCTCOUNT", "COUNTMV"}
 
 
@@ -267,6 +310,103 @@ class _Parser:
             raise ValueError(f"unsupported operator {op}")
         return FilterContext("PREDICATE", predicate=p)
 
+    # ---- HAVING: predicates over post-aggregation values
+    def h_atom(self) -> HavingExpr:
+        if self.accept("op", "("):
+            e = self.h_sum()
+            self.expect("op", ")")
+            return e
+        k, v = self.peek()
+        if k in ("num", "str"):
+            self.next()
+            return HavingExpr("LIT", value=v, op="STR" if k == "str" else None)
+        kind, x = self.agg_or_col()
+        return HavingExpr("AGG", agg=x) if kind == "AGG" else HavingExpr("COL", column=x)
+
+    def h_product(self) -> HavingExpr:
+        e = self.h_atom()
+        while self.peek() in (("op", "*"), ("op", "/")):
+            op = self.next()[1]
+            e = HavingExpr("ARITH", op=op, args=(e, self.h_atom()))
+        return e
+
+    def h_sum(self) -> HavingExpr:
+        e = self.h_product()
+        while True:
+            k, v = self.peek()
+            if (k, v) in (("op", "+"), ("op", "-")):
+                self.next()
+                e = HavingExpr("ARITH", op=v, args=(e, self.h_product()))
+            elif k == "num" and v.startswith("-"):  # `x -1` tokenised as x, -1: a subtraction
+                self.next()
+                e = HavingExpr("ARITH", op="-", args=(e, HavingExpr("LIT", value=v[1:])))
+            else:
+                return e
+
+    def h_predicate(self) -> HavingFilter:
+        k, v = self.peek()
+        if (k, v) == ("op", "("):  # a parenthesised filter or an arithmetic operand: try the filter first
+            save = self.i
+            self.next()
+            try:
+                f = self.h_or()
+                self.expect("op", ")")
+                return f
+            except ValueError:
+                self.i = save
+        if self.accept("kw", "NOT"):
+            return HavingFilter("NOT", [self.h_predicate()])
+        lhs = self.h_sum()
+        leaf = lambda p: HavingFilter("PREDICATE", lhs=lhs, predicate=p)
+        if self.accept("kw", "IS"):
+            neg = self.accept("kw", "NOT")
+            self.expect("kw", "NULL")
+            return leaf(Predicate("IS_NOT_NULL" if neg else "IS_NULL", ""))
+        neg = self.accept("kw", "NOT")
+        if self.accept("kw", "BETWEEN"):
+            lo = self.literal()
+            self.expect("kw", "AND")
+            hi = self.literal()
+            f = leaf(Predicate("RANGE", "", (), lo, hi, True, True))
+            return HavingFilter("NOT", [f]) if neg else f
+        if self.accept("kw", "IN"):
+            self.expect("op", "(")
+            vals = [self.literal()]
+            while self.accept("op", ","):
+                vals.append(self.literal())
+            self.expect("op", ")")
+            return leaf(Predicate("NOT_IN" if neg else "IN", "", tuple(vals)))
+        if neg:
+            raise ValueError("NOT must be followed by IN or BETWEEN")
+        op = self.expect("op")
+        k, v = self.peek()
+        rhs = self.h_sum()
+        if rhs.kind != "LIT":  # CalciteSqlParser: `a <op> b` with a non-literal b -> `minus(a, b) <op> 0`
+            lhs = HavingExpr("ARITH", op="-", args=(lhs, rhs))
+            v = "0"
+        else:
+            v = rhs.value
+        p = {"=": Predicate("EQ", "", (v,)), "!=": Predicate("NOT_EQ", "", (v,)), "<>": Predicate("NOT_EQ", "", (v,)),
+             ">": Predicate("RANGE", "", (), v, UNBOUNDED, False, False),
+             ">=": Predicate("RANGE", "", (), v, UNBOUNDED, True, False),
+             "<": Predicate("RANGE", "", (), UNBOUNDED, v, False, False),
+             "<=": Predicate("RANGE", "", (), UNBOUNDED, v, False, True)}.get(op)
+        if p is None:
+            raise ValueError(f"unsupported operator {op}")
+        return HavingFilter("PREDICATE", lhs=lhs, predicate=p)
+
+    def h_and(self) -> HavingFilter:
+        parts = [self.h_predicate()]
+        while self.accept("kw", "AND"):
+            parts.append(self.h_predicate())
+        return parts[0] if len(parts) == 1 else HavingFilter("AND", _flatten("AND", parts))
+
+    def h_or(self) -> HavingFilter:
+        parts = [self.h_and()]
+        while self.accept("kw", "OR"):
+            parts.append(self.h_and())
+        return parts[0] if len(parts) == 1 else HavingFilter("OR", _flatten("OR", parts))
+
     def and_expr(self) -> FilterContext:
         parts = [self.predicate()]
         while self.accept("kw", "AND"):
@@ -327,6 +467,11 @@ def parse(sql: str) -> QueryContext:
         group_by.append(p.expect("id"))
         while p.accept("op", ","):
             group_by.append(p.expect("id"))
+    having = None
+    if p.accept("kw", "HAVING"):
+        if not group_by:
+            raise ValueError("HAVING without GROUP BY")
+        having = _resolve_having(p.h_or(), select, group_by)
     order_by = []
     if p.accept("kw", "ORDER"):
         p.expect("kw", "BY")
@@ -365,4 +510,26 @@ def parse(sql: str) -> QueryContext:
     if group_by and any(s.kind == "AGG" and s.agg.filter is not None for s in select):
         # QueryContext.generateAggregationFunctions (QueryContext.java:531-533)
         raise ValueError("GROUP BY with FILTER clauses is not supported")
-    return QueryContext(table, select, filt, group_by, order_by, limit, options)
+    return QueryContext(table, select, filt, group_by, order_by, limit, options, having)
+
+
+def _resolve_having(f: HavingFilter, select: List[SelectItem], group_by: List[str]) -> HavingFilter:
+    """A HAVING identifier is a select alias (of an aggregation or a key) or a group-by column (the reference's
+    QueryContext resolves aliases the same way before the reduce)."""
+    aliases = {s.alias: s for s in select if s.alias}
+
+    def expr(e: HavingExpr) -> HavingExpr:
+        if e.kind == "COL":
+            s = aliases.get(e.column)
+            if s is not None:
+                return HavingExpr("AGG", agg=s.agg) if s.kind == "AGG" else HavingExpr("COL", column=s.column)
+            if e.column not in group_by:
+                raise ValueError(f"HAVING column {e.column} is neither a group-by column nor a select alias")
+            return e
+        if e.kind == "ARITH":
+            return HavingExpr("ARITH", op=e.op, args=tuple(expr(a) for a in e.args))
+        return e
+
+    if f.type == "PREDICATE":
+        return HavingFilter("PREDICATE", lhs=expr(f.lhs), predicate=f.predicate)
+    return HavingFilter(f.type, [_resolve_having(c, select, group_by) for c in f.children])
