@@ -171,6 +171,13 @@ hipError_t launch_prefilter(const PreSpec& p, uint32_t bits, uint32_t blocks, hi
 // every segment, bit width a template parameter, values loaded straight into registers; the survivors' doc ids are
 // compacted into one region per item, which the scan kernel then consumes in list mode
 constexpr int kMaxStreamExtra = 3;
+struct ExactSet {       // one segment's IN list of the exact-mode stream leaf, resolved in the stream block's LDS
+  const int32_t* ids;    // its dictIds, or null: values mode ...
+  const void* vals;      // ... its literals in the dictionary's stored type, looked up in `dict` (card entries); both
+  const void* dict;      //     null: stage the leaf's global LUT instead
+  uint32_t n, nwords;    // ids / literals; LUT words (ceil(cardinality / 32))
+  uint32_t card, dtype;
+};
 struct StreamSpec {
   uint32_t num_items, leaf, cap, set_lds_ints;
   uint32_t num_extra;                 // further leaves of the root AND tested in the stream, on the survivors only
@@ -183,9 +190,10 @@ struct StreamSpec {
   uint32_t* docs;                 // [num_items][cap]
   uint32_t* counts;               // [num_items] survivors written (<= cap)
   unsigned int* err;              // bit 3: some item had more than `cap` survivors
-  // exact mode (1 024-thread blocks, one per CU): a coarse IN bitmap's exact LUT (exact_nwords[seg] words, <= 128 KiB)
-  // is staged whole in LDS, so no value is a candidate to resolve
-  const uint32_t* exact_nwords;
+  // exact mode (1 024-thread blocks, one per CU): a coarse IN bitmap's exact LUT (exact[seg].nwords words, <= 128 KiB)
+  // is whole in LDS, so no value is a candidate to resolve: built there from the segment's dictIds (exact[seg].ids), or
+  // staged from the global LUT (ids == null)
+  const ExactSet* exact;
   // further leaves over packed columns of at most kStreamStageBits bits: a wave stages its 64 groups' words of the
   // column into its LDS slice (16-byte coalesced loads) and tests its survivors from there instead of per-doc window
   // reads.  stage_words: words per wave slice (0: off), placed after the IN-set words (set_lds_ints, a multiple of 4).

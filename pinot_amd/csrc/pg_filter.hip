@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include "pg_aux.h"
+#include "pg_dict.h"
 
 namespace pg {
 
@@ -318,7 +319,7 @@ __device__ __forceinline__ void stage_slice(const LeafDesc& X, uint32_t wg0, uin
 // This is SVScanDocIdIterator over the first AND child, the compacted output playing the role of its docId batches.
 // EXTRA: further AND leaves tested on the survivors (their code costs registers: 71 VGPRs at 7 waves per SIMD with,
 // 72 / 7 without).  Items: contiguous ranges per block (block_first), or with `interleave` item b + k * gridDim.x.
-// NT: threads per block.  NT = 1024 is exact mode (p.exact_nwords): one block per CU holding the exact LUT.
+// NT: threads per block.  NT = 1024 is exact mode (p.exact): one block per CU holding the exact LUT.
 constexpr uint32_t kExactLutWords = 32768;  // 128 KiB: the exact LUT of a <= 1 M-entry dictionary
 
 // Words of dynamic LDS the stream's sets / LUT / slices take; the block's append cursor is the word after them (no
@@ -359,10 +360,27 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? (PG_STREAM_PIPE_EXTRA
       nd = sd.num_docs;
       if (EXACT) {
         __syncthreads();  // every thread is done with the previous segment's LUT
-        if (L.kind == LK_SET_LDS) {
+        const ExactSet es = ldcf(p.exact, wi.seg);
+        if (L.kind == LK_SET_LDS && (es.ids || es.vals)) {
+          // the segment's exact LUT built in LDS from its IN list: each thread resolves its dictIds (values mode: the
+          // literal's dictionary lookup, PredicateUtils.getDictIdSet) while the LUT's words are zeroed (16-byte
+          // stores), then one LDS atomic per dictId -- no global LUT, no set_lut_bits launch, no 128 KiB staging read
+          const uint32_t nq = (es.nwords + 3u) / 4u, lim = 32u * es.nwords;
+          auto id_at = [&](uint32_t k) -> int32_t {
+            return es.ids ? es.ids[k] : dict_find_typed(es.dict, es.card, es.dtype, es.vals, k);
+          };
+          const int32_t id0 = tid < es.n ? id_at(tid) : -1;
+          for (uint32_t q0 = tid; q0 < nq; q0 += NT) ((uint4*)lds_sets)[q0] = make_uint4(0u, 0u, 0u, 0u);
+          __syncthreads();
+          if (id0 >= 0 && (uint32_t)id0 < lim) atomicOr(&lds_sets[(uint32_t)id0 >> 5], 1u << (id0 & 31));
+          for (uint32_t k = tid + NT; k < es.n; k += NT) {
+            const int32_t v = id_at(k);
+            if (v >= 0 && (uint32_t)v < lim) atomicOr(&lds_sets[(uint32_t)v >> 5], 1u << (v & 31));
+          }
+        } else if (L.kind == LK_SET_LDS) {
           // the segment's exact LUT (up to 128 KiB) into LDS: 16-byte buffer loads, 8 per thread issued before any is
           // stored (one load latency per segment change instead of one per word; reads past the LUT return 0)
-          const uint32_t nw = ldcf(p.exact_nwords, wi.seg), nq = (nw + 3u) / 4u;
+          const uint32_t nw = es.nwords, nq = (nw + 3u) / 4u;
           const rsrc_t rl = rsrc_of(L.lut, 4u * nw);
           constexpr uint32_t kU = 8;
           for (uint32_t q0 = tid; q0 < nq; q0 += NT * kU) {
@@ -458,8 +476,8 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? (PG_STREAM_PIPE_EXTRA
 
 hipError_t launch_stream(const StreamSpec& p, uint32_t bits, uint32_t blocks, hipStream_t s) {
   if (!p.num_items || !blocks) return hipSuccess;
-  const size_t lds = 4ull * stream_lds_words(p, p.exact_nwords != nullptr) + 16;  // + the cursor word
-  if (p.exact_nwords) {
+  const size_t lds = 4ull * stream_lds_words(p, p.exact != nullptr) + 16;  // + the cursor word
+  if (p.exact) {
     static bool attr = false;  // >64 KiB of dynamic LDS must be opted into per kernel (once per process)
     if (!attr) {
 #define PG_A(b)                                                                                                 \
@@ -477,8 +495,8 @@ hipError_t launch_stream(const StreamSpec& p, uint32_t bits, uint32_t blocks, hi
   switch (bits) {
 #define PG_B(b)                                                                                              \
   case b:                                                                                                    \
-    if (p.exact_nwords && p.num_extra) hipLaunchKernelGGL((stream_kernel<b, true, 1024>), dim3(blocks), dim3(1024), lds, s, p); \
-    else if (p.exact_nwords) hipLaunchKernelGGL((stream_kernel<b, false, 1024>), dim3(blocks), dim3(1024), lds, s, p); \
+    if (p.exact && p.num_extra) hipLaunchKernelGGL((stream_kernel<b, true, 1024>), dim3(blocks), dim3(1024), lds, s, p); \
+    else if (p.exact) hipLaunchKernelGGL((stream_kernel<b, false, 1024>), dim3(blocks), dim3(1024), lds, s, p); \
     else if (p.num_extra) hipLaunchKernelGGL((stream_kernel<b, true, 256>), dim3(blocks), dim3(256), lds, s, p); \
     else hipLaunchKernelGGL((stream_kernel<b, false, 256>), dim3(blocks), dim3(256), lds, s, p);                \
     break;

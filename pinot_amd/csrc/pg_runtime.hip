@@ -1113,7 +1113,9 @@ struct ThreadCtx {  // per calling thread: staging + events, created once
   hipEvent_t ev_a = nullptr, ev_l = nullptr;
   int init() {
     if (ev[0]) return PG_OK;
-    for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+    // timing-only events (phase times via hipEventElapsedTime; nothing waits on them for data): without the
+    // system-scope fence a record costs no L2 write-back / invalidate between the dependent kernels it sits between
+    for (auto& e : ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
     HIP_CHECK(hipEventCreateWithFlags(&ev_a, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&ev_l, hipEventDisableTiming));
     HIP_CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
@@ -1960,6 +1962,11 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   };
   uint64_t scratch_bytes = 0;
   auto scratch_reserve = [&](uint64_t n) { uint64_t at = (scratch_bytes + 255) & ~255ull; scratch_bytes = at + n; return at; };
+  // LK_SET_LDS leaves: their coarse filter bitmap (region) and exact LUT, reserved in scratch once the stream plan is
+  // known -- a segment whose driving IN leaf the exact-mode stream tests builds that leaf's LUT in LDS from its dictIds
+  // and needs neither (nor their zero fill and set_lut_bits job)
+  struct SetLdsRes { uint64_t leaf_index; size_t lut_req; uint64_t region_bytes, lut_bytes; };
+  std::vector<SetLdsRes> set_lds_res;
   uint64_t entries_in_filter = 0;
   // device pointers into arena / scratch are patched once those are allocated
   enum PatchTarget { PT_AUX = 0, PT_WORDS = 1, PT_LUT = 2, PT_RVALS = 3 };
@@ -2071,12 +2078,11 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
             const uint32_t n_region = set_geometry(std::max(c->card, 1u), dl.shift, dl.nbw);
             dl.set_ints = n_region;
             dl.lds_off = set_off[li];
-            // filter bitmap (and, when shift > 0, the exact LUT resolving its candidates) built on the device
-            const uint64_t region_off = scratch_reserve(4ull * n_region);
-            const uint64_t lut_off = dl.shift ? scratch_reserve(4ull * ((c->card + 31) / 32 + 1)) : ~0ull;
-            lut_req(pl, c, lut_off, region_off, dl.shift);
-            patches.push_back({(uint64_t)si * L + li, region_off, false, PT_AUX});
-            if (dl.shift) patches.push_back({(uint64_t)si * L + li, lut_off, false, PT_LUT});
+            // filter bitmap (and, when shift > 0, the exact LUT resolving its candidates) built on the device, in
+            // scratch reserved once the stream plan is known (set_lds_res)
+            set_lds_res.push_back({(uint64_t)si * L + li, luts.size(), 4ull * n_region,
+                                   dl.shift ? 4ull * ((c->card + 31) / 32 + 1) : 0ull});
+            lut_req(pl, c, ~0ull, ~0ull, dl.shift);
           } else {
             dl.kind = LK_SET_LUT;
             const uint64_t lut_off = scratch_reserve(4ull * ((c->card + 31) / 32 + 1));
@@ -3050,7 +3056,45 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   }
   const uint64_t off_items = ar.put(items.data(), items.size() * sizeof(WorkItem));
   for (StreamLaunch& sl : sp.launches) sl.first_off = ar.put(sl.first.data(), sl.first.size() * 4);
-  const uint64_t off_exact = sp.exact ? ar.put(sp.exact_nwords.data(), 4ull * S) : 0;
+  // exact-mode segments whose driving leaf's LUT the stream builds in LDS (ids mode; the leaf read nowhere else: not a
+  // further stream leaf, not in the list scan's phase B); PG_STREAM_LDS_LUT=0 keeps the global LUT staging
+  std::vector<uint8_t> lds_lut(S, 0);
+  std::vector<size_t> exact_req(S, 0);  // the LutReq (ids or literals) of segment si's driving leaf
+  std::vector<LutReq> exact_luts;
+  {
+    const char* ll_env = getenv("PG_STREAM_LDS_LUT");
+    bool ok = sp.on && sp.exact && q.num_items && !(ll_env && atoi(ll_env) == 0);
+    for (uint32_t x : sp.extra) ok = ok && x != sp.leaf;
+    for (uint32_t i = q.opB_begin; i < q.opB_end && ok; i++) ok = q.ops[i] != (int32_t)sp.leaf;
+    if (ok)
+      for (const SetLdsRes& x : set_lds_res) {
+        const uint32_t si = (uint32_t)(x.leaf_index / L), li = (uint32_t)(x.leaf_index % L);
+        if (li != sp.leaf || !sp.exact_nwords[si]) continue;
+        lds_lut[si] = 1;
+        exact_req[si] = exact_luts.size();
+        exact_luts.push_back(luts[x.lut_req]);
+      }
+    std::vector<uint8_t> drop(luts.size(), 0);
+    for (const SetLdsRes& x : set_lds_res) {
+      const uint32_t si = (uint32_t)(x.leaf_index / L), li = (uint32_t)(x.leaf_index % L);
+      if (lds_lut[si] && li == sp.leaf) {
+        drop[x.lut_req] = 1;
+        continue;
+      }
+      LutReq& lr = luts[x.lut_req];
+      lr.region_off = scratch_reserve(x.region_bytes);
+      patches.push_back({x.leaf_index, lr.region_off, false, PT_AUX});
+      if (x.lut_bytes) {
+        lr.lut_off = scratch_reserve(x.lut_bytes);
+        patches.push_back({x.leaf_index, lr.lut_off, false, PT_LUT});
+      }
+    }
+    size_t k = 0;
+    for (size_t i = 0; i < luts.size(); i++)
+      if (!drop[i]) luts[k++] = luts[i];
+    luts.resize(k);
+  }
+  const uint64_t off_exact = sp.exact ? ar.reserve(S * sizeof(ExactSet)) : 0;
   // GM_PART: each block's region of the entry array = the docs of its items (the kernel's [i0, i1) item range)
   uint64_t off_part_base = 0, part_entries = 0;
   if (part.on && blocks) {
@@ -3128,6 +3172,25 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   if (!keycols.empty()) memcpy(&ar.h[off_keycols], keycols.data(), keycols.size() * sizeof(ColDesc));
   if (!segd.empty()) memcpy(&ar.h[off_segs], segd.data(), segd.size() * sizeof(SegDesc));
   if (!lutjobs.empty()) memcpy(&ar.h[off_lutjobs], lutjobs.data(), lutjobs.size() * sizeof(LutJob));
+  if (sp.exact) {
+    std::vector<ExactSet> es(S);
+    for (uint32_t si = 0; si < S; si++) {
+      memset(&es[si], 0, sizeof(ExactSet));
+      es[si].nwords = sp.exact_nwords[si];
+      if (!lds_lut[si]) continue;
+      const LutReq& x = exact_luts[exact_req[si]];
+      es[si].n = x.n;
+      if (x.ids_off != ~0ull) {
+        es[si].ids = (const int32_t*)(dA + x.ids_off);
+      } else {  // values mode: the literals (dictionary's stored type) and the segment's dictionary
+        es[si].vals = dA + x.vals_off;
+        es[si].dict = x.dict;
+        es[si].card = x.card;
+        es[si].dtype = x.dtype;
+      }
+    }
+    memcpy(&ar.h[off_exact], es.data(), S * sizeof(ExactSet));
+  }
   {
     size_t k = 0;
     for (const PrepassOp& op : pre) {
@@ -3193,7 +3256,11 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     }
   }
   HIP_CHECK(launch_roaring_keys((const RoaringJob*)(dA + off_rjobs), (uint32_t)rjobs.size(), roaring_blocks, s));
-  HIP_CHECK(hipEventRecord(ev[4], s));
+  // the pre-pass's end, recorded only when a pre-pass kernel ran (an event record costs the stream a few us between
+  // its dependent kernels: none was launched -> the pre-pass took no time and ev[0] stands for its end)
+  const bool pre_ran = !lutjobs.empty() || !pre.empty() || (!rjobs.empty() && roaring_blocks);
+  if (pre_ran) HIP_CHECK(hipEventRecord(ev[4], s));
+  hipEvent_t ev_pre = pre_ran ? ev[4] : ev[0];
   for (const PreLaunch& pl : pre_launches) {
     PreSpec ps;
     memset(&ps, 0, sizeof(ps));
@@ -3215,7 +3282,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     ss.leaf = sp.leaf;
     ss.cap = sp.cap;
     ss.num_extra = (uint32_t)sp.extra.size();
-    ss.exact_nwords = sp.exact ? (const uint32_t*)(dA + off_exact) : nullptr;
+    ss.exact = sp.exact ? (const ExactSet*)(dA + off_exact) : nullptr;
     ss.interleave = sp.interleave ? 1u : 0u;
     for (size_t x = 0; x < sp.extra.size(); x++) ss.extra[x] = sp.extra[x];
     ss.set_lds_ints = (sp.set_ints + 3u) & ~3u;  // the wave slices start 16-byte aligned after the IN sets
@@ -3497,8 +3564,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   if (cancel.state() == 1) return fail(PG_E_CANCELLED, "query %llu cancelled", (unsigned long long)plan->query_id);
   if (cancel.state() == 2) return fail(PG_E_TIMEOUT, "deadline passed during the scan");
   float pre_ms = 0, filt_ms = 0, scan_ms = 0;
-  (void)hipEventElapsedTime(&pre_ms, ev[0], ev[4]);
-  (void)hipEventElapsedTime(&filt_ms, ev[4], ev[1]);
+  if (ev_pre != ev[0]) (void)hipEventElapsedTime(&pre_ms, ev[0], ev_pre);
+  (void)hipEventElapsedTime(&filt_ms, ev_pre, ev[1]);
   (void)hipEventElapsedTime(&scan_ms, ev[1], ev[2]);
   t_timing.prepass_ms = pre_ms;
   t_timing.prefilter_ms = filt_ms;
