@@ -395,7 +395,7 @@ def main():
     kernels = [k for p, k in (("prepass", "prepass"), ("stream", "stream_kernel"), ("fused_scan", "scan_kernel"),
                               ("partitioned", "part_direct + part_split2s + part_aggregate"),
                               ("index_count", "index_count_kernel")) if p in path]
-    scan_avg_ms = float(np.mean(scan_ms))
+    scan_avg_ms = max(float(np.mean(scan_ms)), 1e-9)  # (0 only with the library's phase timings off)
     alg_bytes = fwd_bytes + dict_bytes
     achieved = plan_bytes / (scan_avg_ms * 1e-3) / 1e9
     alg_achieved = alg_bytes / (scan_avg_ms * 1e-3) / 1e9

@@ -198,6 +198,9 @@ struct StreamSpec {
   // column into its LDS slice (16-byte coalesced loads) and tests its survivors from there instead of per-doc window
   // reads.  stage_words: words per wave slice (0: off), placed after the IN-set words (set_lds_ints, a multiple of 4).
   uint32_t stage_words, stage_pad;
+  // optional [2] wall-clock stamps of the launch (the phase timing without an event record between dependent kernels):
+  // [0] max of ~(block start), i.e. ~(earliest start); [1] the latest block end; both zeroed before the launch
+  unsigned long long* stamp;
 };
 constexpr uint32_t kStreamStageBits = 16;
 hipError_t launch_stream(const StreamSpec& p, uint32_t bits, uint32_t blocks, hipStream_t s);

@@ -344,6 +344,7 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? (PG_STREAM_PIPE_EXTRA
   // the exact LUT's lookups address LDS absolutely (eval_group): the dynamic LDS must start at address 0
   if (EXACT && threadIdx.x == 0 && (uint32_t)(uintptr_t)(lds_cptr)lds_sets != 0u) atomicOr(p.err, 64u);
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  if (p.stamp && tid == 0) atomicMax(&p.stamp[0], ~(unsigned long long)wall_clock64());
   const uint32_t i0 = p.interleave ? ldcf(p.block_first, 0) + blockIdx.x : ldcf(p.block_first, blockIdx.x);
   const uint32_t i1 = ldcf(p.block_first, p.interleave ? gridDim.x : blockIdx.x + 1);
   const uint32_t istep = p.interleave ? gridDim.x : 1u;
@@ -472,6 +473,7 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? (PG_STREAM_PIPE_EXTRA
       if (n > p.cap) atomicOr(p.err, 8u);
     }
   }
+  if (p.stamp && tid == 0) atomicMax(&p.stamp[1], (unsigned long long)wall_clock64());
 }
 
 hipError_t launch_stream(const StreamSpec& p, uint32_t bits, uint32_t blocks, hipStream_t s) {

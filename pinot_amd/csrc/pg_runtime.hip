@@ -1124,6 +1124,13 @@ struct ThreadCtx {  // per calling thread: staging + events, created once
 };
 thread_local ThreadCtx t_ctx;
 
+// A phase-timing event record (t_timing); PG_TIMING_EVENTS=0 skips them (dev A/B of their cost between kernels: the
+// phase times then read 0)
+hipError_t timing_record(hipEvent_t e, hipStream_t s) {
+  static const bool off = getenv("PG_TIMING_EVENTS") && atoi(getenv("PG_TIMING_EVENTS")) == 0;
+  return off ? hipSuccess : hipEventRecord(e, s);
+}
+
 bool pl_too_big(uint32_t ints) { return ints * 4ull > (uint64_t)kLdsSetBytes; }
 
 // Upper bound of the scan grid: a whole number of resident rounds of blocks (2 x the resident blocks per CU, no
@@ -1132,11 +1139,15 @@ bool pl_too_big(uint32_t ints) { return ints * 4ull > (uint64_t)kLdsSetBytes; }
 // overrides both.
 uint64_t g_grid_caps[4] = {0, 0, 0, 0};
 uint32_t g_num_cus = 256;
+uint64_t g_wall_khz = 0;  // wall_clock64() ticks per ms (hipDeviceAttributeWallClockRate)
 void init_grid_caps() {  // under g_init_mu (pg_init), before any query reads them
   int dev_cus = 0;
   if (hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, g_device) != hipSuccess || dev_cus <= 0)
     dev_cus = 256;
   g_num_cus = (uint32_t)dev_cus;
+  int wall_khz = 0;
+  if (hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, g_device) == hipSuccess && wall_khz > 0)
+    g_wall_khz = (uint64_t)wall_khz;
   const char* e = getenv("PG_SCAN_BLOCKS_PER_CU");
   for (int i = 0; i < 4; i++) {
     const bool grouped = i & 1, one_round = i & 2;
@@ -3004,9 +3015,10 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     }
     HIP_CHECK(hipStreamSynchronize(s));  // the pinned staging words are reused below
   }
-  if ((rc = P.seg_matched.alloc_pooled(8ull * (S ? S : 1) + 16))) return rc;
-  if (!fills.add(P.seg_matched.p, 0, 8ull * (S ? S : 1) + 16))
-    HIP_CHECK(hipMemsetAsync(P.seg_matched.p, 0, 8ull * (S ? S : 1) + 16, s));
+  // [S] matched docs | error word | pad | the stream's two wall-clock stamps (StreamSpec.stamp): read back together
+  if ((rc = P.seg_matched.alloc_pooled(8ull * (S ? S : 1) + 32))) return rc;
+  if (!fills.add(P.seg_matched.p, 0, 8ull * (S ? S : 1) + 32))
+    HIP_CHECK(hipMemsetAsync(P.seg_matched.p, 0, 8ull * (S ? S : 1) + 32, s));
   {
     const StateView v = P.view();
     q.i64 = v.i64;
@@ -3234,7 +3246,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   PG_PROF("arena");
   // the arena was built in pinned memory: the device reads it from there
   HIP_CHECK(launch_arena_upload(ar.h.dp, arena.p, ar.h.size(), scratch.p, scratch_bytes, fills, s));
-  HIP_CHECK(hipEventRecord(ev[0], s));
+  HIP_CHECK(timing_record(ev[0], s));
   {
     uint32_t max_n = 0;
     for (const LutReq& r : luts) max_n = std::max(max_n, r.n);
@@ -3259,7 +3271,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   // the pre-pass's end, recorded only when a pre-pass kernel ran (an event record costs the stream a few us between
   // its dependent kernels: none was launched -> the pre-pass took no time and ev[0] stands for its end)
   const bool pre_ran = !lutjobs.empty() || !pre.empty() || (!rjobs.empty() && roaring_blocks);
-  if (pre_ran) HIP_CHECK(hipEventRecord(ev[4], s));
+  if (pre_ran) HIP_CHECK(timing_record(ev[4], s));
   hipEvent_t ev_pre = pre_ran ? ev[4] : ev[0];
   for (const PreLaunch& pl : pre_launches) {
     PreSpec ps;
@@ -3273,6 +3285,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     ps.out = (uint32_t* const*)(dA + off_pre_out);
     HIP_CHECK(launch_prefilter(ps, pl.bits, (uint32_t)std::min<uint64_t>(pl.n_items, (uint64_t)g_num_cus * 8), s));
   }
+  // the pre-filter kernels' end (the stream's own time comes from its stamps: no record between it and the scan)
+  if (!pre_launches.empty()) HIP_CHECK(timing_record(ev[1], s));
   if (sp.on && q.num_items) {
     if ((rc = l_docs.alloc_pooled(4ull * q.num_items * sp.cap + 16)) || (rc = l_counts.alloc_pooled(4ull * q.num_items + 16)))
       return rc;
@@ -3303,6 +3317,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     ss.docs = (uint32_t*)l_docs.p;
     ss.counts = (uint32_t*)l_counts.p;
     ss.err = q.err;
+    ss.stamp = q.seg_matched + (S ? S : 1) + 2;
     for (size_t k = 0; k < sp.launches.size(); k++) {
       const StreamLaunch& sl = sp.launches[k];
       ss.block_first = (const uint32_t*)(dA + sl.first_off);
@@ -3312,7 +3327,6 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     q.list_docs = ss.docs;
     q.list_counts = ss.counts;
   }
-  HIP_CHECK(hipEventRecord(ev[1], s));
   if (is_cancelled(plan->query_id)) { (void)hipStreamSynchronize(s); return fail(PG_E_CANCELLED, "query %llu cancelled", (unsigned long long)plan->query_id); }
   if (plan->deadline_ms && now_ms() > plan->deadline_ms) { (void)hipStreamSynchronize(s); return fail(PG_E_TIMEOUT, "deadline passed"); }
   CancelSlot cancel(plan->query_id, plan->query_id != 0 || plan->deadline_ms != 0);
@@ -3526,8 +3540,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     HIP_CHECK(launch_scan(q, blocks, s));
     scan_ran = true;
   }
-  HIP_CHECK(hipEventRecord(ev[2], s));
-  const uint64_t n_sm = (S ? S : 1) + 2;
+  HIP_CHECK(timing_record(ev[2], s));
+  const uint64_t n_sm = (S ? S : 1) + 4;
   uint64_t* sm = (uint64_t*)t_ctx.readback.get(8ull * n_sm);
   if (!sm) return fail(PG_E_NOMEM, "pinned readback of %llu bytes failed", (unsigned long long)(8ull * n_sm));
   // the match counts + error word, and a small final state, written into mapped host memory by one launch
@@ -3564,9 +3578,19 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   if (cancel.state() == 1) return fail(PG_E_CANCELLED, "query %llu cancelled", (unsigned long long)plan->query_id);
   if (cancel.state() == 2) return fail(PG_E_TIMEOUT, "deadline passed during the scan");
   float pre_ms = 0, filt_ms = 0, scan_ms = 0;
+  // pre-pass: ev[0] -> ev_pre; pre-filter kernels: -> ev[1]; the stream: its wall-clock stamps; the scan: the rest of
+  // ev[0] -> ev[2] (with the launch boundaries between them)
+  float total_ms = 0;
   if (ev_pre != ev[0]) (void)hipEventElapsedTime(&pre_ms, ev[0], ev_pre);
-  (void)hipEventElapsedTime(&filt_ms, ev_pre, ev[1]);
-  (void)hipEventElapsedTime(&scan_ms, ev[1], ev[2]);
+  if (!pre_launches.empty()) (void)hipEventElapsedTime(&filt_ms, ev_pre, ev[1]);
+  (void)hipEventElapsedTime(&total_ms, ev[0], ev[2]);
+  {
+    const uint64_t* st = sm + (S ? S : 1) + 2;
+    if (sp.on && q.num_items && st[1] && ~st[0] <= st[1] && g_wall_khz)
+      filt_ms += (float)((double)(st[1] - ~st[0]) / (double)g_wall_khz);
+  }
+  scan_ms = std::max(0.0f, total_ms - pre_ms - filt_ms);
+  (void)hipGetLastError();  // an elapsed time that could not be read (events skipped) must not stick to a later launch
   t_timing.prepass_ms = pre_ms;
   t_timing.prefilter_ms = filt_ms;
   t_timing.scan_ms = scan_ms;
