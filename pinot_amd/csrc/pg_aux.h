@@ -126,6 +126,8 @@ struct IdxSpec {
   uint32_t num_chunks;
   uint32_t cntmv_slot;              // i64 slot of COUNTMV (~0: none)
   const IdxSeg* segs;
+  const IdxLeaf* leaves;            // [num_segs][num_leaves]
+  const uint32_t* blk_seg;          // block -> its segment
   unsigned long long* i64;          // slot 0: doc count
   unsigned long long* seg_matched;  // [num_segs]
 };

@@ -12,8 +12,14 @@
 // directory entries the leaves select and the count words of the matched docs.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "pg_aux.h"
 #include "pg_roaring.h"
+#if PG_IDX_PROF
+#include <cstdio>
+#include <cstring>
+#endif
 
 namespace pg {
 
@@ -33,107 +39,155 @@ __device__ __forceinline__ uint32_t word_range(int64_t a, int64_t b) {
   return hi & ~lo;
 }
 
-__global__ __launch_bounds__(kIdxNT) void index_count_kernel(IdxSpec p) {
+#if PG_IDX_PROF
+// per-block sums of thread 0's phase cycles: 0 setup, 1-4 the decode's phases (pg_roaring.h), 5 filter + count,
+// 6 reduce; 7 block wall-clock ticks (start to end); g_idx_span: min start, max end of the launch (wall clock)
+__device__ unsigned long long g_idx_prof[8], g_idx_span[2];
+#endif
+
+#ifndef PG_IDX_LATE_COUNT  // 1: the count words are loaded after the decode (32 fewer VGPRs held across it)
+#define PG_IDX_LATE_COUNT 1
+#endif
+#ifndef PG_IDX_WAVES
+#define PG_IDX_WAVES 4  // waves per SIMD the register budget is cut for (4: <= 128 VGPRs)
+#endif
+__global__ __launch_bounds__(kIdxNT, PG_IDX_WAVES) void index_count_kernel(IdxSpec p) {
   extern __shared__ __attribute__((aligned(16))) uint32_t chunks[];  // [num_chunks][2048]
   __shared__ RoaringLds<kIdxNT> S;
   __shared__ RoarView V[kIdxMaxLeaves];
+  __shared__ uint4 D[kIdxMaxLeaves];  // leaf l for the filter: (kind | negate << 8, lo, hi, chunk word offset)
   __shared__ uint32_t nv;
   __shared__ unsigned long long red[2][kIdxNT / 64];
-  static_assert(kIdxMaxLeaves <= kRoarMaxViews, "one view per inverted leaf");
+  static_assert(kIdxMaxLeaves <= kRoarMaxViews && kIdxMaxLeaves <= 64, "one view per inverted leaf");
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  uint32_t lo = 0, hi = p.num_segs;  // the segment whose block range holds this block
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (p.segs[mid].first_block <= blockIdx.x) lo = mid; else hi = mid;
-  }
-  const uint32_t si = lo;
-  const IdxSeg G = p.segs[si];
+  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_ = PG_IDX_PROF ? prof_clk() : 0ull;
+  const unsigned long long w0 = PG_IDX_PROF ? wall_clock64() : 0ull;
+  // the block's segment from the host's block -> segment table (one load), then its descriptor and its leaves' (in
+  // parallel: the leaves are [segment][leaf] in one array)
+  const uint32_t si = ld_global(p.blk_seg + blockIdx.x);
+  const IdxSeg G = ld_global(p.segs + si);
+  IdxLeaf L{};
+  if (tid < p.num_leaves) L = ld_global(p.leaves + (uint64_t)si * p.num_leaves + tid);
   const uint32_t key = G.key0 + (blockIdx.x - G.first_block);
+  const uint32_t nd = G.num_docs;
+  // COUNTMV from the 4-bit count column: this thread's count words of all its chunk words are loaded up front, before
+  // the decode (they do not depend on it: one latency hidden under the directory loads; most words hold a match at
+  // config 5's 5.6 % pass).  Unconditional loads (a word past the segment reads word 0): a select between a load and
+  // zero would wait for the load right here.
+  constexpr uint32_t kWpt = 2048u / kIdxNT;
+  uint4 cwp[kWpt];
+#pragma unroll
+  for (uint32_t k = 0; k < kWpt; k++) cwp[k] = make_uint4(0u, 0u, 0u, 0u);
+  auto load_counts = [&]() {
+    if (p.cntmv_slot != 0xFFFFFFFFu && G.mv_cnt && !(PG_IDX_SKIP & 8)) {
+#pragma unroll
+      for (uint32_t k = 0; k < kWpt; k++) {
+        const uint64_t d0 = (uint64_t)key * 65536u + 32u * (tid + k * kIdxNT);
+        cwp[k] = ld_global((const uint4*)(G.mv_cnt + (d0 < nd ? d0 / 8 : 0)));
+      }
+    }
+  };
+  if (!PG_IDX_LATE_COUNT) load_counts();
   for (uint32_t w = tid; w < p.num_chunks * 2048u; w += kIdxNT) chunks[w] = 0u;
-  // every inverted leaf of the segment, decoded together into its chunk: leaf l's descriptor read by lane l (one
-  // latency), the views compacted by wave 0
+  // every inverted leaf of the segment, decoded together into its chunk: the views compacted by wave 0
   if (tid < 64) {
-    IdxLeaf L{};
-    if (tid < p.num_leaves) L = G.leaves[tid];
     const bool on = tid < p.num_leaves && L.kind == IL_ROARING && L.nids;
     const unsigned long long b = __ballot(on);
     if (on) {
       const uint32_t at = (uint32_t)__popcll(b & ((1ull << tid) - 1ull));
-      V[at] = RoarView{L.roaring, L.cs, L.dir, L.keydir, L.ids, chunks + p.chunk_of[tid] * 2048u, L.nids, L.card};
+      V[at] = RoarView{L.roaring, L.cs, L.dir, L.keydir, L.ids, p.chunk_of[tid] * 2048u, L.nids, L.card};
     }
+    if (tid < p.num_leaves)
+      D[tid] = make_uint4(L.kind | L.negate << 8, (uint32_t)L.lo, (uint32_t)L.hi,
+                          L.kind == IL_ROARING ? p.chunk_of[tid] * 2048u : 0u);
     if (tid == 0) nv = (uint32_t)__popcll(b);
   }
-  __syncthreads();
-  roaring_key_chunks<kIdxNT>(V, nv, key, S);
-  const uint32_t nd = G.num_docs;
+  lds_barrier();
+  if (PG_IDX_PROF && tid == 0) { const unsigned long long n_ = prof_clk(); prof[0] += (n_ - t_) & 0xFFFFFull; t_ = n_; }
+  roaring_key_chunks<kIdxNT>(V, nv, key, S, chunks, PG_IDX_PROF ? prof : nullptr);
+  if (PG_IDX_PROF && tid == 0) t_ = prof_clk();
+  if (PG_IDX_LATE_COUNT) load_counts();
+  // the filter over this thread's kWpt chunk words at once: wave-uniform loops over the (at most two-level) item list,
+  // each leaf's descriptor read once per item (an LDS broadcast), not once per word
+  const int64_t dbase = (int64_t)key * 65536 + 32 * (int64_t)tid;  // doc of word 0's bit 31; word k: + 32 k NT
+  auto leafw = [&](uint32_t l, uint32_t* out) {
+    const uint4 d = D[l];
+    const uint32_t kind = d.x & 0xFFu;
+    if (kind == IL_ROARING) {
+      const uint32_t neg = (d.x >> 8) ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+      for (uint32_t k = 0; k < kWpt; k++) out[k] = chunks[d.w + tid + k * kIdxNT] ^ neg;
+    } else if (kind == IL_DOCRANGE) {
+#pragma unroll
+      for (uint32_t k = 0; k < kWpt; k++) {
+        const int64_t d0 = dbase + 32 * (int64_t)(k * kIdxNT);
+        out[k] = word_range((int64_t)(int32_t)d.y - d0, (int64_t)(int32_t)d.z - d0);
+      }
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < kWpt; k++) out[k] = kind == IL_ALL ? 0xFFFFFFFFu : 0u;
+    }
+  };
+  uint32_t m[kWpt];
+#pragma unroll
+  for (uint32_t k = 0; k < kWpt; k++) m[k] = p.root_or ? 0u : 0xFFFFFFFFu;
+  for (uint32_t i = 0; i < p.num_items; i++) {
+    const uint32_t it = p.item[i];
+    uint32_t v[kWpt];
+    if (it & 0x40000000u) {
+      const uint32_t g = it & 0xFFu;
+      const bool gor = p.group_or[g] != 0;
+#pragma unroll
+      for (uint32_t k = 0; k < kWpt; k++) v[k] = gor ? 0u : 0xFFFFFFFFu;
+      for (uint32_t j = 0; j < p.gn[g]; j++) {
+        const uint32_t gl = p.gleaf[p.gfirst[g] + j];
+        uint32_t x[kWpt];
+        leafw(gl & 0xFFu, x);
+        const uint32_t neg = (gl & 0x80000000u) ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < kWpt; k++) v[k] = gor ? (v[k] | (x[k] ^ neg)) : (v[k] & (x[k] ^ neg));
+      }
+    } else {
+      leafw(it & 0xFFu, v);
+    }
+    const uint32_t neg = (it & 0x80000000u) ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < kWpt; k++) m[k] = p.root_or ? (m[k] | (v[k] ^ neg)) : (m[k] & (v[k] ^ neg));
+  }
   unsigned long long cnt = 0, cmv = 0;
-  // COUNTMV from the 4-bit count column: this thread's count words of all its chunk words are loaded up front (one
-  // latency, not one per word; most words hold a match at config 5's 5.6 % pass)
-  constexpr uint32_t kWpt = 2048u / kIdxNT;
-  uint4 cwp[kWpt];
-  const bool pre_cnt = p.cntmv_slot != 0xFFFFFFFFu && G.mv_cnt;
 #pragma unroll
   for (uint32_t k = 0; k < kWpt; k++) {
     const uint64_t d0 = (uint64_t)key * 65536u + 32u * (tid + k * kIdxNT);
-    cwp[k] = pre_cnt && d0 < nd ? *(const uint4*)(G.mv_cnt + d0 / 8) : make_uint4(0u, 0u, 0u, 0u);
-  }
-#pragma unroll
-  for (uint32_t k = 0; k < kWpt; k++) {
-    const uint32_t w = tid + k * kIdxNT;
-    const uint64_t d0 = (uint64_t)key * 65536u + 32u * w;
-    if (d0 >= nd) break;
-    const uint32_t valid = d0 + 32 <= nd ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (uint32_t)(nd - d0));
-    auto leaf = [&](uint32_t l) -> uint32_t {
-      const IdxLeaf& L = G.leaves[l];
-      switch (L.kind) {
-        case IL_ALL: return 0xFFFFFFFFu;
-        case IL_NONE: return 0u;
-        case IL_DOCRANGE: return word_range((int64_t)L.lo - (int64_t)d0, (int64_t)L.hi - (int64_t)d0);
-        default: {
-          const uint32_t v = chunks[p.chunk_of[l] * 2048u + w];
-          return L.negate ? ~v : v;
-        }
-      }
-    };
-    uint32_t m = p.root_or ? 0u : 0xFFFFFFFFu;
-    for (uint32_t i = 0; i < p.num_items; i++) {  // wave-uniform loops over the (at most two-level) filter
-      const uint32_t it = p.item[i];
-      uint32_t v;
-      if (it & 0x40000000u) {
-        const uint32_t g = it & 0xFFu;
-        v = p.group_or[g] ? 0u : 0xFFFFFFFFu;
-        for (uint32_t k = 0; k < p.gn[g]; k++) {
-          const uint32_t gl = p.gleaf[p.gfirst[g] + k];
-          uint32_t x = leaf(gl & 0xFFu);
-          if (gl & 0x80000000u) x = ~x;
-          v = p.group_or[g] ? (v | x) : (v & x);
-        }
-      } else {
-        v = leaf(it & 0xFFu);
-      }
-      if (it & 0x80000000u) v = ~v;
-      m = p.root_or ? (m | v) : (m & v);
-    }
-    m &= valid;
-    cnt += (uint32_t)__popc(m);
-    if (p.cntmv_slot != 0xFFFFFFFFu && m) {
+    const uint32_t valid = d0 >= nd ? 0u : d0 + 32 <= nd ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (uint32_t)(nd - d0));
+    const uint32_t mk = m[k] & valid;
+    cnt += (uint32_t)__popc(mk);
+    if (p.cntmv_slot != 0xFFFFFFFFu && mk && !(PG_IDX_SKIP & 8)) {
       if (G.mv_cnt) {  // 4-bit counts: docs d0 .. d0 + 31 are the 4 count words at d0 / 8
+        // count word q holds docs 8 q + j at nibble 7 - j; mask byte (mk >> 24 - 8 q) holds them at bit 7 - j: spread
+        // the byte's bit i to nibble i, mask the counts with it, add the nibbles (no per-doc loop, no divergence)
         const uint4 cw = cwp[k];
         const uint32_t c4[4] = {cw.x, cw.y, cw.z, cw.w};
-        for (uint32_t r = m; r; ) {
-          const uint32_t j = (uint32_t)__builtin_clz(r);
-          r &= ~(0x80000000u >> j);
-          cmv += (c4[j >> 3] >> (28u - 4u * (j & 7u))) & 15u;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+          uint32_t x = (mk >> (24u - 8u * q)) & 0xFFu;
+          x = (x | (x << 12)) & 0x000F000Fu;
+          x = (x | (x << 6)) & 0x03030303u;
+          x = (x | (x << 3)) & 0x11111111u;
+          const uint32_t v = c4[q] & (x * 15u);
+          const uint32_t b = (v & 0x0F0F0F0Fu) + ((v >> 4) & 0x0F0F0F0Fu);
+          cmv += (b * 0x01010101u) >> 24;
         }
       } else {
-        for (uint32_t r = m; r; ) {
+        for (uint32_t r = mk; r; ) {
           const uint32_t j = (uint32_t)__builtin_clz(r);
           r &= ~(0x80000000u >> j);
-          cmv += G.mv_offsets[d0 + j + 1] - G.mv_offsets[d0 + j];
+          cmv += ld_global(G.mv_offsets + d0 + j + 1) - ld_global(G.mv_offsets + d0 + j);
         }
       }
     }
   }
+  if (PG_IDX_PROF && tid == 0) { const unsigned long long n_ = prof_clk(); prof[5] += (n_ - t_) & 0xFFFFFull; t_ = n_; }
   // block sums -> one atomic per value
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -141,7 +195,7 @@ __global__ __launch_bounds__(kIdxNT) void index_count_kernel(IdxSpec p) {
     cmv += __shfl_down(cmv, o);
   }
   if (lane == 0) { red[0][wave] = cnt; red[1][wave] = cmv; }
-  __syncthreads();
+  lds_barrier();
   if (tid == 0) {
     unsigned long long c = 0, v = 0;
     for (uint32_t k = 0; k < kIdxNT / 64; k++) { c += red[0][k]; v += red[1][k]; }
@@ -151,20 +205,51 @@ __global__ __launch_bounds__(kIdxNT) void index_count_kernel(IdxSpec p) {
       if (p.cntmv_slot != 0xFFFFFFFFu) atomicAdd(&p.i64[p.cntmv_slot], v);
     }
   }
+#if PG_IDX_PROF
+  if (tid == 0) {
+    prof[6] += (prof_clk() - t_) & 0xFFFFFull;
+    const unsigned long long w1 = wall_clock64();
+    prof[7] = w1 - w0;
+    for (int i = 0; i < 8; i++) atomicAdd(&g_idx_prof[i], prof[i]);
+    atomicMax(&g_idx_span[0], ~w0);
+    atomicMax(&g_idx_span[1], w1);
+  }
+#endif
 }
 
 hipError_t launch_index_count(const IdxSpec& p, uint32_t blocks, hipStream_t s) {
   if (!blocks) return hipSuccess;
-  const size_t lds = (size_t)p.num_chunks * 2048 * 4;
+#ifndef PG_IDX_LDS_PAD  // dev: extra dynamic LDS per block (fewer blocks per CU: the contention experiment)
+#define PG_IDX_LDS_PAD 0
+#endif
+  const size_t lds = (size_t)p.num_chunks * 2048 * 4 + PG_IDX_LDS_PAD;
   if (lds > 64 * 1024) {
     static bool attr = false;  // > 64 KiB of dynamic LDS is opted into once per process
     if (!attr) {
       (void)hipFuncSetAttribute((const void*)index_count_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                kIdxMaxLeaves * 2048 * 4);
+                                (int)std::min<size_t>(kIdxMaxLeaves * 2048 * 4 + PG_IDX_LDS_PAD, 160 * 1024 - 12 * 1024));
       attr = true;
     }
   }
   hipLaunchKernelGGL(index_count_kernel, dim3(blocks), dim3(kIdxNT), lds, s, p);
+#if PG_IDX_PROF
+  {
+    unsigned long long h[8], sp[2];
+    int khz = 0;
+    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
+    if (hipDeviceSynchronize() == hipSuccess && hipMemcpyFromSymbol(h, HIP_SYMBOL(g_idx_prof), sizeof(h)) == hipSuccess &&
+        hipMemcpyFromSymbol(sp, HIP_SYMBOL(g_idx_span), sizeof(sp)) == hipSuccess) {
+      fprintf(stderr, "[idx_prof] blocks=%u lds=%zu per-block kcycles:", blocks, lds);
+      for (int i = 0; i < 7; i++) fprintf(stderr, " %.2f", h[i] / 1e3 / (double)blocks);
+      fprintf(stderr, " | block us %.2f | span us %.2f\n", h[7] / (double)blocks / (khz / 1e3),
+              (double)(sp[1] - ~sp[0]) / (khz / 1e3));
+      memset(h, 0, sizeof(h));
+      memset(sp, 0, sizeof(sp));
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_idx_prof), h, sizeof(h));
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_idx_span), sp, sizeof(sp));
+    }
+  }
+#endif
   return hipGetLastError();
 }
 

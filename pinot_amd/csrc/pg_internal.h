@@ -139,6 +139,33 @@ enum SlotKind : uint32_t { SK_NONE = 0, SK_I64 = 1, SK_FX = 2, SK_MIN = 3, SK_MA
 enum GroupMode : uint32_t { GM_NONE = 0, GM_DENSE = 1, GM_HASH = 2, GM_HASH_SEG = 3, GM_PART = 4 };
 constexpr unsigned long long kEmptyKey = 0xFFFFFFFFFFFFFFFFull;
 
+#ifdef __HIPCC__  // (hipcc only: a plain C++ build of this header, as the fixed-point test does, skips it)
+// A load through a generic pointer that points to global memory, issued as a global load.  A pointer the compiler
+// cannot trace to a kernel argument (one read back from LDS, or from a table in memory) is generic, and its loads
+// compile to flat loads -- which also count in lgkmcnt, so every later LDS wait (a barrier, a ds_read's use) waits
+// for them too: prefetches issued through such pointers would land before the LDS work they were meant to overlap.
+template <typename T>
+__device__ __forceinline__ T ld_global(const T* p) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return *(const __attribute__((address_space(1))) T*)p;
+#else
+  return *p;  // (the host pass only parses device code)
+#endif
+}
+// (HIP's uint2 / uint4 copy through a constructor taking a generic reference, which would turn the load flat again:
+// load them as plain vectors)
+__device__ __forceinline__ uint2 ld_global(const uint2* p) {
+  typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+  const v2u v = *(const __attribute__((address_space(1))) v2u*)p;
+  return make_uint2(v.x, v.y);
+}
+__device__ __forceinline__ uint4 ld_global(const uint4* p) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const v4u v = *(const __attribute__((address_space(1))) v4u*)p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+#endif
+
 __host__ __device__ inline uint64_t mix64(uint64_t x) {  // murmur3 fmix64 (the HashCommon.mix role)
   x ^= x >> 33;
   x *= 0xff51afd7ed558ccdull;

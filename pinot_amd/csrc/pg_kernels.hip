@@ -378,8 +378,8 @@ __global__ __launch_bounds__(256) void roaring_keys_kernel(const RoaringJob* __r
   const RoaringJob J = jobs[lo];
   const uint32_t key = J.key0 + (blockIdx.x - J.first_block), tid = threadIdx.x;
   for (uint32_t w = tid; w < 2048; w += 256) chunk[w] = 0;
-  if (tid == 0) V = RoarView{J.roaring, J.cs, J.dir, J.keydir, J.ids, chunk, J.nids, J.card};
-  roaring_key_chunks<256>(&V, 1, key, S);  // (its first barrier publishes V and the zeroed chunk)
+  if (tid == 0) V = RoarView{J.roaring, J.cs, J.dir, J.keydir, J.ids, 0u, J.nids, J.card};
+  roaring_key_chunks<256>(&V, 1, key, S, chunk);  // (its first barrier publishes V and the zeroed chunk)
   const uint32_t nwords = (J.num_docs + 31) / 32, tail = J.num_docs & 31u;
   for (uint32_t w = tid; w < 2048; w += 256) {
     const uint32_t gw = key * 2048 + w;

@@ -69,12 +69,12 @@ constexpr uint32_t kSplitChunk = PG_SPLIT_CHUNK;
 constexpr int kAggB = PG_AGG_BATCH;  // entries per lane per load batch of the bucket pass  // entries counting-sorted per LDS round (16 per thread): longer runs per digit
 // (16 384 x 1 024 threads, one block per CU: split1 4.08 -> 3.10 ms, split2 2.71 -> 2.15 ms on config 4 vs 4 096 x 256)
 
-// The compile-time knobs (tools/part_variant.sh builds variants with -D) and what they size.  split_round scans the
+// The compile-time knobs (tools/variant.sh pg_part builds variants with -D) and what they size.  split_round scans the
 // digit counts with one thread per digit (<= 256 digits) in whole waves, each thread holds E = chunk / threads
 // entries in registers, and the chunk's sorted entries + digits live in the kernel's static LDS next to cnt / start /
 // cur; part_aggregate and part_direct stride their LDS tables by their thread counts.  A combination outside these
 // bounds would index past an LDS array (the r03 sweep's illegal access came from an ablation build whose flags were
-// not recorded: part_variant.sh now writes them next to the library).
+// not recorded: variant.sh now writes them next to the library).
 static_assert(kST % 64 == 0 && kST >= 256 && kST <= 1024, "split blocks: whole waves, one thread per digit (<= 256)");
 static_assert(kSplitChunk % kST == 0 && kSplitChunk / kST >= 1 && kSplitChunk / kST <= 32,
               "split chunk: E = chunk / threads entries per thread, held in registers");
@@ -92,7 +92,7 @@ __device__ __forceinline__ rsrc_t part_rsrc(const void* p, uint32_t bytes) {
                                            (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
-// ---- dev instrumentation (PG_PART_PROF=1 variant builds only: tools/part_variant.sh): lane 0 of every block sums
+// ---- dev instrumentation (PG_PART_PROF=1 variant builds only: tools/variant.sh pg_part): lane 0 of every block sums
 // clock64() deltas per phase in registers and adds them to g_part_prof[kernel][phase] once at its end; the launch
 // functions synchronise and print the per-block averages to stderr.  Kernels: 0 part_direct, 1 split2s, 2 aggregate.
 #ifndef PG_PART_PROF
@@ -661,7 +661,10 @@ __device__ __forceinline__ uint32_t lds_unpack(const uint32_t* lds, uint32_t p, 
 template <int M>
 __device__ __forceinline__ uint64_t id_of(const ColDesc& c, const int32_t* tab, int64_t base, uint32_t raw) {
   if (M == 0) return raw < c.card ? (uint64_t)(c.vbase + (int64_t)raw - base) : ~0ull;
-  return raw < c.card ? (uint64_t)((int64_t)tab[raw] - base) : ~0ull;
+  // (an unconditional global load at a clamped index: a load under the range check, or through the generic table
+  // pointer -- a flat load, counted in lgkmcnt -- would be waited for by the caller's next LDS atomic)
+  const int32_t x = ld_global(tab + (raw < c.card ? raw : 0u));
+  return raw < c.card ? (uint64_t)((int64_t)x - base) : ~0ull;
 }
 __host__ __device__ __forceinline__ int id_mode(uint32_t key_kind, const ColDesc& c) {
   if (key_kind == PG_KEY_KEYMAP) return 1;

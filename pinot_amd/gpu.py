@@ -5,7 +5,9 @@ engine raises.  Falling back to the CPU is the caller's (Pinot's) decision on PG
 """
 from __future__ import annotations
 
+import collections
 import ctypes as C
+import dataclasses
 import itertools
 import os
 import threading
@@ -82,6 +84,10 @@ class GpuEngine:
         self.device = device
         self._seg_keys: Dict[int, tuple] = {}    # id(segment) -> (segment, seg_key); holds the segment alive
         self._keymaps_uploaded = set()
+        self._plans: "collections.OrderedDict[tuple, tuple]" = collections.OrderedDict()  # compiled-plan cache
+        self._plan_lock = threading.Lock()
+        self.plan_cache_hits = 0
+        self.plan_cache_misses = 0
 
     # ---- residency (IndexingOverrides reader-provider hook)
     def upload_segment(self, seg: ImmutableSegment, table: Table) -> int:
@@ -174,6 +180,9 @@ class GpuEngine:
         if hit is not None:
             check(self.lib.pg_segment_release(hit[1]))
             self._keymaps_uploaded = {k for k in self._keymaps_uploaded if k[0] != hit[1]}
+            with self._plan_lock:  # plans over the released segment can never be hit again (keys are not reused)
+                for ck in [ck for ck in self._plans if hit[1] in ck[2]]:
+                    del self._plans[ck]
 
     # ---- execution
     def make_plan(self, table: Table, query: QueryContext, segments: Optional[Sequence[ImmutableSegment]] = None,
@@ -186,6 +195,35 @@ class GpuEngine:
         keys = [self.upload_segment(s, table) for s in segments]
         plan = CPlan(table, query, segments, keys, flags, trim, id_sets=self.dict_id_sets, config=config)
         self.upload_keymaps(table, plan, segments, keys)
+        return plan
+
+    PLAN_CACHE_SIZE = 64
+
+    def cached_plan(self, table: Table, sql: str, segments: Optional[Sequence[ImmutableSegment]] = None,
+                    flags: int = abi.PG_PLAN_VALUE_SETS, trim=False, config: Optional[InstanceConfig] = None) -> CPlan:
+        """make_plan through a compiled-plan cache (LRU, PLAN_CACHE_SIZE plans).  The reference plans every query from
+        scratch (InstancePlanMakerImplV2.makeInstancePlan, ~microseconds of Java per segment); here lowering a query
+        costs the SQL parse, the per-segment literal -> dictId resolution (one device launch) and the plan image, ~2 ms
+        for config 2's 128 segments, so a server answering the same query text again over the same resident segments
+        reuses the lowered plan.  The key pins everything the plan depends on: the SQL text, the table object, the
+        segments' residency keys (a released and re-uploaded segment gets a new key; keys are never reused), flags,
+        trim and the instance config.  A plan is immutable once built (execution reads its image), so reuse is
+        exact."""
+        segs = list(table.segments if segments is None else segments)
+        keys = tuple(self.upload_segment(s, table) for s in segs)
+        ck = (sql, id(table), keys, flags, trim, None if config is None else dataclasses.astuple(config))
+        with self._plan_lock:
+            hit = self._plans.get(ck)
+            if hit is not None and hit[0] is table:
+                self._plans.move_to_end(ck)
+                self.plan_cache_hits += 1
+                return hit[1]
+        plan = self.make_plan(table, parse(sql), segs, flags, trim, config)
+        with self._plan_lock:
+            self.plan_cache_misses += 1
+            self._plans[ck] = (table, plan)
+            while len(self._plans) > self.PLAN_CACHE_SIZE:
+                self._plans.popitem(last=False)
         return plan
 
     def run_plan(self, plan: CPlan, image: bool = True) -> IntermediateResult:
@@ -244,7 +282,8 @@ class GpuEngine:
 
     def execute(self, table: Table, query, segments=None, flags: int = abi.PG_PLAN_VALUE_SETS, trim=False,
                 config: Optional[InstanceConfig] = None) -> IntermediateResult:
-        if isinstance(query, str):
+        sql = query if isinstance(query, str) else None
+        if sql is not None:
             query = parse(query)
         if has_filtered_aggregations(query):  # FilteredAggregationOperator: one device plan per filter
             if query.group_by:  # the passes are aggregation-only (FilteredAggregationOperator); no group trim applies
@@ -252,6 +291,8 @@ class GpuEngine:
             return execute_filtered(lambda q: self.execute(table, q, segments, flags, config=config), query)
         if trim == "server" and query.group_by and group_trim(query, config).segment_size is not None:
             return self._execute_segment_trimmed(table, query, segments, flags, config)
+        if sql is not None:  # SQL text: through the compiled-plan cache
+            return self.run_plan(self.cached_plan(table, sql, segments, flags, trim, config))
         return self.run_plan(self.make_plan(table, query, segments, flags, trim, config))
 
     def _execute_segment_trimmed(self, table, query, segments, flags, config) -> IntermediateResult:

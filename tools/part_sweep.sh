@@ -1,5 +1,5 @@
 #!/bin/bash
-# highcard bench per library variant (tools/part_variant.sh): "name:ENV=V ..." entries in $VARIANTS
+# highcard bench per library variant (tools/variant.sh pg_part): "name:ENV=V ..." entries in $VARIANTS
 set -o pipefail
 mkdir -p gpurun_out
 for V in $VARIANTS; do

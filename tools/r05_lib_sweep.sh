@@ -1,5 +1,5 @@
 #!/bin/bash
-# config-4 bench per variant library (tools/part_variant.sh builds): names ... ("base" = the main library)
+# config-4 bench per variant library (tools/variant.sh pg_part builds): names ... ("base" = the main library)
 set -o pipefail
 mkdir -p gpurun_out
 for n in "$@"; do
