@@ -89,7 +89,7 @@ __global__ __launch_bounds__(kIdxNT, PG_IDX_WAVES) void index_count_kernel(IdxSp
     }
   };
   if (!PG_IDX_LATE_COUNT) load_counts();
-  for (uint32_t w = tid; w < p.num_chunks * 2048u; w += kIdxNT) chunks[w] = 0u;
+  for (uint32_t w = tid; w < p.num_chunks * 512u; w += kIdxNT) ((uint4*)chunks)[w] = make_uint4(0u, 0u, 0u, 0u);
   // every inverted leaf of the segment, decoded together into its chunk: the views compacted by wave 0
   if (tid < 64) {
     const bool on = tid < p.num_leaves && L.kind == IL_ROARING && L.nids;

@@ -21,7 +21,7 @@ namespace pg {
 #define PG_ROAR_R 4
 #endif
 #ifndef PG_ROAR_Q
-#define PG_ROAR_Q 8
+#define PG_ROAR_Q 4
 #endif
 #ifndef PG_ROAR_SB  // 1: a scheduling barrier after each container's ORs (bounds the addresses live at once)
 #define PG_ROAR_SB 1
@@ -82,13 +82,13 @@ struct RoaringLds {
   static constexpr uint32_t kOwn = 1024;    // 8-quad windows the owner table covers (more quads: a binary search)
   uint32_t bml[NT];            // bitmap containers of this round (payload offsets), OR-ed by the whole block
   uint8_t bview[NT];           //   and their views (more than NT in a round: the finder ORs it in by itself)
-  uint32_t nbml;
+  uint32_t nbml[2];            //   (counters double-buffered by round parity: reset a round ahead, no barrier of their own)
   uint32_t goff[kBig];         // array containers of more than kRoarSmall entries: payload offset,
   uint16_t gcard[kBig];        //   cardinality,
   uint8_t gview[kBig];         //   view,
   uint32_t gpre[kBig + 1];     //   first quad among the round's (exclusive prefix; [ng] = the total)
   uint16_t gown[kOwn];         // the entry holding quad 8 j (the quads' owner search starts there: <= 3 steps)
-  uint32_t ng, gtotal;
+  uint32_t ng[2];
   uint32_t wsum[NT / 64];
   uint32_t vpre[kRoarMaxViews + 1];  // prefix of the views' dictId counts
 };
@@ -122,8 +122,8 @@ __device__ __forceinline__ void roaring_key_chunks(const RoarView* V, uint32_t n
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   uint32_t sink = 0;  // (PG_IDX_SKIP 32 / 64: the loads kept alive without their ORs)
   if (tid == 0) {
-    S.nbml = 0;
-    S.ng = 0;
+    S.nbml[0] = S.nbml[1] = 0;
+    S.ng[0] = S.ng[1] = 0;
     uint32_t a = 0;
     for (uint32_t l = 0; l < nv; l++) { S.vpre[l] = a; a += V[l].nids; }
     S.vpre[nv] = a;
@@ -134,7 +134,7 @@ __device__ __forceinline__ void roaring_key_chunks(const RoarView* V, uint32_t n
   uint32_t vp[kRoarMaxViews];  // view j's first index in the combined list (~0 past the last view): selects by compares
 #pragma unroll
   for (uint32_t j = 0; j < kRoarMaxViews; j++) vp[j] = j < nv ? S.vpre[j] : 0xFFFFFFFFu;
-  for (uint32_t r0 = 0; r0 < nids; r0 += NT * R) {
+  for (uint32_t r0 = 0, par = 0; r0 < nids; r0 += NT * R, par ^= 1u) {
     // 1. the container of `key` of each of this thread's dictIds: the views (LDS), then the R dictIds, then the R
     //    key-major directory entries (one 8-byte load each: the descriptor itself) -- each set of R loads in flight
     //    together, as straight-line code with no branch between a load and the next one (a load under a per-lane
@@ -201,7 +201,7 @@ __device__ __forceinline__ void roaring_key_chunks(const RoarView* V, uint32_t n
 #pragma unroll
     for (int k = 0; k < R; k++) {
       if (c[k].type == 0 && c[k].card > kRoarSmall) {
-        const uint32_t g = atomicAdd(&S.ng, 1u);
+        const uint32_t g = atomicAdd(&S.ng[par], 1u);
         if (g < kBig) {
           S.goff[g] = c[k].offset;
           S.gcard[g] = (uint16_t)c[k].card;
@@ -210,7 +210,7 @@ __device__ __forceinline__ void roaring_key_chunks(const RoarView* V, uint32_t n
           roaring_array_or(V[vw[k]].roaring + c[k].offset, c[k].card, lds + V[vw[k]].chunk);
         }
       } else if (c[k].type == 1) {
-        const uint32_t b = atomicAdd(&S.nbml, 1u);
+        const uint32_t b = atomicAdd(&S.nbml[par], 1u);
         if (b < NT) {
           S.bml[b] = c[k].offset;
           S.bview[b] = (uint8_t)vw[k];
@@ -236,8 +236,12 @@ __device__ __forceinline__ void roaring_key_chunks(const RoarView* V, uint32_t n
       }
     }
     lds_barrier();
-    // exclusive prefix of the listed containers' quads: entries 2 t, 2 t + 1 per thread (wave scan + wave sums)
-    const uint32_t ng = S.ng < kBig ? S.ng : kBig;
+    // exclusive prefix of the listed containers' quads: entries 2 t, 2 t + 1 per thread (wave scan + wave sums); the
+    // owner windows from the prefix in registers (entry g holds quads [gpre[g], gpre[g] + n), so the windows j with
+    // 8 j in that range)
+    const uint32_t ng = S.ng[par] < kBig ? S.ng[par] : kBig;
+    const uint32_t nb = S.nbml[par] < NT ? S.nbml[par] : NT;
+    if (tid == 0) { S.ng[par ^ 1u] = 0; S.nbml[par ^ 1u] = 0; }  // (the previous round's, read before its last barrier)
     const uint32_t q0 = 2 * tid < ng ? ((uint32_t)S.gcard[2 * tid] + 3u) >> 2 : 0u;
     const uint32_t q1 = 2 * tid + 1 < ng ? ((uint32_t)S.gcard[2 * tid + 1] + 3u) >> 2 : 0u;
     uint32_t x = q0 + q1;
@@ -248,28 +252,29 @@ __device__ __forceinline__ void roaring_key_chunks(const RoarView* V, uint32_t n
     }
     if (lane == 63) S.wsum[wave] = x;
     lds_barrier();
-    uint32_t wb = 0;
-    for (uint32_t w = 0; w < wave; w++) wb += S.wsum[w];
+    uint32_t wb = 0, total = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NT / 64; w++) {
+      const uint32_t ws = S.wsum[w];
+      wb += w < wave ? ws : 0u;
+      total += ws;
+    }
     const uint32_t p0 = wb + x - q0 - q1, p1 = wb + x - q1;
     if (2 * tid < kBig) S.gpre[2 * tid] = p0;
     if (2 * tid + 1 < kBig) S.gpre[2 * tid + 1] = p1;
-    if (tid == NT - 1) { S.gtotal = wb + x; S.gpre[ng] = wb + x; }
-    lds_barrier();
-    // the owner windows: entry g holds quads [gpre[g], gpre[g] + n), so the windows j with 8 j in that range
-    const uint32_t total = S.gtotal;
+    if (tid == 0) S.gpre[ng] = total;
     const bool own = total <= 8 * RoaringLds<NT>::kOwn;
     if (own) {
       for (uint32_t j = (p0 + 7) >> 3; j < (p0 + q0 + 7) >> 3; j++) S.gown[j] = (uint16_t)(2 * tid);
       for (uint32_t j = (p1 + 7) >> 3; j < (p1 + q1 + 7) >> 3; j++) S.gown[j] = (uint16_t)(2 * tid + 1);
-      lds_barrier();
     }
+    lds_barrier();
     ROAR_LAP(2);
     // 3. the loads of the first bitmap container's words (this thread's 2048 / NT) and of the large arrays' first quads
     //    are issued, then the small arrays' entries (their loads were in flight over the lists and the scan) and the
     //    quads are OR-ed in.  Every LDS read this needs (list entries, view chunks) comes before the first OR: an LDS
     //    read after an OR would wait for it (lgkmcnt counts in order), one wait per container.
     constexpr uint32_t kWpt = 2048u / NT;
-    const uint32_t nb = S.nbml < NT ? S.nbml : NT;
     uint32_t bw[kWpt];
 #pragma unroll
     for (uint32_t j = 0; j < kWpt; j++) bw[j] = 0u;
@@ -350,9 +355,7 @@ __device__ __forceinline__ void roaring_key_chunks(const RoarView* V, uint32_t n
       for (uint32_t j = 0; j < kWpt; j++)
         if (bw[j]) atomicOr(&chunk[tid + j * NT], __builtin_bitreverse32(bw[j]));
     }
-    lds_barrier();
-    if (tid == 0) { S.nbml = 0; S.ng = 0; }
-    lds_barrier();
+    lds_barrier();  // (the chunks complete; this round's lists free for the next)
     ROAR_LAP(4);
   }
   if ((PG_IDX_SKIP & 96) && sink == 0x9E3779B9u) lds[0] |= 1u;
