@@ -199,7 +199,10 @@ struct StreamSpec {
   // further leaves over packed columns of at most kStreamStageBits bits: a wave stages its 64 groups' words of the
   // column into its LDS slice (16-byte coalesced loads) and tests its survivors from there instead of per-doc window
   // reads.  stage_words: words per wave slice (0: off), placed after the IN-set words (set_lds_ints, a multiple of 4).
-  uint32_t stage_words, stage_pad;
+  // stage_pre: every further leaf has its own slice per wave, DMA'd into LDS at the start of each group round with the
+  // driving leaf's loads (one load latency per round instead of two; set when the driving leaf passes >= 1/16, where
+  // nearly every wave's groups have survivors and the slices would be read anyway)
+  uint32_t stage_words, stage_pre;
   // optional [2] wall-clock stamps of the launch (the phase timing without an event record between dependent kernels):
   // [0] max of ~(block start), i.e. ~(earliest start); [1] the latest block end; both zeroed before the launch
   unsigned long long* stamp;

@@ -325,7 +325,8 @@ constexpr uint32_t kExactLutWords = 32768;  // 128 KiB: the exact LUT of a <= 1 
 // Words of dynamic LDS the stream's sets / LUT / slices take; the block's append cursor is the word after them (no
 // static LDS in the kernel, so the exact LUT sits at LDS address 0).
 __host__ __device__ __forceinline__ uint32_t stream_lds_words(const StreamSpec& p, bool exact) {
-  return exact ? kExactLutWords : p.set_lds_ints + (p.num_extra ? 4u * p.stage_words : 0u);
+  return exact ? kExactLutWords
+               : p.set_lds_ints + (p.num_extra ? 4u * p.stage_words * (p.stage_pre ? p.num_extra : 1u) : 0u);
 }
 
 #ifndef PG_STREAM_PIPE_EXTRA
@@ -420,6 +421,22 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? (PG_STREAM_PIPE_EXTRA
         const uint32_t g = g0 + tid;
         const uint64_t d0 = (uint64_t)g * 32;
         uint32_t m = 0;
+        if (EXTRA && p.stage_pre) {
+          // the further leaves' slices of this wave's 64 groups, DMA'd into LDS (buffer_load ... lds) before the driving
+          // leaf's loads: both in flight together, no registers held (reads past a column return 0)
+          for (uint32_t x = 0; x < p.num_extra; x++) {
+            const LeafDesc X = ldcf(seg_leaves, p.extra[x]);
+            const bool packed = X.kind == LK_RANGE || X.kind == LK_SET_LDS || X.kind == LK_SET_LUT;
+            if (!packed || X.bits * 64u + 4u > p.stage_words) continue;
+            uint32_t* slice = lds_sets + p.set_lds_ints + ((tid >> 6) * p.num_extra + x) * p.stage_words;
+            const rsrc_t rx = rsrc_of(X.words, X.wbytes);
+            const uint32_t nq = 16u * X.bits + 1u, w0 = (g0 + (tid & ~63u)) * X.bits;
+            for (uint32_t q0 = 0; q0 < nq; q0 += 64u)
+              if (q0 + lane < nq)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(slice + 4u * q0), 16,
+                                                         (w0 + 4u * (q0 + lane)) * 4u, 0, 0, 0);
+          }
+        }
         if (PIPE) {
           uint32_t wn[B + 1];
           if (g + NT < wi.tile_end) load_group<B>(rs, g + NT, wn);
@@ -442,8 +459,9 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? (PG_STREAM_PIPE_EXTRA
           const LeafDesc X = ldcf(seg_leaves, p.extra[x]);
           const bool packed = X.kind == LK_RANGE || X.kind == LK_SET_LDS || X.kind == LK_SET_LUT;
           if (EXTRA && p.stage_words && packed && X.bits * 64u + 4u <= p.stage_words) {
-            uint32_t* slice = lds_sets + p.set_lds_ints + (tid >> 6) * p.stage_words;
-            stage_slice(X, g0 + (tid & ~63u), slice, lane);
+            uint32_t* slice = lds_sets + p.set_lds_ints + (p.stage_pre ? (tid >> 6) * p.num_extra + x : (tid >> 6)) * p.stage_words;
+            if (p.stage_pre) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slice's DMA has landed
+            else stage_slice(X, g0 + (tid & ~63u), slice, lane);
             if (m) m &= eval_staged(X, lds_sets, slice, lane, m);
           } else if (m) {
             m &= eval_extra(X, lds_sets, (uint32_t)d0, m);

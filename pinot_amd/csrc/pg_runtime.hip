@@ -2590,6 +2590,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     std::vector<uint32_t> exact_nwords;  // [seg] LUT words
     uint32_t set_ints = 0;        // LDS IN-set words of the streamed leaves
     std::vector<uint32_t> extra;  // further AND children tested in the stream (runtime bit width)
+    double drive_pass = 1.0;      // the driving leaf's estimated pass fraction
     bool extra_lds_free = false;  // the further children need no LDS (allowed beside the exact mode's LUT)
     std::vector<StreamLaunch> launches;
     // overlapped list scan: launches [0, split_launch) stream the items [0, split) (the first half of the segments);
@@ -2609,6 +2610,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       // the others tested on its survivors (doc ranges, constants, packed columns incl. 1-bit doc bitmaps)
       li = q.ops[1];
       pass = leaf_pass[li];
+      sp.drive_pass = pass;
       for (uint32_t i = 2; i + 1 < q.num_ops && pass > 1.0 / 64 && sp.extra.size() < (size_t)kMaxStreamExtra; i++) {
         const int32_t lx = q.ops[i];
         if (lx < 0) break;
@@ -3317,6 +3319,14 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
             bmax = std::max(bmax, dl.bits);
         }
       if (bmax && !sp.exact && !(stg_env && atoi(stg_env) == 0)) ss.stage_words = 64u * bmax + 4u;
+      // the slices DMA'd a round ahead when the driving leaf passes >= 1/16: PG_STREAM_STAGE_PRE=1 enables it (read per
+      // call, tests switch it).  Off by default: measured slower on config 3 (stream 0.602 -> 0.636 ms, r05: the
+      // driving leaf's loads queue behind the slices' DMA in the wave's in-order vmcnt, so every group test waits
+      // for both)
+      const char* pre_env = getenv("PG_STREAM_STAGE_PRE");
+      if (ss.stage_words && sp.drive_pass >= 1.0 / 16 && pre_env && atoi(pre_env) == 1 &&
+          4ull * (ss.set_lds_ints + 4ull * ss.stage_words * ss.num_extra) + 16 <= 48 * 1024)
+        ss.stage_pre = 1;  // (within 48 KiB of LDS per block: the 256-thread blocks stay several per CU)
     }
     ss.segs = q.segs;
     ss.items = q.items;

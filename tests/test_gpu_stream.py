@@ -175,3 +175,19 @@ def test_stream_in_list_coarse_bitmap(k, wide_table, gpu_engine, oracle_engine):
         assert_same_result(g, oracle_engine.execute(wide_table, q), table=wide_table)
         n = gpu_engine.execute(wide_table, q, flags=abi.PG_PLAN_VALUE_SETS | abi.PG_PLAN_NO_STREAM)
         assert_same_result(g, n, table=wide_table)
+
+
+@pytest.mark.parametrize("pre", ["0", "1"])
+def test_stream_further_leaves_slice_prefetch(pre, table, monkeypatch, gpu_engine, oracle_engine):
+    """Config 3's shape: a wide range drives the stream (28 % pass) and the AND's further packed leaves are tested on
+    its survivors from per-wave LDS slices; PG_STREAM_STAGE_PRE=1 DMAs every further leaf's slice at the start of each
+    group round instead of after the driving test (off by default).  Same answers as the oracle either way."""
+    monkeypatch.setenv("PG_STREAM_STAGE_PRE", pre)
+    for sql in ["SELECT SUM(clicks * imps), COUNT(*) FROM t WHERE day BETWEEN 18000 AND 18100 "
+                "AND clicks BETWEEN 1 AND 30 AND acct < 100000",
+                "SELECT tag, SUM(imps) FROM t WHERE day BETWEEN 18100 AND 18250 AND clicks < 20 AND NOT tag = 't3' "
+                "GROUP BY tag ORDER BY tag LIMIT 100"]:
+        q = parse(sql)
+        g = gpu_engine.execute(table, q)
+        assert gpu_engine.last_timing().scan_launches == 2, "the selective stream did not run"
+        assert_same_result(g, oracle_engine.execute(table, q), table=table)
