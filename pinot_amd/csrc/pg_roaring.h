@@ -23,6 +23,12 @@ namespace pg {
 #ifndef PG_ROAR_Q
 #define PG_ROAR_Q 4
 #endif
+#ifndef PG_ROAR_BIG  // large-array list entries per round, in threads (1 or 2)
+#define PG_ROAR_BIG 2
+#endif
+#ifndef PG_ROAR_OWN  // owner-table windows (8 quads each)
+#define PG_ROAR_OWN 1024
+#endif
 #ifndef PG_ROAR_SB  // 1: a scheduling barrier after each container's ORs (bounds the addresses live at once)
 #define PG_ROAR_SB 1
 #endif
@@ -78,8 +84,9 @@ struct RoarView {
 // LDS scratch of one decode (besides the chunks and the views)
 template <int NT>
 struct RoaringLds {
-  static constexpr uint32_t kBig = 2 * NT;  // large array containers listed per round (more: the finder expands it)
-  static constexpr uint32_t kOwn = 1024;    // 8-quad windows the owner table covers (more quads: a binary search)
+  static constexpr uint32_t kBig = PG_ROAR_BIG * NT;  // large array containers listed per round (more: the finder
+                                                      // expands it)
+  static constexpr uint32_t kOwn = PG_ROAR_OWN;  // 8-quad windows the owner table covers (more: a binary search)
   uint32_t bml[NT];            // bitmap containers of this round (payload offsets), OR-ed by the whole block
   uint8_t bview[NT];           //   and their views (more than NT in a round: the finder ORs it in by itself)
   uint32_t nbml[2];            //   (counters double-buffered by round parity: reset a round ahead, no barrier of their own)
