@@ -691,6 +691,30 @@ def test_fused_index_count_wide_mv_rows(gpu_engine, oracle_engine):
         assert "index_count" in gpu_engine.last_trace()["path"]
 
 
+@pytest.mark.parametrize("neg", [False, True])
+def test_fused_index_count_leaf_referenced_twice(neg, gpu_engine, oracle_engine):
+    """An op program that references one inverted leaf twice (the ABI allows it; a JNI caller may send it): the fused
+    count lets the positive leaves of an OR share one LDS chunk only when each is referenced once, so `a AND (a OR c)`
+    still ANDs a's own docs and `NOT a AND (a OR c)` is `NOT a AND c`.  Built from a plan whose second, identical
+    predicate's leaf is replaced by the first in the ops."""
+    rng = np.random.default_rng(11)
+    n = 60000
+    seg = _seg("twice", {"inv1": rng.integers(0, 10, n), "inv2": rng.integers(0, 100, n)}, {"inv1": "INT", "inv2": "INT"},
+               inverted=["inv1", "inv2"])
+    t = Table("t", [seg])
+    sql = ("SELECT COUNT(*) FROM t WHERE " + ("NOT inv1 = 3" if neg else "inv1 = 3") +
+           " AND (inv1 = 3 OR inv2 IN (1, 5, 9, 50))")
+    want = oracle_engine.execute(t, parse(sql))
+    plan = gpu_engine.make_plan(t, parse(sql))
+    assert list(plan.ops).count(1) == 1 and list(plan.ops).count(0) == 1
+    for i, op in enumerate(plan.ops):
+        if op == 1:
+            plan.plan.ops[i] = 0  # the OR's `inv1 = 3` now names the AND's leaf 0
+    got = gpu_engine.run_plan(plan, image=False)
+    assert "index_count" in gpu_engine.last_trace()["path"]
+    assert got.rows == want.rows
+
+
 def test_config5_full_segment_matches_oracle(gpu_engine, oracle_engine):
     """Config 5 at its stated scale: full 7 812 500-doc segments built on the device in the reference's byte layouts
     (sorted pairs, portable-roaring inverted indexes, FixedBitMVForwardIndexWriter MV column: pinot_amd.synth), the
