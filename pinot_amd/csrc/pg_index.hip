@@ -104,7 +104,7 @@ __global__ __launch_bounds__(kIdxNT, PG_IDX_WAVES) void index_count_kernel(IdxSp
     if (tid == 0) nv = (uint32_t)__popcll(b);
   }
   lds_barrier();
-  if (PG_IDX_PROF && tid == 0) { const unsigned long long n_ = prof_clk(); prof[0] += (n_ - t_) & 0xFFFFFull; t_ = n_; }
+  if (PG_IDX_PROF && tid == 0) { const unsigned long long n_ = prof_clk(); prof[0] += n_ - t_; t_ = n_; }
   roaring_key_chunks<kIdxNT>(V, nv, key, S, chunks, PG_IDX_PROF ? prof : nullptr);
   if (PG_IDX_PROF && tid == 0) t_ = prof_clk();
   if (PG_IDX_LATE_COUNT) load_counts();
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(kIdxNT, PG_IDX_WAVES) void index_count_kernel(IdxSp
       }
     }
   }
-  if (PG_IDX_PROF && tid == 0) { const unsigned long long n_ = prof_clk(); prof[5] += (n_ - t_) & 0xFFFFFull; t_ = n_; }
+  if (PG_IDX_PROF && tid == 0) { const unsigned long long n_ = prof_clk(); prof[5] += n_ - t_; t_ = n_; }
   // block sums -> one atomic per value
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -207,7 +207,7 @@ __global__ __launch_bounds__(kIdxNT, PG_IDX_WAVES) void index_count_kernel(IdxSp
   }
 #if PG_IDX_PROF
   if (tid == 0) {
-    prof[6] += (prof_clk() - t_) & 0xFFFFFull;
+    prof[6] += prof_clk() - t_;
     const unsigned long long w1 = wall_clock64();
     prof[7] = w1 - w0;
     for (int i = 0; i < 8; i++) atomicAdd(&g_idx_prof[i], prof[i]);

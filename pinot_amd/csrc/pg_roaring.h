@@ -52,16 +52,15 @@ static_assert(kRoarR >= 1 && kRoarR <= 16 && kRoarQ >= 1 && kRoarQ <= 32, "roari
 #ifndef PG_IDX_SKIP
 #define PG_IDX_SKIP 0
 #endif
-// the 20-bit SHADER_CYCLES hardware register (s_getreg: no memory-counter wait, unlike clock64's s_memtime, which
-// drains every outstanding LDS op at each lap); laps are taken mod 2^20 cycles
-__device__ __forceinline__ unsigned long long prof_clk() {
-  return (unsigned long long)__builtin_amdgcn_s_getreg(29 | (19 << 11));
-}
+// clock64 (s_memtime).  It perturbs what it measures: its result waits on lgkmcnt, and the lap accumulators live in
+// scratch, whose stores wait on vmcnt -- the laps rank the phases, the absolute times run ~2x long.  (The 20-bit
+// SHADER_CYCLES register would avoid the waits, but reads 0 on these boxes.)
+__device__ __forceinline__ unsigned long long prof_clk() { return (unsigned long long)clock64(); }
 #define ROAR_LAP(ph)                                                              \
   do {                                                                            \
     if (PG_IDX_PROF && prof && threadIdx.x == 0) {                                \
       const unsigned long long n_ = prof_clk();                                    \
-      prof[ph] += (n_ - t_) & 0xFFFFFull;                                         \
+      prof[ph] += n_ - t_;                                                        \
       t_ = n_;                                                                    \
     }                                                                             \
   } while (0)
@@ -114,11 +113,11 @@ __device__ __forceinline__ void roaring_array_or(const uint8_t* src, uint32_t ca
 
 // OR the containers of `key` of every view's selected dictIds into the view's chunk (zeroed by the caller).  The views'
 // dictIds are taken as one list, so a round's lookups span the leaves (config 5: 4 leaves of 1 + 20 + 1 + 2 000 ids
-// decode in one round).  Per round, three dependent global loads and nothing more: the directory entries; then every
-// small array container's two quads (its finder, no LDS hand-off), every large array container's quads (the whole
-// block, kRoarQ per thread at once, owner found by a search over the list's quad prefix) and the first bitmap
-// container, all in flight together; runs are expanded by their finder.  Every bit is set by an LDS atomic, so no
-// barrier orders the kinds.  `V` (nv <= kRoarMaxViews entries) is visible to the whole block; starts and ends with a
+// decode in two rounds of NT * kRoarR).  Per round, three dependent global loads: the dictIds, the directory entries,
+// then every small array container's two quads (its finder, no LDS hand-off), every large array container's quads
+// (the whole block, kRoarQ per thread per step, each quad's owner from the 8-quad-window table) and the first bitmap
+// container's words; runs are expanded by their finder.  Every bit is set by an LDS atomic, so no barrier orders the
+// kinds.  `V` (nv <= kRoarMaxViews entries) is visible to the whole block; starts and ends with a
 // block barrier.  `lds`: the chunks' array, a __shared__ array of the caller (so the ORs compile to LDS atomics).
 template <int NT>
 __device__ __forceinline__ void roaring_key_chunks(const RoarView* V, uint32_t nv, uint32_t key, RoaringLds<NT>& S,
