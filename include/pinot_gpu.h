@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 7
+#define PG_ABI_VERSION 8
 
 typedef enum pg_status {
   PG_OK = 0,
@@ -57,8 +57,23 @@ typedef enum pg_status {
 
 /* ---------------------------------------------------------------- device / library */
 
-/* Bind the calling process to HIP device `device` (one process per GPU).  Idempotent. */
+/* Bind the calling process to HIP device `device` (one process per GPU).  Idempotent.  = pg_init_devices(&device, 1). */
 int pg_init(int device);
+/* Bind the process to n logical devices: logical device i runs on HIP device devices[i] (a device may repeat -- two
+ * logical devices sharing one GPU, e.g. to exercise the multi-device combine on a one-GPU host).  SURVEY §8(b)'s
+ * pg_init(device_mask) as an explicit list.  With n > 1 every segment lives on one logical device (pg_segment_place,
+ * else round-robin at its first upload), and pg_execute* runs a plan's segments on their devices concurrently and
+ * merges the partial states inside the library -- over xGMI peer copies -- as one server's combine does
+ * (BaseCombineOperator.mergeResults, operator/combine/BaseCombineOperator.java:190-233): a JNI caller gets one
+ * merged result for all GPUs of the node from one call.  Idempotent for the same list; PG_E_STATE for another. */
+int pg_init_devices(const int *devices, uint32_t n);
+/* Number of logical devices (pg_init_devices' n). */
+int pg_num_devices(uint32_t *out);
+/* Place a segment on logical device `ldev` before its first pg_column_upload (the segment-to-GPU assignment a server
+ * makes when it loads the segment).  PG_E_STATE if it is already resident elsewhere. */
+int pg_segment_place(uint64_t seg_key, uint32_t ldev);
+/* The logical device a resident segment lives on. */
+int pg_segment_device(uint64_t seg_key, uint32_t *ldev);
 /* Copy the calling thread's last error message (NUL-terminated, truncated to n). Returns its length. */
 int pg_last_error(char *buf, size_t n);
 /* Bytes of device memory held by resident segments. */
@@ -209,14 +224,20 @@ typedef struct pg_agg {
   uint32_t key_cardinality;
   int64_t key_base;
   /* SUM / AVG accumulated exactly in fixed point (every input that is not provably an integer, or all of them with
-   * PG_PLAN_F64_SUMS): e != 0 states 2^e >= |every finite input value| over the whole table (from the columns'
-   * metadata min / max), so every GPU and server that merges this plan's partial states uses the same fixed-point
-   * unit; 0 = derive the bound from the plan's resident segments.  Ignored by the other functions. */
+   * PG_PLAN_F64_SUMS).  With PG_SUM_BOUNDS in sum_flags, 2^sum_exp_lo <= |x| <= 2^sum_exp bounds every nonzero finite
+   * input value over the whole table (from the columns' metadata: largest and smallest nonzero |value|, combined
+   * through the expression), so every GPU and server that merges this plan's partial states cuts the sum into the same
+   * exponent windows (pg_partials.fx_sig); without it the library derives the bounds from the plan's resident
+   * segments.  Ignored by the other functions. */
   int32_t sum_exp;
   uint32_t sum_flags;  /* SUM / AVG: PG_SUM_NONFINITE = some input of the table may be +-inf / NaN (a FLOAT / DOUBLE column
-                          holding them, or a product / sum that overflows), so every GPU keeps the same slots for them */
+                          holding them, or a product / sum that overflows), so every GPU keeps the same slots for them;
+                          PG_SUM_BOUNDS = sum_exp / sum_exp_lo are given */
+  int32_t sum_exp_lo;
+  uint32_t pad;
 } pg_agg;
 #define PG_SUM_NONFINITE 0x1u
+#define PG_SUM_BOUNDS 0x2u
 
 typedef enum pg_key_kind {
   PG_KEY_VALUE_OFFSET = 0,  /* INT/LONG dictionary: global id = value - base                         */
@@ -351,7 +372,8 @@ int pg_result_free(pg_result *res);
 
 /* ---------------------------------------------------------------- partial state (multi-GPU) */
 
-/* Per-group partial state of one plan on this device.  Groups are identified by their packed key: the
+/* Per-group partial state of one plan on this device (with several logical devices: the merged state of all of
+ * them, on the first one that ran a segment of the plan; its pg_partials_* calls run there).  Groups are identified by their packed key: the
  * mixed-radix number of their table-global key ids, first key least significant (key k contributes
  * id_k * prod_{j<k} keys[j].cardinality), as DictionaryBasedGroupKeyGenerator forms raw keys (:280-322)
  * but over table-global ids so that segments, GPUs and servers merge by VALUE.
@@ -361,7 +383,8 @@ int pg_result_free(pg_result *res);
  * State arrays, per slot:
  *   i64 [num_slots][n_i64]      merged by SUM (slot 0: doc count; integer sums, AVG counts, COUNTMV)
  *   fx  [num_slots][n_fx][2]    merged by 128-bit SUM: the exact fixed-point sums of SUM / AVG inputs that are not
- *                               provably integers, (lo, hi) two's-complement words (the low word's carry goes to the
+ *                               provably integers, one (lo, hi) two's-complement pair per exponent window of the
+ *                               aggregation (a SUM spans one or more consecutive pairs; the low word's carry goes to the
  *                               high word: a word-wise SUM all-reduce is NOT a merge -- split the words into limbs)
  *   mn  [num_slots][n_min]      merged by MIN (order-preserving int64 image of double MIN)
  *   mx  [num_slots][n_max]      merged by MAX (order-preserving int64 image of double MAX)

@@ -1,7 +1,7 @@
 """ctypes mirror of include/pinot_gpu.h (the C ABI).  Shared by the GPU binding and the oracle."""
 import ctypes as C
 
-PG_ABI_VERSION = 7
+PG_ABI_VERSION = 8
 
 PG_OK, PG_E_INVALID, PG_E_HIP, PG_E_NOMEM, PG_E_NOTFOUND, PG_E_UNSUPPORTED, PG_E_CANCELLED, PG_E_TIMEOUT, \
     PG_E_STATE = 0, -1, -2, -3, -4, -5, -6, -7, -8
@@ -38,7 +38,7 @@ PG_PLAN_VALUE_SETS, PG_PLAN_HASH_GROUPS, PG_PLAN_F64_SUMS, PG_PLAN_NO_STREAM = 0
 PG_PLAN_EXACT_LIMIT = 0x10
 PG_STATE_DENSE, PG_STATE_HASH, PG_STATE_TUPLES = 0, 1, 2
 PG_RESULT_GROUPS_LIMIT_REACHED, PG_RESULT_TRIM_THRESHOLD_REACHED = 0x1, 0x2
-PG_SUM_NONFINITE = 0x1
+PG_SUM_NONFINITE, PG_SUM_BOUNDS = 0x1, 0x2
 PG_EMPTY_KEY = 0xFFFFFFFFFFFFFFFF
 
 
@@ -59,7 +59,7 @@ class pg_leaf(C.Structure):
 class pg_agg(C.Structure):
     _fields_ = [("fn", C.c_uint32), ("op", C.c_uint32), ("col_a", C.c_uint32), ("col_b", C.c_uint32),
                 ("key_kind", C.c_uint32), ("key_cardinality", C.c_uint32), ("key_base", C.c_int64),
-                ("sum_exp", C.c_int32), ("sum_flags", C.c_uint32)]
+                ("sum_exp", C.c_int32), ("sum_flags", C.c_uint32), ("sum_exp_lo", C.c_int32), ("pad", C.c_uint32)]
 
 
 class pg_key(C.Structure):
@@ -165,7 +165,8 @@ EXPORTED = ["pg_init", "pg_last_error", "pg_resident_bytes", "pg_cancel", "pg_ab
             "pg_segment_release", "pg_execute", "pg_result_free", "pg_execute_partial", "pg_partials_finalize",
             "pg_partials_free", "pg_partials_copy", "pg_partials_export", "pg_partials_create", "pg_partials_merge",
             "pg_key_owner", "pg_last_timing", "pg_chunk_decompress", "pg_dict_id_sets", "pg_execute_image",
-            "pg_execute_partial_image", "pg_partials_finalize_image", "pg_last_trace"]
+            "pg_execute_partial_image", "pg_partials_finalize_image", "pg_last_trace", "pg_init_devices",
+            "pg_num_devices", "pg_segment_place", "pg_segment_device"]
 PG_CODEC_PASS_THROUGH, PG_CODEC_SNAPPY, PG_CODEC_ZSTANDARD, PG_CODEC_LZ4, PG_CODEC_LZ4_LENGTH_PREFIXED = 0, 1, 2, 3, 4
 PG_COPY_OUT, PG_COPY_IN = 0, 1
 
@@ -175,6 +176,10 @@ def declare(lib):
     P = C.POINTER
     sigs = {
         "pg_init": ([C.c_int], C.c_int),
+        "pg_init_devices": ([P(C.c_int), C.c_uint32], C.c_int),
+        "pg_num_devices": ([P(C.c_uint32)], C.c_int),
+        "pg_segment_place": ([C.c_uint64, C.c_uint32], C.c_int),
+        "pg_segment_device": ([C.c_uint64, P(C.c_uint32)], C.c_int),
         "pg_last_error": ([C.c_char_p, C.c_size_t], C.c_int),
         "pg_resident_bytes": ([P(C.c_uint64)], C.c_int),
         "pg_cancel": ([C.c_uint64], C.c_int),

@@ -127,11 +127,15 @@ struct IdxSpec {
   uint32_t cntmv_slot;              // i64 slot of COUNTMV (~0: none)
   const IdxSeg* segs;
   const IdxLeaf* leaves;            // [num_segs][num_leaves]
-  const uint32_t* blk_seg;          // block -> its segment
+  const uint32_t* blk_seg;          // unit -> its segment (a unit: one (segment, 64 K-doc key))
   unsigned long long* i64;          // slot 0: doc count
   unsigned long long* seg_matched;  // [num_segs]
+  unsigned int* next_unit;          // persistent grid: the units' claim counter (zero before the launch)
+  uint32_t num_units, pad;
 };
-hipError_t launch_index_count(const IdxSpec& p, uint32_t blocks, hipStream_t s);
+// A persistent grid of at most the resident block slots; each block claims (segment, key) units from next_unit until
+// none is left (the last round of a one-block-per-unit grid was half empty: 1 568 units over 1 024 slots)
+hipError_t launch_index_count(const IdxSpec& p, uint32_t units, hipStream_t s);
 // COUNTMV's count column of an MV forward index: 4 bits per doc (min(count, 15)); *over set when a count exceeds 15
 hipError_t launch_mv_counts(const uint32_t* offsets, uint32_t num_docs, uint32_t* out, unsigned int* over, hipStream_t s);
 hipError_t launch_mv_scan(const uint32_t* words, uint32_t bits, const uint32_t* offsets, uint32_t num_docs,
@@ -395,6 +399,9 @@ hipError_t launch_set_extract(const StateView& v, const FinalSpec& f, const uint
 hipError_t launch_gather_rows(const StateView& v, const uint32_t* slots, uint64_t n, uint64_t key_div, uint8_t* dst,
                               hipStream_t s);
 hipError_t launch_merge_rows(const StateView& v, const uint8_t* rows, uint64_t n, hipStream_t s);
+// Element-wise merge of two dense states of one layout (in-library multi-device combine, pg_init_devices): i64 += ,
+// fx 128-bit += , mn min, mx max, bits |= (AggregationFunction.merge of each function; src arrays on this device)
+hipError_t launch_merge_dense(const StateView& dst, const StateView& src, hipStream_t s);
 // SK_FX pairs <-> 4 x 32-bit limbs per pair (in: fold the limbs' carries back into the pairs)
 hipError_t launch_fx_limbs(unsigned long long* pairs, long long* limbs, uint64_t n, bool in, hipStream_t s);
 hipError_t launch_init_view(const StateView& v, hipStream_t s, FillSpans* defer = nullptr);  // pg_kernels.hip: zero / empty / +-inf state

@@ -188,7 +188,7 @@ __device__ __forceinline__ double fx_value(const StateView& v, const AggSpec& A,
   const unsigned long long* p = v.fx + (s * v.n_fx + A.slot) * 2;
   const int64_t smn = A.sp_min != kNoSp ? (int64_t)v.mn[s * v.n_min + A.sp_min] : 0;
   const int64_t smx = A.sp_max != kNoSp ? (int64_t)v.mx[s * v.n_max + A.sp_max] : 0;
-  return fx_final(A, p[0], p[1], smn, smx);
+  return fx_final(A, (const uint64_t*)p, smn, smx);
 }
 
 // Final value of every aggregation of the groups at `slots` (AggregationFunction.extractFinalResult; AVG keeps
@@ -688,6 +688,35 @@ hipError_t launch_merge_rows(const StateView& v, const uint8_t* rows, uint64_t n
   const uint64_t blocks = (n + 255) / 256;
   hipLaunchKernelGGL(merge_rows_kernel, dim3((uint32_t)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, s, v, rows,
                      n, row_bytes(v));
+  return hipGetLastError();
+}
+
+// Dense merge: every array element-wise, one thread per (slot, word) of each array -- no atomics (each element has
+// one owner), coalesced reads of both states.  fx pairs: one thread per pair, carry from the low word to the high word.
+__global__ void merge_dense_kernel(StateView d, StateView s) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x, t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t G = d.num_slots;
+  for (uint64_t i = t0; i < G * d.n_i64; i += stride) d.i64[i] += s.i64[i];
+  for (uint64_t i = t0; i < G * d.n_fx; i += stride) {
+    const uint64_t lo = d.fx[2 * i] + s.fx[2 * i];
+    d.fx[2 * i + 1] += s.fx[2 * i + 1] + (lo < (uint64_t)s.fx[2 * i] ? 1ull : 0ull);
+    d.fx[2 * i] = lo;
+  }
+  for (uint64_t i = t0; i < G * d.n_min; i += stride) d.mn[i] = s.mn[i] < d.mn[i] ? s.mn[i] : d.mn[i];
+  for (uint64_t i = t0; i < G * d.n_max; i += stride) d.mx[i] = s.mx[i] > d.mx[i] ? s.mx[i] : d.mx[i];
+  const uint64_t nb = G * d.bit_words;
+  const uint64_t nb4 = (d.bits && s.bits && ((uintptr_t)d.bits % 16 == 0) && ((uintptr_t)s.bits % 16 == 0)) ? nb / 4 : 0;
+  for (uint64_t i = t0; i < nb4; i += stride) {  // 16-byte words for the bitmaps (config 4: 1.28 GB of them)
+    uint4 a = ((uint4*)d.bits)[i];
+    const uint4 b = ((const uint4*)s.bits)[i];
+    a.x |= b.x; a.y |= b.y; a.z |= b.z; a.w |= b.w;
+    ((uint4*)d.bits)[i] = a;
+  }
+  for (uint64_t i = 4 * nb4 + t0; i < nb; i += stride) d.bits[i] |= s.bits[i];
+}
+
+hipError_t launch_merge_dense(const StateView& dst, const StateView& src, hipStream_t s) {
+  hipLaunchKernelGGL(merge_dense_kernel, dim3(4096), dim3(256), 0, s, dst, src);
   return hipGetLastError();
 }
 

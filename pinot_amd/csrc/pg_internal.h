@@ -186,10 +186,12 @@ struct AggSpec {
   uint32_t key_card;  // DISTINCTCOUNT: size of the table-global value id space (bits of its bitmap)
   int64_t key_base;
   uint32_t dc_word;   // DISTINCTCOUNT: first uint32 word of this aggregation's bitmap within a slot's row
-  int32_t fx_shift;   // SK_FX: the fixed-point unit is 2^fx_shift
+  int32_t fx_shift;   // SK_FX: the unit of window 0 is 2^fx_shift (fx_split)
   // SK_FX over a column that may hold +-inf / NaN: mn / mx slots that receive the order images of the non-finite
   // inputs (the fixed-point sum skips them), so that finalisation gives IEEE's sum of them (fx_final); else kNoSp
   uint32_t sp_min, sp_max;
+  uint32_t fx_nwin;   // SK_FX: exponent windows = consecutive fx slots slot .. slot + fx_nwin - 1 (fx_split)
+  uint32_t pad_;
 };
 constexpr uint32_t kNoSp = 0xFFFFFFFFu;
 
@@ -272,16 +274,25 @@ __host__ __device__ inline double order_key_decode(int64_t k) {
 }
 
 // ---- exact fixed-point sums (SK_FX)
-// The unit 2^fx_shift is chosen by the host from a bound 2^e >= |every input| of the plan: fx_shift = e + 40 - 126, so a
-// single input needs at most 87 bits and 2^40 inputs sum within 127 bits (no overflow for any table this library can
-// hold).  Inputs of magnitude >= 2^(e - 34) convert exactly; smaller ones round to the nearest unit (2^-86 of the bound:
-// far below a double sum's own rounding error).
-constexpr int kFxSumBits = 126;
-constexpr int kFxCountBits = 40;
-__host__ __device__ inline int32_t fx_shift_for(int32_t bound_exp) { return bound_exp + kFxCountBits - kFxSumBits; }
+// Every finite input is converted EXACTLY: a double is m * 2^q (m < 2^53 an integer, q = its last mantissa bit's
+// exponent), and the host bounds every nonzero finite input of the plan by 2^klo <= |x| <= 2^khi (the columns'
+// smallest nonzero and largest |value|, combined through the expression), so q lies in [u0, qmax] with
+// u0 = max(klo - 52, -1074) and qmax = khi - 52.  That exponent range is cut into windows of kFxWinBits exponents:
+// window w holds the inputs with q - u0 in [32w, 32w + 32), as the 128-bit two's-complement integer x / 2^(u0 + 32w) =
+// m * 2^(q - u0 - 32w) < 2^85, so 2^40 inputs sum within 126 bits (no overflow for any table this library can hold).
+// Each window is one fx slot (consecutive slots of the aggregation); integer adds are associative, and the final value
+// is the windows' exact total rounded once to the nearest double (fx_windows_to_double): the correctly rounded sum of
+// the inputs, for any range of magnitudes (64 windows cover every finite double) and in every order.
+constexpr int kFxWinBits = 32;
+constexpr int kFxMaxWin = 64;
+__host__ __device__ inline int32_t fx_u0(int32_t klo) { return klo - 52 < -1074 ? -1074 : klo - 52; }
+__host__ __device__ inline uint32_t fx_num_windows(int32_t klo, int32_t khi) {
+  const int32_t u0 = fx_u0(klo), qmax = khi - 52;
+  return qmax <= u0 ? 1u : (uint32_t)((qmax - u0) / kFxWinBits + 1);
+}
 
 // x / 2^shift rounded to nearest (ties to even) as a 128-bit two's-complement integer; 0 for +-inf / NaN (those are
-// tracked apart, AggSpec::sp_min / sp_max)
+// tracked apart, AggSpec::sp_min / sp_max).  Exact whenever x's last mantissa bit is at or above 2^shift.
 __host__ __device__ inline void fx_from_double(double x, int32_t shift, uint64_t& lo, uint64_t& hi) {
   uint64_t b;
   __builtin_memcpy(&b, &x, 8);
@@ -309,6 +320,24 @@ __host__ __device__ inline void fx_from_double(double x, int32_t shift, uint64_t
     lo = ~lo + 1;
     hi = ~hi + (lo == 0 ? 1 : 0);
   }
+}
+
+// The window of a finite input x (see above) and its exact value in that window's unit 2^(u0 + 32 w).  Zero, +-inf and
+// NaN give (0, 0) in window 0.  An input outside the host's bounds (never for a validated plan) lands in the nearest
+// window, rounded below it or shifted further above it.
+__host__ __device__ inline uint32_t fx_split(double x, int32_t u0, uint32_t nwin, uint64_t& lo, uint64_t& hi) {
+  uint64_t b;
+  __builtin_memcpy(&b, &x, 8);
+  const int e = (int)((b >> 52) & 0x7FF);
+  const int d = (e ? e : 1) - 1075 - u0;  // q - u0
+  if (e == 0x7FF || d < 0) {
+    fx_from_double(x, u0, lo, hi);
+    return 0;
+  }
+  uint32_t w = (uint32_t)d / kFxWinBits;
+  if (w >= nwin) w = nwin - 1;
+  fx_from_double(x, u0 + kFxWinBits * (int32_t)w, lo, hi);  // exact: x's last bit is at or above the window's unit
+  return w;
 }
 
 // (lo, hi) * 2^shift as the nearest double (ties to even; exact integer rounding of the 128-bit value, then one exact
@@ -347,10 +376,69 @@ __host__ __device__ inline void fx_add(uint64_t& lo, uint64_t& hi, uint64_t blo,
   lo = t;
 }
 
-// The final SUM of an SK_FX aggregation: the fixed-point sum of the finite inputs, unless non-finite inputs were seen
-// (their order images in the sp_min / sp_max slots): IEEE 754 addition gives NaN for any NaN or for +inf with -inf,
-// else the infinity -- whatever the order, so the special cases stay exact too.
-__host__ __device__ inline double fx_final(const AggSpec& A, uint64_t lo, uint64_t hi, int64_t sp_mn, int64_t sp_mx) {
+// The exact total of nwin windows (p[2w], p[2w + 1] = window w's 128-bit sum in units of 2^(u0 + 32 w)) rounded once
+// to the nearest double (ties to even): the windows are added into one two's-complement integer of up to 35 64-bit
+// limbs in units of 2^u0, whose top 53 significant bits (rounded with the bits below) are the result.
+constexpr int kFxLimbs = (kFxWinBits * (kFxMaxWin - 1) + 128) / 64 + 2;
+__host__ __device__ inline double fx_windows_to_double(const uint64_t* p, uint32_t nwin, int32_t u0) {
+  if (nwin <= 1) return fx_to_double(p[0], p[1], u0);
+  if (nwin > (uint32_t)kFxMaxWin) nwin = kFxMaxWin;
+  uint64_t L[kFxLimbs];
+  const int n = (kFxWinBits * ((int)nwin - 1) + 128) / 64 + 2;
+  for (int i = 0; i < n; i++) L[i] = 0;
+  for (uint32_t w = 0; w < nwin; w++) {
+    const uint64_t lo = p[2 * w], hi = p[2 * w + 1];
+    if (!lo && !hi) continue;
+    const uint64_t sgn = (int64_t)hi < 0 ? ~0ull : 0ull;
+    const int bit = kFxWinBits * (int)w, k = bit / 64, s = bit % 64;  // s is 0 or 32
+    uint64_t x[3];
+    if (s) {
+      x[0] = lo << s;
+      x[1] = (hi << s) | (lo >> (64 - s));
+      x[2] = (uint64_t)((int64_t)hi >> (64 - s));
+    } else {
+      x[0] = lo; x[1] = hi; x[2] = sgn;
+    }
+    uint64_t c = 0;
+    for (int i = k; i < n; i++) {
+      const uint64_t a = i - k < 3 ? x[i - k] : sgn;
+      const uint64_t t = L[i] + a, c1 = t < a, t2 = t + c, c2 = t2 < c;
+      L[i] = t2;
+      c = c1 | c2;
+    }
+  }
+  const bool neg = (int64_t)L[n - 1] < 0;
+  if (neg) {
+    uint64_t c = 1;
+    for (int i = 0; i < n; i++) { const uint64_t t = ~L[i] + c; c = (c && t == 0) ? 1 : 0; L[i] = t; }
+  }
+  int top = n - 1;
+  while (top >= 0 && !L[top]) top--;
+  if (top < 0) return 0.0;
+  const int nb = 64 * top + 64 - __builtin_clzll(L[top]);  // significant bits
+  auto bit_at = [&](int i) -> uint64_t { return (L[i / 64] >> (i % 64)) & 1ull; };
+  uint64_t mant = 0;
+  int exp2 = 0;
+  if (nb <= 53) {
+    mant = L[0];
+  } else {
+    const int r = nb - 53;
+    for (int i = 0; i < 53; i++) mant |= bit_at(r + i) << i;
+    const uint64_t round = bit_at(r - 1);
+    bool sticky = false;
+    for (int i = 0; i < (r - 1) / 64 && !sticky; i++) sticky = L[i] != 0;
+    if (!sticky && (r - 1) % 64) sticky = (L[(r - 1) / 64] & ((1ull << ((r - 1) % 64)) - 1)) != 0;
+    if (round && (sticky || (mant & 1))) mant++;
+    exp2 = r;
+  }
+  const double d = __builtin_ldexp((double)mant, exp2 + u0);
+  return neg ? -d : d;
+}
+
+// The final SUM of an SK_FX aggregation from its windows p (fx slots A.slot ..): the exact sum of the finite inputs,
+// unless non-finite inputs were seen (their order images in the sp_min / sp_max slots): IEEE 754 addition gives NaN
+// for any NaN or for +inf with -inf, else the infinity -- whatever the order, so the special cases stay exact too.
+__host__ __device__ inline double fx_final(const AggSpec& A, const uint64_t* p, int64_t sp_mn, int64_t sp_mx) {
   if (A.sp_min != kNoSp) {
     const int64_t kpinf = order_key(__builtin_inf()), kninf = order_key(-__builtin_inf());
     const bool nan = sp_mx > kpinf || sp_mn < kninf, pinf = sp_mx == kpinf, ninf = sp_mn == kninf;
@@ -358,7 +446,7 @@ __host__ __device__ inline double fx_final(const AggSpec& A, uint64_t lo, uint64
     if (pinf) return __builtin_inf();
     if (ninf) return -__builtin_inf();
   }
-  return fx_to_double(lo, hi, A.fx_shift);
+  return fx_windows_to_double(p, A.fx_nwin, A.fx_shift);
 }
 
 

@@ -18,6 +18,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <future>
 #include <cfloat>
 #include <cmath>
 #include <cstdarg>
@@ -28,6 +32,7 @@
 #include <mutex>
 #include <shared_mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -43,8 +48,16 @@ namespace {
 thread_local std::string t_err;
 thread_local pg_timing t_timing{};
 thread_local pg_trace t_trace{};  // pg_last_trace: the calling thread's last device call (pinot_trace.h)
-int g_device = -1;
+int g_device = -1;                // HIP device of logical device 0 (pg_init / pg_init_devices)
 std::mutex g_init_mu;
+// Logical devices (pg_init_devices): logical device i runs on HIP device g_ldev_phys[i]; a device may repeat (two
+// logical devices sharing one GPU, each with its own worker thread and stream).  One entry for pg_init.
+constexpr int kMaxPhys = 64;
+std::vector<int> g_ldev_phys;
+thread_local int t_ldev = 0;      // the logical device this thread works for (a worker's own; 0 for caller threads)
+int cur_phys() {                  // the HIP device this thread's device work goes to
+  return g_ldev_phys.empty() ? std::max(g_device, 0) : g_ldev_phys[(size_t)t_ldev < g_ldev_phys.size() ? t_ldev : 0];
+}
 
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int fail(int code, const char* fmt, ...) {
@@ -66,9 +79,10 @@ int fail(int code, const char* fmt, ...) {
 
 int ensure_device() {
   if (g_device < 0) return fail(PG_E_STATE, "pg_init has not been called");
+  const int dev = cur_phys();
   int cur = -1;
-  if (hipGetDevice(&cur) != hipSuccess || cur != g_device) {
-    if (hipSetDevice(g_device) != hipSuccess) return fail(PG_E_HIP, "hipSetDevice(%d) failed", g_device);
+  if (hipGetDevice(&cur) != hipSuccess || cur != dev) {
+    if (hipSetDevice(dev) != hipSuccess) return fail(PG_E_HIP, "hipSetDevice(%d) failed", dev);
   }
   return PG_OK;
 }
@@ -147,7 +161,7 @@ class DevicePool {
   std::mutex mu_;
   std::unordered_map<uint64_t, std::vector<void*>> free_;
 };
-DevicePool g_pool;
+DevicePool g_pools[kMaxPhys];  // one per HIP device: a block is only ever reused on the device it was allocated on
 
 // Device buffer: resident index buffers own a hipMalloc allocation; per-query buffers borrow a pool block.
 struct DevBuf {
@@ -155,6 +169,7 @@ struct DevBuf {
   uint64_t bytes = 0;
   uint64_t cap = 0;
   bool pooled = false;
+  int pdev = 0;  // pooled: the HIP device (pool) the block came from
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
@@ -162,7 +177,7 @@ struct DevBuf {
   DevBuf& operator=(DevBuf&& o) noexcept {
     if (this != &o) {
       reset();
-      p = o.p; bytes = o.bytes; cap = o.cap; pooled = o.pooled;
+      p = o.p; bytes = o.bytes; cap = o.cap; pooled = o.pooled; pdev = o.pdev;
       o.p = nullptr; o.bytes = 0; o.cap = 0;
     }
     return *this;
@@ -170,7 +185,7 @@ struct DevBuf {
   ~DevBuf() { reset(); }
   void reset() {
     if (p) {
-      if (pooled) g_pool.put(p, cap);
+      if (pooled) g_pools[pdev].put(p, cap);
       else (void)hipFree(p);
     }
     p = nullptr;
@@ -191,7 +206,8 @@ struct DevBuf {
     reset();
     if (n == 0) n = 16;
     pooled = true;
-    p = g_pool.get(n, &cap);
+    pdev = cur_phys();
+    p = g_pools[pdev].get(n, &cap);
     if (!p) return fail(PG_E_NOMEM, "device allocation of %llu bytes failed", (unsigned long long)n);
     bytes = n;
     return PG_OK;
@@ -269,7 +285,8 @@ struct ColumnRes {
   DevBuf dict;
   double dmin = 0, dmax = 0;  // dictionary min / max value (as double; integers exact below 2^53)
   int64_t imin = 0, imax = 0;
-  double fin_abs = 0;         // largest |value| among the finite values (the SK_FX unit's bound)
+  double fin_abs = 0;         // largest |value| among the finite values (the SK_FX windows' upper bound)
+  double fin_min = 0;         // smallest nonzero |value| among the finite values, 0 = none (their lower bound)
   bool nonfinite = false;     // some value is +-inf or NaN (FLOAT / DOUBLE)
   // forward index
   uint32_t fwd = FWD_NONE;
@@ -335,6 +352,7 @@ int build_decoded(ColumnRes& c, hipStream_t s) {
 
 struct SegmentRes {
   std::unordered_map<uint32_t, ColumnRes> cols;
+  uint32_t ldev = 0;  // the logical device holding it (pg_init_devices / pg_segment_place)
 };
 
 std::shared_mutex g_seg_mu;
@@ -385,7 +403,7 @@ struct CancelSlot {
 int init_cancel_flags() {  // under g_init_mu
   if (g_flags) return PG_OK;
   void* p = nullptr;
-  HIP_CHECK(hipHostMalloc(&p, kCancelSlots * 4, hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_CHECK(hipHostMalloc(&p, kCancelSlots * 4, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
   memset(p, 0, kCancelSlots * 4);
   std::lock_guard<std::mutex> g(g_cancel_mu);
   for (uint32_t i = 0; i < kCancelSlots; i++) g_free_slots.push_back(kCancelSlots - 1 - i);
@@ -601,15 +619,20 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
         tmp.dmax = be_value_as_double(hi.data(), d->data_type);
         tmp.imin = be_value_as_i64(lo.data(), d->data_type);
         tmp.imax = be_value_as_i64(hi.data(), d->data_type);
-        if (std::isfinite(tmp.dmin) && std::isfinite(tmp.dmax)) {
+        if (std::isfinite(tmp.dmin) && std::isfinite(tmp.dmax) && d->data_type <= PG_LONG) {
           tmp.fin_abs = std::max(fabs(tmp.dmin), fabs(tmp.dmax));
-        } else {  // a FLOAT / DOUBLE dictionary with +-inf / NaN (sorted as Double.compare: NaN last): scan it once
+          tmp.fin_min = tmp.fin_abs > 0 ? 1.0 : 0.0;  // a nonzero integer is at least 1
+        } else {  // FLOAT / DOUBLE: the smallest nonzero |value| sits anywhere; +-inf / NaN sort to the ends: scan once
           std::vector<uint8_t> all;
           if ((rc = host_copy(src, (uint64_t)w * d->cardinality, on_dev, all))) return rc;
           for (uint32_t i = 0; i < d->cardinality; i++) {
             const double v = be_value_as_double(&all[(uint64_t)i * w], d->data_type);
-            if (std::isfinite(v)) tmp.fin_abs = std::max(tmp.fin_abs, fabs(v));
-            else tmp.nonfinite = true;
+            if (std::isfinite(v)) {
+              tmp.fin_abs = std::max(tmp.fin_abs, fabs(v));
+              if (v != 0 && (tmp.fin_min == 0 || fabs(v) < tmp.fin_min)) tmp.fin_min = fabs(v);
+            } else {
+              tmp.nonfinite = true;
+            }
           }
         }
       }
@@ -746,8 +769,12 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
         const double v = be_value_as_double(&be[(uint64_t)i * w], d->data_type);
         tmp.dmin = std::min(tmp.dmin, v);
         tmp.dmax = std::max(tmp.dmax, v);
-        if (std::isfinite(v)) tmp.fin_abs = std::max(tmp.fin_abs, fabs(v));
-        else tmp.nonfinite = true;
+        if (std::isfinite(v)) {
+          tmp.fin_abs = std::max(tmp.fin_abs, fabs(v));
+          if (v != 0 && (tmp.fin_min == 0 || fabs(v) < tmp.fin_min)) tmp.fin_min = fabs(v);
+        } else {
+          tmp.nonfinite = true;
+        }
         if (d->data_type <= PG_LONG) {
           const int64_t x = be_value_as_i64(&be[(uint64_t)i * w], d->data_type);
           tmp.imin = std::min(tmp.imin, x);
@@ -799,7 +826,10 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
 
   std::unique_lock<std::shared_mutex> lk(g_seg_mu);
   SegmentRes*& seg = g_segs[seg_key];
-  if (!seg) seg = new SegmentRes();
+  if (!seg) {
+    seg = new SegmentRes();
+    seg->ldev = (uint32_t)t_ldev;
+  }
   ColumnRes& c = seg->cols[col_id];
   switch (d->kind) {
     case PG_IDX_DICT:
@@ -807,7 +837,7 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
       c.has_dict = true; c.dtype = tmp.dtype; c.card = tmp.card; c.entry_bytes = tmp.entry_bytes;
       c.dict = std::move(tmp.dict);
       c.dmin = tmp.dmin; c.dmax = tmp.dmax; c.imin = tmp.imin; c.imax = tmp.imax;
-      c.fin_abs = tmp.fin_abs; c.nonfinite = tmp.nonfinite;
+      c.fin_abs = tmp.fin_abs; c.fin_min = tmp.fin_min; c.nonfinite = tmp.nonfinite;
       break;
     case PG_IDX_FWD_SV_BITPACKED: case PG_IDX_FWD_SV_SORTED: case PG_IDX_FWD_MV_BITPACKED:
       c.words.reset(); c.mv_offsets.reset(); c.mv_cnt.reset();
@@ -861,7 +891,7 @@ int upload_column(uint64_t seg_key, uint32_t col_id, const pg_col_desc* d, const
       c.fwd = FWD_RAW; c.num_docs = tmp.num_docs; c.bits = 0; c.num_values = tmp.num_values;
       c.dtype = tmp.dtype; c.card = tmp.card; c.has_dict = false;
       c.dmin = tmp.dmin; c.dmax = tmp.dmax; c.imin = tmp.imin; c.imax = tmp.imax;
-      c.fin_abs = tmp.fin_abs; c.nonfinite = tmp.nonfinite;
+      c.fin_abs = tmp.fin_abs; c.fin_min = tmp.fin_min; c.nonfinite = tmp.nonfinite;
       c.rawv = std::move(tmp.rawv);
       break;
   }
@@ -906,7 +936,9 @@ struct Partials {
   uint32_t fx_sig() const {
     uint64_t h = 0x9E3779B97F4A7C15ull;
     for (const AggSpec& a : aggs)
-      if (a.kind == SK_FX) h = mix64(h ^ ((uint64_t)(uint32_t)a.fx_shift << 32) ^ (a.sp_min != kNoSp ? 1u : 0u) ^ ((uint64_t)a.slot << 8));
+      if (a.kind == SK_FX)
+        h = mix64(h ^ ((uint64_t)(uint32_t)a.fx_shift << 32) ^ (a.sp_min != kNoSp ? 1u : 0u) ^ ((uint64_t)a.slot << 8) ^
+                  ((uint64_t)a.fx_nwin << 20));
     return (uint32_t)(h >> 33);  // 31 bits: a non-negative int64 in the ranks' fingerprint all-reduce
   }
 
@@ -937,9 +969,9 @@ struct Partials {
 // Layout of the state arrays of a plan's aggregations (slot assignment, DISTINCTCOUNT bitmap words).  `integer`
 // bit a: SUM / AVG a accumulates integer-exact in i64, else exactly as SK_FX in units of 2^fx_shift[a], with special
 // slots for non-finite inputs when bit a of `special` is set.
-int agg_layout(const pg_plan* plan, uint32_t integer, const std::vector<int32_t>& fx_shift, uint32_t special,
-               std::vector<AggSpec>& aggs, uint32_t& n_i64, uint32_t& n_fx, uint32_t& n_min, uint32_t& n_max,
-               uint32_t& bit_words);
+int agg_layout(const pg_plan* plan, uint32_t integer, const std::vector<int32_t>& fx_shift,
+               const std::vector<uint32_t>& fx_nwin, uint32_t special, std::vector<AggSpec>& aggs, uint32_t& n_i64,
+               uint32_t& n_fx, uint32_t& n_min, uint32_t& n_max, uint32_t& bit_words);
 
 // Pinot's default numGroupsLimit (InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT)
 constexpr uint64_t kDefaultNumGroupsLimit = 100000;
@@ -1159,9 +1191,9 @@ uint64_t scan_grid_cap(bool grouped, bool one_round = false) {
   return g_grid_caps[(grouped ? 1 : 0) + (one_round ? 2 : 0)];
 }
 
-int agg_layout(const pg_plan* plan, uint32_t integer, const std::vector<int32_t>& fx_shift, uint32_t special,
-               std::vector<AggSpec>& aggs, uint32_t& n_i64, uint32_t& n_fx, uint32_t& n_min, uint32_t& n_max,
-               uint32_t& bit_words) {
+int agg_layout(const pg_plan* plan, uint32_t integer, const std::vector<int32_t>& fx_shift,
+               const std::vector<uint32_t>& fx_nwin, uint32_t special, std::vector<AggSpec>& aggs, uint32_t& n_i64,
+               uint32_t& n_fx, uint32_t& n_min, uint32_t& n_max, uint32_t& bit_words) {
   n_i64 = 1;  // slot 0: doc count (COUNT, AVG count, group presence)
   n_fx = n_min = n_max = bit_words = 0;
   aggs.assign(plan->num_aggs, AggSpec{});
@@ -1184,8 +1216,10 @@ int agg_layout(const pg_plan* plan, uint32_t integer, const std::vector<int32_t>
           s2.slot = n_i64++;
         } else {
           s2.kind = SK_FX;
-          s2.slot = n_fx++;
-          s2.fx_shift = a < fx_shift.size() ? fx_shift[a] : fx_shift_for(1024);
+          s2.slot = n_fx;
+          s2.fx_shift = a < fx_shift.size() ? fx_shift[a] : fx_u0(-1074);
+          s2.fx_nwin = a < fx_nwin.size() ? std::max(1u, std::min(fx_nwin[a], (uint32_t)kFxMaxWin)) : (uint32_t)kFxMaxWin;
+          n_fx += s2.fx_nwin;
           if ((special >> a) & 1u) { s2.sp_min = n_min++; s2.sp_max = n_max++; }
         }
         s2.cnt_slot = 0;
@@ -1469,6 +1503,71 @@ uint32_t leaf_form(const pg_leaf& pl, const LeafDesc& dl) {
   }
 }
 
+// ---- SUM / AVG accumulation layout from the columns' value bounds (compile_and_run, and the multi-device layout that
+// makes every logical device's partial state agree, global_layout)
+struct SumBounds {
+  double bound_a = 0, bound_b = 0, fin_a = 0, fin_b = 0;  // |value| bounds: all values / the finite ones
+  double low_a = 0, low_b = 0;                            // smallest nonzero finite |value| (0 = none)
+  bool all_int = true, nonfinite = false;
+};
+inline double low_min(double x, double y) { return x == 0 ? y : (y == 0 ? x : std::min(x, y)); }
+void sum_bounds_add(SumBounds& b, const ColumnRes* ca, const ColumnRes* cb) {
+  b.all_int &= ca->dtype <= PG_LONG;
+  b.bound_a = std::max(b.bound_a, std::max(fabs(ca->dmin), fabs(ca->dmax)));
+  b.fin_a = std::max(b.fin_a, ca->fin_abs);
+  b.low_a = low_min(b.low_a, ca->fin_min);
+  b.nonfinite |= ca->nonfinite;
+  if (cb) {
+    b.all_int &= cb->dtype <= PG_LONG;
+    b.bound_b = std::max(b.bound_b, std::max(fabs(cb->dmin), fabs(cb->dmax)));
+    b.fin_b = std::max(b.fin_b, cb->fin_abs);
+    b.low_b = low_min(b.low_b, cb->fin_min);
+    b.nonfinite |= cb->nonfinite;
+  }
+}
+// integer-exact accumulation when every partial sum provably fits in int64 (2^62 margin); identical to the reference's
+// double accumulation while |sum| < 2^53, more exact beyond (within the 1e-9 tolerance)
+bool sum_as_int(const SumBounds& b, const pg_agg& g, bool two, uint32_t plan_flags, uint64_t docs) {
+  double vb = b.bound_a;
+  if (two) vb = g.op == PG_EXPR_MUL ? b.bound_a * b.bound_b : b.bound_a + b.bound_b;
+  return b.all_int && !(plan_flags & PG_PLAN_F64_SUMS) && vb * (double)(docs ? docs : 1) < 4.0e18;
+}
+// SK_FX: exponent windows from power-of-two bounds 2^klo <= |x| <= 2^khi of the nonzero finite inputs (an expression of
+// finite operands can still overflow to +-inf: then the upper bound is DBL_MAX's and the non-finite results go to the
+// special slots; a product can underflow: its lower bound is the smallest subnormal).  a*b: the products of the bounds;
+// a+b / a-b: the larger bound doubled, and a nonzero result is a multiple of the smaller operand's last mantissa bit
+// (2^-52 of its lower bound).  `any`: some input may be nonzero.
+void sum_windows(const SumBounds& b, const pg_agg& g, bool two, int& klo, int& khi, bool& nonfinite, bool& any) {
+  double fb = b.fin_a, lb = b.low_a;
+  nonfinite = b.nonfinite;
+  if (two) {
+    if (g.op == PG_EXPR_MUL) {
+      fb = b.fin_a * b.fin_b;
+      lb = b.low_a * b.low_b;
+      if (b.low_a > 0 && b.low_b > 0 && lb == 0) lb = 4.9406564584124654e-324;
+    } else {
+      fb = b.fin_a + b.fin_b;
+      lb = ldexp(low_min(b.low_a, b.low_b), -52);
+      if (low_min(b.low_a, b.low_b) > 0 && lb == 0) lb = 4.9406564584124654e-324;
+    }
+  }
+  if (!std::isfinite(fb)) { fb = DBL_MAX; nonfinite = true; }
+  khi = klo = 0;
+  if (fb > 0) (void)frexp(fb, &khi);  // fb < 2^khi
+  if (lb > 0) { (void)frexp(lb, &klo); klo -= 1; }  // lb >= 2^klo
+  else klo = khi;
+  any = fb > 0;
+}
+
+// Multi-device layout hint (execute_partial_multi -> each logical device's compile_and_run): the layout choices that
+// must agree between the partial states being merged, decided once over the whole plan.
+struct LayoutHint {
+  bool on = false;
+  uint64_t docs = 0;       // the whole plan's docs (dense-vs-hash sizing)
+  uint32_t integer = 0;    // bit a: SUM / AVG a accumulates integer-exact
+};
+thread_local LayoutHint t_layout;
+
 int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t hash_cap, bool allow_stream,
                     bool allow_spec) {
   const double t_enter = wall_ms();
@@ -1524,6 +1623,9 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     auto it = g_segs.find(plan->segments[si].seg_key);
     if (it == g_segs.end()) return fail(PG_E_NOTFOUND, "segment %llu not resident", (unsigned long long)plan->segments[si].seg_key);
     segs[si] = it->second;
+    if (it->second->ldev != (uint32_t)t_ldev)
+      return fail(PG_E_STATE, "segment %llu is resident on logical device %u, not %d",
+                  (unsigned long long)plan->segments[si].seg_key, it->second->ldev, t_ldev);
     if (L && !plan->segments[si].leaves) return fail(PG_E_INVALID, "segment %u has no leaves", si);
   }
 
@@ -1629,6 +1731,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   std::unordered_set<uint32_t> projected;
   uint32_t integer = 0, special = 0;
   std::vector<int32_t> fx_shift(A, 0);
+  std::vector<uint32_t> fx_nwin(A, 1);
   for (uint32_t a = 0; a < A; a++) {
     const pg_agg& g = plan->aggs[a];
     if (g.fn > PG_AGG_COUNTMV) return fail(PG_E_INVALID, "unknown aggregation %u", g.fn);
@@ -1637,8 +1740,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     projected.insert(g.col_a);
     const bool two = (g.fn == PG_AGG_SUM || g.fn == PG_AGG_MIN || g.fn == PG_AGG_MAX || g.fn == PG_AGG_AVG) && g.op != PG_EXPR_COL;
     if (two) projected.insert(g.col_b);
-    double bound_a = 0, bound_b = 0, fin_a = 0, fin_b = 0;  // |value| bounds: all values / the finite ones
-    bool all_int = true, nonfinite = false;
+    SumBounds sb;
     for (uint32_t si = 0; si < S; si++) {
       const ColumnRes* ca = col(si, g.col_a);
       if (!ca) return fail(PG_E_NOTFOUND, "aggregation %u: column %u not resident in segment %u", a, g.col_a, si);
@@ -1660,50 +1762,39 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         continue;
       }
       if (ca->dtype > PG_DOUBLE) return fail(PG_E_UNSUPPORTED, "numeric aggregation on non-numeric column %u", g.col_a);
-      all_int &= ca->dtype <= PG_LONG;
-      bound_a = std::max(bound_a, std::max(fabs(ca->dmin), fabs(ca->dmax)));
-      fin_a = std::max(fin_a, ca->fin_abs);
-      nonfinite |= ca->nonfinite;
+      const ColumnRes* cb = nullptr;
       if (two) {
-        const ColumnRes* cb = col(si, g.col_b);
+        cb = col(si, g.col_b);
         if (!cb || cb->fwd == FWD_NONE || cb->fwd == FWD_MV || (!cb->has_dict && cb->fwd != FWD_RAW) || cb->dtype > PG_DOUBLE)
           return fail(PG_E_UNSUPPORTED, "aggregation %u: second operand column %u unusable", a, g.col_b);
-        all_int &= cb->dtype <= PG_LONG;
-        bound_b = std::max(bound_b, std::max(fabs(cb->dmin), fabs(cb->dmax)));
-        fin_b = std::max(fin_b, cb->fin_abs);
-        nonfinite |= cb->nonfinite;
       }
+      sum_bounds_add(sb, ca, cb);
     }
     if (g.fn == PG_AGG_SUM || g.fn == PG_AGG_AVG) {
-      double vb = bound_a;
-      if (two) vb = g.op == PG_EXPR_MUL ? bound_a * bound_b : bound_a + bound_b;
-      // integer-exact accumulation when every partial sum provably fits in int64 (2^62 margin); identical to the
-      // reference's double accumulation while |sum| < 2^53, more exact beyond (within the 1e-9 tolerance)
-      const bool as_int = all_int && !(plan->flags & PG_PLAN_F64_SUMS) &&
-                          vb * (double)(total_docs ? total_docs : 1) < 4.0e18;
+      const bool as_int = t_layout.on ? ((t_layout.integer >> a) & 1u) != 0 : sum_as_int(sb, g, two, plan->flags, total_docs);
       if (as_int) {
         integer |= 1u << a;
       } else {
-        // SK_FX: the unit from a power-of-two bound of the finite inputs (an expression of finite operands can still
-        // overflow to +-inf: then the bound is DBL_MAX's and the non-finite results go to the special slots)
-        double fb = fin_a;
-        if (two) fb = g.op == PG_EXPR_MUL ? fin_a * fin_b : fin_a + fin_b;
-        if (!std::isfinite(fb)) { fb = DBL_MAX; nonfinite = true; }
-        int e = 0;
-        if (fb > 0) (void)frexp(fb, &e);  // fb <= 2^e
-        if (g.sum_exp) {  // the caller's table-global bound (the same unit on every GPU / server that merges)
-          if (e > g.sum_exp)
-            return fail(PG_E_INVALID, "aggregation %u: inputs up to 2^%d exceed the plan's sum_exp %d", a, e, g.sum_exp);
-          e = g.sum_exp;
+        int klo, khi;
+        bool nonfinite, any;
+        sum_windows(sb, g, two, klo, khi, nonfinite, any);
+        if (g.sum_flags & PG_SUM_BOUNDS) {  // the caller's table-global bounds (the same windows on every GPU / server)
+          if (any && (khi > g.sum_exp || klo < g.sum_exp_lo))
+            return fail(PG_E_INVALID, "aggregation %u: inputs in [2^%d, 2^%d] exceed the plan's sum bounds [2^%d, 2^%d]",
+                        a, klo, khi, g.sum_exp_lo, g.sum_exp);
+          khi = g.sum_exp;
+          klo = g.sum_exp_lo;
         }
-        if (e < -1000 || e > 1024) return fail(PG_E_INVALID, "aggregation %u: sum_exp %d out of range", a, e);
-        fx_shift[a] = fx_shift_for(e);
+        if (klo < -1100 || khi > 1024 || klo > khi)
+          return fail(PG_E_INVALID, "aggregation %u: sum bounds [2^%d, 2^%d] out of range", a, klo, khi);
+        fx_shift[a] = fx_u0(klo);
+        fx_nwin[a] = fx_num_windows(klo, khi);
         if (nonfinite || (g.sum_flags & PG_SUM_NONFINITE)) special |= 1u << a;
       }
     }
   }
   {
-    int rc2 = agg_layout(plan, integer, fx_shift, special, P.aggs, P.n_i64, P.n_fx, P.n_min, P.n_max, P.bit_words);
+    int rc2 = agg_layout(plan, integer, fx_shift, fx_nwin, special, P.aggs, P.n_i64, P.n_fx, P.n_min, P.n_max, P.bit_words);
     if (rc2) return rc2;
     P.layout = integer;
     for (uint32_t a = 0; a < A; a++) q.aggs[a] = P.aggs[a];
@@ -1720,7 +1811,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     P.num_slots = 1;
   } else {
     const bool dense = !(plan->flags & PG_PLAN_HASH_GROUPS) && G <= kDenseMaxSlots &&
-                       G * slot_bytes <= kStateBudget / 4 && G <= 4 * total_docs + 65536;
+                       G * slot_bytes <= kStateBudget / 4 && G <= 4 * (t_layout.on ? t_layout.docs : total_docs) + 65536;
     P.mode = truncating ? GM_HASH_SEG : (dense ? GM_DENSE : GM_HASH);
     if (P.mode == GM_DENSE) {
       P.num_slots = G;
@@ -2527,6 +2618,17 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         }
         for (uint32_t k = 0; k < K; k++)
           if (plan->keys[k].col_id == cid && key_dec(k) == dec) q.key_slot[k] = (uint8_t)slot;
+        // a leaf-sourced slot that aggregation / key uses share is sourced from one of those uses: their column words
+        // exist in every segment, while a segment whose form of the leaf reads no column (isAlwaysTrue: LK_ALL) would
+        // copy nothing and leave the shared slot stale for the aggregation
+        if (c.role == 0) {
+          bool moved = false;
+          for (uint32_t a = 0; a < A && !moved; a++)
+            for (uint32_t k = 0; k < 2 && !moved; k++)
+              if (q.agg_slot[a][k] == slot) { q.staged[slot] = {1u, a, k, q.staged[slot].lds_word_off}; moved = true; }
+          for (uint32_t k = 0; k < K && !moved; k++)
+            if (q.key_slot[k] == slot) { q.staged[slot] = {2u, k, 0u, q.staged[slot].lds_word_off}; moved = true; }
+        }
       }
     }
     q.stage_lds_words = words;
@@ -3145,7 +3247,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   const uint64_t off_rjobs = ar.reserve(rjobs.size() * sizeof(RoaringJob));
   const uint64_t off_ixleaves = ar.reserve(ix.leaves.size() * sizeof(IdxLeaf));
   const uint64_t off_ixsegs = ar.reserve(ix.segs.size() * sizeof(IdxSeg));
-  const uint64_t off_ixblk = ar.reserve(ix.on ? 4ull * ix.blocks : 0ull);  // block -> segment
+  const uint64_t off_ixblk = ar.reserve(ix.on ? 4ull * ix.blocks : 0ull);  // unit -> segment
+  const uint64_t off_ixnext = ar.reserve(ix.on ? 16ull : 0ull);               // the persistent grid's claim counter
   DevBuf arena, scratch;
   DevBuf p_ent0, p_cnt0, p_hist1, p_off1, p_ent1, p_hist2, p_off2, p_ent2, p_temp, p_fill;  // GM_PART pipeline
   DevBuf l_docs, l_counts;  // selective stream: survivor regions + counts
@@ -3233,6 +3336,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     for (uint32_t si = 0; si < S; si++)
       for (uint32_t b = ix.segs[si].first_block; b < (si + 1 < S ? ix.segs[si + 1].first_block : ix.blocks); b++) bs[b] = si;
     ix.spec.blk_seg = (const uint32_t*)(dA + off_ixblk);
+    ix.spec.next_unit = (unsigned int*)(dA + off_ixnext);  // zero: reserved in the arena, which the upload copies
+    ix.spec.num_units = ix.blocks;
     ix.spec.i64 = (unsigned long long*)P.i64.p;
     ix.spec.seg_matched = (unsigned long long*)P.seg_matched.p;
   }
@@ -3829,6 +3934,7 @@ int run_wide(const pg_plan* plan, Partials& P, pg_stats& st) {
 
 struct PartialsImpl {
   Partials P;
+  uint32_t ldev = 0;  // the logical device holding the state (its pg_partials_* calls run there)
 };
 
 // wide-key exchange rows carry their tuple after the state row: K uint32 table-global key ids, padded to 8 bytes
@@ -4008,7 +4114,7 @@ int finalize_small(pg_partials* pp, const pg_plan* plan, pg_result** out, const 
             x = (double)(int64_t)i64[sl * v.n_i64 + g.slot];
           } else {
             const uint64_t* w = fx + (sl * v.n_fx + g.slot) * 2;
-            x = fx_final(g, w[0], w[1], g.sp_min != kNoSp ? mn[sl * v.n_min + g.sp_min] : 0,
+            x = fx_final(g, w, g.sp_min != kNoSp ? mn[sl * v.n_min + g.sp_min] : 0,
                          g.sp_max != kNoSp ? mx[sl * v.n_max + g.sp_max] : 0);
           }
           if (g.fn == PG_AGG_AVG) c = count;
@@ -4594,6 +4700,412 @@ int decode_image(const void* image, uint64_t n, PlanImage& out) {
   return PG_OK;
 }
 
+
+// ------------------------------------------------------------------------------------------ multi-device combine
+//
+// pg_init_devices binds one process to several logical devices (HIP devices, possibly repeated).  Each logical device
+// has one worker thread bound to its GPU, which runs every device call of that logical device (uploads, scans, merges,
+// finalisation) with its own stream and per-thread state.  Segments are placed on a logical device at their first
+// upload (pg_segment_place, else round-robin).  A query's pg_execute* splits the plan's segments by logical device,
+// runs the sub-plans concurrently, and merges the partial states on the first participating device -- the in-process
+// form of BaseCombineOperator.mergeResults (operator/combine/BaseCombineOperator.java:190-233) across GPUs:
+//   * dense states of one layout: the other devices' state arrays are copied over xGMI (hipMemcpyPeerAsync; a plain
+//     device copy when two logical devices share a GPU) and merged element-wise (merge_dense_kernel: SUM, 128-bit
+//     SUM, MIN, MAX, OR) -- AggregationFunction.merge of every group at once;
+//   * anything else (hash tables, tuple states, mixed modes): every device exports its groups as rows
+//     (pg_partials_export), the rows are copied to the merging device and inserted-and-merged into a fresh table
+//     (pg_partials_create / pg_partials_merge: IndexedTable.upsert by key).
+// The layout choices the merge depends on are made once for the whole plan (global_layout: integer-exact vs
+// fixed-point sums and their exponent windows, the dense-vs-hash sizing), so every device's state agrees.
+struct TaskResult {
+  int rc = PG_OK;
+  std::string err;
+  pg_timing timing{};
+  pg_trace trace{};
+};
+
+thread_local bool t_is_worker = false;
+
+struct Worker {
+  uint32_t ldev = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::function<void()>> q;
+  void loop() {
+    t_ldev = (int)ldev;
+    t_is_worker = true;
+    (void)ensure_device();
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return !q.empty(); });
+        f = std::move(q.front());
+        q.pop_front();
+      }
+      f();
+    }
+  }
+};
+std::vector<Worker*>* g_workers = nullptr;  // multi-device mode only; the workers live as long as the process
+
+bool multi_device() { return g_workers != nullptr; }
+bool on_ldev(uint32_t ldev) { return !multi_device() || (t_is_worker && t_ldev == (int)ldev); }
+
+std::future<TaskResult> post(uint32_t ldev, std::function<int()> fn) {
+  auto task = std::make_shared<std::packaged_task<TaskResult()>>([fn = std::move(fn)]() {
+    TaskResult r;
+    try {
+      r.rc = fn();
+    } catch (const std::exception& e) {
+      r.rc = fail(PG_E_NOMEM, "%s", e.what());
+    }
+    if (r.rc) r.err = t_err;
+    r.timing = t_timing;
+    r.trace = t_trace;
+    return r;
+  });
+  std::future<TaskResult> f = task->get_future();
+  Worker* w = (*g_workers)[ldev];
+  {
+    std::lock_guard<std::mutex> g(w->mu);
+    w->q.emplace_back([task] { (*task)(); });
+  }
+  w->cv.notify_one();
+  return f;
+}
+
+// fn on ldev's worker, synchronously (inline when this thread is that worker); its error message (and with `timing`,
+// its timing and trace records) become the calling thread's
+int run_on(uint32_t ldev, std::function<int()> fn, bool timing = false) {
+  if (on_ldev(ldev)) return fn();
+  TaskResult r = post(ldev, std::move(fn)).get();
+  if (r.rc) t_err = r.err;
+  if (timing) {
+    t_timing = r.timing;
+    t_trace = r.trace;
+  }
+  return r.rc;
+}
+
+uint32_t partial_ldev(const pg_partials* p) { return p && p->impl ? ((const PartialsImpl*)p->impl)->ldev : 0u; }
+
+std::mutex g_place_mu;
+std::unordered_map<uint64_t, uint32_t> g_place;  // seg_key -> logical device (multi-device mode)
+uint32_t g_place_next = 0;
+
+// The logical device of a segment: where it is resident, else its placement (pg_segment_place), else the next one
+// round-robin in first-upload order
+uint32_t placement(uint64_t seg_key) {
+  {
+    std::shared_lock<std::shared_mutex> lk(g_seg_mu);
+    auto it = g_segs.find(seg_key);
+    if (it != g_segs.end()) return it->second->ldev;
+  }
+  std::lock_guard<std::mutex> g(g_place_mu);
+  auto it = g_place.find(seg_key);
+  if (it != g_place.end()) return it->second;
+  const uint32_t d = g_place_next++ % (uint32_t)std::max<size_t>(1, g_ldev_phys.size());
+  g_place.emplace(seg_key, d);
+  return d;
+}
+
+// The layout choices every logical device's partial state must share (under g_seg_mu, shared): per SUM / AVG
+// aggregation integer-exact or fixed point over the WHOLE plan's segments and docs, and the fixed-point windows from
+// the table-wide bounds of every segment (unless the caller gave them: PG_SUM_BOUNDS).
+int global_layout(const pg_plan* plan, std::vector<pg_agg>& aggs, LayoutHint& hint) {
+  hint.on = true;
+  hint.docs = 0;
+  hint.integer = 0;
+  for (uint32_t si = 0; si < plan->num_segments; si++) hint.docs += plan->segments[si].num_docs;
+  for (uint32_t a = 0; a < plan->num_aggs; a++) {
+    pg_agg& g = aggs[a];
+    if (g.fn != PG_AGG_SUM && g.fn != PG_AGG_AVG) continue;
+    const bool two = g.op != PG_EXPR_COL;
+    SumBounds sb;
+    for (uint32_t si = 0; si < plan->num_segments; si++) {
+      auto it = g_segs.find(plan->segments[si].seg_key);
+      if (it == g_segs.end()) return fail(PG_E_NOTFOUND, "segment %llu not resident", (unsigned long long)plan->segments[si].seg_key);
+      auto ca = it->second->cols.find(g.col_a);
+      auto cb = two ? it->second->cols.find(g.col_b) : it->second->cols.end();
+      if (ca == it->second->cols.end() || (two && cb == it->second->cols.end()))
+        continue;  // the device's own compile reports the missing column
+      if (ca->second.dtype > PG_DOUBLE || (two && cb->second.dtype > PG_DOUBLE)) continue;
+      sum_bounds_add(sb, &ca->second, two ? &cb->second : nullptr);
+    }
+    if (sum_as_int(sb, g, two, plan->flags, hint.docs)) {
+      hint.integer |= 1u << a;
+      continue;
+    }
+    int klo, khi;
+    bool nonfinite, any;
+    sum_windows(sb, g, two, klo, khi, nonfinite, any);
+    if (!(g.sum_flags & PG_SUM_BOUNDS)) {
+      g.sum_exp = khi;
+      g.sum_exp_lo = klo;
+      g.sum_flags |= PG_SUM_BOUNDS;
+    }
+    if (nonfinite) g.sum_flags |= PG_SUM_NONFINITE;
+  }
+  return PG_OK;
+}
+
+// Copy n bytes of device memory between logical devices (an xGMI peer copy between two GPUs)
+hipError_t copy_between(void* dst, uint32_t dst_ldev, const void* src, uint32_t src_ldev, uint64_t n, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const int dd = g_ldev_phys[dst_ldev], sd = g_ldev_phys[src_ldev];
+  if (dd == sd) return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, s);
+  return hipMemcpyPeerAsync(dst, dd, src, sd, n, s);
+}
+
+// Merge the dense states `others` into `T` (all of one layout), on T's logical device.
+int merge_dense_into(PartialsImpl* T, const std::vector<PartialsImpl*>& others) {
+  hipStream_t s = thread_stream();
+  Partials& P = T->P;
+  const uint64_t G = P.num_slots;
+  const uint64_t bytes[5] = {G * 8ull * P.n_i64, G * 16ull * P.n_fx, G * 8ull * P.n_min, G * 8ull * P.n_max,
+                             G * 4ull * P.bit_words};
+  for (PartialsImpl* O : others) {
+    const Partials& S = O->P;
+    StateView sv = S.view();
+    DevBuf tmp[5];
+    if (g_ldev_phys[O->ldev] != g_ldev_phys[T->ldev]) {  // another GPU: bring its arrays here first
+      void* src[5] = {S.i64.p, S.fx.p, S.mn.p, S.mx.p, S.bits.p};
+      void** dst[5] = {(void**)&sv.i64, (void**)&sv.fx, (void**)&sv.mn, (void**)&sv.mx, (void**)&sv.bits};
+      for (int i = 0; i < 5; i++) {
+        if (!bytes[i]) continue;
+        int rc = tmp[i].alloc_pooled(bytes[i]);
+        if (rc) return rc;
+        HIP_CHECK(copy_between(tmp[i].p, T->ldev, src[i], O->ldev, bytes[i], s));
+        *dst[i] = tmp[i].p;
+      }
+    }
+    HIP_CHECK(launch_merge_dense(P.view(), sv, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    P.flags |= S.flags & PG_RESULT_GROUPS_LIMIT_REACHED;
+  }
+  return PG_OK;
+}
+
+bool same_dense_layout(const std::vector<pg_partials*>& ps) {
+  for (const pg_partials* p : ps)
+    if (p->mode != PG_STATE_DENSE || p->num_slots != ps[0]->num_slots || p->n_i64 != ps[0]->n_i64 ||
+        p->n_fx != ps[0]->n_fx || p->n_min != ps[0]->n_min || p->n_max != ps[0]->n_max ||
+        p->bitmap_words != ps[0]->bitmap_words || ((const PartialsImpl*)p->impl)->P.wide)
+      return false;
+  return true;
+}
+
+int free_partials_everywhere(std::vector<pg_partials*>& ps) {
+  for (pg_partials*& p : ps)
+    if (p) { (void)pg_partials_free(p); p = nullptr; }
+  return PG_OK;
+}
+
+// The in-library combine of the partial states ps (one per participating logical device, ps[0] on the merging
+// device): the merged state, on ps[0]'s device; consumes ps.
+int merge_partials_multi(std::vector<pg_partials*>& ps, pg_partials** out) {
+  for (const pg_partials* p : ps)
+    if (p->layout != ps[0]->layout || p->fx_sig != ps[0]->fx_sig || p->row_bytes != ps[0]->row_bytes) {
+      free_partials_everywhere(ps);
+      return fail(PG_E_INVALID, "partial state layouts differ between logical devices");
+    }
+  pg_stats st{};
+  uint32_t flags = 0;
+  for (const pg_partials* p : ps) {
+    st.num_docs_scanned += p->stats.num_docs_scanned;
+    st.num_entries_scanned_in_filter += p->stats.num_entries_scanned_in_filter;
+    st.num_entries_scanned_post_filter += p->stats.num_entries_scanned_post_filter;
+    st.num_total_docs += p->stats.num_total_docs;
+    st.num_segments_processed += p->stats.num_segments_processed;
+    st.num_segments_matched += p->stats.num_segments_matched;
+    flags |= p->flags & PG_RESULT_GROUPS_LIMIT_REACHED;
+  }
+  const uint32_t d0 = partial_ldev(ps[0]);
+  int rc;
+  if (same_dense_layout(ps)) {
+    std::vector<PartialsImpl*> others;
+    for (size_t i = 1; i < ps.size(); i++) others.push_back((PartialsImpl*)ps[i]->impl);
+    rc = run_on(d0, [&] { return merge_dense_into((PartialsImpl*)ps[0]->impl, others); });
+    pg_partials* m = ps[0];
+    ps[0] = nullptr;
+    free_partials_everywhere(ps);
+    if (rc) { (void)pg_partials_free(m); return rc; }
+    m->stats = st;
+    m->flags = flags;
+    *out = m;
+    return PG_OK;
+  }
+  // the row exchange: every device exports its groups (on its own worker, concurrently), the merging device inserts
+  // them into a fresh table
+  const uint64_t rb = ps[0]->row_bytes;
+  std::vector<DevBuf> rows(ps.size());
+  std::vector<uint64_t> nrows(ps.size(), 0);
+  std::vector<std::future<TaskResult>> fut;
+  for (size_t i = 0; i < ps.size(); i++) {
+    fut.push_back(post(partial_ldev(ps[i]), [&, i] {
+      uint64_t n = 0;
+      int r = pg_partials_export(ps[i], 1, nullptr, 0, &n, nullptr);
+      if (r) return r;
+      if ((r = rows[i].alloc_pooled(n * rb + 8))) return r;
+      nrows[i] = n;
+      return n ? pg_partials_export(ps[i], 1, rows[i].p, n, &n, nullptr) : PG_OK;
+    }));
+  }
+  rc = PG_OK;
+  for (auto& f : fut) {
+    TaskResult r = f.get();
+    if (r.rc && !rc) { rc = r.rc; t_err = r.err; }
+  }
+  pg_partials* m = nullptr;
+  if (!rc) {
+    uint64_t total = 0;
+    for (uint64_t n : nrows) total += n;
+    rc = run_on(d0, [&] {
+      int r = pg_partials_create(ps[0], std::max<uint64_t>(total, 1), &m);
+      if (r) return r;
+      hipStream_t s = thread_stream();
+      for (size_t i = 0; i < ps.size() && !r; i++) {
+        if (!nrows[i]) continue;
+        const uint32_t src = partial_ldev(ps[i]);
+        const void* at = rows[i].p;
+        DevBuf tmp;
+        if (g_ldev_phys[src] != g_ldev_phys[d0]) {
+          if ((r = tmp.alloc_pooled(nrows[i] * rb + 8))) break;
+          if (copy_between(tmp.p, d0, rows[i].p, src, nrows[i] * rb, s) != hipSuccess ||
+              hipStreamSynchronize(s) != hipSuccess) {
+            r = fail(PG_E_HIP, "row copy between logical devices %u and %u failed", src, d0);
+            break;
+          }
+          at = tmp.p;
+        }
+        r = pg_partials_merge(m, at, nrows[i], nullptr);
+      }
+      return r;
+    });
+  }
+  rows.clear();
+  free_partials_everywhere(ps);
+  if (rc) {
+    if (m) (void)pg_partials_free(m);
+    return rc;
+  }
+  m->stats = st;
+  m->flags = flags;
+  *out = m;
+  return PG_OK;
+}
+
+// pg_execute_partial in multi-device mode: the plan's segments split by logical device, one sub-plan per device with
+// segments run concurrently, their states merged (merge_partials_multi).
+int execute_partial_multi(const pg_plan* plan, pg_partials** out) {
+  if (!out) return fail(PG_E_INVALID, "null out");
+  *out = nullptr;
+  if (!plan) return fail(PG_E_INVALID, "null plan");
+  if (plan->abi_version != PG_ABI_VERSION)
+    return fail(PG_E_INVALID, "plan ABI version %u, library %d", plan->abi_version, PG_ABI_VERSION);
+  if (plan->num_segments && !plan->segments) return fail(PG_E_INVALID, "null segment list");
+  if (plan->num_aggs && !plan->aggs) return fail(PG_E_INVALID, "null aggregation list");
+  if (plan->num_aggs > (uint32_t)kMaxAggs) return fail(PG_E_UNSUPPORTED, "more than %d aggregations", kMaxAggs);
+  const double t0 = wall_ms();
+  const uint32_t N = (uint32_t)g_ldev_phys.size();
+  struct Sub {
+    std::vector<pg_segment_ref> segs;
+    pg_plan plan;
+    pg_partials* out = nullptr;
+  };
+  std::vector<Sub> sub(N);
+  std::vector<pg_agg> aggs(plan->aggs, plan->aggs + plan->num_aggs);
+  LayoutHint hint;
+  {
+    std::shared_lock<std::shared_mutex> lk(g_seg_mu);
+    for (uint32_t si = 0; si < plan->num_segments; si++) {
+      auto it = g_segs.find(plan->segments[si].seg_key);
+      if (it == g_segs.end())
+        return fail(PG_E_NOTFOUND, "segment %llu not resident", (unsigned long long)plan->segments[si].seg_key);
+      sub[it->second->ldev].segs.push_back(plan->segments[si]);
+    }
+    const int rc = global_layout(plan, aggs, hint);
+    if (rc) return rc;
+  }
+  std::vector<uint32_t> run;
+  for (uint32_t d = 0; d < N; d++)
+    if (!sub[d].segs.empty()) run.push_back(d);
+  if (run.empty()) run.push_back(0);
+  std::vector<std::future<TaskResult>> fut;
+  for (uint32_t d : run) {
+    Sub& x = sub[d];
+    x.plan = *plan;
+    x.plan.num_segments = (uint32_t)x.segs.size();
+    x.plan.segments = x.segs.empty() ? nullptr : x.segs.data();
+    x.plan.aggs = aggs.empty() ? nullptr : aggs.data();
+    x.plan.stream = nullptr;  // the caller's stream belongs to its own device: each worker uses its own
+    fut.push_back(post(d, [&x, &hint] {
+      t_layout = hint;
+      const int r = pg_execute_partial(&x.plan, &x.out);
+      t_layout = LayoutHint{};
+      return r;
+    }));
+  }
+  int rc = PG_OK;
+  pg_timing tm{};
+  pg_trace tr{};
+  uint64_t matched = 0;
+  for (size_t i = 0; i < fut.size(); i++) {
+    TaskResult r = fut[i].get();
+    if (r.rc && !rc) { rc = r.rc; t_err = r.err; }
+    if (i == 0) { tm = r.timing; tr = r.trace; }
+    tm.scan_ms = std::max(tm.scan_ms, r.timing.scan_ms);
+    tm.prepass_ms = std::max(tm.prepass_ms, r.timing.prepass_ms);
+    tr.path |= r.trace.path;
+    matched += r.trace.num_docs_matched;
+  }
+  std::vector<pg_partials*> ps;
+  for (uint32_t d : run)
+    if (sub[d].out) ps.push_back(sub[d].out);
+  if (rc) {
+    free_partials_everywhere(ps);
+    return rc;
+  }
+  if (ps.size() == 1) {
+    *out = ps[0];
+  } else if ((rc = merge_partials_multi(ps, out))) {
+    return rc;
+  }
+  tm.execute_wall_ms = (float)(wall_ms() - t0);
+  tr.num_docs_matched = matched;
+  tr.num_segments = plan->num_segments;
+  tr.wall_ms = tm.execute_wall_ms;
+  t_timing = tm;
+  t_trace = tr;
+  return PG_OK;
+}
+
+// pg_dict_id_sets over segments resident on several logical devices: each device looks up its own segments
+int dict_id_sets_multi(const uint64_t* seg_keys, uint32_t num_segments, uint32_t col_id, uint32_t data_type,
+                       const void* values, uint32_t num_values, int32_t* out_ids, uint32_t* out_counts) {
+  const uint32_t N = (uint32_t)g_ldev_phys.size();
+  std::vector<std::vector<uint32_t>> idx(N);
+  for (uint32_t si = 0; si < num_segments; si++) idx[placement(seg_keys[si])].push_back(si);
+  for (uint32_t d = 0; d < N; d++) {
+    if (idx[d].empty()) continue;
+    std::vector<uint64_t> keys(idx[d].size());
+    for (size_t i = 0; i < keys.size(); i++) keys[i] = seg_keys[idx[d][i]];
+    std::vector<int32_t> ids((uint64_t)keys.size() * num_values);
+    std::vector<uint32_t> cnt(keys.size());
+    const int rc = run_on(d, [&] {
+      return pg_dict_id_sets(keys.data(), (uint32_t)keys.size(), col_id, data_type, values, num_values, ids.data(),
+                             cnt.data());
+    });
+    if (rc) return rc;
+    for (size_t i = 0; i < keys.size(); i++) {
+      memcpy(out_ids + (uint64_t)idx[d][i] * num_values, ids.data() + i * (uint64_t)num_values, 4ull * num_values);
+      out_counts[idx[d][i]] = cnt[i];
+    }
+  }
+  return PG_OK;
+}
+
 }  // namespace
 
 // ============================================================================================ C ABI
@@ -4613,17 +5125,78 @@ static void segv_trace(int sig) {
   raise(sig);
 }
 
-int pg_init(int device) {
+int pg_init_devices(const int* devices, uint32_t n) {
   std::lock_guard<std::mutex> g(g_init_mu);
   if (getenv("PG_SEGV_TRACE") && atoi(getenv("PG_SEGV_TRACE"))) signal(SIGSEGV, segv_trace);
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(PG_E_HIP, "no HIP device visible");
-  if (device < 0 || device >= n) return fail(PG_E_INVALID, "device %d out of range (%d visible)", device, n);
-  if (g_device >= 0 && g_device != device) return fail(PG_E_STATE, "already bound to device %d", g_device);
-  HIP_CHECK(hipSetDevice(device));
-  g_device = device;
+  if (!devices || n == 0 || n > 64) return fail(PG_E_INVALID, "device list of %u entries", n);
+  int vis = 0;
+  if (hipGetDeviceCount(&vis) != hipSuccess || vis == 0) return fail(PG_E_HIP, "no HIP device visible");
+  for (uint32_t i = 0; i < n; i++)
+    if (devices[i] < 0 || devices[i] >= vis || devices[i] >= kMaxPhys)
+      return fail(PG_E_INVALID, "device %d out of range (%d visible)", devices[i], vis);
+  if (g_device >= 0) {  // idempotent for the same binding
+    if (g_ldev_phys.size() == n && std::equal(g_ldev_phys.begin(), g_ldev_phys.end(), devices)) return PG_OK;
+    return fail(PG_E_STATE, "already bound to device %d (%zu logical devices)", g_device, g_ldev_phys.size());
+  }
+  for (uint32_t i = 0; i < n; i++) {  // xGMI peer access between the distinct GPUs (copies work without it, staged)
+    for (uint32_t j = 0; j < n; j++) {
+      if (devices[i] == devices[j]) continue;
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, devices[i], devices[j]) == hipSuccess && can && hipSetDevice(devices[i]) == hipSuccess) {
+        const hipError_t e = hipDeviceEnablePeerAccess(devices[j], 0);
+        if (e != hipSuccess) (void)hipGetLastError();  // already enabled (another pair entry) is fine
+      }
+    }
+  }
+  HIP_CHECK(hipSetDevice(devices[0]));
+  g_ldev_phys.assign(devices, devices + n);
+  g_device = devices[0];
   init_grid_caps();
-  return init_cancel_flags();
+  int rc = init_cancel_flags();
+  if (rc) return rc;
+  if (n > 1) {
+    auto* ws = new std::vector<Worker*>();
+    for (uint32_t i = 0; i < n; i++) {
+      Worker* w = new Worker();
+      w->ldev = i;
+      ws->push_back(w);
+      std::thread([w] { w->loop(); }).detach();
+    }
+    g_workers = ws;
+  }
+  return PG_OK;
+}
+
+int pg_init(int device) { return pg_init_devices(&device, 1); }
+
+int pg_num_devices(uint32_t* out) {
+  if (!out) return fail(PG_E_INVALID, "null out");
+  *out = (uint32_t)g_ldev_phys.size();
+  return g_device < 0 ? fail(PG_E_STATE, "pg_init has not been called") : PG_OK;
+}
+
+int pg_segment_place(uint64_t seg_key, uint32_t ldev) {
+  if (g_device < 0) return fail(PG_E_STATE, "pg_init has not been called");
+  if (ldev >= g_ldev_phys.size()) return fail(PG_E_INVALID, "logical device %u of %zu", ldev, g_ldev_phys.size());
+  {
+    std::shared_lock<std::shared_mutex> lk(g_seg_mu);
+    auto it = g_segs.find(seg_key);
+    if (it != g_segs.end() && it->second->ldev != ldev)
+      return fail(PG_E_STATE, "segment %llu is resident on logical device %u (release it first)",
+                  (unsigned long long)seg_key, it->second->ldev);
+  }
+  std::lock_guard<std::mutex> g(g_place_mu);
+  g_place[seg_key] = ldev;
+  return PG_OK;
+}
+
+int pg_segment_device(uint64_t seg_key, uint32_t* ldev) {
+  if (!ldev) return fail(PG_E_INVALID, "null out");
+  std::shared_lock<std::shared_mutex> lk(g_seg_mu);
+  auto it = g_segs.find(seg_key);
+  if (it == g_segs.end()) return fail(PG_E_NOTFOUND, "segment %llu not resident", (unsigned long long)seg_key);
+  *ldev = it->second->ldev;
+  return PG_OK;
 }
 
 int pg_last_error(char* buf, size_t n) {
@@ -4655,6 +5228,10 @@ int pg_cancel(uint64_t query_id) {
 }
 
 int pg_column_upload(uint64_t seg_key, uint32_t col_id, const pg_col_desc* desc, const void* src, uint64_t nbytes) {
+  if (multi_device() && !t_is_worker) {
+    const uint32_t d = placement(seg_key);
+    return run_on(d, [=] { return pg_column_upload(seg_key, col_id, desc, src, nbytes); });
+  }
   int rc = ensure_device();
   if (rc) return rc;
   if (!desc || (!src && nbytes)) return fail(PG_E_INVALID, "null descriptor or source");
@@ -4666,6 +5243,13 @@ int pg_column_upload(uint64_t seg_key, uint32_t col_id, const pg_col_desc* desc,
 }
 
 int pg_segment_release(uint64_t seg_key) {
+  if (multi_device() && !t_is_worker) {
+    const uint32_t d = placement(seg_key);
+    const int r = run_on(d, [=] { return pg_segment_release(seg_key); });
+    std::lock_guard<std::mutex> g(g_place_mu);
+    g_place.erase(seg_key);
+    return r;
+  }
   int rc = ensure_device();
   if (rc) return rc;
   std::unique_lock<std::shared_mutex> lk(g_seg_mu);
@@ -4677,12 +5261,14 @@ int pg_segment_release(uint64_t seg_key) {
 }
 
 int pg_execute_partial(const pg_plan* plan, pg_partials** out) {
+  if (multi_device() && !t_is_worker) return execute_partial_multi(plan, out);
   int rc = ensure_device();
   if (rc) return rc;
   if (!out) return fail(PG_E_INVALID, "null out");
   *out = nullptr;
   PartialsImpl* impl = new (std::nothrow) PartialsImpl();
   if (!impl) return fail(PG_E_NOMEM, "out of host memory");
+  impl->ldev = (uint32_t)t_ldev;
   pg_stats st;
   const double t0 = wall_ms();
   t_timing.host_compile_ms = 0;
@@ -4708,6 +5294,7 @@ int pg_execute_partial(const pg_plan* plan, pg_partials** out) {
 }
 
 int pg_partials_finalize(pg_partials* p, const pg_plan* plan, pg_result** out) {
+  if (!on_ldev(partial_ldev(p))) return run_on(partial_ldev(p), [=] { return pg_partials_finalize(p, plan, out); }, true);
   int rc = ensure_device();
   if (rc) return rc;
   if (!p || !plan || !out || !p->impl) return fail(PG_E_INVALID, "null argument");
@@ -4720,6 +5307,7 @@ int pg_partials_finalize(pg_partials* p, const pg_plan* plan, pg_result** out) {
 
 int pg_partials_free(pg_partials* p) {
   if (!p) return PG_OK;
+  if (!on_ldev(partial_ldev(p))) return run_on(partial_ldev(p), [=] { return pg_partials_free(p); });
   ensure_device();
   delete (PartialsImpl*)p->impl;
   free(p);
@@ -4727,6 +5315,8 @@ int pg_partials_free(pg_partials* p) {
 }
 
 int pg_partials_copy(pg_partials* p, int dir, void* i64, void* fx, void* mn, void* mx, void* stream) {
+  if (!on_ldev(partial_ldev(p)))
+    return run_on(partial_ldev(p), [=] { return pg_partials_copy(p, dir, i64, fx, mn, mx, nullptr); });
   int rc = ensure_device();
   if (rc) return rc;
   if (!p || !p->impl || (dir != PG_COPY_OUT && dir != PG_COPY_IN)) return fail(PG_E_INVALID, "bad partials / direction");
@@ -4794,6 +5384,8 @@ int export_wide(Partials& P, uint32_t num_parts, void* dst, uint64_t dst_rows, u
 
 int pg_partials_export(pg_partials* p, uint32_t num_parts, void* dst, uint64_t dst_rows, uint64_t* part_counts,
                        void* stream) {
+  if (!on_ldev(partial_ldev(p)))
+    return run_on(partial_ldev(p), [=] { return pg_partials_export(p, num_parts, dst, dst_rows, part_counts, nullptr); });
   int rc = ensure_device();
   if (rc) return rc;
   if (!p || !p->impl || !num_parts || !part_counts) return fail(PG_E_INVALID, "bad export arguments");
@@ -4828,12 +5420,15 @@ int pg_partials_export(pg_partials* p, uint32_t num_parts, void* dst, uint64_t d
 }
 
 int pg_partials_create(const pg_partials* like, uint64_t capacity, pg_partials** out) {
+  if (!on_ldev(partial_ldev(like)))
+    return run_on(partial_ldev(like), [=] { return pg_partials_create(like, capacity, out); });
   int rc = ensure_device();
   if (rc) return rc;
   if (!like || !like->impl || !out) return fail(PG_E_INVALID, "null argument");
   *out = nullptr;
   PartialsImpl* impl = new (std::nothrow) PartialsImpl();
   if (!impl) return fail(PG_E_NOMEM, "out of host memory");
+  impl->ldev = (uint32_t)t_ldev;
   try {
     hipStream_t s = thread_stream();
     const Partials& L = ((PartialsImpl*)like->impl)->P;
@@ -4868,6 +5463,7 @@ int pg_partials_create(const pg_partials* like, uint64_t capacity, pg_partials**
 }
 
 int pg_partials_merge(pg_partials* p, const void* rows, uint64_t n, void* stream) {
+  if (!on_ldev(partial_ldev(p))) return run_on(partial_ldev(p), [=] { return pg_partials_merge(p, rows, n, nullptr); });
   int rc = ensure_device();
   if (rc) return rc;
   if (!p || !p->impl || (!rows && n)) return fail(PG_E_INVALID, "null argument");
@@ -4908,6 +5504,12 @@ int pg_partials_merge(pg_partials* p, const void* rows, uint64_t n, void* stream
 
 int pg_dict_id_sets(const uint64_t* seg_keys, uint32_t num_segments, uint32_t col_id, uint32_t data_type,
                     const void* values, uint32_t num_values, int32_t* out_ids, uint32_t* out_counts) {
+  if (multi_device() && !t_is_worker && g_device >= 0) {
+    if ((!seg_keys && num_segments) || (!values && num_values) || (!out_ids && num_segments && num_values) ||
+        (!out_counts && num_segments))
+      return fail(PG_E_INVALID, "null argument");
+    return dict_id_sets_multi(seg_keys, num_segments, col_id, data_type, values, num_values, out_ids, out_counts);
+  }
   int rc = ensure_device();
   if (rc) return rc;
   if ((!seg_keys && num_segments) || (!values && num_values) || (!out_ids && num_segments && num_values) ||
@@ -4962,6 +5564,21 @@ int pg_dict_id_sets(const uint64_t* seg_keys, uint32_t num_segments, uint32_t co
 
 int pg_execute(const pg_plan* plan, pg_result** out) {
   if (!out) return fail(PG_E_INVALID, "null out");
+  if (multi_device() && !t_is_worker) {  // the segments' logical devices, their states merged in the library
+    pg_partials* p = nullptr;
+    int rc = execute_partial_multi(plan, &p);
+    if (rc) return rc;
+    const pg_timing te = t_timing;
+    const pg_trace tr = t_trace;
+    rc = pg_partials_finalize(p, plan, out);
+    pg_timing tf = t_timing;
+    t_timing = te;
+    t_timing.finalize_ms = tf.finalize_ms;
+    t_timing.finalize_wall_ms = tf.finalize_wall_ms;
+    t_trace = tr;
+    pg_partials_free(p);
+    return rc;
+  }
   t_prof.n = 0;
   const double t_prof_start = wall_ms();
   pg_partials* p = nullptr;

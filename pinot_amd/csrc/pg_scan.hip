@@ -598,13 +598,15 @@ __device__ __forceinline__ void s_addfx(const GroupState& S, unsigned long long*
     g_addfx(p, lo, hi);
   }
 }
-// One SK_FX input: its exact fixed-point value into the pair, or (+-inf / NaN) its order image into the special slots
+// One SK_FX input: its exact fixed-point value into its exponent window's pair, or (+-inf / NaN) its order image into
+// the special slots
 __device__ __forceinline__ void fx_update(const QuerySpec& q, const GroupState& S, const AggSpec& A, uint64_t g,
                                           double v) {
   if (__builtin_isfinite(v)) {
+    if (v == 0.0) return;
     uint64_t lo, hi;
-    fx_from_double(v, A.fx_shift, lo, hi);
-    s_addfx(S, &S.fx[(g * q.n_fx + A.slot) * 2], lo, hi);
+    const uint32_t w = fx_split(v, A.fx_shift, A.fx_nwin, lo, hi);
+    s_addfx(S, &S.fx[(g * q.n_fx + A.slot + w) * 2], lo, hi);
   } else if (A.sp_min != kNoSp) {
     const long long k = (long long)order_key(v);
     s_min(S, &S.mn[g * q.n_min + A.sp_min], k);

@@ -76,12 +76,20 @@ def fwd_desc(col: Column) -> abi.pg_col_desc:
 
 
 class GpuEngine:
-    """One engine per process, bound to one GPU (one process per GPU)."""
+    """One engine per process: bound to one GPU (one process per GPU; the ranks merge over RCCL, pinot_amd.combine),
+    or with `devices` to several logical devices of this process (pg_init_devices: segments placed on them
+    round-robin or by `place`, every query merged across them inside the library)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, devices: Optional[Sequence[int]] = None):
         self.lib = load_library()
-        check(self.lib.pg_init(device))
+        if devices is not None:
+            arr = (C.c_int * len(devices))(*devices)
+            check(self.lib.pg_init_devices(arr, len(devices)))
+            device = devices[0]
+        else:
+            check(self.lib.pg_init(device))
         self.device = device
+        self.devices = list(devices) if devices is not None else [device]
         self._seg_keys: Dict[int, tuple] = {}    # id(segment) -> (segment, seg_key); holds the segment alive
         self._keymaps_uploaded = set()
         self._plans: "collections.OrderedDict[tuple, tuple]" = collections.OrderedDict()  # compiled-plan cache
@@ -90,11 +98,15 @@ class GpuEngine:
         self.plan_cache_misses = 0
 
     # ---- residency (IndexingOverrides reader-provider hook)
-    def upload_segment(self, seg: ImmutableSegment, table: Table) -> int:
+    def upload_segment(self, seg: ImmutableSegment, table: Table, ldev: Optional[int] = None) -> int:
+        """Make a segment resident (once); ldev: its logical device (pg_segment_place), else the library's
+        round-robin placement."""
         hit = self._seg_keys.get(id(seg))
         if hit is not None:
             return hit[1]
         key = next(_seg_counter)
+        if ldev is not None:
+            check(self.lib.pg_segment_place(key, ldev))
         for name, col in seg.columns.items():
             cid = table.column_ids[name]
             d = fwd_desc(col)
@@ -175,6 +187,12 @@ class GpuEngine:
                                        counts.ctypes.data_as(C.POINTER(C.c_uint32))))
         return ids, counts
 
+    def segment_device(self, seg: ImmutableSegment) -> int:
+        """The logical device a resident segment lives on (pg_segment_device)."""
+        out = C.c_uint32()
+        check(self.lib.pg_segment_device(self._seg_keys[id(seg)][1], C.byref(out)))
+        return out.value
+
     def release(self, seg: ImmutableSegment):
         hit = self._seg_keys.pop(id(seg), None)
         if hit is not None:
@@ -207,8 +225,8 @@ class GpuEngine:
         for config 2's 128 segments, so a server answering the same query text again over the same resident segments
         reuses the lowered plan.  The key pins everything the plan depends on: the SQL text, the table object, the
         segments' residency keys (a released and re-uploaded segment gets a new key; keys are never reused), flags,
-        trim and the instance config.  A plan is immutable once built (execution reads its image), so reuse is
-        exact."""
+        trim and the instance config.  A plan is immutable once built (execution reads its image; each thread's copy
+        of the image carries its own per-call scalars, CPlan.image), so reuse is exact."""
         segs = list(table.segments if segments is None else segments)
         keys = tuple(self.upload_segment(s, table) for s in segs)
         ck = (sql, id(table), keys, flags, trim, None if config is None else dataclasses.astuple(config))
@@ -231,8 +249,8 @@ class GpuEngine:
         pointer-form pg_plan (the in-process form)."""
         res = C.POINTER(abi.pg_result)()
         if image:
-            im = plan.image()
-            check(self.lib.pg_execute_image(plan.image_addr, im.size, C.byref(res)))
+            im, addr = plan.image()
+            check(self.lib.pg_execute_image(addr, im.size, C.byref(res)))
         else:
             check(self.lib.pg_execute(C.byref(plan.plan), C.byref(res)))
         try:
@@ -244,15 +262,15 @@ class GpuEngine:
         """pg_execute_partial(_image): this device's partial state (for the cross-GPU merge, pinot_amd.combine)."""
         p = C.POINTER(abi.pg_partials)()
         if image:
-            im = plan.image()
-            check(self.lib.pg_execute_partial_image(plan.image_addr, im.size, C.byref(p)))
+            im, addr = plan.image()
+            check(self.lib.pg_execute_partial_image(addr, im.size, C.byref(p)))
         else:
             check(self.lib.pg_execute_partial(C.byref(plan.plan), C.byref(p)))
         return p
 
     def _finalize(self, plan: CPlan, p, res):
-        im = plan.image()
-        check(self.lib.pg_partials_finalize_image(p, plan.image_addr, im.size, C.byref(res)))
+        im, addr = plan.image()
+        check(self.lib.pg_partials_finalize_image(p, addr, im.size, C.byref(res)))
 
     def finalize_partial(self, plan: CPlan, p, free: bool = True) -> IntermediateResult:
         res = C.POINTER(abi.pg_result)()

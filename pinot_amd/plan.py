@@ -214,17 +214,33 @@ def lower_predicate(pred: Predicate, col: Column, col_id: int, in_ids: Optional[
     return LoweredLeaf(kind, col_id, excl, lo, hi, ids)
 
 
-def sum_bound(table: "Table", e: Expr) -> Tuple[int, bool]:
-    """(pg_agg.sum_exp, PG_SUM_NONFINITE) of a SUM / AVG input: e with 2^e >= |every finite value| of the expression
-    over the table (a*b: the product of the operand bounds, a+b / a-b their sum; an overflow to inf bounds it by
-    DBL_MAX), so every GPU that merges the plan's partial states sums in the same fixed-point unit (e = 0, "let the
-    device derive it", only when every value is 0), and whether some input may be +-inf / NaN."""
-    b = [table.abs_bound(c) for c in e.cols]
+def sum_bound(table: "Table", e: Expr) -> Tuple[int, int, bool]:
+    """(pg_agg.sum_exp, pg_agg.sum_exp_lo, PG_SUM_NONFINITE) of a SUM / AVG input: 2^lo <= |x| <= 2^hi for every nonzero
+    finite value x of the expression over the table (a*b: the products of the operand bounds; a+b / a-b: the larger
+    bound doubled, and a nonzero result is a multiple of the smaller operand's last mantissa bit, 2^-52 of its lower
+    bound; an overflow to inf bounds it by DBL_MAX, an underflow by the smallest subnormal), so every GPU that merges
+    the plan's partial states cuts the sums into the same exponent windows (pg_internal.h fx_split), and whether some
+    input may be +-inf / NaN.  Sent with PG_SUM_BOUNDS, so an all-zero column (0, 0) is unambiguous."""
+    hi = [table.abs_bound(c) for c in e.cols]
+    lo = [table.abs_low(c) for c in e.cols]
     nonfinite = any(table.has_nonfinite(c) for c in e.cols)
-    v = b[0] if e.op == "COL" else (b[0] * b[1] if e.op == "MUL" else b[0] + b[1])
+    tiny = 5e-324
+    lmin = lambda x, y: y if x == 0 else (x if y == 0 else min(x, y))  # noqa: E731
+    if e.op == "COL":
+        v, low = hi[0], lo[0]
+    elif e.op == "MUL":
+        v, low = hi[0] * hi[1], lo[0] * lo[1]
+        if lo[0] > 0 and lo[1] > 0 and low == 0:
+            low = tiny
+    else:
+        v, low = hi[0] + hi[1], math.ldexp(lmin(lo[0], lo[1]), -52)
+        if lmin(lo[0], lo[1]) > 0 and low == 0:
+            low = tiny
     if not math.isfinite(v):
         v, nonfinite = float(np.finfo(np.float64).max), True
-    return (math.frexp(v)[1] if v > 0 else 0), nonfinite
+    khi = math.frexp(v)[1] if v > 0 else 0            # v < 2^khi
+    klo = math.frexp(low)[1] - 1 if low > 0 else khi  # low >= 2^klo
+    return khi, klo, nonfinite
 
 
 def filter_program(f: Optional[FilterContext]) -> Tuple[List[int], List[Predicate]]:
@@ -264,18 +280,25 @@ class Table:
                     cols.append(c)
         self.column_ids = {c: i for i, c in enumerate(cols)}
         self._key_spaces: Dict[str, "KeySpace"] = {}
-        self._abs_bounds: Dict[str, Tuple[float, bool]] = {}
+        self._abs_bounds: Dict[str, Tuple[float, float, bool]] = {}
 
     def has_nonfinite(self, column: str) -> bool:
-        self.abs_bound(column)
-        return self._abs_bounds[column][1]
+        return self._bounds(column)[2]
 
     def abs_bound(self, column: str) -> float:
         """The largest |finite value| of a numeric column over every segment of the table (ColumnMetadata min / max:
-        the dictionary's ends, or a raw column's values) -- the table-global bound of pg_agg.sum_exp."""
+        the dictionary's ends, or a raw column's values) -- the table-global upper bound of pg_agg.sum_exp."""
+        return self._bounds(column)[0]
+
+    def abs_low(self, column: str) -> float:
+        """The smallest nonzero |finite value| of a numeric column over the table (0: none) -- the lower bound of
+        pg_agg.sum_exp_lo (an integer column: 1)."""
+        return self._bounds(column)[1]
+
+    def _bounds(self, column: str) -> Tuple[float, float, bool]:
         hit = self._abs_bounds.get(column)
         if hit is None:
-            b, nonfinite = 0.0, False
+            b, low, nonfinite = 0.0, 0.0, False
             for seg in self.segments:
                 c = seg.columns.get(column)
                 if c is None:
@@ -283,19 +306,36 @@ class Table:
                 v = np.asarray(c.raw_values if c.dictionary is None else c.dictionary.values)
                 if not v.size or v.dtype.kind not in "iuf":
                     continue
-                if c.dictionary is not None:  # a sorted dictionary: its ends bound it, unless they are not finite
-                    ends = np.abs(v[[0, -1]].astype(np.float64))
-                    if np.isfinite(ends).all():
-                        b = max(b, float(ends.max()))
-                        continue
+                if v.dtype.kind in "iu":  # integers: the ends bound |v| (a sorted dictionary's ends), nonzero |v| >= 1
+                    ends = (v[[0, -1]] if c.dictionary is not None else np.array([v.min(), v.max()])).astype(np.float64)
+                    m = float(np.abs(ends).max())
+                    b = max(b, m)
+                    if m > 0:
+                        low = 1.0 if low == 0 else min(low, 1.0)
+                    continue
+                if c.dictionary is not None and np.isfinite(v[[0, -1]]).all():
+                    # a sorted finite dictionary: its ends bound |v|, the smallest nonzero |v| sits around 0
+                    b = max(b, float(np.abs(v[[0, -1]]).max()))
+                    i = int(np.searchsorted(v, 0.0, side="left"))
+                    j = int(np.searchsorted(v, 0.0, side="right"))
+                    cand = [abs(float(v[i - 1]))] if i > 0 else []
+                    cand += [abs(float(v[j]))] if j < v.size else []
+                    if cand:
+                        m = min(cand)
+                        low = m if low == 0 else min(low, m)
+                    continue
                 a = np.abs(v.astype(np.float64))
                 fin = np.isfinite(a)
                 nonfinite |= not bool(fin.all())
                 a = a[fin]
                 if a.size:
                     b = max(b, float(a.max()))
-            hit = self._abs_bounds[column] = (b, nonfinite)
-        return hit[0]
+                    nz = a[a > 0]
+                    if nz.size:
+                        m = float(nz.min())
+                        low = m if low == 0 else min(low, m)
+            hit = self._abs_bounds[column] = (b, low, nonfinite)
+        return hit
 
     def data_type(self, column: str) -> str:
         return self.segments[0].columns[column].data_type
@@ -854,8 +894,8 @@ class CPlan:
                     aggs[i].key_cardinality = ks.cardinality
                     aggs[i].key_base = ks.base
                 if ag.function in ("SUM", "AVG"):
-                    aggs[i].sum_exp, nonfinite = sum_bound(table, e)
-                    aggs[i].sum_flags = abi.PG_SUM_NONFINITE if nonfinite else 0
+                    aggs[i].sum_exp, aggs[i].sum_exp_lo, nonfinite = sum_bound(table, e)
+                    aggs[i].sum_flags = abi.PG_SUM_BOUNDS | (abi.PG_SUM_NONFINITE if nonfinite else 0)
         self._keep.append(aggs)
         keys = (abi.pg_key * max(len(query.group_by), 1))()
         self.key_spaces = []
@@ -892,6 +932,11 @@ class CPlan:
         if gt is not None and gt.ordered and gt.server_size is not None and gt.threshold < MAX_TRIM_THRESHOLD:
             p.trim_threshold = gt.threshold   # flags PG_RESULT_TRIM_THRESHOLD_REACHED when the merge reaches it
         size, exact = query.limit, False
+        if query.having is not None and query.order_by:
+            # HAVING runs after this cut (reduce_to_rows): keep the broker's table capacity so that groups failing
+            # HAVING cannot take LIMIT slots -- GroupByDataTableReducer keeps getTableCapacity(limit) sorted records and
+            # walks them until `limit` rows pass HAVING (:148-165)
+            size = table_capacity(query.limit, 5000)
         if trim == "server":   # the reference server's IndexedTable result (group_trim); every group when trim is off
             size, exact = group_trim(query, config).server_size, True
         elif not isinstance(trim, bool) and isinstance(trim, int):   # an explicit exact size (per-segment trims)
@@ -915,30 +960,34 @@ class CPlan:
             p.order = order
         self.plan = p
         self.ops = ops
+        # the shared image is built once (under the lock: cached plans are shared by threads); every thread gets its own
+        # copy, whose header carries that call's scalars
         self._image = None
+        self._image_lock = threading.Lock()
+        self._tls = threading.local()
 
-    def image(self) -> np.ndarray:
+    def image(self, query_id: Optional[int] = None, deadline_ms: Optional[int] = None) -> Tuple[np.ndarray, int]:
         """The plan as one relocatable byte image (pg_image_header + arrays at offsets, include/pinot_gpu.h): what a
-        Java GpuPlanMaker fills in a direct ByteBuffer.  Built once per plan; each calling thread gets its own copy, whose
-        header carries the per-call scalars (query id, deadline, flags, limits) -- two threads running the same plan
-        with different query ids or deadlines never see each other's values.  `image_addr` is the calling thread's."""
+        Java GpuPlanMaker fills in a direct ByteBuffer, and its address.  Built once per plan; each calling thread gets
+        its own copy, whose header carries the per-call scalars -- query id and deadline as passed here (default: the
+        plan's own fields), flags and limits from the plan -- so two threads running one cached plan with different
+        query ids or deadlines never see each other's values."""
         if self._image is None:
-            self._image = abi.build_image(self.plan)
-            self._tls = threading.local()
+            with self._image_lock:
+                if self._image is None:
+                    self._image = abi.build_image(self.plan)
         t = self._tls
         if getattr(t, "image", None) is None:
             t.image = self._image.copy()
             t.header = abi.pg_image_header.from_buffer(t.image)
             t.addr = t.image.ctypes.data  # stable while the copy lives (ndarray.ctypes costs ~3 us a call)
-        h, p = t.header, self.plan  # the per-call scalars a caller may set on the plan (cancel id, deadline)
-        h.query_id, h.deadline_ms, h.flags, h.limit = p.query_id, p.deadline_ms, p.flags, p.limit
+        h, p = t.header, self.plan
+        h.query_id = p.query_id if query_id is None else query_id
+        h.deadline_ms = p.deadline_ms if deadline_ms is None else deadline_ms
+        h.flags, h.limit = p.flags, p.limit
         h.num_groups_limit = p.num_groups_limit
         h.trim_threshold = min(p.trim_threshold, 0xFFFFFFFF)
-        return t.image
-
-    @property
-    def image_addr(self) -> int:
-        return self._tls.addr
+        return t.image, t.addr
 
     @staticmethod
     def _batched_in_ids(preds, segments, seg_keys, cid, id_sets) -> dict:

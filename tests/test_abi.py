@@ -89,10 +89,10 @@ def test_oracle_is_not_linked_into_product():
 def image_from_bytes(**over):
     """A one-segment plan image written with struct.pack alone -- offsets, no pointers -- as a Java GpuPlanMaker fills a
     direct ByteBuffer with putInt / putLong: SELECT COUNT(*) WHERE col0 IN (dictIds 1, 3) over segment key 7.
-    header @0 (120 B) | segment @120 (24 B) | leaf @144 (88 B) | ops @232 | agg @240 (40 B) | ids @280 (2 x int32)."""
+    header @0 (120 B) | segment @120 (24 B) | leaf @144 (88 B) | ops @232 | agg @240 (48 B) | ids @288 (2 x int32)."""
     import struct
-    f = dict(magic=abi.PG_IMAGE_MAGIC, abi=abi.PG_ABI_VERSION, n=288, segments_off=120, leaves_off=144, ops_off=232,
-             aggs_off=240, ids_off=280, num_ids=2, num_segments=1)
+    f = dict(magic=abi.PG_IMAGE_MAGIC, abi=abi.PG_ABI_VERSION, n=296, segments_off=120, leaves_off=144, ops_off=232,
+             aggs_off=240, ids_off=288, num_ids=2, num_segments=1)
     f.update(over)
     b = struct.pack("<IIQ8I4Q5Q", f["magic"], f["abi"], f["n"], f["num_segments"], 1, 1, 1, 0, 0, 0, 0,
                     0, 0, 0, 0, f["segments_off"], f["ops_off"], f["aggs_off"], 0, 0)
@@ -100,9 +100,9 @@ def image_from_bytes(**over):
     b += struct.pack("<4I2iQ2q2d2IQ2I", abi.PG_LEAF_SV_SCAN, 0, 0, f["num_ids"], 0, 0, f["ids_off"], 0, 0, 0.0, 0.0,
                      0, 0, 0, 0, 0)
     b += struct.pack("<i", 0) + bytes(4)
-    b += struct.pack("<6Iqi4x", abi.PG_AGG_COUNT, 0, 0, 0, 0, 0, 0, 0)
+    b += struct.pack("<6IqiIiI", abi.PG_AGG_COUNT, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
     b += struct.pack("<2i", 1, 3)
-    assert len(b) == 288
+    assert len(b) == 296
     return b
 
 
@@ -123,14 +123,14 @@ def test_plan_image_from_python_bytes():
     lib = abi.declare(C.CDLL(LIB))
     rc, msg = _run_image(lib, image_from_bytes())
     assert rc == abi.PG_E_STATE, msg
-    bad = [dict(magic=0x1234), dict(abi=abi.PG_ABI_VERSION - 1), dict(n=296), dict(segments_off=272),
-           dict(segments_off=121), dict(leaves_off=250), dict(ids_off=282), dict(ids_off=284),
+    bad = [dict(magic=0x1234), dict(abi=abi.PG_ABI_VERSION - 1), dict(n=304), dict(segments_off=280),
+           dict(segments_off=121), dict(leaves_off=250), dict(ids_off=290), dict(ids_off=292),
            dict(num_ids=0), dict(ops_off=4), dict(aggs_off=256), dict(num_segments=2)]
     for over in bad:
         b = image_from_bytes(**over)
         if "n" in over:
             b = b + bytes(over["n"] - len(b))
-            b = b[:len(b) - 8]  # header says 296, the buffer holds 288
+            b = b[:len(b) - 8]  # header says 304, the buffer holds 296
         rc, msg = _run_image(lib, b)
         assert rc == abi.PG_E_INVALID and msg.startswith("image"), (over, rc, msg)
     rc, msg = _run_image(lib, image_from_bytes(), shift=4)
@@ -160,7 +160,7 @@ def test_plan_image_of_a_lowered_plan(sv_segment):
         out[:, :len(row)] = row
         return out, np.full(len(keys), len(row), dtype=np.uint32)
     cp = CPlan(t, q, t.segments, [11, 12, 13], trim="server", id_sets=id_sets)
-    im = cp.image()
+    im, _ = cp.image()
     h = abi.pg_image_header.from_buffer_copy(im.tobytes()[:C.sizeof(abi.pg_image_header)])
     assert (h.magic, h.num_segments, h.num_leaves, h.image_bytes) == (abi.PG_IMAGE_MAGIC, 3, 2, im.size)
     assert h.flags & abi.PG_PLAN_EXACT_LIMIT and h.limit == 5000 and h.num_order == 1

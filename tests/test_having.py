@@ -105,6 +105,9 @@ def test_device_having(sql, gpu_engine, oracle_engine):
     t_all = Table("t", segs)
     assert_same_result(gpu_engine.execute(t_all, q), oracle_engine.execute(t_all, q), table=t_all)
     want = reduce_to_rows(q, oracle_engine.execute(t_all, q))
+    # trim=True (the final single-server answer): the device's ORDER BY cut keeps the broker's table capacity when
+    # HAVING follows it, so groups failing HAVING never take LIMIT slots
+    assert reduce_to_rows(q, gpu_engine.execute(t_all, q, trim=True))[:2] == want
     tables = []
     for part in (segs[:2], segs[2:]):
         t = Table("t", part)
