@@ -51,9 +51,8 @@ def wide_segments(n=40_000, big_values=(1e30, float(np.finfo(np.float64).max))):
 
 
 @pytest.fixture(scope="module")
-def engine():
-    from pinot_amd.gpu import GpuEngine
-    return GpuEngine(0)
+def engine(gpu_engine):
+    return gpu_engine
 
 
 @pytest.mark.parametrize("sql", QUERIES)
