@@ -214,11 +214,17 @@ def declare(lib):
     return lib
 
 
-def build_image(plan: pg_plan) -> "np.ndarray":
+def build_image(plan: pg_plan, leaf_table=None, regions=()) -> "np.ndarray":
     """The relocatable image (include/pinot_gpu.h, pg_image_header) of a pointer-form pg_plan: every array the plan
     points to copied into one 8-byte-aligned buffer at a byte offset; an array several segments share (values-mode IN
-    literals) is stored once.  Returns a uint8 view of length image_bytes."""
+    literals) is stored once.  Returns a uint8 view of length image_bytes.
+
+    leaf_table: the plan's leaves as ONE [segment][leaf] array in pg_leaf's layout (CPlan), with `regions` = every
+    numpy array its ids / values pointers point into: then the table is copied whole, each region once, and the
+    pointers are turned into offsets with a few vectorized operations instead of a loop over the segments."""
     import numpy as np
+    if leaf_table is not None and plan.num_segments:
+        return _build_image_table(plan, leaf_table, regions)
     buf = bytearray(C.sizeof(pg_image_header))
     placed = {}
     keep = []  # temporaries stay alive while `placed` is keyed by their addresses
@@ -268,4 +274,80 @@ def build_image(plan: pg_plan) -> "np.ndarray":
     buf[:C.sizeof(h)] = bytes(h)
     out = np.empty(len(buf) // 8, dtype=np.uint64).view(np.uint8)
     out[:] = np.frombuffer(bytes(buf), dtype=np.uint8)
+    return out
+
+
+def _build_image_table(plan: pg_plan, tab, regions) -> "np.ndarray":
+    import numpy as np
+    S, L = plan.num_segments, plan.num_leaves
+    parts = [bytes(C.sizeof(pg_image_header))]
+    size = len(parts[0])
+
+    def put(b: bytes, align=8) -> int:
+        nonlocal size
+        pad = -size % align
+        if pad:
+            parts.append(bytes(pad))
+            size += pad
+        off = size
+        parts.append(b)
+        size += len(b)
+        return off
+
+    def addr_of(ptr):
+        return C.cast(ptr, C.c_void_p).value
+
+    h = pg_image_header()
+    h.magic, h.abi_version = PG_IMAGE_MAGIC, plan.abi_version
+    for f in ("num_segments", "num_leaves", "num_ops", "num_aggs", "num_keys", "num_order", "flags",
+              "num_groups_limit", "query_id", "deadline_ms", "limit"):
+        setattr(h, f, getattr(plan, f))
+    h.trim_threshold = min(plan.trim_threshold, 0xFFFFFFFF)
+    h.ops_off = put(C.string_at(addr_of(plan.ops), 4 * plan.num_ops), 4) if plan.num_ops else 0
+    h.aggs_off = put(C.string_at(addr_of(plan.aggs), C.sizeof(pg_agg) * plan.num_aggs)) if plan.num_aggs else 0
+    h.keys_off = put(C.string_at(addr_of(plan.keys), C.sizeof(pg_key) * plan.num_keys)) if plan.num_keys else 0
+    h.order_off = put(C.string_at(addr_of(plan.order), C.sizeof(pg_order) * plan.num_order), 4) if plan.num_order else 0
+    # every region the leaves point into, once (8-byte aligned): regions sorted by address, each pointer's region
+    # found by a search, only the regions some leaf points into copied, then the pointers rewritten as offsets
+    regs = [a for _, a in sorted({int(a.ctypes.data): a for a in regions if a.nbytes}.items())]
+    starts = np.array([a.ctypes.data for a in regs], dtype=np.uint64)
+    ends = starts + np.array([a.nbytes for a in regs], dtype=np.uint64)
+    lt = np.array(tab[:S, :max(L, 1)], copy=True)  # pg_image_leaf has pg_leaf's layout with offsets for pointers
+    found = {}
+    for f, nb in (("ids", 4), ("values", 8)):
+        ptr = lt[f]
+        nz = ptr != 0
+        if not nz.any():
+            continue
+        i = np.searchsorted(starts, ptr[nz], side="right").astype(np.int64) - 1
+        n = lt["num_ids"][nz].astype(np.uint64)
+        if f == "values":
+            nv = lt["num_values"][nz].astype(np.uint64)
+            n = np.where(nv > 0, nv, n)
+        if (i < 0).any() or (ptr[nz] + n * nb > ends[np.maximum(i, 0)]).any():
+            raise ValueError(f"leaf {f} pointer outside the plan's arrays")
+        found[f] = (nz, i)
+    used = np.unique(np.concatenate([x[1] for x in found.values()])) if found else np.zeros(0, np.int64)
+    offs = np.zeros(len(regs), dtype=np.uint64)
+    for r in used:
+        offs[r] = put(np.ascontiguousarray(regs[r]).tobytes())
+    for f, (nz, i) in found.items():
+        ptr = lt[f]
+        ptr[nz] = offs[i] + (ptr[nz] - starts[i])
+    leaves_off = put(lt.tobytes()) if L else 0
+    segs = (pg_image_segment * S)()
+    st = np.frombuffer(segs, dtype=[("seg_key", "<u8"), ("num_docs", "<u4"), ("pad", "<u4"), ("leaves_off", "<u8")])
+    src = (pg_segment_ref * S).from_address(addr_of(plan.segments))
+    sr = np.frombuffer(src, dtype=[("seg_key", "<u8"), ("num_docs", "<u4"), ("pad", "<u4"), ("leaves", "<u8")])
+    st["seg_key"], st["num_docs"] = sr["seg_key"], sr["num_docs"]
+    st["leaves_off"] = (leaves_off + np.arange(S, dtype=np.uint64) * (max(L, 1) * C.sizeof(pg_image_leaf))) if L else 0
+    h.segments_off = put(bytes(segs))
+    pad = -size % 8
+    if pad:
+        parts.append(bytes(pad))
+        size += pad
+    h.image_bytes = size
+    parts[0] = bytes(h)
+    out = np.empty(size // 8, dtype=np.uint64).view(np.uint8)
+    out[:] = np.frombuffer(b"".join(parts), dtype=np.uint8)
     return out

@@ -127,15 +127,11 @@ struct IdxSpec {
   uint32_t cntmv_slot;              // i64 slot of COUNTMV (~0: none)
   const IdxSeg* segs;
   const IdxLeaf* leaves;            // [num_segs][num_leaves]
-  const uint32_t* blk_seg;          // unit -> its segment (a unit: one (segment, 64 K-doc key))
+  const uint32_t* blk_seg;          // block -> its segment
   unsigned long long* i64;          // slot 0: doc count
   unsigned long long* seg_matched;  // [num_segs]
-  unsigned int* next_unit;          // persistent grid: the units' claim counter (zero before the launch)
-  uint32_t num_units, pad;
 };
-// A persistent grid of at most the resident block slots; each block claims (segment, key) units from next_unit until
-// none is left (the last round of a one-block-per-unit grid was half empty: 1 568 units over 1 024 slots)
-hipError_t launch_index_count(const IdxSpec& p, uint32_t units, hipStream_t s);
+hipError_t launch_index_count(const IdxSpec& p, uint32_t blocks, hipStream_t s);
 // COUNTMV's count column of an MV forward index: 4 bits per doc (min(count, 15)); *over set when a count exceeds 15
 hipError_t launch_mv_counts(const uint32_t* offsets, uint32_t num_docs, uint32_t* out, unsigned int* over, hipStream_t s);
 hipError_t launch_mv_scan(const uint32_t* words, uint32_t bits, const uint32_t* offsets, uint32_t num_docs,

@@ -13,7 +13,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdlib>
 
 #include "pg_aux.h"
 #include "pg_roaring.h"
@@ -59,162 +58,152 @@ __global__ __launch_bounds__(kIdxNT, PG_IDX_WAVES) void index_count_kernel(IdxSp
   __shared__ uint4 D[kIdxMaxLeaves];  // leaf l for the filter: (kind | negate << 8, lo, hi, chunk word offset)
   __shared__ uint32_t nv;
   __shared__ unsigned long long red[2][kIdxNT / 64];
-  __shared__ uint32_t unit_s;
   static_assert(kIdxMaxLeaves <= kRoarMaxViews && kIdxMaxLeaves <= 64, "one view per inverted leaf");
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long t_ = PG_IDX_PROF ? prof_clk() : 0ull;
   const unsigned long long w0 = PG_IDX_PROF ? wall_clock64() : 0ull;
-  // persistent: the block's first unit is its index, the next ones are claimed from the counter (every block leaves
-  // once the counter passes num_units, so the grid drains)
-  uint32_t unit = blockIdx.x;
-  for (;;) {
-    if (unit >= p.num_units) break;
-    // the unit's segment from the host's unit -> segment table (one load), then its descriptor and its leaves' (in
-    // parallel: the leaves are [segment][leaf] in one array)
-    const uint32_t si = ld_global(p.blk_seg + unit);
-    const IdxSeg G = ld_global(p.segs + si);
-    IdxLeaf L{};
-    if (tid < p.num_leaves) L = ld_global(p.leaves + (uint64_t)si * p.num_leaves + tid);
-    const uint32_t key = G.key0 + (unit - G.first_block);
-    const uint32_t nd = G.num_docs;
-    // COUNTMV from the 4-bit count column: this thread's count words of all its chunk words are loaded up front, before
-    // the decode (they do not depend on it: one latency hidden under the directory loads; most words hold a match at
-    // config 5's 5.6 % pass).  Unconditional loads (a word past the segment reads word 0): a select between a load and
-    // zero would wait for the load right here.
-    constexpr uint32_t kWpt = 2048u / kIdxNT;
-    uint4 cwp[kWpt];
+  // the block's segment from the host's block -> segment table (one load), then its descriptor and its leaves' (in
+  // parallel: the leaves are [segment][leaf] in one array)
+  const uint32_t si = ld_global(p.blk_seg + blockIdx.x);
+  const IdxSeg G = ld_global(p.segs + si);
+  IdxLeaf L{};
+  if (tid < p.num_leaves) L = ld_global(p.leaves + (uint64_t)si * p.num_leaves + tid);
+  const uint32_t key = G.key0 + (blockIdx.x - G.first_block);
+  const uint32_t nd = G.num_docs;
+  // COUNTMV from the 4-bit count column: this thread's count words of all its chunk words are loaded up front, before
+  // the decode (they do not depend on it: one latency hidden under the directory loads; most words hold a match at
+  // config 5's 5.6 % pass).  Unconditional loads (a word past the segment reads word 0): a select between a load and
+  // zero would wait for the load right here.
+  constexpr uint32_t kWpt = 2048u / kIdxNT;
+  uint4 cwp[kWpt];
 #pragma unroll
-    for (uint32_t k = 0; k < kWpt; k++) cwp[k] = make_uint4(0u, 0u, 0u, 0u);
-    auto load_counts = [&]() {
-      if (p.cntmv_slot != 0xFFFFFFFFu && G.mv_cnt && !(PG_IDX_SKIP & 8)) {
+  for (uint32_t k = 0; k < kWpt; k++) cwp[k] = make_uint4(0u, 0u, 0u, 0u);
+  auto load_counts = [&]() {
+    if (p.cntmv_slot != 0xFFFFFFFFu && G.mv_cnt && !(PG_IDX_SKIP & 8)) {
 #pragma unroll
-        for (uint32_t k = 0; k < kWpt; k++) {
-          const uint64_t d0 = (uint64_t)key * 65536u + 32u * (tid + k * kIdxNT);
-          cwp[k] = ld_global((const uint4*)(G.mv_cnt + (d0 < nd ? d0 / 8 : 0)));
-        }
+      for (uint32_t k = 0; k < kWpt; k++) {
+        const uint64_t d0 = (uint64_t)key * 65536u + 32u * (tid + k * kIdxNT);
+        cwp[k] = ld_global((const uint4*)(G.mv_cnt + (d0 < nd ? d0 / 8 : 0)));
       }
-    };
-    if (!PG_IDX_LATE_COUNT) load_counts();
-    for (uint32_t w = tid; w < p.num_chunks * 512u; w += kIdxNT) ((uint4*)chunks)[w] = make_uint4(0u, 0u, 0u, 0u);
-    // every inverted leaf of the segment, decoded together into its chunk: the views compacted by wave 0
-    if (tid < 64) {
-      const bool on = tid < p.num_leaves && L.kind == IL_ROARING && L.nids;
-      const unsigned long long b = __ballot(on);
-      if (on) {
-        const uint32_t at = (uint32_t)__popcll(b & ((1ull << tid) - 1ull));
-        V[at] = RoarView{L.roaring, L.cs, L.dir, L.keydir, L.ids, p.chunk_of[tid] * 2048u, L.nids, L.card};
-      }
-      if (tid < p.num_leaves)
-        D[tid] = make_uint4(L.kind | L.negate << 8, (uint32_t)L.lo, (uint32_t)L.hi,
-                            L.kind == IL_ROARING ? p.chunk_of[tid] * 2048u : 0u);
-      if (tid == 0) nv = (uint32_t)__popcll(b);
     }
-    lds_barrier();
-    if (PG_IDX_PROF && tid == 0) { const unsigned long long n_ = prof_clk(); prof[0] += n_ - t_; t_ = n_; }
-    roaring_key_chunks<kIdxNT>(V, nv, key, S, chunks, PG_IDX_PROF ? prof : nullptr);
-    if (PG_IDX_PROF && tid == 0) t_ = prof_clk();
-    if (PG_IDX_LATE_COUNT) load_counts();
-    // the filter over this thread's kWpt chunk words at once: wave-uniform loops over the (at most two-level) item list,
-    // each leaf's descriptor read once per item (an LDS broadcast), not once per word
-    const int64_t dbase = (int64_t)key * 65536 + 32 * (int64_t)tid;  // doc of word 0's bit 31; word k: + 32 k NT
-    auto leafw = [&](uint32_t l, uint32_t* out) {
-      const uint4 d = D[l];
-      const uint32_t kind = d.x & 0xFFu;
-      if (kind == IL_ROARING) {
-        const uint32_t neg = (d.x >> 8) ? 0xFFFFFFFFu : 0u;
+  };
+  if (!PG_IDX_LATE_COUNT) load_counts();
+  for (uint32_t w = tid; w < p.num_chunks * 512u; w += kIdxNT) ((uint4*)chunks)[w] = make_uint4(0u, 0u, 0u, 0u);
+  // every inverted leaf of the segment, decoded together into its chunk: the views compacted by wave 0
+  if (tid < 64) {
+    const bool on = tid < p.num_leaves && L.kind == IL_ROARING && L.nids;
+    const unsigned long long b = __ballot(on);
+    if (on) {
+      const uint32_t at = (uint32_t)__popcll(b & ((1ull << tid) - 1ull));
+      V[at] = RoarView{L.roaring, L.cs, L.dir, L.keydir, L.ids, p.chunk_of[tid] * 2048u, L.nids, L.card};
+    }
+    if (tid < p.num_leaves)
+      D[tid] = make_uint4(L.kind | L.negate << 8, (uint32_t)L.lo, (uint32_t)L.hi,
+                          L.kind == IL_ROARING ? p.chunk_of[tid] * 2048u : 0u);
+    if (tid == 0) nv = (uint32_t)__popcll(b);
+  }
+  lds_barrier();
+  if (PG_IDX_PROF && tid == 0) { const unsigned long long n_ = prof_clk(); prof[0] += n_ - t_; t_ = n_; }
+  roaring_key_chunks<kIdxNT>(V, nv, key, S, chunks, PG_IDX_PROF ? prof : nullptr);
+  if (PG_IDX_PROF && tid == 0) t_ = prof_clk();
+  if (PG_IDX_LATE_COUNT) load_counts();
+  // the filter over this thread's kWpt chunk words at once: wave-uniform loops over the (at most two-level) item list,
+  // each leaf's descriptor read once per item (an LDS broadcast), not once per word
+  const int64_t dbase = (int64_t)key * 65536 + 32 * (int64_t)tid;  // doc of word 0's bit 31; word k: + 32 k NT
+  auto leafw = [&](uint32_t l, uint32_t* out) {
+    const uint4 d = D[l];
+    const uint32_t kind = d.x & 0xFFu;
+    if (kind == IL_ROARING) {
+      const uint32_t neg = (d.x >> 8) ? 0xFFFFFFFFu : 0u;
 #pragma unroll
-        for (uint32_t k = 0; k < kWpt; k++) out[k] = chunks[d.w + tid + k * kIdxNT] ^ neg;
-      } else if (kind == IL_DOCRANGE) {
+      for (uint32_t k = 0; k < kWpt; k++) out[k] = chunks[d.w + tid + k * kIdxNT] ^ neg;
+    } else if (kind == IL_DOCRANGE) {
 #pragma unroll
-        for (uint32_t k = 0; k < kWpt; k++) {
-          const int64_t d0 = dbase + 32 * (int64_t)(k * kIdxNT);
-          out[k] = word_range((int64_t)(int32_t)d.y - d0, (int64_t)(int32_t)d.z - d0);
+      for (uint32_t k = 0; k < kWpt; k++) {
+        const int64_t d0 = dbase + 32 * (int64_t)(k * kIdxNT);
+        out[k] = word_range((int64_t)(int32_t)d.y - d0, (int64_t)(int32_t)d.z - d0);
+      }
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < kWpt; k++) out[k] = kind == IL_ALL ? 0xFFFFFFFFu : 0u;
+    }
+  };
+  uint32_t m[kWpt];
+#pragma unroll
+  for (uint32_t k = 0; k < kWpt; k++) m[k] = p.root_or ? 0u : 0xFFFFFFFFu;
+  for (uint32_t i = 0; i < p.num_items; i++) {
+    const uint32_t it = p.item[i];
+    uint32_t v[kWpt];
+    if (it & 0x40000000u) {
+      const uint32_t g = it & 0xFFu;
+      const bool gor = p.group_or[g] != 0;
+#pragma unroll
+      for (uint32_t k = 0; k < kWpt; k++) v[k] = gor ? 0u : 0xFFFFFFFFu;
+      for (uint32_t j = 0; j < p.gn[g]; j++) {
+        const uint32_t gl = p.gleaf[p.gfirst[g] + j];
+        uint32_t x[kWpt];
+        leafw(gl & 0xFFu, x);
+        const uint32_t neg = (gl & 0x80000000u) ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < kWpt; k++) v[k] = gor ? (v[k] | (x[k] ^ neg)) : (v[k] & (x[k] ^ neg));
+      }
+    } else {
+      leafw(it & 0xFFu, v);
+    }
+    const uint32_t neg = (it & 0x80000000u) ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < kWpt; k++) m[k] = p.root_or ? (m[k] | (v[k] ^ neg)) : (m[k] & (v[k] ^ neg));
+  }
+  unsigned long long cnt = 0, cmv = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kWpt; k++) {
+    const uint64_t d0 = (uint64_t)key * 65536u + 32u * (tid + k * kIdxNT);
+    const uint32_t valid = d0 >= nd ? 0u : d0 + 32 <= nd ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (uint32_t)(nd - d0));
+    const uint32_t mk = m[k] & valid;
+    cnt += (uint32_t)__popc(mk);
+    if (p.cntmv_slot != 0xFFFFFFFFu && mk && !(PG_IDX_SKIP & 8)) {
+      if (G.mv_cnt) {  // 4-bit counts: docs d0 .. d0 + 31 are the 4 count words at d0 / 8
+        // count word q holds docs 8 q + j at nibble 7 - j; mask byte (mk >> 24 - 8 q) holds them at bit 7 - j: spread
+        // the byte's bit i to nibble i, mask the counts with it, add the nibbles (no per-doc loop, no divergence)
+        const uint4 cw = cwp[k];
+        const uint32_t c4[4] = {cw.x, cw.y, cw.z, cw.w};
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+          uint32_t x = (mk >> (24u - 8u * q)) & 0xFFu;
+          x = (x | (x << 12)) & 0x000F000Fu;
+          x = (x | (x << 6)) & 0x03030303u;
+          x = (x | (x << 3)) & 0x11111111u;
+          const uint32_t v = c4[q] & (x * 15u);
+          const uint32_t b = (v & 0x0F0F0F0Fu) + ((v >> 4) & 0x0F0F0F0Fu);
+          cmv += (b * 0x01010101u) >> 24;
         }
       } else {
-#pragma unroll
-        for (uint32_t k = 0; k < kWpt; k++) out[k] = kind == IL_ALL ? 0xFFFFFFFFu : 0u;
-      }
-    };
-    uint32_t m[kWpt];
-#pragma unroll
-    for (uint32_t k = 0; k < kWpt; k++) m[k] = p.root_or ? 0u : 0xFFFFFFFFu;
-    for (uint32_t i = 0; i < p.num_items; i++) {
-      const uint32_t it = p.item[i];
-      uint32_t v[kWpt];
-      if (it & 0x40000000u) {
-        const uint32_t g = it & 0xFFu;
-        const bool gor = p.group_or[g] != 0;
-#pragma unroll
-        for (uint32_t k = 0; k < kWpt; k++) v[k] = gor ? 0u : 0xFFFFFFFFu;
-        for (uint32_t j = 0; j < p.gn[g]; j++) {
-          const uint32_t gl = p.gleaf[p.gfirst[g] + j];
-          uint32_t x[kWpt];
-          leafw(gl & 0xFFu, x);
-          const uint32_t neg = (gl & 0x80000000u) ? 0xFFFFFFFFu : 0u;
-#pragma unroll
-          for (uint32_t k = 0; k < kWpt; k++) v[k] = gor ? (v[k] | (x[k] ^ neg)) : (v[k] & (x[k] ^ neg));
-        }
-      } else {
-        leafw(it & 0xFFu, v);
-      }
-      const uint32_t neg = (it & 0x80000000u) ? 0xFFFFFFFFu : 0u;
-#pragma unroll
-      for (uint32_t k = 0; k < kWpt; k++) m[k] = p.root_or ? (m[k] | (v[k] ^ neg)) : (m[k] & (v[k] ^ neg));
-    }
-    unsigned long long cnt = 0, cmv = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kWpt; k++) {
-      const uint64_t d0 = (uint64_t)key * 65536u + 32u * (tid + k * kIdxNT);
-      const uint32_t valid = d0 >= nd ? 0u : d0 + 32 <= nd ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (uint32_t)(nd - d0));
-      const uint32_t mk = m[k] & valid;
-      cnt += (uint32_t)__popc(mk);
-      if (p.cntmv_slot != 0xFFFFFFFFu && mk && !(PG_IDX_SKIP & 8)) {
-        if (G.mv_cnt) {  // 4-bit counts: docs d0 .. d0 + 31 are the 4 count words at d0 / 8
-          // count word q holds docs 8 q + j at nibble 7 - j; mask byte (mk >> 24 - 8 q) holds them at bit 7 - j: spread
-          // the byte's bit i to nibble i, mask the counts with it, add the nibbles (no per-doc loop, no divergence)
-          const uint4 cw = cwp[k];
-          const uint32_t c4[4] = {cw.x, cw.y, cw.z, cw.w};
-#pragma unroll
-          for (uint32_t q = 0; q < 4; q++) {
-            uint32_t x = (mk >> (24u - 8u * q)) & 0xFFu;
-            x = (x | (x << 12)) & 0x000F000Fu;
-            x = (x | (x << 6)) & 0x03030303u;
-            x = (x | (x << 3)) & 0x11111111u;
-            const uint32_t v = c4[q] & (x * 15u);
-            const uint32_t b = (v & 0x0F0F0F0Fu) + ((v >> 4) & 0x0F0F0F0Fu);
-            cmv += (b * 0x01010101u) >> 24;
-          }
-        } else {
-          for (uint32_t r = mk; r; ) {
-            const uint32_t j = (uint32_t)__builtin_clz(r);
-            r &= ~(0x80000000u >> j);
-            cmv += ld_global(G.mv_offsets + d0 + j + 1) - ld_global(G.mv_offsets + d0 + j);
-          }
+        for (uint32_t r = mk; r; ) {
+          const uint32_t j = (uint32_t)__builtin_clz(r);
+          r &= ~(0x80000000u >> j);
+          cmv += ld_global(G.mv_offsets + d0 + j + 1) - ld_global(G.mv_offsets + d0 + j);
         }
       }
     }
-    if (PG_IDX_PROF && tid == 0) { const unsigned long long n_ = prof_clk(); prof[5] += n_ - t_; t_ = n_; }
-    // block sums -> one atomic per value
+  }
+  if (PG_IDX_PROF && tid == 0) { const unsigned long long n_ = prof_clk(); prof[5] += n_ - t_; t_ = n_; }
+  // block sums -> one atomic per value
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      cnt += __shfl_down(cnt, o);
-      cmv += __shfl_down(cmv, o);
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += __shfl_down(cnt, o);
+    cmv += __shfl_down(cmv, o);
+  }
+  if (lane == 0) { red[0][wave] = cnt; red[1][wave] = cmv; }
+  lds_barrier();
+  if (tid == 0) {
+    unsigned long long c = 0, v = 0;
+    for (uint32_t k = 0; k < kIdxNT / 64; k++) { c += red[0][k]; v += red[1][k]; }
+    if (c) {
+      atomicAdd(&p.i64[0], c);
+      atomicAdd(&p.seg_matched[si], c);
+      if (p.cntmv_slot != 0xFFFFFFFFu) atomicAdd(&p.i64[p.cntmv_slot], v);
     }
-    if (lane == 0) { red[0][wave] = cnt; red[1][wave] = cmv; }
-    lds_barrier();
-    if (tid == 0) {
-      unsigned long long c = 0, v = 0;
-      for (uint32_t k = 0; k < kIdxNT / 64; k++) { c += red[0][k]; v += red[1][k]; }
-      if (c) {
-        atomicAdd(&p.i64[0], c);
-        atomicAdd(&p.seg_matched[si], c);
-        if (p.cntmv_slot != 0xFFFFFFFFu) atomicAdd(&p.i64[p.cntmv_slot], v);
-      }
-      unit_s = gridDim.x + atomicAdd(p.next_unit, 1u);  // the next unit (the first gridDim.x are the blocks' own)
-    }
-    lds_barrier();  // unit_s published; every LDS read of this unit (chunks, red, views) is done
-    unit = unit_s;
   }
 #if PG_IDX_PROF
   if (tid == 0) {
@@ -228,8 +217,8 @@ __global__ __launch_bounds__(kIdxNT, PG_IDX_WAVES) void index_count_kernel(IdxSp
 #endif
 }
 
-hipError_t launch_index_count(const IdxSpec& p, uint32_t units, hipStream_t s) {
-  if (!units) return hipSuccess;
+hipError_t launch_index_count(const IdxSpec& p, uint32_t blocks, hipStream_t s) {
+  if (!blocks) return hipSuccess;
 #ifndef PG_IDX_LDS_PAD  // dev: extra dynamic LDS per block (fewer blocks per CU: the contention experiment)
 #define PG_IDX_LDS_PAD 0
 #endif
@@ -242,21 +231,6 @@ hipError_t launch_index_count(const IdxSpec& p, uint32_t units, hipStream_t s) {
       attr = true;
     }
   }
-  // the grid: the resident block slots (blocks per CU at this LDS size x CUs), or fewer when there are fewer units
-  static int num_cus = 0;
-  if (!num_cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || num_cus <= 0)
-      num_cus = 256;
-  }
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, index_count_kernel, kIdxNT, lds) != hipSuccess || per_cu <= 0)
-    per_cu = 1;
-  static const int cap_env = getenv("PG_IDX_GRID") ? atoi(getenv("PG_IDX_GRID")) : 0;  // dev: a fixed grid size
-  uint32_t blocks = (uint32_t)per_cu * (uint32_t)num_cus;
-  if (cap_env > 0) blocks = (uint32_t)cap_env;
-  if (blocks > units) blocks = units;
   hipLaunchKernelGGL(index_count_kernel, dim3(blocks), dim3(kIdxNT), lds, s, p);
 #if PG_IDX_PROF
   {
@@ -265,8 +239,8 @@ hipError_t launch_index_count(const IdxSpec& p, uint32_t units, hipStream_t s) {
     (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
     if (hipDeviceSynchronize() == hipSuccess && hipMemcpyFromSymbol(h, HIP_SYMBOL(g_idx_prof), sizeof(h)) == hipSuccess &&
         hipMemcpyFromSymbol(sp, HIP_SYMBOL(g_idx_span), sizeof(sp)) == hipSuccess) {
-      fprintf(stderr, "[idx_prof] units=%u blocks=%u lds=%zu per-unit kcycles:", units, blocks, lds);
-      for (int i = 0; i < 7; i++) fprintf(stderr, " %.2f", h[i] / 1e3 / (double)units);
+      fprintf(stderr, "[idx_prof] blocks=%u lds=%zu per-block kcycles:", blocks, lds);
+      for (int i = 0; i < 7; i++) fprintf(stderr, " %.2f", h[i] / 1e3 / (double)blocks);
       fprintf(stderr, " | block us %.2f | span us %.2f\n", h[7] / (double)blocks / (khz / 1e3),
               (double)(sp[1] - ~sp[0]) / (khz / 1e3));
       memset(h, 0, sizeof(h));

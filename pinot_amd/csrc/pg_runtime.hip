@@ -3247,8 +3247,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   const uint64_t off_rjobs = ar.reserve(rjobs.size() * sizeof(RoaringJob));
   const uint64_t off_ixleaves = ar.reserve(ix.leaves.size() * sizeof(IdxLeaf));
   const uint64_t off_ixsegs = ar.reserve(ix.segs.size() * sizeof(IdxSeg));
-  const uint64_t off_ixblk = ar.reserve(ix.on ? 4ull * ix.blocks : 0ull);  // unit -> segment
-  const uint64_t off_ixnext = ar.reserve(ix.on ? 16ull : 0ull);               // the persistent grid's claim counter
+  const uint64_t off_ixblk = ar.reserve(ix.on ? 4ull * ix.blocks : 0ull);  // block -> segment
   DevBuf arena, scratch;
   DevBuf p_ent0, p_cnt0, p_hist1, p_off1, p_ent1, p_hist2, p_off2, p_ent2, p_temp, p_fill;  // GM_PART pipeline
   DevBuf l_docs, l_counts;  // selective stream: survivor regions + counts
@@ -3336,8 +3335,6 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     for (uint32_t si = 0; si < S; si++)
       for (uint32_t b = ix.segs[si].first_block; b < (si + 1 < S ? ix.segs[si + 1].first_block : ix.blocks); b++) bs[b] = si;
     ix.spec.blk_seg = (const uint32_t*)(dA + off_ixblk);
-    ix.spec.next_unit = (unsigned int*)(dA + off_ixnext);  // zero: reserved in the arena, which the upload copies
-    ix.spec.num_units = ix.blocks;
     ix.spec.i64 = (unsigned long long*)P.i64.p;
     ix.spec.seg_matched = (unsigned long long*)P.seg_matched.p;
   }

@@ -18,7 +18,7 @@ import numpy as np
 from . import abi
 from .plan import (MAX_TRIM_THRESHOLD, CPlan, ExecutionStats, InstanceConfig, IntermediateResult, Table,
                    UnsupportedQuery, execute_filtered, group_trim, has_filtered_aggregations, merge_intermediate,
-                   top_groups)
+                   query_shape, top_groups)
 from .query import QueryContext, parse
 from .segment import Column, ImmutableSegment
 
@@ -96,6 +96,7 @@ class GpuEngine:
         self._plan_lock = threading.Lock()
         self.plan_cache_hits = 0
         self.plan_cache_misses = 0
+        self.plan_shape_hits = 0   # a cached plan of the same shape re-lowered for new filter literals
 
     # ---- residency (IndexingOverrides reader-provider hook)
     def upload_segment(self, seg: ImmutableSegment, table: Table, ldev: Optional[int] = None) -> int:
@@ -199,7 +200,7 @@ class GpuEngine:
             check(self.lib.pg_segment_release(hit[1]))
             self._keymaps_uploaded = {k for k in self._keymaps_uploaded if k[0] != hit[1]}
             with self._plan_lock:  # plans over the released segment can never be hit again (keys are not reused)
-                for ck in [ck for ck in self._plans if hit[1] in ck[2]]:
+                for ck in [ck for ck in self._plans if hit[1] in ck[3]]:
                     del self._plans[ck]
 
     # ---- execution
@@ -220,25 +221,40 @@ class GpuEngine:
     def cached_plan(self, table: Table, sql: str, segments: Optional[Sequence[ImmutableSegment]] = None,
                     flags: int = abi.PG_PLAN_VALUE_SETS, trim=False, config: Optional[InstanceConfig] = None) -> CPlan:
         """make_plan through a compiled-plan cache (LRU, PLAN_CACHE_SIZE plans).  The reference plans every query from
-        scratch (InstancePlanMakerImplV2.makeInstancePlan, ~microseconds of Java per segment); here lowering a query
-        costs the SQL parse, the per-segment literal -> dictId resolution (one device launch) and the plan image, ~2 ms
-        for config 2's 128 segments, so a server answering the same query text again over the same resident segments
-        reuses the lowered plan.  The key pins everything the plan depends on: the SQL text, the table object, the
-        segments' residency keys (a released and re-uploaded segment gets a new key; keys are never reused), flags,
-        trim and the instance config.  A plan is immutable once built (execution reads its image; each thread's copy
-        of the image carries its own per-call scalars, CPlan.image), so reuse is exact."""
+        scratch (InstancePlanMakerImplV2.makeInstancePlan, ~microseconds of Java per segment); here a server answering
+        the same query text again over the same resident segments reuses the lowered plan, and a query of the same
+        SHAPE with other filter literals (query_shape: a parametrised query) reuses everything but the leaves, which
+        CPlan.relower lowers for the new literals.  The key pins everything the plan depends on: the SQL text or the
+        shape, the table object, the segments' residency keys (a released and re-uploaded segment gets a new key; keys
+        are never reused), flags, trim and the instance config.  A plan is immutable once built (execution reads its
+        image; each thread's copy of the image carries its own per-call scalars, CPlan.image), so reuse is exact."""
         segs = list(table.segments if segments is None else segments)
         keys = tuple(self.upload_segment(s, table) for s in segs)
-        ck = (sql, id(table), keys, flags, trim, None if config is None else dataclasses.astuple(config))
+        rest = (id(table), keys, flags, trim, None if config is None else dataclasses.astuple(config))
+        ck = ("sql", sql) + rest
         with self._plan_lock:
             hit = self._plans.get(ck)
             if hit is not None and hit[0] is table:
                 self._plans.move_to_end(ck)
                 self.plan_cache_hits += 1
                 return hit[1]
-        plan = self.make_plan(table, parse(sql), segs, flags, trim, config)
+        q = parse(sql)
+        sk = ("shape", query_shape(q)) + rest
         with self._plan_lock:
-            self.plan_cache_misses += 1
+            shaped = self._plans.get(sk)
+            if shaped is not None and shaped[0] is not table:
+                shaped = None
+        if shaped is not None:
+            plan = shaped[1].relower(q, self.dict_id_sets)
+            self.upload_keymaps(table, plan, segs, list(keys))
+            with self._plan_lock:
+                self.plan_shape_hits += 1
+        else:
+            plan = self.make_plan(table, q, segs, flags, trim, config)
+            with self._plan_lock:
+                self.plan_cache_misses += 1
+                self._plans[sk] = (table, plan)
+        with self._plan_lock:
             self._plans[ck] = (table, plan)
             while len(self._plans) > self.PLAN_CACHE_SIZE:
                 self._plans.popitem(last=False)

@@ -15,6 +15,7 @@ Host-side mirror of the reference's planning for the hot path:
 """
 from __future__ import annotations
 
+import copy
 import ctypes as C
 import itertools
 import math
@@ -281,6 +282,7 @@ class Table:
         self.column_ids = {c: i for i, c in enumerate(cols)}
         self._key_spaces: Dict[str, "KeySpace"] = {}
         self._abs_bounds: Dict[str, Tuple[float, float, bool]] = {}
+        self._searches: dict = {}      # DictSearch per (column, segment list)
 
     def has_nonfinite(self, column: str) -> bool:
         return self._bounds(column)[2]
@@ -789,6 +791,192 @@ class _Ord:
 
 # ------------------------------------------------------------------------------------------ C plan
 
+# ------------------------------------------------------------------------------------------ query shape
+
+def _filter_shape(f: Optional[FilterContext]):
+    if f is None:
+        return None
+    if f.type == "PREDICATE":
+        p = f.predicate
+        return ("P", p.type, p.column, p.lower == UNBOUNDED, p.upper == UNBOUNDED, p.lower_inclusive,
+                p.upper_inclusive)
+    return (f.type, tuple(_filter_shape(c) for c in f.children))
+
+
+def query_shape(q: QueryContext) -> tuple:
+    """A query with its filter's literals left out: two queries of one shape lower to the same plan but for the
+    leaves (CPlan.relower) -- a server's parametrised queries with fresh literals."""
+    import dataclasses
+    return _filter_shape(q.filter), repr(dataclasses.replace(q, filter=None))
+
+
+# ------------------------------------------------------------------------------------------ vectorized leaf lowering
+
+def _ctypes_dtype(st) -> np.dtype:
+    """A numpy structured dtype with the exact layout of a ctypes Structure (pointers as uint64)."""
+    kinds = {C.c_uint32: "<u4", C.c_int32: "<i4", C.c_int64: "<i8", C.c_uint64: "<u8", C.c_double: "<f8",
+             C.c_void_p: "<u8"}
+    names, formats, offsets = [], [], []
+    for name, ty in st._fields_:
+        names.append(name)
+        formats.append(kinds.get(ty, "<u8"))   # POINTER(...) fields: 8-byte addresses
+        offsets.append(getattr(st, name).offset)
+    return np.dtype({"names": names, "formats": formats, "offsets": offsets, "itemsize": C.sizeof(st)})
+
+
+PG_LEAF_DTYPE = _ctypes_dtype(abi.pg_leaf)
+_NUMERIC_DICT = ("INT", "LONG", "FLOAT", "DOUBLE")
+_SEARCH_MAX_ENTRIES = 8 << 20   # columns whose dictionaries hold more entries over the segments search per segment
+
+
+class DictSearch:
+    """The sorted dictionaries of one numeric column over a list of segments, searchable for every segment at once:
+    each value's rank in the union of the dictionaries, offset by segment (a sorted int64 key), so the insertion point
+    of a literal in every segment's dictionary is two vectorized searches instead of one binary search per segment
+    (BaseImmutableDictionary.binarySearch, once per segment per literal in the reference's predicate evaluators)."""
+
+    def __init__(self, dicts):
+        vals = [d.values for d in dicts]
+        sizes = np.array([len(v) for v in vals], dtype=np.int64)
+        self.off = np.concatenate([[0], np.cumsum(sizes)])
+        allv = np.concatenate(vals) if len(vals) else np.zeros(0)
+        self.union = np.unique(allv)
+        span = len(self.union) + 1
+        seg = np.repeat(np.arange(len(vals), dtype=np.int64), sizes)
+        self.key = seg * span + np.searchsorted(self.union, allv)
+        self.base = np.arange(len(vals), dtype=np.int64) * span
+        self.allv = allv
+        self.sizes = sizes
+
+    def count_below(self, v, inclusive: bool) -> np.ndarray:
+        """Per segment: the number of dictionary values < v (or <= v)."""
+        r = np.searchsorted(self.union, v, side="right" if inclusive else "left")
+        return np.searchsorted(self.key, self.base + r, side="left") - self.off[:-1]
+
+    def index_of(self, v) -> np.ndarray:
+        """Per segment: the dictId of v, or -1 (Dictionary.indexOf)."""
+        i = self.count_below(v, False)
+        at = np.minimum(self.off[:-1] + i, max(len(self.allv) - 1, 0))
+        hit = (i < self.sizes) & (self.allv[at] == v) if len(self.allv) else np.zeros(len(i), dtype=bool)
+        return np.where(hit, i, -1)
+
+
+def _dict_search(table: "Table", column: str, segments) -> Optional[DictSearch]:
+    key = (column, tuple(id(s) for s in segments))
+    cache = table._searches
+    hit = cache.get(key)
+    if hit is None:
+        dicts = [s.columns[column].dictionary for s in segments]
+        if sum(len(d) for d in dicts) > _SEARCH_MAX_ENTRIES:
+            return None
+        hit = cache[key] = (DictSearch(dicts), segments)
+    return hit[0]
+
+
+def lower_leaf_vectorized(table: "Table", pred: Predicate, segments, col_id: int, batch) -> Optional[dict]:
+    """lower_predicate for one leaf over every segment at once, as field arrays of the pg_leaf table (None: a shape
+    the vectorized form does not cover -- the per-segment path lowers it).  Same semantics: predicate evaluator ->
+    dictId range / set per segment, the isAlwaysTrue / isAlwaysFalse shortcuts, the leaf operator choice."""
+    cols = [s.columns.get(pred.column) for s in segments]
+    if any(c is None or c.dictionary is None for c in cols):
+        return None
+    d0 = cols[0].dictionary
+    if d0.data_type not in _NUMERIC_DICT or any(c.dictionary.data_type != d0.data_type for c in cols):
+        return None
+    t = pred.type
+    if t not in ("RANGE", "EQ", "NOT_EQ", "IN", "NOT_IN"):
+        return None
+    S = len(segments)
+    card = np.array([len(c.dictionary) for c in cols], dtype=np.int64)
+    sv = np.array([c.single_value for c in cols], dtype=bool)
+    srt = np.array([c.is_sorted for c in cols], dtype=bool)
+    rng = np.array([c.range_index is not None for c in cols], dtype=bool)
+    inv = np.array([c.inverted is not None for c in cols], dtype=bool)
+    out = {"lo": np.zeros(S, np.int64), "hi": np.zeros(S, np.int64), "exclusive": np.zeros(S, np.int64),
+           "num_ids": np.zeros(S, np.int64), "ids": np.zeros(S, np.uint64), "values": np.zeros(S, np.uint64),
+           "num_values": np.zeros(S, np.int64), "keep": []}
+    if t == "RANGE" or t in ("EQ", "NOT_EQ"):
+        ds = _dict_search(table, pred.column, segments)
+        if ds is None:
+            return None
+        try:
+            if t == "RANGE":
+                start = np.zeros(S, np.int64) if pred.lower == UNBOUNDED else \
+                    ds.count_below(d0._coerce(pred.lower), not pred.lower_inclusive)
+                end = card.copy() if pred.upper == UNBOUNDED else \
+                    ds.count_below(d0._coerce(pred.upper), bool(pred.upper_inclusive))
+            else:
+                idx = ds.index_of(d0._coerce(pred.values[0]))
+        except (ValueError, OverflowError):
+            return None
+        if t == "RANGE":
+            out["lo"], out["hi"] = start, end
+            always_false = end - start <= 0
+            always_true = end - start == card
+        else:
+            found = idx >= 0
+            ids = np.ascontiguousarray(np.where(found, idx, 0), dtype=np.int32)
+            out["keep"].append(ids)
+            out["ids"] = np.where(found, ids.ctypes.data + 4 * np.arange(S, dtype=np.uint64), 0).astype(np.uint64)
+            out["num_ids"] = found.astype(np.int64)
+            if t == "EQ":
+                always_false, always_true = ~found, found & (card == 1)
+            else:
+                out["exclusive"][:] = 1
+                always_false, always_true = found & (card == 1), ~found
+    else:
+        if batch is None:
+            return None
+        ids2, counts, wide = batch
+        cnt = counts.astype(np.int64)
+        n = ids2.shape[1]
+        rows = ids2.ctypes.data + 4 * n * np.arange(S, dtype=np.uint64)
+        first = ids2[:, 0].astype(np.int64)
+        last = ids2[np.arange(S), np.maximum(cnt - 1, 0)].astype(np.int64)
+        has = cnt > 0
+        contiguous = last - first + 1 == cnt
+        out["num_ids"] = cnt
+        out["keep"].append(ids2)
+        if t == "IN":
+            always_false, always_true = ~has, cnt == card
+        else:
+            out["exclusive"][:] = 1
+            always_false, always_true = has & (cnt == card), ~has
+    # leaf operator (FilterOperatorUtils.getLeafFilterOperator): sorted index, range index (RANGE), inverted index
+    # (not RANGE), else a scan
+    kind = np.where(sv, abi.PG_LEAF_SV_SCAN, abi.PG_LEAF_MV_SCAN)
+    if t != "RANGE":
+        kind = np.where(inv, abi.PG_LEAF_INVERTED, kind)
+    else:
+        kind = np.where(rng, abi.PG_LEAF_RANGE_INDEX, kind)
+    kind = np.where(sv & srt, abi.PG_LEAF_SORTED, kind)
+    kind = np.where(always_true, abi.PG_LEAF_MATCH_ALL, kind)
+    kind = np.where(always_false, abi.PG_LEAF_EMPTY, kind)
+    out["kind"] = kind
+    if t in ("IN", "NOT_IN"):
+        shortcut = always_true | always_false
+        # values mode: the literals (one array for every segment) cross instead of a non-contiguous dictId list of a
+        # scan leaf; the device finds the dictIds in the resident dictionary
+        vmode = (~shortcut & has & ~contiguous & ((kind == abi.PG_LEAF_SV_SCAN) | (kind == abi.PG_LEAF_MV_SCAN))
+                 if _IN_VALUES else np.zeros(S, bool))
+        keep_ids = ~shortcut & has
+        out["ids"] = np.where(keep_ids & ~vmode, rows, 0).astype(np.uint64)
+        out["values"] = np.where(vmode, wide.ctypes.data, 0).astype(np.uint64)
+        out["num_values"] = np.where(vmode, len(wide), 0)
+        out["num_ids"] = np.where(keep_ids, cnt, 0)
+        out["keep"].append(wide)
+    else:
+        shortcut = always_true | always_false
+        if t != "RANGE":
+            out["ids"] = np.where(shortcut, 0, out["ids"]).astype(np.uint64)
+            out["num_ids"] = np.where(shortcut, 0, out["num_ids"])
+    for f in ("exclusive",):  # the shortcut leaves carry no exclusivity (LoweredLeaf of EMPTY / MATCH_ALL)
+        out[f] = np.where(shortcut, 0, out[f])
+    out["lo"] = np.where(shortcut, 0, out["lo"])
+    out["hi"] = np.where(shortcut, 0, out["hi"])
+    return out
+
+
 class CPlan:
     """Owns every ctypes array a pg_plan points to (kept alive while the plan is in use)."""
 
@@ -816,55 +1004,7 @@ class CPlan:
         self.leaf_preds = preds
         L = len(preds)
         S = len(segments)
-        seg_arr = (abi.pg_segment_ref * max(S, 1))()
-        self.lowered: List[List[LoweredLeaf]] = []
-        batch = self._batched_in_ids(preds, segments, seg_keys, cid, id_sets) if id_sets is not None and S > 1 else {}
-        self._keep.extend(b[2] for b in batch.values())  # the literal arrays values-mode leaves point to
-        for si, (seg, key) in enumerate(zip(segments, seg_keys)):
-            leaves = (abi.pg_leaf * max(L, 1))()
-            lows = []
-            for li, p in enumerate(preds):
-                if p.column not in seg.columns:
-                    raise UnsupportedQuery(f"unknown column {p.column}")
-                b = batch.get(li)
-                lw = lower_predicate(p, seg.columns[p.column], cid[p.column],
-                                     None if b is None else b[0][si, :b[1][si]])
-                lows.append(lw)
-                leaves[li].kind = lw.kind
-                leaves[li].col_id = lw.col_id
-                leaves[li].exclusive = lw.exclusive
-                leaves[li].lo = lw.lo
-                leaves[li].hi = lw.hi
-                if lw.ids is not None and len(lw.ids):
-                    arr = np.ascontiguousarray(lw.ids, dtype=np.int32)
-                    leaves[li].num_ids = len(arr)
-                    if b is not None and _IN_VALUES and lw.kind in (abi.PG_LEAF_SV_SCAN, abi.PG_LEAF_MV_SCAN) and \
-                            int(arr[-1]) - int(arr[0]) + 1 != len(arr):
-                        # values mode: the predicate's literals (one array for every segment); the device finds their
-                        # dictIds in the resident dictionary (a contiguous id set still crosses as ids: a RANGE leaf)
-                        leaves[li].values = b[2].ctypes.data
-                        leaves[li].num_values = len(b[2])
-                    else:
-                        self._keep.append(arr)
-                        leaves[li].ids = arr.ctypes.data_as(C.POINTER(C.c_int32))
-                if lw.raw is not None:
-                    r = lw.raw
-                    if "values" in r:  # int64 for INT / LONG columns, float64 for FLOAT / DOUBLE
-                        arr = np.ascontiguousarray(r["values"], dtype=np.int64 if r["dtype"] in ("INT", "LONG")
-                                                   else np.float64)
-                        self._keep.append(arr)
-                        leaves[li].num_ids = len(arr)
-                        leaves[li].values = arr.ctypes.data
-                    else:
-                        leaves[li].ilo, leaves[li].ihi = r.get("ilo", 0), r.get("ihi", 0)
-                        leaves[li].dlo, leaves[li].dhi = r.get("dlo", 0.0), r.get("dhi", 0.0)
-                        leaves[li].lo_inclusive, leaves[li].hi_inclusive = r.get("lo_inc", 1), r.get("hi_inc", 1)
-            self.lowered.append(lows)
-            self._keep.append(leaves)
-            seg_arr[si].seg_key = key
-            seg_arr[si].num_docs = seg.num_docs
-            seg_arr[si].leaves = leaves
-        self._keep.append(seg_arr)
+        seg_arr = self._lower_leaves(table, segments, seg_keys, preds, id_sets)
         ops_arr = (C.c_int32 * max(len(ops), 1))(*ops)
         self._keep.append(ops_arr)
 
@@ -966,6 +1106,125 @@ class CPlan:
         self._image_lock = threading.Lock()
         self._tls = threading.local()
 
+    def _lower_leaves(self, table: Table, segments, seg_keys, preds, id_sets):
+        """Every segment's leaves (the filter's predicates lowered into dictId space) as one pg_leaf table and the
+        pg_segment_ref array pointing into it (CPlan.__init__, and relower for a query of the same shape)."""
+        cid = table.column_ids
+        S, L = len(segments), len(preds)
+        self._leaf_keep = []
+        self._lowered = None
+        seg_arr = (abi.pg_segment_ref * max(S, 1))()
+        batch = self._batched_in_ids(preds, segments, seg_keys, cid, id_sets) if id_sets is not None and S > 1 else {}
+        self._leaf_keep.extend(b[2] for b in batch.values())  # the literal arrays values-mode leaves point to
+        # the leaves of every segment as ONE table in pg_leaf's layout ([segment][leaf]), each segment's row pointed to
+        # by its pg_segment_ref; a leaf is lowered for all segments at once where the vectorized form covers it
+        # (lower_leaf_vectorized), else segment by segment (lower_predicate)
+        Lc = max(L, 1)
+        tab = np.zeros((max(S, 1), Lc), dtype=PG_LEAF_DTYPE)
+        self._leaf_tab = tab
+        self._vec: Dict[int, dict] = {}
+        self._per_seg: Dict[Tuple[int, int], LoweredLeaf] = {}
+        self._batch = batch
+        for p in preds:
+            if p.column not in cid or any(p.column not in seg.columns for seg in segments):
+                raise UnsupportedQuery(f"unknown column {p.column}")
+        for li, p in enumerate(preds):
+            b = batch.get(li)
+            vec = lower_leaf_vectorized(table, p, segments, cid[p.column], b) if S > 1 else None
+            if vec is not None:
+                col = tab[:S, li]
+                col["col_id"] = cid[p.column]
+                for f in ("kind", "exclusive", "lo", "hi", "num_ids", "ids", "values", "num_values"):
+                    col[f] = vec[f]
+                self._leaf_keep.extend(vec["keep"])
+                self._vec[li] = vec
+                continue
+            for si, seg in enumerate(segments):
+                lw = lower_predicate(p, seg.columns[p.column], cid[p.column],
+                                     None if b is None else b[0][si, :b[1][si]])
+                self._per_seg[(si, li)] = lw
+                r = tab[si, li]
+                r["kind"], r["col_id"], r["exclusive"], r["lo"], r["hi"] = lw.kind, lw.col_id, lw.exclusive, lw.lo, lw.hi
+                if lw.ids is not None and len(lw.ids):
+                    arr = np.ascontiguousarray(lw.ids, dtype=np.int32)
+                    r["num_ids"] = len(arr)
+                    if b is not None and _IN_VALUES and lw.kind in (abi.PG_LEAF_SV_SCAN, abi.PG_LEAF_MV_SCAN) and \
+                            int(arr[-1]) - int(arr[0]) + 1 != len(arr):
+                        # values mode: the predicate's literals (one array for every segment); the device finds their
+                        # dictIds in the resident dictionary (a contiguous id set still crosses as ids: a RANGE leaf)
+                        r["values"] = b[2].ctypes.data
+                        r["num_values"] = len(b[2])
+                    else:
+                        self._leaf_keep.append(arr)
+                        r["ids"] = arr.ctypes.data
+                if lw.raw is not None:
+                    raw = lw.raw
+                    if "values" in raw:  # int64 for INT / LONG columns, float64 for FLOAT / DOUBLE
+                        arr = np.ascontiguousarray(raw["values"], dtype=np.int64 if raw["dtype"] in ("INT", "LONG")
+                                                   else np.float64)
+                        self._leaf_keep.append(arr)
+                        r["num_ids"] = len(arr)
+                        r["values"] = arr.ctypes.data
+                    else:
+                        r["ilo"], r["ihi"] = raw.get("ilo", 0), raw.get("ihi", 0)
+                        r["dlo"], r["dhi"] = raw.get("dlo", 0.0), raw.get("dhi", 0.0)
+                        r["lo_inclusive"], r["hi_inclusive"] = raw.get("lo_inc", 1), raw.get("hi_inc", 1)
+        base = tab.ctypes.data
+        seg_tab = np.frombuffer(seg_arr, dtype=_ctypes_dtype(abi.pg_segment_ref), count=max(S, 1))
+        seg_tab["seg_key"][:S] = np.asarray(seg_keys, dtype=np.uint64)
+        seg_tab["num_docs"][:S] = [seg.num_docs for seg in segments]
+        seg_tab["leaves"][:S] = base + np.arange(S, dtype=np.uint64) * (Lc * PG_LEAF_DTYPE.itemsize)
+        self._segments = list(segments)
+        self._seg_keys = list(seg_keys)
+        self._leaf_keep.append(seg_arr)
+        return seg_arr
+
+    def relower(self, query: QueryContext, id_sets=None) -> "CPlan":
+        """This plan for `query`, a query of the same shape (query_shape: only the filter's literals differ): the
+        aggregations, keys, ORDER BY / trim and sum bounds are shared, only the leaves are lowered again -- the
+        per-segment predicate evaluators of the new literals (one pg_dict_id_sets launch per IN list)."""
+        ops, preds = filter_program(query.filter)
+        if len(preds) != len(self.leaf_preds):
+            raise ValueError("relower: a query of another shape")
+        new = copy.copy(self)
+        new.query = query
+        new.leaf_preds = preds
+        seg_arr = new._lower_leaves(self.table, self._segments, self._seg_keys, preds, id_sets)
+        p = abi.pg_plan.from_buffer_copy(self.plan)
+        p.segments = seg_arr
+        new.plan = p
+        new._image = None
+        new._image_lock = threading.Lock()
+        new._tls = threading.local()
+        return new
+
+    @property
+    def lowered(self) -> List[List[LoweredLeaf]]:
+        """The lowered leaves as LoweredLeaf records, [segment][leaf] (built on first use: tests and bench.py's byte
+        model read them; execution reads the pg_leaf table)."""
+        if self._lowered is None:
+            out = []
+            L = len(self.leaf_preds)
+            for si in range(len(self._segments)):
+                row = []
+                for li in range(L):
+                    lw = self._per_seg.get((si, li))
+                    if lw is None:
+                        r = self._leaf_tab[si, li]
+                        ids = None
+                        n = int(r["num_ids"])
+                        vec = self._vec[li]
+                        if n and li in self._batch:
+                            ids = np.array(self._batch[li][0][si, :n], dtype=np.int32)
+                        elif n:
+                            ids = np.array([int(vec["keep"][0][si])], dtype=np.int32)
+                        lw = LoweredLeaf(int(r["kind"]), int(r["col_id"]), int(r["exclusive"]), int(r["lo"]),
+                                         int(r["hi"]), ids)
+                    row.append(lw)
+                out.append(row)
+            self._lowered = out
+        return self._lowered
+
     def image(self, query_id: Optional[int] = None, deadline_ms: Optional[int] = None) -> Tuple[np.ndarray, int]:
         """The plan as one relocatable byte image (pg_image_header + arrays at offsets, include/pinot_gpu.h): what a
         Java GpuPlanMaker fills in a direct ByteBuffer, and its address.  Built once per plan; each calling thread gets
@@ -975,7 +1234,8 @@ class CPlan:
         if self._image is None:
             with self._image_lock:
                 if self._image is None:
-                    self._image = abi.build_image(self.plan)
+                    regions = [a for a in self._keep + self._leaf_keep if isinstance(a, np.ndarray)]
+                    self._image = abi.build_image(self.plan, self._leaf_tab, regions)
         t = self._tls
         if getattr(t, "image", None) is None:
             t.image = self._image.copy()

@@ -172,3 +172,51 @@ def test_plan_image_of_a_lowered_plan(sv_segment):
     lib = abi.declare(C.CDLL(LIB))
     rc, msg = _run_image(lib, im.tobytes())
     assert rc == abi.PG_E_STATE, msg
+
+
+def _decode_image_leaves(im):
+    """(seg_key, num_docs, [(leaf fields..., ids tuple, values tuple)]) per segment of an image, offsets resolved."""
+    import numpy as np
+    b = im.tobytes()
+    h = abi.pg_image_header.from_buffer_copy(b[:C.sizeof(abi.pg_image_header)])
+    segs = (abi.pg_image_segment * h.num_segments).from_buffer_copy(
+        b[h.segments_off:h.segments_off + C.sizeof(abi.pg_image_segment) * h.num_segments])
+    out = []
+    for s in segs:
+        leaves = (abi.pg_image_leaf * h.num_leaves).from_buffer_copy(
+            b[s.leaves_off:s.leaves_off + C.sizeof(abi.pg_image_leaf) * h.num_leaves]) if h.num_leaves else []
+        row = []
+        for x in leaves:
+            ids = tuple(np.frombuffer(b, np.int32, x.num_ids, x.ids_off)) if x.ids_off else ()
+            nv = x.num_values or x.num_ids
+            vals = tuple(np.frombuffer(b, np.int64, nv, x.values_off)) if x.values_off else ()
+            row.append((x.kind, x.col_id, x.exclusive, x.num_ids, x.lo, x.hi, x.ilo, x.ihi, x.dlo, x.dhi,
+                        x.lo_inclusive, x.hi_inclusive, x.num_values, ids, vals))
+        out.append((s.seg_key, s.num_docs, row))
+    return h, out
+
+
+def test_vectorized_image_matches_the_per_segment_writer(sv_segment):
+    """The leaf table image (one copy of the [segment][leaf] table, pointers translated by region) holds exactly the
+    plan the per-segment writer produces -- every leaf's fields, dictId lists and literals."""
+    import numpy as np
+    from pinot_amd.plan import CPlan, Table, dict_id_set
+    from pinot_amd.query import parse
+    t = Table("t", [sv_segment] * 3)
+    vals = sv_segment.columns["column9"].dictionary.values
+    lits = ", ".join(str(int(vals[i])) for i in (3, 7, 40, 41, 900))
+    sql = (f"SELECT column11, SUM(column1) FROM t WHERE column9 IN ({lits}) AND column3 > 5 AND column1 <> 3 "
+           "AND column5 = 'gFuH' GROUP BY column11 ORDER BY SUM(column1) DESC LIMIT 3")
+
+    def id_sets(col_id, dt, lit, keys):
+        row = dict_id_set(sv_segment.columns["column9"].dictionary, list(lit))
+        out = np.zeros((len(keys), len(lit)), dtype=np.int32)
+        out[:, :len(row)] = row
+        return out, np.full(len(keys), len(row), dtype=np.uint32)
+    cp = CPlan(t, parse(sql), t.segments, [11, 12, 13], trim="server", id_sets=id_sets)
+    fast, _ = cp.image()
+    slow = abi.build_image(cp.plan)
+    hf, lf = _decode_image_leaves(fast)
+    hs, ls = _decode_image_leaves(slow)
+    assert lf == ls
+    assert (hf.num_segments, hf.num_leaves, hf.flags, hf.limit) == (hs.num_segments, hs.num_leaves, hs.flags, hs.limit)

@@ -54,3 +54,53 @@ def test_released_segment_drops_its_plans(gpu_engine):
     assert gpu_engine.plan_cache_misses == m + 1
     assert before.rows == after.rows
     gpu_engine.release(seg)
+
+
+SHAPE_A = ("SELECT column9, SUM(column1), COUNT(*) FROM t WHERE column7 IN (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12) "
+           "AND column3 > 1000000 GROUP BY column9")
+SHAPE_B = ("SELECT column9, SUM(column1), COUNT(*) FROM t WHERE column7 IN (2, 5, 9, 300, 4000, 70000, 123456) "
+           "AND column3 > 900000000 GROUP BY column9")
+
+
+def test_query_shape_ignores_only_filter_literals():
+    from pinot_amd.plan import query_shape
+    from pinot_amd.query import parse
+    assert query_shape(parse(SHAPE_A)) == query_shape(parse(SHAPE_B))
+    assert query_shape(parse(SHAPE_A)) != query_shape(parse(SHAPE_A.replace("column3 >", "column3 >=")))
+    assert query_shape(parse(SHAPE_A)) != query_shape(parse(SHAPE_A.replace("SUM(column1)", "MAX(column1)")))
+    assert query_shape(parse(SHAPE_A)) != query_shape(parse(SHAPE_A + " LIMIT 7"))
+
+
+def test_relowered_plan_equals_a_fresh_plan(sv_segment):
+    """CPlan.relower (the shape cache's hit): the plan of query A re-lowered for query B's literals is the plan of B --
+    the same image, leaf for leaf."""
+    import numpy as np
+    from pinot_amd.plan import CPlan, dict_id_set
+    from pinot_amd.query import parse
+    from test_abi import _decode_image_leaves
+    t = Table("t", [sv_segment] * 3)
+
+    def id_sets(col_id, dt, lit, keys):
+        name = [c for c, i in t.column_ids.items() if i == col_id][0]
+        row = dict_id_set(sv_segment.columns[name].dictionary, list(lit))
+        out = np.zeros((len(keys), len(lit)), dtype=np.int32)
+        out[:, :len(row)] = row
+        return out, np.full(len(keys), len(row), dtype=np.uint32)
+    a = CPlan(t, parse(SHAPE_A), t.segments, [1, 2, 3], trim="server", id_sets=id_sets)
+    b = CPlan(t, parse(SHAPE_B), t.segments, [1, 2, 3], trim="server", id_sets=id_sets)
+    r = a.relower(parse(SHAPE_B), id_sets)
+    assert _decode_image_leaves(r.image()[0])[1] == _decode_image_leaves(b.image()[0])[1]
+    assert _decode_image_leaves(r.image()[0])[1] != _decode_image_leaves(a.image()[0])[1]
+    assert r.image()[0].tobytes() == b.image()[0].tobytes()
+
+
+@pytest.mark.gpu
+def test_literal_only_change_hits_the_shape_cache(gpu_engine, oracle_engine, sv_table_inter):
+    """A parametrised query with fresh literals misses the SQL-text cache but hits the shape cache (only its leaves
+    are lowered again) and answers as the oracle does."""
+    from pinot_amd.query import parse
+    gpu_engine.execute(sv_table_inter, SHAPE_A)
+    s0, m0 = gpu_engine.plan_shape_hits, gpu_engine.plan_cache_misses
+    got = gpu_engine.execute(sv_table_inter, SHAPE_B)
+    assert gpu_engine.plan_shape_hits == s0 + 1 and gpu_engine.plan_cache_misses == m0
+    assert_same_result(got, oracle_engine.execute(sv_table_inter, parse(SHAPE_B)), table=sv_table_inter)
