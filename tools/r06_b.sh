@@ -1,7 +1,7 @@
 #!/bin/bash
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread --tb=short tests/test_plan_cache.py tests/test_abi.py tests/test_gpu_runtime.py > gpurun_out/b_tests.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/b_tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread --tb=short -m gpu tests/test_plan_cache.py tests/test_gpu_runtime.py tests/test_abi.py > gpurun_out/b_tests.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/b_tests.log; exit 1; }
 tail -1 gpurun_out/b_tests.log
 WORKLOADS="adanalytics index" TAG=r06b STEPS=30 bash tools/bench_all.sh || exit 1
 python3 -c "
