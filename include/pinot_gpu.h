@@ -115,6 +115,12 @@ typedef enum pg_data_type {
 } pg_data_type;
 
 #define PG_SRC_DEVICE 0x1u /* pg_col_desc.flags: `src` is a device pointer (same byte layout) */
+/* col_id flag: a host-built dictionary encoding of the raw (no-dictionary) column col_id & ~PG_COL_DERIVED -- sorted
+ * distinct values (Double.compare order) + bit-packed ids + a keymap to table-global ids -- uploaded for a GROUP BY key or
+ * DISTINCTCOUNT value over a raw FLOAT / DOUBLE column or a raw INT / LONG column whose range spans 2^32 or more (the
+ * reference's NoDictionarySingleColumnGroupKeyGenerator / NoDictionaryMultiColumnGroupKeyGenerator inputs,
+ * DefaultGroupByExecutor.java:85-94).  It counts as that raw column in the statistics (numEntriesScannedPostFilter). */
+#define PG_COL_DERIVED 0x40000000u
 
 typedef struct pg_col_desc {
   uint32_t kind;             /* pg_index_kind */

@@ -14,6 +14,7 @@ PG_INT, PG_LONG, PG_FLOAT, PG_DOUBLE, PG_STRING, PG_BYTES = 0, 1, 2, 3, 4, 5
 DTYPE_CODES = {"INT": PG_INT, "LONG": PG_LONG, "FLOAT": PG_FLOAT, "DOUBLE": PG_DOUBLE, "STRING": PG_STRING,
                "BYTES": PG_BYTES}
 PG_SRC_DEVICE = 1
+PG_COL_DERIVED = 0x40000000
 
 PG_LEAF_MATCH_ALL, PG_LEAF_EMPTY, PG_LEAF_SV_SCAN, PG_LEAF_SORTED, PG_LEAF_INVERTED, PG_LEAF_MV_SCAN, \
     PG_LEAF_RAW_SCAN, PG_LEAF_RANGE_INDEX = range(8)

@@ -1737,9 +1737,9 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     if (g.fn > PG_AGG_COUNTMV) return fail(PG_E_INVALID, "unknown aggregation %u", g.fn);
     if (g.op > PG_EXPR_SUB) return fail(PG_E_INVALID, "unknown expression op %u", g.op);
     if (g.fn == PG_AGG_COUNT) continue;
-    projected.insert(g.col_a);
+    projected.insert(g.col_a & ~PG_COL_DERIVED);
     const bool two = (g.fn == PG_AGG_SUM || g.fn == PG_AGG_MIN || g.fn == PG_AGG_MAX || g.fn == PG_AGG_AVG) && g.op != PG_EXPR_COL;
-    if (two) projected.insert(g.col_b);
+    if (two) projected.insert(g.col_b & ~PG_COL_DERIVED);
     SumBounds sb;
     for (uint32_t si = 0; si < S; si++) {
       const ColumnRes* ca = col(si, g.col_a);
@@ -1799,7 +1799,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     P.layout = integer;
     for (uint32_t a = 0; a < A; a++) q.aggs[a] = P.aggs[a];
   }
-  for (uint32_t k = 0; k < K; k++) projected.insert(plan->keys[k].col_id);
+  for (uint32_t k = 0; k < K; k++) projected.insert(plan->keys[k].col_id & ~PG_COL_DERIVED);
   for (uint32_t a = 0; a < A; a++) q.agg_reads |= plan->aggs[a].fn != PG_AGG_COUNT;
 
   PG_PROF("state");
@@ -3919,11 +3919,11 @@ int run_wide(const pg_plan* plan, Partials& P, pg_stats& st) {
   for (uint32_t a = 0; a < plan->num_aggs; a++) {
     const pg_agg& g = plan->aggs[a];
     if (g.fn == PG_AGG_COUNT) continue;
-    proj.insert(g.col_a);
+    proj.insert(g.col_a & ~PG_COL_DERIVED);
     if ((g.fn == PG_AGG_SUM || g.fn == PG_AGG_MIN || g.fn == PG_AGG_MAX || g.fn == PG_AGG_AVG) && g.op != PG_EXPR_COL)
-      proj.insert(g.col_b);
+      proj.insert(g.col_b & ~PG_COL_DERIVED);
   }
-  for (uint32_t k = 0; k < K; k++) proj.insert(plan->keys[k].col_id);
+  for (uint32_t k = 0; k < K; k++) proj.insert(plan->keys[k].col_id & ~PG_COL_DERIVED);
   P.projected_cols = (uint32_t)proj.size();
   st.num_entries_scanned_post_filter = st.num_docs_scanned * P.projected_cols;
   return PG_OK;

@@ -20,7 +20,7 @@ from .plan import (MAX_TRIM_THRESHOLD, CPlan, ExecutionStats, InstanceConfig, In
                    UnsupportedQuery, execute_filtered, group_trim, has_filtered_aggregations, merge_intermediate,
                    query_shape, top_groups)
 from .query import QueryContext, parse
-from .segment import Column, ImmutableSegment
+from .segment import Column, Dictionary, ImmutableSegment, num_bits_per_value, pack_bits
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PINOT_GPU_LIB", os.path.join(_HERE, "libpinot_gpu.so"))
@@ -164,7 +164,11 @@ class GpuEngine:
             if ks.kind != abi.PG_KEY_KEYMAP:
                 continue
             cid = table.column_ids[ks.column]
+            if ks.derived is not None:
+                cid |= abi.PG_COL_DERIVED
             for seg, key in zip(segments, seg_keys):
+                if ks.derived is not None and (key, cid) not in self._keymaps_uploaded:
+                    self._upload_derived(key, cid, seg.columns[ks.column], ks.derived[table.segments.index(seg)])
                 if (key, cid) in self._keymaps_uploaded:
                     continue
                 km = np.ascontiguousarray(ks.keymaps[table.segments.index(seg)], dtype=np.int32)
@@ -173,6 +177,21 @@ class GpuEngine:
                 d.cardinality = len(km)
                 check(self.lib.pg_column_upload(key, cid, C.byref(d), km.ctypes.data_as(C.c_void_p), km.nbytes))
                 self._keymaps_uploaded.add((key, cid))
+
+    def _upload_derived(self, key, cid, col, derived):
+        """The resident form of a derived key column (KeySpace.derived, col_id | PG_COL_DERIVED): a raw segment's
+        host-built encoding as a LONG dictionary of order keys + a bit-packed SV forward index; a dictionary segment
+        of the same table keeps its own dictionary and forward index (the keymap maps either to the global ids)."""
+        if derived is not None:
+            u, ids = derived
+            b = num_bits_per_value(max(len(u) - 1, 0))
+            col = Column(col.name, "LONG", True, Dictionary("LONG", u), len(ids), b, False, len(ids), 0,
+                         fwd=pack_bits(ids, b), dict_ids=ids)
+        d = fwd_desc(col)
+        dd = abi.pg_col_desc.from_buffer_copy(d)
+        dd.kind = abi.PG_IDX_DICT
+        self._upload(key, cid, dd, col.dictionary.to_bytes())
+        self._upload(key, cid, d, col.fwd)
 
     def dict_id_sets(self, col_id: int, data_type: str, literals: np.ndarray, seg_keys):
         """pg_dict_id_sets: the literals' dictIds in every segment's resident dictionary (one device launch)."""
@@ -212,7 +231,8 @@ class GpuEngine:
         settings (numGroupsLimit comes only from there, as in the reference)."""
         segments = list(table.segments if segments is None else segments)
         keys = [self.upload_segment(s, table) for s in segments]
-        plan = CPlan(table, query, segments, keys, flags, trim, id_sets=self.dict_id_sets, config=config)
+        plan = CPlan(table, query, segments, keys, flags, trim, id_sets=self.dict_id_sets, config=config,
+                     derived_ids=True)
         self.upload_keymaps(table, plan, segments, keys)
         return plan
 

@@ -350,6 +350,29 @@ class Table:
         return ks
 
 
+def order_keys(values: np.ndarray) -> np.ndarray:
+    """Order-preserving int64 images of numeric values in the reference's key order: integers as themselves, FLOAT /
+    DOUBLE by Double.compare (-0.0 < 0.0, one NaN above +inf: Double.doubleToLongBits equality, as fastutil's
+    Double2IntOpenHashMap keys them in the no-dictionary group-key generators)."""
+    v = np.asarray(values)
+    if v.dtype.kind in "iu":
+        return v.astype(np.int64)
+    d = v.astype(np.float64)
+    b = d.view(np.int64).copy()
+    b[np.isnan(d)] = 0x7FF8000000000000
+    return np.where(b >= 0, b, b ^ 0x7FFFFFFFFFFFFFFF)
+
+
+def order_key_values(keys: np.ndarray, data_type: str) -> list:
+    """order_keys' inverse: the values (Python ints / floats) of sorted int64 images."""
+    k = np.asarray(keys, dtype=np.int64)
+    if data_type in ("INT", "LONG"):
+        return k.tolist()
+    b = np.where(k >= 0, k, k ^ 0x7FFFFFFFFFFFFFFF)
+    d = b.view(np.float64)
+    return (d.astype(np.float32).astype(np.float64) if data_type == "FLOAT" else d).tolist()
+
+
 @dataclass
 class KeySpace:
     """Table-global ids for the values of one column (group keys / DISTINCTCOUNT values)."""
@@ -360,24 +383,46 @@ class KeySpace:
     values: Optional[list] = None    # KEYMAP: global id -> value (sorted union)
     keymaps: Optional[List[np.ndarray]] = None  # per segment dictId -> global id
     _values_np: Optional[np.ndarray] = None
+    # raw columns keyed through a host-built dictionary encoding (PG_COL_DERIVED): per segment None (a dictionary
+    # segment) or (sorted distinct order keys int64 = the derived dictionary, per-doc ids into it int32)
+    derived: Optional[List[Optional[Tuple[np.ndarray, np.ndarray]]]] = None
 
     @staticmethod
     def build(column: str, cols: List[Column]) -> "KeySpace":
         dt = cols[0].data_type
         if any(c.dictionary is None for c in cols):
-            # raw (no-dictionary) columns: ids only as value offsets (a keymap needs dictIds)
-            if dt not in ("INT", "LONG"):
+            if dt not in ("INT", "LONG", "FLOAT", "DOUBLE"):
                 raise UnsupportedQuery(f"{column}: raw {dt} column as a key / DISTINCTCOUNT value")
             vals = [c.raw_values if c.dictionary is None else np.asarray(c.dictionary.values) for c in cols]
-            vals = [v for v in vals if v.size]
-            lo = min((int(v.min()) for v in vals), default=0)
-            hi = max((int(v.max()) for v in vals), default=0)
-            span = hi - lo + 1
-            # value offsets are 32-bit key ids (pg_key.cardinality): a group key may span up to 2^32 - 1 values (the
-            # device state then hashes them); a DISTINCTCOUNT value set also needs a dense bitmap (checked at its use)
-            if span >= 1 << 32:
-                raise UnsupportedQuery(f"{column}: raw value range {span} too wide for 32-bit value-offset ids")
-            return KeySpace(column, abi.PG_KEY_VALUE_OFFSET, span, lo)
+            if dt in ("INT", "LONG"):
+                nz = [v for v in vals if v.size]
+                lo = min((int(v.min()) for v in nz), default=0)
+                hi = max((int(v.max()) for v in nz), default=0)
+                span = hi - lo + 1
+                # raw INT / LONG columns: value offsets as 32-bit key ids (pg_key.cardinality), read from the raw
+                # values on the device; a group key may span up to 2^32 - 1 values (the device state then hashes
+                # them); a DISTINCTCOUNT value set also needs a dense bitmap (checked at its use)
+                if span < 1 << 32:
+                    return KeySpace(column, abi.PG_KEY_VALUE_OFFSET, span, lo)
+            # raw FLOAT / DOUBLE, or a wider LONG range: every segment's values dictionary-encoded on the host (sorted
+            # distinct values in the reference's key order + per-doc ids), keymapped to the table's sorted union; the
+            # device groups on that derived encoding (PG_COL_DERIVED), so segments and GPUs merge by value
+            segk, derived = [], []
+            for c, v in zip(cols, vals):
+                ok = order_keys(v)
+                if c.dictionary is None:
+                    u, local = np.unique(ok, return_inverse=True)
+                    segk.append(u)
+                    derived.append((u, local.astype(np.int32)))
+                else:
+                    segk.append(ok)
+                    derived.append(None)
+            allk = np.unique(np.concatenate(segk)) if segk else np.zeros(0, dtype=np.int64)
+            if len(allk) >= 1 << 31:
+                raise UnsupportedQuery(f"{column}: {len(allk)} distinct raw values")
+            keymaps = [np.searchsorted(allk, k).astype(np.int32) for k in segk]
+            return KeySpace(column, abi.PG_KEY_KEYMAP, len(allk), 0, order_key_values(allk, dt), keymaps,
+                            derived=derived)
         if dt in ("INT", "LONG"):
             lo = min(int(c.dictionary.values[0]) for c in cols)
             hi = max(int(c.dictionary.values[-1]) for c in cols)
@@ -982,7 +1027,7 @@ class CPlan:
 
     def __init__(self, table: Table, query: QueryContext, segments: Sequence[ImmutableSegment],
                  seg_keys: Sequence[int], flags: int = 0, trim=False, id_sets=None,
-                 config: Optional["InstanceConfig"] = None):
+                 config: Optional["InstanceConfig"] = None, derived_ids: bool = False):
         """config: the server instance's settings (InstanceConfig; numGroupsLimit, trim sizes, trim threshold).
         flags: PG_PLAN_*.  trim (group-by only): True -- the device applies the query's ORDER BY / LIMIT (boundary
         ties kept: a final, single-server answer); "server" -- the device keeps exactly the rows the reference server's
@@ -991,7 +1036,10 @@ class CPlan:
         ORDER BY (the per-segment trim).
         id_sets(col_id, data_type, literals, seg_keys) -> (ids [S, n] int32, counts [S]): the IN / NOT_IN literals'
         dictIds in every segment in one call (GpuEngine: pg_dict_id_sets on the resident dictionaries); None = per
-        segment on the host."""
+        segment on the host.
+        derived_ids: key / DISTINCTCOUNT columns whose key space is a host-built dictionary encoding of a raw column
+        (KeySpace.derived) are named col_id | PG_COL_DERIVED, the device's resident copy of that encoding (GpuEngine);
+        the oracle reads the raw column itself."""
         self.table = table
         self.query = query
         self.config = config or InstanceConfig()
@@ -1030,6 +1078,8 @@ class CPlan:
                     if ks.kind == abi.PG_KEY_VALUE_OFFSET and ks.cardinality > MAX_VALUE_OFFSET_KEYS:
                         raise UnsupportedQuery(f"DISTINCTCOUNT({e.cols[0]}): raw value range {ks.cardinality} too wide "
                                                "for a value bitmap")
+                    if derived_ids and ks.derived is not None:
+                        aggs[i].col_a |= abi.PG_COL_DERIVED
                     aggs[i].key_kind = ks.kind
                     aggs[i].key_cardinality = ks.cardinality
                     aggs[i].key_base = ks.base
@@ -1040,15 +1090,12 @@ class CPlan:
         keys = (abi.pg_key * max(len(query.group_by), 1))()
         self.key_spaces = []
         for k, col in enumerate(query.group_by):
-            # a raw (no-dictionary) INT / LONG key groups by value offset (NoDictionarySingleColumnGroupKeyGenerator /
-            # NoDictionaryMultiColumnGroupKeyGenerator, DefaultGroupByExecutor.java:85-94); other raw types are not
-            # handled on the device
-            if any(s.columns[col].dictionary is None for s in segments if col in s.columns) and \
-                    table.data_type(col) not in ("INT", "LONG"):
-                raise UnsupportedQuery(f"GROUP BY raw (no-dictionary) {table.data_type(col)} column {col}")
+            # a raw (no-dictionary) key groups by value (NoDictionarySingleColumnGroupKeyGenerator /
+            # NoDictionaryMultiColumnGroupKeyGenerator, DefaultGroupByExecutor.java:85-94): INT / LONG by value offset,
+            # FLOAT / DOUBLE / wide LONG through a derived dictionary encoding (KeySpace.build)
             ks = table.key_space(col)
             self.key_spaces.append(ks)
-            keys[k].col_id = cid[col]
+            keys[k].col_id = cid[col] | (abi.PG_COL_DERIVED if derived_ids and ks.derived is not None else 0)
             keys[k].kind = ks.kind
             keys[k].cardinality = ks.cardinality
             keys[k].base = ks.base

@@ -14,7 +14,8 @@ import os
 import numpy as np
 import pytest
 
-from pinot_amd.plan import Table, UnsupportedQuery, reduce_to_rows
+from pinot_amd import abi
+from pinot_amd.plan import Table, reduce_to_rows
 from pinot_amd.query import parse
 from pinot_amd.segment import (CHUNK_CODECS, Column, ImmutableSegment, chunk_compress, chunk_decompress,
                                raw_forward_bytes, raw_forward_header, raw_forward_values)
@@ -150,11 +151,16 @@ def _raw_segments(n_segs=3, rows=50_000, seed=7, codecs=None):
                 "m_long": rng.integers(-2 ** 40, 2 ** 40, n), "m_float": rng.normal(size=n).astype(np.float32),
                 "m_double": rng.normal(size=n) * 1e3, "u": rng.integers(0, 300, n),
                 # a raw LONG key of a timestamp-like range (~1e9 values: hashed device state)
-                "ts": 1_600_000_000_000 + rng.integers(0, 10 ** 9, n) // 997 * 997}
+                "ts": 1_600_000_000_000 + rng.integers(0, 10 ** 9, n) // 997 * 997,
+                # raw FLOAT / DOUBLE keys and a LONG key wider than 2^32 (derived dictionary encodings on the device)
+                "g_float": (rng.integers(0, 50, n) * 0.25 - 3.0).astype(np.float32),
+                "g_double": rng.integers(-3000, 3000, n) * 0.125 + 1e-3,
+                "wide": rng.integers(0, 300, n) * 2 ** 40 - 2 ** 45}
         segs.append(ImmutableSegment.create(
             f"r{s}", data, {"k": "INT", "m_int": "INT", "m_long": "LONG", "m_float": "FLOAT", "m_double": "DOUBLE",
-                            "u": "INT", "ts": "LONG"},
-            no_dictionary=("m_int", "m_long", "m_float", "m_double", "u", "ts"), raw_version=2 + s % 3,
+                            "u": "INT", "ts": "LONG", "g_float": "FLOAT", "g_double": "DOUBLE", "wide": "LONG"},
+            no_dictionary=("m_int", "m_long", "m_float", "m_double", "u", "ts", "g_float", "g_double", "wide"),
+            raw_version=2 + s % 3,
             raw_compression=codecs))
     return segs
 
@@ -179,6 +185,15 @@ RAW_QUERIES = [
     "SELECT ts, COUNT(*), SUM(m_long) FROM t WHERE m_int > 3000 GROUP BY ts",
     "SELECT u, m_int, COUNT(*) FROM t WHERE m_int BETWEEN -50 AND 50 GROUP BY u, m_int",
     "SELECT u, DISTINCTCOUNT(k), COUNT(*) FROM t GROUP BY u",
+    # raw FLOAT / DOUBLE / wide LONG keys (the generators' Float2Int / Double2Int / Long2Int maps): grouped through a
+    # host-built dictionary encoding of the raw values (KeySpace.build, PG_COL_DERIVED)
+    "SELECT g_float, COUNT(*), SUM(m_int), MAX(m_double) FROM t GROUP BY g_float",
+    "SELECT g_double, k, COUNT(*), AVG(m_float) FROM t WHERE m_int > 0 GROUP BY g_double, k",
+    "SELECT wide, COUNT(*), MIN(m_long), SUM(wide) FROM t WHERE g_float < 5 GROUP BY wide",
+    "SELECT g_float, wide, COUNT(*) FROM t WHERE m_double > 100 GROUP BY g_float, wide",
+    "SELECT k, DISTINCTCOUNT(g_double), DISTINCTCOUNT(wide) FROM t GROUP BY k",
+    "SELECT DISTINCTCOUNT(g_float), DISTINCTCOUNT(g_double), COUNT(*) FROM t WHERE k < 30",
+    "SELECT g_double, SUM(g_double), COUNT(*) FROM t WHERE g_double > 100 GROUP BY g_double",
 ]
 
 
@@ -218,7 +233,7 @@ def test_raw_queries_oracle_vs_numpy(sql, oracle_engine, raw_table):
         for gi in range(len(uniq)):
             m2 = np.zeros_like(mask)
             m2[sel[order[bounds[gi]:bounds[gi + 1]]]] = True
-            for ag, v in zip(q.aggregations, res.rows[tuple(int(x) for x in uniq[gi])]):
+            for ag, v in zip(q.aggregations, res.rows[tuple(x.item() for x in uniq[gi])]):
                 x = _np_agg(ag, vals, m2)
                 if ag.function == "AVG":
                     assert v[1] == x[1] and np.isclose(v[0], x[0], rtol=1e-9)
@@ -281,7 +296,7 @@ def _np_agg(ag, vals, mask):
     if f == "AVG":
         return (float(np.sum(x)), int(x.size))
     if f == "DISTINCTCOUNT":
-        return set(int(y) for y in vals[e.cols[0]][mask])
+        return set(vals[e.cols[0]][mask].tolist())
     raise ValueError(f)
 
 
@@ -319,7 +334,8 @@ def _first_seen_groups(table, cols, where, limit):
     return out
 
 
-@pytest.mark.parametrize("cols,limit", [(("m_int",), 700), (("u", "k"), 1500), (("ts",), 2000)])
+@pytest.mark.parametrize("cols,limit", [(("m_int",), 700), (("u", "k"), 1500), (("ts",), 2000), (("g_double",), 2000),
+                                        (("g_float", "wide"), 3000)])
 def test_raw_group_by_limit_is_first_seen(cols, limit, oracle_engine, raw_table):
     """A raw key's groups under an instance numGroupsLimit: the first `limit` distinct keys in doc order per segment
     (the reference's no-dictionary generators have no array-based holder, so a small key range truncates too), then
@@ -333,14 +349,33 @@ def test_raw_group_by_limit_is_first_seen(cols, limit, oracle_engine, raw_table)
     assert res.groups_limit_reached
 
 
-def test_group_by_raw_float_column_is_unsupported(oracle_engine, raw_table):
-    """Raw FLOAT / DOUBLE keys (the generators' Float2Int / Double2Int maps) are not handled on the device."""
-    with pytest.raises(UnsupportedQuery):
-        oracle_engine.execute(raw_table, parse("SELECT m_float, COUNT(*) FROM t GROUP BY m_float"))
+def test_raw_key_spaces_order_by_value():
+    """Derived key spaces: the table's distinct raw values in the reference's key order (Double.compare: -0.0 below
+    0.0, one NaN above +inf), keymaps from every segment's sorted distinct values to the global ids."""
+    from pinot_amd.plan import KeySpace, order_keys
+    d = np.array([3.5, -0.0, 0.0, np.nan, -np.inf, np.inf, -2.25, 3.5, np.nan], dtype=np.float64)
+    assert np.all(np.diff(order_keys(np.array([-np.inf, -2.25, -0.0, 0.0, 3.5, np.inf, np.nan]))) > 0)
+    segs = [ImmutableSegment.create(f"s{i}", {"x": v}, {"x": "DOUBLE"}, no_dictionary=("x",))
+            for i, v in enumerate((d[:5], d[4:]))]
+    ks = KeySpace.build("x", [s.columns["x"] for s in segs])
+    assert ks.kind == abi.PG_KEY_KEYMAP and ks.cardinality == 7
+    vals = ks.values
+    assert vals[:6] == [-np.inf, -2.25, 0.0, 0.0, 3.5, np.inf] and np.isnan(vals[6])
+    assert np.signbit(vals[2]) and not np.signbit(vals[3])
+    for s, (u, ids), km in zip(segs, ks.derived, ks.keymaps):
+        raw = s.columns["x"].raw_values
+        got = np.asarray(vals)[km[ids]]
+        assert np.array_equal(got, raw, equal_nan=True) and np.array_equal(np.signbit(got), np.signbit(raw))
+    # a LONG key wider than 2^32 values: derived too; a narrow one stays a value-offset space
+    wide = ImmutableSegment.create("w", {"x": np.array([-2 ** 40, 5, 2 ** 40])}, {"x": "LONG"}, no_dictionary=("x",))
+    assert KeySpace.build("x", [wide.columns["x"]]).values == [-2 ** 40, 5, 2 ** 40]
+    narrow = ImmutableSegment.create("n", {"x": np.array([-7, 5, 9])}, {"x": "LONG"}, no_dictionary=("x",))
+    assert KeySpace.build("x", [narrow.columns["x"]]).kind == abi.PG_KEY_VALUE_OFFSET
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cols,limit", [(("m_int",), 700), (("u", "k"), 1500), (("ts",), 2000)])
+@pytest.mark.parametrize("cols,limit", [(("m_int",), 700), (("u", "k"), 1500), (("ts",), 2000), (("g_double",), 2000),
+                                        (("g_float", "wide"), 3000)])
 def test_raw_group_by_limit_gpu(cols, limit, gpu_engine, oracle_engine, raw_table):
     """The device's per-segment truncation of raw keys equals the oracle's first-seen groups (and the limit flag)."""
     from helpers import assert_same_result
