@@ -159,7 +159,7 @@ class GpuEngine:
         spaces = list(plan.key_spaces)
         for ag in plan.aggs:
             if ag.function == "DISTINCTCOUNT":
-                spaces.append(table.key_space(ag.arg.cols[0]))
+                spaces.append(table.value_space(ag.arg.cols[0]))
         for ks in spaces:
             if ks.kind != abi.PG_KEY_KEYMAP:
                 continue
@@ -455,7 +455,7 @@ class GpuEngine:
             sets = (ra["offsets"], ra["ids"].astype(np.int64))
         kinds = [0 if ag.function in ("COUNT", "COUNTMV") else 3 if ag.function == "DISTINCTCOUNT" else
                  1 if ag.function == "AVG" else 2 for ag in plan.aggs]
-        dspaces = [plan.table.key_space(ag.arg.cols[0]) if k == 3 else None for ag, k in zip(plan.aggs, kinds)]
+        dspaces = [plan.table.value_space(ag.arg.cols[0]) if k == 3 else None for ag, k in zip(plan.aggs, kinds)]
         # column-wise conversion (one numpy -> list conversion per key / aggregation column instead of a Python call
         # per element): 90 groups x 2 aggregations decode in ~40 us instead of ~200 us
         kcols = []

@@ -280,7 +280,7 @@ class Table:
                 if c not in cols:
                     cols.append(c)
         self.column_ids = {c: i for i, c in enumerate(cols)}
-        self._key_spaces: Dict[str, "KeySpace"] = {}
+        self._key_spaces: Dict[Tuple[str, bool], "KeySpace"] = {}
         self._abs_bounds: Dict[str, Tuple[float, float, bool]] = {}
         self._searches: dict = {}      # DictSearch per (column, segment list)
 
@@ -342,11 +342,19 @@ class Table:
     def data_type(self, column: str) -> str:
         return self.segments[0].columns[column].data_type
 
-    def key_space(self, column: str) -> "KeySpace":
-        ks = self._key_spaces.get(column)
+    def key_space(self, column: str, derive: bool = False) -> "KeySpace":
+        ks = self._key_spaces.get((column, derive))
         if ks is None:
-            ks = KeySpace.build(column, [s.columns[column] for s in self.segments])
-            self._key_spaces[column] = ks
+            ks = KeySpace.build(column, [s.columns[column] for s in self.segments], derive)
+            self._key_spaces[(column, derive)] = ks
+        return ks
+
+    def value_space(self, column: str) -> "KeySpace":
+        """DISTINCTCOUNT's value ids: the key space, but a raw integer range too wide for a dense value bitmap takes
+        the derived dictionary encoding (distinct values only)."""
+        ks = self.key_space(column)
+        if ks.kind == abi.PG_KEY_VALUE_OFFSET and ks.cardinality > MAX_VALUE_OFFSET_KEYS:
+            ks = self.key_space(column, derive=True)
         return ks
 
 
@@ -388,7 +396,8 @@ class KeySpace:
     derived: Optional[List[Optional[Tuple[np.ndarray, np.ndarray]]]] = None
 
     @staticmethod
-    def build(column: str, cols: List[Column]) -> "KeySpace":
+    def build(column: str, cols: List[Column], derive: bool = False) -> "KeySpace":
+        """derive: a raw INT / LONG column takes the derived encoding even when its range fits value offsets."""
         dt = cols[0].data_type
         if any(c.dictionary is None for c in cols):
             if dt not in ("INT", "LONG", "FLOAT", "DOUBLE"):
@@ -402,7 +411,7 @@ class KeySpace:
                 # raw INT / LONG columns: value offsets as 32-bit key ids (pg_key.cardinality), read from the raw
                 # values on the device; a group key may span up to 2^32 - 1 values (the device state then hashes
                 # them); a DISTINCTCOUNT value set also needs a dense bitmap (checked at its use)
-                if span < 1 << 32:
+                if span < 1 << 32 and not derive:
                     return KeySpace(column, abi.PG_KEY_VALUE_OFFSET, span, lo)
             # raw FLOAT / DOUBLE, or a wider LONG range: every segment's values dictionary-encoded on the host (sorted
             # distinct values in the reference's key order + per-doc ids), keymapped to the table's sorted union; the
@@ -1074,10 +1083,7 @@ class CPlan:
                     if table.data_type(c) in ("STRING", "BYTES") and ag.function not in ("DISTINCTCOUNT",):
                         raise UnsupportedQuery(f"{ag.function} on non-numeric column {c}")
                 if ag.function == "DISTINCTCOUNT":
-                    ks = table.key_space(e.cols[0])
-                    if ks.kind == abi.PG_KEY_VALUE_OFFSET and ks.cardinality > MAX_VALUE_OFFSET_KEYS:
-                        raise UnsupportedQuery(f"DISTINCTCOUNT({e.cols[0]}): raw value range {ks.cardinality} too wide "
-                                               "for a value bitmap")
+                    ks = table.value_space(e.cols[0])
                     if derived_ids and ks.derived is not None:
                         aggs[i].col_a |= abi.PG_COL_DERIVED
                     aggs[i].key_kind = ks.kind

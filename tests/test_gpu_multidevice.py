@@ -6,7 +6,7 @@ the partial states itself (dense states element-wise after a device-to-device co
 exchange), as BaseCombineOperator.mergeResults merges one server's segments (operator/combine/
 BaseCombineOperator.java:190-233).  Every result must equal the CPU oracle over the whole table: configs 2 and 4 (the
 value sets of the DISTINCTCOUNT included), hash-grouped and wide (9-key tuple) group-bys, and exact double sums of
-wide-range data (bit-identical to the one-device run).  The library binds a process once, so each case runs in a
+wide-range data (bit-identical to the one-device run), raw FLOAT / DOUBLE / wide LONG keys.  The library binds a process once, so each case runs in a
 spawned process."""
 import os
 import sys
@@ -100,6 +100,12 @@ def _worker(devices, q):
             assert_same_result(got, orc.execute(tf, qc), table=tf)
             plan2 = eng.make_plan(tf, qc)
             assert _bits(eng.run_plan(plan2).rows) == _bits(got.rows), sql
+        # raw FLOAT / DOUBLE / wide LONG keys and wide DISTINCTCOUNT values (derived encodings, table-global ids)
+        from test_raw_index import RAW_QUERIES, _raw_segments
+        tr = Table("t", _raw_segments(4, 30_000, seed=3))
+        for sql in RAW_QUERIES:
+            if "g_" in sql or "wide" in sql or "DISTINCTCOUNT(ts)" in sql:
+                check(tr, sql)
         q.put((True, sorted(seen_modes)))
     except Exception:
         q.put((False, traceback.format_exc()))

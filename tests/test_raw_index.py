@@ -194,6 +194,9 @@ RAW_QUERIES = [
     "SELECT k, DISTINCTCOUNT(g_double), DISTINCTCOUNT(wide) FROM t GROUP BY k",
     "SELECT DISTINCTCOUNT(g_float), DISTINCTCOUNT(g_double), COUNT(*) FROM t WHERE k < 30",
     "SELECT g_double, SUM(g_double), COUNT(*) FROM t WHERE g_double > 100 GROUP BY g_double",
+    # a raw integer range too wide for a dense value bitmap (~1e9 values): DISTINCTCOUNT over the derived encoding
+    "SELECT k, DISTINCTCOUNT(ts) FROM t WHERE m_int > 4000 GROUP BY k",
+    "SELECT DISTINCTCOUNT(ts), DISTINCTCOUNT(m_int), COUNT(*) FROM t",
 ]
 
 
