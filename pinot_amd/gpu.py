@@ -8,6 +8,7 @@ from __future__ import annotations
 import collections
 import ctypes as C
 import dataclasses
+import importlib.util
 import itertools
 import os
 import threading
@@ -41,6 +42,12 @@ def load_library(path: str = LIB_PATH):
         if _lib is None:
             if not os.path.exists(path):
                 raise FileNotFoundError(f"{path} missing: build it with `make -C pinot_amd/csrc`")
+            # one HIP runtime per process: torch's bundled libamdhip64 carries the same SONAME (libamdhip64.so.7) as
+            # the /opt/rocm one the library is linked against, so with torch loaded first the dynamic linker binds the
+            # library to torch's runtime instead of mapping a second one beside it (torch loaded after the library
+            # would map its own); the Python host uses torch for device memory and streams, so load it first
+            if importlib.util.find_spec("torch") is not None:
+                import torch  # noqa: F401
             _lib = abi.declare(C.CDLL(path))
             if _lib.pg_abi_version() != abi.PG_ABI_VERSION:
                 raise RuntimeError("libpinot_gpu ABI version mismatch")

@@ -220,3 +220,14 @@ def test_vectorized_image_matches_the_per_segment_writer(sv_segment):
     hs, ls = _decode_image_leaves(slow)
     assert lf == ls
     assert (hf.num_segments, hf.num_leaves, hf.flags, hf.limit) == (hs.num_segments, hs.num_leaves, hs.flags, hs.limit)
+
+
+def test_one_hip_runtime_per_process():
+    """The library and torch share one HIP runtime in a Python process (gpu.load_library loads torch first; both
+    libamdhip64 builds have the SONAME libamdhip64.so.7): no second runtime mapped, whichever is imported first."""
+    import subprocess
+    import sys
+    code = ("import pinot_amd.gpu as g; g.load_library(); import torch; "
+            "print(len({l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l}))")
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, check=True)
+    assert out.stdout.strip() == "1", out.stdout + out.stderr
