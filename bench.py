@@ -251,9 +251,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="per CPU leg")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--inflight", type=int, default=4,
-                    help="queries in flight in the timed loop (host threads, each with its own stream; 1 GPU only): "
-                         "one query's host work (lowering to the device plan, launches, result decode) overlaps the "
-                         "previous query's kernels, as concurrent queries on a server do; 1 = strictly serial")
+                    help="queries in flight in the timed loop (host threads, each with its own stream): one query's "
+                         "host work (lowering to the device plan, launches, result decode; at N > 1 the cross-rank "
+                         "merge) overlaps the other queries' kernels, as concurrent queries on a server do; 1 = serial")
     ap.add_argument("--no-full-parity", action="store_true",
                     help="skip the oracle check of the timed result over every segment (parity_full)")
     ap.add_argument("--traffic-file", default=None, help="PMC HBM traffic of the hot-path kernels (tools/profile_bench.sh)")
@@ -409,27 +409,39 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     serial_ms = el / args.steps * 1e3
-    inflight = args.inflight if world == 1 else 1
+    inflight = args.inflight
     if inflight > 1:
-        # the same K steps with `inflight` queries in flight: each host thread runs whole queries (its own stream and
-        # parameter arena in the library); the kernel phase times above (one query at a time) stay the roofline's
+        # the same K steps with `inflight` queries in flight: host threads run the per-GPU part of whole queries (each
+        # its own stream and parameter arena in the library) while this thread completes them in submission order --
+        # at N > 1 the cross-rank merge (its collectives issued by this one thread, in the same order on every rank);
+        # the kernel phase times above (one query at a time) stay the roofline's
         import threading
         from concurrent.futures import ThreadPoolExecutor
         gate = threading.Barrier(inflight)
+        run = eng.run_plan if world == 1 else eng.run_partial
 
         def first(_):  # every pool thread makes its stream / arena before the timed region
             gate.wait()
-            return eng.run_plan(plan)
+            return run(plan)
+
+        def complete(r):
+            return r if world == 1 else merge_partials_across_ranks(eng, plan, r)
 
         with ThreadPoolExecutor(inflight) as ex:
-            list(ex.map(first, range(inflight)))
-            for _ in range(args.warmup):
-                list(ex.map(lambda _: eng.run_plan(plan), range(inflight)))
+            for f in [ex.submit(first, i) for i in range(inflight)]:
+                complete(f.result())
+            for f in [ex.submit(run, plan) for _ in range(args.warmup)]:
+                complete(f.result())
             torch.cuda.synchronize()
+            if dist:
+                dist.barrier()
             t0 = time.perf_counter()
-            futs = [ex.submit(eng.run_plan, plan) for _ in range(args.steps)]
-            res = [f.result() for f in futs][-1]
+            futs = [ex.submit(run, plan) for _ in range(args.steps)]
+            for f in futs:
+                res = complete(f.result())
             torch.cuda.synchronize()
+            if dist:
+                dist.barrier()
             el = time.perf_counter() - t0
     if dist:
         t = torch.tensor([el], dtype=torch.float64, device="cpu" if share else dev)
