@@ -46,7 +46,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, backend="gloo"):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
@@ -54,8 +54,11 @@ def _worker(rank, world, port, q):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import torch
         import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.cuda.set_device(0)
+        if backend == "nccl":  # RCCL (one rank: the box has one GPU, and RCCL refuses two ranks on one device)
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
         from helpers import assert_same_result
         from oracle.oracle import OracleEngine
         from pinot_amd import abi, synth
@@ -86,6 +89,13 @@ def _worker(rank, world, port, q):
             flags = abi.PG_PLAN_VALUE_SETS | (abi.PG_PLAN_HASH_GROUPS if hash_rank0 and rank == 0 else 0)
             plan = eng.make_plan(table, qc, segments=mine, flags=flags)
             assert_same_result(merge_partials_across_ranks(eng, plan, eng.run_partial(plan)), whole, table=table)
+        # queries in flight (bench.py --inflight): worker threads run the per-GPU part while this thread merges each
+        # query across ranks in submission order
+        from concurrent.futures import ThreadPoolExecutor
+        plan = eng.make_plan(table, qc, segments=mine, flags=abi.PG_PLAN_VALUE_SETS)
+        with ThreadPoolExecutor(3) as ex:
+            for f in [ex.submit(eng.run_partial, plan) for _ in range(8)]:
+                assert_same_result(merge_partials_across_ranks(eng, plan, f.result()), whole, table=table)
         q.put((rank, True, paths))
         dist.destroy_process_group()
     except Exception:
@@ -106,6 +116,21 @@ def test_two_ranks_merge_device_partials():
     for rank, ok, info in res:
         assert ok, info
     assert "dense" in res[0][2] and "rows" in res[0][2]
+
+
+def test_rccl_one_rank_merge_device_partials():
+    """The same merges over RCCL (backend "nccl"): one rank, so the collectives are RCCL's single-rank all-reduce /
+    all_to_all / all_gather, run on torch's stream between the library's own streams -- the hand-off of the library's
+    partial state to RCCL and back, on the real collective library (N > 1 needs an 8-GPU node)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(0, 1, _free_port(), q, "nccl"))
+    p.start()
+    rank, ok, info = q.get(timeout=240)
+    p.join(timeout=60)
+    assert ok, info
+    assert "dense" in info and "rows" in info
 
 
 DOUBLE_CASES = [
