@@ -59,9 +59,9 @@ METADATA_BY_ID = {v[0]: (k, v[1]) for k, v in METADATA_KEYS.items()}
 
 # ObjectSerDeUtils.ObjectType ids of the intermediate types the device path produces
 OBJ_STRING, OBJ_LONG, OBJ_DOUBLE, OBJ_AVG_PAIR, OBJ_INT_SET = 0, 1, 2, 4, 9
-OBJ_LONG_SET, OBJ_FLOAT_SET, OBJ_DOUBLE_SET, OBJ_STRING_SET, OBJ_NULL = 15, 16, 17, 18, 100
+OBJ_LONG_SET, OBJ_FLOAT_SET, OBJ_DOUBLE_SET, OBJ_STRING_SET, OBJ_BYTES_SET, OBJ_NULL = 15, 16, 17, 18, 19, 100
 SET_TYPE_OF_COLUMN = {"INT": OBJ_INT_SET, "LONG": OBJ_LONG_SET, "FLOAT": OBJ_FLOAT_SET, "DOUBLE": OBJ_DOUBLE_SET,
-                      "STRING": OBJ_STRING_SET}
+                      "STRING": OBJ_STRING_SET, "BYTES": OBJ_BYTES_SET}
 _SET_FMT = {OBJ_INT_SET: ">i", OBJ_LONG_SET: ">q", OBJ_FLOAT_SET: ">f", OBJ_DOUBLE_SET: ">d"}
 
 # AggregationFunctionType.getName() (pinot-segment-spi/.../AggregationFunctionType.java)
@@ -109,7 +109,7 @@ def _s(b: bytearray, text: str):
 
 def _fixed_width(t: str) -> int:
     """DataTableUtils.computeColumnOffsets for V3."""
-    return {"INT": 4, "LONG": 8, "FLOAT": 8, "DOUBLE": 8, "STRING": 4}.get(t, 8)
+    return {"INT": 4, "LONG": 8, "FLOAT": 8, "DOUBLE": 8, "STRING": 4, "BYTES": 4}.get(t, 8)
 
 
 def serialize_object(type_id: int, value) -> bytes:
@@ -130,6 +130,12 @@ def serialize_object(type_id: int, value) -> bytes:
         for v in sorted(value):
             _s(out, v)
         return bytes(out)
+    if type_id == OBJ_BYTES_SET:  # BYTES_SET_SER_DE (ObjectSerDeUtils.java:774-793): size, then (length, bytes) each
+        out = bytearray(struct.pack(">i", len(value)))
+        for v in sorted(value):
+            raw = bytes.fromhex(v)
+            out += struct.pack(">i", len(raw)) + raw
+        return bytes(out)
     raise ValueError(f"object type {type_id}")
 
 
@@ -148,11 +154,12 @@ def deserialize_object(type_id: int, raw: bytes):
         n = struct.unpack_from(">i", raw)[0]
         w = struct.calcsize(_SET_FMT[type_id])
         return {struct.unpack_from(_SET_FMT[type_id], raw, 4 + i * w)[0] for i in range(n)}
-    if type_id == OBJ_STRING_SET:
+    if type_id in (OBJ_STRING_SET, OBJ_BYTES_SET):
         n, pos, out = struct.unpack_from(">i", raw)[0], 4, set()
         for _ in range(n):
             ln = struct.unpack_from(">i", raw, pos)[0]
-            out.add(raw[pos + 4:pos + 4 + ln].decode("utf-8"))
+            b = raw[pos + 4:pos + 4 + ln]
+            out.add(b.decode("utf-8") if type_id == OBJ_STRING_SET else b.hex())
             pos += 4 + ln
         return out
     raise ValueError(f"object type {type_id}")
@@ -186,7 +193,7 @@ def to_bytes(dt: DataTable) -> bytes:
                     cell = struct.pack(">f", float(v))
                 elif t == "DOUBLE":
                     cell = struct.pack(">d", float(v))
-                elif t == "STRING":
+                elif t in ("STRING", "BYTES"):  # BYTES: its hex string (DataTableBuilderV2V3.setColumn(ByteArray) :69-72)
                     d = dictionary.setdefault(name, {})
                     cell = struct.pack(">i", d.setdefault(str(v), len(d)))
                 elif t == "OBJECT":
@@ -303,7 +310,7 @@ def from_bytes(b: bytes) -> DataTable:
                     row.append(struct.unpack_from(">f", b, at)[0])
                 elif t == "DOUBLE":
                     row.append(struct.unpack_from(">d", b, at)[0])
-                elif t == "STRING":
+                elif t in ("STRING", "BYTES"):
                     row.append(rev[name][struct.unpack_from(">i", b, at)[0]])
                 else:
                     p, ln = struct.unpack_from(">ii", b, at)
@@ -366,7 +373,8 @@ def _cell(ag: Aggregation, v, column_type):
 def result_to_datatable(query: QueryContext, res: IntermediateResult, column_type,
                         groups_limit_reached: bool = False) -> DataTable:
     """The server's DataTable for an aggregation / group-by result (IntermediateResultsBlock.getDataTable).
-    `column_type(name)` gives a column's stored data type (INT / LONG / FLOAT / DOUBLE / STRING)."""
+    `column_type(name)` gives a column's stored data type (INT / LONG / FLOAT / DOUBLE / STRING / BYTES; BYTES values
+    as hex strings, as the reference's DataTable V3 carries them)."""
     aggs = res.aggregations
     md = _stats_metadata(res.stats, groups_limit_reached)
     if not res.group_by:

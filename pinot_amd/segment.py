@@ -228,6 +228,8 @@ class Dictionary:
             return float(np.float32(float(value)))
         if t == "DOUBLE":
             return float(value)
+        if t == "BYTES":
+            return _hex(value)
         return str(value)
 
     def insertion_index_of(self, value) -> int:
@@ -258,7 +260,8 @@ class Dictionary:
             return self.values.astype(_NP_BE[self.data_type]).tobytes()
         out = bytearray()
         for s in self.values:
-            b = s.encode("utf-8") if isinstance(s, str) else bytes(s)
+            # BYTES (hex strings here, as the reference presents them): the raw bytes (BytesDictionary)
+            b = bytes.fromhex(s) if self.data_type == "BYTES" else s.encode("utf-8") if isinstance(s, str) else bytes(s)
             out += b + b"\0" * (self.entry_bytes - len(b))
         return bytes(out)
 
@@ -271,6 +274,9 @@ class Dictionary:
         vals = []
         for i in range(cardinality):
             raw = buf[i * entry_bytes:(i + 1) * entry_bytes]
+            if data_type == "BYTES":  # BytesDictionary: getUnpaddedBytes with padding byte 0
+                vals.append(raw.rstrip(b"\0").hex())
+                continue
             # StringDictionary strips the padding character from the right
             vals.append(raw.rstrip(padding).decode("utf-8"))
         return Dictionary(data_type, vals, entry_bytes)
@@ -282,11 +288,26 @@ def build_dictionary(data_type: str, values) -> (Dictionary, np.ndarray):
         arr = np.asarray(values, dtype=_NP_NATIVE[data_type])
         uniq, inv = np.unique(arr, return_inverse=True)
         return Dictionary(data_type, uniq), inv.astype(np.int32)
+    if data_type == "BYTES":
+        # BYTES values as lowercase hex strings (bytes / bytearray accepted): their string order is the unsigned
+        # lexicographic byte order SegmentDictionaryCreator sorts ByteArray values in; entries are the raw bytes
+        arr = np.asarray([_hex(v) for v in values], dtype=object).astype(str)
+        uniq, inv = np.unique(arr, return_inverse=True)
+        uniq = [str(u) for u in uniq]
+        eb = max((len(u) // 2 for u in uniq), default=0)
+        return Dictionary(data_type, uniq, eb), inv.astype(np.int32)
     arr = np.asarray(values, dtype=object).astype(str)
     uniq, inv = np.unique(arr, return_inverse=True)
     uniq = [str(u) for u in uniq]
     eb = max((len(u.encode("utf-8")) for u in uniq), default=0)
     return Dictionary(data_type, uniq, eb), inv.astype(np.int32)
+
+
+def _hex(v) -> str:
+    """A BYTES value as the reference's hex string form (BytesUtils.toHexString: lowercase)."""
+    if isinstance(v, (bytes, bytearray, memoryview)):
+        return bytes(v).hex()
+    return bytes.fromhex(str(v)).hex()
 
 
 # ----------------------------------------------------------------------------- raw (no-dictionary) forward index
@@ -694,7 +715,7 @@ class ImmutableSegment:
                  "segment.padding.character = \\\\u0000"]
         for c in self.columns.values():
             p = f"column.{c.name}."
-            eb = c.dictionary.entry_bytes if c.data_type == 'STRING' and c.dictionary is not None else 0
+            eb = c.dictionary.entry_bytes if c.data_type in ("STRING", "BYTES") and c.dictionary is not None else 0
             props += [p + f"cardinality = {c.cardinality}", p + f"totalDocs = {c.num_docs}",
                       p + f"dataType = {c.data_type}", p + f"bitsPerElement = {c.bits_per_element}",
                       p + f"lengthOfEachEntry = {eb}",
@@ -781,7 +802,7 @@ class ImmutableSegment:
             dtype = p("dataType")
             card = int(p("cardinality"))
             b = int(p("bitsPerElement"))
-            eb = int(p("lengthOfEachEntry")) if dtype == "STRING" else 0
+            eb = int(p("lengthOfEachEntry")) if dtype in ("STRING", "BYTES") else 0
             if props.get(f"column.{cname}.hasDictionary", "true") == "false":
                 # DefaultIndexReaderProvider.java:92-101: a raw chunked forward index
                 fwd = index_bytes(cname, "raw")

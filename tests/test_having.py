@@ -5,7 +5,7 @@ applied by the broker reduce to its sorted records until LIMIT rows passed (Grou
 HavingFilterHandler).
 
 Pinned by the reference's own known answers: HavingFilterHandlerTest.java:33-104 (rows and isMatch results restated
-below; its all-types case without the BYTES key, which the device path does not group by)."""
+below; its BYTES key case is in tests/test_bytes_columns.py)."""
 import pytest
 
 from helpers import assert_same_result
