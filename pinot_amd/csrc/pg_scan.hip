@@ -1238,6 +1238,9 @@ __device__ __forceinline__ void scan_body() {
     if (tid == 0) q.part_count[blockIdx.x] = h[0];
   } else if (q.use_lds) {
     __syncthreads();
+#ifdef PG_LIST_FLUSH_SKIP  // dev ablation only (wrong results): the block's table is not added to the global state
+    if (q.list_mode) return;
+#endif
     for (uint64_t g = tid; g < q.num_slots; g += kBlock) {
       if (l_i64[g * q.n_i64] == 0) continue;
       for (uint32_t s = 0; s < q.n_i64; s++) {
