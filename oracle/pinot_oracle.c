@@ -743,8 +743,12 @@ static uint64_t raw_key_ids(const orc_column *c, int32_t *ids, uint64_t n, int32
   return m.n;
 }
 
+/* n = the group-by rows; row_doc (NULL: row i is match i) maps a row to its match index: a multi-value key expands
+ * each matched doc into one row per value (DictionaryBasedGroupKeyGenerator.generateKeysForBlock(.., int[][]) :188-200
+ * + getIntRawKeys :472-: a single MV column's raw keys are the doc's dictIds in stored order, SV keys folded in), and
+ * aggregateGroupByMV updates every group of the doc with the doc's value (e.g. SumAggregationFunction.java:239-249) */
 static void aggregate_group_by(const pg_plan *plan, const orc_column *cols, const uint32_t *docs, uint64_t n,
-                               agg_input *inputs, int32_t **key_ids, orc_segment_result *r,
+                               const uint64_t *row_doc, agg_input *inputs, int32_t **key_ids, orc_segment_result *r,
                                uint64_t array_based_threshold, int32_t *const *raw_rep, const uint64_t *raw_cards) {
   uint32_t K = plan->num_keys, A = plan->num_aggs;
   uint64_t card_prod = 1;
@@ -809,19 +813,20 @@ static void aggregate_group_by(const pg_plan *plan, const orc_column *cols, cons
   for (uint64_t i = 0; i < n; i++) {
     int32_t g = gids[i];
     if (g < 0) continue;
-    uint32_t d = docs[i];
+    const uint64_t mi = row_doc ? row_doc[i] : i;  /* the row's match */
+    uint32_t d = docs[mi];
     for (uint32_t a = 0; a < A; a++) {
       const pg_agg *ag = &plan->aggs[a];
       double *v = &vals[(uint64_t)g * A + a];
       switch (ag->fn) {
         case PG_AGG_COUNT: *v += 1.0; break;
         case PG_AGG_COUNTMV: *v += (double)(inputs[a].mv.offsets[d + 1] - inputs[a].mv.offsets[d]); break;
-        case PG_AGG_SUM: *v += agg_value(ag, cols, &inputs[a], i); break;
-        case PG_AGG_AVG: *v += agg_value(ag, cols, &inputs[a], i); cnts[(uint64_t)g * A + a] += 1; break;
-        case PG_AGG_MIN: { double x = agg_value(ag, cols, &inputs[a], i); if (x < *v) *v = x; break; }
-        case PG_AGG_MAX: { double x = agg_value(ag, cols, &inputs[a], i); if (x > *v) *v = x; break; }
+        case PG_AGG_SUM: *v += agg_value(ag, cols, &inputs[a], mi); break;
+        case PG_AGG_AVG: *v += agg_value(ag, cols, &inputs[a], mi); cnts[(uint64_t)g * A + a] += 1; break;
+        case PG_AGG_MIN: { double x = agg_value(ag, cols, &inputs[a], mi); if (x < *v) *v = x; break; }
+        case PG_AGG_MAX: { double x = agg_value(ag, cols, &inputs[a], mi); if (x > *v) *v = x; break; }
         case PG_AGG_DISTINCTCOUNT:
-          pairs[np++] = (((uint64_t)g * A + a) << 32) | (uint32_t)inputs[a].ids_a[i];
+          pairs[np++] = (((uint64_t)g * A + a) << 32) | (uint32_t)inputs[a].ids_a[mi];
           break;
       }
     }
@@ -1006,16 +1011,52 @@ int orc_execute_segment(const pg_plan *plan, uint32_t seg, const orc_column *col
   }
   int32_t *key_ids[64] = {0}, *raw_rep[64] = {0};
   uint64_t raw_cards[64] = {0};
+  int mvk = -1;  /* the (one) multi-value group key */
   for (uint32_t k = 0; k < plan->num_keys; k++) {
     const orc_column *kc = &cols[plan->keys[k].col_id];
+    used[plan->keys[k].col_id] = 1;
+    if (kc->fwd_kind == ORC_FWD_MV) {
+      if (mvk >= 0) {  /* several MV keys (a cartesian product per doc): not restated */
+        for (uint32_t j = 0; j < k; j++) free(key_ids[j]);
+        for (uint32_t a = 0; a < plan->num_aggs; a++) { free(inputs[a].ids_a); free(inputs[a].ids_b); if (inputs[a].has_mv) free(inputs[a].mv.offsets); }
+        free(inputs); free(docs); free(r);
+        return -3;
+      }
+      mvk = (int)k;
+      continue;
+    }
     key_ids[k] = sv_dict_ids_at(kc, docs, n);
     if (kc->fwd_kind == ORC_FWD_RAW) raw_cards[k] = raw_key_ids(kc, key_ids[k], n, &raw_rep[k]);
-    used[plan->keys[k].col_id] = 1;
   }
   for (int i = 0; i < 256; i++) projected += used[i];
+  uint64_t *row_doc = NULL, nrows = n;
+  if (mvk >= 0) {  /* one group-by row per (matched doc, value of its MV key), in doc then stored-value order */
+    const orc_column *kc = &cols[plan->keys[mvk].col_id];
+    mv_view v;
+    mv_open(kc, &v);
+    nrows = 0;
+    for (uint64_t i = 0; i < n; i++) nrows += v.offsets[docs[i] + 1] - v.offsets[docs[i]];
+    row_doc = (uint64_t *)malloc(sizeof(uint64_t) * (nrows ? nrows : 1));
+    int32_t *sv_ids[64];
+    for (uint32_t k = 0; k < plan->num_keys; k++) {
+      sv_ids[k] = key_ids[k];
+      key_ids[k] = (int32_t *)malloc(sizeof(int32_t) * (nrows ? nrows : 1));
+    }
+    uint64_t row = 0;
+    for (uint64_t i = 0; i < n; i++)
+      for (uint64_t j = v.offsets[docs[i]]; j < v.offsets[docs[i] + 1]; j++, row++) {
+        row_doc[row] = i;
+        for (uint32_t k = 0; k < plan->num_keys; k++)
+          key_ids[k][row] = (int)k == mvk ? (int32_t)read_bits(v.raw, j, kc->bits) : sv_ids[k][i];
+      }
+    for (uint32_t k = 0; k < plan->num_keys; k++) free(sv_ids[k]);
+    free(v.offsets);
+  }
 
   if (plan->num_keys == 0) aggregate_only(plan, cols, docs, n, inputs, r);
-  else aggregate_group_by(plan, cols, docs, n, inputs, key_ids, r, array_based_threshold, raw_rep, raw_cards);
+  else aggregate_group_by(plan, cols, docs, nrows, row_doc, inputs, key_ids, r, array_based_threshold, raw_rep,
+                          raw_cards);
+  free(row_doc);
 
   r->stats.num_docs_scanned = n;
   r->stats.num_entries_scanned_in_filter = scanned;

@@ -847,7 +847,7 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
 #pragma unroll
       for (int k = 0; k < NK; k++) {
         kidx[x][k] = 0;
-        if (GROUPED && k < (int)q.num_keys)
+        if (GROUPED && k < (int)q.num_keys && (uint32_t)k != q.mv_key)
           kidx[x][k] = col_id(q, Rows::kTile ? q.key_slot[k] : (uint32_t)kNoSlot, ldc(sd.keycols, k), stage, d[x], rel);
       }
 #pragma unroll
@@ -890,6 +890,40 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
       }
       if (jj[x] >= 32u) continue;
       if constexpr (GROUPED) {
+        if (q.mv_key != kNoMvKey) {
+          // a multi-value key: the doc joins the group of each value in its list, in stored order (duplicates
+          // included), each with the doc's aggregation inputs (aggregateGroupByMV)
+          uint64_t g0 = 0;
+          bool in_range = true;
+#pragma unroll
+          for (int k = 0; k < NK; k++) {
+            if (k >= (int)q.num_keys) break;
+            if ((uint32_t)k == q.mv_key) continue;
+            const uint64_t kid = key_of(q.key_kind[k], q.key_base[k], ldc(sd.keycols, k), kidx[x][k]);
+            in_range &= kid < q.key_card[k];
+            g0 += kid * q.key_stride[k];
+          }
+          const ColDesc mk = ldc(sd.keycols, q.mv_key);
+          const PG_GLOBAL uint32_t* off = glb(mk.mv_offsets);
+          const uint32_t v0 = off[d[x]], v1 = off[d[x] + 1];
+          const rsrc_t rs = make_rsrc(mk.words, mk.wbytes);
+          for (uint32_t v = v0; v < v1; v++) {
+            const uint64_t kid = key_of(q.key_kind[q.mv_key], q.key_base[q.mv_key], mk, unpack(rs, v, mk.bits));
+            if (!in_range || kid >= q.key_card[q.mv_key]) {  // never expected: the host proved the key ranges
+              atomicOr(q.err, 1u);
+              continue;
+            }
+            const uint64_t g = group_slot(q, g0 + kid * q.key_stride[q.mv_key], sd.index, d[x]);
+            if (g == ~0ull) continue;
+            s_add(S, &S.i64[g * q.n_i64], 1ull);
+#pragma unroll
+            for (int a = 0; a < MAXA; a++) {
+              if (a >= (int)q.num_aggs) break;
+              group_update(q, S, q.aggs[a], sd.aggcols + 2 * a, g, d[x], ia[x][a], ib[x][a]);
+            }
+          }
+          continue;
+        }
         uint64_t g = 0;
         bool in_range = true;
 #pragma unroll
@@ -1155,7 +1189,8 @@ __device__ __forceinline__ void scan_body() {
         if (!GROUPED) doc_count += nm;
         if (GROUPED || q.agg_reads) {
           // dense when at least a quarter of the lanes hold >= 8 matches: batched rows; else per-doc rounds
-          if (__popcll(__ballot(nm >= 8)) >= 16) aggregate_dense<GROUPED, MAXA, MAXK>(q, sd, S, st, acc, m, base, tid);
+          if (__popcll(__ballot(nm >= 8)) >= 16 && (!GROUPED || q.mv_key == kNoMvKey))
+            aggregate_dense<GROUPED, MAXA, MAXK>(q, sd, S, st, acc, m, base, tid);
           else aggregate_tile<GROUPED, MAXA, MAXK>(q, sd, S, st, acc, m, rows);
         }
       }

@@ -342,6 +342,9 @@ class Table:
     def data_type(self, column: str) -> str:
         return self.segments[0].columns[column].data_type
 
+    def multi_value(self, column: str) -> bool:
+        return any(not s.columns[column].single_value for s in self.segments if column in s.columns)
+
     def key_space(self, column: str, derive: bool = False) -> "KeySpace":
         ks = self._key_spaces.get((column, derive))
         if ks is None:
@@ -1080,8 +1083,14 @@ class CPlan:
                         raise UnsupportedQuery(f"{ag.function} over an expression")
                     aggs[i].col_b = cid[e.cols[1]]
                 for c in e.cols:
-                    if table.data_type(c) in ("STRING", "BYTES") and ag.function not in ("DISTINCTCOUNT",):
+                    if table.data_type(c) in ("STRING", "BYTES") and ag.function not in ("DISTINCTCOUNT", "COUNTMV"):
                         raise UnsupportedQuery(f"{ag.function} on non-numeric column {c}")
+                    # the SV functions read getXxxValuesSV / getDictionaryIdsSV and COUNTMV getNumMVEntries: a
+                    # function over the other kind of column fails in the reference too (SUMMV, DISTINCTCOUNTMV, ...
+                    # are other functions)
+                    if table.multi_value(c) != (ag.function == "COUNTMV"):
+                        raise UnsupportedQuery(f"{ag.function} over {'multi' if table.multi_value(c) else 'single'}"
+                                               f"-value column {c}")
                 if ag.function == "DISTINCTCOUNT":
                     ks = table.value_space(e.cols[0])
                     if derived_ids and ks.derived is not None:
@@ -1102,6 +1111,10 @@ class CPlan:
             ks = table.key_space(col)
             self.key_spaces.append(ks)
             keys[k].col_id = cid[col] | (abi.PG_COL_DERIVED if derived_ids and ks.derived is not None else 0)
+        # a multi-value key groups each value of a doc's list (DictionaryBasedGroupKeyGenerator :188-200); several would
+        # group the cartesian product of their lists, which neither side restates
+        if sum(table.multi_value(c) for c in query.group_by) > 1:
+            raise UnsupportedQuery("GROUP BY over more than one multi-value column")
             keys[k].kind = ks.kind
             keys[k].cardinality = ks.cardinality
             keys[k].base = ks.base
