@@ -1111,13 +1111,13 @@ class CPlan:
             ks = table.key_space(col)
             self.key_spaces.append(ks)
             keys[k].col_id = cid[col] | (abi.PG_COL_DERIVED if derived_ids and ks.derived is not None else 0)
+            keys[k].kind = ks.kind
+            keys[k].cardinality = ks.cardinality
+            keys[k].base = ks.base
         # a multi-value key groups each value of a doc's list (DictionaryBasedGroupKeyGenerator :188-200); several would
         # group the cartesian product of their lists, which neither side restates
         if sum(table.multi_value(c) for c in query.group_by) > 1:
             raise UnsupportedQuery("GROUP BY over more than one multi-value column")
-            keys[k].kind = ks.kind
-            keys[k].cardinality = ks.cardinality
-            keys[k].base = ks.base
         self._keep.append(keys)
 
         p = abi.pg_plan()

@@ -135,6 +135,16 @@ def _col_val(seg, c, i):
     return [col.dictionary.values[j] for j in col.dict_ids[o[i]:o[i + 1]]]
 
 
+def test_plan_keys_carry_the_key_spaces(mv_table):
+    """The pg_key of every group-by column carries its table-global key space (kind, cardinality, base)."""
+    from pinot_amd.plan import CPlan
+    p = CPlan(mv_table, parse("SELECT k, tags, COUNT(*) FROM t GROUP BY k, tags"), mv_table.segments, [1, 2, 3])
+    for i, c in enumerate(("k", "tags")):
+        ks = mv_table.key_space(c)
+        assert (p.plan.keys[i].kind, p.plan.keys[i].cardinality, p.plan.keys[i].base) == \
+            (ks.kind, ks.cardinality, ks.base) and ks.cardinality > 0
+
+
 @pytest.mark.parametrize("sql", [
     "SELECT tags, words, COUNT(*) FROM t GROUP BY tags, words",   # two MV keys: a cartesian product per doc
     "SELECT k, SUM(tags) FROM t GROUP BY k",                       # an SV function over an MV column
