@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 8
+#define PG_ABI_VERSION 9
 
 typedef enum pg_status {
   PG_OK = 0,
@@ -240,10 +240,15 @@ typedef struct pg_agg {
                           holding them, or a product / sum that overflows), so every GPU keeps the same slots for them;
                           PG_SUM_BOUNDS = sum_exp / sum_exp_lo are given */
   int32_t sum_exp_lo;
-  uint32_t pad;
+  uint32_t flags;   /* PG_AGG_MV_VALUES (ABI 9; zero before) */
 } pg_agg;
 #define PG_SUM_NONFINITE 0x1u
 #define PG_SUM_BOUNDS 0x2u
+/* pg_agg.flags: fn (SUM / MIN / MAX / AVG / DISTINCTCOUNT, op PG_EXPR_COL) over EVERY value of the multi-value column
+ * col_a -- SumMVAggregationFunction, MinMVAggregationFunction, MaxMVAggregationFunction, AvgMVAggregationFunction,
+ * DistinctCountMVAggregationFunction (query/aggregation/function/): the single-value function's intermediate and
+ * final types, aggregate() over getDictionaryIdsMV / getDoubleValuesMV; AVG counts the values, not the docs */
+#define PG_AGG_MV_VALUES 0x1u
 
 typedef enum pg_key_kind {
   PG_KEY_VALUE_OFFSET = 0,  /* INT/LONG dictionary: global id = value - base                         */

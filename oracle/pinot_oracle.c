@@ -488,9 +488,29 @@ static int eval_filter(const pg_plan *plan, const pg_leaf *leaves, const orc_col
 
 typedef struct agg_input {
   int32_t *ids_a, *ids_b;   /* SV dictIds */
-  mv_view mv;               /* COUNTMV */
+  mv_view mv;               /* COUNTMV and the MV-value functions (PG_AGG_MV_VALUES) */
   int has_mv;
+  const orc_column *mvc;    /* PG_AGG_MV_VALUES: the multi-value column */
 } agg_input;
+
+/* A doc's values of a multi-value column in stored order (getDoubleValuesMV / getDictionaryIdsMV): value v of
+ * [mv.offsets[d], mv.offsets[d + 1]) is the dictId packed at position v. */
+static inline int32_t mv_id(const agg_input *in, uint64_t v) {
+  return (int32_t)read_bits(in->mv.raw, v, in->mvc->bits);
+}
+
+/* SumMV / AvgMV / MinMV / MaxMV over doc d (SumMVAggregationFunction.aggregate: `for value : values[i]: sum += value`,
+ * AvgMV counting the values, MinMV / MaxMV by `<` / `>` on the double values): folded into *acc, *cnt += numValues */
+static inline void mv_fold(const pg_agg *g, const agg_input *in, uint32_t d, double *acc, int64_t *cnt) {
+  const uint64_t v0 = in->mv.offsets[d], v1 = in->mv.offsets[d + 1];
+  for (uint64_t v = v0; v < v1; v++) {
+    const double x = dict_double(in->mvc, mv_id(in, v));
+    if (g->fn == PG_AGG_MIN) { if (x < *acc) *acc = x; }
+    else if (g->fn == PG_AGG_MAX) { if (x > *acc) *acc = x; }
+    else *acc += x;
+  }
+  if (cnt) *cnt += (int64_t)(v1 - v0);
+}
 
 /* Transform value: TransformFunction.transformToDoubleValuesSV; MultiplicationTransformFunction
  * (transform/function/MultiplicationTransformFunction.java:91-111) starts from the literal product 1.0
@@ -533,6 +553,23 @@ static void aggregate_only(const pg_plan *plan, const orc_column *cols, const ui
     for (uint32_t a = 0; a < A; a++) {
       const pg_agg *g = &plan->aggs[a];
       agg_input *in = &inputs[a];
+      if (g->flags & PG_AGG_MV_VALUES) {  /* *MVAggregationFunction.aggregate over the block's docs */
+        if (g->fn == PG_AGG_DISTINCTCOUNT) {
+          for (uint64_t i = b0; i < b1; i++)
+            for (uint64_t v = in->mv.offsets[docs[i]]; v < in->mv.offsets[docs[i] + 1]; v++) distinct[a][mv_id(in, v)] = 1;
+        } else if (g->fn == PG_AGG_AVG) {  /* block-local sum and count, then AvgPair.apply */
+          double s2 = 0.0;
+          int64_t c2 = 0;
+          for (uint64_t i = b0; i < b1; i++) mv_fold(g, in, docs[i], &s2, &c2);
+          r->values[a] += s2;
+          r->counts[a] += c2;
+        } else {  /* SUM / MIN / MAX: running value carried through the holder */
+          double m = r->values[a];
+          for (uint64_t i = b0; i < b1; i++) mv_fold(g, in, docs[i], &m, NULL);
+          r->values[a] = m;
+        }
+        continue;
+      }
       switch (g->fn) {
         case PG_AGG_COUNT: r->values[a] += (double)len; break;
         case PG_AGG_COUNTMV: {
@@ -807,7 +844,16 @@ static void aggregate_group_by(const pg_plan *plan, const orc_column *cols, cons
     if (plan->aggs[a].fn == PG_AGG_MAX) for (uint64_t g = 0; g < G; g++) vals[g * A + a] = -INFINITY;
     n_dc += plan->aggs[a].fn == PG_AGG_DISTINCTCOUNT;
   }
-  uint64_t *pairs = n_dc ? (uint64_t *)malloc(sizeof(uint64_t) * (n ? n : 1) * n_dc) : NULL;
+  uint64_t n_pairs = 0;  /* DISTINCTCOUNT: one pair per row, or per value of the row's doc (PG_AGG_MV_VALUES) */
+  for (uint32_t a = 0; a < A; a++) {
+    if (plan->aggs[a].fn != PG_AGG_DISTINCTCOUNT) continue;
+    if (!(plan->aggs[a].flags & PG_AGG_MV_VALUES)) { n_pairs += n; continue; }
+    for (uint64_t i = 0; i < n; i++) {
+      const uint32_t d = docs[row_doc ? row_doc[i] : i];
+      n_pairs += inputs[a].mv.offsets[d + 1] - inputs[a].mv.offsets[d];
+    }
+  }
+  uint64_t *pairs = n_dc ? (uint64_t *)malloc(sizeof(uint64_t) * (n_pairs ? n_pairs : 1)) : NULL;
   uint64_t np = 0;
   /* aggregateGroupBySV: holder[groupId] op= value for each doc (e.g. SumAggregationFunction.java:205-237) */
   for (uint64_t i = 0; i < n; i++) {
@@ -818,6 +864,20 @@ static void aggregate_group_by(const pg_plan *plan, const orc_column *cols, cons
     for (uint32_t a = 0; a < A; a++) {
       const pg_agg *ag = &plan->aggs[a];
       double *v = &vals[(uint64_t)g * A + a];
+      if (ag->flags & PG_AGG_MV_VALUES) {  /* *MVAggregationFunction.aggregateGroupBySV: every value of the doc */
+        const agg_input *in = &inputs[a];
+        if (ag->fn == PG_AGG_DISTINCTCOUNT) {
+          for (uint64_t x = in->mv.offsets[d]; x < in->mv.offsets[d + 1]; x++)
+            pairs[np++] = (((uint64_t)g * A + a) << 32) | (uint32_t)mv_id(in, x);
+        } else if (ag->fn == PG_AGG_AVG) {  /* AvgMV.aggregateOnGroupKey: the doc's values summed, then the pair */
+          double s2 = 0.0;
+          mv_fold(ag, in, d, &s2, &cnts[(uint64_t)g * A + a]);
+          *v += s2;
+        } else {
+          mv_fold(ag, in, d, v, NULL);
+        }
+        continue;
+      }
       switch (ag->fn) {
         case PG_AGG_COUNT: *v += 1.0; break;
         case PG_AGG_COUNTMV: *v += (double)(inputs[a].mv.offsets[d + 1] - inputs[a].mv.offsets[d]); break;
@@ -1004,7 +1064,13 @@ int orc_execute_segment(const pg_plan *plan, uint32_t seg, const orc_column *col
   for (uint32_t a = 0; a < plan->num_aggs; a++) {
     const pg_agg *g = &plan->aggs[a];
     if (g->fn == PG_AGG_COUNT) continue;
-    if (g->fn == PG_AGG_COUNTMV) { mv_open(&cols[g->col_a], &inputs[a].mv); inputs[a].has_mv = 1; used[g->col_a] = 1; continue; }
+    if (g->fn == PG_AGG_COUNTMV || (g->flags & PG_AGG_MV_VALUES)) {
+      mv_open(&cols[g->col_a], &inputs[a].mv);
+      inputs[a].has_mv = 1;
+      inputs[a].mvc = &cols[g->col_a];
+      used[g->col_a] = 1;
+      continue;
+    }
     inputs[a].ids_a = sv_dict_ids_at(&cols[g->col_a], docs, n);
     used[g->col_a] = 1;
     if (g->op != PG_EXPR_COL) { inputs[a].ids_b = sv_dict_ids_at(&cols[g->col_b], docs, n); used[g->col_b] = 1; }

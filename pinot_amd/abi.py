@@ -1,7 +1,7 @@
 """ctypes mirror of include/pinot_gpu.h (the C ABI).  Shared by the GPU binding and the oracle."""
 import ctypes as C
 
-PG_ABI_VERSION = 8
+PG_ABI_VERSION = 9
 
 PG_OK, PG_E_INVALID, PG_E_HIP, PG_E_NOMEM, PG_E_NOTFOUND, PG_E_UNSUPPORTED, PG_E_CANCELLED, PG_E_TIMEOUT, \
     PG_E_STATE = 0, -1, -2, -3, -4, -5, -6, -7, -8
@@ -40,6 +40,7 @@ PG_PLAN_EXACT_LIMIT = 0x10
 PG_STATE_DENSE, PG_STATE_HASH, PG_STATE_TUPLES = 0, 1, 2
 PG_RESULT_GROUPS_LIMIT_REACHED, PG_RESULT_TRIM_THRESHOLD_REACHED = 0x1, 0x2
 PG_SUM_NONFINITE, PG_SUM_BOUNDS = 0x1, 0x2
+PG_AGG_MV_VALUES = 0x1
 PG_EMPTY_KEY = 0xFFFFFFFFFFFFFFFF
 
 
@@ -60,7 +61,7 @@ class pg_leaf(C.Structure):
 class pg_agg(C.Structure):
     _fields_ = [("fn", C.c_uint32), ("op", C.c_uint32), ("col_a", C.c_uint32), ("col_b", C.c_uint32),
                 ("key_kind", C.c_uint32), ("key_cardinality", C.c_uint32), ("key_base", C.c_int64),
-                ("sum_exp", C.c_int32), ("sum_flags", C.c_uint32), ("sum_exp_lo", C.c_int32), ("pad", C.c_uint32)]
+                ("sum_exp", C.c_int32), ("sum_flags", C.c_uint32), ("sum_exp_lo", C.c_int32), ("flags", C.c_uint32)]
 
 
 class pg_key(C.Structure):

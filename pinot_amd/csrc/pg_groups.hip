@@ -211,7 +211,7 @@ __global__ void final_values_kernel(StateView v, FinalSpec f, const uint32_t* __
         case PG_AGG_SUM:
         case PG_AGG_AVG:
           x = A.integer ? (double)(int64_t)v.i64[s * v.n_i64 + A.slot] : fx_value(v, A, s);
-          if (A.fn == PG_AGG_AVG) c = count;
+          if (A.fn == PG_AGG_AVG) c = A.cnt_slot ? (int64_t)v.i64[s * v.n_i64 + A.cnt_slot] : count;
           break;
         case PG_AGG_MIN: x = order_key_decode(v.mn[s * v.n_min + A.slot]); break;
         case PG_AGG_MAX: x = order_key_decode(v.mx[s * v.n_max + A.slot]); break;
@@ -372,7 +372,10 @@ __global__ void order_keys_state_kernel(StateView v, FinalSpec f, const uint32_t
         case PG_AGG_SUM:
         case PG_AGG_AVG:
           x = A.integer ? (double)(int64_t)v.i64[s * v.n_i64 + A.slot] : fx_value(v, A, s);
-          if (A.fn == PG_AGG_AVG) x = count ? x / (double)count : -__builtin_inf();
+          if (A.fn == PG_AGG_AVG) {
+            const int64_t c = A.cnt_slot ? (int64_t)v.i64[s * v.n_i64 + A.cnt_slot] : count;
+            x = c ? x / (double)c : -__builtin_inf();
+          }
           break;
         case PG_AGG_MIN: x = order_key_decode(v.mn[s * v.n_min + A.slot]); break;
         case PG_AGG_MAX: x = order_key_decode(v.mx[s * v.n_max + A.slot]); break;

@@ -192,7 +192,8 @@ struct AggSpec {
   // inputs (the fixed-point sum skips them), so that finalisation gives IEEE's sum of them (fx_final); else kNoSp
   uint32_t sp_min, sp_max;
   uint32_t fx_nwin;   // SK_FX: exponent windows = consecutive fx slots slot .. slot + fx_nwin - 1 (fx_split)
-  uint32_t pad_;
+  uint32_t mv;        // PG_AGG_MV_VALUES: fn over every value of the doc's list in the MV column (AVG: cnt_slot counts
+                      // the values; 0 = the doc count in slot 0)
 };
 constexpr uint32_t kNoSp = 0xFFFFFFFFu;
 
@@ -233,6 +234,7 @@ struct QuerySpec {
   uint32_t n_i64, n_fx, n_min, n_max;  // n_fx: SK_FX slots, 2 words each
   uint32_t dc_row_words;     // uint32 words of DISTINCTCOUNT bitmaps per slot
   uint32_t mv_key;           // the multi-value group key (each value of a doc's list is a group of the doc) or kNoMvKey
+  uint32_t mv_aggs;          // bit a: aggregation a reads every value of an MV column (AggSpec.mv)
   unsigned long long* i64;
   unsigned long long* fx;    // [num_slots][n_fx][2] (lo, hi)
   long long* mn;

@@ -1206,6 +1206,10 @@ int agg_layout(const pg_plan* plan, uint32_t integer, const std::vector<int32_t>
     s2.sp_min = s2.sp_max = kNoSp;
     if (g.fn > PG_AGG_COUNTMV) return fail(PG_E_INVALID, "unknown aggregation %u", g.fn);
     if (g.op > PG_EXPR_SUB) return fail(PG_E_INVALID, "unknown expression op %u", g.op);
+    if (g.flags & ~PG_AGG_MV_VALUES) return fail(PG_E_INVALID, "aggregation %u: unknown flags 0x%x", a, g.flags);
+    s2.mv = (g.flags & PG_AGG_MV_VALUES) ? 1u : 0u;
+    if (s2.mv && (g.fn == PG_AGG_COUNT || g.fn == PG_AGG_COUNTMV || g.op != PG_EXPR_COL))
+      return fail(PG_E_INVALID, "aggregation %u: PG_AGG_MV_VALUES needs SUM / MIN / MAX / AVG / DISTINCTCOUNT of a column", a);
     switch (g.fn) {
       case PG_AGG_COUNT: s2.kind = SK_NONE; s2.slot = 0; break;
       case PG_AGG_COUNTMV: s2.kind = SK_I64; s2.slot = n_i64++; break;
@@ -1222,7 +1226,7 @@ int agg_layout(const pg_plan* plan, uint32_t integer, const std::vector<int32_t>
           n_fx += s2.fx_nwin;
           if ((special >> a) & 1u) { s2.sp_min = n_min++; s2.sp_max = n_max++; }
         }
-        s2.cnt_slot = 0;
+        s2.cnt_slot = (g.fn == PG_AGG_AVG && s2.mv) ? n_i64++ : 0;  // AVGMV counts values, not docs
         break;
       case PG_AGG_MIN: s2.kind = SK_MIN; s2.slot = n_min++; break;
       case PG_AGG_MAX: s2.kind = SK_MAX; s2.slot = n_max++; break;
@@ -1421,6 +1425,7 @@ bool filter_is_match_all(const pg_plan* plan, const pg_leaf* leaves) {
 
 // Aggregation inputs that only need dictionary VALUES (not dictIds) may read a column's decoded forward index.
 bool agg_decodes(const pg_agg& g) {
+  if (g.flags & PG_AGG_MV_VALUES) return false;  // MV values: dictIds through the row offsets + dictionary
   return g.fn == PG_AGG_SUM || g.fn == PG_AGG_MIN || g.fn == PG_AGG_MAX || g.fn == PG_AGG_AVG ||
          (g.fn == PG_AGG_DISTINCTCOUNT && g.key_kind == PG_KEY_VALUE_OFFSET);
 }
@@ -1761,6 +1766,9 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     const bool two = (g.fn == PG_AGG_SUM || g.fn == PG_AGG_MIN || g.fn == PG_AGG_MAX || g.fn == PG_AGG_AVG) && g.op != PG_EXPR_COL;
     if (two) projected.insert(g.col_b & ~PG_COL_DERIVED);
     SumBounds sb;
+    const bool mv = (g.flags & PG_AGG_MV_VALUES) != 0;
+    uint64_t mv_vals = 0;  // MV values: the inputs the integer-exactness bound counts (not the docs)
+    if (mv) q.mv_aggs |= 1u << a;
     for (uint32_t si = 0; si < S; si++) {
       const ColumnRes* ca = col(si, g.col_a);
       if (!ca) return fail(PG_E_NOTFOUND, "aggregation %u: column %u not resident in segment %u", a, g.col_a, si);
@@ -1769,7 +1777,12 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         continue;
       }
       const bool raw_a = ca->fwd == FWD_RAW;
-      if (ca->fwd == FWD_NONE || ca->fwd == FWD_MV || (!ca->has_dict && !raw_a))
+      if (mv != (ca->fwd == FWD_MV))
+        return fail(PG_E_UNSUPPORTED, "aggregation %u: column %u is %s-value", a, g.col_a, mv ? "single" : "multi");
+      if (mv && (!ca->mv_offsets.p || !ca->has_dict))
+        return fail(PG_E_UNSUPPORTED, "aggregation %u: MV column %u needs its row offsets + dictionary", a, g.col_a);
+      mv_vals += ca->num_values;
+      if (ca->fwd == FWD_NONE || (!ca->has_dict && !raw_a))
         return fail(PG_E_UNSUPPORTED, "aggregation %u: column %u needs an SV forward index + dictionary", a, g.col_a);
       if (raw_a && g.fn == PG_AGG_DISTINCTCOUNT && g.key_kind != PG_KEY_VALUE_OFFSET)
         return fail(PG_E_UNSUPPORTED, "DISTINCTCOUNT of raw column %u needs value-offset ids", g.col_a);
@@ -1791,7 +1804,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       sum_bounds_add(sb, ca, cb);
     }
     if (g.fn == PG_AGG_SUM || g.fn == PG_AGG_AVG) {
-      const bool as_int = t_layout.on ? ((t_layout.integer >> a) & 1u) != 0 : sum_as_int(sb, g, two, plan->flags, total_docs);
+      const bool as_int = t_layout.on ? ((t_layout.integer >> a) & 1u) != 0
+                                      : sum_as_int(sb, g, two, plan->flags, mv ? mv_vals : total_docs);
       if (as_int) {
         integer |= 1u << a;
       } else {
@@ -1874,7 +1888,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     const int pe = part_env ? atoi(part_env) : -1;
     uint32_t dc = (uint32_t)kNoSlot, ndc = 0;
     bool ok = P.mode == GM_DENSE && !q.use_lds && K > 0 && P.n_i64 == 1 && !P.n_fx && !P.n_min && !P.n_max &&
-              total_docs > 0 && total_docs < 0xFFFFFFF0ull && pe != 0 && q.mv_key == kNoMvKey;
+              total_docs > 0 && total_docs < 0xFFFFFFF0ull && pe != 0 && q.mv_key == kNoMvKey && !q.mv_aggs;
     for (uint32_t a = 0; a < A && ok; a++) {
       if (P.aggs[a].fn == PG_AGG_DISTINCTCOUNT) { dc = a; ndc++; }
       else if (P.aggs[a].fn != PG_AGG_COUNT) ok = false;
@@ -2573,7 +2587,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     auto key_dec = [&](uint32_t k) { return key_dec_v[k]; };
     for (uint32_t a = 0; a < A; a++) {
       const pg_agg& g = plan->aggs[a];
-      if (g.fn == PG_AGG_COUNT || g.fn == PG_AGG_COUNTMV) continue;
+      if (g.fn == PG_AGG_COUNT || g.fn == PG_AGG_COUNTMV || (g.flags & PG_AGG_MV_VALUES)) continue;
       const int n = (g.op != PG_EXPR_COL && g.fn != PG_AGG_DISTINCTCOUNT) ? 2 : 1;
       for (int k = 0; k < n; k++) {
         const uint32_t cid = k ? g.col_b : g.col_a;
@@ -2636,7 +2650,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
         const bool dec = (c.key >> 32) == 3;
         for (uint32_t a = 0; a < A; a++) {
           const pg_agg& g = plan->aggs[a];
-          if (g.fn == PG_AGG_COUNT || g.fn == PG_AGG_COUNTMV) continue;
+          if (g.fn == PG_AGG_COUNT || g.fn == PG_AGG_COUNTMV || (g.flags & PG_AGG_MV_VALUES)) continue;
           if (g.col_a == cid && agg_dec(a, 0) == dec) q.agg_slot[a][0] = (uint8_t)slot;
           if (g.op != PG_EXPR_COL && g.fn != PG_AGG_DISTINCTCOUNT && g.col_b == cid && agg_dec(a, 1) == dec)
             q.agg_slot[a][1] = (uint8_t)slot;
@@ -4139,7 +4153,7 @@ int finalize_small(pg_partials* pp, const pg_plan* plan, pg_result** out, const 
             x = fx_final(g, w, g.sp_min != kNoSp ? mn[sl * v.n_min + g.sp_min] : 0,
                          g.sp_max != kNoSp ? mx[sl * v.n_max + g.sp_max] : 0);
           }
-          if (g.fn == PG_AGG_AVG) c = count;
+          if (g.fn == PG_AGG_AVG) c = g.cnt_slot ? (int64_t)i64[sl * v.n_i64 + g.cnt_slot] : count;
           break;
         case PG_AGG_MIN: x = order_key_decode(mn[sl * v.n_min + g.slot]); break;
         case PG_AGG_MAX: x = order_key_decode(mx[sl * v.n_max + g.slot]); break;
@@ -4845,6 +4859,7 @@ int global_layout(const pg_plan* plan, std::vector<pg_agg>& aggs, LayoutHint& hi
     if (g.fn != PG_AGG_SUM && g.fn != PG_AGG_AVG) continue;
     const bool two = g.op != PG_EXPR_COL;
     SumBounds sb;
+    uint64_t mv_vals = 0;
     for (uint32_t si = 0; si < plan->num_segments; si++) {
       auto it = g_segs.find(plan->segments[si].seg_key);
       if (it == g_segs.end()) return fail(PG_E_NOTFOUND, "segment %llu not resident", (unsigned long long)plan->segments[si].seg_key);
@@ -4854,8 +4869,9 @@ int global_layout(const pg_plan* plan, std::vector<pg_agg>& aggs, LayoutHint& hi
         continue;  // the device's own compile reports the missing column
       if (ca->second.dtype > PG_DOUBLE || (two && cb->second.dtype > PG_DOUBLE)) continue;
       sum_bounds_add(sb, &ca->second, two ? &cb->second : nullptr);
+      mv_vals += ca->second.num_values;
     }
-    if (sum_as_int(sb, g, two, plan->flags, hint.docs)) {
+    if (sum_as_int(sb, g, two, plan->flags, (g.flags & PG_AGG_MV_VALUES) ? mv_vals : hint.docs)) {
       hint.integer |= 1u << a;
       continue;
     }

@@ -166,7 +166,7 @@ __device__ __forceinline__ uint64_t key_of(uint32_t kind, int64_t base, const Co
 }
 
 __device__ __forceinline__ uint32_t agg_ncols(const AggSpec& A) {
-  if (A.fn == PG_AGG_COUNT || A.fn == PG_AGG_COUNTMV) return 0;
+  if (A.fn == PG_AGG_COUNT || A.fn == PG_AGG_COUNTMV || A.mv) return 0;  // (MV values: read through the row offsets)
   if (A.fn == PG_AGG_DISTINCTCOUNT) return 1;
   return A.op == PG_EXPR_COL ? 1u : 2u;
 }
@@ -613,9 +613,53 @@ __device__ __forceinline__ void fx_update(const QuerySpec& q, const GroupState& 
     s_max(S, &S.mx[g * q.n_max + A.sp_max], k);
   }
 }
+// SUMMV / MINMV / MAXMV / AVGMV / DISTINCTCOUNTMV (PG_AGG_MV_VALUES): every value of doc d's list in the aggregation's
+// multi-value column, in stored order (*MVAggregationFunction: `for (value : valuesArray[i])`); AVGMV also counts the
+// values into its count slot.  noinline: one copy per kernel, not one per unrolled aggregation slot of every shape.
+__device__ __attribute__((noinline)) uint64_t mv_update(const QuerySpec* qp, GroupState S, const AggSpec* Ap,
+                                                        const ColDesc* c, uint64_t g, uint32_t d, uint64_t acc,
+                                                        bool grouped) {
+  const QuerySpec& q = *qp;
+  const AggSpec& A = *Ap;
+  const ColDesc c0 = ldc(c, 0);
+  const PG_GLOBAL uint32_t* off = glb(c0.mv_offsets);
+  const uint32_t v0 = off[d], v1 = off[d + 1];
+  const rsrc_t rs = make_rsrc(c0.words, c0.wbytes);
+  for (uint32_t v = v0; v < v1; v++) {
+    const uint32_t id = unpack(rs, v, c0.bits);
+    switch (A.fn) {
+      case PG_AGG_SUM:
+      case PG_AGG_AVG:
+        if (!A.integer) fx_update(q, S, A, grouped ? g : 0ull, value_f64(A, c, id, 0));
+        else if (grouped) s_add(S, &S.i64[g * q.n_i64 + A.slot], (unsigned long long)value_i64(A, c, id, 0));
+        else acc += (uint64_t)value_i64(A, c, id, 0);
+        break;
+      case PG_AGG_MIN:
+      case PG_AGG_MAX: {
+        const int64_t k = order_key(value_f64(A, c, id, 0));
+        if (grouped && A.fn == PG_AGG_MIN) s_min(S, &S.mn[g * q.n_min + A.slot], (long long)k);
+        else if (grouped) s_max(S, &S.mx[g * q.n_max + A.slot], (long long)k);
+        else if (A.fn == PG_AGG_MIN ? k < (int64_t)acc : k > (int64_t)acc) acc = (uint64_t)k;
+        break;
+      }
+      default: {  // DISTINCTCOUNT
+        const uint64_t key = key_of(A.key_kind, A.key_base, c0, id);
+        if (key < A.key_card) g_or(&q.dbits[(grouped ? g * q.dc_row_words : 0ull) + A.dc_word + (key >> 5)], 1u << (key & 31u));
+        else atomicOr(q.err, 2u);
+      }
+    }
+  }
+  if (A.fn == PG_AGG_AVG) s_add(S, &S.i64[(grouped ? g * q.n_i64 : 0ull) + A.cnt_slot], (unsigned long long)(v1 - v0));
+  return acc;
+}
+
 // Per-doc update of one aggregation in group slot g (aggregateGroupBySV of each function).
 __device__ __forceinline__ void group_update(const QuerySpec& q, const GroupState& S, const AggSpec& A,
                                              const ColDesc* c, uint64_t g, uint32_t d, uint32_t ia, uint32_t ib) {
+  if (A.mv) {  // SUMMV / MINMV / MAXMV / AVGMV / DISTINCTCOUNTMV
+    mv_update(&q, S, &A, c, g, d, 0ull, true);
+    return;
+  }
   switch (A.fn) {
     case PG_AGG_COUNT: break;  // = slot 0
     case PG_AGG_COUNTMV:
@@ -642,6 +686,10 @@ __device__ __forceinline__ void group_update(const QuerySpec& q, const GroupStat
 // aggregation-only shapes registers they do not have.
 __device__ __forceinline__ void acc_update(const QuerySpec& q, const GroupState& S, const AggSpec& A, const ColDesc* c,
                                            uint64_t& acc, uint32_t d, uint32_t ia, uint32_t ib) {
+  if (A.mv) {  // every value of the doc's list; AVGMV's value count into its count slot (the block's table or global)
+    acc = mv_update(&q, S, &A, c, 0ull, d, acc, false);
+    return;
+  }
   switch (A.fn) {
     case PG_AGG_COUNT: break;
     case PG_AGG_COUNTMV: acc += glb(ldc(c, 0).mv_offsets)[d + 1] - glb(ldc(c, 0).mv_offsets)[d]; break;
@@ -676,6 +724,38 @@ __device__ __forceinline__ uint32_t col_id(const QuerySpec& q, uint32_t slot, co
   if (!c.bits) return d;  // raw forward index: the value array is indexed by doc id
   if (slot != kNoSlot) return unpack_lds(stage + q.staged[slot].lds_word_off, rel, c.bits);
   return unpack(make_rsrc(c.words, c.wbytes), d, c.bits);
+}
+
+// GROUP BY a multi-value column: doc d joins the group of each value of its list, in stored order, duplicates
+// included (DictionaryBasedGroupKeyGenerator.generateKeysForBlock(.., int[][]) :188-200), each with the doc's own
+// aggregation inputs (aggregateGroupByMV); g0 = the packed key of the SV keys.  noinline, the aggregations in a
+// runtime loop: one copy per kernel, not one per unrolled aggregation slot of every shape.
+__device__ __attribute__((noinline)) void mv_key_update(const QuerySpec* qp, GroupState S, SegDesc sd, uint32_t d,
+                                                        uint64_t g0) {
+  const QuerySpec& q = *qp;
+  const ColDesc mk = ldc(sd.keycols, q.mv_key);
+  const PG_GLOBAL uint32_t* off = glb(mk.mv_offsets);
+  const uint32_t v0 = off[d], v1 = off[d + 1];
+  const rsrc_t rs = make_rsrc(mk.words, mk.wbytes);
+  for (uint32_t v = v0; v < v1; v++) {
+    const uint64_t kid = key_of(q.key_kind[q.mv_key], q.key_base[q.mv_key], mk, unpack(rs, v, mk.bits));
+    if (kid >= q.key_card[q.mv_key]) {  // never expected: the host proved the key ranges
+      atomicOr(q.err, 1u);
+      continue;
+    }
+    const uint64_t g = group_slot(q, g0 + kid * q.key_stride[q.mv_key], sd.index, d);
+    if (g == ~0ull) continue;
+    s_add(S, &S.i64[g * q.n_i64], 1ull);  // slot 0: (doc, value) count / presence
+#pragma unroll 1
+    for (uint32_t a = 0; a < q.num_aggs; a++) {
+      const AggSpec& A = q.aggs[a];
+      const ColDesc* c = sd.aggcols + 2 * a;
+      const uint32_t nc = agg_ncols(A);
+      const uint32_t ia = nc >= 1 ? col_id(q, kNoSlot, ldc(c, 0), nullptr, d, 0) : 0u;
+      const uint32_t ib = nc >= 2 ? col_id(q, kNoSlot, ldc(c, 1), nullptr, d, 0) : 0u;
+      group_update(q, S, A, c, g, d, ia, ib);
+    }
+  }
 }
 
 // Dense tiles: the aggregation of 8 rows at a time with every dictionary / keymap read of the batch in flight
@@ -891,8 +971,7 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
       if (jj[x] >= 32u) continue;
       if constexpr (GROUPED) {
         if (q.mv_key != kNoMvKey) {
-          // a multi-value key: the doc joins the group of each value in its list, in stored order (duplicates
-          // included), each with the doc's aggregation inputs (aggregateGroupByMV)
+          // a multi-value key: the doc joins the group of each value in its list (mv_key_update)
           uint64_t g0 = 0;
           bool in_range = true;
 #pragma unroll
@@ -903,25 +982,11 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
             in_range &= kid < q.key_card[k];
             g0 += kid * q.key_stride[k];
           }
-          const ColDesc mk = ldc(sd.keycols, q.mv_key);
-          const PG_GLOBAL uint32_t* off = glb(mk.mv_offsets);
-          const uint32_t v0 = off[d[x]], v1 = off[d[x] + 1];
-          const rsrc_t rs = make_rsrc(mk.words, mk.wbytes);
-          for (uint32_t v = v0; v < v1; v++) {
-            const uint64_t kid = key_of(q.key_kind[q.mv_key], q.key_base[q.mv_key], mk, unpack(rs, v, mk.bits));
-            if (!in_range || kid >= q.key_card[q.mv_key]) {  // never expected: the host proved the key ranges
-              atomicOr(q.err, 1u);
-              continue;
-            }
-            const uint64_t g = group_slot(q, g0 + kid * q.key_stride[q.mv_key], sd.index, d[x]);
-            if (g == ~0ull) continue;
-            s_add(S, &S.i64[g * q.n_i64], 1ull);
-#pragma unroll
-            for (int a = 0; a < MAXA; a++) {
-              if (a >= (int)q.num_aggs) break;
-              group_update(q, S, q.aggs[a], sd.aggcols + 2 * a, g, d[x], ia[x][a], ib[x][a]);
-            }
+          if (!in_range) {  // never expected: the host proved the key ranges
+            atomicOr(q.err, 1u);
+            continue;
           }
+          mv_key_update(&q, S, sd, d[x], g0);
           continue;
         }
         uint64_t g = 0;
@@ -1189,7 +1254,7 @@ __device__ __forceinline__ void scan_body() {
         if (!GROUPED) doc_count += nm;
         if (GROUPED || q.agg_reads) {
           // dense when at least a quarter of the lanes hold >= 8 matches: batched rows; else per-doc rounds
-          if (__popcll(__ballot(nm >= 8)) >= 16 && (!GROUPED || q.mv_key == kNoMvKey))
+          if (__popcll(__ballot(nm >= 8)) >= 16 && (!GROUPED || q.mv_key == kNoMvKey) && !q.mv_aggs)
             aggregate_dense<GROUPED, MAXA, MAXK>(q, sd, S, st, acc, m, base, tid);
           else aggregate_tile<GROUPED, MAXA, MAXK>(q, sd, S, st, acc, m, rows);
         }
@@ -1260,7 +1325,9 @@ __device__ __forceinline__ void scan_body() {
         default: break;
       }
     }
-    if (q.use_lds && tid == 0) {  // the one-slot LDS table: SK_FX sums and their special slots
+    if (q.use_lds && tid == 0) {  // the one-slot LDS table: SK_FX sums and their special slots, AVGMV value counts
+      for (uint32_t s = 1; s < q.n_i64; s++)
+        if (l_i64[s]) atomicAdd(&q.i64[s], l_i64[s]);
       for (uint32_t s = 0; s < q.n_fx; s++)
         if (l_fx[2 * s] | l_fx[2 * s + 1]) g_addfx(&q.fx[2 * s], l_fx[2 * s], l_fx[2 * s + 1]);
       for (uint32_t s = 0; s < q.n_min; s++) atomicMin(&q.mn[s], l_mn[s]);

@@ -77,12 +77,12 @@ def column_name(ag: Aggregation) -> str:
     (CountAggregationFunction.java:37,62: COLUMN_NAME = "count_star")."""
     if ag.function == "COUNT":
         return "count_star"
-    return f"{_TYPE_NAME[ag.function]}_{ag.arg}"
+    return f"{_TYPE_NAME[ag.function]}{'MV' if ag.mv else ''}_{ag.arg}"
 
 
 def result_column_name(ag: Aggregation) -> str:
     """AggregationFunction.getResultColumnName(): "<type lower-case>(<expression>)" (group-by tables)."""
-    return f"{_TYPE_NAME[ag.function].lower()}({ag.arg})"
+    return f"{(_TYPE_NAME[ag.function] + ('MV' if ag.mv else '')).lower()}({ag.arg})"
 
 
 @dataclass

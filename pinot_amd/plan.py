@@ -783,7 +783,7 @@ def filtered_aggregation_passes(query: QueryContext) -> List[Tuple[QueryContext,
         combined = f if query.filter is None else FilterContext(
             "AND", (query.filter.children if query.filter.type == "AND" else [query.filter]) +
             (f.children if f.type == "AND" else [f]))
-        out.append((_pass_query(query, combined, [Aggregation(aggs[i].function, aggs[i].arg) for i in idx]), idx))
+        out.append((_pass_query(query, combined, [Aggregation(aggs[i].function, aggs[i].arg, mv=aggs[i].mv) for i in idx]), idx))
     out.append((_pass_query(query, query.filter, [aggs[i] for i in plain] or [Aggregation("COUNT", Expr("STAR"))]),
                 plain))
     return out
@@ -1088,9 +1088,13 @@ class CPlan:
                     # the SV functions read getXxxValuesSV / getDictionaryIdsSV and COUNTMV getNumMVEntries: a
                     # function over the other kind of column fails in the reference too (SUMMV, DISTINCTCOUNTMV, ...
                     # are other functions)
-                    if table.multi_value(c) != (ag.function == "COUNTMV"):
-                        raise UnsupportedQuery(f"{ag.function} over {'multi' if table.multi_value(c) else 'single'}"
+                    if table.multi_value(c) != (ag.function == "COUNTMV" or ag.mv):
+                        raise UnsupportedQuery(f"{ag.name} over {'multi' if table.multi_value(c) else 'single'}"
                                                f"-value column {c}")
+                if ag.mv:
+                    if e.op != "COL":
+                        raise UnsupportedQuery(f"{ag.name} over an expression")
+                    aggs[i].flags = abi.PG_AGG_MV_VALUES
                 if ag.function == "DISTINCTCOUNT":
                     ks = table.value_space(e.cols[0])
                     if derived_ids and ks.derived is not None:

@@ -69,9 +69,17 @@ class Aggregation:
     # `AGG(x) FILTER (WHERE f)`: the aggregation's own filter, ANDed with the query's (QueryContext's
     # filteredAggregationFunctions, QueryContext.java:512-560); part of equality, not of the hash
     filter: Optional[FilterContext] = field(default=None, hash=False)
+    # SUMMV / MINMV / MAXMV / AVGMV / DISTINCTCOUNTMV: `function` over every value of a multi-value column (the same
+    # intermediate and final types as the single-value function: SumMVAggregationFunction extends SumAggregationFunction)
+    mv: bool = False
+
+    @property
+    def name(self) -> str:
+        """The function's SQL name (SUMMV for SUM over MV values)."""
+        return self.function + ("MV" if self.mv else "")
 
     def result_name(self):
-        base = f"{self.function.lower()}({self.arg})"
+        base = f"{self.name.lower()}({self.arg})"
         return base if self.filter is None else f"{base} FILTER(WHERE {filter_str(self.filter)})"
 
 
@@ -168,7 +176,8 @@ _TOKEN = re.compile(r"\s*(?:(?P<num>-?\d+(?:\.\d+)?(?:[eE][-+]?\d+)?)|(?P<str>'(
                     r"(?P<id>[A-Za-z_][A-Za-z0-9_.$]*)|(?P<op><>|!=|<=|>=|[=<>*+\-/(),]))")
 _KEYWORDS = {"SELECT", "FROM", "WHERE", "GROUP", "BY", "ORDER", "LIMIT", "AND", "OR", "NOT", "IN", "BETWEEN",
              "ASC", "DESC", "AS", "OPTION", "IS", "NULL", "HAVING"}
-_AGGS = {"COUNT", "SUM", "MIN", "MAX", "AVG", "DISTINCTCOUNT", "COUNTMV"}
+_AGGS = {"COUNT", "SUM", "MIN", "MAX", "AVG", "DISTINCTCOUNT", "COUNTMV",
+         "SUMMV", "MINMV", "MAXMV", "AVGMV", "DISTINCTCOUNTMV"}
 
 
 def _tokenize(sql: str):
@@ -250,7 +259,8 @@ class _Parser:
                 self.expect("kw", "WHERE")
                 filt = self.or_expr()
                 self.expect("op", ")")
-            return "AGG", Aggregation(fn, e, filt)
+            mv = fn.endswith("MV") and fn != "COUNTMV"
+            return "AGG", Aggregation(fn[:-2] if mv else fn, e, filt, mv)
         return "COL", self.expect("id")
 
     def literal(self) -> str:

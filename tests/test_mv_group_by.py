@@ -21,10 +21,11 @@ def _segments(n_segs=3, seed=11):
         tags = [list(rng.integers(0, 25 + 3 * s, rng.integers(1, 6))) for _ in range(n)]
         tags[0] = [4, 4, 4]  # duplicates in one doc's list: three rows of group 4
         words = [[f"w{x}" for x in rng.integers(0, 9, rng.integers(1, 4))] for _ in range(n)]
+        fm = [list(np.round(rng.normal(size=rng.integers(1, 4)) * 10, 3)) for _ in range(n)]
         data = {"tags": tags, "words": words, "k": rng.integers(0, 5, n), "v": rng.integers(-500, 500, n),
-                "d": np.round(rng.normal(size=n) * 100, 2)}
+                "d": np.round(rng.normal(size=n) * 100, 2), "fm": fm}
         segs.append(ImmutableSegment.create(f"mv{s}", data, {"tags": "INT", "words": "STRING", "k": "INT", "v": "INT",
-                                                            "d": "DOUBLE"}))
+                                                            "d": "DOUBLE", "fm": "DOUBLE"}))
     return segs
 
 
@@ -40,6 +41,15 @@ QUERIES = [
     "SELECT words, COUNT(*), SUM(v) FROM t WHERE d < 50 AND k <> 2 GROUP BY words",
     "SELECT tags, COUNTMV(tags), COUNT(*) FROM t WHERE words = 'w3' GROUP BY tags",
     "SELECT tags, SUM(v) FROM t GROUP BY tags ORDER BY SUM(v) DESC, tags LIMIT 5",
+    # SUMMV / MINMV / MAXMV / AVGMV / DISTINCTCOUNTMV (*MVAggregationFunction: every value of the doc's list; AVGMV
+    # counts values), aggregation-only, grouped, over the MV key's own column, ordered by an MV aggregation
+    "SELECT SUMMV(tags), MINMV(tags), MAXMV(tags), AVGMV(tags), DISTINCTCOUNTMV(tags), COUNTMV(tags), COUNT(*) FROM t "
+    "WHERE k < 3",
+    "SELECT k, SUMMV(tags), AVGMV(fm), MAXMV(fm), MINMV(tags), SUMMV(fm) FROM t GROUP BY k",
+    "SELECT tags, SUMMV(tags), AVGMV(tags), COUNT(*) FROM t WHERE v > 0 GROUP BY tags",
+    "SELECT k, DISTINCTCOUNTMV(words), DISTINCTCOUNTMV(tags) FROM t WHERE d > -50 GROUP BY k",
+    "SELECT MINMV(fm), MAXMV(tags), DISTINCTCOUNTMV(tags), AVGMV(fm) FROM t",
+    "SELECT k, AVGMV(tags) FROM t GROUP BY k ORDER BY AVGMV(tags) DESC LIMIT 3",
 ]
 
 
@@ -72,6 +82,8 @@ def _expected(table, sql):
                         r[a].append(1)
                     elif ag.function == "COUNTMV":
                         r[a].append(len(val(ag.arg.cols[0], i)))
+                    elif ag.mv:  # SUMMV / MINMV / MAXMV / AVGMV / DISTINCTCOUNTMV: every value of the doc's list
+                        r[a].extend(val(ag.arg.cols[0], i))
                     else:
                         r[a].append(val(ag.arg.cols[0], i))
     out = {}
@@ -81,7 +93,7 @@ def _expected(table, sql):
             f = ag.function
             row.append(len(xs) if f == "COUNT" else sum(xs) if f in ("COUNTMV",) else float(np.sum(xs)) if f == "SUM"
                        else float(min(xs)) if f == "MIN" else float(max(xs)) if f == "MAX"
-                       else (float(np.sum(xs)), len(xs)) if f == "AVG" else {y.item() for y in xs})
+                       else (float(np.sum(xs)), len(xs)) if f == "AVG" else {getattr(y, "item", lambda: y)() for y in xs})
         out[key] = row
     return out
 
@@ -145,7 +157,17 @@ def test_plan_keys_carry_the_key_spaces(mv_table):
             (ks.kind, ks.cardinality, ks.base) and ks.cardinality > 0
 
 
+def test_mv_function_names():
+    """SumMV's names: getColumnName "sumMV_tags", getResultColumnName "summv(tags)" (the type name lower-cased)."""
+    from pinot_amd import datatable as dtm
+    ag = parse("SELECT SUMMV(tags), DISTINCTCOUNTMV(words) FROM t").aggregations
+    assert (ag[0].function, ag[0].mv, ag[0].name) == ("SUM", True, "SUMMV")
+    assert dtm.column_name(ag[0]) == "sumMV_tags" and dtm.result_column_name(ag[0]) == "summv(tags)"
+    assert dtm.column_name(ag[1]) == "distinctCountMV_words" and ag[0] != parse("SELECT SUM(tags) FROM t").aggregations[0]
+
+
 @pytest.mark.parametrize("sql", [
+    "SELECT k, SUMMV(v) FROM t GROUP BY k",                        # an MV function over an SV column
     "SELECT tags, words, COUNT(*) FROM t GROUP BY tags, words",   # two MV keys: a cartesian product per doc
     "SELECT k, SUM(tags) FROM t GROUP BY k",                       # an SV function over an MV column
     "SELECT COUNTMV(v) FROM t",                                     # COUNTMV over an SV column
