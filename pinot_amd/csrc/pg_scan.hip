@@ -656,10 +656,6 @@ __device__ __attribute__((noinline)) uint64_t mv_update(const QuerySpec* qp, Gro
 // Per-doc update of one aggregation in group slot g (aggregateGroupBySV of each function).
 __device__ __forceinline__ void group_update(const QuerySpec& q, const GroupState& S, const AggSpec& A,
                                              const ColDesc* c, uint64_t g, uint32_t d, uint32_t ia, uint32_t ib) {
-  if (A.mv) {  // SUMMV / MINMV / MAXMV / AVGMV / DISTINCTCOUNTMV
-    mv_update(&q, S, &A, c, g, d, 0ull, true);
-    return;
-  }
   switch (A.fn) {
     case PG_AGG_COUNT: break;  // = slot 0
     case PG_AGG_COUNTMV:
@@ -686,10 +682,6 @@ __device__ __forceinline__ void group_update(const QuerySpec& q, const GroupStat
 // aggregation-only shapes registers they do not have.
 __device__ __forceinline__ void acc_update(const QuerySpec& q, const GroupState& S, const AggSpec& A, const ColDesc* c,
                                            uint64_t& acc, uint32_t d, uint32_t ia, uint32_t ib) {
-  if (A.mv) {  // every value of the doc's list; AVGMV's value count into its count slot (the block's table or global)
-    acc = mv_update(&q, S, &A, c, 0ull, d, acc, false);
-    return;
-  }
   switch (A.fn) {
     case PG_AGG_COUNT: break;
     case PG_AGG_COUNTMV: acc += glb(ldc(c, 0).mv_offsets)[d + 1] - glb(ldc(c, 0).mv_offsets)[d]; break;
@@ -753,7 +745,8 @@ __device__ __attribute__((noinline)) void mv_key_update(const QuerySpec* qp, Gro
       const uint32_t nc = agg_ncols(A);
       const uint32_t ia = nc >= 1 ? col_id(q, kNoSlot, ldc(c, 0), nullptr, d, 0) : 0u;
       const uint32_t ib = nc >= 2 ? col_id(q, kNoSlot, ldc(c, 1), nullptr, d, 0) : 0u;
-      group_update(q, S, A, c, g, d, ia, ib);
+      if (A.mv) mv_update(&q, S, &A, c, g, d, 0ull, true);
+      else group_update(q, S, A, c, g, d, ia, ib);
     }
   }
 }
@@ -969,7 +962,7 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
         }
       }
       if (jj[x] >= 32u) continue;
-      if constexpr (GROUPED) {
+      if constexpr (GROUPED && MAXA == kMaxAggs) {  // (the multi-value paths live in the widest shapes only)
         if (q.mv_key != kNoMvKey) {
           // a multi-value key: the doc joins the group of each value in its list (mv_key_update)
           uint64_t g0 = 0;
@@ -989,6 +982,8 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
           mv_key_update(&q, S, sd, d[x], g0);
           continue;
         }
+      }
+      if constexpr (GROUPED) {
         uint64_t g = 0;
         bool in_range = true;
 #pragma unroll
@@ -1008,13 +1003,15 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
 #pragma unroll
         for (int a = 0; a < MAXA; a++) {
           if (a >= (int)q.num_aggs) break;
-          group_update(q, S, q.aggs[a], sd.aggcols + 2 * a, g, d[x], ia[x][a], ib[x][a]);
+          if (MAXA == kMaxAggs && q.aggs[a].mv) mv_update(&q, S, &q.aggs[a], sd.aggcols + 2 * a, g, d[x], 0ull, true);
+          else group_update(q, S, q.aggs[a], sd.aggcols + 2 * a, g, d[x], ia[x][a], ib[x][a]);
         }
       } else {
 #pragma unroll
         for (int a = 0; a < MAXA; a++) {
           if (a >= (int)q.num_aggs) break;
-          acc_update(q, S, q.aggs[a], sd.aggcols + 2 * a, acc[a], d[x], ia[x][a], ib[x][a]);
+          if (MAXA == kMaxAggs && q.aggs[a].mv) acc[a] = mv_update(&q, S, &q.aggs[a], sd.aggcols + 2 * a, 0ull, d[x], acc[a], false);
+          else acc_update(q, S, q.aggs[a], sd.aggcols + 2 * a, acc[a], d[x], ia[x][a], ib[x][a]);
         }
       }
     }
@@ -1434,7 +1431,8 @@ uint32_t scan_min_blocks_per_cu(bool grouped) {  // 256-thread blocks: waves/SIM
 
 hipError_t launch_scan(const QuerySpec& q, uint32_t blocks, hipStream_t s, bool co) {
   const size_t lds = scan_lds_bytes(q);
-  const uint32_t na = q.num_aggs;
+  // multi-value keys / aggregations: the widest shapes, the only ones compiled with those paths
+  const uint32_t na = (q.mv_key != kNoMvKey || q.mv_aggs) ? (uint32_t)kMaxAggs : q.num_aggs;
   if (q.num_keys == 0) {
     if (na <= 2) launch_one<false, 2, 0>(q, blocks, lds, s, co);
     else if (na <= 4) launch_one<false, 4, 0>(q, blocks, lds, s, co);
