@@ -83,6 +83,18 @@ class _SegmentColumns:
         self.keep = []
         for name, col in seg.columns.items():
             c = self.arr[table.column_ids[name]]
+            if col.dictionary is None and col.data_type in ("STRING", "BYTES"):
+                # raw var-byte column: the oracle keys it by each doc's value id (equal values, equal ids -- the
+                # generators' first-seen order over values is the same over ids); decoded back from raw_values
+                _, ids = np.unique(np.asarray(col.raw_values, dtype=str), return_inverse=True)
+                d = np.frombuffer(ids.astype(">i4").tobytes() or b"\0", dtype=np.uint8)
+                self.keep.append(d)
+                c.dict = d.ctypes.data
+                c.fwd_kind = ORC_FWD_RAW
+                c.data_type = abi.PG_INT
+                c.num_docs = c.cardinality = c.num_values = col.num_docs
+                c.entry_bytes = 4
+                continue
             if col.dictionary is None:  # raw forward index: the decoded values stand in for the dictionary
                 d = np.frombuffer(col.raw_values.astype(_NP_BE[col.data_type]).tobytes() or b"\0", dtype=np.uint8)
             else:

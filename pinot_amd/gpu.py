@@ -117,6 +117,8 @@ class GpuEngine:
             check(self.lib.pg_segment_place(key, ldev))
         for name, col in seg.columns.items():
             cid = table.column_ids[name]
+            if col.dictionary is None and col.data_type in ("STRING", "BYTES"):
+                continue  # raw STRING / BYTES: resident only as its derived key encoding (upload_keymaps)
             d = fwd_desc(col)
             if col.dictionary is not None:  # raw columns: the chunked forward index alone
                 dd = abi.pg_col_desc.from_buffer_copy(d)

@@ -402,6 +402,25 @@ class KeySpace:
     def build(column: str, cols: List[Column], derive: bool = False) -> "KeySpace":
         """derive: a raw INT / LONG column takes the derived encoding even when its range fits value offsets."""
         dt = cols[0].data_type
+        if any(c.dictionary is None for c in cols) and dt in ("STRING", "BYTES"):
+            # raw STRING / BYTES (var-byte chunks): every raw segment's values dictionary-encoded on the host (sorted
+            # distinct values + per-doc ids), keymapped to the table's sorted union; the derived dictionary holds the
+            # values' ranks in that union (the device only needs the keymap), ids = value order (Python str order:
+            # code points -- Java's String.compareTo orders UTF-16 code units, which differs only beyond U+FFFF; BYTES
+            # as lowercase hex: the unsigned byte order ByteArray.compare uses)
+            segu, locs = [], []
+            for c in cols:
+                if c.dictionary is None:
+                    u, local = np.unique(np.asarray(c.raw_values, dtype=str), return_inverse=True)
+                    segu.append(u)
+                    locs.append(local.astype(np.int32))
+                else:
+                    segu.append(np.asarray(c.dictionary.values, dtype=str))
+                    locs.append(None)
+            allu = np.unique(np.concatenate(segu)) if segu else np.zeros(0, dtype=str)
+            keymaps = [np.searchsorted(allu, u).astype(np.int32) for u in segu]
+            derived = [None if loc is None else (km.astype(np.int64), loc) for km, loc in zip(keymaps, locs)]
+            return KeySpace(column, abi.PG_KEY_KEYMAP, len(allu), 0, allu.tolist(), keymaps, derived=derived)
         if any(c.dictionary is None for c in cols):
             if dt not in ("INT", "LONG", "FLOAT", "DOUBLE"):
                 raise UnsupportedQuery(f"{column}: raw {dt} column as a key / DISTINCTCOUNT value")
@@ -1198,6 +1217,10 @@ class CPlan:
         for p in preds:
             if p.column not in cid or any(p.column not in seg.columns for seg in segments):
                 raise UnsupportedQuery(f"unknown column {p.column}")
+            if any(seg.columns[p.column].dictionary is None and seg.columns[p.column].data_type in ("STRING", "BYTES")
+                   for seg in segments):
+                # (the device holds no form of a raw STRING / BYTES column but its derived key encoding)
+                raise UnsupportedQuery(f"filter on raw (no-dictionary) {table.data_type(p.column)} column {p.column}")
         for li, p in enumerate(preds):
             b = batch.get(li)
             vec = lower_leaf_vectorized(table, p, segments, cid[p.column], b) if S > 1 else None

@@ -472,6 +472,63 @@ def raw_forward_values(buf: bytes, data_type: str, num_docs: Optional[int] = Non
     return np.frombuffer(data, dtype=be, count=n).astype(_NP_NATIVE[data_type])
 
 
+def _var_bytes(v, data_type: str) -> bytes:
+    """A STRING / BYTES value as the bytes the var-byte writer stores (putString: UTF-8; putBytes: the raw bytes)."""
+    return bytes.fromhex(_hex(v)) if data_type == "BYTES" else str(v).encode("utf-8")
+
+
+def raw_var_forward_bytes(values, data_type: str, version: int = 2, docs_per_chunk: int = RAW_DOCS_PER_CHUNK,
+                          compression: str = "LZ4") -> bytes:
+    """Chunked var-byte raw forward index of a STRING / BYTES column (VarByteChunkSVForwardIndexWriter, versions 2 and 3:
+    io/writer/impl/VarByteChunkSVForwardIndexWriter.java:38-166 over BaseChunkSVForwardIndexWriter's header; 1 000 docs
+    per chunk, SingleValueVarByteRawIndexCreator.java:36).  Each chunk = docsPerChunk int32 row offsets (from the chunk
+    start; 0 for the rows a partial last chunk lacks) + the rows' bytes, compressed on its own; the header's
+    lengthOfLongestEntry is the longest value in bytes."""
+    if version not in (2, 3):
+        raise ValueError("var-byte raw forward index: versions 2 and 3 (v4 is a different writer)")
+    codec = CHUNK_CODECS[compression]
+    raw = [_var_bytes(v, data_type) for v in values]
+    n = len(raw)
+    longest = max((len(b) for b in raw), default=0)
+    num_chunks = (n + docs_per_chunk - 1) // docs_per_chunk
+    off_size = 4 if version <= 2 else 8
+    header_size = 7 * 4 + num_chunks * off_size
+    head = struct.pack(">7i", version, num_chunks, docs_per_chunk, longest, n, codec, 28)
+    chunks = []
+    for c in range(num_chunks):
+        rows = raw[c * docs_per_chunk:(c + 1) * docs_per_chunk]
+        offs = np.zeros(docs_per_chunk, dtype=">i4")
+        pos = 4 * docs_per_chunk
+        for i, b in enumerate(rows):
+            offs[i] = pos
+            pos += len(b)
+        chunks.append(chunk_compress(codec, offs.tobytes() + b"".join(rows)))
+    coffs = header_size + np.concatenate([[0], np.cumsum([len(c) for c in chunks])[:-1]]).astype(np.int64) \
+        if num_chunks else np.zeros(0, dtype=np.int64)
+    return head + coffs.astype(">i4" if off_size == 4 else ">i8").tobytes() + b"".join(chunks)
+
+
+def raw_var_forward_values(buf: bytes, data_type: str, num_docs: Optional[int] = None) -> np.ndarray:
+    """Every value of a var-byte raw forward index (VarByteChunkSVForwardIndexReader.getString / getBytes: row i of a
+    chunk spans [offset[i], offset[i + 1]), the last row of the chunk -- or the last doc -- to the chunk's end).
+    STRING values as str, BYTES as lowercase hex strings (object array)."""
+    h = raw_forward_header(buf)
+    n = num_docs if num_docs is not None else h["total"]
+    dpc = h["docs_per_chunk"]
+    ends = list(h["offsets"][1:]) + [len(buf)]
+    cap = dpc * (4 + h["entry"])
+    out = []
+    for c, (a, e) in enumerate(zip(h["offsets"], ends)):
+        chunk = buf[a:e] if h["compression"] == CHUNK_PASS_THROUGH else chunk_decompress(h["compression"], buf[a:e], cap)
+        rows = min(dpc, n - c * dpc)
+        offs = np.frombuffer(chunk, dtype=">i4", count=dpc)
+        for i in range(rows):
+            end = int(offs[i + 1]) if i + 1 < rows else len(chunk)
+            b = chunk[int(offs[i]):end]
+            out.append(b.hex() if data_type == "BYTES" else b.decode("utf-8"))
+    return np.asarray(out, dtype=object)
+
+
 # ----------------------------------------------------------------------------- columns / segments
 
 # ------------------------------------------------------------------------------------------ range index
@@ -658,7 +715,18 @@ class ImmutableSegment:
         for cname, dtype in schema.items():
             vals = data[cname]
             sv = not (len(vals) > 0 and isinstance(vals[0], (list, tuple, np.ndarray)))
-            if cname in no_dictionary:
+            if cname in no_dictionary and dtype in ("STRING", "BYTES"):
+                if not sv:
+                    raise ValueError(f"raw forward index: {cname} must be a single-value column")
+                # SingleValueVarByteRawIndexCreator: var-byte chunks (STRING as given, BYTES as lowercase hex strings)
+                arr = np.asarray([_hex(v) if dtype == "BYTES" else str(v) for v in vals], dtype=object)
+                n = arr.size
+                col = Column(cname, dtype, True, None, n, 0, False, n, 0,
+                             field_type=(field_types or {}).get(cname, "DIMENSION"), raw_values=arr,
+                             raw_cardinality=len(set(arr.tolist())))
+                comp = (raw_compression or {}).get(cname) or ("PASS_THROUGH" if col.field_type == "METRIC" else "LZ4")
+                col.fwd = raw_var_forward_bytes(arr, dtype, min(max(raw_version, 2), 3), compression=comp)
+            elif cname in no_dictionary:
                 if not sv or dtype not in _NP_NATIVE:
                     raise ValueError(f"raw forward index: {cname} must be a single-value numeric column")
                 arr = np.asarray(vals, dtype=_NP_NATIVE[dtype])
@@ -806,7 +874,8 @@ class ImmutableSegment:
             if props.get(f"column.{cname}.hasDictionary", "true") == "false":
                 # DefaultIndexReaderProvider.java:92-101: a raw chunked forward index
                 fwd = index_bytes(cname, "raw")
-                vals = raw_forward_values(fwd, dtype, num_docs)
+                vals = raw_var_forward_values(fwd, dtype, num_docs) if dtype in ("STRING", "BYTES") else \
+                    raw_forward_values(fwd, dtype, num_docs)
                 cols[cname] = Column(cname, dtype, True, None, num_docs, b, False, num_docs, 0, fwd, None,
                                      props.get(f"column.{cname}.columnType", "METRIC"), raw_values=vals,
                                      raw_cardinality=card, range_index=index_bytes(cname, "range"))
