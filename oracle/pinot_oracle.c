@@ -341,6 +341,17 @@ static void eval_leaf(const pg_leaf *l, const orc_column *cols, uint32_t num_doc
         free(ids);
         return;
       }
+      if (c->fwd_kind == ORC_FWD_RAW) {
+        /* a raw STRING / BYTES column (its `dict` = each doc's value rank among the segment's sorted distinct values,
+         * see oracle.py): the raw-value evaluator (RangePredicateEvaluatorFactory.java:526-580, String.equals /
+         * compareTo) restated as the rank's membership in the leaf's set / range (plan.lower_derived_predicate) */
+        for (uint32_t d = 0; d < num_docs; d++) {
+          if (cand && !cand[d]) { out[d] = 0; continue; }
+          out[d] = (uint8_t)(leaf_in_set(l, (int32_t)be32(c->dict + 4ull * d)) ^ ex);
+          (*entries_scanned)++;
+        }
+        return;
+      }
       for (uint32_t d = 0; d < num_docs; d++) {
         if (cand && !cand[d]) { out[d] = 0; continue; }
         out[d] = (uint8_t)(leaf_in_set(l, (int32_t)read_bits(c->fwd, d, c->bits)) ^ ex);

@@ -169,6 +169,10 @@ class GpuEngine:
         for ag in plan.aggs:
             if ag.function == "DISTINCTCOUNT":
                 spaces.append(table.value_space(ag.arg.cols[0]))
+        for p in plan.leaf_preds:  # filters on raw STRING / BYTES columns scan their derived encoding (col | DERIVED)
+            if any(s.columns[p.column].dictionary is None and s.columns[p.column].data_type in ("STRING", "BYTES")
+                   for s in segments):
+                spaces.append(table.key_space(p.column))
         for ks in spaces:
             if ks.kind != abi.PG_KEY_KEYMAP:
                 continue

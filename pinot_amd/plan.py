@@ -29,7 +29,7 @@ import numpy as np
 from . import abi
 from .query import (UNBOUNDED, Aggregation, Expr, FilterContext, Predicate, QueryContext, SelectItem,
                     filter_str)
-from .segment import Column, ImmutableSegment
+from .segment import Column, Dictionary, ImmutableSegment
 
 MAX_VALUE_OFFSET_KEYS = 1 << 26   # integer key ranges up to this size may use value offsets (no keymap) ...
 VALUE_OFFSET_DENSITY = 4          # ... when the range is at most this many times the largest segment cardinality
@@ -213,6 +213,38 @@ def lower_predicate(pred: Predicate, col: Column, col_id: int, in_ids: Optional[
     else:
         kind = abi.PG_LEAF_SV_SCAN if col.single_value else abi.PG_LEAF_MV_SCAN
     return LoweredLeaf(kind, col_id, excl, lo, hi, ids)
+
+
+def derived_dictionary(col: Column) -> Dictionary:
+    """A raw STRING / BYTES column's derived dictionary: its sorted distinct values (BYTES as lowercase hex), the
+    order KeySpace.build's per-doc ids and the resident derived forward index (GpuEngine._upload_derived) number them
+    in.  Built once per column."""
+    d = getattr(col, "_derived_dict", None)
+    if d is None:
+        d = Dictionary(col.data_type, np.unique(np.asarray(col.raw_values, dtype=str)).tolist())
+        col._derived_dict = d
+    return d
+
+
+def lower_derived_predicate(pred: Predicate, col: Column, col_id: int) -> LoweredLeaf:
+    """A predicate on a raw (no-dictionary) STRING / BYTES column.  The reference evaluates it per doc with a raw-value
+    evaluator (Equals / NotEquals / In / NotIn / RangePredicateEvaluatorFactory.newRawValueBasedEvaluator: String.equals
+    / compareTo, ByteArray equality / ByteArray.compare -- RangePredicateEvaluatorFactory.java:526-580) inside a
+    ScanBasedFilterOperator.  Restated over the segment's derived dictionary (sorted distinct values, derived_dictionary):
+    a doc matches iff its value's rank is in the dictId set / range the dictionary evaluator computes for the same
+    literals.  A raw evaluator is never always-true or always-false (FilterPlanNode only short-cuts those), so the leaf
+    stays a scan of every doc: an empty set is the empty range [0, 0), an all-values set its exclusive form.  String
+    order is Python's code-point order (Java's compareTo orders UTF-16 units: they differ only beyond U+FFFF)."""
+    if pred.type in ("IS_NULL", "IS_NOT_NULL"):
+        return lower_predicate(pred, col, col_id)
+    d = derived_dictionary(col)
+    stand_in = Column(col.name, col.data_type, True, d, col.num_docs, 0, False, col.num_docs)
+    lw = lower_predicate(pred, stand_in, col_id)
+    if lw.kind == abi.PG_LEAF_EMPTY:
+        return LoweredLeaf(abi.PG_LEAF_SV_SCAN, col_id, 0, 0, 0, None)
+    if lw.kind == abi.PG_LEAF_MATCH_ALL:
+        return LoweredLeaf(abi.PG_LEAF_SV_SCAN, col_id, 1, 0, 0, None)
+    return lw
 
 
 def sum_bound(table: "Table", e: Expr) -> Tuple[int, int, bool]:
@@ -1078,6 +1110,7 @@ class CPlan:
         if has_filtered_aggregations(query):
             raise UnsupportedQuery("filtered aggregations run as one plan per filter (execute_filtered)")
         self._keep = []
+        self.derived_ids = derived_ids
         cid = table.column_ids
         ops, preds = filter_program(query.filter)
         self.leaf_preds = preds
@@ -1217,10 +1250,7 @@ class CPlan:
         for p in preds:
             if p.column not in cid or any(p.column not in seg.columns for seg in segments):
                 raise UnsupportedQuery(f"unknown column {p.column}")
-            if any(seg.columns[p.column].dictionary is None and seg.columns[p.column].data_type in ("STRING", "BYTES")
-                   for seg in segments):
-                # (the device holds no form of a raw STRING / BYTES column but its derived key encoding)
-                raise UnsupportedQuery(f"filter on raw (no-dictionary) {table.data_type(p.column)} column {p.column}")
+        derived_bit = abi.PG_COL_DERIVED if getattr(self, "derived_ids", False) else 0
         for li, p in enumerate(preds):
             b = batch.get(li)
             vec = lower_leaf_vectorized(table, p, segments, cid[p.column], b) if S > 1 else None
@@ -1233,8 +1263,12 @@ class CPlan:
                 self._vec[li] = vec
                 continue
             for si, seg in enumerate(segments):
-                lw = lower_predicate(p, seg.columns[p.column], cid[p.column],
-                                     None if b is None else b[0][si, :b[1][si]])
+                c = seg.columns[p.column]
+                if c.dictionary is None and c.data_type in ("STRING", "BYTES"):
+                    # the device holds a raw STRING / BYTES column only as its derived encoding (col | DERIVED)
+                    lw = lower_derived_predicate(p, c, cid[p.column] | derived_bit)
+                else:
+                    lw = lower_predicate(p, c, cid[p.column], None if b is None else b[0][si, :b[1][si]])
                 self._per_seg[(si, li)] = lw
                 r = tab[si, li]
                 r["kind"], r["col_id"], r["exclusive"], r["lo"], r["hi"] = lw.kind, lw.col_id, lw.exclusive, lw.lo, lw.hi

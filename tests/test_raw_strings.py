@@ -3,15 +3,17 @@ versions 2 / 3, io/writer/impl/VarByteChunkSVForwardIndexWriter.java:38-166, 1 0
 SingleValueVarByteRawIndexCreator.java:36 writes it) round-tripped through every chunk codec and both segment stores,
 and such columns as group keys and DISTINCTCOUNT values (NoDictionarySingleColumnGroupKeyGenerator.java:93-129 keys
 STRING / BYTES values through its Object2Int map): the device groups them through a host-built dictionary encoding
-(KeySpace.build, PG_COL_DERIVED); a filter on one is UnsupportedQuery (the CPU plan).  Pinned against a Python
-restatement over the decoded values (first-seen truncation under numGroupsLimit included), the GPU against the oracle.
+(KeySpace.build, PG_COL_DERIVED); filters on one (raw-value Equals / In / Range evaluators, String.equals / compareTo,
+RangePredicateEvaluatorFactory.java:526-580) scan that encoding's per-doc ranks (plan.lower_derived_predicate).  Pinned
+against a Python restatement over the decoded values (first-seen truncation under numGroupsLimit included), the GPU
+against the oracle.
 Byte parity of the format is unpinned (the reference holds no var-byte fixture); the layout is checked field by field."""
 import struct
 
 import numpy as np
 import pytest
 
-from pinot_amd.plan import InstanceConfig, Table, UnsupportedQuery, reduce_to_rows
+from pinot_amd.plan import InstanceConfig, Table, reduce_to_rows
 from pinot_amd.query import parse
 from pinot_amd.segment import (CHUNK_CODECS, ImmutableSegment, chunk_decompress, raw_forward_header,
                                raw_var_forward_bytes, raw_var_forward_values)
@@ -136,9 +138,51 @@ def test_first_seen_truncation_of_raw_string_keys(rs_table, oracle_engine):
     assert {k: v[0] for k, v in res.rows.items()} == want and res.groups_limit_reached
 
 
-def test_filter_on_a_raw_string_column_is_unsupported(rs_table, oracle_engine):
-    with pytest.raises(UnsupportedQuery):
-        oracle_engine.execute(rs_table, parse("SELECT COUNT(*) FROM t WHERE w = 'beta'"))
+FILTERS = [
+    ("w = 'beta'", lambda w, b, u, k, v: w == "beta"),
+    ("w <> 'beta'", lambda w, b, u, k, v: w != "beta"),
+    ("w = 'absent'", lambda w, b, u, k, v: False),
+    ("w <> 'absent'", lambda w, b, u, k, v: True),
+    ("w IN ('alpha', '', 'zeta', 'nope')", lambda w, b, u, k, v: w in ("alpha", "", "zeta")),
+    ("w NOT IN ('alpha', 'kappa')", lambda w, b, u, k, v: w not in ("alpha", "kappa")),
+    ("w BETWEEN 'beta' AND 'iota'", lambda w, b, u, k, v: "beta" <= w <= "iota"),
+    ("w > 'eta' AND v < 100", lambda w, b, u, k, v: w > "eta" and v < 100),
+    ("w >= 'zzz'", lambda w, b, u, k, v: w >= "zzz"),
+    ("u < 'user01000' OR k = 2", lambda w, b, u, k, v: u < "user01000" or k == 2),
+    ("b = '0a5a'", lambda w, b, u, k, v: b == "0a5a"),
+    ("b IN ('0a5a', '205a', '275a') AND NOT w = 'alpha'",
+     lambda w, b, u, k, v: b in ("0a5a", "205a", "275a") and w != "alpha"),
+    ("b > '1f5a'", lambda w, b, u, k, v: b > "1f5a"),
+]
+
+
+def _decoded(table):
+    return {c: np.concatenate([_vals(s, c) for s in table.segments]) for c in ("w", "b", "u", "k", "v")}
+
+
+@pytest.mark.parametrize("where,pred", FILTERS, ids=[f[0] for f in FILTERS])
+def test_oracle_filters_raw_strings_by_value(where, pred, rs_table, oracle_engine):
+    """Scan filters on raw STRING / BYTES columns: the oracle (lowered onto each segment's derived dictionary) equals a
+    per-doc evaluation of the raw values, counts and entries scanned included."""
+    cols = _decoded(rs_table)
+    n = len(cols["v"])
+    m = np.array([bool(pred(*(cols[c][i] for c in ("w", "b", "u", "k", "v")))) for i in range(n)])
+    got = oracle_engine.execute(rs_table, parse(f"SELECT COUNT(*), SUM(v) FROM t WHERE {where}"))
+    assert got.rows[()][0] == int(m.sum()) and got.rows[()][1] == float(cols["v"][m].sum())
+    assert got.stats.num_docs_scanned == int(m.sum())
+    grouped = oracle_engine.execute(rs_table, parse(f"SELECT w, COUNT(*) FROM t WHERE {where} GROUP BY w"))
+    want = {}
+    for i in np.flatnonzero(m):
+        want[(cols["w"][i],)] = want.get((cols["w"][i],), 0) + 1
+    assert {k: r[0] for k, r in grouped.rows.items()} == want
+
+
+def test_raw_string_filter_is_a_scan_of_every_doc(rs_table, oracle_engine):
+    """A raw-value evaluator is never always-false (FilterPlanNode short-cuts only those): a literal no segment holds
+    still scans every doc."""
+    r = oracle_engine.execute(rs_table, parse("SELECT COUNT(*) FROM t WHERE w = 'absent'"))
+    assert r.rows[()][0] == 0
+    assert r.stats.num_entries_scanned_in_filter == sum(s.num_docs for s in rs_table.segments)
 
 
 @pytest.mark.gpu
@@ -151,6 +195,17 @@ def test_raw_strings_on_device(sql, rs_table, gpu_engine, oracle_engine):
         assert reduce_to_rows(q, g) == reduce_to_rows(q, o)
     else:
         assert_same_result(g, o, table=rs_table)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("where,pred", FILTERS, ids=[f[0] for f in FILTERS])
+def test_raw_string_filters_on_device(where, pred, rs_table, gpu_engine, oracle_engine):
+    from helpers import assert_same_result
+    for sql in (f"SELECT COUNT(*), SUM(v), MAX(v) FROM t WHERE {where}",
+                f"SELECT w, k, COUNT(*), MIN(v) FROM t WHERE {where} GROUP BY w, k",
+                f"SELECT k, DISTINCTCOUNT(u) FROM t WHERE {where} GROUP BY k"):
+        q = parse(sql)
+        assert_same_result(gpu_engine.execute(rs_table, q), oracle_engine.execute(rs_table, q), table=rs_table)
 
 
 @pytest.mark.gpu
