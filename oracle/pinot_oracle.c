@@ -1088,18 +1088,12 @@ int orc_execute_segment(const pg_plan *plan, uint32_t seg, const orc_column *col
   }
   int32_t *key_ids[64] = {0}, *raw_rep[64] = {0};
   uint64_t raw_cards[64] = {0};
-  int mvk = -1;  /* the (one) multi-value group key */
+  uint32_t mvk[64], nmv = 0;  /* the multi-value group keys, in key order */
   for (uint32_t k = 0; k < plan->num_keys; k++) {
     const orc_column *kc = &cols[plan->keys[k].col_id];
     used[plan->keys[k].col_id] = 1;
     if (kc->fwd_kind == ORC_FWD_MV) {
-      if (mvk >= 0) {  /* several MV keys (a cartesian product per doc): not restated */
-        for (uint32_t j = 0; j < k; j++) free(key_ids[j]);
-        for (uint32_t a = 0; a < plan->num_aggs; a++) { free(inputs[a].ids_a); free(inputs[a].ids_b); if (inputs[a].has_mv) free(inputs[a].mv.offsets); }
-        free(inputs); free(docs); free(r);
-        return -3;
-      }
-      mvk = (int)k;
+      mvk[nmv++] = k;
       continue;
     }
     key_ids[k] = sv_dict_ids_at(kc, docs, n);
@@ -1107,12 +1101,25 @@ int orc_execute_segment(const pg_plan *plan, uint32_t seg, const orc_column *col
   }
   for (int i = 0; i < 256; i++) projected += used[i];
   uint64_t *row_doc = NULL, nrows = n;
-  if (mvk >= 0) {  /* one group-by row per (matched doc, value of its MV key), in doc then stored-value order */
-    const orc_column *kc = &cols[plan->keys[mvk].col_id];
-    mv_view v;
-    mv_open(kc, &v);
+  if (nmv) {
+    /* one group-by row per (matched doc, tuple of the cartesian product of its MV keys' lists): DictionaryBasedGroupKeyGenerator
+     * .getIntRawKeys (:472-540) builds the product with the lowest-index MV key outermost and the last one fastest,
+     * each list in stored order, duplicates kept; rows in doc order */
+    const orc_column *kcs[64];
+    mv_view v[64];
+    int mvpos[64];
+    for (uint32_t k = 0; k < plan->num_keys; k++) mvpos[k] = -1;
+    for (uint32_t m = 0; m < nmv; m++) {
+      kcs[m] = &cols[plan->keys[mvk[m]].col_id];
+      mv_open(kcs[m], &v[m]);
+      mvpos[mvk[m]] = (int)m;
+    }
     nrows = 0;
-    for (uint64_t i = 0; i < n; i++) nrows += v.offsets[docs[i] + 1] - v.offsets[docs[i]];
+    for (uint64_t i = 0; i < n; i++) {
+      uint64_t prod = 1;
+      for (uint32_t m = 0; m < nmv; m++) prod *= v[m].offsets[docs[i] + 1] - v[m].offsets[docs[i]];
+      nrows += prod;
+    }
     row_doc = (uint64_t *)malloc(sizeof(uint64_t) * (nrows ? nrows : 1));
     int32_t *sv_ids[64];
     for (uint32_t k = 0; k < plan->num_keys; k++) {
@@ -1120,14 +1127,27 @@ int orc_execute_segment(const pg_plan *plan, uint32_t seg, const orc_column *col
       key_ids[k] = (int32_t *)malloc(sizeof(int32_t) * (nrows ? nrows : 1));
     }
     uint64_t row = 0;
-    for (uint64_t i = 0; i < n; i++)
-      for (uint64_t j = v.offsets[docs[i]]; j < v.offsets[docs[i] + 1]; j++, row++) {
+    for (uint64_t i = 0; i < n; i++) {
+      uint64_t cur[64];
+      int empty = 0;
+      for (uint32_t m = 0; m < nmv; m++) {
+        cur[m] = v[m].offsets[docs[i]];
+        empty |= cur[m] == v[m].offsets[docs[i] + 1];
+      }
+      if (empty) continue;
+      for (;;) {
         row_doc[row] = i;
         for (uint32_t k = 0; k < plan->num_keys; k++)
-          key_ids[k][row] = (int)k == mvk ? (int32_t)read_bits(v.raw, j, kc->bits) : sv_ids[k][i];
+          key_ids[k][row] = mvpos[k] >= 0 ? (int32_t)read_bits(v[mvpos[k]].raw, cur[mvpos[k]], kcs[mvpos[k]]->bits)
+                                          : sv_ids[k][i];
+        row++;
+        int m = (int)nmv - 1;
+        while (m >= 0 && ++cur[m] == v[m].offsets[docs[i] + 1]) { cur[m] = v[m].offsets[docs[i]]; m--; }
+        if (m < 0) break;
       }
+    }
     for (uint32_t k = 0; k < plan->num_keys; k++) free(sv_ids[k]);
-    free(v.offsets);
+    for (uint32_t m = 0; m < nmv; m++) free(v[m].offsets);
   }
 
   if (plan->num_keys == 0) aggregate_only(plan, cols, docs, n, inputs, r);

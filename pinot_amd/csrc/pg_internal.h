@@ -48,7 +48,6 @@ enum GroupType : uint32_t { GT_ROOT = 0, GT_AND = 1, GT_OR = 2, GT_NOT = 3 };
 // Compaction queue (QuerySpec::queue_mode): docs that pass the staged (phase A) children of a root AND are appended
 // to a per-block LDS queue; the remaining children and the aggregation run over the queue once it holds at least
 // kQueueFlush docs (every lane busy) instead of over a few docs per tile.
-constexpr uint32_t kNoMvKey = 0xFFFFFFFFu;  // QuerySpec.mv_key: no multi-value group key
 constexpr int kQueueRows = 4;
 constexpr int kQueueCap = kBlock * kQueueRows;       // 1024 docs
 constexpr int kQueueFlush = kBlock * 2;              // flush at >= 512 queued docs
@@ -233,7 +232,8 @@ struct QuerySpec {
   uint64_t hmask;            // hash: num_slots - 1
   uint32_t n_i64, n_fx, n_min, n_max;  // n_fx: SK_FX slots, 2 words each
   uint32_t dc_row_words;     // uint32 words of DISTINCTCOUNT bitmaps per slot
-  uint32_t mv_key;           // the multi-value group key (each value of a doc's list is a group of the doc) or kNoMvKey
+  uint32_t mv_keys;          // bit k: group key k is multi-value (a doc joins the group of each tuple of the
+                             // cartesian product of its MV keys' lists); 0: no multi-value group key
   uint32_t mv_aggs;          // bit a: aggregation a reads every value of an MV column (AggSpec.mv)
   unsigned long long* i64;
   unsigned long long* fx;    // [num_slots][n_fx][2] (lo, hi)

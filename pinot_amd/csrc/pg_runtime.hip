@@ -1469,7 +1469,7 @@ void key_coldesc(ColDesc& dc, const ColumnRes* c, const pg_key& key) {
 // A group key column usable in segment si: SV dictIds + dictionary (any key kind), or a raw INT / LONG forward index
 // as value offsets (NoDictionarySingleColumnGroupKeyGenerator.java:51 / NoDictionaryMultiColumnGroupKeyGenerator.java:49
 // key raw values; here the value offset is the key id, so segments and GPUs merge by value as for dictionary keys).
-// A multi-value dictionary column (allow_mv: the plan's one MV key) groups each of a doc's values
+// A multi-value dictionary column (allow_mv: one of the plan's MV keys) groups each of a doc's values
 // (DictionaryBasedGroupKeyGenerator.generateKeysForBlock(.., int[][]) :188-200).
 int check_key_column(const ColumnRes* c, const pg_key& key, uint32_t k, uint32_t si, bool allow_mv = false) {
   if (!c) return fail(PG_E_NOTFOUND, "group key column %u not resident in segment %u", key.col_id, si);
@@ -1714,9 +1714,10 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   const uint64_t limit = plan->num_groups_limit ? plan->num_groups_limit : kDefaultNumGroupsLimit;
   uint64_t seg_groups = 0;  // sum over segments of an upper bound of the segment's distinct keys
   bool truncating = false;
-  q.mv_key = kNoMvKey;
+  q.mv_keys = 0;
   if (K) {
-    // the multi-value key (at most one: several would group the cartesian product of their lists)
+    // the multi-value keys: a doc joins the group of every tuple of the cartesian product of their lists
+    // (DictionaryBasedGroupKeyGenerator.getIntRawKeys :472-540)
     {
       for (uint32_t k = 0; k < K && S; k++) {
         bool mv = false;
@@ -1724,24 +1725,22 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
           const ColumnRes* c = col(si, plan->keys[k].col_id);
           mv |= c && c->fwd == FWD_MV;
         }
-        if (!mv) continue;
-        if (q.mv_key != kNoMvKey) return fail(PG_E_UNSUPPORTED, "group-by over more than one multi-value column");
-        q.mv_key = k;
+        if (mv) q.mv_keys |= 1u << k;
       }
     }
     for (uint32_t si = 0; si < S; si++) {
       uint64_t prod = 1;
       for (uint32_t k = 0; k < K; k++) {
         const ColumnRes* c = col(si, plan->keys[k].col_id);
-        if ((rc = check_key_column(c, plan->keys[k], k, si, k == q.mv_key))) return rc;
-        if (k == q.mv_key && c->fwd != FWD_MV)
+        if ((rc = check_key_column(c, plan->keys[k], k, si, (q.mv_keys >> k) & 1u))) return rc;
+        if (((q.mv_keys >> k) & 1u) && c->fwd != FWD_MV)
           return fail(PG_E_UNSUPPORTED, "group key %u is multi-value in some segments only", k);
         // distinct values in the segment: the dictionary's size, or (raw) at most its docs and the key range
         const uint64_t kc = c->fwd == FWD_RAW ? std::min<uint64_t>(c->num_docs, plan->keys[k].cardinality) : c->card;
         prod = prod > (1ull << 62) / (kc ? kc : 1) ? (1ull << 62) : prod * kc;
       }
       // (an MV key: a doc may hold several groups -- bounded by the key space, not the docs)
-      const uint64_t ub = q.mv_key != kNoMvKey ? prod : std::min<uint64_t>(prod, plan->segments[si].num_docs);
+      const uint64_t ub = q.mv_keys ? prod : std::min<uint64_t>(prod, plan->segments[si].num_docs);
       seg_groups += ub;
       // >=: a segment holding exactly `limit` keys reports numGroupsLimitReached (getNumGroups() >= limit,
       // AggregationGroupByOrderByOperator.java:112-113), which the per-segment table counts
@@ -1848,7 +1847,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
                        G * slot_bytes <= kStateBudget / 4 && G <= 4 * (t_layout.on ? t_layout.docs : total_docs) + 65536;
     // numGroupsLimit truncation assigns ids in first-seen (doc, value) order; the per-segment table orders by first
     // doc only, so a multi-value key that may reach the limit is left to the CPU plan
-    if (truncating && q.mv_key != kNoMvKey)
+    if (truncating && q.mv_keys)
       return fail(PG_E_UNSUPPORTED, "multi-value group key whose segments may reach numGroupsLimit");
     P.mode = truncating ? GM_HASH_SEG : (dense ? GM_DENSE : GM_HASH);
     if (P.mode == GM_DENSE) {
@@ -1888,7 +1887,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     const int pe = part_env ? atoi(part_env) : -1;
     uint32_t dc = (uint32_t)kNoSlot, ndc = 0;
     bool ok = P.mode == GM_DENSE && !q.use_lds && K > 0 && P.n_i64 == 1 && !P.n_fx && !P.n_min && !P.n_max &&
-              total_docs > 0 && total_docs < 0xFFFFFFF0ull && pe != 0 && q.mv_key == kNoMvKey && !q.mv_aggs;
+              total_docs > 0 && total_docs < 0xFFFFFFF0ull && pe != 0 && !q.mv_keys && !q.mv_aggs;
     for (uint32_t a = 0; a < A && ok; a++) {
       if (P.aggs[a].fn == PG_AGG_DISTINCTCOUNT) { dc = a; ndc++; }
       else if (P.aggs[a].fn != PG_AGG_COUNT) ok = false;
@@ -2597,7 +2596,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
       }
     }
     for (uint32_t k = 0; k < K; k++) {
-      if (k == q.mv_key) continue;  // value-indexed words: read per doc through its row offsets
+      if ((q.mv_keys >> k) & 1u) continue;  // value-indexed words: read per doc through its row offsets
       uint32_t bmax = 0;
       for (uint32_t si = 0; si < S; si++) bmax = std::max(bmax, keycols[(uint64_t)si * K + k].bits);
       add(2, k, 0, ((key_dec(k) ? 3ull : 1ull) << 32) | plan->keys[k].col_id, filter_pass, bmax);
@@ -2656,7 +2655,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
             q.agg_slot[a][1] = (uint8_t)slot;
         }
         for (uint32_t k = 0; k < K; k++)
-          if (k != q.mv_key && plan->keys[k].col_id == cid && key_dec(k) == dec) q.key_slot[k] = (uint8_t)slot;
+          if (!((q.mv_keys >> k) & 1u) && plan->keys[k].col_id == cid && key_dec(k) == dec) q.key_slot[k] = (uint8_t)slot;
         // a leaf-sourced slot that aggregation / key uses share is sourced from one of those uses: their column words
         // exist in every segment, while a segment whose form of the leaf reads no column (isAlwaysTrue: LK_ALL) would
         // copy nothing and leave the shared slot stale for the aggregation

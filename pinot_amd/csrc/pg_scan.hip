@@ -718,25 +718,46 @@ __device__ __forceinline__ uint32_t col_id(const QuerySpec& q, uint32_t slot, co
   return unpack(make_rsrc(c.words, c.wbytes), d, c.bits);
 }
 
-// GROUP BY a multi-value column: doc d joins the group of each value of its list, in stored order, duplicates
-// included (DictionaryBasedGroupKeyGenerator.generateKeysForBlock(.., int[][]) :188-200), each with the doc's own
-// aggregation inputs (aggregateGroupByMV); g0 = the packed key of the SV keys.  noinline, the aggregations in a
-// runtime loop: one copy per kernel, not one per unrolled aggregation slot of every shape.
+// GROUP BY multi-value columns: doc d joins the group of each tuple of the cartesian product of its MV keys' lists, in
+// stored order, duplicates included (DictionaryBasedGroupKeyGenerator.generateKeysForBlock(.., int[][]) :188-200,
+// getIntRawKeys :472-540: the lowest MV key outermost), each with the doc's own aggregation inputs
+// (aggregateGroupByMV); g0 = the packed key of the SV keys.  noinline, the aggregations in a runtime loop: one copy
+// per kernel, not one per unrolled aggregation slot of every shape.
 __device__ __attribute__((noinline)) void mv_key_update(const QuerySpec* qp, GroupState S, SegDesc sd, uint32_t d,
                                                         uint64_t g0) {
   const QuerySpec& q = *qp;
-  const ColDesc mk = ldc(sd.keycols, q.mv_key);
-  const PG_GLOBAL uint32_t* off = glb(mk.mv_offsets);
-  const uint32_t v0 = off[d], v1 = off[d + 1];
-  const rsrc_t rs = make_rsrc(mk.words, mk.wbytes);
-  for (uint32_t v = v0; v < v1; v++) {
-    const uint64_t kid = key_of(q.key_kind[q.mv_key], q.key_base[q.mv_key], mk, unpack(rs, v, mk.bits));
-    if (kid >= q.key_card[q.mv_key]) {  // never expected: the host proved the key ranges
+  uint32_t mk_k[kMaxKeys], cur[kMaxKeys], beg[kMaxKeys], end[kMaxKeys];
+  uint32_t nmv = 0;
+  for (uint32_t k = 0; k < q.num_keys; k++) {
+    if (!((q.mv_keys >> k) & 1u)) continue;
+    const ColDesc mk = ldc(sd.keycols, k);
+    const PG_GLOBAL uint32_t* off = glb(mk.mv_offsets);
+    mk_k[nmv] = k;
+    beg[nmv] = cur[nmv] = off[d];
+    end[nmv] = off[d + 1];
+    if (beg[nmv] == end[nmv]) return;  // an empty list: no tuple
+    nmv++;
+  }
+  if (!nmv) return;
+  for (;;) {  // odometer over the lists, the last MV key fastest
+    uint64_t gk = g0;
+    bool in_range = true;
+    for (uint32_t m = 0; m < nmv; m++) {
+      const uint32_t k = mk_k[m];
+      const ColDesc mk = ldc(sd.keycols, k);
+      const uint64_t kid = key_of(q.key_kind[k], q.key_base[k], mk, unpack(make_rsrc(mk.words, mk.wbytes), cur[m], mk.bits));
+      in_range &= kid < q.key_card[k];
+      gk += kid * q.key_stride[k];
+    }
+    int m = (int)nmv - 1;
+    while (m >= 0 && ++cur[m] == end[m]) { cur[m] = beg[m]; m--; }
+    if (!in_range) {  // never expected: the host proved the key ranges
       atomicOr(q.err, 1u);
+      if (m < 0) break;
       continue;
     }
-    const uint64_t g = group_slot(q, g0 + kid * q.key_stride[q.mv_key], sd.index, d);
-    if (g == ~0ull) continue;
+    const uint64_t g = group_slot(q, gk, sd.index, d);
+    if (g == ~0ull) { if (m < 0) break; continue; }
     s_add(S, &S.i64[g * q.n_i64], 1ull);  // slot 0: (doc, value) count / presence
 #pragma unroll 1
     for (uint32_t a = 0; a < q.num_aggs; a++) {
@@ -748,6 +769,7 @@ __device__ __attribute__((noinline)) void mv_key_update(const QuerySpec* qp, Gro
       if (A.mv) mv_update(&q, S, &A, c, g, d, 0ull, true);
       else group_update(q, S, A, c, g, d, ia, ib);
     }
+    if (m < 0) break;
   }
 }
 
@@ -920,7 +942,7 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
 #pragma unroll
       for (int k = 0; k < NK; k++) {
         kidx[x][k] = 0;
-        if (GROUPED && k < (int)q.num_keys && (uint32_t)k != q.mv_key)
+        if (GROUPED && k < (int)q.num_keys && !((q.mv_keys >> k) & 1u))
           kidx[x][k] = col_id(q, Rows::kTile ? q.key_slot[k] : (uint32_t)kNoSlot, ldc(sd.keycols, k), stage, d[x], rel);
       }
 #pragma unroll
@@ -963,14 +985,14 @@ __device__ __forceinline__ void aggregate_tile(const QuerySpec& q, const SegDesc
       }
       if (jj[x] >= 32u) continue;
       if constexpr (GROUPED && MAXA == kMaxAggs) {  // (the multi-value paths live in the widest shapes only)
-        if (q.mv_key != kNoMvKey) {
-          // a multi-value key: the doc joins the group of each value in its list (mv_key_update)
+        if (q.mv_keys) {
+          // multi-value keys: the doc joins the group of each tuple of their lists' product (mv_key_update)
           uint64_t g0 = 0;
           bool in_range = true;
 #pragma unroll
           for (int k = 0; k < NK; k++) {
             if (k >= (int)q.num_keys) break;
-            if ((uint32_t)k == q.mv_key) continue;
+            if ((q.mv_keys >> k) & 1u) continue;
             const uint64_t kid = key_of(q.key_kind[k], q.key_base[k], ldc(sd.keycols, k), kidx[x][k]);
             in_range &= kid < q.key_card[k];
             g0 += kid * q.key_stride[k];
@@ -1251,7 +1273,7 @@ __device__ __forceinline__ void scan_body() {
         if (!GROUPED) doc_count += nm;
         if (GROUPED || q.agg_reads) {
           // dense when at least a quarter of the lanes hold >= 8 matches: batched rows; else per-doc rounds
-          if (__popcll(__ballot(nm >= 8)) >= 16 && (!GROUPED || q.mv_key == kNoMvKey) && !q.mv_aggs)
+          if (__popcll(__ballot(nm >= 8)) >= 16 && (!GROUPED || !q.mv_keys) && !q.mv_aggs)
             aggregate_dense<GROUPED, MAXA, MAXK>(q, sd, S, st, acc, m, base, tid);
           else aggregate_tile<GROUPED, MAXA, MAXK>(q, sd, S, st, acc, m, rows);
         }
@@ -1432,7 +1454,7 @@ uint32_t scan_min_blocks_per_cu(bool grouped) {  // 256-thread blocks: waves/SIM
 hipError_t launch_scan(const QuerySpec& q, uint32_t blocks, hipStream_t s, bool co) {
   const size_t lds = scan_lds_bytes(q);
   // multi-value keys / aggregations: the widest shapes, the only ones compiled with those paths
-  const uint32_t na = (q.mv_key != kNoMvKey || q.mv_aggs) ? (uint32_t)kMaxAggs : q.num_aggs;
+  const uint32_t na = (q.mv_keys || q.mv_aggs) ? (uint32_t)kMaxAggs : q.num_aggs;
   if (q.num_keys == 0) {
     if (na <= 2) launch_one<false, 2, 0>(q, blocks, lds, s, co);
     else if (na <= 4) launch_one<false, 4, 0>(q, blocks, lds, s, co);

@@ -1170,10 +1170,8 @@ class CPlan:
             keys[k].kind = ks.kind
             keys[k].cardinality = ks.cardinality
             keys[k].base = ks.base
-        # a multi-value key groups each value of a doc's list (DictionaryBasedGroupKeyGenerator :188-200); several would
-        # group the cartesian product of their lists, which neither side restates
-        if sum(table.multi_value(c) for c in query.group_by) > 1:
-            raise UnsupportedQuery("GROUP BY over more than one multi-value column")
+        # a multi-value key groups each value of a doc's list (DictionaryBasedGroupKeyGenerator :188-200); several group
+        # each tuple of the cartesian product of their lists (getIntRawKeys :472-540)
         self._keep.append(keys)
 
         p = abi.pg_plan()

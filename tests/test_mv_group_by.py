@@ -3,8 +3,10 @@
 DefaultGroupByExecutor then calls aggregateGroupByMV, e.g. SumAggregationFunction.java:239-249): every matched doc
 joins the group of each value in its list -- duplicates included -- with its own aggregation inputs, and COUNT counts
 (doc, value) pairs.  Pinned against a Python restatement of that rule over the decoded values; the device against the
-oracle.  Shapes the reference rejects or that neither side restates raise UnsupportedQuery: several MV keys (a
-cartesian product per doc), SV functions over MV columns (getXxxValuesSV) and COUNTMV over SV columns."""
+oracle.  Several MV keys group each tuple of the cartesian product of the doc's lists (getIntRawKeys :472-540; the
+reference's own InnerSegmentAggregationMultiValueQueriesTest groups by column3, column6, column7: one SV and two MV
+keys).  Shapes the reference rejects raise UnsupportedQuery: SV functions over MV columns (getXxxValuesSV) and COUNTMV
+over SV columns."""
 import numpy as np
 import pytest
 
@@ -50,6 +52,11 @@ QUERIES = [
     "SELECT k, DISTINCTCOUNTMV(words), DISTINCTCOUNTMV(tags) FROM t WHERE d > -50 GROUP BY k",
     "SELECT MINMV(fm), MAXMV(tags), DISTINCTCOUNTMV(tags), AVGMV(fm) FROM t",
     "SELECT k, AVGMV(tags) FROM t GROUP BY k ORDER BY AVGMV(tags) DESC LIMIT 3",
+    # several MV keys: one group per tuple of the product of the doc's lists (duplicates in a list kept)
+    "SELECT tags, words, COUNT(*), SUM(v) FROM t GROUP BY tags, words",
+    "SELECT k, words, tags, COUNT(*), MAX(d), SUMMV(fm), DISTINCTCOUNT(v) FROM t WHERE v < 200 GROUP BY k, words, tags",
+    "SELECT words, fm, COUNT(*), AVG(v) FROM t WHERE tags IN (1, 2, 3) GROUP BY words, fm",
+    "SELECT tags, k, words, SUM(v) FROM t GROUP BY tags, k, words ORDER BY SUM(v) DESC, tags, k, words LIMIT 6",
 ]
 
 
@@ -168,7 +175,6 @@ def test_mv_function_names():
 
 @pytest.mark.parametrize("sql", [
     "SELECT k, SUMMV(v) FROM t GROUP BY k",                        # an MV function over an SV column
-    "SELECT tags, words, COUNT(*) FROM t GROUP BY tags, words",   # two MV keys: a cartesian product per doc
     "SELECT k, SUM(tags) FROM t GROUP BY k",                       # an SV function over an MV column
     "SELECT COUNTMV(v) FROM t",                                     # COUNTMV over an SV column
     "SELECT DISTINCTCOUNT(tags) FROM t",
