@@ -40,23 +40,27 @@ __device__ __forceinline__ rsrc_t rsrc_of(const void* p, uint32_t bytes) {
                                            (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
+#ifndef PG_STREAM_CPOL
+#define PG_STREAM_CPOL 0  // cache policy of the stream's group loads (gfx950 aux bits: 1 sc0, 2 nt, 16 sc1); 0 = default
+#endif
+
 // The B words of a 32-doc group into registers (buffer loads: reads past the column return 0).
 template <int B>
 __device__ __forceinline__ void load_group(rsrc_t r, uint64_t g, uint32_t (&w)[B + 1]) {
   const uint32_t off = (uint32_t)(g * B * 4u);
 #pragma unroll
   for (int k = 0; k + 4 <= B; k += 4) {
-    const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, off + 4u * k, 0, 0);
+    const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, off + 4u * k, 0, PG_STREAM_CPOL);
     w[k] = x[0]; w[k + 1] = x[1]; w[k + 2] = x[2]; w[k + 3] = x[3];
   }
   constexpr int R = B & 3, K0 = B & ~3;
   if constexpr (R == 1) {
-    w[K0] = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4u * K0, 0, 0);
+    w[K0] = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4u * K0, 0, PG_STREAM_CPOL);
   } else if constexpr (R == 2) {
-    const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, off + 4u * K0, 0, 0);
+    const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, off + 4u * K0, 0, PG_STREAM_CPOL);
     w[K0] = x[0]; w[K0 + 1] = x[1];
   } else if constexpr (R == 3) {
-    const auto x = __builtin_amdgcn_raw_buffer_load_b96(r, off + 4u * K0, 0, 0);
+    const auto x = __builtin_amdgcn_raw_buffer_load_b96(r, off + 4u * K0, 0, PG_STREAM_CPOL);
     w[K0] = x[0]; w[K0 + 1] = x[1]; w[K0 + 2] = x[2];
   }
   w[B] = 0;
