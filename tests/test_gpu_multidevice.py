@@ -6,7 +6,8 @@ the partial states itself (dense states element-wise after a device-to-device co
 exchange), as BaseCombineOperator.mergeResults merges one server's segments (operator/combine/
 BaseCombineOperator.java:190-233).  Every result must equal the CPU oracle over the whole table: configs 2 and 4 (the
 value sets of the DISTINCTCOUNT included), hash-grouped and wide (9-key tuple) group-bys, and exact double sums of
-wide-range data (bit-identical to the one-device run), raw FLOAT / DOUBLE / wide LONG keys.  The library binds a process once, so each case runs in a
+wide-range data (bit-identical to the one-device run), raw FLOAT / DOUBLE / wide LONG keys, raw STRING / BYTES keys
+and filters, several multi-value keys.  The library binds a process once, so each case runs in a
 spawned process."""
 import os
 import sys
@@ -106,6 +107,14 @@ def _worker(devices, q):
         for sql in RAW_QUERIES:
             if "g_" in sql or "wide" in sql or "DISTINCTCOUNT(ts)" in sql:
                 check(tr, sql)
+        # raw STRING / BYTES keys and filters (derived encodings per segment), several multi-value keys
+        from test_mv_group_by import _segments as mv_segments
+        from test_raw_strings import FILTERS, _segments as rs_segments
+        ts = Table("t", rs_segments(4, seed=5))
+        for where, _ in FILTERS[::3]:
+            check(ts, f"SELECT w, k, COUNT(*), SUM(v) FROM t WHERE {where} GROUP BY w, k")
+        tm = Table("t", mv_segments(4, seed=7))
+        check(tm, "SELECT k, words, tags, COUNT(*), MAX(d), SUMMV(fm) FROM t WHERE v < 200 GROUP BY k, words, tags")
         q.put((True, sorted(seen_modes)))
     except Exception:
         q.put((False, traceback.format_exc()))
