@@ -5,7 +5,8 @@ joins the group of each value in its list -- duplicates included -- with its own
 (doc, value) pairs.  Pinned against a Python restatement of that rule over the decoded values; the device against the
 oracle.  Several MV keys group each tuple of the cartesian product of the doc's lists (getIntRawKeys :472-540; the
 reference's own InnerSegmentAggregationMultiValueQueriesTest groups by column3, column6, column7: one SV and two MV
-keys).  Shapes the reference rejects raise UnsupportedQuery: SV functions over MV columns (getXxxValuesSV) and COUNTMV
+keys).  Under numGroupsLimit a segment keeps the keys seen first in (doc, key tuple) order.  Shapes the reference rejects
+raise UnsupportedQuery: SV functions over MV columns (getXxxValuesSV) and COUNTMV
 over SV columns."""
 import numpy as np
 import pytest
@@ -60,12 +61,15 @@ QUERIES = [
 ]
 
 
-def _expected(table, sql):
-    """Python restatement: one row per (matched doc, value of the MV key) in doc / stored order."""
+def _expected(table, sql, limit=None):
+    """Python restatement: one row per (matched doc, tuple of the MV keys' lists) in doc / stored order (the lowest MV
+    key outermost).  limit: numGroupsLimit -- per segment, a key not among the first `limit` keys seen in that order
+    gets INVALID_ID and its rows are dropped (DictionaryBasedGroupKeyGenerator's map-based holders)."""
     q = parse(sql)
     rows = {}
     for seg in table.segments:
         cols = seg.columns
+        seen = set()
 
         def val(c, i):
             col = cols[c]
@@ -83,6 +87,10 @@ def _expected(table, sql):
                 keys = [kk + (y,) for kk in keys for y in (x if isinstance(x, list) else [x])]
             for key in keys:
                 key = tuple(y.item() if hasattr(y, "item") else y for y in key)
+                if limit is not None and key not in seen:
+                    if len(seen) >= limit:
+                        continue
+                    seen.add(key)
                 r = rows.setdefault(key, [[] for _ in q.aggregations])
                 for a, ag in enumerate(q.aggregations):
                     if ag.function == "COUNT":
@@ -195,10 +203,33 @@ def test_mv_group_by_on_device(sql, mv_table, gpu_engine, oracle_engine):
         assert reduce_to_rows(q, g) == reduce_to_rows(q, o)
 
 
+TRUNCATING = [
+    ("SELECT tags, COUNT(*), SUM(v) FROM t GROUP BY tags", 10),
+    ("SELECT k, tags, COUNT(*), MAX(d) FROM t WHERE v > -200 GROUP BY k, tags", 30),
+    ("SELECT tags, words, COUNT(*), SUM(v) FROM t GROUP BY tags, words", 40),
+    ("SELECT k, words, tags, COUNT(*) FROM t GROUP BY k, words, tags", 100),
+]
+
+
+@pytest.mark.parametrize("sql,limit", TRUNCATING)
+def test_oracle_mv_truncation_is_first_seen(sql, limit, mv_table, oracle_engine):
+    """numGroupsLimit with multi-value keys: group ids go to keys in first-seen (doc, key tuple) order per segment."""
+    q = parse(sql)
+    got = oracle_engine.execute(mv_table, q, config=InstanceConfig.with_groups_limit(limit))
+    want = _expected(mv_table, sql, limit=limit)
+    assert set(got.rows) == set(want) and got.groups_limit_reached
+    for key, row in want.items():
+        for ag, g, w in zip(q.aggregations, got.rows[key], row):
+            assert (np.isclose(g, w, rtol=1e-12, atol=1e-9) if isinstance(w, float) else g == w), (key, ag, g, w)
+
+
 @pytest.mark.gpu
-def test_mv_group_by_that_may_truncate_is_left_to_the_cpu(mv_table, gpu_engine):
-    """numGroupsLimit assigns group ids in first-seen (doc, value) order; a segment that may reach the limit is not run
-    on the device with an MV key (PG_E_UNSUPPORTED -> the CPU plan)."""
-    cfg = InstanceConfig.with_groups_limit(10)
-    with pytest.raises(UnsupportedQuery):
-        gpu_engine.execute(mv_table, parse("SELECT tags, COUNT(*) FROM t GROUP BY tags"), config=cfg)
+@pytest.mark.parametrize("sql,limit", TRUNCATING)
+def test_mv_group_by_truncation_on_device(sql, limit, mv_table, gpu_engine, oracle_engine):
+    """The device's per-segment table orders each (segment, key) by its first (doc, tuple position) sighting."""
+    from helpers import assert_same_result
+    cfg = InstanceConfig.with_groups_limit(limit)
+    q = parse(sql)
+    g, o = gpu_engine.execute(mv_table, q, config=cfg), oracle_engine.execute(mv_table, q, config=cfg)
+    assert_same_result(g, o, table=mv_table)
+    assert g.groups_limit_reached == o.groups_limit_reached
