@@ -330,7 +330,7 @@ struct StateView {            // the device arrays of one partial state
   long long* mn;
   long long* mx;
   uint32_t* bits;
-  unsigned int* first_doc;    // GM_HASH_SEG tables
+  unsigned long long* first_doc;  // GM_HASH_SEG tables: doc << 16 | tuple position (QuerySpec.first_doc)
   unsigned int* fill;         // hash tables: claimed keys
   unsigned int* err;          // bit 2: table full
   uint32_t n_i64, n_fx, n_min, n_max, bit_words, max_fill;
@@ -402,7 +402,7 @@ hipError_t launch_merge_dense(const StateView& dst, const StateView& src, hipStr
 hipError_t launch_fx_limbs(unsigned long long* pairs, long long* limbs, uint64_t n, bool in, hipStream_t s);
 hipError_t launch_init_view(const StateView& v, hipStream_t s, FillSpans* defer = nullptr);  // pg_kernels.hip: zero / empty / +-inf state
 hipError_t launch_seg_truncate(const StateView& v, const uint32_t* slots, uint64_t n, uint32_t num_segments,
-                               uint64_t limit, uint64_t* tmp_keys, uint64_t* sorted_keys, uint32_t* sorted_slots,
+                               uint64_t limit, bool mv, uint64_t* tmp_keys, uint64_t* sorted_keys, uint32_t* sorted_slots,
                                uint32_t* seg_first, uint8_t* keep, unsigned int* reached, void* temp, size_t temp_bytes,
                                hipStream_t s);
 

@@ -725,46 +725,51 @@ hipError_t launch_merge_dense(const StateView& dst, const StateView& src, hipStr
 
 // ------------------------------------------------------------------------------------------ numGroupsLimit
 
-// Sort key of an occupied GM_HASH_SEG entry: (segment, first matching doc) -> the segment's first-seen order.
+// Sort key of an occupied GM_HASH_SEG entry -> the segment's first-seen order: (segment, first matching doc) in 32 + 32
+// bits, or with multi-value keys (segment, doc, tuple position) in 16 + 32 + 16 bits (first_doc = doc << 16 | position).
 __global__ void seg_order_kernel(StateView v, const uint32_t* __restrict__ slots, uint64_t n, uint32_t num_segments,
-                                 uint64_t* __restrict__ out) {
+                                 uint32_t shift, uint64_t* __restrict__ out) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint32_t s = slots[i];
     const uint64_t seg = v.keys[s] % num_segments;
-    out[i] = (seg << 32) | v.first_doc[s];
+    const uint64_t first = v.first_doc[s];
+    out[i] = (seg << shift) | (shift == 32 ? first >> 16 : first);
   }
 }
 
 // keep[i] = rank of sorted entry i within its segment < limit (seg_first: first sorted index of each segment).
-__global__ void seg_first_kernel(const uint64_t* __restrict__ sorted, uint64_t n, uint32_t* __restrict__ seg_first) {
+__global__ void seg_first_kernel(const uint64_t* __restrict__ sorted, uint64_t n, uint32_t shift,
+                                 uint32_t* __restrict__ seg_first) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-    if (i == 0 || (sorted[i] >> 32) != (sorted[i - 1] >> 32)) seg_first[sorted[i] >> 32] = (uint32_t)i;
+    if (i == 0 || (sorted[i] >> shift) != (sorted[i - 1] >> shift)) seg_first[sorted[i] >> shift] = (uint32_t)i;
 }
 // reached: set when some segment holds >= limit keys (its rank limit - 1 exists: numGroupsLimitReached)
-__global__ void seg_keep_kernel(const uint64_t* __restrict__ sorted, uint64_t n, const uint32_t* __restrict__ seg_first,
-                                uint64_t limit, uint8_t* __restrict__ keep, unsigned int* __restrict__ reached) {
+__global__ void seg_keep_kernel(const uint64_t* __restrict__ sorted, uint64_t n, uint32_t shift,
+                                const uint32_t* __restrict__ seg_first, uint64_t limit, uint8_t* __restrict__ keep,
+                                unsigned int* __restrict__ reached) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint64_t rank = i - seg_first[sorted[i] >> 32];
+    const uint64_t rank = i - seg_first[sorted[i] >> shift];
     keep[i] = rank < limit;
     if (rank + 1 == limit) atomicOr(reached, 1u);
   }
 }
 
 hipError_t launch_seg_truncate(const StateView& v, const uint32_t* slots, uint64_t n, uint32_t num_segments,
-                               uint64_t limit, uint64_t* tmp_keys, uint64_t* sorted_keys, uint32_t* sorted_slots,
+                               uint64_t limit, bool mv, uint64_t* tmp_keys, uint64_t* sorted_keys, uint32_t* sorted_slots,
                                uint32_t* seg_first, uint8_t* keep, unsigned int* reached, void* temp, size_t temp_bytes,
                                hipStream_t s) {
   if (!n) return hipSuccess;
   const uint64_t blocks = (n + 255) / 256;
   const dim3 g((uint32_t)(blocks < 16384 ? blocks : 16384));
-  hipLaunchKernelGGL(seg_order_kernel, g, dim3(256), 0, s, v, slots, n, num_segments, tmp_keys);
+  const uint32_t shift = mv ? 48u : 32u;
+  hipLaunchKernelGGL(seg_order_kernel, g, dim3(256), 0, s, v, slots, n, num_segments, shift, tmp_keys);
   hipError_t e = launch_sort_pairs(tmp_keys, sorted_keys, slots, sorted_slots, n, temp, temp_bytes, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(seg_first_kernel, g, dim3(256), 0, s, sorted_keys, n, seg_first);
-  hipLaunchKernelGGL(seg_keep_kernel, g, dim3(256), 0, s, sorted_keys, n, seg_first, limit, keep, reached);
+  hipLaunchKernelGGL(seg_first_kernel, g, dim3(256), 0, s, sorted_keys, n, shift, seg_first);
+  hipLaunchKernelGGL(seg_keep_kernel, g, dim3(256), 0, s, sorted_keys, n, shift, seg_first, limit, keep, reached);
   return hipGetLastError();
 }
 

@@ -242,7 +242,8 @@ struct QuerySpec {
   uint32_t* dbits;           // [num_slots][dc_row_words]
   unsigned long long* hkeys; // GM_HASH*: [num_slots] packed keys
   unsigned int* hfill;       // GM_HASH*: claimed keys
-  unsigned int* first_doc;   // GM_HASH_SEG: [num_slots] first matching doc of the (segment, key)
+  unsigned long long* first_doc;  // GM_HASH_SEG: [num_slots] first-seen order of the (segment, key): first matching
+                                  // doc << 16 | the key's position among that doc's multi-value key tuples (0: SV keys)
   const SegDesc* segs;       // [seg]
   const WorkItem* items;     // [item]
   unsigned long long* seg_matched;  // [seg]

@@ -75,7 +75,7 @@ hipError_t launch_init_view(const StateView& v, hipStream_t s, FillSpans* defer)
   if (v.n_fx && (e = fill(v.fx, 0, v.num_slots * v.n_fx * 16)) != hipSuccess) return e;
   if (v.bit_words && (e = fill(v.bits, 0, v.num_slots * v.bit_words * 4ull)) != hipSuccess) return e;
   if (v.keys && (e = fill(v.keys, 0xFF, v.num_slots * 8)) != hipSuccess) return e;
-  if (v.first_doc && (e = fill(v.first_doc, 0xFF, v.num_slots * 4)) != hipSuccess) return e;
+  if (v.first_doc && (e = fill(v.first_doc, 0xFF, v.num_slots * 8)) != hipSuccess) return e;
   if (v.fill && (e = fill(v.fill, 0, 8)) != hipSuccess) return e;  // fill + err
   const uint64_t n = v.num_slots * (v.n_min > v.n_max ? v.n_min : v.n_max);
   if (n) {

@@ -953,7 +953,7 @@ struct Partials {
     v.mn = (long long*)mn.p;
     v.mx = (long long*)mx.p;
     v.bits = (uint32_t*)bits.p;
-    v.first_doc = (unsigned int*)first_doc.p;
+    v.first_doc = (unsigned long long*)first_doc.p;
     v.fill = (unsigned int*)misc.p;
     v.err = misc.p ? (unsigned int*)misc.p + 1 : nullptr;
     v.n_i64 = n_i64; v.n_fx = n_fx; v.n_min = n_min; v.n_max = n_max; v.bit_words = bit_words;
@@ -1254,7 +1254,7 @@ int Partials::alloc_state(hipStream_t s, bool init, FillSpans* defer) {
   if (n_max) { if ((rc = mx.alloc_pooled(G * 8ull * n_max))) return rc; } else mx.reset();
   if (bit_words) { if ((rc = bits.alloc_pooled(G * 4ull * bit_words))) return rc; } else bits.reset();
   if (hash) { if ((rc = keys.alloc_pooled(G * 8ull))) return rc; } else keys.reset();
-  if (mode == GM_HASH_SEG) { if ((rc = first_doc.alloc_pooled(G * 4ull))) return rc; } else first_doc.reset();
+  if (mode == GM_HASH_SEG) { if ((rc = first_doc.alloc_pooled(G * 8ull))) return rc; } else first_doc.reset();
   if ((rc = misc.alloc_pooled(16))) return rc;
   if (init) HIP_CHECK(launch_init_view(view(), s, defer));
   else HIP_CHECK(hipMemsetAsync(misc.p, 0, 16, s));  // every slot is written by the producer (pg_part.hip)
@@ -1319,10 +1319,11 @@ int hash_like(const Partials& src, uint64_t groups, Partials& out, hipStream_t s
 }
 
 // numGroupsLimit (IntGroupIdMap.getGroupId, DictionaryBasedGroupKeyGenerator.java:991-1016): every segment of a
-// GM_HASH_SEG table keeps the `limit` keys whose first matching doc comes first (its group ids 0..limit-1; docs of
-// later keys got INVALID_ID and were dropped); the kept (segment, key) states are then merged by key
-// (GroupByOrderByCombineOperator) into a GM_HASH table that replaces P's state.
-int truncate_and_merge(Partials& P, uint64_t limit, hipStream_t s) {
+// GM_HASH_SEG table keeps the `limit` keys seen first (its group ids 0..limit-1; docs of later keys got INVALID_ID and
+// were dropped) -- first matching doc, then (mv: multi-value keys) the key's position among that doc's key tuples in
+// getIntRawKeys order (:472-540); the kept (segment, key) states are then merged by key (GroupByOrderByCombineOperator)
+// into a GM_HASH table that replaces P's state.
+int truncate_and_merge(Partials& P, uint64_t limit, bool mv, hipStream_t s) {
   const StateView v = P.view();
   const uint64_t cap = P.num_slots;
   Scratch sc(s);
@@ -1344,7 +1345,7 @@ int truncate_and_merge(Partials& P, uint64_t limit, hipStream_t s) {
   unsigned int* reached = sc.get<unsigned int>(1, rc);
   if (rc) return rc;
   HIP_CHECK(hipMemsetAsync(reached, 0, 4, s));
-  HIP_CHECK(launch_seg_truncate(v, slots, n, P.num_segments, limit, tmp_keys, sorted_keys, sorted_slots, seg_first,
+  HIP_CHECK(launch_seg_truncate(v, slots, n, P.num_segments, limit, mv, tmp_keys, sorted_keys, sorted_slots, seg_first,
                                 keep, reached, temp, temp_bytes, s));
   uint32_t hit = 0;
   if ((rc = read_back((uint32_t*)reached, hit, s))) return rc;
@@ -1845,10 +1846,10 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   } else {
     const bool dense = !(plan->flags & PG_PLAN_HASH_GROUPS) && G <= kDenseMaxSlots &&
                        G * slot_bytes <= kStateBudget / 4 && G <= 4 * (t_layout.on ? t_layout.docs : total_docs) + 65536;
-    // numGroupsLimit truncation assigns ids in first-seen (doc, value) order; the per-segment table orders by first
-    // doc only, so a multi-value key that may reach the limit is left to the CPU plan
-    if (truncating && q.mv_keys)
-      return fail(PG_E_UNSUPPORTED, "multi-value group key whose segments may reach numGroupsLimit");
+    // numGroupsLimit truncation assigns ids in first-seen (doc, key tuple) order: the per-segment table's sort key
+    // packs (segment, doc, tuple position) into 16 + 32 + 16 bits for multi-value keys
+    if (truncating && q.mv_keys && S > 0xFFFFu)
+      return fail(PG_E_UNSUPPORTED, "multi-value group keys under numGroupsLimit over more than 65535 segments in one call");
     P.mode = truncating ? GM_HASH_SEG : (dense ? GM_DENSE : GM_HASH);
     if (P.mode == GM_DENSE) {
       P.num_slots = G;
@@ -3773,6 +3774,8 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
     if (err & 8u) return kRetryNoStream;     // more stream survivors than the regions hold: rerun without it
     if (err & 16u) return kRetryExactPart;   // a speculative partition region overflowed: rerun with exact offsets
     if (err & 4u) return kRetryLargerTable;  // hash table over its fill budget: rerun with a larger one
+    if (err & 128u)  // pg_scan.hip mv_key_update: a doc's key tuples beyond the 16-bit first-seen position
+      return fail(PG_E_UNSUPPORTED, "a doc with more than 65535 multi-value key tuples under numGroupsLimit");
     if (err & 64u)  // pg_filter.hip: the exact-mode stream kernel found its LDS LUT at a nonzero base address
       return fail(PG_E_INVALID, "stream kernel LDS layout check failed (code %u): the exact LUT is not at LDS offset 0", err);
     if (err) return fail(PG_E_INVALID, "device bounds check failed (code %u): a %s fell outside the plan's key space", err,
@@ -3781,7 +3784,7 @@ int compile_and_run(const pg_plan* plan, Partials& P, pg_stats& stats, uint64_t 
   stats.num_entries_scanned_post_filter = (stats.num_docs_scanned - ns_docs) * P.projected_cols;
   if (P.mode == GM_HASH_SEG) {
     const double t0 = wall_ms();
-    if ((rc = truncate_and_merge(P, limit, s))) return rc;
+    if ((rc = truncate_and_merge(P, limit, q.mv_keys != 0, s))) return rc;
     t_timing.finalize_wall_ms = (float)(wall_ms() - t0);
   }
   return PG_OK;

@@ -505,12 +505,14 @@ __device__ __forceinline__ uint64_t hash_slot(const QuerySpec& q, uint64_t key) 
 }
 
 // State slot of a doc's group from its packed key (dense: the key itself).  GM_HASH_SEG keys carry the segment and
-// record the segment's first doc of the key (IntGroupIdMap assigns ids in first-seen doc order).
-__device__ __forceinline__ uint64_t group_slot(const QuerySpec& q, uint64_t packed, uint32_t seg, uint32_t doc) {
+// record the segment's first sighting of the key (IntGroupIdMap assigns ids in first-seen order): doc << 16 | pos, pos
+// = the key's position among the doc's multi-value key tuples (0 for single-value keys).
+__device__ __forceinline__ uint64_t group_slot(const QuerySpec& q, uint64_t packed, uint32_t seg, uint32_t doc,
+                                               uint32_t pos = 0) {
   if (q.group_mode == GM_DENSE) return packed;
   if (q.group_mode == GM_HASH) return hash_slot(q, packed);
   const uint64_t h = hash_slot(q, packed * q.num_segments + seg);
-  if (h != ~0ull) atomicMin(&q.first_doc[h], doc);
+  if (h != ~0ull) atomicMin(&q.first_doc[h], ((unsigned long long)doc << 16) | pos);
   return h;
 }
 
@@ -739,7 +741,7 @@ __device__ __attribute__((noinline)) void mv_key_update(const QuerySpec* qp, Gro
     nmv++;
   }
   if (!nmv) return;
-  for (;;) {  // odometer over the lists, the last MV key fastest
+  for (uint32_t pos = 0;; pos++) {  // odometer over the lists, the last MV key fastest; pos = the tuple's position
     uint64_t gk = g0;
     bool in_range = true;
     for (uint32_t m = 0; m < nmv; m++) {
@@ -756,7 +758,11 @@ __device__ __attribute__((noinline)) void mv_key_update(const QuerySpec* qp, Gro
       if (m < 0) break;
       continue;
     }
-    const uint64_t g = group_slot(q, gk, sd.index, d);
+    if (pos > 0xFFFFu && q.group_mode == GM_HASH_SEG) {  // beyond the first-seen order's 16 bits: fail loudly
+      atomicOr(q.err, 128u);
+      break;
+    }
+    const uint64_t g = group_slot(q, gk, sd.index, d, pos);
     if (g == ~0ull) { if (m < 0) break; continue; }
     s_add(S, &S.i64[g * q.n_i64], 1ull);  // slot 0: (doc, value) count / presence
 #pragma unroll 1
