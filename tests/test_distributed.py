@@ -133,6 +133,39 @@ def _worker_sharded(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _worker_sharded_shapes(rank, world, port, q):
+    """Raw STRING / BYTES filters and keys, several multi-value keys (also under numGroupsLimit): each rank's oracle
+    result over its round-robin share of the segments, merged by value, equals the single-process answer."""
+    _init(rank, world, port)
+    from helpers import assert_same_result
+    from oracle.oracle import OracleEngine
+    from pinot_amd.combine import gather_merge_results
+    from pinot_amd.plan import InstanceConfig, Table
+    from pinot_amd.query import parse
+    from test_mv_group_by import _segments as mv_segments
+    from test_raw_strings import _segments as rs_segments
+    ok = True
+    for segs, sqls, cfg in (
+            (rs_segments(4, seed=23), ["SELECT w, k, COUNT(*), SUM(v) FROM t WHERE w > 'beta' AND b <> '0a5a' GROUP BY w, k",
+                                       "SELECT u, DISTINCTCOUNT(b), MAX(v) FROM t WHERE u < 'user01500' GROUP BY u"], None),
+            (mv_segments(4, seed=29), ["SELECT k, words, tags, COUNT(*), SUM(v) FROM t GROUP BY k, words, tags"], None),
+            (mv_segments(4, seed=31), ["SELECT tags, words, COUNT(*), SUM(v) FROM t GROUP BY tags, words"],
+             InstanceConfig.with_groups_limit(40))):
+        full = Table("t", segs)
+        mine = Table("t", segs[rank::world])
+        for sql in sqls:
+            qc = parse(sql)
+            part = OracleEngine().execute(mine, qc, config=cfg) if cfg else OracleEngine().execute(mine, qc)
+            merged = gather_merge_results(part)
+            whole = OracleEngine().execute(full, qc, config=cfg) if cfg else OracleEngine().execute(full, qc)
+            try:
+                assert_same_result(merged, whole, table=full)
+            except AssertionError:
+                ok = False
+    q.put((rank, ok))
+    dist.destroy_process_group()
+
+
 def _run(fn, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -157,3 +190,8 @@ def test_sharded_segments_merge_to_single_process_answer(expected):
     assert all(r[1] for r in res)
     # InterSegmentAggregationSingleValueQueriesTest.java:162-165 known answer, through the 2-rank merge
     assert [list(map(float, row)) for row in res[0][2]] == [[69526727335224.0, 69225631719808.0]]
+
+
+def test_sharded_raw_string_and_multi_value_shapes_merge():
+    res = _run(_worker_sharded_shapes)
+    assert all(ok for _, ok in res)
