@@ -317,6 +317,41 @@ __device__ __forceinline__ void stage_slice(const LeafDesc& X, uint32_t wg0, uin
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+#ifndef PG_STREAM_STAGE_BOTH
+#define PG_STREAM_STAGE_BOTH 0  // 1 (dev variant): the first two further leaves' slices (<= 8 bits) loaded together
+#endif
+
+// The first two further leaves' slices of the wave's 64 groups (<= 8 bits: <= 129 quads, 3 loads per lane each), every
+// load issued before any is stored, so the two slices cost one memory latency instead of two (PG_STREAM_STAGE_BOTH).
+__device__ __forceinline__ void stage_two(const LeafDesc& A, const LeafDesc& B, uint32_t wg0, uint32_t* sa, uint32_t* sb,
+                                          uint32_t lane) {
+  const rsrc_t ra = rsrc_of(A.words, A.wbytes), rb = rsrc_of(B.words, B.wbytes);
+  const uint32_t na = 16u * A.bits + 1u, nb = 16u * B.bits + 1u, wa = wg0 * A.bits, wb = wg0 * B.bits;
+  uint4 va[3], vb[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const uint32_t q = lane + 64u * k;
+    va[k] = vb[k] = make_uint4(0u, 0u, 0u, 0u);
+    if (q < na) {
+      const auto x = __builtin_amdgcn_raw_buffer_load_b128(ra, (wa + 4u * q) * 4u, 0, 0);
+      va[k] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    if (q < nb) {
+      const auto x = __builtin_amdgcn_raw_buffer_load_b128(rb, (wb + 4u * q) * 4u, 0, 0);
+      vb[k] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const uint32_t q = lane + 64u * k;
+    if (q < na) *(uint4*)(sa + 4u * q) = va[k];
+    if (q < nb) *(uint4*)(sb + 4u * q) = vb[k];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // The selective stream: the driving leaf of the root AND over the block's items (32-doc groups, thread-contiguous
 // 16-byte loads, 6 waves per SIMD so ~120 KiB per CU are in flight), survivors appended to the item's region in group
 // order within each wave: one wave prefix sum + one LDS cursor atomic per wave and group round that has a survivor.
@@ -330,7 +365,7 @@ constexpr uint32_t kExactLutWords = 32768;  // 128 KiB: the exact LUT of a <= 1 
 // static LDS in the kernel, so the exact LUT sits at LDS address 0).
 __host__ __device__ __forceinline__ uint32_t stream_lds_words(const StreamSpec& p, bool exact) {
   return exact ? kExactLutWords
-               : p.set_lds_ints + (p.num_extra ? 4u * p.stage_words * (p.stage_pre ? p.num_extra : 1u) : 0u);
+               : p.set_lds_ints + (p.num_extra ? 4u * p.stage_words * ((p.stage_pre || PG_STREAM_STAGE_BOTH) ? p.num_extra : 1u) : 0u);
 }
 
 #ifndef PG_STREAM_PIPE_EXTRA
@@ -458,14 +493,27 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 4 : (EXTRA ? (PG_STREAM_PIPE_EXTRA
           if (L.excl) r = ~r;
           m = r & valid;
         }
+        bool staged2 = false;  // PG_STREAM_STAGE_BOTH: extras 0 and 1 already in their slices
+        if (EXTRA && PG_STREAM_STAGE_BOTH && !p.stage_pre && p.stage_words && p.num_extra >= 2 && __ballot(m != 0)) {
+          const LeafDesc X0 = ldcf(seg_leaves, p.extra[0]), X1 = ldcf(seg_leaves, p.extra[1]);
+          auto two_ok = [](const LeafDesc& X) {
+            return (X.kind == LK_RANGE || X.kind == LK_SET_LDS || X.kind == LK_SET_LUT) && X.bits <= 8u;
+          };
+          if (two_ok(X0) && two_ok(X1)) {
+            uint32_t* s0 = lds_sets + p.set_lds_ints + ((tid >> 6) * p.num_extra) * p.stage_words;
+            stage_two(X0, X1, g0 + (tid & ~63u), s0, s0 + p.stage_words, lane);
+            staged2 = true;
+          }
+        }
         for (uint32_t x = 0; x < (EXTRA ? p.num_extra : 0u); x++) {
           if (__ballot(m != 0) == 0) break;
           const LeafDesc X = ldcf(seg_leaves, p.extra[x]);
           const bool packed = X.kind == LK_RANGE || X.kind == LK_SET_LDS || X.kind == LK_SET_LUT;
           if (EXTRA && p.stage_words && packed && X.bits * 64u + 4u <= p.stage_words) {
-            uint32_t* slice = lds_sets + p.set_lds_ints + (p.stage_pre ? (tid >> 6) * p.num_extra + x : (tid >> 6)) * p.stage_words;
+            uint32_t* slice = lds_sets + p.set_lds_ints +
+                              ((p.stage_pre || PG_STREAM_STAGE_BOTH) ? (tid >> 6) * p.num_extra + x : (tid >> 6)) * p.stage_words;
             if (p.stage_pre) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slice's DMA has landed
-            else stage_slice(X, g0 + (tid & ~63u), slice, lane);
+            else if (!(staged2 && x < 2)) stage_slice(X, g0 + (tid & ~63u), slice, lane);
             if (m) m &= eval_staged(X, lds_sets, slice, lane, m);
           } else if (m) {
             m &= eval_extra(X, lds_sets, (uint32_t)d0, m);
